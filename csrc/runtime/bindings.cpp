@@ -1,0 +1,195 @@
+// pybind11 bindings for the host runtime (module `lazzaro_amd._lib._lzrt`).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "colstore.h"
+#include "tokenizer.h"
+#include "graph_host.h"
+
+namespace py = pybind11;
+using namespace lzrt;
+
+namespace {
+
+Column to_column(const ColSpec& spec, py::handle obj) {
+  Column c;
+  c.type = spec.type;
+  c.dim = spec.dim;
+  switch (spec.type) {
+    case ColType::Str: {
+      for (auto item : obj) c.s.push_back(py::cast<std::string>(item));
+      break;
+    }
+    case ColType::F64: {
+      auto a = py::array_t<double, py::array::c_style | py::array::forcecast>::ensure(obj);
+      c.f64.assign(a.data(), a.data() + a.size());
+      break;
+    }
+    case ColType::F32: {
+      auto a = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(obj);
+      c.f32.assign(a.data(), a.data() + a.size());
+      break;
+    }
+    case ColType::I32: {
+      auto a = py::array_t<int32_t, py::array::c_style | py::array::forcecast>::ensure(obj);
+      c.i32.assign(a.data(), a.data() + a.size());
+      break;
+    }
+    case ColType::I64: {
+      auto a = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(obj);
+      c.i64.assign(a.data(), a.data() + a.size());
+      break;
+    }
+    case ColType::Bool: {
+      auto a = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>::ensure(obj);
+      c.b.assign(a.data(), a.data() + a.size());
+      break;
+    }
+    case ColType::VecF32: {
+      auto a = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(obj);
+      if (a.ndim() != 2) throw std::runtime_error("vector column must be 2-D");
+      c.dim = (uint32_t)a.shape(1);
+      c.f32.assign(a.data(), a.data() + a.size());
+      break;
+    }
+  }
+  return c;
+}
+
+py::object from_column(const Column& c) {
+  switch (c.type) {
+    case ColType::Str: {
+      py::list l(c.s.size());
+      for (size_t i = 0; i < c.s.size(); ++i) l[i] = py::str(c.s[i]);
+      return l;
+    }
+    case ColType::F64: return py::array_t<double>(c.f64.size(), c.f64.data());
+    case ColType::F32: return py::array_t<float>(c.f32.size(), c.f32.data());
+    case ColType::I32: return py::array_t<int32_t>(c.i32.size(), c.i32.data());
+    case ColType::I64: return py::array_t<int64_t>(c.i64.size(), c.i64.data());
+    case ColType::Bool: return py::array_t<uint8_t>(c.b.size(), c.b.data());
+    case ColType::VecF32: {
+      size_t n = c.size();
+      py::array_t<float> a({(py::ssize_t)n, (py::ssize_t)c.dim});
+      if (n) std::memcpy(a.mutable_data(), c.f32.data(), c.f32.size() * 4);
+      return a;
+    }
+  }
+  return py::none();
+}
+
+Predicate make_pred(const std::vector<std::pair<std::string, std::string>>& eq,
+                    const std::string& in_col, const py::object& in_vals) {
+  Predicate p;
+  p.eq = eq;
+  if (!in_col.empty() && !in_vals.is_none()) {
+    p.has_in = true;
+    p.in_col = in_col;
+    for (auto v : in_vals) p.in_vals.insert(py::cast<std::string>(v));
+  }
+  return p;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_lzrt, m) {
+  m.doc() = "lazzaro_amd host runtime: columnar store, tokenizer, graph utilities";
+
+  py::class_<Table>(m, "Table")
+      .def(py::init([](const std::string& dir, const std::vector<std::tuple<std::string, int, int>>& sch) {
+             std::vector<ColSpec> s;
+             for (auto& t : sch) s.push_back({std::get<0>(t), (ColType)std::get<1>(t), (uint32_t)std::get<2>(t)});
+             return new Table(dir, s);
+           }),
+           py::arg("dir"), py::arg("schema"))
+      .def("latest_version", [](Table& t) { py::gil_scoped_release r; return t.latest_version(); })
+      .def("count_rows", [](Table& t) { py::gil_scoped_release r; return t.count_rows(); })
+      .def("compact", [](Table& t) { py::gil_scoped_release r; return t.compact(); })
+      .def("append", [](Table& t, py::dict cols) {
+        std::vector<Column> cs;
+        for (auto& spec : t.schema()) {
+          if (!cols.contains(spec.name.c_str())) throw std::runtime_error("missing column " + spec.name);
+          cs.push_back(to_column(spec, cols[spec.name.c_str()]));
+        }
+        py::gil_scoped_release r;
+        return t.append(cs);
+      })
+      .def("delete_where",
+           [](Table& t, const std::vector<std::pair<std::string, std::string>>& eq, const std::string& in_col,
+              py::object in_vals) {
+             Predicate p = make_pred(eq, in_col, in_vals);
+             uint64_t n = 0, v;
+             {
+               py::gil_scoped_release r;
+               v = t.delete_where(p, &n);
+             }
+             return py::make_tuple(n, v);
+           },
+           py::arg("eq"), py::arg("in_col") = "", py::arg("in_vals") = py::none())
+      .def("scan",
+           [](Table& t, const std::vector<std::pair<std::string, std::string>>& eq, const std::string& in_col,
+              py::object in_vals, const std::vector<std::string>& want) {
+             Predicate p = make_pred(eq, in_col, in_vals);
+             std::vector<Column> cols;
+             {
+               py::gil_scoped_release r;
+               cols = t.scan(p, want);
+             }
+             py::dict d;
+             const auto& sch = t.schema();
+             for (size_t i = 0; i < sch.size(); ++i) {
+               bool w = want.empty();
+               for (auto& n : want) if (n == sch[i].name) w = true;
+               if (w) d[sch[i].name.c_str()] = from_column(cols[i]);
+             }
+             return d;
+           },
+           py::arg("eq") = std::vector<std::pair<std::string, std::string>>{}, py::arg("in_col") = "",
+           py::arg("in_vals") = py::none(), py::arg("want") = std::vector<std::string>{});
+
+  // ---- tokenizer ----
+  py::class_<Tokenizer>(m, "Tokenizer")
+      .def(py::init<int, bool>(), py::arg("vocab_size") = 30522, py::arg("lower") = true)
+      .def("load_vocab", &Tokenizer::load_vocab)
+      .def("has_vocab", &Tokenizer::has_vocab)
+      .def("encode", [](Tokenizer& t, const std::string& s, int max_len) { return t.encode(s, max_len); },
+           py::arg("text"), py::arg("max_len") = 512)
+      .def("encode_batch",
+           [](Tokenizer& t, const std::vector<std::string>& texts, int max_len) {
+             std::vector<int32_t> ids, lens;
+             int S = 0;
+             {
+               py::gil_scoped_release r;
+               S = t.encode_batch(texts, max_len, ids, lens);
+             }
+             py::array_t<int32_t> a({(py::ssize_t)texts.size(), (py::ssize_t)S});
+             if (!ids.empty()) std::memcpy(a.mutable_data(), ids.data(), ids.size() * 4);
+             py::array_t<int32_t> l(lens.size(), lens.data());
+             return py::make_tuple(a, l);
+           },
+           py::arg("texts"), py::arg("max_len") = 512);
+
+  // ---- graph host utilities ----
+  m.def("build_csr",
+        [](py::array_t<int32_t, py::array::c_style | py::array::forcecast> src,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> dst, int n, bool undirected) {
+          std::vector<int64_t> off;
+          std::vector<int32_t> adj, eid;
+          build_csr(src.data(), dst.data(), (int64_t)src.size(), n, undirected, off, adj, eid);
+          return py::make_tuple(py::array_t<int64_t>(off.size(), off.data()),
+                                py::array_t<int32_t>(adj.size(), adj.data()),
+                                py::array_t<int32_t>(eid.size(), eid.data()));
+        });
+  m.def("union_find_components",
+        [](py::array_t<int32_t, py::array::c_style | py::array::forcecast> src,
+           py::array_t<int32_t, py::array::c_style | py::array::forcecast> dst, int n) {
+          std::vector<int32_t> lab;
+          union_find(src.data(), dst.data(), (int64_t)src.size(), n, lab);
+          return py::array_t<int32_t>(lab.size(), lab.data());
+        });
+  m.def("tenant_rank", &tenant_rank, py::arg("tenant"), py::arg("world"),
+        "consistent-hash placement of a tenant id onto one of `world` ranks");
+}

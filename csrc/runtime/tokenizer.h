@@ -1,0 +1,32 @@
+// BERT-style tokenizer (host runtime): basic tokenization (lower-case,
+// whitespace + punctuation split) then WordPiece greedy longest-match against a
+// vocab.txt when one is loaded; without a vocab (no weights ship offline) each
+// word maps to a deterministic hashed id in [1000, vocab_size). Output follows
+// the BERT convention [CLS] ... [SEP] with [PAD]=0, [UNK]=100, [CLS]=101, [SEP]=102.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace lzrt {
+
+class Tokenizer {
+ public:
+  Tokenizer(int vocab_size = 30522, bool lower = true) : vocab_size_(vocab_size), lower_(lower) {}
+  bool load_vocab(const std::string& path);
+  bool has_vocab() const { return !vocab_.empty(); }
+  std::vector<int32_t> encode(const std::string& text, int max_len) const;
+  // pads to the longest sequence (rounded up to a multiple of 8); returns S
+  int encode_batch(const std::vector<std::string>& texts, int max_len, std::vector<int32_t>& ids,
+                   std::vector<int32_t>& lens) const;
+
+ private:
+  int vocab_size_;
+  bool lower_;
+  std::unordered_map<std::string, int32_t> vocab_;
+  void basic_split(const std::string& text, std::vector<std::string>& out) const;
+  void wordpiece(const std::string& w, std::vector<int32_t>& out) const;
+};
+
+}  // namespace lzrt

@@ -1,0 +1,112 @@
+"""In-tree build of the native pieces of lazzaro_amd.
+
+Two shared objects are produced next to the package sources (never in
+site-packages, so the GPU box loads exactly what this tree built):
+
+* ``lazzaro_amd/_lib/liblzk.so`` -- every HIP kernel under ``csrc/kernels`` for
+  gfx950 (CDNA4), one translation unit per file, C ABI (``extern "C" lzk_*``),
+  loaded with ctypes after ``import torch`` so it binds to the same HIP runtime
+  (``libamdhip64.so.7``) torch already mapped.
+* ``lazzaro_amd/_lib/_lzrt*.so`` -- the host runtime (columnar versioned store,
+  WordPiece/hash tokenizer, CSR/graph utilities, tenant placement), C++17 +
+  pybind11, built with g++.
+
+Usage: ``python -m lazzaro_amd._build`` (or ``__graft_entry__.build()``).
+Incremental: a target is rebuilt only when a source or header is newer.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+LIBDIR = os.path.join(ROOT, "lazzaro_amd", "_lib")
+BUILDDIR = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("LZK_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(BUILDDIR, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    flags = [
+        f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+        "-fvisibility=hidden", "-mcode-object-version=5",
+        "-I" + os.path.join(CSRC, "include"),
+    ]
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(BUILDDIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer(o, [s] + headers):
+            todo.append((s, o))
+
+    def comp(so):
+        s, o = so
+        if verbose:
+            print("[hipcc]", os.path.relpath(s, ROOT), flush=True)
+        _run([HIPCC] + flags + ["-c", s, "-o", o])
+
+    if todo:
+        with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            list(ex.map(comp, todo))
+    out = os.path.join(LIBDIR, "liblzk.so")
+    if _newer(out, objs) or not objs:
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    return out
+
+
+def build_runtime(verbose: bool = False) -> str:
+    import pybind11
+
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    out = os.path.join(LIBDIR, "_lzrt" + suffix)
+    if not srcs:
+        return ""
+    if _newer(out, srcs + headers):
+        if verbose:
+            print("[g++] runtime", flush=True)
+        cxx = shutil.which("g++") or "c++"
+        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+               "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
+               "-I" + os.path.join(CSRC, "runtime")] + srcs + ["-o", out, "-lpthread"]
+        _run(cmd)
+    return out
+
+
+def build_all(verbose: bool = True) -> None:
+    k = build_kernels(verbose=verbose)
+    r = build_runtime(verbose=verbose)
+    if verbose:
+        print("built:", k, r)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True)
+    sys.exit(0)

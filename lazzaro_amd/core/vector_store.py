@@ -1,0 +1,250 @@
+"""HBMStore: the ``Store`` protocol over the native columnar store + per-tenant
+HBM vector arenas (replaces reference ``core/vector_store.py:7-244``,
+``LanceDBStore``; exported under that name too for drop-in use).
+
+* Persistence: three versioned columnar tables ``nodes``, ``edges``,
+  ``profiles`` under ``{db_dir}/lancedb/`` with the reference's column names and
+  types. Every committed write bumps the table version, which
+  is what ``get_latest_version``/``MemorySystem.check_for_updates`` poll.
+* Search: each tenant (``user_id``) has its own :class:`VectorArena` in HBM --
+  the tenant "segment" replaces LanceDB's BTREE ``user_id`` prefilter (no mask,
+  no scan of other tenants). ``search_nodes`` runs the fused MFMA top-k kernel;
+  metric defaults to L2 like LanceDB (SURVEY.md §7.4 risk 4).
+* Arenas are built lazily from the table and kept in sync with this process's
+  own writes; writes from other processes are picked up when the table version
+  moves (checked at most every ``consistency_interval`` seconds).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from ..index.arena import VectorArena
+from ..store.colstore import EDGE_SCHEMA, NODE_SCHEMA, PROFILE_SCHEMA, ColumnarTable
+from ..utils.device import default_device
+
+
+def _json(v, default):
+    if v is None:
+        return json.dumps(default)
+    return v if isinstance(v, str) else json.dumps(v)
+
+
+def _unjson(v, default):
+    if isinstance(v, str):
+        try:
+            return json.loads(v)
+        except Exception:
+            return default
+    return v if v is not None else default
+
+
+class HBMStore:
+    def __init__(self, db_dir: str = "db", device=None, metric: str = "l2",
+                 consistency_interval: float = 0.5, keep_fp32: bool = True):
+        self.db_dir = db_dir
+        self._uri = os.path.join(db_dir, "lancedb")
+        os.makedirs(self._uri, exist_ok=True)
+        self.device = device if device is not None else default_device()
+        self.metric = metric
+        self.keep_fp32 = keep_fp32
+        self.consistency_interval = consistency_interval
+        self.nodes_table_name, self.edges_table_name, self.profile_table_name = "nodes", "edges", "profiles"
+        self._nodes_table = ColumnarTable(self._uri, "nodes", NODE_SCHEMA)
+        self._edges_table = ColumnarTable(self._uri, "edges", EDGE_SCHEMA)
+        self._profile_table = ColumnarTable(self._uri, "profiles", PROFILE_SCHEMA)
+        self._arenas: Dict[str, VectorArena] = {}
+        self._synced: Dict[str, int] = {}
+        self._last_check: Dict[str, float] = {}
+        self._lock = threading.RLock()
+        self._dim: Optional[int] = None
+
+    # ------------------------------------------------------------ helpers
+    def _table_dim(self) -> Optional[int]:
+        if self._dim is None:
+            for n, t, d in self._nodes_table.schema:
+                if n == "vector" and d:
+                    self._dim = d
+        return self._dim
+
+    def _arena(self, user_id: str) -> VectorArena:
+        """Tenant arena, rebuilt from the table if another writer moved it."""
+        with self._lock:
+            a = self._arenas.get(user_id)
+            now = time.time()
+            if a is not None and now - self._last_check.get(user_id, 0.0) < self.consistency_interval:
+                return a
+            self._last_check[user_id] = now
+            v = self._nodes_table.version
+            if a is not None and self._synced.get(user_id) == v:
+                return a
+            cols = self._nodes_table.scan_columns([("user_id", user_id)], want=["id", "vector"])
+            a = VectorArena(device=self.device, keep_fp32=self.keep_fp32)
+            ids = cols.get("id", [])
+            if len(ids):
+                vec = cols["vector"]
+                a.add(ids, vec)
+            self._arenas[user_id] = a
+            self._synced[user_id] = v
+            return a
+
+    def _after_write(self, user_id: str, prev_version, new_version: int) -> None:
+        # our write landed directly on the version the arena reflects -> the
+        # arena (already updated in place) is in sync; otherwise another
+        # process wrote in between: force a rebuild on next use.
+        if prev_version is not None and prev_version + 1 == new_version:
+            self._synced[user_id] = new_version
+        else:
+            self._synced.pop(user_id, None)
+            self._last_check.pop(user_id, None)
+
+    # ------------------------------------------------------------ nodes
+    def _node_rows(self, nodes: List[Dict[str, Any]], user_id: str) -> List[Dict[str, Any]]:
+        rows = []
+        dim = self._table_dim()
+        for n in nodes:
+            emb = n.get("embedding", n.get("vector")) or []
+            if dim is None and len(emb):
+                dim = self._dim = len(emb)
+            rows.append({
+                "id": n["id"], "user_id": user_id, "content": n["content"],
+                "vector": list(emb) if len(emb) else [0.0] * (dim or 0),
+                "type": n.get("type", "semantic"),
+                "timestamp": float(n.get("timestamp", 0.0)),
+                "access_count": int(n.get("access_count", 0)),
+                "last_accessed": float(n.get("last_accessed", 0.0)),
+                "salience": float(n.get("salience", 0.5)),
+                "is_super_node": bool(n.get("is_super_node", False)),
+                "child_ids": _json(n.get("child_ids", []), []),
+                "parent_id": n.get("parent_id") or "",
+                "shard_key": n.get("shard_key", "default"),
+                "metadata": _json(n.get("metadata", {}), {}),
+            })
+        return rows
+
+    def add_nodes(self, nodes: List[Dict[str, Any]], user_id: str = "default") -> None:
+        if not nodes:
+            return
+        rows = self._node_rows(nodes, user_id)
+        with self._lock:
+            a = self._arena(user_id)
+            prev = self._synced.get(user_id)
+            v = self._nodes_table.add_rows(rows)
+            a.add([r["id"] for r in rows], np.asarray([r["vector"] for r in rows], dtype=np.float32))
+            self._after_write(user_id, prev, v)
+
+    def get_nodes(self, user_id: str = "default") -> List[Dict[str, Any]]:
+        rows = self._nodes_table.scan([("user_id", user_id)])
+        for r in rows:
+            r["child_ids"] = _unjson(r.get("child_ids"), [])
+            r["metadata"] = _unjson(r.get("metadata"), {})
+        return rows
+
+    def search_nodes(self, query_emb, user_id: str = "default", limit: int = 5) -> List[str]:
+        if query_emb is None or len(query_emb) == 0:
+            return []
+        a = self._arena(user_id)
+        if len(a) == 0 or a.dim != len(query_emb):
+            return []
+        return a.search(query_emb, int(limit), self.metric)[0]
+
+    def search_nodes_batch(self, query_embs, user_id: str = "default", limit: int = 5) -> List[List[str]]:
+        """Batched variant (one kernel launch for all queries)."""
+        a = self._arena(user_id)
+        if len(a) == 0 or len(query_embs) == 0:
+            return [[] for _ in range(len(query_embs))]
+        return a.search(query_embs, int(limit), self.metric)
+
+    def delete_nodes(self, node_ids: Optional[List[str]], user_id: str = "default") -> None:
+        with self._lock:
+            a = self._arena(user_id)
+            prev = self._synced.get(user_id)
+            if not node_ids:
+                n, v = self._nodes_table.delete([("user_id", user_id)])
+                a.clear()
+            else:
+                n, v = self._nodes_table.delete([("user_id", user_id)], "id", list(node_ids))
+                a.delete(node_ids)
+            if n:
+                self._after_write(user_id, prev, v)
+
+    def get_latest_version(self) -> int:
+        return self._nodes_table.version
+
+    def list_users(self) -> List[str]:
+        cols = self._nodes_table.scan_columns(want=["user_id"])
+        return sorted(set(cols.get("user_id", [])))
+
+    # ------------------------------------------------------------ edges
+    def add_edges(self, edges: List[Dict[str, Any]], user_id: str = "default") -> None:
+        if not edges:
+            return
+        rows = []
+        for e in edges:
+            src = e.get("source") or e.get("source_id")
+            tgt = e.get("target") or e.get("target_id")
+            rows.append({
+                "id": e.get("id", f"{src}_{tgt}"), "user_id": user_id,
+                "source_id": src, "target_id": tgt,
+                "weight": float(e.get("weight", 1.0)),
+                "edge_type": e.get("edge_type") or e.get("type", "relates_to"),
+                "co_occurrence": int(e.get("co_occurrence", 1)),
+                "last_updated": float(e.get("last_updated", 0.0)),
+                "metadata": _json(e.get("metadata", {}), {}),
+            })
+        self._edges_table.add_rows(rows)
+
+    def delete_edges(self, source_id: Optional[str] = None, user_id: str = "default") -> None:
+        eq = [("user_id", user_id)]
+        if source_id:
+            eq.append(("source_id", source_id))
+        self._edges_table.delete(eq)
+
+    def get_edges(self, source_id: Optional[str] = None, user_id: str = "default") -> List[Dict[str, Any]]:
+        eq = [("user_id", user_id)]
+        if source_id:
+            eq.append(("source_id", source_id))
+        rows = self._edges_table.scan(eq)
+        for r in rows:
+            r["type"] = r.get("edge_type")
+            r["metadata"] = _unjson(r.get("metadata"), {})
+        return rows
+
+    # ------------------------------------------------------------ profiles
+    def save_profile(self, profile_data: Dict[str, Any], user_id: str = "default") -> None:
+        self._profile_table.delete([("user_id", user_id)])
+        self._profile_table.add_rows([{"user_id": user_id, "data": json.dumps(profile_data),
+                                       "updated_at": time.time()}])
+
+    def load_profile(self, user_id: str = "default") -> Optional[Dict[str, Any]]:
+        rows = self._profile_table.scan([("user_id", user_id)])
+        return json.loads(rows[-1]["data"]) if rows else None
+
+    # ------------------------------------------------------------ legacy aliases
+    def add(self, nodes: List[Dict[str, Any]], user_id: str = "default") -> None:
+        """pre-v0.3 ``VectorStore.add`` (reference tests/test_lancedb_integration.py)"""
+        self.add_nodes(nodes, user_id=user_id)
+
+    def search(self, query_emb, limit: int = 5, user_id: str = "default") -> List[str]:
+        return self.search_nodes(query_emb, user_id=user_id, limit=limit)
+
+    def delete(self, node_ids: List[str], user_id: str = "default") -> None:
+        if node_ids:
+            self.delete_nodes(node_ids, user_id=user_id)
+
+    # ------------------------------------------------------------ misc
+    def compact(self) -> None:
+        for t in (self._nodes_table, self._edges_table, self._profile_table):
+            t.compact()
+
+    def close(self) -> None:
+        self._arenas.clear()
+        self._synced.clear()
+
+
+LanceDBStore = HBMStore  # drop-in name used by reference code

@@ -1,0 +1,260 @@
+"""HBM vector arena: the device-resident replacement for a LanceDB vector column.
+
+One :class:`VectorArena` holds one tenant's (or one shard's) vectors as a
+contiguous ``[capacity, Dpad]`` bf16 matrix on the GPU (Dpad = D rounded up to
+64 so the MFMA kernel's K loop needs no tail), plus
+
+* ``sqn``   fp32 squared norms (exact, computed from the fp32 input) -> L2 bias
+* ``bias``  fp32 0 / -inf per row: tombstones cost nothing in the scan
+* ``X32``   optional exact fp32 copy used to re-rank the kernel's candidates so
+            results match an fp32 reference bit-for-bit in ordering
+
+Capacity grows geometrically (amortised O(1) appends); deletes are tombstones,
+compaction runs when more than half the rows are dead. Rows map to string ids
+(duplicates allowed, like repeated LanceDB ``add`` calls).
+
+Search = ``ops.flat_topk`` (hand-written MFMA kernel) for k <= 16, candidate
+width min(16, 4k) then an fp32 re-rank of those few rows.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import search as S
+from ..utils.device import default_device
+
+NEG_INF = float("-inf")
+
+
+def _pad64(d: int) -> int:
+    return (d + 63) // 64 * 64
+
+
+class VectorArena:
+    def __init__(self, dim: Optional[int] = None, device=None, capacity: int = 256,
+                 keep_fp32: bool = True, store_dtype: Optional[torch.dtype] = None):
+        self.device = torch.device(device) if device is not None else default_device()
+        self.on_gpu = self.device.type == "cuda"
+        self.store_dtype = store_dtype or (torch.bfloat16 if self.on_gpu else torch.float32)
+        self.keep_fp32 = keep_fp32 and self.on_gpu
+        self.dim = dim
+        self.cap = 0
+        self.n = 0
+        self.n_dead = 0
+        self.ids: List[Optional[str]] = []
+        self.rows_of: Dict[str, List[int]] = {}
+        self.X = self.X32 = self.sqn = self.bias = None
+        self._init_cap = capacity
+        self.version = 0  # bumps on every mutation (cache invalidation)
+
+    # ------------------------------------------------------------------ alloc
+    def _alloc(self, cap: int) -> None:
+        D = self.dim
+        Dp = _pad64(D) if self.on_gpu else D
+        X = torch.zeros((cap, Dp), dtype=self.store_dtype, device=self.device)
+        sqn = torch.zeros(cap, dtype=torch.float32, device=self.device)
+        bias = torch.full((cap,), NEG_INF, dtype=torch.float32, device=self.device)
+        X32 = torch.zeros((cap, D), dtype=torch.float32, device=self.device) if self.keep_fp32 else None
+        if self.cap:
+            X[: self.n] = self.X[: self.n]
+            sqn[: self.n] = self.sqn[: self.n]
+            bias[: self.n] = self.bias[: self.n]
+            if X32 is not None:
+                X32[: self.n] = self.X32[: self.n]
+        self.X, self.sqn, self.bias, self.X32 = X, sqn, bias, X32
+        self.cap = cap
+
+    def reserve(self, n: int) -> None:
+        if n > self.cap:
+            self._alloc(max(n, self._init_cap, int(self.cap * 1.5) + 1))
+
+    # -------------------------------------------------------------- mutation
+    def add(self, ids: Sequence[str], vecs) -> None:
+        if len(ids) == 0:
+            return
+        v = torch.as_tensor(np.asarray(vecs, dtype=np.float32)) if not torch.is_tensor(vecs) else vecs.float()
+        if v.dim() == 1:
+            v = v[None, :]
+        if self.dim is None:
+            self.dim = int(v.shape[1])
+        if v.shape[1] != self.dim:
+            raise ValueError(f"vector dim {v.shape[1]} != arena dim {self.dim}")
+        m = v.shape[0]
+        self.reserve(self.n + m)
+        v = v.to(self.device, non_blocking=True)
+        r0, r1 = self.n, self.n + m
+        self.X[r0:r1, : self.dim] = v.to(self.store_dtype)
+        if self.X32 is not None:
+            self.X32[r0:r1] = v
+        self.sqn[r0:r1] = (v.double() ** 2).sum(1).float()
+        self.bias[r0:r1] = 0.0
+        for j, i in enumerate(ids):
+            self.ids.append(i)
+            self.rows_of.setdefault(i, []).append(r0 + j)
+        self.n = r1
+        self.version += 1
+
+    def delete(self, ids: Iterable[str]) -> int:
+        rows = []
+        for i in ids:
+            rs = self.rows_of.pop(i, None)
+            if rs:
+                rows.extend(rs)
+        if not rows:
+            return 0
+        for r in rows:
+            self.ids[r] = None
+        t = torch.as_tensor(rows, dtype=torch.long, device=self.device)
+        self.bias[t] = NEG_INF
+        self.n_dead += len(rows)
+        self.version += 1
+        if self.n_dead * 2 > self.n and self.n > 64:
+            self.compact()
+        return len(rows)
+
+    def clear(self) -> None:
+        self.n = self.n_dead = 0
+        self.ids = []
+        self.rows_of = {}
+        if self.bias is not None:
+            self.bias.fill_(NEG_INF)
+        self.version += 1
+
+    def compact(self) -> None:
+        live = [r for r in range(self.n) if self.ids[r] is not None]
+        idx = torch.as_tensor(live, dtype=torch.long, device=self.device)
+        m = len(live)
+        self.X[:m] = self.X[idx]
+        self.sqn[:m] = self.sqn[idx]
+        self.bias[:m] = 0.0
+        self.bias[m: self.n] = NEG_INF
+        if self.X32 is not None:
+            self.X32[:m] = self.X32[idx]
+        self.ids = [self.ids[r] for r in live]
+        self.rows_of = {}
+        for r, i in enumerate(self.ids):
+            self.rows_of.setdefault(i, []).append(r)
+        self.n, self.n_dead = m, 0
+        self.version += 1
+
+    def __len__(self) -> int:
+        return self.n - self.n_dead
+
+    # ---------------------------------------------------------------- search
+    def _queries(self, q) -> torch.Tensor:
+        qt = torch.as_tensor(np.asarray(q, dtype=np.float32)) if not torch.is_tensor(q) else q.float()
+        if qt.dim() == 1:
+            qt = qt[None, :]
+        if qt.shape[1] != self.dim:
+            raise ValueError(f"query dim {qt.shape[1]} != arena dim {self.dim}")
+        return qt.to(self.device)
+
+    def search_rows(self, q, k: int, metric: str = "l2") -> Tuple[torch.Tensor, torch.Tensor]:
+        """Top-k rows per query. Returns (score, row) with score = -L2^2 for
+        ``l2``, cosine for ``cosine``, dot for ``ip`` (higher = closer)."""
+        qf = self._queries(q)
+        nq = qf.shape[0]
+        if self.n == 0 or len(self) == 0:
+            return (torch.full((nq, k), NEG_INF, device=self.device),
+                    torch.full((nq, k), -1, dtype=torch.long, device=self.device))
+        n = self.n
+        if metric == "cosine":
+            qn = qf / qf.norm(dim=1, keepdim=True).clamp_min(1e-30)
+        else:
+            qn = qf
+        if not self.on_gpu:
+            Xf = self.X[:n]
+            if metric == "cosine":
+                norms = self.sqn[:n].sqrt().clamp_min(1e-30)
+                s = (qn @ Xf.T) / norms[None, :] + self.bias[:n][None, :]
+            elif metric == "l2":
+                s = 2.0 * (qn @ Xf.T) - self.sqn[:n][None, :] + self.bias[:n][None, :] - (qn * qn).sum(1, keepdim=True)
+            else:
+                s = qn @ Xf.T + self.bias[:n][None, :]
+            return _stable_topk(s, k)
+        # GPU: fused MFMA scan over bf16 rows, then exact fp32 re-rank
+        kc = min(16, max(k, 4 * k)) if k <= 16 else k
+        Qb = torch.zeros((nq, self.X.shape[1]), dtype=torch.bfloat16, device=self.device)
+        if metric == "cosine":
+            Qb[:, : self.dim] = qn.to(torch.bfloat16)
+            inv = self.sqn[:n].sqrt().clamp_min(1e-30).reciprocal()
+            # cosine = <q, x>/|x|: fold 1/|x| by scanning normalised rows would
+            # need a second arena; approximate with ip + rerank below.
+            bias = self.bias[:n]
+            alpha = 1.0
+        elif metric == "l2":
+            Qb[:, : self.dim] = qn.to(torch.bfloat16)
+            bias = (self.bias[:n] - self.sqn[:n]).contiguous()
+            alpha = 2.0
+        else:
+            Qb[:, : self.dim] = qn.to(torch.bfloat16)
+            bias = self.bias[:n]
+            alpha = 1.0
+        Xv = self.X[:n]
+        if kc <= 16 and metric != "cosine":
+            cs, cr = S.flat_topk(Xv, Qb, kc, bias=bias, alpha=alpha)
+        else:
+            # cosine on unnormalised rows / very large k: scale rows on the fly
+            Xs = (self.X32[:n] if self.X32 is not None else Xv.float())
+            if metric == "cosine":
+                sc = (qn @ Xs.T) * inv[None, :] + self.bias[:n][None, :]
+            else:
+                sc = alpha * (qn @ Xs.T) + bias[None, :]
+            return _stable_topk(sc, k)
+        return self._rerank(qn, cs, cr, k, metric)
+
+    def _rerank(self, qn, cs, cr, k, metric):
+        if self.X32 is None:
+            return cs[:, :k], cr[:, :k]
+        valid = cr >= 0
+        rows = cr.clamp_min(0)
+        xs = self.X32[rows]  # [nq, kc, D]
+        dot = torch.einsum("qd,qkd->qk", qn, xs)
+        if metric == "l2":
+            s = 2.0 * dot - self.sqn[rows] - (qn * qn).sum(1, keepdim=True)
+        elif metric == "cosine":
+            s = dot / self.sqn[rows].sqrt().clamp_min(1e-30)
+        else:
+            s = dot
+        s = s + self.bias[rows]
+        s = torch.where(valid, s, torch.full_like(s, NEG_INF))
+        # order by (score desc, row asc)
+        key_rows = torch.where(valid, cr, torch.full_like(cr, 1 << 62))
+        o = torch.argsort(key_rows, dim=1, stable=True)
+        s = torch.gather(s, 1, o)
+        r = torch.gather(cr, 1, o)
+        o = torch.argsort(-s, dim=1, stable=True)[:, :k]
+        return torch.gather(s, 1, o), torch.gather(r, 1, o)
+
+    def search(self, q, k: int, metric: str = "l2") -> List[List[str]]:
+        s, r = self.search_rows(q, k, metric)
+        r = r.cpu().tolist()
+        s = s.cpu().tolist()
+        out = []
+        for rs, ss in zip(r, s):
+            out.append([self.ids[x] for x, v in zip(rs, ss) if x >= 0 and v != NEG_INF and self.ids[x] is not None])
+        return out
+
+    def vectors(self, ids: Sequence[str]) -> torch.Tensor:
+        """fp32 vectors of the first row of each id (device tensor)."""
+        rows = [self.rows_of[i][0] for i in ids]
+        t = torch.as_tensor(rows, dtype=torch.long, device=self.device)
+        if self.X32 is not None:
+            return self.X32[t]
+        return self.X[t, : self.dim].float()
+
+
+def _stable_topk(s: torch.Tensor, k: int):
+    n = s.shape[1]
+    kk = min(k, n)
+    o = torch.argsort(-s, dim=1, stable=True)[:, :kk]
+    vs = torch.gather(s, 1, o)
+    if kk < k:
+        pad = k - kk
+        vs = torch.cat([vs, torch.full((s.shape[0], pad), NEG_INF, device=s.device)], 1)
+        o = torch.cat([o, torch.full((s.shape[0], pad), -1, dtype=torch.long, device=s.device)], 1)
+    o = torch.where(torch.isneginf(vs), torch.full_like(o, -1), o)
+    return vs, o

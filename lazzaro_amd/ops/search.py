@@ -1,0 +1,155 @@
+"""Similarity top-k over a vector arena.
+
+``flat_topk`` is the single entry point used by the store's vector search
+(reference ``vector_store.py:132-140``), super-node scoring
+(``memory_system.py:464-472``), consolidation dedupe (``:719-733``) and
+associative linking (``:797-889``).
+
+Scores are ``alpha * <q, x> + bias[row]`` (fp32 accumulate over bf16 operands),
+which expresses all three metrics of the framework:
+
+* ``ip``      alpha=1, no bias
+* ``cosine``  rows and queries pre-normalised, alpha=1
+* ``l2``      alpha=2, bias=-|x|^2  (monotone in -|q-x|^2; LanceDB's default)
+
+Dead rows (tombstones) carry ``bias=-inf``; ``row_label``/``q_label`` restrict
+a query to rows with an equal label (tenant / shard filter; label<0 = any).
+Results are ordered by (score desc, row asc); missing slots are (-inf, -1).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+TARGET_WGS = 512  # 2 resident 256-thread workgroups per CU on 256 CUs
+
+
+def _ref_topk(X, Q, k, bias=None, row_label=None, q_label=None, alpha=1.0, idx_offset=0,
+              chunk=1 << 16):
+    """fp32 torch reference with the same (score desc, index asc) order."""
+    nq = Q.shape[0]
+    n = X.shape[0]
+    dev = X.device
+    best_s = torch.full((nq, 0), float("-inf"), device=dev)
+    best_i = torch.zeros((nq, 0), dtype=torch.long, device=dev)
+    Qf = Q.float()
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        s = alpha * (Qf @ X[c0:c1].float().T)
+        if bias is not None:
+            s = s + bias[c0:c1].float()[None, :]
+        if row_label is not None and q_label is not None:
+            ok = (row_label[c0:c1][None, :] == q_label[:, None]) | (q_label[:, None] < 0)
+            s = s.masked_fill(~ok, float("-inf"))
+        idx = torch.arange(c0, c1, device=dev).expand(nq, -1)
+        cs = torch.cat([best_s, s], 1)
+        ci = torch.cat([best_i, idx], 1)
+        # stable sort on index first, then on score -> ties keep ascending index
+        o = torch.argsort(ci, dim=1, stable=True)
+        cs = torch.gather(cs, 1, o)
+        ci = torch.gather(ci, 1, o)
+        o = torch.argsort(-cs, dim=1, stable=True)[:, :k]
+        best_s = torch.gather(cs, 1, o)
+        best_i = torch.gather(ci, 1, o)
+    if best_s.shape[1] < k:
+        pad = k - best_s.shape[1]
+        best_s = torch.cat([best_s, torch.full((nq, pad), float("-inf"), device=dev)], 1)
+        best_i = torch.cat([best_i, torch.full((nq, pad), -1, dtype=torch.long, device=dev)], 1)
+    best_i = torch.where(torch.isinf(best_s) & (best_s < 0), torch.full_like(best_i, -1),
+                         best_i + idx_offset)
+    return best_s, best_i
+
+
+class _Workspace:
+    """Per-device scratch for partial top-k lists (grown, never shrunk)."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, dev, nbytes):
+        b = self.buf.get(dev)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+            self.buf[dev] = b
+        return b
+
+
+_ws = _Workspace()
+
+
+def flat_topk(X: torch.Tensor, Q: torch.Tensor, k: int, *, bias=None, row_label=None,
+              q_label=None, alpha: float = 1.0, idx_offset: int = 0, n_chunks: int = None):
+    """Exact top-k of ``alpha*Q@X.T + bias`` per query row.
+
+    X: [N, D] bf16 (row stride may exceed D), Q: [nq, D] bf16, D % 64 == 0 on GPU.
+    Returns (scores fp32 [nq, k], rows int64 [nq, k]) with rows offset by idx_offset.
+    """
+    if Q.dim() == 1:
+        Q = Q[None, :]
+    nq, D = Q.shape
+    N = X.shape[0]
+    if not X.is_cuda:
+        return _ref_topk(X, Q, k, bias, row_label, q_label, alpha, idx_offset)
+    L = _lib.lib()
+    kslot = L.lzk_flat_topk_kslot(int(k))
+    if kslot < 0:
+        raise ValueError(f"flat_topk supports k <= 16 per pass (got {k}); use search.topk_large")
+    assert X.dtype == torch.bfloat16 and Q.dtype == torch.bfloat16
+    assert X.shape[1] == D and D % 64 == 0, "D must be a multiple of 64 (pad the arena)"
+    assert X.stride(1) == 1 and Q.stride(1) == 1
+    if N == 0 or nq == 0:
+        dev = X.device
+        return (torch.full((nq, k), float("-inf"), device=dev),
+                torch.full((nq, k), -1, dtype=torch.long, device=dev))
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.shape[0] >= N
+    if row_label is not None:
+        assert row_label.dtype == torch.int32 and q_label is not None
+        assert q_label.dtype == torch.int32 and q_label.shape[0] == nq
+    if n_chunks:
+        # same normalisation as the C launcher: chunks are whole 128-row tiles
+        rpc = -(-(-(-N // n_chunks)) // 128) * 128
+        nch = -(-N // rpc)
+    else:
+        nch = L.lzk_flat_topk_chunks(N, nq, TARGET_WGS)
+    dev = X.device
+    part = nq * nch * kslot
+    ws = _ws.get(dev, part * 8)
+    ps = ws[: part * 4].view(torch.float32)
+    pi = ws[part * 4: part * 8].view(torch.int32)
+    st = _lib.stream_ptr(dev)
+    rc = L.lzk_flat_topk_partial(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq,
+                                 _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label),
+                                 float(alpha), D, kslot, nch, ps.data_ptr(), pi.data_ptr(), st)
+    _lib.check(rc, "lzk_flat_topk_partial")
+    os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    oi = torch.empty((nq, k), dtype=torch.long, device=dev)
+    rc = L.lzk_topk_merge(ps.data_ptr(), pi.data_ptr(), nch * kslot, nq, kslot, int(k),
+                          int(idx_offset), os_.data_ptr(), oi.data_ptr(), st)
+    _lib.check(rc, "lzk_topk_merge")
+    return os_, oi
+
+
+def topk_large(X, Q, k, *, bias=None, alpha=1.0, idx_offset=0, chunk=1 << 20):
+    """k > 16: per-chunk candidate generation with the fused kernel at k=16
+    cannot be exact, so this path scores chunks with the GEMM library and
+    keeps a running torch top-k (used only for rerank candidate lists)."""
+    nq = Q.shape[0]
+    best_s = None
+    best_i = None
+    for c0 in range(0, X.shape[0], chunk):
+        c1 = min(X.shape[0], c0 + chunk)
+        s = alpha * (Q.float() @ X[c0:c1].float().T)
+        if bias is not None:
+            s = s + bias[c0:c1][None, :]
+        ts, ti = torch.topk(s, min(k, c1 - c0), dim=1)
+        ti = ti + c0
+        if best_s is None:
+            best_s, best_i = ts, ti
+        else:
+            cs = torch.cat([best_s, ts], 1)
+            ci = torch.cat([best_i, ti], 1)
+            best_s, o = torch.topk(cs, min(k, cs.shape[1]), dim=1)
+            best_i = torch.gather(ci, 1, o)
+    return best_s, best_i + idx_offset

@@ -1,0 +1,154 @@
+"""Python face of the native versioned columnar store (``csrc/runtime/colstore.*``).
+
+Table layout mirrors the reference's LanceDB database
+(``{db_dir}/lancedb/{nodes,edges,profiles}``, reference vector_store.py:16-85):
+same table names, column names and logical types. Each
+table is a ``<name>.lance/`` directory holding versioned manifests, immutable
+column segments and deletion files written by the C++ runtime.
+``to_arrow``/``from_arrow`` give Arrow interchange (pyarrow) so data can be
+moved into a real LanceDB on a networked machine.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+STR, F64, F32, I32, BOOL, VEC, I64 = 0, 1, 2, 3, 4, 5, 6
+
+
+def _rt():
+    try:
+        from .._lib import _lzrt  # type: ignore
+        return _lzrt
+    except ImportError:
+        from .. import _build
+        _build.build_runtime(verbose=True)
+        from .._lib import _lzrt  # type: ignore
+        return _lzrt
+
+
+NODE_SCHEMA: List[Tuple[str, int, int]] = [
+    ("id", STR, 0), ("user_id", STR, 0), ("content", STR, 0), ("vector", VEC, 0),
+    ("type", STR, 0), ("timestamp", F64, 0), ("access_count", I32, 0),
+    ("last_accessed", F64, 0), ("salience", F32, 0), ("is_super_node", BOOL, 0),
+    ("child_ids", STR, 0), ("parent_id", STR, 0), ("shard_key", STR, 0), ("metadata", STR, 0),
+]
+EDGE_SCHEMA: List[Tuple[str, int, int]] = [
+    ("id", STR, 0), ("user_id", STR, 0), ("source_id", STR, 0), ("target_id", STR, 0),
+    ("weight", F32, 0), ("edge_type", STR, 0), ("co_occurrence", I32, 0),
+    ("last_updated", F64, 0), ("metadata", STR, 0),
+]
+PROFILE_SCHEMA: List[Tuple[str, int, int]] = [
+    ("user_id", STR, 0), ("data", STR, 0), ("updated_at", F64, 0),
+]
+
+_NP = {F64: np.float64, F32: np.float32, I32: np.int32, BOOL: np.uint8, I64: np.int64}
+
+
+class ColumnarTable:
+    def __init__(self, root: str, name: str, schema: List[Tuple[str, int, int]], dim: int = 0):
+        self.name = name
+        self.path = os.path.join(root, name + ".lance")
+        sch = [(n, t, (dim if t == VEC else d)) for n, t, d in schema]
+        self.schema = sch
+        self._t = _rt().Table(self.path, sch)
+
+    @property
+    def version(self) -> int:
+        return int(self._t.latest_version())
+
+    def add_rows(self, rows: Sequence[Dict]) -> int:
+        if not rows:
+            return self.version
+        cols = {}
+        for n, t, _ in self.schema:
+            vals = [r[n] for r in rows]
+            if t == STR:
+                cols[n] = [("" if v is None else str(v)) for v in vals]
+            elif t == VEC:
+                cols[n] = np.asarray(vals, dtype=np.float32).reshape(len(rows), -1)
+            else:
+                cols[n] = np.asarray(vals, dtype=_NP[t])
+        return int(self._t.append(cols))
+
+    def add_columns(self, cols: Dict) -> int:
+        return int(self._t.append(cols))
+
+    def delete(self, eq: Sequence[Tuple[str, str]], in_col: str = "", in_vals=None) -> Tuple[int, int]:
+        n, v = self._t.delete_where(list(eq), in_col, None if in_vals is None else list(in_vals))
+        return int(n), int(v)
+
+    def scan_columns(self, eq: Sequence[Tuple[str, str]] = (), in_col: str = "", in_vals=None,
+                     want: Optional[Sequence[str]] = None) -> Dict:
+        return self._t.scan(list(eq), in_col, None if in_vals is None else list(in_vals), list(want or []))
+
+    def scan(self, eq: Sequence[Tuple[str, str]] = (), in_col: str = "", in_vals=None,
+             want: Optional[Sequence[str]] = None) -> List[Dict]:
+        cols = self.scan_columns(eq, in_col, in_vals, want)
+        if not cols:
+            return []
+        names = list(cols.keys())
+        n = len(cols[names[0]])
+        out = []
+        conv = {}
+        for k in names:
+            c = cols[k]
+            t = next(tt for nn, tt, _ in self.schema if nn == k)
+            if t == VEC:
+                conv[k] = [row.tolist() for row in c]
+            elif t == BOOL:
+                conv[k] = [bool(x) for x in c]
+            elif t in (I32, I64):
+                conv[k] = [int(x) for x in c]
+            elif t in (F32, F64):
+                conv[k] = [float(x) for x in c]
+            else:
+                conv[k] = c
+        for i in range(n):
+            out.append({k: conv[k][i] for k in names})
+        return out
+
+    def count(self) -> int:
+        return int(self._t.count_rows())
+
+    def compact(self) -> int:
+        return int(self._t.compact())
+
+    # ---- Arrow interchange --------------------------------------------------
+    def to_arrow(self):
+        import pyarrow as pa
+
+        cols = self.scan_columns()
+        arrays, fields = [], []
+        for n, t, _ in self.schema:
+            c = cols[n]
+            if t == VEC:
+                dim = c.shape[1] if c.ndim == 2 else 0
+                flat = pa.array(c.reshape(-1), type=pa.float32())
+                arrays.append(pa.FixedSizeListArray.from_arrays(flat, dim))
+                fields.append(pa.field(n, pa.list_(pa.float32(), dim)))
+            elif t == STR:
+                arrays.append(pa.array(c, type=pa.string()))
+                fields.append(pa.field(n, pa.string()))
+            elif t == BOOL:
+                arrays.append(pa.array(c.astype(bool)))
+                fields.append(pa.field(n, pa.bool_()))
+            else:
+                typ = {F64: pa.float64(), F32: pa.float32(), I32: pa.int32(), I64: pa.int64()}[t]
+                arrays.append(pa.array(c, type=typ))
+                fields.append(pa.field(n, typ))
+        return pa.Table.from_arrays(arrays, schema=pa.schema(fields))
+
+    def from_arrow(self, table) -> int:
+        cols = {}
+        for n, t, _ in self.schema:
+            col = table.column(n)
+            if t == VEC:
+                cols[n] = np.asarray(col.to_pylist(), dtype=np.float32)
+            elif t == STR:
+                cols[n] = [("" if v is None else v) for v in col.to_pylist()]
+            else:
+                cols[n] = np.asarray(col.to_pylist(), dtype=_NP[t])
+        return self.add_columns(cols)
