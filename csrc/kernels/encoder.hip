@@ -1,0 +1,401 @@
+// On-device sentence-transformer encoder kernels (BERT family: MiniLM-L6,
+// bge-base, e5-large). Replaces the reference's remote embedding calls
+// (reference src/lazzaro/core/providers.py:36-57, 101-128, 170-196) with a
+// local forward pass; SURVEY.md §2.4 K14.
+//
+//   gemm_bias_act  Y = act(X W^T + b) (+ R)  -- MFMA 128x128x64 tiles, features on
+//                  the MFMA M axis so each lane stores 4 consecutive outputs (8 B)
+//   attention      flash-style per (sequence, head, 32-query block): S^T = K Q^T on
+//                  MFMA, online softmax lane-local (keys in registers), O^T = V^T P
+//                  with the accumulator reused as the B operand (no LDS for P)
+//   layernorm      y = LN(x + r) * g + b, one wave per token row
+//   embed_ln       word + position + type embedding gather fused with LayerNorm
+//   pool_norm      masked mean / CLS pooling + L2 normalisation (+ bf16 copy
+//                  padded to the index arena's width)
+#include "lzk_tile.h"
+
+namespace {
+
+using namespace lzk;
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+
+// ---------------------------------------------------------------- GEMM
+template <int ACT, bool RES>
+__global__ __launch_bounds__(TNT, 2) void gemm_bias_act_kernel(
+    const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
+    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y,
+    long ldy, int K, int n_ft) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tt = logical / n_ft, ft = logical % n_ft;
+  const int n0 = ft * TB, t0 = tt * TB;
+  f32x16 acc[2][2];
+  tile_gemm(smem, W, ldw, n0, N, X, ldx, t0, T, K, acc);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wrow = wave >> 1, wcol = wave & 1, h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int t = t0 + wcol * 64 + cb * 32 + l32;
+    if (t >= T) continue;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wrow * 64 + rb * 32 + 8 * g + 4 * h;
+        if (n >= N) continue;
+        f32x4 bv = *reinterpret_cast<const f32x4*>(bias + n);
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = acc[rb][cb][4 * g + u] + bv[u];
+        if (ACT == 1) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = gelu_erf(v[u]);
+        }
+        if (RES) {
+          u16x4 rv = *reinterpret_cast<const u16x4*>(R + (long)t * ldr + n);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] += bf16_to_f32(rv[u]);
+        }
+        u16x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16(v[u]);
+        *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- attention
+// qkv: [B*S, 3*H] rows (q | k | v), head dim HD in {32, 64}. One wave per (b, head, qblock).
+template <int HD>
+__global__ __launch_bounds__(64) void attention_kernel(
+    const u16* __restrict__ qkv, long ldq, const int* __restrict__ lens, int S, int H, int nheads,
+    float scale_log2, u16* __restrict__ out, long ldo) {
+  constexpr int KSQ = HD / 16;   // k-steps of the S = K Q^T product
+  constexpr int NDB = HD / 32;   // 32-row blocks of the output O^T
+  __shared__ __attribute__((aligned(16))) u16 vt[HD * 40];  // V^T block: [dim][key], padded rows
+  const int lane = threadIdx.x, h = lane >> 5, l32 = lane & 31;
+  const int nqb = (S + 31) / 32;
+  const int qb = blockIdx.x % nqb;
+  const int hd = (blockIdx.x / nqb) % nheads;
+  const int b = blockIdx.x / (nqb * nheads);
+  const int len = lens[b];
+  const long tok0 = (long)b * S;
+  const int q = qb * 32 + l32;
+  const int qc = min(q, S - 1);
+  const u16* qrow = qkv + (tok0 + qc) * ldq + hd * HD;
+  bf16x8 qf[KSQ];
+#pragma unroll
+  for (int s = 0; s < KSQ; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s + 8 * h);
+
+  f32x16 o[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
+  float m = -1e30f, l = 0.f;
+  const int nkb = (len + 31) / 32;
+  for (int kb = 0; kb < nkb; ++kb) {
+    // S^T block [32 keys x 32 queries]: A = K rows, B = Q rows
+    const int key = kb * 32 + l32;
+    const u16* krow = qkv + (tok0 + min(key, S - 1)) * ldq + H + hd * HD;
+    f32x16 st;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) st[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KSQ; ++s) {
+      bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 16 * s + 8 * h);
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st, 0, 0, 0);
+    }
+    // stage V^T for this key block (each lane: one key, HD/2 dims)
+    {
+      const int vk = lane >> 1, vd0 = (lane & 1) * (HD / 2);
+      const u16* vrow = qkv + (tok0 + min(kb * 32 + vk, S - 1)) * ldq + 2 * H + hd * HD + vd0;
+#pragma unroll
+      for (int c = 0; c < HD / 16; ++c) {
+        u16x8 v8 = *reinterpret_cast<const u16x8*>(vrow + 8 * c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vt[(vd0 + 8 * c + j) * 40 + vk] = v8[j];
+      }
+    }
+    // masked online softmax over keys (registers + one cross-half shuffle)
+    float mx = -1e30f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      int kk = kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      float v = (kk < len) ? st[e] * scale_log2 : -1e30f;
+      st[e] = v;
+      mx = fmaxf(mx, v);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float corr = exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float p = exp2f(st[e] - mn);
+      st[e] = p;
+      ps += p;
+    }
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * corr + ps;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < NDB; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[i][e] *= corr;
+    __syncthreads();  // V^T staged (single-wave block: orders the LDS writes)
+    // O^T[dim][q] += V^T[dim][key] . P^T[key][q]; P^T is the accumulator `st`
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (__bf16)st[8 * s + j];
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        const int d = db * 32 + l32;
+        const u16* base = vt + d * 40 + 16 * s + 4 * h;
+        u16x4 lo = *reinterpret_cast<const u16x4*>(base);
+        u16x4 hi = *reinterpret_cast<const u16x4*>(base + 8);
+        u16x8 a8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf16x8 af = __builtin_bit_cast(bf16x8, a8);
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pf, o[db], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (q >= S) return;
+  const float inv = 1.f / l;
+  u16* orow = out + (tok0 + q) * ldo + hd * HD;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u16x4 w;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = f32_to_bf16(o[db][4 * g + u] * inv);
+      *reinterpret_cast<u16x4*>(orow + db * 32 + 8 * g + 4 * h) = w;
+    }
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// one wave per row; H % 4 == 0, H <= 64*4*NC
+template <int NC, bool RES>
+__global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ X, long ldx,
+                                                        const u16* __restrict__ R, long ldr,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ bta, int rows,
+                                                        int H, float eps, u16* __restrict__ Y, long ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[NC][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = (lane + 64 * c) * 4;
+    if (col < H) {
+      u16x4 x = *reinterpret_cast<const u16x4*>(X + (long)row * ldx + col);
+      u16x4 r = {0, 0, 0, 0};
+      if (RES) r = *reinterpret_cast<const u16x4*>(R + (long)row * ldr + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[c][u] = bf16_to_f32(x[u]) + (RES ? bf16_to_f32(r[u]) : 0.f);
+        sum += v[c][u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[c][u] = 0.f;
+    }
+  }
+  const float mean = wave_sum(sum) / H;
+  float var = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = (lane + 64 * c) * 4;
+    if (col < H)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { float d = v[c][u] - mean; var += d * d; }
+  }
+  const float rstd = rsqrtf(wave_sum(var) / H + eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = (lane + 64 * c) * 4;
+    if (col < H) {
+      f32x4 gg = *reinterpret_cast<const f32x4*>(g + col);
+      f32x4 bb = *reinterpret_cast<const f32x4*>(bta + col);
+      u16x4 o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16((v[c][u] - mean) * rstd * gg[u] + bb[u]);
+      *reinterpret_cast<u16x4*>(Y + (long)row * ldy + col) = o;
+    }
+  }
+}
+
+// embeddings (bf16 tables) + LayerNorm, one wave per token
+template <int NC>
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ ids, int T, int S,
+                                                       const u16* __restrict__ wemb,
+                                                       const u16* __restrict__ pemb,
+                                                       const u16* __restrict__ temb,
+                                                       const float* __restrict__ g,
+                                                       const float* __restrict__ bta, int H, float eps,
+                                                       u16* __restrict__ Y) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const int id = ids[t];
+  const int pos = t % S;
+  float v[NC][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = (lane + 64 * c) * 4;
+    if (col < H) {
+      u16x4 a = *reinterpret_cast<const u16x4*>(wemb + (long)id * H + col);
+      u16x4 p = *reinterpret_cast<const u16x4*>(pemb + (long)pos * H + col);
+      u16x4 ty = *reinterpret_cast<const u16x4*>(temb + col);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[c][u] = bf16_to_f32(a[u]) + bf16_to_f32(p[u]) + bf16_to_f32(ty[u]);
+        sum += v[c][u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[c][u] = 0.f;
+    }
+  }
+  const float mean = wave_sum(sum) / H;
+  float var = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = (lane + 64 * c) * 4;
+    if (col < H)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { float d = v[c][u] - mean; var += d * d; }
+  }
+  const float rstd = rsqrtf(wave_sum(var) / H + eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = (lane + 64 * c) * 4;
+    if (col < H) {
+      f32x4 gg = *reinterpret_cast<const f32x4*>(g + col);
+      f32x4 bb = *reinterpret_cast<const f32x4*>(bta + col);
+      u16x4 o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16((v[c][u] - mean) * rstd * gg[u] + bb[u]);
+      *reinterpret_cast<u16x4*>(Y + (long)t * H + col) = o;
+    }
+  }
+}
+
+// pooling (mode 0 = masked mean, 1 = CLS) + L2 normalise; one workgroup per sequence
+__global__ __launch_bounds__(256) void pool_norm_kernel(const u16* __restrict__ X, const int* __restrict__ lens,
+                                                        int S, int H, int mode, float* __restrict__ out32,
+                                                        u16* __restrict__ out16, int ld16) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const int len = max(1, lens[b]);
+  const long base = (long)b * S * H;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // up to H = 1024 with 256 threads
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    int col = threadIdx.x + 256 * c;
+    if (col >= H) continue;
+    float s = 0.f;
+    if (mode == 1) {
+      s = bf16_to_f32(X[base + col]);
+    } else {
+      for (int t = 0; t < len; ++t) s += bf16_to_f32(X[base + (long)t * H + col]);
+      s /= len;
+    }
+    acc[c] = s;
+    ss += s * s;
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float inv = 1.f / fmaxf(sqrtf(tot), 1e-12f);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    int col = threadIdx.x + 256 * c;
+    if (col >= H) continue;
+    float v = acc[c] * inv;
+    if (out32) out32[(long)b * H + col] = v;
+    if (out16) out16[(long)b * ld16 + col] = f32_to_bf16(v);
+  }
+  if (out16)
+    for (int col = H + threadIdx.x; col < ld16; col += 256) out16[(long)b * ld16 + col] = 0;
+}
+
+}  // namespace
+
+LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
+                                 const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
+                                 int act, void* stream) {
+  if (K % TK != 0 || N % 4 != 0 || T <= 0 || N <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int n_ft = (N + TB - 1) / TB, n_tt = (T + TB - 1) / TB;
+  dim3 grid(n_ft * n_tt), block(TNT);
+  const size_t lds = 2 * 2 * TELEMS * sizeof(u16);
+  const u16* x = (const u16*)X;
+  const u16* w = (const u16*)W;
+  const u16* r = (const u16*)R;
+  u16* y = (u16*)Y;
+#define GO(A, RS) hipLaunchKernelGGL((gemm_bias_act_kernel<A, RS>), grid, block, lds, st, x, ldx, T, w, ldw, N, bias, r, ldr, y, ldy, K, n_ft)
+  if (act == 1) { if (r) GO(1, true); else GO(1, false); }
+  else { if (r) GO(0, true); else GO(0, false); }
+#undef GO
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_attention(const void* qkv, long ldq, const int* lens, int B, int S, int H, int nheads,
+                             float scale, void* out, long ldo, void* stream) {
+  const int hdim = H / nheads;
+  if (H != nheads * hdim || (hdim != 32 && hdim != 64)) return (int)hipErrorInvalidValue;
+  const int nqb = (S + 31) / 32;
+  dim3 grid(B * nheads * nqb), block(64);
+  if (hdim == 64)
+    hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, (hipStream_t)stream, (const u16*)qkv, ldq, lens, S, H,
+                       nheads, scale * 1.4426950408889634f, (u16*)out, ldo);
+  else
+    hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, (hipStream_t)stream, (const u16*)qkv, ldq, lens, S, H,
+                       nheads, scale * 1.4426950408889634f, (u16*)out, ldo);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_layernorm(const void* X, long ldx, const void* R, long ldr, const float* g, const float* b,
+                             int rows, int H, float eps, void* Y, long ldy, void* stream) {
+  if (H % 4 != 0 || H > 64 * 4 * 4) return (int)hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X;
+  const u16* r = (const u16*)R;
+  u16* y = (u16*)Y;
+  if (r) hipLaunchKernelGGL((layernorm_kernel<4, true>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows, H, eps, y, ldy);
+  else hipLaunchKernelGGL((layernorm_kernel<4, false>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows, H, eps, y, ldy);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_embed_ln(const int* ids, int T, int S, const void* wemb, const void* pemb, const void* temb,
+                            const float* g, const float* b, int H, float eps, void* Y, void* stream) {
+  if (H % 4 != 0 || H > 64 * 4 * 4) return (int)hipErrorInvalidValue;
+  dim3 grid((T + 3) / 4), block(256);
+  hipLaunchKernelGGL((embed_ln_kernel<4>), grid, block, 0, (hipStream_t)stream, ids, T, S, (const u16*)wemb,
+                     (const u16*)pemb, (const u16*)temb, g, b, H, eps, (u16*)Y);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_pool_norm(const void* X, const int* lens, int B, int S, int H, int mode, float* out32,
+                             void* out16, int ld16, void* stream) {
+  if (H > 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pool_norm_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, (const u16*)X, lens, S, H, mode,
+                     out32, (u16*)out16, ld16);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,366 @@
+// Device graph-maintenance kernels.
+//
+// Replaces the reference's per-object Python loops over the memory graph:
+//   decay + prune     memory_shard.py:64-84, memory_system.py:624-630, :991   (K10)
+//   eviction scoring  memory_system.py:535-578                                (K11)
+//   connected comps   buffer_graph.py:99-120 (recursive DFS)                  (K9)
+//   neighbour boost   memory_system.py:242-260, buffer_graph.py:79-85         (K12)
+//   all-pairs merge   memory_system.py:1065-1120 (intended semantics)         (K7)
+//   centroids         memory_system.py:916-917 (np.mean) / k-means update     (K8)
+//
+// Graph layout: structure-of-arrays in HBM. Nodes: salience f32, access i32,
+// last_accessed f64, alive u8. Edges (COO): src/dst i32, weight f32,
+// co_occurrence i32, last_updated f64.
+#include "lzk_tile.h"
+
+namespace {
+
+constexpr int NTB = 256;
+
+// ------------------------------------------------------------------ K10
+// Pass 1: decay edge weights, flag survivors (w >= thr and both endpoints
+// alive), count survivors per block; the same launch decays node salience
+// (floor 0.2) in a grid-stride loop over nodes.
+__global__ __launch_bounds__(NTB) void decay_flag_kernel(
+    float* __restrict__ w, const int* __restrict__ src, const int* __restrict__ dst, long ne,
+    const unsigned char* __restrict__ alive, float keep, float thr, unsigned char* __restrict__ flag,
+    int* __restrict__ block_cnt, float* __restrict__ sal, long nn, float floor_) {
+  __shared__ int wsum[NTB / 64];
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  int f = 0;
+  if (e < ne) {
+    float v = w[e] * keep;
+    w[e] = v;
+    f = (v >= thr) && (!alive || (alive[src[e]] && alive[dst[e]]));
+    flag[e] = (unsigned char)f;
+  }
+  unsigned long long bal = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < NTB / 64; ++i) s += wsum[i];
+    block_cnt[blockIdx.x] = s;
+  }
+  if (sal) {
+    for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
+      float s = sal[i];
+      sal[i] = s > floor_ ? floor_ + (s - floor_) * keep : floor_;
+    }
+  }
+}
+
+// flag survivors without decaying (eviction: drop edges touching dead nodes)
+__global__ __launch_bounds__(NTB) void flag_alive_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                         long ne, const unsigned char* __restrict__ alive,
+                                                         unsigned char* __restrict__ flag, int* __restrict__ block_cnt) {
+  __shared__ int wsum[NTB / 64];
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  int f = 0;
+  if (e < ne) {
+    f = alive[src[e]] && alive[dst[e]];
+    flag[e] = (unsigned char)f;
+  }
+  unsigned long long bal = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// exclusive scan of per-block counts (single workgroup, chunked)
+__global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int n, int* __restrict__ total) {
+  __shared__ int buf[1024];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    int i = base + threadIdx.x;
+    int v = i < n ? cnt[i] : 0;
+    buf[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      int t = threadIdx.x >= o ? buf[threadIdx.x - o] : 0;
+      __syncthreads();
+      buf[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < n) cnt[i] = carry + buf[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += buf[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// Pass 2: stable scatter of surviving edges into the output arrays.
+__global__ __launch_bounds__(NTB) void compact_kernel(
+    const unsigned char* __restrict__ flag, const int* __restrict__ block_off, long ne,
+    const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ w,
+    const int* __restrict__ co, const double* __restrict__ lu, int* __restrict__ osrc, int* __restrict__ odst,
+    float* __restrict__ ow, int* __restrict__ oco, double* __restrict__ olu) {
+  __shared__ int wpre[NTB / 64];
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  const int f = (e < ne) ? flag[e] : 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long bal = __ballot(f);
+  int before = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) wpre[wv] = __popcll(bal);
+  __syncthreads();
+  int off = block_off[blockIdx.x];
+  for (int i = 0; i < wv; ++i) off += wpre[i];
+  if (f) {
+    int o = off + before;
+    osrc[o] = src[e];
+    odst[o] = dst[e];
+    ow[o] = w[e];
+    if (co) oco[o] = co[e];
+    if (lu) olu[o] = lu[e];
+  }
+}
+
+// ------------------------------------------------------------------ K11
+// importance = 0.5*sal + 0.3*min(1, acc/10) + 0.2/(1 + days_since_access);
+// dead or protected (super) nodes get +inf so they are never selected.
+__global__ __launch_bounds__(NTB) void importance_kernel(const float* __restrict__ sal, const int* __restrict__ acc,
+                                                         const double* __restrict__ last, const unsigned char* __restrict__ alive,
+                                                         const unsigned char* __restrict__ protect, long n, double now,
+                                                         float* __restrict__ out) {
+  const long i = (long)blockIdx.x * NTB + threadIdx.x;
+  if (i >= n) return;
+  if ((alive && !alive[i]) || (protect && protect[i])) { out[i] = __builtin_huge_valf(); return; }
+  double days = (now - last[i]) / 86400.0;
+  double v = 0.5 * (double)sal[i] + 0.3 * fmin(1.0, (double)acc[i] / 10.0) + 0.2 / (1.0 + days);
+  out[i] = (float)v;
+}
+
+__global__ __launch_bounds__(NTB) void mark_dead_kernel(const long* __restrict__ idx, long n, unsigned char* __restrict__ alive) {
+  const long i = (long)blockIdx.x * NTB + threadIdx.x;
+  if (i < n) alive[idx[i]] = 0;
+}
+
+// ------------------------------------------------------------------ K9
+// Connected components: min-label hooking on roots + pointer jumping.
+__device__ __forceinline__ int find_root(const int* __restrict__ p, int x) {
+  int y = p[x];
+  while (y != x) { x = y; y = p[x]; }
+  return x;
+}
+
+__global__ __launch_bounds__(NTB) void cc_hook_kernel(const int* __restrict__ src, const int* __restrict__ dst, long ne,
+                                                      const float* __restrict__ w, float min_w, int* __restrict__ parent,
+                                                      int* __restrict__ changed) {
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  if (e >= ne) return;
+  if (w && w[e] < min_w) return;
+  int ru = find_root(parent, src[e]);
+  int rv = find_root(parent, dst[e]);
+  if (ru == rv) return;
+  int hi = max(ru, rv), lo = min(ru, rv);
+  int old = atomicMin(&parent[hi], lo);
+  if (old != lo) *changed = 1;
+}
+
+__global__ __launch_bounds__(NTB) void cc_compress_kernel(int* __restrict__ parent, long n) {
+  const long i = (long)blockIdx.x * NTB + threadIdx.x;
+  if (i >= n) return;
+  int r = find_root(parent, (int)i);
+  parent[i] = r;
+}
+
+// ------------------------------------------------------------------ K12
+// Boost neighbours of the retrieved seeds over an undirected CSR:
+// neighbours with w >= min_w (excluding seeds) get last_accessed = now and
+// salience = min(1, s + delta); a flag makes the boost idempotent per node.
+__global__ __launch_bounds__(64) void neighbor_boost_kernel(const long* __restrict__ off, const int* __restrict__ adj,
+                                                            const int* __restrict__ eid, const float* __restrict__ w,
+                                                            const int* __restrict__ seeds, int nseeds, float min_w,
+                                                            double now, float delta, float* __restrict__ sal,
+                                                            double* __restrict__ last, int* __restrict__ flag,
+                                                            int* __restrict__ nboost) {
+  const int s = seeds[blockIdx.x];
+  for (long p = off[s] + threadIdx.x; p < off[s + 1]; p += 64) {
+    int nb = adj[p];
+    if (w[eid[p]] < min_w) continue;
+    bool is_seed = false;
+    for (int j = 0; j < nseeds; ++j) is_seed |= (seeds[j] == nb);
+    if (is_seed) continue;
+    if (atomicExch(&flag[nb], 1) == 0) {
+      sal[nb] = fminf(1.f, sal[nb] + delta);
+      last[nb] = now;
+      atomicAdd(nboost, 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ K7
+// All pairs (i < j) with <x_i, x_j> > tau over unit rows: upper-triangular
+// 128x128 MFMA tiles, pairs appended through one atomic counter.
+__global__ __launch_bounds__(lzk::TNT, 2) void pairs_kernel(const u16* __restrict__ X, long ldx, int n, int D, float tau,
+                                                       int ntile, int* __restrict__ count, int max_pairs,
+                                                       int2* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  // linear id -> (ti <= tj)
+  int id = blockIdx.x, ti = 0;
+  while (id >= ntile - ti) { id -= ntile - ti; ++ti; }
+  const int tj = ti + id;
+  f32x16 acc[2][2];
+  lzk::tile_gemm(smem, X, ldx, ti * lzk::TB, n, X, ldx, tj * lzk::TB, n, D, acc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wrow = wave >> 1, wcol = wave & 1, h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        int a = ti * lzk::TB + wrow * 64 + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        int b = tj * lzk::TB + wcol * 64 + cb * 32 + l32;
+        if (a < b && b < n && acc[rb][cb][e] > tau) {
+          int o = atomicAdd(count, 1);
+          if (o < max_pairs) out[o] = make_int2(a, b);
+        }
+      }
+}
+
+// ------------------------------------------------------------------ K8
+// Segmented sums for centroids: one wave per row, f32 atomics into [C, D]
+// (rows of one cluster are contiguous in memory for k-means updates after a
+// sort, so the atomics mostly hit distinct lines).
+__global__ __launch_bounds__(256) void seg_sum_kernel(const u16* __restrict__ X, long ldx, long n, int D,
+                                                      const int* __restrict__ label, float* __restrict__ sums,
+                                                      int* __restrict__ counts) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  const int c = label[r];
+  if (c < 0) return;
+  for (int d = lane * 4; d < D; d += 256) {
+    u16x4 v = *reinterpret_cast<const u16x4*>(X + r * ldx + d);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) atomicAdd(&sums[(long)c * D + d + u], bf16_to_f32(v[u]));
+  }
+  if (lane == 0) atomicAdd(&counts[c], 1);
+}
+
+// centroid = sums / count, optionally L2-normalised; written as fp32 and bf16 (padded)
+__global__ __launch_bounds__(64) void centroid_kernel(const float* __restrict__ sums, const int* __restrict__ counts,
+                                                      int D, int normalize, float* __restrict__ c32,
+                                                      u16* __restrict__ c16, int ld16) {
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const float cnt = (float)max(1, counts[c]);
+  float ss = 0.f;
+  for (int d = lane; d < D; d += 64) { float v = sums[(long)c * D + d] / cnt; ss += v * v; }
+  ss = wave_sum(ss);
+  const float inv = (normalize && ss > 0.f) ? rsqrtf(ss) : 1.f;
+  for (int d = lane; d < D; d += 64) {
+    float v = sums[(long)c * D + d] / cnt * inv;
+    if (c32) c32[(long)c * D + d] = v;
+    if (c16) c16[(long)c * ld16 + d] = f32_to_bf16(v);
+  }
+  if (c16)
+    for (int d = D + lane; d < ld16; d += 64) c16[(long)c * ld16 + d] = 0;
+}
+
+inline dim3 blocks_for(long n, int per = NTB) { return dim3((unsigned)((n + per - 1) / per)); }
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI
+LZK_EXPORT int lzk_decay_flag(float* w, const int* src, const int* dst, long ne, const unsigned char* alive,
+                              float rate, float thr, unsigned char* flag, int* block_cnt, float* sal, long nn,
+                              float floor_, void* stream) {
+  long nb = (ne + NTB - 1) / NTB;
+  if (nb == 0) nb = 1;
+  hipLaunchKernelGGL(decay_flag_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, w, src, dst, ne, alive,
+                     1.f - rate, thr, flag, block_cnt, sal, nn, floor_);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_flag_alive(const int* src, const int* dst, long ne, const unsigned char* alive, unsigned char* flag,
+                              int* block_cnt, void* stream) {
+  long nb = (ne + NTB - 1) / NTB;
+  if (nb == 0) nb = 1;
+  hipLaunchKernelGGL(flag_alive_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, src, dst, ne, alive,
+                     flag, block_cnt);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_scan_blocks(int* cnt, int n, int* total, void* stream) {
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, cnt, n, total);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_compact_edges(const unsigned char* flag, const int* block_off, long ne, const int* src,
+                                 const int* dst, const float* w, const int* co, const double* lu, int* osrc,
+                                 int* odst, float* ow, int* oco, double* olu, void* stream) {
+  if (ne == 0) return 0;
+  hipLaunchKernelGGL(compact_kernel, blocks_for(ne), dim3(NTB), 0, (hipStream_t)stream, flag, block_off, ne, src, dst,
+                     w, co, lu, osrc, odst, ow, oco, olu);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_importance(const float* sal, const int* acc, const double* last, const unsigned char* alive,
+                              const unsigned char* protect, long n, double now, float* out, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(importance_kernel, blocks_for(n), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last, alive,
+                     protect, n, now, out);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_mark_dead(const long* idx, long n, unsigned char* alive, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mark_dead_kernel, blocks_for(n), dim3(NTB), 0, (hipStream_t)stream, idx, n, alive);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_cc_hook(const int* src, const int* dst, long ne, const float* w, float min_w, int* parent,
+                           int* changed, void* stream) {
+  if (ne == 0) return 0;
+  hipLaunchKernelGGL(cc_hook_kernel, blocks_for(ne), dim3(NTB), 0, (hipStream_t)stream, src, dst, ne, w, min_w,
+                     parent, changed);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_cc_compress(int* parent, long n, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(cc_compress_kernel, blocks_for(n), dim3(NTB), 0, (hipStream_t)stream, parent, n);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_neighbor_boost(const long* off, const int* adj, const int* eid, const float* w, const int* seeds,
+                                  int nseeds, float min_w, double now, float delta, float* sal, double* last,
+                                  int* flag, int* nboost, void* stream) {
+  if (nseeds == 0) return 0;
+  hipLaunchKernelGGL(neighbor_boost_kernel, dim3(nseeds), dim3(64), 0, (hipStream_t)stream, off, adj, eid, w, seeds,
+                     nseeds, min_w, now, delta, sal, last, flag, nboost);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_pairs_above(const void* X, long ldx, int n, int D, float tau, int* count, int max_pairs,
+                               void* out, void* stream) {
+  if (D % lzk::TK != 0 || n <= 0) return (int)hipErrorInvalidValue;
+  int nt = (n + lzk::TB - 1) / lzk::TB;
+  long ntri = (long)nt * (nt + 1) / 2;
+  size_t lds = 2 * 2 * lzk::TELEMS * sizeof(u16);
+  hipLaunchKernelGGL(pairs_kernel, dim3((unsigned)ntri), dim3(lzk::TNT), lds, (hipStream_t)stream, (const u16*)X, ldx,
+                     n, D, tau, nt, count, max_pairs, (int2*)out);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_seg_sum(const void* X, long ldx, long n, int D, const int* label, float* sums, int* counts,
+                           void* stream) {
+  if (n == 0) return 0;
+  if (D % 4 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(seg_sum_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, (const u16*)X,
+                     ldx, n, D, label, sums, counts);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_centroids(const float* sums, const int* counts, int C, int D, int normalize, float* c32, void* c16,
+                             int ld16, void* stream) {
+  if (C == 0) return 0;
+  hipLaunchKernelGGL(centroid_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, sums, counts, D, normalize, c32,
+                     (u16*)c16, ld16);
+  return (int)hipGetLastError();
+}

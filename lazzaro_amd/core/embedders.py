@@ -1,0 +1,70 @@
+"""On-device embedding provider (``EmbeddingProvider`` protocol).
+
+Replaces the reference's remote embedders (providers.py:36-57, 101-128,
+170-196): text -> native C++ tokenizer (WordPiece with vocab.txt, hashed ids
+without one) -> :class:`~lazzaro_amd.models.encoder.SentenceEncoder` forward on
+the GPU (hand-written MFMA kernels) -> unit-norm vectors.
+
+Batching: ``batch_embed`` sorts texts by length and runs buckets of up to
+``max_batch`` sequences so padding waste stays small.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..models.encoder import SentenceEncoder, get_config
+from ..utils.device import default_device
+
+
+class Tokenizer:
+    """Thin wrapper over the native tokenizer (``_lzrt.Tokenizer``)."""
+
+    def __init__(self, vocab_file: Optional[str] = None, vocab_size: int = 30522):
+        from ..store.colstore import _rt
+
+        self._t = _rt().Tokenizer(vocab_size, True)
+        if vocab_file:
+            if not self._t.load_vocab(vocab_file):
+                raise FileNotFoundError(vocab_file)
+
+    def encode(self, text: str, max_len: int = 512) -> List[int]:
+        return list(self._t.encode(text, max_len))
+
+    def encode_batch(self, texts: List[str], max_len: int = 512):
+        ids, lens = self._t.encode_batch(list(texts), max_len)
+        return torch.from_numpy(np.asarray(ids)), torch.from_numpy(np.asarray(lens))
+
+
+class OnDeviceEmbedder:
+    def __init__(self, model: str = "bge-base", device=None, weights: Optional[str] = None,
+                 vocab_file: Optional[str] = None, max_len: int = 512, max_batch: int = 1024, seed: int = 0):
+        self.cfg = get_config(model)
+        self.device = torch.device(device) if device is not None else default_device()
+        self.encoder = SentenceEncoder(self.cfg, device=self.device, weights=weights, seed=seed)
+        self.tok = Tokenizer(vocab_file, vocab_size=self.cfg.vocab)
+        self.max_len = min(max_len, self.cfg.max_pos)
+        self.max_batch = max_batch
+        self.dim = self.cfg.hidden
+
+    def embed_tensor(self, texts: List[str], pad_to: int = 0):
+        ids, lens = self.tok.encode_batch(texts, self.max_len)
+        return self.encoder.forward(ids, lens, pad_to=pad_to)
+
+    def embed(self, text: str) -> List[float]:
+        return self.batch_embed([text])[0]
+
+    def batch_embed(self, texts: List[str]) -> List[List[float]]:
+        if not texts:
+            return []
+        order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
+        out: List[Optional[List[float]]] = [None] * len(texts)
+        for s in range(0, len(order), self.max_batch):
+            idx = order[s: s + self.max_batch]
+            v32, _ = self.embed_tensor([texts[i] for i in idx])
+            rows = v32.cpu().tolist()
+            for i, r in zip(idx, rows):
+                out[i] = r
+        return out  # type: ignore[return-value]

@@ -1,0 +1,225 @@
+"""DeviceGraph: an HBM-resident memory graph for consolidation at scale
+(BASELINE.json config 4; SURVEY.md §3.3 hot loops).
+
+The reference keeps the graph as Python objects and runs every consolidation
+step as Python loops (dedupe :719-742, linking :797-889, decay/prune
+memory_shard.py:64-84, eviction :535-578, components buffer_graph.py:99-120,
+super-nodes :893-933). Here one tenant's (or one GPU's share of a) buffer is
+structure-of-arrays in HBM and every step is a kernel:
+
+  ingest(facts)   dedupe = fused MFMA top-1 (K5) -> append rows -> chain edges
+                  -> within-shard top-3 (label-filtered, K6) + global top-3 (K6)
+  maintain()      decay + prune with stable compaction (K10) -> importance
+                  select + tombstone + dead-edge compaction (K11)
+  components()    hook/compress label propagation (K9)
+  cluster()       k-means super-nodes: assign = fused top-1, update = segmented
+                  mean (K16/K8), see :mod:`lazzaro_amd.index.kmeans`
+  boost(seeds)    CSR neighbour boost (K12)
+
+Semantics follow the reference's constants (App. B): dedupe cos > 0.95
+(salience=max, access+1), link top-3 cos > 0.5 with w = 0.8*cos, chain edge
+0.5, decay 0.01/conversation with salience floor 0.2, prune w < 0.5, eviction
+importance 0.5*sal + 0.3*min(1, acc/10) + 0.2/(1+days).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from ..ops import graph_ops as G
+from ..ops.search import flat_topk
+
+NEG_INF = float("-inf")
+
+
+def _pad64(d):
+    return (d + 63) // 64 * 64
+
+
+class DeviceGraph:
+    def __init__(self, dim: int, device=None, capacity: int = 1 << 16, edge_capacity: int = 1 << 18):
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.dim = dim
+        self.Dp = _pad64(dim) if self.device.type == "cuda" else dim
+        self.cap = 0
+        self.n = 0
+        self._alloc(capacity)
+        z = lambda dt: torch.zeros(0, dtype=dt, device=self.device)  # noqa: E731
+        self.edges: Dict[str, torch.Tensor] = {"src": z(torch.int32), "dst": z(torch.int32),
+                                               "w": z(torch.float32), "co": z(torch.int32),
+                                               "lu": z(torch.float64)}
+        self.stats = {"deduped": 0, "inserted": 0, "linked": 0, "pruned": 0, "evicted": 0}
+
+    # ------------------------------------------------------------------ storage
+    def _alloc(self, cap: int) -> None:
+        dev, n = self.device, self.n
+        dt = torch.bfloat16 if dev.type == "cuda" else torch.float32
+        new = {
+            "emb": torch.zeros((cap, self.Dp), dtype=dt, device=dev),
+            "sal": torch.zeros(cap, dtype=torch.float32, device=dev),
+            "acc": torch.zeros(cap, dtype=torch.int32, device=dev),
+            "last": torch.zeros(cap, dtype=torch.float64, device=dev),
+            "ts": torch.zeros(cap, dtype=torch.float64, device=dev),
+            "shard": torch.full((cap,), -1, dtype=torch.int32, device=dev),
+            "alive": torch.zeros(cap, dtype=torch.uint8, device=dev),
+            "super": torch.zeros(cap, dtype=torch.uint8, device=dev),
+            "bias": torch.full((cap,), NEG_INF, dtype=torch.float32, device=dev),
+        }
+        if self.cap:
+            for k, v in new.items():
+                v[:n] = getattr(self, k)[:n]
+        for k, v in new.items():
+            setattr(self, k, v)
+        self.cap = cap
+
+    def reserve(self, n: int) -> None:
+        if n > self.cap:
+            self._alloc(max(n, int(self.cap * 1.5) + 1))
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.edges["src"].numel())
+
+    def num_alive(self) -> int:
+        return int(self.alive[: self.n].sum().item())
+
+    def add_nodes(self, emb: torch.Tensor, shard: torch.Tensor, salience: torch.Tensor,
+                  now: Optional[float] = None, is_super: bool = False) -> torch.Tensor:
+        """Append unit-norm rows; returns their row indices."""
+        m = emb.shape[0]
+        now = time.time() if now is None else now
+        self.reserve(self.n + m)
+        r0, r1 = self.n, self.n + m
+        self.emb[r0:r1, : emb.shape[1]] = emb.to(self.emb.dtype)
+        self.sal[r0:r1] = salience.to(self.device, torch.float32)
+        self.acc[r0:r1] = 0
+        self.last[r0:r1] = now
+        self.ts[r0:r1] = now
+        self.shard[r0:r1] = shard.to(self.device, torch.int32)
+        self.alive[r0:r1] = 1
+        self.super[r0:r1] = 1 if is_super else 0
+        self.bias[r0:r1] = NEG_INF if is_super else 0.0
+        self.n = r1
+        return torch.arange(r0, r1, device=self.device)
+
+    def add_edges(self, src, dst, w, now: Optional[float] = None) -> None:
+        if src.numel() == 0:
+            return
+        now = time.time() if now is None else now
+        e = self.edges
+        e["src"] = torch.cat([e["src"], src.to(torch.int32)])
+        e["dst"] = torch.cat([e["dst"], dst.to(torch.int32)])
+        e["w"] = torch.cat([e["w"], w.to(torch.float32)])
+        e["co"] = torch.cat([e["co"], torch.ones_like(src, dtype=torch.int32)])
+        e["lu"] = torch.cat([e["lu"], torch.full((src.numel(),), now, dtype=torch.float64, device=self.device)])
+
+    # ------------------------------------------------------------------ search
+    def _search(self, q: torch.Tensor, k: int, row_label=None, q_label=None, bias=None):
+        n = self.n
+        if n == 0:
+            m = q.shape[0]
+            return (torch.full((m, k), NEG_INF, device=self.device),
+                    torch.full((m, k), -1, dtype=torch.long, device=self.device))
+        b = self.bias[:n] if bias is None else bias
+        return flat_topk(self.emb[:n], q, k, bias=b, row_label=row_label, q_label=q_label)
+
+    # ------------------------------------------------------------------ ingest
+    def ingest(self, q: torch.Tensor, shard: torch.Tensor, salience: torch.Tensor,
+               now: Optional[float] = None, dedupe_thr: float = 0.95, link_k: int = 3,
+               link_thr: float = 0.5, link_scale: float = 0.8, chain_w: float = 0.5) -> Dict[str, int]:
+        """One consolidation batch of M facts (unit rows ``q`` [M, Dp])."""
+        now = time.time() if now is None else now
+        q = q.to(self.emb.dtype)
+        M = q.shape[0]
+        # K5 dedupe: top-1 over live rows
+        s1, r1 = self._search(q, 1)
+        s1, r1 = s1[:, 0], r1[:, 0]
+        dup = (r1 >= 0) & (s1 > dedupe_thr)
+        if bool(dup.any()):
+            rows = r1[dup]
+            self.sal.index_reduce_(0, rows, salience.to(self.device)[dup].float(), "amax", include_self=True)
+            self.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
+            self.last[rows] = now
+        keep = ~dup
+        nk = int(keep.sum().item())
+        out = {"deduped": M - nk, "inserted": nk, "linked": 0}
+        if nk == 0:
+            return out
+        qn, sh, sl = q[keep], shard.to(self.device)[keep].to(torch.int32), salience.to(self.device)[keep]
+        # linking candidates exclude the batch itself (reference :816-821, :842-847)
+        n_old = self.n
+        rows = self.add_nodes(qn, sh, sl, now)
+        old_bias = self.bias[:self.n].clone()
+        old_bias[n_old:] = NEG_INF
+        # K6a within-shard: label-filtered top-k
+        sw, rw = self._search(qn, link_k, row_label=self.shard[: self.n], q_label=sh, bias=old_bias)
+        # K6b global top-k over all existing non-super rows
+        sg, rg = self._search(qn, link_k, bias=old_bias)
+        src = rows[:, None].expand(-1, link_k)
+        mw = (rw >= 0) & (sw > link_thr)
+        mg = (rg >= 0) & (sg > link_thr)
+        key_w = src[mw] * (1 << 32) + rw[mw]
+        key_g = src[mg] * (1 << 32) + rg[mg]
+        mg_new = ~torch.isin(key_g, key_w)  # skip pairs already linked in-shard
+        es = torch.cat([src[mw], src[mg][mg_new]])
+        ed = torch.cat([rw[mw], rg[mg][mg_new]])
+        ew = torch.cat([sw[mw], sg[mg][mg_new]]) * link_scale
+        # chain edges between consecutive new facts of the same shard
+        if nk > 1:
+            same = sh[1:] == sh[:-1]
+            es = torch.cat([es, rows[:-1][same]])
+            ed = torch.cat([ed, rows[1:][same]])
+            ew = torch.cat([ew, torch.full((int(same.sum()),), chain_w, device=self.device)])
+        self.add_edges(es, ed, ew, now)
+        out["linked"] = int(es.numel())
+        for k_ in out:
+            self.stats[k_] += out[k_]
+        return out
+
+    # ------------------------------------------------------------------ maintenance
+    def decay_prune(self, rate: float = 0.01, threshold: float = 0.5, conversations: int = 1) -> int:
+        """Apply ``conversations`` rounds of decay in one pass (exact for both
+        the edge product and the salience floor recurrence), then prune."""
+        eff = 1.0 - (1.0 - rate) ** conversations
+        n = self.n
+        live_sal = self.sal[:n]
+        self.edges, pruned = G.decay_prune(self.edges, live_sal, self.alive[:n], eff, threshold)
+        self.stats["pruned"] += pruned
+        return pruned
+
+    def enforce_limit(self, max_nodes: int, now: Optional[float] = None) -> int:
+        n_alive = self.num_alive()
+        excess = n_alive - max_nodes
+        if excess <= 0:
+            return 0
+        now = time.time() if now is None else now
+        n = self.n
+        score = G.importance(self.sal[:n], self.acc[:n], self.last[:n], self.alive[:n], self.super[:n], now)
+        victims = G.select_lowest(score, excess)
+        G.mark_dead(self.alive, victims)
+        self.bias[victims] = NEG_INF
+        self.edges = G.drop_dead_edges(self.edges, self.alive[:n])
+        self.stats["evicted"] += int(victims.numel())
+        return int(victims.numel())
+
+    def components(self, min_w: float = 0.0) -> torch.Tensor:
+        e = self.edges
+        return G.connected_components(e["src"], e["dst"], self.n, e["w"], min_w)
+
+    def csr(self):
+        """Undirected CSR (host build in the native runtime, copied to device)."""
+        from ..store.colstore import _rt
+        e = self.edges
+        off, adj, eid = _rt().build_csr(e["src"].cpu().numpy(), e["dst"].cpu().numpy(), self.n, True)
+        t = lambda a: torch.from_numpy(a).to(self.device)  # noqa: E731
+        return t(off), t(adj), t(eid)
+
+    def boost(self, seeds: torch.Tensor, now: Optional[float] = None, csr=None) -> int:
+        now = time.time() if now is None else now
+        off, adj, eid = csr if csr is not None else self.csr()
+        return G.neighbor_boost(off, adj, eid, self.edges["w"], seeds.to(self.device), self.sal, self.last, now)
+
+    def search(self, q: torch.Tensor, k: int = 10):
+        return self._search(q.to(self.emb.dtype), k)

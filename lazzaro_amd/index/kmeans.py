@@ -1,0 +1,88 @@
+"""Spherical k-means on the device -- the scalable form of the reference's
+super-node hierarchy (one mean super-node per shard, memory_system.py:893-933;
+SURVEY.md §2.4 K16/K8) and the coarse quantiser of the IVF-PQ index.
+
+assign: fused MFMA top-1 over the centroid matrix (``flat_topk`` with the
+        centroids as the arena and the data as queries)
+update: segmented mean + L2 renormalisation (``graph_ops.centroids``)
+Distributed: with a process group, per-rank partial sums/counts are combined
+with one all-reduce per iteration so every rank holds the
+same global centroids.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..ops import graph_ops as G
+from ..ops.search import flat_topk
+
+
+def assign(X: torch.Tensor, C16: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Nearest (max inner product) centroid per row of X. Returns (label, score)."""
+    labs, scs = [], []
+    for r0 in range(0, X.shape[0], chunk):
+        s, i = flat_topk(C16, X[r0:r0 + chunk], 1)
+        labs.append(i[:, 0])
+        scs.append(s[:, 0])
+    return torch.cat(labs).to(torch.int32), torch.cat(scs)
+
+
+def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 16) -> torch.Tensor:
+    """Deterministic farthest-first seeding on a subsample (k-means++ without
+    the sampling): avoids two seeds landing in one cluster."""
+    n = X.shape[0]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
+    S = X[sub].float()
+    picks = [0]
+    best = S @ S[0]
+    for _ in range(1, min(k, S.shape[0])):
+        j = int(torch.argmin(best).item())
+        picks.append(j)
+        best = torch.maximum(best, S @ S[j])
+    c = S[picks]
+    if c.shape[0] < k:
+        c = torch.cat([c, S[torch.randint(0, S.shape[0], (k - c.shape[0],), generator=g).to(X.device)]])
+    return c
+
+
+def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, group=None,
+           init: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """X: unit rows [n, Dp] (bf16 on GPU). Returns (centroids fp32 [k, Dp],
+    centroids bf16 [k, Dp], labels int32 [n])."""
+    n, Dp = X.shape
+    dev = X.device
+    if init is None and k <= 4096:
+        c32 = _farthest_first(X, k, seed)
+    elif init is None:
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        c32 = X[torch.randperm(n, generator=g)[:k].to(dev)].float()
+    if init is None:
+        if group is not None and dist.is_initialized():
+            dist.broadcast(c32, src=0, group=group)
+    else:
+        c32 = init.float().to(dev)
+    c32 = c32 / c32.norm(dim=1, keepdim=True).clamp_min(1e-30)
+    c16 = c32.to(X.dtype)
+    lab = None
+    for _ in range(iters):
+        lab, _ = assign(X, c16)
+        if group is None or not dist.is_initialized():
+            c32, c16n, cnt = G.centroids(X, lab, k, normalize=True, pad_to=Dp if X.is_cuda else 0)
+        else:
+            c32u, _, cnt = G.centroids(X, lab, k, normalize=False)
+            sums = c32u * cnt.clamp_min(1)[:, None].float()
+            dist.all_reduce(sums, group=group)
+            dist.all_reduce(cnt, group=group)
+            c32 = sums / cnt.clamp_min(1)[:, None].float()
+            c32 = c32 / c32.norm(dim=1, keepdim=True).clamp_min(1e-30)
+            c16n = None
+        # empty clusters keep their previous centroid
+        empty = cnt == 0
+        if bool(empty.any()):
+            c32[empty] = c16[empty].float()
+        c16 = c32.to(X.dtype) if c16n is None else torch.where(empty[:, None], c16, c16n)
+    return c32, c16, lab

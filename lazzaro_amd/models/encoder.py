@@ -1,0 +1,163 @@
+"""BERT-family sentence encoders that run on-device (SURVEY.md §2.2 "vendor
+embedding models -> on-device encoder", §2.4 K14).
+
+Configs mirror the public checkpoints the north star names (all-MiniLM-L6-v2,
+bge-base-en-v1.5, e5-large-v2): same widths, depths, heads, vocab, positions
+and pooling. Weights are random-init (std 0.02, deterministic seed) unless a
+safetensors file with HuggingFace BERT parameter names is supplied -- no
+checkpoints exist offline (BASELINE.json: "random-init embedding weights").
+
+Forward per layer (all hand-written gfx950 kernels, ``ops.encoder_ops``):
+  qkv = X Wqkv^T + b          fused QKV GEMM (one launch)
+  ctx = attention(qkv)        flash-style, masked, head_dim 32/64
+  X   = LN(ctx Wo^T + b + X)  residual fused into the GEMM epilogue
+  H   = gelu(X W1^T + b1)     GELU fused into the GEMM epilogue
+  X   = LN(H W2^T + b2 + X)
+then masked-mean or CLS pooling + L2 normalisation (one kernel).
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from ..ops import encoder_ops as E
+
+
+@dataclass(frozen=True)
+class EncoderConfig:
+    name: str
+    hidden: int
+    layers: int
+    heads: int
+    ffn: int
+    vocab: int = 30522
+    max_pos: int = 512
+    pooling: str = "mean"  # "mean" | "cls"
+    eps: float = 1e-12
+
+
+CONFIGS: Dict[str, EncoderConfig] = {
+    "minilm-l6": EncoderConfig("minilm-l6", 384, 6, 12, 1536, pooling="mean"),
+    "bge-base": EncoderConfig("bge-base", 768, 12, 12, 3072, pooling="cls"),
+    "e5-large": EncoderConfig("e5-large", 1024, 24, 16, 4096, pooling="mean"),
+    "tiny": EncoderConfig("tiny", 128, 2, 2, 256, vocab=4096, max_pos=128, pooling="mean"),
+}
+ALIASES = {
+    "all-minilm-l6-v2": "minilm-l6", "sentence-transformers/all-minilm-l6-v2": "minilm-l6",
+    "bge-base-en": "bge-base", "bge-base-en-v1.5": "bge-base", "baai/bge-base-en-v1.5": "bge-base",
+    "e5-large-v2": "e5-large", "intfloat/e5-large-v2": "e5-large",
+}
+
+
+def get_config(name: str) -> EncoderConfig:
+    k = name.lower()
+    k = ALIASES.get(k, k)
+    if k not in CONFIGS:
+        raise KeyError(f"unknown encoder {name!r}; known: {sorted(CONFIGS)}")
+    return CONFIGS[k]
+
+
+class SentenceEncoder:
+    """Weights + forward. ``forward(ids [B,S] int32, lens [B] int32)`` returns
+    unit-norm fp32 embeddings [B, H] (and optionally a bf16 copy padded to
+    ``pad_to`` columns, ready to be appended to an HBM arena)."""
+
+    def __init__(self, config, device=None, weights: Optional[str] = None, seed: int = 0,
+                 dtype=torch.bfloat16):
+        self.cfg = get_config(config) if isinstance(config, str) else config
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.dtype = dtype
+        self.p = self._random_init(seed)
+        if weights:
+            self.load_safetensors(weights)
+
+    # --------------------------------------------------------------- weights
+    def _random_init(self, seed: int) -> Dict[str, torch.Tensor]:
+        c, dev = self.cfg, self.device
+        g = torch.Generator(device="cpu").manual_seed(seed)
+
+        def w(*shape):
+            return (torch.randn(*shape, generator=g) * 0.02).to(dev, self.dtype)
+
+        def zeros(n):
+            return torch.zeros(n, dtype=torch.float32, device=dev)
+
+        def ones(n):
+            return torch.ones(n, dtype=torch.float32, device=dev)
+
+        H, Fh = c.hidden, c.ffn
+        p = {"word": w(c.vocab, H), "pos": w(c.max_pos, H), "type": w(2, H),
+             "emb_g": ones(H), "emb_b": zeros(H)}
+        for i in range(c.layers):
+            p[f"{i}.wqkv"] = w(3 * H, H)
+            p[f"{i}.bqkv"] = zeros(3 * H)
+            p[f"{i}.wo"] = w(H, H)
+            p[f"{i}.bo"] = zeros(H)
+            p[f"{i}.ln1_g"], p[f"{i}.ln1_b"] = ones(H), zeros(H)
+            p[f"{i}.w1"] = w(Fh, H)
+            p[f"{i}.b1"] = zeros(Fh)
+            p[f"{i}.w2"] = w(H, Fh)
+            p[f"{i}.b2"] = zeros(H)
+            p[f"{i}.ln2_g"], p[f"{i}.ln2_b"] = ones(H), zeros(H)
+        return p
+
+    def load_safetensors(self, path: str) -> None:
+        """Load HuggingFace BERT-layout weights (optionally ``bert.``-prefixed)."""
+        from safetensors.torch import load_file
+
+        sd = load_file(path)
+        sd = {k[5:] if k.startswith("bert.") else k: v for k, v in sd.items()}
+        dev, dt = self.device, self.dtype
+
+        def get(k):
+            return sd[k]
+
+        self.p["word"] = get("embeddings.word_embeddings.weight").to(dev, dt)
+        self.p["pos"] = get("embeddings.position_embeddings.weight").to(dev, dt)
+        self.p["type"] = get("embeddings.token_type_embeddings.weight").to(dev, dt)
+        self.p["emb_g"] = get("embeddings.LayerNorm.weight").float().to(dev)
+        self.p["emb_b"] = get("embeddings.LayerNorm.bias").float().to(dev)
+        for i in range(self.cfg.layers):
+            pre = f"encoder.layer.{i}."
+            q, k, v = (get(pre + f"attention.self.{n}.weight") for n in ("query", "key", "value"))
+            qb, kb, vb = (get(pre + f"attention.self.{n}.bias") for n in ("query", "key", "value"))
+            self.p[f"{i}.wqkv"] = torch.cat([q, k, v], 0).to(dev, dt).contiguous()
+            self.p[f"{i}.bqkv"] = torch.cat([qb, kb, vb], 0).float().to(dev)
+            self.p[f"{i}.wo"] = get(pre + "attention.output.dense.weight").to(dev, dt)
+            self.p[f"{i}.bo"] = get(pre + "attention.output.dense.bias").float().to(dev)
+            self.p[f"{i}.ln1_g"] = get(pre + "attention.output.LayerNorm.weight").float().to(dev)
+            self.p[f"{i}.ln1_b"] = get(pre + "attention.output.LayerNorm.bias").float().to(dev)
+            self.p[f"{i}.w1"] = get(pre + "intermediate.dense.weight").to(dev, dt)
+            self.p[f"{i}.b1"] = get(pre + "intermediate.dense.bias").float().to(dev)
+            self.p[f"{i}.w2"] = get(pre + "output.dense.weight").to(dev, dt)
+            self.p[f"{i}.b2"] = get(pre + "output.dense.bias").float().to(dev)
+            self.p[f"{i}.ln2_g"] = get(pre + "output.LayerNorm.weight").float().to(dev)
+            self.p[f"{i}.ln2_b"] = get(pre + "output.LayerNorm.bias").float().to(dev)
+
+    def num_params(self) -> int:
+        return sum(t.numel() for t in self.p.values())
+
+    # --------------------------------------------------------------- forward
+    def forward(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0):
+        c, p = self.cfg, self.p
+        B, S = ids.shape
+        ids = ids.to(self.device, torch.int32).contiguous()
+        lens = lens.to(self.device, torch.int32).contiguous()
+        x = E.embed_ln(ids.view(-1), S, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps)
+        for i in range(c.layers):
+            qkv = E.linear(x, p[f"{i}.wqkv"], p[f"{i}.bqkv"])
+            ctx = E.attention(qkv, lens, B, S, c.heads)
+            x = E.layernorm(E.linear(ctx, p[f"{i}.wo"], p[f"{i}.bo"], residual=x),
+                            p[f"{i}.ln1_g"], p[f"{i}.ln1_b"], c.eps)
+            hdn = E.linear(x, p[f"{i}.w1"], p[f"{i}.b1"], act="gelu")
+            x = E.layernorm(E.linear(hdn, p[f"{i}.w2"], p[f"{i}.b2"], residual=x),
+                            p[f"{i}.ln2_g"], p[f"{i}.ln2_b"], c.eps)
+        return E.pool_norm(x, lens, B, S, c.pooling, pad_to)
+
+    def flops(self, tokens: int) -> float:
+        c = self.cfg
+        per_tok = 2 * (3 * c.hidden * c.hidden + c.hidden * c.hidden + 2 * c.hidden * c.ffn) * c.layers
+        return float(per_tok) * tokens

@@ -1,0 +1,121 @@
+"""Encoder ops: GEMM with fused bias/GELU/residual
+epilogue, flash-style attention, LayerNorm, embedding+LayerNorm, pooling+L2.
+
+HIP tensors -> hand-written gfx950 kernels (``csrc/kernels/encoder.hip``);
+CPU tensors -> the fp32 torch reference of the same op (used as the CPU test
+tier and as the numerics oracle in tests/kernels).
+Activations are bf16 row-major ``[tokens, features]``; weights ``[out, in]``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+_lib.register("lzk_gemm_bias_act", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P,
+                                             _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
+_lib.register("lzk_attention", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.F,
+                                         _lib.P, _lib.L, _lib.P])
+_lib.register("lzk_layernorm", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.P, _lib.I, _lib.I,
+                                         _lib.F, _lib.P, _lib.L, _lib.P])
+_lib.register("lzk_embed_ln", _lib.I, [_lib.P, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P,
+                                        _lib.I, _lib.F, _lib.P, _lib.P])
+_lib.register("lzk_pool_norm", _lib.I, [_lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P,
+                                         _lib.I, _lib.P])
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, act: str = "none", residual=None,
+           out=None) -> torch.Tensor:
+    """act(x @ w.T + b) (+ residual). x [T,K] bf16, w [N,K] bf16, b [N] fp32."""
+    T, K = x.shape
+    N = w.shape[0]
+    if not x.is_cuda:
+        y = x.float() @ w.float().T + b.float()
+        if act == "gelu":
+            y = F.gelu(y)
+        if residual is not None:
+            y = y + residual.float()
+        return y.to(x.dtype)
+    assert x.stride(1) == 1 and w.stride(1) == 1 and K % 64 == 0 and N % 4 == 0
+    y = out if out is not None else torch.empty((T, N), dtype=torch.bfloat16, device=x.device)
+    rc = _lib.lib().lzk_gemm_bias_act(x.data_ptr(), x.stride(0), T, w.data_ptr(), w.stride(0), N, b.data_ptr(),
+                                      _lib.ptr(residual), residual.stride(0) if residual is not None else 0,
+                                      y.data_ptr(), y.stride(0), K, 1 if act == "gelu" else 0,
+                                      _lib.stream_ptr(x.device))
+    _lib.check(rc, "lzk_gemm_bias_act")
+    return y
+
+
+def attention(qkv: torch.Tensor, lens: torch.Tensor, B: int, S: int, nheads: int, out=None) -> torch.Tensor:
+    """qkv [B*S, 3H] (q|k|v), head_dim 64; keys >= lens[b] are masked."""
+    H = qkv.shape[1] // 3
+    if not qkv.is_cuda:
+        x = qkv.float().view(B, S, 3, nheads, H // nheads)
+        q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+        s = (q @ k.transpose(-1, -2)) / math.sqrt(H // nheads)
+        mask = torch.arange(S, device=qkv.device)[None, :] >= lens[:, None].to(qkv.device)
+        s = s.masked_fill(mask[:, None, None, :], float("-inf"))
+        o = torch.softmax(s, -1) @ v
+        return o.transpose(1, 2).reshape(B * S, H).to(qkv.dtype)
+    y = out if out is not None else torch.empty((B * S, H), dtype=torch.bfloat16, device=qkv.device)
+    rc = _lib.lib().lzk_attention(qkv.data_ptr(), qkv.stride(0), lens.data_ptr(), B, S, H, nheads,
+                                  1.0 / math.sqrt(H // nheads), y.data_ptr(), y.stride(0),
+                                  _lib.stream_ptr(qkv.device))
+    _lib.check(rc, "lzk_attention")
+    return y
+
+
+def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-12, residual=None,
+              out=None) -> torch.Tensor:
+    if not x.is_cuda:
+        v = x.float() + (residual.float() if residual is not None else 0.0)
+        return F.layer_norm(v, (x.shape[1],), g.float(), b.float(), eps).to(x.dtype)
+    rows, H = x.shape
+    y = out if out is not None else torch.empty_like(x)
+    rc = _lib.lib().lzk_layernorm(x.data_ptr(), x.stride(0), _lib.ptr(residual),
+                                  residual.stride(0) if residual is not None else 0, g.data_ptr(), b.data_ptr(),
+                                  rows, H, float(eps), y.data_ptr(), y.stride(0), _lib.stream_ptr(x.device))
+    _lib.check(rc, "lzk_layernorm")
+    return y
+
+
+def embed_ln(ids: torch.Tensor, S: int, wemb, pemb, temb, g, b, eps: float = 1e-12) -> torch.Tensor:
+    """ids [B*S] int32 -> LN(word[ids] + pos[t % S] + type[0]) bf16 [B*S, H]."""
+    T = ids.numel()
+    H = wemb.shape[1]
+    if not ids.is_cuda:
+        pos = torch.arange(T, device=ids.device) % S
+        v = wemb[ids.long()].float() + pemb[pos].float() + temb[0].float()
+        return F.layer_norm(v, (H,), g.float(), b.float(), eps).to(wemb.dtype)
+    y = torch.empty((T, H), dtype=torch.bfloat16, device=ids.device)
+    rc = _lib.lib().lzk_embed_ln(ids.data_ptr(), T, S, wemb.data_ptr(), pemb.data_ptr(), temb.data_ptr(),
+                                 g.data_ptr(), b.data_ptr(), H, float(eps), y.data_ptr(), _lib.stream_ptr(ids.device))
+    _lib.check(rc, "lzk_embed_ln")
+    return y
+
+
+def pool_norm(x: torch.Tensor, lens: torch.Tensor, B: int, S: int, mode: str = "mean", out16_width: int = 0):
+    """Returns (fp32 [B,H] unit rows, bf16 [B,out16_width] zero-padded copy or None)."""
+    H = x.shape[1]
+    if not x.is_cuda:
+        v = x.float().view(B, S, H)
+        if mode == "cls":
+            p = v[:, 0]
+        else:
+            m = (torch.arange(S, device=x.device)[None, :] < lens[:, None].to(x.device)).float()
+            p = (v * m[..., None]).sum(1) / m.sum(1, keepdim=True).clamp_min(1)
+        p = p / p.norm(dim=1, keepdim=True).clamp_min(1e-12)
+        o16 = None
+        if out16_width:
+            o16 = torch.zeros((B, out16_width), dtype=torch.bfloat16, device=x.device)
+            o16[:, :H] = p.to(torch.bfloat16)
+        return p, o16
+    out32 = torch.empty((B, H), dtype=torch.float32, device=x.device)
+    out16 = torch.empty((B, out16_width), dtype=torch.bfloat16, device=x.device) if out16_width else None
+    rc = _lib.lib().lzk_pool_norm(x.data_ptr(), lens.data_ptr(), B, S, H, 1 if mode == "cls" else 0,
+                                  out32.data_ptr(), _lib.ptr(out16), out16_width, _lib.stream_ptr(x.device))
+    _lib.check(rc, "lzk_pool_norm")
+    return out32, out16

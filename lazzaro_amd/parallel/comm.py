@@ -1,0 +1,118 @@
+"""Communicator: one process per GPU over ``torch.distributed``.
+
+Backend ``nccl`` is RCCL on ROCm (GPU tensors, xGMI); ``gloo`` is used for CPU
+tensors (tests, host metadata). The collectives this engine needs
+(SURVEY.md §2.5):
+
+* ``all_gather_rows``  C1 cross-shard search candidates, C7 tenant directory
+* ``all_to_all_v``     C3 re-sharding rows after consolidation (variable sizes,
+                       count exchange first); all-to-all uses every xGMI link
+                       at once instead of a one-link-bound ring
+* ``all_reduce``       C4 k-means partial sums, C5 component labels
+* ``barrier``          C6 multi-rank commit
+
+``Communicator.local()`` is the world-of-one stand-in so single-process code
+paths call the same API.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class Communicator:
+    def __init__(self, group=None, device: Optional[torch.device] = None):
+        self.group = group
+        self.enabled = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank(group) if self.enabled else 0
+        self.world = dist.get_world_size(group) if self.enabled else 1
+        if device is None:
+            be = dist.get_backend(group) if self.enabled else "gloo"
+            device = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else torch.device("cpu")
+        self.device = torch.device(device)
+
+    @classmethod
+    def local(cls, device=None) -> "Communicator":
+        c = cls.__new__(cls)
+        c.group, c.enabled, c.rank, c.world = None, False, 0, 1
+        c.device = torch.device(device) if device is not None else torch.device("cpu")
+        return c
+
+    @classmethod
+    def init(cls, backend: Optional[str] = None) -> "Communicator":
+        """Initialise from torchrun env vars (RANK/WORLD_SIZE/MASTER_ADDR...)."""
+        if not dist.is_initialized():
+            if int(os.environ.get("WORLD_SIZE", "1")) == 1 and "MASTER_ADDR" not in os.environ:
+                return cls.local()
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            kw = {}
+            if backend == "nccl":
+                local = int(os.environ.get("LOCAL_RANK", "0"))
+                torch.cuda.set_device(local)
+                kw["device_id"] = torch.device("cuda", local)
+            dist.init_process_group(backend, **kw)
+        return cls()
+
+    # ---------------------------------------------------------------- basics
+    def barrier(self) -> None:
+        if self.enabled:
+            dist.barrier(group=self.group)
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.enabled:
+            ops = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+            dist.all_reduce(t, op=ops[op], group=self.group)
+        return t
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.enabled:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate equal-shaped tensors from every rank along dim 0."""
+        if not self.enabled:
+            return t
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def all_gather_object(self, obj) -> List:
+        if not self.enabled:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    # ---------------------------------------------------------------- all-to-all-v
+    def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
+        if not self.enabled:
+            return send_counts.clone()
+        recv = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv, send_counts, group=self.group)
+        return recv
+
+    def all_to_all_v(self, t: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]) -> torch.Tensor:
+        """Rows of ``t`` are grouped by destination rank (send_counts[r] rows
+        for rank r, in rank order); returns rows received, grouped by source."""
+        if not self.enabled:
+            return t
+        out = torch.empty((int(sum(recv_counts)),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_to_all_single(out, t.contiguous(), output_split_sizes=list(map(int, recv_counts)),
+                               input_split_sizes=list(map(int, send_counts)), group=self.group)
+        return out
+
+    def reshard(self, dest: torch.Tensor, *fields: torch.Tensor) -> Tuple[torch.Tensor, ...]:
+        """Route every row of each field to rank ``dest[row]`` (C3). Returns the
+        fields as received on this rank (grouped by source rank, original
+        relative order preserved)."""
+        order = torch.argsort(dest, stable=True)
+        counts = torch.bincount(dest.long(), minlength=self.world).to(torch.int64)
+        sc = counts.to(self.device)
+        rc = self.exchange_counts(sc)
+        s_list, r_list = counts.tolist(), rc.cpu().tolist()
+        return tuple(self.all_to_all_v(f[order.to(f.device)], s_list, r_list) for f in fields)

@@ -1,0 +1,121 @@
+"""Graph kernels (csrc/kernels/graph.hip) vs their torch/host references."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from lazzaro_amd.index.device_graph import DeviceGraph  # noqa: E402
+from lazzaro_amd.index.kmeans import kmeans  # noqa: E402
+from lazzaro_amd.ops import graph_ops as G  # noqa: E402
+
+DEV = "cuda"
+
+
+def _rand_edges(n, ne, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    src = torch.randint(0, n, (ne,), generator=g, dtype=torch.int32)
+    dst = torch.randint(0, n, (ne,), generator=g, dtype=torch.int32)
+    w = torch.rand(ne, generator=g)
+    e = {"src": src, "dst": dst, "w": w, "co": torch.arange(ne, dtype=torch.int32),
+         "lu": torch.rand(ne, generator=g, dtype=torch.float64)}
+    return {k: v.to(dev) for k, v in e.items()}
+
+
+@pytest.mark.parametrize("ne", [0, 1, 1000, 300_001])
+def test_decay_prune_gpu(ne):
+    n = 5000
+    ec, eg = _rand_edges(n, ne, 1, "cpu"), _rand_edges(n, ne, 1, DEV)
+    alive = (torch.rand(n, generator=torch.Generator().manual_seed(2)) > 0.1).to(torch.uint8)
+    sc = torch.rand(n, generator=torch.Generator().manual_seed(3))
+    sg = sc.to(DEV)
+    oc, pc = G.decay_prune(ec, sc, alive, 0.05, 0.4)
+    og, pg = G.decay_prune(eg, sg, alive.to(DEV), 0.05, 0.4)
+    assert pc == pg
+    for k in oc:
+        assert torch.equal(oc[k], og[k].cpu()), k
+    assert torch.allclose(sc, sg.cpu())
+
+
+def test_importance_select_and_drop_dead_gpu():
+    n = 10000
+    g = torch.Generator().manual_seed(5)
+    sal, acc = torch.rand(n, generator=g), torch.randint(0, 20, (n,), generator=g, dtype=torch.int32)
+    last = torch.rand(n, generator=g, dtype=torch.float64) * 1e6
+    prot = (torch.rand(n, generator=g) > 0.95).to(torch.uint8)
+    sc = G.importance(sal, acc, last, None, prot, 2e6)
+    sg = G.importance(sal.to(DEV), acc.to(DEV), last.to(DEV), None, prot.to(DEV), 2e6)
+    assert torch.allclose(sc, sg.cpu(), rtol=1e-6)
+    vc, vg = G.select_lowest(sc, 777), G.select_lowest(sg, 777)
+    assert torch.equal(vc, vg.cpu())
+    alive = torch.ones(n, dtype=torch.uint8, device=DEV)
+    G.mark_dead(alive, vg)
+    e = _rand_edges(n, 50000, 9, DEV)
+    out = G.drop_dead_edges(e, alive)
+    a = alive.cpu().bool()
+    m = a[e["src"].cpu().long()] & a[e["dst"].cpu().long()]
+    assert torch.equal(out["src"].cpu(), e["src"].cpu()[m])
+
+
+@pytest.mark.parametrize("n,ne", [(10, 5), (20000, 15000), (100000, 300000)])
+def test_connected_components_gpu(n, ne):
+    e = _rand_edges(n, ne, 11, "cpu")
+    ref = G.connected_components(e["src"], e["dst"], n, e["w"], 0.3)
+    got = G.connected_components(e["src"].to(DEV), e["dst"].to(DEV), n, e["w"].to(DEV), 0.3)
+    assert torch.equal(ref.to(torch.int32), got.cpu())
+
+
+def test_chain_components_gpu():
+    n = 200000
+    s = torch.arange(n - 1, dtype=torch.int32, device=DEV)
+    lab = G.connected_components(s, s + 1, n)
+    assert int(lab.max()) == 0
+
+
+def test_pairs_above_gpu():
+    g = torch.Generator().manual_seed(3)
+    base = torch.nn.functional.normalize(torch.randn(200, 128, generator=g), dim=1)
+    X = torch.cat([base, base[:50] + 0.01 * torch.randn(50, 128, generator=g)])
+    X = torch.nn.functional.normalize(X, dim=1).to(torch.bfloat16)
+    ref = G.pairs_above(X.float(), 0.95)
+    got = G.pairs_above(X.to(DEV), 0.95).cpu()
+    assert torch.equal(ref, got) and got.shape[0] >= 50
+
+
+def test_centroids_gpu():
+    g = torch.Generator().manual_seed(4)
+    X = torch.nn.functional.normalize(torch.randn(5000, 256, generator=g), dim=1).to(torch.bfloat16)
+    lab = torch.randint(-1, 37, (5000,), generator=g, dtype=torch.int32)
+    c, _, cnt = G.centroids(X.float(), lab, 37)
+    cg, c16, cntg = G.centroids(X.to(DEV), lab.to(DEV), 37, pad_to=256)
+    assert torch.equal(cnt, cntg.cpu()) and torch.allclose(c, cg.cpu(), atol=1e-5)
+
+
+def test_device_graph_gpu_matches_cpu():
+    torch.manual_seed(0)
+    D = 64
+    base = torch.nn.functional.normalize(torch.randn(3000, D), dim=1)
+    shard = torch.randint(0, 5, (3000,))
+    facts = torch.nn.functional.normalize(base[:40] + 0.4 * torch.randn(40, D), dim=1)
+    facts[:5] = base[100:105]
+    fs = torch.randint(0, 5, (40,))
+    res = []
+    for dev in ("cpu", DEV):
+        g = DeviceGraph(D, device=dev)
+        g.add_nodes(base.to(dev), shard.to(dev), torch.full((3000,), 0.5, device=dev), now=1.0)
+        out = g.ingest(facts.to(dev), fs.to(dev), torch.full((40,), 0.7, device=dev), now=2.0)
+        p = g.decay_prune(0.01, 0.5)
+        ev = g.enforce_limit(2900, now=3.0)
+        res.append((out, p, ev, g.num_edges))
+    assert res[0][0]["deduped"] == res[1][0]["deduped"] == 5
+    assert abs(res[0][0]["linked"] - res[1][0]["linked"]) <= 2  # bf16 threshold ties
+    assert res[0][2] == res[1][2]
+
+
+def test_kmeans_gpu():
+    torch.manual_seed(1)
+    centers = torch.nn.functional.normalize(torch.randn(16, 128), dim=1)
+    X = torch.cat([torch.nn.functional.normalize(c + 0.05 * torch.randn(500, 128), dim=1) for c in centers])
+    c32, c16, lab = kmeans(X.to(DEV).to(torch.bfloat16), 16, iters=6)
+    lab = lab.cpu()
+    for j in range(16):
+        assert len(set(lab[j * 500:(j + 1) * 500].tolist())) == 1

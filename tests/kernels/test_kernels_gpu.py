@@ -1,0 +1,117 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same
+op (the CPU path of each op). Runs on the MI355X box (`pytest -m gpu`)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from lazzaro_amd.ops import _lib  # noqa: E402
+from lazzaro_amd.ops import encoder_ops as E  # noqa: E402
+from lazzaro_amd.ops.search import _ref_topk, flat_topk  # noqa: E402
+
+DEV = "cuda"
+
+
+def test_native_library_is_loaded():
+    L = _lib.lib()
+    assert L is not None and _lib.available()
+
+
+@pytest.mark.parametrize("n,d,nq,k,bias,label", [
+    (1000, 64, 7, 5, False, False), (5000, 768, 130, 10, True, False), (33333, 384, 257, 16, False, True),
+    (20000, 1536, 64, 1, True, True), (300, 128, 1, 3, False, False), (129, 64, 129, 8, True, False),
+])
+def test_flat_topk_matches_reference(n, d, nq, k, bias, label):
+    g = torch.Generator(device=DEV).manual_seed(n)
+    X = torch.randn(n, d, device=DEV, generator=g).to(torch.bfloat16)
+    Q = torch.randn(nq, d, device=DEV, generator=g).to(torch.bfloat16)
+    b = torch.randn(n, device=DEV, generator=g) if bias else None
+    rl = torch.randint(0, 3, (n,), device=DEV, dtype=torch.int32, generator=g) if label else None
+    ql = torch.randint(-1, 3, (nq,), device=DEV, dtype=torch.int32, generator=g) if label else None
+    a = 2.0 if bias else 1.0
+    s, i = flat_topk(X, Q, k, bias=b, row_label=rl, q_label=ql, alpha=a)
+    rs, ri = _ref_topk(X.cpu(), Q.cpu(), k, None if b is None else b.cpu(),
+                       None if rl is None else rl.cpu(), None if ql is None else ql.cpu(), a)
+    torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
+    assert (i.cpu() == ri).float().mean() > 0.995  # ulp-level ties may swap
+
+
+def test_flat_topk_tombstones_and_chunks():
+    X = torch.randn(4096, 128, device=DEV).to(torch.bfloat16)
+    bias = torch.zeros(4096, device=DEV)
+    bias[::2] = float("-inf")
+    Q = X[:5].clone()
+    s, i = flat_topk(X, Q, 4, bias=bias, n_chunks=7)
+    assert (i % 2 == 1).all()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("T,N,K,act,res", [(300, 768, 768, "none", False), (64, 2304, 768, "none", False),
+                                           (257, 3072, 768, "gelu", False), (129, 768, 3072, "none", True),
+                                           (1000, 384, 384, "gelu", True)])
+def test_linear(T, N, K, act, res):
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(T, N, device=DEV).to(torch.bfloat16) if res else None
+    y = E.linear(x, w, b, act=act, residual=r)
+    yr = E.linear(x.cpu(), w.cpu(), b.cpu(), act=act, residual=None if r is None else r.cpu())
+    assert _rel(y.cpu(), yr) < 1e-2
+
+
+@pytest.mark.parametrize("B,S,heads,hd", [(3, 40, 12, 64), (2, 32, 4, 64), (5, 70, 12, 32), (1, 130, 16, 64)])
+def test_attention(B, S, heads, hd):
+    H = heads * hd
+    qkv = torch.randn(B * S, 3 * H, device=DEV).to(torch.bfloat16)
+    lens = torch.randint(2, S + 1, (B,), dtype=torch.int32)
+    lens[0] = S
+    o = E.attention(qkv, lens.to(DEV), B, S, heads).cpu().float().view(B, S, H)
+    ref = E.attention(qkv.cpu(), lens, B, S, heads).float().view(B, S, H)
+    for bi in range(B):
+        L = int(lens[bi])
+        assert _rel(o[bi, :L], ref[bi, :L]) < 1e-2
+
+
+def test_layernorm_and_embed_and_pool():
+    T, H = 333, 768
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    r = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    g = torch.rand(H, device=DEV) + 0.5
+    b = torch.randn(H, device=DEV)
+    y = E.layernorm(x, g, b, 1e-12, residual=r)
+    yr = E.layernorm(x.cpu(), g.cpu(), b.cpu(), 1e-12, residual=r.cpu())
+    assert _rel(y.cpu(), yr) < 1e-2
+    V, S, B = 1000, 37, 9
+    we = torch.randn(V, H, device=DEV).to(torch.bfloat16)
+    pe = torch.randn(64, H, device=DEV).to(torch.bfloat16)
+    te = torch.randn(2, H, device=DEV).to(torch.bfloat16)
+    ids = torch.randint(0, V, (B * S,), dtype=torch.int32, device=DEV)
+    e = E.embed_ln(ids, S, we, pe, te, g, b)
+    er = E.embed_ln(ids.cpu(), S, we.cpu(), pe.cpu(), te.cpu(), g.cpu(), b.cpu())
+    assert _rel(e.cpu(), er) < 1e-2
+    lens = torch.randint(1, S + 1, (B,), dtype=torch.int32)
+    for mode in ("mean", "cls"):
+        p32, p16 = E.pool_norm(e, lens.to(DEV), B, S, mode, out16_width=832)
+        r32, r16 = E.pool_norm(er, lens, B, S, mode, out16_width=832)
+        assert _rel(p32.cpu(), r32) < 1e-3
+        assert torch.allclose(p32.norm(dim=1).cpu(), torch.ones(B), atol=1e-4)
+        assert (p16[:, H:] == 0).all()
+
+
+@pytest.mark.parametrize("model", ["tiny", "minilm-l6", "bge-base"])
+def test_encoder_forward_matches_cpu(model):
+    from lazzaro_amd.models.encoder import SentenceEncoder
+    gpu = SentenceEncoder(model, device=DEV, seed=3)
+    cpu = SentenceEncoder(model, device="cpu", seed=3)
+    B, S = 6, 24
+    ids = torch.randint(1000, gpu.cfg.vocab, (B, S), dtype=torch.int32)
+    lens = torch.tensor([24, 20, 3, 17, 24, 9], dtype=torch.int32)
+    a, _ = gpu.forward(ids, lens)
+    b, _ = cpu.forward(ids, lens)
+    cos = (a.cpu() * b).sum(1)
+    assert (cos > 0.99).all(), cos

@@ -1,0 +1,51 @@
+"""CPU tier of the encoder stack: tokenizer + reference forward shapes/norms."""
+import torch
+
+from lazzaro_amd.core.embedders import OnDeviceEmbedder, Tokenizer
+from lazzaro_amd.models.encoder import CONFIGS, SentenceEncoder, get_config
+
+
+def test_tokenizer_hashed_vocab_is_deterministic():
+    t = Tokenizer()
+    a = t.encode("Hello, World! I love Rust.")
+    assert a[0] == 101 and a[-1] == 102 and len(a) == 2 + 8
+    assert a == t.encode("hello , world ! i love rust .")
+    ids, lens = t.encode_batch(["a b c", "hello world"], 16)
+    assert ids.shape[0] == 2 and ids.shape[1] % 8 == 0 and lens.tolist() == [5, 4]
+    assert (ids[1, 4:] == 0).all()
+
+
+def test_tokenizer_wordpiece_with_vocab(tmp_path):
+    vocab = ["[PAD]"] + [f"[unused{i}]" for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]", "play", "##ing", "the"]
+    p = tmp_path / "vocab.txt"
+    p.write_text("\n".join(vocab))
+    t = Tokenizer(str(p))
+    assert t.encode("the playing xyz") == [101, 105, 103, 104, 100, 102]
+
+
+def test_configs():
+    assert get_config("BAAI/bge-base-en-v1.5").hidden == 768
+    assert get_config("all-MiniLM-L6-v2").heads * 32 == 384
+    assert get_config("e5-large-v2").layers == 24 and CONFIGS["bge-base"].pooling == "cls"
+
+
+def test_tiny_encoder_cpu_forward():
+    enc = SentenceEncoder("tiny", device="cpu")
+    ids = torch.randint(1000, 4096, (3, 16), dtype=torch.int32)
+    lens = torch.tensor([16, 5, 9], dtype=torch.int32)
+    v, v16 = enc.forward(ids, lens, pad_to=192)
+    assert v.shape == (3, 128) and torch.allclose(v.norm(dim=1), torch.ones(3), atol=1e-5)
+    assert v16.shape == (3, 192) and (v16[:, 128:] == 0).all()
+    # padding positions must not influence the result
+    ids2 = ids.clone()
+    ids2[1, 5:] = 1234
+    v2, _ = enc.forward(ids2, lens)
+    assert torch.allclose(v[1], v2[1], atol=1e-3)
+
+
+def test_on_device_embedder_cpu():
+    e = OnDeviceEmbedder("tiny", device="cpu")
+    out = e.batch_embed(["first text here", "second", "a much longer third text with more words"])
+    assert len(out) == 3 and len(out[0]) == 128
+    assert abs(sum(x * x for x in out[1]) - 1.0) < 1e-3
+    assert e.embed("second") == out[1] or max(abs(a - b) for a, b in zip(e.embed("second"), out[1])) < 1e-4
