@@ -5,7 +5,7 @@ SURVEY.md §2.4 K16/K8) and the coarse quantiser of the IVF-PQ index.
 assign: fused MFMA top-1 over the centroid matrix (``flat_topk`` with the
         centroids as the arena and the data as queries)
 update: segmented mean + L2 renormalisation (``graph_ops.centroids``)
-Distributed: with a process group, per-rank partial sums/counts are combined
+Distributed: with a :class:`~lazzaro_amd.parallel.Communicator`, per-rank partial sums/counts are combined
 with one all-reduce per iteration so every rank holds the
 same global centroids.
 """
@@ -14,7 +14,6 @@ from __future__ import annotations
 from typing import Optional, Tuple
 
 import torch
-import torch.distributed as dist
 
 from ..ops import graph_ops as G
 from ..ops.search import flat_topk
@@ -49,7 +48,7 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
     return c
 
 
-def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, group=None,
+def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
            init: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """X: unit rows [n, Dp] (bf16 on GPU). Returns (centroids fp32 [k, Dp],
     centroids bf16 [k, Dp], labels int32 [n])."""
@@ -60,9 +59,10 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, group=None,
     elif init is None:
         g = torch.Generator(device="cpu").manual_seed(seed)
         c32 = X[torch.randperm(n, generator=g)[:k].to(dev)].float()
+    distributed = comm is not None and comm.world > 1
     if init is None:
-        if group is not None and dist.is_initialized():
-            dist.broadcast(c32, src=0, group=group)
+        if distributed:
+            comm.broadcast(c32, src=0)
     else:
         c32 = init.float().to(dev)
     c32 = c32 / c32.norm(dim=1, keepdim=True).clamp_min(1e-30)
@@ -70,13 +70,13 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, group=None,
     lab = None
     for _ in range(iters):
         lab, _ = assign(X, c16)
-        if group is None or not dist.is_initialized():
+        if not distributed:
             c32, c16n, cnt = G.centroids(X, lab, k, normalize=True, pad_to=Dp if X.is_cuda else 0)
         else:
             c32u, _, cnt = G.centroids(X, lab, k, normalize=False)
             sums = c32u * cnt.clamp_min(1)[:, None].float()
-            dist.all_reduce(sums, group=group)
-            dist.all_reduce(cnt, group=group)
+            comm.all_reduce(sums)
+            comm.all_reduce(cnt)
             c32 = sums / cnt.clamp_min(1)[:, None].float()
             c32 = c32 / c32.norm(dim=1, keepdim=True).clamp_min(1e-30)
             c16n = None
