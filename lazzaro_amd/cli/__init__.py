@@ -1,0 +1,1 @@
+"""Interactive command-line interface."""

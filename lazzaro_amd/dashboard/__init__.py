@@ -1,0 +1,1 @@
+"""FastAPI dashboard (same routes as the reference, offline-capable page)."""

@@ -1,0 +1,204 @@
+"""Behavioural tests of the orchestrator against the reference semantics
+(SURVEY.md App. A/B/C): consolidation, linking, eviction, hierarchy, async
+mode, multi-tenancy, snapshots."""
+import json
+
+import numpy as np
+
+from lazzaro_amd.core.memory_system import MemorySystem
+from lazzaro_amd.core.providers import HashEmbedder, LocalLLM, ScriptedLLM
+from lazzaro_amd.models.graph import Edge, Node
+
+
+class VecEmbedder:
+    """Maps text -> preset vector (unit axis or given list) for exact control."""
+
+    def __init__(self, table, dim=8):
+        self.table, self.dim = table, dim
+
+    def _v(self, t):
+        v = self.table.get(t)
+        if v is None:
+            v = [0.0] * self.dim
+            v[hash(t) % self.dim] = 1.0
+        return list(v)
+
+    def embed(self, t):
+        return self._v(t)
+
+    def batch_embed(self, ts):
+        return [self._v(t) for t in ts]
+
+
+def facts_json(*facts):
+    return json.dumps({"memories": [dict(content=c, type="semantic", salience=s, topic=tp) for c, s, tp in facts]})
+
+
+def test_chain_and_similarity_links_then_prune():
+    a = [1, 0, 0, 0, 0, 0, 0, 0]
+    b = [0.9, 0.43589, 0, 0, 0, 0, 0, 0]  # cos(a,b)=0.9
+    emb = VecEmbedder({"User likes tea": a, "User likes green tea": b})
+    llm = ScriptedLLM([facts_json(("User likes tea", 0.6, "personal"), ("User likes green tea", 0.6, "personal"))])
+    ms = MemorySystem(llm_provider=llm, embedding_provider=emb, enable_async=False, load_from_disk=False,
+                      max_buffer_size=100)
+    ms.start_conversation()
+    ms.add_to_short_term("I like tea")
+    res = ms.end_conversation()
+    assert "Auto-pruned 1 weak edges" in res  # chain edge 0.5 -> 0.495 < 0.5
+    assert ms.buffer.size() == (2, 0)
+    ms.close()
+
+
+def test_within_shard_links_to_existing():
+    v = {f"User fact {i}": [1.0 if j == i else 0.0 for j in range(8)] for i in range(3)}
+    v["User new fact"] = [0.8, 0.6, 0, 0, 0, 0, 0, 0]
+    emb = VecEmbedder(v)
+    llm = ScriptedLLM([facts_json(*[(f"User fact {i}", 0.9, "work") for i in range(3)]),
+                       facts_json(("User new fact", 0.9, "work"))])
+    ms = MemorySystem(llm_provider=llm, embedding_provider=emb, enable_async=False, load_from_disk=False,
+                      max_buffer_size=100, auto_prune=False)
+    for _ in range(2):
+        ms.start_conversation()
+        ms.add_to_short_term("x")
+        ms.end_conversation()
+    sh = ms.shards["work"]
+    new_id = [n.id for n in sh.nodes.values() if n.content == "User new fact"][0]
+    w = {k: e.weight for k, e in sh.edges.items() if k[0] == new_id}
+    # cos 0.8 and 0.6 to facts 0 and 1 (> 0.5) -> weights 0.8*cos, decayed once
+    assert len(w) == 2
+    assert sorted(round(x, 4) for x in w.values()) == sorted(round(0.8 * c * 0.99, 4) for c in (0.8, 0.6))
+    assert [n.content for n in ms.get_connected_memories(new_id)] in (["User fact 0", "User fact 1"],
+                                                                      ["User fact 1", "User fact 0"])
+    ms.close()
+
+
+def test_buffer_limit_evicts_least_important():
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=False,
+                      load_from_disk=False, max_buffer_size=2)
+    for i, s in enumerate([0.9, 0.1, 0.5]):
+        n = Node(id=f"node_{i}", content=f"c{i}", embedding=[float(i + 1)] * 4, salience=s)
+        ms._get_or_create_shard("default").add_node(n)
+    ms.store.add_nodes([n.to_dict() for n in ms.shards["default"].nodes.values()], ms.user_id)
+    ms._enforce_buffer_limit()
+    assert set(ms.buffer.nodes) == {"node_0", "node_2"}
+    assert "node_1" not in ms.store.search_nodes([2.0] * 4, ms.user_id, limit=3)
+    ms.close()
+
+
+def test_super_nodes_and_hierarchical_retrieval():
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=64), enable_async=False,
+                      load_from_disk=False, max_buffer_size=1000, super_node_threshold=5)
+    emb = HashEmbedder(dim=64)
+    for i in range(7):
+        txt = f"User works on project alpha task {i}"
+        ms._get_or_create_shard("work").add_node(Node(id=f"node_{i+1}", content=txt, embedding=emb.embed(txt)))
+    ms.node_counter = 7
+    ms._create_super_nodes_for_shard("work")
+    assert len(ms.super_nodes) == 1
+    sup = next(iter(ms.super_nodes.values()))
+    assert sup.is_super_node and len(sup.child_ids) == 7
+    assert np.allclose(sup.embedding, np.mean([n.embedding for n in ms.shards["work"].nodes.values()], axis=0))
+    ms._create_super_nodes_for_shard("work")  # one per shard
+    assert len(ms.super_nodes) == 1
+    ids = ms._optimized_retrieval(emb.embed("project alpha task"), "project alpha task")
+    assert len(ids) == 5 and all(i in ms.shards["work"].nodes for i in ids)
+    ms.close()
+
+
+def test_async_consolidation_and_flush():
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=True,
+                      load_from_disk=False, max_buffer_size=100)
+    ms.start_conversation()
+    ms.chat("I started a new job at a robotics company today.")
+    r = ms.end_conversation()
+    assert "consolidation queued" in r
+    ms.flush()
+    assert ms.buffer.size()[0] >= 1 and ms.metrics["consolidation_times"]
+    ms.close()
+
+
+def test_switch_user_isolates_tenants():
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=False,
+                      user_id="alice", max_buffer_size=100)
+    ms.start_conversation()
+    ms.chat("My favorite color is green and I love sailing.")
+    ms.end_conversation()
+    n_alice = ms.buffer.size()[0]
+    assert n_alice >= 1
+    ms.switch_user("bob")
+    assert ms.buffer.size()[0] == 0 and ms.user_id == "bob"
+    assert ms.search_memories("sailing") == []
+    ms.switch_user("alice")
+    assert ms.buffer.size()[0] == n_alice
+    assert sorted(ms.get_all_users()) == ["alice"]
+    assert ms.search_memories("sailing green")
+    ms.close()
+
+
+def test_save_load_state_roundtrip(tmp_path):
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=False,
+                      load_from_disk=False)
+    ms._get_or_create_shard("work").add_node(Node(id="node_1", content="a", embedding=[1.0, 0.0]))
+    ms._get_or_create_shard("work").add_node(Node(id="node_2", content="b", embedding=[0.0, 1.0]))
+    ms.shards["work"].add_edge(Edge(source="node_1", target="node_2", weight=0.7))
+    ms.profile.update_domain("preferences", "tea")
+    ms.max_buffer_size = 42
+    p = str(tmp_path / "s.json")
+    ms.save_state(p)
+    ms2 = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), load_from_disk=False)
+    assert ms2.load_state(p) == f"✓ State loaded from {p}"
+    assert ms2.buffer.get_node("node_2").content == "b" and ms2.max_buffer_size == 42
+    assert ms2.buffer.get_neighbors("node_1") == ["node_2"] and ms2.profile.data["preferences"] == "tea"
+    assert ms2.load_state(str(tmp_path / "missing.json")).startswith("⚠ File")
+    ms.close()
+    ms2.close()
+
+
+def test_merge_modes():
+    def build(mode):
+        ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=False,
+                          load_from_disk=False, merge_mode=mode)
+        sh = ms._get_or_create_shard("default")
+        for i, v in enumerate([[1, 0], [1, 0.001], [0, 1], [1, 0]]):
+            sh.add_node(Node(id=f"node_{i}", content=f"c{i}", embedding=list(map(float, v)), access_count=1))
+        sh.add_edge(Edge(source="node_1", target="node_2", weight=0.9))
+        return ms
+    ms = build("reference")
+    assert ms._merge_similar_nodes() == 0  # reference no-op (indentation bug preserved)
+    ms = build("pairwise")
+    assert ms._merge_similar_nodes() == 2
+    n0 = ms.buffer.get_node("node_0")
+    assert n0.content == "c0 | c1 | c3" and n0.access_count == 3
+    assert ms.buffer.get_neighbors("node_0") == ["node_2"]
+
+
+def test_stats_and_exports():
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=False,
+                      load_from_disk=False)
+    ms.start_conversation()
+    ms.chat("I am learning Japanese from a book.")
+    ms.chat("I am learning Japanese from a book.")
+    s = ms.get_stats()
+    assert set(s) >= {"buffer_nodes", "buffer_edges", "num_shards", "num_super_nodes", "short_term_memories",
+                      "conversation_active", "conversation_count", "profile_domains_filled", "auto_consolidate",
+                      "vector_store", "performance"}
+    assert s["performance"]["cache_hit_rate"].endswith("%") and s["short_term_memories"] == 4
+    assert "SCALABLE MEMORY SYSTEM STATS" in ms.display_stats()
+    ms.end_conversation()
+    md = ms.export_observations()
+    assert md.startswith("# Memory Observations for default")
+    assert isinstance(json.loads(ms.export_observations("json")), list)
+    assert ms.get_insights()
+    assert "User Profile" in ms.display_profile()
+    ms.close()
+
+
+def test_run_consolidation_fallback_profile_from_contents():
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=False,
+                      load_from_disk=False)
+    for i, c in enumerate(["User loves jazz music.", "User prefers tea over coffee.", "User has 5 years of "
+                           "experience in Rust."]):
+        ms._get_or_create_shard("default").add_node(Node(id=f"n{i}", content=c, embedding=[1.0, float(i)]))
+    r = ms.run_consolidation()
+    assert "Updated profile domains" in r and ms.profile.data["preferences"]
+    ms.close()
