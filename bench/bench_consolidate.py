@@ -1,0 +1,197 @@
+"""Consolidation at scale (BASELINE.json config 4): a large episodic buffer whose
+topic shards are partitioned across the GPUs, consolidating batches of
+conversations end to end on device.
+
+One step (= ``--convs`` conversations per rank, ``--facts`` facts each):
+  1. embed the extracted fact texts with the on-device encoder (bge-base)
+  2. all-to-all: route every fact to the rank owning its topic shard (C3)
+  3. all-gather the routed facts; every rank scans its buffer shard with the
+     fused MFMA top-k (k=3) for all of them; all-gather the candidates and
+     merge (C1/K2) -> global dedupe (top-1 > 0.95) and cross-shard links
+  4. owner rank: insert non-duplicates, within-shard links (label-filtered
+     top-3), chain edges, duplicate merges (salience=max, access+1)
+  5. fused decay (0.99^convs) + prune (K10) and eviction to the buffer limit (K11)
+
+Fact *texts* are embedded (the cost is paid) but the vectors used for the
+graph are synthetic controlled ones (perturbations of existing memories with a
+fixed duplicate rate): random-init encoder weights give near-identical
+embeddings for every text, which would make dedupe degenerate.
+turns/sec = conversations consolidated per second over all ranks.
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from lazzaro_amd.index.device_graph import DeviceGraph  # noqa: E402
+from lazzaro_amd.ops.search import flat_topk  # noqa: E402
+from lazzaro_amd.parallel import Communicator  # noqa: E402
+from lazzaro_amd.parallel.sharded import merge_topk  # noqa: E402
+
+N_TOPICS = 64
+ROW_BITS = 40
+
+
+def _unit(x):
+    return x / x.norm(dim=1, keepdim=True).clamp_min(1e-30)
+
+
+class ShardedBuffer:
+    def __init__(self, comm: Communicator, dim: int, nodes_per_rank: int, device, seed: int = 0):
+        self.comm, self.dev = comm, device
+        self.g = DeviceGraph(dim, device=device, capacity=int(nodes_per_rank * 1.25) + 1024,
+                             edge_capacity=nodes_per_rank * 3)
+        gen = torch.Generator(device=device).manual_seed(seed + comm.rank)
+        step = 1 << 20
+        mine = torch.tensor([t for t in range(N_TOPICS) if t % comm.world == comm.rank], device=device)
+        for r0 in range(0, nodes_per_rank, step):
+            m = min(step, nodes_per_rank - r0)
+            v = _unit(torch.randn((m, dim), device=device, generator=gen))
+            topic = mine[torch.randint(0, mine.numel(), (m,), device=device, generator=gen)]
+            self.g.add_nodes(v, topic, torch.rand(m, device=device, generator=gen) * 0.8 + 0.2, now=0.0)
+        # sparse initial association graph
+        ne = nodes_per_rank * 2
+        src = torch.randint(0, nodes_per_rank, (ne,), device=device, generator=gen)
+        dst = torch.randint(0, nodes_per_rank, (ne,), device=device, generator=gen)
+        self.g.add_edges(src, dst, torch.rand(ne, device=device, generator=gen) * 0.5 + 0.5, now=0.0)
+        self.limit = int(nodes_per_rank * 1.1)
+        self.remote_edges = []
+
+    def owner(self, topic: torch.Tensor) -> torch.Tensor:
+        return topic % self.comm.world
+
+    def global_search(self, q: torch.Tensor, k: int):
+        """All-gather queries, local fused top-k, all-gather candidates, merge."""
+        comm = self.comm
+        nq = torch.tensor([q.shape[0]], device=self.dev)
+        sizes = comm.all_gather_rows(nq).tolist()
+        mx = max(sizes) if sizes else 0
+        qp = torch.zeros((mx, q.shape[1]), dtype=q.dtype, device=self.dev)
+        qp[: q.shape[0]] = q
+        allq = comm.all_gather_rows(qp)  # [world*mx, Dp]
+        n = self.g.n
+        s, r = flat_topk(self.g.emb[:n], allq, k, bias=self.g.bias[:n])
+        gid = torch.where(r >= 0, (comm.rank << ROW_BITS) + r, r)
+        S = comm.all_gather_rows(s).view(comm.world, comm.world * mx, k)
+        I = comm.all_gather_rows(gid).view(comm.world, comm.world * mx, k)
+        lo = comm.rank * mx
+        S = S[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
+        I = I[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
+        return merge_topk(S, I, k)
+
+    def consolidate(self, q: torch.Tensor, topic: torch.Tensor, sal: torch.Tensor, convs_total: int, now: float):
+        comm, g = self.comm, self.g
+        # (2) route facts to topic owners
+        if comm.world > 1:
+            q, topic, sal = comm.reshard(self.owner(topic), q, topic, sal)
+        # (3) global dedupe + cross-shard link candidates
+        s, gid = self.global_search(q, 3)
+        dup = (gid[:, 0] >= 0) & (s[:, 0] > 0.95)
+        local_dup = dup & ((gid[:, 0] >> ROW_BITS) == comm.rank)
+        rows = (gid[:, 0][local_dup] & ((1 << ROW_BITS) - 1))
+        if rows.numel():
+            g.sal.index_reduce_(0, rows, sal[local_dup].float(), "amax", include_self=True)
+            g.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
+            g.last[rows] = now
+        keep = ~dup
+        # (4) insert + links (within-shard via DeviceGraph.ingest, cross-shard from the global search)
+        n0 = g.n
+        out = g.ingest(q[keep], topic[keep], sal[keep], now=now, dedupe=False, global_links=False)
+        cross = (s[keep] > 0.5) & (gid[keep] >= 0) & ((gid[keep] >> ROW_BITS) != comm.rank)
+        n_cross = int(cross.sum().item())
+        if n_cross:  # cross-rank associations: local source row -> global target id
+            src = torch.arange(n0, g.n, device=self.dev)[:, None].expand(-1, 3)
+            self.remote_edges.append((src[cross], gid[keep][cross], s[keep][cross] * 0.8))
+        # (5) decay + prune + eviction
+        pruned = g.decay_prune(0.01, 0.5, conversations=convs_total)
+        evicted = g.enforce_limit(self.limit, now=now)
+        return {"routed": int(q.shape[0]), "dup": int(dup.sum().item()), "inserted": out["inserted"],
+                "linked": out["linked"] + n_cross, "pruned": pruned, "evicted": evicted}
+
+
+def synth_facts(buf: ShardedBuffer, n: int, dim: int, dup_rate: float, gen):
+    dev = buf.dev
+    g = buf.g
+    base_rows = torch.randint(0, g.n, (n,), device=dev, generator=gen)
+    base = g.emb[base_rows, :dim].float()
+    noise = torch.randn((n, dim), device=dev, generator=gen)
+    is_dup = torch.rand(n, device=dev, generator=gen) < dup_rate
+    q = torch.where(is_dup[:, None], _unit(base + 0.02 * noise), _unit(base + 1.2 * noise))
+    topic = torch.randint(0, N_TOPICS, (n,), device=dev, generator=gen).to(torch.int32)
+    sal = torch.rand(n, device=dev, generator=gen) * 0.5 + 0.5
+    Dp = g.emb.shape[1]
+    qp = torch.zeros((n, Dp), dtype=g.emb.dtype, device=dev)
+    qp[:, :dim] = q.to(g.emb.dtype)
+    return qp, topic, sal
+
+
+WORDS = "user likes prefers works lives started visited learned project team python rust garden music".split()
+
+
+def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int,
+        encoder=None, dim: int = 768, dup_rate: float = 0.1, seed: int = 7):
+    buf = ShardedBuffer(comm, dim, nodes, dev, seed)
+    gen = torch.Generator(device=dev).manual_seed(seed + 100 + comm.rank)
+    rng = random.Random(seed + comm.rank)
+    texts = [" ".join(rng.choice(WORDS) for _ in range(12)) for _ in range(convs * facts)]
+    now = [1000.0]
+
+    def step():
+        if encoder is not None:
+            ids, lens = encoder.tok.encode_batch(texts, 64)
+            encoder.encoder.forward(ids, lens, pad_to=buf.g.emb.shape[1])
+        q, topic, sal = synth_facts(buf, convs * facts, dim, dup_rate, gen)
+        now[0] += 60.0
+        return buf.consolidate(q, topic, sal, convs * comm.world, now[0])
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    comm.barrier()
+    t0 = time.perf_counter()
+    agg = {}
+    for _ in range(steps):
+        r = step()
+        for k, v in r.items():
+            agg[k] = agg.get(k, 0) + v
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    comm.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")
+    comm.all_reduce(t, "max")
+    el = float(t.item())
+    return {"turns_per_s": round(convs * comm.world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
+            "nodes_per_rank": nodes, "convs_per_rank_step": convs, "facts_per_conv": facts,
+            "buffer_nodes_total": nodes * comm.world, "edges_rank0": buf.g.num_edges, "per_step_rank0": {
+                k: round(v / steps, 1) for k, v in agg.items()}}
+
+
+if __name__ == "__main__":
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=12_500_000)
+    ap.add_argument("--convs", type=int, default=128)
+    ap.add_argument("--facts", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-embed", action="store_true")
+    a = ap.parse_args()
+    comm = Communicator.init()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    enc = None
+    if not a.no_embed and dev.type == "cuda":
+        from lazzaro_amd.core.embedders import OnDeviceEmbedder
+        enc = OnDeviceEmbedder("bge-base", device=dev, max_len=64)
+    res = run(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc)
+    if comm.rank == 0:
+        print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)

@@ -128,15 +128,24 @@ class DeviceGraph:
     # ------------------------------------------------------------------ ingest
     def ingest(self, q: torch.Tensor, shard: torch.Tensor, salience: torch.Tensor,
                now: Optional[float] = None, dedupe_thr: float = 0.95, link_k: int = 3,
-               link_thr: float = 0.5, link_scale: float = 0.8, chain_w: float = 0.5) -> Dict[str, int]:
-        """One consolidation batch of M facts (unit rows ``q`` [M, Dp])."""
+               link_thr: float = 0.5, link_scale: float = 0.8, chain_w: float = 0.5,
+               dedupe: bool = True, global_links: bool = True) -> Dict[str, int]:
+        """One consolidation batch of M facts (unit rows ``q`` [M, Dp]).
+        ``dedupe``/``global_links`` False when a sharded caller already did the
+        global search (see bench/bench_consolidate.py)."""
         now = time.time() if now is None else now
         q = q.to(self.emb.dtype)
         M = q.shape[0]
+        if M == 0:
+            return {"deduped": 0, "inserted": 0, "linked": 0}
         # K5 dedupe: top-1 over live rows
-        s1, r1 = self._search(q, 1)
-        s1, r1 = s1[:, 0], r1[:, 0]
-        dup = (r1 >= 0) & (s1 > dedupe_thr)
+        if dedupe:
+            s1, r1 = self._search(q, 1)
+            s1, r1 = s1[:, 0], r1[:, 0]
+            dup = (r1 >= 0) & (s1 > dedupe_thr)
+        else:
+            dup = torch.zeros(M, dtype=torch.bool, device=self.device)
+            r1 = torch.full((M,), -1, dtype=torch.long, device=self.device)
         if bool(dup.any()):
             rows = r1[dup]
             self.sal.index_reduce_(0, rows, salience.to(self.device)[dup].float(), "amax", include_self=True)
@@ -156,7 +165,11 @@ class DeviceGraph:
         # K6a within-shard: label-filtered top-k
         sw, rw = self._search(qn, link_k, row_label=self.shard[: self.n], q_label=sh, bias=old_bias)
         # K6b global top-k over all existing non-super rows
-        sg, rg = self._search(qn, link_k, bias=old_bias)
+        if global_links:
+            sg, rg = self._search(qn, link_k, bias=old_bias)
+        else:
+            sg = torch.full_like(sw, NEG_INF)
+            rg = torch.full_like(rw, -1)
         src = rows[:, None].expand(-1, link_k)
         mw = (rw >= 0) & (sw > link_thr)
         mg = (rg >= 0) & (sg > link_thr)
