@@ -123,7 +123,8 @@ def synth_facts(buf: ShardedBuffer, n: int, dim: int, dup_rate: float, gen):
     base = g.emb[base_rows, :dim].float()
     noise = torch.randn((n, dim), device=dev, generator=gen)
     is_dup = torch.rand(n, device=dev, generator=gen) < dup_rate
-    q = torch.where(is_dup[:, None], _unit(base + 0.02 * noise), _unit(base + 1.2 * noise))
+    noise = noise / (dim ** 0.5)  # unit-scale perturbation: cos ~0.995 (dup) / ~0.64 (related)
+    q = torch.where(is_dup[:, None], _unit(base + 0.1 * noise), _unit(base + 1.2 * noise))
     topic = torch.randint(0, N_TOPICS, (n,), device=dev, generator=gen).to(torch.int32)
     sal = torch.rand(n, device=dev, generator=gen) * 0.5 + 0.5
     Dp = g.emb.shape[1]

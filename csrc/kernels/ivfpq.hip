@@ -1,0 +1,159 @@
+// IVF-PQ scan (BASELINE config 5: an index that fills the
+// 288 GB of HBM per GPU). LanceDB can build IVF-PQ but the reference never does
+// (vector_store.py:55 only builds a scalar index); this is the MI355X design:
+//
+//   * inverted lists: PQ codes of one list are contiguous [rows][M] uint8
+//     (CSR offsets), ids kept alongside;
+//   * inner-product metric with PQ on coarse residuals, so the lookup table
+//     LUT[j][c] = <q_j, codebook_j[c]> depends on the query only (one LUT per
+//     query, reused by all nprobe lists) and score = <q, centroid> + sum_j LUT;
+//   * one workgroup per (query, probed list): the query's fp32 LUT (M x 256,
+//     64 KiB at M = 64) is staged once in LDS, each thread scores whole code
+//     rows (16-byte code loads, LDS gathers) into a register top-K, then the
+//     256 per-thread lists are reduced by wave argmax rounds + one 4-way merge;
+//   * partial lists go through the shared topk_merge kernel (search.hip).
+#include "lzk_common.h"
+
+namespace {
+
+template <int K>
+struct LaneTopK {
+  float s[K];
+  int i[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { s[j] = LZK_NEG_INF; i[j] = -1; }
+  }
+  __device__ __forceinline__ void push(float v, int r) {  // r increases per thread
+    if (v > s[K - 1]) {
+#pragma unroll
+      for (int j = K - 1; j > 0; --j) {
+        bool up = v > s[j - 1], here = v > s[j];
+        float ns = up ? s[j - 1] : (here ? v : s[j]);
+        int ni = up ? i[j - 1] : (here ? r : i[j]);
+        s[j] = ns; i[j] = ni;
+      }
+      if (v > s[0]) { s[0] = v; i[0] = r; }
+    }
+  }
+};
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void ivfpq_scan_kernel(const unsigned char* __restrict__ codes,
+                                                         const long* __restrict__ list_off,
+                                                         const int* __restrict__ probes,
+                                                         const float* __restrict__ coarse,
+                                                         const float* __restrict__ lut, int nprobe,
+                                                         float* __restrict__ out_s, int* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) float slut[];  // [M][256]
+  __shared__ float ws[4 * K];
+  __shared__ int wi[4 * K];
+  const int qp = blockIdx.x;  // query * nprobe + p
+  const int q = qp / nprobe;
+  const int list = probes[qp];
+  const float base = coarse[qp];
+  const float* L = lut + (long)q * M * 256;
+  for (int t = threadIdx.x * 4; t < M * 256; t += 256 * 4)
+    *reinterpret_cast<f32x4*>(slut + t) = *reinterpret_cast<const f32x4*>(L + t);
+  __syncthreads();
+  LaneTopK<K> top;
+  top.init();
+  const long r0 = (list >= 0) ? list_off[list] : 0, r1 = (list >= 0) ? list_off[list + 1] : 0;
+  for (long r = r0 + threadIdx.x; r < r1; r += 256) {
+    const unsigned char* c = codes + r * M;
+    float s = base;
+#pragma unroll
+    for (int j0 = 0; j0 < M; j0 += 16) {
+      uint4 v = *reinterpret_cast<const uint4*>(c + j0);
+      unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int code = (w[u >> 2] >> (8 * (u & 3))) & 0xff;
+        s += slut[(j0 + u) * 256 + code];
+      }
+    }
+    top.push(s, (int)r);
+  }
+  // wave-level K rounds of argmax over the 64 lane lists
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int j = 0; j < K; ++j) {
+    float hs = top.s[0];
+    int hi = top.i[0] < 0 ? 0x7fffffff : top.i[0];
+    float bs = hs;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      float s2 = __shfl_xor(bs, o, 64);
+      int i2 = __shfl_xor(bi, o, 64);
+      if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) { ws[wv * K + j] = bs; wi[wv * K + j] = bi; }
+    if (hi == bi && hs == bs && bi != 0x7fffffff) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) { top.s[t] = top.s[t + 1]; top.i[t] = top.i[t + 1]; }
+      top.s[K - 1] = LZK_NEG_INF; top.i[K - 1] = -1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int p[4] = {0, 0, 0, 0};
+    for (int j = 0; j < K; ++j) {
+      int w = -1;
+      float bsv = LZK_NEG_INF;
+      int biv = 0x7fffffff;
+      for (int a = 0; a < 4; ++a) {
+        if (p[a] >= K) continue;
+        float s = ws[a * K + p[a]];
+        int i = wi[a * K + p[a]];
+        if (w < 0 || better(s, i, bsv, biv)) { w = a; bsv = s; biv = i; }
+      }
+      p[w] += 1;
+      out_s[(long)qp * K + j] = bsv;
+      out_i[(long)qp * K + j] = (biv == 0x7fffffff || bsv == LZK_NEG_INF) ? -1 : biv;
+    }
+  }
+}
+
+template <int K>
+hipError_t launch_scan(int M, const unsigned char* codes, const long* off, const int* probes, const float* coarse,
+                       const float* lut, int nq, int nprobe, float* os, int* oi, hipStream_t st) {
+  dim3 grid(nq * nprobe), block(256);
+  size_t lds = (size_t)M * 256 * sizeof(float);
+#define GO(MM)                                                                                                      \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)ivfpq_scan_kernel<K, MM>, hipFuncAttributeMaxDynamicSharedMemorySize,   \
+                              (int)lds);                                                                            \
+    hipLaunchKernelGGL((ivfpq_scan_kernel<K, MM>), grid, block, lds, st, codes, off, probes, coarse, lut, nprobe,  \
+                       os, oi);                                                                                     \
+  } while (0)
+  switch (M) {
+    case 16: GO(16); break;
+    case 32: GO(32); break;
+    case 48: GO(48); break;
+    case 64: GO(64); break;
+    case 96: GO(96); break;
+    case 128: GO(128); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef GO
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// partial lists: [nq, nprobe, kslot] (rows index the code array; -1 = empty)
+LZK_EXPORT int lzk_ivfpq_scan(const void* codes, const long* list_off, const int* probes, const float* coarse,
+                              const float* lut, int nq, int nprobe, int M, int kslot, float* os, int* oi,
+                              void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned char* c = (const unsigned char*)codes;
+  hipError_t e;
+  switch (kslot) {
+    case 1: e = launch_scan<1>(M, c, list_off, probes, coarse, lut, nq, nprobe, os, oi, st); break;
+    case 4: e = launch_scan<4>(M, c, list_off, probes, coarse, lut, nq, nprobe, os, oi, st); break;
+    case 10: e = launch_scan<10>(M, c, list_off, probes, coarse, lut, nq, nprobe, os, oi, st); break;
+    case 16: e = launch_scan<16>(M, c, list_off, probes, coarse, lut, nq, nprobe, os, oi, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)e;
+}

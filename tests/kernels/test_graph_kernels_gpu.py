@@ -119,3 +119,26 @@ def test_kmeans_gpu():
     lab = lab.cpu()
     for j in range(16):
         assert len(set(lab[j * 500:(j + 1) * 500].tolist())) == 1
+
+
+def test_ivfpq_gpu_scan_matches_reference():
+    from lazzaro_amd.index.ivfpq import IVFPQIndex, recall_at_k
+    g = torch.Generator().manual_seed(0)
+    d, n = 128, 20000
+    c = torch.nn.functional.normalize(torch.randn(64, d, generator=g), dim=1)
+    x = torch.nn.functional.normalize(c[torch.randint(0, 64, (n,), generator=g)] + 0.1 * torch.randn(n, d, generator=g), dim=1)
+    q = x[:50] + 0.01 * torch.randn(50, d, generator=g)
+    gi = IVFPQIndex(d, nlist=64, m=32, device=DEV, keep_vectors=True)
+    gi.train(x, iters=5, pq_iters=5)
+    gi.add(x)
+    gi._finalize()
+    ci = IVFPQIndex(d, nlist=64, m=32, device="cpu")
+    ci.centroids, ci.codebooks = gi.centroids.cpu(), gi.codebooks.cpu()
+    ci.codes, ci.ids, ci.list_of, ci.list_off = gi.codes.cpu(), gi.ids.cpu(), gi.list_of.cpu(), gi.list_off.cpu()
+    s1, i1 = gi.search(q, 10, nprobe=8)
+    s2, i2 = ci.search(q, 10, nprobe=8)
+    torch.testing.assert_close(s1.cpu(), s2, atol=1e-4, rtol=1e-4)
+    assert (i1.cpu() == i2).float().mean() > 0.98
+    truth = torch.topk(torch.nn.functional.normalize(q, dim=1) @ x.T, 10, dim=1).indices
+    _, i3 = gi.search(q, 10, nprobe=16, rerank=16)
+    assert recall_at_k(i3, truth) > 0.8
