@@ -42,9 +42,10 @@ def main():
     ap.add_argument("--train", type=int, default=262144)
     ap.add_argument("--model", default="e5-large")
     ap.add_argument("--nprobes", default="16,32,64")
+    ap.add_argument("--rerank", type=int, default=256, help="re-rank depth over kept bf16 rows (0 = PQ only)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    idx = IVFPQIndex(a.dim, nlist=a.nlist, m=a.m, device=dev)
+    idx = IVFPQIndex(a.dim, nlist=a.nlist, m=a.m, device=dev, keep_vectors=a.rerank > 0)
     flat = torch.empty((a.n, a.dim), dtype=torch.bfloat16, device=dev)
     t0 = time.time()
     r0 = 0
@@ -82,16 +83,17 @@ def main():
     _, truth = flat_topk(flat, q.to(torch.bfloat16), 10)
     res = []
     for nprobe in map(int, a.nprobes.split(",")):
-        idx.search(q, 10, nprobe=nprobe)
-        torch.cuda.synchronize()
-        t1 = time.time()
-        for _ in range(5):
-            s, ids = idx.search(q, 10, nprobe=nprobe)
-        torch.cuda.synchronize()
-        dt = (time.time() - t1) / 5
-        res.append({"nprobe": nprobe, "ms": round(dt * 1e3, 3), "qps_search": round(a.nq / dt, 1),
-                    "qps_end_to_end": round(a.nq / (dt + t_embed), 1),
-                    "recall_at_10": round(recall_at_k(ids, truth), 4)})
+        for rr in sorted({0, a.rerank}):
+            idx.search(q, 10, nprobe=nprobe, rerank=rr)
+            torch.cuda.synchronize()
+            t1 = time.time()
+            for _ in range(5):
+                s, ids = idx.search(q, 10, nprobe=nprobe, rerank=rr)
+            torch.cuda.synchronize()
+            dt = (time.time() - t1) / 5
+            res.append({"nprobe": nprobe, "rerank": rr, "ms": round(dt * 1e3, 3), "qps_search": round(a.nq / dt, 1),
+                        "qps_end_to_end": round(a.nq / (dt + t_embed), 1),
+                        "recall_at_10": round(recall_at_k(ids, truth), 4)})
     per_vec = a.m + 8
     out = {"metric": "IVF-PQ search QPS @ recall@10", "n": a.n, "dim": a.dim, "nlist": a.nlist, "m": a.m,
            "bytes_per_vector": per_vec, "projected_vectors_in_288GB": int(288e9 / per_vec),

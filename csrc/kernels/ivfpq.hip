@@ -114,6 +114,43 @@ __global__ __launch_bounds__(256) void ivfpq_scan_kernel(const unsigned char* __
   }
 }
 
+// Dense variant for deep candidate lists (re-rank depth >> 16): every scanned
+// row's PQ score is written to out[(query*nprobe + p) * maxlen + pos]; slots
+// past a list's end are -inf. A library top-k over the row then picks k'.
+template <int M>
+__global__ __launch_bounds__(256) void ivfpq_dense_kernel(const unsigned char* __restrict__ codes,
+                                                          const long* __restrict__ list_off,
+                                                          const int* __restrict__ probes,
+                                                          const float* __restrict__ coarse,
+                                                          const float* __restrict__ lut, int nprobe, int maxlen,
+                                                          float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float slut[];
+  const int qp = blockIdx.x;
+  const int q = qp / nprobe;
+  const int list = probes[qp];
+  const float base = coarse[qp];
+  const float* L = lut + (long)q * M * 256;
+  for (int t = threadIdx.x * 4; t < M * 256; t += 256 * 4)
+    *reinterpret_cast<f32x4*>(slut + t) = *reinterpret_cast<const f32x4*>(L + t);
+  __syncthreads();
+  const long r0 = (list >= 0) ? list_off[list] : 0, r1 = (list >= 0) ? list_off[list + 1] : 0;
+  const long n = min((long)maxlen, r1 - r0);
+  float* o = out + (long)qp * maxlen;
+  for (long p = threadIdx.x; p < maxlen; p += 256) {
+    if (p >= n) { o[p] = LZK_NEG_INF; continue; }
+    const unsigned char* c = codes + (r0 + p) * M;
+    float s = base;
+#pragma unroll
+    for (int j0 = 0; j0 < M; j0 += 16) {
+      uint4 v = *reinterpret_cast<const uint4*>(c + j0);
+      unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += slut[(j0 + u) * 256 + ((w[u >> 2] >> (8 * (u & 3))) & 0xff)];
+    }
+    o[p] = s;
+  }
+}
+
 template <int K>
 hipError_t launch_scan(int M, const unsigned char* codes, const long* off, const int* probes, const float* coarse,
                        const float* lut, int nq, int nprobe, float* os, int* oi, hipStream_t st) {
@@ -140,6 +177,32 @@ hipError_t launch_scan(int M, const unsigned char* codes, const long* off, const
 }
 
 }  // namespace
+
+LZK_EXPORT int lzk_ivfpq_dense(const void* codes, const long* list_off, const int* probes, const float* coarse,
+                               const float* lut, int nq, int nprobe, int M, int maxlen, float* out, void* stream) {
+  dim3 grid(nq * nprobe), block(256);
+  size_t lds = (size_t)M * 256 * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned char* c = (const unsigned char*)codes;
+#define GO(MM)                                                                                                       \
+  do {                                                                                                               \
+    (void)hipFuncSetAttribute((const void*)ivfpq_dense_kernel<MM>, hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                              (int)lds);                                                                             \
+    hipLaunchKernelGGL((ivfpq_dense_kernel<MM>), grid, block, lds, st, c, list_off, probes, coarse, lut, nprobe,    \
+                       maxlen, out);                                                                                 \
+  } while (0)
+  switch (M) {
+    case 16: GO(16); break;
+    case 32: GO(32); break;
+    case 48: GO(48); break;
+    case 64: GO(64); break;
+    case 96: GO(96); break;
+    case 128: GO(128); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef GO
+  return (int)hipGetLastError();
+}
 
 // partial lists: [nq, nprobe, kslot] (rows index the code array; -1 = empty)
 LZK_EXPORT int lzk_ivfpq_scan(const void* codes, const long* list_off, const int* probes, const float* coarse,

@@ -33,6 +33,7 @@ import numpy as np
 
 from ..models.graph import Edge, Node
 from .similarity import topk_cosine
+from ..utils.tracing import tracer
 
 EXTRACTION_PROMPT = """Extract distinct, atomic facts from this conversation.
 Categorization Guidelines:
@@ -150,6 +151,20 @@ class ConsolidationMixin:
         n, e = self.buffer.size()
         return f"✓ Consolidation complete. Memory: {n} nodes, {e} edges"
 
+    def _side_stream(self):
+        """Background consolidation runs on its own HIP stream so its kernels
+        overlap the caller's retrieval kernels (SURVEY.md §2.6 async row)."""
+        import contextlib
+
+        import torch
+
+        dev = self._device
+        if dev is None or getattr(dev, "type", "cpu") != "cuda" or not torch.cuda.is_available():
+            return contextlib.nullcontext()
+        if getattr(self, "_cstream", None) is None:
+            self._cstream = torch.cuda.Stream(device=dev)
+        return torch.cuda.stream(self._cstream)
+
     def flush(self, timeout: float = None) -> None:
         """Block until queued background consolidations have finished."""
         pend, self._pending = self._pending, []
@@ -165,10 +180,11 @@ class ConsolidationMixin:
         t0 = time.time()
         memories = [m for b in batches for m in b["memories"]]
         self._say(f"🔄 Processing {len(memories)} memories in background...")
-        response = self._call_llm(
-            [{"role": "system", "content": EXTRACTION_PROMPT},
-             {"role": "user", "content": json.dumps(memories)}],
-            response_format={"type": "json_object"})
+        with tracer.stage("extract_llm", "cpu"):
+            response = self._call_llm(
+                [{"role": "system", "content": EXTRACTION_PROMPT},
+                 {"role": "user", "content": json.dumps(memories)}],
+                response_format={"type": "json_object"})
         try:
             data = _parse_json(response)
         except (json.JSONDecodeError, TypeError) as e:
@@ -184,9 +200,11 @@ class ConsolidationMixin:
         facts = [m for m in facts if isinstance(m, dict)] if isinstance(facts, list) else []
         self._say(f"✓ Extracted {len(facts)} memory candidates")
         kept = [m for m in facts if m.get("content") and len(m.get("content", "")) >= MIN_FACT_LEN]
-        embs = self._batch_embed([m["content"] for m in kept]) if kept else []
-        with self._graph_lock:
-            self._ingest_facts(kept, embs)
+        with self._side_stream():
+            with tracer.stage("embed_facts", self._device):
+                embs = self._batch_embed([m["content"] for m in kept]) if kept else []
+            with self._graph_lock, tracer.stage("ingest", self._device):
+                self._ingest_facts(kept, embs)
         elapsed = time.time() - t0
         self.metrics["consolidation_times"].append(elapsed)
         self._say(f"✓ Background consolidation complete ({elapsed:.2f}s)")

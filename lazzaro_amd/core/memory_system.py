@@ -40,6 +40,7 @@ from .providers import HashEmbedder, LocalLLM, OpenAIEmbedder, OpenAILLM, cosine
 from .query_cache import QueryCache
 from .similarity import EmbeddingCache, topk_cosine
 from .vector_store import HBMStore
+from ..utils.tracing import tracer
 
 # kept for parity with code/tests that patch `...memory_system.openai`
 openai = _providers.openai
@@ -148,6 +149,19 @@ class MemorySystem(ConsolidationMixin):
                         "consolidation_times": []}
         if load_from_disk:
             self._load_from_persistence()
+
+    @classmethod
+    def from_config(cls, cfg=None, **kw) -> "MemorySystem":
+        """Build from a :class:`lazzaro_amd.config.MemoryConfig` (env-aware)."""
+        from ..config import MemoryConfig
+
+        cfg = cfg or MemoryConfig.from_env()
+        emb = kw.pop("embedding_provider", None)
+        if emb is None and cfg.embed_model:
+            from .embedders import OnDeviceEmbedder
+            emb = OnDeviceEmbedder(cfg.embed_model, device=cfg.device, weights=cfg.embed_weights)
+        return cls(**cfg.reference_kwargs(), embedding_provider=emb, device=cfg.device, metric=cfg.metric,
+                   merge_mode=cfg.merge_mode, verbose=cfg.verbose, **kw)
 
     # ------------------------------------------------------------ helpers
     def _say(self, msg: str) -> None:
@@ -316,9 +330,12 @@ class MemorySystem(ConsolidationMixin):
         t0 = time.time()
         self.add_to_short_term(user_message, "episodic", salience=0.7)
         self.conversation_history.append({"role": "user", "content": user_message})
-        q = self._get_embedding(user_message)
-        ids = self._optimized_retrieval(q, user_message)
-        self._boost_neighbors(ids)
+        with tracer.stage("embed_query", self._device):
+            q = self._get_embedding(user_message)
+        with tracer.stage("retrieve", self._device):
+            ids = self._optimized_retrieval(q, user_message)
+        with tracer.stage("boost", self._device):
+            self._boost_neighbors(ids)
         return ids, (time.time() - t0) * 1000.0
 
     @staticmethod
@@ -339,7 +356,8 @@ class MemorySystem(ConsolidationMixin):
         ids, ms = self._retrieve_for(user_message)
         self.metrics["retrieval_times"].append(ms)
         msgs = self._build_messages(ids)
-        response = self._call_llm(msgs)
+        with tracer.stage("llm", "cpu"):
+            response = self._call_llm(msgs)
         self.add_to_short_term(response, "semantic", salience=0.5)
         self.conversation_history.append({"role": "assistant", "content": response})
         self._say(self._timing_line(ms, len(ids)))
@@ -397,8 +415,10 @@ class MemorySystem(ConsolidationMixin):
         return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
 
     def search_memories(self, query: str, limit: int = 5) -> List[Node]:
-        q = self._get_embedding(query)
-        ids = self.vector_store.search_nodes(q, user_id=self.user_id, limit=limit)
+        with tracer.stage("embed_query", self._device):
+            q = self._get_embedding(query)
+        with tracer.stage("search", self._device):
+            ids = self.vector_store.search_nodes(q, user_id=self.user_id, limit=limit)
         return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
 
     def search_memories_batch(self, queries: List[str], limit: int = 5) -> List[List[Node]]:

@@ -30,6 +30,9 @@ from .kmeans import kmeans
 _lib.register("lzk_ivfpq_scan", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I,
                                           _lib.P, _lib.P, _lib.P])
 
+_lib.register("lzk_ivfpq_dense", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I,
+                                           _lib.I, _lib.P, _lib.P])
+
 KSLOTS = (1, 4, 10, 16)
 
 
@@ -168,8 +171,10 @@ class IVFPQIndex:
         kk = max(k, rerank) if rerank else k
         if self.device.type != "cuda":
             s, rows = self._scan_ref(probes, coarse, lut, kk)
-        else:
+        elif kk <= KSLOTS[-1]:
             s, rows = self._scan_gpu(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
+        else:
+            s, rows = self._scan_dense(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
         if rerank and self.vectors is not None:
             valid = rows >= 0
             v = self.vectors[rows.clamp_min(0)].float()[..., : self.dim]
@@ -203,6 +208,26 @@ class IVFPQIndex:
             out_s[qi, : o.numel()] = cs_[o]
             out_r[qi, : o.numel()] = cr_[o]
         return out_s, out_r
+
+    def _scan_dense(self, probes, coarse, lut, k):
+        """Deep candidate lists: dense PQ scores per probed list (HIP kernel),
+        then a library top-k over each query's [nprobe * maxlen] scores."""
+        nq, nprobe = probes.shape
+        lens = (self.list_off[1:] - self.list_off[:-1])
+        maxlen = int(lens[probes.long()].max().item()) if probes.numel() else 0
+        maxlen = max(maxlen, 1)
+        buf = torch.empty((nq, nprobe, maxlen), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().lzk_ivfpq_dense(self.codes.data_ptr(), self.list_off.data_ptr(), probes.data_ptr(),
+                                              coarse.data_ptr(), lut.data_ptr(), nq, nprobe, self.m, maxlen,
+                                              buf.data_ptr(), _lib.stream_ptr(self.device)), "lzk_ivfpq_dense")
+        flat = buf.view(nq, -1)
+        kk = min(k, flat.shape[1])
+        s, pos = torch.topk(flat, kk, dim=1)
+        p, off = pos // maxlen, pos % maxlen
+        lists = torch.gather(probes.long(), 1, p)
+        rows = self.list_off[lists] + off
+        rows = torch.where(torch.isneginf(s), torch.full_like(rows, -1), rows)
+        return s, rows
 
     def _scan_gpu(self, probes, coarse, lut, k):
         nq, nprobe = probes.shape

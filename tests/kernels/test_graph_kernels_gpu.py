@@ -142,3 +142,20 @@ def test_ivfpq_gpu_scan_matches_reference():
     truth = torch.topk(torch.nn.functional.normalize(q, dim=1) @ x.T, 10, dim=1).indices
     _, i3 = gi.search(q, 10, nprobe=16, rerank=16)
     assert recall_at_k(i3, truth) > 0.8
+
+
+def test_ivfpq_dense_deep_rerank():
+    from lazzaro_amd.index.ivfpq import IVFPQIndex, recall_at_k
+    g = torch.Generator().manual_seed(1)
+    d, n = 128, 30000
+    c = torch.nn.functional.normalize(torch.randn(32, d, generator=g), dim=1)
+    x = torch.nn.functional.normalize(c[torch.randint(0, 32, (n,), generator=g)] + 0.15 * torch.randn(n, d, generator=g), dim=1)
+    q = torch.nn.functional.normalize(x[:64] + 0.02 * torch.randn(64, d, generator=g), dim=1)
+    gi = IVFPQIndex(d, nlist=32, m=16, device=DEV, keep_vectors=True)
+    gi.train(x, iters=5, pq_iters=5)
+    gi.add(x)
+    truth = torch.topk(q @ x.T, 10, dim=1).indices
+    _, i_pq = gi.search(q, 10, nprobe=8)
+    _, i_rr = gi.search(q, 10, nprobe=8, rerank=200)
+    r_pq, r_rr = recall_at_k(i_pq, truth), recall_at_k(i_rr, truth)
+    assert r_rr >= r_pq and r_rr > 0.9, (r_pq, r_rr)

@@ -202,3 +202,28 @@ def test_run_consolidation_fallback_profile_from_contents():
     r = ms.run_consolidation()
     assert "Updated profile domains" in r and ms.profile.data["preferences"]
     ms.close()
+
+
+def test_config_and_tracing(monkeypatch):
+    from lazzaro_amd.config import MemoryConfig
+    from lazzaro_amd.utils.tracing import tracer
+    monkeypatch.setenv("LZK_MAX_BUFFER_SIZE", "77")
+    monkeypatch.setenv("LZK_ENABLE_ASYNC", "false")
+    cfg = MemoryConfig.from_env(load_from_disk=False, merge_mode="pairwise")
+    assert cfg.max_buffer_size == 77 and cfg.enable_async is False
+    assert set(cfg.reference_kwargs()) >= {"max_buffer_size", "db_dir", "user_id"}
+    ms = MemorySystem.from_config(cfg, llm_provider=LocalLLM(), embedding_provider=HashEmbedder())
+    assert ms.max_buffer_size == 77 and ms.merge_mode == "pairwise" and not ms.enable_async
+    tracer.enable(True)
+    tracer.reset()
+    try:
+        ms.start_conversation()
+        ms.chat("I enjoy long walks on the beach.")
+        ms.search_memories("beach")
+        ms.end_conversation()
+        s = tracer.summary()
+        assert {"embed_query", "retrieve", "llm", "search", "ingest"} <= set(s)
+        assert s["retrieve"]["calls"] == 1
+    finally:
+        tracer.enable(False)
+    ms.close()
