@@ -64,6 +64,46 @@ struct TileStager {
   }
 };
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+// LDS-DMA staging (global_load_lds_dwordx4): each wave-instruction writes one
+// contiguous 1 KiB piece = 8 tile rows of 128 B, so the XOR swizzle moves to
+// the per-lane SOURCE address (lane l fills physical chunk l&7 of row l>>3 with
+// logical chunk (l&7) ^ ((row>>1)&7)); the MFMA-side read applies the same
+// involution (swz). No staging VGPRs, no ds_write pass.
+struct GldsStager {
+  const u16* asrc[4];
+  const u16* bsrc[4];
+  int piece[4];  // element offset of the wave's 1 KiB pieces inside a tile
+
+  __device__ __forceinline__ void setup(const u16* A, long lda, int a0, int na,
+                                        const u16* B, long ldb, int b0, int nb, int tid) {
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = wave * 4 + i;  // 16 pieces per 128-row tile
+      const int row = 8 * c + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      asrc[i] = A + (long)min(a0 + row, na - 1) * lda + kc * 8;
+      bsrc[i] = B + (long)min(b0 + row, nb - 1) * ldb + kc * 8;
+      piece[i] = c * 512;
+    }
+  }
+  __device__ __forceinline__ void issue(u16* smem, int buf, int ks) {
+    u16* as = smem + buf * 2 * TELEMS;
+    u16* bs = as + TELEMS;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(asrc[i] + ks * TK), (lds_void_t*)(as + piece[i]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(bsrc[i] + ks * TK), (lds_void_t*)(bs + piece[i]), 16, 0, 0);
+    }
+  }
+};
+
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ void tile_zero(f32x16 (&acc)[2][2]) {
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -92,6 +132,31 @@ __device__ __forceinline__ void tile_mma(const u16* smem, int buf, int wrow, int
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// Full K loop with LDS-DMA staging: issue tile k+1's DMA, MFMA on tile k,
+// drain + one barrier per K-step (the barrier both publishes tile k+1 and
+// frees buffer k for the DMA issued at the top of the next step).
+__device__ __forceinline__ void tile_gemm_glds(u16* smem, const u16* A, long lda, int a0, int na,
+                                               const u16* B, long ldb, int b0, int nb, int K,
+                                               f32x16 (&acc)[2][2]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wrow = wave >> 1, wcol = wave & 1;
+  GldsStager st;
+  st.setup(A, lda, a0, na, B, ldb, b0, nb, tid);
+  tile_zero(acc);
+  const int KS = K / TK;
+  st.issue(smem, 0, 0);
+  vm_drain();
+  __syncthreads();
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks + 1 < KS) st.issue(smem, (ks + 1) & 1, ks + 1);
+    __builtin_amdgcn_s_setprio(1);
+    tile_mma(smem, ks & 1, wrow, wcol, lane, acc);
+    __builtin_amdgcn_s_setprio(0);
+    vm_drain();
+    __syncthreads();
   }
 }
 

@@ -14,6 +14,8 @@
 //                  padded to the index arena's width)
 #include "lzk_tile.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace lzk;
@@ -23,7 +25,7 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 // ---------------------------------------------------------------- GEMM
-template <int ACT, bool RES>
+template <int ACT, bool RES, bool GLDS>
 __global__ __launch_bounds__(TNT, 2) void gemm_bias_act_kernel(
     const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
     const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y,
@@ -33,7 +35,8 @@ __global__ __launch_bounds__(TNT, 2) void gemm_bias_act_kernel(
   const int tt = logical / n_ft, ft = logical % n_ft;
   const int n0 = ft * TB, t0 = tt * TB;
   f32x16 acc[2][2];
-  tile_gemm(smem, W, ldw, n0, N, X, ldx, t0, T, K, acc);
+  if (GLDS) tile_gemm_glds(smem, W, ldw, n0, N, X, ldx, t0, T, K, acc);
+  else tile_gemm(smem, W, ldw, n0, N, X, ldx, t0, T, K, acc);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wrow = wave >> 1, wcol = wave & 1, h = lane >> 5, l32 = lane & 31;
@@ -336,9 +339,17 @@ __global__ __launch_bounds__(256) void pool_norm_kernel(const u16* __restrict__ 
 
 }  // namespace
 
+static int g_gemm_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
+
+LZK_EXPORT void lzk_set_staging(int glds) { g_gemm_staging = glds; }
+
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
                                  int act, void* stream) {
+  if (g_gemm_staging < 0) {
+    const char* e = getenv("LZK_STAGING");
+    g_gemm_staging = (e && e[0] == 'r') ? 0 : 1;
+  }
   if (K % TK != 0 || N % 4 != 0 || T <= 0 || N <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const int n_ft = (N + TB - 1) / TB, n_tt = (T + TB - 1) / TB;
@@ -348,9 +359,14 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   const u16* w = (const u16*)W;
   const u16* r = (const u16*)R;
   u16* y = (u16*)Y;
-#define GO(A, RS) hipLaunchKernelGGL((gemm_bias_act_kernel<A, RS>), grid, block, lds, st, x, ldx, T, w, ldw, N, bias, r, ldr, y, ldy, K, n_ft)
-  if (act == 1) { if (r) GO(1, true); else GO(1, false); }
-  else { if (r) GO(0, true); else GO(0, false); }
+#define GO(A, RS, G) hipLaunchKernelGGL((gemm_bias_act_kernel<A, RS, G>), grid, block, lds, st, x, ldx, T, w, ldw, N, bias, r, ldr, y, ldy, K, n_ft)
+  if (g_gemm_staging) {
+    if (act == 1) { if (r) GO(1, true, true); else GO(1, false, true); }
+    else { if (r) GO(0, true, true); else GO(0, false, true); }
+  } else {
+    if (act == 1) { if (r) GO(1, true, false); else GO(1, false, false); }
+    else { if (r) GO(0, true, false); else GO(0, false, false); }
+  }
 #undef GO
   return (int)hipGetLastError();
 }

@@ -20,7 +20,9 @@
 //     per-row label filter (tenant / shard), running per-lane top-K kept in
 //     registers (threshold compare fast path, insertion rarely taken).
 //   * Two-stage: per-(query, chunk) partial top-K, then topk_merge.
-#include "lzk_common.h"
+#include "lzk_tile.h"
+
+#include <cstdlib>
 
 namespace {
 
@@ -60,7 +62,7 @@ struct TopK {
   }
 };
 
-template <int K, bool HAS_BIAS, bool HAS_LABEL>
+template <int K, bool HAS_BIAS, bool HAS_LABEL, bool GLDS>
 __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
     const u16* __restrict__ X, long ldx, int nrows,
     const u16* __restrict__ Qm, long ldq, int nq,
@@ -121,6 +123,50 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
     }
   };
 
+  // LDS-DMA variant: per-lane pre-swizzled sources, wave-uniform 1 KiB pieces
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const u16* gx[4];
+  const u16* gq[4];
+  int gpiece[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = wave_u * 4 + i;
+    const int row = 8 * c + (lane >> 3);
+    const int kc = (lane & 7) ^ ((row >> 1) & 7);
+    gq[i] = Qm + (long)min(q0 + row, nq - 1) * ldq + kc * 8;
+    gx[i] = X;
+    gpiece[i] = c * 512;
+  }
+  auto set_gx = [&](int rt_) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 8 * (wave_u * 4 + i) + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      gx[i] = X + (long)min(row_lo + rt_ * BM + row, nrows - 1) * ldx + kc * 8;
+    }
+  };
+  float* ebias_g = reinterpret_cast<float*>(smem + 4 * TILE_ELEMS);
+  int* elab_g = reinterpret_cast<int*>(ebias_g + 2 * BM);
+  auto gissue = [&](int buf, int ks_, int rt_) {
+    u16* xs = smem + buf * 2 * TILE_ELEMS;
+    u16* qs = xs + TILE_ELEMS;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((lzk::gbl_void_t*)(gx[i] + ks_ * BK), (lzk::lds_void_t*)(xs + gpiece[i]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((lzk::gbl_void_t*)(gq[i] + ks_ * BK), (lzk::lds_void_t*)(qs + gpiece[i]), 16, 0, 0);
+    }
+    if ((HAS_BIAS || HAS_LABEL) && ks_ == 0 && wave_u == 0) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int r = min(row_lo + rt_ * BM + h2 * 64 + lane, nrows - 1);
+        if (HAS_BIAS)
+          __builtin_amdgcn_global_load_lds((lzk::gbl_void_t*)(bias + r), (lzk::lds_void_t*)(ebias_g + (rt_ & 1) * BM + h2 * 64), 4, 0, 0);
+        if (HAS_LABEL)
+          __builtin_amdgcn_global_load_lds((lzk::gbl_void_t*)(row_label + r), (lzk::lds_void_t*)(elab_g + (rt_ & 1) * BM + h2 * 64), 4, 0, 0);
+      }
+    }
+  };
+
   u16x8 rx[4], rq[4];
   float rbias = 0.f;
   int rlab = 0;
@@ -157,9 +203,15 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
   f32x16 acc[2][2];
 
   if (T > 0) {
-    set_xsrc(0);
-    gload(0, 0);
-    swrite(0, 0, 0);
+    if (GLDS) {
+      set_gx(0);
+      gissue(0, 0, 0);
+      lzk::vm_drain();
+    } else {
+      set_xsrc(0);
+      gload(0, 0);
+      swrite(0, 0, 0);
+    }
   }
   __syncthreads();
 
@@ -169,8 +221,13 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
     const int nks = (ks + 1 == KSTEPS) ? 0 : ks + 1;
     const int nrt = (ks + 1 == KSTEPS) ? rt + 1 : rt;
     if (has_next) {
-      if (nks == 0) set_xsrc(nrt);
-      gload(nks, nrt);
+      if (GLDS) {
+        if (nks == 0) set_gx(nrt);
+        gissue((t + 1) & 1, nks, nrt);
+      } else {
+        if (nks == 0) set_xsrc(nrt);
+        gload(nks, nrt);
+      }
     }
     if (ks == 0) {
 #pragma unroll
@@ -181,6 +238,7 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
           for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
     }
     // ---- MFMA over this K-step ----
+    if (GLDS) __builtin_amdgcn_s_setprio(1);
     {
       const u16* xs = smem + (t & 1) * 2 * TILE_ELEMS;
       const u16* qs = xs + TILE_ELEMS;
@@ -204,6 +262,7 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
             acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[rb], bfr[cb], acc[rb][cb], 0, 0, 0);
       }
     }
+    if (GLDS) __builtin_amdgcn_s_setprio(0);
     // ---- fused top-k epilogue at the end of a row tile ----
     if (ks == KSTEPS - 1) {
       const int lrow0 = wrow * 64 + 4 * h;
@@ -236,7 +295,11 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
         }
       }
     }
-    if (has_next) swrite((t + 1) & 1, nks, nrt);
+    if (GLDS) {
+      lzk::vm_drain();
+    } else if (has_next) {
+      swrite((t + 1) & 1, nks, nrt);
+    }
     __syncthreads();
     ks = nks; rt = nrt;
   }
@@ -332,6 +395,16 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   }
 }
 
+int g_search_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
+
+int search_staging() {
+  if (g_search_staging < 0) {
+    const char* e = getenv("LZK_STAGING");
+    g_search_staging = (e && e[0] == 'r') ? 0 : 1;
+  }
+  return g_search_staging;
+}
+
 template <int K>
 hipError_t launch_flat(const u16* X, long ldx, int nrows, const u16* Qm, long ldq, int nq,
                        const float* bias, const int* row_label, const int* q_label,
@@ -345,19 +418,28 @@ hipError_t launch_flat(const u16* X, long ldx, int nrows, const u16* Qm, long ld
   size_t lds_merge = (size_t)BN * 4 * K * 8;
   if (lds_merge > lds) lds = lds_merge;
   dim3 grid(n_qblocks * n_chunks);
-#define LZK_GO(B, L) do { \
-  (void)hipFuncSetAttribute((const void*)flat_topk_kernel<K, B, L>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-  hipLaunchKernelGGL((flat_topk_kernel<K, B, L>), grid, dim3(NT), lds, st, X, ldx, nrows, Qm, ldq, nq, \
+#define LZK_GO(B, L, G) do { \
+  (void)hipFuncSetAttribute((const void*)flat_topk_kernel<K, B, L, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+  hipLaunchKernelGGL((flat_topk_kernel<K, B, L, G>), grid, dim3(NT), lds, st, X, ldx, nrows, Qm, ldq, nq, \
                      bias, row_label, q_label, alpha, D, rows_per_chunk, n_chunks, n_qblocks, ps, pi); } while (0)
-  if (bias && row_label) LZK_GO(true, true);
-  else if (bias) LZK_GO(true, false);
-  else if (row_label) LZK_GO(false, true);
-  else LZK_GO(false, false);
+  if (search_staging() == 1) {
+    if (bias && row_label) LZK_GO(true, true, true);
+    else if (bias) LZK_GO(true, false, true);
+    else if (row_label) LZK_GO(false, true, true);
+    else LZK_GO(false, false, true);
+  } else {
+    if (bias && row_label) LZK_GO(true, true, false);
+    else if (bias) LZK_GO(true, false, false);
+    else if (row_label) LZK_GO(false, true, false);
+    else LZK_GO(false, false, false);
+  }
 #undef LZK_GO
   return hipGetLastError();
 }
 
 }  // namespace
+
+LZK_EXPORT void lzk_set_search_staging(int glds) { g_search_staging = glds; }
 
 // Number of row chunks the partial buffers must be sized for.
 LZK_EXPORT int lzk_flat_topk_chunks(int nrows, int nq, int target_wgs) {
