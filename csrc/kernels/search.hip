@@ -269,28 +269,28 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
       const int tile0 = row_lo + rt * BM + lrow0;
       const float* eb = ebias + (rt & 1) * BM + lrow0;
       const int* el = elab + (rt & 1) * BM + lrow0;
+      const bool full_tile = row_lo + (rt + 1) * BM <= row_hi;  // wave-uniform
+      auto score = [&](int rb, int cb, int e) -> float {
+        float x = alpha * acc[rb][cb][e];
+        if (HAS_BIAS) x += eb[rb * 32 + 8 * (e >> 2) + (e & 3)];
+        bool ok = true;
+        if (!full_tile) ok = tile0 + rb * 32 + (e & 3) + 8 * (e >> 2) < row_hi;
+        if (HAS_LABEL) ok = ok && (qlab[cb] < 0 || el[rb * 32 + 8 * (e >> 2) + (e & 3)] == qlab[cb]);
+        return ok ? x : LZK_NEG_INF;
+      };
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-          int lv[4] = {0, 0, 0, 0};
-          if (HAS_BIAS) bv = *reinterpret_cast<const f32x4*>(eb + rb * 32 + 8 * g);
-          if (HAS_LABEL) {
+        for (int cb = 0; cb < 2; ++cb) {
+          // pre-filter: block max vs the lane's current k-th score; the
+          // per-score insertion path below is rare after warm-up
+          float m = LZK_NEG_INF;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) lv[u] = el[rb * 32 + 8 * g + u];
-          }
+          for (int e = 0; e < 16; ++e) m = fmaxf(m, score(rb, cb, e));
+          if (m > top[cb].s[K - 1]) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int e = 4 * g + u;
-            const int r = tile0 + rb * 32 + 8 * g + u;
-#pragma unroll
-            for (int cb = 0; cb < 2; ++cb) {
-              float v = alpha * acc[rb][cb][e] + bv[u];
-              bool ok = r < row_hi;
-              if (HAS_LABEL) ok = ok && (qlab[cb] < 0 || lv[u] == qlab[cb]);
-              top[cb].push(ok ? v : LZK_NEG_INF, r);
-            }
+            for (int e = 0; e < 16; ++e)
+              top[cb].push(score(rb, cb, e), tile0 + rb * 32 + (e & 3) + 8 * (e >> 2));
           }
         }
       }
