@@ -1,0 +1,215 @@
+// 256x256x64 bf16 MFMA main loop, 8 waves, LDS-DMA staging with a counted
+// vmcnt pipeline (gfx950 / CDNA4). Shared by the flat-search candidate kernel
+// and the encoder projection GEMMs.
+//
+//   C[a][b] = sum_k A[a][k] * B[b][k]   (both operands K-contiguous rows)
+//
+// Geometry
+//   * 512 threads = 8 waves as 2 (A halves) x 4 (B quarters); wave (wr, wc)
+//     owns C rows [wr*128, +128) x cols [wc*64, +64) as 8 x 4 blocks of
+//     v_mfma_f32_16x16x32_bf16 -> acc[8][4] (128 VGPRs).
+//   * One K-tile = 4 half-tiles of 128 rows x 64 k (16 KiB each): HA0, HA1
+//     (A rows 0-127 / 128-255) and HB0, HB1. Two K-tile buffers = 8 slots =
+//     128 KiB of LDS, all in ONE dynamic __shared__ array.
+//   * Each half-tile is staged by 16 wave-level global_load_lds_dwordx4 (1 KiB
+//     = 8 rows x 128 B each, 2 per wave). The LDS image is lane-linear, so the
+//     XOR swizzle (chunk ^= (row>>1)&7) is applied to the per-lane SOURCE
+//     address and undone by the ds_read_b128 address; for the 16x16x32 lane
+//     map every ds_read_b128 lane group touches 16 distinct 16-B bank slots.
+//
+// Schedule (per K-tile t, buffer b = t&1; four phases, each phase is
+//   [ds_reads + DMA issue] s_barrier [lgkmcnt(0) MFMA x16] s_barrier):
+//   p0: read A rows 0-63 of the wave's half + B cols 0-31; issue HA1,HB0 of t+1
+//   p1: read A rows 64-127;                                 issue HB1 of t+1
+//   p2: read B cols 32-63
+//   p3: no reads;                issue HA0 of t+2, then s_waitcnt vmcnt(2)
+//   MFMA quadrants: p0 (A0,B0), p1 (A1,B0), p2 (A1,B1), p3 (A0,B1).
+// The waves with wr == 1 run one barrier behind (an extra s_barrier before
+// the loop, matched by one after it for wr == 0), so on every SIMD one wave's
+// MFMA section overlaps its partner's ds_read/issue section.
+//
+// Hazards, with phases numbered globally (P = 4t + p):
+//   RAW  tile t+1 is complete once every wave passed the vmcnt(2) of phase
+//        4t+3 (only HA0 of t+2 may remain in flight) and the barrier after it;
+//        group 0 reads it after barrier 2P+2, group 1 after 2P+3.
+//   WAR  a slot is re-staged >= 2 phases after its last ds_read (A slots:
+//        last read p1, re-staged at p3 / next p0; B slots: last read p2,
+//        re-staged at next p0 / p1), which orders the DMA after every
+//        reader's lgkmcnt(0) for both barrier offsets.
+// The vmcnt is never 0 in the steady state: one half-tile stays in flight
+// across every K-tile boundary, three more are in flight inside a tile.
+#pragma once
+#include "lzk_common.h"
+
+namespace g256 {
+
+constexpr int BM = 256;
+constexpr int BN = 256;
+constexpr int BK = 64;
+constexpr int NT = 512;
+constexpr int HALF = 128 * BK;                   // bf16 elements per half-tile slot
+constexpr int LDS_BYTES = 8 * HALF * 2;          // 128 KiB
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ int swz(int row, int kc) { return row * BK + ((kc ^ ((row >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void vm2() { asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); }
+
+struct Stager {
+  const u16* src[4][2];  // [slot HA0 HA1 HB0 HB1][piece]
+  int dst[2];            // element offset of the wave's pieces inside a slot
+
+  // rows past na / nb are clamped (callers mask their results)
+  __device__ __forceinline__ void setup(const u16* A, long lda, int a0, int na, const u16* B, long ldb,
+                                        int b0, int nb) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = wave * 2 + i;
+      const int row = 8 * c + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      src[0][i] = A + (long)min(a0 + row, na - 1) * lda + kc * 8;
+      src[1][i] = A + (long)min(a0 + 128 + row, na - 1) * lda + kc * 8;
+      src[2][i] = B + (long)min(b0 + row, nb - 1) * ldb + kc * 8;
+      src[3][i] = B + (long)min(b0 + 128 + row, nb - 1) * ldb + kc * 8;
+      dst[i] = c * 512;
+    }
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(u16* smem, int buf, int ks) const {
+    u16* slot = smem + (buf * 4 + H) * HALF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)(src[H][i] + ks * BK), (lds_void_t*)(slot + dst[i]), 16, 0, 0);
+  }
+};
+
+// 16 MFMAs of one quadrant: A frags a[mb][s] (rows mq*64 + mb*16), B frags
+// b[nb][s] (cols nq*32 + nb*16).
+template <int MQ, int NQ>
+__device__ __forceinline__ void quad_mma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        acc[MQ * 4 + mb][NQ * 2 + nb] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][s], b[nb][s], acc[MQ * 4 + mb][NQ * 2 + nb], 0, 0, 0);
+}
+
+// Full K loop (K = KS * 64). On return acc[i][j][e] holds
+//   C[wr*128 + i*16 + 4*(lane>>4) + e][wc*64 + j*16 + (lane&15)]
+// and every wave has passed the final barrier (smem may be reused).
+__device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane LDS read offsets (elements) inside a slot
+  int aoff[2][4][2], boff[2][2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) aoff[mq][mb][s] = swz(mq * 64 + mb * 16 + l16, 4 * s + lq);
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) boff[nq][nb][s] = swz((wc & 1) * 64 + nq * 32 + nb * 16 + l16, 4 * s + lq);
+  }
+
+  // prologue: tile 0 complete, HA0 of tile 1 in flight
+  st.issue<0>(smem, 0, 0);
+  st.issue<1>(smem, 0, 0);
+  st.issue<2>(smem, 0, 0);
+  st.issue<3>(smem, 0, 0);
+  if (KS > 1) {
+    st.issue<0>(smem, 1, 1);
+    vm2();
+  } else {
+    vm0();
+  }
+  bar();
+  if (wr == 1) bar();
+
+  bf16x8 a0[4][2], a1[4][2], b[2][2];
+  for (int t = 0; t < KS; ++t) {
+    const int buf = t & 1;
+    const u16* As = smem + (buf * 4 + wr) * HALF;
+    const u16* Bs = smem + (buf * 4 + 2 + (wc >> 1)) * HALF;
+    const bool nxt = t + 1 < KS;
+    // ---- p0 ----
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) a0[mb][s] = *reinterpret_cast<const bf16x8*>(As + aoff[0][mb][s]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b[nb][s] = *reinterpret_cast<const bf16x8*>(Bs + boff[0][nb][s]);
+    }
+    if (nxt) {
+      st.issue<1>(smem, buf ^ 1, t + 1);
+      st.issue<2>(smem, buf ^ 1, t + 1);
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    quad_mma<0, 0>(acc, a0, b);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- p1 ----
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) a1[mb][s] = *reinterpret_cast<const bf16x8*>(As + aoff[1][mb][s]);
+    if (nxt) st.issue<3>(smem, buf ^ 1, t + 1);
+    bar();
+    lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    quad_mma<1, 0>(acc, a1, b);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- p2 ----
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b[nb][s] = *reinterpret_cast<const bf16x8*>(Bs + boff[1][nb][s]);
+    bar();
+    lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    quad_mma<1, 1>(acc, a1, b);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- p3 ----
+    if (t + 2 < KS) {
+      st.issue<0>(smem, buf, t + 2);
+      vm2();
+    } else {
+      vm0();
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+    quad_mma<0, 1>(acc, a0, b);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (wr == 0) bar();
+}
+
+}  // namespace g256

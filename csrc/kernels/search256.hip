@@ -1,0 +1,205 @@
+// Flat top-k, large-batch path: threshold-filtered candidate generation on the
+// 256x256 8-wave MFMA pipeline (lzk_g256.h), then an exact per-query select.
+//
+// Same contract as flat_topk_kernel in search.hip (reference
+// src/lazzaro/core/vector_store.py:132-140 search_nodes):
+// score = alpha * <x, q> + bias[row], rows with a different label than the
+// query's (label >= 0) excluded, results ordered by (score desc, row asc).
+//
+// Why a different algorithm at Q >= 256 and N in the millions: a per-lane
+// running top-K costs 2K registers per query column and an insertion network
+// per tile, which caps the tile at 128x128 with 4 waves. Here the top-K state
+// is replaced by ONE number per query, a lower bound `thr[q]` of its k-th best
+// score, taken from an exact top-k over a strided 1/S sample of the rows (the
+// k-th best of a subset never exceeds the k-th best of the whole). Every
+// score >= thr[q] is appended to the query's candidate list (expected ~k*S
+// of N rows); the epilogue is one compare per score, so the 256x256 tile can
+// spend its registers on MFMA accumulators. A query whose list overflows its
+// capacity is flagged and recomputed by the caller with the per-lane kernel.
+#include "lzk_g256.h"
+
+namespace {
+
+using namespace g256;
+
+template <bool HAS_BIAS, bool HAS_LABEL>
+__global__ __launch_bounds__(NT, 1) void flat_cand_kernel(
+    const u16* __restrict__ X, long ldx, int nrows, const u16* __restrict__ Qm, long ldq, int nq, int D,
+    const float* __restrict__ bias, const int* __restrict__ row_label, const int* __restrict__ q_label,
+    float alpha, const float* __restrict__ thr, int n_qt, int cap, int* __restrict__ cnt,
+    float* __restrict__ cs, int* __restrict__ ci) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = logical / n_qt, qt = logical % n_qt;
+  const int r0 = rt * BM, q0 = qt * BN;
+
+  Stager st;
+  st.setup(X, ldx, r0, nrows, Qm, ldq, q0, nq);
+  f32x4 acc[8][4];
+  mainloop(smem, st, D / BK, acc);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  int qq[4], ql[4];
+  float th[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = q0 + wc * 64 + j * 16 + (lane & 15);
+    qq[j] = q;
+    th[j] = (q < nq) ? thr[q] : __builtin_huge_valf();
+    ql[j] = (HAS_LABEL && q < nq) ? q_label[q] : -1;
+  }
+  const bool full = r0 + BM <= nrows;  // wave-uniform
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rb = r0 + wr * 128 + i * 16 + 4 * (lane >> 4);
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    int lv[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = min(rb + e, nrows - 1);
+      if (HAS_BIAS) bv[e] = bias[r];
+      if (HAS_LABEL) lv[e] = row_label[r];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s[4];
+      float m = LZK_NEG_INF;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] = alpha * acc[i][j][e] + bv[e];
+        bool ok = full || (rb + e < nrows);
+        if (HAS_LABEL) ok = ok && (ql[j] < 0 || lv[e] == ql[j]);
+        s[e] = ok ? s[e] : LZK_NEG_INF;
+        m = fmaxf(m, s[e]);
+      }
+      if (m >= th[j]) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (s[e] >= th[j] && s[e] != LZK_NEG_INF) {
+            const int pos = atomicAdd(cnt + qq[j], 1);
+            if (pos < cap) {
+              cs[(long)qq[j] * cap + pos] = s[e];
+              ci[(long)qq[j] * cap + pos] = rb + e;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int K>
+struct TopK {
+  float s[K];
+  int i[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { s[j] = LZK_NEG_INF; i[j] = 0x7fffffff; }
+  }
+  __device__ __forceinline__ void push(float v, int r) {  // arbitrary index order
+    if (!better(v, r, s[K - 1], i[K - 1])) return;
+#pragma unroll
+    for (int j = K - 1; j > 0; --j) {
+      const bool up = better(v, r, s[j - 1], i[j - 1]);
+      const bool here = better(v, r, s[j], i[j]);
+      const float ns = up ? s[j - 1] : (here ? v : s[j]);
+      const int ni = up ? i[j - 1] : (here ? r : i[j]);
+      s[j] = ns; i[j] = ni;
+    }
+    if (better(v, r, s[0], i[0])) { s[0] = v; i[0] = r; }
+  }
+};
+
+// One wave per query: lane-local top-K over the candidate list, then K
+// rounds of wave argmax. ovf[q] = 1 when the list overflowed its capacity.
+template <int K>
+__global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict__ cnt, const float* __restrict__ cs,
+                                                          const int* __restrict__ ci, int cap, int nq, int kout,
+                                                          long idx_offset, float* __restrict__ os,
+                                                          long* __restrict__ oi, int* __restrict__ ovf) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  const int c = cnt[q];
+  if (lane == 0) ovf[q] = c > cap ? 1 : 0;
+  const int n = min(c, cap);
+  TopK<K> top;
+  top.init();
+  const float* s = cs + (long)q * cap;
+  const int* ix = ci + (long)q * cap;
+  for (int p = lane; p < n; p += 64) top.push(s[p], ix[p]);
+  for (int j = 0; j < kout; ++j) {
+    const float hs = top.s[0];
+    const int hi = top.i[0];
+    float bs = hs;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) {
+      const bool none = bi == 0x7fffffff || bs == LZK_NEG_INF;
+      os[(long)q * kout + j] = none ? LZK_NEG_INF : bs;
+      oi[(long)q * kout + j] = none ? -1 : (long)bi + idx_offset;
+    }
+    if (hi == bi && hs == bs && bi != 0x7fffffff) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) { top.s[t] = top.s[t + 1]; top.i[t] = top.i[t + 1]; }
+      top.s[K - 1] = LZK_NEG_INF; top.i[K - 1] = 0x7fffffff;
+    }
+  }
+}
+
+}  // namespace
+
+// Candidate pass. cnt [nq] must be zeroed by the caller (same stream);
+// cs/ci are [nq, cap].
+LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, int D,
+                             const float* bias, const int* row_label, const int* q_label, float alpha,
+                             const float* thr, int cap, int* cnt, float* cs, int* ci, void* stream) {
+  if (D % BK != 0 || nq <= 0 || nrows <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
+  if (row_label && !q_label) return (int)hipErrorInvalidValue;
+  const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
+  const long nblk = (long)n_rt * n_qt;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X;
+  const u16* q = (const u16*)Qm;
+#define LZK_GO(B, L)                                                                                              \
+  do {                                                                                                            \
+    (void)hipFuncSetAttribute((const void*)flat_cand_kernel<B, L>, hipFuncAttributeMaxDynamicSharedMemorySize,   \
+                              LDS_BYTES);                                                                         \
+    hipLaunchKernelGGL((flat_cand_kernel<B, L>), dim3((unsigned)nblk), dim3(NT), LDS_BYTES, st, x, ldx, nrows, q, \
+                       ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, cap, cnt, cs, ci);                 \
+  } while (0)
+  if (bias && row_label) LZK_GO(true, true);
+  else if (bias) LZK_GO(true, false);
+  else if (row_label) LZK_GO(false, true);
+  else LZK_GO(false, false);
+#undef LZK_GO
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_cand_select(const int* cnt, const float* cs, const int* ci, int cap, int nq, int kslot, int kout,
+                               long idx_offset, float* os, long* oi, int* ovf, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((nq + 3) / 4), block(256);
+  if (kout > kslot) return (int)hipErrorInvalidValue;
+#define LZK_SEL(KK) \
+  hipLaunchKernelGGL(cand_select_kernel<KK>, grid, block, 0, st, cnt, cs, ci, cap, nq, kout, idx_offset, os, oi, ovf)
+  switch (kslot) {
+    case 1: LZK_SEL(1); break;
+    case 2: LZK_SEL(2); break;
+    case 4: LZK_SEL(4); break;
+    case 8: LZK_SEL(8); break;
+    case 10: LZK_SEL(10); break;
+    case 16: LZK_SEL(16); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef LZK_SEL
+  return (int)hipGetLastError();
+}

@@ -18,6 +18,8 @@ Results are ordered by (score desc, row asc); missing slots are (-inf, -1).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -76,6 +78,23 @@ class _Workspace:
 
 
 _ws = _Workspace()
+_ws_cand = _Workspace()
+
+# Large-batch candidate path (csrc/kernels/search256.hip): used when the batch
+# fills whole 256-query tiles and the arena is large enough that the strided
+# threshold sample is cheap. LZK_SEARCH=lane forces the per-lane kernel.
+CAND_MIN_ROWS = 1 << 20
+CAND_MIN_Q = 256
+CAND_STRIDE = int(os.environ.get("LZK_CAND_STRIDE", "64"))
+
+
+def _use_cand(N, nq, kslot):
+    mode = os.environ.get("LZK_SEARCH", "auto")
+    if mode == "lane":
+        return False
+    if mode == "cand":
+        return True
+    return N >= CAND_MIN_ROWS and nq >= CAND_MIN_Q and kslot <= 16
 
 
 def flat_topk(X: torch.Tensor, Q: torch.Tensor, k: int, *, bias=None, row_label=None,
@@ -107,6 +126,16 @@ def flat_topk(X: torch.Tensor, Q: torch.Tensor, k: int, *, bias=None, row_label=
     if row_label is not None:
         assert row_label.dtype == torch.int32 and q_label is not None
         assert q_label.dtype == torch.int32 and q_label.shape[0] == nq
+    if n_chunks is None and _use_cand(N, nq, kslot):
+        return _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
+    return _flat_topk_lane(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, n_chunks)
+
+
+def _flat_topk_lane(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, n_chunks):
+    """Per-lane running top-K kernel (search.hip) + partial-list merge."""
+    L = _lib.lib()
+    nq, D = Q.shape
+    N = X.shape[0]
     if n_chunks:
         # same normalisation as the C launcher: chunks are whole 128-row tiles
         rpc = -(-(-(-N // n_chunks)) // 128) * 128
@@ -128,6 +157,55 @@ def flat_topk(X: torch.Tensor, Q: torch.Tensor, k: int, *, bias=None, row_label=
     rc = L.lzk_topk_merge(ps.data_ptr(), pi.data_ptr(), nch * kslot, nq, kslot, int(k),
                           int(idx_offset), os_.data_ptr(), oi.data_ptr(), st)
     _lib.check(rc, "lzk_topk_merge")
+    return os_, oi
+
+
+def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset):
+    """Threshold-filtered candidates on the 256x256 pipeline (search256.hip).
+
+    1. thr[q] = k-th best score over the strided sample X[::S] (exact, lane
+       kernel), lowered by a small margin that covers the fp32 accumulation
+       order difference between the two kernels -> a lower bound of the true
+       k-th score, so every true top-k row passes ``score >= thr``.
+    2. candidate pass over all rows; 3. exact select per query. Queries whose
+       list overflowed are recomputed with the lane kernel.
+    """
+    L = _lib.lib()
+    nq, D = Q.shape
+    N = X.shape[0]
+    dev = X.device
+    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
+    Xs = X[::S]
+    bs = bias[:N:S].contiguous() if bias is not None else None
+    ls = row_label[:N:S].contiguous() if row_label is not None else None
+    ts, _ = _flat_topk_lane(Xs, Q, kslot, kslot, bs, ls, q_label, alpha, 0, None)
+    thr = ts[:, k - 1].contiguous()
+    thr = thr - 2e-4 * (1.0 + thr.abs())
+    thr = torch.nan_to_num(thr, nan=float("-inf"))
+    cap = max(1024, 8 * kslot * S)
+    ws = _ws_cand.get(dev, nq * (4 + 8 * cap))
+    cnt = ws[: nq * 4].view(torch.int32)
+    cs = ws[nq * 4: nq * 4 + nq * cap * 4].view(torch.float32)
+    ci = ws[nq * 4 + nq * cap * 4: nq * 4 + nq * cap * 8].view(torch.int32)
+    cnt.zero_()
+    st = _lib.stream_ptr(dev)
+    rc = L.lzk_flat_cand(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D,
+                         _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha),
+                         thr.data_ptr(), cap, cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), st)
+    _lib.check(rc, "lzk_flat_cand")
+    os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    oi = torch.empty((nq, k), dtype=torch.long, device=dev)
+    ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
+    rc = L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, int(k),
+                           int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
+    _lib.check(rc, "lzk_cand_select")
+    bad = torch.nonzero(ovf).flatten()
+    if bad.numel():
+        sub_q = Q[bad].contiguous()
+        sub_l = q_label[bad].contiguous() if q_label is not None else None
+        s2, i2 = _flat_topk_lane(X, sub_q, k, kslot, bias, row_label, sub_l, alpha, idx_offset, None)
+        os_[bad] = s2
+        oi[bad] = i2
     return os_, oi
 
 

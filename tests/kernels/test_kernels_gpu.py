@@ -38,6 +38,37 @@ def test_flat_topk_matches_reference(n, d, nq, k, bias, label):
     assert (i.cpu() == ri).float().mean() > 0.995  # ulp-level ties may swap
 
 
+@pytest.mark.parametrize("n,d,nq,k,bias,label", [
+    (300_001, 768, 300, 10, True, False), (200_000, 384, 513, 16, False, True), (70_000, 1024, 256, 1, True, True),
+    (140_000, 64, 260, 5, False, False),
+])
+def test_flat_topk_candidate_path(monkeypatch, n, d, nq, k, bias, label):
+    """256x256 pipeline + sampled threshold + select (search256.hip) == reference."""
+    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", 16)
+    g = torch.Generator(device=DEV).manual_seed(n)
+    X = torch.randn(n, d, device=DEV, generator=g).to(torch.bfloat16)
+    Q = torch.randn(nq, d, device=DEV, generator=g).to(torch.bfloat16)
+    b = torch.randn(n, device=DEV, generator=g) if bias else None
+    rl = torch.randint(0, 3, (n,), device=DEV, dtype=torch.int32, generator=g) if label else None
+    ql = torch.randint(-1, 3, (nq,), device=DEV, dtype=torch.int32, generator=g) if label else None
+    a = 2.0 if bias else 1.0
+    s, i = flat_topk(X, Q, k, bias=b, row_label=rl, q_label=ql, alpha=a, idx_offset=5)
+    rs, ri = _ref_topk(X.cpu(), Q.cpu(), k, None if b is None else b.cpu(),
+                       None if rl is None else rl.cpu(), None if ql is None else ql.cpu(), a, idx_offset=5)
+    torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
+    assert (i.cpu() == ri).float().mean() > 0.995
+
+
+def test_flat_topk_candidate_overflow_falls_back(monkeypatch):
+    """All-equal scores overflow every candidate list -> lane-kernel recompute."""
+    monkeypatch.setenv("LZK_SEARCH", "cand")
+    X = torch.ones(100_000, 128, device=DEV, dtype=torch.bfloat16)
+    Q = torch.ones(256, 128, device=DEV, dtype=torch.bfloat16)
+    s, i = flat_topk(X, Q, 4)
+    assert (i.cpu() == torch.arange(4)[None, :]).all() and (s.cpu() == 128.0).all()
+
+
 def test_flat_topk_tombstones_and_chunks():
     X = torch.randn(4096, 128, device=DEV).to(torch.bfloat16)
     bias = torch.zeros(4096, device=DEV)
