@@ -14,7 +14,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from lazzaro_amd.ops import search as S  # noqa: E402
 
 
+import ctypes  # noqa: E402
+
+from lazzaro_amd.ops import _lib  # noqa: E402
+
+_L = _lib.lib()
+_L.lzk_set_cand_persist.argtypes = [ctypes.c_int]
+
+
 def run(path, X, Q, k, bias):
+    if path.startswith("cand"):
+        _L.lzk_set_cand_persist(1 if path == "cand_p" else 0)
+        path = "cand"
     os.environ["LZK_SEARCH"] = path
     return S.flat_topk(X, Q, k, bias=bias, alpha=2.0 if bias is not None else 1.0)
 
@@ -40,12 +51,13 @@ def main():
                 bias[r0:r0 + (1 << 20)] = -(X[r0:r0 + (1 << 20)].float() ** 2).sum(1)
         sl, il = run("lane", X, Q, k, bias)
         sc, ic = run("cand", X, Q, k, bias)
+        sp, ip_ = run("cand_p", X, Q, k, bias)
         torch.cuda.synchronize()
-        same = float((il == ic).float().mean())
-        maxdiff = float((sl - sc).abs().max())
-        times = {"lane": [], "cand": []}
+        same = float(((il == ic) & (il == ip_)).float().mean())
+        maxdiff = float(torch.maximum((sl - sc).abs(), (sl - sp).abs()).max())
+        times = {"lane": [], "cand": [], "cand_p": []}
         for _ in range(5):
-            for p in ("lane", "cand"):
+            for p in ("lane", "cand", "cand_p"):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _ in range(3):

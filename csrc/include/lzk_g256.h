@@ -108,10 +108,29 @@ __device__ __forceinline__ void quad_mma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4
             __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][s], b[nb][s], acc[MQ * 4 + mb][NQ * 2 + nb], 0, 0, 0);
 }
 
-// Full K loop (K = KS * 64). On return acc[i][j][e] holds
+struct NoExtra {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// Prologue DMA of one output tile: the four half-tiles of K-tile 0 into
+// buffer 0, then `extra()` (small per-tile epilogue operands a caller stages
+// into spare LDS), then HA0 of K-tile 1. Every slot must be free (no wave
+// still reading it): call it at kernel start or after body() returned.
+template <class Extra = NoExtra>
+__device__ __forceinline__ void prologue(u16* smem, const Stager& st, int KS, const Extra& extra = Extra()) {
+  st.issue<0>(smem, 0, 0);
+  st.issue<1>(smem, 0, 0);
+  st.issue<2>(smem, 0, 0);
+  st.issue<3>(smem, 0, 0);
+  extra();
+  if (KS > 1) st.issue<0>(smem, 1, 1);
+}
+
+// K loop after prologue() (K = KS * 64). On return acc[i][j][e] holds
 //   C[wr*128 + i*16 + 4*(lane>>4) + e][wc*64 + j*16 + (lane&15)]
-// and every wave has passed the final barrier (smem may be reused).
-__device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
+// and every wave has passed the final barrier with all of its DMA retired
+// (smem may be reused or re-staged).
+__device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -135,17 +154,10 @@ __device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f3
       for (int nb = 0; nb < 2; ++nb) boff[nq][nb][s] = swz((wc & 1) * 64 + nq * 32 + nb * 16 + l16, 4 * s + lq);
   }
 
-  // prologue: tile 0 complete, HA0 of tile 1 in flight
-  st.issue<0>(smem, 0, 0);
-  st.issue<1>(smem, 0, 0);
-  st.issue<2>(smem, 0, 0);
-  st.issue<3>(smem, 0, 0);
-  if (KS > 1) {
-    st.issue<0>(smem, 1, 1);
-    vm2();
-  } else {
-    vm0();
-  }
+  // tile 0 (and anything issued before HA0 of tile 1) complete; at most the
+  // 2 youngest DMAs (HA0 of tile 1) in flight
+  if (KS > 1) vm2();
+  else vm0();
   bar();
   if (wr == 1) bar();
 
@@ -211,5 +223,29 @@ __device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f3
   }
   if (wr == 0) bar();
 }
+
+__device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
+  prologue(smem, st, KS);
+  body(smem, st, KS, acc);
+}
+
+// Persistent tile walk: the blocks resident on one XCD (blocks are dealt to
+// the 8 XCDs round-robin) take consecutive tiles of that XCD's contiguous
+// share, so concurrently running tiles of an XCD share operand panels in its
+// L2. Speed only: every tile is visited exactly once for any grid size.
+struct TileWalk {
+  int next, end, step;
+  __device__ __forceinline__ void init(int n_tiles) {
+    const int G = gridDim.x, b = blockIdx.x;
+    const int x = b % 8, s = b / 8;
+    const int nb = (G - x + 7) / 8;          // blocks on this XCD
+    const int per = (n_tiles + 7) / 8;       // tiles per XCD share
+    const int lo = min(x * per, n_tiles);
+    end = min(lo + per, n_tiles);
+    next = lo + s;
+    step = nb;
+  }
+  __device__ __forceinline__ bool valid(int t) const { return t < end; }
+};
 
 }  // namespace g256

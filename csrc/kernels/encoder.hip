@@ -12,6 +12,7 @@
 //   embed_ln       word + position + type embedding gather fused with LayerNorm
 //   pool_norm      masked mean / CLS pooling + L2 normalisation (+ bf16 copy
 //                  padded to the index arena's width)
+#include "lzk_g256.h"
 #include "lzk_tile.h"
 
 #include <cstdlib>
@@ -68,6 +69,74 @@ __global__ __launch_bounds__(TNT, 2) void gemm_bias_act_kernel(
         for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16(v[u]);
         *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
       }
+    }
+  }
+}
+
+// 256x256 tiles on the 8-wave counted-vmcnt pipeline (lzk_g256.h): features
+// (W rows) on the A side, tokens on B. Epilogue in two passes through the
+// (then idle) LDS: (1) bias + activation in the MFMA layout (lane = token,
+// 4 consecutive features), bf16 into a [token][feature] image with 520-B rows
+// (conflict-free 8-B writes); (2) one wave per token row streams 512
+// contiguous bytes to Y (+ the residual row read the same way), so stores
+// and residual loads are whole cache lines instead of 32-B pieces.
+constexpr int G256_OUT_LD = g256::BN + 4;  // u16 per LDS output row (520 B)
+constexpr int G256_GEMM_LDS = (g256::BM * G256_OUT_LD * 2 > g256::LDS_BYTES) ? g256::BM * G256_OUT_LD * 2
+                                                                              : g256::LDS_BYTES;
+
+template <int ACT, bool RES>
+__global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
+    const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
+    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y,
+    long ldy, int K, int n_ft) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tt = logical / n_ft, ft = logical % n_ft;
+  const int n0 = ft * g256::BM, t0 = tt * g256::BN;
+  g256::Stager st;
+  st.setup(W, ldw, n0, N, X, ldx, t0, T);
+  f32x4 acc[8][4];
+  g256::mainloop(smem, st, K / g256::BK, acc);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // pass 1: registers -> LDS image [token][feature] (all DMA retired, every
+  // wave past the main loop's last barrier)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int nl = wr * 128 + i * 16 + 4 * (lane >> 4);
+    const int n = min(n0 + nl, N - 4);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tl = wc * 64 + j * 16 + (lane & 15);
+      u16x4 o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v = acc[i][j][u] + bv[u];
+        if (ACT == 1) v = gelu_erf(v);
+        o[u] = f32_to_bf16(v);
+      }
+      *reinterpret_cast<u16x4*>(smem + tl * G256_OUT_LD + nl) = o;
+    }
+  }
+  __syncthreads();
+  // pass 2: one wave per token row, 4 features per lane
+  const int nl = lane * 4;
+  const int n = n0 + nl;
+  if (n < N) {
+#pragma unroll 8
+    for (int rr = 0; rr < g256::BN / 8; ++rr) {
+      const int tl = wave * (g256::BN / 8) + rr;
+      const int t = t0 + tl;
+      if (t >= T) break;
+      u16x4 o = *reinterpret_cast<const u16x4*>(smem + tl * G256_OUT_LD + nl);
+      if (RES) {
+        const u16x4 rv = *reinterpret_cast<const u16x4*>(R + (long)t * ldr + n);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16(bf16_to_f32(o[u]) + bf16_to_f32(rv[u]));
+      }
+      *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
     }
   }
 }
@@ -340,8 +409,10 @@ __global__ __launch_bounds__(256) void pool_norm_kernel(const u16* __restrict__ 
 }  // namespace
 
 static int g_gemm_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
+static int g_gemm_tile = -1;     // 256 = 8-wave 256x256 pipeline when the grid fills the chip, 128 = always 128x128
 
 LZK_EXPORT void lzk_set_staging(int glds) { g_gemm_staging = glds; }
+LZK_EXPORT void lzk_set_gemm_tile(int t) { g_gemm_tile = t; }
 
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
@@ -352,6 +423,33 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   }
   if (K % TK != 0 || N % 4 != 0 || T <= 0 || N <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (g_gemm_tile < 0) {
+    const char* e = getenv("LZK_GEMM_TILE");
+    g_gemm_tile = (e && atoi(e) == 128) ? 128 : 256;
+  }
+  {
+    const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
+    // measured (bench/ab_gemm.py): at N = 768 the 1.5-wave quantisation of 3 feature tiles
+    // loses to the 128x128 kernel; from N = 1024 on the 256x256 pipeline wins
+    if (g_gemm_tile == 256 && n_ft * n_tt >= 256 && N >= 1024 && N % 4 == 0) {
+      const u16* x = (const u16*)X;
+      const u16* w = (const u16*)W;
+      const u16* r = (const u16*)R;
+      u16* y = (u16*)Y;
+      dim3 grid(n_ft * n_tt), block(g256::NT);
+#define GO(A, RS)                                                                                             \
+  do {                                                                                                        \
+    (void)hipFuncSetAttribute((const void*)gemm256_bias_act_kernel<A, RS>,                                    \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G256_GEMM_LDS);                     \
+    hipLaunchKernelGGL((gemm256_bias_act_kernel<A, RS>), grid, block, G256_GEMM_LDS, st, x, ldx, T, w, ldw, \
+                       N, bias, r, ldr, y, ldy, K, n_ft);                                                     \
+  } while (0)
+      if (act == 1) { if (r) GO(1, true); else GO(1, false); }
+      else { if (r) GO(0, true); else GO(0, false); }
+#undef GO
+      return (int)hipGetLastError();
+    }
+  }
   const int n_ft = (N + TB - 1) / TB, n_tt = (T + TB - 1) / TB;
   dim3 grid(n_ft * n_tt), block(TNT);
   const size_t lds = 2 * 2 * TELEMS * sizeof(u16);

@@ -18,6 +18,8 @@
 // capacity is flagged and recomputed by the caller with the per-lane kernel.
 #include "lzk_g256.h"
 
+#include <cstdlib>
+
 namespace {
 
 using namespace g256;
@@ -90,6 +92,127 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_kernel(
   }
 }
 
+// Persistent variant: one block per CU walks its XCD's tiles; the next
+// tile's prologue DMA (operand half-tiles AND its epilogue operands: bias,
+// row labels, thresholds, query labels -> spare LDS, double-buffered by tile
+// parity) is issued before this tile's epilogue, so the pipeline fill of
+// tile i+1 overlaps the epilogue of tile i and no epilogue global load can
+// drain the in-flight DMA.
+constexpr int EPI_OFF = 8 * HALF;               // u16 offset of the epilogue area (128 KiB)
+constexpr int CAND_P_LDS = LDS_BYTES + 2 * 4 * 256 * 4;
+
+template <bool HAS_BIAS, bool HAS_LABEL>
+__global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
+    const u16* __restrict__ X, long ldx, int nrows, const u16* __restrict__ Qm, long ldq, int nq, int D,
+    const float* __restrict__ bias, const int* __restrict__ row_label, const int* __restrict__ q_label,
+    float alpha, const float* __restrict__ thr, int n_qt, int n_tiles, int cap, int* __restrict__ cnt,
+    float* __restrict__ cs, int* __restrict__ ci) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  float* epi = reinterpret_cast<float*>(smem + EPI_OFF);  // [parity][thr | bias | lab | qlab][256]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int KS = D / BK;
+
+  TileWalk walk;
+  walk.init(n_tiles);
+  int tile = walk.next;
+  if (!walk.valid(tile)) return;
+
+  auto stage_epi = [&](int tl, int par) {
+    const int r0 = (tl / n_qt) * BM, q0 = (tl % n_qt) * BN;
+    const int a = wave >> 1;  // 0 thr, 1 bias, 2 row label, 3 query label (wave-uniform)
+    const bool need = a == 0 || (a == 1 && HAS_BIAS) || (a >= 2 && HAS_LABEL);
+    if (!need) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = (wave & 1) * 2 + i;
+      const void* src;
+      if (a == 0) src = thr + min(q0 + c * 64 + lane, nq - 1);
+      else if (a == 1) src = bias + min(r0 + c * 64 + lane, nrows - 1);
+      else if (a == 2) src = row_label + min(r0 + c * 64 + lane, nrows - 1);
+      else src = q_label + min(q0 + c * 64 + lane, nq - 1);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(epi + par * 1024 + a * 256 + c * 64), 4, 0, 0);
+    }
+  };
+
+  Stager st;
+  st.setup(X, ldx, (tile / n_qt) * BM, nrows, Qm, ldq, (tile % n_qt) * BN, nq);
+  prologue(smem, st, KS, [&]() { stage_epi(tile, 0); });
+  int par = 0;
+  f32x4 acc[8][4];
+  while (true) {
+    body(smem, st, KS, acc);
+    const int cur = tile, cpar = par;
+    tile += walk.step;
+    const bool more = walk.valid(tile);
+    if (more) {
+      st.setup(X, ldx, (tile / n_qt) * BM, nrows, Qm, ldq, (tile % n_qt) * BN, nq);
+      prologue(smem, st, KS, [&]() { stage_epi(tile, cpar ^ 1); });
+    }
+    // ---- epilogue of `cur` (operands from LDS only) ----
+    {
+      const int r0 = (cur / n_qt) * BM, q0 = (cur % n_qt) * BN;
+      const float* e_thr = epi + cpar * 1024;
+      const float* e_bias = e_thr + 256;
+      const int* e_lab = reinterpret_cast<const int*>(e_thr + 512);
+      const int* e_qlab = reinterpret_cast<const int*>(e_thr + 768);
+      int qq[4], ql[4];
+      float th[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int qlo = wc * 64 + j * 16 + (lane & 15);
+        qq[j] = q0 + qlo;
+        th[j] = (qq[j] < nq) ? e_thr[qlo] : __builtin_huge_valf();
+        ql[j] = HAS_LABEL ? e_qlab[qlo] : -1;
+      }
+      const bool full = r0 + BM <= nrows;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int rl = wr * 128 + i * 16 + 4 * (lane >> 4);
+        const int rb = r0 + rl;
+        f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+        if (HAS_BIAS) bv = *reinterpret_cast<const f32x4*>(e_bias + rl);
+        int lv[4] = {0, 0, 0, 0};
+        if (HAS_LABEL) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) lv[e] = e_lab[rl + e];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float sc[4];
+          float m = LZK_NEG_INF;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            sc[e] = alpha * acc[i][j][e] + bv[e];
+            bool ok = full || (rb + e < nrows);
+            if (HAS_LABEL) ok = ok && (ql[j] < 0 || lv[e] == ql[j]);
+            sc[e] = ok ? sc[e] : LZK_NEG_INF;
+            m = fmaxf(m, sc[e]);
+          }
+          if (m >= th[j]) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (sc[e] >= th[j] && sc[e] != LZK_NEG_INF) {
+                const int pos = atomicAdd(cnt + qq[j], 1);
+                if (pos < cap) {
+                  cs[(long)qq[j] * cap + pos] = sc[e];
+                  ci[(long)qq[j] * cap + pos] = rb + e;
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+    if (!more) break;
+    par = cpar ^ 1;
+  }
+}
+
+int g_cand_persist = -1;
+int g_n_cu = 0;
+
 template <int K>
 struct TopK {
   float s[K];
@@ -156,6 +279,8 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
 
 }  // namespace
 
+LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
+
 // Candidate pass. cnt [nq] must be zeroed by the caller (same stream);
 // cs/ci are [nq, cap].
 LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, int D,
@@ -169,6 +294,32 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* q = (const u16*)Qm;
+  if (g_cand_persist < 0) {
+    const char* e = getenv("LZK_CAND_PERSIST");
+    g_cand_persist = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  if (g_cand_persist && nblk >= g_n_cu) {
+    const int grid = g_n_cu;
+#define LZK_GP(B, L)                                                                                               \
+  do {                                                                                                             \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, L>,                                      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                             \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, L>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx, nrows, q, \
+                       ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs, ci);       \
+  } while (0)
+    if (bias && row_label) LZK_GP(true, true);
+    else if (bias) LZK_GP(true, false);
+    else if (row_label) LZK_GP(false, true);
+    else LZK_GP(false, false);
+#undef LZK_GP
+    return (int)hipGetLastError();
+  }
 #define LZK_GO(B, L)                                                                                              \
   do {                                                                                                            \
     (void)hipFuncSetAttribute((const void*)flat_cand_kernel<B, L>, hipFuncAttributeMaxDynamicSharedMemorySize,   \
