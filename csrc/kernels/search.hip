@@ -69,7 +69,7 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
     const float* __restrict__ bias, const int* __restrict__ row_label,
     const int* __restrict__ q_label, float alpha, int D,
     int rows_per_chunk, int n_chunks, int n_qblocks,
-    float* __restrict__ out_s, int* __restrict__ out_i) {
+    float* __restrict__ out_s, int* __restrict__ out_i, const int* __restrict__ q_active) {
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -82,6 +82,11 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
   const int qb = logical % n_qblocks;
   if (chunk >= n_chunks) return;
   const int q0 = qb * BN;
+  if (q_active) {  // masked re-run: skip query tiles with no active query (block-uniform exit)
+    int any = 0;
+    for (int t = tid; t < BN; t += NT) any |= (q0 + t < nq) && q_active[q0 + t];
+    if (!__syncthreads_or(any)) return;
+  }
   const int row_lo = chunk * rows_per_chunk;
   const int row_hi = min(nrows, row_lo + rows_per_chunk);
   const int ntiles = (row_hi > row_lo) ? (row_hi - row_lo + BM - 1) / BM : 0;
@@ -345,10 +350,11 @@ __global__ __launch_bounds__(NT, 2) void flat_topk_kernel(
 template <int K>
 __global__ __launch_bounds__(256) void topk_merge_kernel(
     const float* __restrict__ ps, const int* __restrict__ pi, int ncand, int nq,
-    int kout, long idx_offset, float* __restrict__ os, long* __restrict__ oi) {
+    int kout, long idx_offset, float* __restrict__ os, long* __restrict__ oi, const int* __restrict__ q_active) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
+  if (q_active && !q_active[q]) return;
   TopK<K> top;
   top.init();
   const float* s = ps + (long)q * ncand;
@@ -409,7 +415,7 @@ template <int K>
 hipError_t launch_flat(const u16* X, long ldx, int nrows, const u16* Qm, long ldq, int nq,
                        const float* bias, const int* row_label, const int* q_label,
                        float alpha, int D, int n_chunks, float* ps, int* pi,
-                       hipStream_t st) {
+                       hipStream_t st, const int* q_active) {
   int n_qblocks = (nq + BN - 1) / BN;
   int rows_per_chunk = ((nrows + n_chunks - 1) / n_chunks + BM - 1) / BM * BM;
   n_chunks = (nrows + rows_per_chunk - 1) / rows_per_chunk;
@@ -421,7 +427,7 @@ hipError_t launch_flat(const u16* X, long ldx, int nrows, const u16* Qm, long ld
 #define LZK_GO(B, L, G) do { \
   (void)hipFuncSetAttribute((const void*)flat_topk_kernel<K, B, L, G>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
   hipLaunchKernelGGL((flat_topk_kernel<K, B, L, G>), grid, dim3(NT), lds, st, X, ldx, nrows, Qm, ldq, nq, \
-                     bias, row_label, q_label, alpha, D, rows_per_chunk, n_chunks, n_qblocks, ps, pi); } while (0)
+                     bias, row_label, q_label, alpha, D, rows_per_chunk, n_chunks, n_qblocks, ps, pi, q_active); } while (0)
   if (search_staging() == 1) {
     if (bias && row_label) LZK_GO(true, true, true);
     else if (bias) LZK_GO(true, false, true);
@@ -462,39 +468,71 @@ LZK_EXPORT int lzk_flat_topk_kslot(int k) {
   return -1;
 }
 
-// Partial pass: ps/pi are [nq, n_chunks, kslot].
-LZK_EXPORT int lzk_flat_topk_partial(const void* X, long ldx, int nrows, const void* Qm, long ldq,
-                                     int nq, const float* bias, const int* row_label,
-                                     const int* q_label, float alpha, int D, int kslot,
-                                     int n_chunks, float* ps, int* pi, void* stream) {
+// Partial pass: ps/pi are [nq, n_chunks, kslot]. q_active (optional): only
+// query tiles holding an active query are computed (the rest of ps/pi is
+// left untouched) -- the device-side fallback of the candidate path.
+static int flat_partial(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, const float* bias,
+                        const int* row_label, const int* q_label, float alpha, int D, int kslot, int n_chunks,
+                        float* ps, int* pi, void* stream, const int* q_active) {
   if (D % BK != 0 || nq <= 0 || nrows <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* q = (const u16*)Qm;
+#define LZK_KS(KK) return launch_flat<KK>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st, q_active)
   switch (kslot) {
-    case 1: return launch_flat<1>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st);
-    case 2: return launch_flat<2>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st);
-    case 4: return launch_flat<4>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st);
-    case 8: return launch_flat<8>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st);
-    case 10: return launch_flat<10>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st);
-    case 16: return launch_flat<16>(x, ldx, nrows, q, ldq, nq, bias, row_label, q_label, alpha, D, n_chunks, ps, pi, st);
+    case 1: LZK_KS(1);
+    case 2: LZK_KS(2);
+    case 4: LZK_KS(4);
+    case 8: LZK_KS(8);
+    case 10: LZK_KS(10);
+    case 16: LZK_KS(16);
     default: return (int)hipErrorInvalidValue;
   }
+#undef LZK_KS
+}
+
+LZK_EXPORT int lzk_flat_topk_partial(const void* X, long ldx, int nrows, const void* Qm, long ldq,
+                                     int nq, const float* bias, const int* row_label,
+                                     const int* q_label, float alpha, int D, int kslot,
+                                     int n_chunks, float* ps, int* pi, void* stream) {
+  return flat_partial(X, ldx, nrows, Qm, ldq, nq, bias, row_label, q_label, alpha, D, kslot, n_chunks, ps, pi,
+                      stream, nullptr);
+}
+
+LZK_EXPORT int lzk_flat_topk_partial_masked(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq,
+                                            const float* bias, const int* row_label, const int* q_label,
+                                            float alpha, int D, int kslot, int n_chunks, float* ps, int* pi,
+                                            const int* q_active, void* stream) {
+  return flat_partial(X, ldx, nrows, Qm, ldq, nq, bias, row_label, q_label, alpha, D, kslot, n_chunks, ps, pi,
+                      stream, q_active);
+}
+
+static int topk_merge(const float* ps, const int* pi, int ncand, int nq, int kslot, int kout, long idx_offset,
+                      float* os, long* oi, void* stream, const int* q_active) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((nq + 3) / 4), block(256);
+  if (kout > kslot) return (int)hipErrorInvalidValue;
+#define LZK_M(KK) hipLaunchKernelGGL(topk_merge_kernel<KK>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi, q_active)
+  switch (kslot) {
+    case 1: LZK_M(1); break;
+    case 2: LZK_M(2); break;
+    case 4: LZK_M(4); break;
+    case 8: LZK_M(8); break;
+    case 10: LZK_M(10); break;
+    case 16: LZK_M(16); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef LZK_M
+  return (int)hipGetLastError();
 }
 
 LZK_EXPORT int lzk_topk_merge(const float* ps, const int* pi, int ncand, int nq, int kslot,
                               int kout, long idx_offset, float* os, long* oi, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  dim3 grid((nq + 3) / 4), block(256);
-  if (kout > kslot) return (int)hipErrorInvalidValue;
-  switch (kslot) {
-    case 1: hipLaunchKernelGGL(topk_merge_kernel<1>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi); break;
-    case 2: hipLaunchKernelGGL(topk_merge_kernel<2>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi); break;
-    case 4: hipLaunchKernelGGL(topk_merge_kernel<4>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi); break;
-    case 8: hipLaunchKernelGGL(topk_merge_kernel<8>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi); break;
-    case 10: hipLaunchKernelGGL(topk_merge_kernel<10>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi); break;
-    case 16: hipLaunchKernelGGL(topk_merge_kernel<16>, grid, block, 0, st, ps, pi, ncand, nq, kout, idx_offset, os, oi); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-  return (int)hipGetLastError();
+  return topk_merge(ps, pi, ncand, nq, kslot, kout, idx_offset, os, oi, stream, nullptr);
+}
+
+// Merge only the active queries' rows of os/oi (others untouched).
+LZK_EXPORT int lzk_topk_merge_masked(const float* ps, const int* pi, int ncand, int nq, int kslot, int kout,
+                                     long idx_offset, float* os, long* oi, const int* q_active, void* stream) {
+  return topk_merge(ps, pi, ncand, nq, kslot, kout, idx_offset, os, oi, stream, q_active);
 }

@@ -60,6 +60,13 @@ def get_config(name: str) -> EncoderConfig:
     return CONFIGS[k]
 
 
+def _to_dev(t: torch.Tensor, device) -> torch.Tensor:
+    t = t.to(torch.int32)
+    if t.device.type == "cpu" and torch.device(device).type == "cuda":
+        return t.contiguous().pin_memory().to(device, non_blocking=True)
+    return t.to(device).contiguous()
+
+
 class SentenceEncoder:
     """Weights + forward. ``forward(ids [B,S] int32, lens [B] int32)`` returns
     unit-norm fp32 embeddings [B, H] (and optionally a bf16 copy padded to
@@ -142,10 +149,13 @@ class SentenceEncoder:
 
     # --------------------------------------------------------------- forward
     def forward(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0):
+        """ids [B, S] / lens [B] (host or device). Host inputs are staged through
+        pinned memory and copied asynchronously, so enqueueing the forward never
+        waits for earlier GPU work."""
         c, p = self.cfg, self.p
         B, S = ids.shape
-        ids = ids.to(self.device, torch.int32).contiguous()
-        lens = lens.to(self.device, torch.int32).contiguous()
+        ids = _to_dev(ids, self.device)
+        lens = _to_dev(lens, self.device)
         x = E.embed_ln(ids.view(-1), S, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps)
         for i in range(c.layers):
             qkv = E.linear(x, p[f"{i}.wqkv"], p[f"{i}.bqkv"])

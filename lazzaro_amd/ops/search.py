@@ -79,6 +79,7 @@ class _Workspace:
 
 _ws = _Workspace()
 _ws_cand = _Workspace()
+_ws_fallback = _Workspace()
 
 # Large-batch candidate path (csrc/kernels/search256.hip): used when the batch
 # fills whole 256-query tiles and the arena is large enough that the strided
@@ -168,7 +169,8 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
        order difference between the two kernels -> a lower bound of the true
        k-th score, so every true top-k row passes ``score >= thr``.
     2. candidate pass over all rows; 3. exact select per query. Queries whose
-       list overflowed are recomputed with the lane kernel.
+       list overflowed are recomputed with the lane kernel (masked launch, no
+       host synchronisation anywhere on this path).
     """
     L = _lib.lib()
     nq, D = Q.shape
@@ -199,13 +201,21 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
     rc = L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, int(k),
                            int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
     _lib.check(rc, "lzk_cand_select")
-    bad = torch.nonzero(ovf).flatten()
-    if bad.numel():
-        sub_q = Q[bad].contiguous()
-        sub_l = q_label[bad].contiguous() if q_label is not None else None
-        s2, i2 = _flat_topk_lane(X, sub_q, k, kslot, bias, row_label, sub_l, alpha, idx_offset, None)
-        os_[bad] = s2
-        oi[bad] = i2
+    # Overflowed queries are recomputed by the lane kernel ON DEVICE: the masked
+    # launch skips every query tile without an overflowed query (a few us when
+    # none overflowed), so the path never synchronises with the host.
+    nch = L.lzk_flat_topk_chunks(N, nq, TARGET_WGS)
+    part = nq * nch * kslot
+    wsf = _ws_fallback.get(dev, part * 8)
+    ps = wsf[: part * 4].view(torch.float32)
+    pi = wsf[part * 4: part * 8].view(torch.int32)
+    rc = L.lzk_flat_topk_partial_masked(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq,
+                                        _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha), D,
+                                        kslot, nch, ps.data_ptr(), pi.data_ptr(), ovf.data_ptr(), st)
+    _lib.check(rc, "lzk_flat_topk_partial_masked")
+    rc = L.lzk_topk_merge_masked(ps.data_ptr(), pi.data_ptr(), nch * kslot, nq, kslot, int(k), int(idx_offset),
+                                 os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
+    _lib.check(rc, "lzk_topk_merge_masked")
     return os_, oi
 
 
