@@ -129,6 +129,23 @@ PYBIND11_MODULE(_lzrt, m) {
              return py::make_tuple(n, v);
            },
            py::arg("eq"), py::arg("in_col") = "", py::arg("in_vals") = py::none())
+      .def("replace_where",
+           [](Table& t, const std::vector<std::pair<std::string, std::string>>& eq, const std::string& in_col,
+              py::object in_vals, py::dict cols) {
+             Predicate p = make_pred(eq, in_col, in_vals);
+             std::vector<Column> cs;
+             for (auto& spec : t.schema()) {
+               if (!cols.contains(spec.name.c_str())) throw std::runtime_error("missing column " + spec.name);
+               cs.push_back(to_column(spec, cols[spec.name.c_str()]));
+             }
+             uint64_t n = 0, v;
+             {
+               py::gil_scoped_release r;
+               v = t.replace_where(p, cs, &n);
+             }
+             return py::make_tuple(n, v);
+           },
+           py::arg("eq"), py::arg("in_col"), py::arg("in_vals"), py::arg("cols"))
       .def("scan",
            [](Table& t, const std::vector<std::pair<std::string, std::string>>& eq, const std::string& in_col,
               py::object in_vals, const std::vector<std::string>& want) {
@@ -190,6 +207,8 @@ PYBIND11_MODULE(_lzrt, m) {
           union_find(src.data(), dst.data(), (int64_t)src.size(), n, lab);
           return py::array_t<int32_t>(lab.size(), lab.data());
         });
+  m.def("tenant_rank_among", &tenant_rank_among, py::arg("tenant"), py::arg("ranks"),
+        "rendezvous-hash owner of a tenant among an explicit set of rank ids");
   m.def("tenant_rank", &tenant_rank, py::arg("tenant"), py::arg("world"),
         "consistent-hash placement of a tenant id onto one of `world` ranks");
 }

@@ -354,15 +354,14 @@ uint64_t Table::append(const std::vector<Column>& cols_in) {
   return m.version;
 }
 
-uint64_t Table::delete_where(const Predicate& p, uint64_t* n_deleted) {
-  lock();
-  Manifest m = load_latest();
+// Marks rows matching p as deleted in m (new deletion files tagged with
+// version nv); fully deleted fragments leave the manifest. Caller holds the lock.
+uint64_t Table::apply_delete(Manifest& m, const Predicate& p, uint64_t nv) {
   std::vector<int> pcols;
   for (auto& kv : p.eq) pcols.push_back(col_index(kv.first));
   if (p.has_in) pcols.push_back(col_index(p.in_col));
   uint64_t total = 0;
   std::vector<Fragment> keep;
-  const uint64_t nv = m.version + 1;
   for (auto& fr : m.frags) {
     load_deleted(fr);
     std::vector<int> need;
@@ -386,21 +385,71 @@ uint64_t Table::delete_where(const Predicate& p, uint64_t* n_deleted) {
     char dn[128];
     snprintf(dn, sizeof dn, "%s-%llu.del", stem.c_str(), (unsigned long long)nv);
     FILE* f = fopen((dir_ + "/_deletions/" + dn).c_str(), "wb");
-    if (!f) { unlock(); throw std::runtime_error("colstore: cannot write deletion file"); }
+    if (!f) throw std::runtime_error("colstore: cannot write deletion file");
     uint64_t nd = del.size();
-    fwrite(&nd, 8, 1, f);
-    fwrite(del.data(), 4, nd, f);
-    fclose(f);
+    bool ok = fwrite(&nd, 8, 1, f) == 1 && fwrite(del.data(), 4, nd, f) == nd;
+    ok = (fclose(f) == 0) && ok;
+    if (!ok) throw std::runtime_error("colstore: short write of deletion file");
     Fragment nf = fr;
     nf.delfile = dn;
     nf.deleted = del;
     keep.push_back(nf);
   }
-  if (total > 0) {
-    m.frags = keep;
+  m.frags = keep;
+  return total;
+}
+
+uint64_t Table::delete_where(const Predicate& p, uint64_t* n_deleted) {
+  lock();
+  Manifest m;
+  uint64_t total = 0;
+  try {
+    m = load_latest();
+    const uint64_t nv = m.version + 1;
+    total = apply_delete(m, p, nv);
+    if (total > 0) {
+      m.version = nv;
+      write_manifest(m);
+    }
+  } catch (...) { unlock(); throw; }
+  unlock();
+  if (n_deleted) *n_deleted = total;
+  return m.version;
+}
+
+// Delete every row matching p AND append cols in ONE committed version: a
+// reader (or a crash) sees either the old rows or the new ones, never a
+// table with the tenant's rows deleted but not yet re-added.
+uint64_t Table::replace_where(const Predicate& p, const std::vector<Column>& cols_in, uint64_t* n_deleted) {
+  if (cols_in.size() != schema_.size()) throw std::runtime_error("colstore: column count mismatch");
+  const size_t n = cols_in.empty() ? 0 : cols_in[0].size();
+  for (auto& c : cols_in) if (c.size() != n) throw std::runtime_error("colstore: ragged columns");
+  lock();
+  Manifest m;
+  uint64_t total = 0;
+  try {
+    m = load_latest();
+    for (size_t i = 0; i < schema_.size(); ++i) {
+      if (schema_[i].type == ColType::VecF32 && n > 0) {
+        uint32_t d = cols_in[i].dim;
+        for (auto& pc : m.schema) if (pc.name == schema_[i].name && pc.dim) schema_[i].dim = pc.dim;
+        if (schema_[i].dim == 0) schema_[i].dim = d;
+        if (schema_[i].dim != d) throw std::runtime_error("colstore: vector dim mismatch");
+      }
+    }
+    const uint64_t nv = m.version + 1;
+    total = apply_delete(m, p, nv);
+    if (n > 0) {
+      std::string file = uniq_name() + ".lzc";
+      write_fragment(file, cols_in);
+      Fragment fr;
+      fr.file = file;
+      fr.rows = n;
+      m.frags.push_back(fr);
+    }
     m.version = nv;
     write_manifest(m);
-  }
+  } catch (...) { unlock(); throw; }
   unlock();
   if (n_deleted) *n_deleted = total;
   return m.version;

@@ -63,6 +63,8 @@ class Table {
   uint64_t latest_version();                          // re-reads disk
   uint64_t append(const std::vector<Column>& cols);   // returns new version
   uint64_t delete_where(const Predicate& p, uint64_t* n_deleted);
+  // atomic delete_where(p) + append(cols) in one version
+  uint64_t replace_where(const Predicate& p, const std::vector<Column>& cols, uint64_t* n_deleted);
   std::vector<Column> scan(const Predicate& p, const std::vector<std::string>& want);
   uint64_t count_rows();
   uint64_t compact();  // rewrite live rows into one fragment (new version)
@@ -78,6 +80,7 @@ class Table {
   std::string dir_;
   std::vector<ColSpec> schema_;
   Manifest load_latest();
+  uint64_t apply_delete(Manifest& m, const Predicate& p, uint64_t nv);
   void write_manifest(const Manifest& m);
   std::vector<Column> read_fragment(const std::string& file, const std::vector<int>& cols);
   void write_fragment(const std::string& file, const std::vector<Column>& cols);

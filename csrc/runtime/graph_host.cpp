@@ -48,16 +48,34 @@ static uint64_t mix64(uint64_t x) {
   return x;
 }
 
+static uint64_t tenant_hash(const std::string& tenant) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : tenant) { h ^= c; h *= 1099511628211ull; }
+  return h;
+}
+
 int tenant_rank(const std::string& tenant, int world) {
   // rendezvous (highest-random-weight) hashing: adding a rank moves only
   // the tenants that now score highest on it.
-  uint64_t h = 1469598103934665603ull;
-  for (unsigned char c : tenant) { h ^= c; h *= 1099511628211ull; }
+  const uint64_t h = tenant_hash(tenant);
   int best = 0;
   uint64_t bw = 0;
   for (int r = 0; r < world; ++r) {
     uint64_t w = mix64(h ^ (0x9e3779b97f4a7c15ull * (uint64_t)(r + 1)));
     if (r == 0 || w > bw) { bw = w; best = r; }
+  }
+  return best;
+}
+
+int tenant_rank_among(const std::string& tenant, const std::vector<int>& ranks) {
+  // same weights as tenant_rank restricted to the surviving rank ids: when a
+  // rank leaves, only the tenants it owned move (each to its runner-up).
+  const uint64_t h = tenant_hash(tenant);
+  int best = -1;
+  uint64_t bw = 0;
+  for (int r : ranks) {
+    uint64_t w = mix64(h ^ (0x9e3779b97f4a7c15ull * (uint64_t)(r + 1)));
+    if (best < 0 || w > bw) { bw = w; best = r; }
   }
   return best;
 }

@@ -11,4 +11,5 @@ void build_csr(const int32_t* src, const int32_t* dst, int64_t ne, int n, bool u
                std::vector<int64_t>& off, std::vector<int32_t>& adj, std::vector<int32_t>& eid);
 void union_find(const int32_t* src, const int32_t* dst, int64_t ne, int n, std::vector<int32_t>& label);
 int tenant_rank(const std::string& tenant, int world);
+int tenant_rank_among(const std::string& tenant, const std::vector<int>& ranks);
 }  // namespace lzrt

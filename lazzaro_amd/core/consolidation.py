@@ -33,6 +33,7 @@ import numpy as np
 
 from ..models.graph import Edge, Node
 from .similarity import topk_cosine
+from ..utils.faults import EmbeddingError, ProviderError, degenerate_embedding
 from ..utils.tracing import tracer
 
 EXTRACTION_PROMPT = """Extract distinct, atomic facts from this conversation.
@@ -173,11 +174,45 @@ class ConsolidationMixin:
 
     # ------------------------------------------------------------ fact extraction
     def _async_consolidate(self):
+        """Fact extraction -> embed -> ingest (reference memory_system.py:651-785).
+
+        Failure policy: the reference drains the queue first and
+        loses the memories when the LLM call, the JSON parse or the embedding
+        fails. Here a failed batch is put back at the FRONT of the queue with an
+        attempt count and retried by the next consolidation; after
+        ``max_consolidation_retries`` attempts it is dropped and counted.
+        ``strict_errors`` re-raises instead."""
         with self._queue_lock:
             if not self.consolidation_queue:
                 return
             batches, self.consolidation_queue = self.consolidation_queue, []
         t0 = time.time()
+        try:
+            self._consolidate_batches(batches)
+        except Exception as e:
+            self.metrics["consolidation_failures"] = self.metrics.get("consolidation_failures", 0) + 1
+            retry = []
+            for b in batches:
+                b = dict(b)
+                b["attempts"] = b.get("attempts", 0) + 1
+                if b["attempts"] < self.max_consolidation_retries:
+                    retry.append(b)
+                else:
+                    self.metrics["dropped_batches"] = self.metrics.get("dropped_batches", 0) + 1
+            with self._queue_lock:
+                self.consolidation_queue[:0] = retry
+            self._say(f"⚠ Consolidation failed ({type(e).__name__}: {e}); "
+                      f"{len(retry)} batch(es) re-queued")
+            if self.strict_errors:
+                raise
+            return
+        elapsed = time.time() - t0
+        self.metrics["consolidation_times"].append(elapsed)
+        self._say(f"✓ Background consolidation complete ({elapsed:.2f}s)")
+        with self._graph_lock:
+            self._save_to_persistence()
+
+    def _consolidate_batches(self, batches: List[Dict]) -> None:
         memories = [m for b in batches for m in b["memories"]]
         self._say(f"🔄 Processing {len(memories)} memories in background...")
         with tracer.stage("extract_llm", "cpu"):
@@ -189,7 +224,7 @@ class ConsolidationMixin:
             data = _parse_json(response)
         except (json.JSONDecodeError, TypeError) as e:
             self._say(f"⚠ Parse error: {e}")
-            return
+            raise ProviderError(f"unparseable extraction response: {e}") from e
         if isinstance(data, dict):
             facts = data.get("memories", [])
         elif isinstance(data, list):
@@ -203,24 +238,26 @@ class ConsolidationMixin:
         with self._side_stream():
             with tracer.stage("embed_facts", self._device):
                 embs = self._batch_embed([m["content"] for m in kept]) if kept else []
+            if kept and all(degenerate_embedding(e) for e in embs):
+                # a provider outage (zero vectors for everything): retry later
+                raise EmbeddingError("embedding provider returned only degenerate vectors")
             with self._graph_lock, tracer.stage("ingest", self._device):
                 self._ingest_facts(kept, embs)
-        elapsed = time.time() - t0
-        self.metrics["consolidation_times"].append(elapsed)
-        self._say(f"✓ Background consolidation complete ({elapsed:.2f}s)")
-        with self._graph_lock:
-            self._save_to_persistence()
 
     def _ingest_facts(self, facts: List[Dict], embs: List[List[float]]) -> List[Tuple[str, str]]:
         # K5: one batched top-1 search for every fact (the store is unchanged
         # during this loop in the reference too, so this is equivalent).
-        valid = [i for i, e in enumerate(embs) if e is not None and len(e) and any(e)]
+        valid = [i for i, e in enumerate(embs) if e is not None and len(e) and not degenerate_embedding(e)]
+        rejected = len(facts) - len(valid)
+        if rejected:
+            self.metrics["rejected_embeddings"] = self.metrics.get("rejected_embeddings", 0) + rejected
         hits = {}
         if valid:
             res = self._search_batch([embs[i] for i in valid], 1)
             hits = {i: (r[0] if r else None) for i, r in zip(valid, res)}
         new_nodes: List[Tuple[str, str]] = []
         rows = []
+        undo = []  # (node, salience, last_accessed, access_count) of merged duplicates
         for i, mem in enumerate(facts):
             content = mem["content"]
             emb = embs[i] if i < len(embs) else []
@@ -233,6 +270,7 @@ class ConsolidationMixin:
             if best_id is not None:
                 best = self.buffer.get_node(best_id)
                 if best is not None and self._cosine_similarity(emb, best.embedding) > DEDUPE_THRESHOLD:
+                    undo.append((best, best.salience, best.last_accessed, best.access_count))
                     best.salience = max(best.salience, mem.get("salience", 0.5))
                     best.last_accessed = time.time()
                     best.access_count += 1
@@ -247,7 +285,15 @@ class ConsolidationMixin:
                          "salience": node.salience, "shard_key": node.shard_key,
                          "timestamp": node.timestamp})
         if rows:
-            self.vector_store.add_nodes(rows, user_id=self.user_id)
+            try:
+                self.vector_store.add_nodes(rows, user_id=self.user_id)
+            except Exception:
+                # roll the graph back so the re-queued batch applies exactly once
+                for nid, skey in new_nodes:
+                    self.shards[skey].remove_node(nid)
+                for node, sal, la, ac in undo:
+                    node.salience, node.last_accessed, node.access_count = sal, la, ac
+                raise
             if self.query_cache:
                 self.query_cache.invalidate_results()
         self._link_within_shards(new_nodes)

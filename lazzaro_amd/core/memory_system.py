@@ -40,6 +40,7 @@ from .providers import HashEmbedder, LocalLLM, OpenAIEmbedder, OpenAILLM, cosine
 from .query_cache import QueryCache
 from .similarity import EmbeddingCache, topk_cosine
 from .vector_store import HBMStore
+from ..utils.faults import StoreError, degenerate_embedding, fault_point
 from ..utils.tracing import tracer
 
 # kept for parity with code/tests that patch `...memory_system.openai`
@@ -89,6 +90,8 @@ class MemorySystem(ConsolidationMixin):
         metric: str = "l2",
         merge_mode: str = "reference",
         verbose: bool = False,
+        strict_errors: bool = False,
+        max_consolidation_retries: int = 3,
     ):
         self.model = model
         self.user_id = user_id
@@ -130,6 +133,11 @@ class MemorySystem(ConsolidationMixin):
         self.prune_threshold = prune_threshold
         self.max_buffer_size = max_buffer_size
         self.merge_mode = merge_mode
+        # failure policy: strict -> typed errors propagate;
+        # otherwise failures are counted in metrics and work is retried
+        self.strict_errors = strict_errors
+        self.max_consolidation_retries = max_consolidation_retries
+        self._persist_pending = False
 
         self.query_cache = QueryCache(max_size=1000) if enable_caching else None
         self.consolidation_queue: List[Dict] = []
@@ -146,7 +154,8 @@ class MemorySystem(ConsolidationMixin):
         self.node_counter = 0
         self.conversation_count = 0
         self.metrics = {"embedding_calls": 0, "llm_calls": 0, "retrieval_times": [],
-                        "consolidation_times": []}
+                        "consolidation_times": [], "consolidation_failures": 0, "dropped_batches": 0,
+                        "persist_failures": 0, "rejected_embeddings": 0}
         if load_from_disk:
             self._load_from_persistence()
 
@@ -194,8 +203,9 @@ class MemorySystem(ConsolidationMixin):
             hit = self.query_cache.get_embedding(text)
             if hit:
                 return hit
+        fault_point("provider.embed")
         emb = self.embedder.embed(text)
-        if self.query_cache:
+        if self.query_cache and not degenerate_embedding(emb):
             self.query_cache.set_embedding(text, emb)
         return emb
 
@@ -203,6 +213,7 @@ class MemorySystem(ConsolidationMixin):
         if not texts:
             return []
         self.metrics["embedding_calls"] += 1
+        fault_point("provider.embed")
         return self.embedder.batch_embed(texts)
 
     def _cosine_similarity(self, v1, v2) -> float:
@@ -210,6 +221,7 @@ class MemorySystem(ConsolidationMixin):
 
     def _call_llm(self, messages: List[Dict], response_format: Dict = None) -> str:
         self.metrics["llm_calls"] += 1
+        fault_point("provider.llm")
         return self.llm.completion(messages, response_format)
 
     def _search_batch(self, embs: List[List[float]], k: int) -> List[List[str]]:
@@ -554,16 +566,35 @@ STORAGE:
 
     # ------------------------------------------------------------ store sync
     def _save_to_persistence(self):
+        """Write the tenant's graph to the store (reference memory_system.py:
+        1275-1302). With a native store the rewrite is one atomic version per
+        table. A failed commit leaves the in-memory graph authoritative: it is
+        counted, logged, and the next save rewrites everything again
+        (``strict_errors`` raises :class:`StoreError` instead)."""
         with self._graph_lock:
             nodes = [n.to_dict() for n in self.buffer.nodes.values()]
             edges = [e.to_dict() for sh in self.shards.values() for e in sh.edges.values()]
-            self.store.delete_nodes([], user_id=self.user_id)
-            self.store.delete_edges(user_id=self.user_id)
-            if nodes:
-                self.store.add_nodes(nodes, user_id=self.user_id)
-            if edges:
-                self.store.add_edges(edges, user_id=self.user_id)
-            self.store.save_profile(self.profile.to_dict(), user_id=self.user_id)
+            try:
+                if hasattr(self.store, "replace_user_nodes"):
+                    self.store.replace_user_nodes(nodes, user_id=self.user_id)
+                    self.store.replace_user_edges(edges, user_id=self.user_id)
+                else:  # third-party Store protocol: the reference's delete + add
+                    self.store.delete_nodes([], user_id=self.user_id)
+                    self.store.delete_edges(user_id=self.user_id)
+                    if nodes:
+                        self.store.add_nodes(nodes, user_id=self.user_id)
+                    if edges:
+                        self.store.add_edges(edges, user_id=self.user_id)
+                self.store.save_profile(self.profile.to_dict(), user_id=self.user_id)
+            except Exception as e:
+                self.metrics["persist_failures"] = self.metrics.get("persist_failures", 0) + 1
+                self._persist_pending = True
+                log.warning("persistence failed for %s: %s", self.user_id, e)
+                self._say(f"⚠ Persistence failed for user {self.user_id}: {e}")
+                if self.strict_errors:
+                    raise StoreError(str(e)) from e
+                return
+            self._persist_pending = False
             try:
                 # our own write is not an "update from elsewhere" (reference
                 # re-loads after its own saves, SURVEY.md App. C)

@@ -138,6 +138,20 @@ class HBMStore:
             a.add([r["id"] for r in rows], np.asarray([r["vector"] for r in rows], dtype=np.float32))
             self._after_write(user_id, prev, v)
 
+    def replace_user_nodes(self, nodes: List[Dict[str, Any]], user_id: str = "default") -> None:
+        """Atomic per-tenant rewrite (one committed version): the delete-all +
+        add-all of the reference's ``_save_to_persistence`` (memory_system.py:
+        1275-1302) without the window in which the tenant has no rows."""
+        rows = self._node_rows(nodes, user_id)
+        with self._lock:
+            a = self._arena(user_id)
+            prev = self._synced.get(user_id)
+            _, v = self._nodes_table.replace_rows([("user_id", user_id)], rows)
+            a.clear()
+            if rows:
+                a.add([r["id"] for r in rows], np.asarray([r["vector"] for r in rows], dtype=np.float32))
+            self._after_write(user_id, prev, v)
+
     def get_nodes(self, user_id: str = "default") -> List[Dict[str, Any]]:
         rows = self._nodes_table.scan([("user_id", user_id)])
         for r in rows:
@@ -181,9 +195,8 @@ class HBMStore:
         return sorted(set(cols.get("user_id", [])))
 
     # ------------------------------------------------------------ edges
-    def add_edges(self, edges: List[Dict[str, Any]], user_id: str = "default") -> None:
-        if not edges:
-            return
+    @staticmethod
+    def _edge_rows(edges: List[Dict[str, Any]], user_id: str) -> List[Dict[str, Any]]:
         rows = []
         for e in edges:
             src = e.get("source") or e.get("source_id")
@@ -197,7 +210,16 @@ class HBMStore:
                 "last_updated": float(e.get("last_updated", 0.0)),
                 "metadata": _json(e.get("metadata", {}), {}),
             })
-        self._edges_table.add_rows(rows)
+        return rows
+
+    def add_edges(self, edges: List[Dict[str, Any]], user_id: str = "default") -> None:
+        if not edges:
+            return
+        self._edges_table.add_rows(self._edge_rows(edges, user_id))
+
+    def replace_user_edges(self, edges: List[Dict[str, Any]], user_id: str = "default") -> None:
+        """Atomic per-tenant edge rewrite (see :meth:`replace_user_nodes`)."""
+        self._edges_table.replace_rows([("user_id", user_id)], self._edge_rows(edges, user_id))
 
     def delete_edges(self, source_id: Optional[str] = None, user_id: str = "default") -> None:
         eq = [("user_id", user_id)]
@@ -217,9 +239,8 @@ class HBMStore:
 
     # ------------------------------------------------------------ profiles
     def save_profile(self, profile_data: Dict[str, Any], user_id: str = "default") -> None:
-        self._profile_table.delete([("user_id", user_id)])
-        self._profile_table.add_rows([{"user_id": user_id, "data": json.dumps(profile_data),
-                                       "updated_at": time.time()}])
+        self._profile_table.replace_rows([("user_id", user_id)], [{"user_id": user_id, "data": json.dumps(profile_data),
+                                                                   "updated_at": time.time()}])
 
     def load_profile(self, user_id: str = "default") -> Optional[Dict[str, Any]]:
         rows = self._profile_table.scan([("user_id", user_id)])

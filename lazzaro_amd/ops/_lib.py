@@ -94,8 +94,11 @@ def stream_ptr(device=None) -> int:
 
 
 def check(rc: int, what: str) -> None:
+    """Every kernel launch reports through here: typed error + fault point."""
+    from ..utils.faults import KernelError, fault_point
+    fault_point("kernel." + what)
     if rc != 0:
-        raise RuntimeError(f"{what} failed with hipError {rc}")
+        raise KernelError(f"{what} failed with hipError {rc}")
 
 
 def ptr(t) -> int:

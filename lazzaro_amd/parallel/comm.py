@@ -22,6 +22,27 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from ..utils.faults import CommError, fault_point
+
+
+def _guarded(name):
+    """Fault point + typed error for one collective."""
+    def deco(fn):
+        def wrapper(self, *a, **kw):
+            fault_point("comm." + name)
+            if not self.enabled:
+                return fn(self, *a, **kw)
+            try:
+                return fn(self, *a, **kw)
+            except CommError:
+                raise
+            except (RuntimeError, ValueError) as e:  # DistBackendError / timeouts derive from RuntimeError
+                raise CommError(f"{name} failed on rank {self.rank}/{self.world}: {e}") from e
+        wrapper.__name__ = fn.__name__
+        wrapper.__doc__ = fn.__doc__
+        return wrapper
+    return deco
+
 
 class Communicator:
     def __init__(self, group=None, device: Optional[torch.device] = None):
@@ -58,21 +79,25 @@ class Communicator:
         return cls()
 
     # ---------------------------------------------------------------- basics
+    @_guarded("barrier")
     def barrier(self) -> None:
         if self.enabled:
             dist.barrier(group=self.group)
 
+    @_guarded("all_reduce")
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.enabled:
             ops = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
             dist.all_reduce(t, op=ops[op], group=self.group)
         return t
 
+    @_guarded("broadcast")
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.enabled:
             dist.broadcast(t, src=src, group=self.group)
         return t
 
+    @_guarded("all_gather_rows")
     def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
         """Concatenate equal-shaped tensors from every rank along dim 0."""
         if not self.enabled:
@@ -81,6 +106,7 @@ class Communicator:
         dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out
 
+    @_guarded("all_gather_object")
     def all_gather_object(self, obj) -> List:
         if not self.enabled:
             return [obj]
@@ -89,6 +115,7 @@ class Communicator:
         return out
 
     # ---------------------------------------------------------------- all-to-all-v
+    @_guarded("exchange_counts")
     def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
         if not self.enabled:
             return send_counts.clone()
@@ -96,6 +123,7 @@ class Communicator:
         dist.all_to_all_single(recv, send_counts, group=self.group)
         return recv
 
+    @_guarded("all_to_all_v")
     def all_to_all_v(self, t: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]) -> torch.Tensor:
         """Rows of ``t`` are grouped by destination rank (send_counts[r] rows
         for rank r, in rank order); returns rows received, grouped by source."""

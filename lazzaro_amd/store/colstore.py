@@ -15,6 +15,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from ..utils.faults import fault_point
+
 STR, F64, F32, I32, BOOL, VEC, I64 = 0, 1, 2, 3, 4, 5, 6
 
 
@@ -59,24 +61,38 @@ class ColumnarTable:
     def version(self) -> int:
         return int(self._t.latest_version())
 
-    def add_rows(self, rows: Sequence[Dict]) -> int:
-        if not rows:
-            return self.version
+    def _columns(self, rows: Sequence[Dict]) -> Dict:
         cols = {}
-        for n, t, _ in self.schema:
+        for n, t, d in self.schema:
             vals = [r[n] for r in rows]
             if t == STR:
                 cols[n] = [("" if v is None else str(v)) for v in vals]
             elif t == VEC:
-                cols[n] = np.asarray(vals, dtype=np.float32).reshape(len(rows), -1)
+                cols[n] = (np.asarray(vals, dtype=np.float32).reshape(len(rows), -1) if rows
+                           else np.zeros((0, d or 0), dtype=np.float32))
             else:
                 cols[n] = np.asarray(vals, dtype=_NP[t])
-        return int(self._t.append(cols))
+        return cols
+
+    def add_rows(self, rows: Sequence[Dict]) -> int:
+        if not rows:
+            return self.version
+        fault_point("store.commit")
+        return int(self._t.append(self._columns(rows)))
+
+    def replace_rows(self, eq: Sequence[Tuple[str, str]], rows: Sequence[Dict]) -> Tuple[int, int]:
+        """Atomically delete the rows matching ``eq`` and append ``rows`` (one
+        committed version). Returns (rows deleted, new version)."""
+        fault_point("store.commit")
+        n, v = self._t.replace_where(list(eq), "", None, self._columns(rows))
+        return int(n), int(v)
 
     def add_columns(self, cols: Dict) -> int:
+        fault_point("store.commit")
         return int(self._t.append(cols))
 
     def delete(self, eq: Sequence[Tuple[str, str]], in_col: str = "", in_vals=None) -> Tuple[int, int]:
+        fault_point("store.commit")
         n, v = self._t.delete_where(list(eq), in_col, None if in_vals is None else list(in_vals))
         return int(n), int(v)
 
