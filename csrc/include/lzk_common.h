@@ -18,6 +18,37 @@ typedef u16 u16x4 __attribute__((ext_vector_type(4)));
 
 #define LZK_EXPORT extern "C" __attribute__((visibility("default")))
 
+// Debug builds (-DLZK_DEBUG=1, `python -m lazzaro_amd._build --debug`, loaded
+// with LZK_DEBUG=1): LZK_DCHECK(cond) in index-driven kernels records the
+// first violated condition (line number) in a per-file device word, prints it
+// once, and skips the offending thread's work instead of faulting the GPU.
+// Use only where an early return cannot strand a barrier. Release builds
+// compile it away. LZK_DEBUG_STATE(name) defines the word and an exported
+// `lzk_<name>_debug_errors()` that returns and clears it.
+#if defined(LZK_DEBUG) && LZK_DEBUG
+#define LZK_DCHECK(cond)                                                                              \
+  do {                                                                                                \
+    if (!(cond)) {                                                                                    \
+      if (atomicCAS(&g_lzk_dbg_err, 0, __LINE__) == 0)                                                \
+        printf("LZK_DCHECK failed: %s (%s:%d) block %d thread %d\n", #cond, __FILE__, __LINE__,       \
+               (int)blockIdx.x, (int)threadIdx.x);                                                    \
+      return;                                                                                         \
+    }                                                                                                 \
+  } while (0)
+#define LZK_DEBUG_STATE(name)                                                                         \
+  static __device__ int g_lzk_dbg_err = 0;                                                            \
+  LZK_EXPORT int lzk_##name##_debug_errors() {                                                        \
+    int v = 0, z = 0;                                                                                 \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_lzk_dbg_err), sizeof(int)) != hipSuccess) return -1;     \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lzk_dbg_err), &z, sizeof(int));                              \
+    return v;                                                                                         \
+  }
+#else
+#define LZK_DCHECK(cond) do { } while (0)
+#define LZK_DEBUG_STATE(name) \
+  LZK_EXPORT int lzk_##name##_debug_errors() { return 0; }
+#endif
+
 // bf16 <-> f32 by bit manipulation (round-to-nearest-even on the way down).
 __device__ __forceinline__ float bf16_to_f32(u16 v) {
   return __uint_as_float(((unsigned)v) << 16);

@@ -13,6 +13,8 @@
 // co_occurrence i32, last_updated f64.
 #include "lzk_tile.h"
 
+LZK_DEBUG_STATE(graph)
+
 namespace {
 
 constexpr int NTB = 256;
@@ -136,7 +138,9 @@ __global__ __launch_bounds__(NTB) void importance_kernel(const float* __restrict
 
 __global__ __launch_bounds__(NTB) void mark_dead_kernel(const long* __restrict__ idx, long n, unsigned char* __restrict__ alive) {
   const long i = (long)blockIdx.x * NTB + threadIdx.x;
-  if (i < n) alive[idx[i]] = 0;
+  if (i >= n) return;
+  LZK_DCHECK(idx[i] >= 0);
+  alive[idx[i]] = 0;
 }
 
 // ------------------------------------------------------------------ K9
@@ -152,6 +156,7 @@ __global__ __launch_bounds__(NTB) void cc_hook_kernel(const int* __restrict__ sr
                                                       int* __restrict__ changed) {
   const long e = (long)blockIdx.x * NTB + threadIdx.x;
   if (e >= ne) return;
+  LZK_DCHECK(src[e] >= 0 && dst[e] >= 0);
   if (w && w[e] < min_w) return;
   int ru = find_root(parent, src[e]);
   int rv = find_root(parent, dst[e]);
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(256) void seg_sum_kernel(const u16* __restrict__ X,
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= n) return;
+  LZK_DCHECK(label[r] >= 0);
   const int c = label[r];
   if (c < 0) return;
   for (int d = lane * 4; d < D; d += 256) {

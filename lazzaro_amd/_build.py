@@ -46,9 +46,18 @@ def _run(cmd):
     return r.stdout
 
 
-def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
+def build_kernels(verbose: bool = False, jobs: int = 8, debug: bool = False, sanitize: str = "") -> str:
+    """Compile every csrc/kernels/*.hip for gfx950 into one C-ABI library.
+
+    debug=True   -> ``liblzk_debug.so`` with ``-DLZK_DEBUG=1``: device-side
+                    bounds asserts (``LZK_DASSERT``) in the index-driven kernels
+                    (graph ops, gathers); loaded instead of liblzk.so when
+                    ``LZK_DEBUG=1``.
+    sanitize="address" (or "undefined") -> host-side sanitizer on the launcher
+                    code only (``-Xarch_host -fsanitize=...``); GPU sanitizers are
+                    not available on this pool. Implies the debug library.
+    """
     os.makedirs(LIBDIR, exist_ok=True)
-    os.makedirs(BUILDDIR, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     flags = [
@@ -56,10 +65,21 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
         "-fvisibility=hidden", "-mcode-object-version=5",
         "-I" + os.path.join(CSRC, "include"),
     ]
+    tag = ""
+    if debug or sanitize:
+        flags.append("-DLZK_DEBUG=1")
+        tag = "_debug"
+    for san in filter(None, sanitize.split(",")):
+        flags += ["-Xarch_host", f"-fsanitize={san}"]
+        tag += "_" + san
+    if sanitize:
+        flags += ["-Xarch_host", "-fno-omit-frame-pointer", "-g"]
+    bdir = BUILDDIR + tag
+    os.makedirs(bdir, exist_ok=True)
     objs = []
     todo = []
     for s in srcs:
-        o = os.path.join(BUILDDIR, os.path.basename(s) + ".o")
+        o = os.path.join(bdir, os.path.basename(s) + ".o")
         objs.append(o)
         if _newer(o, [s] + headers):
             todo.append((s, o))
@@ -73,29 +93,40 @@ def build_kernels(verbose: bool = False, jobs: int = 8) -> str:
     if todo:
         with ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
             list(ex.map(comp, todo))
-    out = os.path.join(LIBDIR, "liblzk.so")
+    out = os.path.join(LIBDIR, f"liblzk{tag}.so")
     if _newer(out, objs) or not objs:
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
+        for san in filter(None, sanitize.split(",")):
+            link += ["-Xarch_host", f"-fsanitize={san}"]
+        _run(link)
     return out
 
 
-def build_runtime(verbose: bool = False) -> str:
+def build_runtime(verbose: bool = False, sanitize: str = "", outdir: str = "") -> str:
+    """Build the pybind11 host runtime. ``sanitize`` ("address", "undefined"
+    or both, comma separated) builds an instrumented copy into ``outdir``
+    (default ``_lib/san``) -- load it with the sanitizer runtime preloaded
+    (see tests/unit/test_sanitizers.py)."""
     import pybind11
 
-    os.makedirs(LIBDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    out = os.path.join(LIBDIR, "_lzrt" + suffix)
+    odir = outdir or (os.path.join(LIBDIR, "san") if sanitize else LIBDIR)
+    os.makedirs(odir, exist_ok=True)
+    out = os.path.join(odir, "_lzrt" + suffix)
     if not srcs:
         return ""
     if _newer(out, srcs + headers):
         if verbose:
-            print("[g++] runtime", flush=True)
+            print("[g++] runtime" + (f" (sanitize={sanitize})" if sanitize else ""), flush=True)
         cxx = shutil.which("g++") or "c++"
-        cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
-               "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
-               "-I" + os.path.join(CSRC, "runtime")] + srcs + ["-o", out, "-lpthread"]
+        opt = ["-O3"]
+        if sanitize:
+            opt = ["-O1", "-g", "-fno-omit-frame-pointer"] + [f"-fsanitize={x}" for x in sanitize.split(",") if x]
+        cmd = [cxx] + opt + ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+                             "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
+                             "-I" + os.path.join(CSRC, "runtime")] + srcs + ["-o", out, "-lpthread"]
         _run(cmd)
     return out
 
@@ -108,5 +139,15 @@ def build_all(verbose: bool = True) -> None:
 
 
 if __name__ == "__main__":
+    import argparse
+
+    ap = argparse.ArgumentParser(description="build the lazzaro_amd native libraries in-tree")
+    ap.add_argument("--debug", action="store_true", help="also build liblzk_debug.so (device bounds asserts)")
+    ap.add_argument("--sanitize", default="", help="host sanitizer(s) for debug builds, e.g. address,undefined")
+    a = ap.parse_args()
     build_all(verbose=True)
+    if a.debug or a.sanitize:
+        print("built:", build_kernels(verbose=True, debug=True, sanitize=a.sanitize))
+    if a.sanitize:
+        print("built:", build_runtime(verbose=True, sanitize=a.sanitize))
     sys.exit(0)

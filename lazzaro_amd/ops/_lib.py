@@ -18,7 +18,9 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_HERE, "_lib", "liblzk.so")
+# LZK_DEBUG=1 selects the build with device-side bounds asserts
+# (``python -m lazzaro_amd._build --debug``)
+LIB_PATH = os.path.join(_HERE, "_lib", "liblzk_debug.so" if os.environ.get("LZK_DEBUG") == "1" else "liblzk.so")
 
 _lock = threading.Lock()
 _lib = None
@@ -75,7 +77,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             if os.environ.get("LZK_AUTOBUILD", "1") == "1":
                 from .. import _build
-                _build.build_kernels(verbose=True)
+                _build.build_kernels(verbose=True, debug=os.environ.get("LZK_DEBUG") == "1")
             if not os.path.exists(LIB_PATH):
                 raise KernelLibraryMissing(
                     f"HIP kernel library not found at {LIB_PATH}; run `python -m lazzaro_amd._build`")

@@ -159,3 +159,29 @@ def test_ivfpq_dense_deep_rerank():
     _, i_rr = gi.search(q, 10, nprobe=8, rerank=200)
     r_pq, r_rr = recall_at_k(i_pq, truth), recall_at_k(i_rr, truth)
     assert r_rr >= r_pq and r_rr > 0.9, (r_pq, r_rr)
+
+
+def test_debug_build_catches_bad_index():
+    """LZK_DEBUG build: a negative edge endpoint is reported by LZK_DCHECK
+    (per-file error word) and skipped instead of being dereferenced."""
+    import ctypes
+    import os
+
+    from lazzaro_amd.ops import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "liblzk_debug.so")
+    if not os.path.exists(path):
+        pytest.skip("debug library not built (python -m lazzaro_amd._build --debug)")
+    L = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    L.lzk_cc_hook.argtypes = [P, P, ctypes.c_long, P, ctypes.c_float, P, P, P]
+    L.lzk_graph_debug_errors.restype = ctypes.c_int
+    assert L.lzk_graph_debug_errors() == 0
+    src = torch.tensor([0, -1, 2], dtype=torch.int32, device="cuda")
+    dst = torch.tensor([1, 2, 0], dtype=torch.int32, device="cuda")
+    parent = torch.arange(3, dtype=torch.int32, device="cuda")
+    changed = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rc = L.lzk_cc_hook(src.data_ptr(), dst.data_ptr(), 3, None, 0.0, parent.data_ptr(), changed.data_ptr(),
+                       _lib.stream_ptr(src.device))
+    torch.cuda.synchronize()
+    assert rc == 0 and L.lzk_graph_debug_errors() > 0
+    assert L.lzk_graph_debug_errors() == 0  # read-and-clear
