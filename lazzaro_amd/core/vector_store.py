@@ -20,7 +20,7 @@ import json
 import os
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Sequence, Any, Dict, List, Optional
 
 import numpy as np
 
@@ -173,6 +173,25 @@ class HBMStore:
         if len(a) == 0 or len(query_embs) == 0:
             return [[] for _ in range(len(query_embs))]
         return a.search(query_embs, int(limit), self.metric)
+
+    def search_nodes_multi(self, query_embs, user_ids: Sequence[str], limit: int = 5) -> List[List[str]]:
+        """Multi-tenant batch: query i searches tenant ``user_ids[i]`` only, all
+        in one kernel launch (serving many users per GPU, BASELINE config 3)."""
+        from ..index.arena import multi_arena_search
+        if len(user_ids) == 0:
+            return []
+        arenas = [self._arena(u) for u in user_ids]
+        dims = {a.dim for a in arenas if len(a)}
+        if len(dims) > 1 or any(a.dim is not None and len(a) and a.dim != len(query_embs[0]) for a in arenas):
+            return [self.search_nodes(q, u, limit) for q, u in zip(query_embs, user_ids)]
+        if not dims:
+            return [[] for _ in user_ids]
+        s, r = multi_arena_search(arenas, query_embs, int(limit), self.metric)
+        s, r = s.cpu().tolist(), r.cpu().tolist()
+        out = []
+        for a, rs, ss in zip(arenas, r, s):
+            out.append([a.ids[x] for x, v in zip(rs, ss) if x >= 0 and v != float("-inf") and a.ids[x] is not None])
+        return out
 
     def delete_nodes(self, node_ids: Optional[List[str]], user_id: str = "default") -> None:
         with self._lock:

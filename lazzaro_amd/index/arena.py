@@ -33,6 +33,40 @@ def _pad64(d: int) -> int:
     return (d + 63) // 64 * 64
 
 
+def multi_arena_search(arenas: Sequence["VectorArena"], queries, k: int, metric: str = "l2"):
+    """Query q searches arenas[q] only; one segment-kernel launch for the
+    whole batch (ops.search.segment_topk). Returns (scores, rows) like
+    :meth:`VectorArena.search_rows` (score = -L2^2 / cosine / dot)."""
+    nq = len(arenas)
+    qf = torch.as_tensor(np.asarray(queries, dtype=np.float32)) if not torch.is_tensor(queries) else queries.float()
+    dev = arenas[0].device if nq else torch.device("cpu")
+    qf = qf.to(dev)
+    if metric == "cosine":
+        qf = qf / qf.norm(dim=1, keepdim=True).clamp_min(1e-30)
+    segs = [a.segment(metric) for a in arenas]
+    rows = [s[0] for s in segs]
+    dt = rows[0].dtype if nq else torch.float32
+    width = max(r.shape[1] for r in rows) if nq else 0
+    D = qf.shape[1]
+    ok = all(r.dtype == dt and (r.shape[0] == 0 or r.shape[1] == width) for r in rows)
+    if not ok:
+        raise ValueError("multi_arena_search: arenas of different dtype / width in one batch")
+    Q = torch.zeros((nq, width), dtype=dt, device=dev)
+    Q[:, :D] = qf.to(dt)
+    # empty segments still need a row pointer of the common stride
+    filler = next((r for r in rows if r.shape[0] > 0), None)
+    if filler is None:
+        return (torch.full((nq, k), NEG_INF, device=dev), torch.full((nq, k), -1, dtype=torch.long, device=dev))
+    rows = [r if r.shape[0] > 0 else filler[:0] for r in rows]
+    zero = torch.zeros(1, dtype=torch.float32, device=dev)
+    biases = [s[1] if s[1] is not None else zero for s in segs]
+    scales = [s[2] if s[2] is not None else torch.ones(max(1, r.shape[0]), device=dev)
+              for s, r in zip(segs, rows)] if metric == "cosine" else None
+    alpha = 2.0 if metric == "l2" else 1.0
+    qbias = -(qf * qf).sum(1) if metric == "l2" else None
+    return S.segment_topk(rows, Q, k, biases=biases, scales=scales, alpha=alpha, qbias=qbias)
+
+
 class VectorArena:
     def __init__(self, dim: Optional[int] = None, device=None, capacity: int = 256,
                  keep_fp32: bool = True, store_dtype: Optional[torch.dtype] = None):
@@ -228,6 +262,31 @@ class VectorArena:
         r = torch.gather(cr, 1, o)
         o = torch.argsort(-s, dim=1, stable=True)[:, :k]
         return torch.gather(s, 1, o), torch.gather(r, 1, o)
+
+    def segment(self, metric: str = "l2"):
+        """(rows, bias, scale) describing this arena for the multi-tenant
+        segment kernel: exact fp32 rows when kept (no re-rank needed), the
+        metric folded into a per-row bias / scale (cached per version)."""
+        key = (metric, self.version, self.n)
+        c = getattr(self, "_seg_cache", None)
+        if c is not None and c[0] == key:
+            return c[1]
+        n = self.n
+        if n == 0 or self.X is None:
+            rows = torch.zeros((0, _pad64(self.dim or 64) if self.on_gpu else (self.dim or 1)),
+                               dtype=self.store_dtype, device=self.device)
+            out = (rows, None, None)
+        else:
+            use32 = self.X32 is not None and self.dim % 32 == 0
+            rows = self.X32[:n] if use32 else self.X[:n]
+            if metric == "l2":
+                bias = (self.bias[:n] - self.sqn[:n]).contiguous()
+            else:
+                bias = self.bias[:n].contiguous()
+            scale = self.sqn[:n].sqrt().clamp_min(1e-30).reciprocal().contiguous() if metric == "cosine" else None
+            out = (rows, bias, scale)
+        self._seg_cache = (key, out)
+        return out
 
     def search(self, q, k: int, metric: str = "l2") -> List[List[str]]:
         s, r = self.search_rows(q, k, metric)

@@ -219,6 +219,64 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
     return os_, oi
 
 
+def segment_topk(xs, Q: torch.Tensor, k: int, *, biases=None, scales=None, alpha: float = 1.0, qbias=None):
+    """Multi-tenant batch: query ``q`` scans only the rows ``xs[q]`` (its tenant's
+    arena or a slice of a shared arena) -- one launch for the whole batch
+    (csrc/kernels/segment.hip).
+
+    score = alpha * <Q[q], xs[q][r]> * scales[q][r] + biases[q][r] + qbias[q].
+    ``xs``: list of 2-D tensors with a common dtype (bf16 or fp32) and row
+    stride; ``biases``/``scales``: None or lists of fp32 vectors. Returns
+    (scores [nq, k] fp32, rows [nq, k] int64 local to each segment, -1 empty).
+    """
+    nq = Q.shape[0]
+    assert len(xs) == nq
+    dev = Q.device
+    D = Q.shape[1]
+    if not Q.is_cuda:
+        out_s = torch.full((nq, k), float("-inf"))
+        out_i = torch.full((nq, k), -1, dtype=torch.long)
+        for q in range(nq):
+            X = xs[q]
+            if X.shape[0] == 0:
+                continue
+            s = alpha * (X[:, :D].float() @ Q[q].float())
+            if scales is not None and scales[q] is not None:
+                s = s * scales[q].float()
+            if biases is not None and biases[q] is not None:
+                s = s + biases[q].float()
+            if qbias is not None:
+                s = s + float(qbias[q])
+            o = torch.argsort(-s, stable=True)[:k]
+            keep = ~torch.isinf(s[o]) | (s[o] > 0)
+            o = o[keep]
+            out_s[q, : o.numel()] = s[o]
+            out_i[q, : o.numel()] = o
+        return out_s, out_i
+    L = _lib.lib()
+    kslot = L.lzk_flat_topk_kslot(int(k))
+    if kslot < 0:
+        raise ValueError("segment_topk supports k <= 16")
+    dt = {torch.bfloat16: 0, torch.float32: 1}[Q.dtype]
+    ld = xs[0].stride(0) if nq else D
+    for X in xs:
+        assert X.dtype == Q.dtype and (X.shape[0] <= 1 or X.stride(0) == ld) and X.stride(-1) == 1
+    def ptrs(ts):
+        return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    xp = ptrs(xs)
+    nr = torch.tensor([X.shape[0] for X in xs], dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+    bp = ptrs(biases) if biases is not None else None
+    sp = ptrs(scales) if scales is not None else None
+    qb = qbias.float().contiguous() if qbias is not None else None
+    os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    oi = torch.empty((nq, k), dtype=torch.long, device=dev)
+    rc = L.lzk_segment_topk(xp.data_ptr(), nr.data_ptr(), int(ld), _lib.ptr(bp), _lib.ptr(sp), Q.data_ptr(),
+                            Q.stride(0), nq, D, dt, float(alpha), _lib.ptr(qb), kslot, int(k), os_.data_ptr(),
+                            oi.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(rc, "lzk_segment_topk")
+    return os_, oi
+
+
 def topk_large(X, Q, k, *, bias=None, alpha=1.0, idx_offset=0, chunk=1 << 20):
     """k > 16: per-chunk candidate generation with the fused kernel at k=16
     cannot be exact, so this path scores chunks with the GEMM library and

@@ -149,3 +149,41 @@ def test_encoder_forward_matches_cpu(model):
     b, _ = cpu.forward(ids, lens)
     cos = (a.cpu() * b).sum(1)
     assert (cos > 0.99).all(), cos
+
+
+@pytest.mark.parametrize("dtype,D", [(torch.bfloat16, 768), (torch.float32, 384), (torch.bfloat16, 64)])
+def test_segment_topk_gpu(dtype, D):
+    from lazzaro_amd.ops.search import segment_topk
+    g = torch.Generator(device=DEV).manual_seed(D)
+    big = torch.randn(5000, D, device=DEV, generator=g).to(dtype)
+    cuts = [(0, 0), (0, 1), (10, 700), (700, 5000), (123, 124), (4000, 4033)]
+    xs = [big[a:b] for a, b in cuts] * 3
+    Q = torch.randn(len(xs), D, device=DEV, generator=g).to(dtype)
+    bias = torch.randn(5000, device=DEV, generator=g)
+    bs = [bias[a:b] if b > a else bias[:1] for a, b in cuts] * 3
+    s, i = segment_topk(xs, Q, 10, biases=bs, alpha=2.0)
+    rs, ri = segment_topk([x.cpu().float() for x in xs], Q.cpu().float(), 10,
+                          biases=[b.cpu() for b in bs], alpha=2.0)
+    torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
+    assert (i.cpu() == ri).float().mean() > 0.99
+
+
+def test_multi_arena_search_gpu():
+    import numpy as np
+
+    from lazzaro_amd.index.arena import VectorArena, multi_arena_search
+    rng = np.random.default_rng(0)
+    arenas = []
+    for t in range(40):
+        a = VectorArena(dim=768, device=DEV)
+        n = int(rng.integers(1, 400))
+        a.add([f"{t}_{i}" for i in range(n)], rng.standard_normal((n, 768)).astype(np.float32))
+        arenas.append(a)
+    owners = [arenas[int(j)] for j in rng.integers(0, 40, 300)]
+    q = rng.standard_normal((300, 768)).astype(np.float32)
+    for metric in ("l2", "cosine", "ip"):
+        s, r = multi_arena_search(owners, q, 5, metric)
+        for j in range(0, 300, 37):
+            rs, rr = owners[j].search_rows(q[j:j + 1], 5, metric)
+            assert torch.equal(r[j].cpu(), rr[0].cpu()), metric
+            torch.testing.assert_close(s[j].cpu(), rs[0].cpu(), atol=1e-3, rtol=1e-4)
