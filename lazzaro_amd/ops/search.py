@@ -253,24 +253,35 @@ def segment_topk(xs, Q: torch.Tensor, k: int, *, biases=None, scales=None, alpha
             out_s[q, : o.numel()] = s[o]
             out_i[q, : o.numel()] = o
         return out_s, out_i
+    dt = Q.dtype
+    ld = xs[0].stride(0) if nq else D
+    for X in xs:
+        assert X.dtype == dt and (X.shape[0] <= 1 or X.stride(0) == ld) and X.stride(-1) == 1
+
+    def ptrs(ts):
+        return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    nr = torch.tensor([X.shape[0] for X in xs], dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+    return segment_topk_ptrs(ptrs(xs), nr, ld, Q, k, bptr=ptrs(biases) if biases is not None else None,
+                             sptr=ptrs(scales) if scales is not None else None, alpha=alpha, qbias=qbias)
+
+
+def segment_topk_ptrs(xptr: torch.Tensor, nrows: torch.Tensor, ld: int, Q: torch.Tensor, k: int, *,
+                      bptr=None, sptr=None, alpha: float = 1.0, qbias=None):
+    """Device-side form of :func:`segment_topk`: ``xptr``/``bptr``/``sptr`` are
+    int64 device tensors of row / bias / scale base addresses per query and
+    ``nrows`` int32 row counts (e.g. gathered from a tenant table with one
+    indexing op), so a serving loop builds no Python lists per batch."""
     L = _lib.lib()
     kslot = L.lzk_flat_topk_kslot(int(k))
     if kslot < 0:
         raise ValueError("segment_topk supports k <= 16")
+    nq, D = Q.shape
+    dev = Q.device
     dt = {torch.bfloat16: 0, torch.float32: 1}[Q.dtype]
-    ld = xs[0].stride(0) if nq else D
-    for X in xs:
-        assert X.dtype == Q.dtype and (X.shape[0] <= 1 or X.stride(0) == ld) and X.stride(-1) == 1
-    def ptrs(ts):
-        return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
-    xp = ptrs(xs)
-    nr = torch.tensor([X.shape[0] for X in xs], dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
-    bp = ptrs(biases) if biases is not None else None
-    sp = ptrs(scales) if scales is not None else None
     qb = qbias.float().contiguous() if qbias is not None else None
     os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oi = torch.empty((nq, k), dtype=torch.long, device=dev)
-    rc = L.lzk_segment_topk(xp.data_ptr(), nr.data_ptr(), int(ld), _lib.ptr(bp), _lib.ptr(sp), Q.data_ptr(),
+    rc = L.lzk_segment_topk(xptr.data_ptr(), nrows.data_ptr(), int(ld), _lib.ptr(bptr), _lib.ptr(sptr), Q.data_ptr(),
                             Q.stride(0), nq, D, dt, float(alpha), _lib.ptr(qb), kslot, int(k), os_.data_ptr(),
                             oi.data_ptr(), _lib.stream_ptr(dev))
     _lib.check(rc, "lzk_segment_topk")
