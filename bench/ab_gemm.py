@@ -55,6 +55,15 @@ def main():
         for tile, v in ts.items():
             m = statistics.median(v)
             out[name][str(tile)] = {"us": round(m * 1e6, 1), "tflops": round(flop / m / 1e12, 1)}
+        # fp8 e4m3 (K % 128 == 0): GEMM alone and with the activation quantisation pass
+        xq, sx = E.quantize_fp8_rows(x)
+        wq, sw = E.quantize_fp8_rows(w)
+        y8 = E.linear_fp8(xq, sx, wq, sw, b, act=act, residual=r).float()
+        t8 = statistics.median(timeit(lambda: E.linear_fp8(xq, sx, wq, sw, b, act=act, residual=r)) for _ in range(5))
+        tq = statistics.median(timeit(lambda: E.quantize_fp8_rows(x)) for _ in range(5))
+        out[name]["fp8"] = {"us": round(t8 * 1e6, 1), "tflops": round(flop / t8 / 1e12, 1),
+                            "quant_us": round(tq * 1e6, 1),
+                            "rel_err_vs_bf16": round(float((y8 - ys[256]).norm() / ys[256].norm()), 4)}
     print(json.dumps(out, indent=1), flush=True)
 
 

@@ -108,6 +108,46 @@ __device__ __forceinline__ void quad_mma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4
             __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb][s], b[nb][s], acc[MQ * 4 + mb][NQ * 2 + nb], 0, 0, 0);
 }
 
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// MFMA policies: how one quadrant's fragments are consumed. The LDS image and
+// the 16-B reads are the same for both: lane group g = lane>>4 reads 16-B
+// chunks g and g+4 of each 128-B K-row. bf16 uses them as k-steps s = 0, 1 of
+// 16x16x32; fp8 concatenates them into the 32-byte operand of the block-scaled
+// 16x16x128 (unit E8M0 scales = plain fp8 GEMM at twice the bf16 rate). Any
+// byte->k assignment is valid as long as A and B use the same one; this one
+// keeps every ds_read_b128 lane group on 16 distinct bank slots.
+struct MmaBf16 {
+  static constexpr int KPER = 64;  // K elements per 128-B K-row
+  template <int MQ, int NQ>
+  __device__ __forceinline__ static void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+    quad_mma<MQ, NQ>(acc, a, b);
+  }
+};
+
+struct MmaFp8 {
+  static constexpr int KPER = 128;
+  __device__ __forceinline__ static i32x8 cat(const bf16x8& lo, const bf16x8& hi) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 l = __builtin_bit_cast(i32x4, lo), h = __builtin_bit_cast(i32x4, hi);
+    return i32x8{l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+  }
+  template <int MQ, int NQ>
+  __device__ __forceinline__ static void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+    i32x8 bb[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) bb[nb] = cat(b[nb][0], b[nb][1]);
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const i32x8 aa = cat(a[mb][0], a[mb][1]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        acc[MQ * 4 + mb][NQ * 2 + nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            aa, bb[nb], acc[MQ * 4 + mb][NQ * 2 + nb], 0, 0, 0, 127, 0, 127);
+    }
+  }
+};
+
 struct NoExtra {
   __device__ __forceinline__ void operator()() const {}
 };
@@ -130,6 +170,7 @@ __device__ __forceinline__ void prologue(u16* smem, const Stager& st, int KS, co
 //   C[wr*128 + i*16 + 4*(lane>>4) + e][wc*64 + j*16 + (lane&15)]
 // and every wave has passed the final barrier with all of its DMA retired
 // (smem may be reused or re-staged).
+template <class Mma = MmaBf16>
 __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -182,7 +223,7 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     bar();
     lgkm0();
     __builtin_amdgcn_s_setprio(1);
-    quad_mma<0, 0>(acc, a0, b);
+    Mma::template quad<0, 0>(acc, a0, b);
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p1 ----
@@ -194,7 +235,7 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     bar();
     lgkm0();
     __builtin_amdgcn_s_setprio(1);
-    quad_mma<1, 0>(acc, a1, b);
+    Mma::template quad<1, 0>(acc, a1, b);
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p2 ----
@@ -205,7 +246,7 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     bar();
     lgkm0();
     __builtin_amdgcn_s_setprio(1);
-    quad_mma<1, 1>(acc, a1, b);
+    Mma::template quad<1, 1>(acc, a1, b);
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p3 ----
@@ -217,16 +258,17 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     }
     bar();
     __builtin_amdgcn_s_setprio(1);
-    quad_mma<0, 1>(acc, a0, b);
+    Mma::template quad<0, 1>(acc, a0, b);
     __builtin_amdgcn_s_setprio(0);
     bar();
   }
   if (wr == 0) bar();
 }
 
+template <class Mma = MmaBf16>
 __device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
   prologue(smem, st, KS);
-  body(smem, st, KS, acc);
+  body<Mma>(smem, st, KS, acc);
 }
 
 // Persistent tile walk: the blocks resident on one XCD (blocks are dealt to

@@ -153,6 +153,101 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   }
 }
 
+// ---------------------------------------------------------------- fp8 path
+// SURVEY.md §2.4 K15 / BASELINE config 5: OCP e4m3 weights (per output
+// channel scale) x e4m3 activations (per token scale) on the block-scaled
+// 16x16x128 MFMA with unit block scales -- the same 256x256 pipeline and LDS
+// image as bf16 (a 128-B K-row holds 128 fp8 instead of 64 bf16), twice the
+// MFMA rate; dequantisation, bias, GELU and residual fused in the epilogue.
+template <int ACT, bool RES>
+__global__ __launch_bounds__(g256::NT, 1) void gemm256_f8_kernel(
+    const unsigned char* __restrict__ Xq, long ldx, int T, const float* __restrict__ sx,
+    const unsigned char* __restrict__ Wq, long ldw, int N, const float* __restrict__ sw,
+    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y, long ldy, int K,
+    int n_ft) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tt = logical / n_ft, ft = logical % n_ft;
+  const int n0 = ft * g256::BM, t0 = tt * g256::BN;
+  g256::Stager st;
+  st.setup(reinterpret_cast<const u16*>(Wq), ldw / 2, n0, N, reinterpret_cast<const u16*>(Xq), ldx / 2, t0, T);
+  f32x4 acc[8][4];
+  g256::mainloop<g256::MmaFp8>(smem, st, K / g256::MmaFp8::KPER, acc);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  float tsc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) tsc[j] = sx[min(t0 + wc * 64 + j * 16 + (lane & 15), T - 1)];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int nl = wr * 128 + i * 16 + 4 * (lane >> 4);
+    const int n = min(n0 + nl, N - 4);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + n);
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(sw + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tl = wc * 64 + j * 16 + (lane & 15);
+      u16x4 o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v = acc[i][j][u] * wv[u] * tsc[j] + bv[u];
+        if (ACT == 1) v = gelu_erf(v);
+        o[u] = f32_to_bf16(v);
+      }
+      *reinterpret_cast<u16x4*>(smem + tl * G256_OUT_LD + nl) = o;
+    }
+  }
+  __syncthreads();
+  const int nl = lane * 4;
+  const int n = n0 + nl;
+  if (n < N) {
+#pragma unroll 8
+    for (int rr = 0; rr < g256::BN / 8; ++rr) {
+      const int tl = wave * (g256::BN / 8) + rr;
+      const int t = t0 + tl;
+      if (t >= T) break;
+      u16x4 o = *reinterpret_cast<const u16x4*>(smem + tl * G256_OUT_LD + nl);
+      if (RES) {
+        const u16x4 rv = *reinterpret_cast<const u16x4*>(R + (long)t * ldr + n);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16(bf16_to_f32(o[u]) + bf16_to_f32(rv[u]));
+      }
+      *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
+    }
+  }
+}
+
+// bf16 rows -> e4m3 rows + per-row scale (amax / 448), one wave per row.
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const u16* __restrict__ X, long ldx, int rows, int D,
+                                                             unsigned char* __restrict__ Q, long ldq,
+                                                             float* __restrict__ scale) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const u16* x = X + (long)row * ldx;
+  float amax = 0.f;
+  for (int c = lane * 8; c < D; c += 512) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(x + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(bf16_to_f32(v[e])));
+  }
+  amax = wave_max(amax);
+  const float sc = amax > 0.f ? amax * (1.f / 448.f) : 1.f;
+  const float inv = 1.f / sc;
+  unsigned char* q = Q + (long)row * ldq;
+  for (int c = lane * 8; c < D; c += 512) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(x + c);
+    int lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(v[0]) * inv, bf16_to_f32(v[1]) * inv, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(v[2]) * inv, bf16_to_f32(v[3]) * inv, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(v[4]) * inv, bf16_to_f32(v[5]) * inv, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(v[6]) * inv, bf16_to_f32(v[7]) * inv, hi, true);
+    *reinterpret_cast<uint2*>(q + c) = make_uint2((unsigned)lo, (unsigned)hi);
+  }
+  if (lane == 0) scale[row] = sc;
+}
+
 // ---------------------------------------------------------------- attention
 // qkv: [B*S, 3*H] rows (q | k | v), head dim HD in {32, 64}. One wave per (b, head, qblock).
 template <int HD>
@@ -478,6 +573,40 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     else { if (r) GO(0, true, false); else GO(0, false, false); }
   }
 #undef GO
+  return (int)hipGetLastError();
+}
+
+// Y[T, N] = act((Xq * sx) (Wq * sw)^T + b) (+ R); Xq/Wq OCP e4m3 rows
+// (ldx/ldw in bytes, even), K % 128 == 0, N % 4 == 0.
+LZK_EXPORT int lzk_gemm_f8(const void* Xq, long ldx, int T, const float* sx, const void* Wq, long ldw, int N,
+                           const float* sw, const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
+                           int act, void* stream) {
+  if (K % 128 != 0 || N % 4 != 0 || T <= 0 || N <= 0 || (ldx & 1) || (ldw & 1)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
+  dim3 grid(n_ft * n_tt), block(g256::NT);
+  const unsigned char* x = (const unsigned char*)Xq;
+  const unsigned char* w = (const unsigned char*)Wq;
+  const u16* r = (const u16*)R;
+  u16* y = (u16*)Y;
+#define GO(A, RS)                                                                                                  \
+  do {                                                                                                             \
+    (void)hipFuncSetAttribute((const void*)gemm256_f8_kernel<A, RS>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                              G256_GEMM_LDS);                                                                      \
+    hipLaunchKernelGGL((gemm256_f8_kernel<A, RS>), grid, block, G256_GEMM_LDS, st, x, ldx, T, sx, w, ldw, N, sw,   \
+                       bias, r, ldr, y, ldy, K, n_ft);                                                             \
+  } while (0)
+  if (act == 1) { if (r) GO(1, true); else GO(1, false); }
+  else { if (r) GO(0, true); else GO(0, false); }
+#undef GO
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_quant_fp8_rows(const void* X, long ldx, int rows, int D, void* Q, long ldq, float* scale,
+                                  void* stream) {
+  if (D % 8 != 0 || rows <= 0) return rows == 0 ? 0 : (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const u16*)X,
+                     ldx, rows, D, (unsigned char*)Q, ldq, scale);
   return (int)hipGetLastError();
 }
 

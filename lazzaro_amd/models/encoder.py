@@ -73,13 +73,39 @@ class SentenceEncoder:
     ``pad_to`` columns, ready to be appended to an HBM arena)."""
 
     def __init__(self, config, device=None, weights: Optional[str] = None, seed: int = 0,
-                 dtype=torch.bfloat16):
+                 dtype=torch.bfloat16, precision: str = "bf16"):
+        """precision: "bf16" (all projections on bf16 MFMA) or "fp8" (SURVEY K15 /
+        BASELINE config 5: projection weights stored as OCP e4m3 with per-output-
+        channel scales, activations quantised per token right before each GEMM,
+        fp32 accumulate, bf16 activations everywhere else)."""
         self.cfg = get_config(config) if isinstance(config, str) else config
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.dtype = dtype
+        if precision not in ("bf16", "fp8"):
+            raise ValueError("precision must be 'bf16' or 'fp8'")
+        self.precision = precision
+        self.q: Dict[str, tuple] = {}
         self.p = self._random_init(seed)
         if weights:
             self.load_safetensors(weights)
+        self._quantize()
+
+    _PROJ = ("wqkv", "wo", "w1", "w2")
+
+    def _quantize(self) -> None:
+        self.q = {}
+        if self.precision != "fp8":
+            return
+        for i in range(self.cfg.layers):
+            for n in self._PROJ:
+                self.q[f"{i}.{n}"] = E.quantize_fp8_rows(self.p[f"{i}.{n}"].contiguous())
+
+    def _lin(self, x, i: int, w: str, b: str, act: str = "none", residual=None):
+        if self.precision == "fp8":
+            xq, sx = E.quantize_fp8_rows(x)
+            wq, sw = self.q[f"{i}.{w}"]
+            return E.linear_fp8(xq, sx, wq, sw, self.p[f"{i}.{b}"], act=act, residual=residual)
+        return E.linear(x, self.p[f"{i}.{w}"], self.p[f"{i}.{b}"], act=act, residual=residual)
 
     # --------------------------------------------------------------- weights
     def _random_init(self, seed: int) -> Dict[str, torch.Tensor]:
@@ -143,6 +169,8 @@ class SentenceEncoder:
             self.p[f"{i}.b2"] = get(pre + "output.dense.bias").float().to(dev)
             self.p[f"{i}.ln2_g"] = get(pre + "output.LayerNorm.weight").float().to(dev)
             self.p[f"{i}.ln2_b"] = get(pre + "output.LayerNorm.bias").float().to(dev)
+        if hasattr(self, "precision"):
+            self._quantize()
 
     def num_params(self) -> int:
         return sum(t.numel() for t in self.p.values())
@@ -158,13 +186,11 @@ class SentenceEncoder:
         lens = _to_dev(lens, self.device)
         x = E.embed_ln(ids.view(-1), S, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps)
         for i in range(c.layers):
-            qkv = E.linear(x, p[f"{i}.wqkv"], p[f"{i}.bqkv"])
+            qkv = self._lin(x, i, "wqkv", "bqkv")
             ctx = E.attention(qkv, lens, B, S, c.heads)
-            x = E.layernorm(E.linear(ctx, p[f"{i}.wo"], p[f"{i}.bo"], residual=x),
-                            p[f"{i}.ln1_g"], p[f"{i}.ln1_b"], c.eps)
-            hdn = E.linear(x, p[f"{i}.w1"], p[f"{i}.b1"], act="gelu")
-            x = E.layernorm(E.linear(hdn, p[f"{i}.w2"], p[f"{i}.b2"], residual=x),
-                            p[f"{i}.ln2_g"], p[f"{i}.ln2_b"], c.eps)
+            x = E.layernorm(self._lin(ctx, i, "wo", "bo", residual=x), p[f"{i}.ln1_g"], p[f"{i}.ln1_b"], c.eps)
+            hdn = self._lin(x, i, "w1", "b1", act="gelu")
+            x = E.layernorm(self._lin(hdn, i, "w2", "b2", residual=x), p[f"{i}.ln2_g"], p[f"{i}.ln2_b"], c.eps)
         return E.pool_norm(x, lens, B, S, c.pooling, pad_to)
 
     def flops(self, tokens: int) -> float:

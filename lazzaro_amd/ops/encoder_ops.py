@@ -17,6 +17,9 @@ from . import _lib
 
 _lib.register("lzk_gemm_bias_act", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P,
                                              _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
+_lib.register("lzk_gemm_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P,
+                                       _lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
+_lib.register("lzk_quant_fp8_rows", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.L, _lib.P, _lib.P])
 _lib.register("lzk_attention", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.F,
                                          _lib.P, _lib.L, _lib.P])
 _lib.register("lzk_layernorm", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.P, _lib.I, _lib.I,
@@ -46,6 +49,55 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, act: str = "none",
                                       y.data_ptr(), y.stride(0), K, 1 if act == "gelu" else 0,
                                       _lib.stream_ptr(x.device))
     _lib.check(rc, "lzk_gemm_bias_act")
+    return y
+
+
+FP8_MAX = 448.0  # OCP e4m3fn (gfx950 MFMA format, == torch.float8_e4m3fn)
+
+
+def quantize_fp8_rows(x: torch.Tensor):
+    """Row-wise symmetric e4m3 quantisation: (q uint8 [R, D], scale fp32 [R])
+    with x ~= float(q) * scale[:, None] (scale = amax / 448)."""
+    R, D = x.shape
+    if not x.is_cuda:
+        xf = x.float()
+        amax = xf.abs().amax(dim=1)
+        sc = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+        q = (xf / sc[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+        return q, sc
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1 and D % 8 == 0
+    q = torch.empty((R, D), dtype=torch.uint8, device=x.device)
+    sc = torch.empty((R,), dtype=torch.float32, device=x.device)
+    rc = _lib.lib().lzk_quant_fp8_rows(x.data_ptr(), x.stride(0), R, D, q.data_ptr(), q.stride(0), sc.data_ptr(),
+                                       _lib.stream_ptr(x.device))
+    _lib.check(rc, "lzk_quant_fp8_rows")
+    return q, sc
+
+
+def dequantize_fp8_rows(q: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.float8_e4m3fn).float() * sc[:, None].float()
+
+
+def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor, b: torch.Tensor,
+               act: str = "none", residual=None, out=None) -> torch.Tensor:
+    """act((xq*sx) @ (wq*sw).T + b) (+ residual) -> bf16. xq [T,K] / wq [N,K]
+    e4m3 bytes (uint8) with per-row scales; K % 128 == 0 on the GPU."""
+    T, K = xq.shape
+    N = wq.shape[0]
+    if not xq.is_cuda:
+        y = dequantize_fp8_rows(xq, sx) @ dequantize_fp8_rows(wq, sw).T + b.float()
+        if act == "gelu":
+            y = F.gelu(y)
+        if residual is not None:
+            y = y + residual.float()
+        return y.to(torch.bfloat16)
+    assert xq.dtype == torch.uint8 and wq.dtype == torch.uint8 and K % 128 == 0 and N % 4 == 0
+    y = out if out is not None else torch.empty((T, N), dtype=torch.bfloat16, device=xq.device)
+    rc = _lib.lib().lzk_gemm_f8(xq.data_ptr(), xq.stride(0), T, sx.data_ptr(), wq.data_ptr(), wq.stride(0), N,
+                                sw.data_ptr(), b.data_ptr(), _lib.ptr(residual),
+                                residual.stride(0) if residual is not None else 0, y.data_ptr(), y.stride(0), K,
+                                1 if act == "gelu" else 0, _lib.stream_ptr(xq.device))
+    _lib.check(rc, "lzk_gemm_f8")
     return y
 
 

@@ -187,3 +187,37 @@ def test_multi_arena_search_gpu():
             rs, rr = owners[j].search_rows(q[j:j + 1], 5, metric)
             assert torch.equal(r[j].cpu(), rr[0].cpu()), metric
             torch.testing.assert_close(s[j].cpu(), rs[0].cpu(), atol=1e-3, rtol=1e-4)
+
+
+def test_quantize_fp8_rows_gpu():
+    x = (torch.randn(1000, 1024, device=DEV) * torch.linspace(0.01, 30, 1000, device=DEV)[:, None]).to(torch.bfloat16)
+    q, s = E.quantize_fp8_rows(x)
+    qr, sr = E.quantize_fp8_rows(x.cpu())
+    torch.testing.assert_close(s.cpu(), sr, rtol=1e-6, atol=0)
+    assert (q.cpu() == qr).float().mean() > 0.999  # RNE in both; ulp ties may differ
+
+
+@pytest.mark.parametrize("T,N,K,act,res", [(8200, 3072, 768, "gelu", False), (300, 1024, 4096, "none", True),
+                                           (64, 256, 128, "none", False), (1000, 2304, 768, "none", True)])
+def test_linear_fp8_gpu(T, N, K, act, res):
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(T, N, device=DEV).to(torch.bfloat16) if res else None
+    xq, sx = E.quantize_fp8_rows(x)
+    wq, sw = E.quantize_fp8_rows(w)
+    y = E.linear_fp8(xq, sx, wq, sw, b, act=act, residual=r)
+    yr = E.linear_fp8(xq.cpu(), sx.cpu(), wq.cpu(), sw.cpu(), b.cpu(), act=act,
+                      residual=None if r is None else r.cpu())
+    assert _rel(y.cpu(), yr) < 1e-2
+
+
+def test_fp8_encoder_gpu_matches_cpu():
+    from lazzaro_amd.models.encoder import SentenceEncoder
+    ids = torch.randint(1000, 4000, (6, 40), dtype=torch.int32)
+    lens = torch.tensor([40, 33, 17, 5, 40, 1], dtype=torch.int32)
+    g = SentenceEncoder("tiny", device=DEV, seed=5, precision="fp8")
+    c = SentenceEncoder("tiny", device="cpu", seed=5, precision="fp8")
+    eg, _ = g.forward(ids, lens)
+    ec, _ = c.forward(ids, lens)
+    assert ((eg.cpu() * ec).sum(1) > 0.999).all()
