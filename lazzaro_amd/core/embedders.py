@@ -15,7 +15,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from ..models.encoder import SentenceEncoder, get_config
+from ..models.encoder import GraphedEncoder, SentenceEncoder, get_config
 from ..utils.device import default_device
 
 
@@ -40,17 +40,33 @@ class Tokenizer:
 
 class OnDeviceEmbedder:
     def __init__(self, model: str = "bge-base", device=None, weights: Optional[str] = None,
-                 vocab_file: Optional[str] = None, max_len: int = 512, max_batch: int = 1024, seed: int = 0):
+                 vocab_file: Optional[str] = None, max_len: int = 512, max_batch: int = 1024, seed: int = 0,
+                 precision: str = "bf16", graphs: bool = True):
         self.cfg = get_config(model)
         self.device = torch.device(device) if device is not None else default_device()
-        self.encoder = SentenceEncoder(self.cfg, device=self.device, weights=weights, seed=seed)
+        self.encoder = SentenceEncoder(self.cfg, device=self.device, weights=weights, seed=seed, precision=precision)
+        # small batches replay a captured hipGraph per (batch, seq) bucket
+        self.graphs = graphs and self.device.type == "cuda"
+        self._graphs = {}
         self.tok = Tokenizer(vocab_file, vocab_size=self.cfg.vocab)
         self.max_len = min(max_len, self.cfg.max_pos)
         self.max_batch = max_batch
         self.dim = self.cfg.hidden
 
+    GRAPH_MAX_BATCH = 8
+
     def embed_tensor(self, texts: List[str], pad_to: int = 0):
         ids, lens = self.tok.encode_batch(texts, self.max_len)
+        B, S = ids.shape
+        if self.graphs and B <= self.GRAPH_MAX_BATCH:
+            bb = 1 << max(0, (B - 1).bit_length())
+            sb = min(self.max_len, max(16, 1 << max(0, (S - 1).bit_length())))
+            if S <= sb:
+                key = (bb, sb, pad_to)
+                g = self._graphs.get(key)
+                if g is None:
+                    g = self._graphs[key] = GraphedEncoder(self.encoder, bb, sb, pad_to)
+                return g(ids, lens)
         return self.encoder.forward(ids, lens, pad_to=pad_to)
 
     def embed(self, text: str) -> List[float]:

@@ -197,3 +197,45 @@ class SentenceEncoder:
         c = self.cfg
         per_tok = 2 * (3 * c.hidden * c.hidden + c.hidden * c.hidden + 2 * c.hidden * c.ffn) * c.layers
         return float(per_tok) * tokens
+
+
+class GraphedEncoder:
+    """hipGraph-captured forward for one (batch, seq_len, pad_to) shape.
+
+    Small batches (the per-turn query embed of ``chat`` / ``search_memories``)
+    are launch-bound: ~7 kernels per layer, ~90 for bge-base, each a few
+    microseconds of GPU work. Capturing the whole forward once and replaying it
+    turns that into one graph launch. Inputs are copied into static device
+    buffers (padding rows get length 1 and are sliced away); outputs are
+    returned as copies so a later replay cannot overwrite them.
+    """
+
+    def __init__(self, enc: "SentenceEncoder", batch: int, seq: int, pad_to: int = 0):
+        if enc.device.type != "cuda":
+            raise ValueError("GraphedEncoder needs a GPU encoder")
+        dev = enc.device
+        self.enc, self.batch, self.seq, self.pad_to = enc, batch, seq, pad_to
+        self.ids = torch.zeros((batch, seq), dtype=torch.int32, device=dev)
+        self.lens = torch.ones((batch,), dtype=torch.int32, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # first-launch work (attribute setup, workspaces) stays out of the graph
+                enc.forward(self.ids, self.lens, pad_to=pad_to)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out32, self.out16 = enc.forward(self.ids, self.lens, pad_to=pad_to)
+
+    def __call__(self, ids: torch.Tensor, lens: torch.Tensor):
+        B, S = ids.shape
+        if B > self.batch or S > self.seq:
+            raise ValueError("input larger than the captured shape")
+        dev = self.ids.device
+        self.ids.zero_()
+        self.lens.fill_(1)
+        self.ids[:B, :S].copy_(ids.to(torch.int32).to(dev, non_blocking=True))
+        self.lens[:B].copy_(lens.to(torch.int32).to(dev, non_blocking=True))
+        self.graph.replay()
+        o16 = self.out16[:B].clone() if self.out16 is not None else None
+        return self.out32[:B].clone(), o16

@@ -221,3 +221,16 @@ def test_fp8_encoder_gpu_matches_cpu():
     eg, _ = g.forward(ids, lens)
     ec, _ = c.forward(ids, lens)
     assert ((eg.cpu() * ec).sum(1) > 0.999).all()
+
+
+def test_graphed_encoder_matches_eager():
+    from lazzaro_amd.core.embedders import OnDeviceEmbedder
+    emb = OnDeviceEmbedder("minilm-l6", device=DEV, max_len=64)
+    texts = ["I like green tea", "my sister moved to Osaka last year and teaches math", "rust"]
+    ids, lens = emb.tok.encode_batch(texts, emb.max_len)
+    eager, _ = emb.encoder.forward(ids, lens)
+    g1, _ = emb.embed_tensor(texts)          # captured (bucket 4 x 16)
+    g2, _ = emb.embed_tensor(texts[:1])      # another bucket
+    assert len(emb._graphs) == 2
+    torch.testing.assert_close(g1, eager, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(g2, eager[:1], atol=1e-5, rtol=1e-5)
