@@ -153,6 +153,72 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   }
 }
 
+// ---------------------------------------------------------------- skinny GEMM
+// T <= 64 tokens (the per-turn query embed of chat/search_memories): the
+// projection is a weight-streaming GEMV, not an MFMA-bound GEMM. One block per
+// 16 output features; its 4 waves split K in quarters, each wave keeps the
+// 16 x T tile in registers (v_mfma_f32_16x16x32_bf16, A = W rows and B = token
+// rows straight from global memory -- weights are read exactly once, tokens
+// are L2-resident), partial sums are reduced through LDS and wave 0 applies
+// bias / GELU / residual. Grid = N/16 blocks instead of the 256-wide tiles'
+// handful, so a 12-layer forward at batch 1 is bounded by weight bytes.
+template <int ACT, bool RES, int NT16>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const u16* __restrict__ X, long ldx, int T,
+                                                          const u16* __restrict__ W, long ldw, int N,
+                                                          const float* __restrict__ bias, const u16* __restrict__ R,
+                                                          long ldr, u16* __restrict__ Y, long ldy, int K) {
+  __shared__ f32x4 part[3][NT16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int f0 = blockIdx.x * 16;
+  const int kq = K / 4, kb = wave * kq;
+  const int fr = min(f0 + (lane & 15), N - 1);
+  const u16* wrow = W + (long)fr * ldw + kb + 8 * (lane >> 4);
+  const u16* xrow[NT16];
+#pragma unroll
+  for (int j = 0; j < NT16; ++j) xrow[j] = X + (long)min(16 * j + (lane & 15), T - 1) * ldx + kb + 8 * (lane >> 4);
+  f32x4 acc[NT16];
+#pragma unroll
+  for (int j = 0; j < NT16; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k = 0; k < kq; k += 32) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(wrow + k);
+#pragma unroll
+    for (int j = 0; j < NT16; ++j) {
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(xrow[j] + k);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+    }
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int j = 0; j < NT16; ++j) part[wave - 1][j][lane] = acc[j];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const int n = f0 + 4 * (lane >> 4);
+  if (n >= N) return;
+  const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + n);
+#pragma unroll
+  for (int j = 0; j < NT16; ++j) {
+    const int t = 16 * j + (lane & 15);
+    f32x4 v = acc[j] + part[0][j][lane] + part[1][j][lane] + part[2][j][lane];
+    if (t >= T) continue;
+    u16x4 o;
+    float r[4] = {0.f, 0.f, 0.f, 0.f};
+    if (RES) {
+      const u16x4 rv = *reinterpret_cast<const u16x4*>(R + (long)t * ldr + n);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) r[u] = bf16_to_f32(rv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float y = v[u] + bv[u];
+      if (ACT == 1) y = gelu_erf(y);
+      o[u] = f32_to_bf16(y + r[u]);
+    }
+    *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
+  }
+}
+
 // ---------------------------------------------------------------- fp8 path
 // SURVEY.md §2.4 K15 / BASELINE config 5: OCP e4m3 weights (per output
 // channel scale) x e4m3 activations (per token scale) on the block-scaled
@@ -530,6 +596,22 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   }
   if (K % TK != 0 || N % 4 != 0 || T <= 0 || N <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (T <= 64 && K % 128 == 0 && g_gemm_tile != 128) {
+    const u16* x = (const u16*)X;
+    const u16* w = (const u16*)W;
+    const u16* r = (const u16*)R;
+    u16* y = (u16*)Y;
+    dim3 grid((N + 15) / 16), block(256);
+#define SK(A, RS, NT) hipLaunchKernelGGL((gemm_skinny_kernel<A, RS, NT>), grid, block, 0, st, x, ldx, T, w, ldw, N, bias, r, ldr, y, ldy, K)
+#define SKT(NT) do { if (act == 1) { if (r) SK(1, true, NT); else SK(1, false, NT); } \
+                     else { if (r) SK(0, true, NT); else SK(0, false, NT); } } while (0)
+    if (T <= 16) SKT(1);
+    else if (T <= 32) SKT(2);
+    else SKT(4);
+#undef SKT
+#undef SK
+    return (int)hipGetLastError();
+  }
   if (g_gemm_tile < 0) {
     const char* e = getenv("LZK_GEMM_TILE");
     g_gemm_tile = (e && atoi(e) == 128) ? 128 : 256;

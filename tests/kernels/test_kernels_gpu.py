@@ -87,7 +87,10 @@ def _rel(a, b):
                                            (1000, 384, 384, "gelu", True),
                                            # grids of >= 256 tiles of 256x256 take the 8-wave pipeline
                                            (8200, 2304, 768, "none", False), (4100, 3072, 768, "gelu", False),
-                                           (16385, 1024, 3072, "none", True), (21000, 1024, 768, "gelu", True)])
+                                           (16385, 1024, 3072, "none", True), (21000, 1024, 768, "gelu", True),
+                                           # T <= 64: skinny weight-streaming kernel
+                                           (1, 768, 768, "gelu", True), (17, 3072, 768, "none", False),
+                                           (40, 768, 3072, "none", True), (64, 1000, 384, "gelu", False)])
 def test_linear(T, N, K, act, res):
     x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
