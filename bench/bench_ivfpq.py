@@ -42,10 +42,13 @@ def main():
     ap.add_argument("--train", type=int, default=262144)
     ap.add_argument("--model", default="e5-large")
     ap.add_argument("--nprobes", default="16,32,64")
-    ap.add_argument("--rerank", type=int, default=256, help="re-rank depth over kept bf16 rows (0 = PQ only)")
+    ap.add_argument("--rerank", type=int, default=256, help="re-rank depth over the kept copy (0 = PQ only)")
+    ap.add_argument("--rerank-dtype", default="fp8", choices=["fp8", "bf16"],
+                    help="re-rank copy: fp8 e4m3 + row scale (D+4 B/vector) or bf16 (2D B/vector)")
+    ap.add_argument("--precision", default="fp8", choices=["fp8", "bf16"], help="query encoder projections")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    idx = IVFPQIndex(a.dim, nlist=a.nlist, m=a.m, device=dev, keep_vectors=a.rerank > 0)
+    idx = IVFPQIndex(a.dim, nlist=a.nlist, m=a.m, device=dev, keep_vectors=a.rerank_dtype if a.rerank > 0 else False)
     flat = torch.empty((a.n, a.dim), dtype=torch.bfloat16, device=dev)
     t0 = time.time()
     r0 = 0
@@ -64,7 +67,7 @@ def main():
     # queries: embed synthetic texts with e5-large (cost measured), search with
     # perturbed corpus rows so recall is meaningful
     from lazzaro_amd.core.embedders import OnDeviceEmbedder
-    emb = OnDeviceEmbedder(a.model, device=dev, max_len=64)
+    emb = OnDeviceEmbedder(a.model, device=dev, max_len=64, precision=a.precision)
     rng = random.Random(0)
     texts = [" ".join(rng.choice("memory user likes python graph kernel music travel".split()) for _ in range(16))
              for _ in range(a.nq)]
@@ -94,11 +97,13 @@ def main():
             res.append({"nprobe": nprobe, "rerank": rr, "ms": round(dt * 1e3, 3), "qps_search": round(a.nq / dt, 1),
                         "qps_end_to_end": round(a.nq / (dt + t_embed), 1),
                         "recall_at_10": round(recall_at_k(ids, truth), 4)})
-    per_vec = a.m + 8
+    per_vec = idx.memory_bytes() / a.n
     out = {"metric": "IVF-PQ search QPS @ recall@10", "n": a.n, "dim": a.dim, "nlist": a.nlist, "m": a.m,
-           "bytes_per_vector": per_vec, "projected_vectors_in_288GB": int(288e9 / per_vec),
+           "encoder": f"{a.model} {a.precision}", "rerank_copy": a.rerank_dtype if a.rerank else None,
+           "bytes_per_vector": round(per_vec, 1), "projected_vectors_in_288GB": int(270e9 / per_vec),
+           "codes_only_bytes_per_vector": a.m + 8, "projected_codes_only_in_288GB": int(270e9 / (a.m + 8)),
            "train_s": round(t_train, 1), "add_s": round(t_add, 1), "add_vectors_per_s": round(a.n / t_add),
-           "embed_ms_%s_batch%d" % (a.model, a.nq): round(t_embed * 1e3, 2), "results": res}
+           "embed_ms_%s_%s_batch%d" % (a.model, a.precision, a.nq): round(t_embed * 1e3, 2), "results": res}
     print(json.dumps(out), flush=True)
 
 

@@ -48,7 +48,11 @@ def _unit(x):
 
 
 class IVFPQIndex:
-    def __init__(self, dim: int, nlist: int = 1024, m: int = 64, device=None, keep_vectors: bool = False):
+    def __init__(self, dim: int, nlist: int = 1024, m: int = 64, device=None, keep_vectors=False):
+        """keep_vectors: False (codes only, 8+m bytes/vector), True / "bf16"
+        (exact re-rank copy, 2*Dp bytes/vector) or "fp8" (OCP e4m3 re-rank copy
+        with a per-row scale, D+4 bytes/vector -- the layout that fills 288 GB
+        with ~250M 1024-d vectors and still re-ranks PQ candidates)."""
         assert dim % m == 0, "dim must be divisible by m"
         self.dim, self.nlist, self.m, self.dsub = dim, nlist, m, dim // m
         self.device = torch.device(device) if device is not None else torch.device("cpu")
@@ -60,8 +64,11 @@ class IVFPQIndex:
         self.ids = torch.zeros(0, dtype=torch.int64, device=self.device)
         self.list_of = torch.zeros(0, dtype=torch.int32, device=self.device)
         self.list_off = torch.zeros(nlist + 1, dtype=torch.int64, device=self.device)
-        self.keep_vectors = keep_vectors
+        self.keep_vectors = "bf16" if keep_vectors is True else (keep_vectors or False)
+        if self.keep_vectors not in (False, "bf16", "fp8"):
+            raise ValueError("keep_vectors must be False, True/'bf16' or 'fp8'")
         self.vectors = None
+        self.vscale = None
         self._dirty = False
 
     # ------------------------------------------------------------------ train
@@ -131,9 +138,21 @@ class IVFPQIndex:
         self.codes = torch.cat([self.codes, torch.cat(codes)])
         self.ids = torch.cat([self.ids, ids.to(self.device)])
         self.list_of = torch.cat([self.list_of, lab])
-        if self.keep_vectors:
+        if self.keep_vectors == "bf16":
             v = self._pad(_unit(x.to(self.device).float()))
             self.vectors = v if self.vectors is None else torch.cat([self.vectors, v])
+        elif self.keep_vectors == "fp8":
+            from ..ops.encoder_ops import quantize_fp8_rows
+            qs, ss = [], []
+            for r0 in range(0, n, batch):
+                v = _unit(x[r0:r0 + batch].to(self.device).float())
+                v = v.to(torch.bfloat16) if self.device.type == "cuda" else v
+                q8, sc = quantize_fp8_rows(v.contiguous())
+                qs.append(q8)
+                ss.append(sc)
+            q8, sc = torch.cat(qs), torch.cat(ss)
+            self.vectors = q8 if self.vectors is None else torch.cat([self.vectors, q8])
+            self.vscale = sc if self.vscale is None else torch.cat([self.vscale, sc])
         self._dirty = True
 
     def _finalize(self) -> None:
@@ -146,6 +165,8 @@ class IVFPQIndex:
         self.list_of = self.list_of[o]
         if self.vectors is not None:
             self.vectors = self.vectors[o]
+        if self.vscale is not None:
+            self.vscale = self.vscale[o]
         cnt = torch.bincount(self.list_of.long(), minlength=self.nlist)
         self.list_off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
         self.list_off[1:] = torch.cumsum(cnt, 0)
@@ -156,7 +177,8 @@ class IVFPQIndex:
 
     def memory_bytes(self) -> int:
         b = self.codes.numel() + self.ids.numel() * 8
-        return b + (self.vectors.numel() * self.vectors.element_size() if self.vectors is not None else 0)
+        b += self.vectors.numel() * self.vectors.element_size() if self.vectors is not None else 0
+        return b + (self.vscale.numel() * 4 if self.vscale is not None else 0)
 
     # ------------------------------------------------------------------ search
     def search(self, q: torch.Tensor, k: int = 10, nprobe: int = 16, rerank: int = 0):
@@ -177,7 +199,11 @@ class IVFPQIndex:
             s, rows = self._scan_dense(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
         if rerank and self.vectors is not None:
             valid = rows >= 0
-            v = self.vectors[rows.clamp_min(0)].float()[..., : self.dim]
+            rr = rows.clamp_min(0)
+            if self.vscale is not None:  # fp8 copy: dequantise the gathered candidates only
+                v = self.vectors[rr].view(torch.float8_e4m3fn).float() * self.vscale[rr][..., None]
+            else:
+                v = self.vectors[rr].float()[..., : self.dim]
             s = torch.einsum("qd,qkd->qk", qf, v)
             s = torch.where(valid, s, torch.full_like(s, float("-inf")))
             s, o = torch.sort(s, dim=1, descending=True, stable=True)

@@ -40,3 +40,17 @@ def test_ivfpq_add_incremental_ids():
     s, ids = idx.search(x[600:601], 1, nprobe=8)
     assert int(ids[0, 0]) >= 10_000 or int(ids[0, 0]) < 500
     assert sorted(idx.ids.tolist())[-1] == 10_499
+
+
+def test_ivfpq_fp8_rerank_copy():
+    d = 64
+    x = _data(4000, d, 5)
+    q = _data(20, d, 6)
+    idx = IVFPQIndex(d, nlist=16, m=16, device="cpu", keep_vectors="fp8")
+    idx.train(x, iters=6, pq_iters=6)
+    idx.add(x)
+    assert idx.vectors.dtype == torch.uint8 and idx.vscale.shape == (4000,)
+    assert idx.memory_bytes() == 4000 * (16 + 8 + d + 4)
+    truth = torch.topk(q @ x.T, 10, dim=1).indices
+    _, ids = idx.search(q, 10, nprobe=16, rerank=32)
+    assert recall_at_k(ids, truth) > 0.8
