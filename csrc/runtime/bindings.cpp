@@ -187,7 +187,21 @@ PYBIND11_MODULE(_lzrt, m) {
              py::array_t<int32_t> l(lens.size(), lens.data());
              return py::make_tuple(a, l);
            },
-           py::arg("texts"), py::arg("max_len") = 512);
+           py::arg("texts"), py::arg("max_len") = 512)
+      .def("encode_chunks",
+           [](Tokenizer& t, const std::vector<std::string>& texts, int max_len, int overlap) {
+             std::vector<int32_t> ids, lens, owner;
+             int S = 0;
+             {
+               py::gil_scoped_release r;
+               S = t.encode_chunks(texts, max_len, overlap, ids, lens, owner);
+             }
+             py::array_t<int32_t> a({(py::ssize_t)lens.size(), (py::ssize_t)S});
+             if (!ids.empty()) std::memcpy(a.mutable_data(), ids.data(), ids.size() * 4);
+             return py::make_tuple(a, py::array_t<int32_t>(lens.size(), lens.data()),
+                                   py::array_t<int32_t>(owner.size(), owner.data()));
+           },
+           py::arg("texts"), py::arg("max_len") = 512, py::arg("overlap") = 64);
 
   // ---- graph host utilities ----
   m.def("build_csr",

@@ -103,4 +103,48 @@ int Tokenizer::encode_batch(const std::vector<std::string>& texts, int max_len, 
   return S;
 }
 
+// Long inputs (SURVEY.md §5 "Long-context": encoder inputs are chunked at the
+// model's max length with overlap and the chunk embeddings averaged): every
+// text becomes ceil((n - overlap) / (body - overlap)) windows of at most
+// `body = max_len - 2` word pieces, each wrapped in [CLS] ... [SEP];
+// owner[w] is the text a window belongs to. Short texts give one window.
+int Tokenizer::encode_chunks(const std::vector<std::string>& texts, int max_len, int overlap,
+                             std::vector<int32_t>& ids, std::vector<int32_t>& lens,
+                             std::vector<int32_t>& owner) const {
+  const int body = std::max(1, max_len - 2);
+  overlap = std::max(0, std::min(overlap, body - 1));
+  const int stride = body - overlap;
+  std::vector<std::vector<int32_t>> wins;
+  owner.clear();
+  for (size_t t = 0; t < texts.size(); ++t) {
+    std::vector<std::string> words;
+    basic_split(texts[t], words);
+    std::vector<int32_t> pieces;
+    for (auto& w : words) wordpiece(w, pieces);
+    size_t start = 0;
+    do {
+      const size_t end = std::min(pieces.size(), start + (size_t)body);
+      std::vector<int32_t> w;
+      w.reserve(end - start + 2);
+      w.push_back(kCls);
+      w.insert(w.end(), pieces.begin() + start, pieces.begin() + end);
+      w.push_back(kSep);
+      wins.push_back(std::move(w));
+      owner.push_back((int32_t)t);
+      if (end >= pieces.size()) break;
+      start += stride;
+    } while (true);
+  }
+  int S = 1;
+  for (auto& w : wins) S = std::max<int>(S, (int)w.size());
+  S = std::min(max_len, (S + 7) / 8 * 8);
+  ids.assign(wins.size() * (size_t)S, kPad);
+  lens.resize(wins.size());
+  for (size_t i = 0; i < wins.size(); ++i) {
+    lens[i] = (int32_t)wins[i].size();
+    std::copy(wins[i].begin(), wins[i].end(), ids.begin() + i * S);
+  }
+  return S;
+}
+
 }  // namespace lzrt

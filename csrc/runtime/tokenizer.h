@@ -4,6 +4,7 @@
 // word maps to a deterministic hashed id in [1000, vocab_size). Output follows
 // the BERT convention [CLS] ... [SEP] with [PAD]=0, [UNK]=100, [CLS]=101, [SEP]=102.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <unordered_map>
@@ -20,6 +21,9 @@ class Tokenizer {
   // pads to the longest sequence (rounded up to a multiple of 8); returns S
   int encode_batch(const std::vector<std::string>& texts, int max_len, std::vector<int32_t>& ids,
                    std::vector<int32_t>& lens) const;
+  // overlapping max_len windows for texts longer than the model (owner = text index)
+  int encode_chunks(const std::vector<std::string>& texts, int max_len, int overlap, std::vector<int32_t>& ids,
+                    std::vector<int32_t>& lens, std::vector<int32_t>& owner) const;
 
  private:
   int vocab_size_;

@@ -37,6 +37,12 @@ class Tokenizer:
         ids, lens = self._t.encode_batch(list(texts), max_len)
         return torch.from_numpy(np.asarray(ids)), torch.from_numpy(np.asarray(lens))
 
+    def encode_chunks(self, texts: List[str], max_len: int = 512, overlap: int = 64):
+        """Overlapping windows for texts longer than ``max_len`` (owner[i] = text)."""
+        ids, lens, owner = self._t.encode_chunks(list(texts), max_len, overlap)
+        return (torch.from_numpy(np.asarray(ids)), torch.from_numpy(np.asarray(lens)),
+                torch.from_numpy(np.asarray(owner)))
+
 
 class OnDeviceEmbedder:
     def __init__(self, model: str = "bge-base", device=None, weights: Optional[str] = None,
@@ -72,9 +78,35 @@ class OnDeviceEmbedder:
     def embed(self, text: str) -> List[float]:
         return self.batch_embed([text])[0]
 
+    def embed_long(self, texts: List[str], overlap: int = 64) -> torch.Tensor:
+        """Texts of any length: windows of the model's max length with
+        ``overlap`` tokens of overlap, window embeddings averaged per text and
+        re-normalised (long-context row). Returns [n, H] fp32."""
+        ids, lens, owner = self.tok.encode_chunks(texts, self.max_len, overlap)
+        outs = []
+        for s in range(0, ids.shape[0], self.max_batch):
+            v, _ = self.encoder.forward(ids[s: s + self.max_batch], lens[s: s + self.max_batch])
+            outs.append(v)
+        v = torch.cat(outs)
+        own = owner.to(v.device).long()
+        acc = torch.zeros((len(texts), v.shape[1]), dtype=v.dtype, device=v.device).index_add_(0, own, v)
+        return acc / acc.norm(dim=1, keepdim=True).clamp_min(1e-30)
+
     def batch_embed(self, texts: List[str]) -> List[List[float]]:
         if not texts:
             return []
+        if any(len(t) > 4 * self.max_len for t in texts):
+            # possibly longer than the model: chunk + average (cheap char-length screen first)
+            long_ids = [i for i, t in enumerate(texts) if len(self.tok.encode(t, 1 << 30)) > self.max_len]
+            if long_ids:
+                out = [None] * len(texts)
+                lv = self.embed_long([texts[i] for i in long_ids]).cpu().tolist()
+                for i, r in zip(long_ids, lv):
+                    out[i] = r
+                rest = [i for i in range(len(texts)) if out[i] is None]
+                for i, r in zip(rest, self.batch_embed([texts[i] for i in rest]) if rest else []):
+                    out[i] = r
+                return out
         order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
         out: List[Optional[List[float]]] = [None] * len(texts)
         for s in range(0, len(order), self.max_batch):

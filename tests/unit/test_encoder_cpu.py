@@ -49,3 +49,20 @@ def test_on_device_embedder_cpu():
     assert len(out) == 3 and len(out[0]) == 128
     assert abs(sum(x * x for x in out[1]) - 1.0) < 1e-3
     assert e.embed("second") == out[1] or max(abs(a - b) for a, b in zip(e.embed("second"), out[1])) < 1e-4
+
+
+def test_long_text_chunking_windows_and_mean():
+    from lazzaro_amd.core.embedders import OnDeviceEmbedder
+    emb = OnDeviceEmbedder("tiny", device="cpu", max_len=32)
+    long = " ".join(f"word{i}" for i in range(100))  # 100 pieces > 30 per window
+    ids, lens, owner = emb.tok.encode_chunks(["short text", long], 32, 8)
+    # body 30, stride 22: windows start at 0, 22, 44, 66 (ends at 96, 100)
+    assert owner.tolist() == [0, 1, 1, 1, 1, 1] and int(lens.max()) == 32
+    assert ids[1, 0] == 101 and ids[1, 31] == 102
+    v = emb.embed_long(["short text", long], overlap=8)
+    assert torch.allclose(v.norm(dim=1), torch.ones(2), atol=1e-5)
+    short_direct = torch.tensor(emb.embed("short text"))
+    assert torch.allclose(v[0], short_direct, atol=1e-5)
+    # batch_embed routes long texts through the chunked path
+    out = emb.batch_embed(["short text", long * 3])
+    assert len(out) == 2 and abs(sum(x * x for x in out[1]) - 1.0) < 1e-4
