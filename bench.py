@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--max-len", type=int, default=64)
     ap.add_argument("--recall-queries", type=int, default=256)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--consolidate-steps", type=int, default=5,
+                    help="second half of the metric: timed consolidation steps on a --rows-node buffer (0 = skip)")
+    ap.add_argument("--consolidate-convs", type=int, default=128, help="conversations per GPU per step")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,6 +169,20 @@ def main():
     tflops_search = 2.0 * a.rows * a.dim * q16.shape[0] / t_search / 1e12
 
     qps = world * a.batch * a.steps / el
+
+    # ---- second half of the metric: consolidate turns/sec (BASELINE config 4
+    # shape: a --rows-node episodic buffer per GPU, batches of conversations
+    # consolidated on device, all-to-all routing + cross-shard dedupe/links) ----
+    consolidate = None
+    if a.consolidate_steps > 0:
+        del X
+        torch.cuda.empty_cache()
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        from bench_consolidate import run as run_consolidate
+        from lazzaro_amd.parallel import Communicator
+        comm = Communicator() if world > 1 else Communicator.local(dev)
+        consolidate = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
+                                      dim=a.dim)
     res = {
         "metric": METRIC,
         "value": round(qps, 2),
@@ -185,6 +202,10 @@ def main():
         "breakdown_ms": {"embed": round(t_embed * 1e3, 3), "search": round(t_search * 1e3, 3)},
         "tflops": {"embed": round(tflops_embed, 1), "search": round(tflops_search, 1)},
     }
+    if consolidate is not None:
+        res["consolidate_turns_per_s"] = consolidate["turns_per_s"]
+        res["consolidate"] = {k: consolidate[k] for k in ("ms_per_step", "nodes_per_rank", "convs_per_rank_step",
+                                                          "facts_per_conv", "per_step_rank0")}
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

@@ -129,6 +129,28 @@ PYBIND11_MODULE(_lzrt, m) {
              return py::make_tuple(n, v);
            },
            py::arg("eq"), py::arg("in_col") = "", py::arg("in_vals") = py::none())
+      .def("stage",
+           [](Table& t, py::dict cols) {
+             std::vector<Column> cs;
+             uint32_t dim = 0;
+             for (auto& spec : t.schema()) {
+               if (!cols.contains(spec.name.c_str())) throw std::runtime_error("missing column " + spec.name);
+               cs.push_back(to_column(spec, cols[spec.name.c_str()]));
+               if (spec.type == ColType::VecF32) dim = cs.back().dim;
+             }
+             std::pair<std::string, uint64_t> r;
+             {
+               py::gil_scoped_release g;
+               r = t.stage(cs);
+             }
+             return py::make_tuple(r.first, r.second, dim);
+           })
+      .def("commit_staged",
+           [](Table& t, const std::vector<std::pair<std::string, uint64_t>>& frags, uint32_t dim) {
+             py::gil_scoped_release g;
+             return t.commit_staged(frags, dim);
+           },
+           py::arg("frags"), py::arg("vec_dim") = 0)
       .def("replace_where",
            [](Table& t, const std::vector<std::pair<std::string, std::string>>& eq, const std::string& in_col,
               py::object in_vals, py::dict cols) {

@@ -534,4 +534,48 @@ uint64_t Table::compact() {
   return m.version;
 }
 
+// Two-phase multi-writer commit: every rank writes its
+// rows as an immutable fragment WITHOUT touching the manifest (stage), the
+// fragments are gathered, and one process publishes them all in a single new
+// version (commit_staged). Readers never observe a partial multi-rank update;
+// a staged fragment that is never committed is unreachable garbage.
+std::pair<std::string, uint64_t> Table::stage(const std::vector<Column>& cols_in) {
+  if (cols_in.size() != schema_.size()) throw std::runtime_error("colstore: column count mismatch");
+  const size_t n = cols_in.empty() ? 0 : cols_in[0].size();
+  for (auto& c : cols_in) if (c.size() != n) throw std::runtime_error("colstore: ragged columns");
+  if (n == 0) return {"", 0};
+  std::string file = uniq_name() + ".lzc";
+  write_fragment(file, cols_in);
+  return {file, n};
+}
+
+uint64_t Table::commit_staged(const std::vector<std::pair<std::string, uint64_t>>& frags, uint32_t vec_dim) {
+  lock();
+  Manifest m;
+  try {
+    m = load_latest();
+    for (auto& sc : schema_)
+      if (sc.type == ColType::VecF32) {
+        for (auto& pc : m.schema) if (pc.name == sc.name && pc.dim) sc.dim = pc.dim;
+        if (sc.dim == 0) sc.dim = vec_dim;
+        if (vec_dim && sc.dim != vec_dim) throw std::runtime_error("colstore: vector dim mismatch");
+      }
+    bool any = false;
+    for (auto& f : frags) {
+      if (f.first.empty() || f.second == 0) continue;
+      Fragment fr;
+      fr.file = f.first;
+      fr.rows = f.second;
+      m.frags.push_back(fr);
+      any = true;
+    }
+    if (any) {
+      m.version += 1;
+      write_manifest(m);
+    }
+  } catch (...) { unlock(); throw; }
+  unlock();
+  return m.version;
+}
+
 }  // namespace lzrt

@@ -15,6 +15,7 @@
 #include <memory>
 #include <string>
 #include <unordered_set>
+#include <utility>
 #include <vector>
 
 namespace lzrt {
@@ -67,6 +68,10 @@ class Table {
   uint64_t replace_where(const Predicate& p, const std::vector<Column>& cols, uint64_t* n_deleted);
   std::vector<Column> scan(const Predicate& p, const std::vector<std::string>& want);
   uint64_t count_rows();
+  // two-phase multi-writer commit: stage() writes a fragment only,
+  // commit_staged() publishes any number of staged fragments in ONE version
+  std::pair<std::string, uint64_t> stage(const std::vector<Column>& cols);
+  uint64_t commit_staged(const std::vector<std::pair<std::string, uint64_t>>& frags, uint32_t vec_dim);
   uint64_t compact();  // rewrite live rows into one fragment (new version)
   const std::vector<ColSpec>& schema() const { return schema_; }
   int col_index(const std::string& name) const;

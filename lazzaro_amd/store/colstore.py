@@ -80,6 +80,20 @@ class ColumnarTable:
         fault_point("store.commit")
         return int(self._t.append(self._columns(rows)))
 
+    def stage_rows(self, rows: Sequence[Dict]):
+        """Write rows as an unpublished fragment -> (file, rows, vector dim)."""
+        fault_point("store.commit")
+        f, n, d = self._t.stage(self._columns(rows))
+        return str(f), int(n), int(d)
+
+    def commit_staged(self, staged: Sequence[Tuple[str, int, int]]) -> int:
+        """Publish staged fragments (from any number of writers) in one version."""
+        fault_point("store.commit")
+        dims = {int(d) for _, n, d in staged if n}
+        if len(dims) > 1:
+            raise ValueError("staged fragments with different vector dims")
+        return int(self._t.commit_staged([(f, int(n)) for f, n, _ in staged], dims.pop() if dims else 0))
+
     def replace_rows(self, eq: Sequence[Tuple[str, str]], rows: Sequence[Dict]) -> Tuple[int, int]:
         """Atomically delete the rows matching ``eq`` and append ``rows`` (one
         committed version). Returns (rows deleted, new version)."""

@@ -132,3 +132,32 @@ def test_distributed_kmeans():
 @pytest.mark.parametrize("world", [2, 4])
 def test_distributed_components(world):
     assert all(spawn(world, _components).values())
+
+
+def _commit(comm):
+    import os
+    import tempfile
+
+    from lazzaro_amd.parallel.commit import distributed_commit
+    from lazzaro_amd.store.colstore import NODE_SCHEMA, ColumnarTable
+    root = os.environ["LZK_TEST_ROOT"]
+    t = ColumnarTable(root, "nodes", NODE_SCHEMA)
+    comm.barrier()
+    v0 = t.version
+    comm.barrier()
+    rows = [dict(id=f"r{comm.rank}_{i}", user_id=f"u{comm.rank}", content="c", vector=[float(comm.rank)] * 4,
+                 type="semantic", timestamp=0.0, access_count=0, last_accessed=0.0, salience=0.5,
+                 is_super_node=False, child_ids="[]", parent_id="", shard_key="default", metadata="{}")
+            for i in range(comm.rank + 2)]
+    v = distributed_commit(comm, t, rows)
+    return (v0, v, t.count(), sorted({r["user_id"] for r in t.scan()}))
+
+
+def test_distributed_commit_is_one_version(tmp_path, monkeypatch):
+    monkeypatch.setenv("LZK_TEST_ROOT", str(tmp_path))
+    out = spawn(3, _commit)
+    v0 = {o[0] for o in out.values()}
+    vs = {o[1] for o in out.values()}
+    assert len(vs) == 1 and vs.pop() == v0.pop() + 1
+    for o in out.values():
+        assert o[2] == 2 + 3 + 4 and o[3] == ["u0", "u1", "u2"]
