@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from lazzaro_amd.index.device_graph import DeviceGraph  # noqa: E402
-from lazzaro_amd.ops.search import flat_topk  # noqa: E402
+from lazzaro_amd.ops.search import flat_topk, flat_topk_dual  # noqa: E402
 from lazzaro_amd.parallel import Communicator  # noqa: E402
 from lazzaro_amd.parallel.sharded import merge_topk  # noqa: E402
 
@@ -67,8 +67,10 @@ class ShardedBuffer:
     def owner(self, topic: torch.Tensor) -> torch.Tensor:
         return topic % self.comm.world
 
-    def global_search(self, q: torch.Tensor, k: int):
-        """All-gather queries, local fused top-k, all-gather candidates, merge."""
+    def global_search(self, q: torch.Tensor, k: int, q_label: torch.Tensor = None):
+        """All-gather queries, local fused top-k, all-gather candidates, merge.
+        With ``q_label`` the same scan (flat_topk_dual) also returns this
+        rank's shard-filtered top-k for its own queries (within-shard links)."""
         comm = self.comm
         nq = torch.tensor([q.shape[0]], device=self.dev)
         sizes = comm.all_gather_rows(nq).tolist()
@@ -77,22 +79,32 @@ class ShardedBuffer:
         qp[: q.shape[0]] = q
         allq = comm.all_gather_rows(qp)  # [world*mx, Dp]
         n = self.g.n
-        s, r = flat_topk(self.g.emb[:n], allq, k, bias=self.g.bias[:n])
+        lo = comm.rank * mx
+        local = None
+        if q_label is None:
+            s, r = flat_topk(self.g.emb[:n], allq, k, bias=self.g.bias[:n])
+        else:
+            ql = torch.full((allq.shape[0],), -1, dtype=torch.int32, device=self.dev)
+            ql[lo: lo + q.shape[0]] = q_label.to(torch.int32)
+            (s, r), (sw, rw) = flat_topk_dual(self.g.emb[:n], allq, k, bias=self.g.bias[:n],
+                                              row_label=self.g.shard[:n], q_label=ql)
+            local = (sw[lo: lo + q.shape[0]], rw[lo: lo + q.shape[0]])
         gid = torch.where(r >= 0, (comm.rank << ROW_BITS) + r, r)
         S = comm.all_gather_rows(s).view(comm.world, comm.world * mx, k)
         I = comm.all_gather_rows(gid).view(comm.world, comm.world * mx, k)
-        lo = comm.rank * mx
         S = S[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
         I = I[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
-        return merge_topk(S, I, k)
+        merged = merge_topk(S, I, k)
+        return merged if q_label is None else (merged, local)
 
     def consolidate(self, q: torch.Tensor, topic: torch.Tensor, sal: torch.Tensor, convs_total: int, now: float):
         comm, g = self.comm, self.g
         # (2) route facts to topic owners
         if comm.world > 1:
             q, topic, sal = comm.reshard(self.owner(topic), q, topic, sal)
-        # (3) global dedupe + cross-shard link candidates
-        s, gid = self.global_search(q, 3)
+        # (3) global dedupe + cross-shard link candidates, and (same scan) the
+        #     within-shard candidates of this rank's facts
+        (s, gid), shard_hits = self.global_search(q, 3, q_label=topic)
         dup = (gid[:, 0] >= 0) & (s[:, 0] > 0.95)
         local_dup = dup & ((gid[:, 0] >> ROW_BITS) == comm.rank)
         rows = (gid[:, 0][local_dup] & ((1 << ROW_BITS) - 1))
@@ -103,7 +115,8 @@ class ShardedBuffer:
         keep = ~dup
         # (4) insert + links (within-shard via DeviceGraph.ingest, cross-shard from the global search)
         n0 = g.n
-        out = g.ingest(q[keep], topic[keep], sal[keep], now=now, dedupe=False, global_links=False)
+        out = g.ingest(q[keep], topic[keep], sal[keep], now=now, dedupe=False, global_links=False,
+                       shard_hits=(shard_hits[0][keep], shard_hits[1][keep]))
         cross = (s[keep] > 0.5) & (gid[keep] >= 0) & ((gid[keep] >> ROW_BITS) != comm.rank)
         n_cross = int(cross.sum().item())
         if n_cross:  # cross-rank associations: local source row -> global target id

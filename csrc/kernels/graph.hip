@@ -54,6 +54,14 @@ __global__ __launch_bounds__(NTB) void decay_flag_kernel(
 }
 
 // flag survivors without decaying (eviction: drop edges touching dead nodes)
+__global__ __launch_bounds__(NTB) void salience_decay_kernel(float* __restrict__ sal, long nn, float keep,
+                                                             float floor_) {
+  for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
+    const float s = sal[i];
+    sal[i] = s > floor_ ? floor_ + (s - floor_) * keep : floor_;
+  }
+}
+
 __global__ __launch_bounds__(NTB) void flag_alive_kernel(const int* __restrict__ src, const int* __restrict__ dst,
                                                          long ne, const unsigned char* __restrict__ alive,
                                                          unsigned char* __restrict__ flag, int* __restrict__ block_cnt) {
@@ -278,8 +286,19 @@ LZK_EXPORT int lzk_decay_flag(float* w, const int* src, const int* dst, long ne,
                               float floor_, void* stream) {
   long nb = (ne + NTB - 1) / NTB;
   if (nb == 0) nb = 1;
+  // The node-salience decay rides in the edge launch only while that grid is
+  // large enough to stream the nodes; a pruned-down edge list (a few blocks)
+  // would leave 10^7 nodes to a handful of workgroups, so it gets its own
+  // right-sized grid-stride launch instead.
+  const long node_blocks = (nn + 4L * NTB - 1) / (4L * NTB);
+  const bool fused = nb >= node_blocks || nb >= 2048;
   hipLaunchKernelGGL(decay_flag_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, w, src, dst, ne, alive,
-                     1.f - rate, thr, flag, block_cnt, sal, nn, floor_);
+                     1.f - rate, thr, flag, block_cnt, fused ? sal : (float*)nullptr, nn, floor_);
+  if (!fused && sal && nn > 0) {
+    const long g = node_blocks < 4096 ? node_blocks : 4096;
+    hipLaunchKernelGGL(salience_decay_kernel, dim3((unsigned)g), dim3(NTB), 0, (hipStream_t)stream, sal, nn,
+                       1.f - rate, floor_);
+  }
   return (int)hipGetLastError();
 }
 

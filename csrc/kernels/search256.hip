@@ -99,16 +99,25 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_kernel(
 // tile i+1 overlaps the epilogue of tile i and no epilogue global load can
 // drain the in-flight DMA.
 constexpr int EPI_OFF = 8 * HALF;               // u16 offset of the epilogue area (128 KiB)
-constexpr int CAND_P_LDS = LDS_BYTES + 2 * 4 * 256 * 4;
+constexpr int EPI_ARRAYS = 5;                   // thr | bias | row label | query label | thr2
+constexpr int CAND_P_LDS = LDS_BYTES + 2 * EPI_ARRAYS * 256 * 4;
 
-template <bool HAS_BIAS, bool HAS_LABEL>
+// DUAL: one GEMM pass serves two searches of the same queries -- list A keeps
+// every row with score >= thr[q] (no label filter), list B keeps rows whose
+// label equals the query's and score >= thr2[q]. Consolidation needs exactly
+// this pair (global dedupe/links + within-shard links, reference
+// memory_system.py:719-733 / :816-836 / :853-889) and the scan is MFMA-bound,
+// so fusing halves its cost.
+template <bool HAS_BIAS, bool HAS_LABEL, bool DUAL>
 __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     const u16* __restrict__ X, long ldx, int nrows, const u16* __restrict__ Qm, long ldq, int nq, int D,
     const float* __restrict__ bias, const int* __restrict__ row_label, const int* __restrict__ q_label,
     float alpha, const float* __restrict__ thr, int n_qt, int n_tiles, int cap, int* __restrict__ cnt,
-    float* __restrict__ cs, int* __restrict__ ci) {
+    float* __restrict__ cs, int* __restrict__ ci, const float* __restrict__ thr2, int* __restrict__ cnt2,
+    float* __restrict__ cs2, int* __restrict__ ci2) {
+  static_assert(!DUAL || HAS_LABEL, "dual search needs labels");
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  float* epi = reinterpret_cast<float*>(smem + EPI_OFF);  // [parity][thr | bias | lab | qlab][256]
+  float* epi = reinterpret_cast<float*>(smem + EPI_OFF);  // [parity][array][256]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -119,20 +128,30 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
   int tile = walk.next;
   if (!walk.valid(tile)) return;
 
+  // 4 wave-level DMAs (64 x 4 B) per array, spread over the 8 waves
   auto stage_epi = [&](int tl, int par) {
     const int r0 = (tl / n_qt) * BM, q0 = (tl % n_qt) * BN;
-    const int a = wave >> 1;  // 0 thr, 1 bias, 2 row label, 3 query label (wave-uniform)
-    const bool need = a == 0 || (a == 1 && HAS_BIAS) || (a >= 2 && HAS_LABEL);
-    if (!need) return;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = (wave & 1) * 2 + i;
+    for (int g = wave; g < 4 * EPI_ARRAYS; g += 8) {
+      const int a = g >> 2, c = g & 3;  // wave-uniform
+      const bool need = a == 0 || (a == 1 && HAS_BIAS) || ((a == 2 || a == 3) && HAS_LABEL) || (a == 4 && DUAL);
+      if (!need) continue;
       const void* src;
       if (a == 0) src = thr + min(q0 + c * 64 + lane, nq - 1);
       else if (a == 1) src = bias + min(r0 + c * 64 + lane, nrows - 1);
       else if (a == 2) src = row_label + min(r0 + c * 64 + lane, nrows - 1);
-      else src = q_label + min(q0 + c * 64 + lane, nq - 1);
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(epi + par * 1024 + a * 256 + c * 64), 4, 0, 0);
+      else if (a == 3) src = q_label + min(q0 + c * 64 + lane, nq - 1);
+      else src = thr2 + min(q0 + c * 64 + lane, nq - 1);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                       (lds_void_t*)(epi + par * (EPI_ARRAYS * 256) + a * 256 + c * 64), 4, 0, 0);
+    }
+  };
+
+  auto append = [&](int* cn, float* cv, int* cix, int q, float v, int r) {
+    const int pos = atomicAdd(cn + q, 1);
+    if (pos < cap) {
+      cv[(long)q * cap + pos] = v;
+      cix[(long)q * cap + pos] = r;
     }
   };
 
@@ -153,17 +172,19 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     // ---- epilogue of `cur` (operands from LDS only) ----
     {
       const int r0 = (cur / n_qt) * BM, q0 = (cur % n_qt) * BN;
-      const float* e_thr = epi + cpar * 1024;
+      const float* e_thr = epi + cpar * (EPI_ARRAYS * 256);
       const float* e_bias = e_thr + 256;
       const int* e_lab = reinterpret_cast<const int*>(e_thr + 512);
       const int* e_qlab = reinterpret_cast<const int*>(e_thr + 768);
+      const float* e_thr2 = e_thr + 1024;
       int qq[4], ql[4];
-      float th[4];
+      float th[4], th2[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int qlo = wc * 64 + j * 16 + (lane & 15);
         qq[j] = q0 + qlo;
         th[j] = (qq[j] < nq) ? e_thr[qlo] : __builtin_huge_valf();
+        th2[j] = (DUAL && qq[j] < nq) ? e_thr2[qlo] : __builtin_huge_valf();
         ql[j] = HAS_LABEL ? e_qlab[qlo] : -1;
       }
       const bool full = r0 + BM <= nrows;
@@ -181,26 +202,27 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float sc[4];
-          float m = LZK_NEG_INF;
+          bool lab_ok[4];
+          float m = LZK_NEG_INF, m2 = LZK_NEG_INF;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             sc[e] = alpha * acc[i][j][e] + bv[e];
-            bool ok = full || (rb + e < nrows);
-            if (HAS_LABEL) ok = ok && (ql[j] < 0 || lv[e] == ql[j]);
-            sc[e] = ok ? sc[e] : LZK_NEG_INF;
+            const bool in = full || (rb + e < nrows);
+            lab_ok[e] = !HAS_LABEL || ql[j] < 0 || lv[e] == ql[j];
+            if (!DUAL && !lab_ok[e]) sc[e] = LZK_NEG_INF;  // single search: label filters list A
+            if (!in) sc[e] = LZK_NEG_INF;
             m = fmaxf(m, sc[e]);
+            if (DUAL && lab_ok[e]) m2 = fmaxf(m2, sc[e]);
           }
           if (m >= th[j]) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (sc[e] >= th[j] && sc[e] != LZK_NEG_INF) {
-                const int pos = atomicAdd(cnt + qq[j], 1);
-                if (pos < cap) {
-                  cs[(long)qq[j] * cap + pos] = sc[e];
-                  ci[(long)qq[j] * cap + pos] = rb + e;
-                }
-              }
-            }
+            for (int e = 0; e < 4; ++e)
+              if (sc[e] >= th[j] && sc[e] != LZK_NEG_INF) append(cnt, cs, ci, qq[j], sc[e], rb + e);
+          }
+          if (DUAL && m2 >= th2[j]) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (lab_ok[e] && sc[e] >= th2[j] && sc[e] != LZK_NEG_INF) append(cnt2, cs2, ci2, qq[j], sc[e], rb + e);
           }
         }
       }
@@ -306,12 +328,13 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
   }
   if (g_cand_persist && nblk >= g_n_cu) {
     const int grid = g_n_cu;
-#define LZK_GP(B, L)                                                                                               \
-  do {                                                                                                             \
-    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, L>,                                      \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                             \
-    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, L>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx, nrows, q, \
-                       ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs, ci);       \
+#define LZK_GP(B, L)                                                                                                \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, L, false>,                                \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, L, false>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,    \
+                       nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs,   \
+                       ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr);                    \
   } while (0)
     if (bias && row_label) LZK_GP(true, true);
     else if (bias) LZK_GP(true, false);
@@ -332,6 +355,40 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
   else if (row_label) LZK_GO(false, true);
   else LZK_GO(false, false);
 #undef LZK_GO
+  return (int)hipGetLastError();
+}
+
+// Dual candidate pass (one GEMM, two lists): list A unfiltered (thr), list B
+// label-filtered (thr2). row_label / q_label required. Counts zeroed by caller.
+LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, int D,
+                                  const float* bias, const int* row_label, const int* q_label, float alpha,
+                                  const float* thr, const float* thr2, int cap, int* cnt, float* cs, int* ci,
+                                  int* cnt2, float* cs2, int* ci2, void* stream) {
+  if (D % BK != 0 || nq <= 0 || nrows <= 0 || cap <= 0 || !row_label || !q_label) return (int)hipErrorInvalidValue;
+  const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
+  const long nblk = (long)n_rt * n_qt;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X;
+  const u16* q = (const u16*)Qm;
+#define LZK_GD(B)                                                                                                   \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, true, true>,                              \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,  \
+                       nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs,   \
+                       ci, thr2, cnt2, cs2, ci2);                                                                   \
+  } while (0)
+  if (bias) LZK_GD(true);
+  else LZK_GD(false);
+#undef LZK_GD
   return (int)hipGetLastError();
 }
 

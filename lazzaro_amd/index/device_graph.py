@@ -29,7 +29,7 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from ..ops import graph_ops as G
-from ..ops.search import flat_topk
+from ..ops.search import flat_topk, flat_topk_dual
 
 NEG_INF = float("-inf")
 
@@ -129,19 +129,33 @@ class DeviceGraph:
     def ingest(self, q: torch.Tensor, shard: torch.Tensor, salience: torch.Tensor,
                now: Optional[float] = None, dedupe_thr: float = 0.95, link_k: int = 3,
                link_thr: float = 0.5, link_scale: float = 0.8, chain_w: float = 0.5,
-               dedupe: bool = True, global_links: bool = True) -> Dict[str, int]:
+               dedupe: bool = True, global_links: bool = True, shard_hits=None) -> Dict[str, int]:
         """One consolidation batch of M facts (unit rows ``q`` [M, Dp]).
+
+        All searches run over the rows that existed before the batch (the
+        reference links new facts to EXISTING memories, memory_system.py:
+        816-821, 842-847) and come from ONE scan (``flat_topk_dual``): the
+        unfiltered top-k gives dedupe (top-1 > 0.95) and global links, the
+        shard-filtered top-k gives within-shard links.
         ``dedupe``/``global_links`` False when a sharded caller already did the
-        global search (see bench/bench_consolidate.py)."""
+        global search; it may then pass its shard-filtered hits (``shard_hits``
+        = (scores, rows) aligned with ``q``) from the same fused scan."""
         now = time.time() if now is None else now
         q = q.to(self.emb.dtype)
         M = q.shape[0]
         if M == 0:
             return {"deduped": 0, "inserted": 0, "linked": 0}
-        # K5 dedupe: top-1 over live rows
+        sh_all = shard.to(self.device).to(torch.int32)
+        if shard_hits is not None:
+            sw_all, rw_all = shard_hits
+            sg_all = rg_all = None
+        elif dedupe or global_links:
+            (sg_all, rg_all), (sw_all, rw_all) = self._search_dual(q, link_k, sh_all)
+        else:
+            sw_all, rw_all = self._search(q, link_k, row_label=self.shard[: self.n], q_label=sh_all)
+            sg_all = rg_all = None
         if dedupe:
-            s1, r1 = self._search(q, 1)
-            s1, r1 = s1[:, 0], r1[:, 0]
+            s1, r1 = sg_all[:, 0], rg_all[:, 0]
             dup = (r1 >= 0) & (s1 > dedupe_thr)
         else:
             dup = torch.zeros(M, dtype=torch.bool, device=self.device)
@@ -156,17 +170,11 @@ class DeviceGraph:
         out = {"deduped": M - nk, "inserted": nk, "linked": 0}
         if nk == 0:
             return out
-        qn, sh, sl = q[keep], shard.to(self.device)[keep].to(torch.int32), salience.to(self.device)[keep]
-        # linking candidates exclude the batch itself (reference :816-821, :842-847)
-        n_old = self.n
+        qn, sh, sl = q[keep], sh_all[keep], salience.to(self.device)[keep]
         rows = self.add_nodes(qn, sh, sl, now)
-        old_bias = self.bias[:self.n].clone()
-        old_bias[n_old:] = NEG_INF
-        # K6a within-shard: label-filtered top-k
-        sw, rw = self._search(qn, link_k, row_label=self.shard[: self.n], q_label=sh, bias=old_bias)
-        # K6b global top-k over all existing non-super rows
-        if global_links:
-            sg, rg = self._search(qn, link_k, bias=old_bias)
+        sw, rw = sw_all[keep], rw_all[keep]
+        if global_links and sg_all is not None:
+            sg, rg = sg_all[keep], rg_all[keep]
         else:
             sg = torch.full_like(sw, NEG_INF)
             rg = torch.full_like(rw, -1)
@@ -190,6 +198,15 @@ class DeviceGraph:
         for k_ in out:
             self.stats[k_] += out[k_]
         return out
+
+    def _search_dual(self, q: torch.Tensor, k: int, q_label: torch.Tensor):
+        n = self.n
+        if n == 0:
+            m = q.shape[0]
+            e = (torch.full((m, k), NEG_INF, device=self.device),
+                 torch.full((m, k), -1, dtype=torch.long, device=self.device))
+            return e, e
+        return flat_topk_dual(self.emb[:n], q, k, bias=self.bias[:n], row_label=self.shard[:n], q_label=q_label)
 
     # ------------------------------------------------------------------ maintenance
     def decay_prune(self, rate: float = 0.01, threshold: float = 0.5, conversations: int = 1) -> int:

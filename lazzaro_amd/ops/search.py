@@ -79,6 +79,7 @@ class _Workspace:
 
 _ws = _Workspace()
 _ws_cand = _Workspace()
+_ws_cand2 = _Workspace()
 _ws_fallback = _Workspace()
 
 # Large-batch candidate path (csrc/kernels/search256.hip): used when the batch
@@ -161,49 +162,44 @@ def _flat_topk_lane(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset,
     return os_, oi
 
 
-def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset):
-    """Threshold-filtered candidates on the 256x256 pipeline (search256.hip).
-
-    1. thr[q] = k-th best score over the strided sample X[::S] (exact, lane
-       kernel), lowered by a small margin that covers the fp32 accumulation
-       order difference between the two kernels -> a lower bound of the true
-       k-th score, so every true top-k row passes ``score >= thr``.
-    2. candidate pass over all rows; 3. exact select per query. Queries whose
-       list overflowed are recomputed with the lane kernel (masked launch, no
-       host synchronisation anywhere on this path).
-    """
-    L = _lib.lib()
-    nq, D = Q.shape
+def _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S):
+    """Lower bound of each query's k-th score: exact top-k over the strided
+    sample X[::S] (lane kernel), lowered by a margin covering the fp32
+    accumulation-order difference between the two kernels."""
     N = X.shape[0]
-    dev = X.device
-    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
-    Xs = X[::S]
     bs = bias[:N:S].contiguous() if bias is not None else None
     ls = row_label[:N:S].contiguous() if row_label is not None else None
-    ts, _ = _flat_topk_lane(Xs, Q, kslot, kslot, bs, ls, q_label, alpha, 0, None)
+    ts, _ = _flat_topk_lane(X[::S], Q, kslot, kslot, bs, ls, q_label, alpha, 0, None)
     thr = ts[:, k - 1].contiguous()
     thr = thr - 2e-4 * (1.0 + thr.abs())
-    thr = torch.nan_to_num(thr, nan=float("-inf"))
-    cap = max(1024, 8 * kslot * S)
-    ws = _ws_cand.get(dev, nq * (4 + 8 * cap))
+    return torch.nan_to_num(thr, nan=float("-inf"))
+
+
+def _cand_lists(dev, nq, cap, slot):
+    ws = (_ws_cand if slot == 0 else _ws_cand2).get(dev, nq * (4 + 8 * cap))
     cnt = ws[: nq * 4].view(torch.int32)
     cs = ws[nq * 4: nq * 4 + nq * cap * 4].view(torch.float32)
     ci = ws[nq * 4 + nq * cap * 4: nq * 4 + nq * cap * 8].view(torch.int32)
     cnt.zero_()
+    return cnt, cs, ci
+
+
+def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap):
+    """Exact per-query select from a candidate list; queries whose list
+    overflowed are recomputed by the lane kernel ON DEVICE (the masked launch
+    skips every query tile without an overflowed query -- a few us when none
+    did), so the path never synchronises with the host."""
+    L = _lib.lib()
+    nq, D = Q.shape
+    N = X.shape[0]
+    dev = X.device
     st = _lib.stream_ptr(dev)
-    rc = L.lzk_flat_cand(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D,
-                         _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha),
-                         thr.data_ptr(), cap, cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), st)
-    _lib.check(rc, "lzk_flat_cand")
     os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oi = torch.empty((nq, k), dtype=torch.long, device=dev)
     ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
     rc = L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, int(k),
                            int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
     _lib.check(rc, "lzk_cand_select")
-    # Overflowed queries are recomputed by the lane kernel ON DEVICE: the masked
-    # launch skips every query tile without an overflowed query (a few us when
-    # none overflowed), so the path never synchronises with the host.
     nch = L.lzk_flat_topk_chunks(N, nq, TARGET_WGS)
     part = nq * nch * kslot
     wsf = _ws_fallback.get(dev, part * 8)
@@ -217,6 +213,69 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
                                  os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
     _lib.check(rc, "lzk_topk_merge_masked")
     return os_, oi
+
+
+def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset):
+    """Threshold-filtered candidates on the 256x256 pipeline (search256.hip).
+
+    1. thr[q] = lower bound of the k-th score (:func:`_sample_threshold`), so
+       every true top-k row passes ``score >= thr``;
+    2. candidate pass over all rows; 3. exact select per query with the
+       on-device overflow fallback (:func:`_select_with_fallback`).
+    """
+    L = _lib.lib()
+    nq, D = Q.shape
+    N = X.shape[0]
+    dev = X.device
+    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
+    thr = _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S)
+    cap = max(1024, 8 * kslot * S)
+    cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    rc = L.lzk_flat_cand(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D,
+                         _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha),
+                         thr.data_ptr(), cap, cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(rc, "lzk_flat_cand")
+    return _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap)
+
+
+def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_label, bias=None,
+                   alpha: float = 1.0, idx_offset: int = 0):
+    """Two searches of the same queries from ONE scan: the unfiltered top-k and
+    the label-filtered top-k (label < 0 = any). Consolidation needs both --
+    global dedupe/links and within-shard links (reference memory_system.py:
+    719-733, 816-836, 853-889) -- and the large-batch scan is MFMA-bound, so
+    the candidate path computes each score once and files it into two lists.
+    Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
+    if Q.dim() == 1:
+        Q = Q[None, :]
+    nq, D = Q.shape
+    N = X.shape[0]
+    if not X.is_cuda:
+        return (_ref_topk(X, Q, k, bias, None, None, alpha, idx_offset),
+                _ref_topk(X, Q, k, bias, row_label, q_label, alpha, idx_offset))
+    L = _lib.lib()
+    kslot = L.lzk_flat_topk_kslot(int(k))
+    if kslot < 0 or N == 0 or nq == 0 or not _use_cand(N, nq, kslot):
+        return (flat_topk(X, Q, k, bias=bias, alpha=alpha, idx_offset=idx_offset),
+                flat_topk(X, Q, k, bias=bias, row_label=row_label, q_label=q_label, alpha=alpha,
+                          idx_offset=idx_offset))
+    assert X.dtype == torch.bfloat16 and Q.dtype == torch.bfloat16 and D % 64 == 0
+    assert row_label.dtype == torch.int32 and q_label.dtype == torch.int32
+    dev = X.device
+    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
+    thr_a = _sample_threshold(X, Q, k, kslot, bias, None, None, alpha, S)
+    thr_b = _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S)
+    cap = max(1024, 8 * kslot * S)
+    ca = _cand_lists(dev, nq, cap, 0)
+    cb = _cand_lists(dev, nq, cap, 1)
+    rc = L.lzk_flat_cand_dual(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D, _lib.ptr(bias),
+                              row_label.data_ptr(), q_label.data_ptr(), float(alpha), thr_a.data_ptr(),
+                              thr_b.data_ptr(), cap, ca[0].data_ptr(), ca[1].data_ptr(), ca[2].data_ptr(),
+                              cb[0].data_ptr(), cb[1].data_ptr(), cb[2].data_ptr(), _lib.stream_ptr(dev))
+    _lib.check(rc, "lzk_flat_cand_dual")
+    ra = _select_with_fallback(X, Q, k, kslot, bias, None, None, alpha, idx_offset, *ca, cap)
+    rb = _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, *cb, cap)
+    return ra, rb
 
 
 def segment_topk(xs, Q: torch.Tensor, k: int, *, biases=None, scales=None, alpha: float = 1.0, qbias=None):

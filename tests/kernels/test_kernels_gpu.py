@@ -237,3 +237,23 @@ def test_graphed_encoder_matches_eager():
     assert len(emb._graphs) == 2
     torch.testing.assert_close(g1, eager, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(g2, eager[:1], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("n,nq,k", [(300_001, 300, 3), (150_000, 512, 10)])
+def test_flat_topk_dual_gpu(monkeypatch, n, nq, k):
+    """One fused scan == the unfiltered and the label-filtered searches."""
+    from lazzaro_amd.ops.search import flat_topk_dual
+    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", 16)
+    g = torch.Generator(device=DEV).manual_seed(n)
+    X = torch.randn(n, 768, device=DEV, generator=g).to(torch.bfloat16)
+    Q = torch.randn(nq, 768, device=DEV, generator=g).to(torch.bfloat16)
+    b = torch.where(torch.rand(n, device=DEV, generator=g) < 0.05, float("-inf"), 0.0)
+    rl = torch.randint(0, 64, (n,), device=DEV, dtype=torch.int32, generator=g)
+    ql = torch.randint(-1, 64, (nq,), device=DEV, dtype=torch.int32, generator=g)
+    (sa, ia), (sb, ib) = flat_topk_dual(X, Q, k, bias=b, row_label=rl, q_label=ql)
+    ra = _ref_topk(X.cpu(), Q.cpu(), k, b.cpu())
+    rb = _ref_topk(X.cpu(), Q.cpu(), k, b.cpu(), rl.cpu(), ql.cpu())
+    for (s, i), (rs, ri) in (((sa, ia), ra), ((sb, ib), rb)):
+        torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
+        assert (i.cpu() == ri).float().mean() > 0.995
