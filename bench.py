@@ -165,7 +165,7 @@ def main():
     hit = sum(len(set(r[j].tolist()) & set(ei[j].tolist())) for j in range(nr))
     recall = hit / float(nr * a.k)
     S_tok = int(ids.shape[1])
-    tflops_embed = emb.encoder.flops(ids.numel()) / t_embed / 1e12
+    tflops_embed = emb.encoder.flops(int(lens.sum())) / t_embed / 1e12  # real (unpadded) tokens
     tflops_search = 2.0 * a.rows * a.dim * q16.shape[0] / t_search / 1e12
 
     qps = world * a.batch * a.steps / el
@@ -200,6 +200,8 @@ def main():
                    "global_batch": world * a.batch, "seq_len": S_tok, "parallelism": "tenant-dp%d" % world},
         "recall_at_10": round(recall, 4),
         "breakdown_ms": {"embed": round(t_embed * 1e3, 3), "search": round(t_search * 1e3, 3)},
+        "tokens_per_query": {"padded": S_tok, "real_mean": round(float(lens.float().mean()), 2),
+                             "encoder_layout": "packed varlen (padding never computed)"},
         "tflops": {"embed": round(tflops_embed, 1), "search": round(tflops_search, 1)},
     }
     if consolidate is not None:

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const u16* __restri
 template <int HD>
 __global__ __launch_bounds__(64) void attention_kernel(
     const u16* __restrict__ qkv, long ldq, const int* __restrict__ lens, int S, int H, int nheads,
-    float scale_log2, u16* __restrict__ out, long ldo) {
+    float scale_log2, u16* __restrict__ out, long ldo, const int* __restrict__ cu) {
   constexpr int KSQ = HD / 16;   // k-steps of the S = K Q^T product
   constexpr int NDB = HD / 32;   // 32-row blocks of the output O^T
   __shared__ __attribute__((aligned(16))) u16 vt[HD * 40];  // V^T block: [dim][key], padded rows
@@ -329,9 +329,13 @@ __global__ __launch_bounds__(64) void attention_kernel(
   const int hd = (blockIdx.x / nqb) % nheads;
   const int b = blockIdx.x / (nqb * nheads);
   const int len = lens[b];
-  const long tok0 = (long)b * S;
+  // padded layout: sequence b owns rows [b*S, b*S + S); packed ("varlen")
+  // layout: rows [cu[b], cu[b] + len) only -- padding tokens are never stored
+  const long tok0 = cu ? (long)cu[b] : (long)b * S;
+  const int Sb = cu ? len : S;
+  if (qb * 32 >= Sb) return;  // whole (single-wave) block past the sequence
   const int q = qb * 32 + l32;
-  const int qc = min(q, S - 1);
+  const int qc = min(q, Sb - 1);
   const u16* qrow = qkv + (tok0 + qc) * ldq + hd * HD;
   bf16x8 qf[KSQ];
 #pragma unroll
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(64) void attention_kernel(
   for (int kb = 0; kb < nkb; ++kb) {
     // S^T block [32 keys x 32 queries]: A = K rows, B = Q rows
     const int key = kb * 32 + l32;
-    const u16* krow = qkv + (tok0 + min(key, S - 1)) * ldq + H + hd * HD;
+    const u16* krow = qkv + (tok0 + min(key, Sb - 1)) * ldq + H + hd * HD;
     f32x16 st;
 #pragma unroll
     for (int e = 0; e < 16; ++e) st[e] = 0.f;
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(64) void attention_kernel(
     // stage V^T for this key block (each lane: one key, HD/2 dims)
     {
       const int vk = lane >> 1, vd0 = (lane & 1) * (HD / 2);
-      const u16* vrow = qkv + (tok0 + min(kb * 32 + vk, S - 1)) * ldq + 2 * H + hd * HD + vd0;
+      const u16* vrow = qkv + (tok0 + min(kb * 32 + vk, Sb - 1)) * ldq + 2 * H + hd * HD + vd0;
 #pragma unroll
       for (int c = 0; c < HD / 16; ++c) {
         u16x8 v8 = *reinterpret_cast<const u16x8*>(vrow + 8 * c);
@@ -413,7 +417,7 @@ __global__ __launch_bounds__(64) void attention_kernel(
     }
     __syncthreads();
   }
-  if (q >= S) return;
+  if (q >= Sb) return;
   const float inv = 1.f / l;
   u16* orow = out + (tok0 + q) * ldo + hd * HD;
 #pragma unroll
@@ -489,12 +493,12 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ i
                                                        const u16* __restrict__ temb,
                                                        const float* __restrict__ g,
                                                        const float* __restrict__ bta, int H, float eps,
-                                                       u16* __restrict__ Y) {
+                                                       u16* __restrict__ Y, const int* __restrict__ posv) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
   const int id = ids[t];
-  const int pos = t % S;
+  const int pos = posv ? posv[t] : t % S;
   float v[NC][4];
   float sum = 0.f;
 #pragma unroll
@@ -541,11 +545,12 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ i
 // pooling (mode 0 = masked mean, 1 = CLS) + L2 normalise; one workgroup per sequence
 __global__ __launch_bounds__(256) void pool_norm_kernel(const u16* __restrict__ X, const int* __restrict__ lens,
                                                         int S, int H, int mode, float* __restrict__ out32,
-                                                        u16* __restrict__ out16, int ld16) {
+                                                        u16* __restrict__ out16, int ld16,
+                                                        const int* __restrict__ cu) {
   __shared__ float red[4];
   const int b = blockIdx.x;
   const int len = max(1, lens[b]);
-  const long base = (long)b * S * H;
+  const long base = (cu ? (long)cu[b] : (long)b * S) * H;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};  // up to H = 1024 with 256 threads
   float ss = 0.f;
 #pragma unroll
@@ -693,17 +698,17 @@ LZK_EXPORT int lzk_quant_fp8_rows(const void* X, long ldx, int rows, int D, void
 }
 
 LZK_EXPORT int lzk_attention(const void* qkv, long ldq, const int* lens, int B, int S, int H, int nheads,
-                             float scale, void* out, long ldo, void* stream) {
+                             float scale, void* out, long ldo, const int* cu, void* stream) {
   const int hdim = H / nheads;
   if (H != nheads * hdim || (hdim != 32 && hdim != 64)) return (int)hipErrorInvalidValue;
   const int nqb = (S + 31) / 32;
   dim3 grid(B * nheads * nqb), block(64);
   if (hdim == 64)
     hipLaunchKernelGGL(attention_kernel<64>, grid, block, 0, (hipStream_t)stream, (const u16*)qkv, ldq, lens, S, H,
-                       nheads, scale * 1.4426950408889634f, (u16*)out, ldo);
+                       nheads, scale * 1.4426950408889634f, (u16*)out, ldo, cu);
   else
     hipLaunchKernelGGL(attention_kernel<32>, grid, block, 0, (hipStream_t)stream, (const u16*)qkv, ldq, lens, S, H,
-                       nheads, scale * 1.4426950408889634f, (u16*)out, ldo);
+                       nheads, scale * 1.4426950408889634f, (u16*)out, ldo, cu);
   return (int)hipGetLastError();
 }
 
@@ -721,18 +726,19 @@ LZK_EXPORT int lzk_layernorm(const void* X, long ldx, const void* R, long ldr, c
 }
 
 LZK_EXPORT int lzk_embed_ln(const int* ids, int T, int S, const void* wemb, const void* pemb, const void* temb,
-                            const float* g, const float* b, int H, float eps, void* Y, void* stream) {
+                            const float* g, const float* b, int H, float eps, void* Y, const int* pos,
+                            void* stream) {
   if (H % 4 != 0 || H > 64 * 4 * 4) return (int)hipErrorInvalidValue;
   dim3 grid((T + 3) / 4), block(256);
   hipLaunchKernelGGL((embed_ln_kernel<4>), grid, block, 0, (hipStream_t)stream, ids, T, S, (const u16*)wemb,
-                     (const u16*)pemb, (const u16*)temb, g, b, H, eps, (u16*)Y);
+                     (const u16*)pemb, (const u16*)temb, g, b, H, eps, (u16*)Y, pos);
   return (int)hipGetLastError();
 }
 
 LZK_EXPORT int lzk_pool_norm(const void* X, const int* lens, int B, int S, int H, int mode, float* out32,
-                             void* out16, int ld16, void* stream) {
+                             void* out16, int ld16, const int* cu, void* stream) {
   if (H > 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(pool_norm_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, (const u16*)X, lens, S, H, mode,
-                     out32, (u16*)out16, ld16);
+                     out32, (u16*)out16, ld16, cu);
   return (int)hipGetLastError();
 }

@@ -176,22 +176,44 @@ class SentenceEncoder:
         return sum(t.numel() for t in self.p.values())
 
     # --------------------------------------------------------------- forward
-    def forward(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0):
+    def forward(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0, packed: Optional[bool] = None):
         """ids [B, S] / lens [B] (host or device). Host inputs are staged through
         pinned memory and copied asynchronously, so enqueueing the forward never
-        waits for earlier GPU work."""
+        waits for earlier GPU work.
+
+        ``packed`` (default: on for host inputs on a GPU): drop the padding
+        tokens before the first layer ("varlen" BERT): every GEMM, LayerNorm and
+        the attention run on sum(lens) tokens instead of B*S -- the padded
+        positions never influence the pooled embedding (keys >= len are
+        masked, pooling stops at len), so they are pure waste."""
         c, p = self.cfg, self.p
         B, S = ids.shape
-        ids = _to_dev(ids, self.device)
-        lens = _to_dev(lens, self.device)
-        x = E.embed_ln(ids.view(-1), S, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps)
+        if packed is None:
+            packed = self.device.type == "cuda" and ids.device.type == "cpu" and lens.device.type == "cpu"
+        if packed:
+            lens_h = lens.to(torch.int64).cpu()
+            S_eff = int(lens_h.max()) if B else 1
+            mask = torch.arange(S)[None, :] < lens_h[:, None]
+            ids_p = _to_dev(ids.cpu()[mask], self.device)
+            pos_p = _to_dev(torch.arange(S).expand(B, S)[mask], self.device)
+            cu_h = torch.zeros(B + 1, dtype=torch.int64)
+            cu_h[1:] = torch.cumsum(lens_h, 0)
+            cu = _to_dev(cu_h, self.device)
+            lens = _to_dev(lens_h, self.device)
+            x = E.embed_ln(ids_p, S_eff, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps, pos=pos_p)
+            S = S_eff
+        else:
+            cu = None
+            ids = _to_dev(ids, self.device)
+            lens = _to_dev(lens, self.device)
+            x = E.embed_ln(ids.view(-1), S, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps)
         for i in range(c.layers):
             qkv = self._lin(x, i, "wqkv", "bqkv")
-            ctx = E.attention(qkv, lens, B, S, c.heads)
+            ctx = E.attention(qkv, lens, B, S, c.heads, cu=cu)
             x = E.layernorm(self._lin(ctx, i, "wo", "bo", residual=x), p[f"{i}.ln1_g"], p[f"{i}.ln1_b"], c.eps)
             hdn = self._lin(x, i, "w1", "b1", act="gelu")
             x = E.layernorm(self._lin(hdn, i, "w2", "b2", residual=x), p[f"{i}.ln2_g"], p[f"{i}.ln2_b"], c.eps)
-        return E.pool_norm(x, lens, B, S, c.pooling, pad_to)
+        return E.pool_norm(x, lens, B, S, c.pooling, pad_to, cu=cu)
 
     def flops(self, tokens: int) -> float:
         c = self.cfg

@@ -21,13 +21,13 @@ _lib.register("lzk_gemm_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _l
                                        _lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
 _lib.register("lzk_quant_fp8_rows", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.L, _lib.P, _lib.P])
 _lib.register("lzk_attention", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.F,
-                                         _lib.P, _lib.L, _lib.P])
+                                         _lib.P, _lib.L, _lib.P, _lib.P])
 _lib.register("lzk_layernorm", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.P, _lib.I, _lib.I,
                                          _lib.F, _lib.P, _lib.L, _lib.P])
 _lib.register("lzk_embed_ln", _lib.I, [_lib.P, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P,
-                                        _lib.I, _lib.F, _lib.P, _lib.P])
+                                        _lib.I, _lib.F, _lib.P, _lib.P, _lib.P])
 _lib.register("lzk_pool_norm", _lib.I, [_lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P,
-                                         _lib.I, _lib.P])
+                                         _lib.I, _lib.P, _lib.P])
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, act: str = "none", residual=None,
@@ -101,9 +101,18 @@ def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.T
     return y
 
 
-def attention(qkv: torch.Tensor, lens: torch.Tensor, B: int, S: int, nheads: int, out=None) -> torch.Tensor:
-    """qkv [B*S, 3H] (q|k|v), head_dim 64; keys >= lens[b] are masked."""
+def attention(qkv: torch.Tensor, lens: torch.Tensor, B: int, S: int, nheads: int, out=None,
+              cu: torch.Tensor = None) -> torch.Tensor:
+    """qkv [B*S, 3H] (q|k|v), head_dim 32/64; keys >= lens[b] are masked.
+    Packed ("varlen") layout when ``cu`` (int32 [B+1] row offsets) is given:
+    qkv holds only the sum(lens) real tokens, S = max(lens)."""
     H = qkv.shape[1] // 3
+    if cu is not None and not qkv.is_cuda:
+        outs = []
+        for b in range(B):
+            r0, r1 = int(cu[b]), int(cu[b + 1])
+            outs.append(attention(qkv[r0:r1], lens[b:b + 1], 1, r1 - r0, nheads))
+        return torch.cat(outs) if outs else qkv[:, :H].clone()
     if not qkv.is_cuda:
         x = qkv.float().view(B, S, 3, nheads, H // nheads)
         q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
@@ -112,9 +121,10 @@ def attention(qkv: torch.Tensor, lens: torch.Tensor, B: int, S: int, nheads: int
         s = s.masked_fill(mask[:, None, None, :], float("-inf"))
         o = torch.softmax(s, -1) @ v
         return o.transpose(1, 2).reshape(B * S, H).to(qkv.dtype)
-    y = out if out is not None else torch.empty((B * S, H), dtype=torch.bfloat16, device=qkv.device)
+    rows = qkv.shape[0] if cu is not None else B * S
+    y = out if out is not None else torch.empty((rows, H), dtype=torch.bfloat16, device=qkv.device)
     rc = _lib.lib().lzk_attention(qkv.data_ptr(), qkv.stride(0), lens.data_ptr(), B, S, H, nheads,
-                                  1.0 / math.sqrt(H // nheads), y.data_ptr(), y.stride(0),
+                                  1.0 / math.sqrt(H // nheads), y.data_ptr(), y.stride(0), _lib.ptr(cu),
                                   _lib.stream_ptr(qkv.device))
     _lib.check(rc, "lzk_attention")
     return y
@@ -134,24 +144,35 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e
     return y
 
 
-def embed_ln(ids: torch.Tensor, S: int, wemb, pemb, temb, g, b, eps: float = 1e-12) -> torch.Tensor:
-    """ids [B*S] int32 -> LN(word[ids] + pos[t % S] + type[0]) bf16 [B*S, H]."""
+def embed_ln(ids: torch.Tensor, S: int, wemb, pemb, temb, g, b, eps: float = 1e-12,
+             pos: torch.Tensor = None) -> torch.Tensor:
+    """ids [T] int32 -> LN(word[ids] + pos_emb[p] + type[0]) bf16 [T, H] with
+    p = t % S (padded batch) or the given per-token positions (packed)."""
     T = ids.numel()
     H = wemb.shape[1]
     if not ids.is_cuda:
-        pos = torch.arange(T, device=ids.device) % S
+        pos = (torch.arange(T, device=ids.device) % S) if pos is None else pos.long()
         v = wemb[ids.long()].float() + pemb[pos].float() + temb[0].float()
         return F.layer_norm(v, (H,), g.float(), b.float(), eps).to(wemb.dtype)
     y = torch.empty((T, H), dtype=torch.bfloat16, device=ids.device)
     rc = _lib.lib().lzk_embed_ln(ids.data_ptr(), T, S, wemb.data_ptr(), pemb.data_ptr(), temb.data_ptr(),
-                                 g.data_ptr(), b.data_ptr(), H, float(eps), y.data_ptr(), _lib.stream_ptr(ids.device))
+                                 g.data_ptr(), b.data_ptr(), H, float(eps), y.data_ptr(), _lib.ptr(pos),
+                                 _lib.stream_ptr(ids.device))
     _lib.check(rc, "lzk_embed_ln")
     return y
 
 
-def pool_norm(x: torch.Tensor, lens: torch.Tensor, B: int, S: int, mode: str = "mean", out16_width: int = 0):
-    """Returns (fp32 [B,H] unit rows, bf16 [B,out16_width] zero-padded copy or None)."""
+def pool_norm(x: torch.Tensor, lens: torch.Tensor, B: int, S: int, mode: str = "mean", out16_width: int = 0,
+              cu: torch.Tensor = None):
+    """Returns (fp32 [B,H] unit rows, bf16 [B,out16_width] zero-padded copy or None).
+    ``cu`` (int32 [B+1]): packed layout, sequence b = rows cu[b]:cu[b+1]."""
     H = x.shape[1]
+    if cu is not None and not x.is_cuda:
+        xs = torch.zeros((B, S, H), dtype=x.dtype)
+        for bb in range(B):
+            r0, r1 = int(cu[bb]), int(cu[bb + 1])
+            xs[bb, : r1 - r0] = x[r0:r1]
+        return pool_norm(xs.view(B * S, H), lens, B, S, mode, out16_width)
     if not x.is_cuda:
         v = x.float().view(B, S, H)
         if mode == "cls":
@@ -168,6 +189,7 @@ def pool_norm(x: torch.Tensor, lens: torch.Tensor, B: int, S: int, mode: str = "
     out32 = torch.empty((B, H), dtype=torch.float32, device=x.device)
     out16 = torch.empty((B, out16_width), dtype=torch.bfloat16, device=x.device) if out16_width else None
     rc = _lib.lib().lzk_pool_norm(x.data_ptr(), lens.data_ptr(), B, S, H, 1 if mode == "cls" else 0,
-                                  out32.data_ptr(), _lib.ptr(out16), out16_width, _lib.stream_ptr(x.device))
+                                  out32.data_ptr(), _lib.ptr(out16), out16_width, _lib.ptr(cu),
+                                  _lib.stream_ptr(x.device))
     _lib.check(rc, "lzk_pool_norm")
     return out32, out16

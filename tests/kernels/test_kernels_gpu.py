@@ -257,3 +257,29 @@ def test_flat_topk_dual_gpu(monkeypatch, n, nq, k):
     for (s, i), (rs, ri) in (((sa, ia), ra), ((sb, ib), rb)):
         torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
         assert (i.cpu() == ri).float().mean() > 0.995
+
+
+def test_packed_varlen_encoder_gpu():
+    from lazzaro_amd.models.encoder import SentenceEncoder
+    enc = SentenceEncoder("bge-base", device=DEV, seed=1)
+    ids = torch.randint(1000, 30000, (37, 40), dtype=torch.int32)
+    lens = torch.randint(2, 41, (37,), dtype=torch.int32)
+    lens[0] = 40
+    for b in range(37):
+        ids[b, lens[b]:] = 0
+    a, a16 = enc.forward(ids, lens, pad_to=768, packed=False)
+    b, b16 = enc.forward(ids, lens, pad_to=768, packed=True)
+    assert ((a * b).sum(1) > 0.9999).all()
+    assert torch.equal(a16[:, 768:], b16[:, 768:]) if a16.shape[1] > 768 else True
+
+
+def test_attention_packed_gpu():
+    B, heads, hd = 5, 12, 64
+    H = heads * hd
+    lens = torch.tensor([40, 3, 33, 64, 1], dtype=torch.int32)
+    cu = torch.zeros(B + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(lens, 0)
+    qkv = torch.randn(int(cu[-1]), 3 * H, device=DEV).to(torch.bfloat16)
+    o = E.attention(qkv, lens.to(DEV), B, int(lens.max()), heads, cu=cu.to(DEV))
+    ref = E.attention(qkv.cpu(), lens, B, int(lens.max()), heads, cu=cu)
+    assert _rel(o.cpu(), ref) < 1e-2

@@ -66,3 +66,16 @@ def test_long_text_chunking_windows_and_mean():
     # batch_embed routes long texts through the chunked path
     out = emb.batch_embed(["short text", long * 3])
     assert len(out) == 2 and abs(sum(x * x for x in out[1]) - 1.0) < 1e-4
+
+
+def test_packed_varlen_forward_matches_padded():
+    from lazzaro_amd.models.encoder import SentenceEncoder
+    enc = SentenceEncoder("tiny", seed=2)
+    ids = torch.randint(1000, 4000, (4, 24), dtype=torch.int32)
+    lens = torch.tensor([24, 7, 15, 2], dtype=torch.int32)
+    for b in range(4):
+        ids[b, lens[b]:] = 0
+    a, _ = enc.forward(ids, lens, packed=False)
+    b, _ = enc.forward(ids, lens, packed=True)
+    torch.testing.assert_close(a, b, atol=2e-2, rtol=0)  # bf16 CPU reference, same math
+    assert ((a * b).sum(1) > 0.9999).all()
