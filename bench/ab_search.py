@@ -20,11 +20,14 @@ from lazzaro_amd.ops import _lib  # noqa: E402
 
 _L = _lib.lib()
 _L.lzk_set_cand_persist.argtypes = [ctypes.c_int]
+_L.lzk_set_g256_opt.argtypes = [ctypes.c_int]
+VARIANTS = os.environ.get("AB_VARIANTS", "lane,cand,cand_p").split(",")
 
 
 def run(path, X, Q, k, bias):
     if path.startswith("cand"):
-        _L.lzk_set_cand_persist(1 if path == "cand_p" else 0)
+        _L.lzk_set_cand_persist(0 if path == "cand" else 1)
+        _L.lzk_set_g256_opt(int(path[len("cand_p"):]) if path.startswith("cand_p") and len(path) > 6 else 0)
         path = "cand"
     os.environ["LZK_SEARCH"] = path
     return S.flat_topk(X, Q, k, bias=bias, alpha=2.0 if bias is not None else 1.0)
@@ -49,15 +52,16 @@ def main():
             bias = torch.empty(n, device=dev)
             for r0 in range(0, n, 1 << 20):
                 bias[r0:r0 + (1 << 20)] = -(X[r0:r0 + (1 << 20)].float() ** 2).sum(1)
-        sl, il = run("lane", X, Q, k, bias)
-        sc, ic = run("cand", X, Q, k, bias)
-        sp, ip_ = run("cand_p", X, Q, k, bias)
+        base_s, base_i = run(VARIANTS[0], X, Q, k, bias)
+        same, maxdiff = 1.0, 0.0
+        for v in VARIANTS[1:]:
+            sv, iv = run(v, X, Q, k, bias)
+            same = min(same, float((iv == base_i).float().mean()))
+            maxdiff = max(maxdiff, float((sv - base_s).abs().max()))
         torch.cuda.synchronize()
-        same = float(((il == ic) & (il == ip_)).float().mean())
-        maxdiff = float(torch.maximum((sl - sc).abs(), (sl - sp).abs()).max())
-        times = {"lane": [], "cand": [], "cand_p": []}
+        times = {v: [] for v in VARIANTS}
         for _ in range(5):
-            for p in ("lane", "cand", "cand_p"):
+            for p in VARIANTS:
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _ in range(3):

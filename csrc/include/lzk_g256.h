@@ -170,7 +170,9 @@ __device__ __forceinline__ void prologue(u16* smem, const Stager& st, int KS, co
 //   C[wr*128 + i*16 + 4*(lane>>4) + e][wc*64 + j*16 + (lane&15)]
 // and every wave has passed the final barrier with all of its DMA retired
 // (smem may be reused or re-staged).
-template <class Mma = MmaBf16>
+// OPT (schedule experiments, A/B in bench/ab_search.py): bit 0 = no
+// s_setprio around the MFMA clusters, bit 1 = no wave-group stagger.
+template <class Mma = MmaBf16, int OPT = 0>
 __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -200,7 +202,7 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
   if (KS > 1) vm2();
   else vm0();
   bar();
-  if (wr == 1) bar();
+  if (!(OPT & 2) && wr == 1) bar();
 
   bf16x8 a0[4][2], a1[4][2], b[2][2];
   for (int t = 0; t < KS; ++t) {
@@ -222,9 +224,9 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     }
     bar();
     lgkm0();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(1);
     Mma::template quad<0, 0>(acc, a0, b);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p1 ----
 #pragma unroll
@@ -234,9 +236,9 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     if (nxt) st.issue<3>(smem, buf ^ 1, t + 1);
     bar();
     lgkm0();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(1);
     Mma::template quad<1, 0>(acc, a1, b);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p2 ----
 #pragma unroll
@@ -245,9 +247,9 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
       for (int nb = 0; nb < 2; ++nb) b[nb][s] = *reinterpret_cast<const bf16x8*>(Bs + boff[1][nb][s]);
     bar();
     lgkm0();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(1);
     Mma::template quad<1, 1>(acc, a1, b);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p3 ----
     if (t + 2 < KS) {
@@ -257,12 +259,12 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
       vm0();
     }
     bar();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(1);
     Mma::template quad<0, 1>(acc, a0, b);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(0);
     bar();
   }
-  if (wr == 0) bar();
+  if (!(OPT & 2) && wr == 0) bar();
 }
 
 template <class Mma = MmaBf16>

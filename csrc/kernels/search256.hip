@@ -108,7 +108,7 @@ constexpr int CAND_P_LDS = LDS_BYTES + 2 * EPI_ARRAYS * 256 * 4;
 // this pair (global dedupe/links + within-shard links, reference
 // memory_system.py:719-733 / :816-836 / :853-889) and the scan is MFMA-bound,
 // so fusing halves its cost.
-template <bool HAS_BIAS, bool HAS_LABEL, bool DUAL>
+template <bool HAS_BIAS, bool HAS_LABEL, bool DUAL, int OPT = 0>
 __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     const u16* __restrict__ X, long ldx, int nrows, const u16* __restrict__ Qm, long ldq, int nq, int D,
     const float* __restrict__ bias, const int* __restrict__ row_label, const int* __restrict__ q_label,
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
   int par = 0;
   f32x4 acc[8][4];
   while (true) {
-    body(smem, st, KS, acc);
+    body<MmaBf16, OPT>(smem, st, KS, acc);
     const int cur = tile, cpar = par;
     tile += walk.step;
     const bool more = walk.valid(tile);
@@ -233,6 +233,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
 }
 
 int g_cand_persist = -1;
+int g_g256_opt = 0;  // schedule experiment selector (see lzk_g256.h body<OPT>)
 int g_n_cu = 0;
 
 template <int K>
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
 }  // namespace
 
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
+LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 
 // Candidate pass. cnt [nq] must be zeroed by the caller (same stream);
 // cs/ci are [nq, cap].
@@ -339,7 +341,20 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
     if (bias && row_label) LZK_GP(true, true);
     else if (bias) LZK_GP(true, false);
     else if (row_label) LZK_GP(false, true);
-    else LZK_GP(false, false);
+    else if (g_g256_opt > 0 && g_g256_opt < 4) {
+#define LZK_GX(O)                                                                                                   \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<false, false, false, O>,                     \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<false, false, false, O>), dim3(grid), dim3(NT), CAND_P_LDS, st, \
+                       x, ldx, nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap,    \
+                       cnt, cs, ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr);          \
+  } while (0)
+      if (g_g256_opt == 1) LZK_GX(1);
+      else if (g_g256_opt == 2) LZK_GX(2);
+      else LZK_GX(3);
+#undef LZK_GX
+    } else LZK_GP(false, false);
 #undef LZK_GP
     return (int)hipGetLastError();
   }
