@@ -161,3 +161,36 @@ def test_distributed_commit_is_one_version(tmp_path, monkeypatch):
     assert len(vs) == 1 and vs.pop() == v0.pop() + 1
     for o in out.values():
         assert o[2] == 2 + 3 + 4 and o[3] == ["u0", "u1", "u2"]
+
+
+def _eight_rank_pipeline(comm):
+    """The 8-GPU node's collective pattern on 8 CPU ranks: tenant placement,
+    all-to-all re-shard, cross-shard search merge and a multi-rank commit."""
+    from lazzaro_amd.ops.search import _ref_topk
+    from lazzaro_amd.parallel import ShardedIndex
+    from lazzaro_amd.parallel.placement import TenantDirectory
+    assert comm.world == 8
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(4001, 32, generator=g)
+    Q = torch.randn(13, 32, generator=g)
+    idx = ShardedIndex.partition(comm, X)
+    s, i = idx.search(Q, 5)
+    rs, ri = _ref_topk(X, Q, 5)
+    ok = bool(torch.allclose(s, rs, atol=1e-5) and torch.equal(i, ri))
+    # re-shard 100 rows per rank to pseudo-random owners
+    rows = torch.arange(100) + 1000 * comm.rank
+    dest = (rows * 7919) % comm.world
+    (got,) = comm.reshard(dest, rows.float())
+    ok = ok and bool(((got.long() * 7919) % comm.world == comm.rank).all())
+    total = comm.all_reduce(torch.tensor([got.numel()], dtype=torch.float64))
+    ok = ok and int(total.item()) == 800
+    d = TenantDirectory(comm)
+    for t in (f"user{i}" for i in range(200)):
+        if d.is_local(t):
+            d.register(t, 1)
+    ok = ok and len(d.all_tenants()) == 200
+    return ok
+
+
+def test_eight_ranks_gloo():
+    assert all(spawn(8, _eight_rank_pipeline).values())
