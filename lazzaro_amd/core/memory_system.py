@@ -344,10 +344,15 @@ class MemorySystem(ConsolidationMixin):
         self.conversation_history.append({"role": "user", "content": user_message})
         with tracer.stage("embed_query", self._device):
             q = self._get_embedding(user_message)
-        with tracer.stage("retrieve", self._device):
-            ids = self._optimized_retrieval(q, user_message)
-        with tracer.stage("boost", self._device):
-            self._boost_neighbors(ids)
+        # readers and the background consolidation writer serialise on the
+        # graph lock (the reference mutates the graph from two worker threads
+        # with no lock at all); the writer holds it only for
+        # the on-device ingest, never across the LLM call
+        with self._graph_lock:
+            with tracer.stage("retrieve", self._device):
+                ids = self._optimized_retrieval(q, user_message)
+            with tracer.stage("boost", self._device):
+                self._boost_neighbors(ids)
         return ids, (time.time() - t0) * 1000.0
 
     @staticmethod
@@ -367,7 +372,9 @@ class MemorySystem(ConsolidationMixin):
     def chat(self, user_message: str) -> str:
         ids, ms = self._retrieve_for(user_message)
         self.metrics["retrieval_times"].append(ms)
-        msgs = self._build_messages(ids)
+        with self._graph_lock:
+            msgs = self._build_messages(ids)
+            node_lines = self._node_lines(ids)
         with tracer.stage("llm", "cpu"):
             response = self._call_llm(msgs)
         self.add_to_short_term(response, "semantic", salience=0.5)
@@ -375,18 +382,20 @@ class MemorySystem(ConsolidationMixin):
         self._say(self._timing_line(ms, len(ids)))
         if ids:
             self._say("   Retrieved Nodes:")
-            for line in self._node_lines(ids):
+            for line in node_lines:
                 self._say(line)
         return response
 
     def chat_stream(self, user_message: str):
         ids, ms = self._retrieve_for(user_message)
+        with self._graph_lock:
+            node_lines = self._node_lines(ids)
+            msgs = self._build_messages(ids)
         yield {"type": "info", "content": self._timing_line(ms, len(ids))}
         if ids:
             yield {"type": "info", "content": "   Retrieved Nodes:"}
-            for line in self._node_lines(ids):
+            for line in node_lines:
                 yield {"type": "info", "content": line}
-        msgs = self._build_messages(ids)
         if hasattr(self.llm, "completion_stream"):
             full = ""
             for chunk in self.llm.completion_stream(msgs):
@@ -416,9 +425,13 @@ class MemorySystem(ConsolidationMixin):
 
     # ------------------------------------------------------------ queries
     def get_connected_memories(self, node_id: str) -> List[Node]:
+        with self._graph_lock:
+            return self._connected(node_id)
+
+    def _connected(self, node_id: str) -> List[Node]:
         ids = []
         seen = set()
-        for sh in self.shards.values():
+        for sh in list(self.shards.values()):
             for s, t in sh.edges.incident(node_id):
                 o = t if s == node_id else s
                 if o not in seen:
@@ -431,16 +444,22 @@ class MemorySystem(ConsolidationMixin):
             q = self._get_embedding(query)
         with tracer.stage("search", self._device):
             ids = self.vector_store.search_nodes(q, user_id=self.user_id, limit=limit)
-        return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
+        with self._graph_lock:
+            return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
 
     def search_memories_batch(self, queries: List[str], limit: int = 5) -> List[List[Node]]:
         """Batched search: one embedding call and one fused top-k launch."""
         embs = self._batch_embed(list(queries))
         res = self._search_batch(embs, limit)
-        return [[n for n in (self.buffer.get_node(i) for i in ids) if n is not None] for ids in res]
+        with self._graph_lock:
+            return [[n for n in (self.buffer.get_node(i) for i in ids) if n is not None] for ids in res]
 
     # ------------------------------------------------------------ stats / display
     def get_stats(self) -> Dict:
+        with self._graph_lock:
+            return self._stats()
+
+    def _stats(self) -> Dict:
         nodes, edges = self.buffer.size()
         rt = self.metrics["retrieval_times"]
         ct = self.metrics["consolidation_times"]
@@ -702,6 +721,10 @@ STORAGE:
 
     # ------------------------------------------------------------ export
     def export_observations(self, format: str = "markdown") -> str:
+        with self._graph_lock:
+            return self._export(format)
+
+    def _export(self, format: str) -> str:
         nodes = [n for sh in self.shards.values() for n in sh.nodes.values() if not n.is_super_node]
         nodes.sort(key=lambda n: (n.salience, n.last_accessed), reverse=True)
         if format == "json":

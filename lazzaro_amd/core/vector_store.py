@@ -162,17 +162,19 @@ class HBMStore:
     def search_nodes(self, query_emb, user_id: str = "default", limit: int = 5) -> List[str]:
         if query_emb is None or len(query_emb) == 0:
             return []
-        a = self._arena(user_id)
-        if len(a) == 0 or a.dim != len(query_emb):
-            return []
-        return a.search(query_emb, int(limit), self.metric)[0]
+        with self._lock:  # writers (add/delete/replace) mutate the arena in place
+            a = self._arena(user_id)
+            if len(a) == 0 or a.dim != len(query_emb):
+                return []
+            return a.search(query_emb, int(limit), self.metric)[0]
 
     def search_nodes_batch(self, query_embs, user_id: str = "default", limit: int = 5) -> List[List[str]]:
         """Batched variant (one kernel launch for all queries)."""
-        a = self._arena(user_id)
-        if len(a) == 0 or len(query_embs) == 0:
-            return [[] for _ in range(len(query_embs))]
-        return a.search(query_embs, int(limit), self.metric)
+        with self._lock:
+            a = self._arena(user_id)
+            if len(a) == 0 or len(query_embs) == 0:
+                return [[] for _ in range(len(query_embs))]
+            return a.search(query_embs, int(limit), self.metric)
 
     def search_nodes_multi(self, query_embs, user_ids: Sequence[str], limit: int = 5) -> List[List[str]]:
         """Multi-tenant batch: query i searches tenant ``user_ids[i]`` only, all
@@ -180,6 +182,11 @@ class HBMStore:
         from ..index.arena import multi_arena_search
         if len(user_ids) == 0:
             return []
+        with self._lock:
+            return self._search_multi(query_embs, user_ids, limit)
+
+    def _search_multi(self, query_embs, user_ids, limit):
+        from ..index.arena import multi_arena_search
         arenas = [self._arena(u) for u in user_ids]
         dims = {a.dim for a in arenas if len(a)}
         if len(dims) > 1 or any(a.dim is not None and len(a) and a.dim != len(query_embs[0]) for a in arenas):

@@ -227,3 +227,38 @@ def test_config_and_tracing(monkeypatch):
     finally:
         tracer.enable(False)
     ms.close()
+
+
+def test_concurrent_chat_and_background_consolidation():
+    """Readers (chat/search) and the async consolidation writer share the
+    graph under the graph lock: no torn reads, no lost memories."""
+    import threading
+
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(), enable_async=True,
+                      load_from_disk=False, max_buffer_size=1000, consolidate_every=1000)
+    errors = []
+    stop = threading.Event()
+
+    def reader():
+        try:
+            while not stop.is_set():
+                ms.search_memories("hobby music city")
+                ms.get_stats()
+        except Exception as e:  # pragma: no cover - the failure we guard against
+            import traceback
+            errors.append("".join(traceback.format_exception(e)))
+
+    t = threading.Thread(target=reader)
+    t.start()
+    try:
+        for i in range(12):
+            ms.start_conversation()
+            ms.chat(f"I moved to city number {i} and I love music genre {i}.")
+            ms.end_conversation()
+    finally:
+        ms.flush()
+        stop.set()
+        t.join()
+    assert not errors, errors
+    assert ms.consolidation_queue == [] and ms.buffer.size()[0] >= 12
+    ms.close()
