@@ -45,10 +45,11 @@ class MemoryConfig:
     merge_mode: str = "reference"         # reference | pairwise
     embed_model: Optional[str] = None     # on-device encoder: minilm-l6 | bge-base | e5-large
     embed_weights: Optional[str] = None   # safetensors path (HF BERT layout)
-    index: str = "flat"                   # flat | ivfpq (DeviceGraph / bench paths)
+    index: str = "flat"                   # flat | ivfpq (store: IVF-PQ for tenants >= ivf_min_rows)
     nlist: int = 4096
     nprobe: int = 32
     pq_m: int = 64
+    ivf_min_rows: int = 1_000_000
     verbose: bool = False
     extra: Dict[str, Any] = field(default_factory=dict)
 

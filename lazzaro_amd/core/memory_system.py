@@ -92,6 +92,8 @@ class MemorySystem(ConsolidationMixin):
         verbose: bool = False,
         strict_errors: bool = False,
         max_consolidation_retries: int = 3,
+        index: str = "flat",
+        index_params: Optional[Dict] = None,
     ):
         self.model = model
         self.user_id = user_id
@@ -114,7 +116,8 @@ class MemorySystem(ConsolidationMixin):
         self.super_nodes: Dict[str, Node] = {}
         self.buffer = BufferGraph(self.shards, self.super_nodes)
         self.profile = Profile()
-        self.store = store if store is not None else HBMStore(db_dir=db_dir, device=device, metric=metric)
+        self.store = store if store is not None else HBMStore(db_dir=db_dir, device=device, metric=metric,
+                                                              index=index, **(index_params or {}))
         self.vector_store = self.store
         self._device = getattr(self.store, "device", None)
         if isinstance(self._device, str):
@@ -169,6 +172,9 @@ class MemorySystem(ConsolidationMixin):
         if emb is None and cfg.embed_model:
             from .embedders import OnDeviceEmbedder
             emb = OnDeviceEmbedder(cfg.embed_model, device=cfg.device, weights=cfg.embed_weights)
+        kw.setdefault("index", cfg.index)
+        kw.setdefault("index_params", {"nlist": cfg.nlist, "nprobe": cfg.nprobe, "pq_m": cfg.pq_m,
+                                       "ivf_min_rows": cfg.ivf_min_rows})
         return cls(**cfg.reference_kwargs(), embedding_provider=emb, device=cfg.device, metric=cfg.metric,
                    merge_mode=cfg.merge_mode, verbose=cfg.verbose, **kw)
 

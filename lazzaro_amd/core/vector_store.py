@@ -46,7 +46,13 @@ def _unjson(v, default):
 
 class HBMStore:
     def __init__(self, db_dir: str = "db", device=None, metric: str = "l2",
-                 consistency_interval: float = 0.5, keep_fp32: bool = True):
+                 consistency_interval: float = 0.5, keep_fp32: bool = True, index: str = "flat",
+                 nlist: int = 4096, nprobe: int = 32, pq_m: int = 64, ivf_min_rows: int = 1_000_000):
+        """index="ivfpq": a tenant arena with >= ivf_min_rows live rows is served
+        by IVF-PQ candidates re-ranked exactly (smaller tenants stay exact flat)."""
+        if index not in ("flat", "ivfpq"):
+            raise ValueError("index must be 'flat' or 'ivfpq'")
+        self.index, self.ivf_params = index, dict(nlist=nlist, nprobe=nprobe, m=pq_m, min_rows=ivf_min_rows)
         self.db_dir = db_dir
         self._uri = os.path.join(db_dir, "lancedb")
         os.makedirs(self._uri, exist_ok=True)
@@ -85,6 +91,8 @@ class HBMStore:
                 return a
             cols = self._nodes_table.scan_columns([("user_id", user_id)], want=["id", "vector"])
             a = VectorArena(device=self.device, keep_fp32=self.keep_fp32)
+            if self.index == "ivfpq":
+                a.enable_ivf(**self.ivf_params)
             ids = cols.get("id", [])
             if len(ids):
                 vec = cols["vector"]

@@ -83,6 +83,8 @@ class VectorArena:
         self.X = self.X32 = self.sqn = self.bias = None
         self._init_cap = capacity
         self.version = 0  # bumps on every mutation (cache invalidation)
+        self.layout_epoch = 0  # bumps when row indices change (clear / compact)
+        self.ivf: Optional["ArenaIVF"] = None
 
     # ------------------------------------------------------------------ alloc
     def _alloc(self, cap: int) -> None:
@@ -156,6 +158,7 @@ class VectorArena:
         if self.bias is not None:
             self.bias.fill_(NEG_INF)
         self.version += 1
+        self.layout_epoch += 1
 
     def compact(self) -> None:
         live = [r for r in range(self.n) if self.ids[r] is not None]
@@ -173,6 +176,7 @@ class VectorArena:
             self.rows_of.setdefault(i, []).append(r)
         self.n, self.n_dead = m, 0
         self.version += 1
+        self.layout_epoch += 1
 
     def __len__(self) -> int:
         return self.n - self.n_dead
@@ -194,6 +198,8 @@ class VectorArena:
         if self.n == 0 or len(self) == 0:
             return (torch.full((nq, k), NEG_INF, device=self.device),
                     torch.full((nq, k), -1, dtype=torch.long, device=self.device))
+        if self.ivf is not None and len(self) >= self.ivf.min_rows:
+            return self.ivf.search(qf, k, metric)
         n = self.n
         if metric == "cosine":
             qn = qf / qf.norm(dim=1, keepdim=True).clamp_min(1e-30)
@@ -263,6 +269,29 @@ class VectorArena:
         o = torch.argsort(-s, dim=1, stable=True)[:, :k]
         return torch.gather(s, 1, o), torch.gather(r, 1, o)
 
+    def enable_ivf(self, nlist: int = 4096, m: int = 64, nprobe: int = 32, min_rows: int = 1_000_000,
+                   candidates: int = 256) -> None:
+        """Serve this arena's searches from an IVF-PQ index once it holds
+        ``min_rows`` live rows (BASELINE config 5: tenants too large for an
+        exhaustive scan per query). Candidates come from the PQ scan kernel,
+        the final top-k is re-ranked EXACTLY on the arena's rows."""
+        self.ivf = ArenaIVF(self, nlist, m, nprobe, min_rows, candidates)
+
+    def _metric_scores(self, qn: torch.Tensor, rows: torch.Tensor, metric: str) -> torch.Tensor:
+        """Exact scores of candidate ``rows`` [nq, c] (-1 = none) for queries qn."""
+        valid = rows >= 0
+        rr = rows.clamp_min(0)
+        xs = self.X32[rr] if self.X32 is not None else self.X[rr, : self.dim].float()
+        dot = torch.einsum("qd,qkd->qk", qn, xs)
+        if metric == "l2":
+            s = 2.0 * dot - self.sqn[rr] - (qn * qn).sum(1, keepdim=True)
+        elif metric == "cosine":
+            s = dot / self.sqn[rr].sqrt().clamp_min(1e-30)
+        else:
+            s = dot
+        s = s + self.bias[rr]
+        return torch.where(valid, s, torch.full_like(s, NEG_INF))
+
     def segment(self, metric: str = "l2"):
         """(rows, bias, scale) describing this arena for the multi-tenant
         segment kernel: exact fp32 rows when kept (no re-rank needed), the
@@ -304,6 +333,66 @@ class VectorArena:
         if self.X32 is not None:
             return self.X32[t]
         return self.X[t, : self.dim].float()
+
+
+class ArenaIVF:
+    """IVF-PQ acceleration attached to one :class:`VectorArena`.
+
+    Row indices of the arena are the index ids, so the PQ candidates are
+    re-ranked exactly against the arena's rows (fp32 copy when kept) with the
+    arena's metric and tombstones. Appends are encoded incrementally; a clear
+    or compaction (row indices change) triggers a rebuild on the next search.
+    """
+
+    def __init__(self, arena: VectorArena, nlist: int, m: int, nprobe: int, min_rows: int, candidates: int):
+        self.arena, self.nlist, self.m, self.nprobe = arena, nlist, m, nprobe
+        self.min_rows, self.candidates = min_rows, candidates
+        self.idx = None
+        self.epoch = -1
+        self.covered = 0
+
+    def _rows(self, r0: int, r1: int) -> torch.Tensor:
+        a = self.arena
+        return a.X32[r0:r1] if a.X32 is not None else a.X[r0:r1, : a.dim].float()
+
+    def sync(self) -> None:
+        from .ivfpq import IVFPQIndex
+        a = self.arena
+        if self.idx is None or self.epoch != a.layout_epoch or a.n < self.covered:
+            m = self.m if a.dim % self.m == 0 else next(d for d in (64, 48, 32, 16, 8, 4, 2, 1) if a.dim % d == 0)
+            nlist = max(16, min(self.nlist, len(a) // 64))
+            self.idx = IVFPQIndex(a.dim, nlist=nlist, m=m, device=a.device)
+            live = torch.nonzero(torch.isfinite(a.bias[: a.n])).flatten()
+            g = torch.Generator(device="cpu").manual_seed(0)
+            pick = live[torch.randperm(live.numel(), generator=g)[: min(live.numel(), 262144)].to(live.device)]
+            self.idx.train(self._rows(0, a.n)[pick], iters=8, pq_iters=8)
+            self.covered = 0
+            self.epoch = a.layout_epoch
+        step = 1 << 20
+        while self.covered < a.n:
+            r1 = min(a.n, self.covered + step)
+            self.idx.add(self._rows(self.covered, r1), ids=torch.arange(self.covered, r1))
+            self.covered = r1
+
+    def search(self, qf: torch.Tensor, k: int, metric: str):
+        self.sync()
+        a = self.arena
+        qn = qf / qf.norm(dim=1, keepdim=True).clamp_min(1e-30) if metric == "cosine" else qf
+        kc = max(self.candidates, 4 * k)
+        _, rows = self.idx.search(qf, kc, nprobe=self.nprobe)
+        s = a._metric_scores(qn, rows.to(a.device), metric)
+        vs, o = _stable_topk_rows(s, rows.to(a.device), k)
+        return vs, o
+
+
+def _stable_topk_rows(s: torch.Tensor, rows: torch.Tensor, k: int):
+    """Top-k of candidate scores ordered (score desc, row asc)."""
+    key = torch.where(rows >= 0, rows, torch.full_like(rows, 1 << 62))
+    o = torch.argsort(key, dim=1, stable=True)
+    s, rows = torch.gather(s, 1, o), torch.gather(rows, 1, o)
+    vs, j = _stable_topk(s, k)
+    r = torch.where(j >= 0, torch.gather(rows, 1, j.clamp_min(0)), j)
+    return vs, r
 
 
 def _stable_topk(s: torch.Tensor, k: int):

@@ -185,3 +185,20 @@ def test_debug_build_catches_bad_index():
     torch.cuda.synchronize()
     assert rc == 0 and L.lzk_graph_debug_errors() > 0
     assert L.lzk_graph_debug_errors() == 0  # read-and-clear
+
+
+def test_store_ivfpq_tenant_gpu(tmp_path):
+    import numpy as np
+
+    from lazzaro_amd.core.vector_store import HBMStore
+    st = HBMStore(db_dir=str(tmp_path), device="cuda", metric="cosine", index="ivfpq", nlist=256, nprobe=16,
+                  pq_m=32, ivf_min_rows=50_000)
+    rng = np.random.default_rng(0)
+    c = rng.standard_normal((500, 256)).astype(np.float32)
+    x = c[rng.integers(0, 500, 120_000)] + 0.5 * rng.standard_normal((120_000, 256)).astype(np.float32) / 16
+    a = st._arena("big")
+    a.add([f"m{i}" for i in range(len(x))], x)
+    q = x[:64] + 0.01 * rng.standard_normal((64, 256)).astype(np.float32)
+    got = st.search_nodes_batch(q, user_id="big", limit=5)
+    assert a.ivf.idx is not None
+    assert sum(g[0] == f"m{i}" for i, g in enumerate(got)) >= 60

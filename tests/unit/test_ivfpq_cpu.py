@@ -54,3 +54,25 @@ def test_ivfpq_fp8_rerank_copy():
     truth = torch.topk(q @ x.T, 10, dim=1).indices
     _, ids = idx.search(q, 10, nprobe=16, rerank=32)
     assert recall_at_k(ids, truth) > 0.8
+
+
+def test_store_ivfpq_tenant_matches_flat_top1(tmp_path):
+    """HBMStore(index="ivfpq"): a tenant above the row threshold is served by
+    IVF-PQ candidates + exact re-rank; near-duplicate queries find their row."""
+    import numpy as np
+
+    from lazzaro_amd.core.vector_store import HBMStore
+    st = HBMStore(db_dir=str(tmp_path / "ivf"), device="cpu", metric="cosine", index="ivfpq",
+                  nlist=32, nprobe=8, pq_m=8, ivf_min_rows=1000)
+    flat = HBMStore(db_dir=str(tmp_path / "flat"), device="cpu", metric="cosine")
+    x = _data(3000, 32, 9).numpy()
+    rows = [{"id": f"m{i}", "content": "c", "embedding": v.tolist()} for i, v in enumerate(x)]
+    st.add_nodes(rows, user_id="big")
+    flat.add_nodes(rows, user_id="big")
+    q = x[:40] + 0.01 * np.random.default_rng(0).standard_normal((40, 32)).astype(np.float32)
+    got = [st.search_nodes(v.tolist(), user_id="big", limit=3) for v in q]
+    want = [flat.search_nodes(v.tolist(), user_id="big", limit=3) for v in q]
+    assert st._arena("big").ivf is not None and st._arena("big").ivf.idx is not None
+    assert sum(g[0] == w[0] for g, w in zip(got, want)) >= 38
+    st.delete_nodes(["m0"], user_id="big")
+    assert "m0" not in st.search_nodes(q[0].tolist(), user_id="big", limit=3)
