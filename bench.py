@@ -116,7 +116,7 @@ def main():
 
     def step(i):
         ids, lens = pending.pop(i) if i in pending else tokenize(i)
-        _, q16 = emb.encoder.forward(ids, lens, pad_to=a.dim)
+        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=2)
         pending[i + 1] = tokenize(i + 1)
         s, r = flat_topk(X, q16, a.k)
         if world > 1:
@@ -152,7 +152,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(3):
-        _, q16 = emb.encoder.forward(ids, lens, pad_to=a.dim)
+        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=2)
     torch.cuda.synchronize()
     t_embed = (time.perf_counter() - t1) / 3
     t1 = time.perf_counter()

@@ -73,6 +73,8 @@ class OnDeviceEmbedder:
                 if g is None:
                     g = self._graphs[key] = GraphedEncoder(self.encoder, bb, sb, pad_to)
                 return g(ids, lens)
+        if B >= 512:  # large batches: two sub-batches on two streams fill each GEMM's tail
+            return self.encoder.forward_streams(ids, lens, pad_to=pad_to, parts=2)
         return self.encoder.forward(ids, lens, pad_to=pad_to)
 
     def embed(self, text: str) -> List[float]:

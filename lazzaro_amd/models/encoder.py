@@ -215,6 +215,34 @@ class SentenceEncoder:
             x = E.layernorm(self._lin(hdn, i, "w2", "b2", residual=x), p[f"{i}.ln2_g"], p[f"{i}.ln2_b"], c.eps)
         return E.pool_norm(x, lens, B, S, c.pooling, pad_to, cu=cu)
 
+    def forward_streams(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0, parts: int = 2):
+        """Split the batch into ``parts`` independent sub-batches and run them on
+        separate HIP streams. Every layer is a chain of dependent kernels whose
+        last wave of 256x256 tiles leaves most CUs idle; kernels of the other
+        sub-batch fill those CUs, so the chip stays busy through each tail."""
+        B = ids.shape[0]
+        if parts <= 1 or self.device.type != "cuda" or B < 2 * parts:
+            return self.forward(ids, lens, pad_to=pad_to)
+        cur = torch.cuda.current_stream(self.device)
+        if not hasattr(self, "_streams") or len(self._streams) < parts:
+            self._streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
+        bounds = [B * i // parts for i in range(parts + 1)]
+        outs = []
+        for i in range(parts):
+            st = self._streams[i]
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                o32, o16 = self.forward(ids[bounds[i]:bounds[i + 1]], lens[bounds[i]:bounds[i + 1]], pad_to=pad_to)
+                outs.append((o32, o16))
+        for i in range(parts):
+            cur.wait_stream(self._streams[i])
+            for t in outs[i]:
+                if t is not None:
+                    t.record_stream(cur)
+        o32 = torch.cat([o[0] for o in outs])
+        o16 = torch.cat([o[1] for o in outs]) if outs[0][1] is not None else None
+        return o32, o16
+
     def flops(self, tokens: int) -> float:
         c = self.cfg
         per_tok = 2 * (3 * c.hidden * c.hidden + c.hidden * c.hidden + 2 * c.hidden * c.ffn) * c.layers
