@@ -55,6 +55,16 @@ def main():
         for tile, v in ts.items():
             m = statistics.median(v)
             out[name][str(tile)] = {"us": round(m * 1e6, 1), "tflops": round(flop / m / 1e12, 1)}
+        # main loop only (epilogue skipped; measurement probe, act=9)
+        if N >= 1024:
+            L.lzk_set_gemm_tile(256)
+            y9 = torch.empty((T, N), dtype=torch.bfloat16, device=dev)
+
+            def probe():
+                L.lzk_gemm_bias_act(x.data_ptr(), x.stride(0), T, w.data_ptr(), w.stride(0), N, b.data_ptr(), None,
+                                    0, y9.data_ptr(), y9.stride(0), K, 9, _lib.stream_ptr(x.device))
+            tp = statistics.median(timeit(probe) for _ in range(5))
+            out[name]["256_mainloop_only_us"] = round(tp * 1e6, 1)
         # fp8 e4m3 (K % 128 == 0): GEMM alone and with the activation quantisation pass
         xq, sx = E.quantize_fp8_rows(x)
         wq, sw = E.quantize_fp8_rows(w)

@@ -112,6 +112,15 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  if (ACT == 9) {  // measurement probe (act=9): main loop only, epilogue cost = difference
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z += acc[i][j][0];
+    if (z != z) Y[threadIdx.x] = 0;
+    return;
+  }
   // pass 1: registers -> LDS image [token][feature] (all DMA retired, every
   // wave past the main loop's last barrier)
 #pragma unroll
@@ -638,7 +647,8 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     hipLaunchKernelGGL((gemm256_bias_act_kernel<A, RS>), grid, block, G256_GEMM_LDS, st, x, ldx, T, w, ldw, \
                        N, bias, r, ldr, y, ldy, K, n_ft);                                                     \
   } while (0)
-      if (act == 1) { if (r) GO(1, true); else GO(1, false); }
+      if (act == 9) GO(9, false);
+      else if (act == 1) { if (r) GO(1, true); else GO(1, false); }
       else { if (r) GO(0, true); else GO(0, false); }
 #undef GO
       return (int)hipGetLastError();
