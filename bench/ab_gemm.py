@@ -65,6 +65,12 @@ def main():
                                     0, y9.data_ptr(), y9.stride(0), K, 9, _lib.stream_ptr(x.device))
             tp = statistics.median(timeit(probe) for _ in range(5))
             out[name]["256_mainloop_only_us"] = round(tp * 1e6, 1)
+
+            def probe_nostore():
+                L.lzk_gemm_bias_act(x.data_ptr(), x.stride(0), T, w.data_ptr(), w.stride(0), N, b.data_ptr(), None,
+                                    0, y9.data_ptr(), y9.stride(0), K, 10, _lib.stream_ptr(x.device))
+            tn = statistics.median(timeit(probe_nostore) for _ in range(5))
+            out[name]["256_no_global_store_us"] = round(tn * 1e6, 1)
         # fp8 e4m3 (K % 128 == 0): GEMM alone and with the activation quantisation pass
         xq, sx = E.quantize_fp8_rows(x)
         wq, sw = E.quantize_fp8_rows(w)

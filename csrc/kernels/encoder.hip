@@ -37,6 +37,22 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f));
 }
 
+// Two lanes of work per instruction: the polynomial and the scaling run as
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32), only v_rcp / v_exp stay scalar
+// -- ~10 VALU ops per element instead of ~18.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 a = __builtin_elementwise_abs(z);
+  const f32x2 d = 1.f + 0.3275911f * a;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const f32x2 p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const f32x2 e = -a * a * 1.4426950408889634f;
+  const f32x2 ex = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  const f32x2 erf = __builtin_elementwise_copysign(1.f - p * ex, z);
+  return 0.5f * x * (1.f + erf);
+}
+
 // ---------------------------------------------------------------- GEMM
 template <int ACT, bool RES, bool GLDS>
 __global__ __launch_bounds__(TNT, 2) void gemm_bias_act_kernel(
@@ -105,13 +121,22 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   const int logical = xcd_remap(blockIdx.x, gridDim.x);
   const int tt = logical / n_ft, ft = logical % n_ft;
   const int n0 = ft * g256::BM, t0 = tt * g256::BN;
-  g256::Stager st;
-  st.setup(W, ldw, n0, N, X, ldx, t0, T);
-  f32x4 acc[8][4];
-  g256::mainloop(smem, st, K / g256::BK, acc);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  float* sbias = reinterpret_cast<float*>(smem + g256::LDS_BYTES / 2);  // 1 KiB past the staging slots
+  g256::Stager st;
+  st.setup(W, ldw, n0, N, X, ldx, t0, T);
+  const int KS = K / g256::BK;
+  // the tile's 256 bias values ride along with the prologue DMA (no global
+  // load latency in the epilogue)
+  g256::prologue(smem, st, KS, [&]() {
+    if (wave < 4)
+      __builtin_amdgcn_global_load_lds((g256::gbl_void_t*)(bias + min(n0 + wave * 64 + lane, N - 1)),
+                                       (g256::lds_void_t*)(sbias + wave * 64), 4, 0, 0);
+  });
+  f32x4 acc[8][4];
+  g256::body(smem, st, KS, acc);
   if (ACT == 9) {  // measurement probe (act=9): main loop only, epilogue cost = difference
     float z = 0.f;
 #pragma unroll
@@ -121,43 +146,58 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
     if (z != z) Y[threadIdx.x] = 0;
     return;
   }
-  // pass 1: registers -> LDS image [token][feature] (all DMA retired, every
-  // wave past the main loop's last barrier)
+  f32x4 bv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bv[i] = *reinterpret_cast<const f32x4*>(sbias + wr * 128 + i * 16 + 4 * (lane >> 4));
+  __syncthreads();  // the output image below overwrites the bias slot
+  // pass 1: registers -> LDS image [token][feature] (bias + activation + one
+  // v_cvt_pk_bf16_f32 per pair; 520-B rows keep the 8-B writes conflict-free)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int nl = wr * 128 + i * 16 + 4 * (lane >> 4);
-    const int n = min(n0 + nl, N - 4);
-    const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + n);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int tl = wc * 64 + j * 16 + (lane & 15);
       u16x4 o;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float v = acc[i][j][u] + bv[u];
-        if (ACT == 1) v = gelu_erf(v);
-        o[u] = f32_to_bf16(v);
+      f32x2 v0 = {acc[i][j][0] + bv[i][0], acc[i][j][1] + bv[i][1]};
+      f32x2 v1 = {acc[i][j][2] + bv[i][2], acc[i][j][3] + bv[i][3]};
+      if (ACT == 1) {
+        v0 = gelu_erf2(v0);
+        v1 = gelu_erf2(v1);
       }
+      o[0] = f32_to_bf16(v0.x);
+      o[1] = f32_to_bf16(v0.y);
+      o[2] = f32_to_bf16(v1.x);
+      o[3] = f32_to_bf16(v1.y);
       *reinterpret_cast<u16x4*>(smem + tl * G256_OUT_LD + nl) = o;
     }
   }
   __syncthreads();
-  // pass 2: one wave per token row, 4 features per lane
-  const int nl = lane * 4;
+  // pass 2: each wave streams 32 token rows, two rows per instruction (lanes
+  // 0-31 / 32-63), 8 features = 16 B per lane: whole cache lines out
+  const int half = lane >> 5;
+  const int nl = (lane & 31) * 8;
   const int n = n0 + nl;
   if (n < N) {
-#pragma unroll 8
-    for (int rr = 0; rr < g256::BN / 8; ++rr) {
-      const int tl = wave * (g256::BN / 8) + rr;
+#pragma unroll 4
+    for (int rr = 0; rr < g256::BN / 16; ++rr) {
+      const int tl = wave * (g256::BN / 8) + 2 * rr + half;
       const int t = t0 + tl;
       if (t >= T) break;
-      u16x4 o = *reinterpret_cast<const u16x4*>(smem + tl * G256_OUT_LD + nl);
+      const u16* src = smem + tl * G256_OUT_LD + nl;
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(src);
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(src + 4);
+      u16x8 o = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (RES) {
-        const u16x4 rv = *reinterpret_cast<const u16x4*>(R + (long)t * ldr + n);
+        const u16x8 rv = *reinterpret_cast<const u16x8*>(R + (long)t * ldr + n);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16(bf16_to_f32(o[u]) + bf16_to_f32(rv[u]));
+        for (int u = 0; u < 8; ++u) o[u] = f32_to_bf16(bf16_to_f32(o[u]) + bf16_to_f32(rv[u]));
       }
-      *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
+      if (ACT == 10) {  // measurement probe: everything but the global store
+        if (o[0] == 0x7fc1 && o[1] == 0x7fc1) Y[t] = 0;
+        continue;
+      }
+      *reinterpret_cast<u16x8*>(Y + (long)t * ldy + n) = o;
     }
   }
 }
@@ -634,7 +674,8 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
     // measured (bench/ab_gemm.py): at N = 768 the 1.5-wave quantisation of 3 feature tiles
     // loses to the 128x128 kernel; from N = 1024 on the 256x256 pipeline wins
-    if (g_gemm_tile == 256 && n_ft * n_tt >= 256 && N >= 1024 && N % 4 == 0) {
+    if (g_gemm_tile == 256 && n_ft * n_tt >= 256 && N >= 1024 && N % 8 == 0 && ldy % 8 == 0 &&
+        (!R || ldr % 8 == 0)) {
       const u16* x = (const u16*)X;
       const u16* w = (const u16*)W;
       const u16* r = (const u16*)R;
@@ -648,6 +689,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
                        N, bias, r, ldr, y, ldy, K, n_ft);                                                     \
   } while (0)
       if (act == 9) GO(9, false);
+      else if (act == 10) GO(10, false);
       else if (act == 1) { if (r) GO(1, true); else GO(1, false); }
       else { if (r) GO(0, true); else GO(0, false); }
 #undef GO
