@@ -53,11 +53,11 @@ def main():
             for r0 in range(0, n, 1 << 20):
                 bias[r0:r0 + (1 << 20)] = -(X[r0:r0 + (1 << 20)].float() ** 2).sum(1)
         base_s, base_i = run(VARIANTS[0], X, Q, k, bias)
-        same, maxdiff = 1.0, 0.0
+        same, maxdiff = {}, {}
         for v in VARIANTS[1:]:
             sv, iv = run(v, X, Q, k, bias)
-            same = min(same, float((iv == base_i).float().mean()))
-            maxdiff = max(maxdiff, float((sv - base_s).abs().max()))
+            same[v] = float((iv == base_i).float().mean())
+            maxdiff[v] = float((sv - base_s).abs().max())
         torch.cuda.synchronize()
         times = {v: [] for v in VARIANTS}
         for _ in range(5):

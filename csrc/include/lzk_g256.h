@@ -156,14 +156,157 @@ struct NoExtra {
 // buffer 0, then `extra()` (small per-tile epilogue operands a caller stages
 // into spare LDS), then HA0 of K-tile 1. Every slot must be free (no wave
 // still reading it): call it at kernel start or after body() returned.
-template <class Extra = NoExtra>
+// Cross-tile prefetch for persistent callers (KS even): the next tile's
+// K-tiles 0 and 1 are staged as if they were K-tiles KS and KS+1 of the
+// current loop (same buffer parity, same slots, same issue points), so the
+// next tile's pipeline fill overlaps this tile's last K-tiles and epilogue
+// instead of following them; extra() goes right after the next K-tile 0.
+// The loop then returns with exactly the DMAs prologue() would have left in
+// flight (next K-tile 1's A half-tile(s), youngest), so the next body starts
+// with the same counted wait. Without prefetch (NoPrefetch, or on() false)
+// the loop drains to vmcnt(0) and the caller runs prologue(). on() must be
+// false when KS is odd (the next K-tile 0 would land in buffer 1).
+struct NoPrefetch {
+  static constexpr bool kAny = false;
+  __device__ __forceinline__ bool on() const { return false; }
+  template <int H>
+  __device__ __forceinline__ void issue(u16*, int, int) const {}
+  __device__ __forceinline__ void extra() const {}
+};
+
+// The next tile's operands as wave-uniform scalars: its per-lane source
+// addresses are rebuilt at each issue (a few VALU in a read section) instead
+// of holding a second Stager's 18 VGPRs through the main loop.
+template <class Extra>
+struct NextTile {
+  static constexpr bool kAny = true;
+  const u16* A;
+  long lda;
+  int a0, na;
+  const u16* B;
+  long ldb;
+  int b0, nb;
+  const Extra* ex;
+  bool enabled;
+  __device__ __forceinline__ bool on() const { return enabled; }
+  template <int H>
+  __device__ __forceinline__ void issue(u16* smem, int buf, int kt) const {
+    Stager s;
+    s.setup(A, lda, a0, na, B, ldb, b0, nb);
+    s.issue<H>(smem, buf, kt);
+  }
+  __device__ __forceinline__ void extra() const { (*ex)(); }
+};
+
+// K-tile kt of the current tile, or (kt >= KS, prefetch on) K-tile kt-KS of the next.
+template <int H, class Pre>
+__device__ __forceinline__ void stage(u16* smem, const Stager& st, const Pre& pre, int buf, int kt, int KS) {
+  if (kt < KS) st.issue<H>(smem, buf, kt);
+  else if (Pre::kAny && pre.on()) pre.template issue<H>(smem, buf, kt - KS);
+}
+
+template <class Extra = NoExtra, int OPT = 0>
 __device__ __forceinline__ void prologue(u16* smem, const Stager& st, int KS, const Extra& extra = Extra()) {
   st.issue<0>(smem, 0, 0);
   st.issue<1>(smem, 0, 0);
   st.issue<2>(smem, 0, 0);
   st.issue<3>(smem, 0, 0);
   extra();
-  if (KS > 1) st.issue<0>(smem, 1, 1);
+  if (KS > 1) {
+    st.issue<0>(smem, 1, 1);
+    if constexpr ((OPT & 8) != 0) st.issue<1>(smem, 1, 1);  // two-phase body: both A halves of tile 1
+  }
+}
+
+// Two-phase K loop (OPT bit 3): the same 64 MFMAs per wave and K-tile as
+// body() below in two 32-MFMA phases, i.e. half the barriers per K-tile.
+//   P0: read a0, a1, b(cols 0-31);  issue HB0, HB1 of t+1   | MFMA (A0,B0) (A1,B0)
+//   P1: read b(cols 32-63);         issue HA0, HA1 of t+2   | MFMA (A1,B1) (A0,B1)
+//       then s_waitcnt vmcnt(4): everything but A(t+2) landed
+// Global intervals (group 0 reads in 4t, 4t+2; group 1 one interval later):
+//   WAR  A slots of a buffer are last read at 4t+1 (group 1, P0) and
+//        re-staged from 4t+2; B slots last read at 4t+3 and re-staged from
+//        4t+4 (P0 of t+1 stages B of t+2 into the other buffer).
+//   RAW  tile t+1 is waited for by group 0 at 4t+2 and group 1 at 4t+3, and
+//        first read at 4t+4 behind the barrier.
+template <class Mma, class Pre = NoPrefetch>
+__device__ __forceinline__ void body2(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4], bool stagger,
+                                      const Pre& pre = Pre()) {
+  const bool pre_on = Pre::kAny && pre.on();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int aoff[2][4][2], boff[2][2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) aoff[mq][mb][s] = swz(mq * 64 + mb * 16 + l16, 4 * s + lq);
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) boff[nq][nb][s] = swz((wc & 1) * 64 + nq * 32 + nb * 16 + l16, 4 * s + lq);
+  }
+  if (KS > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else vm0();
+  bar();
+  if (stagger && wr == 1) bar();
+
+  bf16x8 a0[4][2], a1[4][2], b[2][2];
+  for (int t = 0; t < KS; ++t) {
+    const int buf = t & 1;
+    const u16* As = smem + (buf * 4 + wr) * HALF;
+    const u16* Bs = smem + (buf * 4 + 2 + (wc >> 1)) * HALF;
+    // ---- P0 ----
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) a0[mb][s] = *reinterpret_cast<const bf16x8*>(As + aoff[0][mb][s]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b[nb][s] = *reinterpret_cast<const bf16x8*>(Bs + boff[0][nb][s]);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) a1[mb][s] = *reinterpret_cast<const bf16x8*>(As + aoff[1][mb][s]);
+    }
+    if (t + 1 < KS || pre_on) {
+      stage<2>(smem, st, pre, buf ^ 1, t + 1, KS);
+      stage<3>(smem, st, pre, buf ^ 1, t + 1, KS);
+      if (t + 1 == KS) pre.extra();
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    Mma::template quad<0, 0>(acc, a0, b);
+    Mma::template quad<1, 0>(acc, a1, b);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- P1 ----
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) b[nb][s] = *reinterpret_cast<const bf16x8*>(Bs + boff[1][nb][s]);
+    if (t + 2 < KS || pre_on) {
+      stage<0>(smem, st, pre, buf, t + 2, KS);
+      stage<1>(smem, st, pre, buf, t + 2, KS);
+      // t + 2 == KS + 1: this tile's operands all landed at P1 of K-tile KS-2
+      if (t + 2 <= KS) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      vm0();
+    }
+    bar();
+    lgkm0();
+    __builtin_amdgcn_s_setprio(1);
+    Mma::template quad<1, 1>(acc, a1, b);
+    Mma::template quad<0, 1>(acc, a0, b);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (stagger && wr == 0) bar();
 }
 
 // K loop after prologue() (K = KS * 64). On return acc[i][j][e] holds
@@ -172,8 +315,10 @@ __device__ __forceinline__ void prologue(u16* smem, const Stager& st, int KS, co
 // (smem may be reused or re-staged).
 // OPT (schedule experiments, A/B in bench/ab_search.py): bit 0 = no
 // s_setprio around the MFMA clusters, bit 1 = no wave-group stagger.
-template <class Mma = MmaBf16, int OPT = 0>
-__device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
+template <class Mma = MmaBf16, int OPT = 0, class Pre = NoPrefetch>
+__device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4],
+                                     const Pre& pre = Pre()) {
+  const bool pre_on = Pre::kAny && pre.on();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -218,9 +363,9 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) b[nb][s] = *reinterpret_cast<const bf16x8*>(Bs + boff[0][nb][s]);
     }
-    if (nxt) {
-      st.issue<1>(smem, buf ^ 1, t + 1);
-      st.issue<2>(smem, buf ^ 1, t + 1);
+    if (nxt || pre_on) {
+      stage<1>(smem, st, pre, buf ^ 1, t + 1, KS);
+      stage<2>(smem, st, pre, buf ^ 1, t + 1, KS);
     }
     bar();
     lgkm0();
@@ -233,7 +378,10 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) a1[mb][s] = *reinterpret_cast<const bf16x8*>(As + aoff[1][mb][s]);
-    if (nxt) st.issue<3>(smem, buf ^ 1, t + 1);
+    if (nxt || pre_on) {
+      stage<3>(smem, st, pre, buf ^ 1, t + 1, KS);
+      if (!nxt) pre.extra();
+    }
     bar();
     lgkm0();
     if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(1);
@@ -252,9 +400,9 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
     if constexpr (!(OPT & 1)) __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- p3 ----
-    if (t + 2 < KS) {
-      st.issue<0>(smem, buf, t + 2);
-      vm2();
+    if (t + 2 < KS || pre_on) {
+      stage<0>(smem, st, pre, buf, t + 2, KS);
+      if (t + 2 <= KS) vm2();  // t + 2 == KS + 1: this tile's operands all landed at p3 of K-tile KS-2
     } else {
       vm0();
     }
@@ -269,8 +417,8 @@ __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 
 
 template <class Mma = MmaBf16>
 __device__ __forceinline__ void mainloop(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4]) {
-  prologue(smem, st, KS);
-  body<Mma>(smem, st, KS, acc);
+  prologue<NoExtra, 8>(smem, st, KS);
+  body2<Mma>(smem, st, KS, acc, true);
 }
 
 // Persistent tile walk: the blocks resident on one XCD (blocks are dealt to

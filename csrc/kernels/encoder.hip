@@ -112,7 +112,7 @@ constexpr int G256_OUT_LD = g256::BN + 4;  // u16 per LDS output row (520 B)
 constexpr int G256_GEMM_LDS = (g256::BM * G256_OUT_LD * 2 > g256::LDS_BYTES) ? g256::BM * G256_OUT_LD * 2
                                                                               : g256::LDS_BYTES;
 
-template <int ACT, bool RES>
+template <int ACT, bool RES, int BODY = 0>
 __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
     const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
     const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y,
@@ -130,13 +130,19 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   const int KS = K / g256::BK;
   // the tile's 256 bias values ride along with the prologue DMA (no global
   // load latency in the epilogue)
-  g256::prologue(smem, st, KS, [&]() {
+  auto stage_bias = [&]() {
     if (wave < 4)
       __builtin_amdgcn_global_load_lds((g256::gbl_void_t*)(bias + min(n0 + wave * 64 + lane, N - 1)),
                                        (g256::lds_void_t*)(sbias + wave * 64), 4, 0, 0);
-  });
+  };
   f32x4 acc[8][4];
-  g256::body(smem, st, KS, acc);
+  if constexpr (BODY == 1) {  // two-phase main loop (lzk_g256.h body2)
+    g256::prologue<decltype(stage_bias), 8>(smem, st, KS, stage_bias);
+    g256::body2<g256::MmaBf16>(smem, st, KS, acc, true);
+  } else {
+    g256::prologue(smem, st, KS, stage_bias);
+    g256::body(smem, st, KS, acc);
+  }
   if (ACT == 9) {  // measurement probe (act=9): main loop only, epilogue cost = difference
     float z = 0.f;
 #pragma unroll
@@ -637,9 +643,11 @@ __global__ __launch_bounds__(256) void pool_norm_kernel(const u16* __restrict__ 
 
 static int g_gemm_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
 static int g_gemm_tile = -1;     // 256 = 8-wave 256x256 pipeline when the grid fills the chip, 128 = always 128x128
+static int g_g256_body = -1;     // 256x256 main loop: 0 = four-phase body, 1 = two-phase body2 (default; LZK_G256_BODY)
 
 LZK_EXPORT void lzk_set_staging(int glds) { g_gemm_staging = glds; }
 LZK_EXPORT void lzk_set_gemm_tile(int t) { g_gemm_tile = t; }
+LZK_EXPORT void lzk_set_g256_body(int b) { g_g256_body = b; }
 
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
@@ -681,18 +689,28 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
       const u16* r = (const u16*)R;
       u16* y = (u16*)Y;
       dim3 grid(n_ft * n_tt), block(g256::NT);
-#define GO(A, RS)                                                                                             \
+      if (g_g256_body < 0) {
+        const char* e = getenv("LZK_G256_BODY");
+        g_g256_body = e ? atoi(e) : 1;  // body2: 2-4 % faster on the bge-base projections (bench/ab_body.py)
+      }
+#define GO1(A, RS, BD)                                                                                        \
   do {                                                                                                        \
-    (void)hipFuncSetAttribute((const void*)gemm256_bias_act_kernel<A, RS>,                                    \
+    (void)hipFuncSetAttribute((const void*)gemm256_bias_act_kernel<A, RS, BD>,                                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, G256_GEMM_LDS);                     \
-    hipLaunchKernelGGL((gemm256_bias_act_kernel<A, RS>), grid, block, G256_GEMM_LDS, st, x, ldx, T, w, ldw, \
-                       N, bias, r, ldr, y, ldy, K, n_ft);                                                     \
+    hipLaunchKernelGGL((gemm256_bias_act_kernel<A, RS, BD>), grid, block, G256_GEMM_LDS, st, x, ldx, T, w,  \
+                       ldw, N, bias, r, ldr, y, ldy, K, n_ft);                                                \
+  } while (0)
+#define GO(A, RS)                        \
+  do {                                   \
+    if (g_g256_body == 1) GO1(A, RS, 1); \
+    else GO1(A, RS, 0);                  \
   } while (0)
       if (act == 9) GO(9, false);
       else if (act == 10) GO(10, false);
       else if (act == 1) { if (r) GO(1, true); else GO(1, false); }
       else { if (r) GO(0, true); else GO(0, false); }
 #undef GO
+#undef GO1
       return (int)hipGetLastError();
     }
   }

@@ -157,17 +157,39 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
 
   Stager st;
   st.setup(X, ldx, (tile / n_qt) * BM, nrows, Qm, ldq, (tile % n_qt) * BN, nq);
-  prologue(smem, st, KS, [&]() { stage_epi(tile, 0); });
+  auto ex0 = [&]() { stage_epi(tile, 0); };
+  prologue<decltype(ex0), OPT>(smem, st, KS, ex0);
+  // OPT bit 5: cross-tile prefetch (lzk_g256.h NextTile) -- needs an even K-tile count
+  const bool can_pre = ((OPT & 32) != 0) && (KS % 2 == 0);
   int par = 0;
   f32x4 acc[8][4];
   while (true) {
-    body<MmaBf16, OPT>(smem, st, KS, acc);
     const int cur = tile, cpar = par;
     tile += walk.step;
     const bool more = walk.valid(tile);
+    const int nr0 = (tile / n_qt) * BM, nc0 = (tile % n_qt) * BN;
+    auto exn = [&]() { stage_epi(tile, cpar ^ 1); };
+    const NextTile<decltype(exn)> pre{X, ldx, nr0, nrows, Qm, ldq, nc0, nq, &exn, more && can_pre};
+    if constexpr ((OPT & 8) != 0) body2<MmaBf16>(smem, st, KS, acc, !(OPT & 2), pre);
+    else body<MmaBf16, (OPT & 3)>(smem, st, KS, acc, pre);
     if (more) {
-      st.setup(X, ldx, (tile / n_qt) * BM, nrows, Qm, ldq, (tile % n_qt) * BN, nq);
-      prologue(smem, st, KS, [&]() { stage_epi(tile, cpar ^ 1); });
+      st.setup(X, ldx, nr0, nrows, Qm, ldq, nc0, nq);
+      if (!can_pre) prologue<decltype(exn), OPT>(smem, st, KS, exn);
+    }
+    if constexpr ((OPT & 4) != 0) {
+      // probe only: the GEMM without the candidate epilogue (one max per
+      // lane keeps the accumulators live)
+      float m = LZK_NEG_INF;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) m = fmaxf(m, acc[i][j][e]);
+      if (m > 1e30f) append(cnt, cs, ci, 0, m, cur);
+      if (!more) break;
+      par = cpar ^ 1;
+      continue;
     }
     // ---- epilogue of `cur` (operands from LDS only) ----
     {
@@ -188,19 +210,39 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
         ql[j] = HAS_LABEL ? e_qlab[qlo] : -1;
       }
       const bool full = r0 + BM <= nrows;
+      // OPT bit 4: column prefilter. For alpha > 0 every score of query
+      // column j is <= alpha * max_i acc[i][j] + max(bias over the wave's
+      // rows), so a column whose bound is below its threshold (the common
+      // case: ~k*S/N of the scores pass) skips the per-score pass -- ~70
+      // VALU per tile instead of ~320. Labels only remove rows, and list B's
+      // threshold is covered by min(th, th2), so the bound is conservative.
+      float bmax = 0.f;
+      if constexpr ((OPT & 16) != 0 && HAS_BIAS)
+        bmax = wave_max(fmaxf(e_bias[wr * 128 + lane], e_bias[wr * 128 + 64 + lane]));
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int rl = wr * 128 + i * 16 + 4 * (lane >> 4);
-        const int rb = r0 + rl;
-        f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-        if (HAS_BIAS) bv = *reinterpret_cast<const f32x4*>(e_bias + rl);
-        int lv[4] = {0, 0, 0, 0};
-        if (HAS_LABEL) {
+      for (int j = 0; j < 4; ++j) {
+        if constexpr ((OPT & 16) != 0) {
+          float mx = acc[0][j][0];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) lv[e] = e_lab[rl + e];
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mx = fmaxf(mx, acc[i][j][e]);
+          const float tmin = DUAL ? fminf(th[j], th2[j]) : th[j];
+          // slack of a few ulp: the per-score path may contract alpha*acc+bias differently
+          // (tmin = +inf -> NaN -> skipped; tmin = -inf -> kept)
+          if (alpha > 0.f && !(alpha * mx + bmax >= tmin - 1e-6f * fabsf(tmin))) continue;
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int i = 0; i < 8; ++i) {
+          const int rl = wr * 128 + i * 16 + 4 * (lane >> 4);
+          const int rb = r0 + rl;
+          f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+          if (HAS_BIAS) bv = *reinterpret_cast<const f32x4*>(e_bias + rl);
+          int lv[4] = {0, 0, 0, 0};
+          if (HAS_LABEL) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lv[e] = e_lab[rl + e];
+          }
           float sc[4];
           bool lab_ok[4];
           float m = LZK_NEG_INF, m2 = LZK_NEG_INF;
@@ -233,7 +275,14 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
 }
 
 int g_cand_persist = -1;
-int g_g256_opt = 0;  // schedule experiment selector (see lzk_g256.h body<OPT>)
+// Schedule of the persistent candidate kernel (OPT bits): bit 3 = two-phase
+// main loop (body2), bit 4 = column prefilter in the epilogue. Interleaved A/B
+// on one MI355X, 10M x 768 x 1024 queries (bench/ab_search.py,
+// profiles/ab_search_sched_r1.json): four-phase 13.73 ms, +body2 13.09,
+// +prefilter 13.38, both 12.80 ms (-6.8 %); cross-tile prefetch (bit 5) was
+// 8 % slower and stays an A/B knob only.
+constexpr int kCandOpt = 24;
+int g_g256_opt = 0;  // A/B override of kCandOpt for the plain (no bias / label) variant; 100 = OPT 0
 int g_n_cu = 0;
 
 template <int K>
@@ -332,16 +381,16 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
     const int grid = g_n_cu;
 #define LZK_GP(B, L)                                                                                                \
   do {                                                                                                              \
-    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, L, false>,                                \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, L, false, kCandOpt>,                                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
-    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, L, false>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,    \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, L, false, kCandOpt>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,    \
                        nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs,   \
                        ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr);                    \
   } while (0)
     if (bias && row_label) LZK_GP(true, true);
     else if (bias) LZK_GP(true, false);
     else if (row_label) LZK_GP(false, true);
-    else if (g_g256_opt > 0 && g_g256_opt < 4) {
+    else if (g_g256_opt > 0) {
 #define LZK_GX(O)                                                                                                   \
   do {                                                                                                              \
     (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<false, false, false, O>,                     \
@@ -350,9 +399,22 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
                        x, ldx, nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap,    \
                        cnt, cs, ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr);          \
   } while (0)
-      if (g_g256_opt == 1) LZK_GX(1);
-      else if (g_g256_opt == 2) LZK_GX(2);
-      else LZK_GX(3);
+      switch (g_g256_opt) {
+        case 1: LZK_GX(1); break;
+        case 2: LZK_GX(2); break;
+        case 4: LZK_GX(4); break;
+        case 8: LZK_GX(8); break;
+        case 16: LZK_GX(16); break;
+        case 24: LZK_GX(24); break;
+        case 26: LZK_GX(26); break;
+        case 32: LZK_GX(32); break;
+        case 36: LZK_GX(36); break;
+        case 40: LZK_GX(40); break;
+        case 48: LZK_GX(48); break;
+        case 56: LZK_GX(56); break;
+        case 100: LZK_GX(0); break;
+        default: LZK_GX(kCandOpt); break;
+      }
 #undef LZK_GX
     } else LZK_GP(false, false);
 #undef LZK_GP
@@ -395,9 +457,9 @@ LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void
   const u16* q = (const u16*)Qm;
 #define LZK_GD(B)                                                                                                   \
   do {                                                                                                              \
-    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, true, true>,                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, true, true, kCandOpt>,                              \
                               hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
-    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,  \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true, kCandOpt>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,  \
                        nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs,   \
                        ci, thr2, cnt2, cs2, ci2);                                                                   \
   } while (0)

@@ -283,3 +283,30 @@ def test_attention_packed_gpu():
     o = E.attention(qkv, lens.to(DEV), B, int(lens.max()), heads, cu=cu.to(DEV))
     ref = E.attention(qkv.cpu(), lens, B, int(lens.max()), heads, cu=cu)
     assert _rel(o.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("opt", [100, 8, 16, 24, 32, 48, 40, 56])
+@pytest.mark.parametrize("n,d,nq", [(200_000, 768, 512), (150_000, 64, 300), (120_000, 192, 256),
+                                    (90_001, 128, 257)])
+def test_cand_schedule_variants(monkeypatch, opt, n, d, nq):
+    """Every main-loop / epilogue schedule of the persistent candidate kernel
+    (lzk_g256.h body / body2, cross-tile prefetch, column prefilter) returns
+    the reference top-k, for even and odd K-tile counts (d=64, 192: KS odd)."""
+    import ctypes
+    L = _lib.lib()
+    L.lzk_set_g256_opt.argtypes = [ctypes.c_int]
+    L.lzk_set_cand_persist.argtypes = [ctypes.c_int]
+    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", 16)
+    g = torch.Generator(device=DEV).manual_seed(n + d + opt)
+    X = torch.randn(n, d, device=DEV, generator=g).to(torch.bfloat16)
+    Q = torch.randn(nq, d, device=DEV, generator=g).to(torch.bfloat16)
+    L.lzk_set_cand_persist(1)
+    L.lzk_set_g256_opt(opt)
+    try:
+        s, i = flat_topk(X, Q, 10)
+    finally:
+        L.lzk_set_g256_opt(-1)
+    rs, ri = _ref_topk(X.cpu(), Q.cpu(), 10)
+    torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
+    assert (i.cpu() == ri).float().mean() > 0.995
