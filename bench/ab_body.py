@@ -19,6 +19,8 @@ from lazzaro_amd.ops import encoder_ops as E  # noqa: E402
 
 L = _lib.lib()
 L.lzk_set_g256_body.argtypes = [ctypes.c_int]
+L.lzk_set_g256_min_n.argtypes = [ctypes.c_int]
+L.lzk_set_g256_min_tiles.argtypes = [ctypes.c_int]
 
 
 def timeit(fn, it=10):
@@ -35,17 +37,22 @@ def main():
     dev = "cuda"
     out = {}
     for T in (11264, 22528):
-        for name, (N, K, act) in {"qkv": (2304, 768, "none"), "ffn1": (3072, 768, "gelu")}.items():
+        for name, (N, K, act) in {"qkv": (2304, 768, "none"), "ffn1": (3072, 768, "gelu"),
+                                  "o": (768, 768, "none"), "ffn2": (768, 3072, "none")}.items():
             x = torch.randn(T, K, device=dev).to(torch.bfloat16)
             w = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
             b = torch.randn(N, device=dev)
             ys, ts = {}, {0: [], 1: []}
+            L.lzk_set_g256_min_tiles(1)
+            L.lzk_set_g256_min_n(N)  # arm 1 = two-phase 256x256; arm 0 = four-phase (N >= 1024) / 128x128 (N = 768)
             for bd in (0, 1):
                 L.lzk_set_g256_body(bd)
+                L.lzk_set_g256_min_n(N if bd else 1024)
                 ys[bd] = E.linear(x, w, b, act=act).float()
             for _ in range(5):
                 for bd in (0, 1):
                     L.lzk_set_g256_body(bd)
+                    L.lzk_set_g256_min_n(N if bd else 1024)
                     ts[bd].append(timeit(lambda: E.linear(x, w, b, act=act)))
             flop = 2.0 * T * N * K
             r = {"rel_diff": float((ys[0] - ys[1]).norm() / ys[0].norm())}
@@ -60,13 +67,22 @@ def main():
     emb = OnDeviceEmbedder("bge-base", device=torch.device(dev), max_len=64, seed=0)
     texts = B.synth_texts(1024, random.Random(1234))
     ids, lens = emb.tok.encode_batch(texts, emb.max_len)
-    ts = {0: [], 1: []}
+    # arms: (main loop, smallest N on the 256 path, sub-batch streams)
+    # arms: (main loop, smallest N on the 256 path, smallest grid on it, sub-batch streams)
+    arms = {"body0": (0, 1024, 256, 2), "body1": (1, 1024, 256, 2), "body1_n768_t128": (1, 768, 128, 2),
+            "body1_t128": (1, 1024, 128, 2), "body1_n768_t128_3s": (1, 768, 128, 3),
+            "body1_n768_t64_4s": (1, 768, 64, 4), "body1_n768_1s": (1, 768, 256, 1)}
+    ts = {a: [] for a in arms}
     for _ in range(5):
-        for bd in (0, 1):
+        for a, (bd, mn, mt, parts) in arms.items():
             L.lzk_set_g256_body(bd)
-            ts[bd].append(timeit(lambda: emb.encoder.forward_streams(ids, lens, pad_to=768, parts=2), it=5))
-    out["embed_forward_ms"] = {f"body{bd}": round(statistics.median(v) * 1e3, 3) for bd, v in ts.items()}
+            L.lzk_set_g256_min_n(mn)
+            L.lzk_set_g256_min_tiles(mt)
+            ts[a].append(timeit(lambda: emb.encoder.forward_streams(ids, lens, pad_to=768, parts=parts), it=5))
+    out["embed_forward_ms"] = {a: round(statistics.median(v) * 1e3, 3) for a, v in ts.items()}
     L.lzk_set_g256_body(-1)
+    L.lzk_set_g256_min_n(-1)
+    L.lzk_set_g256_min_tiles(-1)
     print(json.dumps(out, indent=1), flush=True)
 
 

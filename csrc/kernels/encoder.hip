@@ -648,6 +648,10 @@ static int g_g256_body = -1;     // 256x256 main loop: 0 = four-phase body, 1 = 
 LZK_EXPORT void lzk_set_staging(int glds) { g_gemm_staging = glds; }
 LZK_EXPORT void lzk_set_gemm_tile(int t) { g_gemm_tile = t; }
 LZK_EXPORT void lzk_set_g256_body(int b) { g_g256_body = b; }
+static int g_g256_min_n = -1;  // smallest N routed to the 256x256 pipeline (LZK_G256_MIN_N)
+LZK_EXPORT void lzk_set_g256_min_n(int n) { g_g256_min_n = n; }
+static int g_g256_min_tiles = -1;  // smallest grid routed to the 256x256 pipeline (LZK_G256_MIN_TILES)
+LZK_EXPORT void lzk_set_g256_min_tiles(int n) { g_g256_min_tiles = n; }
 
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
@@ -680,9 +684,19 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   }
   {
     const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
-    // measured (bench/ab_gemm.py): at N = 768 the 1.5-wave quantisation of 3 feature tiles
-    // loses to the 128x128 kernel; from N = 1024 on the 256x256 pipeline wins
-    if (g_gemm_tile == 256 && n_ft * n_tt >= 256 && N >= 1024 && N % 8 == 0 && ldy % 8 == 0 &&
+    // measured (bench/ab_body.py, profiles/ab_body_r1.json): with the two-phase main loop the
+    // 256x256 pipeline beats the 128x128 kernel even on half the chip -- bge-base O / FFN2
+    // (N = 768) at 11k tokens: 132 tiles, 24 / 60 us vs 34 / 90 us -- so every grid of at
+    // least 128 tiles takes it; the whole 2-stream bench forward 5.72 -> 5.13 ms
+    if (g_g256_min_n < 0) {
+      const char* e = getenv("LZK_G256_MIN_N");
+      g_g256_min_n = e ? atoi(e) : 768;
+    }
+    if (g_g256_min_tiles < 0) {
+      const char* e = getenv("LZK_G256_MIN_TILES");
+      g_g256_min_tiles = e ? atoi(e) : 128;
+    }
+    if (g_gemm_tile == 256 && n_ft * n_tt >= g_g256_min_tiles && N >= g_g256_min_n && N % 8 == 0 && ldy % 8 == 0 &&
         (!R || ldr % 8 == 0)) {
       const u16* x = (const u16*)X;
       const u16* w = (const u16*)W;
