@@ -160,7 +160,7 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
     def step():
         if encoder is not None:
             ids, lens = encoder.tok.encode_batch(texts, 64)
-            encoder.encoder.forward(ids, lens, pad_to=buf.g.emb.shape[1])
+            encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=2)
         q, topic, sal = synth_facts(buf, convs * facts, dim, dup_rate, gen)
         now[0] += 60.0
         return buf.consolidate(q, topic, sal, convs * comm.world, now[0])

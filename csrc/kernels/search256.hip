@@ -282,6 +282,11 @@ int g_cand_persist = -1;
 // +prefilter 13.38, both 12.80 ms (-6.8 %); cross-tile prefetch (bit 5) was
 // 8 % slower and stays an A/B knob only.
 constexpr int kCandOpt = 24;
+// The dual kernel's list-B threshold comes from a 1/S sample of one shard's
+// rows, so it is low and the column prefilter rarely skips: bench/ab_dual.py
+// (profiles/ab_dual_r1.json) 0: 16.27 ms, body2: 15.65, +prefilter 15.90.
+constexpr int kDualOpt = 8;
+int g_dual_opt = -1;  // A/B override of kCandOpt for the dual kernel (lzk_set_dual_opt)
 int g_g256_opt = 0;  // A/B override of kCandOpt for the plain (no bias / label) variant; 100 = OPT 0
 int g_n_cu = 0;
 
@@ -353,6 +358,7 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
 
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
+LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
 
 // Candidate pass. cnt [nq] must be zeroed by the caller (same stream);
 // cs/ci are [nq, cap].
@@ -455,17 +461,27 @@ LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* q = (const u16*)Qm;
-#define LZK_GD(B)                                                                                                   \
+#define LZK_GDO(B, O)                                                                                              \
   do {                                                                                                              \
-    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, true, true, kCandOpt>,                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, true, true, O>,                           \
                               hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
-    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true, kCandOpt>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,  \
-                       nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs,   \
-                       ci, thr2, cnt2, cs2, ci2);                                                                   \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true, O>), dim3(grid), dim3(NT), CAND_P_LDS, st, x,    \
+                       ldx, nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt,  \
+                       cs, ci, thr2, cnt2, cs2, ci2);                                                               \
+  } while (0)
+#define LZK_GD(B)                              \
+  do {                                         \
+    switch (g_dual_opt) {                      \
+      case 0: LZK_GDO(B, 0); break;            \
+      case 8: LZK_GDO(B, 8); break;            \
+      case 16: LZK_GDO(B, 16); break;          \
+      default: LZK_GDO(B, kDualOpt); break;    \
+    }                                          \
   } while (0)
   if (bias) LZK_GD(true);
   else LZK_GD(false);
 #undef LZK_GD
+#undef LZK_GDO
   return (int)hipGetLastError();
 }
 
