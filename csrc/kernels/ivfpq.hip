@@ -151,6 +151,118 @@ __global__ __launch_bounds__(256) void ivfpq_dense_kernel(const unsigned char* _
   }
 }
 
+
+// Exact re-rank of a deep candidate list (IVF-PQ candidates, BASELINE config 5):
+// score = <q, v_row> over the kept copy -- fp8 e4m3 with a per-row scale
+// (D + 4 B/vector) or bf16 -- then the top-k by (score desc, row asc). One
+// 256-thread block per query: the query is staged once in LDS as fp32; 16 lanes
+// score one row (16-B loads, 256 contiguous bytes per group and step), so a
+// wave has 4 rows and a block 16 rows in flight per step; scores go to LDS and
+// wave 0 selects (lane-local top-K, then k rounds of wave argmax). Replaces a
+// gather + fp32 dequantise + batched GEMM + sort chain of library kernels.
+template <int K>
+struct RerankTopK {
+  float s[K];
+  int i[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < K; ++j) { s[j] = LZK_NEG_INF; i[j] = 0x7fffffff; }
+  }
+  __device__ __forceinline__ void push(float v, int r) {
+    if (!better(v, r, s[K - 1], i[K - 1])) return;
+#pragma unroll
+    for (int j = K - 1; j > 0; --j) {
+      const bool up = better(v, r, s[j - 1], i[j - 1]);
+      const bool here = better(v, r, s[j], i[j]);
+      const float ns = up ? s[j - 1] : (here ? v : s[j]);
+      const int ni = up ? i[j - 1] : (here ? r : i[j]);
+      s[j] = ns; i[j] = ni;
+    }
+    if (better(v, r, s[0], i[0])) { s[0] = v; i[0] = r; }
+  }
+};
+
+template <bool FP8, int K>
+__global__ __launch_bounds__(256) void rerank_kernel(const unsigned char* __restrict__ V, long ldv,
+                                                     const float* __restrict__ vscale, const long* __restrict__ rows,
+                                                     int R, const float* __restrict__ Q, int D, int kout,
+                                                     float* __restrict__ os, long* __restrict__ oi) {
+  extern __shared__ __attribute__((aligned(16))) float rsm[];  // [D] query | [R] scores
+  float* qs = rsm;
+  float* sc = rsm + D;
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, l16 = lane & 15;
+  for (int d = threadIdx.x; d < D; d += 256) qs[d] = Q[(long)q * D + d];
+  __syncthreads();
+  const long* rq = rows + (long)q * R;
+  const int row_bytes = FP8 ? D : 2 * D;  // multiple of 256 (checked by the launcher)
+  const int steps = row_bytes / 256;
+  for (int c0 = wave * 4; c0 < R; c0 += 16) {
+    const int c = c0 + g;
+    const long r = c < R ? rq[c] : -1;
+    float a = 0.f;
+    if (r >= 0) {
+      const unsigned char* v = V + r * ldv;
+      for (int j = 0; j < steps; ++j) {
+        const int b = j * 256 + l16 * 16;
+        const uint4 w = *reinterpret_cast<const uint4*>(v + b);
+        const unsigned u[4] = {w.x, w.y, w.z, w.w};
+        if constexpr (FP8) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)u[t], false);
+            const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)u[t], true);
+            const float* qq = qs + b + 4 * t;
+            a = fmaf(lo[0], qq[0], fmaf(lo[1], qq[1], fmaf(hi[0], qq[2], fmaf(hi[1], qq[3], a))));
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float* qq = qs + b / 2 + 2 * t;
+            a = fmaf(__uint_as_float(u[t] << 16), qq[0], fmaf(__uint_as_float(u[t] & 0xffff0000u), qq[1], a));
+          }
+        }
+      }
+    }
+    a += __shfl_xor(a, 8, 64);
+    a += __shfl_xor(a, 4, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 1, 64);
+    if (l16 == 0 && c < R) sc[c] = r >= 0 ? (FP8 ? a * vscale[r] : a) : LZK_NEG_INF;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  RerankTopK<K> top;
+  top.init();
+  for (int c = lane; c < R; c += 64) {
+    const long r = rq[c];
+    if (r >= 0) top.push(sc[c], (int)r);
+  }
+  for (int j = 0; j < kout; ++j) {
+    const float hs = top.s[0];
+    const int hi = top.i[0];
+    float bs = hs;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) {
+      const bool none = bi == 0x7fffffff || bs == LZK_NEG_INF;
+      os[(long)q * kout + j] = none ? LZK_NEG_INF : bs;
+      oi[(long)q * kout + j] = none ? -1 : (long)bi;
+    }
+    if (hi == bi && hs == bs && bi != 0x7fffffff) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) { top.s[t] = top.s[t + 1]; top.i[t] = top.i[t + 1]; }
+      top.s[K - 1] = LZK_NEG_INF; top.i[K - 1] = 0x7fffffff;
+    }
+  }
+}
+
 template <int K>
 hipError_t launch_scan(int M, const unsigned char* codes, const long* off, const int* probes, const float* coarse,
                        const float* lut, int nq, int nprobe, float* os, int* oi, hipStream_t st) {
@@ -219,4 +331,35 @@ LZK_EXPORT int lzk_ivfpq_scan(const void* codes, const long* list_off, const int
     default: return (int)hipErrorInvalidValue;
   }
   return (int)e;
+}
+
+// Re-rank: V rows of ldv bytes (fp8: D bytes + vscale[row]; bf16: 2D bytes),
+// rows [nq, R] int64 (-1 = empty), Q [nq, D] fp32 -> top-kout per query.
+LZK_EXPORT int lzk_rerank(const void* V, long ldv, int fp8, const float* vscale, const long* rows, int nq, int R,
+                          const float* Q, int D, int kslot, int kout, float* os, long* oi, void* stream) {
+  const int row_bytes = fp8 ? D : 2 * D;
+  if (nq <= 0 || R <= 0 || row_bytes % 256 != 0 || (ldv & 15) || kout > kslot || (fp8 && !vscale))
+    return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(D + R) * sizeof(float);
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned char* v = (const unsigned char*)V;
+#define RR(F, KK)                                                                                                   \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)rerank_kernel<F, KK>, hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                              (int)lds);                                                                            \
+    hipLaunchKernelGGL((rerank_kernel<F, KK>), dim3(nq), dim3(256), lds, st, v, ldv, vscale, rows, R, Q, D, kout,  \
+                       os, oi);                                                                                     \
+  } while (0)
+#define RK(KK) do { if (fp8) RR(true, KK); else RR(false, KK); } while (0)
+  switch (kslot) {
+    case 1: RK(1); break;
+    case 4: RK(4); break;
+    case 10: RK(10); break;
+    case 16: RK(16); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef RK
+#undef RR
+  return (int)hipGetLastError();
 }

@@ -33,6 +33,9 @@ _lib.register("lzk_ivfpq_scan", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P,
 _lib.register("lzk_ivfpq_dense", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I,
                                            _lib.I, _lib.P, _lib.P])
 
+_lib.register("lzk_rerank", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.I, _lib.I, _lib.P, _lib.I,
+                                      _lib.I, _lib.I, _lib.P, _lib.P, _lib.P])
+
 KSLOTS = (1, 4, 10, 16)
 
 
@@ -197,7 +200,9 @@ class IVFPQIndex:
             s, rows = self._scan_gpu(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
         else:
             s, rows = self._scan_dense(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
-        if rerank and self.vectors is not None:
+        if rerank and self.vectors is not None and self._rerank_gpu_ok(k):
+            s, rows = self._rerank_gpu(qf, rows.contiguous(), k)
+        elif rerank and self.vectors is not None:
             valid = rows >= 0
             rr = rows.clamp_min(0)
             if self.vscale is not None:  # fp8 copy: dequantise the gathered candidates only
@@ -211,6 +216,30 @@ class IVFPQIndex:
         s, rows = s[:, :k], rows[:, :k]
         ids = torch.where(rows >= 0, self.ids[rows.clamp_min(0)], torch.full_like(rows, -1))
         return s, ids
+
+    def _rerank_gpu_ok(self, k: int) -> bool:
+        if self.device.type != "cuda" or k > KSLOTS[-1]:
+            return False
+        w = self.vectors.shape[1]
+        row_bytes = w if self.vscale is not None else 2 * w
+        return row_bytes % 256 == 0
+
+    def _rerank_gpu(self, qf: torch.Tensor, rows: torch.Tensor, k: int):
+        """Fused exact re-rank over the kept copy (csrc/kernels/ivfpq.hip
+        rerank_kernel): no dequantised [nq, R, D] intermediate."""
+        nq, R = rows.shape
+        fp8 = self.vscale is not None
+        w = self.vectors.shape[1]
+        Q = torch.zeros((nq, w), dtype=torch.float32, device=self.device)
+        Q[:, : qf.shape[1]] = qf
+        ks = _kslot(k)
+        os_ = torch.empty((nq, k), dtype=torch.float32, device=self.device)
+        oi = torch.empty((nq, k), dtype=torch.long, device=self.device)
+        ldv = self.vectors.stride(0) * self.vectors.element_size()
+        _lib.check(_lib.lib().lzk_rerank(self.vectors.data_ptr(), ldv, int(fp8), _lib.ptr(self.vscale),
+                                         rows.data_ptr(), nq, R, Q.data_ptr(), w, ks, k, os_.data_ptr(),
+                                         oi.data_ptr(), _lib.stream_ptr(self.device)), "lzk_rerank")
+        return os_, oi
 
     def _scan_ref(self, probes, coarse, lut, k):
         nq = probes.shape[0]

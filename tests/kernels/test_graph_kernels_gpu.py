@@ -202,3 +202,22 @@ def test_store_ivfpq_tenant_gpu(tmp_path):
     got = st.search_nodes_batch(q, user_id="big", limit=5)
     assert a.ivf.idx is not None
     assert sum(g[0] == f"m{i}" for i, g in enumerate(got)) >= 60
+
+
+@pytest.mark.parametrize("keep", ["fp8", "bf16"])
+def test_ivfpq_fused_rerank_matches_library_path(monkeypatch, keep):
+    """rerank_kernel (ivfpq.hip) == gather + dequantise + GEMM + sort."""
+    from lazzaro_amd.index.ivfpq import IVFPQIndex
+    g = torch.Generator(device="cuda").manual_seed(3)
+    d = 256
+    x = torch.nn.functional.normalize(torch.randn(60_000, d, device="cuda", generator=g), dim=1)
+    idx = IVFPQIndex(d, nlist=64, m=32, device="cuda", keep_vectors=keep)
+    idx.train(x[:20_000], iters=4, pq_iters=4)
+    idx.add(x)
+    q = torch.nn.functional.normalize(x[:300] + 0.2 * torch.randn(300, d, device="cuda", generator=g) / d ** 0.5,
+                                      dim=1)
+    s1, i1 = idx.search(q, 10, nprobe=8, rerank=200)
+    monkeypatch.setattr(IVFPQIndex, "_rerank_gpu_ok", lambda self, k: False)
+    s2, i2 = idx.search(q, 10, nprobe=8, rerank=200)
+    torch.testing.assert_close(s1, s2, atol=1e-4, rtol=1e-4)
+    assert (i1 == i2).float().mean() > 0.99
