@@ -487,55 +487,75 @@ __global__ __launch_bounds__(64) void attention_kernel(
 }
 
 // ---------------------------------------------------------------- LayerNorm
-// one wave per row; H % 4 == 0, H <= 64*4*NC
-template <int NC, bool RES>
+// y = LN(x (+ r)) * g + b. One wave per RPW rows, NC chunks of 4 features per
+// lane (H <= 256 * NC): gamma/beta are loaded once per wave and reused for its
+// RPW rows, and every row's loads are issued before the first reduction so a
+// wave has RPW * NC (x2 with the residual) 8-B loads in flight instead of NC.
+template <int NC, bool RES, int RPW>
 __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ X, long ldx,
                                                         const u16* __restrict__ R, long ldr,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ bta, int rows,
                                                         int H, float eps, u16* __restrict__ Y, long ldy) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  float v[NC][4];
-  float sum = 0.f;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  f32x4 gg[NC], bb[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    int col = (lane + 64 * c) * 4;
+    const int col = (lane + 64 * c) * 4;
     if (col < H) {
-      u16x4 x = *reinterpret_cast<const u16x4*>(X + (long)row * ldx + col);
-      u16x4 r = {0, 0, 0, 0};
-      if (RES) r = *reinterpret_cast<const u16x4*>(R + (long)row * ldr + col);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[c][u] = bf16_to_f32(x[u]) + (RES ? bf16_to_f32(r[u]) : 0.f);
-        sum += v[c][u];
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[c][u] = 0.f;
+      gg[c] = *reinterpret_cast<const f32x4*>(g + col);
+      bb[c] = *reinterpret_cast<const f32x4*>(bta + col);
     }
   }
-  const float mean = wave_sum(sum) / H;
-  float var = 0.f;
+  float v[RPW][NC][4];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    int col = (lane + 64 * c) * 4;
-    if (col < H)
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = min(row0 + rr, rows - 1);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { float d = v[c][u] - mean; var += d * d; }
+    for (int c = 0; c < NC; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < H) {
+        const u16x4 x = *reinterpret_cast<const u16x4*>(X + (long)row * ldx + col);
+        u16x4 r = {0, 0, 0, 0};
+        if (RES) r = *reinterpret_cast<const u16x4*>(R + (long)row * ldr + col);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[rr][c][u] = bf16_to_f32(x[u]) + (RES ? bf16_to_f32(r[u]) : 0.f);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[rr][c][u] = 0.f;
+      }
+    }
   }
-  const float rstd = rsqrtf(wave_sum(var) / H + eps);
+  const float invH = 1.f / H;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    int col = (lane + 64 * c) * 4;
-    if (col < H) {
-      f32x4 gg = *reinterpret_cast<const f32x4*>(g + col);
-      f32x4 bb = *reinterpret_cast<const f32x4*>(bta + col);
-      u16x4 o;
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = row0 + rr;
+    if (row >= rows) break;  // wave-uniform
+    float sum = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16((v[c][u] - mean) * rstd * gg[u] + bb[u]);
-      *reinterpret_cast<u16x4*>(Y + (long)row * ldy + col) = o;
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sum += v[rr][c][u];
+    const float mean = wave_sum(sum) * invH;
+    float var = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if ((lane + 64 * c) * 4 < H)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { const float d = v[rr][c][u] - mean; var += d * d; }
+    }
+    const float rstd = rsqrtf(wave_sum(var) * invH + eps);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      if (col < H) {
+        u16x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = f32_to_bf16((v[rr][c][u] - mean) * rstd * gg[c][u] + bb[c][u]);
+        *reinterpret_cast<u16x4*>(Y + (long)row * ldy + col) = o;
+      }
     }
   }
 }
@@ -798,14 +818,25 @@ LZK_EXPORT int lzk_attention(const void* qkv, long ldq, const int* lens, int B, 
 
 LZK_EXPORT int lzk_layernorm(const void* X, long ldx, const void* R, long ldr, const float* g, const float* b,
                              int rows, int H, float eps, void* Y, long ldy, void* stream) {
-  if (H % 4 != 0 || H > 64 * 4 * 4) return (int)hipErrorInvalidValue;
-  dim3 grid((rows + 3) / 4), block(256);
+  if (H % 4 != 0 || H > 64 * 4 * 4 || rows <= 0) return (int)hipErrorInvalidValue;
+  constexpr int RPW = 4;
+  dim3 grid((rows + 4 * RPW - 1) / (4 * RPW)), block(256);
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* r = (const u16*)R;
   u16* y = (u16*)Y;
-  if (r) hipLaunchKernelGGL((layernorm_kernel<4, true>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows, H, eps, y, ldy);
-  else hipLaunchKernelGGL((layernorm_kernel<4, false>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows, H, eps, y, ldy);
+#define LN(NC)                                                                                                  \
+  do {                                                                                                          \
+    if (r) hipLaunchKernelGGL((layernorm_kernel<NC, true, RPW>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows, \
+                              H, eps, y, ldy);                                                                  \
+    else hipLaunchKernelGGL((layernorm_kernel<NC, false, RPW>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows,  \
+                            H, eps, y, ldy);                                                                    \
+  } while (0)
+  if (H <= 256) LN(1);
+  else if (H <= 512) LN(2);
+  else if (H <= 768) LN(3);
+  else LN(4);
+#undef LN
   return (int)hipGetLastError();
 }
 

@@ -311,3 +311,16 @@ def test_cand_schedule_variants(monkeypatch, opt, n, d, nq):
     rs, ri = _ref_topk(X.cpu(), Q.cpu(), 10)
     torch.testing.assert_close(s.cpu(), rs, atol=2e-3, rtol=1e-4)
     assert (i.cpu() == ri).float().mean() > 0.995
+
+
+@pytest.mark.parametrize("T,H,res", [(1, 384, True), (17, 768, False), (4097, 768, True), (333, 1024, True),
+                                     (70, 1000, False)])
+def test_layernorm_shapes(T, H, res):
+    """Rows-per-wave LayerNorm: partial last wave, every NC, with/without residual."""
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    r = torch.randn(T, H, device=DEV).to(torch.bfloat16) if res else None
+    g = torch.rand(H, device=DEV) + 0.5
+    b = torch.randn(H, device=DEV)
+    y = E.layernorm(x, g, b, 1e-12, residual=r)
+    yr = E.layernorm(x.cpu(), g.cpu(), b.cpu(), 1e-12, residual=None if r is None else r.cpu())
+    assert _rel(y.cpu(), yr) < 1e-2
