@@ -62,6 +62,7 @@ class ShardedBuffer:
         dst = torch.randint(0, nodes_per_rank, (ne,), device=device, generator=gen)
         self.g.add_edges(src, dst, torch.rand(ne, device=device, generator=gen) * 0.5 + 0.5, now=0.0)
         self.limit = int(nodes_per_rank * 1.1)
+        self.rows_added = nodes_per_rank  # host-side upper bound on live rows
         self.remote_edges = []
 
     def owner(self, topic: torch.Tensor) -> torch.Tensor:
@@ -72,12 +73,15 @@ class ShardedBuffer:
         With ``q_label`` the same scan (flat_topk_dual) also returns this
         rank's shard-filtered top-k for its own queries (within-shard links)."""
         comm = self.comm
-        nq = torch.tensor([q.shape[0]], device=self.dev)
-        sizes = comm.all_gather_rows(nq).tolist()
-        mx = max(sizes) if sizes else 0
-        qp = torch.zeros((mx, q.shape[1]), dtype=q.dtype, device=self.dev)
-        qp[: q.shape[0]] = q
-        allq = comm.all_gather_rows(qp)  # [world*mx, Dp]
+        if comm.world > 1:
+            nq = torch.tensor([q.shape[0]], device=self.dev)
+            sizes = comm.all_gather_rows(nq).tolist()
+            mx = max(sizes) if sizes else 0
+            qp = torch.zeros((mx, q.shape[1]), dtype=q.dtype, device=self.dev)
+            qp[: q.shape[0]] = q
+            allq = comm.all_gather_rows(qp)  # [world*mx, Dp]
+        else:
+            mx, allq = q.shape[0], q
         n = self.g.n
         lo = comm.rank * mx
         local = None
@@ -90,14 +94,21 @@ class ShardedBuffer:
                                               row_label=self.g.shard[:n], q_label=ql)
             local = (sw[lo: lo + q.shape[0]], rw[lo: lo + q.shape[0]])
         gid = torch.where(r >= 0, (comm.rank << ROW_BITS) + r, r)
-        S = comm.all_gather_rows(s).view(comm.world, comm.world * mx, k)
-        I = comm.all_gather_rows(gid).view(comm.world, comm.world * mx, k)
-        S = S[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
-        I = I[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
-        merged = merge_topk(S, I, k)
+        if comm.world > 1:
+            S = comm.all_gather_rows(s).view(comm.world, comm.world * mx, k)
+            I = comm.all_gather_rows(gid).view(comm.world, comm.world * mx, k)
+            S = S[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
+            I = I[:, lo: lo + q.shape[0]].permute(1, 0, 2).reshape(q.shape[0], -1)
+            merged = merge_topk(S, I, k)
+        else:
+            merged = (s, gid)
         return merged if q_label is None else (merged, local)
 
     def consolidate(self, q: torch.Tensor, topic: torch.Tensor, sal: torch.Tensor, convs_total: int, now: float):
+        """One batch, host-sync-free except the edge compaction: duplicates are
+        merged by masked index reductions and the batch is ingested with
+        DeviceGraph.ingest_fixed (fixed shapes, tombstoned duplicate rows).
+        Returns device counts."""
         comm, g = self.comm, self.g
         # (2) route facts to topic owners
         if comm.world > 1:
@@ -107,25 +118,30 @@ class ShardedBuffer:
         (s, gid), shard_hits = self.global_search(q, 3, q_label=topic)
         dup = (gid[:, 0] >= 0) & (s[:, 0] > 0.95)
         local_dup = dup & ((gid[:, 0] >> ROW_BITS) == comm.rank)
-        rows = (gid[:, 0][local_dup] & ((1 << ROW_BITS) - 1))
-        if rows.numel():
-            g.sal.index_reduce_(0, rows, sal[local_dup].float(), "amax", include_self=True)
-            g.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
-            g.last[rows] = now
-        keep = ~dup
-        # (4) insert + links (within-shard via DeviceGraph.ingest, cross-shard from the global search)
+        rows = torch.where(gid[:, 0] >= 0, gid[:, 0] & ((1 << ROW_BITS) - 1), 0)
+        neg = torch.full_like(sal, float("-inf"))
+        g.sal.index_reduce_(0, rows, torch.where(local_dup, sal.float(), neg), "amax", include_self=True)
+        g.acc.index_add_(0, rows, local_dup.to(torch.int32))
+        g.last.index_reduce_(0, rows, torch.where(local_dup, torch.full_like(neg, now, dtype=torch.float64),
+                                                  torch.full_like(neg, float("-inf"), dtype=torch.float64)),
+                             "amax", include_self=True)
+        # (4) insert + links (within-shard + same-rank global hits; fixed shapes)
         n0 = g.n
-        out = g.ingest(q[keep], topic[keep], sal[keep], now=now, dedupe=False, global_links=False,
-                       shard_hits=(shard_hits[0][keep], shard_hits[1][keep]))
-        cross = (s[keep] > 0.5) & (gid[keep] >= 0) & ((gid[keep] >> ROW_BITS) != comm.rank)
-        n_cross = int(cross.sum().item())
-        if n_cross:  # cross-rank associations: local source row -> global target id
+        own = (gid >= 0) & ((gid >> ROW_BITS) == comm.rank)
+        local_g = (torch.where(own, s, neg[:, None].expand_as(s)), torch.where(own, gid & ((1 << ROW_BITS) - 1), -1))
+        out = g.ingest_fixed(q, topic, sal, dup, shard_hits, global_hits=local_g, now=now)
+        self.rows_added += q.shape[0]
+        n_cross = torch.zeros((), dtype=torch.int64, device=self.dev)
+        if comm.world > 1:  # cross-rank associations: local source row -> global target id
+            cross = (s > 0.5) & (gid >= 0) & ~own & ~dup[:, None]
             src = torch.arange(n0, g.n, device=self.dev)[:, None].expand(-1, 3)
-            self.remote_edges.append((src[cross], gid[keep][cross], s[keep][cross] * 0.8))
+            self.remote_edges.append((src[cross], gid[cross], s[cross] * 0.8))
+            n_cross = cross.sum()
         # (5) decay + prune + eviction
         pruned = g.decay_prune(0.01, 0.5, conversations=convs_total)
-        evicted = g.enforce_limit(self.limit, now=now)
-        return {"routed": int(q.shape[0]), "dup": int(dup.sum().item()), "inserted": out["inserted"],
+        pruned = pruned - (q.shape[0] * 7 - out["linked"])  # minus ingest_fixed's untaken-link placeholders
+        evicted = g.enforce_limit(self.limit, now=now, alive_upper=self.rows_added)
+        return {"routed": q.shape[0], "dup": dup.sum(), "inserted": out["inserted"],
                 "linked": out["linked"] + n_cross, "pruned": pruned, "evicted": evicted}
 
 
@@ -157,10 +173,34 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
     texts = [" ".join(rng.choice(WORDS) for _ in range(12)) for _ in range(convs * facts)]
     now = [1000.0]
 
-    def step():
-        if encoder is not None:
-            ids, lens = encoder.tok.encode_batch(texts, 64)
+    # Fact embedding is pipelined one batch ahead on a side stream (as the
+    # MemorySystem's background consolidation does): batch i+1's encoder
+    # kernels fill the GPU while the host waits on batch i's data-dependent
+    # steps (compaction sizes, counts). The main stream waits for the batch's
+    # own embedding before consolidating it.
+    side = torch.cuda.Stream(dev) if encoder is not None and dev.type == "cuda" else None
+    pending = []
+
+    def launch_embed():
+        if encoder is None:
+            return
+        ids, lens = encoder.tok.encode_batch(texts, 64)
+        if side is None:
             encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=2)
+            return
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=2)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        pending.append(ev)
+
+    def step():
+        if encoder is not None and not pending:
+            launch_embed()
+        if pending:
+            torch.cuda.current_stream(dev).wait_event(pending.pop(0))
+        launch_embed()  # next batch's facts, overlapped with this batch's consolidation
         q, topic, sal = synth_facts(buf, convs * facts, dim, dup_rate, gen)
         now[0] += 60.0
         return buf.consolidate(q, topic, sal, convs * comm.world, now[0])
@@ -173,9 +213,10 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
     agg = {}
     for _ in range(steps):
         r = step()
-        for k, v in r.items():
+        for k, v in r.items():  # device counts stay on device until the end
             agg[k] = agg.get(k, 0) + v
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    agg = {k: float(v) for k, v in agg.items()}
     comm.barrier()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")

@@ -199,6 +199,63 @@ class DeviceGraph:
             self.stats[k_] += out[k_]
         return out
 
+    def ingest_fixed(self, q: torch.Tensor, shard: torch.Tensor, salience: torch.Tensor, dead: torch.Tensor,
+                     shard_hits, global_hits=None, now: Optional[float] = None, link_k: int = 3,
+                     link_thr: float = 0.5, link_scale: float = 0.8, chain_w: float = 0.5,
+                     invalid_w: float = -1.0) -> Dict[str, torch.Tensor]:
+        """Host-sync-free form of :meth:`ingest` for a pipelined caller that
+        already searched (``shard_hits`` / ``global_hits`` = (scores, rows)
+        aligned with ``q``) and decided the duplicates (``dead`` bool [M]).
+
+        Every shape is fixed by M, so no step waits for a device count: all M
+        facts get rows, the duplicates' rows are tombstoned at once (alive 0,
+        bias -inf: invisible to search, eviction and links), and all M*(2k+1)
+        candidate edges are appended with weight ``invalid_w`` where the link
+        is not taken -- the next decay/prune compaction removes them, exactly
+        as it removes weak edges. Same links as :meth:`ingest`: top-k in-shard
+        and global hits above ``link_thr`` (w = link_scale*cos, a global hit
+        already linked in-shard is skipped), chain edges between consecutive
+        KEPT facts of the same shard. Returns device counts (no .item())."""
+        now = time.time() if now is None else now
+        M = q.shape[0]
+        dev = self.device
+        if M == 0:
+            z = torch.zeros((), dtype=torch.int64, device=dev)
+            return {"deduped": z, "inserted": z, "linked": z}
+        dead = dead.to(dev).bool()
+        keep = ~dead
+        sh = shard.to(dev).to(torch.int32)
+        rows = self.add_nodes(q.to(self.emb.dtype), sh, salience.to(dev), now)
+        self.alive[rows] = keep.to(torch.uint8)
+        self.bias[rows] = torch.where(keep, 0.0, NEG_INF)
+        sw, rw = shard_hits
+        src = rows[:, None].expand(-1, link_k)
+        mw = (rw >= 0) & (sw > link_thr) & keep[:, None]
+        es, ed, ew = [src.reshape(-1)], [rw.reshape(-1)], [torch.where(mw, sw * link_scale, invalid_w).reshape(-1)]
+        n_link = mw.sum()
+        if global_hits is not None:
+            sg, rg = global_hits
+            mg = (rg >= 0) & (sg > link_thr) & keep[:, None]
+            in_shard = ((rg[:, :, None] == rw[:, None, :]) & mw[:, None, :]).any(dim=2)
+            mg = mg & ~in_shard
+            es.append(src.reshape(-1))
+            ed.append(rg.reshape(-1))
+            ew.append(torch.where(mg, sg * link_scale, invalid_w).reshape(-1))
+            n_link = n_link + mg.sum()
+        # chain: each kept fact to the previous kept fact of the batch, same shard
+        idx = torch.arange(M, device=dev)
+        prev = torch.cummax(torch.where(keep, idx, -1), 0).values
+        prev = torch.cat([torch.full((1,), -1, dtype=prev.dtype, device=dev), prev[:-1]])
+        pc = prev.clamp_min(0)
+        mc = keep & (prev >= 0) & (sh[pc] == sh)
+        es.append(rows[pc])
+        ed.append(rows)
+        ew.append(torch.where(mc, torch.full_like(salience.to(dev).float(), chain_w), invalid_w))
+        n_link = n_link + mc.sum()
+        self.add_edges(torch.cat(es), torch.cat(ed), torch.cat(ew).float(), now)
+        n_keep = keep.sum()
+        return {"deduped": M - n_keep, "inserted": n_keep, "linked": n_link}
+
     def _search_dual(self, q: torch.Tensor, k: int, q_label: torch.Tensor):
         n = self.n
         if n == 0:
@@ -219,7 +276,11 @@ class DeviceGraph:
         self.stats["pruned"] += pruned
         return pruned
 
-    def enforce_limit(self, max_nodes: int, now: Optional[float] = None) -> int:
+    def enforce_limit(self, max_nodes: int, now: Optional[float] = None, alive_upper: Optional[int] = None) -> int:
+        """``alive_upper``: a host-side upper bound on live rows (e.g. rows ever
+        added); when it is within the limit the device count is not read."""
+        if alive_upper is not None and alive_upper <= max_nodes:
+            return 0
         n_alive = self.num_alive()
         excess = n_alive - max_nodes
         if excess <= 0:

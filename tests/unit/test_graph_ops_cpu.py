@@ -91,3 +91,33 @@ def test_kmeans_cpu_separates_clusters():
     assert len(set(lab.tolist())) == 4
     for j in range(4):
         assert len(set(lab[j * 100:(j + 1) * 100].tolist())) == 1
+
+
+def test_ingest_fixed_links_and_tombstones():
+    """Sync-free batch ingest: duplicate rows are tombstoned, untaken links get
+    weight -1 (pruned by the next compaction), chains skip dead facts."""
+    import torch
+    from lazzaro_amd.index.device_graph import DeviceGraph
+    g = DeviceGraph(4, device="cpu", capacity=16)
+    g.add_nodes(torch.eye(4), torch.tensor([0, 0, 1, 1]), torch.full((4,), 0.5), now=0.0)
+    q = torch.nn.functional.normalize(torch.tensor([[1.0, 0.1, 0, 0], [0, 1.0, 0, 0], [1.0, 0.05, 0, 0],
+                                                    [0, 0, 1.0, 0.2]]), dim=1)
+    shard = torch.tensor([0, 0, 0, 1])
+    dead = torch.tensor([False, True, False, False])
+    # (scores, rows) per fact: in-shard top-2 and global top-2
+    sw = torch.tensor([[0.99, 0.1], [0.9, 0.2], [0.98, 0.05], [0.97, 0.4]])
+    rw = torch.tensor([[0, 1], [1, 0], [0, 1], [2, 3]])
+    sg = torch.tensor([[0.99, 0.6], [0.9, 0.2], [0.98, 0.45], [0.97, 0.7]])
+    rg = torch.tensor([[0, 2], [1, 0], [0, 3], [2, 0]])
+    out = g.ingest_fixed(q, shard, torch.full((4,), 0.7), dead, (sw, rw), global_hits=(sg, rg), now=1.0,
+                         link_k=2)
+    assert int(out["inserted"]) == 3 and int(out["deduped"]) == 1
+    assert g.n == 8 and g.alive[4:8].tolist() == [1, 0, 1, 1] and g.bias[5].item() == float("-inf")
+    e = g.edges
+    live = e["w"] > -1
+    got = sorted(zip(e["src"][live].tolist(), e["dst"][live].tolist(), [round(w, 3) for w in e["w"][live].tolist()]))
+    want = sorted([(4, 0, round(0.99 * 0.8, 3)), (6, 0, round(0.98 * 0.8, 3)), (7, 2, round(0.97 * 0.8, 3)),
+                   (4, 2, round(0.6 * 0.8, 3)), (7, 0, round(0.7 * 0.8, 3)),  # global hits not linked in-shard
+                   (4, 6, 0.5)])                 # chain: fact 0 -> fact 2 (fact 1 is a duplicate)
+    assert got == want, got
+    assert int(out["linked"]) == len(want)
