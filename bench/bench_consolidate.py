@@ -139,7 +139,7 @@ class ShardedBuffer:
             n_cross = cross.sum()
         # (5) decay + prune + eviction
         pruned = g.decay_prune(0.01, 0.5, conversations=convs_total)
-        pruned = pruned - (q.shape[0] * 7 - out["linked"])  # minus ingest_fixed's untaken-link placeholders
+        pruned = pruned - out["placeholders"]  # ingest_fixed's untaken-link placeholders are not prunes
         evicted = g.enforce_limit(self.limit, now=now, alive_upper=self.rows_added)
         return {"routed": q.shape[0], "dup": dup.sum(), "inserted": out["inserted"],
                 "linked": out["linked"] + n_cross, "pruned": pruned, "evicted": evicted}

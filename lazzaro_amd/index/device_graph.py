@@ -221,7 +221,7 @@ class DeviceGraph:
         dev = self.device
         if M == 0:
             z = torch.zeros((), dtype=torch.int64, device=dev)
-            return {"deduped": z, "inserted": z, "linked": z}
+            return {"deduped": z, "inserted": z, "linked": z, "placeholders": z}
         dead = dead.to(dev).bool()
         keep = ~dead
         sh = shard.to(dev).to(torch.int32)
@@ -254,7 +254,8 @@ class DeviceGraph:
         n_link = n_link + mc.sum()
         self.add_edges(torch.cat(es), torch.cat(ed), torch.cat(ew).float(), now)
         n_keep = keep.sum()
-        return {"deduped": M - n_keep, "inserted": n_keep, "linked": n_link}
+        appended = sum(int(t.numel()) for t in es)
+        return {"deduped": M - n_keep, "inserted": n_keep, "linked": n_link, "placeholders": appended - n_link}
 
     def _search_dual(self, q: torch.Tensor, k: int, q_label: torch.Tensor):
         n = self.n
