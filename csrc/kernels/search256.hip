@@ -238,33 +238,30 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
           const int rb = r0 + rl;
           f32x4 bv = {0.f, 0.f, 0.f, 0.f};
           if (HAS_BIAS) bv = *reinterpret_cast<const f32x4*>(e_bias + rl);
-          int lv[4] = {0, 0, 0, 0};
-          if (HAS_LABEL) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) lv[e] = e_lab[rl + e];
-          }
           float sc[4];
-          bool lab_ok[4];
-          float m = LZK_NEG_INF, m2 = LZK_NEG_INF;
+          float m = LZK_NEG_INF;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             sc[e] = alpha * acc[i][j][e] + bv[e];
             const bool in = full || (rb + e < nrows);
-            lab_ok[e] = !HAS_LABEL || ql[j] < 0 || lv[e] == ql[j];
-            if (!DUAL && !lab_ok[e]) sc[e] = LZK_NEG_INF;  // single search: label filters list A
             if (!in) sc[e] = LZK_NEG_INF;
+            if constexpr (HAS_LABEL && !DUAL) {  // single search: the label filters list A
+              if (ql[j] >= 0 && e_lab[rl + e] != ql[j]) sc[e] = LZK_NEG_INF;
+            }
             m = fmaxf(m, sc[e]);
-            if (DUAL && lab_ok[e]) m2 = fmaxf(m2, sc[e]);
           }
           if (m >= th[j]) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
               if (sc[e] >= th[j] && sc[e] != LZK_NEG_INF) append(cnt, cs, ci, qq[j], sc[e], rb + e);
           }
-          if (DUAL && m2 >= th2[j]) {
+          // dual: list B's label test only where a score clears its (low)
+          // threshold -- the unlabelled max bounds the labelled one
+          if (DUAL && m >= th2[j]) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (lab_ok[e] && sc[e] >= th2[j] && sc[e] != LZK_NEG_INF) append(cnt2, cs2, ci2, qq[j], sc[e], rb + e);
+              if (sc[e] >= th2[j] && sc[e] != LZK_NEG_INF && (ql[j] < 0 || e_lab[rl + e] == ql[j]))
+                append(cnt2, cs2, ci2, qq[j], sc[e], rb + e);
           }
         }
       }
