@@ -72,11 +72,11 @@ def main():
     texts = [" ".join(rng.choice("memory user likes python graph kernel music travel".split()) for _ in range(16))
              for _ in range(a.nq)]
     ids_, lens = emb.tok.encode_batch(texts, 64)
-    emb.encoder.forward(ids_, lens)
+    emb.encoder.forward_streams(ids_, lens, parts=2)
     torch.cuda.synchronize()
     t1 = time.time()
     for _ in range(3):
-        emb.encoder.forward(ids_, lens)
+        emb.encoder.forward_streams(ids_, lens, parts=2)
     torch.cuda.synchronize()
     t_embed = (time.time() - t1) / 3
     g = torch.Generator(device=dev).manual_seed(9)
