@@ -560,6 +560,72 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ 
   }
 }
 
+// Same op for H % 256 == 0 (bge-base 768, e5-large 1024): half a wave per
+// row, each lane moving C chunks of 8 features as 16-B loads and stores (H =
+// 32 lanes * 8 * C), two rows per wave-instruction, RPW row pairs per wave.
+template <int C, bool RES, int RPW>
+__global__ __launch_bounds__(256) void layernorm16_kernel(const u16* __restrict__ X, long ldx,
+                                                          const u16* __restrict__ R, long ldr,
+                                                          const float* __restrict__ g,
+                                                          const float* __restrict__ bta, int rows, float eps,
+                                                          u16* __restrict__ Y, long ldy) {
+  constexpr int H = C * 256;
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 * RPW;
+  if (row0 >= rows) return;
+  float v[RPW][C][8];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = min(row0 + 2 * rr + half, rows - 1);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int col = c * 256 + l32 * 8;
+      const u16x8 x = *reinterpret_cast<const u16x8*>(X + (long)row * ldx + col);
+      u16x8 r = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (RES) r = *reinterpret_cast<const u16x8*>(R + (long)row * ldr + col);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[rr][c][u] = bf16_to_f32(x[u]) + (RES ? bf16_to_f32(r[u]) : 0.f);
+    }
+  }
+  constexpr float invH = 1.f / H;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[rr][c][u];
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);  // within the half wave
+    const float mean = sum * invH;
+    float var = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { const float d = v[rr][c][u] - mean; var += d * d; }
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) var += __shfl_xor(var, o, 64);
+    const float rstd = rsqrtf(var * invH + eps);
+    const int row = row0 + 2 * rr + half;
+    if (row < rows) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int col = c * 256 + l32 * 8;
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + col), g1 = *reinterpret_cast<const f32x4*>(g + col + 4);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(bta + col), b1 = *reinterpret_cast<const f32x4*>(bta + col + 4);
+        u16x8 o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          o[u] = f32_to_bf16((v[rr][c][u] - mean) * rstd * g0[u] + b0[u]);
+          o[u + 4] = f32_to_bf16((v[rr][c][u + 4] - mean) * rstd * g1[u] + b1[u]);
+        }
+        *reinterpret_cast<u16x8*>(Y + (long)row * ldy + col) = o;
+      }
+    }
+  }
+}
+
 // embeddings (bf16 tables) + LayerNorm, one wave per token
 template <int NC>
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ ids, int T, int S,
@@ -825,6 +891,24 @@ LZK_EXPORT int lzk_layernorm(const void* X, long ldx, const void* R, long ldr, c
   const u16* x = (const u16*)X;
   const u16* r = (const u16*)R;
   u16* y = (u16*)Y;
+  const bool v16 = (H == 768 || H == 1024) && ldx % 8 == 0 && ldy % 8 == 0 && (!r || ldr % 8 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y) |
+                     reinterpret_cast<uintptr_t>(R)) & 15) == 0;
+  if (v16) {
+    constexpr int RP = 2;  // row pairs per wave -> 16 rows per 256-thread block
+    dim3 grid16((rows + 16 - 1) / 16);
+#define LN16(C)                                                                                                 \
+  do {                                                                                                          \
+    if (r) hipLaunchKernelGGL((layernorm16_kernel<C, true, RP>), grid16, block, 0, st, x, ldx, r, ldr, g, b,    \
+                              rows, eps, y, ldy);                                                               \
+    else hipLaunchKernelGGL((layernorm16_kernel<C, false, RP>), grid16, block, 0, st, x, ldx, r, ldr, g, b,     \
+                            rows, eps, y, ldy);                                                                 \
+  } while (0)
+    if (H == 768) LN16(3);
+    else LN16(4);
+#undef LN16
+    return (int)hipGetLastError();
+  }
 #define LN(NC)                                                                                                  \
   do {                                                                                                          \
     if (r) hipLaunchKernelGGL((layernorm_kernel<NC, true, RPW>), grid, block, 0, st, x, ldx, r, ldr, g, b, rows, \
