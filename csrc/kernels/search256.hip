@@ -24,6 +24,13 @@ namespace {
 
 using namespace g256;
 
+// Diagnostic stamps (OPT bit 8, never in a default build's path): wave 0
+// lane 0 of each block records s_memtime around the phases of its first
+// kStampTiles tiles into g_stamps[block][tile][4]: before the K loop's
+// first wait, after it, after the K loop, after the epilogue.
+constexpr int kStampTiles = 32;
+__device__ unsigned long long* g_stamps = nullptr;
+
 template <bool HAS_BIAS, bool HAS_LABEL>
 __global__ __launch_bounds__(NT, 1) void flat_cand_kernel(
     const u16* __restrict__ X, long ldx, int nrows, const u16* __restrict__ Qm, long ldq, int nq, int D,
@@ -100,7 +107,23 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_kernel(
 // drain the in-flight DMA.
 constexpr int EPI_OFF = 8 * HALF;               // u16 offset of the epilogue area (128 KiB)
 constexpr int EPI_ARRAYS = 5;                   // thr | bias | row label | query label | thr2
-constexpr int CAND_P_LDS = LDS_BYTES + 2 * EPI_ARRAYS * 256 * 4;
+constexpr int CNT_OFF = EPI_OFF + 2 * EPI_ARRAYS * 256 * 2;  // u16 offset of the block's append counter
+constexpr int CAND_P_LDS = LDS_BYTES + 2 * EPI_ARRAYS * 256 * 4 + 16;
+typedef __attribute__((address_space(3))) int lds_int;
+
+// Candidate appends go to a block-private region (no returning global
+// atomic in the scan): the slot comes from an LDS counter (ds_add_rtn, an
+// lgkmcnt wait) and the (query, row, score, list) record is a plain 16-B
+// store. A returning global atomic would make the compiler wait vmcnt(0) --
+// i.e. for the next tile's in-flight operand DMA -- in the middle of the
+// epilogue, and would break the counted vmcnt at the next K loop's start.
+// cand_gather_kernel then files the records into the per-query lists. A
+// record that does not fit marks its query overflowed (exact fallback).
+struct BlkCands {
+  int4* buf;  // [grid][cap]
+  int cap;
+  int* cnt;   // [grid] records written
+};
 
 // DUAL: one GEMM pass serves two searches of the same queries -- list A keeps
 // every row with score >= thr[q] (no label filter), list B keeps rows whose
@@ -114,10 +137,12 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     const float* __restrict__ bias, const int* __restrict__ row_label, const int* __restrict__ q_label,
     float alpha, const float* __restrict__ thr, int n_qt, int n_tiles, int cap, int* __restrict__ cnt,
     float* __restrict__ cs, int* __restrict__ ci, const float* __restrict__ thr2, int* __restrict__ cnt2,
-    float* __restrict__ cs2, int* __restrict__ ci2) {
+    float* __restrict__ cs2, int* __restrict__ ci2, BlkCands blk) {
   static_assert(!DUAL || HAS_LABEL, "dual search needs labels");
   extern __shared__ __attribute__((aligned(16))) u16 smem[];
   float* epi = reinterpret_cast<float*>(smem + EPI_OFF);  // [parity][array][256]
+  lds_int* lcnt = (lds_int*)(smem + CNT_OFF);
+  if (threadIdx.x == 0) *lcnt = 0;  // ordered before any append by the K loop's barriers
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -126,7 +151,10 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
   TileWalk walk;
   walk.init(n_tiles);
   int tile = walk.next;
-  if (!walk.valid(tile)) return;
+  if (!walk.valid(tile)) {
+    if (threadIdx.x == 0) blk.cnt[blockIdx.x] = 0;
+    return;
+  }
 
   // 4 wave-level DMAs (64 x 4 B) per array, spread over the 8 waves
   auto stage_epi = [&](int tl, int par) {
@@ -147,12 +175,12 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     }
   };
 
-  auto append = [&](int* cn, float* cv, int* cix, int q, float v, int r) {
-    const int pos = atomicAdd(cn + q, 1);
-    if (pos < cap) {
-      cv[(long)q * cap + pos] = v;
-      cix[(long)q * cap + pos] = r;
-    }
+  // one record per (query, row) with its list mask (bit 0: list A, bit 1:
+  // list B): one append site per score keeps the fully unrolled epilogue
+  // small -- the kernel's code must stay inside the CU's instruction cache
+  auto append = [&](int lists, int q, float v, int r) {
+    const int pos = __atomic_fetch_add(lcnt, 1, __ATOMIC_RELAXED);
+    if (pos < blk.cap) blk.buf[(long)blockIdx.x * blk.cap + pos] = make_int4(q, r, __float_as_int(v), lists);
   };
 
   Stager st;
@@ -163,6 +191,15 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
   const bool can_pre = ((OPT & 32) != 0) && (KS % 2 == 0);
   int par = 0;
   f32x4 acc[8][4];
+  int tix = 0;
+  auto stamp = [&](int slot) {
+    if constexpr ((OPT & 256) != 0) {
+      unsigned long long t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      if (threadIdx.x == 0 && tix < kStampTiles && g_stamps)
+        g_stamps[((long)blockIdx.x * kStampTiles + tix) * 4 + slot] = t;
+    }
+  };
   while (true) {
     const int cur = tile, cpar = par;
     tile += walk.step;
@@ -170,8 +207,15 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     const int nr0 = (tile / n_qt) * BM, nc0 = (tile % n_qt) * BN;
     auto exn = [&]() { stage_epi(tile, cpar ^ 1); };
     const NextTile<decltype(exn)> pre{X, ldx, nr0, nrows, Qm, ldq, nc0, nq, &exn, more && can_pre};
+    if constexpr ((OPT & 256) != 0) {  // diagnostic: the K loop's first wait, stamped on its own
+      stamp(0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      bar();
+      stamp(1);
+    }
     if constexpr ((OPT & 8) != 0) body2<MmaBf16>(smem, st, KS, acc, !(OPT & 2), pre);
     else body<MmaBf16, (OPT & 3)>(smem, st, KS, acc, pre);
+    stamp(2);
     if (more) {
       st.setup(X, ldx, nr0, nrows, Qm, ldq, nc0, nq);
       if (!can_pre) prologue<decltype(exn), OPT>(smem, st, KS, exn);
@@ -186,7 +230,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e) m = fmaxf(m, acc[i][j][e]);
-      if (m > 1e30f) append(cnt, cs, ci, 0, m, cur);
+      if (m > 1e30f) append(1, 0, m, cur);
       if (!more) break;
       par = cpar ^ 1;
       continue;
@@ -250,24 +294,64 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
             }
             m = fmaxf(m, sc[e]);
           }
-          if (m >= th[j]) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (sc[e] >= th[j] && sc[e] != LZK_NEG_INF) append(cnt, cs, ci, qq[j], sc[e], rb + e);
-          }
           // dual: list B's label test only where a score clears its (low)
           // threshold -- the unlabelled max bounds the labelled one
-          if (DUAL && m >= th2[j]) {
+          const float tlo = DUAL ? fminf(th[j], th2[j]) : th[j];
+          if (m >= tlo) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (sc[e] >= th2[j] && sc[e] != LZK_NEG_INF && (ql[j] < 0 || e_lab[rl + e] == ql[j]))
-                append(cnt2, cs2, ci2, qq[j], sc[e], rb + e);
+            for (int e = 0; e < 4; ++e) {
+              int lists = (sc[e] >= th[j]) ? 1 : 0;
+              if (DUAL && sc[e] >= th2[j] && (ql[j] < 0 || e_lab[rl + e] == ql[j])) lists |= 2;
+              if (lists && sc[e] != LZK_NEG_INF) append(lists, qq[j], sc[e], rb + e);
+            }
           }
         }
       }
     }
+    stamp(3);
+    ++tix;
     if (!more) break;
     par = cpar ^ 1;
+  }
+  bar();  // every wave's appends done
+  if (threadIdx.x == 0) blk.cnt[blockIdx.x] = *lcnt;  // > cap: records were dropped
+}
+
+// Files the block-private candidate records into the per-query lists read by
+// cand_select_kernel (cnt zeroed by the caller before the scan). A block that
+// dropped records (count > bcap: pathological score distributions) marks
+// every query overflowed, so the select's exact fallback recomputes them all.
+__global__ __launch_bounds__(256) void cand_gather_kernel(const int4* __restrict__ buf, int bcap,
+                                                          const int* __restrict__ bcnt, int cap, int nq,
+                                                          int* __restrict__ cnt, float* __restrict__ cs,
+                                                          int* __restrict__ ci, int* __restrict__ cnt2,
+                                                          float* __restrict__ cs2, int* __restrict__ ci2) {
+  const int b = blockIdx.y;
+  const int n0 = bcnt[b];
+  if (n0 > bcap) {
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += gridDim.x * 256) {
+      atomicOr(cnt + q, 0x40000000);  // idempotent across blocks: the count stays positive
+      if (cnt2) atomicOr(cnt2 + q, 0x40000000);
+    }
+  }
+  const int n = min(n0, bcap);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+    const int4 v = buf[(long)b * bcap + e];
+    if ((unsigned)v.x >= (unsigned)nq) continue;  // (a +inf score of a padding query column)
+    if (v.w & 1) {
+      const int pos = atomicAdd(cnt + v.x, 1);
+      if ((unsigned)pos < (unsigned)cap) {
+        cs[(long)v.x * cap + pos] = __int_as_float(v.z);
+        ci[(long)v.x * cap + pos] = v.y;
+      }
+    }
+    if (v.w & 2) {
+      const int pos = atomicAdd(cnt2 + v.x, 1);
+      if ((unsigned)pos < (unsigned)cap) {
+        cs2[(long)v.x * cap + pos] = __int_as_float(v.z);
+        ci2[(long)v.x * cap + pos] = v.y;
+      }
+    }
   }
 }
 
@@ -356,13 +440,19 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
+LZK_EXPORT int lzk_set_stamp_buffer(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p));
+}
+LZK_EXPORT int lzk_stamp_tiles() { return kStampTiles; }
 
 // Candidate pass. cnt [nq] must be zeroed by the caller (same stream);
 // cs/ci are [nq, cap].
 LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, int D,
                              const float* bias, const int* row_label, const int* q_label, float alpha,
-                             const float* thr, int cap, int* cnt, float* cs, int* ci, void* stream) {
+                             const float* thr, int cap, int* cnt, float* cs, int* ci, void* blk_buf, int blk_cap,
+                             int* blk_cnt, void* stream) {
   if (D % BK != 0 || nq <= 0 || nrows <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
+  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt};
   if (row_label && !q_label) return (int)hipErrorInvalidValue;
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
@@ -381,6 +471,7 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
       g_n_cu = 256;
   }
   if (g_cand_persist && nblk >= g_n_cu) {
+    if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;  // lzk_cand_grid() > 0: records needed
     const int grid = g_n_cu;
 #define LZK_GP(B, L)                                                                                                \
   do {                                                                                                              \
@@ -388,7 +479,7 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
                               hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
     hipLaunchKernelGGL((flat_cand_persistent_kernel<B, L, false, kCandOpt>), dim3(grid), dim3(NT), CAND_P_LDS, st, x, ldx,    \
                        nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs,   \
-                       ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr);                    \
+                       ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr, blk);               \
   } while (0)
     if (bias && row_label) LZK_GP(true, true);
     else if (bias) LZK_GP(true, false);
@@ -400,7 +491,7 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
                               hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
     hipLaunchKernelGGL((flat_cand_persistent_kernel<false, false, false, O>), dim3(grid), dim3(NT), CAND_P_LDS, st, \
                        x, ldx, nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap,    \
-                       cnt, cs, ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr);          \
+                       cnt, cs, ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr, blk);     \
   } while (0)
       switch (g_g256_opt) {
         case 1: LZK_GX(1); break;
@@ -410,6 +501,8 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
         case 16: LZK_GX(16); break;
         case 24: LZK_GX(24); break;
         case 26: LZK_GX(26); break;
+        case 280: LZK_GX(280); break;
+        case 312: LZK_GX(312); break;
         case 32: LZK_GX(32); break;
         case 36: LZK_GX(36); break;
         case 40: LZK_GX(40); break;
@@ -443,7 +536,10 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
 LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, int D,
                                   const float* bias, const int* row_label, const int* q_label, float alpha,
                                   const float* thr, const float* thr2, int cap, int* cnt, float* cs, int* ci,
-                                  int* cnt2, float* cs2, int* ci2, void* stream) {
+                                  int* cnt2, float* cs2, int* ci2, void* blk_buf, int blk_cap, int* blk_cnt,
+                                  void* stream) {
+  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt};
+  if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;
   if (D % BK != 0 || nq <= 0 || nrows <= 0 || cap <= 0 || !row_label || !q_label) return (int)hipErrorInvalidValue;
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
@@ -464,7 +560,7 @@ LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void
                               hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
     hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true, O>), dim3(grid), dim3(NT), CAND_P_LDS, st, x,    \
                        ldx, nrows, q, ldq, nq, D, bias, row_label, q_label, alpha, thr, n_qt, (int)nblk, cap, cnt,  \
-                       cs, ci, thr2, cnt2, cs2, ci2);                                                               \
+                       cs, ci, thr2, cnt2, cs2, ci2, blk);                                                          \
   } while (0)
 #define LZK_GD(B)                              \
   do {                                         \
@@ -500,4 +596,31 @@ LZK_EXPORT int lzk_cand_select(const int* cnt, const float* cs, const int* ci, i
   }
 #undef LZK_SEL
   return (int)hipGetLastError();
+}
+
+// Records of the last candidate pass -> per-query lists (grid = the pass's grid).
+LZK_EXPORT int lzk_cand_gather(const void* blk_buf, int blk_cap, const int* blk_cnt, int grid, int cap, int nq,
+                               int* cnt, float* cs, int* ci, int* cnt2, float* cs2, int* ci2, void* stream) {
+  if (grid <= 0 || blk_cap <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cand_gather_kernel, dim3(4, grid), dim3(256), 0, (hipStream_t)stream, (const int4*)blk_buf,
+                     blk_cap, blk_cnt, cap, nq, cnt, cs, ci, cnt2, cs2, ci2);
+  return (int)hipGetLastError();
+}
+
+// Grid of the persistent candidate pass for a shape (the gather's grid); 0
+// when lzk_flat_cand would take the non-persistent kernel (global appends).
+LZK_EXPORT int lzk_cand_grid(int nrows, int nq, int dual) {
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  if (g_cand_persist < 0) {
+    const char* e = getenv("LZK_CAND_PERSIST");
+    g_cand_persist = (e && e[0] == '0') ? 0 : 1;
+  }
+  const long nblk = (long)((nrows + BM - 1) / BM) * ((nq + BN - 1) / BN);
+  if (dual) return (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  return (g_cand_persist && nblk >= g_n_cu) ? g_n_cu : 0;
 }

@@ -81,6 +81,19 @@ _ws = _Workspace()
 _ws_cand = _Workspace()
 _ws_cand2 = _Workspace()
 _ws_fallback = _Workspace()
+_ws_blk = _Workspace()
+
+
+def _blk_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
+    """Block-private candidate records of one persistent pass (search256.hip
+    BlkCands): int4 [grid, cap] + int32 counts [grid]; cap ~8x the expected
+    records per block (a block that overflows marks its queries for the
+    exact fallback)."""
+    cap = max(8192, 8 * lists * nq * kslot * S // max(grid, 1))
+    ws = _ws_blk.get(dev, grid * cap * 16 + grid * 4)
+    buf = ws[: grid * cap * 16]
+    cnt = ws[grid * cap * 16: grid * cap * 16 + grid * 4].view(torch.int32)
+    return buf, cap, cnt
 
 # Large-batch candidate path (csrc/kernels/search256.hip): used when the batch
 # fills whole 256-query tiles and the arena is large enough that the strided
@@ -231,10 +244,20 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
     thr = _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S)
     cap = max(1024, 8 * kslot * S)
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    grid = L.lzk_cand_grid(N, nq, 0)
+    st = _lib.stream_ptr(dev)
+    if grid > 0:
+        bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, S, 1)
+        bargs = (bbuf.data_ptr(), bcap, bcnt.data_ptr())
+    else:
+        bargs = (None, 0, None)
     rc = L.lzk_flat_cand(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D,
                          _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha),
-                         thr.data_ptr(), cap, cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), _lib.stream_ptr(dev))
+                         thr.data_ptr(), cap, cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), *bargs, st)
     _lib.check(rc, "lzk_flat_cand")
+    if grid > 0:
+        _lib.check(L.lzk_cand_gather(bargs[0], bcap, bargs[2], grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
+                                     ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
     return _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap)
 
 
@@ -268,11 +291,18 @@ def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_lab
     cap = max(1024, 8 * kslot * S)
     ca = _cand_lists(dev, nq, cap, 0)
     cb = _cand_lists(dev, nq, cap, 1)
+    grid = L.lzk_cand_grid(N, nq, 1)
+    bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, S, 2)
+    st = _lib.stream_ptr(dev)
     rc = L.lzk_flat_cand_dual(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D, _lib.ptr(bias),
                               row_label.data_ptr(), q_label.data_ptr(), float(alpha), thr_a.data_ptr(),
                               thr_b.data_ptr(), cap, ca[0].data_ptr(), ca[1].data_ptr(), ca[2].data_ptr(),
-                              cb[0].data_ptr(), cb[1].data_ptr(), cb[2].data_ptr(), _lib.stream_ptr(dev))
+                              cb[0].data_ptr(), cb[1].data_ptr(), cb[2].data_ptr(), bbuf.data_ptr(), bcap,
+                              bcnt.data_ptr(), st)
     _lib.check(rc, "lzk_flat_cand_dual")
+    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, ca[0].data_ptr(),
+                                 ca[1].data_ptr(), ca[2].data_ptr(), cb[0].data_ptr(), cb[1].data_ptr(),
+                                 cb[2].data_ptr(), st), "lzk_cand_gather")
     ra = _select_with_fallback(X, Q, k, kslot, bias, None, None, alpha, idx_offset, *ca, cap)
     rb = _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, *cb, cap)
     return ra, rb
