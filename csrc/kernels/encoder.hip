@@ -773,14 +773,15 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     // measured (bench/ab_body.py, profiles/ab_body_r1.json): with the two-phase main loop the
     // 256x256 pipeline beats the 128x128 kernel even on half the chip -- bge-base O / FFN2
     // (N = 768) at 11k tokens: 132 tiles, 24 / 60 us vs 34 / 90 us -- so every grid of at
-    // least 128 tiles takes it; the whole 2-stream bench forward 5.72 -> 5.13 ms
+    // least 64 tiles takes it (from 128: bench forward 5.72 -> 5.13 ms; from 64: the consolidation
+    // bench's 7k-token fact halves 21.8 -> 21.1 ms per step)
     if (g_g256_min_n < 0) {
       const char* e = getenv("LZK_G256_MIN_N");
       g_g256_min_n = e ? atoi(e) : 768;
     }
     if (g_g256_min_tiles < 0) {
       const char* e = getenv("LZK_G256_MIN_TILES");
-      g_g256_min_tiles = e ? atoi(e) : 128;
+      g_g256_min_tiles = e ? atoi(e) : 64;
     }
     if (g_gemm_tile == 256 && n_ft * n_tt >= g_g256_min_tiles && N >= g_g256_min_n && N % 8 == 0 && ldy % 8 == 0 &&
         (!R || ldr % 8 == 0)) {

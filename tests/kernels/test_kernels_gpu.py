@@ -85,9 +85,10 @@ def _rel(a, b):
 @pytest.mark.parametrize("T,N,K,act,res", [(300, 768, 768, "none", False), (64, 2304, 768, "none", False),
                                            (257, 3072, 768, "gelu", False), (129, 768, 3072, "none", True),
                                            (1000, 384, 384, "gelu", True),
-                                           # grids of >= 128 tiles of 256x256 take the 8-wave pipeline
+                                           # grids of >= 64 tiles of 256x256 take the 8-wave pipeline
                                            (8200, 2304, 768, "none", False), (4100, 3072, 768, "gelu", False),
                                            (11300, 768, 768, "none", True), (11001, 768, 3072, "none", True),
+                                           (6000, 768, 3072, "none", True), (5000, 768, 768, "none", True),
                                            (16385, 1024, 3072, "none", True), (21000, 1024, 768, "gelu", True),
                                            # T <= 64: skinny weight-streaming kernel
                                            (1, 768, 768, "gelu", True), (17, 3072, 768, "none", False),
