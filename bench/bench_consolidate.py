@@ -180,11 +180,18 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
     # own embedding before consolidating it.
     side = torch.cuda.Stream(dev) if encoder is not None and dev.type == "cuda" else None
     pending = []
+    tokens = []  # host-tokenised batches, one step ahead of their embedding launch
+
+    def tokenize():
+        if encoder is not None:
+            tokens.append(encoder.tok.encode_batch(texts, 64))
 
     def launch_embed():
         if encoder is None:
             return
-        ids, lens = encoder.tok.encode_batch(texts, 64)
+        if not tokens:
+            tokenize()
+        ids, lens = tokens.pop(0)
         if side is None:
             encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=2)
             return
@@ -201,6 +208,7 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
         if pending:
             torch.cuda.current_stream(dev).wait_event(pending.pop(0))
         launch_embed()  # next batch's facts, overlapped with this batch's consolidation
+        tokenize()      # the batch after next, on the host while the GPU has queued work
         q, topic, sal = synth_facts(buf, convs * facts, dim, dup_rate, gen)
         now[0] += 60.0
         return buf.consolidate(q, topic, sal, convs * comm.world, now[0])
