@@ -64,16 +64,21 @@ def _ref_topk(X, Q, k, bias=None, row_label=None, q_label=None, alpha=1.0, idx_o
 
 
 class _Workspace:
-    """Per-device scratch for partial top-k lists (grown, never shrunk)."""
+    """Scratch for partial / candidate lists (grown, never shrunk), one buffer
+    per (device, stream): kernels on one stream reuse it in stream order, and
+    two streams searching at once (e.g. background consolidation on its side
+    stream beside retrieval on the main stream) never share one."""
 
     def __init__(self):
         self.buf = {}
 
     def get(self, dev, nbytes):
-        b = self.buf.get(dev)
+        dev = torch.device(dev)
+        key = (dev, torch.cuda.current_stream(dev).cuda_stream) if dev.type == "cuda" else (dev, 0)
+        b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
             b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
-            self.buf[dev] = b
+            self.buf[key] = b
         return b
 
 

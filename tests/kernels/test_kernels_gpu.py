@@ -325,3 +325,29 @@ def test_layernorm_shapes(T, H, res):
     y = E.layernorm(x, g, b, 1e-12, residual=r)
     yr = E.layernorm(x.cpu(), g.cpu(), b.cpu(), 1e-12, residual=None if r is None else r.cpu())
     assert _rel(y.cpu(), yr) < 1e-2
+
+
+def test_concurrent_streams_do_not_share_workspaces():
+    """Searches issued on two HIP streams at once (retrieval beside background
+    consolidation) each get their own scratch lists."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    X1 = torch.randn(200_000, 256, device=DEV, generator=g).to(torch.bfloat16)
+    X2 = torch.randn(150_000, 256, device=DEV, generator=g).to(torch.bfloat16)
+    Q1 = torch.randn(3, 256, device=DEV, generator=g).to(torch.bfloat16)
+    Q2 = torch.randn(5, 256, device=DEV, generator=g).to(torch.bfloat16)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(4):
+        with torch.cuda.stream(s1):
+            a = flat_topk(X1, Q1, 10)
+        with torch.cuda.stream(s2):
+            b = flat_topk(X2, Q2, 10)
+        outs.append((a, b))
+    torch.cuda.synchronize()
+    ra = _ref_topk(X1.cpu(), Q1.cpu(), 10)
+    rb = _ref_topk(X2.cpu(), Q2.cpu(), 10)
+    for (sa, ia), (sb, ib) in outs:
+        torch.testing.assert_close(sa.cpu(), ra[0], atol=2e-3, rtol=1e-4)
+        torch.testing.assert_close(sb.cpu(), rb[0], atol=2e-3, rtol=1e-4)
+        assert (ia.cpu() == ra[1]).float().mean() > 0.99 and (ib.cpu() == rb[1]).float().mean() > 0.99
