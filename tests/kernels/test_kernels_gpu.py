@@ -351,3 +351,21 @@ def test_concurrent_streams_do_not_share_workspaces():
         torch.testing.assert_close(sa.cpu(), ra[0], atol=2e-3, rtol=1e-4)
         torch.testing.assert_close(sb.cpu(), rb[0], atol=2e-3, rtol=1e-4)
         assert (ia.cpu() == ra[1]).float().mean() > 0.99 and (ib.cpu() == rb[1]).float().mean() > 0.99
+
+
+def test_forward_streams_matches_forward():
+    """Two-stream sub-batch forward (the bench's embed path) == one forward,
+    on a batch large enough for the 256x256 GEMM paths."""
+    from lazzaro_amd.models.encoder import SentenceEncoder
+    enc = SentenceEncoder("bge-base", device=DEV, seed=2)
+    g = torch.Generator().manual_seed(5)
+    B = 1024
+    ids = torch.randint(1000, 30000, (B, 32), dtype=torch.int32, generator=g)
+    lens = torch.randint(12, 27, (B,), dtype=torch.int32, generator=g)
+    for b in range(B):
+        ids[b, lens[b]:] = 0
+    a32, a16 = enc.forward(ids, lens, pad_to=768)
+    b32, b16 = enc.forward_streams(ids, lens, pad_to=768, parts=2)
+    torch.cuda.synchronize()
+    assert ((a32 * b32).sum(1) > 0.9999).all()
+    assert torch.equal(a16, b16) or (a16.float() - b16.float()).abs().max() < 1e-2
