@@ -21,36 +21,52 @@ namespace {
 
 using namespace lzk;
 
-// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
-// output resolution): 18 VALU ops with one v_rcp and one v_exp and no branch,
-// vs ~40 with divergent branches for the libm erff. The GEMM epilogue is not
-// overlapped with MFMA work at one block per CU, so its VALU count is wall time.
-__device__ __forceinline__ float erf_fast(float z) {
-  const float a = fabsf(z);
-  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * a);
-  const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  const float y = 1.f - p * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
-  return copysignf(y, z);
-}
+// GELU(x) = x/2 (1 + erf(x/sqrt2)) with erf as an odd degree-17 polynomial
+// z P(z^2) (least-squares minimax fit on |z| <= 3, coefficients below), z
+// clamped to +-Zc beyond. The polynomial's terms cancel heavily near |z| = 3,
+// so its value there depends on the FMA evaluation order at the 1e-5 level;
+// the negative tail therefore clamps x itself (x >= -Zc sqrt2): GELU of any
+// x below is returned as GELU(-4.24) ~ 1e-5 (true value < 5e-5) instead of
+// x * 1e-5 growing with |x|. |error| < 1e-4 over the fp32 range (test:
+// tests/kernels/test_kernels_gpu.py::test_gelu_polynomial_extremes), far below
+// a bf16 ulp of the output. Only FMAs -- no v_rcp / v_exp, which issue at a
+// quarter of the VALU rate (the erf-based epilogue cost the FFN1 tiles ~6 us
+// per 256x256 tile at 11k tokens).
+#define LZK_GELU_P(X) \
+  X(1.128268480e+00f) X(-3.753148913e-01f) X(1.110793427e-01f) X(-2.510286681e-02f) X(4.235429689e-03f) \
+  X(-5.110373604e-04f) X(4.106058259e-05f) X(-1.944826636e-06f) X(4.074221138e-08f)
+constexpr float kGeluZc = 3.000014066696167f;
+constexpr float kGeluXc = 4.2426605f;  // Zc * sqrt(2)
+constexpr float kGeluC[9] = {
+#define LZK_C(v) v,
+    LZK_GELU_P(LZK_C)
+#undef LZK_C
+};
 
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f));
+  const float xc = fmaxf(x, -kGeluXc);
+  const float z = fminf(xc * 0.70710678118654752f, kGeluZc);
+  const float u = z * z;
+  float p = kGeluC[8];
+#pragma unroll
+  for (int k = 7; k >= 0; --k) p = __builtin_fmaf(p, u, kGeluC[k]);
+  const float hx = 0.5f * xc;
+  return __builtin_fmaf(hx, p * z, hx);
 }
 
-// Two lanes of work per instruction: the polynomial and the scaling run as
-// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32), only v_rcp / v_exp stay scalar
-// -- ~10 VALU ops per element instead of ~18.
+// Two lanes of work per instruction: the clamps are scalar v_max / v_min,
+// everything else packed fp32 (v_pk_mul_f32 / v_pk_fma_f32).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
-  const f32x2 z = x * 0.70710678118654752f;
-  const f32x2 a = __builtin_elementwise_abs(z);
-  const f32x2 d = 1.f + 0.3275911f * a;
-  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  const f32x2 p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  const f32x2 e = -a * a * 1.4426950408889634f;
-  const f32x2 ex = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-  const f32x2 erf = __builtin_elementwise_copysign(1.f - p * ex, z);
-  return 0.5f * x * (1.f + erf);
+  const f32x2 xc = {fmaxf(x.x, -kGeluXc), fmaxf(x.y, -kGeluXc)};
+  const f32x2 zs = xc * 0.70710678118654752f;
+  const f32x2 z = {fminf(zs.x, kGeluZc), fminf(zs.y, kGeluZc)};
+  const f32x2 u = z * z;
+  f32x2 p = {kGeluC[8], kGeluC[8]};
+#pragma unroll
+  for (int k = 7; k >= 0; --k) p = __builtin_elementwise_fma(p, u, (f32x2){kGeluC[k], kGeluC[k]});
+  const f32x2 hx = 0.5f * xc;
+  return __builtin_elementwise_fma(hx, p * z, hx);
 }
 
 // ---------------------------------------------------------------- GEMM
@@ -738,6 +754,9 @@ static int g_g256_min_n = -1;  // smallest N routed to the 256x256 pipeline (LZK
 LZK_EXPORT void lzk_set_g256_min_n(int n) { g_g256_min_n = n; }
 static int g_g256_min_tiles = -1;  // smallest grid routed to the 256x256 pipeline (LZK_G256_MIN_TILES)
 LZK_EXPORT void lzk_set_g256_min_tiles(int n) { g_g256_min_tiles = n; }
+static int g_g256_tail = -1;  // largest last-round fill (% of the CUs) split off to the 128x128 kernel (LZK_G256_TAIL)
+LZK_EXPORT void lzk_set_g256_tail(int pct) { g_g256_tail = pct; }
+static int g_n_cu_enc = 0;
 
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
@@ -764,6 +783,21 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
 #undef SK
     return (int)hipGetLastError();
   }
+  // 128x128 launch over token rows [0, Tn) of x / r / y
+  auto launch128 = [&](const u16* x, int Tn, const u16* r, u16* y, int tiles, int nft) {
+    dim3 grid(tiles), block(TNT);
+    const size_t lds = 2 * 2 * TELEMS * sizeof(u16);
+    const u16* w = (const u16*)W;
+#define GO(A, RS, G) hipLaunchKernelGGL((gemm_bias_act_kernel<A, RS, G>), grid, block, lds, st, x, ldx, Tn, w, ldw, N, bias, r, ldr, y, ldy, K, nft)
+    if (g_gemm_staging) {
+      if (act == 1) { if (r) GO(1, true, true); else GO(1, false, true); }
+      else { if (r) GO(0, true, true); else GO(0, false, true); }
+    } else {
+      if (act == 1) { if (r) GO(1, true, false); else GO(1, false, false); }
+      else { if (r) GO(0, true, false); else GO(0, false, false); }
+    }
+#undef GO
+  };
   if (g_gemm_tile < 0) {
     const char* e = getenv("LZK_GEMM_TILE");
     g_gemm_tile = (e && atoi(e) == 128) ? 128 : 256;
@@ -783,13 +817,11 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
       const char* e = getenv("LZK_G256_MIN_TILES");
       g_g256_min_tiles = e ? atoi(e) : 64;
     }
-    if (g_gemm_tile == 256 && n_ft * n_tt >= g_g256_min_tiles && N >= g_g256_min_n && N % 8 == 0 && ldy % 8 == 0 &&
-        (!R || ldr % 8 == 0)) {
-      const u16* x = (const u16*)X;
-      const u16* w = (const u16*)W;
-      const u16* r = (const u16*)R;
-      u16* y = (u16*)Y;
-      dim3 grid(n_ft * n_tt), block(g256::NT);
+    const u16* w = (const u16*)W;
+    // 256x256 launch over token rows [0, Tn) of x / r / y
+    auto launch256 = [&](const u16* x, int Tn, const u16* r, u16* y) {
+      const int ntt = (Tn + g256::BN - 1) / g256::BN;
+      dim3 grid(n_ft * ntt), block(g256::NT);
       if (g_g256_body < 0) {
         const char* e = getenv("LZK_G256_BODY");
         g_g256_body = e ? atoi(e) : 1;  // body2: 2-4 % faster on the bge-base projections (bench/ab_body.py)
@@ -798,7 +830,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   do {                                                                                                        \
     (void)hipFuncSetAttribute((const void*)gemm256_bias_act_kernel<A, RS, BD>,                                \
                               hipFuncAttributeMaxDynamicSharedMemorySize, G256_GEMM_LDS);                     \
-    hipLaunchKernelGGL((gemm256_bias_act_kernel<A, RS, BD>), grid, block, G256_GEMM_LDS, st, x, ldx, T, w,  \
+    hipLaunchKernelGGL((gemm256_bias_act_kernel<A, RS, BD>), grid, block, G256_GEMM_LDS, st, x, ldx, Tn, w,   \
                        ldw, N, bias, r, ldr, y, ldy, K, n_ft);                                                \
   } while (0)
 #define GO(A, RS)                        \
@@ -812,25 +844,51 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
       else { if (r) GO(0, true); else GO(0, false); }
 #undef GO
 #undef GO1
+    };
+    if (g_gemm_tile == 256 && n_ft * n_tt >= g_g256_min_tiles && N >= g_g256_min_n && N % 8 == 0 && ldy % 8 == 0 &&
+        (!R || ldr % 8 == 0)) {
+      const u16* x = (const u16*)X;
+      const u16* r = (const u16*)R;
+      u16* y = (u16*)Y;
+      // Tile-quantisation tail: a grid of n_cu * q + f tiles costs q + 1 full
+      // rounds of 256x256 tiles. When the last round would be at most
+      // g_g256_tail % full, the 256x256 kernel takes only the token rows that
+      // fill whole rounds and the leftover rows (< 1 round of tiles, usually a
+      // few hundred tokens) go to the 128x128 kernel, whose 4x smaller tiles
+      // spread them over 4x more CUs (bge-base FFN2 at 22.6k tokens: 267 tiles
+      // = 255 + 825 tokens).
+      if (g_n_cu_enc <= 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&g_n_cu_enc, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            g_n_cu_enc <= 0)
+          g_n_cu_enc = 256;
+      }
+      if (g_g256_tail < 0) {
+        const char* e = getenv("LZK_G256_TAIL");
+        // off by default: in isolation FFN2 at 22.6k tokens gains 132 -> 119 us, but the
+        // 128x128 tail kernels run at ~1/4 of the per-CU rate (one small tile per CU) and the
+        // whole forward loses (bench/ab_tail.py, profiles/ab_tail_r1.json: 1 stream 5.54 ->
+        // 5.76 ms, 2 streams 4.97 -> 5.11 ms)
+        g_g256_tail = e ? atoi(e) : 0;
+      }
+      const int tiles = n_ft * n_tt, P = g_n_cu_enc;
+      const int q = tiles / P, f = tiles - q * P;
+      const int tt0 = (q * P) / n_ft;  // whole token tiles inside q full rounds
+      if (q >= 1 && f > 0 && f * 100 <= g_g256_tail * P && tt0 > 0 && act != 9 && act != 10) {
+        const int T0 = tt0 * g256::BN;
+        launch256(x, T0, r, y);
+        const int T1 = T - T0;
+        const int n128 = (N + TB - 1) / TB, t128 = (T1 + TB - 1) / TB;
+        launch128(x + (long)T0 * ldx, T1, r ? r + (long)T0 * ldr : nullptr, y + (long)T0 * ldy, n128 * t128, n128);
+        return (int)hipGetLastError();
+      }
+      launch256(x, T, r, y);
       return (int)hipGetLastError();
     }
   }
   const int n_ft = (N + TB - 1) / TB, n_tt = (T + TB - 1) / TB;
-  dim3 grid(n_ft * n_tt), block(TNT);
-  const size_t lds = 2 * 2 * TELEMS * sizeof(u16);
-  const u16* x = (const u16*)X;
-  const u16* w = (const u16*)W;
-  const u16* r = (const u16*)R;
-  u16* y = (u16*)Y;
-#define GO(A, RS, G) hipLaunchKernelGGL((gemm_bias_act_kernel<A, RS, G>), grid, block, lds, st, x, ldx, T, w, ldw, N, bias, r, ldr, y, ldy, K, n_ft)
-  if (g_gemm_staging) {
-    if (act == 1) { if (r) GO(1, true, true); else GO(1, false, true); }
-    else { if (r) GO(0, true, true); else GO(0, false, true); }
-  } else {
-    if (act == 1) { if (r) GO(1, true, false); else GO(1, false, false); }
-    else { if (r) GO(0, true, false); else GO(0, false, false); }
-  }
-#undef GO
+  launch128((const u16*)X, T, (const u16*)R, (u16*)Y, n_ft * n_tt, n_ft);
   return (int)hipGetLastError();
 }
 

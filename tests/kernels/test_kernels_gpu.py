@@ -369,3 +369,21 @@ def test_forward_streams_matches_forward():
     torch.cuda.synchronize()
     assert ((a32 * b32).sum(1) > 0.9999).all()
     assert torch.equal(a16, b16) or (a16.float() - b16.float()).abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("T", [48, 64 * 5, 6144])
+def test_gelu_polynomial_extremes(T):
+    """The FMA-only GELU (odd polynomial erf, exact saturation) over the whole
+    fp32 range through the three GEMM paths (skinny, 128x128, 256x256 from 64
+    tiles): identity weights make the GEMM exact, so the output is GELU(x)."""
+    from lazzaro_amd.ops import encoder_ops as E
+    g = torch.Generator().manual_seed(3)
+    K = 768
+    x = torch.cat([torch.linspace(-8, 8, T * K // 2), (torch.rand(T * K - T * K // 2, generator=g) - 0.5) * 600])
+    x = x[torch.randperm(x.numel(), generator=g)].view(T, K).to(torch.bfloat16)
+    w = torch.eye(K, dtype=torch.bfloat16)
+    b = torch.zeros(K)
+    y = E.linear(x.to(DEV), w.to(DEV), b.to(DEV), act="gelu").float().cpu()
+    ref = torch.nn.functional.gelu(x.double()).float()
+    tol = 1e-4 + ref.abs() * 2.0 ** -8
+    assert ((y - ref).abs() <= tol).all(), float((y - ref).abs().max())
