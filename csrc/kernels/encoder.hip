@@ -224,6 +224,158 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   }
 }
 
+// Persistent variant: one block per CU walks its XCD's contiguous share of
+// the tiles (g256::TileWalk). After a tile's K loop the NEXT tile's prologue
+// DMA (first K-tiles + its 256 bias values, parity double-buffered) is issued
+// before this tile's epilogue, which then runs from registers -- bias, GELU,
+// residual, bf16 -- with 8-B stores straight from the MFMA layout (no LDS
+// image, so the staging slots are free for the next tile's DMA). The HBM
+// latency of each tile's first K-tiles hides behind the previous epilogue
+// instead of every block of a round waiting for it at once, and there is no
+// per-tile launch / drain. Residual rows are loaded before the next prologue
+// so their wait does not also wait for the DMA.
+constexpr int G256P_EPI_OFF = G256_GEMM_LDS;  // bytes; past the output image
+constexpr int G256P_LDS = G256P_EPI_OFF + 2 * 256 * 4;
+
+// IMG 1: the one-tile kernel's LDS-image epilogue (coalesced 16-B stores), the
+// next tile's prologue issued after it (the image overlays the staging slots).
+template <int ACT, bool RES, int IMG>
+__global__ __launch_bounds__(g256::NT, 1) void gemm256p_kernel(
+    const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
+    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y, long ldy, int K,
+    int n_ft, int n_tiles) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  float* epi = reinterpret_cast<float*>(smem + G256P_EPI_OFF / 2);  // [parity][256] bias
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int KS = K / g256::BK;
+  g256::TileWalk walk;
+  walk.init(n_tiles);
+  int tile = walk.next;
+  if (!walk.valid(tile)) return;
+  auto stage_bias = [&](int tl, int par) {
+    const int n0 = (tl % n_ft) * g256::BM;
+    if (wave < 4)
+      __builtin_amdgcn_global_load_lds((g256::gbl_void_t*)(bias + min(n0 + wave * 64 + lane, N - 1)),
+                                       (g256::lds_void_t*)(epi + par * 256 + wave * 64), 4, 0, 0);
+  };
+  g256::Stager st;
+  st.setup(W, ldw, (tile % n_ft) * g256::BM, N, X, ldx, (tile / n_ft) * g256::BN, T);
+  auto ex0 = [&]() { stage_bias(tile, 0); };
+  g256::prologue<decltype(ex0), 8>(smem, st, KS, ex0);
+  int par = 0;
+  f32x4 acc[8][4];
+  while (true) {
+    const int cur = tile, cpar = par;
+    tile += walk.step;
+    const bool more = walk.valid(tile);
+    g256::body2<g256::MmaBf16>(smem, st, KS, acc, true);
+    if constexpr (IMG == 1) {
+      const int n0 = (cur % n_ft) * g256::BM, t0 = (cur / n_ft) * g256::BN;
+      const float* eb = epi + cpar * 256;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int nl = wr * 128 + i * 16 + 4 * (lane >> 4);
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(eb + nl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int tl = wc * 64 + j * 16 + (lane & 15);
+          f32x2 v0 = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1]};
+          f32x2 v1 = {acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+          if (ACT == 1) {
+            v0 = gelu_erf2(v0);
+            v1 = gelu_erf2(v1);
+          }
+          u16x4 o;
+          o[0] = f32_to_bf16(v0.x);
+          o[1] = f32_to_bf16(v0.y);
+          o[2] = f32_to_bf16(v1.x);
+          o[3] = f32_to_bf16(v1.y);
+          *reinterpret_cast<u16x4*>(smem + tl * G256_OUT_LD + nl) = o;
+        }
+      }
+      __syncthreads();
+      const int half = lane >> 5;
+      const int nl = (lane & 31) * 8;
+      const int n = n0 + nl;
+      if (n < N) {
+#pragma unroll 4
+        for (int rr = 0; rr < g256::BN / 16; ++rr) {
+          const int tl = wave * (g256::BN / 8) + 2 * rr + half;
+          const int t = t0 + tl;
+          if (t >= T) break;
+          const u16* src = smem + tl * G256_OUT_LD + nl;
+          const u16x4 lo = *reinterpret_cast<const u16x4*>(src);
+          const u16x4 hi = *reinterpret_cast<const u16x4*>(src + 4);
+          u16x8 o = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (RES) {
+            const u16x8 rv = *reinterpret_cast<const u16x8*>(R + (long)t * ldr + n);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = f32_to_bf16(bf16_to_f32(o[u]) + bf16_to_f32(rv[u]));
+          }
+          *reinterpret_cast<u16x8*>(Y + (long)t * ldy + n) = o;
+        }
+      }
+      __syncthreads();  // image reads done before the next prologue's DMA overwrites the slots
+      if (!more) break;
+      st.setup(W, ldw, (tile % n_ft) * g256::BM, N, X, ldx, (tile / n_ft) * g256::BN, T);
+      auto exn = [&]() { stage_bias(tile, cpar ^ 1); };
+      g256::prologue<decltype(exn), 8>(smem, st, KS, exn);
+      par = cpar ^ 1;
+      continue;
+    }
+    const int n0 = (cur % n_ft) * g256::BM, t0 = (cur / n_ft) * g256::BN;
+    const int tb = t0 + wc * 64 + (lane & 15);
+    u16x4 rv[8][4];
+    if constexpr (RES) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int n = min(n0 + wr * 128 + i * 16 + 4 * (lane >> 4), N - 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t = min(tb + j * 16, T - 1);
+          rv[i][j] = *reinterpret_cast<const u16x4*>(R + (long)t * ldr + n);
+        }
+      }
+    }
+    if (more) {
+      st.setup(W, ldw, (tile % n_ft) * g256::BM, N, X, ldx, (tile / n_ft) * g256::BN, T);
+      auto exn = [&]() { stage_bias(tile, cpar ^ 1); };
+      g256::prologue<decltype(exn), 8>(smem, st, KS, exn);
+    }
+    const float* eb = epi + cpar * 256;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int nl = wr * 128 + i * 16 + 4 * (lane >> 4);
+      const int n = n0 + nl;
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(eb + nl);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = tb + j * 16;
+        f32x2 v0 = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1]};
+        f32x2 v1 = {acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
+        if (ACT == 1) {
+          v0 = gelu_erf2(v0);
+          v1 = gelu_erf2(v1);
+        }
+        if constexpr (RES) {
+          v0 += (f32x2){bf16_to_f32(rv[i][j][0]), bf16_to_f32(rv[i][j][1])};
+          v1 += (f32x2){bf16_to_f32(rv[i][j][2]), bf16_to_f32(rv[i][j][3])};
+        }
+        u16x4 o;
+        o[0] = f32_to_bf16(v0.x);
+        o[1] = f32_to_bf16(v0.y);
+        o[2] = f32_to_bf16(v1.x);
+        o[3] = f32_to_bf16(v1.y);
+        if (t < T && n < N) *reinterpret_cast<u16x4*>(Y + (long)t * ldy + n) = o;
+      }
+    }
+    if (!more) break;
+    par = cpar ^ 1;
+  }
+}
+
 // ---------------------------------------------------------------- skinny GEMM
 // T <= 64 tokens (the per-turn query embed of chat/search_memories): the
 // projection is a weight-streaming GEMV, not an MFMA-bound GEMM. One block per
@@ -757,6 +909,8 @@ LZK_EXPORT void lzk_set_g256_min_tiles(int n) { g_g256_min_tiles = n; }
 static int g_g256_tail = -1;  // largest last-round fill (% of the CUs) split off to the 128x128 kernel (LZK_G256_TAIL)
 LZK_EXPORT void lzk_set_g256_tail(int pct) { g_g256_tail = pct; }
 static int g_n_cu_enc = 0;
+static int g_g256_persist = -1;  // persistent 256x256 GEMM: 1 = register epilogue, 2 = LDS image (LZK_G256_PERSIST)
+LZK_EXPORT void lzk_set_g256_persist(int p) { g_g256_persist = p; }
 
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
@@ -822,6 +976,42 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     auto launch256 = [&](const u16* x, int Tn, const u16* r, u16* y) {
       const int ntt = (Tn + g256::BN - 1) / g256::BN;
       dim3 grid(n_ft * ntt), block(g256::NT);
+      if (g_g256_persist < 0) {
+        const char* e = getenv("LZK_G256_PERSIST");
+        // off by default (bench/ab_persist.py, profiles/ab_persist_r1.json): with the LDS-image
+        // epilogue (2) the per-GEMM times equal the one-tile kernel's and the whole forward is
+        // slower (2 streams 5.14 -> 5.50 ms); 8-B stores straight from the MFMA layout (1) cost
+        // ~3.5 us per 256x256 tile more than the coalesced image stores (QKV 93 -> 107 us)
+        g_g256_persist = e ? atoi(e) : 0;
+      }
+      if ((g_g256_persist == 1 || g_g256_persist == 2) && (act == 0 || act == 1)) {
+        if (g_n_cu_enc <= 0) {
+          int dev = 0;
+          (void)hipGetDevice(&dev);
+          if (hipDeviceGetAttribute(&g_n_cu_enc, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+              g_n_cu_enc <= 0)
+            g_n_cu_enc = 256;
+        }
+        const int tiles = n_ft * ntt;
+        dim3 pgrid(tiles < g_n_cu_enc ? tiles : g_n_cu_enc);
+#define GP1(A, RS, IM)                                                                                             \
+  do {                                                                                                             \
+    (void)hipFuncSetAttribute((const void*)gemm256p_kernel<A, RS, IM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              G256P_LDS);                                                                          \
+    hipLaunchKernelGGL((gemm256p_kernel<A, RS, IM>), pgrid, block, G256P_LDS, st, x, ldx, Tn, w, ldw, N, bias, r,  \
+                       ldr, y, ldy, K, n_ft, tiles);                                                               \
+  } while (0)
+#define GP(A, RS)                                   \
+  do {                                              \
+    if (g_g256_persist == 2) GP1(A, RS, 1);         \
+    else GP1(A, RS, 0);                             \
+  } while (0)
+        if (act == 1) { if (r) GP(1, true); else GP(1, false); }
+        else { if (r) GP(0, true); else GP(0, false); }
+#undef GP
+#undef GP1
+        return;
+      }
       if (g_g256_body < 0) {
         const char* e = getenv("LZK_G256_BODY");
         g_g256_body = e ? atoi(e) : 1;  // body2: 2-4 % faster on the bge-base projections (bench/ab_body.py)
