@@ -101,6 +101,8 @@ def main():
     from lazzaro_amd.core.embedders import OnDeviceEmbedder
     from lazzaro_amd.ops.search import flat_topk
 
+    # sub-batch streams of the embed (bge-base at 1024 queries: 2 fills the GEMM tail waves)
+    parts = int(os.environ.get("LZK_EMBED_PARTS", "2"))
     rng = random.Random(1234 + rank)
     emb = OnDeviceEmbedder(a.model, device=dev, max_len=a.max_len, seed=0)
     assert emb.dim == a.dim, f"model width {emb.dim} != --dim {a.dim}"
@@ -116,7 +118,7 @@ def main():
 
     def step(i):
         ids, lens = pending.pop(i) if i in pending else tokenize(i)
-        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=2)
+        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts)
         pending[i + 1] = tokenize(i + 1)
         s, r = flat_topk(X, q16, a.k)
         if world > 1:
@@ -152,7 +154,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(3):
-        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=2)
+        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts)
     torch.cuda.synchronize()
     t_embed = (time.perf_counter() - t1) / 3
     t1 = time.perf_counter()
