@@ -91,7 +91,7 @@ class ShardedBuffer:
             ql = torch.full((allq.shape[0],), -1, dtype=torch.int32, device=self.dev)
             ql[lo: lo + q.shape[0]] = q_label.to(torch.int32)
             (s, r), (sw, rw) = flat_topk_dual(self.g.emb[:n], allq, k, bias=self.g.bias[:n],
-                                              row_label=self.g.shard[:n], q_label=ql)
+                                              row_label=self.g.shard[:n], q_label=ql, n_labels=N_TOPICS)
             local = (sw[lo: lo + q.shape[0]], rw[lo: lo + q.shape[0]])
         gid = torch.where(r >= 0, (comm.rank << ROW_BITS) + r, r)
         if comm.world > 1:

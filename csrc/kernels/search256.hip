@@ -394,17 +394,21 @@ struct TopK {
 };
 
 // One wave per query: lane-local top-K over the candidate list, then K
-// rounds of wave argmax. ovf[q] = 1 when the list overflowed its capacity.
+// rounds of wave argmax. ovf[q] = 1 when the list overflowed its capacity, or
+// (need != null) when it holds fewer than need[q] entries: a speculative
+// threshold above the query's true k-th score -- both recomputed exactly by
+// the caller's masked fallback.
 template <int K>
 __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict__ cnt, const float* __restrict__ cs,
                                                           const int* __restrict__ ci, int cap, int nq, int kout,
                                                           long idx_offset, float* __restrict__ os,
-                                                          long* __restrict__ oi, int* __restrict__ ovf) {
+                                                          long* __restrict__ oi, int* __restrict__ ovf,
+                                                          const int* __restrict__ need) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
   const int c = cnt[q];
-  if (lane == 0) ovf[q] = c > cap ? 1 : 0;
+  if (lane == 0) ovf[q] = (c > cap || (need && c < need[q])) ? 1 : 0;
   const int n = min(c, cap);
   TopK<K> top;
   top.init();
@@ -579,12 +583,13 @@ LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void
 }
 
 LZK_EXPORT int lzk_cand_select(const int* cnt, const float* cs, const int* ci, int cap, int nq, int kslot, int kout,
-                               long idx_offset, float* os, long* oi, int* ovf, void* stream) {
+                               long idx_offset, float* os, long* oi, int* ovf, const int* need, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((nq + 3) / 4), block(256);
   if (kout > kslot) return (int)hipErrorInvalidValue;
 #define LZK_SEL(KK) \
-  hipLaunchKernelGGL(cand_select_kernel<KK>, grid, block, 0, st, cnt, cs, ci, cap, nq, kout, idx_offset, os, oi, ovf)
+  hipLaunchKernelGGL(cand_select_kernel<KK>, grid, block, 0, st, cnt, cs, ci, cap, nq, kout, idx_offset, os, oi, ovf, \
+                     need)
   switch (kslot) {
     case 1: LZK_SEL(1); break;
     case 2: LZK_SEL(2); break;

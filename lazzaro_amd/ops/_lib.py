@@ -43,7 +43,7 @@ _SIGS = {
     "lzk_flat_cand": (I, [P, L, I, P, L, I, I, P, P, P, F, P, I, P, P, P, P, I, P, P]),
     "lzk_cand_gather": (I, [P, I, P, I, I, I, P, P, P, P, P, P, P]),
     "lzk_cand_grid": (I, [I, I, I]),
-    "lzk_cand_select": (I, [P, P, P, I, I, I, I, L, P, P, P, P]),
+    "lzk_cand_select": (I, [P, P, P, I, I, I, I, L, P, P, P, P, P]),
 }
 
 

@@ -202,11 +202,14 @@ def _cand_lists(dev, nq, cap, slot):
     return cnt, cs, ci
 
 
-def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap):
+def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap,
+                          need=None):
     """Exact per-query select from a candidate list; queries whose list
-    overflowed are recomputed by the lane kernel ON DEVICE (the masked launch
-    skips every query tile without an overflowed query -- a few us when none
-    did), so the path never synchronises with the host."""
+    overflowed -- or, with ``need``, holds fewer than need[q] entries (a
+    speculative threshold that turned out too high) -- are recomputed by the
+    lane kernel ON DEVICE (the masked launch skips every query tile without
+    such a query -- a few us when none did), so the path never synchronises
+    with the host."""
     L = _lib.lib()
     nq, D = Q.shape
     N = X.shape[0]
@@ -216,7 +219,7 @@ def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_o
     oi = torch.empty((nq, k), dtype=torch.long, device=dev)
     ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
     rc = L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, int(k),
-                           int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
+                           int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), _lib.ptr(need), st)
     _lib.check(rc, "lzk_cand_select")
     nch = L.lzk_flat_topk_chunks(N, nq, TARGET_WGS)
     part = nq * nch * kslot
@@ -266,13 +269,57 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
     return _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap)
 
 
+# Speculative list-B threshold of flat_topk_dual (LZK_DUAL_SPEC=1): aim for
+# this many expected label rows above it. Off by default: on the 10M x 1024
+# consolidation shape it cuts the scan 13.93 -> 12.90 ms (bench/probe_dual_thr.py:
+# list-B candidates 198 -> 16 per query), but the top-16 sample pass it needs
+# costs ~1.1 ms more than the top-4 one, so the whole call ties (15.07 vs
+# 15.13 ms, bench/ab_dual_spec.py, profiles/ab_dual_spec_r1.json).
+DUAL_SPEC = os.environ.get("LZK_DUAL_SPEC", "0") == "1"
+DUAL_SPEC_E = float(os.environ.get("LZK_DUAL_SPEC_E", "16"))
+SPEC_SLOTS = 16
+
+
+def _margin(t):
+    t = t - 2e-4 * (1.0 + t.abs())
+    return torch.nan_to_num(t, nan=float("-inf"))
+
+
+def _spec_threshold_b(ts, thr_b, row_label, q_label, n_labels, N, S, k):
+    """Speculative list-B thresholds from the global sample's top-16 ``ts``.
+
+    The safe bound ``thr_b`` (k-th best of the label-filtered 1/S sample)
+    sits around the label's top k*S rows, so ~k*S*n_labels rows of ALL labels
+    clear it and each costs the scan's per-score label test. The global
+    sample's j-th best leaves about E = j*S*n_l/N rows of a label with n_l
+    rows above it; j is chosen per query for E ~ DUAL_SPEC_E. The list stays
+    exact: a query whose list ends up with fewer than k entries is recomputed
+    by the select's fallback (need[q] = k), so only speed depends on the
+    estimate. Returns (thr, need)."""
+    dev = ts.device
+    lab = row_label.to(torch.float32)
+    hist = torch.histc(lab, bins=n_labels, min=0, max=n_labels)  # rows per label (no host sync)
+    ql = q_label.long()
+    n_l = torch.where(ql >= 0, hist[ql.clamp(0, n_labels - 1)], torch.full_like(ql, N, dtype=torch.float32))
+    n_l = torch.where((ql >= n_labels), torch.zeros_like(n_l), n_l)
+    j = torch.ceil(DUAL_SPEC_E * N / (S * n_l.clamp_min(1.0))).long()
+    ok = j <= ts.shape[1]
+    cand = _margin(ts.gather(1, (j.clamp(1, ts.shape[1]) - 1)[:, None])[:, 0])
+    spec = ok & (cand > thr_b)
+    thr = torch.where(spec, cand, thr_b).contiguous()
+    need = torch.where(spec, torch.full_like(ql, k), torch.zeros_like(ql)).to(torch.int32).contiguous()
+    return thr, need
+
+
 def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_label, bias=None,
-                   alpha: float = 1.0, idx_offset: int = 0):
+                   alpha: float = 1.0, idx_offset: int = 0, n_labels: int = None):
     """Two searches of the same queries from ONE scan: the unfiltered top-k and
     the label-filtered top-k (label < 0 = any). Consolidation needs both --
     global dedupe/links and within-shard links (reference memory_system.py:
     719-733, 816-836, 853-889) -- and the large-batch scan is MFMA-bound, so
     the candidate path computes each score once and files it into two lists.
+    ``n_labels`` (row labels in [0, n_labels)) enables the speculative
+    list-B threshold (:func:`_spec_threshold_b`); results are exact either way.
     Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
     if Q.dim() == 1:
         Q = Q[None, :]
@@ -291,8 +338,15 @@ def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_lab
     assert row_label.dtype == torch.int32 and q_label.dtype == torch.int32
     dev = X.device
     S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
-    thr_a = _sample_threshold(X, Q, k, kslot, bias, None, None, alpha, S)
     thr_b = _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S)
+    need_b = None
+    if DUAL_SPEC and n_labels and S > 1 and kslot < SPEC_SLOTS:
+        bs = bias[:N:S].contiguous() if bias is not None else None
+        ts, _ = _flat_topk_lane(X[::S], Q, SPEC_SLOTS, SPEC_SLOTS, bs, None, None, alpha, 0, None)
+        thr_a = _margin(ts[:, k - 1]).contiguous()
+        thr_b, need_b = _spec_threshold_b(ts, thr_b, row_label, q_label, int(n_labels), N, S, k)
+    else:
+        thr_a = _sample_threshold(X, Q, k, kslot, bias, None, None, alpha, S)
     cap = max(1024, 8 * kslot * S)
     ca = _cand_lists(dev, nq, cap, 0)
     cb = _cand_lists(dev, nq, cap, 1)
@@ -309,7 +363,7 @@ def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_lab
                                  ca[1].data_ptr(), ca[2].data_ptr(), cb[0].data_ptr(), cb[1].data_ptr(),
                                  cb[2].data_ptr(), st), "lzk_cand_gather")
     ra = _select_with_fallback(X, Q, k, kslot, bias, None, None, alpha, idx_offset, *ca, cap)
-    rb = _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, *cb, cap)
+    rb = _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, *cb, cap, need=need_b)
     return ra, rb
 
 

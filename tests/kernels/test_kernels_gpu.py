@@ -250,19 +250,26 @@ def test_graphed_encoder_matches_eager():
     torch.testing.assert_close(g2, eager[:1], atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("n,nq,k", [(300_001, 300, 3), (150_000, 512, 10)])
-def test_flat_topk_dual_gpu(monkeypatch, n, nq, k):
+@pytest.mark.parametrize("n,nq,k,stride,n_labels,spec_e", [
+    (300_001, 300, 3, 16, None, 16.0), (150_000, 512, 10, 16, None, 16.0),
+    # speculative list-B threshold (~16 expected label rows above it), and a
+    # deliberately too-high one (~1 row): underflowing queries must come back
+    # exact through the select's fallback
+    (300_001, 300, 3, 64, 64, 16.0), (300_001, 300, 3, 64, 64, 1.0)])
+def test_flat_topk_dual_gpu(monkeypatch, n, nq, k, stride, n_labels, spec_e):
     """One fused scan == the unfiltered and the label-filtered searches."""
     from lazzaro_amd.ops.search import flat_topk_dual
     monkeypatch.setenv("LZK_SEARCH", "cand")
-    monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", 16)
+    monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", stride)
+    monkeypatch.setattr("lazzaro_amd.ops.search.DUAL_SPEC", n_labels is not None)
+    monkeypatch.setattr("lazzaro_amd.ops.search.DUAL_SPEC_E", spec_e)
     g = torch.Generator(device=DEV).manual_seed(n)
     X = torch.randn(n, 768, device=DEV, generator=g).to(torch.bfloat16)
     Q = torch.randn(nq, 768, device=DEV, generator=g).to(torch.bfloat16)
     b = torch.where(torch.rand(n, device=DEV, generator=g) < 0.05, float("-inf"), 0.0)
     rl = torch.randint(0, 64, (n,), device=DEV, dtype=torch.int32, generator=g)
     ql = torch.randint(-1, 64, (nq,), device=DEV, dtype=torch.int32, generator=g)
-    (sa, ia), (sb, ib) = flat_topk_dual(X, Q, k, bias=b, row_label=rl, q_label=ql)
+    (sa, ia), (sb, ib) = flat_topk_dual(X, Q, k, bias=b, row_label=rl, q_label=ql, n_labels=n_labels)
     ra = _ref_topk(X.cpu(), Q.cpu(), k, b.cpu())
     rb = _ref_topk(X.cpu(), Q.cpu(), k, b.cpu(), rl.cpu(), ql.cpu())
     for (s, i), (rs, ri) in (((sa, ia), ra), ((sb, ib), rb)):
