@@ -179,6 +179,9 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
     # steps (compaction sizes, counts). The main stream waits for the batch's
     # own embedding before consolidating it.
     side = torch.cuda.Stream(dev) if encoder is not None and dev.type == "cuda" else None
+    # sub-batch streams of the fact embed: 1 (14k tokens; two streams measured 6.50k vs 6.75k
+    # turns/s in bench.py, profiles/ab_splitk_r1.json -- unlike the 22.6k-token query batch)
+    parts = int(os.environ.get("LZK_FACT_PARTS", "1"))
     pending = []
     tokens = []  # host-tokenised batches, one step ahead of their embedding launch
 
@@ -193,11 +196,11 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
             tokenize()
         ids, lens = tokens.pop(0)
         if side is None:
-            encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=2)
+            encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=parts)
             return
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=2)
+            encoder.encoder.forward_streams(ids, lens, pad_to=buf.g.emb.shape[1], parts=parts)
             ev = torch.cuda.Event()
             ev.record(side)
         pending.append(ev)

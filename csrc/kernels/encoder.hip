@@ -128,13 +128,15 @@ constexpr int G256_OUT_LD = g256::BN + 4;  // u16 per LDS output row (520 B)
 constexpr int G256_GEMM_LDS = (g256::BM * G256_OUT_LD * 2 > g256::LDS_BYTES) ? g256::BM * G256_OUT_LD * 2
                                                                               : g256::LDS_BYTES;
 
-template <int ACT, bool RES, int BODY = 0>
-__global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
-    const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
-    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y,
-    long ldy, int K, int n_ft) {
-  extern __shared__ __attribute__((aligned(16))) u16 smem[];
-  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+// One 256x256 output tile `logical` (token tile = logical / n_ft). `plain`
+// (wave-uniform): no bias and no residual -- the second K-half of a split-K
+// pair (gemm256_split2_kernel).
+template <int ACT, bool RES, int BODY>
+__device__ __forceinline__ void gemm256_tile(u16* smem, const u16* __restrict__ X, long ldx, int T,
+                                             const u16* __restrict__ W, long ldw, int N,
+                                             const float* __restrict__ bias, const u16* __restrict__ R, long ldr,
+                                             u16* __restrict__ Y, long ldy, int K, int n_ft, int logical,
+                                             bool plain) {
   const int tt = logical / n_ft, ft = logical % n_ft;
   const int n0 = ft * g256::BM, t0 = tt * g256::BN;
   const int lane = threadIdx.x & 63;
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   // the tile's 256 bias values ride along with the prologue DMA (no global
   // load latency in the epilogue)
   auto stage_bias = [&]() {
-    if (wave < 4)
+    if (wave < 4 && !plain)
       __builtin_amdgcn_global_load_lds((g256::gbl_void_t*)(bias + min(n0 + wave * 64 + lane, N - 1)),
                                        (g256::lds_void_t*)(sbias + wave * 64), 4, 0, 0);
   };
@@ -170,7 +172,9 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
   }
   f32x4 bv[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) bv[i] = *reinterpret_cast<const f32x4*>(sbias + wr * 128 + i * 16 + 4 * (lane >> 4));
+  for (int i = 0; i < 8; ++i)
+    bv[i] = plain ? (f32x4){0.f, 0.f, 0.f, 0.f}
+                  : *reinterpret_cast<const f32x4*>(sbias + wr * 128 + i * 16 + 4 * (lane >> 4));
   __syncthreads();  // the output image below overwrites the bias slot
   // pass 1: registers -> LDS image [token][feature] (bias + activation + one
   // v_cvt_pk_bf16_f32 per pair; 520-B rows keep the 8-B writes conflict-free)
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
       const u16x4 lo = *reinterpret_cast<const u16x4*>(src);
       const u16x4 hi = *reinterpret_cast<const u16x4*>(src + 4);
       u16x8 o = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      if (RES) {
+      if (RES && !plain) {
         const u16x8 rv = *reinterpret_cast<const u16x8*>(R + (long)t * ldr + n);
 #pragma unroll
         for (int u = 0; u < 8; ++u) o[u] = f32_to_bf16(bf16_to_f32(o[u]) + bf16_to_f32(rv[u]));
@@ -222,6 +226,36 @@ __global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
       *reinterpret_cast<u16x8*>(Y + (long)t * ldy + n) = o;
     }
   }
+}
+
+template <int ACT, bool RES, int BODY = 0>
+__global__ __launch_bounds__(g256::NT, 1) void gemm256_bias_act_kernel(
+    const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
+    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Y,
+    long ldy, int K, int n_ft) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  gemm256_tile<ACT, RES, BODY>(smem, X, ldx, T, W, ldw, N, bias, R, ldr, Y, ldy, K, n_ft,
+                               xcd_remap(blockIdx.x, gridDim.x), false);
+}
+
+// Split-K pair in ONE launch: tiles [0, tiles) form Ya = X[:, :K/2] W[:, :K/2]^T
+// + b (+ R), tiles [tiles, 2 tiles) Yb = X[:, K/2:] W[:, K/2:]^T; the consumer
+// (LayerNorm with residual) adds Ya + Yb in fp32. For the N = 768 projections
+// (O, FFN2 of bge-base) a token batch gives only 3 feature tiles per 256 tokens,
+// so e.g. 270 full-K tiles cost 2 rounds on 256 CUs; 540 half-K tiles cost
+// 3 half-length rounds (1.5), and FFN2's K = 3072 tiles are the longest of the
+// layer.
+template <bool RES>
+__global__ __launch_bounds__(g256::NT, 1) void gemm256_split2_kernel(
+    const u16* __restrict__ X, long ldx, int T, const u16* __restrict__ W, long ldw, int N,
+    const float* __restrict__ bias, const u16* __restrict__ R, long ldr, u16* __restrict__ Ya,
+    u16* __restrict__ Yb, long ldy, int K, int n_ft) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int half = logical & 1, tile = logical >> 1;
+  const int Kh = K / 2;
+  gemm256_tile<0, RES, 1>(smem, X + half * Kh, ldx, T, W + half * Kh, ldw, N, bias, R, ldr, half ? Yb : Ya, ldy,
+                          Kh, n_ft, tile, half != 0);
 }
 
 // Persistent variant: one block per CU walks its XCD's contiguous share of
@@ -1079,6 +1113,28 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   }
   const int n_ft = (N + TB - 1) / TB, n_tt = (T + TB - 1) / TB;
   launch128((const u16*)X, T, (const u16*)R, (u16*)Y, n_ft * n_tt, n_ft);
+  return (int)hipGetLastError();
+}
+
+// Split-K pair (gemm256_split2_kernel): Ya = X[:, :K/2] W[:, :K/2]^T + b (+ R),
+// Yb = X[:, K/2:] W[:, K/2:]^T, one launch. K % 128 == 0, N % 8 == 0.
+LZK_EXPORT int lzk_gemm_split2(const void* X, long ldx, int T, const void* W, long ldw, int N, const float* bias,
+                               const void* R, long ldr, void* Ya, void* Yb, long ldy, int K, void* stream) {
+  if (K % (2 * g256::BK) != 0 || N % 8 != 0 || ldy % 8 != 0 || (R && ldr % 8 != 0) || T <= 0 || N <= 0)
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
+  dim3 grid(2 * n_ft * n_tt), block(g256::NT);
+#define GO(RS)                                                                                                     \
+  do {                                                                                                             \
+    (void)hipFuncSetAttribute((const void*)gemm256_split2_kernel<RS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              G256_GEMM_LDS);                                                                      \
+    hipLaunchKernelGGL((gemm256_split2_kernel<RS>), grid, block, G256_GEMM_LDS, st, (const u16*)X, ldx, T,         \
+                       (const u16*)W, ldw, N, bias, (const u16*)R, ldr, (u16*)Ya, (u16*)Yb, ldy, K, n_ft);         \
+  } while (0)
+  if (R) GO(true);
+  else GO(false);
+#undef GO
   return (int)hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ then masked-mean or CLS pooling + L2 normalisation (one kernel).
 from __future__ import annotations
 
 import dataclasses
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -106,6 +107,34 @@ class SentenceEncoder:
             wq, sw = self.q[f"{i}.{w}"]
             return E.linear_fp8(xq, sx, wq, sw, self.p[f"{i}.{b}"], act=act, residual=residual)
         return E.linear(x, self.p[f"{i}.{w}"], self.p[f"{i}.{b}"], act=act, residual=residual)
+
+    def _lin_ln(self, x, i: int, w: str, b: str, residual, ln: str, split: bool):
+        """LN(x W^T + b + residual). ``split``: the projection as a split-K
+        pair (E.linear_split2, one launch with twice the tiles) whose two
+        halves the LayerNorm adds -- for the hidden-width projections, whose
+        few 256-wide feature tiles leave the last round of a grid mostly empty."""
+        p, eps = self.p, self.cfg.eps
+        if split:
+            ya, yb = E.linear_split2(x, p[f"{i}.{w}"], p[f"{i}.{b}"], residual=residual)
+            return E.layernorm(ya, p[f"{i}.{ln}_g"], p[f"{i}.{ln}_b"], eps, residual=yb)
+        return E.layernorm(self._lin(x, i, w, b, residual=residual), p[f"{i}.{ln}_g"], p[f"{i}.{ln}_b"], eps)
+
+    # split-K mode of the hidden-width projections (LZK_SPLITK: 0 off, 1 FFN2, 2 O and FFN2).
+    # Off by default: in bench.py (same box, profiles/ab_splitk_r1.json) FFN2 split costs the
+    # two-stream embed 5.28 -> 5.75 ms and ties on one stream (5.96 / 5.97 ms)
+    SPLITK = int(os.environ.get("LZK_SPLITK", "0"))
+
+    def _split_ok(self, x, K: int) -> bool:
+        # only grids that take the 256x256 pipeline anyway (>= 64 full-K tiles)
+        H = self.cfg.hidden
+        return (self.precision == "bf16" and x.is_cuda and K % 128 == 0 and H % 8 == 0
+                and ((H + 255) // 256) * ((x.shape[0] + 255) // 256) >= 64)
+
+    def _split_o(self, x) -> bool:
+        return SentenceEncoder.SPLITK >= 2 and self._split_ok(x, self.cfg.hidden)
+
+    def _split_ffn2(self, x) -> bool:
+        return SentenceEncoder.SPLITK >= 1 and self._split_ok(x, self.cfg.ffn)
 
     # --------------------------------------------------------------- weights
     def _random_init(self, seed: int) -> Dict[str, torch.Tensor]:
@@ -210,9 +239,9 @@ class SentenceEncoder:
         for i in range(c.layers):
             qkv = self._lin(x, i, "wqkv", "bqkv")
             ctx = E.attention(qkv, lens, B, S, c.heads, cu=cu)
-            x = E.layernorm(self._lin(ctx, i, "wo", "bo", residual=x), p[f"{i}.ln1_g"], p[f"{i}.ln1_b"], c.eps)
+            x = self._lin_ln(ctx, i, "wo", "bo", x, "ln1", split=self._split_o(x))
             hdn = self._lin(x, i, "w1", "b1", act="gelu")
-            x = E.layernorm(self._lin(hdn, i, "w2", "b2", residual=x), p[f"{i}.ln2_g"], p[f"{i}.ln2_b"], c.eps)
+            x = self._lin_ln(hdn, i, "w2", "b2", x, "ln2", split=self._split_ffn2(x))
         return E.pool_norm(x, lens, B, S, c.pooling, pad_to, cu=cu)
 
     def forward_streams(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0, parts: int = 2):

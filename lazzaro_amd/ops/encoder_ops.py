@@ -17,6 +17,8 @@ from . import _lib
 
 _lib.register("lzk_gemm_bias_act", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P,
                                              _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
+_lib.register("lzk_gemm_split2", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.L,
+                                           _lib.P, _lib.P, _lib.L, _lib.I, _lib.P])
 _lib.register("lzk_gemm_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P,
                                        _lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
 _lib.register("lzk_quant_fp8_rows", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.L, _lib.P, _lib.P])
@@ -50,6 +52,29 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, act: str = "none",
                                       _lib.stream_ptr(x.device))
     _lib.check(rc, "lzk_gemm_bias_act")
     return y
+
+
+def linear_split2(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, residual=None):
+    """Split-K pair for a following LayerNorm: (ya, yb) with ya + yb ==
+    x @ w.T + b (+ residual) -- ya = first K-half + b (+ residual), yb =
+    second K-half -- from ONE launch with twice the tiles of :func:`linear`
+    (csrc/kernels/encoder.hip gemm256_split2_kernel). K % 128 == 0."""
+    T, K = x.shape
+    N = w.shape[0]
+    if not x.is_cuda:
+        h = K // 2
+        ya = x[:, :h].float() @ w[:, :h].float().T + b.float()
+        if residual is not None:
+            ya = ya + residual.float()
+        return ya.to(x.dtype), (x[:, h:].float() @ w[:, h:].float().T).to(x.dtype)
+    assert x.stride(1) == 1 and w.stride(1) == 1 and K % 128 == 0 and N % 8 == 0
+    ya = torch.empty((T, N), dtype=torch.bfloat16, device=x.device)
+    yb = torch.empty((T, N), dtype=torch.bfloat16, device=x.device)
+    rc = _lib.lib().lzk_gemm_split2(x.data_ptr(), x.stride(0), T, w.data_ptr(), w.stride(0), N, b.data_ptr(),
+                                    _lib.ptr(residual), residual.stride(0) if residual is not None else 0,
+                                    ya.data_ptr(), yb.data_ptr(), ya.stride(0), K, _lib.stream_ptr(x.device))
+    _lib.check(rc, "lzk_gemm_split2")
+    return ya, yb
 
 
 FP8_MAX = 448.0  # OCP e4m3fn (gfx950 MFMA format, == torch.float8_e4m3fn)

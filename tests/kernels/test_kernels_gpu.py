@@ -403,3 +403,47 @@ def test_gelu_polynomial_extremes(T):
     ref = torch.nn.functional.gelu(x.double()).float()
     tol = 1e-4 + ref.abs() * 2.0 ** -8
     assert ((y - ref).abs() <= tol).all(), float((y - ref).abs().max())
+
+
+@pytest.mark.parametrize("T,N,K,res", [(5000, 768, 3072, True), (22585, 768, 768, True), (700, 1024, 4096, False)])
+def test_linear_split2(T, N, K, res):
+    """Split-K pair: ya + yb == x @ w.T + b (+ r), each half from its K range."""
+    g = torch.Generator().manual_seed(T)
+    x = torch.randn(T, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, generator=g)
+    r = torch.randn(T, N, generator=g).to(torch.bfloat16) if res else None
+    ya, yb = E.linear_split2(x.to(DEV), w.to(DEV), b.to(DEV), residual=r.to(DEV) if res else None)
+    h = K // 2
+    ra = x[:, :h].float() @ w[:, :h].float().T + b
+    if res:
+        ra = ra + r.float()
+    rb = x[:, h:].float() @ w[:, h:].float().T
+    for y, ref in ((ya, ra), (yb, rb)):
+        y = y.float().cpu()
+        assert float((y - ref).norm() / ref.norm()) < 4e-3
+    full = x.float() @ w.float().T + b + (r.float() if res else 0)
+    s = ya.float().cpu() + yb.float().cpu()
+    assert float((s - full).norm() / full.norm()) < 4e-3
+
+
+def test_split_k_forward_matches():
+    """The encoder forward with the split-K O / FFN2 projections (+ LN of the
+    two halves) == the single-GEMM forward."""
+    from lazzaro_amd.models.encoder import SentenceEncoder
+    enc = SentenceEncoder("bge-base", device=DEV, seed=4)
+    g = torch.Generator().manual_seed(9)
+    B = 1024
+    ids = torch.randint(1000, 30000, (B, 32), dtype=torch.int32, generator=g)
+    lens = torch.randint(12, 33, (B,), dtype=torch.int32, generator=g)
+    for i in range(B):
+        ids[i, lens[i]:] = 0
+    old = SentenceEncoder.SPLITK
+    try:
+        SentenceEncoder.SPLITK = 0
+        a, _ = enc.forward(ids, lens, pad_to=768)
+        SentenceEncoder.SPLITK = 2
+        b, _ = enc.forward(ids, lens, pad_to=768)
+    finally:
+        SentenceEncoder.SPLITK = old
+    assert ((a * b).sum(1) > 0.9995).all(), float((a * b).sum(1).min())
