@@ -113,19 +113,22 @@ def main():
         return emb.tok.encode_batch(pool[i % len(pool)], emb.max_len)
 
     # host tokenization of batch i+1 overlaps the device work of batch i
-    # (serving-style pipelining; the tokenizer still runs inside the timed loop)
+    # (serving-style pipelining; the tokenizer still runs inside the timed loop).
+    # It runs after batch i's search is enqueued: in the embed's shadow (~5 ms)
+    # it sometimes finished late and the search started up to 1.7 ms after the
+    # embed (rocprofv3 trace, profiles/r1_bench_rocprof_v4); the search gives it ~12 ms.
     pending = {}
 
     def step(i):
         ids, lens = pending.pop(i) if i in pending else tokenize(i)
         _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts)
-        pending[i + 1] = tokenize(i + 1)
         s, r = flat_topk(X, q16, a.k)
         if world > 1:
             out_r = torch.empty((world * r.shape[0], a.k), dtype=r.dtype, device=dev)
             out_s = torch.empty((world * s.shape[0], a.k), dtype=s.dtype, device=dev)
             dist.all_gather_into_tensor(out_r, r)
             dist.all_gather_into_tensor(out_s, s)
+        pending[i + 1] = tokenize(i + 1)
         return q16, s, r
 
     for i in range(a.warmup):

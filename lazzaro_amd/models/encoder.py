@@ -256,21 +256,45 @@ class SentenceEncoder:
         if not hasattr(self, "_streams") or len(self._streams) < parts:
             self._streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
         bounds = [B * i // parts for i in range(parts + 1)]
+        if not SentenceEncoder.CALLER_STREAM:  # every sub-batch on a side stream
+            outs = []
+            for i in range(parts):
+                st = self._streams[i]
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    outs.append(self.forward(ids[bounds[i]:bounds[i + 1]], lens[bounds[i]:bounds[i + 1]],
+                                             pad_to=pad_to))
+            for i in range(parts):
+                cur.wait_stream(self._streams[i])
+                for t in outs[i]:
+                    if t is not None:
+                        t.record_stream(cur)
+            o32 = torch.cat([o[0] for o in outs])
+            o16 = torch.cat([o[1] for o in outs]) if outs[0][1] is not None else None
+            return o32, o16
+        # sub-batch 0 runs on the caller's stream itself: its first kernels
+        # follow the previous work on the same queue at once, while a side
+        # stream's cross-queue wait resolves ~0.2 ms after that work ends
+        # (rocprofv3 trace of bench.py: 0.2 ms idle per step before the embed)
+        for i in range(1, parts):
+            self._streams[i - 1].wait_stream(cur)
         outs = []
         for i in range(parts):
-            st = self._streams[i]
-            st.wait_stream(cur)
+            st = cur if i == 0 else self._streams[i - 1]
             with torch.cuda.stream(st):
                 o32, o16 = self.forward(ids[bounds[i]:bounds[i + 1]], lens[bounds[i]:bounds[i + 1]], pad_to=pad_to)
                 outs.append((o32, o16))
-        for i in range(parts):
-            cur.wait_stream(self._streams[i])
+        for i in range(1, parts):
+            cur.wait_stream(self._streams[i - 1])
             for t in outs[i]:
                 if t is not None:
                     t.record_stream(cur)
         o32 = torch.cat([o[0] for o in outs])
         o16 = torch.cat([o[1] for o in outs]) if outs[0][1] is not None else None
         return o32, o16
+
+    # forward_streams: sub-batch 0 on the caller's stream (LZK_CALLER_STREAM=0: all on side streams)
+    CALLER_STREAM = os.environ.get("LZK_CALLER_STREAM", "1") != "0"
 
     def flops(self, tokens: int) -> float:
         c = self.cfg
