@@ -103,6 +103,7 @@ def main():
 
     # sub-batch streams of the embed (bge-base at 1024 queries: 2 fills the GEMM tail waves)
     parts = int(os.environ.get("LZK_EMBED_PARTS", "2"))
+    frac = float(os.environ.get("LZK_EMBED_FRAC", "0"))  # share of sub-batch 0 (0 = equal parts)
     rng = random.Random(1234 + rank)
     emb = OnDeviceEmbedder(a.model, device=dev, max_len=a.max_len, seed=0)
     assert emb.dim == a.dim, f"model width {emb.dim} != --dim {a.dim}"
@@ -121,7 +122,7 @@ def main():
 
     def step(i):
         ids, lens = pending.pop(i) if i in pending else tokenize(i)
-        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts)
+        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts, first_frac=frac)
         s, r = flat_topk(X, q16, a.k)
         if world > 1:
             out_r = torch.empty((world * r.shape[0], a.k), dtype=r.dtype, device=dev)
@@ -157,7 +158,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(3):
-        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts)
+        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts, first_frac=frac)
     torch.cuda.synchronize()
     t_embed = (time.perf_counter() - t1) / 3
     t1 = time.perf_counter()

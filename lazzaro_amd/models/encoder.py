@@ -244,18 +244,25 @@ class SentenceEncoder:
             x = self._lin_ln(hdn, i, "w2", "b2", x, "ln2", split=self._split_ffn2(x))
         return E.pool_norm(x, lens, B, S, c.pooling, pad_to, cu=cu)
 
-    def forward_streams(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0, parts: int = 2):
+    def forward_streams(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0, parts: int = 2,
+                        first_frac: float = 0.0):
         """Split the batch into ``parts`` independent sub-batches and run them on
         separate HIP streams. Every layer is a chain of dependent kernels whose
         last wave of 256x256 tiles leaves most CUs idle; kernels of the other
-        sub-batch fill those CUs, so the chip stays busy through each tail."""
+        sub-batch fill those CUs, so the chip stays busy through each tail.
+        ``first_frac`` > 0: sub-batch 0 (on the caller's stream, which starts
+        first) takes that share of the batch, the rest split evenly."""
         B = ids.shape[0]
         if parts <= 1 or self.device.type != "cuda" or B < 2 * parts:
             return self.forward(ids, lens, pad_to=pad_to)
         cur = torch.cuda.current_stream(self.device)
         if not hasattr(self, "_streams") or len(self._streams) < parts:
             self._streams = [torch.cuda.Stream(self.device) for _ in range(parts)]
-        bounds = [B * i // parts for i in range(parts + 1)]
+        if first_frac > 0.0:
+            b0 = min(B - (parts - 1), max(1, int(round(B * first_frac))))
+            bounds = [0] + [b0 + (B - b0) * i // (parts - 1) for i in range(parts)]
+        else:
+            bounds = [B * i // parts for i in range(parts + 1)]
         if not SentenceEncoder.CALLER_STREAM:  # every sub-batch on a side stream
             outs = []
             for i in range(parts):
