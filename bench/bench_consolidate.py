@@ -11,6 +11,8 @@ One step (= ``--convs`` conversations per rank, ``--facts`` facts each):
   4. owner rank: insert non-duplicates, within-shard links (label-filtered
      top-3), chain edges, duplicate merges (salience=max, access+1)
   5. fused decay (0.99^convs) + prune (K10) and eviction to the buffer limit (K11)
+  6. every ``--cluster-every`` steps: two-level hierarchical clustering of the
+     whole buffer into super-nodes (distributed spherical k-means, K16/C4)
 
 Fact *texts* are embedded (the cost is paid) but the vectors used for the
 graph are synthetic controlled ones (perturbations of existing memories with a
@@ -31,6 +33,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from lazzaro_amd.index.device_graph import DeviceGraph  # noqa: E402
+from lazzaro_amd.index.kmeans import kmeans  # noqa: E402
 from lazzaro_amd.ops.search import flat_topk, flat_topk_dual  # noqa: E402
 from lazzaro_amd.parallel import Communicator  # noqa: E402
 from lazzaro_amd.parallel.sharded import merge_topk  # noqa: E402
@@ -64,6 +67,7 @@ class ShardedBuffer:
         self.limit = int(nodes_per_rank * 1.1)
         self.rows_added = nodes_per_rank  # host-side upper bound on live rows
         self.remote_edges = []
+        self.fine = self.super_fine = self.super_top = None
 
     def owner(self, topic: torch.Tensor) -> torch.Tensor:
         return topic % self.comm.world
@@ -144,6 +148,24 @@ class ShardedBuffer:
         return {"routed": q.shape[0], "dup": dup.sum(), "inserted": out["inserted"],
                 "linked": out["linked"] + n_cross, "pruned": pruned, "evicted": evicted}
 
+    def cluster(self, n_fine: int, n_top: int, iters: int) -> None:
+        """Two-level hierarchical clustering of the whole buffer (K16; the
+        scalable form of the reference's per-shard mean super-node,
+        memory_system.py:893-933): spherical k-means into ``n_fine``
+        super-nodes over every rank's rows (fused MFMA top-1 assign, segmented
+        mean, one all-reduce of partial sums per iteration, C4), warm-started
+        from the previous pass; then the fine centroids (identical on every
+        rank) into ``n_top`` topic super-nodes. Tombstoned rows keep label -1."""
+        g = self.g
+        X = g.emb[: g.n]
+        comm = self.comm if self.comm.world > 1 else None
+        c32, c16, lab = kmeans(X, n_fine, iters=iters, comm=comm, init=self.fine)
+        self.fine = c32
+        _, _, top = kmeans(c16, n_top, iters=iters + 2, seed=1)
+        lab = torch.where(g.alive[: g.n] > 0, lab, torch.full_like(lab, -1))
+        self.super_fine = lab
+        self.super_top = torch.where(lab >= 0, top.to(lab.dtype)[lab.clamp_min(0).long()], lab)
+
 
 def synth_facts(buf: ShardedBuffer, n: int, dim: int, dup_rate: float, gen):
     dev = buf.dev
@@ -162,11 +184,17 @@ def synth_facts(buf: ShardedBuffer, n: int, dim: int, dup_rate: float, gen):
     return qp, topic, sal
 
 
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 WORDS = "user likes prefers works lives started visited learned project team python rust garden music".split()
 
 
 def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int,
-        encoder=None, dim: int = 768, dup_rate: float = 0.1, seed: int = 7):
+        encoder=None, dim: int = 768, dup_rate: float = 0.1, seed: int = 7,
+        cluster_every: int = 0, n_fine: int = 4096, n_top: int = 64, cluster_iters: int = 2):
     buf = ShardedBuffer(comm, dim, nodes, dev, seed)
     gen = torch.Generator(device=dev).manual_seed(seed + 100 + comm.rank)
     rng = random.Random(seed + comm.rank)
@@ -214,8 +242,25 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
         tokenize()      # the batch after next, on the host while the GPU has queued work
         q, topic, sal = synth_facts(buf, convs * facts, dim, dup_rate, gen)
         now[0] += 60.0
-        return buf.consolidate(q, topic, sal, convs * comm.world, now[0])
+        out = buf.consolidate(q, topic, sal, convs * comm.world, now[0])
+        n_steps[0] += 1
+        if cluster_every and n_steps[0] % cluster_every == 0:
+            buf.cluster(n_fine, n_top, cluster_iters)
+        return out
 
+    n_steps = [0]
+    clus_ms = None
+    if cluster_every:
+        # first pass seeds the fine centroids (farthest-first); it is not
+        # part of the steady state, so it runs (and is timed) before warmup
+        _sync(dev)
+        t0 = time.perf_counter()
+        buf.cluster(n_fine, n_top, cluster_iters)
+        _sync(dev)
+        t1 = time.perf_counter()
+        buf.cluster(n_fine, n_top, cluster_iters)
+        _sync(dev)
+        clus_ms = {"seed_pass": round((t1 - t0) * 1e3, 1), "warm_pass": round((time.perf_counter() - t1) * 1e3, 1)}
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev) if dev.type == "cuda" else None
@@ -236,7 +281,12 @@ def run(comm: Communicator, dev, nodes: int, convs: int, facts: int, steps: int,
     return {"turns_per_s": round(convs * comm.world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
             "nodes_per_rank": nodes, "convs_per_rank_step": convs, "facts_per_conv": facts,
             "buffer_nodes_total": nodes * comm.world, "edges_rank0": buf.g.num_edges, "per_step_rank0": {
-                k: round(v / steps, 1) for k, v in agg.items()}}
+                k: round(v / steps, 1) for k, v in agg.items()},
+            "hierarchical_clustering": None if not cluster_every else {
+                "every_steps": cluster_every, "fine_super_nodes": n_fine, "top_super_nodes": n_top,
+                "iters_per_pass": cluster_iters, "ms_rank0": clus_ms,
+                "fine_clusters_used": int((torch.bincount(buf.super_fine[buf.super_fine >= 0].long(),
+                                                          minlength=n_fine) > 0).sum())}}
 
 
 if __name__ == "__main__":
@@ -250,6 +300,10 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-embed", action="store_true")
+    ap.add_argument("--cluster-every", type=int, default=10, help="steps between hierarchical clustering passes (0=off)")
+    ap.add_argument("--fine", type=int, default=4096, help="fine super-nodes (k-means level 1)")
+    ap.add_argument("--top", type=int, default=64, help="topic super-nodes (k-means level 2)")
+    ap.add_argument("--cluster-iters", type=int, default=2)
     a = ap.parse_args()
     comm = Communicator.init()
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -258,6 +312,7 @@ if __name__ == "__main__":
     if not a.no_embed and dev.type == "cuda":
         from lazzaro_amd.core.embedders import OnDeviceEmbedder
         enc = OnDeviceEmbedder("bge-base", device=dev, max_len=64)
-    res = run(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc)
+    res = run(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, cluster_every=a.cluster_every,
+              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters)
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)

@@ -257,6 +257,64 @@ __global__ __launch_bounds__(256) void seg_sum_kernel(const u16* __restrict__ X,
   if (lane == 0) atomicAdd(&counts[c], 1);
 }
 
+// Atomic-free segmented sum over label-sorted rows: one workgroup per cluster,
+// its 4 waves stride over the cluster's rows (two rows in flight per wave),
+// each lane owns 4 consecutive dims of every 256-dim slice in registers; the
+// waves meet once in LDS. Reads each row once (1.5 KB contiguous at d=768)
+// instead of D fp32 atomics per row onto a few thousand hot addresses.
+constexpr int SEG_MAXV = 8;  // D <= 2048
+__global__ __launch_bounds__(256) void seg_sum_sorted_kernel(const u16* __restrict__ X, long ldx, int D,
+                                                             const long* __restrict__ order,
+                                                             const long* __restrict__ off,
+                                                             float* __restrict__ sums, int* __restrict__ counts) {
+  __shared__ float red[4][SEG_MAXV * 256];
+  const int c = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long b = off[c], e = off[c + 1];
+  float acc[SEG_MAXV][4];
+#pragma unroll
+  for (int v = 0; v < SEG_MAXV; ++v)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[v][u] = 0.f;
+  long i = b + wave;
+  for (; i + 4 < e; i += 8) {
+    const u16* r0 = X + order[i] * ldx;
+    const u16* r1 = X + order[i + 4] * ldx;
+#pragma unroll
+    for (int v = 0; v < SEG_MAXV; ++v) {
+      const int d = (v * 64 + lane) * 4;
+      if (d < D) {
+        const u16x4 x0 = *reinterpret_cast<const u16x4*>(r0 + d);
+        const u16x4 x1 = *reinterpret_cast<const u16x4*>(r1 + d);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[v][u] += bf16_to_f32(x0[u]) + bf16_to_f32(x1[u]);
+      }
+    }
+  }
+  if (i < e) {
+    const u16* r0 = X + order[i] * ldx;
+#pragma unroll
+    for (int v = 0; v < SEG_MAXV; ++v) {
+      const int d = (v * 64 + lane) * 4;
+      if (d < D) {
+        const u16x4 x0 = *reinterpret_cast<const u16x4*>(r0 + d);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[v][u] += bf16_to_f32(x0[u]);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < SEG_MAXV; ++v) {
+    const int d = (v * 64 + lane) * 4;
+    if (d < D)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) red[wave][d + u] = acc[v][u];
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += 256)
+    sums[(long)c * D + d] = (red[0][d] + red[1][d]) + (red[2][d] + red[3][d]);
+  if (threadIdx.x == 0) counts[c] = (int)(e - b);
+}
+
 // centroid = sums / count, optionally L2-normalised; written as fp32 and bf16 (padded)
 __global__ __launch_bounds__(64) void centroid_kernel(const float* __restrict__ sums, const int* __restrict__ counts,
                                                       int D, int normalize, float* __restrict__ c32,
@@ -379,6 +437,17 @@ LZK_EXPORT int lzk_seg_sum(const void* X, long ldx, long n, int D, const int* la
   if (D % 4 != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(seg_sum_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, (const u16*)X,
                      ldx, n, D, label, sums, counts);
+  return (int)hipGetLastError();
+}
+
+// order: row indices sorted by label; off: [C+1] segment offsets into order.
+// Writes every cluster's sums/counts (no pre-zeroing needed).
+LZK_EXPORT int lzk_seg_sum_sorted(const void* X, long ldx, int D, const long* order, const long* off, int C,
+                                  float* sums, int* counts, void* stream) {
+  if (C == 0) return 0;
+  if (D % 4 != 0 || D > SEG_MAXV * 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(seg_sum_sorted_kernel, dim3((unsigned)C), dim3(256), 0, (hipStream_t)stream, (const u16*)X, ldx,
+                     D, order, off, sums, counts);
   return (int)hipGetLastError();
 }
 

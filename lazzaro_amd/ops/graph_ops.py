@@ -29,6 +29,7 @@ _lib.register("lzk_neighbor_boost", I, [P, P, P, P, P, I, F, D_, F, P, P, P, P, 
 _lib.register("lzk_pairs_above", I, [P, L, I, I, F, P, I, P, P])
 _lib.register("lzk_seg_sum", I, [P, L, L, I, P, P, P, P])
 _lib.register("lzk_centroids", I, [P, P, I, I, I, P, P, I, P])
+_lib.register("lzk_seg_sum_sorted", I, [P, L, I, P, P, I, P, P, P])
 
 SALIENCE_FLOOR = 0.2
 
@@ -201,6 +202,25 @@ def pairs_above(X: torch.Tensor, tau: float, max_pairs: int = 1 << 22) -> torch.
     return p[o].to(torch.int32)
 
 
+SEG_SUM_ATOMIC = False  # True: per-element fp32 atomics (the original K8 kernel) instead of sort + segment
+
+
+def _seg_sum_sorted(X: torch.Tensor, label: torch.Tensor, C: int):
+    """Per-cluster row sums without atomics: stable sort of the labels (rows
+    with label < 0 go to a sentinel segment past the last cluster), then one
+    workgroup per cluster streams its rows (lzk_seg_sum_sorted)."""
+    n, D = X.shape
+    key = torch.where(label >= 0, label, torch.full_like(label, C))
+    order = torch.argsort(key, stable=True).contiguous()
+    off = torch.zeros(C + 2, dtype=torch.int64, device=X.device)
+    off[1:] = torch.cumsum(torch.bincount(key.long(), minlength=C + 1)[: C + 1], 0)
+    sums = torch.empty((C, D), dtype=torch.float32, device=X.device)
+    cnt = torch.empty(C, dtype=torch.int32, device=X.device)
+    _lib.check(_lib.lib().lzk_seg_sum_sorted(X.data_ptr(), X.stride(0), D, order.data_ptr(), off.data_ptr(), C,
+                                             sums.data_ptr(), cnt.data_ptr(), _st(X)), "seg_sum_sorted")
+    return sums, cnt
+
+
 def centroids(X: torch.Tensor, label: torch.Tensor, C: int, normalize: bool = True, pad_to: int = 0):
     """K8: per-cluster mean of rows (optionally L2-normalised). Returns
     (fp32 [C, D], bf16 [C, pad_to] or None, counts [C])."""
@@ -219,11 +239,16 @@ def centroids(X: torch.Tensor, label: torch.Tensor, C: int, normalize: bool = Tr
             c16 = torch.zeros((C, pad_to), dtype=torch.bfloat16)
             c16[:, :D] = c32.to(torch.bfloat16)
         return c32, c16, cnt
-    sums = torch.zeros((C, D), dtype=torch.float32, device=X.device)
-    cnt = torch.zeros(C, dtype=torch.int32, device=X.device)
+    if X.dtype != torch.bfloat16 or X.stride(1) != 1 or label.numel() != n:
+        raise ValueError("centroids: GPU rows must be a bf16 [n, D] view with unit column stride and n labels")
     label = label.to(torch.int32).contiguous()
-    _lib.check(_lib.lib().lzk_seg_sum(X.data_ptr(), X.stride(0), n, D, label.data_ptr(), sums.data_ptr(),
-                                      cnt.data_ptr(), _st(X)), "seg_sum")
+    if D <= 2048 and not SEG_SUM_ATOMIC:
+        sums, cnt = _seg_sum_sorted(X, label, C)
+    else:
+        sums = torch.zeros((C, D), dtype=torch.float32, device=X.device)
+        cnt = torch.zeros(C, dtype=torch.int32, device=X.device)
+        _lib.check(_lib.lib().lzk_seg_sum(X.data_ptr(), X.stride(0), n, D, label.data_ptr(), sums.data_ptr(),
+                                          cnt.data_ptr(), _st(X)), "seg_sum")
     c32 = torch.empty((C, D), dtype=torch.float32, device=X.device)
     c16 = torch.empty((C, pad_to), dtype=torch.bfloat16, device=X.device) if pad_to else None
     _lib.check(_lib.lib().lzk_centroids(sums.data_ptr(), cnt.data_ptr(), C, D, int(normalize), c32.data_ptr(),

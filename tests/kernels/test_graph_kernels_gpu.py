@@ -90,6 +90,29 @@ def test_centroids_gpu():
     assert torch.equal(cnt, cntg.cpu()) and torch.allclose(c, cg.cpu(), atol=1e-5)
 
 
+@pytest.mark.parametrize("atomic", [False, True])
+@pytest.mark.parametrize("D", [256, 768, 2048])
+def test_seg_sum_paths_gpu(atomic, D, monkeypatch):
+    """Sorted (atomic-free) and atomic segmented sums vs an fp32 reference:
+    uneven clusters (one empty, one holding a third of the rows), label -1
+    rows, a strided (padded-arena) view, un-normalised sums."""
+    monkeypatch.setattr(G, "SEG_SUM_ATOMIC", atomic)
+    g = torch.Generator().manual_seed(D)
+    n, C = 7001, 53
+    full = torch.randn(n, D + 64, generator=g).to(torch.bfloat16)
+    X = full[:, :D]
+    lab = torch.randint(-1, C, (n,), generator=g, dtype=torch.int32)
+    lab[lab == 7] = 8
+    lab[: n // 3] = 11
+    m = lab >= 0
+    ref = torch.zeros(C, D).index_add_(0, lab[m].long(), X[m].float())
+    rc = torch.bincount(lab[m].long(), minlength=C).to(torch.int32)
+    c32, _, cnt = G.centroids(full.to(DEV)[:, :D], lab.to(DEV), C, normalize=False)
+    sums = c32.cpu() * cnt.cpu().clamp_min(1)[:, None].float()
+    assert torch.equal(cnt.cpu(), rc) and int(cnt[7]) == 0
+    assert torch.allclose(sums, ref, atol=2e-3, rtol=1e-4)
+
+
 def test_device_graph_gpu_matches_cpu():
     torch.manual_seed(0)
     D = 64
