@@ -1,6 +1,7 @@
-"""A/B: k-means centroid update (K8) at buffer scale -- per-element fp32
-atomics vs sort + one workgroup per cluster (lzk_seg_sum_sorted). Also times
-the fused MFMA top-1 assign of the same pass for scale. Prints one JSON line."""
+"""A/B of one k-means pass at buffer scale (12.5M x 768, 4096 centroids):
+assign = flat_topk(k=1) on the 128x128 lane kernel vs the 256x256 flat_top1
+argmax kernel; centroid update (K8) = per-element fp32 atomics vs sort + one
+workgroup per cluster (lzk_seg_sum_sorted). Prints one JSON line."""
 from __future__ import annotations
 
 import json
@@ -35,7 +36,17 @@ def main(n=12_500_000, D=768, C=4096):
         X[r0:r0 + x.shape[0]] = torch.nn.functional.normalize(x, dim=1).to(torch.bfloat16)
     C16 = X[torch.randperm(n, device=dev, generator=g)[:C]].contiguous()
     lab, _ = assign(X, C16)
-    out = {"n": n, "D": D, "C": C, "assign_ms": round(timed(lambda: assign(X, C16), 3), 2)}
+    import lazzaro_amd.index.kmeans as K
+    out = {"n": n, "D": D, "C": C}
+    for mode in ("lane", "top1"):
+        K.ASSIGN = mode
+        out[f"assign_{mode}_ms"] = round(timed(lambda: assign(X, C16), 3), 2)
+        out[f"assign_{mode}_pflops"] = round(2.0 * n * C * D / (out[f"assign_{mode}_ms"] * 1e-3) / 1e15, 3)
+    K.ASSIGN = "lane"
+    la, _ = assign(X, C16)
+    K.ASSIGN = "top1"
+    lb, _ = assign(X, C16)
+    out["assign_label_agreement"] = float((la == lb).float().mean())
     res = {}
     for atomic in (True, False):
         G.SEG_SUM_ATOMIC = atomic

@@ -439,7 +439,92 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
   }
 }
 
+// Exact top-1 (argmax) per query on the 256x256 pipeline: the k-means assign
+// step (every buffer row against a few thousand
+// centroids). With k = 1 the per-query state is one (score, row) pair, so the
+// epilogue folds each lane's 32 accumulators, then the 4 row groups of a wave
+// by shuffles, and merges across row tiles with one 64-bit atomicMax per
+// (query, wave row) on a packed key: order-preserving score bits high,
+// (~row) low -> max score, smallest row on ties. Blocks of one query tile
+// are adjacent (row tile = fastest index), so a query tile is read from HBM
+// once and the small centroid matrix stays in L2.
+__device__ __forceinline__ unsigned long long top1_pack(float s, int r) {
+  unsigned u = __float_as_uint(s);
+  const unsigned key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)key << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)r);
+}
+
+__global__ __launch_bounds__(NT, 1) void flat_top1_kernel(const u16* __restrict__ X, long ldx, int nrows,
+                                                          const u16* __restrict__ Qm, long ldq, int nq, int D,
+                                                          int n_rt, unsigned long long* __restrict__ best) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = logical % n_rt, qt = logical / n_rt;
+  const int r0 = rt * BM, q0 = qt * BN;
+  Stager st;
+  st.setup(X, ldx, r0, nrows, Qm, ldq, q0, nq);
+  f32x4 acc[8][4];
+  mainloop(smem, st, D / BK, acc);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float m = LZK_NEG_INF;
+    int mr = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rb = r0 + wr * 128 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // rows ascend within a lane: strict > keeps the smaller row
+        const float v = acc[i][j][e];
+        if (rb + e < nrows && v > m) { m = v; mr = rb + e; }
+      }
+    }
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float om = __shfl_xor(m, off);
+      const int orr = __shfl_xor(mr, off);
+      if (om > m || (om == m && orr < mr)) { m = om; mr = orr; }
+    }
+    const int q = q0 + wc * 64 + j * 16 + (lane & 15);
+    if ((lane >> 4) == 0 && q < nq && mr < nrows) atomicMax(best + q, top1_pack(m, mr));
+  }
+}
+
+__global__ __launch_bounds__(256) void top1_decode_kernel(const unsigned long long* __restrict__ best, int nq,
+                                                          float* __restrict__ score, int* __restrict__ row) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const unsigned long long b = best[q];
+  if (b == 0ull) { score[q] = LZK_NEG_INF; row[q] = -1; return; }
+  const unsigned key = (unsigned)(b >> 32);
+  const unsigned u = (key & 0x80000000u) ? (key & 0x7fffffffu) : ~key;
+  score[q] = __uint_as_float(u);
+  row[q] = (int)(0xFFFFFFFFu - (unsigned)(b & 0xFFFFFFFFull));
+}
+
 }  // namespace
+
+// Exact argmax of Q @ X.T per query (no bias/labels). ws: [nq] u64 scratch.
+// score fp32 [nq], row int32 [nq] (-1 when nrows == 0).
+LZK_EXPORT int lzk_flat_top1(const void* X, long ldx, int nrows, const void* Qm, long ldq, int nq, int D, void* ws,
+                             float* score, int* row, void* stream) {
+  if (D % BK != 0 || nq <= 0 || nrows <= 0) return (int)hipErrorInvalidValue;
+  const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
+  const long nblk = (long)n_rt * n_qt;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned long long* best = (unsigned long long*)ws;
+  hipError_t e = hipMemsetAsync(best, 0, (size_t)nq * 8, st);
+  if (e != hipSuccess) return (int)e;
+  (void)hipFuncSetAttribute((const void*)flat_top1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  hipLaunchKernelGGL(flat_top1_kernel, dim3((unsigned)nblk), dim3(NT), LDS_BYTES, st, (const u16*)X, ldx, nrows,
+                     (const u16*)Qm, ldq, nq, D, n_rt, best);
+  hipLaunchKernelGGL(top1_decode_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, best, nq, score, row);
+  return (int)hipGetLastError();
+}
 
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }

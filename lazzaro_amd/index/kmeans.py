@@ -11,16 +11,24 @@ same global centroids.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
 
 from ..ops import graph_ops as G
-from ..ops.search import flat_topk
+from ..ops.search import flat_top1, flat_topk
+
+
+# "top1": the 256x256 argmax kernel (flat_top1); "lane": flat_topk(k=1) on the 128x128 per-lane kernel
+ASSIGN = os.environ.get("LZK_ASSIGN", "top1")
 
 
 def assign(X: torch.Tensor, C16: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:
     """Nearest (max inner product) centroid per row of X. Returns (label, score)."""
+    if ASSIGN == "top1" and X.is_cuda:
+        s, i = flat_top1(C16, X.contiguous() if X.stride(1) != 1 else X)
+        return i, s
     labs, scs = [], []
     for r0 in range(0, X.shape[0], chunk):
         s, i = flat_topk(C16, X[r0:r0 + chunk], 1)
@@ -36,12 +44,13 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
     g = torch.Generator(device="cpu").manual_seed(seed)
     sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
     S = X[sub].float()
-    picks = [0]
-    best = S @ S[0]
-    for _ in range(1, min(k, S.shape[0])):
-        j = int(torch.argmin(best).item())
-        picks.append(j)
-        best = torch.maximum(best, S @ S[j])
+    m = min(k, S.shape[0])
+    picks = torch.zeros(m, dtype=torch.long, device=S.device)
+    best = torch.mv(S, S[0])
+    for t in range(1, m):  # picks stay on the device: no host sync per seed
+        j = torch.argmin(best).view(1)
+        picks[t:t + 1] = j
+        best = torch.maximum(best, torch.mv(S, S.index_select(0, j)[0]))
     c = S[picks]
     if c.shape[0] < k:
         c = torch.cat([c, S[torch.randint(0, S.shape[0], (k - c.shape[0],), generator=g).to(X.device)]])

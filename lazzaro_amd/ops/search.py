@@ -151,6 +151,31 @@ def flat_topk(X: torch.Tensor, Q: torch.Tensor, k: int, *, bias=None, row_label=
     return _flat_topk_lane(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, n_chunks)
 
 
+def flat_top1(X: torch.Tensor, Q: torch.Tensor):
+    """Exact argmax of ``Q @ X.T`` per query: (score fp32 [nq], row int32 [nq]).
+
+    The k-means assign shape (millions of queries, a few thousand rows) on the
+    256x256 MFMA pipeline with a packed 64-bit atomicMax merge across row
+    tiles (search256.hip flat_top1_kernel); ties go to the smaller row.
+    """
+    nq, D = Q.shape
+    N = X.shape[0]
+    if not X.is_cuda:
+        s, i = _ref_topk(X, Q, 1, None, None, None, 1.0, 0)
+        return s[:, 0], i[:, 0].to(torch.int32)
+    assert X.dtype == torch.bfloat16 and Q.dtype == torch.bfloat16
+    assert X.shape[1] == D and D % 64 == 0 and X.stride(1) == 1 and Q.stride(1) == 1
+    dev = X.device
+    if N == 0 or nq == 0:
+        return torch.full((nq,), float("-inf"), device=dev), torch.full((nq,), -1, dtype=torch.int32, device=dev)
+    ws = torch.empty(nq, dtype=torch.int64, device=dev)
+    score = torch.empty(nq, dtype=torch.float32, device=dev)
+    row = torch.empty(nq, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().lzk_flat_top1(X.data_ptr(), X.stride(0), N, Q.data_ptr(), Q.stride(0), nq, D, ws.data_ptr(),
+                                        score.data_ptr(), row.data_ptr(), _lib.stream_ptr(dev)), "lzk_flat_top1")
+    return score, row
+
+
 def _flat_topk_lane(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, n_chunks):
     """Per-lane running top-K kernel (search.hip) + partial-list merge."""
     L = _lib.lib()

@@ -244,3 +244,39 @@ def test_ivfpq_fused_rerank_matches_library_path(monkeypatch, keep):
     s2, i2 = idx.search(q, 10, nprobe=8, rerank=200)
     torch.testing.assert_close(s1, s2, atol=1e-4, rtol=1e-4)
     assert (i1 == i2).float().mean() > 0.99
+
+
+@pytest.mark.parametrize("N,nq", [(37, 300), (4096, 1000), (1000, 70001)])
+def test_flat_top1_gpu(N, nq):
+    """256x256 argmax kernel (k-means assign) vs an fp32 reference: partial row
+    and query tiles, negative best scores, exact duplicate rows (tie -> the
+    smaller row)."""
+    from lazzaro_amd.ops.search import flat_top1
+    g = torch.Generator().manual_seed(N + nq)
+    D = 192
+    X = torch.randn(N, D, generator=g).to(torch.bfloat16)
+    X[N // 2] = X[N // 3]  # duplicate rows: equal scores, keep the smaller index
+    Q = torch.randn(nq, D, generator=g).to(torch.bfloat16)
+    Q[:5] = -X[:5]  # a few queries whose best score is small
+    ref = Q.float() @ X.float().T
+    s, r = flat_top1(X.to(DEV), Q.to(DEV))
+    s, r = s.cpu(), r.cpu().long()
+    assert bool((r >= 0).all()) and bool((r < N).all())
+    best = ref.max(dim=1).values
+    got = ref.gather(1, r[:, None])[:, 0]
+    assert torch.allclose(s, got, atol=1e-3, rtol=1e-4)
+    assert bool((got >= best - 1e-3).all())
+    assert int((r == N // 2).sum()) == 0  # the duplicate's larger index never wins
+
+
+def test_kmeans_assign_paths_agree_gpu(monkeypatch):
+    import lazzaro_amd.index.kmeans as K
+    g = torch.Generator().manual_seed(5)
+    X = torch.nn.functional.normalize(torch.randn(20000, 128, generator=g), dim=1).to(torch.bfloat16).to(DEV)
+    C = X[:300].contiguous()
+    monkeypatch.setattr(K, "ASSIGN", "lane")
+    la, sa = K.assign(X, C)
+    monkeypatch.setattr(K, "ASSIGN", "top1")
+    lb, sb = K.assign(X, C)
+    assert torch.allclose(sa, sb, atol=1e-4)
+    assert float((la == lb).float().mean()) > 0.999
