@@ -124,9 +124,9 @@ class ShardedBuffer:
         local_dup = dup & ((gid[:, 0] >> ROW_BITS) == comm.rank)
         rows = torch.where(gid[:, 0] >= 0, gid[:, 0] & ((1 << ROW_BITS) - 1), 0)
         neg = torch.full_like(sal, float("-inf"))
-        g.sal.index_reduce_(0, rows, torch.where(local_dup, sal.float(), neg), "amax", include_self=True)
+        g.sal.scatter_reduce_(0, rows, torch.where(local_dup, sal.float(), neg), "amax", include_self=True)
         g.acc.index_add_(0, rows, local_dup.to(torch.int32))
-        g.last.index_reduce_(0, rows, torch.where(local_dup, torch.full_like(neg, now, dtype=torch.float64),
+        g.last.scatter_reduce_(0, rows, torch.where(local_dup, torch.full_like(neg, now, dtype=torch.float64),
                                                   torch.full_like(neg, float("-inf"), dtype=torch.float64)),
                              "amax", include_self=True)
         # (4) insert + links (within-shard + same-rank global hits; fixed shapes)

@@ -162,7 +162,7 @@ class DeviceGraph:
             r1 = torch.full((M,), -1, dtype=torch.long, device=self.device)
         if bool(dup.any()):
             rows = r1[dup]
-            self.sal.index_reduce_(0, rows, salience.to(self.device)[dup].float(), "amax", include_self=True)
+            self.sal.scatter_reduce_(0, rows, salience.to(self.device)[dup].float(), "amax", include_self=True)
             self.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
             self.last[rows] = now
         keep = ~dup
