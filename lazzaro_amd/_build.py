@@ -134,8 +134,10 @@ def build_runtime(verbose: bool = False, sanitize: str = "", outdir: str = "") -
 def build_all(verbose: bool = True) -> None:
     k = build_kernels(verbose=verbose)
     r = build_runtime(verbose=verbose)
+    # device-bounds-checked twin, loaded only by the LZK_DEBUG tests
+    d = build_kernels(verbose=verbose, debug=True)
     if verbose:
-        print("built:", k, r)
+        print("built:", k, r, d)
 
 
 if __name__ == "__main__":
