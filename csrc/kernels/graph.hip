@@ -246,9 +246,8 @@ __global__ __launch_bounds__(256) void seg_sum_kernel(const u16* __restrict__ X,
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= n) return;
-  LZK_DCHECK(label[r] >= 0);
   const int c = label[r];
-  if (c < 0) return;
+  if (c < 0) return;  // negative label = tombstoned row (valid input)
   for (int d = lane * 4; d < D; d += 256) {
     u16x4 v = *reinterpret_cast<const u16x4*>(X + r * ldx + d);
 #pragma unroll

@@ -1,0 +1,259 @@
+// Tenant-graph maintenance kernels: the device engine under MemorySystem
+// (lazzaro_amd/engine/tenant_graph.py).
+//
+// One tenant's memory graph lives in HBM as structure-of-arrays:
+//   nodes  sal f32 | acc i32 | last f64 | kind u8 (0 free, 1 node, 2 ghost =
+//          id still referenced by an edge) | sup u8 (super-node) | shard i32 |
+//          dirty u8 (changed since the last persistence commit)
+//   edges  src/dst i32 | w f32 | co i32 | lu f64 | meta i32 = shard | type<<24
+//          (the shard the reference stores the edge in: MemoryShard.edges)
+//
+// These kernels replace the per-object Python loops of the reference:
+//   decay + prune      memory_shard.py:64-84 via memory_system.py:624-630, :991
+//   node removal       memory_system.py:558-569 (evict: node + its shard's edges)
+//   neighbour boost    memory_system.py:242-260 (visible arcs, CSR)
+//   retrieval touch    buffer_graph.py:79-85
+//   importance         memory_system.py:541-549
+#include "lzk_common.h"
+
+LZK_DEBUG_STATE(tenant)
+
+namespace {
+
+constexpr int NTB = 256;
+constexpr float SAL_FLOOR = 0.2f;
+
+__device__ __forceinline__ int block_ballot_count(int f, int* wsum) {
+  unsigned long long bal = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(bal);
+  __syncthreads();
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < NTB / 64; ++i) s += wsum[i];
+  return s;
+}
+
+// Edge pass: w *= keep (keep == 1 -> no decay); flag survivors w >= thr
+// (flag == nullptr -> no prune). Node pass (same launch, grid-stride): the
+// salience of shard nodes (kind 1, not super) decays towards the floor.
+__global__ __launch_bounds__(NTB) void tg_decay_kernel(float* __restrict__ w, long ne, float keep, float thr,
+                                                       unsigned char* __restrict__ flag, int* __restrict__ block_cnt,
+                                                       float* __restrict__ sal, const unsigned char* __restrict__ kind,
+                                                       const unsigned char* __restrict__ sup, long nn, int do_nodes) {
+  __shared__ int wsum[NTB / 64];
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  int f = 0;
+  if (e < ne) {
+    float v = w[e];
+    if (keep != 1.f) {
+      v *= keep;
+      w[e] = v;
+    }
+    f = v >= thr;
+    if (flag) flag[e] = (unsigned char)f;
+  }
+  if (flag) {
+    const int s = block_ballot_count(f, wsum);
+    if (threadIdx.x == 0) block_cnt[blockIdx.x] = s;
+  }
+  if (do_nodes) {
+    for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
+      if (kind[i] != 1 || sup[i]) continue;
+      const float s = sal[i];
+      sal[i] = s > SAL_FLOOR ? SAL_FLOOR + (s - SAL_FLOOR) * keep : SAL_FLOOR;
+    }
+  }
+}
+
+// Node-only salience decay (when the edge grid is too small to stream nodes).
+__global__ __launch_bounds__(NTB) void tg_node_decay_kernel(float* __restrict__ sal, const unsigned char* __restrict__ kind,
+                                                            const unsigned char* __restrict__ sup, long nn, float keep) {
+  for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
+    if (kind[i] != 1 || sup[i]) continue;
+    const float s = sal[i];
+    sal[i] = s > SAL_FLOOR ? SAL_FLOOR + (s - SAL_FLOOR) * keep : SAL_FLOOR;
+  }
+}
+
+// Node removal: an edge is dropped when an endpoint is being removed AND the
+// edge lives in that endpoint's shard (the reference deletes only the removed
+// node's shard's incident edges; edges other shards store survive, dangling).
+__global__ __launch_bounds__(NTB) void tg_flag_remove_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                             const int* __restrict__ meta, long ne,
+                                                             const unsigned char* __restrict__ rm,
+                                                             const int* __restrict__ shard,
+                                                             unsigned char* __restrict__ flag,
+                                                             int* __restrict__ block_cnt) {
+  __shared__ int wsum[NTB / 64];
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  int f = 0;
+  if (e < ne) {
+    const int s = src[e], d = dst[e], es = meta[e] & 0xFFFFFF;
+    LZK_DCHECK(s >= 0 && d >= 0);
+    const bool drop = (rm[s] && shard[s] == es) || (rm[d] && shard[d] == es);
+    f = !drop;
+    flag[e] = (unsigned char)f;
+  }
+  const int s = block_ballot_count(f, wsum);
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s;
+}
+
+// Stable scatter of flagged edges (block offsets from lzk_scan_blocks).
+__global__ __launch_bounds__(NTB) void tg_compact_kernel(const unsigned char* __restrict__ flag,
+                                                         const int* __restrict__ block_off, long ne,
+                                                         const int* __restrict__ src, const int* __restrict__ dst,
+                                                         const float* __restrict__ w, const int* __restrict__ co,
+                                                         const double* __restrict__ lu, const int* __restrict__ meta,
+                                                         int* __restrict__ osrc, int* __restrict__ odst,
+                                                         float* __restrict__ ow, int* __restrict__ oco,
+                                                         double* __restrict__ olu, int* __restrict__ ometa) {
+  __shared__ int wpre[NTB / 64];
+  const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  const int f = (e < ne) ? flag[e] : 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long bal = __ballot(f);
+  const int before = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) wpre[wv] = __popcll(bal);
+  __syncthreads();
+  int off = block_off[blockIdx.x];
+  for (int i = 0; i < wv; ++i) off += wpre[i];
+  if (f) {
+    const int o = off + before;
+    osrc[o] = src[e];
+    odst[o] = dst[e];
+    ow[o] = w[e];
+    oco[o] = co[e];
+    olu[o] = lu[e];
+    ometa[o] = meta[e];
+  }
+}
+
+// Neighbour boost over the visible-arc CSR (arc a->b exists when the edge is
+// stored in a's shard, the reference's MemoryShard.get_neighbors visibility).
+// One wave per seed; a neighbour with w >= min_w that is a live node and not
+// a seed gets last = now, sal = min(1, sal + delta) once per call: the stamp
+// word holds the call's epoch, so no per-call clear of an N-sized array.
+__global__ __launch_bounds__(64) void tg_boost_kernel(const long* __restrict__ off, const int* __restrict__ adj,
+                                                      const int* __restrict__ eid, const float* __restrict__ w,
+                                                      const int* __restrict__ seeds, int nseeds,
+                                                      const unsigned char* __restrict__ kind,
+                                                      const unsigned char* __restrict__ sup, float min_w, double now,
+                                                      float delta, float* __restrict__ sal, double* __restrict__ last,
+                                                      unsigned char* __restrict__ dirty, int* __restrict__ stamp,
+                                                      int epoch, int* __restrict__ nboost) {
+  const int s = seeds[blockIdx.x];
+  if (s < 0 || sup[s]) return;  // super-nodes live outside the shards: no neighbours
+  for (long p = off[s] + threadIdx.x; p < off[s + 1]; p += 64) {
+    const int nb = adj[p];
+    LZK_DCHECK(nb >= 0);
+    if (w[eid[p]] < min_w || kind[nb] != 1) continue;
+    bool is_seed = false;
+    for (int j = 0; j < nseeds; ++j) is_seed |= (seeds[j] == nb);
+    if (is_seed) continue;
+    if (atomicExch(&stamp[nb], epoch) != epoch) {
+      sal[nb] = fminf(1.f, sal[nb] + delta);
+      last[nb] = now;
+      dirty[nb] = 1;
+      atomicAdd(nboost, 1);
+    }
+  }
+}
+
+// Retrieval access update (BufferGraph.update_access) for a few rows.
+__global__ __launch_bounds__(64) void tg_touch_kernel(const long* __restrict__ rows, int n, int* __restrict__ acc,
+                                                      double* __restrict__ last, float* __restrict__ sal,
+                                                      unsigned char* __restrict__ dirty, double now, float delta) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const long r = rows[i];
+  LZK_DCHECK(r >= 0);
+  acc[r] += 1;
+  last[r] = now;
+  sal[r] = fminf(1.f, sal[r] + delta);
+  dirty[r] = 1;
+}
+
+// Eviction importance in double precision (the reference scores in Python
+// floats; an fp32 score would merge near-ties and change the victim order).
+// Non-candidates (not a live shard node, or a super-node) get +inf.
+__global__ __launch_bounds__(NTB) void tg_importance_kernel(const float* __restrict__ sal, const int* __restrict__ acc,
+                                                            const double* __restrict__ last,
+                                                            const unsigned char* __restrict__ kind,
+                                                            const unsigned char* __restrict__ sup, long n, double now,
+                                                            double* __restrict__ out) {
+  const long i = (long)blockIdx.x * NTB + threadIdx.x;
+  if (i >= n) return;
+  if (kind[i] != 1 || sup[i]) {
+    out[i] = __builtin_huge_val();
+    return;
+  }
+  const double days = (now - last[i]) / 86400.0;
+  out[i] = (double)sal[i] * 0.5 + fmin(1.0, (double)acc[i] / 10.0) * 0.3 + (1.0 / (1.0 + days)) * 0.2;
+}
+
+inline unsigned blocks_for(long n, int per = NTB) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+
+// ---------------------------------------------------------------- C ABI
+LZK_EXPORT int lzk_tg_decay(float* w, long ne, float keep, float thr, unsigned char* flag, int* block_cnt, float* sal,
+                            const unsigned char* kind, const unsigned char* sup, long nn, int decay_nodes,
+                            void* stream) {
+  long nb = (ne + NTB - 1) / NTB;
+  if (nb == 0) nb = 1;
+  // nodes ride in the edge launch only while its grid can stream them
+  const long node_blocks = (nn + 4L * NTB - 1) / (4L * NTB);
+  const bool fused = decay_nodes && (nb >= node_blocks || nb >= 2048);
+  if (ne > 0 || fused)
+    hipLaunchKernelGGL(tg_decay_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, w, ne, keep, thr, flag,
+                       block_cnt, sal, kind, sup, nn, fused ? 1 : 0);
+  if (decay_nodes && !fused && nn > 0) {
+    const long g = node_blocks < 4096 ? node_blocks : 4096;
+    hipLaunchKernelGGL(tg_node_decay_kernel, dim3((unsigned)g), dim3(NTB), 0, (hipStream_t)stream, sal, kind, sup, nn,
+                       keep);
+  }
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_flag_remove(const int* src, const int* dst, const int* meta, long ne, const unsigned char* rm,
+                                  const int* shard, unsigned char* flag, int* block_cnt, void* stream) {
+  if (ne == 0) return 0;
+  hipLaunchKernelGGL(tg_flag_remove_kernel, dim3(blocks_for(ne)), dim3(NTB), 0, (hipStream_t)stream, src, dst, meta,
+                     ne, rm, shard, flag, block_cnt);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_compact(const unsigned char* flag, const int* block_off, long ne, const int* src, const int* dst,
+                              const float* w, const int* co, const double* lu, const int* meta, int* osrc, int* odst,
+                              float* ow, int* oco, double* olu, int* ometa, void* stream) {
+  if (ne == 0) return 0;
+  hipLaunchKernelGGL(tg_compact_kernel, dim3(blocks_for(ne)), dim3(NTB), 0, (hipStream_t)stream, flag, block_off, ne,
+                     src, dst, w, co, lu, meta, osrc, odst, ow, oco, olu, ometa);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_boost(const long* off, const int* adj, const int* eid, const float* w, const int* seeds,
+                            int nseeds, const unsigned char* kind, const unsigned char* sup, float min_w, double now,
+                            float delta, float* sal, double* last, unsigned char* dirty, int* stamp, int epoch,
+                            int* nboost, void* stream) {
+  if (nseeds <= 0) return 0;
+  hipLaunchKernelGGL(tg_boost_kernel, dim3(nseeds), dim3(64), 0, (hipStream_t)stream, off, adj, eid, w, seeds, nseeds,
+                     kind, sup, min_w, now, delta, sal, last, dirty, stamp, epoch, nboost);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_touch(const long* rows, int n, int* acc, double* last, float* sal, unsigned char* dirty,
+                            double now, float delta, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(tg_touch_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, rows, n, acc,
+                     last, sal, dirty, now, delta);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_importance(const float* sal, const int* acc, const double* last, const unsigned char* kind,
+                                 const unsigned char* sup, long n, double now, double* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(tg_importance_kernel, dim3(blocks_for(n)), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last,
+                     kind, sup, n, now, out);
+  return (int)hipGetLastError();
+}

@@ -11,6 +11,12 @@ site-packages, so the GPU box loads exactly what this tree built):
   WordPiece/hash tokenizer, CSR/graph utilities, tenant placement), C++17 +
   pybind11, built with g++.
 
+* ``lazzaro_amd/_lib/liblzk_debug.so`` -- the same kernels with
+  ``-DLZK_DEBUG=1`` device bounds asserts. ``build_all`` always produces it
+  (in a second, parallel compile) because the GPU tier's debug-build test loads
+  it on a box that never builds; the release ``liblzk.so`` is what every other
+  process loads.
+
 Usage: ``python -m lazzaro_amd._build`` (or ``__graft_entry__.build()``).
 Incremental: a target is rebuilt only when a source or header is newer.
 """
@@ -132,10 +138,13 @@ def build_runtime(verbose: bool = False, sanitize: str = "", outdir: str = "") -
 
 
 def build_all(verbose: bool = True) -> None:
-    k = build_kernels(verbose=verbose)
-    r = build_runtime(verbose=verbose)
-    # device-bounds-checked twin, loaded only by the LZK_DEBUG tests
-    d = build_kernels(verbose=verbose, debug=True)
+    """Release kernels, host runtime and the device-bounds-checked debug twin
+    (loaded only by the LZK_DEBUG tests), the three built concurrently."""
+    with ThreadPoolExecutor(max_workers=3) as ex:
+        fk = ex.submit(build_kernels, verbose, 4)
+        fr = ex.submit(build_runtime, verbose)
+        fd = ex.submit(build_kernels, verbose, 4, True)
+        k, r, d = fk.result(), fr.result(), fd.result()
     if verbose:
         print("built:", k, r, d)
 
@@ -144,7 +153,7 @@ if __name__ == "__main__":
     import argparse
 
     ap = argparse.ArgumentParser(description="build the lazzaro_amd native libraries in-tree")
-    ap.add_argument("--debug", action="store_true", help="also build liblzk_debug.so (device bounds asserts)")
+    ap.add_argument("--debug", action="store_true", help="(build_all already builds liblzk_debug.so; kept for compatibility)")
     ap.add_argument("--sanitize", default="", help="host sanitizer(s) for debug builds, e.g. address,undefined")
     a = ap.parse_args()
     build_all(verbose=True)

@@ -1,18 +1,24 @@
-"""Consolidation pipeline of :class:`MemorySystem` (mixin).
+"""Consolidation pipeline of :class:`MemorySystem` (mixin), on the device graph.
 
 Reference: ``core/memory_system.py:535-1120`` (buffer-limit eviction,
 end-of-conversation fact extraction, dedupe, associative linking, super-node
 hierarchy, deep consolidation, profile extraction, merge-similar).
 
-Same observable behaviour and constants; the engine work is
-batched instead of pairwise:
+Same observable behaviour and constants; every graph step
+runs on the tenant's :class:`~lazzaro_amd.engine.TenantGraph` (HBM columns +
+HIP kernels on a GPU, the same tensor code on the CPU):
 
-* dedupe (reference :719-733) = ONE batched top-1 store search for all new
-  facts -- equivalent because the store does not change inside the loop;
-* linking (:797-889) = one ``[new x existing]`` cosine top-3 per pass
-  (``similarity.topk_cosine``: float64 host GEMM or the MFMA kernel on GPU);
-* eviction scores (:535-578) are one vectorised importance + stable argsort;
-* component edge averages (:970-985) are one pass over the edges.
+* dedupe, within-shard links and cross-memory links of a batch of M facts come
+  from ONE fused scan (``flat_topk_dual``: a global and a shard-filtered list)
+  with exact float64 re-ranking -- the reference does M store searches plus
+  2*M*N Python cosines (:719-733, :797-889);
+* decay + auto-prune is one kernel pass over the edge and node columns
+  (``tg_decay_kernel``), eviction is ``tg_importance_kernel`` + a stable select
+  + ``tg_flag_remove`` compaction, neighbour boost ``tg_boost_kernel``;
+* connected components are the hook/compress kernels; per-component edge
+  weight averages one segmented reduction;
+* the pairwise merge (opt-in) takes candidate pairs from the MFMA
+  ``pairs_kernel`` and confirms them in float64.
 
 Fixes, all behind documented defaults:
 * embeddings are aligned per kept fact (reference :706/:720 misalignment);
@@ -26,13 +32,12 @@ from __future__ import annotations
 
 import json
 import time
-from collections import defaultdict
-from typing import Dict, List, Set, Tuple
+from typing import Dict, List, Sequence, Set, Tuple
 
 import numpy as np
+import torch
 
-from ..models.graph import Edge, Node
-from .similarity import topk_cosine
+from ..engine.tenant_graph import NODE, SHARD_MASK, TenantGraph
 from ..utils.faults import EmbeddingError, ProviderError, degenerate_embedding
 from ..utils.tracing import tracer
 
@@ -61,6 +66,7 @@ LINK_TOPK = 3
 LINK_WEIGHT_SCALE = 0.8
 CHAIN_WEIGHT = 0.5
 MIN_FACT_LEN = 5
+DECAY_RATE = 0.01
 
 
 def _parse_json(response: str):
@@ -72,41 +78,19 @@ def _parse_json(response: str):
 
 
 class ConsolidationMixin:
+    graph: TenantGraph
+
     # ------------------------------------------------------------ eviction
     def _enforce_buffer_limit(self):
-        total, _ = self.buffer.size()
-        if total <= self.max_buffer_size:
+        g = self.graph
+        if g.num_nodes() <= self.max_buffer_size:
             return
-        excess = total - self.max_buffer_size
-        now = time.time()
-        cand: List[Tuple[str, str]] = []
-        sal, acc, last = [], [], []
-        for sh in self.shards.values():
-            for nid, n in sh.nodes.items():
-                if n.is_super_node:
-                    continue
-                cand.append((nid, n.shard_key))
-                sal.append(n.salience)
-                acc.append(n.access_count)
-                last.append(n.last_accessed)
-        if not cand:
-            return
-        sal = np.asarray(sal, dtype=np.float64)
-        acc = np.asarray(acc, dtype=np.float64)
-        days = (now - np.asarray(last, dtype=np.float64)) / 86400.0
-        importance = 0.5 * sal + 0.3 * np.minimum(1.0, acc / 10.0) + 0.2 / (1.0 + days)
-        order = np.argsort(importance, kind="stable")[:excess]
-        victims = [cand[i] for i in order]
-        removed = 0
-        for nid, skey in victims:
-            sh = self.shards.get(skey)
-            if sh is not None and sh.remove_node(nid):
-                removed += 1
-        if removed:
-            ids = [nid for nid, _ in victims]
-            self._emb_cache.forget(ids)
-            self.vector_store.delete_nodes(ids, user_id=self.user_id)
-            self._say(f"⚠ Buffer limit reached! Archived {removed} old nodes (limit: {self.max_buffer_size})")
+        with tracer.stage("evict", self._device):
+            victims = g.evict(self.max_buffer_size)
+        if victims:
+            ids = [g.ids[r] for r in victims]
+            self._store_delete(ids)
+            self._say(f"⚠ Buffer limit reached! Archived {len(victims)} old nodes (limit: {self.max_buffer_size})")
 
     # ------------------------------------------------------------ end of conversation
     def end_conversation(self) -> str:
@@ -128,12 +112,12 @@ class ConsolidationMixin:
             results.append(self._consolidate_to_buffer())
 
         with self._graph_lock:
-            self.buffer.apply_temporal_decay(decay_rate=0.01)
+            # decay (memory_shard.py:64-77) and auto-prune (:79-84) in one pass
+            with tracer.stage("decay_prune", self._device):
+                pruned = self.graph.decay(DECAY_RATE, self.prune_threshold if self.auto_prune else None)
             results.append("✓ Applied temporal decay")
-            if self.auto_prune:
-                pruned = self.buffer.prune_weak_edges(threshold=self.prune_threshold)
-                if pruned > 0:
-                    results.append(f"✓ Auto-pruned {pruned} weak edges")
+            if self.auto_prune and pruned > 0:
+                results.append(f"✓ Auto-pruned {pruned} weak edges")
             self._enforce_buffer_limit()
             self.conversation_count += 1
             if self.auto_consolidate and self.conversation_count % self.consolidate_every == 0:
@@ -151,20 +135,6 @@ class ConsolidationMixin:
         self._async_consolidate()
         n, e = self.buffer.size()
         return f"✓ Consolidation complete. Memory: {n} nodes, {e} edges"
-
-    def _side_stream(self):
-        """Background consolidation runs on its own HIP stream so its kernels
-        overlap the caller's retrieval kernels (SURVEY.md §2.6 async row)."""
-        import contextlib
-
-        import torch
-
-        dev = self._device
-        if dev is None or getattr(dev, "type", "cpu") != "cuda" or not torch.cuda.is_available():
-            return contextlib.nullcontext()
-        if getattr(self, "_cstream", None) is None:
-            self._cstream = torch.cuda.Stream(device=dev)
-        return torch.cuda.stream(self._cstream)
 
     def flush(self, timeout: float = None) -> None:
         """Block until queued background consolidations have finished."""
@@ -235,201 +205,310 @@ class ConsolidationMixin:
         facts = [m for m in facts if isinstance(m, dict)] if isinstance(facts, list) else []
         self._say(f"✓ Extracted {len(facts)} memory candidates")
         kept = [m for m in facts if m.get("content") and len(m.get("content", "")) >= MIN_FACT_LEN]
-        with self._side_stream():
-            with tracer.stage("embed_facts", self._device):
-                embs = self._batch_embed([m["content"] for m in kept]) if kept else []
-            if kept and all(degenerate_embedding(e) for e in embs):
-                # a provider outage (zero vectors for everything): retry later
-                raise EmbeddingError("embedding provider returned only degenerate vectors")
-            with self._graph_lock, tracer.stage("ingest", self._device):
-                self._ingest_facts(kept, embs)
+        with tracer.stage("embed_facts", self._device):
+            embs = self._batch_embed_any([m["content"] for m in kept]) if kept else None
+        if kept and self._all_degenerate(embs):
+            # a provider outage (zero vectors for everything): retry later
+            raise EmbeddingError("embedding provider returned only degenerate vectors")
+        with self._graph_lock, tracer.stage("ingest", self._device):
+            self._ingest_facts(kept, embs)
 
-    def _ingest_facts(self, facts: List[Dict], embs: List[List[float]]) -> List[Tuple[str, str]]:
-        # K5: one batched top-1 search for every fact (the store is unchanged
-        # during this loop in the reference too, so this is equivalent).
-        valid = [i for i, e in enumerate(embs) if e is not None and len(e) and not degenerate_embedding(e)]
-        rejected = len(facts) - len(valid)
+    @staticmethod
+    def _all_degenerate(embs) -> bool:
+        if embs is None:
+            return True
+        if torch.is_tensor(embs):
+            if embs.numel() == 0:
+                return True
+            ok = torch.isfinite(embs).all(1) & (embs.abs().sum(1) > 0)
+            return not bool(ok.any())
+        return all(degenerate_embedding(e) for e in embs)
+
+    # ------------------------------------------------------------ ingest (K5 + K6)
+    def _ingest_facts(self, facts: List[Dict], embs) -> List[Tuple[str, str]]:
+        """Dedupe, insert and link one batch of extracted facts (reference
+        :706-785) on the device graph. ``embs``: [M, D] tensor or list of
+        vectors aligned with ``facts``. Returns [(new node id, shard key)]."""
+        g = self.graph
+        M = len(facts)
+        if M == 0:
+            return []
+        now = time.time()
+        E, valid = self._fact_matrix(embs, M)
+        rejected = M - int(valid.sum())
         if rejected:
             self.metrics["rejected_embeddings"] = self.metrics.get("rejected_embeddings", 0) + rejected
-        hits = {}
-        if valid:
-            res = self._search_batch([embs[i] for i in valid], 1)
-            hits = {i: (r[0] if r else None) for i, r in zip(valid, res)}
-        new_nodes: List[Tuple[str, str]] = []
-        rows = []
-        undo = []  # (node, salience, last_accessed, access_count) of merged duplicates
-        for i, mem in enumerate(facts):
-            content = mem["content"]
-            emb = embs[i] if i < len(embs) else []
-            if i not in hits:
-                self._say("   (skipped fact with empty/zero embedding)")
-                continue
-            shard_key = mem.get("topic", self._infer_shard_key(content))
-            shard = self._get_or_create_shard(shard_key)
-            best_id = hits.get(i)
-            if best_id is not None:
-                best = self.buffer.get_node(best_id)
-                if best is not None and self._cosine_similarity(emb, best.embedding) > DEDUPE_THRESHOLD:
-                    undo.append((best, best.salience, best.last_accessed, best.access_count))
-                    best.salience = max(best.salience, mem.get("salience", 0.5))
-                    best.last_accessed = time.time()
-                    best.access_count += 1
-                    self._say(f"   (Merged semantic duplicate into {best.id})")
-                    continue
-            nid = self._generate_node_id()
-            node = Node(id=nid, content=content, embedding=list(emb), type=mem.get("type", "semantic"),
-                        salience=mem.get("salience", 0.5), shard_key=shard_key)
-            shard.add_node(node)
-            new_nodes.append((nid, shard_key))
-            rows.append({"id": nid, "content": content, "embedding": node.embedding, "type": node.type,
-                         "salience": node.salience, "shard_key": node.shard_key,
-                         "timestamp": node.timestamp})
-        if rows:
+            self._say("   (skipped fact(s) with empty/zero embedding)")
+        vidx = np.nonzero(valid)[0]
+        if vidx.size == 0:
+            return []
+        # shards are created in fact order, duplicates included (reference :716-718)
+        shard_keys = [facts[i].get("topic", self._infer_shard_key(facts[i]["content"])) for i in vidx]
+        codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int32)
+        Q = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
+        sal_in = torch.as_tensor([float(facts[i].get("salience", 0.5)) for i in vidx], dtype=torch.float32)
+
+        with g.on_stream():
+            dup_rows, (ls, lr), (ws, wr) = self._scan_batch(Q, torch.as_tensor(codes))
+        # --- dedupe: best store row is a node and cosine > 0.95 (reference :719-742)
+        dup = dup_rows >= 0
+        undo = None
+        if bool(dup.any()):
+            rows = dup_rows[dup]
+            with g.on_stream():
+                undo = (rows.clone(), g.sal[rows].clone(), g.last[rows].clone(), g.acc[rows].clone())
+                g.sal.scatter_reduce_(0, rows, sal_in.to(g.device)[dup.to(sal_in.device)], "amax", include_self=True)
+                g.last[rows] = now
+                g.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
+                g.dirty[rows] = 1
+            g._bump()
+            for _ in range(int(dup.sum())):
+                self._say("   (Merged semantic duplicate)")
+        keep = (~dup).cpu().numpy()
+        kidx = np.nonzero(keep)[0]
+        if kidx.size == 0:
+            return []
+        kfacts = [facts[vidx[i]] for i in kidx]
+        ids = [self._generate_node_id() for _ in kidx]
+        kcodes = codes[kidx]
+        kt = torch.as_tensor(kidx, dtype=torch.long).to(g.device)
+        stored = self._store_binds_graph()
+        rows = g.add_nodes(ids, [f["content"] for f in kfacts], Q[kt.to(Q.device)], shard=kcodes,
+                           types=[f.get("type", "semantic") for f in kfacts], sal=sal_in[torch.as_tensor(kidx)],
+                           now=now, stored=stored)
+        new_nodes = [(i, shard_keys[j]) for i, j in zip(ids, kidx)]
+        if not stored:
             try:
-                self.vector_store.add_nodes(rows, user_id=self.user_id)
+                self.vector_store.add_nodes([
+                    {"id": i, "content": f["content"], "embedding": g.embedding(int(r)), "type": f.get("type", "semantic"),
+                     "salience": float(f.get("salience", 0.5)), "shard_key": sk, "timestamp": now}
+                    for i, f, r, (_, sk) in zip(ids, kfacts, rows.tolist(), new_nodes)], user_id=self.user_id)
             except Exception:
                 # roll the graph back so the re-queued batch applies exactly once
-                for nid, skey in new_nodes:
-                    self.shards[skey].remove_node(nid)
-                for node, sal, la, ac in undo:
-                    node.salience, node.last_accessed, node.access_count = sal, la, ac
+                g.remove_nodes(rows, drop_edges=True)
+                self.node_counter -= len(ids)
+                if undo is not None:
+                    with g.on_stream():
+                        r_, s_, l_, a_ = undo
+                        g.sal[r_], g.last[r_], g.acc[r_] = s_, l_, a_
+                    g._bump()
                 raise
-            if self.query_cache:
-                self.query_cache.invalidate_results()
-        self._link_within_shards(new_nodes)
-        self._link_to_existing_memories(new_nodes)
+        if self.query_cache:
+            self.query_cache.invalidate_results()
+        with tracer.stage("link", self._device):
+            made = self._link_batch(rows, kcodes, (ws[kt], wr[kt]), (ls[kt], lr[kt]), now)
+        if made:
+            self._say(f"✓ Created {made} cross-conversation links")
         self._enforce_buffer_limit()
         if self.enable_hierarchy:
             for skey in dict.fromkeys(sk for _, sk in new_nodes):
-                sh = self.shards.get(skey)
-                if sh is not None and len(sh.nodes) > self.super_node_threshold:
+                c = g.shard_code.get(skey)
+                if c is not None and g.shard_count[c] > self.super_node_threshold:
                     self._create_super_nodes_for_shard(skey)
         return new_nodes
 
-    # ------------------------------------------------------------ linking (K6)
-    def _link_within_shards(self, new_nodes: List[Tuple[str, str]]):
-        groups: Dict[str, List[str]] = defaultdict(list)
-        for nid, sk in new_nodes:
-            groups[sk].append(nid)
-        for sk, ids in groups.items():
-            if len(ids) < 2:
+    def _fact_matrix(self, embs, M: int):
+        """[M, D] fp32 device tensor + valid mask (right dim, finite, non-zero)."""
+        g = self.graph
+        if torch.is_tensor(embs):
+            E = embs.to(g.device, torch.float32)
+            if g.dim is None:
+                g._set_dim(E.shape[1])
+            if E.shape[1] != g.dim:
+                return E, np.zeros(M, dtype=bool)
+            ok = torch.isfinite(E).all(1) & (E.abs().sum(1) > 0)
+            return E, ok.cpu().numpy()
+        rows = list(embs) if embs is not None else []
+        if g.dim is None:
+            for e in rows:
+                if e is not None and len(e):
+                    g._set_dim(len(e))
+                    break
+        D = g.dim or 0
+        A = np.zeros((M, D), dtype=np.float32)
+        ok = np.zeros(M, dtype=bool)
+        for i in range(M):
+            e = rows[i] if i < len(rows) else None
+            if e is None or len(e) != D or degenerate_embedding(e):
                 continue
-            shard = self.shards[sk]
-            for a, b in zip(ids, ids[1:]):
-                shard.add_edge(Edge(source=a, target=b, weight=CHAIN_WEIGHT, edge_type="relates_to"))
-            new_set = set(ids)
-            cand_ids = [x for x in shard.nodes if x not in new_set]
-            if not cand_ids:
-                continue
-            Q = self._emb_cache.matrix([shard.nodes[x] for x in ids])
-            C = self._emb_cache.matrix([shard.nodes[x] for x in cand_ids], dim=Q.shape[1])
-            sims, idx = topk_cosine(Q, C, LINK_TOPK, device=self._device)
-            for qi, nid in enumerate(ids):
-                for s, j in zip(sims[qi], idx[qi]):
-                    if j >= 0 and s > LINK_THRESHOLD:
-                        shard.add_edge(Edge(source=nid, target=cand_ids[j], weight=float(s) * LINK_WEIGHT_SCALE,
-                                            edge_type="relates_to"))
+            A[i] = np.asarray(e, dtype=np.float32)
+            ok[i] = np.isfinite(A[i]).all()
+        return torch.from_numpy(A).to(g.device), ok
 
-    def _edge_exists_any(self, a: str, b: str) -> bool:
-        for sh in self.shards.values():
-            if (a, b) in sh.edges or (b, a) in sh.edges:
-                return True
-        return False
+    def _store_binds_graph(self) -> bool:
+        return getattr(self.vector_store, "bound_graph", lambda u: None)(self.user_id) is self.graph
 
-    def _link_to_existing_memories(self, new_nodes: List[Tuple[str, str]]):
-        if not new_nodes:
-            return
-        new_ids = {nid for nid, _ in new_nodes}
-        existing: Dict[str, Node] = {}
-        for sh in self.shards.values():
-            for nid, n in sh.nodes.items():
-                if nid not in new_ids and not n.is_super_node:
-                    existing[nid] = n
-        if not existing:
-            return
-        ex_ids = list(existing.keys())
-        live = [(nid, sk, self.buffer.get_node(nid)) for nid, sk in new_nodes]
-        live = [(nid, sk, n) for nid, sk, n in live if n is not None]
-        if not live:
-            return
-        Q = self._emb_cache.matrix([n for _, _, n in live])
-        C = self._emb_cache.matrix([existing[x] for x in ex_ids], dim=Q.shape[1])
-        sims, idx = topk_cosine(Q, C, LINK_TOPK, device=self._device)
-        made = 0
-        for qi, (nid, sk, _) in enumerate(live):
-            for s, j in zip(sims[qi], idx[qi]):
-                if j < 0 or not s > LINK_THRESHOLD:
-                    continue
-                tgt = ex_ids[j]
-                if self._edge_exists_any(nid, tgt):
-                    continue
-                sh = self.shards.get(sk)
-                if sh is not None:
-                    sh.add_edge(Edge(source=nid, target=tgt, weight=float(s) * LINK_WEIGHT_SCALE,
-                                     edge_type="relates_to"))
-                    made += 1
-        if made:
-            self._say(f"✓ Created {made} cross-conversation links")
+    def _scan_batch(self, Q: torch.Tensor, codes: torch.Tensor):
+        """Dedupe best rows + link candidate lists for a fact batch.
+
+        Returns (dup_row [M] long, -1 = not a duplicate), (global top-3 sims,
+        rows) over existing non-super nodes, (same-shard top-3 sims, rows).
+        Fast path (GPU, unit rows, store == graph nodes): one dual scan; the
+        dedupe top-1 over store rows is the better of the global list's head
+        and the (few) super-node rows. Otherwise the store search runs as the
+        reference does it (L2 top-1 over the store's rows) and the links use
+        the exact float64 scan."""
+        g = self.graph
+        n = g.n
+        M = Q.shape[0]
+        dev = g.device
+        link_mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
+        fast = g._use_kernel(M) and self._store_binds_graph() and self.vector_store.metric == "l2" and \
+            not bool(((g.stored[:n] == 1) & (g.kind[:n] != NODE)).any()) and \
+            not bool(((g.kind[:n] == NODE) & (g.stored[:n] == 0)).any())
+        kq = max(LINK_TOPK, 1)
+        (gs, gr), (ws, wr) = g.cos_topk(Q, kq, link_mask, dual_label=codes)
+        Qd = Q.to(dev, torch.float64)
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        if fast:
+            best_s, best_r = gs[:, 0].clone(), gr[:, 0].clone()
+            if g.n_super:
+                srows = torch.as_tensor(g.node_rows_where(super_=True), dtype=torch.long).to(dev)
+                ss, sr = g._exact_cos(Qn, torch.zeros(n, dtype=torch.bool, device=dev).index_fill_(0, srows, True), 1)
+                better = (ss[:, 0] > best_s) | ((ss[:, 0] == best_s) & (sr[:, 0] < best_r))
+                best_s = torch.where(better, ss[:, 0], best_s)
+                best_r = torch.where(better, sr[:, 0], best_r)
+            dup_rows = torch.where((best_r >= 0) & (best_s > DEDUPE_THRESHOLD), best_r, -1)
+        else:
+            _, top = self._store_top1(Q)
+            r1 = top.to(dev).reshape(M, -1)[:, 0]
+            ok = r1 >= 0
+            rr = r1.clamp_min(0)
+            isnode = (g.kind[rr] == NODE) & ok
+            X = g.emb32[rr].double()
+            nrm = g.sqn[rr].double().sqrt()
+            cs = (Qn * X).sum(1) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))
+            dup_rows = torch.where(isnode & (cs > DEDUPE_THRESHOLD), r1, -1)
+        return dup_rows, (gs, gr), (ws, wr)
+
+    def _store_top1(self, Q: torch.Tensor):
+        """Top-1 of the store's vector search for each fact -> graph rows."""
+        g = self.graph
+        if self._store_binds_graph():
+            return g.store_search(Q, 1, self.vector_store.metric)
+        ids = self._search_batch(Q.cpu().tolist(), 1)
+        rows = torch.as_tensor([g.row_of.get(r[0], -1) if r else -1 for r in ids], dtype=torch.long)
+        return None, rows
+
+    def _link_batch(self, rows: torch.Tensor, codes: np.ndarray, shard_hits, global_hits, now: float) -> int:
+        """Chain + within-shard + cross-memory edges for the new rows
+        (reference _link_within_shards :797-836, _link_to_existing :838-891).
+        Returns the number of cross-conversation links (the reference's count)."""
+        g = self.graph
+        dev = g.device
+        k = int(rows.numel())
+        rows = rows.to(dev)
+        ct = torch.as_tensor(codes, dtype=torch.int32).to(dev)
+        es, ed, ew, eh = [], [], [], []
+        # chain edges between consecutive new nodes of the same shard, in order
+        order = np.argsort(codes, kind="stable")
+        oc = codes[order]
+        same = np.nonzero(oc[1:] == oc[:-1])[0]
+        # the reference only links within shards that received >= 2 new nodes
+        if same.size:
+            a = torch.as_tensor(order[same], dtype=torch.long).to(dev)
+            b = torch.as_tensor(order[same + 1], dtype=torch.long).to(dev)
+            es.append(rows[a])
+            ed.append(rows[b])
+            ew.append(torch.full((a.numel(),), CHAIN_WEIGHT, device=dev))
+            eh.append(ct[a])
+        sw, sr = shard_hits
+        src = rows[:, None].expand(-1, sr.shape[1])
+        # within-shard similarity links only for shards with >= 2 new nodes (reference :814-815)
+        multi = np.zeros(k, dtype=bool)
+        uc, cnt = np.unique(codes, return_counts=True)
+        multi_codes = set(uc[cnt >= 2].tolist())
+        for i, c in enumerate(codes.tolist()):
+            multi[i] = c in multi_codes
+        mt = torch.as_tensor(multi).to(dev)
+        mw = (sr >= 0) & (sw > LINK_THRESHOLD) & mt[:, None]
+        es.append(src[mw])
+        ed.append(sr[mw])
+        ew.append((sw[mw] * LINK_WEIGHT_SCALE).float())
+        eh.append(ct[:, None].expand_as(sr)[mw])
+        gw, gr = global_hits
+        mg = (gr >= 0) & (gw > LINK_THRESHOLD)
+        # skip a cross-memory pair already linked within the shard (either direction)
+        in_shard = ((gr[:, :, None] == sr[:, None, :]) & mw[:, None, :]).any(dim=2)
+        mg = mg & ~in_shard
+        srcg = rows[:, None].expand(-1, gr.shape[1])
+        es.append(srcg[mg])
+        ed.append(gr[mg])
+        ew.append((gw[mg] * LINK_WEIGHT_SCALE).float())
+        eh.append(ct[:, None].expand_as(gr)[mg])
+        made = int(mg.sum())
+        S, Dd = torch.cat(es), torch.cat(ed)
+        if S.numel():
+            # keep the reference's edge order: per new node, chain first, then
+            # within-shard links, then cross-memory links
+            g.append_edges(S, Dd, torch.cat(ew), torch.cat(eh), g.etype("relates_to"), now=now)
+        return made
 
     # ------------------------------------------------------------ hierarchy (K8/K16)
     def _create_super_nodes_for_shard(self, shard_key: str):
-        shard = self.shards[shard_key]
-        if len(shard.nodes) < self.super_node_threshold:
+        g = self.graph
+        c = g.shard_code.get(shard_key)
+        if c is None or g.shard_count[c] < self.super_node_threshold:
             return
-        if any(n.shard_key == shard_key for n in self.super_nodes.values()):
+        srows = g.node_rows_where(super_=True)
+        if srows.size and (g.mirror("shard")[srows] == c).any():
             return
-        self._say(f"  Creating super-node for shard '{shard_key}' ({len(shard.nodes)} nodes)")
-        nodes = list(shard.nodes.values())
+        rows = g.node_rows_where(c, super_=False)
+        self._say(f"  Creating super-node for shard '{shard_key}' ({rows.size} nodes)")
         sid = f"super_{shard_key}_{int(time.time())}"
-        summary = f"Topic: {shard_key}. Contains memories about: " + "; ".join(n.content for n in nodes[:3])
-        embs = [n.embedding for n in nodes if n.embedding]
-        mean = np.mean(np.asarray(embs, dtype=np.float64), axis=0).tolist() if embs else []
-        sup = Node(id=sid, content=summary, embedding=mean, type="semantic", is_super_node=True,
-                   child_ids=[n.id for n in nodes], shard_key=shard_key)
-        for n in nodes:
-            n.parent_id = sid
-        self.super_nodes[sid] = sup
-        self._say(f"  ✓ Created super-node {sid} with {len(nodes)} children")
+        summary = f"Topic: {shard_key}. Contains memories about: " + "; ".join(g.content[r] for r in rows[:3])
+        rt = torch.as_tensor(rows, dtype=torch.long).to(g.device)
+        mean = g.mean_embedding(rt)
+        child_ids = [g.ids[r] for r in rows]
+        srow = g.add_nodes([sid], [summary], (mean[None, :].float() if mean is not None else None),
+                           shard=[c], sup=[1], children={0: child_ids}, stored=False)
+        with g.on_stream():
+            g.parent[rt] = srow.to(torch.int32)[0]
+            g.dirty[rt] = 1
+        g._bump()
+        self._say(f"  ✓ Created super-node {sid} with {rows.size} children")
 
     # ------------------------------------------------------------ deep consolidation
     def run_consolidation(self, weight_threshold: float = 0.6, merge_similar: bool = True) -> str:
         results = []
         self._say("🔄 Running consolidation...")
+        g = self.graph
         with self._graph_lock:
             if merge_similar:
                 merged = self._merge_similar_nodes(similarity_threshold=DEDUPE_THRESHOLD)
                 if merged > 0:
                     results.append(f"✓ Merged {merged} similar nodes")
-            comps = self.buffer.get_connected_components()
-            comp_of = {}
-            for ci, comp in enumerate(comps):
-                for nid in comp:
-                    comp_of[nid] = ci
-            wsum = defaultdict(float)
-            wcnt = defaultdict(int)
-            for sh in self.shards.values():
-                for (s, t), e in sh.edges.items():
-                    cs = comp_of.get(s)
-                    if cs is not None and cs == comp_of.get(t):
-                        wsum[cs] += e.weight
-                        wcnt[cs] += 1
+            with tracer.stage("components", self._device):
+                comps = g.components()
+                wsum, wcnt = g.component_edge_stats(comps)
+            contents = []
+            sup = g.mirror("sup")
+            kind = g.mirror("kind")
+            for i, comp in enumerate(comps):
+                if comp.size < 3 or not wcnt[i] or not wsum[i] / wcnt[i] > 0.3:
+                    contents.append(None)
+                    continue
+                contents.append([g.content[r] for r in comp.tolist() if kind[r] == NODE and not sup[r]])
         updates = 0
-        for ci, comp in enumerate(comps):
-            if len(comp) < 3 or not wcnt.get(ci):
+        for cs in contents:
+            if cs is None:
                 continue
-            if wsum[ci] / wcnt[ci] > 0.3:
-                r = self._extract_profile_from_component(comp)
-                if "Updated" in r:
-                    updates += 1
-                    results.append(r)
+            r = self._extract_profile_from_contents(cs) if cs else "No content to extract"
+            if "Updated" in r:
+                updates += 1
+                results.append(r)
         with self._graph_lock:
-            pruned = self.buffer.prune_weak_edges(threshold=self.prune_threshold)
+            pruned = g.prune(self.prune_threshold)
         if pruned > 0:
             results.append(f"✓ Pruned {pruned} weak edges")
         if updates > 0:
             results.append(f"✓ Updated {updates} profile domains")
         else:
-            contents = [n.content for n in self.buffer.nodes.values() if not n.is_super_node]
+            with self._graph_lock:
+                rows = g.ordered_node_rows()
+                sup = g.mirror("sup")
+                contents = [g.content[r] for r in rows if not sup[r]]
             if len(contents) >= 3:
                 r = self._extract_profile_from_contents(contents)
                 if "Updated" in r:
@@ -476,50 +555,93 @@ class ConsolidationMixin:
         return "Failed to extract profile"
 
     # ------------------------------------------------------------ merge (K7)
+    def _similar_pairs(self, rows: np.ndarray, tau: float) -> List[Tuple[int, int]]:
+        """Pairs (i < j, positions into ``rows``) with cosine > tau, sorted.
+        GPU + unit rows: candidates from the MFMA all-pairs kernel at a
+        lowered threshold (bf16 error margin), confirmed in float64."""
+        g = self.graph
+        m = rows.size
+        if m < 2:
+            return []
+        rt = torch.as_tensor(rows, dtype=torch.long).to(g.device)
+        with g.on_stream():
+            X = g.emb32[rt].double()
+            nrm = g.sqn[rt].double().sqrt()
+            U = X / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[:, None]
+            if g._use_kernel(m) and m * m >= (1 << 20):
+                from ..ops.graph_ops import pairs_above
+                U16 = torch.zeros((m, g.Dp), dtype=torch.bfloat16, device=g.device)
+                U16[:, : g.dim] = U.to(torch.bfloat16)
+                cand = pairs_above(U16, tau - 0.02).long()
+                if cand.numel() == 0:
+                    return []
+                cs = (U[cand[:, 0]] * U[cand[:, 1]]).sum(1)
+                p = cand[cs > tau]
+            else:
+                S = U @ U.T
+                iu = torch.triu_indices(m, m, 1, device=g.device)
+                keep = S[iu[0], iu[1]] > tau
+                p = torch.stack([iu[0][keep], iu[1][keep]], 1)
+            if p.numel() == 0:
+                return []
+            o = torch.argsort(p[:, 0] * m + p[:, 1])
+            return [tuple(x) for x in p[o].cpu().tolist()]
+
     def _merge_similar_nodes(self, similarity_threshold: float = DEDUPE_THRESHOLD) -> int:
-        nodes = self.buffer.nodes
-        if len(nodes) < 2:
+        g = self.graph
+        if g.num_nodes() < 2:
             return 0
         if self.merge_mode != "pairwise":
             # reference behaviour: the inner loop is dedented out of the outer
             # one (memory_system.py:1073-1077) so nothing is ever compared
             return 0
-        items = [(nid, n) for nid, n in nodes.items() if not n.is_super_node]
-        if len(items) < 2:
+        # the intended semantics: for i < j in node order, merge j into i
+        rows = g.ordered_node_rows()
+        rows = rows[g.mirror("sup")[rows] == 0]
+        pairs = self._similar_pairs(rows, similarity_threshold)
+        if not pairs:
             return 0
-        M = self._emb_cache.matrix([n for _, n in items])
-        S = M @ M.T
-        processed: Set[str] = set()
+        processed: Set[int] = set()
         merged = 0
-        for i, (id1, n1) in enumerate(items):
-            if id1 in processed:
+        touched_store = []
+        sal, acc = g.mirror("sal").copy(), g.mirror("acc").copy()
+        for i, j in pairs:
+            if i in processed or j in processed:
                 continue
-            for j in range(i + 1, len(items)):
-                id2, n2 = items[j]
-                if id2 in processed or not S[i, j] > similarity_threshold:
-                    continue
-                n1.content = f"{n1.content} | {n2.content}"
-                n1.salience = max(n1.salience, n2.salience)
-                n1.access_count += n2.access_count
-                for sh in self.shards.values():
-                    if id2 not in sh.nodes:
-                        continue
-                    for key in list(sh.edges.incident(id2)):
-                        e = sh.edges.pop(key)
-                        s, t = key
-                        e.source, e.target = (id1 if s == id2 else s), (id1 if t == id2 else t)
-                        if (e.source, e.target) in sh.edges:
-                            sh.add_edge(e)
-                        else:
-                            sh.edges[(e.source, e.target)] = e
-                    del sh.nodes[id2]
-                    break
-                processed.add(id2)
-                merged += 1
-                self._emb_cache.forget([id2])
-                self.vector_store.delete_nodes([id2, id1], user_id=self.user_id)
-                self.vector_store.add_nodes([{
+            r1, r2 = int(rows[i]), int(rows[j])
+            g.content[r1] = f"{g.content[r1]} | {g.content[r2]}"
+            sal[r1] = max(sal[r1], sal[r2])
+            acc[r1] = acc[r1] + acc[r2]
+            g.set_scalar(r1, "sal", float(sal[r1]))
+            g.set_scalar(r1, "acc", int(acc[r1]))
+            self._rewire(r2, r1)
+            g.remove_nodes([r2], drop_edges=False, unstore=True)
+            processed.add(j)
+            merged += 1
+            touched_store.append((g.ids[r2], g.ids[r1]))
+        for id2, id1 in touched_store:
+            self._store_delete([id2, id1])
+            n1 = self.buffer.get_node(id1)
+            if n1 is not None:
+                self._store_add_rows([g.row_of[id1]], [{
                     "id": id1, "content": n1.content, "embedding": n1.embedding, "type": n1.type,
-                    "salience": n1.salience, "shard_key": n1.shard_key, "timestamp": n1.timestamp}],
-                    user_id=self.user_id)
+                    "salience": n1.salience, "shard_key": n1.shard_key, "timestamp": n1.timestamp}])
         return merged
+
+    def _rewire(self, r_from: int, r_to: int) -> None:
+        """Move the edges of ``r_from``'s shard that touch it onto ``r_to``; a
+        moved edge whose new key already exists strengthens that edge
+        (reference memory_system.py:1087-1104)."""
+        g = self.graph
+        sc = int(g.mirror("shard")[r_from])
+        idx = g.edges_incident(r_from, sc)
+        if idx.numel() == 0:
+            return
+        with g.on_stream():
+            e = g.e
+            s, d = e["src"][idx].clone(), e["dst"][idx].clone()
+            w, co, lu, meta = e["w"][idx].clone(), e["co"][idx].clone(), e["lu"][idx].clone(), e["meta"][idx].clone()
+        g.remove_edges(idx)
+        s = torch.where(s == r_from, torch.full_like(s, r_to), s)
+        d = torch.where(d == r_from, torch.full_like(d, r_to), d)
+        g.upsert_edges(s, d, w, meta & SHARD_MASK, (meta >> 24) & 0x3F, co=co, lu=lu)

@@ -94,6 +94,19 @@ class OnDeviceEmbedder:
         acc = torch.zeros((len(texts), v.shape[1]), dtype=v.dtype, device=v.device).index_add_(0, own, v)
         return acc / acc.norm(dim=1, keepdim=True).clamp_min(1e-30)
 
+    def batch_embed_tensor(self, texts: List[str]) -> torch.Tensor:
+        """[n, H] fp32 unit vectors on the encoder's device, in input order
+        (no host round trip: the memory graph ingests / searches with it)."""
+        if any(len(t) > 4 * self.max_len for t in texts):
+            return torch.as_tensor(np.asarray(self.batch_embed(texts), dtype=np.float32)).to(self.device)
+        order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
+        out = torch.empty((len(texts), self.dim), dtype=torch.float32, device=self.device)
+        for s in range(0, len(order), self.max_batch):
+            idx = order[s: s + self.max_batch]
+            v32, _ = self.embed_tensor([texts[i] for i in idx])
+            out[torch.as_tensor(idx, dtype=torch.long, device=self.device)] = v32.float()
+        return out
+
     def batch_embed(self, texts: List[str]) -> List[List[float]]:
         if not texts:
             return []

@@ -2,16 +2,24 @@
 ``src/lazzaro/core/memory_system.py:21-1550``).
 
 Public API, constructor kwargs and defaults are the reference's (SURVEY.md
-App. A/B) so existing code switches by changing the import. The engine under
-it is MI355X-first:
+App. A/B) so existing code switches by changing the import. Underneath, the
+tenant's memory graph is a :class:`~lazzaro_amd.engine.TenantGraph`: node
+and edge columns in HBM (``device=cuda``) or host memory (``device=cpu``),
+and every graph operation -- dedupe, linking, decay/prune, eviction, neighbour
+boost, components, super-node centroids, the store's vector search -- is a
+HIP kernel or a batched tensor op on it (see :mod:`lazzaro_amd.engine`).
+``shards`` / ``super_nodes`` / ``buffer`` and the ``Node`` / ``Edge`` objects
+they hand out are façades over those columns (:mod:`lazzaro_amd.engine.views`).
 
-* vectors live in per-tenant HBM arenas (``HBMStore``); search, dedupe, super
-  node scoring and linking are batched device/host GEMMs with fused top-k
-  (``lazzaro_amd.ops``), never per-pair Python loops;
-* persistence is the native versioned columnar store;
-* embeddings can run on-device (``core.embedders.OnDeviceEmbedder``: BERT-family
-  encoders on hand-written MFMA GEMM / attention / LayerNorm kernels);
-* background consolidation is serialised against the caller with a graph lock.
+* The default store (``HBMStore``) serves this tenant's vector search from the
+  graph's own rows (one copy of the vectors in HBM) and persists changes
+  incrementally: each commit writes the rows and edges that changed, plus
+  deletions, instead of the reference's delete-all + add-all per save
+  (:1275-1302). Temporal decay is not a row change: each row records the
+  decay clock at which it was written and a reload replays the decay since.
+* Embeddings can run on-device (``core.embedders.OnDeviceEmbedder``) and stay
+  device tensors into the graph.
+* Background consolidation is serialised against the caller with a graph lock.
 
 Constructor additions (all keyword, all optional): ``device``, ``metric``
 (store search metric, default "l2" like LanceDB), ``merge_mode``
@@ -21,24 +29,27 @@ from __future__ import annotations
 
 import json
 import logging
+import math
 import os
+import re
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional
 
 import numpy as np
+import torch
 
+from ..engine.tenant_graph import NODE, TenantGraph
+from ..engine.views import GraphBuffer, NodeView, ShardView, ShardsMap, SuperNodesMap, import_edges, import_nodes
 from ..models.graph import Edge, Node
 from . import providers as _providers
-from .buffer_graph import BufferGraph
 from .consolidation import ConsolidationMixin
 from .interfaces import EmbeddingProvider, LLMProvider, Store
 from .memory_shard import MemoryShard
 from .profile import EMPTY_CONTEXT, Profile
 from .providers import HashEmbedder, LocalLLM, OpenAIEmbedder, OpenAILLM, cosine
 from .query_cache import QueryCache
-from .similarity import EmbeddingCache, topk_cosine
 from .vector_store import HBMStore
 from ..utils.faults import StoreError, degenerate_embedding, fault_point
 from ..utils.tracing import tracer
@@ -61,6 +72,8 @@ HISTORY_WINDOW = 10
 SUPER_MATCH = 0.4
 SUPER_CHILDREN = 10
 RESULT_LIMIT = 5
+SALIENCE_FLOOR = 0.2
+_NODE_ID = re.compile(r"^node_(\d+)$")
 
 
 class MemorySystem(ConsolidationMixin):
@@ -112,17 +125,13 @@ class MemorySystem(ConsolidationMixin):
         else:
             self.embedder = _default_local_embedder()
 
-        self.shards: Dict[str, MemoryShard] = {}
-        self.super_nodes: Dict[str, Node] = {}
-        self.buffer = BufferGraph(self.shards, self.super_nodes)
         self.profile = Profile()
         self.store = store if store is not None else HBMStore(db_dir=db_dir, device=device, metric=metric,
                                                               index=index, **(index_params or {}))
         self.vector_store = self.store
-        self._device = getattr(self.store, "device", None)
-        if isinstance(self._device, str):
-            import torch
-            self._device = torch.device(self._device)
+        dev = device if device is not None else getattr(self.store, "device", None)
+        self._device = torch.device(dev) if dev is not None else torch.device("cpu")
+        self.graph = self._new_graph()
 
         self.enable_sharding = enable_sharding
         self.enable_hierarchy = enable_hierarchy
@@ -149,7 +158,6 @@ class MemorySystem(ConsolidationMixin):
         self._pending = []
         self._queue_lock = threading.Lock()
         self._graph_lock = threading.RLock()
-        self._emb_cache = EmbeddingCache()
 
         self.conversation_active = False
         self.short_term_memory: List[Dict] = []
@@ -178,6 +186,48 @@ class MemorySystem(ConsolidationMixin):
         return cls(**cfg.reference_kwargs(), embedding_provider=emb, device=cfg.device, metric=cfg.metric,
                    merge_mode=cfg.merge_mode, verbose=cfg.verbose, **kw)
 
+    # ------------------------------------------------------------ graph + views
+    def _new_graph(self) -> TenantGraph:
+        g = TenantGraph(device=self._device)
+        attach = getattr(self.store, "attach", None)
+        if attach is not None:
+            attach(self.user_id, g)
+        return g
+
+    @property
+    def shards(self) -> ShardsMap:
+        return ShardsMap(self.graph)
+
+    @shards.setter
+    def shards(self, value: Dict[str, MemoryShard]) -> None:
+        with self._graph_lock:
+            self._replace_graph()
+            for k, sh in value.items():
+                self.shards[k] = sh
+
+    @property
+    def super_nodes(self) -> SuperNodesMap:
+        return SuperNodesMap(self.graph)
+
+    @super_nodes.setter
+    def super_nodes(self, value: Dict[str, Node]) -> None:
+        with self._graph_lock:
+            sm = self.super_nodes
+            for k in list(sm):
+                del sm[k]
+            for k, n in value.items():
+                sm[k] = n
+
+    @property
+    def buffer(self) -> GraphBuffer:
+        return GraphBuffer(self.graph)
+
+    def _replace_graph(self) -> None:
+        detach = getattr(self.store, "detach", None)
+        if detach is not None:
+            detach(self.user_id)
+        self.graph = self._new_graph()
+
     # ------------------------------------------------------------ helpers
     def _say(self, msg: str) -> None:
         log.info(msg)
@@ -198,10 +248,7 @@ class MemorySystem(ConsolidationMixin):
         return time.strftime("%Y-%m")
 
     def _get_or_create_shard(self, shard_key: str) -> MemoryShard:
-        sh = self.shards.get(shard_key)
-        if sh is None:
-            sh = self.shards[shard_key] = MemoryShard(shard_key)
-        return sh
+        return ShardView(self.graph, self.graph.shard_id(shard_key))
 
     def _get_embedding(self, text: str) -> List[float]:
         self.metrics["embedding_calls"] += 1
@@ -222,6 +269,16 @@ class MemorySystem(ConsolidationMixin):
         fault_point("provider.embed")
         return self.embedder.batch_embed(texts)
 
+    def _batch_embed_any(self, texts: List[str]):
+        """Batch embedding as a device tensor when the provider can produce
+        one (on-device encoder: no host round trip), else the protocol's lists."""
+        # a class-level method only (a MagicMock provider answers every getattr)
+        if getattr(type(self.embedder), "batch_embed_tensor", None) is None or not texts:
+            return self._batch_embed(texts)
+        self.metrics["embedding_calls"] += 1
+        fault_point("provider.embed")
+        return self.embedder.batch_embed_tensor(texts)
+
     def _cosine_similarity(self, v1, v2) -> float:
         return cosine(v1, v2)
 
@@ -230,11 +287,23 @@ class MemorySystem(ConsolidationMixin):
         fault_point("provider.llm")
         return self.llm.completion(messages, response_format)
 
-    def _search_batch(self, embs: List[List[float]], k: int) -> List[List[str]]:
+    def _search_batch(self, embs, k: int) -> List[List[str]]:
         fn = getattr(self.vector_store, "search_nodes_batch", None)
         if fn is not None:
             return fn(embs, user_id=self.user_id, limit=k)
         return [self.vector_store.search_nodes(e, user_id=self.user_id, limit=k) for e in embs]
+
+    def _store_delete(self, ids: List[str]) -> None:
+        if ids:
+            self.vector_store.delete_nodes(ids, user_id=self.user_id)
+
+    def _store_add_rows(self, rows: List[int], dicts: List[Dict]) -> None:
+        """Re-add rows to the store (merge): the bound store only flags them;
+        a third-party store gets the reference's add_nodes."""
+        if self._store_binds_graph():
+            self.graph.mark_stored(rows)
+        else:
+            self.vector_store.add_nodes(dicts, user_id=self.user_id)
 
     # ------------------------------------------------------------ conversation
     def start_conversation(self) -> str:
@@ -255,44 +324,51 @@ class MemorySystem(ConsolidationMixin):
 
     # ------------------------------------------------------------ retrieval
     def _boost_neighbors(self, retrieved_ids: List[str]):
-        neigh = []
-        seen = set()
-        for nid in retrieved_ids:
-            for nb in self.buffer.get_neighbors(nid):
-                if nb not in seen:
-                    seen.add(nb)
-                    neigh.append(nb)
-        count = 0
-        now = time.time()
-        for nid in neigh:
-            if nid in retrieved_ids:
-                continue
-            n = self.buffer.get_node(nid)
-            if n is not None:
-                n.last_accessed = now
-                n.salience = min(1.0, n.salience + 0.02)
-                count += 1
+        """Reference :242-260 on the device graph: one ``tg_boost_kernel``
+        launch over the visible-arc CSR of the retrieved rows."""
+        g = self.graph
+        rows = [g.node_row(i, include_super=False) for i in retrieved_ids]
+        count = g.boost(rows)
         if count:
             self._say(f"   (Graph: Boosted {count} neighbor nodes via association)")
 
-    def _optimized_retrieval(self, query_emb: List[float], query_text: str) -> List[str]:
+    def _super_best(self, query_emb) -> int:
+        """Row of the super-node most similar to the query (float64 cosine,
+        first on ties), or -1 when none beats SUPER_MATCH (reference :464-472)."""
+        g = self.graph
+        srows = g.node_rows_where(super_=True)
+        if srows.size == 0 or g.dim is None:
+            return -1
+        q = torch.as_tensor(np.asarray(query_emb, dtype=np.float64)) if not torch.is_tensor(query_emb) \
+            else query_emb.double()
+        if q.numel() != g.dim:
+            return -1
+        with g.on_stream():
+            rt = torch.as_tensor(srows, dtype=torch.long).to(g.device)
+            X = g.emb32[rt].double()
+            nx = g.sqn[rt].double().sqrt()
+            qd = q.to(g.device).reshape(-1)
+            nq = qd.norm()
+            s = (X @ qd) / torch.where(nx * nq > 0, nx * nq, torch.ones_like(nx))
+            s = torch.where((nx > 0) & (nq > 0), s, torch.zeros_like(s))
+            j = int(torch.argmax(s))  # first maximum
+            best = float(s[j])
+        return int(srows[j]) if best > SUPER_MATCH else -1
+
+    def _optimized_retrieval(self, query_emb, query_text: str) -> List[str]:
         if self.query_cache:
             cached = self.query_cache.get_results(query_text)
             if cached:
                 return cached
+        g = self.graph
         retrieved: List[str] = []
-        if self.enable_hierarchy and self.super_nodes:
-            sup = list(self.super_nodes.values())
-            q = np.asarray(query_emb, dtype=np.float64)
-            qn = np.linalg.norm(q)
-            qu = q / qn if qn > 0 else q
-            S = self._emb_cache.matrix(sup, dim=qu.shape[0])
-            sims, idx = topk_cosine(qu[None, :], S, 1)
-            if idx[0, 0] >= 0 and sims[0, 0] > SUPER_MATCH:
-                best = sup[idx[0, 0]]
-                for cid in best.child_ids[:SUPER_CHILDREN]:
-                    c = self.buffer.get_node(cid)
-                    if c is not None and not c.is_super_node:
+        if self.enable_hierarchy and g.n_super:
+            sr = self._super_best(query_emb)
+            if sr >= 0:
+                kind, sup = g.mirror("kind"), g.mirror("sup")
+                for cid in g.children.get(sr, [])[:SUPER_CHILDREN]:
+                    r = g.row_of.get(cid)
+                    if r is not None and kind[r] == NODE and not sup[r]:
                         retrieved.append(cid)
                 if len(retrieved) >= RESULT_LIMIT:
                     if self.query_cache:
@@ -300,20 +376,19 @@ class MemorySystem(ConsolidationMixin):
                     return retrieved[:RESULT_LIMIT]
         limit = 10 if not retrieved else 5
         vec_ids = self.vector_store.search_nodes(query_emb, user_id=self.user_id, limit=limit)
+        kind = g.mirror("kind")
         seen_ids = set(retrieved)
         seen_content = set()
         final = []
         for rid in retrieved:
-            n = self.buffer.get_node(rid)
-            if n is not None:
-                seen_content.add(n.content)
-                final.append(rid)
+            seen_content.add(g.content[g.row_of[rid]])
+            final.append(rid)
         for rid in vec_ids:
             if rid in seen_ids:
                 continue
-            n = self.buffer.get_node(rid)
-            if n is not None and n.content not in seen_content:
-                seen_content.add(n.content)
+            r = g.row_of.get(rid)
+            if r is not None and kind[r] == NODE and g.content[r] not in seen_content:
+                seen_content.add(g.content[r])
                 final.append(rid)
                 seen_ids.add(rid)
         final = final[:RESULT_LIMIT]
@@ -327,12 +402,10 @@ class MemorySystem(ConsolidationMixin):
         if pc and pc != EMPTY_CONTEXT:
             parts.append(f"User Profile:\n{pc}\n")
         if retrieved_ids:
-            texts = []
-            for nid in retrieved_ids:
-                n = self.buffer.get_node(nid)
-                if n is not None:
-                    texts.append(f"- {n.content}")
-                    self.buffer.update_access(nid)
+            g = self.graph
+            rows = [g.node_row(i) for i in retrieved_ids]
+            texts = [f"- {g.content[r]}" for r in rows if r >= 0]
+            g.touch(rows)  # update_access for each retrieved node (buffer_graph.py:79-85)
             if texts:
                 parts.append("Relevant Information from Past Conversations (Use if relevant to the query):\n"
                              + "\n".join(texts) + "\n")
@@ -367,20 +440,23 @@ class MemorySystem(ConsolidationMixin):
         return f"[{emoji} Retrieval: {ms:.0f}ms, Retrieved: {n} nodes]"
 
     def _node_lines(self, ids: List[str]) -> List[str]:
+        g = self.graph
         out = []
+        sh = g.mirror("shard")
         for nid in ids:
-            n = self.buffer.get_node(nid)
-            if n is not None:
-                snip = n.content[:60] + "..." if len(n.content) > 60 else n.content
-                out.append(f"   • [{nid}] ({n.shard_key}) {snip}")
+            r = g.node_row(nid)
+            if r >= 0:
+                c = g.content[r]
+                snip = c[:60] + "..." if len(c) > 60 else c
+                out.append(f"   • [{nid}] ({g.shard_names[sh[r]] if sh[r] >= 0 else 'default'}) {snip}")
         return out
 
     def chat(self, user_message: str) -> str:
         ids, ms = self._retrieve_for(user_message)
         self.metrics["retrieval_times"].append(ms)
         with self._graph_lock:
-            msgs = self._build_messages(ids)
             node_lines = self._node_lines(ids)
+            msgs = self._build_messages(ids)
         with tracer.stage("llm", "cpu"):
             response = self._call_llm(msgs)
         self.add_to_short_term(response, "semantic", salience=0.5)
@@ -417,7 +493,7 @@ class MemorySystem(ConsolidationMixin):
 
     def _get_relevant_shards(self, query: str, max_shards: int = 3) -> List[str]:
         """Recency/size shard ranking (present but unused in the reference, :516-533)."""
-        if not self.enable_sharding or not self.shards:
+        if not self.enable_sharding or not len(self.shards):
             return ["default"]
         if len(self.shards) <= 5:
             return list(self.shards.keys())
@@ -435,15 +511,26 @@ class MemorySystem(ConsolidationMixin):
             return self._connected(node_id)
 
     def _connected(self, node_id: str) -> List[Node]:
-        ids = []
-        seen = set()
-        for sh in list(self.shards.values()):
-            for s, t in sh.edges.incident(node_id):
-                o = t if s == node_id else s
-                if o not in seen:
-                    seen.add(o)
-                    ids.append(o)
-        return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
+        """Other endpoints of every edge touching the node, any shard, in the
+        reference's order (shards in order, edges in order; :1441-1458)."""
+        g = self.graph
+        r = g.row_of.get(node_id)
+        if r is None:
+            return []
+        idx = g.edges_incident(r)
+        with g.on_stream():
+            sh = (g.e["meta"][idx] & 0xFFFFFF).long()
+            o = torch.sort(sh, stable=True).indices
+            idx = idx[o]
+            s, d = g.e["src"][idx].tolist(), g.e["dst"][idx].tolist()
+        out, seen = [], set()
+        for a, b in zip(s, d):
+            o_ = b if a == r else a
+            if o_ not in seen:
+                seen.add(o_)
+                out.append(o_)
+        kind = g.mirror("kind")
+        return [NodeView.of(g, x) for x in out if kind[x] == NODE]
 
     def search_memories(self, query: str, limit: int = 5) -> List[Node]:
         with tracer.stage("embed_query", self._device):
@@ -454,11 +541,20 @@ class MemorySystem(ConsolidationMixin):
             return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
 
     def search_memories_batch(self, queries: List[str], limit: int = 5) -> List[List[Node]]:
-        """Batched search: one embedding call and one fused top-k launch."""
-        embs = self._batch_embed(list(queries))
-        res = self._search_batch(embs, limit)
+        """Batched ``search_memories``: one embedding call (device tensor when
+        the encoder is on-device), one fused top-k launch, one id mapping."""
+        with tracer.stage("embed_query", self._device):
+            embs = self._batch_embed_any(list(queries))
+        with tracer.stage("search", self._device):
+            res = self._search_batch(embs, limit)
         with self._graph_lock:
-            return [[n for n in (self.buffer.get_node(i) for i in ids) if n is not None] for ids in res]
+            g = self.graph
+            kind = g.mirror("kind")
+            out = []
+            for ids in res:
+                rows = [g.row_of.get(i, -1) for i in ids]
+                out.append([NodeView.of(g, r) for r in rows if r >= 0 and kind[r] == NODE])
+            return out
 
     # ------------------------------------------------------------ stats / display
     def get_stats(self) -> Dict:
@@ -466,7 +562,8 @@ class MemorySystem(ConsolidationMixin):
             return self._stats()
 
     def _stats(self) -> Dict:
-        nodes, edges = self.buffer.size()
+        g = self.graph
+        nodes, edges = g.num_nodes(), g.num_edges
         rt = self.metrics["retrieval_times"]
         ct = self.metrics["consolidation_times"]
         avg_r = float(np.mean(rt)) if rt else 0.0
@@ -476,8 +573,8 @@ class MemorySystem(ConsolidationMixin):
         return {
             "buffer_nodes": nodes,
             "buffer_edges": edges,
-            "num_shards": len(self.shards),
-            "num_super_nodes": len(self.super_nodes),
+            "num_shards": len(g.live_shards()),
+            "num_super_nodes": g.n_super,
             "short_term_memories": len(self.short_term_memory),
             "conversation_active": self.conversation_active,
             "conversation_count": self.conversation_count,
@@ -493,6 +590,18 @@ class MemorySystem(ConsolidationMixin):
                 "embedding_calls": self.metrics["embedding_calls"],
             },
         }
+
+    def engine_stats(self) -> Dict:
+        """Engine-level metrics beyond the reference's ``get_stats`` (SURVEY.md
+        §5 metrics row): device, HBM bytes held by the tenant graph, rows,
+        edges, per-stage timings from the tracer when enabled."""
+        g = self.graph
+        nbytes = sum(t.numel() * t.element_size() for t in
+                     [g.emb32, g.emb16, g.sqn] + [getattr(g, c) for c, _, _ in TenantGraph.NODE_COLS]
+                     + list(g.e.values()) if t is not None)
+        return {"device": str(self._device), "rows": g.n, "capacity": g.cap, "nodes": g.num_nodes(),
+                "edges": g.num_edges, "graph_bytes": int(nbytes), "dim": g.dim,
+                "decay_clock": g.decay_log, "stages": tracer.summary()}
 
     def display_stats(self) -> str:
         s = self.get_stats()
@@ -530,7 +639,7 @@ STORAGE:
 """
 
     def display_memories(self, limit: int = 10) -> str:
-        if not self.buffer.nodes:
+        if self.graph.num_nodes() == 0:
             return "No memories stored yet."
         nodes = self.buffer.get_all_nodes_summary()
         out = [f"\n💭 Stored Memories (showing {min(limit, len(nodes))} of {len(nodes)}):"]
@@ -547,16 +656,17 @@ STORAGE:
     _SETTINGS = ("auto_consolidate", "consolidate_every", "auto_prune", "prune_threshold", "max_buffer_size")
 
     def save_state(self, filename: str = "memory_state.json") -> str:
-        state = {
-            "shards": {k: {"nodes": [n.to_dict() for n in sh.nodes.values()],
-                           "edges": [e.to_dict() for e in sh.edges.values()]}
-                       for k, sh in self.shards.items()},
-            "super_nodes": [n.to_dict() for n in self.super_nodes.values()],
-            "profile": self.profile.to_dict(),
-            "node_counter": self.node_counter,
-            "conversation_count": self.conversation_count,
-            "settings": {k: getattr(self, k) for k in self._SETTINGS},
-        }
+        with self._graph_lock:
+            state = {
+                "shards": {k: {"nodes": [n.to_dict() for n in sh.nodes.values()],
+                               "edges": [e.to_dict() for e in sh.edges.values()]}
+                           for k, sh in self.shards.items()},
+                "super_nodes": [n.to_dict() for n in self.super_nodes.values()],
+                "profile": self.profile.to_dict(),
+                "node_counter": self.node_counter,
+                "conversation_count": self.conversation_count,
+                "settings": {k: getattr(self, k) for k in self._SETTINGS},
+            }
         with open(filename, "w") as f:
             json.dump(state, f, indent=2)
         return f"✓ State saved to {filename}"
@@ -568,20 +678,19 @@ STORAGE:
         except FileNotFoundError:
             return f"⚠ File {filename} not found"
         with self._graph_lock:
-            shards: Dict[str, MemoryShard] = {}
+            self._replace_graph()
+            g = self.graph
             for k, d in state.get("shards", {}).items():
-                sh = MemoryShard(k)
-                for nd in d.get("nodes", []):
-                    sh.add_node(Node.from_dict(nd))
-                for ed in d.get("edges", []):
-                    sh.add_edge(Edge.from_dict(ed))
-                shards[k] = sh
-            self.shards = shards
-            self.super_nodes = {n["id"]: Node.from_dict(n) for n in state.get("super_nodes", [])}
-            self.buffer = BufferGraph(self.shards, self.super_nodes)  # reference forgets this
-            pd = state.get("profile", {})
-            self.profile.data = pd.get("data", self.profile.data)
-            self.profile.last_updated = pd.get("last_updated", time.time())
+                g.shard_id(k)
+                nodes = [Node.from_dict(nd) for nd in d.get("nodes", [])]
+                import_nodes(g, nodes, [k] * len(nodes), supers=[False] * len(nodes))
+                edges = [Edge.from_dict(ed) for ed in d.get("edges", [])]
+                import_edges(g, edges, [k] * len(edges))
+            sups = [Node.from_dict(n) for n in state.get("super_nodes", [])]
+            import_nodes(g, sups, [n.shard_key or "default" for n in sups], supers=[True] * len(sups))
+            pd_ = state.get("profile", {})
+            self.profile.data = pd_.get("data", self.profile.data)
+            self.profile.last_updated = pd_.get("last_updated", time.time())
             self.node_counter = state.get("node_counter", 0)
             self.conversation_count = state.get("conversation_count", 0)
             for k, v in state.get("settings", {}).items():
@@ -590,27 +699,29 @@ STORAGE:
         return f"✓ State loaded from {filename}"
 
     # ------------------------------------------------------------ store sync
+    def _profile_blob(self) -> Dict:
+        d = self.profile.to_dict()
+        d["_engine"] = {"decay_clock": self.graph.decay_log, "node_counter": self.node_counter}
+        return d
+
     def _save_to_persistence(self):
-        """Write the tenant's graph to the store (reference memory_system.py:
-        1275-1302). With a native store the rewrite is one atomic version per
-        table. A failed commit leaves the in-memory graph authoritative: it is
-        counted, logged, and the next save rewrites everything again
-        (``strict_errors`` raises :class:`StoreError` instead)."""
+        """Persist the tenant (reference memory_system.py:1275-1302).
+
+        With the default store (graph-bound ``HBMStore``) this is ONE
+        incremental commit per table: rows and edges changed since the last
+        commit are upserted, removed ones deleted -- O(changes), not O(graph).
+        A third-party ``Store`` gets the reference's delete-all + add-all.
+        A failed commit leaves the graph authoritative and the change set
+        pending (it is retried by the next save); ``strict_errors`` raises
+        :class:`StoreError` instead."""
         with self._graph_lock:
-            nodes = [n.to_dict() for n in self.buffer.nodes.values()]
-            edges = [e.to_dict() for sh in self.shards.values() for e in sh.edges.values()]
             try:
-                if hasattr(self.store, "replace_user_nodes"):
-                    self.store.replace_user_nodes(nodes, user_id=self.user_id)
-                    self.store.replace_user_edges(edges, user_id=self.user_id)
-                else:  # third-party Store protocol: the reference's delete + add
-                    self.store.delete_nodes([], user_id=self.user_id)
-                    self.store.delete_edges(user_id=self.user_id)
-                    if nodes:
-                        self.store.add_nodes(nodes, user_id=self.user_id)
-                    if edges:
-                        self.store.add_edges(edges, user_id=self.user_id)
-                self.store.save_profile(self.profile.to_dict(), user_id=self.user_id)
+                with tracer.stage("persist", "cpu"):
+                    if self._store_binds_graph():
+                        self._commit_incremental()
+                    else:
+                        self._rewrite_all()
+                    self.store.save_profile(self._profile_blob(), user_id=self.user_id)
             except Exception as e:
                 self.metrics["persist_failures"] = self.metrics.get("persist_failures", 0) + 1
                 self._persist_pending = True
@@ -630,70 +741,81 @@ STORAGE:
                 self.query_cache.invalidate_results()
         self._say(f"✓ State persisted for user: {self.user_id}")
 
+    def _commit_incremental(self) -> None:
+        g = self.graph
+        rows = g.take_dirty_rows()
+        eidx = g.take_dirty_edges()
+        del_ids, del_edges = g.take_deleted()
+        try:
+            kind = g.mirror("kind")
+            rows = rows[kind[rows] == NODE] if rows.size else rows
+            node_cols = export_node_columns(g, rows)
+            edge_cols = export_edge_columns(g, eidx)
+            self.store.commit_tenant(self.user_id, node_cols, del_ids, edge_cols,
+                                     [f"{s}_{t}" for s, t in del_edges])
+        except Exception:
+            g.restore_tracking(rows, eidx, del_ids, del_edges)
+            raise
+        g.mark_stored(rows)
+        # ids deleted from the table leave the searchable set too
+        gone = [i for i in del_ids if g.node_row(i) < 0]
+        if gone:
+            g.unstore(gone)
+
+    def _rewrite_all(self) -> None:
+        nodes = [n.to_dict() for n in self.buffer.nodes.values()]
+        edges = [e.to_dict() for sh in self.shards.values() for e in sh.edges.values()]
+        if hasattr(self.store, "replace_user_nodes"):
+            self.store.replace_user_nodes(nodes, user_id=self.user_id)
+            self.store.replace_user_edges(edges, user_id=self.user_id)
+        else:  # third-party Store protocol: the reference's delete + add
+            self.store.delete_nodes([], user_id=self.user_id)
+            self.store.delete_edges(user_id=self.user_id)
+            if nodes:
+                self.store.add_nodes(nodes, user_id=self.user_id)
+            if edges:
+                self.store.add_edges(edges, user_id=self.user_id)
+        self.graph.clear_tracking()
+
     def _load_from_persistence(self):
+        """Rebuild the tenant graph from the store (reference :1304-1410):
+        columns go straight into the graph (vectors: one host->device copy),
+        no per-row ``Node`` objects; decay since each row was written is
+        replayed from the persisted decay clock."""
         self._say(f"🔄 Loading state for user: {self.user_id}...")
         with self._graph_lock:
-            rows = self.store.get_nodes(user_id=self.user_id)
-            shards: Dict[str, MemoryShard] = {}
-            supers: Dict[str, Node] = {}
-            for nd in rows:
-                nd = dict(nd)
-                if "vector" in nd:
-                    v = nd.pop("vector")
-                    nd["embedding"] = v.tolist() if hasattr(v, "tolist") else list(v)
-                if isinstance(nd.get("child_ids"), str):
-                    try:
-                        nd["child_ids"] = json.loads(nd["child_ids"])
-                    except json.JSONDecodeError:
-                        nd["child_ids"] = []
-                n = Node.from_dict(nd)
-                if n.is_super_node:
-                    supers[n.id] = n
-                else:
-                    sh = shards.get(n.shard_key)
-                    if sh is None:
-                        sh = shards[n.shard_key] = MemoryShard(n.shard_key)
-                    sh.add_node(n)
-            edge_rows = self.store.get_edges(user_id=self.user_id) if rows else []
-            for ed in edge_rows:
-                ed = dict(ed)
-                if "source_id" in ed:
-                    ed["source"] = ed.pop("source_id")
-                if "target_id" in ed:
-                    ed["target"] = ed.pop("target_id")
-                if "type" in ed and "edge_type" not in ed:
-                    ed["edge_type"] = ed.pop("type")
-                e = Edge.from_dict(ed)
-                src = supers.get(e.source)
-                if src is None:
-                    for sh in shards.values():
-                        if e.source in sh.nodes:
-                            src = sh.nodes[e.source]
-                            break
-                if src is not None and src.shard_key in shards:
-                    shards[src.shard_key].add_edge(e)
-            prof = self.store.load_profile(user_id=self.user_id) if rows else None
-            self.shards = shards
-            self.super_nodes = supers
-            self.buffer = BufferGraph(self.shards, self.super_nodes)
+            loader = getattr(self.store, "load_tenant", None)
+            if loader is not None:
+                ncols, ecols = loader(self.user_id)
+            else:
+                ncols, ecols = _rows_to_columns(self.store.get_nodes(user_id=self.user_id)), None
+            n_rows = len(ncols.get("id", [])) if ncols else 0
+            if ecols is None and n_rows:
+                ecols = _edge_rows_to_columns(self.store.get_edges(user_id=self.user_id))
+            prof = self.store.load_profile(user_id=self.user_id) if n_rows else None
+            self._replace_graph()
+            eng = (prof or {}).get("_engine", {}) if isinstance(prof, dict) else {}
+            clock = float(eng.get("decay_clock", 0.0))
+            n_edges = 0
+            if n_rows:
+                bulk_load(self.graph, ncols, ecols, clock)
+                n_edges = self.graph.num_edges
             self.profile = Profile.from_dict(prof) if prof else Profile()
             try:
                 self._last_nodes_version = self.store.get_latest_version()
             except Exception:
                 self._last_nodes_version = 0
-            mx = 0
-            for nid in self.buffer.nodes:
-                if nid.startswith("node_"):
-                    try:
-                        mx = max(mx, int(nid.split("_")[1]))
-                    except ValueError:
-                        pass
-            if rows:
+            if n_rows:
+                mx = int(eng.get("node_counter", 0))
+                for nid in ncols["id"]:
+                    m = _NODE_ID.match(nid)
+                    if m:
+                        mx = max(mx, int(m.group(1)))
                 self.node_counter = mx
             if self.query_cache:
                 self.query_cache.invalidate_results()
-        if rows:
-            self._say(f"✓ Restored state ({len(self.buffer.nodes)} nodes, {len(edge_rows)} edges)")
+        if n_rows:
+            self._say(f"✓ Restored state ({self.graph.num_nodes()} nodes, {n_edges} edges)")
         else:
             self._say("ℹ No saved state found.")
 
@@ -721,8 +843,12 @@ STORAGE:
             self.flush()
         else:
             self._save_to_persistence()
-        self.user_id = new_user_id
-        self._load_from_persistence()
+        with self._graph_lock:
+            detach = getattr(self.store, "detach", None)
+            if detach is not None:
+                detach(self.user_id)
+            self.user_id = new_user_id
+            self._load_from_persistence()
         self._say(f"👤 Switched context to user: {new_user_id}")
 
     # ------------------------------------------------------------ export
@@ -730,13 +856,24 @@ STORAGE:
         with self._graph_lock:
             return self._export(format)
 
+    def _top_observations(self, k: int = 50) -> List[NodeView]:
+        """Top ``k`` shard nodes by (salience, last_accessed) descending
+        (reference :1505-1512), selected on the device."""
+        g = self.graph
+        rows = g.ordered_node_rows()
+        rows = rows[g.mirror("sup")[rows] == 0]
+        if rows.size == 0:
+            return []
+        sal, last = g.mirror("sal")[rows].astype(np.float64), g.mirror("last")[rows]
+        o = np.lexsort((-last, -sal), axis=0) if rows.size else rows
+        return [NodeView.of(g, int(r)) for r in rows[o][:k]]
+
     def _export(self, format: str) -> str:
-        nodes = [n for sh in self.shards.values() for n in sh.nodes.values() if not n.is_super_node]
-        nodes.sort(key=lambda n: (n.salience, n.last_accessed), reverse=True)
+        nodes = self._top_observations(50)
         if format == "json":
-            return json.dumps([n.to_dict() for n in nodes[:50]], indent=2)
+            return json.dumps([n.to_dict() for n in nodes], indent=2)
         lines = [f"# Memory Observations for {self.user_id}", ""]
-        for n in nodes[:50]:
+        for n in nodes:
             lines += [f"### {n.type.capitalize()} Memory ({n.shard_key})",
                       f"- **Content**: {n.content}",
                       f"- **Salience**: {n.salience:.2f}",
@@ -763,6 +900,195 @@ Be clinical yet insightful. Do not include conversational filler."""
             self.background_executor.shutdown(wait=True)
         if hasattr(self, "store") and self.store is not None:
             self.store.close()
+
+
+# ---------------------------------------------------------------- columnar I/O
+def export_node_columns(g: TenantGraph, rows: np.ndarray) -> Dict:
+    """Store columns (SURVEY.md App. D + ``decay_clock``) of graph rows."""
+    rows = np.asarray(rows, dtype=np.int64)
+    n = rows.size
+    D = g.dim or 0
+    if n == 0:
+        return {"id": [], "count": 0}
+    with g.on_stream():
+        rt = torch.as_tensor(rows).to(g.device)
+        vec = g.emb32[rt].cpu().numpy() if g.dim is not None else np.zeros((n, 0), dtype=np.float32)
+        cols = {k: getattr(g, c)[rt].cpu().numpy() for k, c in
+                (("timestamp", "ts"), ("access_count", "acc"), ("last_accessed", "last"), ("salience", "sal"),
+                 ("is_super_node", "sup"), ("parent", "parent"), ("shard", "shard"))}
+    for j, r in enumerate(rows.tolist()):
+        if r in g.odd_emb and D:
+            vec[j] = 0.0
+    par = cols.pop("parent")
+    sh = cols.pop("shard")
+    ids = [g.ids[r] for r in rows.tolist()]
+    return {
+        "count": n,
+        "id": ids,
+        "content": [g.content[r] for r in rows.tolist()],
+        "vector": np.ascontiguousarray(vec, dtype=np.float32),
+        "type": [g.types[r] for r in rows.tolist()],
+        "timestamp": cols["timestamp"].astype(np.float64),
+        "access_count": cols["access_count"].astype(np.int32),
+        "last_accessed": cols["last_accessed"].astype(np.float64),
+        "salience": cols["salience"].astype(np.float32),
+        "is_super_node": cols["is_super_node"].astype(np.uint8),
+        "child_ids": [json.dumps(g.children.get(r, [])) for r in rows.tolist()],
+        "parent_id": [g.ids[p] if p >= 0 else "" for p in par.tolist()],
+        "shard_key": [g.shard_names[s] if s >= 0 else "default" for s in sh.tolist()],
+        "metadata": ["{}"] * n,
+        "decay_clock": np.full(n, g.decay_log, dtype=np.float64),
+    }
+
+
+def export_edge_columns(g: TenantGraph, idx: np.ndarray) -> Dict:
+    idx = np.asarray(idx, dtype=np.int64)
+    n = idx.size
+    if n == 0:
+        return {"count": 0, "id": []}
+    with g.on_stream():
+        it = torch.as_tensor(idx).to(g.device)
+        s, d = g.e["src"][it].cpu().numpy(), g.e["dst"][it].cpu().numpy()
+        w, co = g.e["w"][it].cpu().numpy(), g.e["co"][it].cpu().numpy()
+        lu, meta = g.e["lu"][it].cpu().numpy(), g.e["meta"][it].cpu().numpy()
+    ids = g.ids
+    src = [ids[a] for a in s.tolist()]
+    dst = [ids[b] for b in d.tolist()]
+    return {
+        "count": n,
+        "id": [f"{a}_{b}" for a, b in zip(src, dst)],
+        "source_id": src, "target_id": dst,
+        "weight": w.astype(np.float32),
+        "edge_type": [g.etype_names[(m >> 24) & 0x3F] for m in meta.tolist()],
+        "co_occurrence": co.astype(np.int32),
+        "last_updated": lu.astype(np.float64),
+        "metadata": ["{}"] * n,
+        "decay_clock": np.full(n, g.decay_log, dtype=np.float64),
+    }
+
+
+def _rows_to_columns(rows: List[Dict]) -> Dict:
+    """Reference-shaped node dicts (``Store.get_nodes``) -> columns."""
+    if not rows:
+        return {"id": []}
+    vec = [r.get("vector", r.get("embedding")) for r in rows]
+    dims = {len(v) for v in vec if v is not None and len(v)}
+    D = dims.pop() if len(dims) == 1 else 0
+    V = np.zeros((len(rows), D), dtype=np.float32)
+    odd = {}
+    for i, v in enumerate(vec):
+        if v is not None and len(v):
+            if len(v) == D:
+                V[i] = np.asarray(v, dtype=np.float32)
+            else:
+                odd[i] = list(v)
+
+    def js(v):
+        if isinstance(v, str):
+            return v
+        return json.dumps(v if v is not None else [])
+    return {
+        "id": [r["id"] for r in rows], "content": [r.get("content", "") for r in rows], "vector": V,
+        "_odd": odd, "_has": [v is not None and len(v) > 0 for v in vec],
+        "type": [r.get("type", "semantic") for r in rows],
+        "timestamp": np.asarray([float(r.get("timestamp", 0.0)) for r in rows]),
+        "access_count": np.asarray([int(r.get("access_count", 0)) for r in rows], dtype=np.int32),
+        "last_accessed": np.asarray([float(r.get("last_accessed", 0.0)) for r in rows]),
+        "salience": np.asarray([float(r.get("salience", 0.5)) for r in rows], dtype=np.float32),
+        "is_super_node": np.asarray([bool(r.get("is_super_node", False)) for r in rows], dtype=np.uint8),
+        "child_ids": [js(r.get("child_ids", [])) for r in rows],
+        "parent_id": [r.get("parent_id") or "" for r in rows],
+        "shard_key": [r.get("shard_key", "default") for r in rows],
+    }
+
+
+def _edge_rows_to_columns(rows: List[Dict]) -> Dict:
+    if not rows:
+        return {"id": []}
+    return {
+        "id": [r.get("id", "") for r in rows],
+        "source_id": [r.get("source_id", r.get("source")) for r in rows],
+        "target_id": [r.get("target_id", r.get("target")) for r in rows],
+        "weight": np.asarray([float(r.get("weight", 1.0)) for r in rows], dtype=np.float32),
+        "edge_type": [r.get("edge_type") or r.get("type") or "relates_to" for r in rows],
+        "co_occurrence": np.asarray([int(r.get("co_occurrence", 1)) for r in rows], dtype=np.int32),
+        "last_updated": np.asarray([float(r.get("last_updated", 0.0)) for r in rows]),
+    }
+
+
+def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> None:
+    """Columns -> an empty tenant graph (reference _load_from_persistence
+    :1304-1410 semantics): super rows go to ``super_nodes``; an edge goes to
+    its source node's shard and is dropped when its source is not a node;
+    repeated (source, target) rows strengthen like ``MemoryShard.add_edge``.
+    Rows written at an older decay clock get the decay applied since."""
+    import pandas as pd
+
+    ids = list(nc["id"])
+    N = len(ids)
+    if N == 0:
+        return
+    is_sup = np.asarray(nc["is_super_node"]).astype(bool)
+    shard_keys = list(nc["shard_key"])
+    # reference shard creation order: first non-super occurrence
+    for k, s in zip(shard_keys, is_sup):
+        if not s and k not in g.shard_code:
+            g.shard_id(k)
+    codes = np.asarray([g.shard_code[k] if k in g.shard_code else g.shard_id(k, live=False)
+                        for k in shard_keys], dtype=np.int32)
+    dc = np.asarray(nc.get("decay_clock", np.zeros(N)), dtype=np.float64)
+    fac = np.exp(np.minimum(0.0, clock - dc))
+    sal = np.asarray(nc["salience"], dtype=np.float64)
+    decayed = fac < 1.0
+    sal = np.where(decayed & ~is_sup, np.where(sal > SALIENCE_FLOOR, SALIENCE_FLOOR + (sal - SALIENCE_FLOOR) * fac,
+                                               SALIENCE_FLOOR), sal)
+    V = nc["vector"]
+    has = nc.get("_has")
+    emb = torch.from_numpy(np.ascontiguousarray(V, dtype=np.float32)) if V.shape[1] else None
+    if emb is not None and g.on_gpu:
+        emb = emb.pin_memory()
+    children = {}
+    for j in np.nonzero(is_sup)[0].tolist():
+        try:
+            children[j] = json.loads(nc["child_ids"][j]) if isinstance(nc["child_ids"][j], str) \
+                else list(nc["child_ids"][j])
+        except json.JSONDecodeError:
+            children[j] = []
+    parents = list(nc["parent_id"])
+    rows = g.add_nodes(ids, list(nc["content"]), emb, shard=codes, types=list(nc["type"]), sal=sal.astype(np.float32),
+                       acc=np.asarray(nc["access_count"]), last=np.asarray(nc["last_accessed"]),
+                       ts=np.asarray(nc["timestamp"]), sup=is_sup.astype(np.uint8),
+                       parents=parents if any(parents) else None, children=children, stored=True)
+    if has is not None and not all(has):
+        miss = torch.as_tensor([not h for h in has]).to(g.device)
+        with g.on_stream():
+            g.has_emb[rows[miss]] = 0
+        g._bump(store=True)
+    for j, v in nc.get("_odd", {}).items():
+        g.odd_emb[int(rows[j])] = v
+    if ec is not None and len(ec.get("id", [])):
+        idx = pd.Index(g.ids)
+        src = idx.get_indexer(pd.Index(list(ec["source_id"])))
+        node_src = src >= 0
+        if node_src.any():
+            kind = g.mirror("kind")
+            node_src &= kind[np.maximum(src, 0)] == NODE
+        keep = np.nonzero(node_src)[0]
+        if keep.size:
+            tgt_ids = [ec["target_id"][i] for i in keep.tolist()]
+            dst = np.asarray([g._ensure_row(t) for t in tgt_ids], dtype=np.int64)
+            s = src[keep].astype(np.int64)
+            sh = g.mirror("shard")[s]
+            w = np.asarray(ec["weight"], dtype=np.float64)[keep]
+            edc = np.asarray(ec.get("decay_clock", np.zeros(len(ec["id"]))), dtype=np.float64)[keep]
+            w = w * np.exp(np.minimum(0.0, clock - edc))
+            et = [g.etype(ec["edge_type"][i] or "relates_to") for i in keep.tolist()]
+            g.upsert_edges(torch.as_tensor(s), torch.as_tensor(dst), torch.as_tensor(w, dtype=torch.float32),
+                           torch.as_tensor(sh, dtype=torch.int32), torch.as_tensor(et, dtype=torch.int32),
+                           co=torch.as_tensor(np.asarray(ec["co_occurrence"])[keep], dtype=torch.int32),
+                           lu=torch.as_tensor(np.asarray(ec["last_updated"])[keep], dtype=torch.float64))
+    g.decay_log = clock
+    g.clear_tracking()
 
 
 def _default_local_embedder() -> EmbeddingProvider:

@@ -13,6 +13,12 @@ HBM vector arenas (replaces reference ``core/vector_store.py:7-244``,
 * Arenas are built lazily from the table and kept in sync with this process's
   own writes; writes from other processes are picked up when the table version
   moves (checked at most every ``consistency_interval`` seconds).
+* A ``MemorySystem`` *attaches* its tenant graph (:meth:`attach`): that
+  tenant's searches then run over the graph's own HBM rows (no second copy of
+  the vectors), store membership is the graph's ``stored`` column, and
+  persistence is incremental (:meth:`commit_tenant` upserts changed rows and
+  deletes removed ones in one version per table; :meth:`load_tenant` returns
+  raw columns for a bulk reload).
 """
 from __future__ import annotations
 
@@ -23,6 +29,7 @@ import time
 from typing import Sequence, Any, Dict, List, Optional
 
 import numpy as np
+import torch
 
 from ..index.arena import VectorArena
 from ..store.colstore import EDGE_SCHEMA, NODE_SCHEMA, PROFILE_SCHEMA, ColumnarTable
@@ -69,6 +76,55 @@ class HBMStore:
         self._last_check: Dict[str, float] = {}
         self._lock = threading.RLock()
         self._dim: Optional[int] = None
+        self._graphs: Dict[str, object] = {}
+
+    # ------------------------------------------------------------ attached tenant graphs
+    def attach(self, user_id: str, graph) -> None:
+        """Serve ``user_id``'s vector search from ``graph`` (a TenantGraph)."""
+        with self._lock:
+            self._graphs[user_id] = graph
+            self._arenas.pop(user_id, None)
+            self._synced.pop(user_id, None)
+
+    def detach(self, user_id: str) -> None:
+        with self._lock:
+            self._graphs.pop(user_id, None)
+
+    def bound_graph(self, user_id: str):
+        return self._graphs.get(user_id)
+
+    def commit_tenant(self, user_id: str, node_cols: Dict, delete_ids: Sequence[str], edge_cols: Dict,
+                      delete_edge_ids: Sequence[str]) -> int:
+        """Incremental commit of one tenant: upsert the given node / edge rows
+        and delete the given ids, one version per touched table. Returns the
+        nodes table version."""
+        with self._lock:
+            up = list(node_cols.get("id", []))
+            if up or delete_ids:
+                n = len(up)
+                if n and self._dim is None and node_cols["vector"].shape[1]:
+                    self._dim = node_cols["vector"].shape[1]
+                cols = self._nodes_table.fill_columns({k: v for k, v in node_cols.items() if k != "count"}, n,
+                                                      {"user_id": user_id})
+                if n == 0:
+                    cols["vector"] = np.zeros((0, self._table_dim() or 0), dtype=np.float32)
+                self._nodes_table.upsert_columns([("user_id", user_id)], "id", up + list(delete_ids), cols)
+            eu = list(edge_cols.get("id", []))
+            if eu or delete_edge_ids:
+                cols = self._edges_table.fill_columns({k: v for k, v in edge_cols.items() if k != "count"}, len(eu),
+                                                      {"user_id": user_id})
+                self._edges_table.upsert_columns([("user_id", user_id)], "id", eu + list(delete_edge_ids), cols)
+            return self._nodes_table.version
+
+    def load_tenant(self, user_id: str):
+        """(node columns, edge columns) of one tenant, as stored."""
+        nc = self._nodes_table.scan_columns([("user_id", user_id)])
+        if not nc or not len(nc.get("id", [])):
+            return {"id": []}, {"id": []}
+        if nc["vector"].ndim == 2 and nc["vector"].shape[1]:
+            self._dim = self._dim or nc["vector"].shape[1]
+        ec = self._edges_table.scan_columns([("user_id", user_id)])
+        return nc, (ec if ec else {"id": []})
 
     # ------------------------------------------------------------ helpers
     def _table_dim(self) -> Optional[int]:
@@ -132,6 +188,7 @@ class HBMStore:
                 "parent_id": n.get("parent_id") or "",
                 "shard_key": n.get("shard_key", "default"),
                 "metadata": _json(n.get("metadata", {}), {}),
+                "decay_clock": float(n.get("decay_clock", 0.0)),
             })
         return rows
 
@@ -140,11 +197,27 @@ class HBMStore:
             return
         rows = self._node_rows(nodes, user_id)
         with self._lock:
+            g = self._graphs.get(user_id)
+            if g is not None:
+                self._nodes_table.add_rows(rows)
+                self._graph_store_rows(g, rows)
+                return
             a = self._arena(user_id)
             prev = self._synced.get(user_id)
             v = self._nodes_table.add_rows(rows)
             a.add([r["id"] for r in rows], np.asarray([r["vector"] for r in rows], dtype=np.float32))
             self._after_write(user_id, prev, v)
+
+    @staticmethod
+    def _graph_store_rows(g, rows: List[Dict[str, Any]]) -> None:
+        """Rows written to an attached tenant join its searchable set: known
+        ids are flagged; unknown ids become store-only (ghost) rows."""
+        known = [g.row_of.get(r["id"], -1) for r in rows]
+        g.mark_stored([k for k in known if k >= 0])
+        new = [r for r, k in zip(rows, known) if k < 0]
+        if new:
+            g.add_nodes([r["id"] for r in new], [r["content"] for r in new], [r["vector"] for r in new],
+                        shard=[g.shard_id(r["shard_key"], live=False) for r in new], stored=True, ghost=True)
 
     def replace_user_nodes(self, nodes: List[Dict[str, Any]], user_id: str = "default") -> None:
         """Atomic per-tenant rewrite (one committed version): the delete-all +
@@ -170,6 +243,13 @@ class HBMStore:
     def search_nodes(self, query_emb, user_id: str = "default", limit: int = 5) -> List[str]:
         if query_emb is None or len(query_emb) == 0:
             return []
+        g = self._graphs.get(user_id)
+        if g is not None:
+            q = query_emb if torch.is_tensor(query_emb) else torch.from_numpy(
+                np.asarray(query_emb, dtype=np.float32))
+            if g.dim is None or q.shape[-1] != g.dim:
+                return []
+            return g.search_ids(q, int(limit), self.metric)[0]
         with self._lock:  # writers (add/delete/replace) mutate the arena in place
             a = self._arena(user_id)
             if len(a) == 0 or a.dim != len(query_emb):
@@ -177,7 +257,17 @@ class HBMStore:
             return a.search(query_emb, int(limit), self.metric)[0]
 
     def search_nodes_batch(self, query_embs, user_id: str = "default", limit: int = 5) -> List[List[str]]:
-        """Batched variant (one kernel launch for all queries)."""
+        """Batched variant (one kernel launch for all queries). ``query_embs``
+        may be a device tensor (kept on the device end to end)."""
+        g = self._graphs.get(user_id)
+        if g is not None:
+            Q = query_embs if torch.is_tensor(query_embs) else torch.as_tensor(
+                np.asarray(query_embs, dtype=np.float32))
+            if len(Q) == 0:
+                return []
+            if g.dim is None or Q.shape[-1] != g.dim:
+                return [[] for _ in range(len(Q))]
+            return g.search_ids(Q, int(limit), self.metric)
         with self._lock:
             a = self._arena(user_id)
             if len(a) == 0 or len(query_embs) == 0:
@@ -209,6 +299,16 @@ class HBMStore:
         return out
 
     def delete_nodes(self, node_ids: Optional[List[str]], user_id: str = "default") -> None:
+        g = self._graphs.get(user_id)
+        if g is not None:
+            with self._lock:
+                if not node_ids:
+                    self._nodes_table.delete([("user_id", user_id)])
+                    g.unstore(list(g.ids))
+                else:
+                    self._nodes_table.delete([("user_id", user_id)], "id", list(node_ids))
+                    g.unstore(node_ids)
+            return
         with self._lock:
             a = self._arena(user_id)
             prev = self._synced.get(user_id)
@@ -298,6 +398,7 @@ class HBMStore:
             t.compact()
 
     def close(self) -> None:
+        self._graphs.clear()
         self._arenas.clear()
         self._synced.clear()
 

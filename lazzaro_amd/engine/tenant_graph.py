@@ -1,0 +1,1059 @@
+"""TenantGraph: one tenant's memory graph as structure-of-arrays in HBM.
+
+This is the engine under :class:`~lazzaro_amd.core.memory_system.MemorySystem`.
+The reference keeps a tenant's graph as Python ``Node``/``Edge`` objects in
+per-topic dicts (``core/memory_shard.py:30-88``, ``core/buffer_graph.py``) and
+runs every maintenance step as a Python loop over them. Here the graph is a
+set of device columns and every step is a kernel or a batched tensor op:
+
+=====================  ==========================================  =====================
+reference step          reference code                              here
+=====================  ==========================================  =====================
+dedupe (top-1, >0.95)   memory_system.py:719-742                    fused MFMA top-k scan
+link within shard       memory_system.py:797-836                    label-filtered list of
+link to existing        memory_system.py:838-891                    the same dual scan
+decay + prune           memory_shard.py:64-84, :624-630, :991       ``tg_decay_kernel``
+evict (importance)      memory_system.py:535-578                    ``tg_importance_kernel``
+                                                                    + stable select +
+                                                                    ``tg_flag_remove``
+components              buffer_graph.py:99-120                      ``cc_hook/compress``
+neighbour boost         memory_system.py:242-260                    ``tg_boost_kernel``
+retrieval touch         buffer_graph.py:79-85                       ``tg_touch_kernel``
+super-node centroid     memory_system.py:893-933                    segmented mean
+store vector search     vector_store.py:132-140                     fused MFMA top-k +
+                                                                    fp32 re-rank
+=====================  ==========================================  =====================
+
+Node columns (row-indexed; rows are never reused while referenced):
+
+* ``emb32`` fp32 [cap, D]: exact vectors (the store's precision, reference
+  ``vector_store.py:37``); ``emb16`` bf16 [cap, Dp] on the GPU: the operand of
+  the MFMA scans (Dp = D rounded up to 64); ``sqn`` fp32 |x|^2.
+* ``sal f32, acc i32, last f64, ts f64, shard i32, kind u8, sup u8,
+  has_emb u8, parent i32, stored u8, dirty u8``. ``kind``: 0 free, 1 node,
+  2 ghost -- an id that is not (or no longer) a node but is still an edge
+  endpoint or a store row (the reference keeps dangling edges of removed
+  nodes in other shards, and the store may hold rows the graph dropped).
+* host lists: ``ids``, ``content``, ``types``; ``children`` (super rows).
+
+Edge columns: ``src/dst i32, w f32, co i32, lu f64, meta i32`` with ``meta =
+shard | type << 24 | dirty << 30``: the shard that stores the edge matters,
+because the reference's ``get_neighbors`` only sees edges of the node's own
+shard (``buffer_graph.py:72-77``); that visibility drives the neighbour boost.
+
+Decisions are taken in float64 from the fp32 columns (the reference computes
+cosine in float64, ``memory_system.py:197-203``); the bf16 MFMA scans only
+nominate candidates, which are re-ranked exactly.
+
+Deliberate differences (documented in docs/INVENTORY.md):
+* connected components treat an edge as connecting both endpoints whichever
+  shard stores it (the reference's recursive DFS sees a cross-shard edge from
+  one side only, which makes its components depend on the visit order);
+* ties in similarity / importance break by row (insertion) order.
+"""
+from __future__ import annotations
+
+import math
+import threading
+import time
+from contextlib import contextmanager
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import tenant_ops as T
+
+FREE, NODE, GHOST = 0, 1, 2
+NEG_INF = float("-inf")
+SHARD_MASK = 0xFFFFFF
+TYPE_SHIFT = 24
+EDIRTY = 1 << 30
+MAX_ETYPES = 64
+
+# below this many query x row products the exact float64 GEMM is used directly
+KERNEL_MIN_WORK = 1 << 22
+CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-rank
+
+
+def _pad64(d: int) -> int:
+    return (d + 63) // 64 * 64
+
+
+class TenantGraph:
+    NODE_COLS = (("sal", torch.float32, 0.0), ("acc", torch.int32, 0), ("last", torch.float64, 0.0),
+                 ("ts", torch.float64, 0.0), ("shard", torch.int32, -1), ("kind", torch.uint8, FREE),
+                 ("sup", torch.uint8, 0), ("has_emb", torch.uint8, 0), ("parent", torch.int32, -1),
+                 ("stored", torch.uint8, 0), ("dirty", torch.uint8, 0))
+
+    def __init__(self, device=None, dim: Optional[int] = None, capacity: int = 256):
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.on_gpu = self.device.type == "cuda"
+        self.dim: Optional[int] = None
+        self.Dp = 0
+        self.n = 0
+        self.cap = 0
+        self._init_cap = capacity
+        self.ids: List[str] = []
+        self.content: List[str] = []
+        self.types: List[str] = []
+        self.row_of: Dict[str, int] = {}
+        self.children: Dict[int, List[str]] = {}
+        self.odd_emb: Dict[int, list] = {}
+        self.shard_names: List[str] = []
+        self.shard_code: Dict[str, int] = {}
+        self.shard_live: List[bool] = []
+        self.shard_count: List[int] = []  # live non-super nodes per shard
+        self.n_super = 0
+        self.etype_names: List[str] = []
+        self.etype_code: Dict[str, int] = {}
+        self.max_norm_dev = 0.0  # max | |x| - 1 | over embedded rows
+        self.decay_log = 0.0  # sum of log(1 - rate) over every decay applied
+        self.version = 0  # bumps on any mutation (views / caches)
+        self.edge_version = 0
+        self._csr = None
+        self._csr_version = -1
+        self._boost_state = T.BoostState()
+        self._bias_cache: Dict[str, Tuple[int, torch.Tensor]] = {}
+        self._store_version = 0
+        self._mirror: Dict[str, Tuple[int, np.ndarray]] = {}
+        self.deleted_ids: Dict[str, None] = {}  # node ids to delete from the store at the next commit
+        self.deleted_edges: Dict[Tuple[str, str], None] = {}
+        self.track = True
+        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.lock = threading.RLock()
+        z = lambda dt: torch.zeros(0, dtype=dt, device=self.device)  # noqa: E731
+        self.e = {"src": z(torch.int32), "dst": z(torch.int32), "w": z(torch.float32), "co": z(torch.int32),
+                  "lu": z(torch.float64), "meta": z(torch.int32)}
+        self.emb32 = self.emb16 = self.sqn = None
+        for name, dt, _ in self.NODE_COLS:
+            setattr(self, name, z(dt))
+        if dim:
+            self._set_dim(dim)
+
+    # ------------------------------------------------------------------ streams
+    @contextmanager
+    def on_stream(self):
+        """Run device work on the graph's own HIP stream, ordered after the
+        caller's stream and before anything the caller does next."""
+        if not self.on_gpu:
+            yield
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream == self.stream.cuda_stream:
+            yield
+            return
+        self.stream.wait_stream(cur)
+        try:
+            with torch.cuda.stream(self.stream):
+                yield
+        finally:
+            cur.wait_stream(self.stream)
+
+    # ------------------------------------------------------------------ storage
+    def _set_dim(self, d: int) -> None:
+        self.dim = int(d)
+        self.Dp = _pad64(self.dim) if self.on_gpu else self.dim
+        self._alloc(max(self.cap, self._init_cap))
+
+    def _alloc(self, cap: int) -> None:
+        dev, n = self.device, self.n
+        new = {}
+        for name, dt, fill in self.NODE_COLS:
+            t = torch.full((cap,), fill, dtype=dt, device=dev)
+            if self.cap:
+                t[:n] = getattr(self, name)[:n]
+            new[name] = t
+        if self.dim is not None:
+            e32 = torch.zeros((cap, self.dim), dtype=torch.float32, device=dev)
+            sq = torch.zeros(cap, dtype=torch.float32, device=dev)
+            e16 = torch.zeros((cap, self.Dp), dtype=torch.bfloat16, device=dev) if self.on_gpu else None
+            if self.cap and self.emb32 is not None and self.emb32.shape[1] == self.dim:
+                e32[:n] = self.emb32[:n]
+                sq[:n] = self.sqn[:n]
+                if e16 is not None:
+                    e16[:n] = self.emb16[:n]
+            self.emb32, self.sqn, self.emb16 = e32, sq, e16
+        for k, v in new.items():
+            setattr(self, k, v)
+        self.cap = cap
+
+    def reserve(self, n: int) -> None:
+        if n > self.cap:
+            self._alloc(max(n, self._init_cap, int(self.cap * 1.5) + 1))
+
+    def _bump(self, edges: bool = False, store: bool = False) -> None:
+        self.version += 1
+        if edges:
+            self.edge_version += 1
+        if store:
+            self._store_version += 1
+
+    # ------------------------------------------------------------------ codes
+    def shard_id(self, name: str, live: bool = True) -> int:
+        """Code of shard ``name`` (created on first use). ``live=False`` gives a
+        code without making the shard visible in ``MemorySystem.shards``
+        (a super-node's or store-only row's label)."""
+        c = self.shard_code.get(name)
+        if c is None:
+            c = len(self.shard_names)
+            if c > SHARD_MASK:
+                raise OverflowError("too many shards")
+            self.shard_names.append(name)
+            self.shard_code[name] = c
+            self.shard_live.append(live)
+            self.shard_count.append(0)
+        elif live and not self.shard_live[c]:
+            self.shard_live[c] = True
+        return c
+
+    def live_shards(self) -> List[str]:
+        return [s for s, live in zip(self.shard_names, self.shard_live) if live]
+
+    def etype(self, name: str) -> int:
+        c = self.etype_code.get(name)
+        if c is None:
+            c = len(self.etype_names)
+            if c >= MAX_ETYPES:
+                raise OverflowError("too many edge types")
+            self.etype_names.append(name)
+            self.etype_code[name] = c
+        return c
+
+    # ------------------------------------------------------------------ nodes
+    def _as_emb(self, emb, m: int):
+        """(fp32 [m, D] device tensor, None | (has-embedding flags, odd-dim rows))."""
+        if torch.is_tensor(emb):
+            t = emb.to(self.device, torch.float32)
+            if t.dim() == 1:
+                t = t[None, :]
+            if self.dim is None and t.shape[1] > 0:
+                self._set_dim(t.shape[1])
+            if t.shape[1] != self.dim:
+                raise ValueError(f"embedding dim {t.shape[1]} != tenant dim {self.dim}")
+            return t.contiguous(), None
+        rows = list(emb) if emb is not None else [None] * m
+        if self.dim is None:
+            for r in rows:
+                if r is not None and len(r) > 0:
+                    self._set_dim(len(r))
+                    break
+        D = self.dim or 0
+        out = np.zeros((m, D), dtype=np.float32)
+        ok = [False] * m
+        odd = {}
+        for i, r in enumerate(rows):
+            if r is None or len(r) == 0:
+                continue
+            if len(r) != D:
+                odd[i] = list(r)
+                continue
+            out[i] = np.asarray(r, dtype=np.float32)
+            ok[i] = True
+        return torch.from_numpy(out).to(self.device), (ok, odd)
+
+    def add_nodes(self, ids: Sequence[str], contents: Sequence[str], emb=None, *, shard=None, types=None,
+                  sal=None, acc=None, last=None, ts=None, sup=None, parents: Optional[Sequence[Optional[str]]] = None,
+                  children: Optional[Dict[int, List[str]]] = None, stored: bool = False,
+                  now: Optional[float] = None, ghost: bool = False) -> torch.Tensor:
+        """Append (or replace, by id) ``m`` nodes. Scalars may be python
+        sequences, tensors or scalars; ``shard`` holds shard codes; ``children``
+        maps batch position -> child id list (super-nodes). ``ghost``: rows
+        that are store members only, not graph nodes. Returns rows [m]."""
+        m = len(ids)
+        dev = self.device
+        if m == 0:
+            return torch.zeros(0, dtype=torch.long, device=dev)
+        now = time.time() if now is None else now
+        with self.on_stream():
+            return self._add_nodes(ids, contents, emb, shard, types, sal, acc, last, ts, sup, parents, children,
+                                   stored, now, ghost)
+
+    def _add_nodes(self, ids, contents, emb, shard, types, sal, acc, last, ts, sup, parents, children, stored, now,
+                   ghost=False):
+        m = len(ids)
+        dev = self.device
+        e32, info = self._as_emb(emb, m)
+        rows = [self.row_of.get(i, -1) for i in ids]
+        fresh = sum(1 for r in rows if r < 0)
+        self.reserve(self.n + fresh)
+        kind_h = self.mirror("kind") if fresh < m else None
+        r_next = self.n
+        rl = []
+        tlist = types if (types is not None and not isinstance(types, str)) else None
+        tdef = types if isinstance(types, str) else "semantic"
+        for j, (i, r) in enumerate(zip(ids, rows)):
+            t = tlist[j] if tlist is not None else tdef
+            if r < 0:
+                r = r_next
+                r_next += 1
+                self.ids.append(i)
+                self.content.append(contents[j])
+                self.types.append(t)
+                self.row_of[i] = r
+            else:
+                if kind_h is not None and r < len(kind_h) and kind_h[r] == NODE:
+                    self._unlink_row(r)
+                self.content[r] = contents[j]
+                self.types[r] = t
+            rl.append(r)
+        self.n = r_next
+        rt = torch.as_tensor(rl, dtype=torch.long).to(dev)
+
+        def col(v, dt, default):
+            if v is None:
+                return torch.full((m,), default, dtype=dt, device=dev)
+            if torch.is_tensor(v):
+                return v.to(dev, dt).reshape(-1).expand(m).contiguous() if v.numel() == 1 else v.to(dev, dt)
+            if isinstance(v, (int, float, bool, np.number)):
+                return torch.full((m,), v, dtype=dt, device=dev)
+            return torch.as_tensor(np.asarray(v)).to(dev, dt)
+
+        sh = col(shard, torch.int32, 0)
+        supv = col(sup, torch.uint8, 0)
+        self.sal[rt] = col(sal, torch.float32, 0.5)
+        self.acc[rt] = col(acc, torch.int32, 0)
+        self.last[rt] = col(last, torch.float64, now)
+        self.ts[rt] = col(ts, torch.float64, now)
+        self.shard[rt] = sh
+        self.kind[rt] = GHOST if ghost else NODE
+        self.sup[rt] = supv
+        self.stored[rt] = 1 if stored else 0
+        self.dirty[rt] = 1
+        if parents is not None and any(parents):
+            par = [self._ensure_row(p) if p else -1 for p in parents]
+            self.parent[rt] = torch.as_tensor(par, dtype=torch.int32).to(dev)
+        else:
+            self.parent[rt] = -1
+        if self.dim is not None:
+            if info is None:
+                has = torch.ones(m, dtype=torch.bool, device=dev)
+            else:
+                ok, odd = info
+                has = torch.as_tensor(ok, dtype=torch.bool).to(dev)
+                for j, v in odd.items():
+                    self.odd_emb[rl[j]] = v
+            e32 = e32 * has[:, None].to(e32.dtype)
+            self.emb32[rt] = e32
+            nrm2 = (e32.double() ** 2).sum(1)
+            self.sqn[rt] = nrm2.float()
+            if self.emb16 is not None:
+                self.emb16[rt, : self.dim] = e32.to(torch.bfloat16)
+            self.has_emb[rt] = has.to(torch.uint8)
+            if info is None or any(info[0]):
+                dv = torch.where(has, (nrm2.sqrt() - 1.0).abs(), torch.zeros_like(nrm2)).max()
+                self.max_norm_dev = max(self.max_norm_dev, float(dv))
+        elif info is not None:
+            for j, v in info[1].items():
+                self.odd_emb[rl[j]] = v
+        # host counters
+        sup_any = bool(supv.any()) if m > 64 else None
+        if ghost:
+            pass
+        elif sup_any is False:
+            cnt = np.bincount(sh.cpu().numpy(), minlength=len(self.shard_count))
+            for c in np.nonzero(cnt)[0]:
+                self.shard_count[int(c)] += int(cnt[c])
+        else:
+            sh_h = sh.tolist()
+            sup_h = supv.tolist()
+            for j in range(m):
+                if sup_h[j]:
+                    self.n_super += 1
+                else:
+                    self.shard_count[sh_h[j]] += 1
+        if children is not None:
+            for j, ch in children.items():
+                self.children[rl[j]] = list(ch)
+        if self.deleted_ids:
+            for i in ids:
+                self.deleted_ids.pop(i, None)
+        self._bump(store=True)
+        return rt
+
+    def _ensure_row(self, node_id: str) -> int:
+        """Row of ``node_id``; unknown ids become ghost rows (edge endpoints /
+        parent references to nodes that do not exist, as the reference allows)."""
+        r = self.row_of.get(node_id)
+        if r is not None:
+            return r
+        self.reserve(self.n + 1)
+        r = self.n
+        self.n += 1
+        self.ids.append(node_id)
+        self.content.append("")
+        self.types.append("semantic")
+        self.row_of[node_id] = r
+        with self.on_stream():
+            self.kind[r] = GHOST
+            self.shard[r] = -1
+        self._bump()
+        return r
+
+    def _unlink_row(self, r: int) -> None:
+        """Forget a live node's host counters before its row is replaced."""
+        if int(self.mirror("sup")[r]):
+            self.n_super -= 1
+        else:
+            s = int(self.mirror("shard")[r])
+            if s >= 0:
+                self.shard_count[s] -= 1
+        self.children.pop(r, None)
+        self.odd_emb.pop(r, None)
+
+    def rows_of(self, ids: Iterable[str]) -> List[int]:
+        return [self.row_of.get(i, -1) for i in ids]
+
+    def node_row(self, node_id: str, include_super: bool = True) -> int:
+        """Row of a live node (-1 if the id is not a node)."""
+        r = self.row_of.get(node_id)
+        if r is None or self.kind_h(r) != NODE:
+            return -1
+        if not include_super and self.sup_h(r):
+            return -1
+        return r
+
+    # host mirrors of device columns (refreshed when the graph version moves)
+    def mirror(self, name: str) -> np.ndarray:
+        m = self._mirror.get(name)
+        if m is not None and m[0] == self.version and len(m[1]) == self.n:
+            return m[1]
+        with self.on_stream():
+            a = getattr(self, name)[: self.n].cpu().numpy()
+        self._mirror[name] = (self.version, a)
+        return a
+
+    def kind_h(self, r: int) -> int:
+        return int(self.mirror("kind")[r])
+
+    def sup_h(self, r: int) -> int:
+        return int(self.mirror("sup")[r])
+
+    def node_rows_where(self, shard_code: Optional[int] = None, super_: Optional[bool] = None) -> np.ndarray:
+        """Live node rows (ascending) filtered by shard code / super flag."""
+        kind = self.mirror("kind")
+        m = kind == NODE
+        if shard_code is not None:
+            m &= self.mirror("shard") == shard_code
+        if super_ is not None:
+            m &= (self.mirror("sup") != 0) == super_
+        return np.nonzero(m)[0]
+
+    def ordered_node_rows(self) -> np.ndarray:
+        """Live node rows in the reference's ``BufferGraph.nodes`` order:
+        super-nodes first, then each shard (creation order) in insertion order."""
+        kind, sup, sh = self.mirror("kind"), self.mirror("sup"), self.mirror("shard")
+        live = np.nonzero(kind == NODE)[0]
+        if live.size == 0:
+            return live
+        key = np.where(sup[live] != 0, -1, sh[live]).astype(np.int64)
+        o = np.lexsort((live, key))
+        return live[o]
+
+    def set_scalar(self, r: int, name: str, value) -> None:
+        col = getattr(self, name)
+        with self.on_stream():
+            col[r] = value
+            self.dirty[r] = 1
+        m = self._mirror.get(name)
+        if m is not None and m[0] == self.version and r < len(m[1]):
+            m[1][r] = value
+        self._mirror.pop("dirty", None)
+
+    def get_scalar(self, r: int, name: str):
+        return self.mirror(name)[r].item()
+
+    def embedding(self, r: int) -> list:
+        if r in self.odd_emb:
+            return list(self.odd_emb[r])
+        if self.dim is None or not int(self.mirror("has_emb")[r]):
+            return []
+        with self.on_stream():
+            return self.emb32[r].double().cpu().tolist()
+
+    def set_embedding(self, r: int, emb) -> None:
+        self.odd_emb.pop(r, None)
+        if emb is None or len(emb) == 0:
+            if self.dim is not None:
+                with self.on_stream():
+                    self.emb32[r] = 0
+                    self.sqn[r] = 0
+                    self.has_emb[r] = 0
+                    if self.emb16 is not None:
+                        self.emb16[r] = 0
+            self._bump(store=True)
+            return
+        if self.dim is None:
+            self._set_dim(len(emb))
+        if len(emb) != self.dim:
+            self.odd_emb[r] = list(emb)
+            self._bump(store=True)
+            return
+        v = torch.as_tensor(np.asarray(emb, dtype=np.float32)).to(self.device)
+        with self.on_stream():
+            self.emb32[r] = v
+            n2 = float((v.double() ** 2).sum())
+            self.sqn[r] = n2
+            self.has_emb[r] = 1
+            self.dirty[r] = 1
+            if self.emb16 is not None:
+                self.emb16[r, : self.dim] = v.to(torch.bfloat16)
+        self.max_norm_dev = max(self.max_norm_dev, abs(math.sqrt(n2) - 1.0))
+        self._bump(store=True)
+
+    # ------------------------------------------------------------------ edges
+    @property
+    def num_edges(self) -> int:
+        return int(self.e["src"].numel())
+
+    def append_edges(self, src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, shard: torch.Tensor,
+                     etype: int = 0, co=None, lu=None, now: Optional[float] = None) -> None:
+        """Append edges known not to exist yet (every edge a consolidation
+        creates starts at a node of this batch)."""
+        m = int(src.numel())
+        if m == 0:
+            return
+        now = time.time() if now is None else now
+        dev = self.device
+        with self.on_stream():
+            e = self.e
+            meta = (shard.to(dev, torch.int32) & SHARD_MASK) | (etype << TYPE_SHIFT) | EDIRTY
+            e["src"] = torch.cat([e["src"], src.to(dev, torch.int32)])
+            e["dst"] = torch.cat([e["dst"], dst.to(dev, torch.int32)])
+            e["w"] = torch.cat([e["w"], w.to(dev, torch.float32)])
+            e["co"] = torch.cat([e["co"], (co.to(dev, torch.int32) if co is not None
+                                           else torch.ones(m, dtype=torch.int32, device=dev))])
+            e["lu"] = torch.cat([e["lu"], (lu.to(dev, torch.float64) if lu is not None
+                                           else torch.full((m,), now, dtype=torch.float64, device=dev))])
+            e["meta"] = torch.cat([e["meta"], meta.to(torch.int32)])
+        self._bump(edges=True)
+
+    def upsert_edges(self, src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, shard: torch.Tensor,
+                     etype: torch.Tensor, co=None, lu=None, now: Optional[float] = None) -> int:
+        """``MemoryShard.add_edge`` for a batch, in order (reference
+        memory_shard.py:42-52): an edge whose (shard, source, target) already
+        exists -- or appeared earlier in the batch -- strengthens it (weight +0.1
+        capped at 1, co_occurrence +1) instead of being added. Returns #new."""
+        m = int(src.numel())
+        if m == 0:
+            return 0
+        now = time.time() if now is None else now
+        with self.on_stream():
+            return self._upsert_edges(src, dst, w, shard, etype, co, lu, now)
+
+    def _upsert_edges(self, src, dst, w, shard, etype, co, lu, now):
+        m = int(src.numel())
+        dev = self.device
+        e = self.e
+        ne = self.num_edges
+        src, dst = src.to(dev, torch.int64), dst.to(dev, torch.int64)
+        shard = shard.to(dev, torch.int64)
+        s_all = torch.cat([e["src"].long(), src])
+        d_all = torch.cat([e["dst"].long(), dst])
+        h_all = torch.cat([(e["meta"] & SHARD_MASK).long(), shard])
+        # lexicographic stable sort by (shard, src, dst); equal keys keep position order
+        o = torch.sort(d_all, stable=True).indices
+        o = o[torch.sort(s_all[o], stable=True).indices]
+        o = o[torch.sort(h_all[o], stable=True).indices]
+        hs, ss, ds = h_all[o], s_all[o], d_all[o]
+        newgrp = torch.ones(ne + m, dtype=torch.bool, device=dev)
+        newgrp[1:] = (hs[1:] != hs[:-1]) | (ss[1:] != ss[:-1]) | (ds[1:] != ds[:-1])
+        gid = torch.cumsum(newgrp.long(), 0) - 1
+        head = o[newgrp]  # position of each group's first element
+        cnt = torch.zeros(int(head.numel()), dtype=torch.int64, device=dev).index_add_(0, gid, torch.ones_like(gid))
+        extra = (cnt - 1).to(torch.float32)  # strengthening adds per group
+        old_head = head < ne
+        hi, ex = head[old_head], extra[old_head]
+        t = ex > 0
+        hi, ex = hi[t], ex[t]
+        if hi.numel():
+            e["w"][hi] = torch.clamp(e["w"][hi] + 0.1 * ex, max=1.0)
+            e["co"][hi] = e["co"][hi] + ex.to(torch.int32)
+            e["lu"][hi] = now
+            e["meta"][hi] = e["meta"][hi] | EDIRTY
+        n_new = 0
+        new_head = ~old_head
+        if bool(new_head.any()):
+            bi, oo = torch.sort(head[new_head] - ne)  # batch positions of first occurrences, in order
+            ex = extra[new_head][oo]
+            w0 = w.to(dev, torch.float32)[bi]
+            ww = torch.where(ex > 0, torch.clamp(w0 + 0.1 * ex, max=1.0), w0)
+            cc = (co.to(dev, torch.int32)[bi] if co is not None
+                  else torch.ones_like(bi, dtype=torch.int32)) + ex.to(torch.int32)
+            ll = lu.to(dev, torch.float64)[bi] if lu is not None else None
+            self.append_edges(src[bi], dst[bi], ww, shard[bi].to(torch.int32), 0, cc, ll, now)
+            k = int(bi.numel())
+            et = etype.to(dev, torch.int32)[bi]
+            tail = self.e["meta"][-k:]
+            self.e["meta"][-k:] = (tail & ~(0x3F << TYPE_SHIFT)) | (et << TYPE_SHIFT)
+            n_new = k
+        self._bump(edges=True)
+        return n_new
+
+    def edge_index(self, s: int, d: int, shard_code: int) -> int:
+        e = self.e
+        with self.on_stream():
+            m = (e["src"] == s) & (e["dst"] == d) & ((e["meta"] & SHARD_MASK) == shard_code)
+            nz = torch.nonzero(m).flatten()
+            return int(nz[0]) if nz.numel() else -1
+
+    def edges_of_shard(self, shard_code: int) -> torch.Tensor:
+        with self.on_stream():
+            return torch.nonzero((self.e["meta"] & SHARD_MASK) == shard_code).flatten()
+
+    def edges_incident(self, r: int, shard_code: Optional[int] = None) -> torch.Tensor:
+        e = self.e
+        with self.on_stream():
+            m = (e["src"] == r) | (e["dst"] == r)
+            if shard_code is not None:
+                m &= (e["meta"] & SHARD_MASK) == shard_code
+            return torch.nonzero(m).flatten()
+
+    def remove_edges(self, idx: torch.Tensor) -> None:
+        if idx.numel() == 0:
+            return
+        with self.on_stream():
+            e = self.e
+            idx = idx.to(self.device)
+            if self.track:
+                self._note_dropped(e["src"][idx], e["dst"][idx])
+            keep = torch.ones(self.num_edges, dtype=torch.bool, device=self.device)
+            keep[idx] = False
+            self.e = {k: v[keep] for k, v in e.items()}
+        self._bump(edges=True)
+
+    def _note_dropped(self, s: torch.Tensor, d: torch.Tensor) -> None:
+        if s.numel() == 0:
+            return
+        ids = self.ids
+        for a, b in zip(s.tolist(), d.tolist()):
+            self.deleted_edges[(ids[a], ids[b])] = None
+
+    # ------------------------------------------------------------------ maintenance
+    def decay(self, rate: float = 0.01, prune_threshold: Optional[float] = None, decay_nodes: bool = True) -> int:
+        """Temporal decay of all edges and shard-node saliences (+ optional
+        prune) in one kernel pass. Returns the number of pruned edges."""
+        with self.on_stream():
+            self.e, n, dropped = T.decay_prune(self.e, self.sal[: self.n], self.kind[: self.n], self.sup[: self.n],
+                                               rate, prune_threshold, decay_nodes, want_dropped=self.track)
+        if rate:
+            self.decay_log += math.log1p(-rate)
+        if dropped is not None and n:
+            self._note_dropped(*dropped)
+        self._bump(edges=bool(n) or bool(rate))
+        return n
+
+    def prune(self, threshold: float) -> int:
+        return self.decay(0.0, threshold, decay_nodes=False)
+
+    def remove_nodes(self, rows, drop_edges: bool = True, unstore: bool = False) -> int:
+        """Remove live nodes: each becomes a ghost row (its id may still be an
+        edge endpoint) and -- ``drop_edges`` -- its own shard's incident edges go
+        (reference ``_enforce_buffer_limit`` :558-569). Returns #removed."""
+        rl = rows.tolist() if torch.is_tensor(rows) else list(rows)
+        if not rl:
+            return 0
+        kind = self.mirror("kind")
+        live = sorted({r for r in rl if 0 <= r < self.n and kind[r] == NODE})
+        if not live:
+            return 0
+        for r in live:
+            self._unlink_row(r)
+        with self.on_stream():
+            rt = torch.as_tensor(live, dtype=torch.long).to(self.device)
+            if drop_edges and self.num_edges:
+                rm = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+                rm[rt] = 1
+                self.e, n, dropped = T.remove_edges_of(self.e, rm, self.shard[: self.n], want_dropped=self.track)
+                if dropped is not None and n:
+                    self._note_dropped(*dropped)
+            self.kind[rt] = GHOST
+            if unstore:
+                self.stored[rt] = 0
+        for r in live:
+            self.deleted_ids[self.ids[r]] = None
+        self._bump(edges=True, store=True)
+        return len(live)
+
+    def unstore(self, ids: Iterable[str]) -> None:
+        rows = [r for r in self.rows_of(ids) if r >= 0]
+        if rows:
+            with self.on_stream():
+                self.stored[torch.as_tensor(rows, dtype=torch.long).to(self.device)] = 0
+            self._bump(store=True)
+
+    def mark_stored(self, rows) -> None:
+        rows = torch.as_tensor(rows, dtype=torch.long) if not torch.is_tensor(rows) else rows
+        if rows.numel():
+            with self.on_stream():
+                self.stored[rows.to(self.device)] = 1
+            self._bump(store=True)
+
+    def evict(self, max_nodes: int, now: Optional[float] = None) -> List[int]:
+        """Buffer-limit eviction (reference memory_system.py:535-578): when the
+        node count (super-nodes included) exceeds ``max_nodes``, the ``excess``
+        shard nodes of lowest importance go, with their shard's edges.
+        Victim order: importance, then the reference's iteration order (shard
+        creation order, then insertion order). Returns victim rows."""
+        total = self.num_nodes()
+        if total <= max_nodes:
+            return []
+        excess = total - max_nodes
+        now = time.time() if now is None else now
+        n = self.n
+        with self.on_stream():
+            score = T.importance(self.sal[:n], self.acc[:n], self.last[:n], self.kind[:n], self.sup[:n], now)
+            okey = self.shard[:n].long() * (1 << 32) + torch.arange(n, device=self.device)
+            o1 = torch.sort(okey, stable=True).indices
+            o2 = torch.sort(score[o1], stable=True).indices
+            order = o1[o2][:excess]
+            order = order[torch.isfinite(score[order])]
+            victims = order.tolist()
+        self.remove_nodes(victims, drop_edges=True, unstore=True)
+        return victims
+
+    def num_nodes(self) -> int:
+        return int(sum(self.shard_count) + self.n_super)
+
+    # ------------------------------------------------------------------ queries
+    def neighbors(self, r: int, min_weight: float = 0.3) -> List[int]:
+        """``MemoryShard.get_neighbors`` of a shard node: other endpoints of the
+        edges its shard stores, with w >= min_weight, in edge order."""
+        if r < 0 or self.kind_h(r) != NODE or self.sup_h(r):
+            return []
+        sc = int(self.mirror("shard")[r])
+        e = self.e
+        with self.on_stream():
+            m = ((e["src"] == r) | (e["dst"] == r)) & ((e["meta"] & SHARD_MASK) == sc) & (e["w"] >= min_weight)
+            idx = torch.nonzero(m).flatten()
+            s, d = e["src"][idx].tolist(), e["dst"][idx].tolist()
+        return [b if a == r else a for a, b in zip(s, d)]
+
+    def csr(self):
+        if self._csr is None or self._csr_version != self.edge_version or self._csr[0].numel() != self.n + 1:
+            with self.on_stream():
+                self._csr = T.build_visible_csr(self.e, self.shard[: self.n], self.n)
+            self._csr_version = self.edge_version
+        return self._csr
+
+    def boost(self, seed_rows: Sequence[int], now: Optional[float] = None, min_w: float = 0.3,
+              delta: float = 0.02) -> int:
+        seeds = [r for r in seed_rows if r >= 0]
+        if not seeds or self.num_edges == 0:
+            return 0
+        now = time.time() if now is None else now
+        csr = self.csr()
+        with self.on_stream():
+            st = torch.as_tensor(seeds, dtype=torch.int32).to(self.device)
+            k = T.neighbor_boost(csr, self.e["w"], st, self.kind, self.sup, self.sal, self.last, self.dirty, now,
+                                 self._boost_state, min_w, delta)
+        if k:
+            self._bump()
+        return k
+
+    def touch(self, rows: Sequence[int], now: Optional[float] = None) -> None:
+        rows = [r for r in rows if r >= 0]
+        if not rows:
+            return
+        now = time.time() if now is None else now
+        with self.on_stream():
+            T.touch(torch.as_tensor(rows, dtype=torch.long).to(self.device), self.acc, self.last, self.sal,
+                    self.dirty, now)
+        self._bump()
+
+    def components(self) -> List[np.ndarray]:
+        """Connected components containing at least one live node, as arrays of
+        rows (ghost endpoints included, like the reference's DFS that follows
+        edges to missing ids), ordered by their first member in
+        ``ordered_node_rows`` order; members in row order."""
+        n = self.n
+        if n == 0:
+            return []
+        with self.on_stream():
+            lab = T.components(self.e["src"], self.e["dst"], n)
+            lab_h = lab.cpu().numpy() if torch.is_tensor(lab) else np.asarray(lab)
+            touched = np.zeros(n, dtype=bool)
+            if self.num_edges:
+                touched[self.e["src"].cpu().numpy()] = True
+                touched[self.e["dst"].cpu().numpy()] = True
+        kind = self.mirror("kind")
+        order = self.ordered_node_rows()
+        member = (kind == NODE) | ((kind == GHOST) & touched)
+        rows = np.nonzero(member)[0]
+        if rows.size == 0:
+            return []
+        labs = lab_h[rows]
+        o = np.argsort(labs, kind="stable")
+        rows, labs = rows[o], labs[o]
+        uniq, start = np.unique(labs, return_index=True)
+        groups = np.split(rows, start[1:])
+        # position of each label's first member in the reference node order
+        pos = np.full(n, np.iinfo(np.int64).max, dtype=np.int64)
+        pos[order] = np.arange(order.size)
+        first = np.full(n, np.iinfo(np.int64).max, dtype=np.int64)
+        np.minimum.at(first, lab_h[order], pos[order])
+        keyed = [(int(first[lb]), g) for lb, g in zip(uniq.tolist(), groups) if first[lb] < np.iinfo(np.int64).max]
+        keyed.sort(key=lambda x: x[0])
+        return [g for _, g in keyed]
+
+    def component_edge_stats(self, comps: List[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
+        """(sum of weights, count) of edges with both endpoints in the same
+        component, per component (reference memory_system.py:970-985)."""
+        C = len(comps)
+        if C == 0 or self.num_edges == 0:
+            return np.zeros(C), np.zeros(C, dtype=np.int64)
+        cid = np.full(self.n, -1, dtype=np.int64)
+        for i, g in enumerate(comps):
+            cid[g] = i
+        with self.on_stream():
+            cid_t = torch.as_tensor(cid).to(self.device)
+            cs, ct = cid_t[self.e["src"].long()], cid_t[self.e["dst"].long()]
+            ok = (cs >= 0) & (cs == ct)
+            wsum = torch.zeros(C, dtype=torch.float64, device=self.device).index_add_(
+                0, cs[ok], self.e["w"][ok].double())
+            wcnt = torch.bincount(cs[ok], minlength=C)
+            return wsum.cpu().numpy(), wcnt.cpu().numpy()
+
+    # ------------------------------------------------------------------ search
+    def unit_rows(self) -> bool:
+        return self.max_norm_dev < 1e-3
+
+    def _exact_cos(self, Qn: torch.Tensor, mask: torch.Tensor, k: int, row_label=None, q_label=None,
+                   chunk: int = 1 << 18):
+        """Exact float64 cosine top-k (ties -> lower row). Qn: unit fp64 [M, D]."""
+        M = Qn.shape[0]
+        n = self.n
+        dev = self.device
+        best_s = torch.full((M, 0), NEG_INF, dtype=torch.float64, device=dev)
+        best_i = torch.zeros((M, 0), dtype=torch.long, device=dev)
+        for c0 in range(0, n, chunk):
+            c1 = min(n, c0 + chunk)
+            X = self.emb32[c0:c1].double()
+            nrm = self.sqn[c0:c1].double().sqrt()
+            s = (Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]
+            ok = mask[c0:c1][None, :].expand(M, -1)
+            if row_label is not None:
+                ok = ok & (row_label[c0:c1][None, :] == q_label[:, None])
+            s = torch.where(ok, s, torch.full_like(s, NEG_INF))
+            idx = torch.arange(c0, c1, device=dev).expand(M, -1)
+            cs, ci = torch.cat([best_s, s], 1), torch.cat([best_i, idx], 1)
+            o = torch.sort(cs, dim=1, descending=True, stable=True).indices[:, :k]
+            best_s, best_i = torch.gather(cs, 1, o), torch.gather(ci, 1, o)
+        return self._pad_k(best_s, best_i, k)
+
+    @staticmethod
+    def _pad_k(s, i, k):
+        M = s.shape[0]
+        if s.shape[1] < k:
+            pad = k - s.shape[1]
+            s = torch.cat([s, torch.full((M, pad), NEG_INF, dtype=s.dtype, device=s.device)], 1)
+            i = torch.cat([i, torch.full((M, pad), -1, dtype=torch.long, device=i.device)], 1)
+        i = torch.where(torch.isneginf(s), torch.full_like(i, -1), i)
+        return s, i
+
+    def _rerank_cos(self, Qn: torch.Tensor, cand: torch.Tensor, k: int):
+        """Exact float64 cosine of kernel candidates ``cand`` [M, c] (-1 empty),
+        sorted (score desc, row asc), cut to k."""
+        valid = cand >= 0
+        rows = cand.clamp_min(0)
+        X = self.emb32[rows].double()  # [M, c, D]
+        nrm = self.sqn[rows].double().sqrt()
+        s = torch.einsum("md,mcd->mc", Qn, X) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))
+        s = torch.where(valid, s, torch.full_like(s, NEG_INF))
+        key = torch.where(valid, cand, torch.full_like(cand, 1 << 62))
+        o = torch.argsort(key, dim=1, stable=True)
+        s, cand = torch.gather(s, 1, o), torch.gather(cand, 1, o)
+        o = torch.sort(s, dim=1, descending=True, stable=True).indices[:, :k]
+        return self._pad_k(torch.gather(s, 1, o), torch.gather(cand, 1, o), k)
+
+    def _use_kernel(self, M: int) -> bool:
+        return self.on_gpu and self.unit_rows() and M * self.n >= KERNEL_MIN_WORK
+
+    def _q16(self, Qn: torch.Tensor) -> torch.Tensor:
+        q = torch.zeros((Qn.shape[0], self.Dp), dtype=torch.bfloat16, device=self.device)
+        q[:, : self.dim] = Qn.to(torch.bfloat16)
+        return q
+
+    def cos_topk(self, Q: torch.Tensor, k: int, mask: torch.Tensor, dual_label: Optional[torch.Tensor] = None):
+        """Cosine top-k of each query row among rows where ``mask``. With
+        ``dual_label`` (shard code per query) also returns the top-k restricted
+        to rows of the query's shard, from the same scan. Scores are exact
+        float64 (kernel candidates re-ranked). Returns (s, rows) or
+        ((s, rows), (s_shard, rows_shard))."""
+        with self.on_stream():
+            return self._cos_topk(Q, k, mask, dual_label)
+
+    def _cos_topk(self, Q, k, mask, dual_label):
+        from ..ops.search import flat_topk, flat_topk_dual
+        M = Q.shape[0]
+        n = self.n
+        dev = self.device
+        if n == 0 or M == 0 or self.dim is None:
+            e = self._pad_k(torch.zeros((M, 0), dtype=torch.float64, device=dev),
+                            torch.zeros((M, 0), dtype=torch.long, device=dev), k)
+            return (e, e) if dual_label is not None else e
+        Qd = Q.to(dev, torch.float64)
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        lab = self.shard[:n]
+        if self._use_kernel(M) and k <= CAND_SLOTS:
+            bias = torch.where(mask, 0.0, NEG_INF).to(torch.float32).contiguous()
+            q16 = self._q16(Qn)
+            X = self.emb16[:n]
+            if dual_label is not None:
+                ql = dual_label.to(dev, torch.int32).contiguous()
+                (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
+                                                  bias=bias)
+                return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
+            _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
+            return self._rerank_cos(Qn, ra, k)
+        if dual_label is not None:
+            ql = dual_label.to(dev, torch.int32)
+            return (self._exact_cos(Qn, mask, k), self._exact_cos(Qn, mask, k, row_label=lab, q_label=ql))
+        return self._exact_cos(Qn, mask, k)
+
+    def store_bias(self, metric: str) -> torch.Tensor:
+        """Per-row fp32 score bias of the store search: -inf for rows not in
+        the store; -|x|^2 for L2 (scores = 2<q,x> - |x|^2)."""
+        c = self._bias_cache.get(metric)
+        if c is not None and c[0] == self._store_version and c[1].numel() == self.n:
+            return c[1]
+        n = self.n
+        ok = (self.stored[:n] == 1) & (self.kind[:n] != FREE)
+        b = torch.where(ok, 0.0, NEG_INF).to(torch.float32)
+        if metric == "l2":
+            b = b - self.sqn[:n]
+        b = b.contiguous()
+        self._bias_cache[metric] = (self._store_version, b)
+        return b
+
+    def store_search(self, Q: torch.Tensor, k: int, metric: str = "l2"):
+        """The store's vector search over this tenant (reference
+        ``LanceDBStore.search_nodes``: flat scan, L2 unless told otherwise,
+        vector_store.py:132-140). fp32 scores -- -|q-x|^2 for L2, cosine, or
+        dot -- higher is closer; bf16 MFMA candidates are re-ranked in fp32.
+        Returns (scores [M, k], rows [M, k])."""
+        with self.on_stream():
+            return self._store_search(Q, k, metric)
+
+    def _store_search(self, Q, k, metric):
+        from ..ops.search import flat_topk
+        n = self.n
+        dev = self.device
+        Qf = Q.to(dev, torch.float32)
+        if Qf.dim() == 1:
+            Qf = Qf[None, :]
+        M = Qf.shape[0]
+        if n == 0 or self.dim is None or Qf.shape[1] != self.dim:
+            return self._pad_k(torch.zeros((M, 0), device=dev), torch.zeros((M, 0), dtype=torch.long, device=dev), k)
+        if metric == "cosine":
+            qn = Qf.norm(dim=1, keepdim=True)
+            Qf = Qf / torch.where(qn > 0, qn, torch.ones_like(qn))
+        bias = self.store_bias("l2" if metric == "l2" else "ip")
+        alpha = 2.0 if metric == "l2" else 1.0
+        kc = min(CAND_SLOTS, max(k, 2 * k))
+        if self.on_gpu and k <= CAND_SLOTS and (metric != "cosine" or self.unit_rows()) \
+                and M * n >= KERNEL_MIN_WORK // 16:
+            _, cand = flat_topk(self.emb16[:n], self._q16(Qf), kc, bias=bias, alpha=alpha)
+            return self._rerank_store(Qf, cand, k, metric, bias)
+        return self._exact_store(Qf, k, metric, bias)
+
+    def _store_scores(self, Qf, X, sqn, bias, metric):
+        dot = Qf @ X.T if X.dim() == 2 else torch.einsum("md,mcd->mc", Qf, X)
+        if metric == "l2":
+            return 2.0 * dot + bias - (Qf * Qf).sum(1, keepdim=True)
+        if metric == "cosine":
+            nrm = sqn.sqrt()
+            return dot / torch.where(nrm > 0, nrm, torch.ones_like(nrm)) + bias
+        return dot + bias
+
+    def _exact_store(self, Qf, k, metric, bias, chunk: int = 1 << 18):
+        n = self.n
+        M = Qf.shape[0]
+        best_s = torch.full((M, 0), NEG_INF, device=self.device)
+        best_i = torch.zeros((M, 0), dtype=torch.long, device=self.device)
+        for c0 in range(0, n, chunk):
+            c1 = min(n, c0 + chunk)
+            s = self._store_scores(Qf, self.emb32[c0:c1], self.sqn[c0:c1][None, :], bias[c0:c1][None, :], metric)
+            idx = torch.arange(c0, c1, device=self.device).expand(M, -1)
+            cs, ci = torch.cat([best_s, s], 1), torch.cat([best_i, idx], 1)
+            o = torch.sort(cs, dim=1, descending=True, stable=True).indices[:, :k]
+            best_s, best_i = torch.gather(cs, 1, o), torch.gather(ci, 1, o)
+        return self._pad_k(best_s, best_i, k)
+
+    def _rerank_store(self, Qf, cand, k, metric, bias):
+        valid = cand >= 0
+        rows = cand.clamp_min(0)
+        s = self._store_scores(Qf, self.emb32[rows], self.sqn[rows], bias[rows], metric)
+        s = torch.where(valid, s, torch.full_like(s, NEG_INF))
+        key = torch.where(valid, cand, torch.full_like(cand, 1 << 62))
+        o = torch.argsort(key, dim=1, stable=True)
+        s, cand = torch.gather(s, 1, o), torch.gather(cand, 1, o)
+        o = torch.sort(s, dim=1, descending=True, stable=True).indices[:, :k]
+        return self._pad_k(torch.gather(s, 1, o), torch.gather(cand, 1, o), k)
+
+    def search_ids(self, Q, k: int, metric: str = "l2") -> List[List[str]]:
+        _, r = self.store_search(Q, k, metric)
+        ids = self.ids
+        return [[ids[x] for x in row if x >= 0] for row in r.cpu().tolist()]
+
+    # ------------------------------------------------------------------ centroid
+    def mean_embedding(self, rows: torch.Tensor) -> Optional[torch.Tensor]:
+        """Mean embedding (float64) of the rows that have one (reference
+        ``np.mean`` of the children's embeddings, memory_system.py:916-917)."""
+        if self.dim is None or rows.numel() == 0:
+            return None
+        with self.on_stream():
+            rows = rows.to(self.device)
+            has = self.has_emb[rows].bool()
+            if not bool(has.any()):
+                return None
+            return self.emb32[rows[has]].double().mean(0)
+
+    # ------------------------------------------------------------------ persistence helpers
+    def take_dirty_rows(self) -> np.ndarray:
+        """Rows changed since the last commit (new / boosted / touched /
+        merged), cleared on return."""
+        if self.n == 0:
+            return np.zeros(0, dtype=np.int64)
+        with self.on_stream():
+            n = self.n
+            d = torch.nonzero(self.dirty[:n]).flatten()
+            self.dirty[:n] = 0
+            out = d.cpu().numpy()
+        self._mirror.pop("dirty", None)
+        return out
+
+    def take_dirty_edges(self) -> np.ndarray:
+        if self.num_edges == 0:
+            return np.zeros(0, dtype=np.int64)
+        with self.on_stream():
+            m = (self.e["meta"] & EDIRTY) != 0
+            idx = torch.nonzero(m).flatten()
+            self.e["meta"] &= ~EDIRTY
+            return idx.cpu().numpy()
+
+    def restore_tracking(self, rows, eidx, del_ids, del_edges) -> None:
+        """Undo ``take_*`` after a failed commit (the change set stays pending)."""
+        with self.on_stream():
+            if len(rows):
+                self.dirty[torch.as_tensor(np.asarray(rows), dtype=torch.long).to(self.device)] = 1
+            if len(eidx):
+                it = torch.as_tensor(np.asarray(eidx), dtype=torch.long).to(self.device)
+                self.e["meta"][it] |= EDIRTY
+        for i in del_ids:
+            self.deleted_ids[i] = None
+        for k in del_edges:
+            self.deleted_edges[k] = None
+        self._mirror.pop("dirty", None)
+
+    def take_deleted(self):
+        ids, edges = list(self.deleted_ids), list(self.deleted_edges)
+        self.deleted_ids, self.deleted_edges = {}, {}
+        return ids, edges
+
+    def clear_tracking(self) -> None:
+        """Forget pending changes (the caller wrote a full snapshot)."""
+        self.take_dirty_rows()
+        self.take_dirty_edges()
+        self.take_deleted()

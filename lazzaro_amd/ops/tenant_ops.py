@@ -1,0 +1,244 @@
+"""Tenant-graph maintenance ops (``csrc/kernels/tenant.hip``).
+
+Device tensors go through the HIP kernels; CPU tensors through torch code that
+computes the same thing (the CPU test tier, not a fallback: ``_lib.lib()``
+raises on a GPU box without the kernel library).
+
+Layout (see :mod:`lazzaro_amd.engine.tenant_graph`): nodes ``sal f32, acc
+i32, last f64, kind u8, sup u8, shard i32, dirty u8``; edges ``src/dst i32,
+w f32, co i32, lu f64, meta i32 (shard | type << 24)``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
+D_ = C.c_double
+
+_lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, P])
+_lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, P, P])
+_lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
+_lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, F, P, P, P, P, I, P, P])
+_lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, F, P])
+_lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
+_lib.register("lzk_scan_blocks", I, [P, I, P, P])
+
+SALIENCE_FLOOR = 0.2
+EDGE_COLS = ("src", "dst", "w", "co", "lu", "meta")
+NTB = 256
+
+
+def _st(t: torch.Tensor) -> int:
+    return _lib.stream_ptr(t.device)
+
+
+def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, ne: int):
+    """Stable device compaction of the flagged edges (scan + scatter)."""
+    L_ = _lib.lib()
+    dev = e["src"].device
+    total = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(L_.lzk_scan_blocks(bc.data_ptr(), bc.numel(), total.data_ptr(), _st(bc)), "scan_blocks")
+    n_out = int(total.item())
+    if n_out == ne:
+        return e, 0
+    out = {k: torch.empty(n_out, dtype=e[k].dtype, device=dev) for k in EDGE_COLS}
+    if n_out:
+        _lib.check(L_.lzk_tg_compact(flag.data_ptr(), bc.data_ptr(), ne, *(e[k].data_ptr() for k in EDGE_COLS),
+                                     *(out[k].data_ptr() for k in EDGE_COLS), _st(flag)), "tg_compact")
+    return out, ne - n_out
+
+
+def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, threshold: Optional[float],
+                decay_nodes: bool = True, want_dropped: bool = False):
+    """Temporal decay of every edge and shard-node salience (reference
+    memory_shard.py:64-77), then, if ``threshold`` is not None, removal of
+    edges with ``w < threshold`` (:79-84) with stable compaction.
+
+    Returns (edges, n_pruned, dropped) where ``dropped`` is (src, dst) of the
+    pruned edges when ``want_dropped`` (for incremental persistence)."""
+    ne = int(e["src"].numel())
+    keep = 1.0 - rate
+    nn = int(sal.numel()) if sal is not None else 0
+    dropped = None
+    if not e["src"].is_cuda:
+        if rate:
+            e["w"].mul_(keep)
+        if decay_nodes and nn:
+            m = (kind == 1) & (sup == 0)
+            dec = torch.where(sal > SALIENCE_FLOOR, SALIENCE_FLOOR + (sal - SALIENCE_FLOOR) * keep,
+                              torch.full_like(sal, SALIENCE_FLOOR))
+            sal.copy_(torch.where(m, dec, sal))
+        if threshold is None or ne == 0:
+            return e, 0, dropped
+        f = e["w"] >= threshold
+        if want_dropped:
+            dropped = (e["src"][~f], e["dst"][~f])
+        n_keep = int(f.sum())
+        if n_keep == ne:
+            return e, 0, dropped
+        return {k: v[f] for k, v in e.items()}, ne - n_keep, dropped
+    dev = e["src"].device
+    nb = max(1, (ne + NTB - 1) // NTB)
+    flag = torch.empty(max(ne, 1), dtype=torch.uint8, device=dev) if threshold is not None else None
+    bc = torch.empty(nb, dtype=torch.int32, device=dev) if threshold is not None else None
+    thr = float(threshold) if threshold is not None else float("-inf")
+    _lib.check(_lib.lib().lzk_tg_decay(e["w"].data_ptr(), ne, float(keep), thr, _lib.ptr(flag), _lib.ptr(bc),
+                                       _lib.ptr(sal), _lib.ptr(kind), _lib.ptr(sup), nn,
+                                       1 if (decay_nodes and nn) else 0, _st(e["w"])), "tg_decay")
+    if threshold is None or ne == 0:
+        return e, 0, dropped
+    if want_dropped:
+        f = flag[:ne] == 0
+        dropped = (e["src"][f], e["dst"][f])
+    out, n = _compact(e, flag, bc, ne)
+    return out, n, dropped
+
+
+def remove_edges_of(e: Dict[str, torch.Tensor], rm: torch.Tensor, shard: torch.Tensor, want_dropped: bool = False):
+    """Drop the edges that a removed node's shard stores (reference
+    memory_system.py:558-569): edge dropped iff an endpoint has ``rm`` set and
+    the edge's shard equals that endpoint's shard. Returns (edges, n, dropped)."""
+    ne = int(e["src"].numel())
+    if ne == 0:
+        return e, 0, None
+    es = e["meta"] & 0xFFFFFF
+    if not e["src"].is_cuda:
+        s, d = e["src"].long(), e["dst"].long()
+        drop = (rm[s].bool() & (shard[s] == es)) | (rm[d].bool() & (shard[d] == es))
+        dropped = (e["src"][drop], e["dst"][drop]) if want_dropped else None
+        n = int(drop.sum())
+        if n == 0:
+            return e, 0, dropped
+        keep = ~drop
+        return {k: v[keep] for k, v in e.items()}, n, dropped
+    dev = e["src"].device
+    nb = max(1, (ne + NTB - 1) // NTB)
+    flag = torch.empty(ne, dtype=torch.uint8, device=dev)
+    bc = torch.empty(nb, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().lzk_tg_flag_remove(e["src"].data_ptr(), e["dst"].data_ptr(), e["meta"].data_ptr(), ne,
+                                             rm.data_ptr(), shard.data_ptr(), flag.data_ptr(), bc.data_ptr(),
+                                             _st(flag)), "tg_flag_remove")
+    dropped = None
+    if want_dropped:
+        f = flag == 0
+        dropped = (e["src"][f], e["dst"][f])
+    out, n = _compact(e, flag, bc, ne)
+    return out, n, dropped
+
+
+def build_visible_csr(e: Dict[str, torch.Tensor], shard: torch.Tensor, n: int):
+    """CSR of visible arcs: a->b for an edge (a, b) or (b, a) stored in a's
+    shard, ordered per source by edge index (the reference's dict order), built
+    on the tensors' device. Returns (off int64 [n+1], adj int32, eid int32)."""
+    dev = e["src"].device
+    ne = int(e["src"].numel())
+    if ne == 0:
+        return (torch.zeros(n + 1, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.int32, device=dev),
+                torch.zeros(0, dtype=torch.int32, device=dev))
+    s, d = e["src"].long(), e["dst"].long()
+    es = e["meta"] & 0xFFFFFF
+    fwd = shard[s] == es
+    bwd = (shard[d] == es) & (s != d)
+    frm = torch.stack([s, d], 1).reshape(-1)
+    to = torch.stack([d, s], 1).reshape(-1)
+    ok = torch.stack([fwd, bwd], 1).reshape(-1)
+    eid = torch.arange(ne, device=dev).repeat_interleave(2)
+    frm, to, eid = frm[ok], to[ok], eid[ok]
+    order = torch.sort(frm, stable=True).indices
+    frm, to, eid = frm[order], to[order], eid[order]
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(torch.bincount(frm, minlength=n)[:n], 0)
+    return off, to.to(torch.int32), eid.to(torch.int32)
+
+
+class BoostState:
+    """Per-graph epoch stamps so a boost never clears an N-sized array."""
+
+    def __init__(self):
+        self.stamp: Optional[torch.Tensor] = None
+        self.epoch = 0
+
+    def next(self, n: int, dev) -> Tuple[torch.Tensor, int]:
+        if self.stamp is None or self.stamp.numel() < n or self.stamp.device != torch.device(dev) \
+                or self.epoch >= (1 << 30):
+            self.stamp = torch.zeros(max(n, 1024) * 3 // 2, dtype=torch.int32, device=dev)
+            self.epoch = 0
+        self.epoch += 1
+        return self.stamp, self.epoch
+
+
+def neighbor_boost(csr, w, seeds: torch.Tensor, kind, sup, sal, last, dirty, now: float, state: BoostState,
+                   min_w: float = 0.3, delta: float = 0.02) -> int:
+    """Reference ``_boost_neighbors`` (memory_system.py:242-260): neighbours
+    (visible, w >= min_w, live nodes, not seeds) of the seeds get
+    last_accessed = now and salience + delta (capped at 1), once each."""
+    if seeds.numel() == 0:
+        return 0
+    off, adj, eid = csr
+    if not sal.is_cuda:
+        seen = set()
+        ss = set(int(x) for x in seeds.tolist())
+        for s in seeds.tolist():
+            if s < 0 or int(sup[s]):
+                continue
+            for p in range(int(off[s]), int(off[s + 1])):
+                nb = int(adj[p])
+                if float(w[int(eid[p])]) < min_w or nb in ss or nb in seen or int(kind[nb]) != 1:
+                    continue
+                seen.add(nb)
+                sal[nb] = min(1.0, float(sal[nb]) + delta)
+                last[nb] = now
+                dirty[nb] = 1
+        return len(seen)
+    stamp, ep = state.next(int(sal.numel()), sal.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=sal.device)
+    seeds = seeds.to(torch.int32).contiguous()
+    _lib.check(_lib.lib().lzk_tg_boost(off.data_ptr(), adj.data_ptr(), eid.data_ptr(), w.data_ptr(),
+                                       seeds.data_ptr(), seeds.numel(), kind.data_ptr(), sup.data_ptr(), float(min_w),
+                                       float(now), float(delta), sal.data_ptr(), last.data_ptr(), dirty.data_ptr(),
+                                       stamp.data_ptr(), ep, cnt.data_ptr(), _st(sal)), "tg_boost")
+    return int(cnt.item())
+
+
+def touch(rows: torch.Tensor, acc, last, sal, dirty, now: float, delta: float = 0.05) -> None:
+    """``BufferGraph.update_access`` for each row (buffer_graph.py:79-85)."""
+    if rows.numel() == 0:
+        return
+    if not sal.is_cuda:
+        for r in rows.tolist():
+            acc[r] += 1
+            last[r] = now
+            sal[r] = min(1.0, float(sal[r]) + delta)
+            dirty[r] = 1
+        return
+    rows = rows.to(torch.int64).contiguous()
+    _lib.check(_lib.lib().lzk_tg_touch(rows.data_ptr(), rows.numel(), acc.data_ptr(), last.data_ptr(),
+                                       sal.data_ptr(), dirty.data_ptr(), float(now), float(delta), _st(sal)),
+               "tg_touch")
+
+
+def importance(sal, acc, last, kind, sup, now: float) -> torch.Tensor:
+    """Eviction score (memory_system.py:541-549) in float64; +inf for rows that
+    are not evictable (not a live shard node, or a super-node)."""
+    if not sal.is_cuda:
+        days = (now - last) / 86400.0
+        v = sal.double() * 0.5 + torch.clamp(acc.double() / 10.0, max=1.0) * 0.3 + (1.0 / (1.0 + days)) * 0.2
+        bad = (kind != 1) | (sup != 0)
+        return torch.where(bad, torch.full_like(v, float("inf")), v)
+    out = torch.empty(sal.numel(), dtype=torch.float64, device=sal.device)
+    _lib.check(_lib.lib().lzk_tg_importance(sal.data_ptr(), acc.data_ptr(), last.data_ptr(), kind.data_ptr(),
+                                            sup.data_ptr(), sal.numel(), float(now), out.data_ptr(), _st(sal)),
+               "tg_importance")
+    return out
+
+
+def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:
+    """Undirected connected components (label = smallest row of the
+    component): device hook/compress kernels (graph.hip) or host union-find."""
+    from .graph_ops import connected_components
+    return connected_components(src, dst, n)

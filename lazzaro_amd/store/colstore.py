@@ -36,11 +36,12 @@ NODE_SCHEMA: List[Tuple[str, int, int]] = [
     ("type", STR, 0), ("timestamp", F64, 0), ("access_count", I32, 0),
     ("last_accessed", F64, 0), ("salience", F32, 0), ("is_super_node", BOOL, 0),
     ("child_ids", STR, 0), ("parent_id", STR, 0), ("shard_key", STR, 0), ("metadata", STR, 0),
+    ("decay_clock", F64, 0),
 ]
 EDGE_SCHEMA: List[Tuple[str, int, int]] = [
     ("id", STR, 0), ("user_id", STR, 0), ("source_id", STR, 0), ("target_id", STR, 0),
     ("weight", F32, 0), ("edge_type", STR, 0), ("co_occurrence", I32, 0),
-    ("last_updated", F64, 0), ("metadata", STR, 0),
+    ("last_updated", F64, 0), ("metadata", STR, 0), ("decay_clock", F64, 0),
 ]
 PROFILE_SCHEMA: List[Tuple[str, int, int]] = [
     ("user_id", STR, 0), ("data", STR, 0), ("updated_at", F64, 0),
@@ -64,7 +65,8 @@ class ColumnarTable:
     def _columns(self, rows: Sequence[Dict]) -> Dict:
         cols = {}
         for n, t, d in self.schema:
-            vals = [r[n] for r in rows]
+            dflt = 0.0 if t in (F64, F32) else (0 if t in (I32, I64, BOOL) else ("{}" if n == "metadata" else ""))
+            vals = [r.get(n, dflt) for r in rows]
             if t == STR:
                 cols[n] = [("" if v is None else str(v)) for v in vals]
             elif t == VEC:
@@ -99,6 +101,32 @@ class ColumnarTable:
         committed version). Returns (rows deleted, new version)."""
         fault_point("store.commit")
         n, v = self._t.replace_where(list(eq), "", None, self._columns(rows))
+        return int(n), int(v)
+
+    def fill_columns(self, cols: Dict, n: int, const: Dict) -> Dict:
+        """Complete a column dict for ``n`` rows: ``const`` gives values for
+        columns held constant (e.g. user_id), missing ones get defaults."""
+        out = {}
+        for name, t, d in self.schema:
+            if name in const:
+                v = const[name]
+                out[name] = [v] * n if t == STR else np.full(n, v, dtype=_NP[t])
+            elif name in cols:
+                out[name] = cols[name]
+            elif t == STR:
+                out[name] = ["{}" if name == "metadata" else ""] * n
+            elif t == VEC:
+                out[name] = np.zeros((n, d or 0), dtype=np.float32)
+            else:
+                out[name] = np.zeros(n, dtype=_NP[t])
+        return out
+
+    def upsert_columns(self, eq: Sequence[Tuple[str, str]], key: str, keys: Sequence[str], cols: Dict
+                       ) -> Tuple[int, int]:
+        """One committed version that deletes the rows matching ``eq`` whose
+        ``key`` is in ``keys`` and appends ``cols`` (upsert + delete)."""
+        fault_point("store.commit")
+        n, v = self._t.replace_where(list(eq), key, list(keys), cols)
         return int(n), int(v)
 
     def add_columns(self, cols: Dict) -> int:

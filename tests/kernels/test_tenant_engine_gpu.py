@@ -1,0 +1,247 @@
+"""The device engine under MemorySystem (engine/tenant_graph.py,
+csrc/kernels/tenant.hip) on an MI355X vs the same engine on the CPU.
+
+* kernel-level: each tenant kernel against the torch reference of tenant_ops;
+* system-level: the same MemorySystem scenario (conversations, chat with
+  boost/touch, dedupe, linking, decay/prune, eviction, super-nodes, deep
+  consolidation, persistence reload) on cuda and on cpu must produce the same
+  nodes, edges, saliences, access counts and profile; and a large-tenant
+  scenario that takes the fused MFMA scan path (bf16 candidates + float64
+  re-rank) must take the same decisions as the CPU's exact float64 scan.
+"""
+import itertools
+import json
+import time
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from lazzaro_amd.core.memory_system import MemorySystem  # noqa: E402
+from lazzaro_amd.core.providers import HashEmbedder, LocalLLM  # noqa: E402
+from lazzaro_amd.engine.tenant_graph import NODE, TenantGraph  # noqa: E402
+from lazzaro_amd.ops import tenant_ops as T  # noqa: E402
+
+DEV = "cuda"
+
+
+def _edges(n, ne, seed, dev, n_shards=4):
+    g = torch.Generator().manual_seed(seed)
+    e = {"src": torch.randint(0, n, (ne,), generator=g, dtype=torch.int32),
+         "dst": torch.randint(0, n, (ne,), generator=g, dtype=torch.int32),
+         "w": torch.rand(ne, generator=g), "co": torch.arange(ne, dtype=torch.int32),
+         "lu": torch.rand(ne, generator=g, dtype=torch.float64),
+         "meta": torch.randint(0, n_shards, (ne,), generator=g, dtype=torch.int32) | (1 << 24)}
+    return {k: v.to(dev) for k, v in e.items()}
+
+
+def _nodes(n, seed, dev, n_shards=4):
+    g = torch.Generator().manual_seed(seed)
+    return {"sal": torch.rand(n, generator=g), "kind": torch.randint(0, 3, (n,), generator=g).to(torch.uint8),
+            "sup": (torch.rand(n, generator=g) > 0.9).to(torch.uint8),
+            "shard": torch.randint(0, n_shards, (n,), generator=g, dtype=torch.int32),
+            "acc": torch.randint(0, 20, (n,), generator=g, dtype=torch.int32),
+            "last": torch.rand(n, generator=g, dtype=torch.float64) * 1e6,
+            "dirty": torch.zeros(n, dtype=torch.uint8)}
+
+
+@pytest.mark.parametrize("ne,thr", [(0, 0.5), (1, 0.5), (5000, 0.4), (400_001, 0.3), (70_000, None)])
+def test_decay_prune_kernel(ne, thr):
+    n = 20000
+    ec, eg = _edges(n, ne, 1, "cpu"), _edges(n, ne, 1, DEV)
+    nc = _nodes(n, 2, "cpu")
+    ng = {k: v.to(DEV) for k, v in nc.items()}
+    oc, pc, dc = T.decay_prune(ec, nc["sal"], nc["kind"], nc["sup"], 0.05, thr, True, want_dropped=True)
+    og, pg, dg = T.decay_prune(eg, ng["sal"], ng["kind"], ng["sup"], 0.05, thr, True, want_dropped=True)
+    assert pc == pg
+    for k in oc:
+        assert torch.equal(oc[k], og[k].cpu()), k
+    assert torch.equal(nc["sal"], ng["sal"].cpu())
+    if thr is not None and pc:
+        assert torch.equal(dc[0], dg[0].cpu()) and torch.equal(dc[1], dg[1].cpu())
+
+
+@pytest.mark.parametrize("ne", [1000, 300_000])
+def test_remove_edges_of_kernel(ne):
+    n = 10000
+    ec, eg = _edges(n, ne, 3, "cpu"), _edges(n, ne, 3, DEV)
+    nc = _nodes(n, 4, "cpu")
+    rm = (torch.rand(n, generator=torch.Generator().manual_seed(5)) > 0.8).to(torch.uint8)
+    oc, kc, _ = T.remove_edges_of(ec, rm, nc["shard"])
+    og, kg, _ = T.remove_edges_of(eg, rm.to(DEV), nc["shard"].to(DEV))
+    assert kc == kg and kc > 0
+    for k in oc:
+        assert torch.equal(oc[k], og[k].cpu()), k
+
+
+def test_visible_csr_boost_touch_importance_kernels():
+    n, ne = 5000, 40000
+    ec, eg = _edges(n, ne, 6, "cpu"), _edges(n, ne, 6, DEV)
+    nc = _nodes(n, 7, "cpu")
+    ng = {k: v.to(DEV) for k, v in nc.items()}
+    cc = T.build_visible_csr(ec, nc["shard"], n)
+    cg = T.build_visible_csr(eg, ng["shard"], n)
+    for a, b in zip(cc, cg):
+        assert torch.equal(a, b.cpu())
+    seeds = torch.tensor([3, 17, 999, 4000, 17], dtype=torch.int32)
+    st_c, st_g = T.BoostState(), T.BoostState()
+    kc = T.neighbor_boost(cc, ec["w"], seeds, nc["kind"], nc["sup"], nc["sal"], nc["last"], nc["dirty"], 5e6, st_c)
+    kg = T.neighbor_boost(cg, eg["w"], seeds.to(DEV), ng["kind"], ng["sup"], ng["sal"], ng["last"], ng["dirty"], 5e6,
+                          st_g)
+    assert kc == kg and kc > 0
+    for k in ("sal", "last", "dirty"):
+        assert torch.equal(nc[k], ng[k].cpu()), k
+    # a second call on the same stamp array boosts again (new epoch)
+    kg2 = T.neighbor_boost(cg, eg["w"], seeds.to(DEV), ng["kind"], ng["sup"], ng["sal"], ng["last"], ng["dirty"],
+                           6e6, st_g)
+    assert kg2 == kg
+    rows = torch.tensor([1, 2, 3, 4999], dtype=torch.long)
+    T.touch(rows, nc["acc"], nc["last"], nc["sal"], nc["dirty"], 7e6)
+    T.touch(rows.to(DEV), ng["acc"], ng["last"], ng["sal"], ng["dirty"], 7e6)
+    for k in ("acc", "last", "sal", "dirty"):
+        assert torch.equal(nc[k], ng[k].cpu()), k
+    ic = T.importance(nc["sal"], nc["acc"], nc["last"], nc["kind"], nc["sup"], 8e6)
+    ig = T.importance(ng["sal"], ng["acc"], ng["last"], ng["kind"], ng["sup"], 8e6)
+    assert torch.allclose(ic, ig.cpu(), rtol=1e-12, atol=0)
+
+
+# ---------------------------------------------------------------- system level
+class _Clock:
+    def __init__(self):
+        self.t = 1.7e9
+
+    def __call__(self):
+        self.t += 1.0
+        return self.t
+
+
+def _snapshot(ms):
+    g = ms.graph
+    nodes = {}
+    for nid, n in ms.buffer.nodes.items():
+        nodes[nid] = (n.content, n.shard_key, n.is_super_node, round(n.salience, 5), n.access_count,
+                      tuple(n.child_ids), n.parent_id)
+    edges = {}
+    for sk, sh in ms.shards.items():
+        for key, e in sh.edges.items():
+            edges[(sk,) + key] = (round(e.weight, 5), e.co_occurrence, e.edge_type)
+    return nodes, edges, json.dumps(ms.profile.data, sort_keys=True), ms.get_stats()["buffer_edges"], g.num_nodes()
+
+
+TURNS = ["I work on a robotics project with my colleague Ana and we have a deadline on Friday.",
+         "My family lives in Lisbon and my hobby is sailing on weekends.",
+         "I am learning Japanese from a book and practice every morning.",
+         "I go to the gym for exercise and track my sleep and diet.",
+         "I started a new project on GPU kernels for a client meeting.",
+         "My friend Tom visits home every summer and we cook together.",
+         "I study distributed systems in an online course.",
+         "I run five kilometres for fitness and drink green tea."]
+
+
+def _scenario(device, tmp_path, monkeypatch):
+    monkeypatch.setattr(time, "time", _Clock())
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=64), enable_async=False,
+                      db_dir=str(tmp_path / device), device=device, max_buffer_size=14, super_node_threshold=3,
+                      consolidate_every=3, prune_threshold=0.3)
+    for i, t in enumerate(itertools.islice(itertools.cycle(TURNS), 14)):
+        ms.start_conversation()
+        ms.chat(t)
+        ms.chat(TURNS[(i * 3) % len(TURNS)])
+        ms.end_conversation()
+    snap = _snapshot(ms)
+    hits = [n.id for n in ms.search_memories("robotics project deadline", limit=5)]
+    conn = {nid: sorted(x.id for x in ms.get_connected_memories(nid)) for nid in list(ms.buffer.nodes)[:6]}
+    ms.close()
+    ms2 = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=64), enable_async=False,
+                       db_dir=str(tmp_path / device), device=device, max_buffer_size=14, super_node_threshold=3)
+    reload_snap = _snapshot(ms2)
+    ms2.close()
+    return snap, hits, conn, reload_snap
+
+
+def test_memory_system_cuda_matches_cpu(tmp_path, monkeypatch):
+    cpu = _scenario("cpu", tmp_path, monkeypatch)
+    gpu = _scenario(DEV, tmp_path, monkeypatch)
+    (nc, ec, pc, bc, cc), (ng, eg, pg, bg, cg) = cpu[0], gpu[0]
+    assert nc.keys() == ng.keys() and cc == cg and cc > 0
+    for k in nc:
+        assert nc[k] == ng[k], k
+    assert ec == eg and bc == bg and pc == pg and len(ec) > 0
+    assert cpu[1] == gpu[1] and cpu[2] == gpu[2]
+    # a reload from the incremental store reproduces the in-memory graph
+    assert cpu[3][0].keys() == nc.keys() and gpu[3][0].keys() == ng.keys()
+    for k in nc:
+        assert cpu[3][0][k][:3] == nc[k][:3] and abs(cpu[3][0][k][3] - nc[k][3]) < 1e-4
+        assert gpu[3][0][k][:3] == ng[k][:3] and abs(gpu[3][0][k][3] - ng[k][3]) < 1e-4
+    assert cpu[3][1].keys() == ec.keys() and gpu[3][1].keys() == eg.keys()
+
+
+def _clustered(n, d, n_clusters, seed, noise=0.35):
+    g = torch.Generator().manual_seed(seed)
+    C = torch.randn(n_clusters, d, generator=g)
+    C = C / C.norm(dim=1, keepdim=True)
+    lab = torch.randint(0, n_clusters, (n,), generator=g)
+    X = C[lab] + noise * torch.randn(n, d, generator=g) / d ** 0.5
+    return X / X.norm(dim=1, keepdim=True), lab
+
+
+def test_large_tenant_kernel_path_matches_exact_cpu(tmp_path, monkeypatch):
+    """60k-node tenant: dedupe + links from the fused dual MFMA scan on the
+    GPU vs the exact float64 scan on the CPU; then decay/prune, eviction,
+    components + profile and super-nodes. Identical decisions expected."""
+    monkeypatch.setattr(time, "time", _Clock())
+    N, D, M = 60000, 128, 256
+    X, lab = _clustered(N + M, D, 64, 11)
+    out = {}
+    for dev in ("cpu", DEV):
+        ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
+                          db_dir=str(tmp_path / dev), device=dev, load_from_disk=False, max_buffer_size=N + 64,
+                          super_node_threshold=10 ** 9)
+        g = ms.graph
+        shards = [g.shard_id(f"topic{c % 8}") for c in range(64)]
+        g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"fact {i}" for i in range(N)], X[:N],
+                    shard=np.asarray([shards[int(c)] for c in lab[:N]], dtype=np.int32),
+                    sal=torch.rand(N, generator=torch.Generator().manual_seed(1)), stored=True)
+        ms.node_counter = N
+        # duplicates of existing rows + genuinely new facts
+        Q = torch.cat([X[:32], X[N:N + M - 32]])
+        facts = [{"content": f"new {j}", "salience": 0.9, "topic": f"topic{int(lab[j if j < 32 else N + j - 32]) % 8}"}
+                 for j in range(M)]
+        assert g._use_kernel(M) == (dev == DEV)
+        new = ms._ingest_facts(facts, Q)
+        pruned = g.decay(0.01, 0.5)
+        victims = g.evict(N + 32)
+        comps = g.components()
+        ws, wc = g.component_edge_stats(comps)
+        out[dev] = (new, pruned, victims, g.num_edges, [c.tolist() for c in comps if c.size > 1],
+                    np.round(ws, 6).tolist(), wc.tolist(), g.sal[: g.n].cpu().numpy(), g.acc[: g.n].cpu().numpy(),
+                    {k: v.cpu() for k, v in g.e.items()})
+        ms.close()
+    c, gg = out["cpu"], out[DEV]
+    assert c[0] == gg[0] and len(c[0]) == M - 32
+    assert c[1] == gg[1] and c[2] == gg[2] and c[3] == gg[3] and c[3] > 0
+    assert c[4] == gg[4] and c[5] == gg[5] and c[6] == gg[6]
+    assert np.array_equal(c[7], gg[7]) and np.array_equal(c[8], gg[8])
+    for k in c[9]:
+        assert torch.equal(c[9][k], gg[9][k]), k
+
+
+def test_store_search_fp32_exact_recall_gpu():
+    """HBM store search (bf16 MFMA candidates + fp32 re-rank) == exact fp32
+    L2 top-10 over the original fp32 vectors."""
+    g = TenantGraph(device=DEV)
+    N, D = 300_000, 768
+    gen = torch.Generator().manual_seed(3)
+    X = torch.randn(N, D, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=0, stored=True)
+    Q = torch.randn(512, D, generator=gen)
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    _, rows = g.store_search(Q.to(DEV), 10, "l2")
+    Xg, Qg = X.to(DEV), Q.to(DEV)
+    d2 = (Qg * Qg).sum(1, keepdim=True) - 2 * Qg @ Xg.T + (Xg * Xg).sum(1)[None, :]
+    truth = torch.topk(-d2, 10, dim=1).indices
+    hit = sum(len(set(a) & set(b)) for a, b in zip(rows.cpu().tolist(), truth.cpu().tolist()))
+    assert hit / (512 * 10) == 1.0

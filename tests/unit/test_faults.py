@@ -112,9 +112,16 @@ def test_store_failure_keeps_graph_and_retries_on_next_save(tmp_path):
 
 
 def test_store_failure_during_ingest_rolls_back_then_retries(tmp_path):
+    """Third-party store (not graph-bound): the reference's add_nodes at
+    ingest fails -> the graph is rolled back and the batch re-queued."""
+    from lazzaro_amd.core.vector_store import HBMStore
+
+    class PlainStore(HBMStore):  # opts out of graph binding: behaves like any Store
+        attach = None
+
     llm = ScriptedLLM([_facts("User keeps bees on a rooftop")] * 2)
     ms = MemorySystem(llm_provider=llm, embedding_provider=HashEmbedder(), enable_async=False,
-                      db_dir=str(tmp_path), max_buffer_size=100)
+                      store=PlainStore(db_dir=str(tmp_path)), max_buffer_size=100)
     ms.start_conversation()
     ms.add_to_short_term("I keep bees on a rooftop")
     with armed("store.commit", 1, StoreError):
@@ -122,6 +129,25 @@ def test_store_failure_during_ingest_rolls_back_then_retries(tmp_path):
     assert ms.buffer.size()[0] == 0 and len(ms.consolidation_queue) == 1
     ms._async_consolidate()
     assert ms.buffer.size()[0] == 1 and ms.consolidation_queue == []
+    assert len(ms.store.get_nodes(user_id="default")) == 1
+    ms.close()
+
+
+def test_bound_store_commit_failure_stays_pending(tmp_path):
+    """Graph-bound store: the batch is in the graph; the failed incremental
+    commit keeps its change set pending and the next save writes it once."""
+    llm = ScriptedLLM([_facts("User keeps bees on a rooftop")])
+    ms = MemorySystem(llm_provider=llm, embedding_provider=HashEmbedder(), enable_async=False,
+                      db_dir=str(tmp_path), max_buffer_size=100)
+    ms.start_conversation()
+    ms.add_to_short_term("I keep bees on a rooftop")
+    with armed("store.commit", 2, StoreError):  # both saves of a sync end_conversation
+        ms.end_conversation()
+    assert ms.buffer.size()[0] == 1 and ms._persist_pending
+    assert ms.metrics["persist_failures"] == 2 and ms.store.get_nodes(user_id="default") == []
+    ms._save_to_persistence()
+    assert not ms._persist_pending and len(ms.store.get_nodes(user_id="default")) == 1
+    ms._save_to_persistence()
     assert len(ms.store.get_nodes(user_id="default")) == 1
     ms.close()
 
