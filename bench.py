@@ -1,20 +1,35 @@
 #!/usr/bin/env python
-"""Headline benchmark (BASELINE.json config 2, tenant-sharded for N GPUs).
+"""Headline benchmark (BASELINE.json config 2; tenant-DP over N GPUs).
 
-Metric: search_memories QPS (+ recall@10) on a 10M x d=768 index with the
-bge-base-en (d=768) encoder running on-device; one step = one batch of
-``--batch`` query texts per GPU going through the full search_memories path:
+Metric: ``search_memories`` QPS + recall@10 on a 10M x d=768 tenant, measured
+through the public API. One step = one batch of ``--batch`` query texts per
+GPU through ``MemorySystem.search_memories_stream`` (the pipelined form of
+``search_memories_batch``; reference flow memory_system.py:1460-1472 ->
+vector_store.py:132-140):
 
-    native tokenizer -> bge-base forward (MFMA GEMM/attention/LN kernels)
-    -> fused MFMA flat top-10 over the GPU's 10M-row HBM arena
-    -> RCCL all-gather of (score, row) results to the router rank
+    native tokenizer -> bge-base forward on device (MFMA GEMM / attention / LN
+    kernels) -> store search over the tenant's HBM rows: fused MFMA candidate
+    scan (L2 = 2<q,x> - |x|^2, the store's default metric like LanceDB) +
+    exact fp32 re-rank against the fp32 vectors (the reference stores fp32,
+    vector_store.py:37) -> row -> Node mapping (rows the graph does not hold
+    as nodes are skipped, as in the reference)
 
-Scaling is weak: every GPU owns its own 10M-row tenant shard (tenant-DP, the
-framework's primary scale-out axis) and serves its own query stream, so the
-whole-job value is the sum over GPUs. Data is synthetic: random unit vectors
-for the index, synthetic query sentences, random-init encoder weights (no
-checkpoints offline). recall@10 is measured outside the timed region against an
-exact fp32 scan of the same rows.
+Nothing is skipped inside the timed region; host tokenisation and result
+mapping of one batch overlap the device work of the next (serving pipeline).
+
+Scaling is weak: every GPU owns its own 10M-row tenant (tenant-DP, the
+framework's primary scale-out axis) and serves that tenant's query stream, so
+the whole-job value is the sum over GPUs. Data is synthetic: random unit
+vectors for the stored memories, synthetic query sentences, random-init
+encoder weights (no checkpoints offline).
+
+recall@10 (outside the timed region) is measured against a float64 exact scan
+of the ORIGINAL fp32 vectors, for (a) the benchmark's encoder queries and (b)
+random unit queries (the random-init encoder's outputs are nearly identical,
+so (a) alone would be a weak test).
+
+The second half of the metric (consolidate turns/sec) follows in the same JSON
+line (``--consolidate-steps``; bench/bench_consolidate.py).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 launch with
 torch.distributed.run (one rank per GPU, RCCL backend).
@@ -24,6 +39,7 @@ import json
 import os
 import random
 import sys
+import tempfile
 import time
 
 import torch
@@ -38,28 +54,44 @@ WORDS = ("memory project meeting deadline client python rust family friend hobby
          "book tutorial health exercise diet sleep fitness travel music coffee garden kernel graph vector "
          "search index cluster agent profile language data science model train deploy server cache user "
          "prefers likes works lives started finished visited reading writing running cooking painting").split()
+SHARDS = ("work", "personal", "learning", "health", "2026-10")
 
 
 def synth_texts(n, rng, lo=12, hi=26):
     return [" ".join(rng.choice(WORDS) for _ in range(rng.randint(lo, hi))) + "." for _ in range(n)]
 
 
-def make_index(rows, dim, dev, seed):
-    g = torch.Generator(device=dev).manual_seed(seed)
-    X = torch.empty((rows, dim), dtype=torch.bfloat16, device=dev)
-    step = 1 << 20
-    for r0 in range(0, rows, step):
-        r1 = min(rows, r0 + step)
-        v = torch.randn((r1 - r0, dim), device=dev, generator=g)
-        X[r0:r1] = (v / v.norm(dim=1, keepdim=True)).to(torch.bfloat16)
-    return X
+def populate(ms, rows, dim, dev, seed, chunk=1 << 20):
+    """A ``rows``-memory tenant: random unit fp32 vectors written straight
+    into the tenant graph's HBM columns as stored nodes (what a reload of a
+    persisted tenant produces), spread over the reference's keyword shards."""
+    g = ms.graph
+    g._set_dim(dim)
+    g.reserve(rows)
+    codes = torch.tensor([g.shard_id(s) for s in SHARDS], dtype=torch.int32, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    now = time.time()
+    for r0 in range(0, rows, chunk):
+        r1 = min(rows, r0 + chunk)
+        v = torch.randn((r1 - r0, dim), device=dev, generator=gen)
+        v /= v.norm(dim=1, keepdim=True)
+        ids = [f"node_{i}" for i in range(r0 + 1, r1 + 1)]
+        contents = [f"memory {i}" for i in range(r0 + 1, r1 + 1)]
+        sh = codes[torch.arange(r0, r1, device=dev) % len(SHARDS)]
+        g.add_nodes(ids, contents, v, shard=sh, stored=True, now=now, sal=0.5)
+    ms.node_counter = rows
+    g.clear_tracking()
 
 
-def exact_topk(X, Q, k, chunk=1 << 21):
+def exact_l2_topk(g, Q, k, chunk=1 << 20):
+    """Ground truth: float64 L2 top-k over the fp32 rows (ties -> lower row)."""
+    n = g.n
+    Qd = Q.double()
     best_s = best_i = None
-    Qf = Q.float()
-    for c0 in range(0, X.shape[0], chunk):
-        s = Qf @ X[c0:c0 + chunk].float().T
+    for c0 in range(0, n, chunk):
+        c1 = min(n, c0 + chunk)
+        X = g.emb32[c0:c1].double()
+        s = -((Qd * Qd).sum(1, keepdim=True) - 2.0 * (Qd @ X.T) + (X * X).sum(1)[None, :])
         ts, ti = torch.topk(s, k, dim=1)
         ti += c0
         if best_s is None:
@@ -71,12 +103,20 @@ def exact_topk(X, Q, k, chunk=1 << 21):
     return best_s, best_i
 
 
+def recall(found_rows, truth_rows):
+    hit = tot = 0
+    for f, t in zip(found_rows, truth_rows.tolist()):
+        hit += len(set(f) & set(t))
+        tot += len(t)
+    return hit / max(tot, 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=10_000_000, help="index rows per GPU")
+    ap.add_argument("--rows", type=int, default=10_000_000, help="memories in each GPU's tenant")
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--batch", type=int, default=1024, help="queries per GPU per step")
     ap.add_argument("--k", type=int, default=10)
@@ -99,91 +139,85 @@ def main():
     torch.cuda.set_device(dev)
 
     from lazzaro_amd.core.embedders import OnDeviceEmbedder
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import LocalLLM
     from lazzaro_amd.ops.search import flat_topk
 
-    # sub-batch streams of the embed (bge-base at 1024 queries: 2 fills the GEMM tail waves)
-    parts = int(os.environ.get("LZK_EMBED_PARTS", "2"))
-    frac = float(os.environ.get("LZK_EMBED_FRAC", "0"))  # share of sub-batch 0 (0 = equal parts)
     rng = random.Random(1234 + rank)
     emb = OnDeviceEmbedder(a.model, device=dev, max_len=a.max_len, seed=0)
     assert emb.dim == a.dim, f"model width {emb.dim} != --dim {a.dim}"
-    X = make_index(a.rows, a.dim, dev, seed=100 + rank)
+    tmp = tempfile.mkdtemp(prefix="lzbench_")
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, device=dev, db_dir=tmp,
+                      load_from_disk=False, enable_async=False, max_buffer_size=2 * a.rows,
+                      user_id=f"tenant{rank}")
+    t_load = time.perf_counter()
+    populate(ms, a.rows, a.dim, dev, seed=100 + rank)
+    torch.cuda.synchronize()
+    t_load = time.perf_counter() - t_load
+    g = ms.graph
     pool = [synth_texts(a.batch, rng) for _ in range(4)]
 
-    def tokenize(i):
-        return emb.tok.encode_batch(pool[i % len(pool)], emb.max_len)
+    def batches(n, start=0):
+        return (pool[(start + i) % len(pool)] for i in range(n))
 
-    # host tokenization of batch i+1 overlaps the device work of batch i
-    # (serving-style pipelining; the tokenizer still runs inside the timed loop).
-    # It runs after batch i's search is enqueued: in the embed's shadow (~5 ms)
-    # it sometimes finished late and the search started up to 1.7 ms after the
-    # embed (rocprofv3 trace, profiles/r1_bench_rocprof_v4); the search gives it ~12 ms.
-    pending = {}
-
-    def step(i):
-        ids, lens = pending.pop(i) if i in pending else tokenize(i)
-        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts, first_frac=frac)
-        s, r = flat_topk(X, q16, a.k)
-        if world > 1:
-            out_r = torch.empty((world * r.shape[0], a.k), dtype=r.dtype, device=dev)
-            out_s = torch.empty((world * s.shape[0], a.k), dtype=s.dtype, device=dev)
-            dist.all_gather_into_tensor(out_r, r)
-            dist.all_gather_into_tensor(out_s, s)
-        pending[i + 1] = tokenize(i + 1)
-        return q16, s, r
-
-    for i in range(a.warmup):
-        step(i)
-    pending.clear()
+    for _ in ms.search_memories_stream(batches(a.warmup), limit=a.k):
+        pass
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
+    n_res = 0
+    for res in ms.search_memories_stream(batches(a.steps), limit=a.k):
+        n_res += len(res)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    assert n_res == a.steps * a.batch
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-
-    # ---- untimed: component breakdown + recall@10 vs exact fp32 scan ----
-    texts = pool[0]
-    ids, lens = emb.tok.encode_batch(texts, emb.max_len)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(3):
-        _, q16 = emb.encoder.forward_streams(ids, lens, pad_to=a.dim, parts=parts, first_frac=frac)
-    torch.cuda.synchronize()
-    t_embed = (time.perf_counter() - t1) / 3
-    t1 = time.perf_counter()
-    for _ in range(3):
-        s, r = flat_topk(X, q16, a.k)
-    torch.cuda.synchronize()
-    t_search = (time.perf_counter() - t1) / 3
-    nr = min(a.recall_queries, q16.shape[0])
-    _, ei = exact_topk(X, q16[:nr], a.k)
-    hit = sum(len(set(r[j].tolist()) & set(ei[j].tolist())) for j in range(nr))
-    recall = hit / float(nr * a.k)
-    S_tok = int(ids.shape[1])
-    tflops_embed = emb.encoder.flops(int(lens.sum())) / t_embed / 1e12  # real (unpadded) tokens
-    tflops_search = 2.0 * a.rows * a.dim * q16.shape[0] / t_search / 1e12
-
     qps = world * a.batch * a.steps / el
 
-    # ---- second half of the metric: consolidate turns/sec (BASELINE config 4
-    # shape: a --rows-node episodic buffer per GPU, batches of conversations
-    # consolidated on device, all-to-all routing + cross-shard dedupe/links) ----
+    # ---- untimed: breakdown + recall vs float64 truth over the fp32 vectors ----
+    def timeit(fn, n=3):
+        fn()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(n):
+            out = fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t1) / n * 1e3, out
+
+    t_embed, Qe = timeit(lambda: emb.batch_embed_tensor(pool[0]))
+    t_store, (_, rows_e) = timeit(lambda: g.store_search(Qe, a.k, "l2"))
+    Xb, bias = g.emb16[: g.n], g.store_bias("l2")
+    q16 = g._q16(Qe)
+    t_kernel, _ = timeit(lambda: flat_topk(Xb, q16, 16, bias=bias, alpha=2.0))
+    t_batch, res0 = timeit(lambda: ms.search_memories_batch(pool[0], limit=a.k))
+    nr = min(a.recall_queries, a.batch)
+    _, truth_e = exact_l2_topk(g, Qe[:nr], a.k)
+    api_rows = [[n._r for n in r] for r in res0[:nr]]
+    rec_api = recall(api_rows, truth_e)
+    gen = torch.Generator(device=dev).manual_seed(999 + rank)
+    Qr = torch.randn((nr, a.dim), device=dev, generator=gen)
+    Qr /= Qr.norm(dim=1, keepdim=True)
+    _, rows_r = g.store_search(Qr, a.k, "l2")
+    _, truth_r = exact_l2_topk(g, Qr, a.k)
+    rec_rand = recall(rows_r.cpu().tolist(), truth_r)
+    S_tok = int(emb.tok.encode_batch(pool[0], emb.max_len)[0].shape[1])
+    lens = emb.tok.encode_batch(pool[0], emb.max_len)[1]
+
+    # ---- second half of the metric: consolidate turns/sec ----
     consolidate = None
     if a.consolidate_steps > 0:
-        del X
+        ms.close()
+        del ms, g, Xb, bias, q16, Qe
         torch.cuda.empty_cache()
-        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
         from lazzaro_amd.parallel import Communicator
         comm = Communicator() if world > 1 else Communicator.local(dev)
@@ -201,14 +235,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (random unit-vector index, synthetic query texts, random-init encoder weights)",
-        "config": {"model": "bge-base-en (d=768) on-device embed + flat top-%d over %d x %d per GPU" % (a.k, a.rows, a.dim),
+        "data": "synthetic (random unit fp32 memory vectors, synthetic query texts, random-init encoder weights)",
+        "config": {"model": "bge-base-en (d=768) on-device embed + MemorySystem.search_memories top-%d over a "
+                            "%d x %d fp32 tenant per GPU (L2, fp32 re-rank)" % (a.k, a.rows, a.dim),
                    "global_batch": world * a.batch, "seq_len": S_tok, "parallelism": "tenant-dp%d" % world},
-        "recall_at_10": round(recall, 4),
-        "breakdown_ms": {"embed": round(t_embed * 1e3, 3), "search": round(t_search * 1e3, 3)},
-        "tokens_per_query": {"padded": S_tok, "real_mean": round(float(lens.float().mean()), 2),
-                             "encoder_layout": "packed varlen (padding never computed)"},
-        "tflops": {"embed": round(tflops_embed, 1), "search": round(tflops_search, 1)},
+        "path": "MemorySystem.search_memories_stream (pipelined search_memories_batch)",
+        "recall_at_10": round(rec_api, 4),
+        "recall_at_10_random_queries": round(rec_rand, 4),
+        "recall_truth": "float64 exact L2 over the stored fp32 vectors",
+        "breakdown_ms": {"embed": round(t_embed, 3), "store_search": round(t_store, 3),
+                         "raw_scan_kernel": round(t_kernel, 3), "search_memories_batch_unpipelined": round(t_batch, 3)},
+        "tokens_per_query": {"padded": S_tok, "real_mean": round(float(lens.float().mean()), 2)},
+        "load_s": round(t_load, 1),
     }
     if consolidate is not None:
         res["consolidate_turns_per_s"] = consolidate["turns_per_s"]

@@ -33,6 +33,18 @@ __device__ __forceinline__ int block_ballot_count(int f, int* wsum) {
   return s;
 }
 
+// Salience decay towards the floor, rounded op by op exactly like the CPU
+// path (an fma contraction would differ in the last ulp).
+__device__ __forceinline__ float decay_sal(float s, float keep) {
+#pragma clang fp contract(off)
+  return s > SAL_FLOOR ? SAL_FLOOR + (s - SAL_FLOOR) * keep : SAL_FLOOR;
+}
+
+// Salience bump min(1, s + delta) in double precision, then stored as fp32:
+// the reference adds Python floats (memory_system.py:242-260,
+// buffer_graph.py:79-85), so this rounds exactly once like the CPU path.
+__device__ __forceinline__ float bump_sal(float s, double delta) { return (float)fmin(1.0, (double)s + delta); }
+
 // Edge pass: w *= keep (keep == 1 -> no decay); flag survivors w >= thr
 // (flag == nullptr -> no prune). Node pass (same launch, grid-stride): the
 // salience of shard nodes (kind 1, not super) decays towards the floor.
@@ -60,7 +72,7 @@ __global__ __launch_bounds__(NTB) void tg_decay_kernel(float* __restrict__ w, lo
     for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
       if (kind[i] != 1 || sup[i]) continue;
       const float s = sal[i];
-      sal[i] = s > SAL_FLOOR ? SAL_FLOOR + (s - SAL_FLOOR) * keep : SAL_FLOOR;
+      sal[i] = decay_sal(s, keep);
     }
   }
 }
@@ -71,7 +83,7 @@ __global__ __launch_bounds__(NTB) void tg_node_decay_kernel(float* __restrict__ 
   for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
     if (kind[i] != 1 || sup[i]) continue;
     const float s = sal[i];
-    sal[i] = s > SAL_FLOOR ? SAL_FLOOR + (s - SAL_FLOOR) * keep : SAL_FLOOR;
+    sal[i] = decay_sal(s, keep);
   }
 }
 
@@ -138,7 +150,7 @@ __global__ __launch_bounds__(64) void tg_boost_kernel(const long* __restrict__ o
                                                       const int* __restrict__ seeds, int nseeds,
                                                       const unsigned char* __restrict__ kind,
                                                       const unsigned char* __restrict__ sup, float min_w, double now,
-                                                      float delta, float* __restrict__ sal, double* __restrict__ last,
+                                                      double delta, float* __restrict__ sal, double* __restrict__ last,
                                                       unsigned char* __restrict__ dirty, int* __restrict__ stamp,
                                                       int epoch, int* __restrict__ nboost) {
   const int s = seeds[blockIdx.x];
@@ -151,7 +163,7 @@ __global__ __launch_bounds__(64) void tg_boost_kernel(const long* __restrict__ o
     for (int j = 0; j < nseeds; ++j) is_seed |= (seeds[j] == nb);
     if (is_seed) continue;
     if (atomicExch(&stamp[nb], epoch) != epoch) {
-      sal[nb] = fminf(1.f, sal[nb] + delta);
+      sal[nb] = bump_sal(sal[nb], delta);
       last[nb] = now;
       dirty[nb] = 1;
       atomicAdd(nboost, 1);
@@ -162,14 +174,14 @@ __global__ __launch_bounds__(64) void tg_boost_kernel(const long* __restrict__ o
 // Retrieval access update (BufferGraph.update_access) for a few rows.
 __global__ __launch_bounds__(64) void tg_touch_kernel(const long* __restrict__ rows, int n, int* __restrict__ acc,
                                                       double* __restrict__ last, float* __restrict__ sal,
-                                                      unsigned char* __restrict__ dirty, double now, float delta) {
+                                                      unsigned char* __restrict__ dirty, double now, double delta) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
   const long r = rows[i];
   LZK_DCHECK(r >= 0);
   acc[r] += 1;
   last[r] = now;
-  sal[r] = fminf(1.f, sal[r] + delta);
+  sal[r] = bump_sal(sal[r], delta);
   dirty[r] = 1;
 }
 
@@ -181,6 +193,7 @@ __global__ __launch_bounds__(NTB) void tg_importance_kernel(const float* __restr
                                                             const unsigned char* __restrict__ kind,
                                                             const unsigned char* __restrict__ sup, long n, double now,
                                                             double* __restrict__ out) {
+#pragma clang fp contract(off)
   const long i = (long)blockIdx.x * NTB + threadIdx.x;
   if (i >= n) return;
   if (kind[i] != 1 || sup[i]) {
@@ -234,7 +247,7 @@ LZK_EXPORT int lzk_tg_compact(const unsigned char* flag, const int* block_off, l
 
 LZK_EXPORT int lzk_tg_boost(const long* off, const int* adj, const int* eid, const float* w, const int* seeds,
                             int nseeds, const unsigned char* kind, const unsigned char* sup, float min_w, double now,
-                            float delta, float* sal, double* last, unsigned char* dirty, int* stamp, int epoch,
+                            double delta, float* sal, double* last, unsigned char* dirty, int* stamp, int epoch,
                             int* nboost, void* stream) {
   if (nseeds <= 0) return 0;
   hipLaunchKernelGGL(tg_boost_kernel, dim3(nseeds), dim3(64), 0, (hipStream_t)stream, off, adj, eid, w, seeds, nseeds,
@@ -243,7 +256,7 @@ LZK_EXPORT int lzk_tg_boost(const long* off, const int* adj, const int* eid, con
 }
 
 LZK_EXPORT int lzk_tg_touch(const long* rows, int n, int* acc, double* last, float* sal, unsigned char* dirty,
-                            double now, float delta, void* stream) {
+                            double now, double delta, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(tg_touch_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, rows, n, acc,
                      last, sal, dirty, now, delta);

@@ -99,6 +99,13 @@ class OnDeviceEmbedder:
         (no host round trip: the memory graph ingests / searches with it)."""
         if any(len(t) > 4 * self.max_len for t in texts):
             return torch.as_tensor(np.asarray(self.batch_embed(texts), dtype=np.float32)).to(self.device)
+        if self.device.type == "cuda":
+            # the GPU forward packs tokens (padding is never computed), so no
+            # length sort / scatter: input order, and nothing here waits for
+            # the device (host inputs go through pinned async copies)
+            outs = [self.embed_tensor(texts[s: s + self.max_batch])[0] for s in range(0, len(texts), self.max_batch)]
+            out = outs[0] if len(outs) == 1 else torch.cat(outs)
+            return out if out.dtype == torch.float32 else out.float()
         order = sorted(range(len(texts)), key=lambda i: len(texts[i]))
         out = torch.empty((len(texts), self.dim), dtype=torch.float32, device=self.device)
         for s in range(0, len(order), self.max_batch):

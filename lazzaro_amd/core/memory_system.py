@@ -35,7 +35,7 @@ import re
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from typing import Dict, List, Optional
+from typing import Dict, Iterable, List, Optional
 
 import numpy as np
 import torch
@@ -541,17 +541,63 @@ class MemorySystem(ConsolidationMixin):
             return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
 
     def search_memories_batch(self, queries: List[str], limit: int = 5) -> List[List[Node]]:
-        """Batched ``search_memories``: one embedding call (device tensor when
-        the encoder is on-device), one fused top-k launch, one id mapping."""
+        """Batched ``search_memories`` (reference :1460-1472 per query): one
+        embedding call (a device tensor when the encoder is on-device), one
+        store search -- the fused MFMA candidate scan plus an fp32 re-rank
+        over the tenant's HBM rows -- and one row -> Node mapping."""
+        return self._search_finish(self._search_submit(queries, limit))
+
+    def search_memories_stream(self, batches: Iterable[List[str]], limit: int = 5):
+        """Pipelined ``search_memories_batch`` for serving loops: batch i+1 is
+        tokenised and its embed + scan enqueued on the device BEFORE the host
+        waits for batch i and maps its rows to Nodes, so host work (tokenizer,
+        result mapping) hides under device work. Yields one result list per
+        input batch, in order; results equal ``search_memories_batch``."""
+        pending = None
+        for qs in batches:
+            h = self._search_submit(qs, limit)
+            if pending is not None:
+                yield self._search_finish(pending)
+            pending = h
+        if pending is not None:
+            yield self._search_finish(pending)
+
+    def _search_submit(self, queries, limit: int):
+        """Enqueue embed + store search; returns a handle for _search_finish.
+        With the graph-bound store the result rows stay on the device and come
+        back with one async copy into pinned memory (no host sync here)."""
+        queries = list(queries)
         with tracer.stage("embed_query", self._device):
-            embs = self._batch_embed_any(list(queries))
+            embs = self._batch_embed_any(queries)
+        with self._graph_lock:
+            g = self.graph
+            if (torch.is_tensor(embs) and self._store_binds_graph() and g.dim is not None
+                    and embs.shape[-1] == g.dim and len(queries)):
+                with tracer.stage("search", self._device):
+                    _, rows = g.store_search(embs, int(limit), getattr(self.store, "metric", "l2"))
+                if rows.is_cuda:
+                    host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
+                    host.copy_(rows, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    return ("rows", g, host, ev)
+                return ("rows", g, rows, None)
         with tracer.stage("search", self._device):
-            res = self._search_batch(embs, limit)
+            return ("ids", None, self._search_batch(embs, limit), None)
+
+    def _search_finish(self, h) -> List[List[Node]]:
+        kind_, g0, data, ev = h
+        if ev is not None:
+            ev.synchronize()
         with self._graph_lock:
             g = self.graph
             kind = g.mirror("kind")
+            if kind_ == "rows" and g is g0:
+                return [[NodeView.of(g, r) for r in row if r >= 0 and kind[r] == NODE] for row in data.tolist()]
+            if kind_ == "rows":  # the tenant was switched while the search ran
+                data = [[g0.ids[r] for r in row if r >= 0] for row in data.tolist()]
             out = []
-            for ids in res:
+            for ids in data:
                 rows = [g.row_of.get(i, -1) for i in ids]
                 out.append([NodeView.of(g, r) for r in rows if r >= 0 and kind[r] == NODE])
             return out

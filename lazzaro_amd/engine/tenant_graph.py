@@ -274,31 +274,43 @@ class TenantGraph:
         m = len(ids)
         dev = self.device
         e32, info = self._as_emb(emb, m)
-        rows = [self.row_of.get(i, -1) for i in ids]
-        fresh = sum(1 for r in rows if r < 0)
-        self.reserve(self.n + fresh)
-        kind_h = self.mirror("kind") if fresh < m else None
-        r_next = self.n
-        rl = []
         tlist = types if (types is not None and not isinstance(types, str)) else None
         tdef = types if isinstance(types, str) else "semantic"
-        for j, (i, r) in enumerate(zip(ids, rows)):
-            t = tlist[j] if tlist is not None else tdef
-            if r < 0:
-                r = r_next
-                r_next += 1
-                self.ids.append(i)
-                self.content.append(contents[j])
-                self.types.append(t)
-                self.row_of[i] = r
-            else:
-                if kind_h is not None and r < len(kind_h) and kind_h[r] == NODE:
-                    self._unlink_row(r)
-                self.content[r] = contents[j]
-                self.types[r] = t
-            rl.append(r)
-        self.n = r_next
-        rt = torch.as_tensor(rl, dtype=torch.long).to(dev)
+        n0 = self.n
+        if len(set(ids)) == m and self.row_of.keys().isdisjoint(ids):
+            # bulk append of fresh ids (loads, large ingests): no per-row loop
+            self.reserve(n0 + m)
+            self.ids.extend(ids)
+            self.content.extend(contents)
+            self.types.extend(tlist if tlist is not None else [tdef] * m)
+            self.row_of.update(zip(ids, range(n0, n0 + m)))
+            self.n = n0 + m
+            rl = range(n0, n0 + m)
+            rt = torch.arange(n0, n0 + m, dtype=torch.long, device=dev)
+        else:
+            rows = [self.row_of.get(i, -1) for i in ids]
+            fresh = sum(1 for r in rows if r < 0)
+            self.reserve(self.n + fresh)
+            kind_h = self.mirror("kind") if fresh < m else None
+            r_next = self.n
+            rl = []
+            for j, (i, r) in enumerate(zip(ids, rows)):
+                t = tlist[j] if tlist is not None else tdef
+                if r < 0:
+                    r = r_next
+                    r_next += 1
+                    self.ids.append(i)
+                    self.content.append(contents[j])
+                    self.types.append(t)
+                    self.row_of[i] = r
+                else:
+                    if kind_h is not None and r < len(kind_h) and kind_h[r] == NODE:
+                        self._unlink_row(r)
+                    self.content[r] = contents[j]
+                    self.types[r] = t
+                rl.append(r)
+            self.n = r_next
+            rt = torch.as_tensor(rl, dtype=torch.long).to(dev)
 
         def col(v, dt, default):
             if v is None:

@@ -23,8 +23,8 @@ D_ = C.c_double
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
-_lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, F, P, P, P, P, I, P, P])
-_lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, F, P])
+_lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
+_lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 

@@ -196,6 +196,7 @@ def test_large_tenant_kernel_path_matches_exact_cpu(tmp_path, monkeypatch):
     X, lab = _clustered(N + M, D, 64, 11)
     out = {}
     for dev in ("cpu", DEV):
+        monkeypatch.setattr(time, "time", _Clock())  # same clock readings for both devices
         ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
                           db_dir=str(tmp_path / dev), device=dev, load_from_disk=False, max_buffer_size=N + 64,
                           super_node_threshold=10 ** 9)
@@ -236,7 +237,7 @@ def test_store_search_fp32_exact_recall_gpu():
     gen = torch.Generator().manual_seed(3)
     X = torch.randn(N, D, generator=gen)
     X = X / X.norm(dim=1, keepdim=True)
-    g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=0, stored=True)
+    g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
     Q = torch.randn(512, D, generator=gen)
     Q = Q / Q.norm(dim=1, keepdim=True)
     _, rows = g.store_search(Q.to(DEV), 10, "l2")
@@ -245,3 +246,25 @@ def test_store_search_fp32_exact_recall_gpu():
     truth = torch.topk(-d2, 10, dim=1).indices
     hit = sum(len(set(a) & set(b)) for a, b in zip(rows.cpu().tolist(), truth.cpu().tolist()))
     assert hit / (512 * 10) == 1.0
+
+
+def test_search_memories_stream_matches_batch_gpu(tmp_path):
+    """Pipelined search_memories_stream == search_memories_batch per batch on
+    a 200k-memory tenant (device rows -> pinned async copy -> Node views)."""
+    from lazzaro_amd.core.embedders import OnDeviceEmbedder
+
+    emb = OnDeviceEmbedder("minilm-l6", device=DEV, max_len=32)
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, enable_async=False,
+                      db_dir=str(tmp_path), device=DEV, load_from_disk=False, max_buffer_size=10 ** 7)
+    g = ms.graph
+    N = 200_000
+    gen = torch.Generator().manual_seed(5)
+    X = torch.randn(N, emb.dim, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"m{i}" for i in range(N)], X, shard=g.shard_id("work"),
+                stored=True)
+    batches = [[f"query {b} {j} about project deadline" for j in range(300)] for b in range(3)]
+    want = [[[n.id for n in r] for r in ms.search_memories_batch(qs, limit=10)] for qs in batches]
+    got = [[[n.id for n in r] for r in res] for res in ms.search_memories_stream(batches, limit=10)]
+    assert got == want and all(len(r) == 10 for b in got for r in b)
+    ms.close()

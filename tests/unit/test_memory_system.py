@@ -262,3 +262,20 @@ def test_concurrent_chat_and_background_consolidation():
     assert not errors, errors
     assert ms.consolidation_queue == [] and ms.buffer.size()[0] >= 12
     ms.close()
+
+
+def test_search_memories_stream_matches_batch(tmp_path):
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=32), enable_async=False,
+                      db_dir=str(tmp_path), load_from_disk=False, max_buffer_size=10 ** 6)
+    g = ms.graph
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((500, 32)).astype(np.float32)
+    g.add_nodes([f"node_{i + 1}" for i in range(500)], [f"m{i}" for i in range(500)], X.tolist(),
+                shard=g.shard_id("work"), stored=True)
+    batches = [[f"q {b} {j}" for j in range(7)] for b in range(4)]
+    want = [[[n.id for n in r] for r in ms.search_memories_batch(qs, limit=5)] for qs in batches]
+    got = [[[n.id for n in r] for r in res] for res in ms.search_memories_stream(batches, limit=5)]
+    assert got == want and all(len(r) == 5 for b in got for r in b)
+    assert [[n.id for n in ms.search_memories(q, limit=5)] for q in batches[0]] == want[0]
+    ms.close()
