@@ -898,6 +898,39 @@ STORAGE:
         self._say(f"👤 Switched context to user: {new_user_id}")
 
     # ------------------------------------------------------------ export
+    def graph_json(self) -> Dict:
+        """The dashboard's ``/api/graph`` payload (reference dashboard/api.py:
+        71-112: shard nodes and each shard's edges in shard order, then the
+        super-nodes under shard "global"), built from the graph columns in one
+        pass under the graph lock (a background consolidation may be writing)."""
+        with self._graph_lock:
+            g = self.graph
+            rows = g.ordered_node_rows()
+            sup, sh = g.mirror("sup"), g.mirror("shard")
+            sal, acc = g.mirror("sal"), g.mirror("acc")
+            nodes, supers = [], []
+            names, ids, content, types = g.shard_names, g.ids, g.content, g.types
+            for r in rows.tolist():
+                if sup[r]:
+                    supers.append({"id": ids[r], "content": content[r], "type": "super_node",
+                                   "salience": float(sal[r]), "shard": "global", "is_super_node": True})
+                else:
+                    nodes.append({"id": ids[r], "content": content[r], "type": types[r], "salience": float(sal[r]),
+                                  "shard": names[sh[r]], "access_count": int(acc[r]), "is_super_node": False})
+            links = []
+            if g.num_edges:
+                with g.on_stream():
+                    meta = g.e["meta"].cpu().numpy()
+                    s, d, w = g.e["src"].cpu().numpy(), g.e["dst"].cpu().numpy(), g.e["w"].cpu().numpy()
+                es = meta & 0xFFFFFF
+                live = np.asarray(g.shard_live, dtype=bool)[es]
+                order = np.argsort(es, kind="stable")
+                order = order[live[order]]
+                et = g.etype_names
+                links = [{"source": ids[s[i]], "target": ids[d[i]], "weight": float(w[i]),
+                          "type": et[(meta[i] >> 24) & 0x3F]} for i in order.tolist()]
+            return {"nodes": nodes + supers, "links": links}
+
     def export_observations(self, format: str = "markdown") -> str:
         with self._graph_lock:
             return self._export(format)

@@ -77,17 +77,7 @@ async def get_graph():
     if not _ms:
         return {"nodes": [], "links": []}
     _ms.check_for_updates()
-    nodes, links = [], []
-    for key, sh in _ms.shards.items():
-        for nid, n in sh.nodes.items():
-            nodes.append({"id": nid, "content": n.content, "type": n.type, "salience": n.salience, "shard": key,
-                          "access_count": n.access_count, "is_super_node": n.is_super_node})
-        for (s, t), e in sh.edges.items():
-            links.append({"source": s, "target": t, "weight": e.weight, "type": e.edge_type})
-    for nid, n in _ms.super_nodes.items():
-        nodes.append({"id": nid, "content": n.content, "type": "super_node", "salience": n.salience,
-                      "shard": "global", "is_super_node": True})
-    return {"nodes": nodes, "links": links}
+    return _ms.graph_json()
 
 
 @app.get("/api/profile")
@@ -95,7 +85,8 @@ async def get_profile():
     if not _ms:
         return {}
     _ms.check_for_updates()
-    return _ms.profile.to_dict()
+    with _ms._graph_lock:
+        return _ms.profile.to_dict()
 
 
 @app.post("/api/consolidate")

@@ -3,18 +3,22 @@
 langchain_integration.py:32-51, autogen_integration.py:40-56)."""
 from __future__ import annotations
 
+from contextlib import nullcontext
 from typing import List, Tuple
 
 from ..core.profile import EMPTY_CONTEXT
 
 
 def retrieve(ms, query: str) -> Tuple[str, List[str]]:
-    """(profile context or "", retrieved memory contents) for ``query``."""
+    """(profile context or "", retrieved memory contents) for ``query``.
+    The graph read runs under the MemorySystem's graph lock: a background
+    consolidation may be writing the same tenant graph."""
     q = ms._get_embedding(query)
-    ids = ms._optimized_retrieval(q, query)
-    prof = ms.profile.get_context()
+    with getattr(ms, "_graph_lock", None) or nullcontext():
+        ids = ms._optimized_retrieval(q, query)
+        prof = ms.profile.get_context()
+        texts = [n.content for n in (ms.buffer.get_node(i) for i in ids) if n is not None]
     prof = prof if prof and prof != EMPTY_CONTEXT else ""
-    texts = [n.content for n in (ms.buffer.get_node(i) for i in ids) if n is not None]
     return prof, texts
 
 

@@ -134,3 +134,61 @@ def test_adk_plugin():
     empty = _ms(db_dir="other")
     assert LazzaroADKPlugin(empty).retrieve("x") == "No relevant memories found."
     ms.close()
+
+
+def _graph_via_views(ms):
+    """The reference's /api/graph construction over the shard/super-node façades."""
+    nodes, links = [], []
+    for key, sh in ms.shards.items():
+        for nid, n in sh.nodes.items():
+            nodes.append({"id": nid, "content": n.content, "type": n.type, "salience": n.salience, "shard": key,
+                          "access_count": n.access_count, "is_super_node": n.is_super_node})
+        for (s, t), e in sh.edges.items():
+            links.append({"source": s, "target": t, "weight": e.weight, "type": e.edge_type})
+    for nid, n in ms.super_nodes.items():
+        nodes.append({"id": nid, "content": n.content, "type": "super_node", "salience": n.salience,
+                      "shard": "global", "is_super_node": True})
+    return {"nodes": nodes, "links": links}
+
+
+def test_graph_json_matches_views_and_dashboard_polls_during_async_consolidation():
+    import threading
+
+    from lazzaro_amd.dashboard import api
+    ms = _ms(super_node_threshold=2, max_buffer_size=200)
+    for i in range(4):
+        _seed(ms)
+        ms.start_conversation()
+        ms.chat(f"My project number {i} has a deadline with client {i}. I read book {i} for my course.")
+        ms.end_conversation()
+    assert ms.graph_json() == _graph_via_views(ms) and ms.graph_json()["links"]
+    ms.close()
+    # the dashboard reads while the background worker consolidates
+    ms = _ms(enable_async=True, super_node_threshold=2, max_buffer_size=200)
+    api.set_memory_system(ms)
+    c = TestClient(api.app)
+    errors, stop = [], threading.Event()
+
+    def poll():
+        try:
+            while not stop.is_set():
+                for route in ("/api/graph", "/api/profile", "/api/stats", "/api/export"):
+                    assert c.get(route).status_code == 200
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    t = threading.Thread(target=poll)
+    t.start()
+    for i in range(6):
+        ms.start_conversation()
+        ms.chat(f"I work on project {i} with a colleague and exercise at the gym {i} times a week.")
+        ms.chat(f"My family visits home in summer {i} and I study a course on kernels.")
+        ms.end_conversation()
+    ms.flush()
+    stop.set()
+    t.join()
+    assert not errors, errors
+    g = c.get("/api/graph").json()
+    assert len(g["nodes"]) == ms.get_stats()["buffer_nodes"]
+    api.set_memory_system(None)
+    ms.close()
