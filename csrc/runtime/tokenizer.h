@@ -1,8 +1,11 @@
-// BERT-style tokenizer (host runtime): basic tokenization (lower-case,
-// whitespace + punctuation split) then WordPiece greedy longest-match against a
-// vocab.txt when one is loaded; without a vocab (no weights ship offline) each
-// word maps to a deterministic hashed id in [1000, vocab_size). Output follows
-// the BERT convention [CLS] ... [SEP] with [PAD]=0, [UNK]=100, [CLS]=101, [SEP]=102.
+// BERT-style tokenizer (host runtime): the BERT basic tokenizer on UTF-8 code
+// points (clean text, isolate CJK ideographs, strip accents + lower-case for
+// uncased models, split on whitespace and Unicode punctuation; tables in
+// unicode_tables.h) then WordPiece greedy longest-match against a vocab.txt
+// when one is loaded; without a vocab (no weights ship offline) each word maps
+// to a deterministic hashed id in [1000, vocab_size). Output: [CLS] ... [SEP];
+// special ids come from the vocab ([PAD]=0, [UNK]=100, [CLS]=101, [SEP]=102
+// without one).
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -29,6 +32,7 @@ class Tokenizer {
   int vocab_size_;
   bool lower_;
   std::unordered_map<std::string, int32_t> vocab_;
+  int32_t pad_ = 0, unk_ = 100, cls_ = 101, sep_ = 102;
   void basic_split(const std::string& text, std::vector<std::string>& out) const;
   void wordpiece(const std::string& w, std::vector<int32_t>& out) const;
 };

@@ -67,6 +67,7 @@ LINK_WEIGHT_SCALE = 0.8
 CHAIN_WEIGHT = 0.5
 MIN_FACT_LEN = 5
 DECAY_RATE = 0.01
+PROFILE_CONTENTS = 10  # contents per profile prompt (reference memory_system.py:1032)
 
 
 def _parse_json(response: str):
@@ -480,21 +481,13 @@ class ConsolidationMixin:
                 if merged > 0:
                     results.append(f"✓ Merged {merged} similar nodes")
             with tracer.stage("components", self._device):
-                comps = g.components()
-                wsum, wcnt = g.component_edge_stats(comps)
-            contents = []
-            sup = g.mirror("sup")
-            kind = g.mirror("kind")
-            for i, comp in enumerate(comps):
-                if comp.size < 3 or not wcnt[i] or not wsum[i] / wcnt[i] > 0.3:
-                    contents.append(None)
-                    continue
-                contents.append([g.content[r] for r in comp.tolist() if kind[r] == NODE and not sup[r]])
+                # components with >= 3 members and mean edge weight > 0.3
+                # (reference :967-990), as their first 10 shard-node rows
+                digest = g.component_digest(3, 0.3, PROFILE_CONTENTS)
+            contents = [[g.content[r] for r in rows.tolist()] for rows in digest]
         updates = 0
         for cs in contents:
-            if cs is None:
-                continue
-            r = self._extract_profile_from_contents(cs) if cs else "No content to extract"
+            r = self._extract_profile_from_contents(cs)
             if "Updated" in r:
                 updates += 1
                 results.append(r)
@@ -507,8 +500,8 @@ class ConsolidationMixin:
         else:
             with self._graph_lock:
                 rows = g.ordered_node_rows()
-                sup = g.mirror("sup")
-                contents = [g.content[r] for r in rows if not sup[r]]
+                rows = rows[g.mirror("sup")[rows] == 0]
+                contents = [g.content[r] for r in rows[:PROFILE_CONTENTS].tolist()]
             if len(contents) >= 3:
                 r = self._extract_profile_from_contents(contents)
                 if "Updated" in r:
@@ -530,7 +523,7 @@ class ConsolidationMixin:
     def _extract_profile_from_contents(self, contents: List[str]) -> str:
         if not contents:
             return "No content to extract"
-        prompt = "Related memories:\n" + "\n".join(f"- {c}" for c in contents[:10])
+        prompt = "Related memories:\n" + "\n".join(f"- {c}" for c in contents[:PROFILE_CONTENTS])
         response = self._call_llm([{"role": "system", "content": PROFILE_PROMPT},
                                    {"role": "user", "content": prompt}],
                                   response_format={"type": "json_object"})

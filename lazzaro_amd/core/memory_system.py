@@ -131,6 +131,10 @@ class MemorySystem(ConsolidationMixin):
         self.vector_store = self.store
         dev = device if device is not None else getattr(self.store, "device", None)
         self._device = torch.device(dev) if dev is not None else torch.device("cpu")
+        # one lock serialises every reader and writer of the tenant graph --
+        # the caller, the background consolidation worker and the store's
+        # search over the bound graph (TenantGraph.lock is this lock)
+        self._graph_lock = threading.RLock()
         self.graph = self._new_graph()
 
         self.enable_sharding = enable_sharding
@@ -157,7 +161,6 @@ class MemorySystem(ConsolidationMixin):
         self.background_executor = ThreadPoolExecutor(max_workers=1) if enable_async else None
         self._pending = []
         self._queue_lock = threading.Lock()
-        self._graph_lock = threading.RLock()
 
         self.conversation_active = False
         self.short_term_memory: List[Dict] = []
@@ -189,6 +192,7 @@ class MemorySystem(ConsolidationMixin):
     # ------------------------------------------------------------ graph + views
     def _new_graph(self) -> TenantGraph:
         g = TenantGraph(device=self._device)
+        g.lock = self._graph_lock
         attach = getattr(self.store, "attach", None)
         if attach is not None:
             attach(self.user_id, g)
@@ -535,9 +539,9 @@ class MemorySystem(ConsolidationMixin):
     def search_memories(self, query: str, limit: int = 5) -> List[Node]:
         with tracer.stage("embed_query", self._device):
             q = self._get_embedding(query)
-        with tracer.stage("search", self._device):
-            ids = self.vector_store.search_nodes(q, user_id=self.user_id, limit=limit)
         with self._graph_lock:
+            with tracer.stage("search", self._device):
+                ids = self.vector_store.search_nodes(q, user_id=self.user_id, limit=limit)
             return [n for n in (self.buffer.get_node(i) for i in ids) if n is not None]
 
     def search_memories_batch(self, queries: List[str], limit: int = 5) -> List[List[Node]]:

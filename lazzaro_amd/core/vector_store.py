@@ -247,9 +247,10 @@ class HBMStore:
         if g is not None:
             q = query_emb if torch.is_tensor(query_emb) else torch.from_numpy(
                 np.asarray(query_emb, dtype=np.float32))
-            if g.dim is None or q.shape[-1] != g.dim:
-                return []
-            return g.search_ids(q, int(limit), self.metric)[0]
+            with g.lock:  # the tenant's graph lock: a consolidation may be writing
+                if g.dim is None or q.shape[-1] != g.dim:
+                    return []
+                return g.search_ids(q, int(limit), self.metric)[0]
         with self._lock:  # writers (add/delete/replace) mutate the arena in place
             a = self._arena(user_id)
             if len(a) == 0 or a.dim != len(query_emb):
@@ -265,9 +266,10 @@ class HBMStore:
                 np.asarray(query_embs, dtype=np.float32))
             if len(Q) == 0:
                 return []
-            if g.dim is None or Q.shape[-1] != g.dim:
-                return [[] for _ in range(len(Q))]
-            return g.search_ids(Q, int(limit), self.metric)
+            with g.lock:
+                if g.dim is None or Q.shape[-1] != g.dim:
+                    return [[] for _ in range(len(Q))]
+                return g.search_ids(Q, int(limit), self.metric)
         with self._lock:
             a = self._arena(user_id)
             if len(a) == 0 or len(query_embs) == 0:

@@ -808,6 +808,57 @@ class TenantGraph:
         keyed.sort(key=lambda x: x[0])
         return [g for _, g in keyed]
 
+    def component_digest(self, min_size: int = 3, min_avg_w: float = 0.3, take: int = 10) -> List[np.ndarray]:
+        """``run_consolidation``'s view of the components (reference
+        memory_system.py:967-990) without materialising them: components
+        with >= ``min_size`` members whose mean edge weight exceeds
+        ``min_avg_w``, in the order of :meth:`components`, each as the first
+        ``take`` of its live shard-node rows (row order) -- the only rows the
+        profile prompt reads (:1032). Components with none are left out.
+        Labels, sizes, weight sums and the ordering are device reductions;
+        only the <= ``take`` rows per qualifying component reach the host."""
+        n = self.n
+        if n == 0 or self.num_edges == 0:
+            return []
+        dev = self.device
+        with self.on_stream():
+            lab = T.components(self.e["src"], self.e["dst"], n)
+            lab = lab.to(dev).long()
+            src, dst = self.e["src"].long(), self.e["dst"].long()
+            kind = self.kind[:n]
+            touched = torch.zeros(n, dtype=torch.bool, device=dev)
+            touched[src] = True
+            touched[dst] = True
+            member = (kind == NODE) | ((kind == GHOST) & touched)
+            size = torch.bincount(lab[member], minlength=n)
+            el = lab[src]
+            wsum = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, el, self.e["w"].double())
+            wcnt = torch.bincount(el, minlength=n)
+            ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1).double() > min_avg_w)
+            # reference order: a component's first member in BufferGraph.nodes order
+            order = torch.as_tensor(self.ordered_node_rows(), dtype=torch.long).to(dev)
+            BIG = 1 << 62
+            pos = torch.full((n,), BIG, dtype=torch.long, device=dev)
+            pos[order] = torch.arange(order.numel(), device=dev)
+            first = torch.full((n,), BIG, dtype=torch.long, device=dev)
+            first.scatter_reduce_(0, lab, pos, "amin", include_self=True)
+            ok &= first < BIG
+            cand = torch.nonzero(ok[lab] & (kind == NODE) & (self.sup[:n] == 0)).flatten()
+            if cand.numel() == 0:
+                return []
+            key = first[lab[cand]]
+            o = torch.argsort(key * n + cand)  # (component order, row)
+            cand, key = cand[o], key[o]
+            newg = torch.ones_like(key, dtype=torch.bool)
+            newg[1:] = key[1:] != key[:-1]
+            gstart = torch.cummax(torch.where(newg, torch.arange(key.numel(), device=dev), torch.zeros_like(key)),
+                                  0).values
+            rank = torch.arange(key.numel(), device=dev) - gstart
+            sel = rank < take
+            rows_h, key_h = cand[sel].cpu().numpy(), key[sel].cpu().numpy()
+        cut = np.nonzero(np.diff(key_h))[0] + 1
+        return np.split(rows_h, cut)
+
     def component_edge_stats(self, comps: List[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
         """(sum of weights, count) of edges with both endpoints in the same
         component, per component (reference memory_system.py:970-985)."""

@@ -215,6 +215,12 @@ class SentenceEncoder:
         the attention run on sum(lens) tokens instead of B*S -- the padded
         positions never influence the pooled embedding (keys >= len are
         masked, pooling stops at len), so they are pure waste."""
+        x, lens_d, cu, B, S = self._layers(ids, lens, packed)
+        return E.pool_norm(x, lens_d, B, S, self.cfg.pooling, pad_to, cu=cu)
+
+    def _layers(self, ids: torch.Tensor, lens: torch.Tensor, packed: Optional[bool]):
+        """Embedding + every transformer layer. Returns (token states, lens on
+        the device, cu row offsets (packed) or None, B, S)."""
         c, p = self.cfg, self.p
         B, S = ids.shape
         if packed is None:
@@ -242,7 +248,26 @@ class SentenceEncoder:
             x = self._lin_ln(ctx, i, "wo", "bo", x, "ln1", split=self._split_o(x))
             hdn = self._lin(x, i, "w1", "b1", act="gelu")
             x = self._lin_ln(hdn, i, "w2", "b2", x, "ln2", split=self._split_ffn2(x))
-        return E.pool_norm(x, lens, B, S, c.pooling, pad_to, cu=cu)
+        return x, lens, cu, B, S
+
+    def hidden_states(self, ids: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+        """Last-layer token states [B, S, H] fp32 (HF ``last_hidden_state``;
+        rows past each sequence's length are zero) -- for parity checks."""
+        B, S = ids.shape
+        x, lens_d, cu, B, S_eff = self._layers(ids, lens, None)
+        H = self.cfg.hidden
+        out = torch.zeros((B, S, H), dtype=torch.float32, device=x.device)
+        lh = lens.to(torch.int64).cpu().tolist()
+        if cu is not None:
+            off = 0
+            for b, n in enumerate(lh):
+                out[b, :n] = x[off: off + n].float()
+                off += n
+        else:
+            xs = x.view(B, S_eff, H)
+            for b, n in enumerate(lh):
+                out[b, :n] = xs[b, :n].float()
+        return out
 
     def forward_streams(self, ids: torch.Tensor, lens: torch.Tensor, pad_to: int = 0, parts: int = 2,
                         first_frac: float = 0.0):

@@ -279,3 +279,36 @@ def test_search_memories_stream_matches_batch(tmp_path):
     assert got == want and all(len(r) == 5 for b in got for r in b)
     assert [[n.id for n in ms.search_memories(q, limit=5)] for q in batches[0]] == want[0]
     ms.close()
+
+
+def test_component_digest_matches_materialised_components():
+    """run_consolidation's device digest == the per-component reference logic
+    (size >= 3, mean edge weight > 0.3, first 10 live shard-node rows)."""
+    import torch
+
+    from lazzaro_amd.engine.tenant_graph import NODE, TenantGraph
+    rng = np.random.default_rng(3)
+    g = TenantGraph(device="cpu", dim=8)
+    n = 400
+    codes = [g.shard_id(f"s{i}") for i in range(4)]
+    g.add_nodes([f"node_{i}" for i in range(n)], [f"c{i}" for i in range(n)],
+                rng.standard_normal((n, 8)).astype(np.float32).tolist(), shard=[codes[i % 4] for i in range(n)],
+                sup=[1 if i % 97 == 0 else 0 for i in range(n)])
+    ne = 300
+    s = torch.as_tensor(rng.integers(0, n, ne), dtype=torch.int32)
+    d = torch.as_tensor(rng.integers(0, n, ne), dtype=torch.int32)
+    g.append_edges(s, d, torch.as_tensor(rng.uniform(0.1, 1.0, ne), dtype=torch.float32),
+                   torch.as_tensor([codes[int(x) % 4] for x in s], dtype=torch.int32))
+    g.remove_nodes([5, 6, 7, 50])  # ghosts that are still edge endpoints
+    comps = g.components()
+    ws, wc = g.component_edge_stats(comps)
+    kind, sup = g.mirror("kind"), g.mirror("sup")
+    want = []
+    for i, c in enumerate(comps):
+        if c.size < 3 or not wc[i] or not ws[i] / wc[i] > 0.3:
+            continue
+        rows = [r for r in c.tolist() if kind[r] == NODE and not sup[r]][:10]
+        if rows:
+            want.append(rows)
+    got = [r.tolist() for r in g.component_digest(3, 0.3, 10)]
+    assert got == want and len(want) > 3
