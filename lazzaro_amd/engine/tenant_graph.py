@@ -80,6 +80,28 @@ def _pad64(d: int) -> int:
     return (d + 63) // 64 * 64
 
 
+def _seg_sum_count(keys: torch.Tensor, vals: torch.Tensor, n: int):
+    """(sum of ``vals`` per key, count per key) for keys in [0, n) by sort +
+    prefix sum. A float64 ``index_add_`` into few keys (one giant component
+    holding millions of edges) is a contended fp64 atomic on one address --
+    minutes on the GPU; this is a sort and a scan, and deterministic."""
+    dev = keys.device
+    sums = torch.zeros(n, dtype=torch.float64, device=dev)
+    cnts = torch.zeros(n, dtype=torch.int64, device=dev)
+    if keys.numel() == 0:
+        return sums, cnts
+    o = torch.argsort(keys, stable=True)
+    k = keys[o]
+    c = torch.cumsum(vals[o].double(), 0)
+    last = torch.ones_like(k, dtype=torch.bool)
+    last[:-1] = k[1:] != k[:-1]
+    idx = torch.nonzero(last).flatten()
+    ends = c[idx]
+    sums[k[idx]] = ends - torch.cat([ends.new_zeros(1), ends[:-1]])
+    cnts[k[idx]] = idx - torch.cat([idx.new_full((1,), -1), idx[:-1]])
+    return sums, cnts
+
+
 class TenantGraph:
     NODE_COLS = (("sal", torch.float32, 0.0), ("acc", torch.int32, 0), ("last", torch.float64, 0.0),
                  ("ts", torch.float64, 0.0), ("shard", torch.int32, -1), ("kind", torch.uint8, FREE),
@@ -830,10 +852,9 @@ class TenantGraph:
             touched[src] = True
             touched[dst] = True
             member = (kind == NODE) | ((kind == GHOST) & touched)
-            size = torch.bincount(lab[member], minlength=n)
-            el = lab[src]
-            wsum = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, el, self.e["w"].double())
-            wcnt = torch.bincount(el, minlength=n)
+            lm = lab[member]
+            size = _seg_sum_count(lm, torch.zeros(lm.shape, dtype=torch.float32, device=dev), n)[1]
+            wsum, wcnt = _seg_sum_count(lab[src], self.e["w"], n)
             ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1).double() > min_avg_w)
             # reference order: a component's first member in BufferGraph.nodes order
             order = torch.as_tensor(self.ordered_node_rows(), dtype=torch.long).to(dev)
@@ -851,8 +872,7 @@ class TenantGraph:
             cand, key = cand[o], key[o]
             newg = torch.ones_like(key, dtype=torch.bool)
             newg[1:] = key[1:] != key[:-1]
-            gstart = torch.cummax(torch.where(newg, torch.arange(key.numel(), device=dev), torch.zeros_like(key)),
-                                  0).values
+            gstart = torch.nonzero(newg).flatten()[torch.cumsum(newg.long(), 0) - 1]
             rank = torch.arange(key.numel(), device=dev) - gstart
             sel = rank < take
             rows_h, key_h = cand[sel].cpu().numpy(), key[sel].cpu().numpy()
@@ -872,9 +892,7 @@ class TenantGraph:
             cid_t = torch.as_tensor(cid).to(self.device)
             cs, ct = cid_t[self.e["src"].long()], cid_t[self.e["dst"].long()]
             ok = (cs >= 0) & (cs == ct)
-            wsum = torch.zeros(C, dtype=torch.float64, device=self.device).index_add_(
-                0, cs[ok], self.e["w"][ok].double())
-            wcnt = torch.bincount(cs[ok], minlength=C)
+            wsum, wcnt = _seg_sum_count(cs[ok], self.e["w"][ok], C)
             return wsum.cpu().numpy(), wcnt.cpu().numpy()
 
     # ------------------------------------------------------------------ search

@@ -96,7 +96,8 @@ def test_visible_csr_boost_touch_importance_kernels():
     # a second call on the same stamp array boosts again (new epoch)
     kg2 = T.neighbor_boost(cg, eg["w"], seeds.to(DEV), ng["kind"], ng["sup"], ng["sal"], ng["last"], ng["dirty"],
                            6e6, st_g)
-    assert kg2 == kg
+    kc2 = T.neighbor_boost(cc, ec["w"], seeds, nc["kind"], nc["sup"], nc["sal"], nc["last"], nc["dirty"], 6e6, st_c)
+    assert kg2 == kg == kc2
     rows = torch.tensor([1, 2, 3, 4999], dtype=torch.long)
     T.touch(rows, nc["acc"], nc["last"], nc["sal"], nc["dirty"], 7e6)
     T.touch(rows.to(DEV), ng["acc"], ng["last"], ng["sal"], ng["dirty"], 7e6)
