@@ -29,7 +29,10 @@ random unit queries (the random-init encoder's outputs are nearly identical,
 so (a) alone would be a weak test).
 
 The second half of the metric (consolidate turns/sec) follows in the same JSON
-line (``--consolidate-steps``; bench/bench_consolidate.py).
+line (``--consolidate-steps``): ``MemorySystem.consolidate_batch`` on a
+10M-memory tenant per GPU -- embed, dedupe, links, decay/prune, eviction,
+run_consolidation, k-means hierarchy and the persistence commit, all timed
+(bench/bench_consolidate.py).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 launch with
 torch.distributed.run (one rank per GPU, RCCL backend).
@@ -215,7 +218,7 @@ def main():
     consolidate = None
     if a.consolidate_steps > 0:
         ms.close()
-        del ms, g, Xb, bias, q16, Qe
+        del ms, g, Xb, bias, q16, Qe, res0, api_rows
         torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
@@ -251,7 +254,9 @@ def main():
     if consolidate is not None:
         res["consolidate_turns_per_s"] = consolidate["turns_per_s"]
         res["consolidate"] = {k: consolidate[k] for k in ("ms_per_step", "nodes_per_rank", "convs_per_rank_step",
-                                                          "facts_per_conv", "per_step_rank0")}
+                                                          "facts_per_conv", "per_step_rank0", "nodes_rank0",
+                                                          "edges_rank0", "path", "hierarchical_clustering",
+                                                          "persistence")}
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

@@ -68,6 +68,7 @@ CHAIN_WEIGHT = 0.5
 MIN_FACT_LEN = 5
 DECAY_RATE = 0.01
 PROFILE_CONTENTS = 10  # contents per profile prompt (reference memory_system.py:1032)
+SALIENCE_FLOOR_ = 0.2  # node salience decays towards it (reference memory_shard.py:64-77)
 
 
 def _parse_json(response: str):
@@ -124,6 +125,7 @@ class ConsolidationMixin:
             if self.auto_consolidate and self.conversation_count % self.consolidate_every == 0:
                 self._say(f"🔄 Auto-consolidation triggered (every {self.consolidate_every} conversations)...")
                 results.append(self.run_consolidation())
+            self._maybe_cluster(self.conversation_count - 1)
             self.short_term_memory = []
             self.conversation_history = []
             self._save_to_persistence()
@@ -250,7 +252,8 @@ class ConsolidationMixin:
         sal_in = torch.as_tensor([float(facts[i].get("salience", 0.5)) for i in vidx], dtype=torch.float32)
 
         with g.on_stream():
-            dup_rows, (ls, lr), (ws, wr) = self._scan_batch(Q, torch.as_tensor(codes))
+            (br, bs, bnode), (ls, lr), (ws, wr) = self._scan_batch(Q, torch.as_tensor(codes))
+            dup_rows = torch.where(bnode & (br >= 0) & (bs > DEDUPE_THRESHOLD), br, -1)
         # --- dedupe: best store row is a node and cosine > 0.95 (reference :719-742)
         dup = dup_rows >= 0
         undo = None
@@ -301,7 +304,7 @@ class ConsolidationMixin:
         if made:
             self._say(f"✓ Created {made} cross-conversation links")
         self._enforce_buffer_limit()
-        if self.enable_hierarchy:
+        if self.enable_hierarchy and getattr(self, "hierarchy_mode", "reference") == "reference":
             for skey in dict.fromkeys(sk for _, sk in new_nodes):
                 c = g.shard_code.get(skey)
                 if c is not None and g.shard_count[c] > self.super_node_threshold:
@@ -342,8 +345,9 @@ class ConsolidationMixin:
     def _scan_batch(self, Q: torch.Tensor, codes: torch.Tensor):
         """Dedupe best rows + link candidate lists for a fact batch.
 
-        Returns (dup_row [M] long, -1 = not a duplicate), (global top-3 sims,
-        rows) over existing non-super nodes, (same-shard top-3 sims, rows).
+        Returns (store top-1 row [M] (-1 none), its cosine, whether it is a
+        live node), (global top-3 sims, rows) over existing non-super nodes,
+        (same-shard top-3 sims, rows).
         Fast path (GPU, unit rows, store == graph nodes): one dual scan; the
         dedupe top-1 over store rows is the better of the global list's head
         and the (few) super-node rows. Otherwise the store search runs as the
@@ -370,18 +374,18 @@ class ConsolidationMixin:
                 better = (ss[:, 0] > best_s) | ((ss[:, 0] == best_s) & (sr[:, 0] < best_r))
                 best_s = torch.where(better, ss[:, 0], best_s)
                 best_r = torch.where(better, sr[:, 0], best_r)
-            dup_rows = torch.where((best_r >= 0) & (best_s > DEDUPE_THRESHOLD), best_r, -1)
+            isnode = best_r >= 0
         else:
             _, top = self._store_top1(Q)
-            r1 = top.to(dev).reshape(M, -1)[:, 0]
-            ok = r1 >= 0
-            rr = r1.clamp_min(0)
+            best_r = top.to(dev).reshape(M, -1)[:, 0]
+            ok = best_r >= 0
+            rr = best_r.clamp_min(0)
             isnode = (g.kind[rr] == NODE) & ok
             X = g.emb32[rr].double()
             nrm = g.sqn[rr].double().sqrt()
-            cs = (Qn * X).sum(1) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))
-            dup_rows = torch.where(isnode & (cs > DEDUPE_THRESHOLD), r1, -1)
-        return dup_rows, (gs, gr), (ws, wr)
+            best_s = (Qn * X).sum(1) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))
+            best_s = torch.where(ok, best_s, torch.full_like(best_s, float("-inf")))
+        return (best_r, best_s, isnode), (gs, gr), (ws, wr)
 
     def _store_top1(self, Q: torch.Tensor):
         """Top-1 of the store's vector search for each fact -> graph rows."""
@@ -445,6 +449,299 @@ class ConsolidationMixin:
             # within-shard links, then cross-memory links
             g.append_edges(S, Dd, torch.cat(ew), torch.cat(eh), g.etype("relates_to"), now=now)
         return made
+
+    # ------------------------------------------------------------ batched end_conversation
+    def consolidate_batch(self, conversations: Sequence[Sequence[Dict]], embeddings=None,
+                          now: float = None) -> Dict[str, int]:
+        """``end_conversation`` for B finished conversations at once, given
+        their extracted facts (``conversations[c]`` = fact dicts with
+        ``content`` / ``type`` / ``salience`` / ``topic``, the extraction
+        LLM's output, reference :684-716). ``embeddings``: optional [F, D]
+        vectors aligned with the flattened facts (else the embedder runs once
+        for the whole batch).
+
+        Result = B sequential ``end_conversation`` calls (reference :580-649,
+        :706-891) -- conversation c's facts dedupe against, and link to, the
+        graph plus the facts kept from conversations < c; then decay
+        (0.01 per conversation) and auto-prune -- computed in one device pass:
+
+        * ONE fused scan of all facts against the pre-batch graph (dedupe
+          top-1 + within-shard and cross-memory top-3), plus an F x F float64
+          block for the facts of earlier conversations in the batch; in-batch
+          duplicate chains are resolved by a fixed point;
+        * decay is applied in closed form: the pre-batch graph by
+          (1-r)^B in one ``tg_decay_kernel`` pass, a new node / edge of
+          conversation c by (1-r)^(B-c) at insert (the decays of the
+          end_conversation calls that follow it); a duplicate merge onto a
+          node keeps max(decayed salience, decayed fact salience) -- exactly
+          the sequential result, as decay is monotone;
+        * eviction to ``max_buffer_size``, super-node creation, the
+          ``run_consolidation`` trigger (once if any of the B counts crosses a
+          multiple of ``consolidate_every``) and the persistence commit run
+          once per batch instead of once per conversation.
+
+        Returns counts: conversations, facts, dup, inserted, linked (edges
+        created), cross_links (the reference's "cross-conversation links"),
+        pruned (edges removed by decay, incl. new ones below the threshold),
+        evicted."""
+        flat, conv, idx = [], [], []
+        j = 0
+        for c, fs in enumerate(conversations):
+            for f in fs:
+                if isinstance(f, dict) and f.get("content") and len(f["content"]) >= MIN_FACT_LEN:
+                    flat.append(f)
+                    conv.append(c)
+                    idx.append(j)
+                j += 1
+        B = len(conversations)
+        now = time.time() if now is None else now
+        stats = {"conversations": B, "facts": len(flat), "dup": 0, "inserted": 0, "linked": 0, "cross_links": 0,
+                 "pruned": 0, "evicted": 0}
+        if B == 0:
+            return stats
+        if embeddings is not None and len(flat):
+            E = embeddings if torch.is_tensor(embeddings) else torch.as_tensor(np.asarray(embeddings, np.float32))
+            embs = E[torch.as_tensor(idx, dtype=torch.long).to(E.device)] if len(idx) != len(E) else E
+        elif flat:
+            with tracer.stage("embed_facts", self._device):
+                embs = self._batch_embed_any([f["content"] for f in flat])
+        else:
+            embs = None
+        with self._graph_lock, tracer.stage("consolidate_batch", self._device):
+            self._consolidate_batch(flat, np.asarray(conv, dtype=np.int64), B, embs, now, stats)
+            self._enforce_buffer_limit_counted(stats)
+            c0 = self.conversation_count
+            self.conversation_count += B
+            if self.auto_consolidate and (self.conversation_count // self.consolidate_every
+                                          > c0 // self.consolidate_every):
+                self.run_consolidation()
+            self._maybe_cluster(c0)
+            self._save_to_persistence()
+        return stats
+
+    def _maybe_cluster(self, c0: int) -> None:
+        """hierarchy_mode="kmeans": re-cluster when the conversation count
+        crosses a multiple of hierarchy_params["every"]."""
+        if not self.enable_hierarchy or getattr(self, "hierarchy_mode", "reference") != "kmeans":
+            return
+        hp = self.hierarchy_params
+        if self.conversation_count // hp["every"] > c0 // hp["every"] or getattr(self.graph, "hier", None) is None:
+            with tracer.stage("cluster", self._device):
+                self.graph.cluster_pass(hp["fine"], hp["top"], hp["iters"])
+
+    def _enforce_buffer_limit_counted(self, stats: Dict[str, int]) -> None:
+        g = self.graph
+        if g.num_nodes() <= self.max_buffer_size:
+            return
+        with tracer.stage("evict", self._device):
+            victims = g.evict(self.max_buffer_size)
+        if victims:
+            self._store_delete([g.ids[r] for r in victims])
+            stats["evicted"] += len(victims)
+
+    def _consolidate_batch(self, facts: List[Dict], conv: np.ndarray, B: int, embs, now: float,
+                           stats: Dict[str, int]) -> None:
+        g = self.graph
+        keep = 1.0 - DECAY_RATE
+        thr = self.prune_threshold if self.auto_prune else None
+        M = len(facts)
+        if M:
+            E, valid = self._fact_matrix(embs, M)
+            rejected = M - int(valid.sum())
+            if rejected:
+                self.metrics["rejected_embeddings"] = self.metrics.get("rejected_embeddings", 0) + rejected
+            vidx = np.nonzero(valid)[0]
+            facts = [facts[i] for i in vidx]
+            conv = conv[vidx]
+            E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
+            M = len(facts)
+        if M == 0:
+            stats["pruned"] += g.decay(1.0 - keep ** B, thr)
+            return
+        dev = g.device
+        # shards are created in fact order, duplicates included (reference :716-718)
+        shard_keys = [f.get("topic", self._infer_shard_key(f["content"])) for f in facts]
+        codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int32)
+        sal_in = torch.as_tensor([float(f.get("salience", 0.5)) for f in facts], dtype=torch.float64).to(dev)
+        ct = torch.as_tensor(conv).to(dev)
+        Q = E.to(dev, torch.float32)
+        Qd = Q.double()
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        NEG = float("-inf")
+
+        # ---- 1. one scan of the batch against the pre-batch graph
+        if g.n:
+            with g.on_stream():
+                (gb_r, gb_s, gb_node), (gs, gr), (ws, wr) = self._scan_batch(Q, torch.as_tensor(codes))
+        else:
+            gb_r = torch.full((M,), -1, dtype=torch.long, device=dev)
+            gb_s = torch.full((M,), NEG, dtype=torch.float64, device=dev)
+            gb_node = torch.zeros(M, dtype=torch.bool, device=dev)
+            gs = ws = torch.full((M, LINK_TOPK), NEG, dtype=torch.float64, device=dev)
+            gr = wr = torch.full((M, LINK_TOPK), -1, dtype=torch.long, device=dev)
+
+        # ---- 2. in-batch dedupe: the store top-1 over graph rows + the facts
+        # kept from earlier conversations, to a fixed point
+        S = Qn @ Qn.T
+        earlier = ct[None, :] < ct[:, None]  # [j, i]: fact i is from an earlier conversation than j
+        ins = torch.ones(M, dtype=torch.bool, device=dev)
+        for _ in range(M + 1):
+            A = torch.where(earlier & ins[None, :], S, torch.full_like(S, NEG))
+            bb_s = A.max(1).values
+            bb_i = torch.argmax((A == bb_s[:, None]).to(torch.int8), 1)
+            batch_best = bb_s > gb_s
+            best_s = torch.where(batch_best, bb_s, gb_s)
+            dup = (best_s > DEDUPE_THRESHOLD) & (batch_best | gb_node)
+            if torch.equal(~dup, ins):
+                break
+            ins = ~dup
+        dup_graph = dup & ~batch_best
+        dup_batch = dup & batch_best
+
+        def decayed(s: torch.Tensor, n: torch.Tensor) -> torch.Tensor:
+            kn = torch.pow(torch.full_like(s, keep), n.double())
+            return torch.where(s > SALIENCE_FLOOR_, SALIENCE_FLOOR_ + (s - SALIENCE_FLOOR_) * kn,
+                               torch.full_like(s, SALIENCE_FLOOR_))
+
+        left = (B - ct).double()  # decays still to come for a fact of conversation c
+        sal_dec = decayed(sal_in, left)
+
+        # ---- 3. decay + prune the pre-batch graph by B conversations at once
+        stats["pruned"] += g.decay(1.0 - keep ** B, thr)
+
+        # ---- 4. duplicate merges (reference :736-740)
+        ndup = int(dup.sum())
+        stats["dup"] += ndup
+        if bool(dup_graph.any()):
+            rows = gb_r[dup_graph]
+            with g.on_stream():
+                g.sal.scatter_reduce_(0, rows, sal_dec[dup_graph].float(), "amax", include_self=True)
+                g.last[rows] = now
+                g.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
+                g.dirty[rows] = 1
+            g._bump()
+        sal_new = sal_dec.clone()
+        acc_new = torch.zeros(M, dtype=torch.int32, device=dev)
+        if bool(dup_batch.any()):
+            tgt = bb_i[dup_batch]
+            sal_new.scatter_reduce_(0, tgt, sal_dec[dup_batch], "amax", include_self=True)
+            acc_new.index_add_(0, tgt, torch.ones_like(tgt, dtype=torch.int32))
+        for _ in range(ndup):
+            self._say("   (Merged semantic duplicate)")
+
+        # ---- 5. insert the kept facts (conversation order) with pre-decayed salience
+        kidx = torch.nonzero(ins).flatten()
+        kh = kidx.cpu().numpy()
+        if kh.size == 0:
+            return
+        kfacts = [facts[i] for i in kh]
+        ids = [self._generate_node_id() for _ in kh]
+        rows = g.add_nodes(ids, [f["content"] for f in kfacts], Q[kidx], shard=codes[kh],
+                           types=[f.get("type", "semantic") for f in kfacts], sal=sal_new[kidx].float(),
+                           acc=acc_new[kidx], now=now, stored=self._store_binds_graph())
+        stats["inserted"] += int(kh.size)
+        if not self._store_binds_graph():
+            self.vector_store.add_nodes([
+                {"id": i, "content": f["content"], "embedding": g.embedding(int(r)), "type": f.get("type", "semantic"),
+                 "salience": float(f.get("salience", 0.5)), "shard_key": shard_keys[j], "timestamp": now}
+                for i, f, r, j in zip(ids, kfacts, rows.tolist(), kh.tolist())], user_id=self.user_id)
+        if self.query_cache:
+            self.query_cache.invalidate_results()
+        new_row = torch.full((M,), -1, dtype=torch.long, device=dev)
+        new_row[kidx] = rows.to(dev)
+
+        # ---- 6. links of the kept facts (reference :797-891), pre-decayed
+        self._link_batch_multi(kidx, new_row, codes, ct, S, earlier, (ws, wr), (gs, gr), keep, B, thr, now, stats)
+        if self.enable_hierarchy and getattr(self, "hierarchy_mode", "reference") == "reference":
+            for skey in dict.fromkeys(shard_keys[j] for j in kh.tolist()):
+                c = g.shard_code.get(skey)
+                if c is not None and g.shard_count[c] > self.super_node_threshold:
+                    self._create_super_nodes_for_shard(skey)
+
+    def _link_batch_multi(self, kidx, new_row, codes, ct, S, earlier, shard_hits, global_hits, keep, B, thr, now,
+                          stats) -> None:
+        g = self.graph
+        dev = g.device
+        M = S.shape[0]
+        NEG = float("-inf")
+        K = kidx.numel()
+        kc = ct[kidx]
+        kcode = torch.as_tensor(codes).to(dev)[kidx].long()
+        # shards with >= 2 new nodes in the same conversation (reference :814-815)
+        key = kc * (1 << 24) + kcode
+        uniq, inv, cnt = torch.unique(key, return_inverse=True, return_counts=True)
+        multi = cnt[inv] >= 2
+        ins_b = torch.zeros(M, dtype=torch.bool, device=dev)
+        ins_b[kidx] = True
+        code_all = torch.as_tensor(codes).to(dev).long()
+        es, ed, ew, eh, order = [], [], [], [], []
+        # chain edges between consecutive new nodes of a (conversation, shard)
+        o = torch.argsort(key * K + torch.arange(K, device=dev))
+        ks = key[o]
+        adj = torch.nonzero(ks[1:] == ks[:-1]).flatten()
+        if adj.numel():
+            a, b = o[adj], o[adj + 1]
+            es.append(new_row[kidx[a]])
+            ed.append(new_row[kidx[b]])
+            ew.append(torch.full((a.numel(),), CHAIN_WEIGHT, dtype=torch.float64, device=dev))
+            eh.append(kcode[a])
+            order.append(kc[a] * 4)
+        Sk = S[kidx]  # [K, M]
+        ek = earlier[kidx] & ins_b[None, :]
+
+        def merged_top(graph_s, graph_r, batch_mask):
+            bs = torch.where(batch_mask, Sk, torch.full_like(Sk, NEG))
+            t = min(LINK_TOPK, M)
+            tb_s, tb_i = torch.topk(bs, t, dim=1)
+            tb_r = torch.where(torch.isneginf(tb_s), torch.full_like(tb_i, -1), new_row[tb_i])
+            cs = torch.cat([graph_s[kidx], tb_s], 1)
+            cr = torch.cat([graph_r[kidx], tb_r], 1)
+            keyr = torch.where(cr >= 0, cr, torch.full_like(cr, 1 << 62))
+            o2 = torch.argsort(keyr, dim=1, stable=True)
+            cs, cr = torch.gather(cs, 1, o2), torch.gather(cr, 1, o2)
+            o3 = torch.sort(cs, dim=1, descending=True, stable=True).indices[:, :LINK_TOPK]
+            return torch.gather(cs, 1, o3), torch.gather(cr, 1, o3)
+
+        # within-shard similarity links: same shard, from the graph or earlier conversations
+        sw_, sr_ = merged_top(shard_hits[0], shard_hits[1], ek & (code_all[None, :] == kcode[:, None]))
+        src = new_row[kidx][:, None].expand(-1, LINK_TOPK)
+        mw = (sr_ >= 0) & (sw_ > LINK_THRESHOLD) & multi[:, None]
+        es.append(src[mw])
+        ed.append(sr_[mw])
+        ew.append(sw_[mw] * LINK_WEIGHT_SCALE)
+        eh.append(kcode[:, None].expand_as(sr_)[mw])
+        order.append(kc[:, None].expand_as(sr_)[mw] * 4 + 1)
+        # cross-memory links: any non-super node, skipping pairs linked within the shard
+        gw_, gr_ = merged_top(global_hits[0], global_hits[1], ek)
+        mg = (gr_ >= 0) & (gw_ > LINK_THRESHOLD)
+        mg &= ~((gr_[:, :, None] == sr_[:, None, :]) & mw[:, None, :]).any(dim=2)
+        es.append(src[mg])
+        ed.append(gr_[mg])
+        ew.append(gw_[mg] * LINK_WEIGHT_SCALE)
+        eh.append(kcode[:, None].expand_as(gr_)[mg])
+        order.append(kc[:, None].expand_as(gr_)[mg] * 4 + 2)
+        n_cross = int(mg.sum())
+        if n_cross:
+            self._say(f"✓ Created {n_cross} cross-conversation links")
+        Sr, Dr = torch.cat(es), torch.cat(ed)
+        if Sr.numel() == 0:
+            return
+        W = torch.cat(ew)
+        Ord = torch.cat(order)
+        # decays of the end_conversation calls from the edge's conversation on
+        W = W * torch.pow(torch.full_like(W, keep), (B - torch.div(Ord, 4, rounding_mode="floor")).double())
+        stats["linked"] += int(Sr.numel())
+        stats["cross_links"] += n_cross
+        H = torch.cat(eh)
+        o = torch.argsort(Ord, stable=True)
+        Sr, Dr, W, H = Sr[o], Dr[o], W[o], H[o]
+        if thr is not None:
+            alive = W >= thr
+            stats["pruned"] += int((~alive).sum())
+            Sr, Dr, W, H = Sr[alive], Dr[alive], W[alive], H[alive]
+        if Sr.numel():
+            g.append_edges(Sr, Dr, W.float(), H.to(torch.int32), g.etype("relates_to"), now=now)
 
     # ------------------------------------------------------------ hierarchy (K8/K16)
     def _create_super_nodes_for_shard(self, shard_key: str):

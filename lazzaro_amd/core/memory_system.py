@@ -107,6 +107,8 @@ class MemorySystem(ConsolidationMixin):
         max_consolidation_retries: int = 3,
         index: str = "flat",
         index_params: Optional[Dict] = None,
+        hierarchy_mode: str = "reference",
+        hierarchy_params: Optional[Dict] = None,
     ):
         self.model = model
         self.user_id = user_id
@@ -149,6 +151,14 @@ class MemorySystem(ConsolidationMixin):
         self.prune_threshold = prune_threshold
         self.max_buffer_size = max_buffer_size
         self.merge_mode = merge_mode
+        # "reference": one mean super-node per shard once it passes
+        # super_node_threshold (memory_system.py:893-933); "kmeans": a
+        # two-level k-means hierarchy over the whole tenant, re-clustered every
+        # hierarchy_params["every"] conversations (TenantGraph.cluster_pass)
+        if hierarchy_mode not in ("reference", "kmeans"):
+            raise ValueError("hierarchy_mode must be 'reference' or 'kmeans'")
+        self.hierarchy_mode = hierarchy_mode
+        self.hierarchy_params = {"fine": 4096, "top": 64, "every": 50, "iters": 2, **(hierarchy_params or {})}
         # failure policy: strict -> typed errors propagate;
         # otherwise failures are counted in metrics and work is retried
         self.strict_errors = strict_errors
@@ -366,7 +376,15 @@ class MemorySystem(ConsolidationMixin):
                 return cached
         g = self.graph
         retrieved: List[str] = []
-        if self.enable_hierarchy and g.n_super:
+        if self.enable_hierarchy and self.hierarchy_mode == "kmeans":
+            q = query_emb if torch.is_tensor(query_emb) else torch.as_tensor(np.asarray(query_emb, np.float64))
+            if g.dim is not None and q.numel() == g.dim:
+                retrieved = [g.ids[r] for r in g.hier_children(q, SUPER_MATCH, SUPER_CHILDREN)]
+                if len(retrieved) >= RESULT_LIMIT:
+                    if self.query_cache:
+                        self.query_cache.set_results(query_text, retrieved[:RESULT_LIMIT])
+                    return retrieved[:RESULT_LIMIT]
+        elif self.enable_hierarchy and g.n_super:
             sr = self._super_best(query_emb)
             if sr >= 0:
                 kind, sup = g.mirror("kind"), g.mirror("sup")

@@ -1078,6 +1078,70 @@ class TenantGraph:
         ids = self.ids
         return [[ids[x] for x in row if x >= 0] for row in r.cpu().tolist()]
 
+    # ------------------------------------------------------------------ k-means hierarchy (K16)
+    def cluster_pass(self, n_fine: int = 4096, n_top: int = 64, iters: int = 2, seed: int = 0) -> Dict:
+        """Two-level hierarchical clustering of the live shard nodes (SURVEY.md
+        §2.4 K16; ``MemorySystem(hierarchy_mode="kmeans")``): spherical k-means
+        into ``n_fine`` clusters over the tenant's rows in place (fused MFMA
+        argmax assign + sorted segment sums; dead rows masked, no gather),
+        warm-started from the previous pass, then the fine centroids into
+        ``n_top`` topic clusters -- the scalable form of the reference's one
+        mean super-node per shard (memory_system.py:893-933). Keeps
+        ``self.hier``: top centroids, each row's fine / top label and the
+        rows ordered by (top cluster, row) for child lookups."""
+        from ..index.kmeans import kmeans
+
+        n = self.n
+        if n == 0 or self.dim is None:
+            return {}
+        with self.on_stream():
+            live = (self.kind[:n] == NODE) & (self.sup[:n] == 0) & (self.has_emb[:n] == 1)
+            n_live = int(live.sum())
+            if n_live == 0:
+                return {}
+            if self.on_gpu:
+                X = self.emb16[:n]
+            else:
+                X = self.emb32[:n] / self.sqn[:n].sqrt().clamp_min(1e-30)[:, None]
+            kf = min(n_fine, n_live)
+            kt = min(n_top, kf)
+            prev = getattr(self, "hier", None) or {}
+            init_f = prev.get("fine_c") if prev.get("fine_c") is not None and prev["fine_c"].shape[0] == kf else None
+            fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live)
+            init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
+            tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
+            lab = lab.long()
+            top = torch.where(lab >= 0, top_of_fine.long()[lab.clamp_min(0)], torch.full_like(lab, -1))
+            rows = torch.nonzero(top >= 0).flatten()
+            o = torch.argsort(top[rows] * n + rows)
+            perm = rows[o]
+            cnt = torch.bincount(top[rows], minlength=kt)
+            start = torch.zeros(kt + 1, dtype=torch.long, device=self.device)
+            start[1:] = torch.cumsum(cnt, 0)
+            self.hier = {"fine_c": fc32, "top_c": tc32, "fine": lab.to(torch.int32), "top": top.to(torch.int32),
+                         "perm": perm, "start": start, "n": n, "version": self.version}
+        return {"fine": kf, "top": kt, "rows": n_live}
+
+    def hier_children(self, q: torch.Tensor, threshold: float, limit: int) -> List[int]:
+        """Hierarchical retrieval over the k-means topics (the reference's
+        super-node step, memory_system.py:464-482): the top cluster most
+        similar to ``q`` (float64 cosine) if it beats ``threshold``, and its
+        first ``limit`` live members (row order). [] otherwise."""
+        h = getattr(self, "hier", None)
+        if not h or self.dim is None:
+            return []
+        with self.on_stream():
+            C = h["top_c"][:, : self.dim].double()
+            qd = q.to(self.device).double().reshape(-1)
+            s = (C @ qd) / (C.norm(dim=1) * qd.norm()).clamp_min(1e-30)
+            t = int(torch.argmax(s))
+            if float(s[t]) <= threshold:
+                return []
+            a, b = int(h["start"][t]), int(h["start"][t + 1])
+            cand = h["perm"][a: min(b, a + 8 * limit)]
+            ok = (self.kind[cand] == NODE) & (self.sup[cand] == 0)
+            return cand[ok][:limit].tolist()
+
     # ------------------------------------------------------------------ centroid
     def mean_embedding(self, rows: torch.Tensor) -> Optional[torch.Tensor]:
         """Mean embedding (float64) of the rows that have one (reference

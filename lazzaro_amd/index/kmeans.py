@@ -37,12 +37,16 @@ def assign(X: torch.Tensor, C16: torch.Tensor, chunk: int = 1 << 20) -> Tuple[to
     return torch.cat(labs).to(torch.int32), torch.cat(scs)
 
 
-def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 16) -> torch.Tensor:
+def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 16,
+                    rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Deterministic farthest-first seeding on a subsample (k-means++ without
-    the sampling): avoids two seeds landing in one cluster."""
-    n = X.shape[0]
+    the sampling): avoids two seeds landing in one cluster. ``rows``: the
+    eligible row indices (default all)."""
+    n = X.shape[0] if rows is None else rows.numel()
     g = torch.Generator(device="cpu").manual_seed(seed)
     sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
+    if rows is not None:
+        sub = rows[sub]
     S = X[sub].float()
     m = min(k, S.shape[0])
     picks = torch.zeros(m, dtype=torch.long, device=S.device)
@@ -58,13 +62,16 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
 
 
 def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
-           init: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+           init: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None
+           ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """X: unit rows [n, Dp] (bf16 on GPU). Returns (centroids fp32 [k, Dp],
-    centroids bf16 [k, Dp], labels int32 [n])."""
+    centroids bf16 [k, Dp], labels int32 [n]). ``mask`` (bool [n]): rows
+    that take part (others get label -1 and do not move the centroids) --
+    an arena with tombstones is clustered in place, without a gather."""
     n, Dp = X.shape
     dev = X.device
     if init is None and k <= 4096:
-        c32 = _farthest_first(X, k, seed)
+        c32 = _farthest_first(X, k, seed, rows=None if mask is None else torch.nonzero(mask).flatten())
     elif init is None:
         g = torch.Generator(device="cpu").manual_seed(seed)
         c32 = X[torch.randperm(n, generator=g)[:k].to(dev)].float()
@@ -79,6 +86,8 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
     lab = None
     for _ in range(iters):
         lab, _ = assign(X, c16)
+        if mask is not None:
+            lab = torch.where(mask, lab, torch.full_like(lab, -1))
         if not distributed:
             c32, c16n, cnt = G.centroids(X, lab, k, normalize=True, pad_to=Dp if X.is_cuda else 0)
         else:

@@ -312,3 +312,118 @@ def test_component_digest_matches_materialised_components():
             want.append(rows)
     got = [r.tolist() for r in g.component_digest(3, 0.3, 10)]
     assert got == want and len(want) > 3
+
+
+def _batch_scenario(seed=0, n_conv=7, per=5, dim=16):
+    rng = np.random.default_rng(seed)
+    centers = rng.standard_normal((4, dim))
+    pool = []
+    convs = []
+    for c in range(n_conv):
+        fs = []
+        for j in range(per):
+            r = rng.random()
+            if pool and r < 0.25:  # near-duplicate of an earlier fact (cos > 0.95)
+                base = pool[rng.integers(len(pool))][1]
+                v = base + 0.02 * rng.standard_normal(dim)
+            else:  # related to a topic centre (links with cos > 0.5)
+                v = centers[rng.integers(4)] + 0.6 * rng.standard_normal(dim)
+            v = v / np.linalg.norm(v)
+            content = f"fact {c}.{j} about things"
+            topic = ["work", "personal", "learning"][rng.integers(3)]
+            fs.append({"content": content, "type": "semantic", "salience": float(rng.uniform(0.3, 0.9)),
+                       "topic": topic})
+            pool.append((content, v))
+        convs.append(fs)
+    return convs, {c: v.tolist() for c, v in pool}
+
+
+def _graph_state(ms):
+    nodes = {n.content: (n.shard_key, n.salience, n.access_count) for n in ms.buffer.nodes.values()}
+    edges = {}
+    for sk, sh in ms.shards.items():
+        for (s, t), e in sh.edges.items():
+            edges[(sk, ms.buffer.get_node(s).content, ms.buffer.get_node(t).content)] = (round(e.weight, 6),
+                                                                                         e.co_occurrence)
+    return nodes, edges
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_consolidate_batch_equals_sequential_end_conversations(tmp_path, seed):
+    """B conversations through consolidate_batch == B sequential
+    end_conversation calls (dedupe incl. earlier conversations of the batch,
+    within-shard + cross links, decay + prune in closed form)."""
+    convs, table = _batch_scenario(seed)
+    seed = [[{"content": f"seed memory {i}", "type": "semantic", "salience": 0.7,
+              "topic": ["work", "personal", "learning"][i % 3]} for i in range(6)]]
+    rng = np.random.default_rng(9)
+    for i in range(6):
+        v = rng.standard_normal(16)
+        table[f"seed memory {i}"] = (v / np.linalg.norm(v)).tolist()
+    kw = dict(enable_async=False, load_from_disk=False, max_buffer_size=10 ** 6, consolidate_every=10 ** 6,
+              super_node_threshold=10 ** 6)
+    # sequential reference
+    seq = MemorySystem(llm_provider=ScriptedLLM([json.dumps({"memories": f}) for f in seed + convs]),
+                       embedding_provider=VecEmbedder(table, 16), db_dir=str(tmp_path / "a"), **kw)
+    for _ in range(len(seed) + len(convs)):
+        seq.start_conversation()
+        seq.add_to_short_term("conversation text")
+        seq.end_conversation()
+    # batched: the seed conversation sequentially, then one batch
+    bat = MemorySystem(llm_provider=ScriptedLLM([json.dumps({"memories": f}) for f in seed]),
+                       embedding_provider=VecEmbedder(table, 16), db_dir=str(tmp_path / "b"), **kw)
+    bat.start_conversation()
+    bat.add_to_short_term("conversation text")
+    bat.end_conversation()
+    flat = [f for c in convs for f in c]
+    st = bat.consolidate_batch(convs, embeddings=np.asarray([table[f["content"]] for f in flat], np.float32))
+    a, b = _graph_state(seq), _graph_state(bat)
+    assert st["dup"] > 0 and st["linked"] > 0 and st["inserted"] + st["dup"] == len(flat)
+    assert a[0].keys() == b[0].keys()
+    for k in a[0]:
+        assert a[0][k][0] == b[0][k][0] and a[0][k][2] == b[0][k][2] and abs(a[0][k][1] - b[0][k][1]) < 1e-5, k
+    assert a[1].keys() == b[1].keys() and len(a[1]) > 0
+    for k in a[1]:
+        assert abs(a[1][k][0] - b[1][k][0]) < 1e-5 and a[1][k][1] == b[1][k][1], k
+    assert seq.conversation_count == bat.conversation_count
+    seq.close()
+    bat.close()
+
+
+def test_kmeans_hierarchy_mode_clusters_and_retrieves(tmp_path):
+    """hierarchy_mode="kmeans": a two-level k-means pass over the tenant after
+    every `every` conversations; retrieval's hierarchical step returns members
+    of the query's topic cluster (reference super-node step, :464-482)."""
+    rng = np.random.default_rng(4)
+    dim = 16
+    centers = rng.standard_normal((4, dim))
+    centers /= np.linalg.norm(centers, axis=1, keepdims=True)
+    convs, vecs = [], []
+    for c in range(12):
+        fs = []
+        for j in range(5):
+            k = (c * 5 + j) % 4
+            v = centers[k] + 0.15 * rng.standard_normal(dim)
+            vecs.append(v / np.linalg.norm(v))
+            fs.append({"content": f"cluster {k} fact {c}.{j}", "salience": 0.6, "topic": "work"})
+        convs.append(fs)
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=VecEmbedder({}, dim), enable_async=False,
+                      load_from_disk=False, db_dir=str(tmp_path), max_buffer_size=10 ** 6, consolidate_every=10 ** 6,
+                      hierarchy_mode="kmeans", hierarchy_params={"fine": 8, "top": 4, "every": 5, "iters": 4})
+    ms.consolidate_batch(convs, embeddings=np.asarray(vecs, np.float32))
+    g = ms.graph
+    assert g.hier and g.hier["top_c"].shape[0] == 4 and ms.get_stats()["num_super_nodes"] == 0
+    tops = g.hier["top"][: g.n].tolist()
+    # facts of one generating centre share a topic cluster
+    by_center = {}
+    for r in range(g.n):
+        if g.kind_h(r) == 1:
+            by_center.setdefault(g.content[r].split()[1], set()).add(tops[r])
+    assert all(len(v) == 1 for v in by_center.values()) and len({min(v) for v in by_center.values()}) == 4
+    q = centers[2]
+    ids = ms._optimized_retrieval(q.tolist(), "a query near centre 2")
+    assert len(ids) == 5 and all(ms.buffer.get_node(i).content.startswith("cluster 2") for i in ids)
+    ms.close()
