@@ -78,7 +78,7 @@ def build_tenant(dev, nodes: int, dim: int, encoder, seed: int, db_dir: str, clu
         dst = torch.randint(0, nodes, (init_edges,), device=dev, generator=gen)
         w = torch.rand(init_edges, device=dev, generator=gen) * 0.5 + 0.5
         g.append_edges(src.int(), dst.int(), w, g.shard[src], g.etype("relates_to"))
-    g.clear_tracking()
+    g.clear_tracking(stored=False)  # the synthetic edges are not in the store
     return ms
 
 

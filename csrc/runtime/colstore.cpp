@@ -1,6 +1,9 @@
 // Versioned columnar table store -- implementation. See colstore.h.
 #include "colstore.h"
 
+#include <arrow/api.h>
+#include <arrow/io/api.h>
+#include <arrow/ipc/api.h>
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/file.h>
@@ -19,7 +22,174 @@
 
 namespace lzrt {
 
-static const char kMagic[4] = {'L', 'Z', 'C', '1'};
+namespace {
+
+constexpr uint64_t kKeepManifests = 64;  // older manifests are garbage-collected
+
+template <class T>
+T ok_or_throw(arrow::Result<T> r, const char* what) {
+  if (!r.ok()) throw std::runtime_error(std::string("colstore: ") + what + ": " + r.status().ToString());
+  return std::move(r).ValueOrDie();
+}
+
+void check(const arrow::Status& s, const char* what) {
+  if (!s.ok()) throw std::runtime_error(std::string("colstore: ") + what + ": " + s.ToString());
+}
+
+void mkdirs(const std::string& p) {
+  std::string cur;
+  for (size_t i = 0; i < p.size(); ++i) {
+    cur.push_back(p[i]);
+    if (p[i] == '/' || i + 1 == p.size()) ::mkdir(cur.c_str(), 0755);
+  }
+}
+
+std::string uniq_name() {
+  static std::atomic<uint64_t> ctr{0};
+  std::random_device rd;
+  uint64_t t = (uint64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count();
+  char buf[64];
+  snprintf(buf, sizeof buf, "%016llx%08x%04llx", (unsigned long long)t, (unsigned)rd(),
+           (unsigned long long)(ctr++ & 0xffff));
+  return buf;
+}
+
+std::string manifest_path(const std::string& dir, uint64_t v) {
+  char name[64];
+  snprintf(name, sizeof name, "/_versions/%020llu.manifest", (unsigned long long)v);
+  return dir + name;
+}
+
+void atomic_write(const std::string& path, const std::string& text) {
+  std::string tmp = path + ".tmp-" + uniq_name();
+  {
+    std::ofstream f(tmp);
+    f << text;
+    f.flush();
+    if (!f) throw std::runtime_error("colstore: write failed " + tmp);
+  }
+  if (::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("colstore: rename failed " + path);
+}
+
+std::shared_ptr<arrow::DataType> arrow_type(const ColSpec& c) {
+  switch (c.type) {
+    case ColType::Str: return arrow::utf8();
+    case ColType::F64: return arrow::float64();
+    case ColType::F32: return arrow::float32();
+    case ColType::I32: return arrow::int32();
+    case ColType::I64: return arrow::int64();
+    case ColType::Bool: return arrow::boolean();
+    case ColType::VecF32: return arrow::fixed_size_list(arrow::float32(), (int32_t)c.dim);
+  }
+  return arrow::null();
+}
+
+std::shared_ptr<arrow::Array> to_arrow(const Column& c) {
+  const int64_t n = (int64_t)c.size();
+  switch (c.type) {
+    case ColType::Str: {
+      arrow::StringBuilder b;
+      int64_t bytes = 0;
+      for (auto& x : c.s) bytes += (int64_t)x.size();
+      check(b.Reserve(n), "reserve");
+      check(b.ReserveData(bytes), "reserve");
+      for (auto& x : c.s) b.UnsafeAppend(x);
+      return ok_or_throw(b.Finish(), "string column");
+    }
+    case ColType::F64: {
+      arrow::DoubleBuilder b;
+      check(b.AppendValues(c.f64.data(), n), "f64 column");
+      return ok_or_throw(b.Finish(), "f64 column");
+    }
+    case ColType::F32: {
+      arrow::FloatBuilder b;
+      check(b.AppendValues(c.f32.data(), n), "f32 column");
+      return ok_or_throw(b.Finish(), "f32 column");
+    }
+    case ColType::I32: {
+      arrow::Int32Builder b;
+      check(b.AppendValues(c.i32.data(), n), "i32 column");
+      return ok_or_throw(b.Finish(), "i32 column");
+    }
+    case ColType::I64: {
+      arrow::Int64Builder b;
+      check(b.AppendValues(c.i64.data(), n), "i64 column");
+      return ok_or_throw(b.Finish(), "i64 column");
+    }
+    case ColType::Bool: {
+      arrow::BooleanBuilder b;
+      check(b.AppendValues(c.b.data(), n), "bool column");
+      return ok_or_throw(b.Finish(), "bool column");
+    }
+    case ColType::VecF32: {
+      arrow::FloatBuilder vb;
+      check(vb.AppendValues(c.f32.data(), (int64_t)c.f32.size()), "vector column");
+      auto values = ok_or_throw(vb.Finish(), "vector column");
+      return ok_or_throw(arrow::FixedSizeListArray::FromArrays(values, (int32_t)c.dim), "vector column");
+    }
+  }
+  return nullptr;
+}
+
+// Arrow array -> Column payload of the requested type (missing -> defaults).
+void from_arrow(const std::shared_ptr<arrow::Array>& a, Column& c, uint64_t nrows) {
+  if (!a) {
+    switch (c.type) {
+      case ColType::Str: c.s.assign(nrows, ""); break;
+      case ColType::F64: c.f64.assign(nrows, 0.0); break;
+      case ColType::F32: c.f32.assign(nrows, 0.f); break;
+      case ColType::I32: c.i32.assign(nrows, 0); break;
+      case ColType::I64: c.i64.assign(nrows, 0); break;
+      case ColType::Bool: c.b.assign(nrows, 0); break;
+      case ColType::VecF32: c.f32.assign(nrows * c.dim, 0.f); break;
+    }
+    return;
+  }
+  switch (c.type) {
+    case ColType::Str: {
+      auto s = std::static_pointer_cast<arrow::StringArray>(a);
+      c.s.resize(nrows);
+      for (uint64_t r = 0; r < nrows; ++r) c.s[r] = std::string(s->GetView((int64_t)r));
+      break;
+    }
+    case ColType::F64: {
+      auto x = std::static_pointer_cast<arrow::DoubleArray>(a);
+      c.f64.assign(x->raw_values(), x->raw_values() + nrows);
+      break;
+    }
+    case ColType::F32: {
+      auto x = std::static_pointer_cast<arrow::FloatArray>(a);
+      c.f32.assign(x->raw_values(), x->raw_values() + nrows);
+      break;
+    }
+    case ColType::I32: {
+      auto x = std::static_pointer_cast<arrow::Int32Array>(a);
+      c.i32.assign(x->raw_values(), x->raw_values() + nrows);
+      break;
+    }
+    case ColType::I64: {
+      auto x = std::static_pointer_cast<arrow::Int64Array>(a);
+      c.i64.assign(x->raw_values(), x->raw_values() + nrows);
+      break;
+    }
+    case ColType::Bool: {
+      auto x = std::static_pointer_cast<arrow::BooleanArray>(a);
+      c.b.resize(nrows);
+      for (uint64_t r = 0; r < nrows; ++r) c.b[r] = x->Value((int64_t)r) ? 1 : 0;
+      break;
+    }
+    case ColType::VecF32: {
+      auto l = std::static_pointer_cast<arrow::FixedSizeListArray>(a);
+      c.dim = (uint32_t)l->list_type()->list_size();
+      auto v = std::static_pointer_cast<arrow::FloatArray>(l->values());
+      const float* p = v->raw_values() + l->value_offset(0);
+      c.f32.assign(p, p + nrows * (size_t)c.dim);
+      break;
+    }
+  }
+}
+
+}  // namespace
 
 size_t Column::size() const {
   switch (type) {
@@ -48,56 +218,54 @@ void Column::append_from(const Column& o, size_t r) {
   }
 }
 
-static void mkdirs(const std::string& p) {
-  std::string cur;
-  for (size_t i = 0; i < p.size(); ++i) {
-    cur.push_back(p[i]);
-    if (p[i] == '/' || i + 1 == p.size()) ::mkdir(cur.c_str(), 0755);
-  }
-}
-
-static std::string uniq_name() {
-  static std::atomic<uint64_t> ctr{0};
-  std::random_device rd;
-  uint64_t t = (uint64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count();
-  char buf[64];
-  snprintf(buf, sizeof buf, "%016llx%08x%04llx", (unsigned long long)t, (unsigned)rd(),
-           (unsigned long long)(ctr++ & 0xffff));
-  return buf;
-}
-
-Table::Table(std::string dir, std::vector<ColSpec> schema) : dir_(std::move(dir)), schema_(std::move(schema)) {
+Table::Table(std::string dir, std::vector<ColSpec> schema, std::vector<std::string> key_cols)
+    : dir_(std::move(dir)), schema_(std::move(schema)), key_cols_(std::move(key_cols)) {
   mkdirs(dir_ + "/_versions");
   mkdirs(dir_ + "/data");
   mkdirs(dir_ + "/_deletions");
-  lock();
-  Manifest m = load_latest();
-  if (m.version == 0) {
-    m.version = 1;
-    m.schema = schema_;
-    write_manifest(m);
-  } else {
-    // adopt persisted dims for vector columns
-    for (auto& c : schema_)
-      for (auto& pc : m.schema)
-        if (pc.name == c.name && c.type == ColType::VecF32 && c.dim == 0) c.dim = pc.dim;
+  for (auto& k : key_cols_) {
+    int c = col_index(k);
+    if (c < 0 || schema_[c].type != ColType::Str) throw std::runtime_error("colstore: bad key column " + k);
+    key_idx_.push_back(c);
   }
+  lock();
+  try {
+    uint64_t v = latest_version();
+    if (v == 0) {
+      cur_version_ = 1;
+      write_manifest(1);
+    } else {
+      refresh();
+    }
+  } catch (...) { unlock(); throw; }
   unlock();
 }
 
+Table::~Table() {
+  if (lock_fd_ >= 0) ::close(lock_fd_);
+}
+
 void Table::lock() {
-  if (lock_fd_ >= 0) return;
+  mu_.lock();
+  if (lock_depth_++ > 0) return;
   std::string lp = dir_ + "/_lock";
   lock_fd_ = ::open(lp.c_str(), O_CREAT | O_RDWR, 0644);
-  if (lock_fd_ < 0) throw std::runtime_error("colstore: cannot open lock " + lp);
+  if (lock_fd_ < 0) {
+    --lock_depth_;
+    mu_.unlock();
+    throw std::runtime_error("colstore: cannot open lock " + lp);
+  }
   ::flock(lock_fd_, LOCK_EX);
 }
 
 void Table::unlock() {
-  if (lock_fd_ < 0) return;
-  ::flock(lock_fd_, LOCK_UN);
-  ::close(lock_fd_);
-  lock_fd_ = -1;
+  if (lock_depth_ <= 0) return;
+  if (--lock_depth_ == 0 && lock_fd_ >= 0) {
+    ::flock(lock_fd_, LOCK_UN);
+    ::close(lock_fd_);
+    lock_fd_ = -1;
+  }
+  mu_.unlock();
 }
 
 int Table::col_index(const std::string& name) const {
@@ -107,213 +275,183 @@ int Table::col_index(const std::string& name) const {
 }
 
 uint64_t Table::latest_version() {
+  FILE* f = fopen((dir_ + "/_latest").c_str(), "r");
+  if (f) {
+    unsigned long long v = 0;
+    int got = fscanf(f, "%llu", &v);
+    fclose(f);
+    if (got == 1 && v > 0) return v;
+  }
+  // no pointer file (a table from an older writer): newest manifest on disk
   uint64_t best = 0;
   DIR* d = ::opendir((dir_ + "/_versions").c_str());
   if (!d) return 0;
   while (dirent* e = ::readdir(d)) {
     const char* n = e->d_name;
     size_t L = strlen(n);
-    if (L > 9 && strcmp(n + L - 9, ".manifest") == 0) {
-      uint64_t v = strtoull(n, nullptr, 10);
-      best = std::max(best, v);
-    }
+    if (L > 9 && strcmp(n + L - 9, ".manifest") == 0) best = std::max<uint64_t>(best, strtoull(n, nullptr, 10));
   }
   ::closedir(d);
   return best;
 }
 
-Table::Manifest Table::load_latest() {
-  Manifest m;
-  uint64_t v = latest_version();
-  if (v == 0) return m;
-  char name[64];
-  snprintf(name, sizeof name, "/_versions/%020llu.manifest", (unsigned long long)v);
-  std::ifstream f(dir_ + name);
-  if (!f) return m;
+void Table::read_manifest(uint64_t v, std::vector<Frag>& out, std::vector<ColSpec>* sch) {
+  std::ifstream f(manifest_path(dir_, v));
+  if (!f) throw std::runtime_error("colstore: missing manifest v" + std::to_string(v) + " in " + dir_);
   std::string line;
   while (std::getline(f, line)) {
     std::istringstream is(line);
     std::string tag;
     is >> tag;
-    if (tag == "version") {
-      is >> m.version;
-    } else if (tag == "col") {
+    if (tag == "col" && sch) {
       ColSpec c;
       int t;
       is >> c.name >> t >> c.dim;
       c.type = (ColType)t;
-      m.schema.push_back(c);
+      sch->push_back(c);
     } else if (tag == "frag") {
-      Fragment fr;
+      Frag fr;
       is >> fr.file >> fr.rows >> fr.delfile;
       if (fr.delfile == "-") fr.delfile.clear();
-      m.frags.push_back(fr);
+      out.push_back(std::move(fr));
     }
   }
-  if (m.version == 0) m.version = v;
-  return m;
 }
 
-void Table::write_manifest(const Manifest& m) {
-  char name[64];
-  snprintf(name, sizeof name, "/_versions/%020llu.manifest", (unsigned long long)m.version);
-  std::string tmp = dir_ + "/_versions/.tmp-" + uniq_name();
+void Table::write_manifest(uint64_t v) {
+  std::ostringstream o;
+  o << "LZMANIFEST 2\nversion " << v << "\n";
+  for (auto& c : schema_) o << "col " << c.name << " " << (int)c.type << " " << c.dim << "\n";
+  for (auto& fr : frags_) o << "frag " << fr.file << " " << fr.rows << " " << (fr.delfile.empty() ? "-" : fr.delfile) << "\n";
+  atomic_write(manifest_path(dir_, v), o.str());
+  atomic_write(dir_ + "/_latest", std::to_string(v) + "\n");
+  cur_version_ = v;
+  if (v > kKeepManifests) ::unlink(manifest_path(dir_, v - kKeepManifests).c_str());
+}
+
+void Table::load_dead(Frag& f) {
+  f.dead.assign(f.rows, 0);
+  f.n_dead = 0;
+  if (f.delfile.empty()) return;
+  auto file = ok_or_throw(arrow::io::MemoryMappedFile::Open(dir_ + "/_deletions/" + f.delfile, arrow::io::FileMode::READ),
+                          "open deletion file");
+  auto rd = ok_or_throw(arrow::ipc::RecordBatchFileReader::Open(file), "read deletion file");
+  for (int b = 0; b < rd->num_record_batches(); ++b) {
+    auto batch = ok_or_throw(rd->ReadRecordBatch(b), "deletion batch");
+    auto rows = std::static_pointer_cast<arrow::UInt32Array>(batch->column(0));
+    for (int64_t i = 0; i < rows->length(); ++i) {
+      uint32_t r = rows->Value(i);
+      if (r < f.rows && !f.dead[r]) { f.dead[r] = 1; ++f.n_dead; }
+    }
+  }
+}
+
+void Table::write_dead(Frag& f, uint64_t v) {
+  arrow::UInt32Builder b;
+  check(b.Reserve((int64_t)f.n_dead), "reserve");
+  for (uint64_t r = 0; r < f.rows; ++r)
+    if (f.dead[r]) b.UnsafeAppend((uint32_t)r);
+  auto arr = ok_or_throw(b.Finish(), "deletion column");
+  auto sch = arrow::schema({arrow::field("row", arrow::uint32())});
+  std::string stem = f.file.substr(0, f.file.rfind('.'));
+  char dn[160];
+  snprintf(dn, sizeof dn, "%s-%llu.arrow", stem.c_str(), (unsigned long long)v);
+  std::string tmp = dir_ + "/_deletions/.tmp-" + uniq_name();
   {
-    std::ofstream f(tmp);
-    f << "LZMANIFEST 1\n";
-    f << "version " << m.version << "\n";
-    for (auto& c : schema_) f << "col " << c.name << " " << (int)c.type << " " << c.dim << "\n";
-    for (auto& fr : m.frags)
-      f << "frag " << fr.file << " " << fr.rows << " " << (fr.delfile.empty() ? "-" : fr.delfile) << "\n";
-    f.flush();
-    if (!f) throw std::runtime_error("colstore: manifest write failed");
+    auto out = ok_or_throw(arrow::io::FileOutputStream::Open(tmp), "open deletion file");
+    auto w = ok_or_throw(arrow::ipc::MakeFileWriter(out, sch), "deletion writer");
+    check(w->WriteRecordBatch(*arrow::RecordBatch::Make(sch, arr->length(), {arr})), "write deletions");
+    check(w->Close(), "close deletions");
+    check(out->Close(), "close deletions");
   }
-  if (::rename(tmp.c_str(), (dir_ + name).c_str()) != 0)
-    throw std::runtime_error("colstore: manifest rename failed");
+  if (::rename(tmp.c_str(), (dir_ + "/_deletions/" + dn).c_str()) != 0)
+    throw std::runtime_error("colstore: deletion rename failed");
+  f.delfile = dn;
 }
 
-static size_t payload_bytes(const Column& c) {
-  size_t n = c.size();
-  switch (c.type) {
-    case ColType::Str: {
-      size_t tot = 0;
-      for (auto& x : c.s) tot += x.size();
-      return 8 * (n + 1) + tot;
-    }
-    case ColType::F64: case ColType::I64: return 8 * n;
-    case ColType::F32: case ColType::I32: return 4 * n;
-    case ColType::Bool: return n;
-    case ColType::VecF32: return 4 * n * (size_t)c.dim;
+void Table::refresh() {
+  uint64_t v = latest_version();
+  if (v == 0 || v == cur_version_) return;
+  std::vector<Frag> nf;
+  std::vector<ColSpec> sch;
+  read_manifest(v, nf, &sch);
+  for (auto& c : schema_)  // adopt persisted vector dims
+    for (auto& pc : sch)
+      if (pc.name == c.name && c.type == ColType::VecF32 && c.dim == 0) c.dim = pc.dim;
+  // incremental when the old fragments are an unchanged prefix (pure appends
+  // by another writer); anything else rebuilds the state
+  bool prefix = nf.size() >= frags_.size();
+  for (size_t i = 0; prefix && i < frags_.size(); ++i)
+    prefix = nf[i].file == frags_[i].file && nf[i].delfile == frags_[i].delfile;
+  size_t from = prefix ? frags_.size() : 0;
+  if (!prefix) {
+    frags_.clear();
+    index_.clear();
+    indexed_ = false;
+    indexed_frags_ = 0;
   }
-  return 0;
+  for (size_t i = from; i < nf.size(); ++i) {
+    load_dead(nf[i]);
+    frags_.push_back(std::move(nf[i]));
+  }
+  cur_version_ = v;
+  if (indexed_)
+    for (uint32_t fi = (uint32_t)indexed_frags_; fi < frags_.size(); ++fi) index_fragment(fi);
 }
 
-void Table::write_fragment(const std::string& file, const std::vector<Column>& cols) {
-  std::string tmp = dir_ + "/data/.tmp-" + uniq_name();
-  FILE* f = fopen(tmp.c_str(), "wb");
-  if (!f) throw std::runtime_error("colstore: cannot write " + tmp);
-  uint32_t nc = (uint32_t)cols.size();
-  uint64_t nrows = cols.empty() ? 0 : cols[0].size();
-  fwrite(kMagic, 1, 4, f);
-  fwrite(&nc, 4, 1, f);
-  fwrite(&nrows, 8, 1, f);
-  uint64_t hdr = 4 + 4 + 8;
-  for (size_t i = 0; i < cols.size(); ++i) hdr += 4 + schema_[i].name.size() + 1 + 4 + 8 + 8;
-  uint64_t off = hdr;
-  for (size_t i = 0; i < cols.size(); ++i) {
-    uint32_t L = (uint32_t)schema_[i].name.size();
-    fwrite(&L, 4, 1, f);
-    fwrite(schema_[i].name.data(), 1, L, f);
-    uint8_t t = (uint8_t)cols[i].type;
-    fwrite(&t, 1, 1, f);
-    uint32_t dim = cols[i].dim;
-    fwrite(&dim, 4, 1, f);
-    uint64_t nb = payload_bytes(cols[i]);
-    fwrite(&off, 8, 1, f);
-    fwrite(&nb, 8, 1, f);
-    off += nb;
+std::string Table::make_key(const std::vector<Column>& cols, size_t r) const {
+  std::string k;
+  for (size_t i = 0; i < key_idx_.size(); ++i) {
+    if (i) k.push_back('\x1f');
+    k += cols[key_idx_[i]].s[r];
   }
-  for (auto& c : cols) {
-    switch (c.type) {
-      case ColType::Str: {
-        uint64_t o = 0;
-        fwrite(&o, 8, 1, f);
-        for (auto& x : c.s) { o += x.size(); fwrite(&o, 8, 1, f); }
-        for (auto& x : c.s) fwrite(x.data(), 1, x.size(), f);
-        break;
-      }
-      case ColType::F64: fwrite(c.f64.data(), 8, c.f64.size(), f); break;
-      case ColType::I64: fwrite(c.i64.data(), 8, c.i64.size(), f); break;
-      case ColType::F32: case ColType::VecF32: fwrite(c.f32.data(), 4, c.f32.size(), f); break;
-      case ColType::I32: fwrite(c.i32.data(), 4, c.i32.size(), f); break;
-      case ColType::Bool: fwrite(c.b.data(), 1, c.b.size(), f); break;
-    }
-  }
-  if (fflush(f) != 0 || fclose(f) != 0) throw std::runtime_error("colstore: write failed");
-  if (::rename(tmp.c_str(), (dir_ + "/data/" + file).c_str()) != 0)
-    throw std::runtime_error("colstore: fragment rename failed");
+  return k;
 }
 
-std::vector<Column> Table::read_fragment(const std::string& file, const std::vector<int>& want) {
-  std::string p = dir_ + "/data/" + file;
-  FILE* f = fopen(p.c_str(), "rb");
-  if (!f) throw std::runtime_error("colstore: missing fragment " + p);
-  char mg[4];
-  uint32_t nc;
-  uint64_t nrows;
-  if (fread(mg, 1, 4, f) != 4 || memcmp(mg, kMagic, 4) != 0) { fclose(f); throw std::runtime_error("colstore: bad magic " + p); }
-  if (fread(&nc, 4, 1, f) != 1 || fread(&nrows, 8, 1, f) != 1) { fclose(f); throw std::runtime_error("colstore: bad header"); }
-  struct Ent { std::string name; ColType t; uint32_t dim; uint64_t off, nb; };
-  std::vector<Ent> ents(nc);
-  for (auto& e : ents) {
-    uint32_t L;
-    if (fread(&L, 4, 1, f) != 1) break;
-    e.name.resize(L);
-    if (L && fread(&e.name[0], 1, L, f) != L) break;
-    uint8_t t;
-    if (fread(&t, 1, 1, f) != 1) break;
-    e.t = (ColType)t;
-    if (fread(&e.dim, 4, 1, f) != 1 || fread(&e.off, 8, 1, f) != 1 || fread(&e.nb, 8, 1, f) != 1) break;
-  }
-  std::vector<Column> out(schema_.size());
-  for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
-  for (int ci : want) {
-    const std::string& nm = schema_[ci].name;
-    const Ent* e = nullptr;
-    for (auto& x : ents) if (x.name == nm) { e = &x; break; }
-    Column& c = out[ci];
-    if (!e) {  // column added after this fragment was written: defaults
-      switch (c.type) {
-        case ColType::Str: c.s.assign(nrows, ""); break;
-        case ColType::F64: c.f64.assign(nrows, 0.0); break;
-        case ColType::F32: c.f32.assign(nrows, 0.f); break;
-        case ColType::I32: c.i32.assign(nrows, 0); break;
-        case ColType::I64: c.i64.assign(nrows, 0); break;
-        case ColType::Bool: c.b.assign(nrows, 0); break;
-        case ColType::VecF32: c.f32.assign(nrows * c.dim, 0.f); break;
-      }
-      continue;
-    }
-    c.dim = e->dim;
-    fseek(f, (long)e->off, SEEK_SET);
-    switch (c.type) {
-      case ColType::Str: {
-        std::vector<uint64_t> offs(nrows + 1);
-        fread(offs.data(), 8, nrows + 1, f);
-        std::string blob(offs[nrows], '\0');
-        if (!blob.empty()) fread(&blob[0], 1, blob.size(), f);
-        c.s.resize(nrows);
-        for (uint64_t r = 0; r < nrows; ++r) c.s[r] = blob.substr(offs[r], offs[r + 1] - offs[r]);
-        break;
-      }
-      case ColType::F64: c.f64.resize(nrows); fread(c.f64.data(), 8, nrows, f); break;
-      case ColType::I64: c.i64.resize(nrows); fread(c.i64.data(), 8, nrows, f); break;
-      case ColType::F32: c.f32.resize(nrows); fread(c.f32.data(), 4, nrows, f); break;
-      case ColType::I32: c.i32.resize(nrows); fread(c.i32.data(), 4, nrows, f); break;
-      case ColType::Bool: c.b.resize(nrows); fread(c.b.data(), 1, nrows, f); break;
-      case ColType::VecF32: c.f32.resize(nrows * (size_t)e->dim); fread(c.f32.data(), 4, c.f32.size(), f); break;
-    }
-  }
-  fclose(f);
-  return out;
+void Table::index_fragment(uint32_t fi) {
+  Frag& f = frags_[fi];
+  uint64_t nrows = 0;
+  auto cols = read_fragment(f.file, key_idx_, &nrows);
+  for (uint64_t r = 0; r < nrows; ++r)
+    if (!f.dead[r]) index_.emplace(make_key(cols, r), std::make_pair(fi, (uint32_t)r));
+  indexed_frags_ = std::max<uint64_t>(indexed_frags_, fi + 1);
 }
 
-void Table::load_deleted(Fragment& fr) {
-  if (fr.del_loaded) return;
-  fr.del_loaded = true;
-  fr.deleted.clear();
-  if (fr.delfile.empty()) return;
-  FILE* f = fopen((dir_ + "/_deletions/" + fr.delfile).c_str(), "rb");
-  if (!f) return;
-  uint64_t n = 0;
-  fread(&n, 8, 1, f);
-  fr.deleted.resize(n);
-  fread(fr.deleted.data(), 4, n, f);
-  fclose(f);
+void Table::ensure_index() {
+  if (indexed_ || key_idx_.empty()) return;
+  index_.clear();
+  indexed_frags_ = 0;
+  for (uint32_t fi = 0; fi < frags_.size(); ++fi) index_fragment(fi);
+  indexed_ = true;
 }
 
-bool Table::matches(const std::vector<Column>& cols, const std::vector<int>& pcols,
-                    const Predicate& p, size_t r) const {
+// The predicate names exactly the key columns (eq on all but the last, IN on
+// the last; or eq on all) -> the keys it selects.
+bool Table::keyed(const Predicate& p, std::vector<std::string>* keys) const {
+  if (key_cols_.empty()) return false;
+  const size_t K = key_cols_.size();
+  std::string prefix;
+  if (p.has_in) {
+    if (p.eq.size() != K - 1 || p.in_col != key_cols_[K - 1]) return false;
+  } else if (p.eq.size() != K) {
+    return false;
+  }
+  for (size_t i = 0; i + (p.has_in ? 1 : 0) < K; ++i) {
+    if (p.eq[i].first != key_cols_[i]) return false;
+    if (i) prefix.push_back('\x1f');
+    prefix += p.eq[i].second;
+  }
+  keys->clear();
+  if (!p.has_in) {
+    keys->push_back(prefix);
+  } else {
+    for (auto& v : p.in_vals) keys->push_back(K > 1 ? prefix + '\x1f' + v : v);
+  }
+  return true;
+}
+
+bool Table::matches(const std::vector<Column>& cols, const std::vector<int>& pcols, const Predicate& p,
+                    size_t r) const {
   for (size_t i = 0; i < p.eq.size(); ++i) {
     int ci = pcols[i];
     if (ci < 0 || cols[ci].s[r] != p.eq[i].second) return false;
@@ -325,96 +463,136 @@ bool Table::matches(const std::vector<Column>& cols, const std::vector<int>& pco
   return true;
 }
 
-uint64_t Table::append(const std::vector<Column>& cols_in) {
-  if (cols_in.size() != schema_.size()) throw std::runtime_error("colstore: column count mismatch");
-  size_t n = cols_in.empty() ? 0 : cols_in[0].size();
-  for (auto& c : cols_in) if (c.size() != n) throw std::runtime_error("colstore: ragged columns");
-  lock();
-  Manifest m = load_latest();
-  if (n == 0) { unlock(); return m.version; }
-  for (size_t i = 0; i < schema_.size(); ++i) {
-    if (schema_[i].type == ColType::VecF32) {
-      uint32_t d = cols_in[i].dim;
-      for (auto& pc : m.schema) if (pc.name == schema_[i].name && pc.dim) schema_[i].dim = pc.dim;
-      if (schema_[i].dim == 0) schema_[i].dim = d;
-      if (schema_[i].dim != d) { unlock(); throw std::runtime_error("colstore: vector dim mismatch"); }
+// Marks rows matching p as deleted (deletion files tagged with version nv).
+// Keyed predicates touch only the selected rows. Caller holds the lock and has
+// refreshed.
+uint64_t Table::apply_delete(const Predicate& p, uint64_t nv) {
+  uint64_t total = 0;
+  std::vector<uint8_t> touched(frags_.size(), 0);
+  std::vector<std::string> keys;
+  if (keyed(p, &keys)) {
+    ensure_index();
+    for (auto& k : keys) {
+      auto range = index_.equal_range(k);
+      for (auto it = range.first; it != range.second; ++it) {
+        auto [fi, r] = it->second;
+        Frag& f = frags_[fi];
+        if (!f.dead[r]) { f.dead[r] = 1; ++f.n_dead; ++total; touched[fi] = 1; }
+      }
+      index_.erase(range.first, range.second);
+    }
+  } else {
+    std::vector<int> pcols;
+    for (auto& kv : p.eq) pcols.push_back(col_index(kv.first));
+    if (p.has_in) pcols.push_back(col_index(p.in_col));
+    std::vector<int> need;
+    for (int c : pcols) if (c >= 0 && std::find(need.begin(), need.end(), c) == need.end()) need.push_back(c);
+    for (auto& k : key_idx_) if (std::find(need.begin(), need.end(), k) == need.end()) need.push_back(k);
+    for (uint32_t fi = 0; fi < frags_.size(); ++fi) {
+      Frag& f = frags_[fi];
+      if (f.n_dead == f.rows) continue;
+      uint64_t nrows = 0;
+      auto cols = read_fragment(f.file, need, &nrows);
+      for (uint64_t r = 0; r < nrows; ++r) {
+        if (f.dead[r] || !matches(cols, pcols, p, r)) continue;
+        f.dead[r] = 1;
+        ++f.n_dead;
+        ++total;
+        touched[fi] = 1;
+        if (indexed_) {
+          auto range = index_.equal_range(make_key(cols, r));
+          for (auto it = range.first; it != range.second; ++it)
+            if (it->second == std::make_pair(fi, (uint32_t)r)) { index_.erase(it); break; }
+        }
+      }
     }
   }
-  std::string file = uniq_name() + ".lzc";
-  try {
-    write_fragment(file, cols_in);
-    Fragment fr;
-    fr.file = file;
-    fr.rows = n;
-    m.frags.push_back(fr);
-    m.version += 1;
-    write_manifest(m);
-  } catch (...) { unlock(); throw; }
-  unlock();
-  return m.version;
+  for (uint32_t fi = 0; fi < frags_.size(); ++fi)
+    if (touched[fi]) write_dead(frags_[fi], nv);
+  return total;
 }
 
-// Marks rows matching p as deleted in m (new deletion files tagged with
-// version nv); fully deleted fragments leave the manifest. Caller holds the lock.
-uint64_t Table::apply_delete(Manifest& m, const Predicate& p, uint64_t nv) {
-  std::vector<int> pcols;
-  for (auto& kv : p.eq) pcols.push_back(col_index(kv.first));
-  if (p.has_in) pcols.push_back(col_index(p.in_col));
-  uint64_t total = 0;
-  std::vector<Fragment> keep;
-  for (auto& fr : m.frags) {
-    load_deleted(fr);
-    std::vector<int> need;
-    for (int c : pcols) if (c >= 0) need.push_back(c);
-    auto cols = read_fragment(fr.file, need);
-    std::vector<uint32_t> del = fr.deleted;
-    std::vector<char> dead(fr.rows, 0);
-    for (auto d : del) if (d < fr.rows) dead[d] = 1;
-    uint64_t added = 0;
-    for (uint64_t r = 0; r < fr.rows; ++r) {
-      if (dead[r]) continue;
-      if (matches(cols, pcols, p, r)) { dead[r] = 1; ++added; }
-    }
-    if (added == 0) { keep.push_back(fr); continue; }
-    total += added;
-    uint64_t live = 0;
-    del.clear();
-    for (uint64_t r = 0; r < fr.rows; ++r) { if (dead[r]) del.push_back((uint32_t)r); else ++live; }
-    if (live == 0) continue;  // fragment fully deleted: drop from this version
-    std::string stem = fr.file.substr(0, fr.file.size() - 4);
-    char dn[128];
-    snprintf(dn, sizeof dn, "%s-%llu.del", stem.c_str(), (unsigned long long)nv);
-    FILE* f = fopen((dir_ + "/_deletions/" + dn).c_str(), "wb");
-    if (!f) throw std::runtime_error("colstore: cannot write deletion file");
-    uint64_t nd = del.size();
-    bool ok = fwrite(&nd, 8, 1, f) == 1 && fwrite(del.data(), 4, nd, f) == nd;
-    ok = (fclose(f) == 0) && ok;
-    if (!ok) throw std::runtime_error("colstore: short write of deletion file");
-    Fragment nf = fr;
-    nf.delfile = dn;
-    nf.deleted = del;
-    keep.push_back(nf);
+void Table::fix_dims(const std::vector<Column>& cols) {
+  for (size_t i = 0; i < schema_.size(); ++i) {
+    if (schema_[i].type != ColType::VecF32 || cols[i].size() == 0) continue;
+    if (schema_[i].dim == 0) schema_[i].dim = cols[i].dim;
+    if (schema_[i].dim != cols[i].dim) throw std::runtime_error("colstore: vector dim mismatch");
   }
-  m.frags = keep;
-  return total;
+}
+
+void Table::add_fragment(const std::string& file, uint64_t rows, const std::vector<Column>* cols) {
+  Frag f;
+  f.file = file;
+  f.rows = rows;
+  f.dead.assign(rows, 0);
+  frags_.push_back(std::move(f));
+  const uint32_t fi = (uint32_t)frags_.size() - 1;
+  if (!indexed_) return;
+  if (cols) {
+    for (uint64_t r = 0; r < rows; ++r) index_.emplace(make_key(*cols, r), std::make_pair(fi, (uint32_t)r));
+    indexed_frags_ = fi + 1;
+  } else {
+    index_fragment(fi);
+  }
+}
+
+void Table::write_fragment(const std::string& file, const std::vector<Column>& cols) {
+  arrow::FieldVector fields;
+  std::vector<std::shared_ptr<arrow::Array>> arrays;
+  for (size_t i = 0; i < cols.size(); ++i) {
+    ColSpec spec = schema_[i];
+    if (spec.type == ColType::VecF32) spec.dim = cols[i].dim ? cols[i].dim : spec.dim;
+    fields.push_back(arrow::field(spec.name, arrow_type(spec), false));
+    arrays.push_back(to_arrow(cols[i]));
+  }
+  auto sch = arrow::schema(fields);
+  const int64_t n = cols.empty() ? 0 : (int64_t)cols[0].size();
+  std::string tmp = dir_ + "/data/.tmp-" + uniq_name();
+  {
+    auto out = ok_or_throw(arrow::io::FileOutputStream::Open(tmp), "open fragment");
+    auto w = ok_or_throw(arrow::ipc::MakeFileWriter(out, sch), "fragment writer");
+    check(w->WriteRecordBatch(*arrow::RecordBatch::Make(sch, n, arrays)), "write fragment");
+    check(w->Close(), "close fragment");
+    check(out->Close(), "close fragment");
+  }
+  if (::rename(tmp.c_str(), (dir_ + "/data/" + file).c_str()) != 0)
+    throw std::runtime_error("colstore: fragment rename failed");
+}
+
+std::vector<Column> Table::read_fragment(const std::string& file, const std::vector<int>& want, uint64_t* nrows) {
+  auto mm = ok_or_throw(arrow::io::MemoryMappedFile::Open(dir_ + "/data/" + file, arrow::io::FileMode::READ),
+                        "open fragment");
+  auto rd = ok_or_throw(arrow::ipc::RecordBatchFileReader::Open(mm), "read fragment");
+  std::vector<Column> out(schema_.size());
+  for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
+  std::shared_ptr<arrow::RecordBatch> batch;
+  if (rd->num_record_batches() > 0) batch = ok_or_throw(rd->ReadRecordBatch(0), "fragment batch");
+  const uint64_t n = batch ? (uint64_t)batch->num_rows() : 0;
+  *nrows = n;
+  for (int ci : want) {
+    std::shared_ptr<arrow::Array> a = batch ? batch->GetColumnByName(schema_[ci].name) : nullptr;
+    from_arrow(a, out[ci], n);
+  }
+  return out;
+}
+
+uint64_t Table::append(const std::vector<Column>& cols_in) {
+  Predicate none;
+  return replace_where(none, cols_in, nullptr);
 }
 
 uint64_t Table::delete_where(const Predicate& p, uint64_t* n_deleted) {
   lock();
-  Manifest m;
   uint64_t total = 0;
   try {
-    m = load_latest();
-    const uint64_t nv = m.version + 1;
-    total = apply_delete(m, p, nv);
-    if (total > 0) {
-      m.version = nv;
-      write_manifest(m);
-    }
+    refresh();
+    const uint64_t nv = cur_version_ + 1;
+    total = apply_delete(p, nv);
+    if (total > 0) write_manifest(nv);
   } catch (...) { unlock(); throw; }
   unlock();
   if (n_deleted) *n_deleted = total;
-  return m.version;
+  return cur_version_;
 }
 
 // Delete every row matching p AND append cols in ONE committed version: a
@@ -424,42 +602,34 @@ uint64_t Table::replace_where(const Predicate& p, const std::vector<Column>& col
   if (cols_in.size() != schema_.size()) throw std::runtime_error("colstore: column count mismatch");
   const size_t n = cols_in.empty() ? 0 : cols_in[0].size();
   for (auto& c : cols_in) if (c.size() != n) throw std::runtime_error("colstore: ragged columns");
+  const bool has_pred = !p.eq.empty() || p.has_in;
   lock();
-  Manifest m;
   uint64_t total = 0;
   try {
-    m = load_latest();
-    for (size_t i = 0; i < schema_.size(); ++i) {
-      if (schema_[i].type == ColType::VecF32 && n > 0) {
-        uint32_t d = cols_in[i].dim;
-        for (auto& pc : m.schema) if (pc.name == schema_[i].name && pc.dim) schema_[i].dim = pc.dim;
-        if (schema_[i].dim == 0) schema_[i].dim = d;
-        if (schema_[i].dim != d) throw std::runtime_error("colstore: vector dim mismatch");
-      }
-    }
-    const uint64_t nv = m.version + 1;
-    total = apply_delete(m, p, nv);
+    refresh();
+    if (n > 0) fix_dims(cols_in);
+    const uint64_t nv = cur_version_ + 1;
+    if (has_pred) total = apply_delete(p, nv);
     if (n > 0) {
-      std::string file = uniq_name() + ".lzc";
+      std::string file = uniq_name() + ".arrow";
       write_fragment(file, cols_in);
-      Fragment fr;
-      fr.file = file;
-      fr.rows = n;
-      m.frags.push_back(fr);
+      add_fragment(file, n, &cols_in);
     }
-    m.version = nv;
-    write_manifest(m);
+    if (n > 0 || total > 0 || has_pred) write_manifest(nv);
   } catch (...) { unlock(); throw; }
   unlock();
   if (n_deleted) *n_deleted = total;
-  return m.version;
+  return cur_version_;
 }
 
 std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::string>& want_names) {
-  Manifest m = load_latest();
-  for (auto& c : schema_)
-    for (auto& pc : m.schema)
-      if (pc.name == c.name && c.type == ColType::VecF32 && c.dim == 0) c.dim = pc.dim;
+  lock();  // a consistent fragment list (writers append under the same lock)
+  std::vector<Frag> frags;
+  try {
+    refresh();
+    frags = frags_;
+  } catch (...) { unlock(); throw; }
+  unlock();
   std::vector<int> pcols;
   for (auto& kv : p.eq) pcols.push_back(col_index(kv.first));
   if (p.has_in) pcols.push_back(col_index(p.in_col));
@@ -473,16 +643,48 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
   for (int c : pcols) if (c >= 0 && std::find(need.begin(), need.end(), c) == need.end()) need.push_back(c);
   std::vector<Column> out(schema_.size());
   for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
-  for (auto& fr : m.frags) {
-    load_deleted(fr);
-    auto cols = read_fragment(fr.file, need);
-    std::vector<char> dead(fr.rows, 0);
-    for (auto d : fr.deleted) if (d < fr.rows) dead[d] = 1;
-    for (uint64_t r = 0; r < fr.rows; ++r) {
-      if (dead[r] || !matches(cols, pcols, p, r)) continue;
+  for (auto& fr : frags) {
+    if (fr.n_dead == fr.rows) continue;
+    uint64_t nrows = 0;
+    auto cols = read_fragment(fr.file, need, &nrows);
+    for (int c : want)
+      if (out[c].type == ColType::VecF32 && out[c].dim == 0) out[c].dim = cols[c].dim;
+    std::vector<uint32_t> sel;
+    sel.reserve(nrows);
+    for (uint64_t r = 0; r < nrows; ++r)
+      if (!fr.dead[r] && (pcols.empty() || matches(cols, pcols, p, r))) sel.push_back((uint32_t)r);
+    if (sel.size() == nrows) {  // the whole fragment (a tenant's commit): bulk moves
       for (int c : want) {
-        if (out[c].type == ColType::VecF32 && out[c].dim == 0) out[c].dim = cols[c].dim;
-        out[c].append_from(cols[c], r);
+        Column& o = out[c];
+        Column& s = cols[c];
+        switch (o.type) {
+          case ColType::Str: o.s.insert(o.s.end(), std::make_move_iterator(s.s.begin()), std::make_move_iterator(s.s.end())); break;
+          case ColType::F64: o.f64.insert(o.f64.end(), s.f64.begin(), s.f64.end()); break;
+          case ColType::F32: case ColType::VecF32: o.f32.insert(o.f32.end(), s.f32.begin(), s.f32.end()); break;
+          case ColType::I32: o.i32.insert(o.i32.end(), s.i32.begin(), s.i32.end()); break;
+          case ColType::I64: o.i64.insert(o.i64.end(), s.i64.begin(), s.i64.end()); break;
+          case ColType::Bool: o.b.insert(o.b.end(), s.b.begin(), s.b.end()); break;
+        }
+      }
+      continue;
+    }
+    for (int c : want) {
+      Column& o = out[c];
+      Column& s = cols[c];
+      switch (o.type) {
+        case ColType::Str: for (uint32_t r : sel) o.s.push_back(std::move(s.s[r])); break;
+        case ColType::F64: for (uint32_t r : sel) o.f64.push_back(s.f64[r]); break;
+        case ColType::F32: for (uint32_t r : sel) o.f32.push_back(s.f32[r]); break;
+        case ColType::I32: for (uint32_t r : sel) o.i32.push_back(s.i32[r]); break;
+        case ColType::I64: for (uint32_t r : sel) o.i64.push_back(s.i64[r]); break;
+        case ColType::Bool: for (uint32_t r : sel) o.b.push_back(s.b[r]); break;
+        case ColType::VecF32: {
+          const size_t d = s.dim, base = o.f32.size();
+          o.f32.resize(base + sel.size() * d);
+          for (size_t j = 0; j < sel.size(); ++j)
+            std::memcpy(o.f32.data() + base + j * d, s.f32.data() + (size_t)sel[j] * d, d * sizeof(float));
+          break;
+        }
       }
     }
   }
@@ -490,48 +692,49 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
 }
 
 uint64_t Table::count_rows() {
-  Manifest m = load_latest();
+  lock();
   uint64_t n = 0;
-  for (auto& fr : m.frags) { load_deleted(fr); n += fr.rows - fr.deleted.size(); }
+  try {
+    refresh();
+    for (auto& fr : frags_) n += fr.rows - fr.n_dead;
+  } catch (...) { unlock(); throw; }
+  unlock();
   return n;
 }
 
 uint64_t Table::compact() {
   lock();
-  Manifest m = load_latest();
-  if (m.frags.size() <= 1) {
-    bool clean = m.frags.empty() || m.frags[0].delfile.empty();
-    if (clean) { unlock(); return m.version; }
-  }
-  std::vector<int> all;
-  for (size_t i = 0; i < schema_.size(); ++i) all.push_back((int)i);
-  std::vector<Column> out(schema_.size());
-  for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
-  for (auto& fr : m.frags) {
-    load_deleted(fr);
-    auto cols = read_fragment(fr.file, all);
-    std::vector<char> dead(fr.rows, 0);
-    for (auto d : fr.deleted) if (d < fr.rows) dead[d] = 1;
-    for (uint64_t r = 0; r < fr.rows; ++r)
-      if (!dead[r])
-        for (size_t c = 0; c < schema_.size(); ++c) {
-          if (out[c].type == ColType::VecF32 && out[c].dim == 0) out[c].dim = cols[c].dim;
-          out[c].append_from(cols[c], r);
-        }
-  }
-  m.frags.clear();
-  if (!out.empty() && out[0].size() > 0) {
-    std::string file = uniq_name() + ".lzc";
-    write_fragment(file, out);
-    Fragment fr;
-    fr.file = file;
-    fr.rows = out[0].size();
-    m.frags.push_back(fr);
-  }
-  m.version += 1;
-  write_manifest(m);
+  try {
+    refresh();
+    bool clean = frags_.size() <= 1 && (frags_.empty() || frags_[0].n_dead == 0);
+    if (clean) { unlock(); return cur_version_; }
+    std::vector<int> all;
+    for (size_t i = 0; i < schema_.size(); ++i) all.push_back((int)i);
+    std::vector<Column> out(schema_.size());
+    for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
+    for (auto& fr : frags_) {
+      uint64_t nrows = 0;
+      auto cols = read_fragment(fr.file, all, &nrows);
+      for (uint64_t r = 0; r < nrows; ++r)
+        if (!fr.dead[r])
+          for (size_t c = 0; c < schema_.size(); ++c) {
+            if (out[c].type == ColType::VecF32 && out[c].dim == 0) out[c].dim = cols[c].dim;
+            out[c].append_from(cols[c], r);
+          }
+    }
+    frags_.clear();
+    index_.clear();
+    indexed_ = false;
+    indexed_frags_ = 0;
+    if (!out.empty() && out[0].size() > 0) {
+      std::string file = uniq_name() + ".arrow";
+      write_fragment(file, out);
+      add_fragment(file, out[0].size(), nullptr);
+    }
+    write_manifest(cur_version_ + 1);
+  } catch (...) { unlock(); throw; }
   unlock();
-  return m.version;
+  return cur_version_;
 }
 
 // Two-phase multi-writer commit: every rank writes its
@@ -544,38 +747,30 @@ std::pair<std::string, uint64_t> Table::stage(const std::vector<Column>& cols_in
   const size_t n = cols_in.empty() ? 0 : cols_in[0].size();
   for (auto& c : cols_in) if (c.size() != n) throw std::runtime_error("colstore: ragged columns");
   if (n == 0) return {"", 0};
-  std::string file = uniq_name() + ".lzc";
+  std::string file = uniq_name() + ".arrow";
   write_fragment(file, cols_in);
   return {file, n};
 }
 
 uint64_t Table::commit_staged(const std::vector<std::pair<std::string, uint64_t>>& frags, uint32_t vec_dim) {
   lock();
-  Manifest m;
   try {
-    m = load_latest();
+    refresh();
     for (auto& sc : schema_)
       if (sc.type == ColType::VecF32) {
-        for (auto& pc : m.schema) if (pc.name == sc.name && pc.dim) sc.dim = pc.dim;
         if (sc.dim == 0) sc.dim = vec_dim;
         if (vec_dim && sc.dim != vec_dim) throw std::runtime_error("colstore: vector dim mismatch");
       }
     bool any = false;
     for (auto& f : frags) {
       if (f.first.empty() || f.second == 0) continue;
-      Fragment fr;
-      fr.file = f.first;
-      fr.rows = f.second;
-      m.frags.push_back(fr);
+      add_fragment(f.first, f.second, nullptr);
       any = true;
     }
-    if (any) {
-      m.version += 1;
-      write_manifest(m);
-    }
+    if (any) write_manifest(cur_version_ + 1);
   } catch (...) { unlock(); throw; }
   unlock();
-  return m.version;
+  return cur_version_;
 }
 
 }  // namespace lzrt

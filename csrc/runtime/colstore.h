@@ -1,19 +1,30 @@
-// Versioned columnar table store (host runtime, C++17).
+// Versioned columnar table store (host runtime, C++20 + Arrow C++).
 //
 // Replaces the reference's LanceDB tables (vector_store.py:14-244): each table
 // lives in `{root}/{name}.lance/` with
-//   _versions/<v>.manifest   text manifest, written to a temp file + rename
-//   data/<frag>.lzc          immutable column segments (one per append)
-//   _deletions/<frag>-<v>.del sorted uint32 row offsets deleted in a fragment
+//   _versions/<v>.manifest    text manifest, written to a temp file + rename
+//   _latest                   the newest version number (O(1) version polls)
+//   data/<frag>.arrow         immutable fragments: Arrow IPC files, one record
+//                             batch, the table's schema (vector column =
+//                             fixed_size_list<float32>[dim], like LanceDB's);
+//                             readable by pyarrow.ipc without this runtime
+//   _deletions/<frag>-<v>.arrow  deleted row offsets of a fragment (uint32
+//                             column "row", Arrow IPC)
 // Commits take an flock on `<table>/_lock`, so several processes (memory
-// system + dashboard) can share a directory; versions are monotone and every
-// committed operation bumps the version (like Lance MVCC). Readers always see
-// the newest manifest. NOTE: the byte format is this framework's own segment
-// format, not Lance v2; Arrow IPC export/import is done in Python (pyarrow).
+// system + dashboard) share a directory; versions are monotone and every
+// committed operation bumps the version (like Lance MVCC).
+//
+// Keyed writes are O(changed rows): a table opened with key columns (nodes /
+// edges: user_id + id, profiles: user_id) keeps an in-memory key -> (fragment,
+// row) index, refreshed incrementally from the manifest when another process
+// commits, so an upsert / delete by key never scans the table. Other
+// predicates scan the memory-mapped fragments.
 #pragma once
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
 #include <utility>
 #include <vector>
@@ -42,14 +53,6 @@ struct Column {
   void append_from(const Column& o, size_t row);
 };
 
-struct Fragment {
-  std::string file;
-  uint64_t rows = 0;
-  std::string delfile;  // "" = none
-  std::vector<uint32_t> deleted;  // loaded lazily
-  bool del_loaded = false;
-};
-
 struct Predicate {
   // conjunction of equalities on string columns + optional IN on one string column
   std::vector<std::pair<std::string, std::string>> eq;
@@ -60,8 +63,9 @@ struct Predicate {
 
 class Table {
  public:
-  Table(std::string dir, std::vector<ColSpec> schema);
-  uint64_t latest_version();                          // re-reads disk
+  Table(std::string dir, std::vector<ColSpec> schema, std::vector<std::string> key_cols = {});
+  ~Table();
+  uint64_t latest_version();                          // reads `_latest`
   uint64_t append(const std::vector<Column>& cols);   // returns new version
   uint64_t delete_where(const Predicate& p, uint64_t* n_deleted);
   // atomic delete_where(p) + append(cols) in one version
@@ -75,26 +79,49 @@ class Table {
   uint64_t compact();  // rewrite live rows into one fragment (new version)
   const std::vector<ColSpec>& schema() const { return schema_; }
   int col_index(const std::string& name) const;
+  std::string fragment_dir() const { return dir_ + "/data"; }
 
  private:
-  struct Manifest {
-    uint64_t version = 0;
-    std::vector<ColSpec> schema;
-    std::vector<Fragment> frags;
+  struct Frag {
+    std::string file;
+    uint64_t rows = 0;
+    std::string delfile;      // "" = none
+    std::vector<uint8_t> dead;  // per row (loaded with the fragment's deletion file)
+    uint64_t n_dead = 0;
   };
   std::string dir_;
   std::vector<ColSpec> schema_;
-  Manifest load_latest();
-  uint64_t apply_delete(Manifest& m, const Predicate& p, uint64_t nv);
-  void write_manifest(const Manifest& m);
-  std::vector<Column> read_fragment(const std::string& file, const std::vector<int>& cols);
-  void write_fragment(const std::string& file, const std::vector<Column>& cols);
-  void load_deleted(Fragment& f);
-  bool matches(const std::vector<Column>& cols, const std::vector<int>& pcols,
-               const Predicate& p, size_t r) const;
+  std::vector<std::string> key_cols_;
+  std::vector<int> key_idx_;
+  // committed state this process has loaded (== the manifest of cur_version_)
+  uint64_t cur_version_ = 0;
+  std::vector<Frag> frags_;
+  // key -> (frag, row); a multimap: the edge id "{src}_{tgt}" repeats when
+  // two shards hold the same pair, and a keyed delete removes every row
+  std::unordered_multimap<std::string, std::pair<uint32_t, uint32_t>> index_;
+  bool indexed_ = false;
+  uint64_t indexed_frags_ = 0;  // fragments [0, indexed_frags_) are in index_
   int lock_fd_ = -1;
+  int lock_depth_ = 0;
+  std::recursive_mutex mu_;  // threads of this process (the flock is per process)
+
   void lock();
   void unlock();
+  void refresh();  // load the newest manifest (incrementally)
+  void read_manifest(uint64_t v, std::vector<Frag>& out, std::vector<ColSpec>* sch);
+  void write_manifest(uint64_t v);
+  void load_dead(Frag& f);
+  void write_dead(Frag& f, uint64_t v);
+  void ensure_index();
+  void index_fragment(uint32_t fi);
+  std::string make_key(const std::vector<Column>& cols, size_t r) const;
+  bool keyed(const Predicate& p, std::vector<std::string>* keys) const;
+  uint64_t apply_delete(const Predicate& p, uint64_t nv);
+  void add_fragment(const std::string& file, uint64_t rows, const std::vector<Column>* cols);
+  void fix_dims(const std::vector<Column>& cols);
+  std::vector<Column> read_fragment(const std::string& file, const std::vector<int>& want, uint64_t* nrows);
+  void write_fragment(const std::string& file, const std::vector<Column>& cols);
+  bool matches(const std::vector<Column>& cols, const std::vector<int>& pcols, const Predicate& p, size_t r) const;
 };
 
 }  // namespace lzrt

@@ -8,8 +8,9 @@ site-packages, so the GPU box loads exactly what this tree built):
   loaded with ctypes after ``import torch`` so it binds to the same HIP runtime
   (``libamdhip64.so.7``) torch already mapped.
 * ``lazzaro_amd/_lib/_lzrt*.so`` -- the host runtime (columnar versioned store,
-  WordPiece/hash tokenizer, CSR/graph utilities, tenant placement), C++17 +
-  pybind11, built with g++.
+  WordPiece/hash tokenizer, CSR/graph utilities, tenant placement), C++20 +
+  pybind11, built with g++ and linked against the Arrow C++ library inside
+  pyarrow (the store's fragments are Arrow IPC files).
 
 * ``lazzaro_amd/_lib/liblzk_debug.so`` -- the same kernels with
   ``-DLZK_DEBUG=1`` device bounds asserts. ``build_all`` always produces it
@@ -24,6 +25,7 @@ from __future__ import annotations
 
 import glob
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -130,9 +132,18 @@ def build_runtime(verbose: bool = False, sanitize: str = "", outdir: str = "") -
         opt = ["-O3"]
         if sanitize:
             opt = ["-O1", "-g", "-fno-omit-frame-pointer"] + [f"-fsanitize={x}" for x in sanitize.split(",") if x]
-        cmd = [cxx] + opt + ["-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+        # the columnar store writes / memory-maps Arrow IPC fragments with the
+        # Arrow C++ library that ships inside pyarrow (linked by soname + rpath)
+        import pyarrow as pa
+
+        pa_dir = pa.get_library_dirs()[0]
+        arrow_so = sorted(f for f in os.listdir(pa_dir) if re.fullmatch(r"libarrow\.so\.\d+", f))
+        if not arrow_so:
+            raise RuntimeError(f"no libarrow.so.<N> in {pa_dir} (pyarrow wheel)")
+        cmd = [cxx] + opt + ["-std=c++20", "-shared", "-fPIC", "-fvisibility=hidden",
                              "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
-                             "-I" + os.path.join(CSRC, "runtime")] + srcs + ["-o", out, "-lpthread"]
+                             "-I" + pa.get_include(), "-I" + os.path.join(CSRC, "runtime")] + srcs + [
+            "-o", out, "-L" + pa_dir, "-l:" + arrow_so[0], "-Wl,-rpath," + pa_dir, "-lpthread"]
         _run(cmd)
     return out
 

@@ -37,7 +37,7 @@ from typing import Dict, List, Sequence, Set, Tuple
 import numpy as np
 import torch
 
-from ..engine.tenant_graph import NODE, SHARD_MASK, TenantGraph
+from ..engine.tenant_graph import NODE, SHARD_MASK, TYPE_MASK, TenantGraph
 from ..utils.faults import EmbeddingError, ProviderError, degenerate_embedding
 from ..utils.tracing import tracer
 
@@ -796,8 +796,7 @@ class ConsolidationMixin:
             results.append(f"✓ Updated {updates} profile domains")
         else:
             with self._graph_lock:
-                rows = g.ordered_node_rows()
-                rows = rows[g.mirror("sup")[rows] == 0]
+                rows = g.ordered_node_rows_dev(super_=False)
                 contents = [g.content[r] for r in rows[:PROFILE_CONTENTS].tolist()]
             if len(contents) >= 3:
                 r = self._extract_profile_from_contents(contents)
@@ -934,4 +933,4 @@ class ConsolidationMixin:
         g.remove_edges(idx)
         s = torch.where(s == r_from, torch.full_like(s, r_to), s)
         d = torch.where(d == r_from, torch.full_like(d, r_to), d)
-        g.upsert_edges(s, d, w, meta & SHARD_MASK, (meta >> 24) & 0x3F, co=co, lu=lu)
+        g.upsert_edges(s, d, w, meta & SHARD_MASK, (meta >> 24) & TYPE_MASK, co=co, lu=lu)

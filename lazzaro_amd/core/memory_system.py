@@ -40,7 +40,7 @@ from typing import Dict, Iterable, List, Optional
 import numpy as np
 import torch
 
-from ..engine.tenant_graph import NODE, TenantGraph
+from ..engine.tenant_graph import NODE, TYPE_MASK, TenantGraph
 from ..engine.views import GraphBuffer, NodeView, ShardView, ShardsMap, SuperNodesMap, import_edges, import_nodes
 from ..models.graph import Edge, Node
 from . import providers as _providers
@@ -950,7 +950,7 @@ STORAGE:
                 order = order[live[order]]
                 et = g.etype_names
                 links = [{"source": ids[s[i]], "target": ids[d[i]], "weight": float(w[i]),
-                          "type": et[(meta[i] >> 24) & 0x3F]} for i in order.tolist()]
+                          "type": et[(meta[i] >> 24) & TYPE_MASK]} for i in order.tolist()]
             return {"nodes": nodes + supers, "links": links}
 
     def export_observations(self, format: str = "markdown") -> str:
@@ -1060,7 +1060,7 @@ def export_edge_columns(g: TenantGraph, idx: np.ndarray) -> Dict:
         "id": [f"{a}_{b}" for a, b in zip(src, dst)],
         "source_id": src, "target_id": dst,
         "weight": w.astype(np.float32),
-        "edge_type": [g.etype_names[(m >> 24) & 0x3F] for m in meta.tolist()],
+        "edge_type": [g.etype_names[(m >> 24) & TYPE_MASK] for m in meta.tolist()],
         "co_occurrence": co.astype(np.int32),
         "last_updated": lu.astype(np.float64),
         "metadata": ["{}"] * n,

@@ -37,7 +37,7 @@ Node columns (row-indexed; rows are never reused while referenced):
 * host lists: ``ids``, ``content``, ``types``; ``children`` (super rows).
 
 Edge columns: ``src/dst i32, w f32, co i32, lu f64, meta i32`` with ``meta =
-shard | type << 24 | dirty << 30``: the shard that stores the edge matters,
+shard | type << 24 | stored << 29 | dirty << 30``: the shard that stores the edge matters,
 because the reference's ``get_neighbors`` only sees edges of the node's own
 shard (``buffer_graph.py:72-77``); that visibility drives the neighbour boost.
 
@@ -68,8 +68,10 @@ FREE, NODE, GHOST = 0, 1, 2
 NEG_INF = float("-inf")
 SHARD_MASK = 0xFFFFFF
 TYPE_SHIFT = 24
-EDIRTY = 1 << 30
-MAX_ETYPES = 64
+TYPE_MASK = 0x1F
+ESTORED = 1 << 29  # the edge is in the persistent store (its removal must be committed)
+EDIRTY = 1 << 30  # changed since the last commit
+MAX_ETYPES = TYPE_MASK + 1
 
 # below this many query x row products the exact float64 GEMM is used directly
 KERNEL_MIN_WORK = 1 << 22
@@ -484,6 +486,18 @@ class TenantGraph:
         o = np.lexsort((live, key))
         return live[o]
 
+    def ordered_node_rows_dev(self, super_: Optional[bool] = None) -> torch.Tensor:
+        """:meth:`ordered_node_rows` as a device sort (no host mirror of the
+        columns); ``super_`` filters super / shard nodes."""
+        n = self.n
+        with self.on_stream():
+            m = self.kind[:n] == NODE
+            if super_ is not None:
+                m &= (self.sup[:n] != 0) == super_
+            live = torch.nonzero(m).flatten()
+            key = torch.where(self.sup[live] != 0, torch.full_like(live, -1), self.shard[live].long())
+            return live[torch.argsort((key + 1) * max(n, 1) + live)]
+
     def set_scalar(self, r: int, name: str, value) -> None:
         col = getattr(self, name)
         with self.on_stream():
@@ -619,7 +633,7 @@ class TenantGraph:
             k = int(bi.numel())
             et = etype.to(dev, torch.int32)[bi]
             tail = self.e["meta"][-k:]
-            self.e["meta"][-k:] = (tail & ~(0x3F << TYPE_SHIFT)) | (et << TYPE_SHIFT)
+            self.e["meta"][-k:] = (tail & ~(TYPE_MASK << TYPE_SHIFT)) | (et << TYPE_SHIFT)
             n_new = k
         self._bump(edges=True)
         return n_new
@@ -650,13 +664,19 @@ class TenantGraph:
             e = self.e
             idx = idx.to(self.device)
             if self.track:
-                self._note_dropped(e["src"][idx], e["dst"][idx])
+                self._note_dropped(e["src"][idx], e["dst"][idx], e["meta"][idx])
             keep = torch.ones(self.num_edges, dtype=torch.bool, device=self.device)
             keep[idx] = False
             self.e = {k: v[keep] for k, v in e.items()}
         self._bump(edges=True)
 
-    def _note_dropped(self, s: torch.Tensor, d: torch.Tensor) -> None:
+    def _note_dropped(self, s: torch.Tensor, d: torch.Tensor, meta: Optional[torch.Tensor] = None) -> None:
+        """Queue removed edges for deletion from the store -- only those the
+        store holds (ESTORED): an edge created and pruned between two
+        commits never reached it."""
+        if meta is not None:
+            keep = (meta & ESTORED) != 0
+            s, d = s[keep], d[keep]
         if s.numel() == 0:
             return
         ids = self.ids
@@ -857,7 +877,7 @@ class TenantGraph:
             wsum, wcnt = _seg_sum_count(lab[src], self.e["w"], n)
             ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1).double() > min_avg_w)
             # reference order: a component's first member in BufferGraph.nodes order
-            order = torch.as_tensor(self.ordered_node_rows(), dtype=torch.long).to(dev)
+            order = self.ordered_node_rows_dev()
             BIG = 1 << 62
             pos = torch.full((n,), BIG, dtype=torch.long, device=dev)
             pos[order] = torch.arange(order.numel(), device=dev)
@@ -1176,6 +1196,7 @@ class TenantGraph:
             m = (self.e["meta"] & EDIRTY) != 0
             idx = torch.nonzero(m).flatten()
             self.e["meta"] &= ~EDIRTY
+            self.e["meta"][idx] |= ESTORED
             return idx.cpu().numpy()
 
     def restore_tracking(self, rows, eidx, del_ids, del_edges) -> None:
@@ -1197,8 +1218,13 @@ class TenantGraph:
         self.deleted_ids, self.deleted_edges = {}, {}
         return ids, edges
 
-    def clear_tracking(self) -> None:
-        """Forget pending changes (the caller wrote a full snapshot)."""
+    def clear_tracking(self, stored: bool = True) -> None:
+        """Forget pending changes: the caller wrote a full snapshot
+        (``stored``), or the graph was filled from data the store does not
+        hold and none of it should ever be deleted from it (``stored=False``)."""
         self.take_dirty_rows()
         self.take_dirty_edges()
         self.take_deleted()
+        if not stored and self.num_edges:
+            with self.on_stream():
+                self.e["meta"] &= ~ESTORED

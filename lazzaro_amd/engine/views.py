@@ -35,7 +35,7 @@ import torch
 from ..core.memory_shard import MemoryShard
 from ..core.buffer_graph import BufferGraph
 from ..models.graph import Edge, Node
-from .tenant_graph import GHOST, NODE, SHARD_MASK, TYPE_SHIFT, EDIRTY, TenantGraph
+from .tenant_graph import GHOST, NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT, EDIRTY, TenantGraph
 
 DEFAULT_SHARD = "default"
 SALIENCE_FLOOR = 0.2
@@ -236,13 +236,13 @@ class EdgeView(Edge):
 
     @property
     def edge_type(self) -> str:
-        return self._g.etype_names[(int(self._get("meta")) >> TYPE_SHIFT) & 0x3F]
+        return self._g.etype_names[(int(self._get("meta")) >> TYPE_SHIFT) & TYPE_MASK]
 
     @edge_type.setter
     def edge_type(self, v: str) -> None:
         c = self._g.etype(v)
         m = int(self._get("meta"))
-        self._set("meta", (m & ~(0x3F << TYPE_SHIFT)) | (c << TYPE_SHIFT))
+        self._set("meta", (m & ~(TYPE_MASK << TYPE_SHIFT)) | (c << TYPE_SHIFT))
 
     def __eq__(self, other):
         if isinstance(other, EdgeView):

@@ -59,8 +59,8 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
     memory_shard.py:64-77), then, if ``threshold`` is not None, removal of
     edges with ``w < threshold`` (:79-84) with stable compaction.
 
-    Returns (edges, n_pruned, dropped) where ``dropped`` is (src, dst) of the
-    pruned edges when ``want_dropped`` (for incremental persistence)."""
+    Returns (edges, n_pruned, dropped) where ``dropped`` is (src, dst, meta)
+    of the pruned edges when ``want_dropped`` (for incremental persistence)."""
     ne = int(e["src"].numel())
     keep = 1.0 - rate
     nn = int(sal.numel()) if sal is not None else 0
@@ -77,7 +77,7 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
             return e, 0, dropped
         f = e["w"] >= threshold
         if want_dropped:
-            dropped = (e["src"][~f], e["dst"][~f])
+            dropped = (e["src"][~f], e["dst"][~f], e["meta"][~f])
         n_keep = int(f.sum())
         if n_keep == ne:
             return e, 0, dropped
@@ -94,7 +94,7 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
         return e, 0, dropped
     if want_dropped:
         f = flag[:ne] == 0
-        dropped = (e["src"][f], e["dst"][f])
+        dropped = (e["src"][f], e["dst"][f], e["meta"][f])
     out, n = _compact(e, flag, bc, ne)
     return out, n, dropped
 
@@ -110,7 +110,7 @@ def remove_edges_of(e: Dict[str, torch.Tensor], rm: torch.Tensor, shard: torch.T
     if not e["src"].is_cuda:
         s, d = e["src"].long(), e["dst"].long()
         drop = (rm[s].bool() & (shard[s] == es)) | (rm[d].bool() & (shard[d] == es))
-        dropped = (e["src"][drop], e["dst"][drop]) if want_dropped else None
+        dropped = (e["src"][drop], e["dst"][drop], e["meta"][drop]) if want_dropped else None
         n = int(drop.sum())
         if n == 0:
             return e, 0, dropped
@@ -126,7 +126,7 @@ def remove_edges_of(e: Dict[str, torch.Tensor], rm: torch.Tensor, shard: torch.T
     dropped = None
     if want_dropped:
         f = flag == 0
-        dropped = (e["src"][f], e["dst"][f])
+        dropped = (e["src"][f], e["dst"][f], e["meta"][f])
     out, n = _compact(e, flag, bc, ne)
     return out, n, dropped
 

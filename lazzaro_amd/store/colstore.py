@@ -4,9 +4,12 @@ Table layout mirrors the reference's LanceDB database
 (``{db_dir}/lancedb/{nodes,edges,profiles}``, reference vector_store.py:16-85):
 same table names, column names and logical types. Each
 table is a ``<name>.lance/`` directory holding versioned manifests, immutable
-column segments and deletion files written by the C++ runtime.
-``to_arrow``/``from_arrow`` give Arrow interchange (pyarrow) so data can be
-moved into a real LanceDB on a networked machine.
+fragments and deletion files written by the C++ runtime. Fragments and
+deletion files are Arrow IPC files (``data/*.arrow``, ``_deletions/*.arrow``)
+that pyarrow reads directly (:func:`read_fragments`); ``to_arrow`` gives the
+table's live rows as one ``pyarrow.Table`` for moving into a real LanceDB
+(``lance.write_dataset``) on a networked machine. The byte format of the
+Lance v2 file itself is not reproduced.
 """
 from __future__ import annotations
 
@@ -50,13 +53,21 @@ PROFILE_SCHEMA: List[Tuple[str, int, int]] = [
 _NP = {F64: np.float64, F32: np.float32, I32: np.int32, BOOL: np.uint8, I64: np.int64}
 
 
+# key columns of the reference's tables: a row is identified by (user_id, id)
+# (nodes, edges) or user_id (profiles); keyed upserts / deletes are O(rows
+# changed) through the runtime's in-memory key index
+KEYS = {"nodes": ["user_id", "id"], "edges": ["user_id", "id"], "profiles": ["user_id"]}
+
+
 class ColumnarTable:
-    def __init__(self, root: str, name: str, schema: List[Tuple[str, int, int]], dim: int = 0):
+    def __init__(self, root: str, name: str, schema: List[Tuple[str, int, int]], dim: int = 0,
+                 key_cols: Optional[Sequence[str]] = None):
         self.name = name
         self.path = os.path.join(root, name + ".lance")
         sch = [(n, t, (dim if t == VEC else d)) for n, t, d in schema]
         self.schema = sch
-        self._t = _rt().Table(self.path, sch)
+        keys = list(key_cols) if key_cols is not None else KEYS.get(name, [])
+        self._t = _rt().Table(self.path, sch, keys)
 
     @property
     def version(self) -> int:
@@ -168,6 +179,14 @@ class ColumnarTable:
             out.append({k: conv[k][i] for k in names})
         return out
 
+    def fragment_files(self) -> List[str]:
+        """Arrow IPC files of the fragments and deletion files on disk."""
+        out = []
+        for sub in ("data", "_deletions"):
+            d = os.path.join(self.path, sub)
+            out += sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(".arrow"))
+        return out
+
     def count(self) -> int:
         return int(self._t.count_rows())
 
@@ -210,3 +229,29 @@ class ColumnarTable:
             else:
                 cols[n] = np.asarray(col.to_pylist(), dtype=_NP[t])
         return self.add_columns(cols)
+
+
+def read_fragments(table_dir: str):
+    """The live rows of a table directory read with pyarrow alone (no
+    ``_lzrt``): the newest manifest's fragments minus their deletion files."""
+    import pyarrow as pa
+    import pyarrow.ipc as ipc
+
+    with open(os.path.join(table_dir, "_latest")) as f:
+        v = int(f.read().strip())
+    frags = []
+    with open(os.path.join(table_dir, "_versions", "%020d.manifest" % v)) as f:
+        for line in f:
+            p = line.split()
+            if p and p[0] == "frag":
+                frags.append((p[1], None if p[3] == "-" else p[3]))
+    parts = []
+    for fn, dl in frags:
+        t = ipc.open_file(os.path.join(table_dir, "data", fn)).read_all()
+        if dl:
+            dead = ipc.open_file(os.path.join(table_dir, "_deletions", dl)).read_all().column("row").to_numpy()
+            keep = np.ones(t.num_rows, dtype=bool)
+            keep[dead] = False
+            t = t.filter(pa.array(keep))
+        parts.append(t)
+    return pa.concat_tables(parts) if parts else None

@@ -427,3 +427,19 @@ def test_kmeans_hierarchy_mode_clusters_and_retrieves(tmp_path):
     ids = ms._optimized_retrieval(q.tolist(), "a query near centre 2")
     assert len(ids) == 5 and all(ms.buffer.get_node(i).content.startswith("cluster 2") for i in ids)
     ms.close()
+
+
+def test_ordered_node_rows_dev_matches_host():
+    import torch
+
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    g = TenantGraph(device="cpu", dim=4)
+    codes = [g.shard_id(f"s{i}") for i in range(3)]
+    rng = np.random.default_rng(1)
+    n = 300
+    g.add_nodes([f"n{i}" for i in range(n)], [""] * n, rng.standard_normal((n, 4)).astype(np.float32).tolist(),
+                shard=[codes[int(x)] for x in rng.integers(0, 3, n)], sup=[1 if i % 50 == 7 else 0 for i in range(n)])
+    g.remove_nodes([3, 4, 100])
+    assert g.ordered_node_rows_dev().tolist() == g.ordered_node_rows().tolist()
+    host = g.ordered_node_rows()
+    assert g.ordered_node_rows_dev(super_=False).tolist() == host[g.mirror("sup")[host] == 0].tolist()
