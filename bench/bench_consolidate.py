@@ -145,6 +145,10 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     comm.all_reduce(t, "max")
     el = float(t.item())
     g = ms.graph
+    from lazzaro_amd.utils.tracing import tracer
+    if tracer.enabled:  # LZK_TRACE=1: per-stage device time (hipEvents), warmup included
+        import json as _json
+        print(_json.dumps({"stages_ms": tracer.summary()}), flush=True)
     out = {"turns_per_s": round(convs * comm.world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
            "nodes_per_rank": nodes, "convs_per_rank_step": convs, "facts_per_conv": facts,
            "buffer_nodes_total": nodes * comm.world, "nodes_rank0": g.num_nodes(), "edges_rank0": g.num_edges,

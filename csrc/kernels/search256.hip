@@ -20,6 +20,8 @@
 
 #include <cstdlib>
 
+LZK_DEBUG_STATE(search256)
+
 namespace {
 
 using namespace g256;
@@ -131,7 +133,10 @@ struct BlkCands {
 // this pair (global dedupe/links + within-shard links, reference
 // memory_system.py:719-733 / :816-836 / :853-889) and the scan is MFMA-bound,
 // so fusing halves its cost.
-template <bool HAS_BIAS, bool HAS_LABEL, bool DUAL, int OPT = 0>
+// MMA = MmaFp8: the rows / queries are e4m3 bytes passed as u16 pairs (row
+// strides and D in u16 units), so one 128-B K-row feeds the block-scaled
+// 16x16x128 MFMA at twice the bf16 rate -- same LDS image and schedule.
+template <bool HAS_BIAS, bool HAS_LABEL, bool DUAL, int OPT = 0, class MMA = MmaBf16>
 __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
     const u16* __restrict__ X, long ldx, int nrows, const u16* __restrict__ Qm, long ldq, int nq, int D,
     const float* __restrict__ bias, const int* __restrict__ row_label, const int* __restrict__ q_label,
@@ -213,8 +218,8 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
       bar();
       stamp(1);
     }
-    if constexpr ((OPT & 8) != 0) body2<MmaBf16>(smem, st, KS, acc, !(OPT & 2), pre);
-    else body<MmaBf16, (OPT & 3)>(smem, st, KS, acc, pre);
+    if constexpr ((OPT & 8) != 0) body2<MMA>(smem, st, KS, acc, !(OPT & 2), pre);
+    else body<MMA, (OPT & 3)>(smem, st, KS, acc, pre);
     stamp(2);
     if (more) {
       st.setup(X, ldx, nr0, nrows, Qm, ldq, nc0, nq);
@@ -505,6 +510,54 @@ __global__ __launch_bounds__(256) void top1_decode_kernel(const unsigned long lo
   row[q] = (int)(0xFFFFFFFFu - (unsigned)(b & 0xFFFFFFFFull));
 }
 
+// Exact re-score of the candidate lists of a low-precision (fp8) scan: the
+// list entry (q, row) gets alpha * <Q16[q], X16[row]> + bias[row] from the
+// bf16 rows (fp32 accumulate), so the top-k select that follows ranks by the
+// same scores as the bf16 path. One 256-thread block per query, 4 waves take
+// alternate candidates; lanes read consecutive 8-B chunks of a row.
+__global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict__ X, long ldx,
+                                                           const u16* __restrict__ Qm, long ldq, int D,
+                                                           const float* __restrict__ bias, float alpha,
+                                                           const int* __restrict__ cnt, int cap,
+                                                           float* __restrict__ cs, const int* __restrict__ ci) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = min(cnt[q] & 0x3fffffff, cap);
+  const int chunks = D >> 2;  // 4 bf16 per 8-B chunk
+  constexpr int MAXC = 8;     // D <= 64 * 4 * MAXC = 2048
+  float qv[MAXC][4];
+#pragma unroll
+  for (int t = 0; t < MAXC; ++t) {
+    const int c = lane + 64 * t;
+    if (c < chunks) {
+      const uint2 u = *reinterpret_cast<const uint2*>(Qm + (long)q * ldq + 4 * c);
+      qv[t][0] = __uint_as_float(u.x << 16); qv[t][1] = __uint_as_float(u.x & 0xffff0000u);
+      qv[t][2] = __uint_as_float(u.y << 16); qv[t][3] = __uint_as_float(u.y & 0xffff0000u);
+    }
+  }
+  for (int p = wave; p < n; p += 4) {
+    const long idx = (long)q * cap + p;
+    const int r = ci[idx];
+    LZK_DCHECK(r >= 0);
+    const u16* xr = X + (long)r * ldx;
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < MAXC; ++t) {
+      const int c = lane + 64 * t;
+      if (c < chunks) {
+        const uint2 u = *reinterpret_cast<const uint2*>(xr + 4 * c);
+        acc = fmaf(qv[t][0], __uint_as_float(u.x << 16), acc);
+        acc = fmaf(qv[t][1], __uint_as_float(u.x & 0xffff0000u), acc);
+        acc = fmaf(qv[t][2], __uint_as_float(u.y << 16), acc);
+        acc = fmaf(qv[t][3], __uint_as_float(u.y & 0xffff0000u), acc);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) cs[idx] = alpha * acc + (bias ? bias[r] : 0.f);
+  }
+}
+
 }  // namespace
 
 // Exact argmax of Q @ X.T per query (no bias/labels). ws: [nq] u64 scratch.
@@ -713,4 +766,63 @@ LZK_EXPORT int lzk_cand_grid(int nrows, int nq, int dual) {
   const long nblk = (long)((nrows + BM - 1) / BM) * ((nq + BN - 1) / BN);
   if (dual) return (int)(nblk < g_n_cu ? nblk : g_n_cu);
   return (g_cand_persist && nblk >= g_n_cu) ? g_n_cu : 0;
+}
+
+// fp8 candidate pass (rows / queries: e4m3 bytes, row strides in bytes,
+// D_bytes % 128 == 0): score = alpha * <q8, x8> + bias[row] >= thr[q] is
+// appended to the block-private records (persistent grid = one block per CU).
+// Re-score the gathered lists exactly with lzk_cand_rescore before selecting.
+LZK_EXPORT int lzk_flat_cand_f8(const void* X8, long ldx_bytes, int nrows, const void* Q8, long ldq_bytes, int nq,
+                                int D_bytes, const float* bias, float alpha, const float* thr, int cap, int* cnt,
+                                float* cs, int* ci, void* blk_buf, int blk_cap, int* blk_cnt, void* stream) {
+  if (D_bytes % 128 != 0 || (ldx_bytes | ldq_bytes) % 16 != 0 || nq <= 0 || nrows <= 0 || cap <= 0)
+    return (int)hipErrorInvalidValue;
+  if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;
+  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt};
+  const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
+  const long nblk = (long)n_rt * n_qt;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X8;
+  const u16* q = (const u16*)Q8;
+#define LZK_GF(B)                                                                                                   \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, false, false, kCandOpt, MmaFp8>,          \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, false, false, kCandOpt, MmaFp8>), dim3(grid), dim3(NT),     \
+                       CAND_P_LDS, st, x, ldx_bytes / 2, nrows, q, ldq_bytes / 2, nq, D_bytes / 2, bias,            \
+                       (const int*)nullptr, (const int*)nullptr, alpha, thr, n_qt, (int)nblk, cap, cnt, cs, ci,      \
+                       (const float*)nullptr, (int*)nullptr, (float*)nullptr, (int*)nullptr, blk);                  \
+  } while (0)
+  if (bias) LZK_GF(true);
+  else LZK_GF(false);
+#undef LZK_GF
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  const long nblk = (long)((nrows + BM - 1) / BM) * ((nq + BN - 1) / BN);
+  return (int)(nblk < g_n_cu ? nblk : g_n_cu);
+}
+
+// Exact bf16 re-score of candidate lists in place (see cand_rescore_kernel).
+LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long ldq, int nq, int D, const float* bias,
+                                float alpha, const int* cnt, int cap, float* cs, const int* ci, void* stream) {
+  if (D % 4 != 0 || D > 2048 || nq <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cand_rescore_kernel, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, (const u16*)X16, ldx,
+                     (const u16*)Q16, ldq, D, bias, alpha, cnt, cap, cs, ci);
+  return (int)hipGetLastError();
 }

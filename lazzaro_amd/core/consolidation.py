@@ -514,7 +514,8 @@ class ConsolidationMixin:
             self.conversation_count += B
             if self.auto_consolidate and (self.conversation_count // self.consolidate_every
                                           > c0 // self.consolidate_every):
-                self.run_consolidation()
+                with tracer.stage("run_consolidation", self._device):
+                    self.run_consolidation()
             self._maybe_cluster(c0)
             self._save_to_persistence()
         return stats
@@ -572,7 +573,7 @@ class ConsolidationMixin:
 
         # ---- 1. one scan of the batch against the pre-batch graph
         if g.n:
-            with g.on_stream():
+            with g.on_stream(), tracer.stage("cb_scan", self._device):
                 (gb_r, gb_s, gb_node), (gs, gr), (ws, wr) = self._scan_batch(Q, torch.as_tensor(codes))
         else:
             gb_r = torch.full((M,), -1, dtype=torch.long, device=dev)
@@ -608,7 +609,8 @@ class ConsolidationMixin:
         sal_dec = decayed(sal_in, left)
 
         # ---- 3. decay + prune the pre-batch graph by B conversations at once
-        stats["pruned"] += g.decay(1.0 - keep ** B, thr)
+        with tracer.stage("cb_decay", self._device):
+            stats["pruned"] += g.decay(1.0 - keep ** B, thr)
 
         # ---- 4. duplicate merges (reference :736-740)
         ndup = int(dup.sum())
@@ -637,9 +639,10 @@ class ConsolidationMixin:
             return
         kfacts = [facts[i] for i in kh]
         ids = [self._generate_node_id() for _ in kh]
-        rows = g.add_nodes(ids, [f["content"] for f in kfacts], Q[kidx], shard=codes[kh],
-                           types=[f.get("type", "semantic") for f in kfacts], sal=sal_new[kidx].float(),
-                           acc=acc_new[kidx], now=now, stored=self._store_binds_graph())
+        with tracer.stage("cb_insert", self._device):
+            rows = g.add_nodes(ids, [f["content"] for f in kfacts], Q[kidx], shard=codes[kh],
+                               types=[f.get("type", "semantic") for f in kfacts], sal=sal_new[kidx].float(),
+                               acc=acc_new[kidx], now=now, stored=self._store_binds_graph())
         stats["inserted"] += int(kh.size)
         if not self._store_binds_graph():
             self.vector_store.add_nodes([
@@ -652,7 +655,9 @@ class ConsolidationMixin:
         new_row[kidx] = rows.to(dev)
 
         # ---- 6. links of the kept facts (reference :797-891), pre-decayed
-        self._link_batch_multi(kidx, new_row, codes, ct, S, earlier, (ws, wr), (gs, gr), keep, B, thr, now, stats)
+        with tracer.stage("cb_link", self._device):
+            self._link_batch_multi(kidx, new_row, codes, ct, S, earlier, (ws, wr), (gs, gr), keep, B, thr, now,
+                                   stats)
         if self.enable_hierarchy and getattr(self, "hierarchy_mode", "reference") == "reference":
             for skey in dict.fromkeys(shard_keys[j] for j in kh.tolist()):
                 c = g.shard_code.get(skey)

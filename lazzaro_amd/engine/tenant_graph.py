@@ -54,6 +54,7 @@ Deliberate differences (documented in docs/INVENTORY.md):
 from __future__ import annotations
 
 import math
+import os
 import threading
 import time
 from contextlib import contextmanager
@@ -76,6 +77,10 @@ MAX_ETYPES = TYPE_MASK + 1
 # below this many query x row products the exact float64 GEMM is used directly
 KERNEL_MIN_WORK = 1 << 22
 CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-rank
+# fp8 candidate scan of the store search: large batches over large tenants
+# (the candidate kernel's regime), margin in standard deviations of the fp8
+# score error (see TenantGraph._fp8_candidates)
+FP8_MIN_Q, FP8_MIN_ROWS, FP8_MARGIN_Z = 256, 1 << 20, 8.0
 
 
 def _pad64(d: int) -> int:
@@ -149,7 +154,9 @@ class TenantGraph:
         z = lambda dt: torch.zeros(0, dtype=dt, device=self.device)  # noqa: E731
         self.e = {"src": z(torch.int32), "dst": z(torch.int32), "w": z(torch.float32), "co": z(torch.int32),
                   "lu": z(torch.float64), "meta": z(torch.int32)}
-        self.emb32 = self.emb16 = self.sqn = None
+        self.emb32 = self.emb16 = self.emb8 = self.sqn = None
+        self.sumsq = None  # per-dimension sum of x_i^2 over inserted rows (fp8 error model)
+        self.n_sumsq = 0
         for name, dt, _ in self.NODE_COLS:
             setattr(self, name, z(dt))
         if dim:
@@ -192,15 +199,34 @@ class TenantGraph:
             e32 = torch.zeros((cap, self.dim), dtype=torch.float32, device=dev)
             sq = torch.zeros(cap, dtype=torch.float32, device=dev)
             e16 = torch.zeros((cap, self.Dp), dtype=torch.bfloat16, device=dev) if self.on_gpu else None
+            e8 = torch.zeros((cap, self.Dp), dtype=torch.uint8, device=dev) if self._fp8_ok() else None
             if self.cap and self.emb32 is not None and self.emb32.shape[1] == self.dim:
                 e32[:n] = self.emb32[:n]
                 sq[:n] = self.sqn[:n]
                 if e16 is not None:
                     e16[:n] = self.emb16[:n]
-            self.emb32, self.sqn, self.emb16 = e32, sq, e16
+                if e8 is not None and self.emb8 is not None:
+                    e8[:n] = self.emb8[:n]
+            self.emb32, self.sqn, self.emb16, self.emb8 = e32, sq, e16, e8
+            if self.sumsq is None or self.sumsq.numel() != self.dim:
+                self.sumsq = torch.zeros(self.dim, dtype=torch.float64, device=dev)
         for k, v in new.items():
             setattr(self, k, v)
         self.cap = cap
+
+    # fp8 (e4m3) copy of the rows for the store search's candidate scan
+    # (ops.search.flat_topk_fp8): rows are scaled by FP8_ROW_SCALE, which
+    # keeps unit-norm rows (|x_i| <= 1) inside e4m3's normal range
+    FP8_ROW_SCALE = 64.0
+    FP8_SCAN = os.environ.get("LZK_SEARCH_FP8", "1") != "0"
+
+    def _fp8_ok(self) -> bool:
+        return self.on_gpu and self.FP8_SCAN and self.Dp % 128 == 0
+
+    def _write_fp8(self, rt, e32: torch.Tensor) -> None:
+        if self.emb8 is not None:
+            from ..ops.search import quantize_e4m3
+            self.emb8[rt, : self.dim] = quantize_e4m3(e32, self.FP8_ROW_SCALE)
 
     def reserve(self, n: int) -> None:
         if n > self.cap:
@@ -375,6 +401,9 @@ class TenantGraph:
             self.sqn[rt] = nrm2.float()
             if self.emb16 is not None:
                 self.emb16[rt, : self.dim] = e32.to(torch.bfloat16)
+            self._write_fp8(rt, e32)
+            self.sumsq += (e32.double() ** 2).sum(0)
+            self.n_sumsq += m
             self.has_emb[rt] = has.to(torch.uint8)
             if info is None or any(info[0]):
                 dv = torch.where(has, (nrm2.sqrt() - 1.0).abs(), torch.zeros_like(nrm2)).max()
@@ -529,6 +558,8 @@ class TenantGraph:
                     self.has_emb[r] = 0
                     if self.emb16 is not None:
                         self.emb16[r] = 0
+                    if self.emb8 is not None:
+                        self.emb8[r] = 0
             self._bump(store=True)
             return
         if self.dim is None:
@@ -546,6 +577,7 @@ class TenantGraph:
             self.dirty[r] = 1
             if self.emb16 is not None:
                 self.emb16[r, : self.dim] = v.to(torch.bfloat16)
+            self._write_fp8(r, v[None, :])
         self.max_norm_dev = max(self.max_norm_dev, abs(math.sqrt(n2) - 1.0))
         self._bump(store=True)
 
@@ -758,9 +790,26 @@ class TenantGraph:
         with self.on_stream():
             score = T.importance(self.sal[:n], self.acc[:n], self.last[:n], self.kind[:n], self.sup[:n], now)
             okey = self.shard[:n].long() * (1 << 32) + torch.arange(n, device=self.device)
-            o1 = torch.sort(okey, stable=True).indices
-            o2 = torch.sort(score[o1], stable=True).indices
-            order = o1[o2][:excess]
+            if excess * 64 < n:
+                # k-th smallest score by radix select, then the tied rows in
+                # (shard, row) order by a top-k: O(n) passes instead of two
+                # full stable sorts of the tenant
+                t = torch.kthvalue(score, excess).values
+                lt = torch.nonzero(score < t).flatten()
+                m = excess - int(lt.numel())
+                big = torch.iinfo(torch.int64).max
+                tie_key = torch.where(score == t, okey, torch.full_like(okey, big))
+                tv, ti = torch.topk(tie_key, m, largest=False, sorted=True)
+                ti = ti[tv != big]
+                # victims in the sequential order: score, then (shard, row)
+                cand = torch.cat([lt, ti])
+                o1 = torch.sort(okey[cand], stable=True).indices
+                cand = cand[o1]
+                order = cand[torch.sort(score[cand], stable=True).indices]
+            else:
+                o1 = torch.sort(okey, stable=True).indices
+                o2 = torch.sort(score[o1], stable=True).indices
+                order = o1[o2][:excess]
             order = order[torch.isfinite(score[order])]
             victims = order.tolist()
         self.remove_nodes(victims, drop_edges=True, unstore=True)
@@ -1055,9 +1104,34 @@ class TenantGraph:
         kc = min(CAND_SLOTS, max(k, 2 * k))
         if self.on_gpu and k <= CAND_SLOTS and (metric != "cosine" or self.unit_rows()) \
                 and M * n >= KERNEL_MIN_WORK // 16:
-            _, cand = flat_topk(self.emb16[:n], self._q16(Qf), kc, bias=bias, alpha=alpha)
+            q16 = self._q16(Qf)
+            if self.emb8 is not None and self.unit_rows() and M >= FP8_MIN_Q and n >= FP8_MIN_ROWS:
+                _, cand = self._fp8_candidates(Qf, q16, kc, bias, alpha)
+            else:
+                _, cand = flat_topk(self.emb16[:n], q16, kc, bias=bias, alpha=alpha)
             return self._rerank_store(Qf, cand, k, metric, bias)
         return self._exact_store(Qf, k, metric, bias)
+
+    def _fp8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
+        """Store-search candidates from the fp8 scan (rows in ``emb8``),
+        re-scored from the bf16 rows. The threshold margin covers the fp8
+        rounding of rows and queries: with relative rounding error u = 2^-4
+        per element (e4m3), <q,x> is off by about
+        u * sqrt(2/3) * sqrt(sum_i q_i^2 E[x_i^2]) (E over the tenant's rows,
+        tracked per dimension); the margin is FP8_MARGIN_Z of those, plus the
+        subnormal floor."""
+        from ..ops.search import flat_topk_fp8, quantize_e4m3
+        n = self.n
+        qmax = float(Qf.abs().max().clamp_min(1e-30))
+        sq = 64.0 / qmax
+        q8 = torch.zeros((Qf.shape[0], self.Dp), dtype=torch.uint8, device=self.device)
+        q8[:, : self.dim] = quantize_e4m3(Qf, sq)
+        mu2 = (self.sumsq / max(self.n_sumsq, 1)).to(torch.float64)
+        sig = (2.0 / 3.0) ** 0.5 * 2.0 ** -4 * torch.sqrt((Qf.double() ** 2 * mu2[None, :]).sum(1))
+        floor = 2.0 ** -9 * (1.0 / self.FP8_ROW_SCALE + 1.0 / sq) * Qf.double().abs().sum(1).clamp_min(1.0)
+        margin = (abs(alpha) * (FP8_MARGIN_Z * sig + floor)).float().contiguous()
+        return flat_topk_fp8(self.emb8, q8, self.FP8_ROW_SCALE * sq, self.emb16[:n], q16, kc, bias=bias,
+                             alpha=alpha, margin=margin)
 
     def _store_scores(self, Qf, X, sqn, bias, metric):
         dot = Qf @ X.T if X.dim() == 2 else torch.einsum("md,mcd->mc", Qf, X)

@@ -294,6 +294,66 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
     return _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap)
 
 
+_lib.register("lzk_flat_cand_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F,
+                                           _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
+_lib.register("lzk_cand_grid_f8", _lib.I, [_lib.I, _lib.I])
+_lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
+                                           _lib.I, _lib.P, _lib.P, _lib.P])
+
+FP8_MAX = 448.0
+
+
+def quantize_e4m3(x: torch.Tensor, scale: float, out: torch.Tensor = None) -> torch.Tensor:
+    """x * scale as OCP e4m3 bytes (uint8), saturated to +-448."""
+    q = (x.float() * scale).clamp_(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    if out is not None:
+        out.copy_(q)
+        return out
+    return q
+
+
+def flat_topk_fp8(X8: torch.Tensor, Q8: torch.Tensor, scale2: float, X16: torch.Tensor, Q16: torch.Tensor, k: int,
+                  *, bias=None, alpha: float = 1.0, margin=None):
+    """Top-k of ``alpha * <Q, X> + bias`` with the candidate scan on the fp8
+    MFMA (twice the bf16 rate, half the bytes) and exact bf16 scores for the
+    candidates.
+
+    X8 / Q8: e4m3 bytes [N, Dp] / [nq, Dp] of X16 / Q16 times per-tensor
+    scales with product ``scale2`` (Dp % 128 == 0); X16 / Q16 the bf16 rows
+    and queries. ``margin`` [nq] (fp32, >= 0): the fp8 error allowance -- the
+    sampled threshold (exact bf16 k-th best of a 1/S row sample, a lower bound
+    of the true k-th score) is lowered by it, so a row whose exact score clears
+    the true k-th best stays a candidate unless its fp8 error exceeds the
+    margin. Candidates are re-scored from the bf16 rows (``cand_rescore``) and
+    selected exactly; overflowed lists go to the exact bf16 fallback.
+    Returns (scores fp32 [nq, k], rows int64 [nq, k]) like :func:`flat_topk`."""
+    L = _lib.lib()
+    nq, Dp = Q16.shape
+    N = X16.shape[0]
+    kslot = L.lzk_flat_topk_kslot(int(k))
+    assert kslot > 0 and X8.dtype == torch.uint8 and Q8.dtype == torch.uint8 and Dp % 128 == 0
+    assert X8.shape[1] == Dp and X8.stride(1) == 1 and Q8.stride(1) == 1 and X8.shape[0] >= N
+    dev = X16.device
+    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
+    thr = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
+    if margin is not None:
+        thr = (thr - margin).contiguous()
+    cap = max(2048, 32 * kslot * S)
+    cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    grid = L.lzk_cand_grid_f8(N, nq)
+    bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 4 * S, 1)
+    st = _lib.stream_ptr(dev)
+    _lib.check(L.lzk_flat_cand_f8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp, _lib.ptr(bias),
+                                  float(alpha / scale2), thr.data_ptr(), cap, cnt.data_ptr(), cs.data_ptr(),
+                                  ci.data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st), "lzk_flat_cand_f8")
+    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
+                                 ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
+    _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
+                                  _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(), st),
+               "lzk_cand_rescore")
+    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
+
+
 # Speculative list-B threshold of flat_topk_dual (LZK_DUAL_SPEC=1): aim for
 # this many expected label rows above it. Off by default: on the 10M x 1024
 # consolidation shape it cuts the scan 13.93 -> 12.90 ms (bench/probe_dual_thr.py:

@@ -269,3 +269,63 @@ def test_search_memories_stream_matches_batch_gpu(tmp_path):
     got = [[[n.id for n in r] for r in res] for res in ms.search_memories_stream(batches, limit=10)]
     assert got == want and all(len(r) == 10 for b in got for r in b)
     ms.close()
+
+
+@pytest.mark.parametrize("data", ["isotropic", "clustered"])
+def test_store_search_fp8_scan_exact_recall_gpu(data):
+    """Large tenant (> FP8_MIN_ROWS) + large batch: candidates from the fp8
+    MFMA scan with the error-model margin, re-scored from bf16 and re-ranked
+    in fp32 == exact fp32 L2 top-10 over the original vectors."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    g = TenantGraph(device=DEV)
+    N, D = (1 << 20) + 4096, 768
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    if data == "isotropic":
+        X = torch.randn(N, D, device=DEV, generator=gen)
+    else:
+        C = torch.randn(256, D, device=DEV, generator=gen)
+        X = C[torch.randint(0, 256, (N,), device=DEV, generator=gen)] + 0.5 * torch.randn(N, D, device=DEV,
+                                                                                        generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
+    assert g.emb8 is not None
+    Q = torch.randn(512, D, device=DEV, generator=gen)
+    if data == "clustered":
+        Q = X[torch.randint(0, N, (512,), device=DEV, generator=gen)] + 0.3 * Q / D ** 0.5
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    assert 512 >= TG.FP8_MIN_Q and N >= TG.FP8_MIN_ROWS
+    _, rows = g.store_search(Q, 10, "l2")
+    Xd, Qd = X.double(), Q.double()
+    truth = []
+    for c0 in range(0, N, 1 << 18):
+        s = 2 * Qd @ Xd[c0:c0 + (1 << 18)].T - (Xd[c0:c0 + (1 << 18)] ** 2).sum(1)[None, :]
+        v, i = torch.topk(s, 10, dim=1)
+        truth.append((v, i + c0))
+    v = torch.cat([t[0] for t in truth], 1)
+    i = torch.cat([t[1] for t in truth], 1)
+    top = torch.gather(i, 1, torch.topk(v, 10, dim=1).indices)
+    hit = sum(len(set(a) & set(b)) for a, b in zip(rows.cpu().tolist(), top.cpu().tolist()))
+    assert hit / (512 * 10) == 1.0
+    # and the bf16 scan gives the same rows
+    TG.TenantGraph.FP8_SCAN, g.emb8 = False, None
+    _, rows16 = g.store_search(Q, 10, "l2")
+    TG.TenantGraph.FP8_SCAN = True
+    assert torch.equal(rows16, rows)
+
+
+def test_flat_topk_fp8_matches_bf16_candidates_gpu():
+    from lazzaro_amd.ops.search import flat_topk, flat_topk_fp8, quantize_e4m3
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    N, D, nq = 1_500_000, 384, 768
+    X = torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    Q = torch.randn(nq, D, device=DEV, generator=gen)
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
+    bias = -(X * X).sum(1).contiguous()
+    s16, r16 = flat_topk(X16, Q16, 10, bias=bias, alpha=2.0)
+    X8, Q8 = quantize_e4m3(X, 64.0), quantize_e4m3(Q, 64.0)
+    margin = torch.full((nq,), 0.04, device=DEV)
+    s8, r8 = flat_topk_fp8(X8, Q8, 64.0 * 64.0, X16, Q16, 10, bias=bias, alpha=2.0, margin=margin)
+    same = sum(len(set(a) & set(b)) for a, b in zip(r8.cpu().tolist(), r16.cpu().tolist())) / (nq * 10)
+    assert same >= 0.999 and torch.allclose(s8, s16, atol=1e-4, rtol=0)

@@ -443,3 +443,27 @@ def test_ordered_node_rows_dev_matches_host():
     assert g.ordered_node_rows_dev().tolist() == g.ordered_node_rows().tolist()
     host = g.ordered_node_rows()
     assert g.ordered_node_rows_dev(super_=False).tolist() == host[g.mirror("sup")[host] == 0].tolist()
+
+
+def test_evict_select_matches_full_sort_with_ties():
+    """Eviction's radix-select + top-k path == the full (importance, shard,
+    row) order, with heavy score ties (reference :541-578 victim order)."""
+    import torch
+
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    from lazzaro_amd.ops import tenant_ops as T
+    rng = np.random.default_rng(2)
+    n = 20000
+    g = TenantGraph(device="cpu", dim=4)
+    codes = [g.shard_id(f"s{i}") for i in range(4)]
+    sh = rng.integers(0, 4, n)
+    g.add_nodes([f"n{i}" for i in range(n)], [""] * n, rng.standard_normal((n, 4)).astype(np.float32).tolist(),
+                shard=[codes[int(x)] for x in sh], sal=rng.choice([0.3, 0.5, 0.7], n).astype(np.float32),
+                acc=rng.integers(0, 3, n), last=np.full(n, 1000.0), sup=[1 if i % 997 == 0 else 0 for i in range(n)])
+    now = 5000.0
+    score = T.importance(g.sal[:n], g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now).numpy()
+    okey = np.asarray(g.shard[:n]).astype(np.int64) * (1 << 32) + np.arange(n)
+    excess = 150
+    want = np.lexsort((okey, score))[:excess].tolist()
+    got = g.evict(g.num_nodes() - excess, now=now)
+    assert got == want
