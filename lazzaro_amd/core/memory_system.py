@@ -387,18 +387,18 @@ class MemorySystem(ConsolidationMixin):
         elif self.enable_hierarchy and g.n_super:
             sr = self._super_best(query_emb)
             if sr >= 0:
-                kind, sup = g.mirror("kind"), g.mirror("sup")
-                for cid in g.children.get(sr, [])[:SUPER_CHILDREN]:
-                    r = g.row_of.get(cid)
-                    if r is not None and kind[r] == NODE and not sup[r]:
-                        retrieved.append(cid)
+                kids = [(cid, g.row_of.get(cid)) for cid in g.children.get(sr, [])[:SUPER_CHILDREN]]
+                kids = [(cid, r) for cid, r in kids if r is not None]
+                kind, sup = g.flags_of([r for _, r in kids])
+                retrieved += [cid for (cid, _), k, sp in zip(kids, kind, sup) if k == NODE and not sp]
                 if len(retrieved) >= RESULT_LIMIT:
                     if self.query_cache:
                         self.query_cache.set_results(query_text, retrieved[:RESULT_LIMIT])
                     return retrieved[:RESULT_LIMIT]
         limit = 10 if not retrieved else 5
         vec_ids = self.vector_store.search_nodes(query_emb, user_id=self.user_id, limit=limit)
-        kind = g.mirror("kind")
+        vrows = [g.row_of.get(rid, -1) for rid in vec_ids]
+        vkind = dict(zip(vrows, g.flags_of([r for r in vrows if r >= 0])[0])) if vrows else {}
         seen_ids = set(retrieved)
         seen_content = set()
         final = []
@@ -409,7 +409,7 @@ class MemorySystem(ConsolidationMixin):
             if rid in seen_ids:
                 continue
             r = g.row_of.get(rid)
-            if r is not None and kind[r] == NODE and g.content[r] not in seen_content:
+            if r is not None and vkind.get(r) == NODE and g.content[r] not in seen_content:
                 seen_content.add(g.content[r])
                 final.append(rid)
                 seen_ids.add(rid)
@@ -551,8 +551,8 @@ class MemorySystem(ConsolidationMixin):
             if o_ not in seen:
                 seen.add(o_)
                 out.append(o_)
-        kind = g.mirror("kind")
-        return [NodeView.of(g, x) for x in out if kind[x] == NODE]
+        kind = g.flags_of(out)[0]
+        return [NodeView.of(g, x) for x, k in zip(out, kind) if k == NODE]
 
     def search_memories(self, query: str, limit: int = 5) -> List[Node]:
         with tracer.stage("embed_query", self._device):
@@ -597,6 +597,11 @@ class MemorySystem(ConsolidationMixin):
                     and embs.shape[-1] == g.dim and len(queries)):
                 with tracer.stage("search", self._device):
                     _, rows = g.store_search(embs, int(limit), getattr(self.store, "metric", "l2"))
+                    # rows the graph does not hold as nodes are skipped (reference
+                    # :1467-1472): marked on the device, so mapping needs no mirror
+                    with g.on_stream():
+                        rows = torch.where((rows >= 0) & (g.kind[rows.clamp_min(0)] == NODE), rows,
+                                           torch.full_like(rows, -1))
                 if rows.is_cuda:
                     host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
                     host.copy_(rows, non_blocking=True)
@@ -613,15 +618,15 @@ class MemorySystem(ConsolidationMixin):
             ev.synchronize()
         with self._graph_lock:
             g = self.graph
-            kind = g.mirror("kind")
-            if kind_ == "rows" and g is g0:
-                return [[NodeView.of(g, r) for r in row if r >= 0 and kind[r] == NODE] for row in data.tolist()]
+            if kind_ == "rows" and g is g0:  # non-node rows were set to -1 on the device
+                return [[NodeView.of(g, r) for r in row if r >= 0] for row in data.tolist()]
             if kind_ == "rows":  # the tenant was switched while the search ran
                 data = [[g0.ids[r] for r in row if r >= 0] for row in data.tolist()]
             out = []
             for ids in data:
-                rows = [g.row_of.get(i, -1) for i in ids]
-                out.append([NodeView.of(g, r) for r in rows if r >= 0 and kind[r] == NODE])
+                rows = [r for r in (g.row_of.get(i, -1) for i in ids) if r >= 0]
+                kind = g.flags_of(rows)[0]
+                out.append([NodeView.of(g, r) for r, k in zip(rows, kind) if k == NODE])
             return out
 
     # ------------------------------------------------------------ stats / display
@@ -815,8 +820,10 @@ STORAGE:
         eidx = g.take_dirty_edges()
         del_ids, del_edges = g.take_deleted()
         try:
-            kind = g.mirror("kind")
-            rows = rows[kind[rows] == NODE] if rows.size else rows
+            if rows.size:  # kind of the dirty rows only (no mirror of the whole column)
+                with g.on_stream():
+                    k = g.kind[torch.as_tensor(rows).to(g.device)].cpu().numpy()
+                rows = rows[k == NODE]
             node_cols = export_node_columns(g, rows)
             edge_cols = export_edge_columns(g, eidx)
             self.store.commit_tenant(self.user_id, node_cols, del_ids, edge_cols,

@@ -218,7 +218,12 @@ class TenantGraph:
     # (ops.search.flat_topk_fp8): rows are scaled by FP8_ROW_SCALE, which
     # keeps unit-norm rows (|x_i| <= 1) inside e4m3's normal range
     FP8_ROW_SCALE = 64.0
-    FP8_SCAN = os.environ.get("LZK_SEARCH_FP8", "1") != "0"
+    # Off by default: on 10M x 768 x 1024 queries the fp8 candidate kernel
+    # measured 12.1 ms vs 13.4 ms bf16, but the wider fp8 margin grows the
+    # lists ~5x and their bf16 re-score costs 5.9 ms, so the whole store
+    # search is 19.8 vs 14.2 ms (bench/ab_fp8_search.py,
+    # profiles/ab_fp8_search_r2.json). LZK_SEARCH_FP8=1 turns it on.
+    FP8_SCAN = os.environ.get("LZK_SEARCH_FP8", "0") == "1"
 
     def _fp8_ok(self) -> bool:
         return self.on_gpu and self.FP8_SCAN and self.Dp % 128 == 0
@@ -488,6 +493,20 @@ class TenantGraph:
         self._mirror[name] = (self.version, a)
         return a
 
+    def flags_of(self, rows: Sequence[int]) -> Tuple[np.ndarray, np.ndarray]:
+        """(kind, sup) of a few rows by one device gather -- the hot paths
+        (retrieval, search result mapping) must not mirror whole columns of a
+        multi-million-row tenant after every mutation."""
+        if len(rows) == 0:
+            return np.zeros(0, np.uint8), np.zeros(0, np.uint8)
+        m = self._mirror.get("kind")
+        if m is not None and m[0] == self.version and len(m[1]) == self.n:
+            return m[1][np.asarray(rows)], self.mirror("sup")[np.asarray(rows)]
+        with self.on_stream():
+            rt = torch.as_tensor(np.asarray(rows), dtype=torch.long).to(self.device)
+            both = torch.stack([self.kind[rt], self.sup[rt]]).cpu().numpy()
+        return both[0], both[1]
+
     def kind_h(self, r: int) -> int:
         return int(self.mirror("kind")[r])
 
@@ -737,14 +756,25 @@ class TenantGraph:
         edge endpoint) and -- ``drop_edges`` -- its own shard's incident edges go
         (reference ``_enforce_buffer_limit`` :558-569). Returns #removed."""
         rl = rows.tolist() if torch.is_tensor(rows) else list(rows)
-        if not rl:
+        cand = sorted({r for r in rl if 0 <= r < self.n})
+        if not cand:
             return 0
-        kind = self.mirror("kind")
-        live = sorted({r for r in rl if 0 <= r < self.n and kind[r] == NODE})
+        # kind / sup / shard of just these rows (one small copy, no mirror of
+        # the whole tenant's columns)
+        with self.on_stream():
+            ct = torch.as_tensor(cand, dtype=torch.long).to(self.device)
+            info = torch.stack([self.kind[ct].int(), self.sup[ct].int(), self.shard[ct]]).cpu().numpy()
+        keep = info[0] == NODE
+        live = [r for r, k in zip(cand, keep) if k]
         if not live:
             return 0
-        for r in live:
-            self._unlink_row(r)
+        for r, sp, sh in zip(live, info[1][keep].tolist(), info[2][keep].tolist()):
+            if sp:
+                self.n_super -= 1
+            elif sh >= 0:
+                self.shard_count[sh] -= 1
+            self.children.pop(r, None)
+            self.odd_emb.pop(r, None)
         with self.on_stream():
             rt = torch.as_tensor(live, dtype=torch.long).to(self.device)
             if drop_edges and self.num_edges:
@@ -791,10 +821,10 @@ class TenantGraph:
             score = T.importance(self.sal[:n], self.acc[:n], self.last[:n], self.kind[:n], self.sup[:n], now)
             okey = self.shard[:n].long() * (1 << 32) + torch.arange(n, device=self.device)
             if excess * 64 < n:
-                # k-th smallest score by radix select, then the tied rows in
-                # (shard, row) order by a top-k: O(n) passes instead of two
-                # full stable sorts of the tenant
-                t = torch.kthvalue(score, excess).values
+                # the k-th smallest score (a top-k: torch.kthvalue is ~100x
+                # slower on ROCm), then the tied rows in (shard, row) order by
+                # a top-k: O(n) passes instead of two full stable sorts
+                t = torch.topk(score, excess, largest=False, sorted=False).values.max()
                 lt = torch.nonzero(score < t).flatten()
                 m = excess - int(lt.numel())
                 big = torch.iinfo(torch.int64).max

@@ -277,6 +277,7 @@ def test_store_search_fp8_scan_exact_recall_gpu(data):
     MFMA scan with the error-model margin, re-scored from bf16 and re-ranked
     in fp32 == exact fp32 L2 top-10 over the original vectors."""
     from lazzaro_amd.engine import tenant_graph as TG
+    TG.TenantGraph.FP8_SCAN = True
     g = TenantGraph(device=DEV)
     N, D = (1 << 20) + 4096, 768
     gen = torch.Generator(device=DEV).manual_seed(7)
@@ -309,7 +310,6 @@ def test_store_search_fp8_scan_exact_recall_gpu(data):
     # and the bf16 scan gives the same rows
     TG.TenantGraph.FP8_SCAN, g.emb8 = False, None
     _, rows16 = g.store_search(Q, 10, "l2")
-    TG.TenantGraph.FP8_SCAN = True
     assert torch.equal(rows16, rows)
 
 
