@@ -70,8 +70,10 @@ def build_tenant(dev, nodes: int, dim: int, encoder, seed: int, db_dir: str, clu
                       db_dir=db_dir, load_from_disk=False, enable_async=False, max_buffer_size=nodes,
                       hierarchy_mode="kmeans", hierarchy_params={"fine": n_fine, "top": n_top,
                                                                  "every": cluster_convs, "iters": cluster_iters})
-    populate(ms, nodes, dim, dev, seed=seed)
     g = ms.graph
+    g._set_dim(dim)
+    g.reserve(int(nodes * 1.02) + 4096)  # inserts get fresh rows: headroom so the timed steps never re-allocate
+    populate(ms, nodes, dim, dev, seed=seed)
     if init_edges:
         gen = torch.Generator(device=dev).manual_seed(seed + 1)
         src = torch.randint(0, nodes, (init_edges,), device=dev, generator=gen)
