@@ -17,9 +17,14 @@ vector_store.py:132-140):
 Nothing is skipped inside the timed region; host tokenisation and result
 mapping of one batch overlap the device work of the next (serving pipeline).
 
-Scaling is weak: every GPU owns its own 10M-row tenant (tenant-DP, the
-framework's primary scale-out axis) and serves that tenant's query stream, so
-the whole-job value is the sum over GPUs. Data is synthetic: random unit
+Scaling is weak: the job is a ``DistributedMemoryService`` (one process per
+GPU, RCCL); every GPU owns a 10M-row tenant (tenant-DP, the framework's
+primary scale-out axis, placed by rendezvous hashing) and serves the query
+stream of its tenants -- front ends route users to owners with the same hash,
+so the timed path has no collective -- and the whole-job value is the sum over
+GPUs. The routed path (queries for remote tenants: all-to-all there and back)
+and the global cross-tenant search (all-gather + merge) are measured
+separately under "serving". Data is synthetic: random unit
 vectors for the stored memories, synthetic query sentences, random-init
 encoder weights (no checkpoints offline).
 
@@ -130,32 +135,59 @@ def main():
     ap.add_argument("--consolidate-steps", type=int, default=5,
                     help="second half of the metric: timed consolidation steps on a --rows-node buffer (0 = skip)")
     ap.add_argument("--consolidate-convs", type=int, default=128, help="conversations per GPU per step")
+    ap.add_argument("--cpu", action="store_true", help="CPU / gloo dry run of the whole flow (tests only)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    if a.cpu:
+        if world > 1:
+            dist.init_process_group("gloo")
+        dev = torch.device("cpu")
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
 
     from lazzaro_amd.core.embedders import OnDeviceEmbedder
     from lazzaro_amd.core.memory_system import MemorySystem
     from lazzaro_amd.core.providers import LocalLLM
     from lazzaro_amd.ops.search import flat_topk
+    from lazzaro_amd.parallel import Communicator
+    from lazzaro_amd.parallel.service import DistributedMemoryService
 
     rng = random.Random(1234 + rank)
     emb = OnDeviceEmbedder(a.model, device=dev, max_len=a.max_len, seed=0)
     assert emb.dim == a.dim, f"model width {emb.dim} != --dim {a.dim}"
-    tmp = tempfile.mkdtemp(prefix="lzbench_")
-    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, device=dev, db_dir=tmp,
-                      load_from_disk=False, enable_async=False, max_buffer_size=2 * a.rows,
-                      user_id=f"tenant{rank}")
+    # the serving layer: tenants placed on ranks by rendezvous hashing; each
+    # rank's tenant is the first name the placement gives it (a real HRW
+    # assignment), holding --rows memories in this GPU's HBM
+    comm = Communicator() if world > 1 else Communicator.local(dev)
+    tmp = os.environ.get("LZK_BENCH_DB") or tempfile.mkdtemp(prefix="lzbench_")
+
+    def factory(user):
+        return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, device=dev, db_dir=tmp,
+                            load_from_disk=False, enable_async=False, max_buffer_size=2 * a.rows, user_id=user)
+
+    svc = DistributedMemoryService(comm, factory)
+    tenants = {}
+    for j in range(100000):
+        o = svc.owner(f"tenant{j}")
+        tenants.setdefault(o, f"tenant{j}")
+        if len(tenants) == world:
+            break
+    me = tenants[rank]
+    ms = svc.system(me)
     t_load = time.perf_counter()
     populate(ms, a.rows, a.dim, dev, seed=100 + rank)
-    torch.cuda.synchronize()
+    sync()
     t_load = time.perf_counter() - t_load
     g = ms.graph
     pool = [synth_texts(a.batch, rng) for _ in range(4)]
@@ -165,18 +197,18 @@ def main():
 
     for _ in ms.search_memories_stream(batches(a.warmup), limit=a.k):
         pass
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     n_res = 0
     for res in ms.search_memories_stream(batches(a.steps), limit=a.k):
         n_res += len(res)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     el = time.perf_counter() - t0
     assert n_res == a.steps * a.batch
     if world > 1:
@@ -185,21 +217,46 @@ def main():
         el = float(t.item())
     qps = world * a.batch * a.steps / el
 
+    # ---- untimed: the routed path (requests for every rank's tenant cross the
+    # network: one all-to-all-v of the queries, one back with the results) and
+    # a global cross-tenant search (all-gather of candidates + merge) ----
+    routed = {}
+    if world > 1:
+        reqs = [(tenants[r], "search_memories", q, a.k) for r in range(world) for q in pool[1][: a.batch // world]]
+        svc.serve(reqs)
+        sync()
+        dist.barrier()
+        t1 = time.perf_counter()
+        out = svc.serve(reqs)
+        sync()
+        dist.barrier()
+        routed["routed_search_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+        routed["routed_queries_per_rank"] = len(reqs)
+        assert all(len(r) == a.k for r in out)
+        qv = emb.batch_embed_tensor(pool[2][:1])[0]
+        svc.search_global(qv, limit=a.k)
+        t1 = time.perf_counter()
+        svc.search_global(qv, limit=a.k)
+        routed["global_search_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+
     # ---- untimed: breakdown + recall vs float64 truth over the fp32 vectors ----
     def timeit(fn, n=3):
         fn()
-        torch.cuda.synchronize()
+        sync()
         t1 = time.perf_counter()
         for _ in range(n):
             out = fn()
-        torch.cuda.synchronize()
+        sync()
         return (time.perf_counter() - t1) / n * 1e3, out
 
     t_embed, Qe = timeit(lambda: emb.batch_embed_tensor(pool[0]))
     t_store, (_, rows_e) = timeit(lambda: g.store_search(Qe, a.k, "l2"))
-    Xb, bias = g.emb16[: g.n], g.store_bias("l2")
-    q16 = g._q16(Qe)
-    t_kernel, _ = timeit(lambda: flat_topk(Xb, q16, 16, bias=bias, alpha=2.0))
+    Xb = bias = q16 = None
+    t_kernel = None
+    if dev.type == "cuda":  # the bare candidate-scan kernel, for reference
+        Xb, bias = g.emb16[: g.n], g.store_bias("l2")
+        q16 = g._q16(Qe)
+        t_kernel, _ = timeit(lambda: flat_topk(Xb, q16, 16, bias=bias, alpha=2.0))
     t_batch, res0 = timeit(lambda: ms.search_memories_batch(pool[0], limit=a.k))
     nr = min(a.recall_queries, a.batch)
     _, truth_e = exact_l2_topk(g, Qe[:nr], a.k)
@@ -217,13 +274,12 @@ def main():
     # ---- second half of the metric: consolidate turns/sec ----
     consolidate = None
     if a.consolidate_steps > 0:
-        ms.close()
-        del ms, g, Xb, bias, q16, Qe, res0, api_rows
-        torch.cuda.empty_cache()
+        svc.close()
+        del ms, g, Xb, bias, q16, Qe, res0, api_rows, svc
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
-        from lazzaro_amd.parallel import Communicator
-        comm = Communicator() if world > 1 else Communicator.local(dev)
         consolidate = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
                                       dim=a.dim)
     res = {
@@ -239,15 +295,18 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random unit fp32 memory vectors, synthetic query texts, random-init encoder weights)",
-        "config": {"model": "bge-base-en (d=768) on-device embed + MemorySystem.search_memories top-%d over a "
-                            "%d x %d fp32 tenant per GPU (L2, fp32 re-rank)" % (a.k, a.rows, a.dim),
+        "config": {"model": "%s (d=%d) on-device embed + MemorySystem.search_memories top-%d over a "
+                            "%d x %d fp32 tenant per GPU (L2, fp32 re-rank)"
+                            % ({"bge-base": "bge-base-en"}.get(a.model, a.model), a.dim, a.k, a.rows, a.dim),
                    "global_batch": world * a.batch, "seq_len": S_tok, "parallelism": "tenant-dp%d" % world},
-        "path": "MemorySystem.search_memories_stream (pipelined search_memories_batch)",
+        "path": "DistributedMemoryService -> owner's MemorySystem.search_memories_stream (pipelined "
+                "search_memories_batch); tenants placed by rendezvous hashing, one per GPU",
+        "serving": routed,
         "recall_at_10": round(rec_api, 4),
         "recall_at_10_random_queries": round(rec_rand, 4),
         "recall_truth": "float64 exact L2 over the stored fp32 vectors",
         "breakdown_ms": {"embed": round(t_embed, 3), "store_search": round(t_store, 3),
-                         "raw_scan_kernel": round(t_kernel, 3), "search_memories_batch_unpipelined": round(t_batch, 3)},
+                         "raw_scan_kernel": None if t_kernel is None else round(t_kernel, 3), "search_memories_batch_unpipelined": round(t_batch, 3)},
         "tokens_per_query": {"padded": S_tok, "real_mean": round(float(lens.float().mean()), 2)},
         "load_s": round(t_load, 1),
     }

@@ -1,0 +1,212 @@
+"""DistributedMemoryService: the MemorySystem API served by a one-process-per-
+GPU job (tenant-DP).
+
+Every tenant (``user_id``) is owned by exactly one rank (rendezvous hashing,
+:mod:`.placement`); the owner holds the tenant's ``MemorySystem`` -- its graph
+in that GPU's HBM -- and all ranks share one versioned columnar store
+directory, so ownership can move (elastic re-placement) by reloading from it.
+The reference is a single-process library (memory_system.py:21-1550); its
+per-user flows map onto this service as:
+
+* per-tenant calls -- ``chat``, ``search_memories`` (batched per tenant),
+  ``end_conversation``, ``add_to_short_term``, ``get_stats``,
+  ``get_connected_memories``, ``export_observations``, ``run_consolidation`` ...
+  -- execute on the owner. :meth:`serve` is the SPMD entry point: every rank
+  passes the requests its front end received (any tenant); requests for
+  remote tenants travel to their owner in ONE all-to-all-v of serialized
+  bytes (C3 over RCCL/xGMI or gloo), results come back the same way. Local
+  requests never touch the network.
+* ``get_all_users`` -- the tenant directory: store users plus every rank's
+  resident tenants, all-gathered (C7; reference :1430-1439).
+* :meth:`search_global` -- one query against EVERY tenant (cross-tenant /
+  global search): each rank runs the fused top-k over its resident tenants,
+  then an all-gather of the (score, tenant, node) candidates and a merge (C1
+  + K2) give every rank the same exact global top-k.
+
+All collective methods must be called by every rank in the same order.
+"""
+from __future__ import annotations
+
+import json
+from collections import OrderedDict
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+from .comm import Communicator
+from .placement import tenant_rank
+
+# tenant methods a remote request may invoke (the public per-user API)
+ALLOWED = {"chat", "search_memories", "end_conversation", "start_conversation", "add_to_short_term",
+           "get_stats", "get_connected_memories", "export_observations", "run_consolidation", "get_insights",
+           "consolidate_batch", "display_stats", "display_memories", "display_profile", "graph_json"}
+
+
+def node_dict(n) -> Dict:
+    """A Node (or NodeView) as the JSON the service returns."""
+    return {"id": n.id, "content": n.content, "type": n.type, "salience": float(n.salience),
+            "shard_key": n.shard_key, "access_count": int(n.access_count), "is_super_node": bool(n.is_super_node)}
+
+
+def _jsonable(v):
+    if hasattr(v, "id") and hasattr(v, "content") and hasattr(v, "salience"):
+        return node_dict(v)
+    if isinstance(v, (list, tuple)):
+        return [_jsonable(x) for x in v]
+    if isinstance(v, dict):
+        return {str(k): _jsonable(x) for k, x in v.items()}
+    if isinstance(v, (str, int, float, bool)) or v is None:
+        return v
+    if torch.is_tensor(v):
+        return v.tolist()
+    return str(v)
+
+
+class DistributedMemoryService:
+    def __init__(self, comm: Communicator, factory: Callable[[str], object], owner: Callable[[str], int] = None,
+                 max_resident: int = 1 << 30):
+        """``factory(user_id)`` builds the tenant's MemorySystem on this rank
+        (sharing one store / embedder / device); ``owner`` overrides the
+        rendezvous-hash placement (e.g. :class:`~.elastic.ElasticPlacement`);
+        at most ``max_resident`` tenants stay in memory (LRU; an evicted
+        tenant is persisted and reloaded from the store on its next request)."""
+        self.comm = comm
+        self.factory = factory
+        self._owner = owner
+        self.max_resident = max_resident
+        self.systems: "OrderedDict[str, object]" = OrderedDict()
+
+    # ------------------------------------------------------------ placement
+    def owner(self, user: str) -> int:
+        return self._owner(user) if self._owner is not None else tenant_rank(user, self.comm.world)
+
+    def is_local(self, user: str) -> bool:
+        return self.owner(user) == self.comm.rank
+
+    def system(self, user: str):
+        """The resident MemorySystem of a tenant this rank owns."""
+        if not self.is_local(user):
+            raise KeyError(f"tenant {user!r} is owned by rank {self.owner(user)}, not {self.comm.rank}")
+        ms = self.systems.get(user)
+        if ms is None:
+            ms = self.factory(user)
+            self.systems[user] = ms
+            while len(self.systems) > self.max_resident:
+                _, old = self.systems.popitem(last=False)
+                old._save_to_persistence()
+                old.close()
+        else:
+            self.systems.move_to_end(user)
+        return ms
+
+    # ------------------------------------------------------------ request routing
+    def _exchange(self, outgoing: List[List]) -> List[List]:
+        """outgoing[r] = JSON-able items for rank r -> items received per rank."""
+        comm = self.comm
+        if comm.world == 1:
+            return outgoing
+        payload = [json.dumps(x).encode() for x in outgoing]
+        dev = comm.device
+        send = torch.tensor([len(p) for p in payload], dtype=torch.int64, device=dev)
+        recv = comm.exchange_counts(send)
+        buf = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if sum(map(len, payload)) else \
+            torch.zeros(0, dtype=torch.uint8)
+        got = comm.all_to_all_v(buf.to(dev), send.tolist(), recv.tolist()).cpu().numpy().tobytes()
+        out, off = [], 0
+        for n in recv.tolist():
+            out.append(json.loads(got[off: off + n].decode()) if n else [])
+            off += n
+        return out
+
+    def serve(self, requests: Sequence[Tuple]) -> List:
+        """SPMD: ``requests`` = [(user_id, method, args...)] received by this
+        rank's front end. Each runs on the tenant's owner -- remote ones via
+        one all-to-all-v there and one back -- in this rank's order per
+        tenant; ``search_memories`` requests of one tenant are batched into a
+        single ``search_memories_batch``. Returns one JSON-able result per
+        request (Nodes as dicts)."""
+        comm = self.comm
+        out_req: List[List] = [[] for _ in range(comm.world)]
+        for i, req in enumerate(requests):
+            user, method = req[0], req[1]
+            if method not in ALLOWED:
+                raise ValueError(f"method {method!r} is not served")
+            out_req[self.owner(user)].append([i, user, method, list(req[2:])])
+        inbox = self._exchange(out_req)
+        replies: List[List] = [[] for _ in range(comm.world)]
+        for src, items in enumerate(inbox):
+            replies[src] = self._execute(items)
+        back = self._exchange(replies)
+        result: List = [None] * len(requests)
+        for items in back:
+            for i, r in items:
+                result[i] = r
+        return result
+
+    def _execute(self, items: List[List]) -> List[List]:
+        """Run one source rank's requests on this (owner) rank, in order;
+        consecutive search_memories of a tenant form one batch."""
+        out = []
+        j = 0
+        while j < len(items):
+            i, user, method, args = items[j]
+            ms = self.system(user)
+            if method == "search_memories":
+                k = j
+                qs, ids, limit = [], [], args[1] if len(args) > 1 else 5
+                while k < len(items) and items[k][1] == user and items[k][2] == "search_memories" and \
+                        (items[k][3][1] if len(items[k][3]) > 1 else 5) == limit:
+                    ids.append(items[k][0])
+                    qs.append(items[k][3][0])
+                    k += 1
+                res = ms.search_memories_batch(qs, limit=limit)
+                out += [[ii, [node_dict(n) for n in r]] for ii, r in zip(ids, res)]
+                j = k
+                continue
+            out.append([i, _jsonable(getattr(ms, method)(*args))])
+            j += 1
+        return out
+
+    # ------------------------------------------------------------ directory (C7)
+    def get_all_users(self) -> List[str]:
+        mine = set(self.systems)
+        for ms in list(self.systems.values())[:1]:
+            try:
+                mine |= set(ms.get_all_users())
+            except Exception:
+                pass
+        parts = self.comm.all_gather_object(sorted(mine))
+        return sorted({u for p in parts for u in p})
+
+    # ------------------------------------------------------------ global search (C1 + K2)
+    def search_global(self, query_emb: torch.Tensor, limit: int = 5, metric: str = "l2") -> List[Dict]:
+        """Top-``limit`` over every resident tenant of every rank for one
+        query vector (exact store scores: -|q-x|^2 for L2). Returns the same
+        list of {user_id, node...} dicts on every rank."""
+        comm = self.comm
+        cands = []
+        for user, ms in self.systems.items():
+            g = ms.graph
+            if g.dim is None or g.dim != query_emb.numel():
+                continue
+            with ms._graph_lock:
+                s, r = g.store_search(query_emb.reshape(1, -1).to(g.device), limit, metric)
+                s, r = s[0].cpu().tolist(), r[0].cpu().tolist()
+                for sc, row in zip(s, r):
+                    if row >= 0 and g.kind_h(row) == 1:
+                        cands.append((sc, user, row, node_dict(_view(g, row))))
+        cands.sort(key=lambda c: (-c[0], c[1], c[2]))
+        cands = cands[:limit]
+        parts = comm.all_gather_object([(c[0], c[1], c[2], c[3]) for c in cands])
+        allc = sorted((c for p in parts for c in p), key=lambda c: (-c[0], c[1], c[2]))[:limit]
+        return [dict(user_id=u, score=sc, **nd) for sc, u, _, nd in allc]
+
+    def close(self) -> None:
+        for ms in self.systems.values():
+            ms.close()
+        self.systems.clear()
+
+
+def _view(g, row):
+    from ..engine.views import NodeView
+    return NodeView.of(g, row)
