@@ -50,6 +50,11 @@ class MemoryConfig:
     nprobe: int = 32
     pq_m: int = 64
     ivf_min_rows: int = 1_000_000
+    hierarchy_mode: str = "reference"     # reference (one mean super-node per shard) | kmeans (two-level)
+    hierarchy_fine: int = 4096            # kmeans: fine clusters
+    hierarchy_top: int = 64               # kmeans: top-level clusters
+    hierarchy_every: int = 50             # kmeans: re-cluster every N conversations
+    strict_errors: bool = False
     verbose: bool = False
     extra: Dict[str, Any] = field(default_factory=dict)
 

@@ -196,6 +196,10 @@ class MemorySystem(ConsolidationMixin):
         kw.setdefault("index", cfg.index)
         kw.setdefault("index_params", {"nlist": cfg.nlist, "nprobe": cfg.nprobe, "pq_m": cfg.pq_m,
                                        "ivf_min_rows": cfg.ivf_min_rows})
+        kw.setdefault("hierarchy_mode", cfg.hierarchy_mode)
+        kw.setdefault("hierarchy_params", {"fine": cfg.hierarchy_fine, "top": cfg.hierarchy_top,
+                                           "every": cfg.hierarchy_every})
+        kw.setdefault("strict_errors", cfg.strict_errors)
         return cls(**cfg.reference_kwargs(), embedding_provider=emb, device=cfg.device, metric=cfg.metric,
                    merge_mode=cfg.merge_mode, verbose=cfg.verbose, **kw)
 

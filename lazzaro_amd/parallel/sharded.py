@@ -6,8 +6,8 @@
   Q*k*12 bytes per rank: latency-bound, tens of microseconds on xGMI) -> merge
   (K2). Every rank gets the same exact global top-k.
 * :func:`distributed_components` -- connected components over edges spread
-  across ranks (C5): local hook/compress on a replicated parent array, then an
-  all-reduce(MIN) of the parents until no rank changes anything.
+  across ranks (C5): local hook/compress once, then boundary-label exchange
+  (all-to-all-v of only the shared vertices whose label changed).
 """
 from __future__ import annotations
 
@@ -63,21 +63,94 @@ class ShardedIndex:
         return merge_topk(gs, gi, k)
 
 
-def distributed_components(comm: Communicator, src: torch.Tensor, dst: torch.Tensor, n_global: int,
-                           w: Optional[torch.Tensor] = None, min_w: float = 0.0, max_rounds: int = 64) -> torch.Tensor:
-    """Global component labels (min node id) for edges partitioned across ranks."""
-    label = G.connected_components(src, dst, n_global, w, min_w).to(torch.int64)
-    for _ in range(max_rounds):
-        before = label.clone()
-        comm.all_reduce(label, "min")
-        # re-hook locally: edges whose endpoints now carry different labels
-        ls = label[src.long()]
-        ld = label[dst.long()]
-        s2 = torch.cat([ls, torch.arange(n_global, device=label.device)])
-        d2 = torch.cat([ld, label])
-        label = G.connected_components(s2.to(torch.int32), d2.to(torch.int32), n_global).to(torch.int64)
-        changed = torch.tensor([int(not torch.equal(label, before))], device=label.device)
-        comm.all_reduce(changed, "max")
-        if int(changed.item()) == 0:
+def _route(comm: Communicator, dest: torch.Tensor, rows: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Send ``rows[i]`` to rank ``dest[i]`` (one all-to-all-v). Returns the
+    rows received and the source rank of each."""
+    world = comm.world
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world).to(torch.int64)
+    rc = comm.exchange_counts(counts.to(comm.device)).cpu()
+    got = comm.all_to_all_v(rows[order].to(comm.device), counts.tolist(), rc.tolist()).to(rows.device)
+    return got, torch.repeat_interleave(torch.arange(world, device=rows.device), rc.to(rows.device))
+
+
+def distributed_components(comm: Communicator, src: torch.Tensor, dst: torch.Tensor, n_global: Optional[int] = None,
+                           w: Optional[torch.Tensor] = None, min_w: float = 0.0, max_rounds: int = 1 << 20,
+                           stats: Optional[dict] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Connected components of a graph whose edges are spread over ranks
+    (the reference's single-process DFS is
+    buffer_graph.py:99-120). Returns ``(verts, labels)``: the vertices this
+    rank's edges touch (sorted global ids) and their global component label
+    (the smallest vertex id of the component).
+
+    Boundary-label exchange, no replicated state: each rank contracts its own
+    edges once (device hook/compress CC over compact local ids); every vertex
+    is owned by rank ``v % world``. Round 0 sends each touched vertex's label
+    to its owner, which learns the vertices that several ranks touch (the
+    boundary) and who subscribes to them. Every later round sends only
+    boundary vertices whose label went down, the owner forwards new minima to
+    the subscribers, and each rank re-propagates inside its local components
+    (a segmented min). Per-round traffic is O(changed boundary vertices), not
+    O(n_global); the round count is bounded by the diameter of the graph of
+    local components. ``n_global`` is accepted for API compatibility."""
+    dev = src.device
+    s, d = src.long(), dst.long()
+    if w is not None:
+        keep = w >= min_w
+        s, d = s[keep], d[keep]
+    E = s.numel()
+    verts, inv = torch.unique(torch.cat([s, d]), return_inverse=True)
+    nl = verts.numel()
+    comp = G.connected_components(inv[:E].to(torch.int32), inv[E:].to(torch.int32), nl).to(dev).long() \
+        if nl else torch.zeros(0, dtype=torch.long, device=dev)
+    big = torch.iinfo(torch.int64).max
+
+    def propagate(lab):
+        m = torch.full((nl,), big, dtype=torch.int64, device=dev).scatter_reduce(0, comp, lab, "amin")
+        return m[comp]
+
+    label = propagate(verts.clone())
+    st = {"rounds": 0, "rows_sent": 0, "first_round_rows": int(nl)}
+    world = comm.world
+    if world == 1:
+        if stats is not None:
+            stats.update(st)
+        return verts, label
+    # round 0: subscribe every touched vertex at its owner
+    got, frm = _route(comm, verts % world, torch.stack([verts, label], 1))
+    uv, uinv = torch.unique(got[:, 0], return_inverse=True)
+    cur = torch.full((uv.numel(),), big, dtype=torch.int64, device=dev).scatter_reduce(0, uinv, got[:, 1], "amin")
+    shared = torch.bincount(uinv, minlength=uv.numel()) >= 2
+    sub = shared[uinv]
+    sub_v, sub_rank = uinv[sub], frm[sub]  # subscriptions to boundary vertices
+    o = torch.argsort(sub_v, stable=True)
+    sub_v, sub_rank = sub_v[o], sub_rank[o]
+    reply = torch.stack([uv[sub_v], cur[sub_v]], 1)
+    back, _ = _route(comm, sub_rank, reply)
+    bpos = torch.searchsorted(verts, back[:, 0])  # this rank's boundary vertices
+    is_b = torch.zeros(nl, dtype=torch.bool, device=dev)
+    is_b[bpos] = True
+    bnd = torch.nonzero(is_b).flatten()
+    for rnd in range(max_rounds):
+        new = label.clone().scatter_reduce_(0, bpos, back[:, 1], "amin")
+        new = propagate(new)
+        dec = bnd[new[bnd] < label[bnd]]
+        label = new
+        msg = torch.stack([verts[dec], label[dec]], 1)
+        st["rounds"] = rnd + 1
+        st["rows_sent"] += int(dec.numel())
+        flag = torch.tensor([int(dec.numel())], dtype=torch.int64, device=comm.device)
+        comm.all_reduce(flag, "max")
+        if int(flag.item()) == 0:
             break
-    return label
+        got, _ = _route(comm, msg[:, 0] % world, msg)
+        gi = torch.searchsorted(uv, got[:, 0])
+        nxt = cur.clone().scatter_reduce_(0, gi, got[:, 1], "amin")
+        chg = nxt < cur
+        cur = nxt
+        sel = chg[sub_v]
+        back, _ = _route(comm, sub_rank[sel], torch.stack([uv[sub_v[sel]], cur[sub_v[sel]]], 1))
+        bpos = torch.searchsorted(verts, back[:, 0])
+    if stats is not None:
+        stats.update(st)
+    return verts, label

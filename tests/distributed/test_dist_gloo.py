@@ -98,6 +98,13 @@ def _kmeans(comm):
     return bool(same and pure)
 
 
+def _full_labels(comm, n, verts, lab):
+    full = torch.arange(n, dtype=torch.int64)
+    for v, l in comm.all_gather_object((verts.tolist(), lab.tolist())):
+        full[torch.tensor(v, dtype=torch.long)] = torch.tensor(l, dtype=torch.int64)
+    return full
+
+
 def _components(comm):
     from lazzaro_amd.ops import graph_ops as G
     from lazzaro_amd.parallel import distributed_components
@@ -107,8 +114,47 @@ def _components(comm):
     dst = torch.randint(0, n, (240,), generator=g, dtype=torch.int32)
     ref = G.connected_components(src, dst, n).to(torch.int64)
     mine = torch.arange(240) % comm.world == comm.rank
-    lab = distributed_components(comm, src[mine], dst[mine], n)
-    return bool(torch.equal(lab, ref))
+    verts, lab = distributed_components(comm, src[mine], dst[mine], n)
+    return bool(torch.equal(_full_labels(comm, n, verts, lab), ref))
+
+
+def _components_local(comm):
+    """Each rank's edges stay in its own id block except a chain of bridges:
+    after the subscription round only the bridge vertices travel, and the
+    labels are the single-process ones."""
+    from lazzaro_amd.ops import graph_ops as G
+    from lazzaro_amd.parallel import distributed_components
+    W, per = comm.world, 5000
+    n = W * per
+    g = torch.Generator().manual_seed(7)
+    srcs, dsts = [], []
+    for r in range(W):  # a long path inside each block (deep local structure) + random chords
+        base = r * per
+        p = torch.arange(base, base + per - 1)
+        srcs += [p, base + torch.randint(0, per, (2000,), generator=g)]
+        dsts += [p + 1, base + torch.randint(0, per, (2000,), generator=g)]
+    src, dst = torch.cat(srcs), torch.cat(dsts)
+    owner = src // per
+    # bridges: the last vertex of block r to the first of block r+1, held by rank r
+    bs = torch.arange(W - 1) * per + per - 1
+    src, dst, owner = torch.cat([src, bs]), torch.cat([dst, bs + 1]), torch.cat([owner, torch.arange(W - 1)])
+    ref = G.connected_components(src.int(), dst.int(), n).to(torch.int64)
+    mine = owner == comm.rank
+    st = {}
+    verts, lab = distributed_components(comm, src[mine].int(), dst[mine].int(), n, stats=st)
+    ok = bool(torch.equal(_full_labels(comm, n, verts, lab), ref)) and bool((ref == 0).all())
+    # after subscription, traffic is per boundary vertex, not per vertex
+    return ok and st["rows_sent"] <= 2 * W and st["rounds"] <= W + 1
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_components(world):
+    assert all(spawn(world, _components).values())
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_distributed_components_boundary_traffic(world):
+    assert all(spawn(world, _components_local).values())
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -127,11 +173,6 @@ def test_tenant_placement():
 
 def test_distributed_kmeans():
     assert all(spawn(2, _kmeans).values())
-
-
-@pytest.mark.parametrize("world", [2, 4])
-def test_distributed_components(world):
-    assert all(spawn(world, _components).values())
 
 
 def _commit(comm):

@@ -209,11 +209,14 @@ def test_config_and_tracing(monkeypatch):
     from lazzaro_amd.utils.tracing import tracer
     monkeypatch.setenv("LZK_MAX_BUFFER_SIZE", "77")
     monkeypatch.setenv("LZK_ENABLE_ASYNC", "false")
+    monkeypatch.setenv("LZK_HIERARCHY_MODE", "kmeans")
+    monkeypatch.setenv("LZK_HIERARCHY_EVERY", "7")
     cfg = MemoryConfig.from_env(load_from_disk=False, merge_mode="pairwise")
     assert cfg.max_buffer_size == 77 and cfg.enable_async is False
     assert set(cfg.reference_kwargs()) >= {"max_buffer_size", "db_dir", "user_id"}
     ms = MemorySystem.from_config(cfg, llm_provider=LocalLLM(), embedding_provider=HashEmbedder())
     assert ms.max_buffer_size == 77 and ms.merge_mode == "pairwise" and not ms.enable_async
+    assert ms.hierarchy_mode == "kmeans" and ms.hierarchy_params["every"] == 7
     tracer.enable(True)
     tracer.reset()
     try:
