@@ -64,21 +64,45 @@ def _jsonable(v):
 
 class DistributedMemoryService:
     def __init__(self, comm: Communicator, factory: Callable[[str], object], owner: Callable[[str], int] = None,
-                 max_resident: int = 1 << 30):
+                 max_resident: int = 1 << 30, placement=None):
         """``factory(user_id)`` builds the tenant's MemorySystem on this rank
-        (sharing one store / embedder / device); ``owner`` overrides the
-        rendezvous-hash placement (e.g. :class:`~.elastic.ElasticPlacement`);
-        at most ``max_resident`` tenants stay in memory (LRU; an evicted
-        tenant is persisted and reloaded from the store on its next request)."""
+        (sharing one store / embedder / device; it must load the tenant from
+        the store); ``owner`` overrides the rendezvous-hash placement;
+        ``placement`` (an :class:`~.elastic.ElasticPlacement`) places tenants
+        over the ORIGINAL ids of the live ranks, so :meth:`reform` after a rank
+        failure moves only the dead ranks' tenants. At most ``max_resident``
+        tenants stay in memory (LRU; an evicted tenant is persisted and
+        reloaded from the store on its next request)."""
         self.comm = comm
         self.factory = factory
         self._owner = owner
+        self.placement = placement
         self.max_resident = max_resident
         self.systems: "OrderedDict[str, object]" = OrderedDict()
 
     # ------------------------------------------------------------ placement
     def owner(self, user: str) -> int:
-        return self._owner(user) if self._owner is not None else tenant_rank(user, self.comm.world)
+        """The CURRENT communicator rank that owns ``user``."""
+        if self._owner is not None:
+            return self._owner(user)
+        if self.placement is not None:
+            return self.placement.alive.index(self.placement.owner(user))
+        return tenant_rank(user, self.comm.world)
+
+    def reform(self, comm: Communicator, placement) -> List[str]:
+        """Adopt the re-formed group after a rank failure
+        (:func:`~.elastic.reform_group` + ``ElasticPlacement.remove``):
+        tenants this rank no longer owns are persisted and released; tenants
+        that moved here are loaded from the shared store by ``factory`` on
+        their first request (every durable byte is in the store, so a dead
+        rank loses no committed state). Returns the released tenants."""
+        self.comm, self.placement, self._owner = comm, placement, None
+        gone = [u for u in self.systems if not self.is_local(u)]
+        for u in gone:
+            ms = self.systems.pop(u)
+            ms._save_to_persistence()
+            ms.close()
+        return gone
 
     def is_local(self, user: str) -> bool:
         return self.owner(user) == self.comm.rank
