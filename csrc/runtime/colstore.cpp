@@ -1,4 +1,5 @@
 // Versioned columnar table store -- implementation. See colstore.h.
+#include <cstdlib>
 #include "colstore.h"
 
 #include <arrow/api.h>
@@ -84,46 +85,49 @@ std::shared_ptr<arrow::DataType> arrow_type(const ColSpec& c) {
   return arrow::null();
 }
 
-std::shared_ptr<arrow::Array> to_arrow(const Column& c) {
-  const int64_t n = (int64_t)c.size();
+// Rows [r0, r1) of a column -> Arrow array. Fragments are written as several
+// record batches (write_fragment): one Arrow array holds < 2^31 values / string
+// bytes, and a 10M x 768 vector column is 7.7G floats.
+std::shared_ptr<arrow::Array> to_arrow(const Column& c, int64_t r0, int64_t r1) {
+  const int64_t n = r1 - r0;
   switch (c.type) {
     case ColType::Str: {
       arrow::StringBuilder b;
       int64_t bytes = 0;
-      for (auto& x : c.s) bytes += (int64_t)x.size();
+      for (int64_t r = r0; r < r1; ++r) bytes += (int64_t)c.s[r].size();
       check(b.Reserve(n), "reserve");
       check(b.ReserveData(bytes), "reserve");
-      for (auto& x : c.s) b.UnsafeAppend(x);
+      for (int64_t r = r0; r < r1; ++r) b.UnsafeAppend(c.s[r]);
       return ok_or_throw(b.Finish(), "string column");
     }
     case ColType::F64: {
       arrow::DoubleBuilder b;
-      check(b.AppendValues(c.f64.data(), n), "f64 column");
+      check(b.AppendValues(c.f64.data() + r0, n), "f64 column");
       return ok_or_throw(b.Finish(), "f64 column");
     }
     case ColType::F32: {
       arrow::FloatBuilder b;
-      check(b.AppendValues(c.f32.data(), n), "f32 column");
+      check(b.AppendValues(c.f32.data() + r0, n), "f32 column");
       return ok_or_throw(b.Finish(), "f32 column");
     }
     case ColType::I32: {
       arrow::Int32Builder b;
-      check(b.AppendValues(c.i32.data(), n), "i32 column");
+      check(b.AppendValues(c.i32.data() + r0, n), "i32 column");
       return ok_or_throw(b.Finish(), "i32 column");
     }
     case ColType::I64: {
       arrow::Int64Builder b;
-      check(b.AppendValues(c.i64.data(), n), "i64 column");
+      check(b.AppendValues(c.i64.data() + r0, n), "i64 column");
       return ok_or_throw(b.Finish(), "i64 column");
     }
     case ColType::Bool: {
       arrow::BooleanBuilder b;
-      check(b.AppendValues(c.b.data(), n), "bool column");
+      check(b.AppendValues(c.b.data() + r0, n), "bool column");
       return ok_or_throw(b.Finish(), "bool column");
     }
     case ColType::VecF32: {
       arrow::FloatBuilder vb;
-      check(vb.AppendValues(c.f32.data(), (int64_t)c.f32.size()), "vector column");
+      check(vb.AppendValues(c.f32.data() + (size_t)r0 * c.dim, n * (int64_t)c.dim), "vector column");
       auto values = ok_or_throw(vb.Finish(), "vector column");
       return ok_or_throw(arrow::FixedSizeListArray::FromArrays(values, (int32_t)c.dim), "vector column");
     }
@@ -131,51 +135,52 @@ std::shared_ptr<arrow::Array> to_arrow(const Column& c) {
   return nullptr;
 }
 
-// Arrow array -> Column payload of the requested type (missing -> defaults).
+// Append an Arrow array's nrows rows to a Column of the requested type
+// (missing array -> defaults).
 void from_arrow(const std::shared_ptr<arrow::Array>& a, Column& c, uint64_t nrows) {
   if (!a) {
     switch (c.type) {
-      case ColType::Str: c.s.assign(nrows, ""); break;
-      case ColType::F64: c.f64.assign(nrows, 0.0); break;
-      case ColType::F32: c.f32.assign(nrows, 0.f); break;
-      case ColType::I32: c.i32.assign(nrows, 0); break;
-      case ColType::I64: c.i64.assign(nrows, 0); break;
-      case ColType::Bool: c.b.assign(nrows, 0); break;
-      case ColType::VecF32: c.f32.assign(nrows * c.dim, 0.f); break;
+      case ColType::Str: c.s.resize(c.s.size() + nrows); break;
+      case ColType::F64: c.f64.resize(c.f64.size() + nrows, 0.0); break;
+      case ColType::F32: c.f32.resize(c.f32.size() + nrows, 0.f); break;
+      case ColType::I32: c.i32.resize(c.i32.size() + nrows, 0); break;
+      case ColType::I64: c.i64.resize(c.i64.size() + nrows, 0); break;
+      case ColType::Bool: c.b.resize(c.b.size() + nrows, 0); break;
+      case ColType::VecF32: c.f32.resize(c.f32.size() + nrows * c.dim, 0.f); break;
     }
     return;
   }
   switch (c.type) {
     case ColType::Str: {
       auto s = std::static_pointer_cast<arrow::StringArray>(a);
-      c.s.resize(nrows);
-      for (uint64_t r = 0; r < nrows; ++r) c.s[r] = std::string(s->GetView((int64_t)r));
+      c.s.reserve(c.s.size() + nrows);
+      for (uint64_t r = 0; r < nrows; ++r) c.s.emplace_back(s->GetView((int64_t)r));
       break;
     }
     case ColType::F64: {
       auto x = std::static_pointer_cast<arrow::DoubleArray>(a);
-      c.f64.assign(x->raw_values(), x->raw_values() + nrows);
+      c.f64.insert(c.f64.end(), x->raw_values(), x->raw_values() + nrows);
       break;
     }
     case ColType::F32: {
       auto x = std::static_pointer_cast<arrow::FloatArray>(a);
-      c.f32.assign(x->raw_values(), x->raw_values() + nrows);
+      c.f32.insert(c.f32.end(), x->raw_values(), x->raw_values() + nrows);
       break;
     }
     case ColType::I32: {
       auto x = std::static_pointer_cast<arrow::Int32Array>(a);
-      c.i32.assign(x->raw_values(), x->raw_values() + nrows);
+      c.i32.insert(c.i32.end(), x->raw_values(), x->raw_values() + nrows);
       break;
     }
     case ColType::I64: {
       auto x = std::static_pointer_cast<arrow::Int64Array>(a);
-      c.i64.assign(x->raw_values(), x->raw_values() + nrows);
+      c.i64.insert(c.i64.end(), x->raw_values(), x->raw_values() + nrows);
       break;
     }
     case ColType::Bool: {
       auto x = std::static_pointer_cast<arrow::BooleanArray>(a);
-      c.b.resize(nrows);
-      for (uint64_t r = 0; r < nrows; ++r) c.b[r] = x->Value((int64_t)r) ? 1 : 0;
+      c.b.reserve(c.b.size() + nrows);
+      for (uint64_t r = 0; r < nrows; ++r) c.b.push_back(x->Value((int64_t)r) ? 1 : 0);
       break;
     }
     case ColType::VecF32: {
@@ -183,7 +188,7 @@ void from_arrow(const std::shared_ptr<arrow::Array>& a, Column& c, uint64_t nrow
       c.dim = (uint32_t)l->list_type()->list_size();
       auto v = std::static_pointer_cast<arrow::FloatArray>(l->values());
       const float* p = v->raw_values() + l->value_offset(0);
-      c.f32.assign(p, p + nrows * (size_t)c.dim);
+      c.f32.insert(c.f32.end(), p, p + nrows * (size_t)c.dim);
       break;
     }
   }
@@ -539,19 +544,42 @@ void Table::add_fragment(const std::string& file, uint64_t rows, const std::vect
 void Table::write_fragment(const std::string& file, const std::vector<Column>& cols) {
   arrow::FieldVector fields;
   std::vector<std::shared_ptr<arrow::Array>> arrays;
+  int64_t width = 1;  // values per row of the widest column
   for (size_t i = 0; i < cols.size(); ++i) {
     ColSpec spec = schema_[i];
     if (spec.type == ColType::VecF32) spec.dim = cols[i].dim ? cols[i].dim : spec.dim;
+    if (spec.type == ColType::VecF32) width = std::max<int64_t>(width, spec.dim);
     fields.push_back(arrow::field(spec.name, arrow_type(spec), false));
-    arrays.push_back(to_arrow(cols[i]));
   }
   auto sch = arrow::schema(fields);
   const int64_t n = cols.empty() ? 0 : (int64_t)cols[0].size();
+  // record batches of <= 2^30 values per array and <= 2^30 string bytes
+  // (LZK_COLSTORE_BATCH_VALUES lowers the cap: tests exercise multi-batch files)
+  static const int64_t kMaxVals = [] {
+    const char* e = getenv("LZK_COLSTORE_BATCH_VALUES");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (int64_t)v : (int64_t(1) << 30);
+  }();
   std::string tmp = dir_ + "/data/.tmp-" + uniq_name();
   {
     auto out = ok_or_throw(arrow::io::FileOutputStream::Open(tmp), "open fragment");
     auto w = ok_or_throw(arrow::ipc::MakeFileWriter(out, sch), "fragment writer");
-    check(w->WriteRecordBatch(*arrow::RecordBatch::Make(sch, n, arrays)), "write fragment");
+    int64_t r0 = 0;
+    do {
+      int64_t r1 = std::min<int64_t>(n, r0 + std::max<int64_t>(1, kMaxVals / width));
+      for (size_t i = 0; i < cols.size(); ++i) {
+        if (cols[i].type != ColType::Str) continue;
+        int64_t bytes = 0;
+        for (int64_t r = r0; r < r1; ++r) {
+          bytes += (int64_t)cols[i].s[r].size();
+          if (bytes > kMaxVals) { r1 = std::max<int64_t>(r0 + 1, r); break; }
+        }
+      }
+      arrays.clear();
+      for (size_t i = 0; i < cols.size(); ++i) arrays.push_back(to_arrow(cols[i], r0, r1));
+      check(w->WriteRecordBatch(*arrow::RecordBatch::Make(sch, r1 - r0, arrays)), "write fragment");
+      r0 = r1;
+    } while (r0 < n);
     check(w->Close(), "close fragment");
     check(out->Close(), "close fragment");
   }
@@ -565,14 +593,14 @@ std::vector<Column> Table::read_fragment(const std::string& file, const std::vec
   auto rd = ok_or_throw(arrow::ipc::RecordBatchFileReader::Open(mm), "read fragment");
   std::vector<Column> out(schema_.size());
   for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
-  std::shared_ptr<arrow::RecordBatch> batch;
-  if (rd->num_record_batches() > 0) batch = ok_or_throw(rd->ReadRecordBatch(0), "fragment batch");
-  const uint64_t n = batch ? (uint64_t)batch->num_rows() : 0;
-  *nrows = n;
-  for (int ci : want) {
-    std::shared_ptr<arrow::Array> a = batch ? batch->GetColumnByName(schema_[ci].name) : nullptr;
-    from_arrow(a, out[ci], n);
+  uint64_t n = 0;
+  for (int bi = 0; bi < rd->num_record_batches(); ++bi) {
+    auto batch = ok_or_throw(rd->ReadRecordBatch(bi), "fragment batch");
+    const uint64_t m = (uint64_t)batch->num_rows();
+    for (int ci : want) from_arrow(batch->GetColumnByName(schema_[ci].name), out[ci], m);
+    n += m;
   }
+  *nrows = n;
   return out;
 }
 

@@ -778,7 +778,8 @@ STORAGE:
     # ------------------------------------------------------------ store sync
     def _profile_blob(self) -> Dict:
         d = self.profile.to_dict()
-        d["_engine"] = {"decay_clock": self.graph.decay_log, "node_counter": self.node_counter}
+        d["_engine"] = {"decay_clock": self.graph.decay_log, "node_counter": self.node_counter,
+                        "max_node_id": getattr(self, "_max_node_id", 0)}
         return d
 
     def _save_to_persistence(self):
@@ -830,6 +831,9 @@ STORAGE:
                 rows = rows[k == NODE]
             node_cols = export_node_columns(g, rows)
             edge_cols = export_edge_columns(g, eidx)
+            # largest node_<n> id ever committed (O(changed rows)): a reload
+            # restores node_counter from it without scanning every id
+            self._max_node_id = max(getattr(self, "_max_node_id", 0), _max_node_num(node_cols.get("id", [])))
             self.store.commit_tenant(self.user_id, node_cols, del_ids, edge_cols,
                                      [f"{s}_{t}" for s, t in del_edges])
         except Exception:
@@ -842,6 +846,7 @@ STORAGE:
             g.unstore(gone)
 
     def _rewrite_all(self) -> None:
+        self._max_node_id = max(getattr(self, "_max_node_id", 0), _max_node_num(self.graph.ids))
         nodes = [n.to_dict() for n in self.buffer.nodes.values()]
         edges = [e.to_dict() for sh in self.shards.values() for e in sh.edges.values()]
         if hasattr(self.store, "replace_user_nodes"):
@@ -873,6 +878,7 @@ STORAGE:
                 ecols = _edge_rows_to_columns(self.store.get_edges(user_id=self.user_id))
             prof = self.store.load_profile(user_id=self.user_id) if n_rows else None
             self._replace_graph()
+            self._max_node_id = 0
             eng = (prof or {}).get("_engine", {}) if isinstance(prof, dict) else {}
             clock = float(eng.get("decay_clock", 0.0))
             n_edges = 0
@@ -885,11 +891,11 @@ STORAGE:
             except Exception:
                 self._last_nodes_version = 0
             if n_rows:
-                mx = int(eng.get("node_counter", 0))
-                for nid in ncols["id"]:
-                    m = _NODE_ID.match(nid)
-                    if m:
-                        mx = max(mx, int(m.group(1)))
+                if "max_node_id" in eng:  # written by this engine: no per-id scan
+                    mx = max(int(eng.get("node_counter", 0)), int(eng["max_node_id"]))
+                else:  # a store written elsewhere: the largest node_<n> id
+                    mx = max(int(eng.get("node_counter", 0)), _max_node_num(ncols["id"]))
+                self._max_node_id = mx
                 self.node_counter = mx
             if self.query_cache:
                 self.query_cache.invalidate_results()
@@ -1142,12 +1148,16 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
         return
     is_sup = np.asarray(nc["is_super_node"]).astype(bool)
     shard_keys = list(nc["shard_key"])
-    # reference shard creation order: first non-super occurrence
-    for k, s in zip(shard_keys, is_sup):
-        if not s and k not in g.shard_code:
+    # reference shard creation order: first non-super occurrence (factorize
+    # keeps first-appearance order), then any key only super rows use
+    keys = pd.Series(shard_keys, dtype=object)
+    for k in pd.unique(keys[~is_sup]):
+        if k not in g.shard_code:
             g.shard_id(k)
-    codes = np.asarray([g.shard_code[k] if k in g.shard_code else g.shard_id(k, live=False)
-                        for k in shard_keys], dtype=np.int32)
+    kcode, kuniq = pd.factorize(keys, sort=False)
+    ucode = np.asarray([g.shard_code[k] if k in g.shard_code else g.shard_id(k, live=False) for k in kuniq],
+                       dtype=np.int32)
+    codes = ucode[kcode]
     dc = np.asarray(nc.get("decay_clock", np.zeros(N)), dtype=np.float64)
     fac = np.exp(np.minimum(0.0, clock - dc))
     sal = np.asarray(nc["salience"], dtype=np.float64)
@@ -1156,9 +1166,10 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
                                                SALIENCE_FLOOR), sal)
     V = nc["vector"]
     has = nc.get("_has")
-    emb = torch.from_numpy(np.ascontiguousarray(V, dtype=np.float32)) if V.shape[1] else None
-    if emb is not None and g.on_gpu:
-        emb = emb.pin_memory()
+    emb = None
+    if V.shape[1]:
+        emb = _h2d(np.ascontiguousarray(V, dtype=np.float32), g.device) if g.on_gpu else torch.from_numpy(
+            np.ascontiguousarray(V, dtype=np.float32))
     children = {}
     for j in np.nonzero(is_sup)[0].tolist():
         try:
@@ -1201,6 +1212,40 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
                            lu=torch.as_tensor(np.asarray(ec["last_updated"])[keep], dtype=torch.float64))
     g.decay_log = clock
     g.clear_tracking()
+
+
+def _max_node_num(ids) -> int:
+    """Largest n of the ``node_<n>`` ids (reference id scheme), 0 if none."""
+    mx = 0
+    for nid in ids:
+        m = _NODE_ID.match(nid)
+        if m:
+            mx = max(mx, int(m.group(1)))
+    return mx
+
+
+def _h2d(a: np.ndarray, dev, chunk_bytes: int = 64 << 20) -> torch.Tensor:
+    """Host array -> device tensor through two pinned staging buffers (the
+    memcpy into one overlaps the async copy out of the other): no pinning of
+    the whole array, no pageable-memory DMA."""
+    out = torch.empty(a.shape, dtype=torch.from_numpy(a[:0]).dtype, device=dev)
+    flat_src = a.reshape(-1)
+    flat_dst = out.view(-1)
+    per = max(1, chunk_bytes // a.itemsize)
+    bufs = [torch.empty(per, dtype=out.dtype).pin_memory() for _ in range(2)]
+    evs = [None, None]
+    st = torch.cuda.current_stream(dev)
+    for j, c0 in enumerate(range(0, flat_src.size, per)):
+        c1 = min(flat_src.size, c0 + per)
+        b = j & 1
+        if evs[b] is not None:
+            evs[b].synchronize()
+        bufs[b][: c1 - c0].numpy()[:] = flat_src[c0:c1]
+        flat_dst[c0:c1].copy_(bufs[b][: c1 - c0], non_blocking=True)
+        evs[b] = torch.cuda.Event()
+        evs[b].record(st)
+    st.synchronize()
+    return out
 
 
 def _default_local_embedder() -> EmbeddingProvider:

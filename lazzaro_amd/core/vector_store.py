@@ -118,7 +118,10 @@ class HBMStore:
 
     def load_tenant(self, user_id: str):
         """(node columns, edge columns) of one tenant, as stored."""
-        nc = self._nodes_table.scan_columns([("user_id", user_id)])
+        # the columns the graph loader reads (not user_id / metadata: at 10M
+        # rows every string column costs seconds of Python objects)
+        want = [c for c, _, _ in self._nodes_table.schema if c not in ("user_id", "metadata")]
+        nc = self._nodes_table.scan_columns([("user_id", user_id)], want=want)
         if not nc or not len(nc.get("id", [])):
             return {"id": []}, {"id": []}
         if nc["vector"].ndim == 2 and nc["vector"].shape[1]:

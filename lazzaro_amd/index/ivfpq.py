@@ -1,8 +1,9 @@
 """IVF-PQ index (BASELINE config 5).
 
-Memory: ``M`` bytes of PQ code + 8 bytes of id per vector, so one MI355X
-(288 GB HBM) holds ~3.5 billion 1024-d vectors at M=64 -- vs 2 KB/vector for
-bf16 flat storage. Inner-product metric on unit vectors (cosine).
+Memory: ``M`` bytes of PQ code + 20 bytes of list id / position / id per
+vector, so one MI355X (288 GB HBM) holds ~3 billion 1024-d vectors at M=64
+codes-only, ~200M with an fp8 re-rank copy -- vs 2 KB/vector for bf16 flat
+storage. Inner-product metric on unit vectors (cosine).
 
 * train: coarse k-means (``kmeans``: fused MFMA top-1 assign + segmented mean)
   and ``M`` residual sub-quantisers of 256 codewords each
@@ -11,8 +12,9 @@ bf16 flat storage. Inner-product metric on unit vectors (cosine).
 * search: coarse probe (top-nprobe centroids), per-query LUT
           ``<q_j, codebook_j[c]>`` (one batched GEMM), HIP ``ivfpq_scan``
           kernel per (query, probed list) with a fused top-k, shared
-          ``topk_merge`` kernel; optional exact re-rank of the candidates
-          against kept bf16/fp8 rows.
+          ``topk_merge`` kernel; deep lists (re-rank depth > 16) from
+          ``ivfpq_scan_deep`` (each wave's best rows per list); optional exact
+          re-rank of the candidates against kept bf16/fp8 rows.
 CPU tensors run a torch reference of the same pipeline (tests).
 """
 from __future__ import annotations
@@ -30,8 +32,9 @@ from .kmeans import kmeans
 _lib.register("lzk_ivfpq_scan", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I,
                                           _lib.P, _lib.P, _lib.P])
 
-_lib.register("lzk_ivfpq_dense", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I,
-                                           _lib.I, _lib.P, _lib.P])
+_lib.register("lzk_ivfpq_scan_deep", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I,
+                                               _lib.P, _lib.P, _lib.P])
+_lib.register("lzk_ivfpq_deep_width", _lib.I, [])
 
 _lib.register("lzk_rerank", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.I, _lib.I, _lib.P, _lib.I,
                                       _lib.I, _lib.I, _lib.P, _lib.P, _lib.P])
@@ -52,10 +55,17 @@ def _unit(x):
 
 class IVFPQIndex:
     def __init__(self, dim: int, nlist: int = 1024, m: int = 64, device=None, keep_vectors=False):
-        """keep_vectors: False (codes only, 8+m bytes/vector), True / "bf16"
-        (exact re-rank copy, 2*Dp bytes/vector) or "fp8" (OCP e4m3 re-rank copy
-        with a per-row scale, D+4 bytes/vector -- the layout that fills 288 GB
-        with ~250M 1024-d vectors and still re-ranks PQ candidates)."""
+        """keep_vectors: False (codes only, m+20 bytes/vector), True / "bf16"
+        (exact re-rank copy, 2*Dp bytes/vector), "int8" or "fp8" (re-rank
+        copy with a per-row scale, D+4 bytes/vector -- the layout that fills
+        288 GB with ~200M 1024-d vectors and still re-ranks PQ candidates;
+        int8's uniform grid is ~3x finer than e4m3 on embedding rows, so it
+        is the one to use for recall).
+
+        Storage is preallocated (:meth:`reserve`) and written in place. Code
+        rows (``codes``, ``list_of``) are kept sorted by list (CSR) and carry
+        ``pos`` = the insertion row of each; the re-rank copy and the ids stay
+        in insertion order, so sorting never moves the big vector copy."""
         assert dim % m == 0, "dim must be divisible by m"
         self.dim, self.nlist, self.m, self.dsub = dim, nlist, m, dim // m
         self.device = torch.device(device) if device is not None else torch.device("cpu")
@@ -63,16 +73,82 @@ class IVFPQIndex:
         self.centroids = None      # fp32 [nlist, dim]
         self.centroids16 = None    # bf16 [nlist, Dp] (GPU assign)
         self.codebooks = None      # fp32 [m, 256, dsub]
-        self.codes = torch.zeros((0, m), dtype=torch.uint8, device=self.device)
-        self.ids = torch.zeros(0, dtype=torch.int64, device=self.device)
-        self.list_of = torch.zeros(0, dtype=torch.int32, device=self.device)
-        self.list_off = torch.zeros(nlist + 1, dtype=torch.int64, device=self.device)
         self.keep_vectors = "bf16" if keep_vectors is True else (keep_vectors or False)
-        if self.keep_vectors not in (False, "bf16", "fp8"):
-            raise ValueError("keep_vectors must be False, True/'bf16' or 'fp8'")
-        self.vectors = None
-        self.vscale = None
+        if self.keep_vectors not in (False, "bf16", "fp8", "int8"):
+            raise ValueError("keep_vectors must be False, True/'bf16', 'int8' or 'fp8'")
+        self.n = 0
+        self.cap = 0
+        z = lambda *s, dt: torch.zeros(s, dtype=dt, device=self.device)  # noqa: E731
+        self._codes = z(0, m, dt=torch.uint8)
+        self._list = z(0, dt=torch.int32)
+        self._pos = z(0, dt=torch.int64)
+        self._vids = z(0, dt=torch.int64)
+        self._vec = None
+        self._vscale = None
+        self.list_off = z(nlist + 1, dt=torch.int64)
         self._dirty = False
+
+    # ------------------------------------------------------------------ storage
+    def reserve(self, n: int) -> None:
+        """Capacity for ``n`` vectors (grows by copying; call once up front to
+        build a large index without reallocations)."""
+        if n <= self.cap:
+            return
+        cap = max(n, int(self.cap * 1.5) + 1)
+        k = self.n
+
+        def grow(t, shape, dt):
+            new = torch.zeros(shape, dtype=dt, device=self.device)
+            if t is not None and k:
+                new[:k] = t[:k]
+            return new
+        self._codes = grow(self._codes, (cap, self.m), torch.uint8)
+        self._list = grow(self._list, (cap,), torch.int32)
+        self._pos = grow(self._pos, (cap,), torch.int64)
+        self._vids = grow(self._vids, (cap,), torch.int64)
+        if self.keep_vectors == "bf16":
+            w = self.Dp if self.device.type == "cuda" else self.dim
+            self._vec = grow(self._vec, (cap, w), torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        elif self.keep_vectors in ("fp8", "int8"):
+            self._vec = grow(self._vec, (cap, self.dim), torch.uint8)
+            self._vscale = grow(self._vscale, (cap,), torch.float32)
+        self.cap = cap
+
+    # views of the live rows (code order) -- and setters for hand-built indexes
+    @property
+    def codes(self) -> torch.Tensor:
+        return self._codes[: self.n]
+
+    @codes.setter
+    def codes(self, v: torch.Tensor) -> None:
+        self._codes, self.n, self.cap = v.to(self.device), v.shape[0], v.shape[0]
+        self._pos = torch.arange(self.n, device=self.device)
+
+    @property
+    def list_of(self) -> torch.Tensor:
+        return self._list[: self.n]
+
+    @list_of.setter
+    def list_of(self, v: torch.Tensor) -> None:
+        self._list = v.to(self.device, torch.int32)
+
+    @property
+    def ids(self) -> torch.Tensor:
+        """ids in code order."""
+        return self._vids[self._pos[: self.n]]
+
+    @ids.setter
+    def ids(self, v: torch.Tensor) -> None:
+        self._vids = v.to(self.device, torch.int64)
+        self._pos = torch.arange(v.shape[0], device=self.device)
+
+    @property
+    def vectors(self):
+        return None if self._vec is None else self._vec[: self.n]
+
+    @property
+    def vscale(self):
+        return None if self._vscale is None else self._vscale[: self.n]
 
     # ------------------------------------------------------------------ train
     def _pad(self, x: torch.Tensor) -> torch.Tensor:
@@ -129,63 +205,67 @@ class IVFPQIndex:
         return lab, codes
 
     def add(self, x: torch.Tensor, ids: Optional[torch.Tensor] = None, batch: int = 1 << 18) -> None:
-        n0 = self.ids.numel()
+        n0 = self.n
         n = x.shape[0]
+        self.reserve(n0 + n)
         ids = torch.arange(n0, n0 + n, dtype=torch.int64) if ids is None else ids.to(torch.int64)
-        labs, codes = [], []
+        self._vids[n0:n0 + n] = ids.to(self.device)
+        self._pos[n0:n0 + n] = torch.arange(n0, n0 + n, device=self.device)
         for r0 in range(0, n, batch):
-            l, c = self.encode(x[r0:r0 + batch])
-            labs.append(l)
-            codes.append(c)
-        lab = torch.cat(labs)
-        self.codes = torch.cat([self.codes, torch.cat(codes)])
-        self.ids = torch.cat([self.ids, ids.to(self.device)])
-        self.list_of = torch.cat([self.list_of, lab])
-        if self.keep_vectors == "bf16":
-            v = self._pad(_unit(x.to(self.device).float()))
-            self.vectors = v if self.vectors is None else torch.cat([self.vectors, v])
-        elif self.keep_vectors == "fp8":
-            from ..ops.encoder_ops import quantize_fp8_rows
-            qs, ss = [], []
-            for r0 in range(0, n, batch):
-                v = _unit(x[r0:r0 + batch].to(self.device).float())
-                v = v.to(torch.bfloat16) if self.device.type == "cuda" else v
+            r1 = min(n, r0 + batch)
+            xb = _unit(x[r0:r1].to(self.device).float())
+            lab, codes = self.encode(xb)
+            self._list[n0 + r0:n0 + r1] = lab
+            self._codes[n0 + r0:n0 + r1] = codes
+            if self.keep_vectors == "bf16":
+                self._vec[n0 + r0:n0 + r1] = self._pad(xb) if self.device.type == "cuda" else xb
+            elif self.keep_vectors == "fp8":
+                from ..ops.encoder_ops import quantize_fp8_rows
+                v = xb.to(torch.bfloat16) if self.device.type == "cuda" else xb
                 q8, sc = quantize_fp8_rows(v.contiguous())
-                qs.append(q8)
-                ss.append(sc)
-            q8, sc = torch.cat(qs), torch.cat(ss)
-            self.vectors = q8 if self.vectors is None else torch.cat([self.vectors, q8])
-            self.vscale = sc if self.vscale is None else torch.cat([self.vscale, sc])
+                self._vec[n0 + r0:n0 + r1] = q8
+                self._vscale[n0 + r0:n0 + r1] = sc
+            elif self.keep_vectors == "int8":
+                sc = xb.abs().amax(1).clamp_min(1e-30) / 127.0
+                q = torch.round(xb / sc[:, None]).clamp_(-127, 127).to(torch.int8)
+                self._vec[n0 + r0:n0 + r1] = q.view(torch.uint8)
+                self._vscale[n0 + r0:n0 + r1] = sc
+        self.n = n0 + n
         self._dirty = True
 
-    def _finalize(self) -> None:
-        """Sort rows by list id (CSR) -- amortised over a batch of adds."""
+    def _finalize(self, chunk: int = 1 << 24) -> None:
+        """Sort the code rows by list id (CSR) -- amortised over a batch of
+        adds; the codes are permuted in chunks into one new buffer, the
+        vectors never move (``pos`` follows the codes)."""
         if not self._dirty:
             return
-        o = torch.argsort(self.list_of, stable=True)
-        self.codes = self.codes[o].contiguous()
-        self.ids = self.ids[o]
-        self.list_of = self.list_of[o]
-        if self.vectors is not None:
-            self.vectors = self.vectors[o]
-        if self.vscale is not None:
-            self.vscale = self.vscale[o]
-        cnt = torch.bincount(self.list_of.long(), minlength=self.nlist)
+        n = self.n
+        o = torch.argsort(self._list[:n], stable=True)
+        codes = torch.empty_like(self._codes)
+        for c0 in range(0, n, chunk):
+            codes[c0:c0 + chunk] = self._codes[o[c0:c0 + chunk]]
+        self._codes = codes
+        self._list[:n] = self._list[:n][o]
+        self._pos[:n] = self._pos[:n][o]
+        cnt = torch.bincount(self._list[:n].long(), minlength=self.nlist)
         self.list_off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
         self.list_off[1:] = torch.cumsum(cnt, 0)
         self._dirty = False
 
     def __len__(self) -> int:
-        return int(self.ids.numel())
+        return int(self.n)
 
     def memory_bytes(self) -> int:
-        b = self.codes.numel() + self.ids.numel() * 8
-        b += self.vectors.numel() * self.vectors.element_size() if self.vectors is not None else 0
-        return b + (self.vscale.numel() * 4 if self.vscale is not None else 0)
+        b = self.n * (self.m + 4 + 8 + 8)  # codes, list id, pos, id
+        if self._vec is not None:
+            b += self.n * self._vec.shape[1] * self._vec.element_size()
+        return b + (self.n * 4 if self._vscale is not None else 0)
 
     # ------------------------------------------------------------------ search
     def search(self, q: torch.Tensor, k: int = 10, nprobe: int = 16, rerank: int = 0):
-        """Returns (scores fp32 [nq, k], ids int64 [nq, k])."""
+        """Returns (scores fp32 [nq, k], ids int64 [nq, k]). ``rerank`` > 0:
+        the best ``rerank`` PQ candidates are re-scored exactly against the
+        kept copy (scores then are exact inner products)."""
         self._finalize()
         qf = _unit(q.to(self.device).float())
         nq = qf.shape[0]
@@ -199,44 +279,50 @@ class IVFPQIndex:
         elif kk <= KSLOTS[-1]:
             s, rows = self._scan_gpu(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
         else:
-            s, rows = self._scan_dense(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
-        if rerank and self.vectors is not None and self._rerank_gpu_ok(k):
-            s, rows = self._rerank_gpu(qf, rows.contiguous(), k)
-        elif rerank and self.vectors is not None:
-            valid = rows >= 0
-            rr = rows.clamp_min(0)
-            if self.vscale is not None:  # fp8 copy: dequantise the gathered candidates only
-                v = self.vectors[rr].view(torch.float8_e4m3fn).float() * self.vscale[rr][..., None]
+            s, rows = self._scan_deep(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
+        if rerank and self._vec is not None:
+            vrows = torch.where(rows >= 0, self._pos[rows.clamp_min(0)], torch.full_like(rows, -1))
+            if self._rerank_gpu_ok(k):
+                s, vr = self._rerank_gpu(qf, vrows.contiguous(), k)
             else:
-                v = self.vectors[rr].float()[..., : self.dim]
-            s = torch.einsum("qd,qkd->qk", qf, v)
-            s = torch.where(valid, s, torch.full_like(s, float("-inf")))
-            s, o = torch.sort(s, dim=1, descending=True, stable=True)
-            rows = torch.gather(rows, 1, o)
+                valid = vrows >= 0
+                vv = vrows.clamp_min(0)
+                if self._vscale is not None:  # fp8 / int8 copy: dequantise the gathered candidates only
+                    dt = torch.int8 if self.keep_vectors == "int8" else torch.float8_e4m3fn
+                    v = self._vec[vv].view(dt).float() * self._vscale[vv][..., None]
+                else:
+                    v = self._vec[vv].float()[..., : self.dim]
+                sc = torch.einsum("qd,qkd->qk", qf, v)
+                sc = torch.where(valid, sc, torch.full_like(sc, float("-inf")))
+                s, o = torch.sort(sc, dim=1, descending=True, stable=True)
+                vr = torch.gather(vrows, 1, o)
+            s, vr = s[:, :k], vr[:, :k]
+            return s, torch.where(vr >= 0, self._vids[vr.clamp_min(0)], torch.full_like(vr, -1))
         s, rows = s[:, :k], rows[:, :k]
-        ids = torch.where(rows >= 0, self.ids[rows.clamp_min(0)], torch.full_like(rows, -1))
+        ids = torch.where(rows >= 0, self._vids[self._pos[rows.clamp_min(0)]], torch.full_like(rows, -1))
         return s, ids
 
     def _rerank_gpu_ok(self, k: int) -> bool:
         if self.device.type != "cuda" or k > KSLOTS[-1]:
             return False
-        w = self.vectors.shape[1]
-        row_bytes = w if self.vscale is not None else 2 * w
+        w = self._vec.shape[1]
+        row_bytes = w if self._vscale is not None else 2 * w
         return row_bytes % 256 == 0
 
     def _rerank_gpu(self, qf: torch.Tensor, rows: torch.Tensor, k: int):
         """Fused exact re-rank over the kept copy (csrc/kernels/ivfpq.hip
-        rerank_kernel): no dequantised [nq, R, D] intermediate."""
+        rerank_kernel): no dequantised [nq, R, D] intermediate. ``rows`` are
+        vector (insertion) rows; returns (scores, vector rows)."""
         nq, R = rows.shape
-        fp8 = self.vscale is not None
-        w = self.vectors.shape[1]
+        fmt = {"fp8": 1, "int8": 2}.get(self.keep_vectors, 0)
+        w = self._vec.shape[1]
         Q = torch.zeros((nq, w), dtype=torch.float32, device=self.device)
         Q[:, : qf.shape[1]] = qf
         ks = _kslot(k)
         os_ = torch.empty((nq, k), dtype=torch.float32, device=self.device)
         oi = torch.empty((nq, k), dtype=torch.long, device=self.device)
-        ldv = self.vectors.stride(0) * self.vectors.element_size()
-        _lib.check(_lib.lib().lzk_rerank(self.vectors.data_ptr(), ldv, int(fp8), _lib.ptr(self.vscale),
+        ldv = self._vec.stride(0) * self._vec.element_size()
+        _lib.check(_lib.lib().lzk_rerank(self._vec.data_ptr(), ldv, fmt, _lib.ptr(self._vscale),
                                          rows.data_ptr(), nq, R, Q.data_ptr(), w, ks, k, os_.data_ptr(),
                                          oi.data_ptr(), _lib.stream_ptr(self.device)), "lzk_rerank")
         return os_, oi
@@ -246,6 +332,7 @@ class IVFPQIndex:
         out_s = torch.full((nq, k), float("-inf"), device=self.device)
         out_r = torch.full((nq, k), -1, dtype=torch.long, device=self.device)
         ar = torch.arange(self.m, device=self.device)
+        codes = self.codes
         for qi in range(nq):
             cand_s, cand_r = [], []
             for p in range(probes.shape[1]):
@@ -253,7 +340,7 @@ class IVFPQIndex:
                 r0, r1 = int(self.list_off[l]), int(self.list_off[l + 1])
                 if r1 == r0:
                     continue
-                c = self.codes[r0:r1].long()
+                c = codes[r0:r1].long()
                 cand_s.append(coarse[qi, p] + lut[qi][ar[None, :], c].sum(1))
                 cand_r.append(torch.arange(r0, r1, device=self.device))
             if not cand_s:
@@ -264,24 +351,25 @@ class IVFPQIndex:
             out_r[qi, : o.numel()] = cr_[o]
         return out_s, out_r
 
-    def _scan_dense(self, probes, coarse, lut, k):
-        """Deep candidate lists: dense PQ scores per probed list (HIP kernel),
-        then a library top-k over each query's [nprobe * maxlen] scores."""
+    def _scan_deep(self, probes, coarse, lut, k):
+        """Deep candidate lists (re-rank depth >> 16): each (query, probed
+        list) block emits its waves' best rows (``ivfpq_scan_deep_kernel``,
+        4 x 128 per list), then a top-k over the query's nprobe x 512 PQ scores."""
         nq, nprobe = probes.shape
-        lens = (self.list_off[1:] - self.list_off[:-1])
-        maxlen = int(lens[probes.long()].max().item()) if probes.numel() else 0
-        maxlen = max(maxlen, 1)
-        buf = torch.empty((nq, nprobe, maxlen), dtype=torch.float32, device=self.device)
-        _lib.check(_lib.lib().lzk_ivfpq_dense(self.codes.data_ptr(), self.list_off.data_ptr(), probes.data_ptr(),
-                                              coarse.data_ptr(), lut.data_ptr(), nq, nprobe, self.m, maxlen,
-                                              buf.data_ptr(), _lib.stream_ptr(self.device)), "lzk_ivfpq_dense")
-        flat = buf.view(nq, -1)
-        kk = min(k, flat.shape[1])
-        s, pos = torch.topk(flat, kk, dim=1)
-        p, off = pos // maxlen, pos % maxlen
-        lists = torch.gather(probes.long(), 1, p)
-        rows = self.list_off[lists] + off
+        L = _lib.lib()
+        W = L.lzk_ivfpq_deep_width()
+        os_ = torch.empty((nq, nprobe * W), dtype=torch.float32, device=self.device)
+        oi = torch.empty((nq, nprobe * W), dtype=torch.int32, device=self.device)
+        _lib.check(L.lzk_ivfpq_scan_deep(self._codes.data_ptr(), self.list_off.data_ptr(), probes.data_ptr(),
+                                         coarse.data_ptr(), lut.data_ptr(), nq, nprobe, self.m, os_.data_ptr(),
+                                         oi.data_ptr(), _lib.stream_ptr(self.device)), "lzk_ivfpq_scan_deep")
+        kk = min(k, os_.shape[1])
+        s, j = torch.topk(os_, kk, dim=1)
+        rows = torch.gather(oi, 1, j).long()
         rows = torch.where(torch.isneginf(s), torch.full_like(rows, -1), rows)
+        if kk < k:
+            s = torch.cat([s, torch.full((nq, k - kk), float("-inf"), device=self.device)], 1)
+            rows = torch.cat([rows, torch.full((nq, k - kk), -1, dtype=torch.long, device=self.device)], 1)
         return s, rows
 
     def _scan_gpu(self, probes, coarse, lut, k):
@@ -293,7 +381,7 @@ class IVFPQIndex:
         pi = ws[part * 4: part * 8].view(torch.int32)
         st = _lib.stream_ptr(self.device)
         L = _lib.lib()
-        _lib.check(L.lzk_ivfpq_scan(self.codes.data_ptr(), self.list_off.data_ptr(), probes.data_ptr(),
+        _lib.check(L.lzk_ivfpq_scan(self._codes.data_ptr(), self.list_off.data_ptr(), probes.data_ptr(),
                                     coarse.data_ptr(), lut.data_ptr(), nq, nprobe, self.m, ks, ps.data_ptr(),
                                     pi.data_ptr(), st), "lzk_ivfpq_scan")
         os_ = torch.empty((nq, k), dtype=torch.float32, device=self.device)

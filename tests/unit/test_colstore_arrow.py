@@ -114,3 +114,35 @@ def test_memory_system_commit_writes_only_changes(tmp_path):
                        db_dir=str(tmp_path), max_buffer_size=10 ** 6)
     assert ms2.get_stats()["buffer_nodes"] == ms.get_stats()["buffer_nodes"] == nodes.count()
     ms2.close()
+
+
+def test_fragment_written_as_several_record_batches(tmp_path):
+    """A fragment larger than one Arrow array's capacity is written as several
+    record batches (a 10M x 768 vector column is 7.7G floats > 2^31); the
+    runtime and pyarrow both read every batch back in order."""
+    import subprocess
+    import sys
+    import textwrap
+    code = textwrap.dedent(f"""
+        import numpy as np, pyarrow.ipc as ipc
+        from lazzaro_amd.store.colstore import ColumnarTable, NODE_SCHEMA, read_fragments
+        t = ColumnarTable({str(tmp_path)!r}, "nodes", NODE_SCHEMA)
+        n = 1000
+        rows = [dict(id=f"n{{i}}", user_id="u", content="c" * (i % 7), vector=[float(i)] * 8, type="semantic",
+                     timestamp=float(i), access_count=i, last_accessed=0.0, salience=0.5, is_super_node=False,
+                     child_ids="[]", parent_id="", shard_key="s", metadata="{{}}") for i in range(n)]
+        t.add_rows(rows)
+        f = t.fragment_files()[0]
+        assert ipc.open_file(f).num_record_batches > 1
+        got = t.scan_columns([("user_id", "u")])
+        assert list(got["id"]) == [f"n{{i}}" for i in range(n)]
+        assert np.array_equal(got["vector"][:, 0], np.arange(n, dtype=np.float32))
+        pa_t = read_fragments(t.path)
+        assert pa_t.num_rows == n and pa_t.column("id").to_pylist() == [f"n{{i}}" for i in range(n)]
+        print("ok")
+    """)
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, LZK_COLSTORE_BATCH_VALUES="1000", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
