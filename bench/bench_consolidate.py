@@ -155,6 +155,9 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
            "nodes_per_rank": nodes, "convs_per_rank_step": convs, "facts_per_conv": facts,
            "buffer_nodes_total": nodes * comm.world, "nodes_rank0": g.num_nodes(), "edges_rank0": g.num_edges,
            "per_step_rank0": {k: round(v / steps, 1) for k, v in agg.items()},
+           # per-rank scan work (facts x rows of the rank's own tenant): no
+           # rank ever scans another rank's rows, so it is independent of N
+           "scan_facts_x_rows_per_rank_step": int(convs * facts * g.n),
            "path": "MemorySystem.consolidate_batch (tenant-DP)",
            "hierarchical_clustering": {"mode": "kmeans", "every_steps": cluster_every, "fine": n_fine, "top": n_top,
                                        "iters_per_pass": cluster_iters, "seed_pass_ms": round(seed_ms, 1)},

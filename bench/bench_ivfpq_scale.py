@@ -32,17 +32,33 @@ def log(*a):
 
 
 class Mixture:
-    def __init__(self, d, clusters, noise, seed, dev):
+    """Gaussian mixture. ``intrinsic`` = 0: isotropic in all d dimensions
+    (every direction carries cluster noise -- product quantisation's worst
+    case); ``intrinsic`` = k > 0: the mixture lives in a random k-dimensional
+    subspace (orthonormal basis P) plus a small isotropic ambient term
+    (``ambient`` of the energy) -- the low intrinsic dimensionality that
+    learned embeddings have."""
+
+    def __init__(self, d, clusters, noise, seed, dev, intrinsic=0, ambient=0.1):
         self.d, self.noise, self.seed, self.dev = d, noise, seed, dev
+        self.k, self.ambient = intrinsic or d, ambient if intrinsic else 0.0
         g = torch.Generator(device=dev).manual_seed(seed)
-        self.centers = torch.nn.functional.normalize(torch.randn(clusters, d, device=dev, generator=g), dim=1)
+        self.centers = torch.nn.functional.normalize(torch.randn(clusters, self.k, device=dev, generator=g), dim=1)
+        self.P = None
+        if intrinsic:
+            q, _ = torch.linalg.qr(torch.randn(d, self.k, device=dev, generator=g))
+            self.P = q.T.contiguous()  # [k, d]
 
     def chunk(self, c, m):
         """Chunk ``c`` of ``m`` points (deterministic in (seed, c))."""
         g = torch.Generator(device=self.dev).manual_seed(self.seed * 1_000_003 + 7919 * (c + 1))
         lab = torch.randint(0, self.centers.shape[0], (m,), device=self.dev, generator=g)
-        x = self.centers[lab]
-        x += torch.randn(m, self.d, device=self.dev, generator=g).mul_(self.noise / self.d ** 0.5)
+        z = self.centers[lab]
+        z += torch.randn(m, self.k, device=self.dev, generator=g).mul_(self.noise / self.k ** 0.5)
+        if self.P is None:
+            return torch.nn.functional.normalize(z, dim=1)
+        x = torch.nn.functional.normalize(z, dim=1) @ self.P
+        x += torch.randn(m, self.d, device=self.dev, generator=g).mul_(self.ambient / self.d ** 0.5)
         return torch.nn.functional.normalize(x, dim=1)
 
 
@@ -52,6 +68,8 @@ def main():
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--clusters", type=int, default=100_000)
     ap.add_argument("--noise", type=float, default=1.0)
+    ap.add_argument("--intrinsic", type=int, default=0, help="mixture subspace dimension (0 = isotropic)")
+    ap.add_argument("--ambient", type=float, default=0.1)
     ap.add_argument("--nlist", type=int, default=16384)
     ap.add_argument("--m", type=int, default=64)
     ap.add_argument("--keep", default="int8", choices=["int8", "fp8", "bf16"])
@@ -63,7 +81,7 @@ def main():
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    mix = Mixture(a.dim, a.clusters, a.noise, 1, dev)
+    mix = Mixture(a.dim, a.clusters, a.noise, 1, dev, a.intrinsic, a.ambient)
     n_chunks = (a.n + a.chunk - 1) // a.chunk
     sizes = [min(a.chunk, a.n - c * a.chunk) for c in range(n_chunks)]
 
@@ -88,8 +106,8 @@ def main():
     t_add = time.time() - t0
     log(f"built {a.n:,} vectors in {t_add:.0f}s; index {idx.memory_bytes() / 1e9:.1f} GB")
 
-    q = Mixture(a.dim, a.clusters, a.noise, 1, dev)
-    q.seed = 99  # same centres, fresh points
+    q = Mixture(a.dim, a.clusters, a.noise, 1, dev, a.intrinsic, a.ambient)
+    q.seed = 99  # same centres and subspace, fresh points
     Q = q.chunk(0, a.nq)
     Q16 = Q.to(torch.bfloat16)
     best_s = torch.full((a.nq, 10), float("-inf"), device=dev)
@@ -125,7 +143,9 @@ def main():
             res.append(r)
             log(json.dumps(r))
     out = {"metric": "IVF-PQ QPS vs recall@10 (exact fp32 truth)", "n": a.n, "dim": a.dim,
-           "data": f"synthetic Gaussian mixture, {a.clusters} clusters, noise {a.noise}, unit-normalised",
+           "data": (f"synthetic Gaussian mixture, {a.clusters} clusters, noise {a.noise}, "
+                    + (f"in a random {a.intrinsic}-d subspace + {a.ambient} ambient noise, " if a.intrinsic
+                       else "isotropic, ") + "unit-normalised"),
            "nlist": a.nlist, "m": a.m, "rerank_copy": a.keep, "nq": a.nq,
            "index_bytes": idx.memory_bytes(), "bytes_per_vector": round(idx.memory_bytes() / a.n, 1),
            "hbm_allocated_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),

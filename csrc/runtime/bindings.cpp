@@ -4,6 +4,8 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <string_view>
+#include <unordered_map>
 
 #include "colstore.h"
 #include "tokenizer.h"
@@ -71,9 +73,40 @@ py::array_t<T> adopt(std::vector<T>&& v, std::vector<py::ssize_t> shape) {
 py::object from_column(Column& c) {
   switch (c.type) {
     case ColType::Str: {
-      py::list l(c.s.size());
-      for (size_t i = 0; i < c.s.size(); ++i) l[i] = py::str(c.s[i]);
-      return l;
+      // CPython API directly (a 10M-row column is 10M objects), and values
+      // that repeat (type, shard_key, parent_id, "[]", "{}") share one str
+      // object -- a bounded intern cache, so unique columns (id, content)
+      // only pay for its lookups until it fills
+      const size_t n = c.s.size();
+      PyObject* l = PyList_New((Py_ssize_t)n);
+      if (!l) throw py::error_already_set();
+      std::unordered_map<std::string_view, PyObject*> cache;
+      constexpr size_t kCacheMax = 4096;
+      size_t misses = 0;
+      for (size_t i = 0; i < n; ++i) {
+        const std::string& v = c.s[i];
+        PyObject* o = nullptr;
+        if (misses < 4 * kCacheMax) {
+          auto it = cache.find(std::string_view(v));
+          if (it != cache.end()) {
+            o = it->second;
+            Py_INCREF(o);
+          } else {
+            ++misses;
+          }
+        }
+        if (!o) {
+          o = PyUnicode_DecodeUTF8(v.data(), (Py_ssize_t)v.size(), "replace");
+          if (!o) { Py_DECREF(l); throw py::error_already_set(); }
+          if (cache.size() < kCacheMax && misses < 4 * kCacheMax) {
+            Py_INCREF(o);
+            cache.emplace(std::string_view(v), o);
+          }
+        }
+        PyList_SET_ITEM(l, (Py_ssize_t)i, o);
+      }
+      for (auto& kv : cache) Py_DECREF(kv.second);
+      return py::reinterpret_steal<py::object>(l);
     }
     case ColType::F64: { auto n = (py::ssize_t)c.f64.size(); return adopt(std::move(c.f64), {n}); }
     case ColType::F32: { auto n = (py::ssize_t)c.f32.size(); return adopt(std::move(c.f32), {n}); }

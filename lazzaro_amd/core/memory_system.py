@@ -1240,7 +1240,7 @@ def _h2d(a: np.ndarray, dev, chunk_bytes: int = 64 << 20) -> torch.Tensor:
         b = j & 1
         if evs[b] is not None:
             evs[b].synchronize()
-        bufs[b][: c1 - c0].numpy()[:] = flat_src[c0:c1]
+        bufs[b][: c1 - c0].copy_(torch.from_numpy(flat_src[c0:c1]))  # multi-threaded host copy
         flat_dst[c0:c1].copy_(bufs[b][: c1 - c0], non_blocking=True)
         evs[b] = torch.cuda.Event()
         evs[b].record(st)

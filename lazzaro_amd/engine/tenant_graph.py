@@ -332,13 +332,18 @@ class TenantGraph:
         tlist = types if (types is not None and not isinstance(types, str)) else None
         tdef = types if isinstance(types, str) else "semantic"
         n0 = self.n
-        if len(set(ids)) == m and self.row_of.keys().isdisjoint(ids):
+        fresh_map = dict(zip(ids, range(n0, n0 + m))) if not self.row_of else None  # empty graph (a load)
+        if (fresh_map is not None and len(fresh_map) == m) or (
+                fresh_map is None and len(set(ids)) == m and self.row_of.keys().isdisjoint(ids)):
             # bulk append of fresh ids (loads, large ingests): no per-row loop
             self.reserve(n0 + m)
             self.ids.extend(ids)
             self.content.extend(contents)
             self.types.extend(tlist if tlist is not None else [tdef] * m)
-            self.row_of.update(zip(ids, range(n0, n0 + m)))
+            if fresh_map is not None:
+                self.row_of = fresh_map
+            else:
+                self.row_of.update(zip(ids, range(n0, n0 + m)))
             self.n = n0 + m
             rl = range(n0, n0 + m)
             rt = torch.arange(n0, n0 + m, dtype=torch.long, device=dev)
