@@ -35,7 +35,7 @@ import re
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from typing import Dict, Iterable, List, Optional
+from typing import Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -1013,6 +1013,55 @@ Be clinical yet insightful. Do not include conversational filler."""
         return self._call_llm([{"role": "system", "content": sys_prompt},
                                {"role": "user", "content": f"User Observations:\n{obs}"}])
 
+    # ------------------------------------------------------------ live migration (C3)
+    def export_state(self) -> Tuple[Dict, torch.Tensor]:
+        """The tenant's graph as (JSON-able metadata, fp32 vector rows on the
+        device) -- what :meth:`import_state` on another rank rebuilds it from
+        without touching the store (``DistributedMemoryService.migrate``)."""
+        with self._graph_lock:
+            g = self.graph
+            rows = g.node_rows_where()
+            nc = export_node_columns(g, rows, device_vectors=True)
+            vec = nc.pop("vector", None)
+            if vec is None:
+                vec = torch.zeros((0, g.dim or 0), device=g.device)
+            nc.pop("count", None)
+            rl = rows.tolist()
+            nc["_has"] = g.has_emb[torch.as_tensor(rows, dtype=torch.long).to(g.device)].bool().cpu().tolist() \
+                if rows.size else []
+            nc["_odd"] = {str(j): g.odd_emb[r] for j, r in enumerate(rl) if r in g.odd_emb}
+            ec = export_edge_columns(g, np.arange(g.num_edges))
+            ec.pop("count", None)
+            meta = {"nodes": _jsonable_cols(nc), "edges": _jsonable_cols(ec), "profile": self._profile_blob(),
+                    "conversation_count": self.conversation_count}
+            return meta, vec.reshape(len(rl), -1)
+
+    def import_state(self, meta: Dict, vectors: torch.Tensor) -> None:
+        """Replace this tenant's graph by an :meth:`export_state` image."""
+        with self._graph_lock:
+            self._replace_graph()
+            nc = dict(meta["nodes"])
+            if nc.get("id"):
+                for k in ("timestamp", "access_count", "last_accessed", "salience", "is_super_node", "decay_clock"):
+                    if k in nc:
+                        nc[k] = np.asarray(nc[k])
+                nc["_odd"] = {int(j): v for j, v in nc.get("_odd", {}).items()}
+                nc["vector"] = vectors
+                ec = dict(meta["edges"]) if meta["edges"].get("id") else None
+                if ec is not None:
+                    for k in ("weight", "co_occurrence", "last_updated", "decay_clock"):
+                        if k in ec:
+                            ec[k] = np.asarray(ec[k])
+                prof = meta.get("profile") or {}
+                eng = prof.get("_engine", {})
+                bulk_load(self.graph, nc, ec, float(eng.get("decay_clock", 0.0)))
+                self.node_counter = max(int(eng.get("node_counter", 0)), int(eng.get("max_node_id", 0)))
+                self._max_node_id = int(eng.get("max_node_id", 0))
+                self.profile = Profile.from_dict(prof)
+            self.conversation_count = int(meta.get("conversation_count", 0))
+            if self.query_cache:
+                self.query_cache.invalidate_results()
+
     def close(self):
         if self.background_executor:
             self.background_executor.shutdown(wait=True)
@@ -1021,8 +1070,10 @@ Be clinical yet insightful. Do not include conversational filler."""
 
 
 # ---------------------------------------------------------------- columnar I/O
-def export_node_columns(g: TenantGraph, rows: np.ndarray) -> Dict:
-    """Store columns (SURVEY.md App. D + ``decay_clock``) of graph rows."""
+def export_node_columns(g: TenantGraph, rows: np.ndarray, device_vectors: bool = False) -> Dict:
+    """Store columns (SURVEY.md App. D + ``decay_clock``) of graph rows.
+    ``device_vectors``: the vector column stays a device tensor (migration
+    over the interconnect) instead of a host array."""
     rows = np.asarray(rows, dtype=np.int64)
     n = rows.size
     D = g.dim or 0
@@ -1030,7 +1081,10 @@ def export_node_columns(g: TenantGraph, rows: np.ndarray) -> Dict:
         return {"id": [], "count": 0}
     with g.on_stream():
         rt = torch.as_tensor(rows).to(g.device)
-        vec = g.emb32[rt].cpu().numpy() if g.dim is not None else np.zeros((n, 0), dtype=np.float32)
+        if device_vectors:
+            vec = g.emb32[rt].clone() if g.dim is not None else torch.zeros((n, 0), device=g.device)
+        else:
+            vec = g.emb32[rt].cpu().numpy() if g.dim is not None else np.zeros((n, 0), dtype=np.float32)
         cols = {k: getattr(g, c)[rt].cpu().numpy() for k, c in
                 (("timestamp", "ts"), ("access_count", "acc"), ("last_accessed", "last"), ("salience", "sal"),
                  ("is_super_node", "sup"), ("parent", "parent"), ("shard", "shard"))}
@@ -1044,7 +1098,7 @@ def export_node_columns(g: TenantGraph, rows: np.ndarray) -> Dict:
         "count": n,
         "id": ids,
         "content": [g.content[r] for r in rows.tolist()],
-        "vector": np.ascontiguousarray(vec, dtype=np.float32),
+        "vector": vec if torch.is_tensor(vec) else np.ascontiguousarray(vec, dtype=np.float32),
         "type": [g.types[r] for r in rows.tolist()],
         "timestamp": cols["timestamp"].astype(np.float64),
         "access_count": cols["access_count"].astype(np.int32),
@@ -1167,7 +1221,9 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
     V = nc["vector"]
     has = nc.get("_has")
     emb = None
-    if V.shape[1]:
+    if torch.is_tensor(V):  # already a tensor (a migrated tenant's device rows)
+        emb = V.to(g.device, torch.float32) if V.shape[1] else None
+    elif V.shape[1]:
         emb = _h2d(np.ascontiguousarray(V, dtype=np.float32), g.device) if g.on_gpu else torch.from_numpy(
             np.ascontiguousarray(V, dtype=np.float32))
     children = {}
@@ -1212,6 +1268,10 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
                            lu=torch.as_tensor(np.asarray(ec["last_updated"])[keep], dtype=torch.float64))
     g.decay_log = clock
     g.clear_tracking()
+
+
+def _jsonable_cols(cols: Dict) -> Dict:
+    return {k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in cols.items()}
 
 
 def _max_node_num(ids) -> int:

@@ -27,10 +27,12 @@ All collective methods must be called by every rank in the same order.
 """
 from __future__ import annotations
 
+import inspect
 import json
 from collections import OrderedDict
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from .comm import Communicator
@@ -78,11 +80,14 @@ class DistributedMemoryService:
         self._owner = owner
         self.placement = placement
         self.max_resident = max_resident
+        self._moved: Dict[str, int] = {}  # migrate() overrides of the placement
         self.systems: "OrderedDict[str, object]" = OrderedDict()
 
     # ------------------------------------------------------------ placement
     def owner(self, user: str) -> int:
         """The CURRENT communicator rank that owns ``user``."""
+        if user in self._moved:
+            return self._moved[user]
         if self._owner is not None:
             return self._owner(user)
         if self.placement is not None:
@@ -97,6 +102,7 @@ class DistributedMemoryService:
         their first request (every durable byte is in the store, so a dead
         rank loses no committed state). Returns the released tenants."""
         self.comm, self.placement, self._owner = comm, placement, None
+        self._moved = {}
         gone = [u for u in self.systems if not self.is_local(u)]
         for u in gone:
             ms = self.systems.pop(u)
@@ -113,7 +119,7 @@ class DistributedMemoryService:
             raise KeyError(f"tenant {user!r} is owned by rank {self.owner(user)}, not {self.comm.rank}")
         ms = self.systems.get(user)
         if ms is None:
-            ms = self.factory(user)
+            ms = self._build(user)
             self.systems[user] = ms
             while len(self.systems) > self.max_resident:
                 _, old = self.systems.popitem(last=False)
@@ -122,6 +128,58 @@ class DistributedMemoryService:
         else:
             self.systems.move_to_end(user)
         return ms
+
+    def migrate(self, moves: Dict[str, int]) -> List[str]:
+        """SPMD live re-shard of tenants (C3): ``moves`` = {user: new rank},
+        identical on every rank. A resident tenant's owner commits it, exports
+        its graph (``MemorySystem.export_state``) and ships it in two
+        all-to-all-v exchanges -- the fp32 vector rows device to device over
+        RCCL/xGMI, the other columns as serialized bytes -- and the new owner
+        rebuilds it with ``import_state`` (no store read). Tenants that are
+        not resident anywhere just change owner (loaded from the store on
+        first use). Returns the tenants this rank received."""
+        comm = self.comm
+        me = comm.rank
+        out_meta: List[List] = [[] for _ in range(comm.world)]
+        out_vec: List[List[torch.Tensor]] = [[] for _ in range(comm.world)]
+        for user in sorted(moves):
+            dst = int(moves[user])
+            if user in self.systems and dst != me:
+                ms = self.systems.pop(user)
+                ms._save_to_persistence()
+                meta, vec = ms.export_state()
+                out_meta[dst].append([user, meta, list(vec.shape)])
+                out_vec[dst].append(vec.reshape(-1).float())
+                ms.close()
+        got_meta = self._exchange(out_meta)
+        dev = comm.device
+        send = [torch.cat(v) if v else torch.zeros(0) for v in out_vec]
+        counts = [int(t.numel()) for t in send]
+        flat = torch.cat([t.to(dev) for t in send]) if sum(counts) else torch.zeros(0, device=dev)
+        rc = comm.exchange_counts(torch.tensor(counts, dtype=torch.int64, device=dev)).cpu().tolist()
+        recv = comm.all_to_all_v(flat, counts, rc) if comm.world > 1 else flat
+        self._moved.update({u: int(r) for u, r in moves.items()})
+        received, off = [], 0
+        for src in range(comm.world):
+            for user, meta, shape in got_meta[src]:
+                n = int(np.prod(shape)) if shape else 0
+                vec = recv[off: off + n].reshape(shape)
+                off += n
+                ms = self._build(user, load=False)
+                ms.import_state(meta, vec)
+                self.systems[user] = ms
+                received.append(user)
+        return received
+
+    def _build(self, user: str, load: bool = True):
+        """factory(user[, load_from_disk=...]): a factory without the keyword
+        always loads the tenant from the store itself."""
+        try:
+            params = inspect.signature(self.factory).parameters
+            kw = "load_from_disk" in params or any(p.kind == p.VAR_KEYWORD for p in params.values())
+        except (TypeError, ValueError):
+            kw = False
+        return self.factory(user, load_from_disk=load) if kw else self.factory(user)
 
     # ------------------------------------------------------------ request routing
     def _exchange(self, outgoing: List[List]) -> List[List]:

@@ -116,3 +116,50 @@ def test_service_matches_single_process(world, tmp_path):
     assert all(g == globs[0] for g in globs) and len(globs[0]) == 4
     for u in USERS:
         assert merged[u] == ref[u], u
+
+
+def _factory_kw(db, user, load_from_disk=True):
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    return MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=32), enable_async=False,
+                        db_dir=db, user_id=user, device="cpu", max_buffer_size=50, super_node_threshold=3,
+                        load_from_disk=load_from_disk)
+
+
+def _migrate_workload(comm, db):
+    from lazzaro_amd.parallel.service import DistributedMemoryService
+    svc = DistributedMemoryService(comm, functools.partial(_factory_kw, db))
+    mine = [u for u in USERS if svc.is_local(u)]
+    for s in range(len(_script(USERS[0])) - 3):  # the conversations only
+        svc.serve([(u,) + _script(u)[s] for u in mine])
+    probe = [(u, "search_memories", "project deadline hobby", 3) for u in USERS]
+    before = svc.serve(probe if comm.rank == 0 else [])
+    stats_before = svc.serve([(u, "get_stats") for u in USERS] if comm.rank == 0 else [])
+    moves = {u: (svc.owner(u) + 1) % comm.world for u in USERS}
+    received = svc.migrate(moves)
+    # the moved tenants were rebuilt from the interconnect image, not the store
+    fresh = all(not svc.systems[u].graph.n == 0 for u in received)
+    after = svc.serve(probe if comm.rank == 0 else [])
+    stats_after = svc.serve([(u, "get_stats") for u in USERS] if comm.rank == 0 else [])
+    resident = sorted(svc.systems)
+    owners = {u: svc.owner(u) for u in USERS}
+    svc.close()
+    return json.dumps({"before": before, "after": after, "sb": _strip(stats_before), "sa": _strip(stats_after),
+                       "received": received, "resident": resident, "owners": owners, "fresh": fresh,
+                       "moves": moves})
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_service_live_migration(world, tmp_path):
+    """migrate(): tenants change owner over all-to-all-v (vectors + columns)
+    and answer exactly as before; ownership is consistent on every rank."""
+    outs = spawn(world, functools.partial(_migrate_workload, db=str(tmp_path / f"mig{world}")))
+    d = {r: json.loads(v) for r, v in outs.items()}
+    assert d[0]["before"] == d[0]["after"] and any(d[0]["before"])
+    for a, b in zip(d[0]["sb"], d[0]["sa"]):
+        assert {k: v for k, v in a.items() if k != "memory"} == {k: v for k, v in b.items() if k != "memory"}
+    for r, x in d.items():
+        assert x["owners"] == d[0]["owners"] and x["fresh"]
+        assert sorted(x["received"]) == sorted(u for u, m in x["moves"].items() if m == r and u in
+                                               {u2 for y in d.values() for u2 in y["resident"]})
+        assert all(x["owners"][u] == r for u in x["resident"])
