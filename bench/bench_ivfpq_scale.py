@@ -140,6 +140,11 @@ def main():
             dt = (time.time() - t1) / 3
             r = {"nprobe": nprobe, "rerank": rr, "ms_per_batch": round(dt * 1e3, 2), "qps": round(a.nq / dt, 1),
                  "recall_at_10": round(recall_at_k(ids, best_i), 4)}
+            lc = getattr(idx, "last_candidates", None)
+            if rr > 16 and lc is not None:
+                cap = max(idx.CAND_CAP * rr, idx.CAND_MIN)
+                r["threshold_rows_mean"] = round(float(lc.float().mean()), 1)
+                r["overflow_queries"] = int((lc > cap).sum())
             res.append(r)
             log(json.dumps(r))
     out = {"metric": "IVF-PQ QPS vs recall@10 (exact fp32 truth)", "n": a.n, "dim": a.dim,

@@ -179,6 +179,66 @@ __global__ __launch_bounds__(256) void ivfpq_scan_deep_kernel(const unsigned cha
   }
 }
 
+// Threshold pass of the deep candidate search: every row of a probed list
+// whose PQ score reaches the query's threshold thr[q] is appended to the
+// query's list (score, code row). thr[q] is the R-th best PQ score of the
+// first pass's per-list pools -- a lower bound of the true R-th best over the
+// probed lists -- so the appended set holds the exact PQ top-R however the
+// query's neighbours concentrate in one list (the per-list pools cap at
+// 4 x DEEP_W). Appends are wave-aggregated (ballot + one atomicAdd per wave
+// per step); cnt[q] keeps counting past cap so the caller sees an overflow.
+template <int M>
+__global__ __launch_bounds__(256) void ivfpq_scan_thresh_kernel(const unsigned char* __restrict__ codes,
+                                                                const long* __restrict__ list_off,
+                                                                const int* __restrict__ probes,
+                                                                const float* __restrict__ coarse,
+                                                                const float* __restrict__ lut,
+                                                                const float* __restrict__ thr, int nprobe, int cap,
+                                                                int* __restrict__ cnt, float* __restrict__ out_s,
+                                                                int* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) float slut[];  // [M][256]
+  const int qp = blockIdx.x;
+  const int q = qp / nprobe;
+  const int list = probes[qp];
+  const float base = coarse[qp];
+  const float t = thr[q];
+  const float* L = lut + (long)q * M * 256;
+  for (int i = threadIdx.x * 4; i < M * 256; i += 256 * 4)
+    *reinterpret_cast<f32x4*>(slut + i) = *reinterpret_cast<const f32x4*>(L + i);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long r0 = (list >= 0) ? list_off[list] : 0, r1 = (list >= 0) ? list_off[list + 1] : 0;
+  for (long rb = r0; rb < r1; rb += 256) {  // uniform trip count: every lane reaches the ballot
+    const long r = rb + threadIdx.x;
+    float s = LZK_NEG_INF;
+    if (r < r1) {
+      const unsigned char* c = codes + r * M;
+      s = base;
+#pragma unroll
+      for (int j0 = 0; j0 < M; j0 += 16) {
+        uint4 v = *reinterpret_cast<const uint4*>(c + j0);
+        unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += slut[(j0 + u) * 256 + ((w[u >> 2] >> (8 * (u & 3))) & 0xff)];
+      }
+    }
+    const bool take = r < r1 && s >= t;
+    const unsigned long long m = __ballot(take);
+    if (m == 0ull) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    int pos0 = 0;
+    if (lane == leader) pos0 = atomicAdd(cnt + q, __popcll(m));
+    pos0 = __shfl(pos0, leader, 64);
+    if (take) {
+      const int pos = pos0 + __popcll(m & ((1ull << lane) - 1ull));
+      if (pos < cap) {
+        out_s[(long)q * cap + pos] = s;
+        out_i[(long)q * cap + pos] = (int)r;
+      }
+    }
+  }
+}
+
 // Exact re-rank of a deep candidate list (IVF-PQ candidates, BASELINE config 5):
 // score = <q, v_row> over the kept copy -- FMT 1: fp8 e4m3, FMT 2: int8, each
 // with a per-row scale (D + 4 B/vector), or FMT 0: bf16 -- then the top-k by
@@ -357,6 +417,35 @@ LZK_EXPORT int lzk_ivfpq_scan_deep(const void* codes, const long* list_off, cons
 }
 
 LZK_EXPORT int lzk_ivfpq_deep_width() { return 4 * DEEP_W; }
+
+// threshold pass: cnt [nq] zeroed by the caller; out [nq, cap]
+LZK_EXPORT int lzk_ivfpq_scan_thresh(const void* codes, const long* list_off, const int* probes, const float* coarse,
+                                     const float* lut, const float* thr, int nq, int nprobe, int M, int cap, int* cnt,
+                                     float* os, int* oi, void* stream) {
+  if (nq <= 0 || nprobe <= 0 || cap <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)nq * nprobe), block(256);
+  size_t lds = (size_t)M * 256 * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned char* c = (const unsigned char*)codes;
+#define GO(MM)                                                                                                      \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)ivfpq_scan_thresh_kernel<MM>,                                            \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                \
+    hipLaunchKernelGGL((ivfpq_scan_thresh_kernel<MM>), grid, block, lds, st, c, list_off, probes, coarse, lut, thr, \
+                       nprobe, cap, cnt, os, oi);                                                                   \
+  } while (0)
+  switch (M) {
+    case 16: GO(16); break;
+    case 32: GO(32); break;
+    case 48: GO(48); break;
+    case 64: GO(64); break;
+    case 96: GO(96); break;
+    case 128: GO(128); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef GO
+  return (int)hipGetLastError();
+}
 
 // partial lists: [nq, nprobe, kslot] (rows index the code array; -1 = empty)
 LZK_EXPORT int lzk_ivfpq_scan(const void* codes, const long* list_off, const int* probes, const float* coarse,

@@ -214,6 +214,9 @@ class TenantGraph:
             setattr(self, k, v)
         self.cap = cap
 
+    # rows of the mini-batch k-means refinement steps of cluster_pass
+    CLUSTER_SAMPLE = 1 << 20
+
     # fp8 (e4m3) copy of the rows for the store search's candidate scan
     # (ops.search.flat_topk_fp8): rows are scaled by FP8_ROW_SCALE, which
     # keeps unit-norm rows (|x_i| <= 1) inside e4m3's normal range
@@ -1236,7 +1239,10 @@ class TenantGraph:
             kt = min(n_top, kf)
             prev = getattr(self, "hier", None) or {}
             init_f = prev.get("fine_c") if prev.get("fine_c") is not None and prev["fine_c"].shape[0] == kf else None
-            fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live)
+            # large tenants: mini-batch refinement steps on a 1M-row sample,
+            # then one full assign + update (labels for every row)
+            smp = self.CLUSTER_SAMPLE if n_live > 2 * self.CLUSTER_SAMPLE else 0
+            fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp)
             init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
             tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
             lab = lab.long()

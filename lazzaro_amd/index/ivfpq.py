@@ -35,6 +35,8 @@ _lib.register("lzk_ivfpq_scan", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P,
 _lib.register("lzk_ivfpq_scan_deep", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I, _lib.I,
                                                _lib.P, _lib.P, _lib.P])
 _lib.register("lzk_ivfpq_deep_width", _lib.I, [])
+_lib.register("lzk_ivfpq_scan_thresh", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.I,
+                                                _lib.I, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P])
 
 _lib.register("lzk_rerank", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.I, _lib.I, _lib.P, _lib.I,
                                       _lib.I, _lib.I, _lib.P, _lib.P, _lib.P])
@@ -276,6 +278,8 @@ class IVFPQIndex:
         kk = max(k, rerank) if rerank else k
         if self.device.type != "cuda":
             s, rows = self._scan_ref(probes, coarse, lut, kk)
+        elif rerank and self._vec is not None and kk > KSLOTS[-1]:
+            s, rows = self._scan_candidates(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
         elif kk <= KSLOTS[-1]:
             s, rows = self._scan_gpu(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, kk)
         else:
@@ -371,6 +375,39 @@ class IVFPQIndex:
             s = torch.cat([s, torch.full((nq, k - kk), float("-inf"), device=self.device)], 1)
             rows = torch.cat([rows, torch.full((nq, k - kk), -1, dtype=torch.long, device=self.device)], 1)
         return s, rows
+
+    # threshold-pass buffer: CAND_CAP x the requested depth (at least
+    # CAND_MIN): with weak PQ codes a crowded list makes the pooled threshold
+    # loose, and everything above it must fit before the PQ top-R is taken
+    CAND_CAP = 16
+    CAND_MIN = 32768
+
+    def _scan_candidates(self, probes, coarse, lut, R):
+        """Re-rank candidates: the exact PQ top-R over the probed lists (plus
+        ties). Pass 1 (``ivfpq_scan_deep``) pools each list's best rows; the
+        R-th best pooled score is a lower bound of the true R-th best; pass 2
+        (``ivfpq_scan_thresh``) appends EVERY probed row at or above it, so a
+        query whose neighbours crowd into one list still gets all of them.
+        Returns (PQ scores, code rows) [nq, R] of the collected rows' PQ
+        top-R, -1 padded."""
+        nq, nprobe = probes.shape
+        ps, _ = self._scan_deep(probes, coarse, lut, R)
+        thr = ps[:, R - 1].contiguous()  # -inf when the pools hold fewer than R rows: take everything
+        cap = max(self.CAND_CAP * R, self.CAND_MIN)
+        L = _lib.lib()
+        cnt = torch.zeros(nq, dtype=torch.int32, device=self.device)
+        os_ = torch.empty((nq, cap), dtype=torch.float32, device=self.device)
+        oi = torch.empty((nq, cap), dtype=torch.int32, device=self.device)
+        _lib.check(L.lzk_ivfpq_scan_thresh(self._codes.data_ptr(), self.list_off.data_ptr(), probes.data_ptr(),
+                                           coarse.data_ptr(), lut.data_ptr(), thr.data_ptr(), nq, nprobe, self.m,
+                                           cap, cnt.data_ptr(), os_.data_ptr(), oi.data_ptr(),
+                                           _lib.stream_ptr(self.device)), "lzk_ivfpq_scan_thresh")
+        self.last_candidates = cnt  # per-query count (> cap: overflowed, kept the first cap)
+        valid = torch.arange(cap, device=self.device)[None, :] < cnt.clamp(max=cap)[:, None]
+        sc = torch.where(valid, os_, torch.full_like(os_, float("-inf")))
+        ts, j = torch.topk(sc, min(R, cap), dim=1)
+        rows = torch.gather(oi, 1, j).long()
+        return ts, torch.where(torch.isneginf(ts), torch.full_like(rows, -1), rows)
 
     def _scan_gpu(self, probes, coarse, lut, k):
         nq, nprobe = probes.shape

@@ -62,12 +62,18 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
 
 
 def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
-           init: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None
-           ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+           init: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
+           sample: int = 0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """X: unit rows [n, Dp] (bf16 on GPU). Returns (centroids fp32 [k, Dp],
     centroids bf16 [k, Dp], labels int32 [n]). ``mask`` (bool [n]): rows
     that take part (others get label -1 and do not move the centroids) --
-    an arena with tombstones is clustered in place, without a gather."""
+    an arena with tombstones is clustered in place, without a gather.
+    ``sample`` > 0 and fewer than the participating rows: every iteration but
+    the last refines the centroids on a fresh random ``sample``-row subset
+    (mini-batch Lloyd steps); the last one assigns and updates over all rows,
+    so every row's label is exact for the returned centroids' predecessors as
+    in the full algorithm -- at 10M rows x 4096 centroids a full assign is
+    63 TFLOP, a 1M-row one 6.3."""
     n, Dp = X.shape
     dev = X.device
     if init is None and k <= 4096:
@@ -84,7 +90,26 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
     c32 = c32 / c32.norm(dim=1, keepdim=True).clamp_min(1e-30)
     c16 = c32.to(X.dtype)
     lab = None
-    for _ in range(iters):
+    rows_all = torch.nonzero(mask).flatten() if (sample and mask is not None) else None
+    n_part = int(rows_all.numel()) if rows_all is not None else n
+    for it in range(iters):
+        if sample and n_part > sample and it < iters - 1:
+            g = torch.Generator(device="cpu").manual_seed(seed * 7919 + it + 1)
+            pick = torch.randperm(n_part, generator=g)[:sample].to(dev)
+            Xs = X[rows_all[pick] if rows_all is not None else pick]
+            ls, _ = assign(Xs, c16)
+            c32n, c16n, cnt = G.centroids(Xs, ls, k, normalize=not distributed, pad_to=Dp if X.is_cuda else 0)
+            if distributed:
+                sums = c32n * cnt.clamp_min(1)[:, None].float()
+                comm.all_reduce(sums)
+                comm.all_reduce(cnt)
+                c32n = sums / cnt.clamp_min(1)[:, None].float()
+                c32n = c32n / c32n.norm(dim=1, keepdim=True).clamp_min(1e-30)
+                c16n = None
+            empty = cnt == 0
+            c32 = torch.where(empty[:, None], c32, c32n)
+            c16 = c32.to(X.dtype) if c16n is None else torch.where(empty[:, None], c16, c16n)
+            continue
         lab, _ = assign(X, c16)
         if mask is not None:
             lab = torch.where(mask, lab, torch.full_like(lab, -1))

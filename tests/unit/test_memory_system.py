@@ -470,3 +470,19 @@ def test_evict_select_matches_full_sort_with_ties():
     want = np.lexsort((okey, score))[:excess].tolist()
     got = g.evict(g.num_nodes() - excess, now=now)
     assert got == want
+
+
+def test_kmeans_minibatch_sample_matches_quality():
+    """kmeans(sample=...): refinement steps on a random subset, last step on
+    all rows -- every masked-in row labelled, clusters recovered."""
+    import torch
+    from lazzaro_amd.index.kmeans import kmeans
+    g = torch.Generator().manual_seed(0)
+    C, per, d = 8, 400, 32
+    cen = torch.nn.functional.normalize(torch.randn(C, d, generator=g), dim=1)
+    X = torch.nn.functional.normalize(cen.repeat_interleave(per, 0) + 0.05 * torch.randn(C * per, d, generator=g), dim=1)
+    mask = torch.rand(C * per, generator=g) > 0.05
+    c32, _, lab = kmeans(X, C, iters=4, seed=1, mask=mask, sample=500)
+    assert bool((lab[mask] >= 0).all()) and bool((lab[~mask] == -1).all())
+    pure = sum(len(set(lab[j * per:(j + 1) * per][mask[j * per:(j + 1) * per]].tolist())) == 1 for j in range(C))
+    assert pure >= C - 1
