@@ -128,7 +128,9 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     def step():
         conversations, V = synth_batch(ms, convs, facts, dim, dup_rate, gen, rng)
         texts = [f["content"] for c in conversations for f in c]
-        ms._batch_embed_any(texts)  # the fact embedding runs (see module doc)
+        from lazzaro_amd.utils.tracing import tracer as _tr
+        with _tr.stage("fact_embed", dev):
+            ms._batch_embed_any(texts)  # the fact embedding runs (see module doc)
         return ms.consolidate_batch(conversations, embeddings=V)
 
     for _ in range(warmup):

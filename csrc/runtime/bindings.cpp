@@ -63,11 +63,11 @@ Column to_column(const ColSpec& spec, py::handle obj) {
 
 // numpy array that takes ownership of the vector's buffer (no copy: a
 // 10M x 768 vector column is 30 GB)
-template <class T>
-py::array_t<T> adopt(std::vector<T>&& v, std::vector<py::ssize_t> shape) {
-  auto* heap = new std::vector<T>(std::move(v));
-  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::vector<T>*>(p); });
-  return py::array_t<T>(shape, heap->data(), owner);
+template <class V>
+py::array_t<typename V::value_type> adopt(V&& v, std::vector<py::ssize_t> shape) {
+  auto* heap = new V(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<V*>(p); });
+  return py::array_t<typename V::value_type>(shape, heap->data(), owner);
 }
 
 py::object from_column(Column& c) {

@@ -127,9 +127,11 @@ std::shared_ptr<arrow::Array> to_arrow(const Column& c, int64_t r0, int64_t r1) 
       return ok_or_throw(b.Finish(), "bool column");
     }
     case ColType::VecF32: {
-      arrow::FloatBuilder vb;
-      check(vb.AppendValues(c.f32.data() + (size_t)r0 * c.dim, n * (int64_t)c.dim), "vector column");
-      auto values = ok_or_throw(vb.Finish(), "vector column");
+      // zero-copy: the Arrow array wraps the column's memory (alive until
+      // the fragment is written); no 30 GB builder copy for a 10M-row commit
+      const int64_t nv = n * (int64_t)c.dim;
+      auto buf = arrow::Buffer::Wrap(c.f32.data() + (size_t)r0 * c.dim, (size_t)nv);
+      auto values = std::make_shared<arrow::FloatArray>(nv, buf);
       return ok_or_throw(arrow::FixedSizeListArray::FromArrays(values, (int32_t)c.dim), "vector column");
     }
   }
@@ -708,7 +710,10 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
         switch (o.type) {
           case ColType::Str: o.s.insert(o.s.end(), std::make_move_iterator(s.s.begin()), std::make_move_iterator(s.s.end())); break;
           case ColType::F64: o.f64.insert(o.f64.end(), s.f64.begin(), s.f64.end()); break;
-          case ColType::F32: case ColType::VecF32: o.f32.insert(o.f32.end(), s.f32.begin(), s.f32.end()); break;
+          case ColType::F32: case ColType::VecF32:
+            if (o.f32.empty()) o.f32 = std::move(s.f32);  // the common single-fragment load: no copy
+            else o.f32.insert(o.f32.end(), s.f32.begin(), s.f32.end());
+            break;
           case ColType::I32: o.i32.insert(o.i32.end(), s.i32.begin(), s.i32.end()); break;
           case ColType::I64: o.i64.insert(o.i64.end(), s.i64.begin(), s.i64.end()); break;
           case ColType::Bool: o.b.insert(o.b.end(), s.b.begin(), s.b.end()); break;

@@ -39,13 +39,30 @@ struct ColSpec {
   uint32_t dim = 0;  // VecF32 only (0 = inferred on first append)
 };
 
+// Allocator whose value-less construct() leaves the element uninitialised, so
+// resize() before a bulk (parallel) copy does not zero-fill first: a reload
+// moves a 30 GB vector column.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind { using other = DefaultInitAlloc<U>; };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept { ::new ((void*)p) U; }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+using FloatVec = std::vector<float, DefaultInitAlloc<float>>;
+
 // A materialised column (host memory). Exactly one payload is used.
 struct Column {
   ColType type;
   uint32_t dim = 0;
   std::vector<std::string> s;
   std::vector<double> f64;
-  std::vector<float> f32;  // F32 and VecF32 (row-major n*dim)
+  FloatVec f32;  // F32 and VecF32 (row-major n*dim)
   std::vector<int32_t> i32;
   std::vector<int64_t> i64;
   std::vector<uint8_t> b;

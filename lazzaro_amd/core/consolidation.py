@@ -537,7 +537,8 @@ class ConsolidationMixin:
         with tracer.stage("evict", self._device):
             victims = g.evict(self.max_buffer_size)
         if victims:
-            self._store_delete([g.ids[r] for r in victims])
+            with tracer.stage("evict_store", "cpu"):
+                self._store_delete([g.ids[r] for r in victims])
             stats["evicted"] += len(victims)
 
     def _consolidate_batch(self, facts: List[Dict], conv: np.ndarray, B: int, embs, now: float,
@@ -584,19 +585,20 @@ class ConsolidationMixin:
 
         # ---- 2. in-batch dedupe: the store top-1 over graph rows + the facts
         # kept from earlier conversations, to a fixed point
-        S = Qn @ Qn.T
-        earlier = ct[None, :] < ct[:, None]  # [j, i]: fact i is from an earlier conversation than j
-        ins = torch.ones(M, dtype=torch.bool, device=dev)
-        for _ in range(M + 1):
-            A = torch.where(earlier & ins[None, :], S, torch.full_like(S, NEG))
-            bb_s = A.max(1).values
-            bb_i = torch.argmax((A == bb_s[:, None]).to(torch.int8), 1)
-            batch_best = bb_s > gb_s
-            best_s = torch.where(batch_best, bb_s, gb_s)
-            dup = (best_s > DEDUPE_THRESHOLD) & (batch_best | gb_node)
-            if torch.equal(~dup, ins):
-                break
-            ins = ~dup
+        with tracer.stage("cb_dedupe", self._device):
+            S = Qn @ Qn.T
+            earlier = ct[None, :] < ct[:, None]  # [j, i]: fact i is from an earlier conversation than j
+            ins = torch.ones(M, dtype=torch.bool, device=dev)
+            for _ in range(M + 1):
+                A = torch.where(earlier & ins[None, :], S, torch.full_like(S, NEG))
+                bb_s = A.max(1).values
+                bb_i = torch.argmax((A == bb_s[:, None]).to(torch.int8), 1)
+                batch_best = bb_s > gb_s
+                best_s = torch.where(batch_best, bb_s, gb_s)
+                dup = (best_s > DEDUPE_THRESHOLD) & (batch_best | gb_node)
+                if torch.equal(~dup, ins):
+                    break
+                ins = ~dup
         dup_graph = dup & ~batch_best
         dup_batch = dup & batch_best
 

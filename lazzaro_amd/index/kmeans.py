@@ -94,8 +94,10 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
     n_part = int(rows_all.numel()) if rows_all is not None else n
     for it in range(iters):
         if sample and n_part > sample and it < iters - 1:
-            g = torch.Generator(device="cpu").manual_seed(seed * 7919 + it + 1)
-            pick = torch.randperm(n_part, generator=g)[:sample].to(dev)
+            # uniform draws on the device (a host randperm of 10M rows costs
+            # more than the sampled assign saves); repeats are harmless here
+            g = torch.Generator(device=dev).manual_seed(seed * 7919 + it + 1)
+            pick = torch.randint(0, n_part, (sample,), device=dev, generator=g)
             Xs = X[rows_all[pick] if rows_all is not None else pick]
             ls, _ = assign(Xs, c16)
             c32n, c16n, cnt = G.centroids(Xs, ls, k, normalize=not distributed, pad_to=Dp if X.is_cuda else 0)

@@ -9,7 +9,7 @@ timelines show ``lzk:<stage>`` spans around the kernels:
     from lazzaro_amd.utils.tracing import tracer
     with tracer.stage("search"):
         ...
-    tracer.summary()   # {"search": {"calls": n, "total_ms": .., "avg_ms": .., "p95_ms": ..}}
+    tracer.summary()   # {"search": {"calls": n, "total_ms": .., "avg_ms": .., "p50_ms": .., "p95_ms": ..}}
 
 Enabled by ``LZK_TRACE=1`` (or ``tracer.enable()``); disabled it costs one
 attribute check per stage.
@@ -106,6 +106,7 @@ class Tracer:
         for k, v in self._times.items():
             vs = sorted(v)
             out[k] = {"calls": len(v), "total_ms": round(sum(v), 3), "avg_ms": round(sum(v) / len(v), 4),
+                      "p50_ms": round(vs[len(vs) // 2], 4),
                       "p95_ms": round(vs[min(len(vs) - 1, int(0.95 * len(vs)))], 4)}
         return out
 
