@@ -270,3 +270,37 @@ LZK_EXPORT int lzk_tg_importance(const float* sal, const int* acc, const double*
                      kind, sup, n, now, out);
   return (int)hipGetLastError();
 }
+
+// Result fields of a multi-tenant search (DistributedMemoryService): result
+// (q, j) is row rows[q * k + j] of query q's tenant, whose columns live in
+// separate allocations -- per-query base pointers [5][nq] (sal f32, acc i32,
+// kind u8, sup u8, shard i32). One launch instead of a gather per tenant.
+__global__ __launch_bounds__(256) void tg_gather_fields_kernel(const long* __restrict__ rows, int nq, int k,
+                                                                const unsigned long long* __restrict__ base,
+                                                                float* __restrict__ o_sal, int* __restrict__ o_acc,
+                                                                unsigned char* __restrict__ o_kind,
+                                                                unsigned char* __restrict__ o_sup,
+                                                                int* __restrict__ o_shard) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long)nq * k) return;
+  const int q = (int)(t / k);
+  const long r = rows[t];
+  if (r < 0) {
+    o_sal[t] = 0.f; o_acc[t] = 0; o_kind[t] = 0; o_sup[t] = 0; o_shard[t] = -1;
+    return;
+  }
+  o_sal[t] = reinterpret_cast<const float*>(base[q])[r];
+  o_acc[t] = reinterpret_cast<const int*>(base[nq + q])[r];
+  o_kind[t] = reinterpret_cast<const unsigned char*>(base[2 * nq + q])[r];
+  o_sup[t] = reinterpret_cast<const unsigned char*>(base[3 * nq + q])[r];
+  o_shard[t] = reinterpret_cast<const int*>(base[4 * nq + q])[r];
+}
+
+LZK_EXPORT int lzk_tg_gather_fields(const long* rows, int nq, int k, const void* base, float* o_sal, int* o_acc,
+                                    unsigned char* o_kind, unsigned char* o_sup, int* o_shard, void* stream) {
+  const long n = (long)nq * k;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(tg_gather_fields_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     rows, nq, k, (const unsigned long long*)base, o_sal, o_acc, o_kind, o_sup, o_shard);
+  return (int)hipGetLastError();
+}

@@ -109,6 +109,20 @@ def _seg_sum_count(keys: torch.Tensor, vals: torch.Tensor, n: int):
     return sums, cnts
 
 
+_SIDE_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(dev: torch.device):
+    """One side HIP stream per device, shared by every tenant graph on it: a
+    rank serving 10^4 tenants must not create 10^4 streams (the hardware has
+    a few queues), and tenants' side work needs no mutual concurrency."""
+    st = _SIDE_STREAMS.get(dev)
+    if st is None:
+        st = torch.cuda.Stream(device=dev)
+        _SIDE_STREAMS[dev] = st
+    return st
+
+
 class TenantGraph:
     NODE_COLS = (("sal", torch.float32, 0.0), ("acc", torch.int32, 0), ("last", torch.float64, 0.0),
                  ("ts", torch.float64, 0.0), ("shard", torch.int32, -1), ("kind", torch.uint8, FREE),
@@ -149,7 +163,7 @@ class TenantGraph:
         self.deleted_ids: Dict[str, None] = {}  # node ids to delete from the store at the next commit
         self.deleted_edges: Dict[Tuple[str, str], None] = {}
         self.track = True
-        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.stream = _side_stream(self.device) if self.on_gpu else None
         self.lock = threading.RLock()
         z = lambda dt: torch.zeros(0, dtype=dt, device=self.device)  # noqa: E731
         self.e = {"src": z(torch.int32), "dst": z(torch.int32), "w": z(torch.float32), "co": z(torch.int32),

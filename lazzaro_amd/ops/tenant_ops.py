@@ -11,8 +11,9 @@ w f32, co i32, lu f64, meta i32 (shard | type << 24)``.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, Optional, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -27,6 +28,7 @@ _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P,
 _lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
+_lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 
 SALIENCE_FLOOR = 0.2
 EDGE_COLS = ("src", "dst", "w", "co", "lu", "meta")
@@ -242,3 +244,34 @@ def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:
     component): device hook/compress kernels (graph.hip) or host union-find."""
     from .graph_ops import connected_components
     return connected_components(src, dst, n)
+
+
+def gather_fields(rows: torch.Tensor, graphs: Sequence) -> Dict[str, np.ndarray]:
+    """(salience, access count, kind, super flag, shard) of result rows
+    [nq, k] where query q's rows belong to ``graphs[q]`` (a TenantGraph per
+    query): one device gather over per-query base pointers, one host copy."""
+    nq, k = rows.shape
+    dev = rows.device
+    if not rows.is_cuda:
+        out = {n: np.zeros((nq, k), dt) for n, dt in (("sal", np.float32), ("acc", np.int32), ("kind", np.uint8),
+                                                      ("sup", np.uint8), ("shard", np.int32))}
+        out["shard"][:] = -1
+        rh = rows.numpy()
+        for q, g in enumerate(graphs):
+            for j, r in enumerate(rh[q]):
+                if r >= 0:
+                    for n in out:
+                        out[n][q, j] = getattr(g, n)[int(r)]
+        return out
+    base = torch.tensor([[getattr(g, c).data_ptr() for g in graphs] for c in ("sal", "acc", "kind", "sup", "shard")],
+                        dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    o = {"sal": torch.empty((nq, k), dtype=torch.float32, device=dev),
+         "acc": torch.empty((nq, k), dtype=torch.int32, device=dev),
+         "kind": torch.empty((nq, k), dtype=torch.uint8, device=dev),
+         "sup": torch.empty((nq, k), dtype=torch.uint8, device=dev),
+         "shard": torch.empty((nq, k), dtype=torch.int32, device=dev)}
+    rows = rows.to(torch.int64).contiguous()
+    _lib.check(_lib.lib().lzk_tg_gather_fields(rows.data_ptr(), nq, k, base.data_ptr(), o["sal"].data_ptr(),
+                                                o["acc"].data_ptr(), o["kind"].data_ptr(), o["sup"].data_ptr(),
+                                                o["shard"].data_ptr(), _st(rows)), "tg_gather_fields")
+    return {n: t.cpu().numpy() for n, t in o.items()}

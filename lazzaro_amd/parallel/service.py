@@ -203,9 +203,9 @@ class DistributedMemoryService:
     def serve(self, requests: Sequence[Tuple]) -> List:
         """SPMD: ``requests`` = [(user_id, method, args...)] received by this
         rank's front end. Each runs on the tenant's owner -- remote ones via
-        one all-to-all-v there and one back -- in this rank's order per
-        tenant; ``search_memories`` requests of one tenant are batched into a
-        single ``search_memories_batch``. Returns one JSON-able result per
+        one all-to-all-v there and one back -- in order per tenant; the
+        ``search_memories`` requests of all tenants an owner receives run as
+        one batch (:meth:`_search_many`). Returns one JSON-able result per
         request (Nodes as dicts)."""
         comm = self.comm
         out_req: List[List] = [[] for _ in range(comm.world)]
@@ -216,8 +216,25 @@ class DistributedMemoryService:
             out_req[self.owner(user)].append([i, user, method, list(req[2:])])
         inbox = self._exchange(out_req)
         replies: List[List] = [[] for _ in range(comm.world)]
+        # searches of every source and tenant run as one batch (one embed,
+        # one multi-tenant scan on the GPU); a tenant's mutating request
+        # first flushes its pending searches, so per-tenant order holds
+        pending: List[Tuple] = []
+
+        def flush():
+            if pending:
+                for (src, i, *_), r in zip(pending, self._search_many(pending)):
+                    replies[src].append([i, r])
+                pending.clear()
         for src, items in enumerate(inbox):
-            replies[src] = self._execute(items)
+            for i, user, method, args in items:
+                if method == "search_memories":
+                    pending.append((src, i, user, args[0], int(args[1]) if len(args) > 1 else 5))
+                    continue
+                if any(p[2] == user for p in pending):
+                    flush()
+                replies[src].append([i, _jsonable(getattr(self.system(user), method)(*args))])
+        flush()
         back = self._exchange(replies)
         result: List = [None] * len(requests)
         for items in back:
@@ -225,29 +242,86 @@ class DistributedMemoryService:
                 result[i] = r
         return result
 
-    def _execute(self, items: List[List]) -> List[List]:
-        """Run one source rank's requests on this (owner) rank, in order;
-        consecutive search_memories of a tenant form one batch."""
-        out = []
-        j = 0
-        while j < len(items):
-            i, user, method, args = items[j]
-            ms = self.system(user)
-            if method == "search_memories":
+    # fused multi-tenant search: below this many tenants
+    # in a batch the per-tenant path is used
+    FUSED_MIN_TENANTS = 2
+
+    def _search_many(self, pending: List[Tuple]) -> List[List[Dict]]:
+        """search_memories for (src, i, user, query, limit) requests of many
+        tenants. GPU, one shared embedder, L2 stores bound to their graphs:
+        ONE embed of all queries and ONE ``segment_topk`` launch in which
+        each query scans only its tenant's fp32 rows (score 2<q,x> - |x|^2 -
+        |q|^2 = -|q-x|^2 with the store's row mask as bias -- the exact fp32
+        L2 of the reference's store search). Otherwise per tenant."""
+        users = [p[2] for p in pending]
+        systems = {u: self.system(u) for u in dict.fromkeys(users)}
+        first = next(iter(systems.values()))
+        fused = (len(systems) >= self.FUSED_MIN_TENANTS and first.graph.on_gpu
+                 and first.graph.dim is not None and first.graph.dim % 32 == 0
+                 and all(ms.embedder is first.embedder and ms._store_binds_graph()
+                         and getattr(ms.store, "metric", "l2") == "l2" for ms in systems.values())
+                 and max(p[4] for p in pending) <= 16)
+        if not fused:
+            out, j = [], 0
+            while j < len(pending):  # consecutive same-tenant, same-limit runs batch
                 k = j
-                qs, ids, limit = [], [], args[1] if len(args) > 1 else 5
-                while k < len(items) and items[k][1] == user and items[k][2] == "search_memories" and \
-                        (items[k][3][1] if len(items[k][3]) > 1 else 5) == limit:
-                    ids.append(items[k][0])
-                    qs.append(items[k][3][0])
+                while k < len(pending) and pending[k][2] == pending[j][2] and pending[k][4] == pending[j][4]:
                     k += 1
-                res = ms.search_memories_batch(qs, limit=limit)
-                out += [[ii, [node_dict(n) for n in r]] for ii, r in zip(ids, res)]
+                res = systems[pending[j][2]].search_memories_batch([p[3] for p in pending[j:k]], limit=pending[j][4])
+                out += [[node_dict(n) for n in r] for r in res]
                 j = k
-                continue
-            out.append([i, _jsonable(getattr(ms, method)(*args))])
-            j += 1
-        return out
+            return out
+        from ..ops.search import segment_topk_ptrs
+        from ..utils.tracing import tracer
+        with tracer.stage("mt_embed", first._device):
+            embs = first._batch_embed_any([p[3] for p in pending])
+        dev = first.graph.device
+        Q = (embs if torch.is_tensor(embs) else torch.as_tensor(np.asarray(embs, np.float32))).to(dev, torch.float32)
+        locks = [systems[u]._graph_lock for u in sorted(systems)]
+        for lk in locks:
+            lk.acquire()
+        try:
+            t_host = tracer.stage("mt_prep", "cpu")
+            t_host.__enter__()
+            D = Q.shape[1]
+            graphs = {u: ms.graph for u, ms in systems.items()}
+            ok = {u: g.dim == D and g.n > 0 and g.emb32 is not None for u, g in graphs.items()}
+            xp = [graphs[u].emb32.data_ptr() if ok[u] else 0 for u in users]
+            bp = [graphs[u].store_bias("l2").data_ptr() if ok[u] else 0 for u in users]
+            nr = [graphs[u].n if ok[u] else 0 for u in users]
+            host = torch.tensor([xp, bp], dtype=torch.int64).pin_memory()
+            ptrs = host.to(dev, non_blocking=True)
+            nrows = torch.tensor(nr, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+            t_host.__exit__(None, None, None)
+            qb = -(Q * Q).sum(1)
+            k = max(p[4] for p in pending)
+            with tracer.stage("mt_scan", first._device):
+                _, rows = segment_topk_ptrs(ptrs[0], nrows, D, Q.contiguous(), k, bptr=ptrs[1], alpha=2.0, qbias=qb)
+            # the result rows' fields in one gather over per-query column
+            # pointers (the tenants' columns are separate allocations)
+            from ..ops.tenant_ops import gather_fields
+            qg = [graphs[u] for u in users]
+            with tracer.stage("mt_fields", "cpu"):
+                f = gather_fields(rows, qg)
+            # python lists, not numpy scalars: ~10k result dicts per batch
+            t_host = tracer.stage("mt_results", "cpu")
+            t_host.__enter__()
+            rl, kl, sl = rows.cpu().tolist(), f["kind"].tolist(), f["sal"].tolist()
+            al, pl, hl = f["acc"].tolist(), f["sup"].tolist(), f["shard"].tolist()
+            out = []
+            for q, p in enumerate(pending):
+                g = qg[q]
+                ids, content, types, names = g.ids, g.content, g.types, g.shard_names
+                rq, kq, sq, aq, pq, hq = rl[q], kl[q], sl[q], al[q], pl[q], hl[q]
+                out.append([{"id": ids[r], "content": content[r], "type": types[r], "salience": sq[j],
+                             "shard_key": names[hq[j]] if hq[j] >= 0 else "default", "access_count": aq[j],
+                             "is_super_node": bool(pq[j])}
+                            for j, r in enumerate(rq[: p[4]]) if r >= 0 and kq[j] == 1])
+            t_host.__exit__(None, None, None)
+            return out
+        finally:
+            for lk in reversed(locks):
+                lk.release()
 
     # ------------------------------------------------------------ directory (C7)
     def get_all_users(self) -> List[str]:

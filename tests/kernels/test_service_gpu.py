@@ -1,0 +1,56 @@
+"""DistributedMemoryService on one GPU: the fused multi-tenant search (one
+embed + one segment_topk launch over every tenant's fp32 rows) returns what
+each tenant's own MemorySystem.search_memories_batch returns."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class RandEmbedder:
+    """text -> a fixed pseudo-random unit vector (no ties between rows)."""
+
+    def __init__(self, dim=64):
+        self.dim = dim
+
+    def _v(self, t):
+        seed = int.from_bytes(hashlib.md5(t.encode()).digest()[:4], "little")
+        v = np.random.default_rng(seed).standard_normal(self.dim).astype(np.float32)
+        return (v / np.linalg.norm(v)).tolist()
+
+    def embed(self, t):
+        return self._v(t)
+
+    def batch_embed(self, ts):
+        return [self._v(t) for t in ts]
+
+
+def test_fused_multi_tenant_search_matches_per_tenant(tmp_path):
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import LocalLLM
+    from lazzaro_amd.parallel import Communicator
+    from lazzaro_amd.parallel.service import DistributedMemoryService
+    emb = RandEmbedder()
+
+    def factory(user, load_from_disk=True):
+        return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, enable_async=False,
+                            db_dir=str(tmp_path), user_id=user, device="cuda", load_from_disk=load_from_disk,
+                            max_buffer_size=10 ** 6)
+    svc = DistributedMemoryService(Communicator.local(torch.device("cuda")), factory)
+    users = [f"t{i}" for i in range(24)]
+    rng = np.random.default_rng(0)
+    for j, u in enumerate(users):
+        ms = svc.system(u)
+        n = 50 + 37 * j
+        texts = [f"{u} memory {i}" for i in range(n)]
+        V = torch.tensor(emb.batch_embed(texts), device="cuda")
+        ms.graph.add_nodes([f"{u}_n{i}" for i in range(n)], texts, V, shard=ms.graph.shard_id("work"), stored=True)
+    reqs = [(users[int(rng.integers(len(users)))], "search_memories", f"query {q}", 5) for q in range(200)]
+    fused = svc.serve(reqs)
+    for (u, _, q, k), got in zip(reqs, fused):
+        ref = svc.system(u).search_memories_batch([q], limit=k)[0]
+        assert [n["id"] for n in got] == [n.id for n in ref], u
+    svc.close()
