@@ -84,23 +84,26 @@ def build_tenant(dev, nodes: int, dim: int, encoder, seed: int, db_dir: str, clu
     return ms
 
 
-def synth_batch(ms, convs: int, facts: int, dim: int, dup_rate: float, gen, rng):
-    """Conversations of extracted facts + controlled vectors: a duplicate
-    (cos ~0.995) or a related memory (cos ~0.64) of a random live row."""
+def synth_facts(convs: int, facts: int, rng):
+    """The extraction LLM's output for ``convs`` conversations (fact dicts).
+    Generated before the timed loop: it stands in for the LLM, it is not
+    engine work."""
+    return [[{"content": " ".join(rng.choice(WORDS) for _ in range(12)), "type": "semantic",
+              "salience": round(rng.uniform(0.4, 0.95), 3), "topic": rng.choice(SHARDS)} for _ in range(facts)]
+            for _ in range(convs)]
+
+
+def synth_vectors(ms, n: int, dim: int, dup_rate: float, gen):
+    """Controlled fact vectors: a duplicate (cos ~0.995) or a related memory
+    (cos ~0.64) of a random live row of the tenant's CURRENT graph."""
     g = ms.graph
     dev = g.device
-    n = convs * facts
     base_rows = torch.randint(0, g.n, (n,), device=dev, generator=gen)
     base = g.emb32[base_rows].float()
     noise = torch.randn((n, dim), device=dev, generator=gen) / (dim ** 0.5)
     is_dup = torch.rand(n, device=dev, generator=gen) < dup_rate
-    V = torch.where(is_dup[:, None], _unit(base + 0.1 * noise), _unit(base + 1.2 * noise))
-    conversations = []
-    for c in range(convs):
-        conversations.append([{"content": " ".join(rng.choice(WORDS) for _ in range(12)), "type": "semantic",
-                               "salience": round(rng.uniform(0.4, 0.95), 3), "topic": rng.choice(SHARDS)}
-                              for _ in range(facts)])
-    return conversations, V
+    return torch.where(is_dup[:, None], _unit(base + 0.1 * noise), _unit(base + 1.2 * noise))
+
 
 
 def _sync(dev):
@@ -125,8 +128,11 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     _sync(dev)
     seed_ms = (time.perf_counter() - t0) * 1e3
 
+    batches = iter([synth_facts(convs, facts, rng) for _ in range(warmup + steps)])
+
     def step():
-        conversations, V = synth_batch(ms, convs, facts, dim, dup_rate, gen, rng)
+        conversations = next(batches)
+        V = synth_vectors(ms, convs * facts, dim, dup_rate, gen)
         texts = [f["content"] for c in conversations for f in c]
         from lazzaro_amd.utils.tracing import tracer as _tr
         with _tr.stage("fact_embed", dev):

@@ -803,8 +803,8 @@ class ConsolidationMixin:
             results.append(f"✓ Updated {updates} profile domains")
         else:
             with self._graph_lock:
-                rows = g.ordered_node_rows_dev(super_=False)
-                contents = [g.content[r] for r in rows[:PROFILE_CONTENTS].tolist()]
+                rows = g.first_node_rows_dev(PROFILE_CONTENTS, super_=False)
+                contents = [g.content[r] for r in rows.tolist()]
             if len(contents) >= 3:
                 r = self._extract_profile_from_contents(contents)
                 if "Updated" in r:

@@ -568,6 +568,23 @@ class TenantGraph:
             key = torch.where(self.sup[live] != 0, torch.full_like(live, -1), self.shard[live].long())
             return live[torch.argsort((key + 1) * max(n, 1) + live)]
 
+    def first_node_rows_dev(self, k: int, super_: Optional[bool] = None) -> torch.Tensor:
+        """The first ``k`` rows of :meth:`ordered_node_rows_dev` by one top-k
+        pass (no sort of the tenant's rows)."""
+        n = self.n
+        with self.on_stream():
+            m = self.kind[:n] == NODE
+            if super_ is not None:
+                m &= (self.sup[:n] != 0) == super_
+            r = torch.arange(n, device=self.device)
+            key = torch.where(self.sup[:n] != 0, torch.zeros_like(r), self.shard[:n].long() + 1) * max(n, 1) + r
+            key = torch.where(m, key, torch.full_like(key, 1 << 62))
+            kk = min(k, int(m.sum()))
+            if kk == 0:
+                return torch.zeros(0, dtype=torch.long, device=self.device)
+            v, i = torch.topk(key, kk, largest=False, sorted=True)
+            return i
+
     def set_scalar(self, r: int, name: str, value) -> None:
         col = getattr(self, name)
         with self.on_stream():
@@ -965,38 +982,42 @@ class TenantGraph:
             return []
         dev = self.device
         with self.on_stream():
-            lab = T.components(self.e["src"], self.e["dst"], n)
-            lab = lab.to(dev).long()
+            # a row no edge touches is a singleton component (size 1 < min_size):
+            # the components are computed over the edge endpoints only, so
+            # the cost follows the edges, not the tenant's rows
             src, dst = self.e["src"].long(), self.e["dst"].long()
-            kind = self.kind[:n]
-            touched = torch.zeros(n, dtype=torch.bool, device=dev)
-            touched[src] = True
-            touched[dst] = True
-            member = (kind == NODE) | ((kind == GHOST) & touched)
-            lm = lab[member]
-            size = _seg_sum_count(lm, torch.zeros(lm.shape, dtype=torch.float32, device=dev), n)[1]
-            wsum, wcnt = _seg_sum_count(lab[src], self.e["w"], n)
+            E = src.numel()
+            verts, inv = torch.unique(torch.cat([src, dst]), return_inverse=True)
+            nv = verts.numel()
+            cl = T.components(inv[:E].to(torch.int32), inv[E:].to(torch.int32), nv).to(dev).long()
+            kind_v = self.kind[verts]
+            member = kind_v != FREE  # live nodes and ghost endpoints (the DFS follows edges to them)
+            size = _seg_sum_count(cl[member], torch.zeros(int(member.sum()), dtype=torch.float32, device=dev), nv)[1]
+            wsum, wcnt = _seg_sum_count(cl[inv[:E]], self.e["w"], nv)
             ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1).double() > min_avg_w)
-            # reference order: a component's first member in BufferGraph.nodes order
-            order = self.ordered_node_rows_dev()
+            # reference order: a component's first member in BufferGraph.nodes
+            # order = the smallest (super ? 0 : shard + 1) * n + row among its
+            # live nodes -- compared as keys, no sort of the tenant's rows
             BIG = 1 << 62
-            pos = torch.full((n,), BIG, dtype=torch.long, device=dev)
-            pos[order] = torch.arange(order.numel(), device=dev)
-            first = torch.full((n,), BIG, dtype=torch.long, device=dev)
-            first.scatter_reduce_(0, lab, pos, "amin", include_self=True)
+            sup_v = self.sup[verts] != 0
+            okey = torch.where(sup_v, torch.zeros_like(verts), self.shard[verts].long() + 1) * max(n, 1) + verts
+            okey = torch.where(kind_v == NODE, okey, torch.full_like(okey, BIG))
+            first = torch.full((nv,), BIG, dtype=torch.long, device=dev)
+            first.scatter_reduce_(0, cl, okey, "amin", include_self=True)
             ok &= first < BIG
-            cand = torch.nonzero(ok[lab] & (kind == NODE) & (self.sup[:n] == 0)).flatten()
+            cand = torch.nonzero(ok[cl] & (kind_v == NODE) & ~sup_v).flatten()
             if cand.numel() == 0:
                 return []
-            key = first[lab[cand]]
-            o = torch.argsort(key * n + cand)  # (component order, row)
-            cand, key = cand[o], key[o]
+            key = first[cl[cand]]
+            rowsv = verts[cand]
+            o = torch.argsort(key * n + rowsv)  # (component order, row)
+            rowsv, key = rowsv[o], key[o]
             newg = torch.ones_like(key, dtype=torch.bool)
             newg[1:] = key[1:] != key[:-1]
             gstart = torch.nonzero(newg).flatten()[torch.cumsum(newg.long(), 0) - 1]
             rank = torch.arange(key.numel(), device=dev) - gstart
             sel = rank < take
-            rows_h, key_h = cand[sel].cpu().numpy(), key[sel].cpu().numpy()
+            rows_h, key_h = rowsv[sel].cpu().numpy(), key[sel].cpu().numpy()
         cut = np.nonzero(np.diff(key_h))[0] + 1
         return np.split(rows_h, cut)
 
