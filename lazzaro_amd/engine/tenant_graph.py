@@ -1277,7 +1277,15 @@ class TenantGraph:
             # large tenants: mini-batch refinement steps on a 1M-row sample,
             # then one full assign + update (labels for every row)
             smp = self.CLUSTER_SAMPLE if n_live > 2 * self.CLUSTER_SAMPLE else 0
-            fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp)
+            # warm passes over large tenants: the full-data assign searches a
+            # row's fine clusters only under its nearest previous topic
+            fa = None
+            if smp and init_f is not None and prev.get("top_c16") is not None and prev.get("top_of_fine") is not None:
+                from ..index.kmeans import assign_two_level
+                T16, tof = prev["top_c16"], prev["top_of_fine"]
+                fa = lambda Xa, C16: assign_two_level(Xa, C16, T16, tof)  # noqa: E731
+            fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp,
+                                     full_assign=fa)
             init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
             tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
             lab = lab.long()
@@ -1289,7 +1297,8 @@ class TenantGraph:
             start = torch.zeros(kt + 1, dtype=torch.long, device=self.device)
             start[1:] = torch.cumsum(cnt, 0)
             self.hier = {"fine_c": fc32, "top_c": tc32, "fine": lab.to(torch.int32), "top": top.to(torch.int32),
-                         "perm": perm, "start": start, "n": n, "version": self.version}
+                         "perm": perm, "start": start, "n": n, "version": self.version,
+                         "top_c16": tc16, "top_of_fine": top_of_fine}
         return {"fine": kf, "top": kt, "rows": n_live}
 
     def hier_children(self, q: torch.Tensor, threshold: float, limit: int) -> List[int]:

@@ -306,3 +306,21 @@ def test_kmeans_assign_paths_agree_gpu(monkeypatch):
     lb, sb = K.assign(X, C)
     assert torch.allclose(sa, sb, atol=1e-4)
     assert float((la == lb).float().mean()) > 0.999
+
+
+def test_two_level_assign_gpu_matches_full():
+    """assign_two_level on the GPU (per-topic fused argmax launches) agrees
+    with the full 256x256 argmax assign on well-separated topics."""
+    from lazzaro_amd.index.kmeans import assign, assign_two_level
+    g = torch.Generator(device="cuda").manual_seed(5)
+    d, T, per = 128, 16, 32
+    tops = torch.nn.functional.normalize(torch.randn(T, d, device="cuda", generator=g), dim=1)
+    fine = torch.nn.functional.normalize(tops.repeat_interleave(per, 0)
+                                         + 0.15 * torch.randn(T * per, d, device="cuda", generator=g), dim=1)
+    top_of = torch.arange(T, device="cuda").repeat_interleave(per)
+    X = torch.nn.functional.normalize(fine[torch.randint(0, T * per, (200_000,), device="cuda", generator=g)]
+                                      + 0.03 * torch.randn(200_000, d, device="cuda", generator=g), dim=1)
+    b = lambda t: t.to(torch.bfloat16).contiguous()  # noqa: E731
+    l_full, _ = assign(b(X), b(fine))
+    l_two, _ = assign_two_level(b(X), b(fine), b(tops), top_of)
+    assert (l_full.long() == l_two.long()).float().mean() > 0.995

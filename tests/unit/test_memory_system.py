@@ -486,3 +486,21 @@ def test_kmeans_minibatch_sample_matches_quality():
     assert bool((lab[mask] >= 0).all()) and bool((lab[~mask] == -1).all())
     pure = sum(len(set(lab[j * per:(j + 1) * per][mask[j * per:(j + 1) * per]].tolist())) == 1 for j in range(C))
     assert pure >= C - 1
+
+
+def test_two_level_assign_matches_full_on_separated_topics():
+    """assign_two_level (fine clusters searched under the nearest topic only)
+    equals the full assign when topics are well separated."""
+    import torch
+    from lazzaro_amd.index.kmeans import assign, assign_two_level
+    g = torch.Generator().manual_seed(3)
+    d, T, per = 32, 4, 6
+    tops = torch.nn.functional.normalize(torch.randn(T, d, generator=g), dim=1)
+    fine = torch.nn.functional.normalize(tops.repeat_interleave(per, 0) + 0.2 * torch.randn(T * per, d, generator=g),
+                                         dim=1)
+    top_of = torch.arange(T).repeat_interleave(per)
+    X = torch.nn.functional.normalize(fine[torch.randint(0, T * per, (3000,), generator=g)]
+                                      + 0.05 * torch.randn(3000, d, generator=g), dim=1)
+    l_full, _ = assign(X, fine)
+    l_two, _ = assign_two_level(X, fine, tops, top_of)
+    assert (l_full.long() == l_two.long()).float().mean() > 0.99
