@@ -179,7 +179,8 @@ class MemorySystem(ConsolidationMixin):
         self.conversation_count = 0
         self.metrics = {"embedding_calls": 0, "llm_calls": 0, "retrieval_times": [],
                         "consolidation_times": [], "consolidation_failures": 0, "dropped_batches": 0,
-                        "persist_failures": 0, "rejected_embeddings": 0}
+                        "persist_failures": 0, "rejected_embeddings": 0, "search_queries": 0,
+                        "search_batches": 0, "search_ms": 0.0}
         if load_from_disk:
             self._load_from_persistence()
 
@@ -571,7 +572,16 @@ class MemorySystem(ConsolidationMixin):
         embedding call (a device tensor when the encoder is on-device), one
         store search -- the fused MFMA candidate scan plus an fp32 re-rank
         over the tenant's HBM rows -- and one row -> Node mapping."""
-        return self._search_finish(self._search_submit(queries, limit))
+        t0 = time.perf_counter()
+        out = self._search_finish(self._search_submit(queries, limit))
+        self._count_search(len(out), (time.perf_counter() - t0) * 1e3)
+        return out
+
+    def _count_search(self, n: int, ms: float) -> None:
+        m = self.metrics
+        m["search_queries"] = m.get("search_queries", 0) + n
+        m["search_batches"] = m.get("search_batches", 0) + 1
+        m["search_ms"] = m.get("search_ms", 0.0) + ms
 
     def search_memories_stream(self, batches: Iterable[List[str]], limit: int = 5):
         """Pipelined ``search_memories_batch`` for serving loops: batch i+1 is
@@ -666,19 +676,32 @@ class MemorySystem(ConsolidationMixin):
                 "llm_calls": self.metrics["llm_calls"],
                 "embedding_calls": self.metrics["embedding_calls"],
             },
+            # engine metrics: the device, the tenant graph's HBM
+            # footprint, search throughput of search_memories[_batch]
+            "engine": self._engine_brief(),
         }
+
+    def _engine_brief(self) -> Dict:
+        g, m = self.graph, self.metrics
+        sq, sms = m.get("search_queries", 0), m.get("search_ms", 0.0)
+        return {"device": str(self._device), "graph_rows": g.n, "hbm_graph_bytes": self._graph_bytes(),
+                "search_queries": sq, "search_qps": round(sq / (sms / 1e3), 1) if sms > 0 else 0.0,
+                "avg_search_batch_ms": round(sms / m["search_batches"], 3) if m.get("search_batches") else 0.0}
+
+    def _graph_bytes(self) -> int:
+        g = self.graph
+        return int(sum(t.numel() * t.element_size() for t in
+                       [g.emb32, g.emb16, g.emb8, g.sqn] + [getattr(g, c) for c, _, _ in TenantGraph.NODE_COLS]
+                       + list(g.e.values()) if t is not None))
 
     def engine_stats(self) -> Dict:
         """Engine-level metrics beyond the reference's ``get_stats`` (SURVEY.md
         §5 metrics row): device, HBM bytes held by the tenant graph, rows,
         edges, per-stage timings from the tracer when enabled."""
         g = self.graph
-        nbytes = sum(t.numel() * t.element_size() for t in
-                     [g.emb32, g.emb16, g.sqn] + [getattr(g, c) for c, _, _ in TenantGraph.NODE_COLS]
-                     + list(g.e.values()) if t is not None)
         return {"device": str(self._device), "rows": g.n, "capacity": g.cap, "nodes": g.num_nodes(),
-                "edges": g.num_edges, "graph_bytes": int(nbytes), "dim": g.dim,
-                "decay_clock": g.decay_log, "stages": tracer.summary()}
+                "edges": g.num_edges, "graph_bytes": self._graph_bytes(), "dim": g.dim,
+                "decay_clock": g.decay_log, "stages": tracer.summary(), **self._engine_brief()}
 
     def display_stats(self) -> str:
         s = self.get_stats()

@@ -43,7 +43,7 @@ def _factory(db, user):
 def _strip(v):
     """Drop wall-clock dependent fields before comparing."""
     if isinstance(v, dict):
-        return {k: _strip(x) for k, x in v.items() if k not in ("performance",)}
+        return {k: _strip(x) for k, x in v.items() if k not in ("performance", "engine")}
     if isinstance(v, list):
         return [_strip(x) for x in v]
     if isinstance(v, str) and v.startswith("["):

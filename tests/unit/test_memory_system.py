@@ -504,3 +504,19 @@ def test_two_level_assign_matches_full_on_separated_topics():
     l_full, _ = assign(X, fine)
     l_two, _ = assign_two_level(X, fine, tops, top_of)
     assert (l_full.long() == l_two.long()).float().mean() > 0.99
+
+
+def test_get_stats_engine_block():
+    """get_stats keeps the reference's keys and adds the engine metrics
+    (device, HBM bytes of the tenant graph, search throughput)."""
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=32), enable_async=False,
+                      load_from_disk=False)
+    ms.start_conversation()
+    ms.chat("I like sailing and my sister lives in Porto.")
+    ms.end_conversation()
+    ms.search_memories_batch(["sailing", "Porto", "sister"], limit=2)
+    s = ms.get_stats()
+    assert {"buffer_nodes", "buffer_edges", "performance"} <= set(s)
+    e = s["engine"]
+    assert e["search_queries"] == 3 and e["hbm_graph_bytes"] > 0 and e["search_qps"] > 0
+    ms.close()
