@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--model", default="bge-base")
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--stream", type=int, default=1, help="1: serve_stream (pipelined rounds), 0: serve per round")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
@@ -91,7 +92,7 @@ def main():
     torch.cuda.synchronize()
     comm.barrier()
     t0 = time.perf_counter()
-    outs = [svc.serve(r) for r in reqs]
+    outs = list(svc.serve_stream(reqs)) if a.stream else [svc.serve(r) for r in reqs]
     torch.cuda.synchronize()
     comm.barrier()
     el = time.perf_counter() - t0
@@ -123,7 +124,8 @@ def main():
            "users_total": a.users_total, "users_per_gpu": len(mine), "rows_total": int(rt.item()),
            "batch_per_rank": a.batch, "k": a.k, "model": a.model, "populate_s": round(t_pop, 1),
            "exact_match_vs_per_tenant_search": f"{int(ok[0])}/{int(ok[1])}",
-           "path": "serve() -> owner's one embed + one segment_topk over tenants' fp32 rows -> Node dicts",
+           "path": ("serve_stream() (round i+1 enqueued before round i is materialised)" if a.stream else "serve()")
+           + " -> owner's one embed + one segment_topk over tenants' fp32 rows -> Node dicts",
            "data": "synthetic (random unit vectors, synthetic query texts, random-init encoder)"}
     from lazzaro_amd.utils.tracing import tracer
     if tracer.enabled:

@@ -246,10 +246,11 @@ def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:
     return connected_components(src, dst, n)
 
 
-def gather_fields(rows: torch.Tensor, graphs: Sequence) -> Dict[str, np.ndarray]:
+def gather_fields(rows: torch.Tensor, graphs: Sequence, device_out: bool = False) -> Dict:
     """(salience, access count, kind, super flag, shard) of result rows
     [nq, k] where query q's rows belong to ``graphs[q]`` (a TenantGraph per
-    query): one device gather over per-query base pointers, one host copy."""
+    query): one device gather over per-query base pointers, one host copy
+    (``device_out``: the device tensors, for an asynchronous copy)."""
     nq, k = rows.shape
     dev = rows.device
     if not rows.is_cuda:
@@ -274,4 +275,6 @@ def gather_fields(rows: torch.Tensor, graphs: Sequence) -> Dict[str, np.ndarray]
     _lib.check(_lib.lib().lzk_tg_gather_fields(rows.data_ptr(), nq, k, base.data_ptr(), o["sal"].data_ptr(),
                                                 o["acc"].data_ptr(), o["kind"].data_ptr(), o["sup"].data_ptr(),
                                                 o["shard"].data_ptr(), _st(rows)), "tg_gather_fields")
+    if device_out:
+        return o
     return {n: t.cpu().numpy() for n, t in o.items()}

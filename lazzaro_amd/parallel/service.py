@@ -205,8 +205,27 @@ class DistributedMemoryService:
         rank's front end. Each runs on the tenant's owner -- remote ones via
         one all-to-all-v there and one back -- in order per tenant; the
         ``search_memories`` requests of all tenants an owner receives run as
-        one batch (:meth:`_search_many`). Returns one JSON-able result per
+        one batch (:meth:`_search_submit`). Returns one JSON-able result per
         request (Nodes as dicts)."""
+        return self._serve_finish(self._serve_submit(requests))
+
+    def serve_stream(self, rounds: Iterable[Sequence[Tuple]]):
+        """Pipelined :meth:`serve` for serving loops (SPMD, every rank the
+        same number of rounds): round i+1's requests are routed and its
+        batched search enqueued on the GPU BEFORE round i's results are
+        materialised and returned, so the host work of one round hides
+        under the device work of the next. Yields one result list per round,
+        equal to ``serve`` of that round."""
+        prev = None
+        for reqs in rounds:
+            h = self._serve_submit(reqs)
+            if prev is not None:
+                yield self._serve_finish(prev)
+            prev = h
+        if prev is not None:
+            yield self._serve_finish(prev)
+
+    def _serve_submit(self, requests: Sequence[Tuple]):
         comm = self.comm
         out_req: List[List] = [[] for _ in range(comm.world)]
         for i, req in enumerate(requests):
@@ -223,7 +242,7 @@ class DistributedMemoryService:
 
         def flush():
             if pending:
-                for (src, i, *_), r in zip(pending, self._search_many(pending)):
+                for (src, i, *_), r in zip(pending, self._search_finish(self._search_submit(pending))):
                     replies[src].append([i, r])
                 pending.clear()
         for src, items in enumerate(inbox):
@@ -234,9 +253,16 @@ class DistributedMemoryService:
                 if any(p[2] == user for p in pending):
                     flush()
                 replies[src].append([i, _jsonable(getattr(self.system(user), method)(*args))])
-        flush()
+        handle = self._search_submit(pending) if pending else None
+        return len(requests), replies, list(pending), handle
+
+    def _serve_finish(self, state) -> List:
+        n, replies, pending, handle = state
+        if handle is not None:
+            for (src, i, *_), r in zip(pending, self._search_finish(handle)):
+                replies[src].append([i, r])
         back = self._exchange(replies)
-        result: List = [None] * len(requests)
+        result: List = [None] * n
         for items in back:
             for i, r in items:
                 result[i] = r
@@ -246,13 +272,16 @@ class DistributedMemoryService:
     # in a batch the per-tenant path is used
     FUSED_MIN_TENANTS = 2
 
-    def _search_many(self, pending: List[Tuple]) -> List[List[Dict]]:
+    def _search_submit(self, pending: List[Tuple]):
         """search_memories for (src, i, user, query, limit) requests of many
         tenants. GPU, one shared embedder, L2 stores bound to their graphs:
         ONE embed of all queries and ONE ``segment_topk`` launch in which
         each query scans only its tenant's fp32 rows (score 2<q,x> - |x|^2 -
         |q|^2 = -|q-x|^2 with the store's row mask as bias -- the exact fp32
-        L2 of the reference's store search). Otherwise per tenant."""
+        L2 of the reference's store search), then one pointer-table gather of
+        the result rows' fields, copied to pinned memory asynchronously: the
+        returned handle is finished by :meth:`_search_finish` (which holds
+        the tenants' graph locks until then). Otherwise per tenant, at once."""
         users = [p[2] for p in pending]
         systems = {u: self.system(u) for u in dict.fromkeys(users)}
         first = next(iter(systems.values()))
@@ -270,8 +299,9 @@ class DistributedMemoryService:
                 res = systems[pending[j][2]].search_memories_batch([p[3] for p in pending[j:k]], limit=pending[j][4])
                 out += [[node_dict(n) for n in r] for r in res]
                 j = k
-            return out
+            return ("done", out)
         from ..ops.search import segment_topk_ptrs
+        from ..ops.tenant_ops import gather_fields
         from ..utils.tracing import tracer
         with tracer.stage("mt_embed", first._device):
             embs = first._batch_embed_any([p[3] for p in pending])
@@ -281,43 +311,55 @@ class DistributedMemoryService:
         for lk in locks:
             lk.acquire()
         try:
-            t_host = tracer.stage("mt_prep", "cpu")
-            t_host.__enter__()
-            D = Q.shape[1]
-            graphs = {u: ms.graph for u, ms in systems.items()}
-            ok = {u: g.dim == D and g.n > 0 and g.emb32 is not None for u, g in graphs.items()}
-            xp = [graphs[u].emb32.data_ptr() if ok[u] else 0 for u in users]
-            bp = [graphs[u].store_bias("l2").data_ptr() if ok[u] else 0 for u in users]
-            nr = [graphs[u].n if ok[u] else 0 for u in users]
-            host = torch.tensor([xp, bp], dtype=torch.int64).pin_memory()
-            ptrs = host.to(dev, non_blocking=True)
-            nrows = torch.tensor(nr, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
-            t_host.__exit__(None, None, None)
+            with tracer.stage("mt_prep", "cpu"):
+                D = Q.shape[1]
+                graphs = {u: ms.graph for u, ms in systems.items()}
+                ok = {u: g.dim == D and g.n > 0 and g.emb32 is not None for u, g in graphs.items()}
+                xp = [graphs[u].emb32.data_ptr() if ok[u] else 0 for u in users]
+                bp = [graphs[u].store_bias("l2").data_ptr() if ok[u] else 0 for u in users]
+                nr = [graphs[u].n if ok[u] else 0 for u in users]
+                ptrs = torch.tensor([xp, bp], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+                nrows = torch.tensor(nr, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
             qb = -(Q * Q).sum(1)
             k = max(p[4] for p in pending)
             with tracer.stage("mt_scan", first._device):
                 _, rows = segment_topk_ptrs(ptrs[0], nrows, D, Q.contiguous(), k, bptr=ptrs[1], alpha=2.0, qbias=qb)
             # the result rows' fields in one gather over per-query column
             # pointers (the tenants' columns are separate allocations)
-            from ..ops.tenant_ops import gather_fields
             qg = [graphs[u] for u in users]
-            with tracer.stage("mt_fields", "cpu"):
-                f = gather_fields(rows, qg)
-            # python lists, not numpy scalars: ~10k result dicts per batch
-            t_host = tracer.stage("mt_results", "cpu")
-            t_host.__enter__()
-            rl, kl, sl = rows.cpu().tolist(), f["kind"].tolist(), f["sal"].tolist()
-            al, pl, hl = f["acc"].tolist(), f["sup"].tolist(), f["shard"].tolist()
-            out = []
-            for q, p in enumerate(pending):
-                g = qg[q]
-                ids, content, types, names = g.ids, g.content, g.types, g.shard_names
-                rq, kq, sq, aq, pq, hq = rl[q], kl[q], sl[q], al[q], pl[q], hl[q]
-                out.append([{"id": ids[r], "content": content[r], "type": types[r], "salience": sq[j],
-                             "shard_key": names[hq[j]] if hq[j] >= 0 else "default", "access_count": aq[j],
-                             "is_super_node": bool(pq[j])}
-                            for j, r in enumerate(rq[: p[4]]) if r >= 0 and kq[j] == 1])
-            t_host.__exit__(None, None, None)
+            f = gather_fields(rows, qg, device_out=True)
+            f["rows"] = rows
+            host = {n: torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for n, t in f.items()}
+            for n, t in f.items():
+                host[n].copy_(t, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            return ("fused", pending, qg, host, ev, locks, (Q, ptrs, nrows, f))
+        except BaseException:
+            for lk in reversed(locks):
+                lk.release()
+            raise
+
+    def _search_finish(self, h) -> List[List[Dict]]:
+        if h[0] == "done":
+            return h[1]
+        from ..utils.tracing import tracer
+        _, pending, qg, host, ev, locks, _keep = h
+        try:
+            ev.synchronize()
+            with tracer.stage("mt_results", "cpu"):
+                # python lists, not numpy scalars: ~10k result dicts per batch
+                rl, kl, sl = host["rows"].tolist(), host["kind"].tolist(), host["sal"].tolist()
+                al, pl, hl = host["acc"].tolist(), host["sup"].tolist(), host["shard"].tolist()
+                out = []
+                for q, p in enumerate(pending):
+                    g = qg[q]
+                    ids, content, types, names = g.ids, g.content, g.types, g.shard_names
+                    rq, kq, sq, aq, pq, hq = rl[q], kl[q], sl[q], al[q], pl[q], hl[q]
+                    out.append([{"id": ids[r], "content": content[r], "type": types[r], "salience": sq[j],
+                                 "shard_key": names[hq[j]] if hq[j] >= 0 else "default", "access_count": aq[j],
+                                 "is_super_node": bool(pq[j])}
+                                for j, r in enumerate(rq[: p[4]]) if r >= 0 and kq[j] == 1])
             return out
         finally:
             for lk in reversed(locks):

@@ -54,3 +54,31 @@ def test_fused_multi_tenant_search_matches_per_tenant(tmp_path):
         ref = svc.system(u).search_memories_batch([q], limit=k)[0]
         assert [n["id"] for n in got] == [n.id for n in ref], u
     svc.close()
+
+
+def test_serve_stream_equals_serve(tmp_path):
+    """serve_stream (round i+1 routed and its batched search enqueued before
+    round i's results are built) returns exactly what serve returns."""
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import LocalLLM
+    from lazzaro_amd.parallel import Communicator
+    from lazzaro_amd.parallel.service import DistributedMemoryService
+    emb = RandEmbedder()
+
+    def factory(user, load_from_disk=True):
+        return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, enable_async=False,
+                            db_dir=str(tmp_path), user_id=user, device="cuda", load_from_disk=load_from_disk)
+    svc = DistributedMemoryService(Communicator.local(torch.device("cuda")), factory)
+    users = [f"s{i}" for i in range(10)]
+    for j, u in enumerate(users):
+        g = svc.system(u).graph
+        texts = [f"{u} fact {i}" for i in range(40 + 9 * j)]
+        g.add_nodes([f"{u}_{i}" for i in range(len(texts))], texts, torch.tensor(emb.batch_embed(texts), device="cuda"),
+                    shard=g.shard_id("work"), stored=True)
+    rng = np.random.default_rng(1)
+    rounds = [[(users[int(rng.integers(10))], "search_memories", f"r{r} q{q}", 4) for q in range(64)]
+              for r in range(5)]
+    want = [svc.serve(r) for r in rounds]
+    got = list(svc.serve_stream(rounds))
+    assert got == want
+    svc.close()
