@@ -399,10 +399,106 @@ class DistributedMemoryService:
         allc = sorted((c for p in parts for c in p), key=lambda c: (-c[0], c[1], c[2]))[:limit]
         return [dict(user_id=u, score=sc, **nd) for sc, u, _, nd in allc]
 
+    # ------------------------------------------------------------ row-sharded tenants
+    def shard_of(self, user: str):
+        """This rank's shard of a row-sharded tenant (a tenant too large for
+        one GPU: every rank holds the rows whose id hashes to it, persisted
+        as tenant ``user@r/world``)."""
+        sid = f"{user}@{self.comm.rank}/{self.comm.world}"
+        ms = self.sharded.get(sid)
+        if ms is None:
+            ms = self._build(sid)
+            self.sharded[sid] = ms
+        return ms
+
+    @property
+    def sharded(self) -> Dict[str, object]:
+        if not hasattr(self, "_sharded"):
+            self._sharded: Dict[str, object] = {}
+        return self._sharded
+
+    def add_sharded(self, user: str, ids: Sequence[str], contents: Sequence[str], vectors) -> int:
+        """SPMD: rows given on any rank go to the rank their id hashes to --
+        one all-to-all-v of the vectors (C3 re-shard) and one of the ids and
+        texts -- and are stored there as memories of the tenant's local
+        shard. Returns the rows this rank received."""
+        comm = self.comm
+        V = torch.as_tensor(np.asarray(vectors, np.float32)) if not torch.is_tensor(vectors) else vectors.float()
+        D = V.shape[1] if V.dim() == 2 and V.shape[0] else 0
+        D = int(max(comm.all_gather_object(D)))
+        dest = [tenant_rank(i, comm.world) for i in ids]
+        meta: List[List] = [[] for _ in range(comm.world)]
+        order = sorted(range(len(ids)), key=lambda j: dest[j])
+        for j in order:
+            meta[dest[j]].append([ids[j], contents[j]])
+        counts = [len(m) * D for m in meta]
+        flat = V[torch.as_tensor(order, dtype=torch.long)].reshape(-1) if order else torch.zeros(0)
+        rc = comm.exchange_counts(torch.tensor(counts, dtype=torch.int64, device=comm.device)).cpu().tolist()
+        got = comm.all_to_all_v(flat.to(comm.device), counts, rc) if comm.world > 1 else flat
+        got_meta = self._exchange(meta)
+        rows = [m for part in got_meta for m in part]
+        if not rows:
+            return 0
+        ms = self.shard_of(user)
+        g = ms.graph
+        with ms._graph_lock:
+            g.add_nodes([r[0] for r in rows], [r[1] for r in rows], got.reshape(len(rows), D).to(g.device),
+                        shard=g.shard_id("default"), stored=ms._store_binds_graph())
+            ms._save_to_persistence()
+        return len(rows)
+
+    def search_sharded(self, user: str, queries: Sequence[str], limit: int = 5) -> List[List[Dict]]:
+        """SPMD search of a row-sharded tenant: every rank embeds the
+        queries (replicated encoder, no broadcast: C2), runs the store search
+        over its shard, then ONE all-gather of the (score, rank, row)
+        candidates and a merge give every rank the exact global top-``limit``
+        (C1 + K2); the owner of each winning row supplies its node dict
+        through one more all-gather."""
+        comm = self.comm
+        ms = self.shard_of(user)
+        g = ms.graph
+        embs = ms._batch_embed_any(list(queries))
+        Q = (embs if torch.is_tensor(embs) else torch.as_tensor(np.asarray(embs, np.float32))).float()
+        nq = len(queries)
+        with ms._graph_lock:
+            if g.n and g.dim == Q.shape[1]:
+                s, r = g.store_search(Q.to(g.device), limit, getattr(ms.store, "metric", "l2"))
+                s, r = s.cpu(), r.cpu()
+                kind = g.mirror("kind")
+                ok = (r >= 0) & torch.as_tensor(kind)[r.clamp_min(0)].eq(1)
+                s = torch.where(ok, s, torch.full_like(s, float("-inf")))
+            else:
+                s = torch.full((nq, limit), float("-inf"))
+                r = torch.full((nq, limit), -1, dtype=torch.long)
+        # C1: all-gather of fixed-size candidate lists; K2: merge by (score
+        # desc, (rank, row) asc) -- the same total order on every rank
+        from .sharded import merge_topk
+        key = torch.where(r >= 0, comm.rank * (1 << 40) + r, torch.full_like(r, -1))
+        gs = comm.all_gather_rows(s.float().contiguous().to(comm.device))
+        gk = comm.all_gather_rows(key.contiguous().to(comm.device))
+        W = comm.world
+        gs = gs.view(W, nq, -1).permute(1, 0, 2).reshape(nq, -1)
+        gk = gk.view(W, nq, -1).permute(1, 0, 2).reshape(nq, -1)
+        ms_, mk = merge_topk(gs, gk, limit)
+        ms_, mk = ms_.cpu(), mk.cpu()
+        winners: List[List[Tuple[int, int]]] = [
+            [(int(k_) >> 40, int(k_) & ((1 << 40) - 1)) for sc, k_ in zip(ms_[q].tolist(), mk[q].tolist())
+             if k_ >= 0 and sc != float("-inf")] for q in range(nq)]
+        mine = {}
+        with ms._graph_lock:
+            for q in range(nq):
+                for rk, row in winners[q]:
+                    if rk == comm.rank:
+                        mine[(q, row)] = node_dict(_view(g, row))
+        parts = comm.all_gather_object(list(mine.items()))
+        nodes = {(key[0], rk, key[1]): v for rk, p in enumerate(parts) for key, v in p}
+        return [[nodes[(q, rk, row)] for rk, row in winners[q]] for q in range(nq)]
+
     def close(self) -> None:
-        for ms in self.systems.values():
+        for ms in list(self.systems.values()) + list(self.sharded.values()):
             ms.close()
         self.systems.clear()
+        self.sharded.clear()
 
 
 def _view(g, row):
