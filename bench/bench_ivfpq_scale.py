@@ -78,6 +78,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--nprobes", default="16,32,64,128")
     ap.add_argument("--reranks", default="0,256,1024")
+    ap.add_argument("--embed-model", default="e5-large", help="query encoder timed per batch ('' = none)")
+    ap.add_argument("--embed-precision", default="fp8", choices=["fp8", "bf16"])
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -128,6 +130,28 @@ def main():
     torch.cuda.synchronize()
     log(f"exact truth in {time.time() - t0:.0f}s")
 
+    # the query side of config 5: e5-large (d=1024) on-device embed of nq
+    # synthetic texts, timed; the search itself uses mixture queries (a
+    # random-init encoder maps every text to nearly one vector, so recall
+    # needs controlled query vectors)
+    t_embed = 0.0
+    if a.embed_model:
+        import random as _r
+
+        from lazzaro_amd.core.embedders import OnDeviceEmbedder
+        enc = OnDeviceEmbedder(a.embed_model, device=dev, max_len=64, precision=a.embed_precision)
+        rr = _r.Random(0)
+        words = "memory user likes python graph kernel music travel project deadline family".split()
+        texts = [" ".join(rr.choice(words) for _ in range(16)) for _ in range(a.nq)]
+        enc.batch_embed_tensor(texts)
+        torch.cuda.synchronize()
+        t1 = time.time()
+        for _ in range(3):
+            enc.batch_embed_tensor(texts)
+        torch.cuda.synchronize()
+        t_embed = (time.time() - t1) / 3
+        log(f"{a.embed_model} {a.embed_precision} embed of {a.nq} queries: {t_embed * 1e3:.2f} ms")
+        del enc
     res = []
     for nprobe in map(int, a.nprobes.split(",")):
         for rr in map(int, a.reranks.split(",")):
@@ -140,6 +164,8 @@ def main():
             dt = (time.time() - t1) / 3
             r = {"nprobe": nprobe, "rerank": rr, "ms_per_batch": round(dt * 1e3, 2), "qps": round(a.nq / dt, 1),
                  "recall_at_10": round(recall_at_k(ids, best_i), 4)}
+            if t_embed:
+                r["qps_with_embed"] = round(a.nq / (dt + t_embed), 1)
             lc = getattr(idx, "last_candidates", None)
             if rr > 16 and lc is not None:
                 cap = max(idx.CAND_CAP * rr, idx.CAND_MIN)
@@ -154,7 +180,10 @@ def main():
            "nlist": a.nlist, "m": a.m, "rerank_copy": a.keep, "nq": a.nq,
            "index_bytes": idx.memory_bytes(), "bytes_per_vector": round(idx.memory_bytes() / a.n, 1),
            "hbm_allocated_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
-           "train_s": round(t_train, 1), "build_s": round(t_add, 1), "results": res}
+           "train_s": round(t_train, 1), "build_s": round(t_add, 1),
+           "query_embed": {"model": a.embed_model, "precision": a.embed_precision,
+                           "ms_per_batch": round(t_embed * 1e3, 2)} if a.embed_model else None,
+           "results": res}
     line = json.dumps(out)
     print(line, flush=True)
     if a.out:
