@@ -85,6 +85,8 @@ class HBMStore:
             self._graphs[user_id] = graph
             self._arenas.pop(user_id, None)
             self._synced.pop(user_id, None)
+            if self.index == "ivfpq":  # large tenants: IVF-PQ candidates + exact fp32 re-rank on the graph
+                graph.ann_cfg = dict(self.ivf_params)
 
     def detach(self, user_id: str) -> None:
         with self._lock:

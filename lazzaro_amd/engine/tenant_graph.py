@@ -164,6 +164,10 @@ class TenantGraph:
         self.deleted_edges: Dict[Tuple[str, str], None] = {}
         self.track = True
         self.stream = _side_stream(self.device) if self.on_gpu else None
+        self.ann_cfg: Optional[Dict] = None  # store index="ivfpq": IVF-PQ for large tenants (HBMStore.attach)
+        self._ann = None
+        self._ann_covered = 0
+        self._ann_stale = False
         self.lock = threading.RLock()
         z = lambda dt: torch.zeros(0, dtype=dt, device=self.device)  # noqa: E731
         self.e = {"src": z(torch.int32), "dst": z(torch.int32), "w": z(torch.float32), "co": z(torch.int32),
@@ -381,6 +385,8 @@ class TenantGraph:
                     self.types.append(t)
                     self.row_of[i] = r
                 else:
+                    if r < self._ann_covered:
+                        self._ann_stale = True  # re-added id: its row gets a new vector
                     if kind_h is not None and r < len(kind_h) and kind_h[r] == NODE:
                         self._unlink_row(r)
                     self.content[r] = contents[j]
@@ -608,6 +614,8 @@ class TenantGraph:
 
     def set_embedding(self, r: int, emb) -> None:
         self.odd_emb.pop(r, None)
+        if r < self._ann_covered:
+            self._ann_stale = True  # an indexed row's vector changed: rebuild the IVF-PQ codes
         if emb is None or len(emb) == 0:
             if self.dim is not None:
                 with self.on_stream():
@@ -1174,6 +1182,12 @@ class TenantGraph:
             Qf = Qf / torch.where(qn > 0, qn, torch.ones_like(qn))
         bias = self.store_bias("l2" if metric == "l2" else "ip")
         alpha = 2.0 if metric == "l2" else 1.0
+        cfg = self.ann_cfg
+        if cfg is not None and n >= cfg["min_rows"] and self.unit_rows():
+            # IVF-PQ candidates (the store's index="ivfpq"), re-ranked exactly
+            # in fp32 against this graph's rows with the store's row mask
+            cand = self._ann_candidates(Qf, max(cfg.get("rerank", 1024), k), cfg)
+            return self._rerank_store(Qf, cand, k, metric, bias)
         kc = min(CAND_SLOTS, max(k, 2 * k))
         if self.on_gpu and k <= CAND_SLOTS and (metric != "cosine" or self.unit_rows()) \
                 and M * n >= KERNEL_MIN_WORK // 16:
@@ -1184,6 +1198,32 @@ class TenantGraph:
                 _, cand = flat_topk(self.emb16[:n], q16, kc, bias=bias, alpha=alpha)
             return self._rerank_store(Qf, cand, k, metric, bias)
         return self._exact_store(Qf, k, metric, bias)
+
+    def _ann_candidates(self, Qf: torch.Tensor, R: int, cfg: Dict) -> torch.Tensor:
+        """Graph rows [M, R] from the tenant's IVF-PQ index, built on first
+        use over the unit rows (ids = rows) and extended with the rows
+        appended since; rebuilt when an embedding was rewritten in place.
+        Removed / unstored rows stay in the index and are dropped by the
+        re-rank's -inf bias."""
+        from ..index.ivfpq import IVFPQIndex
+        n = self.n
+        idx = self._ann
+        if idx is None or self._ann_stale or self._ann_covered > n:
+            m = cfg["m"] if self.dim % cfg["m"] == 0 else next(d for d in (64, 48, 32, 16, 8) if self.dim % d == 0)
+            nlist = max(16, min(cfg["nlist"], n // 64))
+            idx = IVFPQIndex(self.dim, nlist=nlist, m=m, device=self.device)
+            live = torch.nonzero(self.has_emb[:n] == 1).flatten()
+            g = torch.Generator(device="cpu").manual_seed(0)
+            pick = live[torch.randperm(live.numel(), generator=g)[: min(live.numel(), 262144)].to(live.device)]
+            idx.train(self.emb32[pick], iters=8, pq_iters=8)
+            idx.reserve(n)
+            self._ann, self._ann_covered, self._ann_stale = idx, 0, False
+        step = 1 << 20
+        while self._ann_covered < n:
+            r1 = min(n, self._ann_covered + step)
+            idx.add(self.emb32[self._ann_covered:r1], ids=torch.arange(self._ann_covered, r1))
+            self._ann_covered = r1
+        return idx.candidate_ids(Qf, R, cfg["nprobe"])
 
     def _fp8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
         """Store-search candidates from the fp8 scan (rows in ``emb8``),

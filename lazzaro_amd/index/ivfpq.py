@@ -245,7 +245,8 @@ class IVFPQIndex:
         o = torch.argsort(self._list[:n], stable=True)
         codes = torch.empty_like(self._codes)
         for c0 in range(0, n, chunk):
-            codes[c0:c0 + chunk] = self._codes[o[c0:c0 + chunk]]
+            c1 = min(n, c0 + chunk)
+            codes[c0:c1] = self._codes[o[c0:c1]]
         self._codes = codes
         self._list[:n] = self._list[:n][o]
         self._pos[:n] = self._pos[:n][o]
@@ -305,6 +306,25 @@ class IVFPQIndex:
         s, rows = s[:, :k], rows[:, :k]
         ids = torch.where(rows >= 0, self._vids[self._pos[rows.clamp_min(0)]], torch.full_like(rows, -1))
         return s, ids
+
+    def candidate_ids(self, q: torch.Tensor, R: int, nprobe: int = 16) -> torch.Tensor:
+        """The ids of the exact PQ top-``R`` rows over the ``nprobe`` probed
+        lists per query ([nq, R] int64, -1 padded) -- for a caller that
+        re-ranks with its own exact vectors (TenantGraph's fp32 rows)."""
+        self._finalize()
+        qf = _unit(q.to(self.device).float())
+        nq = qf.shape[0]
+        nprobe = min(nprobe, self.nlist)
+        coarse, probes = torch.topk(qf @ self.centroids.T, nprobe, dim=1)
+        lut = torch.einsum("qmd,mcd->qmc", qf.view(nq, self.m, self.dsub), self.codebooks).contiguous()
+        if self.device.type != "cuda":
+            _, rows = self._scan_ref(probes, coarse, lut, R)
+        elif R <= KSLOTS[-1]:
+            _, rows = self._scan_gpu(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, R)
+        else:
+            _, rows = self._scan_candidates(probes.to(torch.int32).contiguous(), coarse.contiguous(), lut, R)
+        rows = rows.long()
+        return torch.where(rows >= 0, self._vids[self._pos[rows.clamp_min(0)]], torch.full_like(rows, -1))
 
     def _rerank_gpu_ok(self, k: int) -> bool:
         if self.device.type != "cuda" or k > KSLOTS[-1]:

@@ -329,3 +329,30 @@ def test_flat_topk_fp8_matches_bf16_candidates_gpu():
     s8, r8 = flat_topk_fp8(X8, Q8, 64.0 * 64.0, X16, Q16, 10, bias=bias, alpha=2.0, margin=margin)
     same = sum(len(set(a) & set(b)) for a, b in zip(r8.cpu().tolist(), r16.cpu().tolist())) / (nq * 10)
     assert same >= 0.999 and torch.allclose(s8, s16, atol=1e-4, rtol=0)
+
+
+def test_ivfpq_store_under_tenant_graph_gpu(tmp_path):
+    """index="ivfpq" on the GPU: the tenant graph's store search takes IVF-PQ
+    candidates (deep pool + threshold pass) re-ranked exactly in fp32."""
+    import torch
+
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    g0 = torch.Generator(device="cuda").manual_seed(0)
+    C, per, d = 400, 500, 128
+    cen = torch.nn.functional.normalize(torch.randn(C, d, device="cuda", generator=g0), dim=1)
+    X = torch.nn.functional.normalize(cen.repeat_interleave(per, 0)
+                                      + 0.5 * torch.randn(C * per, d, device="cuda", generator=g0) / d ** 0.5, dim=1)
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=d), enable_async=False,
+                      load_from_disk=False, db_dir=str(tmp_path), device="cuda", index="ivfpq",
+                      index_params={"nlist": 512, "nprobe": 16, "pq_m": 32, "ivf_min_rows": 100_000})
+    g = ms.graph
+    g.add_nodes([f"m{i}" for i in range(len(X))], [""] * len(X), X, shard=g.shard_id("w"), stored=True)
+    q = torch.nn.functional.normalize(X[:256] + 0.3 * torch.randn(256, d, device="cuda", generator=g0) / d ** 0.5,
+                                      dim=1)
+    _, rows = g.store_search(q, 10, "l2")
+    assert g._ann is not None
+    truth = torch.topk(-torch.cdist(q, X), 10, dim=1).indices
+    hit = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(rows.cpu(), truth.cpu())) / truth.numel()
+    assert hit > 0.9, hit
+    ms.close()

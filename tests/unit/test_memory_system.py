@@ -520,3 +520,33 @@ def test_get_stats_engine_block():
     e = s["engine"]
     assert e["search_queries"] == 3 and e["hbm_graph_bytes"] > 0 and e["search_qps"] > 0
     ms.close()
+
+
+def test_ivfpq_index_under_the_tenant_graph(tmp_path):
+    """MemorySystem(index="ivfpq"): a tenant above ivf_min_rows is searched
+    through IVF-PQ candidates re-ranked exactly on the graph's fp32 rows --
+    removed rows never come back, fresh rows are indexed on the next search."""
+    import torch
+    g0 = torch.Generator().manual_seed(0)
+    C, per, d = 20, 200, 32
+    cen = torch.nn.functional.normalize(torch.randn(C, d, generator=g0), dim=1)
+    X = torch.nn.functional.normalize(cen.repeat_interleave(per, 0) + 0.3 * torch.randn(C * per, d, generator=g0), dim=1)
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=d), enable_async=False,
+                      load_from_disk=False, db_dir=str(tmp_path), index="ivfpq",
+                      index_params={"nlist": 16, "nprobe": 16, "pq_m": 8, "ivf_min_rows": 1000})
+    g = ms.graph
+    g.add_nodes([f"m{i}" for i in range(len(X))], [f"c{i}" for i in range(len(X))], X, shard=g.shard_id("w"),
+                stored=True)
+    q = X[:40] + 0.01 * torch.randn(40, d, generator=g0)
+    s, rows = g.store_search(q, 5, "l2")
+    assert g._ann is not None and g._ann_covered == len(X)
+    truth = torch.topk(-torch.cdist(q, X), 5, dim=1).indices
+    hit = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(rows, truth)) / truth.numel()
+    assert hit > 0.95
+    g.remove_nodes([0], unstore=True)
+    _, rows = g.store_search(X[:1], 3, "l2")
+    assert 0 not in rows[0].tolist()
+    g.add_nodes(["fresh"], ["f"], X[5:6] * 1.0, shard=g.shard_id("w"), stored=True)
+    _, rows = g.store_search(X[5:6], 2, "l2")
+    assert g._ann_covered == g.n and set(rows[0].tolist()) == {5, g.n - 1}
+    ms.close()
