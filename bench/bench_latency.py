@@ -3,8 +3,11 @@
 query text -> on-device embedding -> exact top-k over one user's memories.
 
 Reports p50/p99 for: the bge-base query embed eager vs hipGraph replay, the
-single-query flat scan of a 1M-row and a 10M-row arena, and the end-to-end
-``HBMStore.search_nodes`` call. Synthetic data, random-init weights.
+single-query flat scan of a 1M-row and a 10M-row arena, the end-to-end
+``HBMStore.search_nodes`` call, and through ``MemorySystem`` on the GPU:
+``search_memories`` and the chat retrieval (embed + retrieve + boost, LLM
+excluded) over 200k- and 10M-memory tenants. Synthetic data, random-init
+weights.
 """
 import argparse
 import json
@@ -81,6 +84,28 @@ def main():
         res["store_search_200k"] = timed(lambda: st.search_nodes(qv, user_id="u", limit=5), a.iters // 2)
         res["embed_plus_store_search_200k"] = timed(
             lambda: st.search_nodes(emb.embed(q), user_id="u", limit=5), a.iters // 2)
+    # through the product API: MemorySystem on the GPU, the tenant graph in
+    # HBM (search_memories = embed + store search + Node mapping; the chat
+    # retrieval = embed + hierarchical/vector retrieval + neighbour boost,
+    # LLM excluded), tenants of 200k and 10M memories
+    from bench import populate
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import LocalLLM
+    for n in (200_000, 10_000_000):
+        with tempfile.TemporaryDirectory() as d:
+            ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, device=dev, db_dir=d,
+                              load_from_disk=False, enable_async=False, enable_caching=False,
+                              max_buffer_size=2 * n)
+            populate(ms, n, 768, dev, seed=1)
+            ms.start_conversation()
+            tag = f"{n // 1000}k" if n < 1_000_000 else f"{n // 1_000_000}M"
+            ms.search_memories(q, limit=5)
+            res[f"api_search_memories_{tag}"] = timed(lambda: ms.search_memories(q, limit=5), a.iters // 2)
+            ms._retrieve_for(q)
+            res[f"api_chat_retrieval_{tag}"] = timed(lambda: ms._retrieve_for(q), a.iters // 2)
+            ms.close()
+            del ms
+            torch.cuda.empty_cache()
     print(json.dumps(res), flush=True)
 
 

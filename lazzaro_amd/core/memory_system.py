@@ -346,7 +346,7 @@ class MemorySystem(ConsolidationMixin):
         """Reference :242-260 on the device graph: one ``tg_boost_kernel``
         launch over the visible-arc CSR of the retrieved rows."""
         g = self.graph
-        rows = [g.node_row(i, include_super=False) for i in retrieved_ids]
+        rows = g.node_rows_of(retrieved_ids, include_super=False)
         count = g.boost(rows)
         if count:
             self._say(f"   (Graph: Boosted {count} neighbor nodes via association)")
@@ -430,7 +430,7 @@ class MemorySystem(ConsolidationMixin):
             parts.append(f"User Profile:\n{pc}\n")
         if retrieved_ids:
             g = self.graph
-            rows = [g.node_row(i) for i in retrieved_ids]
+            rows = g.node_rows_of(retrieved_ids)
             texts = [f"- {g.content[r]}" for r in rows if r >= 0]
             g.touch(rows)  # update_access for each retrieved node (buffer_graph.py:79-85)
             if texts:
@@ -469,9 +469,14 @@ class MemorySystem(ConsolidationMixin):
     def _node_lines(self, ids: List[str]) -> List[str]:
         g = self.graph
         out = []
-        sh = g.mirror("shard")
-        for nid in ids:
-            r = g.node_row(nid)
+        rows = g.node_rows_of(ids)
+        live = [r for r in rows if r >= 0]
+        sh = {}
+        if live:  # the shard codes of these rows only (a turn must not mirror a 10M-row column)
+            with g.on_stream():
+                codes = g.shard[torch.as_tensor(live, dtype=torch.long).to(g.device)].cpu().tolist()
+            sh = dict(zip(live, codes))
+        for nid, r in zip(ids, rows):
             if r >= 0:
                 c = g.content[r]
                 snip = c[:60] + "..." if len(c) > 60 else c

@@ -511,6 +511,21 @@ class TenantGraph:
             return -1
         return r
 
+    def node_rows_of(self, ids: Sequence[str], include_super: bool = True) -> List[int]:
+        """:meth:`node_row` for many ids with one small device gather of
+        their (kind, sup) -- no whole-column mirror on the per-turn path."""
+        rows = [self.row_of.get(i, -1) for i in ids]
+        known = [r for r in rows if r >= 0]
+        if not known:
+            return [-1] * len(rows)
+        kind, sup = self.flags_of(known)
+        ok = {r: (k == NODE and (include_super or not sp)) for r, k, sp in zip(known, kind.tolist(), sup.tolist())}
+        return [r if r >= 0 and ok[r] else -1 for r in rows]
+
+    def _mirror_fresh(self, name: str) -> bool:
+        m = self._mirror.get(name)
+        return m is not None and m[0] == self.version and len(m[1]) == self.n
+
     # host mirrors of device columns (refreshed when the graph version moves)
     def mirror(self, name: str) -> np.ndarray:
         m = self._mirror.get(name)
@@ -543,6 +558,14 @@ class TenantGraph:
 
     def node_rows_where(self, shard_code: Optional[int] = None, super_: Optional[bool] = None) -> np.ndarray:
         """Live node rows (ascending) filtered by shard code / super flag."""
+        if super_ is True and shard_code is None and not self._mirror_fresh("kind"):
+            # the few super-node rows by a device select: retrieval's
+            # super-node step must not mirror two whole columns per turn
+            if self.n_super == 0:
+                return np.zeros(0, dtype=np.int64)
+            n = self.n
+            with self.on_stream():
+                return torch.nonzero((self.kind[:n] == NODE) & (self.sup[:n] != 0)).flatten().cpu().numpy()
         kind = self.mirror("kind")
         m = kind == NODE
         if shard_code is not None:
