@@ -174,6 +174,98 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     return out
 
 
+def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: int, warmup: int, encoder=None,
+                dim: int = 768, dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096,
+                n_top: int = 64, cluster_iters: int = 2, init_edges: int = None, db_dir: str = None):
+    """BASELINE config 4 as ONE tenant: a ``nodes_per_rank * world``-node
+    buffer row-sharded over the ranks (``ShardedMemorySystem``); every step
+    each rank brings ``convs`` conversations, the whole batch is consolidated
+    over the whole buffer (facts all-gathered, each rank scans them against
+    its rows, top-3 lists merged, global eviction, distributed CC, distributed
+    k-means hierarchy), each rank commits its rows. Per-rank scan work is
+    (world * convs * facts) x nodes_per_rank: the buffer is split N ways,
+    every fact is compared with every memory (the reference's semantics)."""
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
+
+    world = comm.world
+    db_dir = db_dir or tempfile.mkdtemp(prefix=f"lzshc{comm.rank}_")
+    init_edges = 2 * nodes_per_rank if init_edges is None else init_edges
+    sm = ShardedMemorySystem(comm, "buffer", max_buffer_size=nodes_per_rank * world, llm_provider=LocalLLM(),
+                             embedding_provider=encoder or HashEmbedder(dim=dim), db_dir=db_dir, device=dev,
+                             hierarchy_params={"fine": n_fine, "top": n_top, "every": cluster_every * convs * world,
+                                               "iters": cluster_iters})
+    g = sm.g
+    g._set_dim(dim)
+    g.reserve(int(nodes_per_rank * 1.05) + 65536)
+    codes = torch.tensor(sm.register_shards(SHARDS), dtype=torch.int32, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(seed + 31 * comm.rank)
+    now = time.time()
+    chunk = 1 << 20
+    t0 = time.perf_counter()
+    for r0 in range(0, nodes_per_rank, chunk):  # collective per chunk: global node numbers, rank-major
+        r1 = min(nodes_per_rank, r0 + chunk)
+        v = torch.randn((r1 - r0, dim), device=dev, generator=gen)
+        v /= v.norm(dim=1, keepdim=True)
+        sm.add_memories([f"memory {comm.rank}.{i}" for i in range(r0, r1)], v, salience=0.5, now=now,
+                        shard_codes=codes[torch.arange(r0, r1, device=dev) % len(SHARDS)])
+    if init_edges:
+        src = torch.randint(0, nodes_per_rank, (init_edges,), device=dev, generator=gen)
+        dst = torch.randint(0, nodes_per_rank, (init_edges,), device=dev, generator=gen)
+        w = torch.rand(init_edges, device=dev, generator=gen) * 0.5 + 0.5
+        g.append_edges(src.int(), dst.int(), w, g.shard[src], g.etype("relates_to"))
+    g.clear_tracking(stored=False)
+    _sync(dev)
+    load_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    sm.cluster_pass()
+    _sync(dev)
+    seed_ms = (time.perf_counter() - t0) * 1e3
+    rng = random.Random(seed + comm.rank)
+    batches = iter([synth_facts(convs, facts, rng) for _ in range(warmup + steps)])
+
+    def step():
+        conversations = next(batches)
+        V = synth_vectors(sm.local, convs * facts, dim, dup_rate, gen)
+        if encoder is not None:
+            from lazzaro_amd.utils.tracing import tracer as _tr
+            with _tr.stage("fact_embed", dev):
+                sm.local._batch_embed_any([f["content"] for c in conversations for f in c])
+        return sm.consolidate_batch(conversations, embeddings=V)
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    agg = {}
+    for _ in range(steps):
+        for k, v in step().items():
+            agg[k] = agg.get(k, 0) + v
+    _sync(dev)
+    comm.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")
+    comm.all_reduce(t, "max")
+    el = float(t.item())
+    from lazzaro_amd.utils.tracing import tracer
+    stages = {k: v["p50_ms"] for k, v in tracer.summary().items()} if tracer.enabled else None
+    st = sm.get_stats()
+    out = {"turns_per_s": round(convs * world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
+           "buffer_nodes_total": st["total_nodes"], "nodes_per_rank": nodes_per_rank, "edges_total": st["total_edges"],
+           "convs_per_rank_step": convs, "facts_per_conv": facts,
+           "per_step": {k: round(v / steps, 1) for k, v in agg.items()},
+           "scan_facts_x_rows_per_rank_step": int(world * convs * facts * nodes_per_rank),
+           "path": "ShardedMemorySystem.consolidate_batch (one tenant row-sharded over the ranks)",
+           "hierarchical_clustering": {"mode": "distributed kmeans", "every_steps": cluster_every, "fine": n_fine,
+                                       "top": n_top, "iters_per_pass": cluster_iters,
+                                       "seed_pass_ms": round(seed_ms, 1)},
+           "load_s": round(load_s, 1), "stages_p50_ms": stages,
+           "persistence": "incremental columnar commit of each rank's rows per step"}
+    sm.close()
+    return out
+
+
 if __name__ == "__main__":
     import argparse
     import json
@@ -192,6 +284,8 @@ if __name__ == "__main__":
     ap.add_argument("--top", type=int, default=64)
     ap.add_argument("--cluster-iters", type=int, default=2)
     ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--sharded", action="store_true",
+                    help="config 4 as one tenant row-sharded over the ranks (--nodes per rank)")
     a = ap.parse_args()
     comm = Communicator.init()
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -200,7 +294,8 @@ if __name__ == "__main__":
     if not a.no_embed and dev.type == "cuda":
         from lazzaro_amd.core.embedders import OnDeviceEmbedder
         enc = OnDeviceEmbedder("bge-base", device=dev, max_len=64)
-    res = run(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
-              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters)
+    fn = run_sharded if a.sharded else run
+    res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
+             n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters)
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)

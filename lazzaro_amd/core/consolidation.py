@@ -71,6 +71,133 @@ PROFILE_CONTENTS = 10  # contents per profile prompt (reference memory_system.py
 SALIENCE_FLOOR_ = 0.2  # node salience decays towards it (reference memory_shard.py:64-77)
 
 
+def batch_dedupe(Qn: torch.Tensor, ct: torch.Tensor, gb_s: torch.Tensor, gb_node: torch.Tensor):
+    """In-batch dedupe of a fact batch (reference :719-741 applied to B
+    conversations in order): fact j is a duplicate when its best match -- the
+    store top-1 over the pre-batch graph (``gb_s``, cosine; ``gb_node``: it is
+    a live node) or a KEPT fact of an earlier conversation -- exceeds
+    DEDUPE_THRESHOLD. Kept-ness depends on earlier facts' decisions, so the
+    masks are iterated to their fixed point. Qn: unit fp64 [M, D]; ct: the
+    conversation of each fact [M]. Returns (S = Qn Qn^T, earlier[j, i],
+    dup, batch_best, bb_i, ins)."""
+    NEG = float("-inf")
+    M = Qn.shape[0]
+    S = Qn @ Qn.T
+    earlier = ct[None, :] < ct[:, None]  # [j, i]: fact i is from an earlier conversation than j
+    ins = torch.ones(M, dtype=torch.bool, device=Qn.device)
+    for _ in range(M + 1):
+        A = torch.where(earlier & ins[None, :], S, torch.full_like(S, NEG))
+        bb_s = A.max(1).values
+        bb_i = torch.argmax((A == bb_s[:, None]).to(torch.int8), 1)
+        batch_best = bb_s > gb_s
+        best_s = torch.where(batch_best, bb_s, gb_s)
+        dup = (best_s > DEDUPE_THRESHOLD) & (batch_best | gb_node)
+        if torch.equal(~dup, ins):
+            break
+        ins = ~dup
+    return S, earlier, dup, batch_best, bb_i, ins
+
+
+def salience_decayed(s: torch.Tensor, n: torch.Tensor, keep: float) -> torch.Tensor:
+    """Node salience after ``n`` decays (floor SALIENCE_FLOOR_, memory_shard.py:64-77)."""
+    kn = torch.pow(torch.full_like(s, keep), n.double())
+    return torch.where(s > SALIENCE_FLOOR_, SALIENCE_FLOOR_ + (s - SALIENCE_FLOOR_) * kn,
+                       torch.full_like(s, SALIENCE_FLOOR_))
+
+
+def batch_link_plan(kidx, new_row, code_all, ct, S, earlier, shard_hits, global_hits, keep: float, B: int, thr,
+                    stats: Dict[str, int]):
+    """Edges created by the kept facts of a batch (reference :797-891), in
+    the reference's order (per conversation: chain, within-shard, cross-memory)
+    and pre-decayed by the end_conversation calls from their conversation on.
+
+    ``kidx``: kept fact positions; ``new_row[M]``: the node key each fact
+    became (-1 not kept) -- graph rows here, global node numbers for a
+    row-sharded tenant; ``code_all[M]``: shard codes; ``shard_hits`` /
+    ``global_hits``: (sims [M, 3], keys [M, 3]) from the pre-batch graph in the
+    same key space. Updates stats (linked, cross_links, pruned). Returns
+    (src, dst, w fp64, shard) keys or None, and the cross-link count."""
+    dev = S.device
+    M = S.shape[0]
+    NEG = float("-inf")
+    K = kidx.numel()
+    kc = ct[kidx]
+    kcode = code_all[kidx].long()
+    # shards with >= 2 new nodes in the same conversation (reference :814-815)
+    key = kc * (1 << 24) + kcode
+    uniq, inv, cnt = torch.unique(key, return_inverse=True, return_counts=True)
+    multi = cnt[inv] >= 2
+    ins_b = torch.zeros(M, dtype=torch.bool, device=dev)
+    ins_b[kidx] = True
+    code_all = code_all.long()
+    es, ed, ew, eh, order = [], [], [], [], []
+    # chain edges between consecutive new nodes of a (conversation, shard)
+    o = torch.argsort(key * K + torch.arange(K, device=dev))
+    ks = key[o]
+    adj = torch.nonzero(ks[1:] == ks[:-1]).flatten()
+    if adj.numel():
+        a, b = o[adj], o[adj + 1]
+        es.append(new_row[kidx[a]])
+        ed.append(new_row[kidx[b]])
+        ew.append(torch.full((a.numel(),), CHAIN_WEIGHT, dtype=torch.float64, device=dev))
+        eh.append(kcode[a])
+        order.append(kc[a] * 4)
+    Sk = S[kidx]  # [K, M]
+    ek = earlier[kidx] & ins_b[None, :]
+
+    def merged_top(graph_s, graph_r, batch_mask):
+        bs = torch.where(batch_mask, Sk, torch.full_like(Sk, NEG))
+        t = min(LINK_TOPK, M)
+        tb_s, tb_i = torch.topk(bs, t, dim=1)
+        tb_r = torch.where(torch.isneginf(tb_s), torch.full_like(tb_i, -1), new_row[tb_i])
+        cs = torch.cat([graph_s[kidx], tb_s], 1)
+        cr = torch.cat([graph_r[kidx], tb_r], 1)
+        keyr = torch.where(cr >= 0, cr, torch.full_like(cr, 1 << 62))
+        o2 = torch.argsort(keyr, dim=1, stable=True)
+        cs, cr = torch.gather(cs, 1, o2), torch.gather(cr, 1, o2)
+        o3 = torch.sort(cs, dim=1, descending=True, stable=True).indices[:, :LINK_TOPK]
+        return torch.gather(cs, 1, o3), torch.gather(cr, 1, o3)
+
+    # within-shard similarity links: same shard, from the graph or earlier conversations
+    sw_, sr_ = merged_top(shard_hits[0], shard_hits[1], ek & (code_all[None, :] == kcode[:, None]))
+    src = new_row[kidx][:, None].expand(-1, LINK_TOPK)
+    mw = (sr_ >= 0) & (sw_ > LINK_THRESHOLD) & multi[:, None]
+    es.append(src[mw])
+    ed.append(sr_[mw])
+    ew.append(sw_[mw] * LINK_WEIGHT_SCALE)
+    eh.append(kcode[:, None].expand_as(sr_)[mw])
+    order.append(kc[:, None].expand_as(sr_)[mw] * 4 + 1)
+    # cross-memory links: any non-super node, skipping pairs linked within the shard
+    gw_, gr_ = merged_top(global_hits[0], global_hits[1], ek)
+    mg = (gr_ >= 0) & (gw_ > LINK_THRESHOLD)
+    mg &= ~((gr_[:, :, None] == sr_[:, None, :]) & mw[:, None, :]).any(dim=2)
+    es.append(src[mg])
+    ed.append(gr_[mg])
+    ew.append(gw_[mg] * LINK_WEIGHT_SCALE)
+    eh.append(kcode[:, None].expand_as(gr_)[mg])
+    order.append(kc[:, None].expand_as(gr_)[mg] * 4 + 2)
+    n_cross = int(mg.sum())
+    Sr, Dr = torch.cat(es), torch.cat(ed)
+    if Sr.numel() == 0:
+        return None, n_cross
+    W = torch.cat(ew)
+    Ord = torch.cat(order)
+    # decays of the end_conversation calls from the edge's conversation on
+    W = W * torch.pow(torch.full_like(W, keep), (B - torch.div(Ord, 4, rounding_mode="floor")).double())
+    stats["linked"] += int(Sr.numel())
+    stats["cross_links"] += n_cross
+    H = torch.cat(eh)
+    o = torch.argsort(Ord, stable=True)
+    Sr, Dr, W, H = Sr[o], Dr[o], W[o], H[o]
+    if thr is not None:
+        alive = W >= thr
+        stats["pruned"] += int((~alive).sum())
+        Sr, Dr, W, H = Sr[alive], Dr[alive], W[alive], H[alive]
+    if Sr.numel() == 0:
+        return None, n_cross
+    return (Sr, Dr, W, H), n_cross
+
+
 def _parse_json(response: str):
     if response is None:
         raise json.JSONDecodeError("empty", "", 0)
@@ -586,29 +713,12 @@ class ConsolidationMixin:
         # ---- 2. in-batch dedupe: the store top-1 over graph rows + the facts
         # kept from earlier conversations, to a fixed point
         with tracer.stage("cb_dedupe", self._device):
-            S = Qn @ Qn.T
-            earlier = ct[None, :] < ct[:, None]  # [j, i]: fact i is from an earlier conversation than j
-            ins = torch.ones(M, dtype=torch.bool, device=dev)
-            for _ in range(M + 1):
-                A = torch.where(earlier & ins[None, :], S, torch.full_like(S, NEG))
-                bb_s = A.max(1).values
-                bb_i = torch.argmax((A == bb_s[:, None]).to(torch.int8), 1)
-                batch_best = bb_s > gb_s
-                best_s = torch.where(batch_best, bb_s, gb_s)
-                dup = (best_s > DEDUPE_THRESHOLD) & (batch_best | gb_node)
-                if torch.equal(~dup, ins):
-                    break
-                ins = ~dup
+            S, earlier, dup, batch_best, bb_i, ins = batch_dedupe(Qn, ct, gb_s, gb_node)
         dup_graph = dup & ~batch_best
         dup_batch = dup & batch_best
 
-        def decayed(s: torch.Tensor, n: torch.Tensor) -> torch.Tensor:
-            kn = torch.pow(torch.full_like(s, keep), n.double())
-            return torch.where(s > SALIENCE_FLOOR_, SALIENCE_FLOOR_ + (s - SALIENCE_FLOOR_) * kn,
-                               torch.full_like(s, SALIENCE_FLOOR_))
-
         left = (B - ct).double()  # decays still to come for a fact of conversation c
-        sal_dec = decayed(sal_in, left)
+        sal_dec = salience_decayed(sal_in, left, keep)
 
         # ---- 3. decay + prune the pre-batch graph by B conversations at once
         with tracer.stage("cb_decay", self._device):
@@ -669,85 +779,12 @@ class ConsolidationMixin:
     def _link_batch_multi(self, kidx, new_row, codes, ct, S, earlier, shard_hits, global_hits, keep, B, thr, now,
                           stats) -> None:
         g = self.graph
-        dev = g.device
-        M = S.shape[0]
-        NEG = float("-inf")
-        K = kidx.numel()
-        kc = ct[kidx]
-        kcode = torch.as_tensor(codes).to(dev)[kidx].long()
-        # shards with >= 2 new nodes in the same conversation (reference :814-815)
-        key = kc * (1 << 24) + kcode
-        uniq, inv, cnt = torch.unique(key, return_inverse=True, return_counts=True)
-        multi = cnt[inv] >= 2
-        ins_b = torch.zeros(M, dtype=torch.bool, device=dev)
-        ins_b[kidx] = True
-        code_all = torch.as_tensor(codes).to(dev).long()
-        es, ed, ew, eh, order = [], [], [], [], []
-        # chain edges between consecutive new nodes of a (conversation, shard)
-        o = torch.argsort(key * K + torch.arange(K, device=dev))
-        ks = key[o]
-        adj = torch.nonzero(ks[1:] == ks[:-1]).flatten()
-        if adj.numel():
-            a, b = o[adj], o[adj + 1]
-            es.append(new_row[kidx[a]])
-            ed.append(new_row[kidx[b]])
-            ew.append(torch.full((a.numel(),), CHAIN_WEIGHT, dtype=torch.float64, device=dev))
-            eh.append(kcode[a])
-            order.append(kc[a] * 4)
-        Sk = S[kidx]  # [K, M]
-        ek = earlier[kidx] & ins_b[None, :]
-
-        def merged_top(graph_s, graph_r, batch_mask):
-            bs = torch.where(batch_mask, Sk, torch.full_like(Sk, NEG))
-            t = min(LINK_TOPK, M)
-            tb_s, tb_i = torch.topk(bs, t, dim=1)
-            tb_r = torch.where(torch.isneginf(tb_s), torch.full_like(tb_i, -1), new_row[tb_i])
-            cs = torch.cat([graph_s[kidx], tb_s], 1)
-            cr = torch.cat([graph_r[kidx], tb_r], 1)
-            keyr = torch.where(cr >= 0, cr, torch.full_like(cr, 1 << 62))
-            o2 = torch.argsort(keyr, dim=1, stable=True)
-            cs, cr = torch.gather(cs, 1, o2), torch.gather(cr, 1, o2)
-            o3 = torch.sort(cs, dim=1, descending=True, stable=True).indices[:, :LINK_TOPK]
-            return torch.gather(cs, 1, o3), torch.gather(cr, 1, o3)
-
-        # within-shard similarity links: same shard, from the graph or earlier conversations
-        sw_, sr_ = merged_top(shard_hits[0], shard_hits[1], ek & (code_all[None, :] == kcode[:, None]))
-        src = new_row[kidx][:, None].expand(-1, LINK_TOPK)
-        mw = (sr_ >= 0) & (sw_ > LINK_THRESHOLD) & multi[:, None]
-        es.append(src[mw])
-        ed.append(sr_[mw])
-        ew.append(sw_[mw] * LINK_WEIGHT_SCALE)
-        eh.append(kcode[:, None].expand_as(sr_)[mw])
-        order.append(kc[:, None].expand_as(sr_)[mw] * 4 + 1)
-        # cross-memory links: any non-super node, skipping pairs linked within the shard
-        gw_, gr_ = merged_top(global_hits[0], global_hits[1], ek)
-        mg = (gr_ >= 0) & (gw_ > LINK_THRESHOLD)
-        mg &= ~((gr_[:, :, None] == sr_[:, None, :]) & mw[:, None, :]).any(dim=2)
-        es.append(src[mg])
-        ed.append(gr_[mg])
-        ew.append(gw_[mg] * LINK_WEIGHT_SCALE)
-        eh.append(kcode[:, None].expand_as(gr_)[mg])
-        order.append(kc[:, None].expand_as(gr_)[mg] * 4 + 2)
-        n_cross = int(mg.sum())
+        plan, n_cross = batch_link_plan(kidx, new_row, torch.as_tensor(codes).to(g.device), ct, S, earlier,
+                                        shard_hits, global_hits, keep, B, thr, stats)
         if n_cross:
             self._say(f"✓ Created {n_cross} cross-conversation links")
-        Sr, Dr = torch.cat(es), torch.cat(ed)
-        if Sr.numel() == 0:
-            return
-        W = torch.cat(ew)
-        Ord = torch.cat(order)
-        # decays of the end_conversation calls from the edge's conversation on
-        W = W * torch.pow(torch.full_like(W, keep), (B - torch.div(Ord, 4, rounding_mode="floor")).double())
-        stats["linked"] += int(Sr.numel())
-        stats["cross_links"] += n_cross
-        H = torch.cat(eh)
-        o = torch.argsort(Ord, stable=True)
-        Sr, Dr, W, H = Sr[o], Dr[o], W[o], H[o]
-        if thr is not None:
-            alive = W >= thr
-            stats["pruned"] += int((~alive).sum())
-            Sr, Dr, W, H = Sr[alive], Dr[alive], W[alive], H[alive]
-        if Sr.numel():
+        if plan is not None:
+            Sr, Dr, W, H = plan
             g.append_edges(Sr, Dr, W.float(), H.to(torch.int32), g.etype("relates_to"), now=now)
 
     # ------------------------------------------------------------ hierarchy (K8/K16)

@@ -1309,7 +1309,7 @@ class TenantGraph:
         return [[ids[x] for x in row if x >= 0] for row in r.cpu().tolist()]
 
     # ------------------------------------------------------------------ k-means hierarchy (K16)
-    def cluster_pass(self, n_fine: int = 4096, n_top: int = 64, iters: int = 2, seed: int = 0) -> Dict:
+    def cluster_pass(self, n_fine: int = 4096, n_top: int = 64, iters: int = 2, seed: int = 0, comm=None) -> Dict:
         """Two-level hierarchical clustering of the live shard nodes (SURVEY.md
         §2.4 K16; ``MemorySystem(hierarchy_mode="kmeans")``): spherical k-means
         into ``n_fine`` clusters over the tenant's rows in place (fused MFMA
@@ -1318,7 +1318,12 @@ class TenantGraph:
         ``n_top`` topic clusters -- the scalable form of the reference's one
         mean super-node per shard (memory_system.py:893-933). Keeps
         ``self.hier``: top centroids, each row's fine / top label and the
-        rows ordered by (top cluster, row) for child lookups."""
+        rows ordered by (top cluster, row) for child lookups.
+
+        ``comm`` (world > 1): the rows are one row-sharded tenant's local part;
+        the fine level is the distributed k-means (centroid sums all-reduced,
+        SURVEY.md §2.5 C4) and the topic level runs replicated on the
+        identical fine centroids, so every rank holds the same hierarchy."""
         from ..index.kmeans import kmeans
 
         n = self.n
@@ -1327,13 +1332,20 @@ class TenantGraph:
         with self.on_stream():
             live = (self.kind[:n] == NODE) & (self.sup[:n] == 0) & (self.has_emb[:n] == 1)
             n_live = int(live.sum())
-            if n_live == 0:
+            dist = comm is not None and comm.world > 1
+            if dist:
+                t = torch.tensor([n_live], dtype=torch.int64, device=comm.device)
+                comm.all_reduce(t)
+                n_glob = int(t.item())
+            else:
+                n_glob = n_live
+            if n_glob == 0:
                 return {}
             if self.on_gpu:
                 X = self.emb16[:n]
             else:
                 X = self.emb32[:n] / self.sqn[:n].sqrt().clamp_min(1e-30)[:, None]
-            kf = min(n_fine, n_live)
+            kf = min(n_fine, n_glob)
             kt = min(n_top, kf)
             prev = getattr(self, "hier", None) or {}
             init_f = prev.get("fine_c") if prev.get("fine_c") is not None and prev["fine_c"].shape[0] == kf else None
@@ -1348,7 +1360,7 @@ class TenantGraph:
                 T16, tof = prev["top_c16"], prev["top_of_fine"]
                 fa = lambda Xa, C16: assign_two_level(Xa, C16, T16, tof)  # noqa: E731
             fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp,
-                                     full_assign=fa)
+                                     full_assign=fa, comm=comm if dist else None)
             init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
             tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
             lab = lab.long()
@@ -1362,7 +1374,7 @@ class TenantGraph:
             self.hier = {"fine_c": fc32, "top_c": tc32, "fine": lab.to(torch.int32), "top": top.to(torch.int32),
                          "perm": perm, "start": start, "n": n, "version": self.version,
                          "top_c16": tc16, "top_of_fine": top_of_fine}
-        return {"fine": kf, "top": kt, "rows": n_live}
+        return {"fine": kf, "top": kt, "rows": n_glob}
 
     def hier_children(self, q: torch.Tensor, threshold: float, limit: int) -> List[int]:
         """Hierarchical retrieval over the k-means topics (the reference's

@@ -1,0 +1,824 @@
+"""One tenant's memory row-sharded over the ranks of a job (BASELINE config 4:
+a 100M-node episodic buffer across the GPUs of a node; SURVEY.md §2.6
+"Row-sharded index", §2.5 C1/C3/C4/C5).
+
+:class:`ShardedMemorySystem` keeps the tenant's rows split over the ranks --
+each rank's part is an ordinary :class:`~lazzaro_amd.core.MemorySystem` graph
+(HBM columns, HIP kernels, incremental persistence under the tenant id
+``"{user}@{rank}/{world}"``) -- and runs the reference's consolidation over
+the WHOLE buffer with the sequential semantics of the single-process engine:
+``consolidate_batch`` on N ranks gives the nodes, saliences, edges and
+eviction victims that ``MemorySystem.consolidate_batch`` gives on one process
+holding the union of the rows and all ranks' conversations (rank-major
+order). Reference flow: ``memory_system.py:580-649`` (end_conversation),
+``:651-891`` (dedupe, links), ``:535-578`` (eviction), ``:935-1010``
+(run_consolidation).
+
+Per batch (every call is collective; each rank brings its own conversations):
+
+1. fact rows (vector, salience, conversation, shard key) are all-gathered
+   (C1, F x (4 D + 24) bytes): dedupe and linking compare every fact with
+   every row of the tenant, so each rank scans ALL facts against ITS rows --
+   one fused MFMA dual scan (global + same-shard top-3, float64 re-rank);
+2. the per-rank top-3 lists (score, global node number, shard, owner row)
+   are all-gathered and merged (K2) -- ties break on the global node number,
+   the single-process row order;
+3. the in-batch dedupe fixed point and the link plan
+   (:func:`~lazzaro_amd.core.consolidation.batch_link_plan`) run replicated on
+   the merged lists (F x F, identical on every rank), so every rank knows
+   every decision without a further exchange;
+4. each rank applies what it owns: decay + prune of its edges (one
+   ``tg_decay_kernel`` pass), duplicate merges onto its rows, inserts of the
+   kept facts of its own conversations (node ids ``node_<n>`` numbered
+   globally in batch order), and the new edges whose source it holds; an
+   edge to a node held elsewhere points at a ghost row carrying the remote
+   node's id and shard (the reference's dangling-edge semantics do the rest);
+5. eviction to the GLOBAL ``max_buffer_size``: each rank's ``excess`` lowest
+   (importance, shard, node number) candidates are all-gathered and the same
+   global victims picked everywhere; edges of a victim's shard that point at
+   it are dropped on every rank;
+6. ``run_consolidation``: connected components over every rank's edges by
+   boundary-label exchange (:func:`~.sharded.distributed_components`, C5),
+   component sizes / mean weights / first members reduced at the label's
+   home rank (all-to-all-v), profile prompts assembled on rank 0;
+7. ``hierarchy_params``: the two-level k-means hierarchy over all rows
+   (distributed fine level, all-reduced centroid sums, C4);
+8. each rank commits its own changed rows / edges (colstore fragment per
+   rank) -- no rank ever writes another's rows.
+
+Per-rank work per batch is (all facts) x (own rows): at a fixed buffer the
+scan is split N ways (strong scaling of the buffer); the exchanged bytes are
+O(facts), never O(rows).
+
+Not supported for a row-sharded tenant: the reference's per-shard mean
+super-nodes (``hierarchy_mode="reference"``: a shard's members span ranks;
+the k-means hierarchy replaces them) and ``merge_mode="pairwise"``
+(reference default is the no-op).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..core.consolidation import (DECAY_RATE, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS, batch_dedupe,
+                                  batch_link_plan, salience_decayed)
+from ..engine.tenant_graph import GHOST, NODE
+from ..ops import tenant_ops as T
+from ..utils.tracing import tracer
+from .comm import Communicator
+from .sharded import _route, distributed_components
+
+NEG_INF = float("-inf")
+BIG = 1 << 62
+NUM_BITS = 40  # global node numbers < 2^40; (shard + 1) << 40 | number orders nodes as the reference does
+
+
+def shard_user_id(user: str, rank: int, world: int) -> str:
+    return f"{user}@{rank}/{world}"
+
+
+class ShardedMemorySystem:
+    """A tenant whose rows are split over ``comm``'s ranks (see module doc).
+
+    ``local_kwargs`` go to each rank's :class:`MemorySystem` (providers,
+    ``db_dir``, ``store``, ``device``...). ``max_buffer_size`` is the GLOBAL
+    node limit. ``hierarchy_params`` ({"fine", "top", "every", "iters"})
+    turns on the distributed k-means hierarchy, re-clustered whenever the
+    global conversation count crosses a multiple of ``every``."""
+
+    def __init__(self, comm: Optional[Communicator] = None, user_id: str = "default", *,
+                 max_buffer_size: int = 10, consolidate_every: int = 3, auto_consolidate: bool = True,
+                 auto_prune: bool = True, prune_threshold: float = 0.5,
+                 hierarchy_params: Optional[Dict] = None, **local_kwargs):
+        from ..core.memory_system import MemorySystem
+
+        self.comm = comm or Communicator.local()
+        self.user_id = user_id
+        self.max_buffer_size = int(max_buffer_size)
+        self.consolidate_every = int(consolidate_every)
+        self.auto_consolidate = auto_consolidate
+        self.auto_prune = auto_prune
+        self.prune_threshold = float(prune_threshold)
+        self.hierarchy_params = dict(hierarchy_params) if hierarchy_params else None
+        local_kwargs.setdefault("enable_async", False)
+        local_kwargs.setdefault("load_from_disk", False)
+        local_kwargs.setdefault("enable_caching", False)
+        self.local = MemorySystem(user_id=shard_user_id(user_id, self.comm.rank, self.comm.world),
+                                  max_buffer_size=1 << 62, auto_consolidate=False, enable_hierarchy=False,
+                                  auto_prune=auto_prune, prune_threshold=prune_threshold, **local_kwargs)
+        self.g = self.local.graph
+        self.device = self.g.device
+        self.num = torch.full((0,), -1, dtype=torch.long, device=self.device)  # global node number per row
+        # rank holding each row's node (a ghost row: the remote holder)
+        self.holder = torch.full((0,), -1, dtype=torch.long, device=self.device)
+        self.next_id = 0  # last global node number handed out (identical on every rank)
+        self.conversation_count = 0
+
+    # ------------------------------------------------------------------ plumbing
+    @property
+    def rank(self) -> int:
+        return self.comm.rank
+
+    @property
+    def world(self) -> int:
+        return self.comm.world
+
+    def _to_comm(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to(self.comm.device) if self.world > 1 else t
+
+    def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Equal-shaped tensors of every rank, concatenated in rank order."""
+        if self.world == 1:
+            return t
+        return self.comm.all_gather_rows(self._to_comm(t.contiguous())).to(t.device)
+
+    def _gather_var(self, t: torch.Tensor) -> Tuple[torch.Tensor, List[int]]:
+        """Variable-length rows of every rank in rank order (+ per-rank counts)."""
+        if self.world == 1:
+            return t, [int(t.shape[0])]
+        cnt = self._gather_rows(torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)).tolist()
+        mx = max(cnt)
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        g = self._gather_rows(pad)
+        idx = torch.cat([torch.arange(r * mx, r * mx + c) for r, c in enumerate(cnt)]).to(t.device)
+        return g[idx], cnt
+
+    def _sum(self, *vals) -> List[int]:
+        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)
+        if self.world > 1:
+            t = self.comm.all_reduce(self._to_comm(t)).to(self.device)
+        return [int(x) for x in t.tolist()]
+
+    def _sync_num(self) -> None:
+        n = self.g.n
+        if self.num.numel() < n:
+            grow = torch.full((max(n, 2 * self.num.numel()) - self.num.numel(),), -1, dtype=torch.long,
+                              device=self.device)
+            self.num = torch.cat([self.num, grow])
+            self.holder = torch.cat([self.holder, grow.clone()])
+
+    def _rows_of_nums(self, nums: torch.Tensor) -> torch.Tensor:
+        """Local row holding each global node number (live or ghost), -1 if
+        none: one sort of the number column + a binary search (no host map)."""
+        n = self.g.n
+        if n == 0 or nums.numel() == 0:
+            return torch.full_like(nums, -1)
+        key = self.num[:n]
+        o = torch.argsort(key)
+        ks = key[o]
+        pos = torch.searchsorted(ks, nums).clamp_max(n - 1)
+        return torch.where(ks[pos] == nums, o[pos], torch.full_like(nums, -1))
+
+    def _register_shards(self, keys: Sequence[str]) -> np.ndarray:
+        return np.asarray([self.g.shard_id(k) for k in keys], dtype=np.int32)
+
+    # ------------------------------------------------------------------ loading
+    def register_shards(self, names: Sequence[str]) -> List[int]:
+        """Create shards in this order on every rank (call with the same list
+        everywhere) so raw shard codes can be passed to :meth:`add_memories`."""
+        return self._register_shards(names).tolist()
+
+    def add_memories(self, contents: Sequence[str], vectors: torch.Tensor, shard_keys: Optional[Sequence[str]] = None,
+                     salience=0.5, now: Optional[float] = None, types="semantic", shard_codes=None) -> torch.Tensor:
+        """Collective bulk insert of already-extracted memories (a tenant load
+        or a migration): every rank passes its own rows; they get global node
+        numbers in rank-major order and stay on the rank that passed them.
+        ``shard_keys`` are registered in that global order on every rank so the
+        shard codes agree everywhere; ``shard_codes`` (codes of shards created
+        by :meth:`register_shards`) skip that exchange for bulk loads.
+        Returns this rank's new rows."""
+        m = len(contents)
+        if shard_codes is None:
+            keys_all = [k for ks in self.comm.all_gather_object(list(shard_keys)) for k in ks] \
+                if self.world > 1 else list(shard_keys)
+        counts = self._gather_rows(torch.tensor([m], dtype=torch.int64, device=self.device)).tolist()
+        off = sum(counts[: self.rank])
+        codes = self._register_shards(keys_all)[off: off + m] if shard_codes is None else shard_codes
+        base = self.next_id
+        self.next_id += sum(counts)
+        if m == 0:
+            return torch.zeros(0, dtype=torch.long, device=self.device)
+        nums = torch.arange(base + off + 1, base + off + m + 1, dtype=torch.long, device=self.device)
+        ids = [f"node_{i}" for i in range(base + off + 1, base + off + m + 1)]
+        now = time.time() if now is None else now
+        rows = self.g.add_nodes(ids, list(contents), vectors, shard=codes, types=types, sal=salience, now=now,
+                                stored=True)
+        self._sync_num()
+        self.num[rows] = nums
+        self.holder[rows] = self.rank
+        self.local.node_counter = self.next_id
+        return rows
+
+    # ------------------------------------------------------------------ queries
+    def num_nodes(self) -> int:
+        return self._sum(self.g.num_nodes())[0]
+
+    def num_edges(self) -> int:
+        return self._sum(self.g.num_edges)[0]
+
+    def _candidates(self, Q: torch.Tensor, codes: torch.Tensor):
+        """Global (dual) top-3 of every fact over every rank's live nodes:
+        local fused scan, all-gather of the lists, merge by (score desc,
+        node number asc). Returns ((s, num, shard, rank, row) global,
+        (same) same-shard), each s [F, 3] fp64 and ints [F, 3]."""
+        g = self.g
+        F = Q.shape[0]
+        dev = self.device
+        k = LINK_TOPK
+        if g.n and g.num_nodes():
+            n = g.n
+            mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
+            (gs, gr), (ws, wr) = g.cos_topk(Q, k, mask, dual_label=codes)
+        else:
+            gs = ws = torch.full((F, k), NEG_INF, dtype=torch.float64, device=dev)
+            gr = wr = torch.full((F, k), -1, dtype=torch.long, device=dev)
+
+        def pack(s, r):
+            ok = r >= 0
+            rr = r.clamp_min(0)
+            num = torch.where(ok, self.num[rr], torch.full_like(r, -1))
+            sh = torch.where(ok, g.shard[rr].long() if g.n else torch.zeros_like(r), torch.full_like(r, -1))
+            own = torch.where(ok, torch.full_like(r, self.rank), torch.full_like(r, -1))
+            return s, torch.stack([num, sh, own, torch.where(ok, r, torch.full_like(r, -1))], 2)
+
+        out = []
+        for s, r in ((gs, gr), (ws, wr)):
+            s, meta = pack(s, r)
+            if self.world > 1:
+                s = self._gather_rows(s).view(self.world, F, k).permute(1, 0, 2).reshape(F, -1)
+                meta = self._gather_rows(meta).view(self.world, F, k, 4).permute(1, 0, 2, 3).reshape(F, -1, 4)
+                key = torch.where(meta[:, :, 0] >= 0, meta[:, :, 0], torch.full_like(meta[:, :, 0], BIG))
+                o = torch.argsort(key, dim=1, stable=True)
+                s = torch.gather(s, 1, o)
+                meta = torch.gather(meta, 1, o[:, :, None].expand(-1, -1, 4))
+                o = torch.sort(s, dim=1, descending=True, stable=True).indices[:, :k]
+                s = torch.gather(s, 1, o)
+                meta = torch.gather(meta, 1, o[:, :, None].expand(-1, -1, 4))
+            out.append((s, meta))
+        return out
+
+    def search_memories_batch(self, queries: Sequence[str], limit: int = 5) -> List[List[Dict]]:
+        """Collective ``search_memories`` over the whole tenant (reference
+        :1460-1472): every rank embeds its own queries, the query rows are
+        all-gathered, each rank runs the store search (fused scan + fp32
+        re-rank, L2) over its rows, the (score, owner, row) lists are merged
+        (ties -> lower node number) and the winners' node dicts are returned
+        to the rank that asked. Returns this rank's results."""
+        g = self.g
+        dev = self.device
+        qs = list(queries)
+        E = self.local._batch_embed_any(qs) if qs else None
+        D = g.dim
+        E = (E.to(dev, torch.float32) if torch.is_tensor(E) else
+             torch.as_tensor(np.asarray(E, np.float32)).to(dev)) if qs else torch.zeros((0, D), device=dev)
+        Qa, qcnt = self._gather_var(E)
+        nq = Qa.shape[0]
+        if nq == 0:
+            return [[] for _ in qs]
+        if g.n and g.num_nodes():
+            sc, rows = g.store_search(Qa.float(), limit, self.local.vector_store.metric)
+            sc, rows = sc.to(dev).double(), rows.to(dev).long()
+            ok = rows >= 0
+            sc = torch.where(ok, sc, torch.full_like(sc, NEG_INF))
+            num = torch.where(ok, self.num[rows.clamp_min(0)], torch.full_like(rows, -1))
+        else:
+            sc = torch.full((nq, limit), NEG_INF, dtype=torch.float64, device=dev)
+            rows = num = torch.full((nq, limit), -1, dtype=torch.long, device=dev)
+        meta = torch.stack([num, torch.where(num >= 0, torch.full_like(num, self.rank), num), rows], 2)
+        if self.world > 1:
+            sc = self._gather_rows(sc).view(self.world, nq, limit).permute(1, 0, 2).reshape(nq, -1)
+            meta = self._gather_rows(meta).view(self.world, nq, limit, 3).permute(1, 0, 2, 3).reshape(nq, -1, 3)
+            key = torch.where(meta[:, :, 0] >= 0, meta[:, :, 0], torch.full_like(meta[:, :, 0], BIG))
+            o = torch.argsort(key, dim=1, stable=True)
+            sc, meta = torch.gather(sc, 1, o), torch.gather(meta, 1, o[:, :, None].expand(-1, -1, 3))
+            o = torch.sort(sc, dim=1, descending=True, stable=True).indices[:, :limit]
+            sc, meta = torch.gather(sc, 1, o), torch.gather(meta, 1, o[:, :, None].expand(-1, -1, 3))
+        mh = meta.cpu().numpy()
+        sh = sc.cpu().numpy()
+        # the node dicts of the winners this rank holds, sent to the asking rank
+        qoff = np.cumsum([0] + qcnt)
+        mine = {}
+        for q in range(nq):
+            for j in range(limit):
+                if mh[q, j, 0] >= 0 and mh[q, j, 1] == self.rank and np.isfinite(sh[q, j]):
+                    mine[(q, j)] = self._node_dict(int(mh[q, j, 2]))
+        parts = self.comm.all_gather_object(mine) if self.world > 1 else [mine]
+        got = {}
+        for p in parts:
+            got.update(p)
+        q0 = int(qoff[self.rank])
+        return [[got[(q0 + i, j)] for j in range(limit) if (q0 + i, j) in got] for i in range(len(qs))]
+
+    def _node_dict(self, r: int) -> Dict:
+        g = self.g
+        with g.on_stream():
+            sal, acc, last, ts, sh = (float(g.sal[r]), int(g.acc[r]), float(g.last[r]), float(g.ts[r]),
+                                      int(g.shard[r]))
+        return {"id": g.ids[r], "content": g.content[r], "type": g.types[r], "salience": sal,
+                "access_count": acc, "last_accessed": last, "timestamp": ts,
+                "shard_key": g.shard_names[sh] if 0 <= sh < len(g.shard_names) else None}
+
+    # ------------------------------------------------------------------ consolidation
+    def consolidate_batch(self, conversations: Sequence[Sequence[Dict]], embeddings=None,
+                          now: Optional[float] = None) -> Dict[str, int]:
+        """Collective batched ``end_conversation`` (see module doc). Each rank
+        passes its own finished conversations' extracted facts (and optionally
+        their vectors, aligned with the flattened facts). Returns the counts of
+        the WHOLE batch (identical on every rank)."""
+        g = self.g
+        dev = self.device
+        flat, conv, idx = [], [], []
+        j = 0
+        for c, fs in enumerate(conversations):
+            for f in fs:
+                if isinstance(f, dict) and f.get("content") and len(f["content"]) >= MIN_FACT_LEN:
+                    flat.append(f)
+                    conv.append(c)
+                    idx.append(j)
+                j += 1
+        # the batch clock: one `now` for every rank (rank 0's)
+        t_now = torch.tensor([time.time() if now is None else now], dtype=torch.float64, device=dev)
+        if self.world > 1:
+            t_now = self.comm.broadcast(self._to_comm(t_now), 0).to(dev)
+        now = float(t_now.item())
+        m = len(flat)
+        if embeddings is not None and m:
+            E = embeddings if torch.is_tensor(embeddings) else torch.as_tensor(np.asarray(embeddings, np.float32))
+            E = E[torch.as_tensor(idx, dtype=torch.long).to(E.device)] if len(idx) != len(E) else E
+        elif m:
+            with tracer.stage("embed_facts", dev):
+                E = self.local._batch_embed_any([f["content"] for f in flat])
+        else:
+            E = None
+        if m:
+            E, valid = self.local._fact_matrix(E, m)
+            vidx = np.nonzero(valid)[0]
+            flat = [flat[i] for i in vidx]
+            conv = [conv[i] for i in vidx]
+            E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)].to(dev, torch.float32)
+            m = len(flat)
+        if g.dim is None and E is not None and E.shape[1]:
+            g._set_dim(E.shape[1])
+        D = g.dim or 0
+        if E is None:
+            E = torch.zeros((0, D), dtype=torch.float32, device=dev)
+        B_loc = len(conversations)
+        stats = {"conversations": 0, "facts": 0, "dup": 0, "inserted": 0, "linked": 0, "cross_links": 0,
+                 "pruned": 0, "evicted": 0}
+        with self.local._graph_lock, tracer.stage("sharded_consolidate", dev):
+            self._consolidate(flat, conv, E, B_loc, now, stats)
+            self._evict(now, stats)
+            c0 = self.conversation_count
+            self.conversation_count += stats["conversations"]
+            if self.auto_consolidate and (self.conversation_count // self.consolidate_every
+                                          > c0 // self.consolidate_every):
+                with tracer.stage("run_consolidation", dev):
+                    self.run_consolidation()
+            hp = self.hierarchy_params
+            if hp and (self.conversation_count // hp["every"] > c0 // hp["every"]
+                       or getattr(g, "hier", None) is None):
+                with tracer.stage("cluster", dev):
+                    self.cluster_pass()
+            self.local.node_counter = self.next_id
+            with tracer.stage("persist", "cpu"):
+                self.local._save_to_persistence()
+        return stats
+
+    def _consolidate(self, flat, conv, E, B_loc, now, stats) -> None:
+        g = self.g
+        dev = self.device
+        comm = self.comm
+        keep = 1.0 - DECAY_RATE
+        thr = self.prune_threshold if self.auto_prune else None
+        m = len(flat)
+        # ---- 1. the global fact batch (rank-major conversation order)
+        with tracer.stage("sc_gather", dev):
+            bl = self._gather_rows(torch.tensor([B_loc], dtype=torch.int64, device=dev)).tolist()
+            B = int(sum(bl))
+            c_off = int(sum(bl[: self.rank]))
+            keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
+            keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self.world > 1 else keys
+            sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float64, device=dev)
+            ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
+            Qa, fcnt = self._gather_var(E)
+            sal_in, _ = self._gather_var(sal_l)
+            ct, _ = self._gather_var(ct_l)
+        stats["conversations"] = B
+        F = int(Qa.shape[0])
+        stats["facts"] = F
+        if F == 0:
+            stats["pruned"] += self._sum(g.decay(1.0 - keep ** B, thr))[0]
+            return
+        f_off = int(sum(fcnt[: self.rank]))
+        origin = torch.repeat_interleave(torch.arange(self.world, device=dev),
+                                         torch.tensor(fcnt, dtype=torch.long, device=dev))
+        codes = self._register_shards(keys_all)
+        code_t = torch.as_tensor(codes).to(dev)
+        Q = Qa.float()
+        Qd = Q.double()
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+
+        # ---- 2. every fact against every rank's rows: local dual scan + merge
+        with tracer.stage("sc_scan", dev), g.on_stream():
+            (gs, gm), (ws, wm) = self._candidates(Q, code_t)
+        gb_s = gs[:, 0]
+        gb_node = gm[:, 0, 0] >= 0
+
+        # ---- 3. replicated decisions
+        with tracer.stage("sc_dedupe", dev):
+            S, earlier, dup, batch_best, bb_i, ins = batch_dedupe(Qn, ct, gb_s, gb_node)
+        dup_graph = dup & ~batch_best
+        dup_batch = dup & batch_best
+        sal_dec = salience_decayed(sal_in, (B - ct).double(), keep)
+
+        # ---- 4. decay + prune this rank's edges / node saliences by B conversations
+        with tracer.stage("sc_decay", dev):
+            stats["pruned"] += self._sum(g.decay(1.0 - keep ** B, thr))[0]
+
+        # ---- 5. duplicate merges onto the rows this rank holds
+        stats["dup"] += int(dup.sum())
+        mine_dup = dup_graph & (gm[:, 0, 2] == self.rank)
+        if bool(mine_dup.any()):
+            rows = gm[:, 0, 3][mine_dup]
+            with g.on_stream():
+                g.sal.scatter_reduce_(0, rows, sal_dec[mine_dup].float(), "amax", include_self=True)
+                g.last[rows] = now
+                g.acc.index_add_(0, rows, torch.ones_like(rows, dtype=torch.int32))
+                g.dirty[rows] = 1
+            g._bump()
+        sal_new = sal_dec.clone()
+        acc_new = torch.zeros(F, dtype=torch.int32, device=dev)
+        if bool(dup_batch.any()):
+            tgt = bb_i[dup_batch]
+            sal_new.scatter_reduce_(0, tgt, sal_dec[dup_batch], "amax", include_self=True)
+            acc_new.index_add_(0, tgt, torch.ones_like(tgt, dtype=torch.int32))
+
+        # ---- 6. inserts: kept facts numbered globally in batch order, each
+        # held by the rank whose conversation it came from
+        kidx = torch.nonzero(ins).flatten()
+        K = int(kidx.numel())
+        if K == 0:
+            return
+        base = self.next_id
+        self.next_id += K
+        stats["inserted"] += K
+        new_num = torch.full((F,), -1, dtype=torch.long, device=dev)
+        new_num[kidx] = torch.arange(base + 1, base + K + 1, dtype=torch.long, device=dev)
+        mk = kidx[origin[kidx] == self.rank]
+        row_of_fact = torch.full((F,), -1, dtype=torch.long, device=dev)
+        if mk.numel():
+            mkh = mk.cpu().numpy()
+            nums_h = new_num[mk].cpu().numpy()
+            lf = [flat[int(i) - f_off] for i in mkh]
+            with tracer.stage("sc_insert", dev):
+                rows = g.add_nodes([f"node_{int(x)}" for x in nums_h], [f["content"] for f in lf], Q[mk],
+                                   shard=codes[mkh], types=[f.get("type", "semantic") for f in lf],
+                                   sal=sal_new[mk].float(), acc=acc_new[mk], now=now, stored=True)
+            self._sync_num()
+            self.num[rows] = new_num[mk]
+            self.holder[rows] = self.rank
+            row_of_fact[mk] = rows.to(dev)
+        if self.local.query_cache:
+            self.local.query_cache.invalidate_results()
+
+        # ---- 7. links (global node numbers), kept where this rank holds the source
+        with tracer.stage("sc_link", dev):
+            plan, _ = batch_link_plan(kidx, new_num, code_t, ct, S, earlier, (ws, wm[:, :, 0]),
+                                      (gs, gm[:, :, 0]), keep, B, thr, stats)
+            if plan is not None:
+                self._apply_edges(plan, new_num, row_of_fact, origin, code_t, (gm, wm), now)
+
+    def _apply_edges(self, plan, new_num, row_of_fact, origin, code_t, hits, now) -> None:
+        """Append the planned edges whose source this rank holds; an endpoint
+        held elsewhere becomes (or reuses) a ghost row with its id and shard."""
+        g = self.g
+        dev = self.device
+        Sn, Dn, W, H = plan
+        base = int(new_num[new_num >= 0].min()) if bool((new_num >= 0).any()) else 0
+        # source = a new node: its fact position = kept index
+        kept = torch.nonzero(new_num >= 0).flatten()
+        src_fact = kept[Sn - base]
+        mine = origin[src_fact] == self.rank
+        if not bool(mine.any()):
+            return
+        src_fact, Dn, W, H = src_fact[mine], Dn[mine], W[mine], H[mine]
+        src_rows = row_of_fact[src_fact]
+        # destination: a new node of this batch (its fact tells the holder and
+        # shard) or an existing node from the merged candidate lists
+        is_new = Dn >= base
+        dst_rows = torch.full_like(Dn, -1)
+        dst_shard = torch.full_like(Dn, -1)
+        dst_hold = torch.full_like(Dn, -1)
+        dst_fact = kept[(Dn - base).clamp_min(0).clamp_max(max(kept.numel() - 1, 0))]
+        nf = is_new & (origin[dst_fact] == self.rank)
+        dst_rows = torch.where(nf, row_of_fact[dst_fact], dst_rows)
+        dst_shard = torch.where(is_new, code_t[dst_fact].long(), dst_shard)
+        dst_hold = torch.where(is_new, origin[dst_fact], dst_hold)
+        # existing nodes: (number -> shard, holder, row) from the candidate lists
+        metas = torch.cat([h.reshape(-1, 4) for h in hits])
+        metas = metas[metas[:, 0] >= 0]
+        if metas.numel():
+            un, first = np.unique(metas[:, 0].cpu().numpy(), return_index=True)
+            info = metas[torch.as_tensor(first, dtype=torch.long).to(dev)]
+            un_t = torch.as_tensor(un).to(dev)
+            pos = torch.searchsorted(un_t, Dn.clamp_max(int(un[-1])))
+            hit = (~is_new) & (un_t[pos.clamp_max(un_t.numel() - 1)] == Dn)
+            pi = info[pos.clamp_max(un_t.numel() - 1)]
+            dst_shard = torch.where(hit, pi[:, 1], dst_shard)
+            dst_hold = torch.where(hit, pi[:, 2], dst_hold)
+            dst_rows = torch.where(hit & (pi[:, 2] == self.rank), pi[:, 3], dst_rows)
+        # remote endpoints -> ghost rows (created once per id)
+        need = torch.nonzero(dst_rows < 0).flatten()
+        if need.numel():
+            dn_h = Dn[need].cpu().numpy()
+            sh_h = dst_shard[need].cpu().numpy()
+            ho_h = dst_hold[need].cpu().numpy()
+            ids = [f"node_{int(x)}" for x in dn_h]
+            have = [g.row_of.get(i, -1) for i in ids]
+            fresh = {}
+            for i, r, s_, h_ in zip(ids, have, sh_h.tolist(), ho_h.tolist()):
+                if r < 0 and i not in fresh:
+                    fresh[i] = (s_, h_)
+            if fresh:
+                fid = list(fresh)
+                rows_new = g.add_nodes(fid, [""] * len(fid), None, shard=[fresh[i][0] for i in fid], ghost=True,
+                                       stored=False, now=now)
+                self._sync_num()
+                self.num[rows_new] = torch.as_tensor([int(i[5:]) for i in fid], dtype=torch.long).to(dev)
+                self.holder[rows_new] = torch.as_tensor([fresh[i][1] for i in fid], dtype=torch.long).to(dev)
+            rr = torch.as_tensor([g.row_of[i] for i in ids], dtype=torch.long).to(dev)
+            dst_rows[need] = rr
+        g.append_edges(src_rows, dst_rows, W.float(), H.to(torch.int32), g.etype("relates_to"), now=now)
+
+    # ------------------------------------------------------------------ eviction
+    def _evict(self, now: float, stats: Dict[str, int]) -> None:
+        """Global buffer limit (reference :535-578 over the whole tenant)."""
+        g = self.g
+        dev = self.device
+        total = self._sum(g.num_nodes())[0]
+        excess = total - self.max_buffer_size
+        if excess <= 0:
+            return
+        with tracer.stage("sc_evict", dev):
+            n = g.n
+            m = min(excess, n)
+            cand_s = torch.full((excess,), float("inf"), dtype=torch.float64, device=dev)
+            cand_k = torch.full((excess,), BIG, dtype=torch.long, device=dev)
+            cand_r = torch.full((excess,), -1, dtype=torch.long, device=dev)
+            if m:
+                with g.on_stream():
+                    score = T.importance(g.sal[:n], g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now)
+                    okey = (g.shard[:n].long() + 1) * (1 << NUM_BITS) + self.num[:n]
+                    # this rank's m lowest (score, shard, number): a top-k for the
+                    # threshold, then the tied rows by key (no full sort)
+                    t = torch.topk(score, m, largest=False, sorted=False).values.max()
+                    lt = torch.nonzero(score < t).flatten()
+                    rest = m - int(lt.numel())
+                    tie = torch.where(score == t, okey, torch.full_like(okey, BIG))
+                    tv, ti = torch.topk(tie, rest, largest=False, sorted=True) if rest > 0 else (tie[:0], lt[:0])
+                    cand = torch.cat([lt, ti[tv != BIG]])
+                    cand = cand[torch.isfinite(score[cand])]
+                    c = int(cand.numel())
+                    cand_s[:c] = score[cand]
+                    cand_k[:c] = okey[cand]
+                    cand_r[:c] = cand
+            alls = self._gather_rows(cand_s)
+            allk = self._gather_rows(cand_k)
+            o = torch.argsort(allk, stable=True)
+            o = o[torch.sort(alls[o], stable=True).indices][:excess]
+            o = o[torch.isfinite(alls[o])]
+            stats["evicted"] += int(o.numel())
+            if o.numel() == 0:
+                return
+            owner = o // excess
+            pos = o % excess
+            mine = cand_r[pos[owner == self.rank]]
+            victims = mine.tolist()
+            if victims:
+                g.remove_nodes(victims, drop_edges=True, unstore=True)
+                self.local._store_delete([g.ids[r] for r in victims])
+            # edges held here that point at a victim held elsewhere: the
+            # victim's shard drops them (its ghost row carries that shard)
+            other = allk[o[owner != self.rank]] & ((1 << NUM_BITS) - 1)
+            if other.numel() and g.num_edges:
+                rows = self._rows_of_nums(other)
+                rows = rows[rows >= 0]
+                if rows.numel():
+                    with g.on_stream():
+                        rm = torch.zeros(g.n, dtype=torch.uint8, device=dev)
+                        rm[rows] = 1
+                        g.e, k, dropped = T.remove_edges_of(g.e, rm, g.shard[: g.n], want_dropped=g.track)
+                    if dropped is not None and k:
+                        g._note_dropped(*dropped)
+                    g._bump(edges=True)
+
+    # ------------------------------------------------------------------ deep consolidation
+    def component_digest(self, min_size: int = 3, min_avg_w: float = 0.3,
+                         take: int = PROFILE_CONTENTS) -> List[List[str]]:
+        """``run_consolidation``'s component view of the WHOLE tenant
+        (reference :967-990; single-process ``TenantGraph.component_digest``):
+        components over every rank's edges with >= ``min_size`` members and
+        mean edge weight > ``min_avg_w``, ordered by their first member in the
+        reference node order, each as the contents of its first ``take`` live
+        nodes. Collective; rank 0 gets the list, the others []."""
+        g = self.g
+        dev = self.device
+        W = self.world
+        n = g.n
+        if n and g.num_edges:
+            s_num = self.num[g.e["src"].long()]
+            d_num = self.num[g.e["dst"].long()]
+            w = g.e["w"].double()
+        else:
+            s_num = d_num = torch.zeros(0, dtype=torch.long, device=dev)
+            w = torch.zeros(0, dtype=torch.float64, device=dev)
+        cdev = self.comm.device if W > 1 else dev
+        verts, lab = distributed_components(self.comm, s_num.to(cdev), d_num.to(cdev))
+        verts, lab = verts.to(dev), lab.to(dev)
+
+        def home(t):
+            return (t % W) if W > 1 else torch.zeros_like(t)
+
+        def route(dest, rows):
+            if W == 1:
+                return rows
+            got, _ = _route(self.comm, dest.to(cdev), rows.to(cdev))
+            return got.to(dev)
+
+        # members: every distinct vertex (live node or ghost endpoint), counted at its home rank
+        got = route(home(verts), torch.stack([verts, lab], 1))
+        if got.numel():
+            uv, first = np.unique(got[:, 0].cpu().numpy(), return_index=True)
+            vl = got[torch.as_tensor(first, dtype=torch.long).to(dev), 1]
+            ul, cnt = torch.unique(vl, return_counts=True)
+            part_size = torch.stack([ul, cnt], 1)
+        else:
+            part_size = torch.zeros((0, 2), dtype=torch.long, device=dev)
+        # edge weight sums by the source's label; first member key by live nodes
+        if s_num.numel():
+            el = lab[torch.searchsorted(verts, s_num)]
+            ul, inv = torch.unique(el, return_inverse=True)
+            ws = torch.zeros(ul.numel(), dtype=torch.float64, device=dev).index_add_(0, inv, w)
+            wc = torch.bincount(inv, minlength=ul.numel()).double()
+            part_w = torch.stack([ul.double(), ws, wc], 1)
+        else:
+            part_w = torch.zeros((0, 3), dtype=torch.float64, device=dev)
+        # the live nodes this rank holds that any rank's edges touch: a rank
+        # touching a node through a ghost row sends (vertex, label) to the
+        # ghost's holder
+        rows_t = self._rows_of_nums(verts)
+        hold = torch.where(rows_t >= 0, self.holder[rows_t.clamp_min(0)], torch.full_like(rows_t, -1))
+        rem = (hold >= 0) & (hold != self.rank)
+        got = route(hold[rem], torch.stack([verts[rem], lab[rem]], 1)) if W > 1 else \
+            torch.zeros((0, 2), dtype=torch.long, device=dev)
+        if got.numel():
+            vv = torch.cat([verts[~rem], got[:, 0]])
+            ll = torch.cat([lab[~rem], got[:, 1]])
+            vv, o = torch.unique(vv, return_inverse=True)
+            verts, lab = vv, torch.zeros_like(vv).scatter_(0, o, ll)
+        else:
+            verts, lab = verts[~rem], lab[~rem]
+        if verts.numel():
+            rows_l = self._rows_of_nums(verts)
+            okr = rows_l >= 0
+            rr = rows_l.clamp_min(0)
+            live = okr & (g.kind[rr] == NODE) & (g.sup[rr] == 0)
+            key = (g.shard[rr].long() + 1) * (1 << NUM_BITS) + verts
+            lv = torch.nonzero(live).flatten()
+            ul, inv = torch.unique(lab[lv], return_inverse=True)
+            fk = torch.full((ul.numel(),), BIG, dtype=torch.long, device=dev).scatter_reduce_(0, inv, key[lv], "amin")
+            part_f = torch.stack([ul, fk], 1)
+        else:
+            lv = torch.zeros(0, dtype=torch.long, device=dev)
+            rows_l = key = torch.zeros(0, dtype=torch.long, device=dev)
+            part_f = torch.zeros((0, 2), dtype=torch.long, device=dev)
+        ps = route(home(part_size[:, 0]), part_size)
+        pw = route(home(part_w[:, 0].long()), part_w)
+        pf = route(home(part_f[:, 0]), part_f)
+        labels = torch.unique(torch.cat([ps[:, 0], pw[:, 0].long(), pf[:, 0]]))
+        qual = torch.zeros((0, 2), dtype=torch.long, device=dev)
+        if labels.numel():
+            L = labels.numel()
+            size = torch.zeros(L, dtype=torch.long, device=dev).index_add_(0, torch.searchsorted(labels, ps[:, 0].contiguous()),
+                                                                           ps[:, 1])
+            wi = torch.searchsorted(labels, pw[:, 0].long())
+            wsum = torch.zeros(L, dtype=torch.float64, device=dev).index_add_(0, wi, pw[:, 1])
+            wcnt = torch.zeros(L, dtype=torch.float64, device=dev).index_add_(0, wi, pw[:, 2])
+            fst = torch.full((L,), BIG, dtype=torch.long, device=dev).scatter_reduce_(
+                0, torch.searchsorted(labels, pf[:, 0].contiguous()), pf[:, 1], "amin")
+            ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1) > min_avg_w) & (fst < BIG)
+            qual = torch.stack([labels[ok], fst[ok]], 1)
+        qual, _ = self._gather_var(qual)  # every qualifying (label, first key), replicated
+        if qual.numel() == 0:
+            return []
+        # each rank's first `take` live members (node-number order) per qualifying component
+        mine = []
+        if lv.numel():
+            ql = qual[:, 0]
+            o = torch.argsort(ql)
+            ql_s, qf_s = ql[o], qual[o, 1]
+            li = torch.searchsorted(ql_s, lab[lv]).clamp_max(ql_s.numel() - 1)
+            inq = ql_s[li] == lab[lv]
+            sel = lv[inq]
+            if sel.numel():
+                fk = qf_s[li[inq]]
+                vn = verts[sel]
+                oo = torch.argsort(vn)
+                oo = oo[torch.sort(fk[oo], stable=True).indices]
+                fk, vn, rsel = fk[oo], vn[oo], rows_l[sel][oo]
+                newg = torch.ones_like(fk, dtype=torch.bool)
+                newg[1:] = fk[1:] != fk[:-1]
+                gstart = torch.nonzero(newg).flatten()[torch.cumsum(newg.long(), 0) - 1]
+                rank_in = torch.arange(fk.numel(), device=dev) - gstart
+                keepm = rank_in < take
+                for f_, v_, r_ in zip(fk[keepm].tolist(), vn[keepm].tolist(), rsel[keepm].tolist()):
+                    mine.append((f_, v_, g.content[r_]))
+        parts = self.comm.all_gather_object(mine) if W > 1 else [mine]
+        if self.rank != 0:
+            return []
+        allm = sorted(x for p in parts for x in p)
+        out: List[List[str]] = []
+        last = None
+        for f_, _, c in allm:
+            if f_ != last:
+                out.append([])
+                last = f_
+            if len(out[-1]) < take:
+                out[-1].append(c)
+        return out
+
+    def _first_contents(self, take: int = PROFILE_CONTENTS) -> List[str]:
+        """Contents of the tenant's first ``take`` live nodes in the reference
+        node order (shard creation order, then insertion). Rank 0 gets them."""
+        g = self.g
+        n = g.n
+        mine = []
+        if n:
+            with g.on_stream():
+                live = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
+                key = torch.where(live, (g.shard[:n].long() + 1) * (1 << NUM_BITS) + self.num[:n],
+                                  torch.full((n,), BIG, dtype=torch.long, device=self.device))
+                k = min(take, n)
+                v, r = torch.topk(key, k, largest=False, sorted=True)
+                r = r[v < BIG]
+                mine = [(int(key[x]), g.content[x]) for x in r.tolist()]
+        parts = self.comm.all_gather_object(mine) if self.world > 1 else [mine]
+        return [c for _, c in sorted(x for p in parts for x in p)[:take]] if self.rank == 0 else []
+
+    def run_consolidation(self) -> str:
+        """Collective deep consolidation (reference :935-1010) over the whole
+        tenant: component digest (distributed CC), profile extraction on rank 0
+        (the tenant's profile is broadcast afterwards), prune of every rank's
+        weak edges. The reference's merge step is its no-op default."""
+        ms = self.local
+        results = []
+        with tracer.stage("components", self.device):
+            digest = self.component_digest(3, 0.3, PROFILE_CONTENTS)
+        updates = 0
+        for cs in digest:
+            r = ms._extract_profile_from_contents(cs)
+            if "Updated" in r:
+                updates += 1
+                results.append(r)
+        pruned = self._sum(self.g.prune(self.prune_threshold))[0]
+        if pruned > 0:
+            results.append(f"✓ Pruned {pruned} weak edges")
+        upd = self._sum(updates)[0]
+        if upd > 0:
+            results.append(f"✓ Updated {upd} profile domains")
+        else:
+            contents = self._first_contents(PROFILE_CONTENTS)
+            if self.rank == 0 and len(contents) >= 3:
+                r = ms._extract_profile_from_contents(contents)
+                if "Updated" in r:
+                    results.append(r)
+        if self.world > 1:
+            prof = self.comm.all_gather_object(dict(ms.profile.data) if self.rank == 0 else None)[0]
+            for k, v in prof.items():
+                if ms.profile.data.get(k) != v:
+                    ms.profile.update_domain(k, v)
+        if not results:
+            results.append("✓ No consolidation actions needed")
+        return "\n".join(results)
+
+    def cluster_pass(self) -> Dict:
+        hp = self.hierarchy_params or {"fine": 4096, "top": 64, "iters": 2}
+        return self.g.cluster_pass(hp["fine"], hp["top"], hp["iters"], comm=self.comm if self.world > 1 else None)
+
+    @property
+    def profile(self):
+        return self.local.profile
+
+    def get_stats(self) -> Dict:
+        nodes, edges = self._sum(self.g.num_nodes(), self.g.num_edges)
+        return {"user_id": self.user_id, "ranks": self.world, "total_nodes": nodes, "total_edges": edges,
+                "local_nodes": self.g.num_nodes(), "local_edges": self.g.num_edges,
+                "conversations": self.conversation_count, "next_node_id": self.next_id}
+
+    def close(self) -> None:
+        self.local.close()

@@ -1,0 +1,224 @@
+"""Row-sharded tenant (lazzaro_amd/parallel/sharded_memory.py) on CPU with
+gloo: ONE tenant's buffer split over 1, 2 and 3 ranks, consolidated batch by
+batch, ends in exactly the state a single-process ``MemorySystem`` reaches on
+the union of the rows and all ranks' conversations -- the same node ids,
+saliences and access counts, the same edges and weights, the same eviction
+victims and per-batch counts, the same component digest and profile.
+
+Data: clustered unit vectors (so links clear the 0.5 threshold), facts that
+are near-duplicates of stored memories, related memories or new, a buffer
+limit that forces eviction every batch, distinct saliences (no importance
+ties), and a shard first seen mid-run."""
+import functools
+import math
+import random
+
+import pytest
+import torch
+
+from tests.distributed.test_dist_gloo import spawn
+
+DIM = 32
+ROWS = 180
+LIMIT = 200
+STEPS = 4
+CONVS = 12
+TOPICS = ["work", "personal", "learning"]
+QUERIES = ["fact about work", "memory 12", "learning something new", "health and sleep", "personal", "memory 7 x"]
+
+
+def _unit(x):
+    return x / x.norm(dim=-1, keepdim=True)
+
+
+CPU = {"rows": ROWS, "dim": DIM, "limit": LIMIT, "steps": STEPS, "convs": CONVS, "device": "cpu"}
+
+
+def _data(cfg=CPU):
+    """Union rows + per-step global conversation lists (deterministic)."""
+    ROWS, DIM, STEPS, CONVS = cfg["rows"], cfg["dim"], cfg["steps"], cfg["convs"]
+    noise = 0.18 * (32 / DIM) ** 0.5 * 1.0
+    g = torch.Generator().manual_seed(5)
+    centers = _unit(torch.randn(8, DIM, generator=g))
+    lab = torch.randint(0, 8, (ROWS,), generator=g)
+    X = _unit(centers[lab] + noise * torch.randn(ROWS, DIM, generator=g))
+    rng = random.Random(11)
+    sal0 = [round(rng.uniform(0.3, 0.95), 6) for _ in range(ROWS)]
+    keys0 = [TOPICS[i % 3] for i in range(ROWS)]
+    steps = []
+    for s in range(STEPS):
+        convs, vecs = [], []
+        for c in range(CONVS):
+            facts = []
+            for f in range(rng.randint(1, 4)):
+                kind = rng.random()
+                if kind < 0.2:
+                    v = _unit(X[rng.randrange(ROWS)] + noise / 9 * torch.randn(DIM, generator=g))  # duplicate
+                elif kind < 0.3 and vecs:
+                    v = _unit(vecs[rng.randrange(len(vecs))] + noise / 9 * torch.randn(DIM, generator=g))  # in-batch
+                elif kind < 0.8:
+                    v = _unit(centers[rng.randrange(8)] + noise * torch.randn(DIM, generator=g))  # related
+                else:
+                    v = _unit(torch.randn(DIM, generator=g))  # new
+                topic = "health" if (s >= 2 and kind > 0.9) else TOPICS[rng.randrange(3)]
+                facts.append({"content": f"fact {s}.{c}.{f} about {topic}", "type": "semantic",
+                              "salience": round(rng.uniform(0.3, 0.95), 6), "topic": topic})
+                vecs.append(v)
+            convs.append(facts)
+        steps.append((convs, torch.stack(vecs)))
+    return X, sal0, keys0, steps
+
+
+def _split(n, world, r):
+    per = [n // world + (1 if i < n % world else 0) for i in range(world)]
+    lo = sum(per[:r])
+    return lo, lo + per[r]
+
+
+def _graph_state(g):
+    from lazzaro_amd.engine.tenant_graph import NODE
+    n = g.n
+    kind, sal, acc, sh = (g.kind[:n].tolist(), g.sal[:n].tolist(), g.acc[:n].tolist(), g.shard[:n].tolist())
+    nodes = {g.ids[r]: (round(sal[r], 5), acc[r], g.shard_names[sh[r]]) for r in range(n) if kind[r] == NODE}
+    e = g.e
+    edges = {}
+    for s, d, w, m in zip(e["src"].tolist(), e["dst"].tolist(), e["w"].tolist(), e["meta"].tolist()):
+        edges[(g.ids[s], g.ids[d])] = (round(w, 5), g.shard_names[m & 0xFFFFFF])
+    return nodes, edges
+
+
+def _now(s):
+    return 1.7e9 + 3600.0 * s
+
+
+def _single(tmp, cfg=CPU):
+    """The single-process engine on the union."""
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    X, sal0, keys0, steps = _data(cfg)
+    dev = cfg["device"]
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=cfg["dim"]), enable_async=False,
+                      db_dir=tmp, user_id="solo", device=dev, max_buffer_size=cfg["limit"], enable_hierarchy=False,
+                      load_from_disk=False, enable_caching=False)
+    g = ms.graph
+    codes = [g.shard_id(k) for k in keys0]
+    R = cfg["rows"]
+    g.add_nodes([f"node_{i + 1}" for i in range(R)], [f"memory {i + 1}" for i in range(R)], X.to(dev),
+                shard=codes, sal=torch.tensor(sal0), now=_now(-1), stored=True)
+    ms.node_counter = R
+    stats = []
+    for s, (convs, V) in enumerate(steps):
+        import lazzaro_amd.engine.tenant_graph as tgm
+        real = tgm.time.time
+        tgm.time.time = lambda s=s: _now(s)  # the single-process eviction reads the wall clock
+        try:
+            stats.append(ms.consolidate_batch(convs, embeddings=V.to(dev), now=_now(s)))
+        finally:
+            tgm.time.time = real
+    nodes, edges = _graph_state(g)
+    digest = g.component_digest(3, 0.3, 10)
+    contents = [[g.content[r] for r in rows.tolist()] for rows in digest]
+    prof = dict(ms.profile.data)
+    found = [[n.id for n in res] for res in ms.search_memories_batch(QUERIES, 5)]
+    ms.close()
+    return stats, nodes, edges, contents, prof, found
+
+
+def _sharded(comm, cfg=CPU):
+    import tempfile
+
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
+    X, sal0, keys0, steps = _data(cfg)
+    dev = cfg["device"]
+    tmp = tempfile.mkdtemp(prefix=f"lzsh{comm.rank}_")
+    sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
+                             embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev)
+    lo, hi = _split(cfg["rows"], comm.world, comm.rank)
+    sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],
+                    salience=torch.tensor(sal0[lo:hi]), now=_now(-1))
+    stats = []
+    for s, (convs, V) in enumerate(steps):
+        c0, c1 = _split(len(convs), comm.world, comm.rank)
+        f0 = sum(len(c) for c in convs[:c0])
+        f1 = f0 + sum(len(c) for c in convs[c0:c1])
+        stats.append(sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1].to(dev), now=_now(s)))
+    nodes, edges = _graph_state(sm.g)
+    parts = comm.all_gather_object((nodes, edges))
+    contents = sm.component_digest(3, 0.3, 10)
+    prof = dict(sm.profile.data)
+    total = sm.num_nodes()
+    q0, q1 = _split(len(QUERIES), comm.world, comm.rank)
+    found = [[d["id"] for d in res] for res in sm.search_memories_batch(QUERIES[q0:q1], 5)]
+    found = [f for part in comm.all_gather_object(found) for f in part]
+    sm.close()
+    if comm.rank != 0:
+        return {"stats": stats, "prof": prof}
+    nodes_all, edges_all = {}, {}
+    for n_, e_ in parts:
+        assert not (set(n_) & set(nodes_all)), "a node is live on two ranks"
+        nodes_all.update(n_)
+        edges_all.update(e_)
+    single = _single(tempfile.mkdtemp(prefix="lzsolo_"), cfg)
+    return {"stats": stats, "nodes": nodes_all, "edges": edges_all, "contents": contents, "prof": prof,
+            "total": total, "found": found, "single": single}
+
+
+def check_equivalent(out, world, limit):
+    r0 = out[0]
+    s_stats, s_nodes, s_edges, s_contents, s_prof, s_found = r0["single"]
+    assert r0["stats"] == s_stats
+    for r in range(world):  # every rank reports the same whole-batch counts and profile
+        assert out[r]["stats"] == s_stats
+        assert out[r]["prof"] == s_prof
+    assert sum(st["evicted"] for st in s_stats) > 0 and sum(st["dup"] for st in s_stats) > 0
+    assert sum(st["linked"] for st in s_stats) > 0 and s_edges
+    assert r0["nodes"] == s_nodes
+    assert r0["total"] == len(s_nodes) == limit
+    assert set(r0["edges"]) == set(s_edges)
+    for k, (w, sh) in s_edges.items():
+        w2, sh2 = r0["edges"][k]
+        assert sh2 == sh and math.isclose(w, w2, abs_tol=1e-4)
+    assert r0["contents"] == s_contents
+    assert r0["found"] == s_found and all(len(f) == 5 for f in s_found)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_tenant_matches_single_process(world):
+    check_equivalent(spawn(world, _sharded), world, LIMIT)
+
+
+def _sharded_hierarchy(comm):
+    import tempfile
+
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
+    X, sal0, keys0, steps = _data()
+    sm = ShardedMemorySystem(comm, "big", max_buffer_size=LIMIT, llm_provider=LocalLLM(),
+                             embedding_provider=HashEmbedder(dim=DIM), db_dir=tempfile.mkdtemp(), device="cpu",
+                             hierarchy_params={"fine": 16, "top": 4, "every": 12, "iters": 3})
+    lo, hi = _split(ROWS, comm.world, comm.rank)
+    sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi], keys0[lo:hi], now=_now(-1))
+    convs, V = steps[0]
+    c0, c1 = _split(len(convs), comm.world, comm.rank)
+    f0 = sum(len(c) for c in convs[:c0])
+    f1 = f0 + sum(len(c) for c in convs[c0:c1])
+    sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1], now=_now(0))
+    h = sm.g.hier
+    fine = h["fine"][: sm.g.n]
+    n_lab = int((fine >= 0).sum())
+    tot = torch.tensor([n_lab])
+    comm.all_reduce(tot)
+    cents = comm.all_gather_object(h["top_c"].tolist())
+    out = {"labelled": int(tot), "nodes": sm.num_nodes(), "same_centroids": all(c == cents[0] for c in cents),
+           "shape": list(h["fine_c"].shape)}
+    sm.close()
+    return out
+
+
+def test_sharded_hierarchy_distributed_kmeans():
+    out = spawn(2, _sharded_hierarchy)
+    for r in range(2):
+        assert out[r]["same_centroids"]  # the topic level is identical on every rank
+        assert out[r]["labelled"] == out[r]["nodes"]  # every live node of the tenant has a fine cluster
+        assert out[r]["shape"][0] == 16
