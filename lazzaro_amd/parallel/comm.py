@@ -16,6 +16,7 @@ paths call the same API.
 """
 from __future__ import annotations
 
+import json
 import os
 from typing import List, Optional, Sequence, Tuple
 
@@ -132,6 +133,23 @@ class Communicator:
         out = torch.empty((int(sum(recv_counts)),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_to_all_single(out, t.contiguous(), output_split_sizes=list(map(int, recv_counts)),
                                input_split_sizes=list(map(int, send_counts)), group=self.group)
+        return out
+
+    def exchange_objects(self, outgoing: List) -> List:
+        """``outgoing[r]`` = a JSON-able object for rank r -> the objects
+        received, one per source rank (JSON bytes over one all-to-all-v)."""
+        if not self.enabled:
+            return list(outgoing)
+        payload = [json.dumps(x).encode() for x in outgoing]
+        send = torch.tensor([len(p) for p in payload], dtype=torch.int64, device=self.device)
+        recv = self.exchange_counts(send)
+        buf = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if sum(map(len, payload)) else \
+            torch.zeros(0, dtype=torch.uint8)
+        got = self.all_to_all_v(buf.to(self.device), send.tolist(), recv.tolist()).cpu().numpy().tobytes()
+        out, off = [], 0
+        for n in recv.tolist():
+            out.append(json.loads(got[off: off + n].decode()) if n else None)
+            off += n
         return out
 
     def reshard(self, dest: torch.Tensor, *fields: torch.Tensor) -> Tuple[torch.Tensor, ...]:

@@ -28,7 +28,6 @@ All collective methods must be called by every rank in the same order.
 from __future__ import annotations
 
 import inspect
-import json
 from collections import OrderedDict
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -184,21 +183,9 @@ class DistributedMemoryService:
     # ------------------------------------------------------------ request routing
     def _exchange(self, outgoing: List[List]) -> List[List]:
         """outgoing[r] = JSON-able items for rank r -> items received per rank."""
-        comm = self.comm
-        if comm.world == 1:
+        if self.comm.world == 1:
             return outgoing
-        payload = [json.dumps(x).encode() for x in outgoing]
-        dev = comm.device
-        send = torch.tensor([len(p) for p in payload], dtype=torch.int64, device=dev)
-        recv = comm.exchange_counts(send)
-        buf = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if sum(map(len, payload)) else \
-            torch.zeros(0, dtype=torch.uint8)
-        got = comm.all_to_all_v(buf.to(dev), send.tolist(), recv.tolist()).cpu().numpy().tobytes()
-        out, off = [], 0
-        for n in recv.tolist():
-            out.append(json.loads(got[off: off + n].decode()) if n else [])
-            off += n
-        return out
+        return [x if x is not None else [] for x in self.comm.exchange_objects(outgoing)]
 
     def serve(self, requests: Sequence[Tuple]) -> List:
         """SPMD: ``requests`` = [(user_id, method, args...)] received by this

@@ -65,7 +65,7 @@ import torch
 
 from ..core.consolidation import (DECAY_RATE, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS, batch_dedupe,
                                   batch_link_plan, salience_decayed)
-from ..engine.tenant_graph import GHOST, NODE
+from ..engine.tenant_graph import NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT
 from ..ops import tenant_ops as T
 from ..utils.tracing import tracer
 from .comm import Communicator
@@ -361,8 +361,11 @@ class ShardedMemorySystem:
             conv = [conv[i] for i in vidx]
             E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)].to(dev, torch.float32)
             m = len(flat)
-        if g.dim is None and E is not None and E.shape[1]:
-            g._set_dim(E.shape[1])
+        d = torch.tensor([g.dim or (int(E.shape[1]) if E is not None else 0)], dtype=torch.int64, device=dev)
+        if self.world > 1:
+            d = self.comm.all_reduce(self._to_comm(d), "max").to(dev)
+        if g.dim is None and int(d.item()):
+            g._set_dim(int(d.item()))
         D = g.dim or 0
         if E is None:
             E = torch.zeros((0, D), dtype=torch.float32, device=dev)
@@ -616,6 +619,130 @@ class ShardedMemorySystem:
                     if dropped is not None and k:
                         g._note_dropped(*dropped)
                     g._bump(edges=True)
+
+    # ------------------------------------------------------------------ re-shard
+    def rebalance(self) -> Dict[str, int]:
+        """Collective all-to-all re-shard: move live rows
+        from ranks above the even share to ranks below it -- inserts land on
+        the rank whose conversation made them and eviction is global, so the
+        split drifts. A moved node takes its vector, scalars, content and its
+        outgoing edges (edges live with their source) to the new holder; the old
+        row becomes a ghost, ghost rows everywhere learn the new holder (one
+        all-gather of the moved numbers). Node numbers do not change, so every
+        later decision is unchanged. Returns {"moved": rows moved in total}."""
+        g = self.g
+        dev = self.device
+        W = self.world
+        if W == 1:
+            return {"moved": 0}
+        counts = self._gather_rows(torch.tensor([g.num_nodes()], dtype=torch.int64, device=dev)).tolist()
+        T_ = sum(counts)
+        tgt = [T_ // W + (1 if r < T_ % W else 0) for r in range(W)]
+        sur = [c - t for c, t in zip(counts, tgt)]
+        moves = [[0] * W for _ in range(W)]
+        need = [[r, -x] for r, x in enumerate(sur) if x < 0]
+        j = 0
+        for r, x in enumerate(sur):
+            while x > 0 and j < len(need):
+                k = min(x, need[j][1])
+                moves[r][need[j][0]] += k
+                x -= k
+                need[j][1] -= k
+                if need[j][1] == 0:
+                    j += 1
+        total_moved = sum(map(sum, moves))
+        if total_moved == 0:
+            return {"moved": 0}
+        n = g.n
+        D = g.dim
+        n_out = sum(moves[self.rank])
+        if n_out:
+            with g.on_stream():
+                live = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
+                key = torch.where(live, self.num[:n], torch.full((n,), -1, dtype=torch.long, device=dev))
+                _, rows_out = torch.topk(key, n_out)  # the most recent nodes move
+                rows_out = rows_out[torch.argsort(self.num[rows_out])]
+            dest = torch.repeat_interleave(torch.arange(W, device=dev),
+                                           torch.tensor(moves[self.rank], dtype=torch.long, device=dev))
+        else:
+            rows_out = torch.zeros(0, dtype=torch.long, device=dev)
+            dest = torch.zeros(0, dtype=torch.long, device=dev)
+        ro = rows_out
+        num_f = torch.stack([self.num[ro].double(), g.shard[ro].double(), g.sal[ro].double(), g.acc[ro].double(),
+                             g.last[ro], g.ts[ro]], 1) if n_out else torch.zeros((0, 6), dtype=torch.float64,
+                                                                                   device=dev)
+        emb = g.emb32[ro] if n_out else torch.zeros((0, D), dtype=torch.float32, device=dev)
+        rh = ro.tolist()
+        texts = [[] for _ in range(W)]
+        for r_, d_ in zip(rh, dest.tolist()):
+            texts[d_].append([g.content[r_], g.types[r_]])
+        # outgoing edges of the moved rows travel with them
+        if n_out and g.num_edges:
+            mv = torch.zeros(n, dtype=torch.bool, device=dev)
+            mv[ro] = True
+            dest_of = torch.full((n,), -1, dtype=torch.long, device=dev)
+            dest_of[ro] = dest
+            e = g.e
+            eidx = torch.nonzero(mv[e["src"].long()]).flatten()
+            s_, d_ = e["src"][eidx].long(), e["dst"][eidx].long()
+            edge_f = torch.stack([self.num[s_].double(), self.num[d_].double(),
+                                  (e["meta"][eidx] & SHARD_MASK).double(),
+                                  ((e["meta"][eidx] >> TYPE_SHIFT) & TYPE_MASK).double(), e["w"][eidx].double(),
+                                  e["co"][eidx].double(), e["lu"][eidx], g.shard[d_].double(),
+                                  self.holder[d_].double()], 1)
+            edest = dest_of[s_]
+        else:
+            eidx = torch.zeros(0, dtype=torch.long, device=dev)
+            edge_f = torch.zeros((0, 9), dtype=torch.float64, device=dev)
+            edest = torch.zeros(0, dtype=torch.long, device=dev)
+        cd = self.comm.device
+        r_num, r_emb = (x.to(dev) for x in self.comm.reshard(dest.to(cd), num_f.to(cd), emb.to(cd)))
+        (r_edge,) = (x.to(dev) for x in self.comm.reshard(edest.to(cd), edge_f.to(cd)))
+        got_txt = self.comm.exchange_objects(texts)
+        # sender: the moved rows become ghosts held elsewhere, their edges leave
+        if n_out:
+            if eidx.numel():
+                g.remove_edges(eidx)
+            g.remove_nodes(rh, drop_edges=False, unstore=True)
+            self.holder[ro] = dest
+        # receiver: the rows arrive (a ghost row of the same id turns live)
+        m_in = int(r_num.shape[0])
+        if m_in:
+            txt = [t for part in got_txt if part for t in part]
+            nums = r_num[:, 0].long()
+            rows = g.add_nodes([f"node_{int(x)}" for x in nums.tolist()], [t[0] for t in txt], r_emb,
+                               shard=r_num[:, 1].int(), types=[t[1] for t in txt], sal=r_num[:, 2].float(),
+                               acc=r_num[:, 3].int(), last=r_num[:, 4], ts=r_num[:, 5], stored=True)
+            self._sync_num()
+            self.num[rows] = nums
+            self.holder[rows] = self.rank
+        if r_edge.shape[0]:
+            src = self._rows_of_nums(r_edge[:, 0].long())
+            dn = r_edge[:, 1].long()
+            dst = self._rows_of_nums(dn)
+            miss = torch.nonzero(dst < 0).flatten()
+            if miss.numel():
+                un, first = np.unique(dn[miss].cpu().numpy(), return_index=True)
+                fi = miss[torch.as_tensor(first, dtype=torch.long).to(dev)]
+                rows_g = g.add_nodes([f"node_{int(x)}" for x in un], [""] * len(un), None,
+                                     shard=r_edge[fi, 7].int(), ghost=True, stored=False)
+                self._sync_num()
+                self.num[rows_g] = torch.as_tensor(un).to(dev)
+                self.holder[rows_g] = r_edge[fi, 8].long()
+                dst = self._rows_of_nums(dn)
+            et = r_edge[:, 3].long()
+            for t in torch.unique(et).tolist():
+                sel = et == t
+                g.append_edges(src[sel], dst[sel], r_edge[sel, 4].float(), r_edge[sel, 2].int(), int(t),
+                               co=r_edge[sel, 5].int(), lu=r_edge[sel, 6])
+        # every ghost row of a moved node learns its new holder
+        moved = torch.stack([self.num[ro] if n_out else torch.zeros(0, dtype=torch.long, device=dev), dest], 1)
+        allm, _ = self._gather_var(moved)
+        if allm.numel():
+            rr = self._rows_of_nums(allm[:, 0])
+            ok = rr >= 0
+            self.holder[rr[ok]] = allm[ok, 1]
+        return {"moved": total_moved}
 
     # ------------------------------------------------------------------ deep consolidation
     def component_digest(self, min_size: int = 3, min_avg_w: float = 0.3,

@@ -69,8 +69,13 @@ def _data(cfg=CPU):
     return X, sal0, keys0, steps
 
 
-def _split(n, world, r):
-    per = [n // world + (1 if i < n % world else 0) for i in range(world)]
+def _split(n, world, r, weights=None):
+    if weights:
+        w = weights[:world]
+        per = [n * x // sum(w) for x in w]
+        per[0] += n - sum(per)
+    else:
+        per = [n // world + (1 if i < n % world else 0) for i in range(world)]
     lo = sum(per[:r])
     return lo, lo + per[r]
 
@@ -134,15 +139,21 @@ def _sharded(comm, cfg=CPU):
     tmp = tempfile.mkdtemp(prefix=f"lzsh{comm.rank}_")
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
                              embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev)
-    lo, hi = _split(cfg["rows"], comm.world, comm.rank)
+    rebal = cfg.get("rebalance", False)
+    lo, hi = _split(cfg["rows"], comm.world, comm.rank, [5, 1, 2] if rebal else None)
     sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],
                     salience=torch.tensor(sal0[lo:hi]), now=_now(-1))
+    spread = []
     stats = []
     for s, (convs, V) in enumerate(steps):
         c0, c1 = _split(len(convs), comm.world, comm.rank)
         f0 = sum(len(c) for c in convs[:c0])
         f1 = f0 + sum(len(c) for c in convs[c0:c1])
         stats.append(sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1].to(dev), now=_now(s)))
+        if rebal:  # all-to-all re-shard to even shares between batches; decisions must not change
+            sm.rebalance()
+            cnt = comm.all_gather_object(sm.g.num_nodes())
+            spread.append(max(cnt) - min(cnt))
     nodes, edges = _graph_state(sm.g)
     parts = comm.all_gather_object((nodes, edges))
     contents = sm.component_digest(3, 0.3, 10)
@@ -161,7 +172,7 @@ def _sharded(comm, cfg=CPU):
         edges_all.update(e_)
     single = _single(tempfile.mkdtemp(prefix="lzsolo_"), cfg)
     return {"stats": stats, "nodes": nodes_all, "edges": edges_all, "contents": contents, "prof": prof,
-            "total": total, "found": found, "single": single}
+            "total": total, "found": found, "single": single, "spread": spread}
 
 
 def check_equivalent(out, world, limit):
@@ -186,6 +197,15 @@ def check_equivalent(out, world, limit):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_tenant_matches_single_process(world):
     check_equivalent(spawn(world, _sharded), world, LIMIT)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tenant_rebalance_keeps_semantics(world):
+    """Uneven initial split (5:1:2) re-sharded to even shares after every
+    batch by all-to-all (C3): still the single-process state, shares within 1."""
+    out = spawn(world, functools.partial(_sharded, cfg=dict(CPU, rebalance=True)))
+    check_equivalent(out, world, LIMIT)
+    assert all(s <= 1 for s in out[0]["spread"])
 
 
 def _sharded_hierarchy(comm):
