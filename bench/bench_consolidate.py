@@ -61,14 +61,14 @@ def _unit(x):
 
 
 def build_tenant(dev, nodes: int, dim: int, encoder, seed: int, db_dir: str, cluster_convs: int, n_fine: int,
-                 n_top: int, cluster_iters: int, init_edges: int):
+                 n_top: int, cluster_iters: int, init_edges: int, prune_threshold: float = 0.5):
     from bench import populate  # the headline bench's tenant loader
     from lazzaro_amd.core.memory_system import MemorySystem
     from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
 
     ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=encoder or HashEmbedder(dim=dim), device=dev,
                       db_dir=db_dir, load_from_disk=False, enable_async=False, max_buffer_size=nodes,
-                      hierarchy_mode="kmeans", hierarchy_params={"fine": n_fine, "top": n_top,
+                      prune_threshold=prune_threshold, hierarchy_mode="kmeans", hierarchy_params={"fine": n_fine, "top": n_top,
                                                                  "every": cluster_convs, "iters": cluster_iters})
     g = ms.graph
     g._set_dim(dim)
@@ -113,11 +113,12 @@ def _sync(dev):
 
 def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, encoder=None, dim: int = 768,
         dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096, n_top: int = 64,
-        cluster_iters: int = 2, init_edges: int = None, db_dir: str = None):
+        cluster_iters: int = 2, init_edges: int = None, db_dir: str = None, prune_threshold: float = 0.5):
     db_dir = db_dir or tempfile.mkdtemp(prefix=f"lzcons{comm.rank}_")
     init_edges = 2 * nodes if init_edges is None else init_edges
     ms = build_tenant(dev, nodes, dim, encoder, seed + 31 * comm.rank, db_dir, cluster_every * convs, n_fine, n_top,
-                      cluster_iters, init_edges)
+                      cluster_iters, init_edges, prune_threshold)
+    edges_start = ms.graph.num_edges
     gen = torch.Generator(device=dev).manual_seed(seed + 100 + comm.rank)
     rng = random.Random(seed + comm.rank)
     # the first k-means pass seeds the hierarchy (farthest-first); steady-state
@@ -161,6 +162,7 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
         print(_json.dumps({"stages_ms": tracer.summary()}), flush=True)
     out = {"turns_per_s": round(convs * comm.world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
            "nodes_per_rank": nodes, "convs_per_rank_step": convs, "facts_per_conv": facts,
+           "prune_threshold": prune_threshold, "edges_rank0_at_start": edges_start,
            "buffer_nodes_total": nodes * comm.world, "nodes_rank0": g.num_nodes(), "edges_rank0": g.num_edges,
            "per_step_rank0": {k: round(v / steps, 1) for k, v in agg.items()},
            # per-rank scan work (facts x rows of the rank's own tenant): no
@@ -284,6 +286,10 @@ if __name__ == "__main__":
     ap.add_argument("--top", type=int, default=64)
     ap.add_argument("--cluster-iters", type=int, default=2)
     ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--prune-threshold", type=float, default=0.5,
+                    help="MemorySystem(prune_threshold=): 0.5 is the reference default; 0 keeps every edge "
+                         "(decay still runs on all of them) -- the large-graph variant")
+    ap.add_argument("--init-edges", type=int, default=None, help="seeded edges (default 2 x nodes)")
     ap.add_argument("--sharded", action="store_true",
                     help="config 4 as one tenant row-sharded over the ranks (--nodes per rank)")
     a = ap.parse_args()
@@ -296,6 +302,7 @@ if __name__ == "__main__":
         enc = OnDeviceEmbedder("bge-base", device=dev, max_len=64)
     fn = run_sharded if a.sharded else run
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
-             n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters)
+             n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
+             **({} if a.sharded else {"prune_threshold": a.prune_threshold}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)
