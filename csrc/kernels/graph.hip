@@ -174,6 +174,53 @@ __global__ __launch_bounds__(NTB) void cc_hook_kernel(const int* __restrict__ sr
   if (old != lo) *changed = 1;
 }
 
+// One-pass lock-free union-find (the iterative hook/compress above needs a
+// host-synchronised convergence loop). Every edge unites its endpoints'
+// trees by CAS-hooking the larger root under the smaller, retrying from the
+// value the CAS returns. Parent pointers only ever move to smaller indices
+// and trees only merge, so a stale read (per-XCD L2s are not coherent, L1 is
+// never refreshed by other CUs) can only name an older ancestor: two finds
+// that agree are in the same tree, and every failed CAS strictly lowers one
+// of the two roots, so each edge terminates. Reads and the path-halving
+// writes are agent-scope (sc1, L2-served / write-through), so no dirty L2
+// line can later overwrite a hook made on another XCD. After the pass (and
+// cc_compress_kernel) every row's label is the smallest row of its
+// component -- the same contract as the iterative kernels.
+__device__ __forceinline__ int uf_ld(const int* p, int x) {
+  return __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int uf_find(int* __restrict__ p, int x) {
+  int y = uf_ld(p, x);
+  while (y != x) {
+    const int z = uf_ld(p, y);
+    if (z == y) return y;
+    __hip_atomic_store(p + x, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // path halving: z is an ancestor of x
+    x = z;
+    y = uf_ld(p, x);
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(NTB) void uf_union_kernel(const int* __restrict__ src, const int* __restrict__ dst, long ne,
+                                                       const float* __restrict__ w, float min_w,
+                                                       int* __restrict__ parent) {
+  for (long e = (long)blockIdx.x * NTB + threadIdx.x; e < ne; e += (long)gridDim.x * NTB) {
+    if (w && w[e] < min_w) continue;
+    int a = src[e], b = dst[e];
+    LZK_DCHECK(a >= 0 && b >= 0);
+    while (true) {
+      a = uf_find(parent, a);
+      b = uf_find(parent, b);
+      if (a == b) break;
+      if (a < b) { const int t = a; a = b; b = t; }  // hook the larger root a under b
+      const int old = atomicCAS(parent + a, a, b);
+      if (old == a) break;
+      a = old;  // a was hooked meanwhile: continue from its (smaller) parent
+    }
+  }
+}
+
 __global__ __launch_bounds__(NTB) void cc_compress_kernel(int* __restrict__ parent, long n) {
   const long i = (long)blockIdx.x * NTB + threadIdx.x;
   if (i >= n) return;
@@ -401,6 +448,16 @@ LZK_EXPORT int lzk_cc_hook(const int* src, const int* dst, long ne, const float*
   if (ne == 0) return 0;
   hipLaunchKernelGGL(cc_hook_kernel, blocks_for(ne), dim3(NTB), 0, (hipStream_t)stream, src, dst, ne, w, min_w,
                      parent, changed);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_uf_union(const int* src, const int* dst, long ne, const float* w, float min_w, int* parent,
+                            void* stream) {
+  if (ne == 0) return 0;
+  // grid-stride: enough blocks to fill every CU several times over
+  const long nb0 = (ne + NTB - 1) / NTB, nb = nb0 < 256L * 32 ? nb0 : 256L * 32;
+  hipLaunchKernelGGL(uf_union_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, src, dst, ne, w, min_w,
+                     parent);
   return (int)hipGetLastError();
 }
 

@@ -1013,42 +1013,63 @@ class TenantGraph:
             return []
         dev = self.device
         with self.on_stream():
-            # a row no edge touches is a singleton component (size 1 < min_size):
-            # the components are computed over the edge endpoints only, so
-            # the cost follows the edges, not the tenant's rows
-            src, dst = self.e["src"].long(), self.e["dst"].long()
-            E = src.numel()
-            verts, inv = torch.unique(torch.cat([src, dst]), return_inverse=True)
-            nv = verts.numel()
-            cl = T.components(inv[:E].to(torch.int32), inv[E:].to(torch.int32), nv).to(dev).long()
-            kind_v = self.kind[verts]
-            member = kind_v != FREE  # live nodes and ghost endpoints (the DFS follows edges to them)
-            size = _seg_sum_count(cl[member], torch.zeros(int(member.sum()), dtype=torch.float32, device=dev), nv)[1]
-            wsum, wcnt = _seg_sum_count(cl[inv[:E]], self.e["w"], nv)
-            ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1).double() > min_avg_w)
+            # Labels over the rows (one union-find pass over the edges); a row
+            # no edge touches is a singleton (size 1 < min_size, no edge
+            # weight), so only the touched rows are grouped. Every per-component
+            # reduction is a sort + scan: a component holding millions of rows
+            # would serialise atomics on one address (a scatter "amin" of the
+            # first-member keys took 119 ms at 10M rows / 20M edges).
+            src, dst = self.e["src"], self.e["dst"]
+            lab = T.components(src, dst, n).to(dev).long()
+            touched = torch.zeros(n, dtype=torch.bool, device=dev)
+            touched[src.long()] = True
+            touched[dst.long()] = True
+            # members: live nodes and ghost endpoints (the DFS follows edges to them)
+            rows = torch.nonzero(touched & (self.kind[:n] != FREE)).flatten()
+            if rows.numel() == 0:
+                return []
+            o = torch.argsort(lab[rows], stable=True)
+            rows = rows[o]  # grouped by component, row order inside each group
+            L = lab[rows]
+            newg = torch.ones_like(L, dtype=torch.bool)
+            newg[1:] = L[1:] != L[:-1]
+            gid = torch.cumsum(newg.long(), 0) - 1
+            starts = torch.nonzero(newg).flatten()
+            G = starts.numel()
+            size = torch.diff(starts, append=starts.new_full((1,), L.numel()))
+            wsum, wcnt = _seg_sum_count(lab[src.long()], self.e["w"], n)
+            gl = L[starts]
+            ok = (size >= min_size) & (wcnt[gl] > 0) & (wsum[gl] / wcnt[gl].clamp_min(1).double() > min_avg_w)
             # reference order: a component's first member in BufferGraph.nodes
             # order = the smallest (super ? 0 : shard + 1) * n + row among its
-            # live nodes -- compared as keys, no sort of the tenant's rows
+            # live nodes; min per group by one sort of (group, key) composites
             BIG = 1 << 62
-            sup_v = self.sup[verts] != 0
-            okey = torch.where(sup_v, torch.zeros_like(verts), self.shard[verts].long() + 1) * max(n, 1) + verts
-            okey = torch.where(kind_v == NODE, okey, torch.full_like(okey, BIG))
-            first = torch.full((nv,), BIG, dtype=torch.long, device=dev)
-            first.scatter_reduce_(0, cl, okey, "amin", include_self=True)
+            kind_r, sup_r = self.kind[rows], self.sup[rows] != 0
+            okey = torch.where(sup_r, torch.zeros_like(rows), self.shard[rows].long() + 1) * max(n, 1) + rows
+            node = kind_r == NODE
+            kbits = max(1, int(okey.max()).bit_length() + 1)
+            if kbits + max(1, G.bit_length()) <= 62:
+                comp = gid * (1 << kbits) + torch.where(node, okey, torch.full_like(okey, (1 << kbits) - 1))
+                cs = torch.sort(comp).values
+                fk = cs[starts] & ((1 << kbits) - 1)
+                first = torch.where(fk == (1 << kbits) - 1, torch.full_like(fk, BIG), fk)
+            else:  # keys too wide to pack: scatter min
+                first = torch.full((G,), BIG, dtype=torch.long, device=dev)
+                first.scatter_reduce_(0, gid, torch.where(node, okey, torch.full_like(okey, BIG)), "amin")
             ok &= first < BIG
-            cand = torch.nonzero(ok[cl] & (kind_v == NODE) & ~sup_v).flatten()
-            if cand.numel() == 0:
+            cand = ok[gid] & node & ~sup_r
+            ci = torch.nonzero(cand).flatten()
+            if ci.numel() == 0:
                 return []
-            key = first[cl[cand]]
-            rowsv = verts[cand]
-            o = torch.argsort(key * n + rowsv)  # (component order, row)
-            rowsv, key = rowsv[o], key[o]
-            newg = torch.ones_like(key, dtype=torch.bool)
-            newg[1:] = key[1:] != key[:-1]
-            gstart = torch.nonzero(newg).flatten()[torch.cumsum(newg.long(), 0) - 1]
-            rank = torch.arange(key.numel(), device=dev) - gstart
-            sel = rank < take
-            rows_h, key_h = rowsv[sel].cpu().numpy(), key[sel].cpu().numpy()
+            # rank of each candidate among its group's candidates (row order)
+            cg = gid[ci]
+            cnew = torch.ones_like(cg, dtype=torch.bool)
+            cnew[1:] = cg[1:] != cg[:-1]
+            cstart = torch.nonzero(cnew).flatten()[torch.cumsum(cnew.long(), 0) - 1]
+            sel = ci[(torch.arange(ci.numel(), device=dev) - cstart) < take]
+            rowsv, key = rows[sel], first[gid[sel]]
+            o = torch.argsort(key * n + rowsv)  # (component order, row): at most take rows per component
+            rows_h, key_h = rowsv[o].cpu().numpy(), key[o].cpu().numpy()
         cut = np.nonzero(np.diff(key_h))[0] + 1
         return np.split(rows_h, cut)
 

@@ -25,6 +25,7 @@ _lib.register("lzk_importance", I, [P, P, P, P, P, L, D_, P, P])
 _lib.register("lzk_mark_dead", I, [P, L, P, P])
 _lib.register("lzk_cc_hook", I, [P, P, L, P, F, P, P, P])
 _lib.register("lzk_cc_compress", I, [P, L, P])
+_lib.register("lzk_uf_union", I, [P, P, L, P, F, P, P])
 _lib.register("lzk_neighbor_boost", I, [P, P, P, P, P, I, F, D_, F, P, P, P, P, P])
 _lib.register("lzk_pairs_above", I, [P, L, I, I, F, P, I, P, P])
 _lib.register("lzk_seg_sum", I, [P, L, L, I, P, P, P, P])
@@ -134,8 +135,13 @@ def mark_dead(alive: torch.Tensor, idx: torch.Tensor) -> None:
 
 
 def connected_components(src: torch.Tensor, dst: torch.Tensor, n: int, w: Optional[torch.Tensor] = None,
-                         min_w: float = 0.0, max_iter: int = 64) -> torch.Tensor:
-    """K9: undirected components; label = smallest node index in the component."""
+                         min_w: float = 0.0, max_iter: int = 64, method: str = "uf") -> torch.Tensor:
+    """K9: undirected components; label = smallest node index in the component.
+
+    GPU ``method="uf"`` (default): one lock-free union-find pass over the
+    edges (``uf_union_kernel``) + one compress pass -- two launches, no host
+    synchronisation. ``method="hook"``: the iterative min-label hooking +
+    pointer jumping, one host-checked round trip per iteration."""
     if not src.is_cuda:
         from ..store.colstore import _rt
         s, d = src, dst
@@ -145,8 +151,14 @@ def connected_components(src: torch.Tensor, dst: torch.Tensor, n: int, w: Option
         lab = _rt().union_find_components(s.numpy().astype("int32"), d.numpy().astype("int32"), n)
         return torch.from_numpy(lab)
     parent = torch.arange(n, dtype=torch.int32, device=src.device)
-    changed = torch.zeros(1, dtype=torch.int32, device=src.device)
     L_ = _lib.lib()
+    if method == "uf":
+        src, dst = src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous()
+        _lib.check(L_.lzk_uf_union(src.data_ptr(), dst.data_ptr(), src.numel(), _lib.ptr(w), float(min_w),
+                                   parent.data_ptr(), _st(src)), "uf_union")
+        _lib.check(L_.lzk_cc_compress(parent.data_ptr(), n, _st(src)), "cc_compress")
+        return parent
+    changed = torch.zeros(1, dtype=torch.int32, device=src.device)
     for _ in range(max_iter):
         changed.zero_()
         _lib.check(L_.lzk_cc_hook(src.data_ptr(), dst.data_ptr(), src.numel(), _lib.ptr(w), float(min_w),

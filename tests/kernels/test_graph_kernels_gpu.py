@@ -69,6 +69,22 @@ def test_chain_components_gpu():
     s = torch.arange(n - 1, dtype=torch.int32, device=DEV)
     lab = G.connected_components(s, s + 1, n)
     assert int(lab.max()) == 0
+    # reversed and shuffled chain (worst case for index-ordered hooking)
+    p = torch.randperm(n - 1, generator=torch.Generator().manual_seed(4)).to(DEV)
+    lab = G.connected_components((s + 1).flip(0)[p], s.flip(0)[p], n)
+    assert int(lab.max()) == 0
+
+
+@pytest.mark.parametrize("method", ["uf", "hook"])
+@pytest.mark.parametrize("n,ne,seed", [(2_000_000, 4_000_000, 1), (3_000_000, 1_000_000, 2), (50_000, 2, 3)])
+def test_components_methods_large_gpu(method, n, ne, seed):
+    """Union-find and hook/compress give the host union-find's labels
+    (smallest row per component) on a giant-component graph, a graph of many
+    small components and a nearly empty one."""
+    e = _rand_edges(n, ne, seed, "cpu")
+    ref = G.connected_components(e["src"], e["dst"], n)
+    got = G.connected_components(e["src"].to(DEV), e["dst"].to(DEV), n, method=method)
+    assert torch.equal(ref.to(torch.int32), got.cpu())
 
 
 def test_pairs_above_gpu():
