@@ -109,6 +109,21 @@ def _seg_sum_count(keys: torch.Tensor, vals: torch.Tensor, n: int):
     return sums, cnts
 
 
+def _seg_min(keys: torch.Tensor, vals: torch.Tensor, n: int, fill: int) -> torch.Tensor:
+    """Minimum of int64 ``vals`` per key in [0, n) (``fill`` where a key has
+    none) by two stable sorts -- no contended atomic min on a huge key."""
+    out = torch.full((n,), fill, dtype=torch.long, device=keys.device)
+    if keys.numel() == 0:
+        return out
+    o = torch.argsort(vals, stable=True)
+    o = o[torch.argsort(keys[o], stable=True)]
+    k = keys[o]
+    head = torch.ones_like(k, dtype=torch.bool)
+    head[1:] = k[1:] != k[:-1]
+    out[k[head]] = vals[o][head]
+    return out
+
+
 _SIDE_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 
@@ -1053,9 +1068,8 @@ class TenantGraph:
                 cs = torch.sort(comp).values
                 fk = cs[starts] & ((1 << kbits) - 1)
                 first = torch.where(fk == (1 << kbits) - 1, torch.full_like(fk, BIG), fk)
-            else:  # keys too wide to pack: scatter min
-                first = torch.full((G,), BIG, dtype=torch.long, device=dev)
-                first.scatter_reduce_(0, gid, torch.where(node, okey, torch.full_like(okey, BIG)), "amin")
+            else:  # keys too wide to pack
+                first = _seg_min(gid, torch.where(node, okey, torch.full_like(okey, BIG)), G, BIG)
             ok &= first < BIG
             cand = ok[gid] & node & ~sup_r
             ci = torch.nonzero(cand).flatten()

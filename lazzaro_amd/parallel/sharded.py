@@ -105,9 +105,10 @@ def distributed_components(comm: Communicator, src: torch.Tensor, dst: torch.Ten
         if nl else torch.zeros(0, dtype=torch.long, device=dev)
     big = torch.iinfo(torch.int64).max
 
-    def propagate(lab):
-        m = torch.full((nl,), big, dtype=torch.int64, device=dev).scatter_reduce(0, comp, lab, "amin")
-        return m[comp]
+    from ..engine.tenant_graph import _seg_min
+
+    def propagate(lab):  # segmented min by sorts: a giant local component is one key
+        return _seg_min(comp, lab, nl, big)[comp]
 
     label = propagate(verts.clone())
     st = {"rounds": 0, "rows_sent": 0, "first_round_rows": int(nl)}

@@ -65,7 +65,7 @@ import torch
 
 from ..core.consolidation import (DECAY_RATE, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS, batch_dedupe,
                                   batch_link_plan, salience_decayed)
-from ..engine.tenant_graph import NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT
+from ..engine.tenant_graph import NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT, _seg_min, _seg_sum_count
 from ..ops import tenant_ops as T
 from ..utils.tracing import tracer
 from .comm import Communicator
@@ -790,8 +790,8 @@ class ShardedMemorySystem:
         if s_num.numel():
             el = lab[torch.searchsorted(verts, s_num)]
             ul, inv = torch.unique(el, return_inverse=True)
-            ws = torch.zeros(ul.numel(), dtype=torch.float64, device=dev).index_add_(0, inv, w)
-            wc = torch.bincount(inv, minlength=ul.numel()).double()
+            ws, wc = _seg_sum_count(inv, w, ul.numel())  # sort + scan: no contended fp64 atomics
+            wc = wc.double()
             part_w = torch.stack([ul.double(), ws, wc], 1)
         else:
             part_w = torch.zeros((0, 3), dtype=torch.float64, device=dev)
@@ -818,7 +818,7 @@ class ShardedMemorySystem:
             key = (g.shard[rr].long() + 1) * (1 << NUM_BITS) + verts
             lv = torch.nonzero(live).flatten()
             ul, inv = torch.unique(lab[lv], return_inverse=True)
-            fk = torch.full((ul.numel(),), BIG, dtype=torch.long, device=dev).scatter_reduce_(0, inv, key[lv], "amin")
+            fk = _seg_min(inv, key[lv], ul.numel(), BIG)
             part_f = torch.stack([ul, fk], 1)
         else:
             lv = torch.zeros(0, dtype=torch.long, device=dev)
