@@ -22,7 +22,7 @@ def test_bench_two_ranks_cpu(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--cpu", "--gpus", "2", "--rows", "6000", "--dim", "128", "--model", "tiny", "--batch", "32",
-           "--steps", "2", "--warmup", "1", "--recall-queries", "8", "--consolidate-steps", "1",
+           "--steps", "2", "--warmup", "1", "--prewarm-s", "0.2", "--recall-queries", "8", "--consolidate-steps", "1",
            "--consolidate-convs", "4"]
     env = dict(os.environ, PYTHONPATH=ROOT, LZK_BENCH_DB=str(tmp_path / "db"))
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
