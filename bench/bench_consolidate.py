@@ -61,14 +61,15 @@ def _unit(x):
 
 
 def build_tenant(dev, nodes: int, dim: int, encoder, seed: int, db_dir: str, cluster_convs: int, n_fine: int,
-                 n_top: int, cluster_iters: int, init_edges: int, prune_threshold: float = 0.5):
+                 n_top: int, cluster_iters: int, init_edges: int, prune_threshold: float = 0.5,
+                 persist_async: bool = False):
     from bench import populate  # the headline bench's tenant loader
     from lazzaro_amd.core.memory_system import MemorySystem
     from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
 
     ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=encoder or HashEmbedder(dim=dim), device=dev,
                       db_dir=db_dir, load_from_disk=False, enable_async=False, max_buffer_size=nodes,
-                      prune_threshold=prune_threshold, hierarchy_mode="kmeans", hierarchy_params={"fine": n_fine, "top": n_top,
+                      prune_threshold=prune_threshold, persist_async=persist_async, hierarchy_mode="kmeans", hierarchy_params={"fine": n_fine, "top": n_top,
                                                                  "every": cluster_convs, "iters": cluster_iters})
     g = ms.graph
     g._set_dim(dim)
@@ -113,11 +114,12 @@ def _sync(dev):
 
 def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, encoder=None, dim: int = 768,
         dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096, n_top: int = 64,
-        cluster_iters: int = 2, init_edges: int = None, db_dir: str = None, prune_threshold: float = 0.5):
+        cluster_iters: int = 2, init_edges: int = None, db_dir: str = None, prune_threshold: float = 0.5,
+        persist_async: bool = False):
     db_dir = db_dir or tempfile.mkdtemp(prefix=f"lzcons{comm.rank}_")
     init_edges = 2 * nodes if init_edges is None else init_edges
     ms = build_tenant(dev, nodes, dim, encoder, seed + 31 * comm.rank, db_dir, cluster_every * convs, n_fine, n_top,
-                      cluster_iters, init_edges, prune_threshold)
+                      cluster_iters, init_edges, prune_threshold, persist_async)
     edges_start = ms.graph.num_edges
     gen = torch.Generator(device=dev).manual_seed(seed + 100 + comm.rank)
     rng = random.Random(seed + comm.rank)
@@ -149,6 +151,7 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     for _ in range(steps):
         for k, v in step().items():
             agg[k] = agg.get(k, 0) + v
+    ms.flush_persistence()  # write-behind commits of the timed steps land inside the timed region
     _sync(dev)
     comm.barrier()
     el = time.perf_counter() - t0
@@ -171,7 +174,9 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
            "path": "MemorySystem.consolidate_batch (tenant-DP)",
            "hierarchical_clustering": {"mode": "kmeans", "every_steps": cluster_every, "fine": n_fine, "top": n_top,
                                        "iters_per_pass": cluster_iters, "seed_pass_ms": round(seed_ms, 1)},
-           "persistence": "incremental columnar commit per step (db on local disk)"}
+           "persistence": "incremental columnar commit per step (db on local disk)" + (
+               ", write-behind (persist_async: commits on a writer thread, flushed inside the timed region)"
+               if persist_async else "")}
     ms.close()
     return out
 
@@ -289,6 +294,7 @@ if __name__ == "__main__":
     ap.add_argument("--prune-threshold", type=float, default=0.5,
                     help="MemorySystem(prune_threshold=): 0.5 is the reference default; 0 keeps every edge "
                          "(decay still runs on all of them) -- the large-graph variant")
+    ap.add_argument("--persist-async", action="store_true", help="MemorySystem(persist_async=True)")
     ap.add_argument("--init-edges", type=int, default=None, help="seeded edges (default 2 x nodes)")
     ap.add_argument("--sharded", action="store_true",
                     help="config 4 as one tenant row-sharded over the ranks (--nodes per rank)")
@@ -303,6 +309,6 @@ if __name__ == "__main__":
     fn = run_sharded if a.sharded else run
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
-             **({} if a.sharded else {"prune_threshold": a.prune_threshold}))
+             **({} if a.sharded else {"prune_threshold": a.prune_threshold, "persist_async": a.persist_async}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)

@@ -271,6 +271,7 @@ class ConsolidationMixin:
         pend, self._pending = self._pending, []
         for f in pend:
             f.result(timeout=timeout)
+        self.flush_persistence()
 
     # ------------------------------------------------------------ fact extraction
     def _async_consolidate(self):

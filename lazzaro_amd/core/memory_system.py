@@ -109,6 +109,7 @@ class MemorySystem(ConsolidationMixin):
         index_params: Optional[Dict] = None,
         hierarchy_mode: str = "reference",
         hierarchy_params: Optional[Dict] = None,
+        persist_async: bool = False,
     ):
         self.model = model
         self.user_id = user_id
@@ -164,6 +165,14 @@ class MemorySystem(ConsolidationMixin):
         self.strict_errors = strict_errors
         self.max_consolidation_retries = max_consolidation_retries
         self._persist_pending = False
+        # write-behind persistence (opt-in): a save snapshots the changed
+        # rows on the caller's thread and one writer thread commits the
+        # snapshots in order, so the store I/O overlaps the next device work
+        self.persist_async = bool(persist_async)
+        self._writer = ThreadPoolExecutor(max_workers=1) if self.persist_async else None
+        self._writes: List = []
+        self._unwritten: List = []  # snapshots whose commit failed, retried first
+        self._wb_lock = threading.Lock()
 
         self.query_cache = QueryCache(max_size=1000) if enable_caching else None
         self.consolidation_queue: List[Dict] = []
@@ -820,6 +829,9 @@ STORAGE:
         A failed commit leaves the graph authoritative and the change set
         pending (it is retried by the next save); ``strict_errors`` raises
         :class:`StoreError` instead."""
+        if self._writer is not None and self._store_binds_graph():
+            self._save_write_behind()
+            return
         with self._graph_lock:
             try:
                 with tracer.stage("persist", "cpu"):
@@ -827,7 +839,8 @@ STORAGE:
                         self._commit_incremental()
                     else:
                         self._rewrite_all()
-                    self.store.save_profile(self._profile_blob(), user_id=self.user_id)
+                    with tracer.stage("persist_profile", "cpu"):
+                        self.store.save_profile(self._profile_blob(), user_id=self.user_id)
             except Exception as e:
                 self.metrics["persist_failures"] = self.metrics.get("persist_failures", 0) + 1
                 self._persist_pending = True
@@ -847,7 +860,9 @@ STORAGE:
                 self.query_cache.invalidate_results()
         self._say(f"✓ State persisted for user: {self.user_id}")
 
-    def _commit_incremental(self) -> None:
+    def _snapshot_incremental(self):
+        """Take the change set (dirty rows / edges, deletions) and export it
+        as store columns. Returns (tracking, commit_tenant arguments)."""
         g = self.graph
         rows = g.take_dirty_rows()
         eidx = g.take_dirty_edges()
@@ -857,21 +872,95 @@ STORAGE:
                 with g.on_stream():
                     k = g.kind[torch.as_tensor(rows).to(g.device)].cpu().numpy()
                 rows = rows[k == NODE]
-            node_cols = export_node_columns(g, rows)
-            edge_cols = export_edge_columns(g, eidx)
+            with tracer.stage("persist_export", "cpu"):
+                node_cols = export_node_columns(g, rows)
+                edge_cols = export_edge_columns(g, eidx)
             # largest node_<n> id ever committed (O(changed rows)): a reload
             # restores node_counter from it without scanning every id
             self._max_node_id = max(getattr(self, "_max_node_id", 0), _max_node_num(node_cols.get("id", [])))
-            self.store.commit_tenant(self.user_id, node_cols, del_ids, edge_cols,
-                                     [f"{s}_{t}" for s, t in del_edges])
         except Exception:
             g.restore_tracking(rows, eidx, del_ids, del_edges)
             raise
+        return (rows, eidx, del_ids, del_edges), (self.user_id, node_cols, del_ids, edge_cols,
+                                                   [f"{s}_{t}" for s, t in del_edges])
+
+    def _commit_incremental(self) -> None:
+        tracking, args = self._snapshot_incremental()
+        try:
+            with tracer.stage("persist_write", "cpu"):
+                self.store.commit_tenant(*args)
+        except Exception:
+            self.graph.restore_tracking(*tracking)
+            raise
+        self._mark_committed(tracking[0], tracking[2])
+
+    def _mark_committed(self, rows, del_ids) -> None:
+        g = self.graph
         g.mark_stored(rows)
         # ids deleted from the table leave the searchable set too
         gone = [i for i in del_ids if g.node_row(i) < 0]
         if gone:
             g.unstore(gone)
+
+    # ------------------------------------------------------------ write-behind
+    def _save_write_behind(self) -> None:
+        """``persist_async``: snapshot on this thread (under the graph lock),
+        commit on the writer thread. The rows are searchable from now on, as
+        after a synchronous save; a commit that fails keeps its snapshot and
+        is retried before the next one (upserts / deletes by id, in order)."""
+        with self._graph_lock:
+            with tracer.stage("persist", "cpu"):
+                try:
+                    tracking, args = self._snapshot_incremental()
+                except Exception as e:
+                    self._persist_failed(e)
+                    return
+                self._mark_committed(tracking[0], tracking[2])
+                prof = self._profile_blob()
+                self._writes = [f for f in self._writes if not f.done()]
+                self._writes.append(self._writer.submit(self._write_job, args, prof))
+            if self.query_cache:
+                self.query_cache.invalidate_results()
+
+    def _write_job(self, args, prof) -> None:
+        with self._wb_lock:
+            queue, self._unwritten = self._unwritten + [(args, prof)], []
+            for i, (a, p) in enumerate(queue):
+                try:
+                    with tracer.stage("persist_write", "cpu"):
+                        self.store.commit_tenant(*a)
+                        self.store.save_profile(p, user_id=a[0])
+                except Exception as e:
+                    self._unwritten = queue[i:]
+                    self.metrics["persist_failures"] = self.metrics.get("persist_failures", 0) + 1
+                    log.warning("write-behind commit failed for %s: %s", a[0], e)
+                    return
+            try:
+                self._last_nodes_version = self.store.get_latest_version()
+            except Exception:
+                pass
+
+    def flush_persistence(self) -> None:
+        """Wait for the write-behind commits; retry any failed snapshot once
+        more (``strict_errors``: raise :class:`StoreError` if it still fails)."""
+        if self._writer is None:
+            return
+        pend, self._writes = self._writes, []
+        for f in pend:
+            f.result()
+        if self._unwritten:
+            with self._wb_lock:
+                args, prof = self._unwritten.pop()
+            self._writer.submit(self._write_job, args, prof).result()
+            if self._unwritten and self.strict_errors:
+                raise StoreError(f"write-behind commit failed for {self.user_id}")
+
+    def _persist_failed(self, e) -> None:
+        self.metrics["persist_failures"] = self.metrics.get("persist_failures", 0) + 1
+        self._persist_pending = True
+        log.warning("persistence failed for %s: %s", self.user_id, e)
+        if self.strict_errors:
+            raise StoreError(str(e)) from e
 
     def _rewrite_all(self) -> None:
         self._max_node_id = max(getattr(self, "_max_node_id", 0), _max_node_num(self.graph.ids))
@@ -894,6 +983,8 @@ STORAGE:
         columns go straight into the graph (vectors: one host->device copy),
         no per-row ``Node`` objects; decay since each row was written is
         replayed from the persisted decay clock."""
+        if getattr(self, "_writer", None) is not None:
+            self.flush_persistence()  # our own queued commits land before we read
         self._say(f"🔄 Loading state for user: {self.user_id}...")
         with self._graph_lock:
             loader = getattr(self.store, "load_tenant", None)
@@ -933,6 +1024,7 @@ STORAGE:
             self._say("ℹ No saved state found.")
 
     def check_for_updates(self) -> bool:
+        self.flush_persistence()
         try:
             v = self.store.get_latest_version()
             if not hasattr(self, "_last_nodes_version") or v > self._last_nodes_version:
@@ -956,6 +1048,7 @@ STORAGE:
             self.flush()
         else:
             self._save_to_persistence()
+        self.flush_persistence()
         with self._graph_lock:
             detach = getattr(self.store, "detach", None)
             if detach is not None:
@@ -1093,6 +1186,9 @@ Be clinical yet insightful. Do not include conversational filler."""
     def close(self):
         if self.background_executor:
             self.background_executor.shutdown(wait=True)
+        if self._writer is not None:
+            self.flush_persistence()
+            self._writer.shutdown(wait=True)
         if hasattr(self, "store") and self.store is not None:
             self.store.close()
 

@@ -551,3 +551,40 @@ def test_ivfpq_index_under_the_tenant_graph(tmp_path):
     _, rows = g.store_search(X[5:6], 2, "l2")
     assert g._ann_covered == g.n and set(rows[0].tolist()) == {5, g.n - 1}
     ms.close()
+
+
+@pytest.mark.parametrize("fail", [False, True])
+def test_write_behind_persistence_equals_sync(tmp_path, fail):
+    """persist_async=True: commits run on the writer thread, in order; what a
+    fresh MemorySystem reloads equals the synchronous run's store. With an
+    injected commit failure the snapshot is kept and retried before the next
+    one, so nothing is lost."""
+    from lazzaro_amd.utils.faults import injector
+
+    convs, table = _batch_scenario(5, n_conv=6)
+    kw = dict(enable_async=False, max_buffer_size=20, consolidate_every=2, super_node_threshold=10 ** 6)
+
+    def run(db, persist_async):
+        ms = MemorySystem(llm_provider=ScriptedLLM([json.dumps({"memories": f}) for f in convs]),
+                          embedding_provider=VecEmbedder(table, 16), db_dir=db, load_from_disk=False,
+                          persist_async=persist_async, **kw)
+        for i in range(len(convs)):
+            if fail and persist_async and i == 2:
+                injector.arm("store.commit", 1)
+            ms.start_conversation()
+            ms.add_to_short_term("conversation text")
+            ms.end_conversation()
+        ms.close()
+        injector.disarm()
+        back = MemorySystem(llm_provider=LocalLLM(), embedding_provider=VecEmbedder(table, 16), db_dir=db,
+                            load_from_disk=True, **kw)
+        st = _graph_state(back)
+        back.close()
+        return st, ms.metrics.get("persist_failures", 0)
+
+    (a, _), (b, nfail) = run(str(tmp_path / "sync"), False), run(str(tmp_path / "wb"), True)
+    assert a[0].keys() == b[0].keys() and len(a[0]) > 0
+    for k in a[0]:
+        assert a[0][k][0] == b[0][k][0] and abs(a[0][k][1] - b[0][k][1]) < 1e-6, k
+    assert a[1] == b[1]
+    assert nfail == (1 if fail else 0)
