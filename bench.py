@@ -144,12 +144,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # launched by torchrun (even with one rank): the process group and every
+    # collective code path are live -- a 1-rank torchrun run on one GPU
+    # exercises the RCCL calls of the N-GPU job
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
     if a.cpu:
-        if world > 1:
+        if distributed:
             dist.init_process_group("gloo")
         dev = torch.device("cpu")
     else:
-        if world > 1:
+        if distributed:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dev = torch.device("cuda", local)
@@ -172,7 +176,7 @@ def main():
     # the serving layer: tenants placed on ranks by rendezvous hashing; each
     # rank's tenant is the first name the placement gives it (a real HRW
     # assignment), holding --rows memories in this GPU's HBM
-    comm = Communicator() if world > 1 else Communicator.local(dev)
+    comm = Communicator() if distributed else Communicator.local(dev)
     tmp = os.environ.get("LZK_BENCH_DB") or tempfile.mkdtemp(prefix="lzbench_")
 
     def factory(user):
@@ -211,7 +215,7 @@ def main():
     for _ in ms.search_memories_stream(batches(a.warmup), limit=a.k):
         pass
     sync()
-    if world > 1:
+    if distributed:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -219,12 +223,12 @@ def main():
     for res in ms.search_memories_stream(batches(a.steps), limit=a.k):
         n_res += len(res)
     sync()
-    if world > 1:
+    if distributed:
         dist.barrier()
     sync()
     el = time.perf_counter() - t0
     assert n_res == a.steps * a.batch
-    if world > 1:
+    if distributed:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -234,7 +238,7 @@ def main():
     # network: one all-to-all-v of the queries, one back with the results) and
     # a global cross-tenant search (all-gather of candidates + merge) ----
     routed = {}
-    if world > 1:
+    if distributed:
         reqs = [(tenants[r], "search_memories", q, a.k) for r in range(world) for q in pool[1][: a.batch // world]]
         svc.serve(reqs)
         sync()
@@ -353,7 +357,7 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

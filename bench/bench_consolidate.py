@@ -312,3 +312,7 @@ if __name__ == "__main__":
              **({} if a.sharded else {"prune_threshold": a.prune_threshold, "persist_async": a.persist_async}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)
+    if comm.enabled:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
