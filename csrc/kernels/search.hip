@@ -401,6 +401,69 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   }
 }
 
+// K2 across ranks: merge the all-gathered candidate lists [nq, ncand] whose
+// ids are GLOBAL 64-bit keys (row offset + local row, or tenant<<32 | row)
+// into the exact top-kout by (score desc, id asc); id < 0 marks an empty slot.
+// One wave per query; every lane keeps a sorted K-list of its strided share,
+// then kout rounds of a wave-wide (score, id) argmax pop the global order.
+// Replaces two full argsorts of [nq, world*k] (parallel/sharded.py merge_topk).
+__device__ __forceinline__ bool better64(float a, long ia, float b, long ib) {
+  return a > b || (a == b && ia < ib);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void topk_merge64_kernel(
+    const float* __restrict__ ps, const long* __restrict__ pi, int ncand, int nq,
+    int kout, float* __restrict__ os, long* __restrict__ oi) {
+  constexpr long NONE = 0x7fffffffffffffffL;
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;  // whole wave exits together (q is wave-uniform)
+  float ts[K];
+  long ti[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) { ts[j] = LZK_NEG_INF; ti[j] = NONE; }
+  const float* s = ps + (long)q * ncand;
+  const long* ix = pi + (long)q * ncand;
+  for (int c = lane; c < ncand; c += 64) {
+    float v = s[c];
+    long r = ix[c];
+    if (r < 0) continue;
+    if (better64(v, r, ts[K - 1], ti[K - 1])) {
+#pragma unroll
+      for (int j = K - 1; j > 0; --j) {
+        bool up = better64(v, r, ts[j - 1], ti[j - 1]);
+        bool here = better64(v, r, ts[j], ti[j]);
+        float ns = up ? ts[j - 1] : (here ? v : ts[j]);
+        long ni = up ? ti[j - 1] : (here ? r : ti[j]);
+        ts[j] = ns; ti[j] = ni;
+      }
+      if (better64(v, r, ts[0], ti[0])) { ts[0] = v; ti[0] = r; }
+    }
+  }
+  for (int j = 0; j < kout; ++j) {
+    float hs = ts[0];
+    long hi = ti[0];
+    float bs = hs; long bi = hi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      float s2 = __shfl_xor(bs, o, 64);
+      long i2 = __shfl_xor(bi, o, 64);
+      if (better64(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) {
+      os[(long)q * kout + j] = bs;
+      oi[(long)q * kout + j] = (bi == NONE) ? -1 : bi;
+    }
+    // ids are unique per query, so exactly one lane owns the winner
+    if (hi == bi && hs == bs && bi != NONE) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) { ts[t] = ts[t + 1]; ti[t] = ti[t + 1]; }
+      ts[K - 1] = LZK_NEG_INF; ti[K - 1] = NONE;
+    }
+  }
+}
+
 int g_search_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
 
 int search_staging() {
@@ -529,6 +592,25 @@ static int topk_merge(const float* ps, const int* pi, int ncand, int nq, int ksl
 LZK_EXPORT int lzk_topk_merge(const float* ps, const int* pi, int ncand, int nq, int kslot,
                               int kout, long idx_offset, float* os, long* oi, void* stream) {
   return topk_merge(ps, pi, ncand, nq, kslot, kout, idx_offset, os, oi, stream, nullptr);
+}
+
+// Cross-rank merge of all-gathered candidates with 64-bit global ids:
+// ps/pi [nq, ncand] -> os/oi [nq, kout], kout <= 32. Each lane's list holds
+// the best K of its share, so kout <= K keeps the result exact.
+LZK_EXPORT int lzk_topk_merge64(const float* ps, const long* pi, int ncand, int nq, int kout, float* os, long* oi,
+                                void* stream) {
+  if (nq <= 0) return 0;
+  if (kout < 1 || ncand < 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((nq + 3) / 4), block(256);
+#define LZK_M64(KK) hipLaunchKernelGGL(topk_merge64_kernel<KK>, grid, block, 0, st, ps, pi, ncand, nq, kout, os, oi)
+  if (kout <= 4) LZK_M64(4);
+  else if (kout <= 10) LZK_M64(10);
+  else if (kout <= 16) LZK_M64(16);
+  else if (kout <= 32) LZK_M64(32);
+  else return (int)hipErrorInvalidValue;
+#undef LZK_M64
+  return (int)hipGetLastError();
 }
 
 // Merge only the active queries' rows of os/oi (others untouched).

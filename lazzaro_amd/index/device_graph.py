@@ -38,6 +38,26 @@ def _pad64(d):
     return (d + 63) // 64 * 64
 
 
+def csr_undirected(src: torch.Tensor, dst: torch.Tensor, n: int):
+    """Undirected CSR built with tensor ops on the tensors' device: arcs
+    ordered per source by edge index, self-loops once -- the same layout as
+    the native host build (csrc/runtime/graph_host.cpp build_csr).
+    Returns (off int64 [n+1], adj int32, eid int32)."""
+    dev = src.device
+    s, d = src.long(), dst.long()
+    ne = s.numel()
+    frm = torch.stack([s, d], 1).reshape(-1)
+    to = torch.stack([d, s], 1).reshape(-1)
+    eid = torch.arange(ne, device=dev).repeat_interleave(2)
+    ok = torch.ones(2 * ne, dtype=torch.bool, device=dev)
+    ok[1::2] = s != d
+    frm, to, eid = frm[ok], to[ok], eid[ok]
+    order = torch.sort(frm, stable=True).indices
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(torch.bincount(frm, minlength=n)[:n], 0)
+    return off, to[order].to(torch.int32), eid[order].to(torch.int32)
+
+
 class DeviceGraph:
     def __init__(self, dim: int, device=None, capacity: int = 1 << 16, edge_capacity: int = 1 << 18):
         self.device = torch.device(device) if device is not None else torch.device("cpu")
@@ -301,9 +321,13 @@ class DeviceGraph:
         return G.connected_components(e["src"], e["dst"], self.n, e["w"], min_w)
 
     def csr(self):
-        """Undirected CSR (host build in the native runtime, copied to device)."""
-        from ..store.colstore import _rt
+        """Undirected CSR, per-source arcs in edge-index order (self-loops once).
+        Device graphs build it in HBM (stable sort of the arc sources + bincount
+        scan, no host round trip); CPU graphs use the native runtime build."""
         e = self.edges
+        if self.device.type == "cuda":
+            return csr_undirected(e["src"], e["dst"], self.n)
+        from ..store.colstore import _rt
         off, adj, eid = _rt().build_csr(e["src"].cpu().numpy(), e["dst"].cpu().numpy(), self.n, True)
         t = lambda a: torch.from_numpy(a).to(self.device)  # noqa: E731
         return t(off), t(adj), t(eid)

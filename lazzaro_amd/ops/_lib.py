@@ -38,6 +38,7 @@ _SIGS = {
     "lzk_topk_merge": (I, [P, P, I, I, I, I, L, P, P, P]),
     "lzk_flat_topk_partial_masked": (I, [P, L, I, P, L, I, P, P, P, F, I, I, I, P, P, P, P]),
     "lzk_topk_merge_masked": (I, [P, P, I, I, I, I, L, P, P, P, P]),
+    "lzk_topk_merge64": (I, [P, P, I, I, I, P, P, P]),
     "lzk_segment_topk": (I, [P, P, L, P, P, P, L, I, I, I, F, P, I, I, P, P, P]),
     "lzk_flat_cand_dual": (I, [P, L, I, P, L, I, I, P, P, P, F, P, P, I, P, P, P, P, P, P, P, I, P, P]),
     "lzk_flat_cand": (I, [P, L, I, P, L, I, I, P, P, P, F, P, I, P, P, P, P, I, P, P]),

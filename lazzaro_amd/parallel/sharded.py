@@ -24,7 +24,22 @@ NEG_INF = float("-inf")
 
 
 def merge_topk(scores: torch.Tensor, ids: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Merge candidate lists [nq, C] -> top-k by (score desc, id asc)."""
+    """Merge candidate lists [nq, C] -> top-k by (score desc, id asc).
+
+    Device tensors (k <= 32) run the K2 ``topk_merge64_kernel`` (search.hip):
+    one wave per query, no sort of the gathered lists. Empty slots (id < 0)
+    sort last and come back as (-inf, -1) in both paths."""
+    if scores.is_cuda and 0 < k <= 32 and scores.shape[1] >= k:
+        from ..ops import _lib
+
+        nq, nc = scores.shape
+        s = scores.float().contiguous()
+        i = ids.long().contiguous()
+        os_ = torch.empty((nq, k), dtype=torch.float32, device=s.device)
+        oi = torch.empty((nq, k), dtype=torch.long, device=s.device)
+        _lib.check(_lib.lib().lzk_topk_merge64(s.data_ptr(), i.data_ptr(), nc, nq, k, os_.data_ptr(), oi.data_ptr(),
+                                               _lib.stream_ptr(s.device)), "lzk_topk_merge64")
+        return os_, oi
     big = torch.iinfo(torch.int64).max
     key_ids = torch.where(ids < 0, torch.full_like(ids, big), ids)
     o = torch.argsort(key_ids, dim=1, stable=True)

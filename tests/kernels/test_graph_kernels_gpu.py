@@ -340,3 +340,20 @@ def test_two_level_assign_gpu_matches_full():
     l_full, _ = assign(b(X), b(fine))
     l_two, _ = assign_two_level(b(X), b(fine), b(tops), top_of)
     assert (l_full.long() == l_two.long()).float().mean() > 0.995
+
+
+def test_device_csr_matches_host_build():
+    """K13: DeviceGraph.csr on the device equals the native host build
+    (same per-source arc order, self-loops once)."""
+    from lazzaro_amd.store.colstore import _rt
+
+    n, ne = 3000, 20000
+    e = _rand_edges(n, ne, 7, DEV)
+    e["src"][:50] = e["dst"][:50]  # self-loops
+    g = DeviceGraph.__new__(DeviceGraph)
+    g.device, g.n, g.edges = torch.device(DEV), n, e
+    off, adj, eid = g.csr()
+    ho, ha, he = _rt().build_csr(e["src"].cpu().numpy(), e["dst"].cpu().numpy(), n, True)
+    assert torch.equal(off.cpu(), torch.from_numpy(ho))
+    assert torch.equal(adj.cpu(), torch.from_numpy(ha))
+    assert torch.equal(eid.cpu(), torch.from_numpy(he))

@@ -447,3 +447,23 @@ def test_split_k_forward_matches():
     finally:
         SentenceEncoder.SPLITK = old
     assert ((a * b).sum(1) > 0.9995).all(), float((a * b).sum(1).min())
+
+
+@pytest.mark.parametrize("k", [1, 4, 10, 16, 32])
+def test_cross_rank_merge_kernel_matches_sort_merge(k):
+    """K2 across ranks: topk_merge64_kernel vs the two-argsort merge on the CPU
+    (64-bit global ids, tied scores, empty slots, lists from 8 'ranks')."""
+    from lazzaro_amd.parallel.sharded import merge_topk
+
+    g = torch.Generator().manual_seed(k)
+    nq, world, kk = 300, 8, 32
+    s = torch.randn(nq, world * kk, generator=g)
+    s[:, ::7] = 0.25  # ties broken by id
+    ids = torch.randperm(nq * world * kk, generator=g).view(nq, -1) * 1000003 + (1 << 33)
+    empty = torch.rand(nq, world * kk, generator=g) < 0.2
+    s[empty] = float("-inf")
+    ids[empty] = -1
+    rs, ri = merge_topk(s, ids, k)
+    gs, gi = merge_topk(s.cuda(), ids.cuda(), k)
+    assert torch.equal(ri, gi.cpu())
+    assert torch.equal(rs, gs.cpu())

@@ -121,3 +121,23 @@ def test_ingest_fixed_links_and_tombstones():
                    (4, 6, 0.5)])                 # chain: fact 0 -> fact 2 (fact 1 is a duplicate)
     assert got == want, got
     assert int(out["linked"]) == len(want)
+
+
+def test_csr_undirected_tensor_build_matches_native():
+    """The tensor-op CSR build DeviceGraph uses on the GPU equals the native
+    host build (arc order, self-loops once), run here on CPU tensors."""
+    import torch
+
+    from lazzaro_amd.index.device_graph import csr_undirected
+    from lazzaro_amd.store.colstore import _rt
+
+    g = torch.Generator().manual_seed(3)
+    n, ne = 500, 4000
+    src = torch.randint(0, n, (ne,), generator=g, dtype=torch.int32)
+    dst = torch.randint(0, n, (ne,), generator=g, dtype=torch.int32)
+    src[:20] = dst[:20]
+    off, adj, eid = csr_undirected(src, dst, n)
+    ho, ha, he = _rt().build_csr(src.numpy(), dst.numpy(), n, True)
+    assert torch.equal(off, torch.from_numpy(ho))
+    assert torch.equal(adj, torch.from_numpy(ha))
+    assert torch.equal(eid, torch.from_numpy(he))
