@@ -490,7 +490,9 @@ class ConsolidationMixin:
             not bool(((g.stored[:n] == 1) & (g.kind[:n] != NODE)).any()) and \
             not bool(((g.kind[:n] == NODE) & (g.stored[:n] == 0)).any())
         kq = max(LINK_TOPK, 1)
-        (gs, gr), (ws, wr) = g.cos_topk(Q, kq, link_mask, dual_label=codes)
+        # decisions read only entries above LINK_THRESHOLD (links: cos > 0.5;
+        # dedupe: top-1 > 0.95), so the scan may skip everything below it
+        (gs, gr), (ws, wr) = g.cos_topk(Q, kq, link_mask, dual_label=codes, min_score=LINK_THRESHOLD)
         Qd = Q.to(dev, torch.float64)
         qn = Qd.norm(dim=1, keepdim=True)
         Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))

@@ -81,6 +81,10 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
 FP8_MIN_Q, FP8_MIN_ROWS, FP8_MARGIN_Z = 256, 1 << 20, 8.0
+# cos_topk(min_score=): kernel threshold slack below min_score. Unit rows and
+# queries rounded to bf16 (relative 2^-9 each) move a cosine by at most
+# 2^-8 * sum|q_i x_i| <= 2^-8 ~ 0.0039, plus fp32 accumulation order.
+COS_FLOOR_SLACK = 0.01
 
 
 def _pad64(d: int) -> int:
@@ -1163,16 +1167,23 @@ class TenantGraph:
         q[:, : self.dim] = Qn.to(torch.bfloat16)
         return q
 
-    def cos_topk(self, Q: torch.Tensor, k: int, mask: torch.Tensor, dual_label: Optional[torch.Tensor] = None):
+    def cos_topk(self, Q: torch.Tensor, k: int, mask: torch.Tensor, dual_label: Optional[torch.Tensor] = None,
+                 min_score: Optional[float] = None):
         """Cosine top-k of each query row among rows where ``mask``. With
         ``dual_label`` (shard code per query) also returns the top-k restricted
         to rows of the query's shard, from the same scan. Scores are exact
         float64 (kernel candidates re-ranked). Returns (s, rows) or
-        ((s, rows), (s_shard, rows_shard))."""
-        with self.on_stream():
-            return self._cos_topk(Q, k, mask, dual_label)
+        ((s, rows), (s_shard, rows_shard)).
 
-    def _cos_topk(self, Q, k, mask, dual_label):
+        ``min_score``: the caller acts only on entries with cos >= min_score;
+        the GPU dual scan may then leave lower-scoring slots empty (-inf, -1)
+        instead of finding them. Every entry >= min_score is still returned
+        exactly (the kernel threshold is lowered by COS_FLOOR_SLACK, which
+        exceeds the bf16 score error of unit rows: |err| <= 2^-8)."""
+        with self.on_stream():
+            return self._cos_topk(Q, k, mask, dual_label, min_score)
+
+    def _cos_topk(self, Q, k, mask, dual_label, min_score=None):
         from ..ops.search import flat_topk, flat_topk_dual
         M = Q.shape[0]
         n = self.n
@@ -1191,8 +1202,9 @@ class TenantGraph:
             X = self.emb16[:n]
             if dual_label is not None:
                 ql = dual_label.to(dev, torch.int32).contiguous()
+                floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
                 (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
-                                                  bias=bias)
+                                                  bias=bias, floor=floor)
                 return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
             _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
             return self._rerank_cos(Qn, ra, k)

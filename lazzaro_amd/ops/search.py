@@ -397,7 +397,7 @@ def _spec_threshold_b(ts, thr_b, row_label, q_label, n_labels, N, S, k):
 
 
 def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_label, bias=None,
-                   alpha: float = 1.0, idx_offset: int = 0, n_labels: int = None):
+                   alpha: float = 1.0, idx_offset: int = 0, n_labels: int = None, floor: float = None):
     """Two searches of the same queries from ONE scan: the unfiltered top-k and
     the label-filtered top-k (label < 0 = any). Consolidation needs both --
     global dedupe/links and within-shard links (reference memory_system.py:
@@ -405,6 +405,11 @@ def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_lab
     the candidate path computes each score once and files it into two lists.
     ``n_labels`` (row labels in [0, n_labels)) enables the speculative
     list-B threshold (:func:`_spec_threshold_b`); results are exact either way.
+    ``floor``: the caller only needs entries scoring >= floor (consolidation
+    acts on cos > 0.5 only): both candidate thresholds are raised to it, so
+    the lists stay short and list B's label test almost never runs; slots
+    with no such entry come back as (-inf, -1). The caller lowers ``floor``
+    by its bf16 error allowance.
     Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
     if Q.dim() == 1:
         Q = Q[None, :]
@@ -432,6 +437,10 @@ def flat_topk_dual(X: torch.Tensor, Q: torch.Tensor, k: int, *, row_label, q_lab
         thr_b, need_b = _spec_threshold_b(ts, thr_b, row_label, q_label, int(n_labels), N, S, k)
     else:
         thr_a = _sample_threshold(X, Q, k, kslot, bias, None, None, alpha, S)
+    if floor is not None:
+        thr_a = thr_a.clamp_min(float(floor)).contiguous()
+        thr_b = thr_b.clamp_min(float(floor)).contiguous()
+        need_b = None
     cap = max(1024, 8 * kslot * S)
     ca = _cand_lists(dev, nq, cap, 0)
     cb = _cand_lists(dev, nq, cap, 1)
