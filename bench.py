@@ -133,7 +133,7 @@ def main():
     ap.add_argument("--recall-queries", type=int, default=256)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--prewarm-s", type=float, default=3.0, help="untimed GPU clock ramp before the warmup steps")
-    ap.add_argument("--consolidate-steps", type=int, default=5,
+    ap.add_argument("--consolidate-steps", type=int, default=10,
                     help="second half of the metric: timed consolidation steps on a --rows-node buffer (0 = skip)")
     ap.add_argument("--consolidate-convs", type=int, default=128, help="conversations per GPU per step")
     ap.add_argument("--no-persistent-graph", dest="persistent_graph", action="store_false",

@@ -10,6 +10,7 @@ Batching: ``batch_embed`` sorts texts by length and runs buckets of up to
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -17,6 +18,9 @@ import torch
 
 from ..models.encoder import GraphedEncoder, SentenceEncoder, get_config
 from ..utils.device import default_device
+
+# sub-batches (HIP streams) of a large-batch embed; bench/ab_embed_parts.py
+EMBED_PARTS = max(1, int(os.environ.get("LZK_EMBED_PARTS", "2")))
 
 
 class Tokenizer:
@@ -73,8 +77,8 @@ class OnDeviceEmbedder:
                 if g is None:
                     g = self._graphs[key] = GraphedEncoder(self.encoder, bb, sb, pad_to)
                 return g(ids, lens)
-        if B >= 512:  # large batches: two sub-batches on two streams fill each GEMM's tail
-            return self.encoder.forward_streams(ids, lens, pad_to=pad_to, parts=2)
+        if B >= 512:  # large batches: sub-batches on separate streams fill each GEMM's tail
+            return self.encoder.forward_streams(ids, lens, pad_to=pad_to, parts=EMBED_PARTS)
         return self.encoder.forward(ids, lens, pad_to=pad_to)
 
     def embed(self, text: str) -> List[float]:
