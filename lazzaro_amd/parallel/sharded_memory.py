@@ -63,8 +63,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..core.consolidation import (DECAY_RATE, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS, batch_dedupe,
-                                  batch_link_plan, salience_decayed)
+from ..core.consolidation import (DECAY_RATE, LINK_THRESHOLD, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS,
+                                  batch_dedupe, batch_link_plan, salience_decayed)
 from ..engine.tenant_graph import NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT, _seg_min, _seg_sum_count
 from ..ops import tenant_ops as T
 from ..utils.tracing import tracer
@@ -232,7 +232,8 @@ class ShardedMemorySystem:
         if g.n and g.num_nodes():
             n = g.n
             mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
-            (gs, gr), (ws, wr) = g.cos_topk(Q, k, mask, dual_label=codes)
+            # decisions read only entries above LINK_THRESHOLD (as in _scan_batch)
+            (gs, gr), (ws, wr) = g.cos_topk(Q, k, mask, dual_label=codes, min_score=LINK_THRESHOLD)
         else:
             gs = ws = torch.full((F, k), NEG_INF, dtype=torch.float64, device=dev)
             gr = wr = torch.full((F, k), -1, dtype=torch.long, device=dev)
