@@ -253,6 +253,7 @@ class TenantGraph:
 
     # rows of the mini-batch k-means refinement steps of cluster_pass
     CLUSTER_SAMPLE = 1 << 20
+    SAMPLE_TWO_LEVEL = os.environ.get("LZK_SAMPLE_ASSIGN", "two_level") != "full"
 
     # fp8 (e4m3) copy of the rows for the store search's candidate scan
     # (ops.search.flat_topk_fp8): rows are scaled by FP8_ROW_SCALE, which
@@ -1406,8 +1407,10 @@ class TenantGraph:
                 from ..index.kmeans import assign_two_level
                 T16, tof = prev["top_c16"], prev["top_of_fine"]
                 fa = lambda Xa, C16: assign_two_level(Xa, C16, T16, tof)  # noqa: E731
+            # the mini-batch steps: the same two-level assign (LZK_SAMPLE_ASSIGN=full: flat over all fine)
+            sa = fa if self.SAMPLE_TWO_LEVEL else None
             fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp,
-                                     full_assign=fa, comm=comm if dist else None)
+                                     full_assign=fa, sample_assign=sa, comm=comm if dist else None)
             init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
             tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
             lab = lab.long()

@@ -105,7 +105,8 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
 
 def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
            init: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-           sample: int = 0, full_assign=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+           sample: int = 0, full_assign=None,
+           sample_assign=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """X: unit rows [n, Dp] (bf16 on GPU). Returns (centroids fp32 [k, Dp],
     centroids bf16 [k, Dp], labels int32 [n]). ``mask`` (bool [n]): rows
     that take part (others get label -1 and do not move the centroids) --
@@ -116,7 +117,8 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
     so every row's label is exact for the returned centroids' predecessors as
     in the full algorithm -- at 10M rows x 4096 centroids a full assign is
     63 TFLOP, a 1M-row one 6.3. ``full_assign(X, C16)``: replaces the
-    assign of the full-data steps (e.g. :func:`assign_two_level`)."""
+    assign of the full-data steps (e.g. :func:`assign_two_level`);
+    ``sample_assign(Xs, C16)`` the same for the mini-batch steps."""
     n, Dp = X.shape
     dev = X.device
     if init is None and k <= 4096:
@@ -142,7 +144,7 @@ def kmeans(X: torch.Tensor, k: int, iters: int = 10, seed: int = 0, comm=None,
             g = torch.Generator(device=dev).manual_seed(seed * 7919 + it + 1)
             pick = torch.randint(0, n_part, (sample,), device=dev, generator=g)
             Xs = X[rows_all[pick] if rows_all is not None else pick]
-            ls, _ = assign(Xs, c16)
+            ls, _ = (sample_assign or assign)(Xs, c16)
             c32n, c16n, cnt = G.centroids(Xs, ls, k, normalize=not distributed, pad_to=Dp if X.is_cuda else 0)
             if distributed:
                 sums = c32n * cnt.clamp_min(1)[:, None].float()
