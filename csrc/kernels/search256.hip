@@ -498,6 +498,67 @@ __global__ __launch_bounds__(NT, 1) void flat_top1_kernel(const u16* __restrict_
   }
 }
 
+// Grouped top-1 (the two-level k-means assign in ONE launch): query group g
+// (the data rows whose nearest topic is g, given as row indices `qidx` into
+// Xq -- no gather of the rows) is scored only against its own centroid range
+// (centroids sorted by topic). Each block is one (centroid tile, query tile)
+// of one group, from a host-built table {c0, nc, p0, np}: centroid rows
+// [c0, c0 + min(256, nc)) x query positions [p0, p0 + min(256, np)).
+// Result per query position: packed (score, sorted centroid index), merged
+// with the same 64-bit atomicMax as flat_top1_kernel, so ties go to the
+// smaller centroid index -- identical to one flat_top1 per group.
+__global__ __launch_bounds__(NT, 1) void flat_top1_grouped_kernel(const u16* __restrict__ C, long ldc,
+                                                                  const u16* __restrict__ Xq, long ldx,
+                                                                  const int* __restrict__ qidx,
+                                                                  const int4* __restrict__ blocks, int D,
+                                                                  unsigned long long* __restrict__ best) {
+  extern __shared__ __attribute__((aligned(16))) u16 smem[];
+  const int4 bd = blocks[xcd_remap(blockIdx.x, gridDim.x)];
+  const int c0 = bd.x, nc = bd.y, p0 = bd.z, np = bd.w;
+  Stager st;
+  st.setup(C + (long)c0 * ldc, ldc, 0, nc, Xq, ldx, 0, 1);
+  {  // query operand: the indexed data rows (clamped to the tile's last query)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (wave * 2 + i) + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      LZK_DCHECK(qidx[p0 + min(row, np - 1)] >= 0);
+      st.src[2][i] = Xq + (long)qidx[p0 + min(row, np - 1)] * ldx + kc * 8;
+      st.src[3][i] = Xq + (long)qidx[p0 + min(128 + row, np - 1)] * ldx + kc * 8;
+    }
+  }
+  f32x4 acc[8][4];
+  mainloop(smem, st, D / BK, acc);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float m = LZK_NEG_INF;
+    int mr = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rb = wr * 128 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = acc[i][j][e];
+        if (rb + e < nc && v > m) { m = v; mr = rb + e; }
+      }
+    }
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float om = __shfl_xor(m, off);
+      const int orr = __shfl_xor(mr, off);
+      if (om > m || (om == m && orr < mr)) { m = om; mr = orr; }
+    }
+    const int q = wc * 64 + j * 16 + (lane & 15);
+    if ((lane >> 4) == 0 && q < np && mr < nc) atomicMax(best + p0 + q, top1_pack(m, c0 + mr));
+  }
+}
+
 __global__ __launch_bounds__(256) void top1_decode_kernel(const unsigned long long* __restrict__ best, int nq,
                                                           float* __restrict__ score, int* __restrict__ row) {
   const int q = blockIdx.x * 256 + threadIdx.x;
@@ -576,6 +637,27 @@ LZK_EXPORT int lzk_flat_top1(const void* X, long ldx, int nrows, const void* Qm,
   hipLaunchKernelGGL(flat_top1_kernel, dim3((unsigned)nblk), dim3(NT), LDS_BYTES, st, (const u16*)X, ldx, nrows,
                      (const u16*)Qm, ldq, nq, D, n_rt, best);
   hipLaunchKernelGGL(top1_decode_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, best, nq, score, row);
+  return (int)hipGetLastError();
+}
+
+// Grouped argmax (two-level k-means assign): blocks [nblk] int4 {c0, nc, p0,
+// np} built by the caller (every nc, np >= 1; c0 + nc <= centroid rows;
+// p0 + np <= npos; qidx[0, npos) valid rows of Xq). ws: [npos] u64 scratch.
+// score fp32 / pos int32 [npos]: best sorted-centroid index per query position.
+LZK_EXPORT int lzk_flat_top1_grouped(const void* C, long ldc, const void* Xq, long ldx, const int* qidx, int npos,
+                                     const void* blocks, int nblk, int D, void* ws, float* score, int* row,
+                                     void* stream) {
+  if (D % BK != 0 || npos <= 0 || nblk <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned long long* best = (unsigned long long*)ws;
+  hipError_t e = hipMemsetAsync(best, 0, (size_t)npos * 8, st);
+  if (e != hipSuccess) return (int)e;
+  (void)hipFuncSetAttribute((const void*)flat_top1_grouped_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_BYTES);
+  hipLaunchKernelGGL(flat_top1_grouped_kernel, dim3((unsigned)nblk), dim3(NT), LDS_BYTES, st, (const u16*)C, ldc,
+                     (const u16*)Xq, ldx, qidx, (const int4*)blocks, D, best);
+  hipLaunchKernelGGL(top1_decode_kernel, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, st, best, npos, score,
+                     row);
   return (int)hipGetLastError();
 }
 

@@ -37,6 +37,67 @@ def assign(X: torch.Tensor, C16: torch.Tensor, chunk: int = 1 << 20) -> Tuple[to
     return torch.cat(labs).to(torch.int32), torch.cat(scs)
 
 
+# two-level assign in one grouped launch (flat_top1_grouped_kernel) instead of
+# a gather + flat_top1 per topic group; LZK_GROUPED_ASSIGN=0 for the loop
+GROUPED = os.environ.get("LZK_GROUPED_ASSIGN", "1") != "0"
+GROUP_TILE = 256  # the 256x256 pipeline's tile edge (lzk_g256.h BM = BN)
+
+
+def _assign_grouped(X: torch.Tensor, C16: torch.Tensor, tl: torch.Tensor, top_of: torch.Tensor,
+                    t: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Rows sorted by topic (positions), fine centroids sorted by topic; one
+    block per (centroid tile, query tile) of every topic group. The kernel
+    reads each row straight from X by index (no gather) and returns, per
+    position, the best sorted-centroid index with flat_top1's tie order."""
+    import numpy as np
+
+    from ..ops import _lib
+
+    n = X.shape[0]
+    dev = X.device
+    fo = torch.argsort(top_of, stable=True)
+    fcnt = np.asarray(torch.bincount(top_of, minlength=t)[:t].tolist(), dtype=np.int64)
+    ro = torch.argsort(tl, stable=True)
+    rcnt = np.asarray(torch.bincount(tl, minlength=t)[:t].tolist(), dtype=np.int64)
+    fstart = np.concatenate([[0], np.cumsum(fcnt)[:-1]])
+    rstart = np.concatenate([[0], np.cumsum(rcnt)[:-1]])
+    T = GROUP_TILE
+    parts = []
+    for c in np.nonzero((fcnt > 0) & (rcnt > 0))[0]:
+        nf, nr = int(fcnt[c]), int(rcnt[c])
+        rt = np.arange(0, nf, T)
+        qt = np.arange(0, nr, T)
+        q, r = np.meshgrid(qt, rt, indexing="ij")  # centroid tile fastest: a query tile's blocks are adjacent
+        q, r = q.ravel(), r.ravel()
+        parts.append(np.stack([fstart[c] + r, nf - r, rstart[c] + q, nr - q], 1))
+    Cs = C16[fo].contiguous()
+    qidx = ro.to(torch.int32).contiguous()
+    score = torch.full((n,), float("-inf"), dtype=torch.float32, device=dev)
+    pos = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    if parts:
+        blk = np.concatenate(parts).astype(np.int32)
+        assert blk[:, 1].min() >= 1 and blk[:, 3].min() >= 1
+        assert int((blk[:, 0] + np.minimum(blk[:, 1], T)).max()) <= Cs.shape[0]
+        assert int((blk[:, 2] + np.minimum(blk[:, 3], T)).max()) <= n
+        blocks = torch.from_numpy(blk).to(dev)
+        ws = torch.empty(n, dtype=torch.int64, device=dev)
+        _lib.check(_lib.lib().lzk_flat_top1_grouped(Cs.data_ptr(), Cs.stride(0), X.data_ptr(), X.stride(0),
+                                                     qidx.data_ptr(), n, blocks.data_ptr(), int(blk.shape[0]),
+                                                     X.shape[1], ws.data_ptr(), score.data_ptr(), pos.data_ptr(),
+                                                     _lib.stream_ptr(dev)), "lzk_flat_top1_grouped")
+    lab = torch.empty(n, dtype=torch.int32, device=dev)
+    sc = torch.empty(n, dtype=torch.float32, device=dev)
+    lab[ro] = fo[pos.long().clamp_min(0)].to(torch.int32)
+    sc[ro] = score
+    lone = np.nonzero((fcnt == 0) & (rcnt > 0))[0]
+    if lone.size:  # rows whose topic has no fine centroid: the full search
+        lone_t = torch.as_tensor(lone, device=dev)
+        rr = torch.nonzero(torch.isin(tl, lone_t)).flatten()
+        li, si = assign(X[rr].contiguous(), C16)
+        lab[rr], sc[rr] = li.to(torch.int32), si.float()
+    return lab, sc
+
+
 def assign_two_level(X: torch.Tensor, C16: torch.Tensor, T16: torch.Tensor, top_of: torch.Tensor,
                      chunk: int = 1 << 22) -> Tuple[torch.Tensor, torch.Tensor]:
     """Nearest fine centroid per row, searched only under the row's nearest
@@ -51,6 +112,8 @@ def assign_two_level(X: torch.Tensor, C16: torch.Tensor, T16: torch.Tensor, top_
     tl, _ = assign(X, T16)
     tl = tl.long()
     t = T16.shape[0]
+    if GROUPED and X.is_cuda and X.dtype == torch.bfloat16 and n > 0:
+        return _assign_grouped(X, C16, tl, top_of.long(), t)
     fo = torch.argsort(top_of.long(), stable=True)
     fcnt = torch.bincount(top_of.long(), minlength=t).tolist()
     ro = torch.argsort(tl, stable=True)

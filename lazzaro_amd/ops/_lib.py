@@ -43,6 +43,7 @@ _SIGS = {
     "lzk_flat_cand_dual": (I, [P, L, I, P, L, I, I, P, P, P, F, P, P, I, P, P, P, P, P, P, P, I, P, P]),
     "lzk_flat_cand": (I, [P, L, I, P, L, I, I, P, P, P, F, P, I, P, P, P, P, I, P, P]),
     "lzk_flat_top1": (I, [P, L, I, P, L, I, I, P, P, P, P]),
+    "lzk_flat_top1_grouped": (I, [P, L, P, L, P, I, P, I, I, P, P, P, P]),
     "lzk_cand_gather": (I, [P, I, P, I, I, I, P, P, P, P, P, P, P]),
     "lzk_cand_grid": (I, [I, I, I]),
     "lzk_cand_select": (I, [P, P, P, I, I, I, I, L, P, P, P, P, P]),

@@ -357,3 +357,32 @@ def test_device_csr_matches_host_build():
     assert torch.equal(off.cpu(), torch.from_numpy(ho))
     assert torch.equal(adj.cpu(), torch.from_numpy(ha))
     assert torch.equal(eid.cpu(), torch.from_numpy(he))
+
+
+def test_grouped_two_level_assign_matches_group_loop():
+    """flat_top1_grouped_kernel (one launch, rows read by index) equals the
+    gather + flat_top1 per topic group, bit for bit: labels and scores,
+    including topics with > 256 fine centroids (several centroid tiles) and
+    a topic with none (full-search fallback); scores match an fp32 dot."""
+    import lazzaro_amd.index.kmeans as KM
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    n, d, k, t = 150_000, 768, 1100, 24
+    X = torch.nn.functional.normalize(torch.randn(n, d, generator=g), dim=1).to(torch.bfloat16).to(DEV)
+    C = torch.nn.functional.normalize(torch.randn(k, d, generator=g), dim=1).to(torch.bfloat16).to(DEV)
+    T = torch.nn.functional.normalize(torch.randn(t, d, generator=g), dim=1).to(torch.bfloat16).to(DEV)
+    top_of = torch.randint(1, t, (k,), generator=g)
+    top_of[:300] = 5  # one topic with 300+ fine centroids: two centroid tiles
+    top_of[top_of == 0] = 1  # topic 0 has no fine centroid
+    top_of = top_of.to(DEV)
+    try:
+        KM.GROUPED = True
+        lg, sg = KM.assign_two_level(X, C, T, top_of)
+        KM.GROUPED = False
+        ll, sl = KM.assign_two_level(X, C, T, top_of)
+    finally:
+        KM.GROUPED = True
+    assert torch.equal(lg, ll)
+    assert torch.equal(sg, sl)
+    ref = (X.float() * C[lg.long()].float()).sum(1)
+    assert torch.allclose(sg, ref, atol=1e-3)
