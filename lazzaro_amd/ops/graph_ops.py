@@ -223,7 +223,10 @@ def _seg_sum_sorted(X: torch.Tensor, label: torch.Tensor, C: int):
     workgroup per cluster streams its rows (lzk_seg_sum_sorted)."""
     n, D = X.shape
     key = torch.where(label >= 0, label, torch.full_like(label, C))
-    order = torch.argsort(key, stable=True).contiguous()
+    # the radix sort's passes scale with the key width: 16-bit keys (C < 32767,
+    # e.g. 4096 k-means clusters) take half the passes of int32 ones; a
+    # stable sort of equal key values gives the same order either way
+    order = torch.argsort(key.to(torch.int16) if C < 32767 else key, stable=True).contiguous()
     off = torch.zeros(C + 2, dtype=torch.int64, device=X.device)
     off[1:] = torch.cumsum(torch.bincount(key.long(), minlength=C + 1)[: C + 1], 0)
     sums = torch.empty((C, D), dtype=torch.float32, device=X.device)
