@@ -1,16 +1,11 @@
-// Device graph-maintenance kernels.
-//
-// Replaces the reference's per-object Python loops over the memory graph:
-//   decay + prune     memory_shard.py:64-84, memory_system.py:624-630, :991   (K10)
-//   eviction scoring  memory_system.py:535-578                                (K11)
+// Graph kernels shared by the tenant engine.
+// The per-edge / per-node maintenance kernels (decay + prune, eviction
+// scoring, neighbour boost, touch) live in tenant.hip, on the TenantGraph
+// columns; this file holds the whole-graph algorithms:
 //   connected comps   buffer_graph.py:99-120 (recursive DFS)                  (K9)
-//   neighbour boost   memory_system.py:242-260, buffer_graph.py:79-85         (K12)
 //   all-pairs merge   memory_system.py:1065-1120 (intended semantics)         (K7)
 //   centroids         memory_system.py:916-917 (np.mean) / k-means update     (K8)
-//
-// Graph layout: structure-of-arrays in HBM. Nodes: salience f32, access i32,
-// last_accessed f64, alive u8. Edges (COO): src/dst i32, weight f32,
-// co_occurrence i32, last_updated f64.
+// plus the block-count scan used by every stable compaction.
 #include "lzk_tile.h"
 
 LZK_DEBUG_STATE(graph)
@@ -18,65 +13,6 @@ LZK_DEBUG_STATE(graph)
 namespace {
 
 constexpr int NTB = 256;
-
-// ------------------------------------------------------------------ K10
-// Pass 1: decay edge weights, flag survivors (w >= thr and both endpoints
-// alive), count survivors per block; the same launch decays node salience
-// (floor 0.2) in a grid-stride loop over nodes.
-__global__ __launch_bounds__(NTB) void decay_flag_kernel(
-    float* __restrict__ w, const int* __restrict__ src, const int* __restrict__ dst, long ne,
-    const unsigned char* __restrict__ alive, float keep, float thr, unsigned char* __restrict__ flag,
-    int* __restrict__ block_cnt, float* __restrict__ sal, long nn, float floor_) {
-  __shared__ int wsum[NTB / 64];
-  const long e = (long)blockIdx.x * NTB + threadIdx.x;
-  int f = 0;
-  if (e < ne) {
-    float v = w[e] * keep;
-    w[e] = v;
-    f = (v >= thr) && (!alive || (alive[src[e]] && alive[dst[e]]));
-    flag[e] = (unsigned char)f;
-  }
-  unsigned long long bal = __ballot(f);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(bal);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < NTB / 64; ++i) s += wsum[i];
-    block_cnt[blockIdx.x] = s;
-  }
-  if (sal) {
-    for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
-      float s = sal[i];
-      sal[i] = s > floor_ ? floor_ + (s - floor_) * keep : floor_;
-    }
-  }
-}
-
-// flag survivors without decaying (eviction: drop edges touching dead nodes)
-__global__ __launch_bounds__(NTB) void salience_decay_kernel(float* __restrict__ sal, long nn, float keep,
-                                                             float floor_) {
-  for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
-    const float s = sal[i];
-    sal[i] = s > floor_ ? floor_ + (s - floor_) * keep : floor_;
-  }
-}
-
-__global__ __launch_bounds__(NTB) void flag_alive_kernel(const int* __restrict__ src, const int* __restrict__ dst,
-                                                         long ne, const unsigned char* __restrict__ alive,
-                                                         unsigned char* __restrict__ flag, int* __restrict__ block_cnt) {
-  __shared__ int wsum[NTB / 64];
-  const long e = (long)blockIdx.x * NTB + threadIdx.x;
-  int f = 0;
-  if (e < ne) {
-    f = alive[src[e]] && alive[dst[e]];
-    flag[e] = (unsigned char)f;
-  }
-  unsigned long long bal = __ballot(f);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = __popcll(bal);
-  __syncthreads();
-  if (threadIdx.x == 0) block_cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-}
 
 // exclusive scan of per-block counts (single workgroup, chunked)
 __global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int n, int* __restrict__ total) {
@@ -101,54 +37,6 @@ __global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int n
     __syncthreads();
   }
   if (threadIdx.x == 0) *total = carry;
-}
-
-// Pass 2: stable scatter of surviving edges into the output arrays.
-__global__ __launch_bounds__(NTB) void compact_kernel(
-    const unsigned char* __restrict__ flag, const int* __restrict__ block_off, long ne,
-    const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ w,
-    const int* __restrict__ co, const double* __restrict__ lu, int* __restrict__ osrc, int* __restrict__ odst,
-    float* __restrict__ ow, int* __restrict__ oco, double* __restrict__ olu) {
-  __shared__ int wpre[NTB / 64];
-  const long e = (long)blockIdx.x * NTB + threadIdx.x;
-  const int f = (e < ne) ? flag[e] : 0;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned long long bal = __ballot(f);
-  int before = __popcll(bal & ((1ull << lane) - 1ull));
-  if (lane == 0) wpre[wv] = __popcll(bal);
-  __syncthreads();
-  int off = block_off[blockIdx.x];
-  for (int i = 0; i < wv; ++i) off += wpre[i];
-  if (f) {
-    int o = off + before;
-    osrc[o] = src[e];
-    odst[o] = dst[e];
-    ow[o] = w[e];
-    if (co) oco[o] = co[e];
-    if (lu) olu[o] = lu[e];
-  }
-}
-
-// ------------------------------------------------------------------ K11
-// importance = 0.5*sal + 0.3*min(1, acc/10) + 0.2/(1 + days_since_access);
-// dead or protected (super) nodes get +inf so they are never selected.
-__global__ __launch_bounds__(NTB) void importance_kernel(const float* __restrict__ sal, const int* __restrict__ acc,
-                                                         const double* __restrict__ last, const unsigned char* __restrict__ alive,
-                                                         const unsigned char* __restrict__ protect, long n, double now,
-                                                         float* __restrict__ out) {
-  const long i = (long)blockIdx.x * NTB + threadIdx.x;
-  if (i >= n) return;
-  if ((alive && !alive[i]) || (protect && protect[i])) { out[i] = __builtin_huge_valf(); return; }
-  double days = (now - last[i]) / 86400.0;
-  double v = 0.5 * (double)sal[i] + 0.3 * fmin(1.0, (double)acc[i] / 10.0) + 0.2 / (1.0 + days);
-  out[i] = (float)v;
-}
-
-__global__ __launch_bounds__(NTB) void mark_dead_kernel(const long* __restrict__ idx, long n, unsigned char* __restrict__ alive) {
-  const long i = (long)blockIdx.x * NTB + threadIdx.x;
-  if (i >= n) return;
-  LZK_DCHECK(idx[i] >= 0);
-  alive[idx[i]] = 0;
 }
 
 // ------------------------------------------------------------------ K9
@@ -226,31 +114,6 @@ __global__ __launch_bounds__(NTB) void cc_compress_kernel(int* __restrict__ pare
   if (i >= n) return;
   int r = find_root(parent, (int)i);
   parent[i] = r;
-}
-
-// ------------------------------------------------------------------ K12
-// Boost neighbours of the retrieved seeds over an undirected CSR:
-// neighbours with w >= min_w (excluding seeds) get last_accessed = now and
-// salience = min(1, s + delta); a flag makes the boost idempotent per node.
-__global__ __launch_bounds__(64) void neighbor_boost_kernel(const long* __restrict__ off, const int* __restrict__ adj,
-                                                            const int* __restrict__ eid, const float* __restrict__ w,
-                                                            const int* __restrict__ seeds, int nseeds, float min_w,
-                                                            double now, float delta, float* __restrict__ sal,
-                                                            double* __restrict__ last, int* __restrict__ flag,
-                                                            int* __restrict__ nboost) {
-  const int s = seeds[blockIdx.x];
-  for (long p = off[s] + threadIdx.x; p < off[s + 1]; p += 64) {
-    int nb = adj[p];
-    if (w[eid[p]] < min_w) continue;
-    bool is_seed = false;
-    for (int j = 0; j < nseeds; ++j) is_seed |= (seeds[j] == nb);
-    if (is_seed) continue;
-    if (atomicExch(&flag[nb], 1) == 0) {
-      sal[nb] = fminf(1.f, sal[nb] + delta);
-      last[nb] = now;
-      atomicAdd(nboost, 1);
-    }
-  }
 }
 
 // ------------------------------------------------------------------ K7
@@ -384,62 +247,8 @@ inline dim3 blocks_for(long n, int per = NTB) { return dim3((unsigned)((n + per 
 
 }  // namespace
 
-// ---------------------------------------------------------------- C ABI
-LZK_EXPORT int lzk_decay_flag(float* w, const int* src, const int* dst, long ne, const unsigned char* alive,
-                              float rate, float thr, unsigned char* flag, int* block_cnt, float* sal, long nn,
-                              float floor_, void* stream) {
-  long nb = (ne + NTB - 1) / NTB;
-  if (nb == 0) nb = 1;
-  // The node-salience decay rides in the edge launch only while that grid is
-  // large enough to stream the nodes; a pruned-down edge list (a few blocks)
-  // would leave 10^7 nodes to a handful of workgroups, so it gets its own
-  // right-sized grid-stride launch instead.
-  const long node_blocks = (nn + 4L * NTB - 1) / (4L * NTB);
-  const bool fused = nb >= node_blocks || nb >= 2048;
-  hipLaunchKernelGGL(decay_flag_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, w, src, dst, ne, alive,
-                     1.f - rate, thr, flag, block_cnt, fused ? sal : (float*)nullptr, nn, floor_);
-  if (!fused && sal && nn > 0) {
-    const long g = node_blocks < 4096 ? node_blocks : 4096;
-    hipLaunchKernelGGL(salience_decay_kernel, dim3((unsigned)g), dim3(NTB), 0, (hipStream_t)stream, sal, nn,
-                       1.f - rate, floor_);
-  }
-  return (int)hipGetLastError();
-}
-
-LZK_EXPORT int lzk_flag_alive(const int* src, const int* dst, long ne, const unsigned char* alive, unsigned char* flag,
-                              int* block_cnt, void* stream) {
-  long nb = (ne + NTB - 1) / NTB;
-  if (nb == 0) nb = 1;
-  hipLaunchKernelGGL(flag_alive_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, src, dst, ne, alive,
-                     flag, block_cnt);
-  return (int)hipGetLastError();
-}
-
 LZK_EXPORT int lzk_scan_blocks(int* cnt, int n, int* total, void* stream) {
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, cnt, n, total);
-  return (int)hipGetLastError();
-}
-
-LZK_EXPORT int lzk_compact_edges(const unsigned char* flag, const int* block_off, long ne, const int* src,
-                                 const int* dst, const float* w, const int* co, const double* lu, int* osrc,
-                                 int* odst, float* ow, int* oco, double* olu, void* stream) {
-  if (ne == 0) return 0;
-  hipLaunchKernelGGL(compact_kernel, blocks_for(ne), dim3(NTB), 0, (hipStream_t)stream, flag, block_off, ne, src, dst,
-                     w, co, lu, osrc, odst, ow, oco, olu);
-  return (int)hipGetLastError();
-}
-
-LZK_EXPORT int lzk_importance(const float* sal, const int* acc, const double* last, const unsigned char* alive,
-                              const unsigned char* protect, long n, double now, float* out, void* stream) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(importance_kernel, blocks_for(n), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last, alive,
-                     protect, n, now, out);
-  return (int)hipGetLastError();
-}
-
-LZK_EXPORT int lzk_mark_dead(const long* idx, long n, unsigned char* alive, void* stream) {
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(mark_dead_kernel, blocks_for(n), dim3(NTB), 0, (hipStream_t)stream, idx, n, alive);
   return (int)hipGetLastError();
 }
 
@@ -464,15 +273,6 @@ LZK_EXPORT int lzk_uf_union(const int* src, const int* dst, long ne, const float
 LZK_EXPORT int lzk_cc_compress(int* parent, long n, void* stream) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(cc_compress_kernel, blocks_for(n), dim3(NTB), 0, (hipStream_t)stream, parent, n);
-  return (int)hipGetLastError();
-}
-
-LZK_EXPORT int lzk_neighbor_boost(const long* off, const int* adj, const int* eid, const float* w, const int* seeds,
-                                  int nseeds, float min_w, double now, float delta, float* sal, double* last,
-                                  int* flag, int* nboost, void* stream) {
-  if (nseeds == 0) return 0;
-  hipLaunchKernelGGL(neighbor_boost_kernel, dim3(nseeds), dim3(64), 0, (hipStream_t)stream, off, adj, eid, w, seeds,
-                     nseeds, min_w, now, delta, sal, last, flag, nboost);
   return (int)hipGetLastError();
 }
 

@@ -13,7 +13,7 @@ Behavioural parity notes:
 * ``get_connected_components`` returns the same sets as the reference's
   recursive DFS but runs iteratively, so a 1,500-node chain no longer hits
   ``RecursionError`` (SURVEY.md §6 probe, reference :107-112). Device-scale
-  graphs use the ``cc_label_prop`` HIP kernel via ``index.device_graph``.
+  graphs use the ``uf_union_kernel`` union-find (``TenantGraph.component_digest``).
 """
 from __future__ import annotations
 

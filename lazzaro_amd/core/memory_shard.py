@@ -11,8 +11,8 @@ prune_weak_edges/size``). Differences that are engine-level, not behavioural:
   the same (edge-insertion) order. Direct ``del shard.edges[k]`` keeps working.
 * decay/prune keep the reference's arithmetic exactly (edge ``w *= 1-r``;
   salience ``0.2 + (s-0.2)(1-r)`` with floor 0.2; prune ``w < thr``). Bulk
-  decay/prune of large device-resident graphs runs in the fused HIP kernel
-  (``ops.graph.decay_prune``), see :mod:`lazzaro_amd.index.device_graph`.
+  decay/prune of a tenant's device-resident graph runs in the fused HIP
+  kernel ``tg_decay_kernel`` (``ops.tenant_ops.decay``, ``TenantGraph.decay``).
 """
 from __future__ import annotations
 

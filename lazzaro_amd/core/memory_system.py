@@ -129,6 +129,9 @@ class MemorySystem(ConsolidationMixin):
             self.embedder = _default_local_embedder()
 
         self.profile = Profile()
+        # a store passed in may be shared by many tenants (the service's
+        # factory): close() then only unbinds this tenant's graph from it
+        self._owns_store = store is None
         self.store = store if store is not None else HBMStore(db_dir=db_dir, device=device, metric=metric,
                                                               index=index, **(index_params or {}))
         self.vector_store = self.store
@@ -1189,8 +1192,13 @@ Be clinical yet insightful. Do not include conversational filler."""
         if self._writer is not None:
             self.flush_persistence()
             self._writer.shutdown(wait=True)
-        if hasattr(self, "store") and self.store is not None:
-            self.store.close()
+        if getattr(self, "store", None) is None:
+            return
+        detach = getattr(type(self.store), "detach", None)
+        if getattr(self, "_owns_store", True) or detach is None:
+            self.store.close()  # reference :1545-1550 (a third-party store is closed as there)
+        elif self.store.bound_graph(self.user_id) is self.graph:
+            self.store.detach(self.user_id)
 
 
 # ---------------------------------------------------------------- columnar I/O

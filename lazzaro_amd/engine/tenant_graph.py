@@ -979,9 +979,18 @@ class TenantGraph:
         if not rows:
             return
         now = time.time() if now is None else now
+        # tg_touch_kernel updates each listed row with plain stores, so a row
+        # listed twice in one launch would count once: a repeated row is
+        # applied in a further launch per repeat (the reference's
+        # update_access per occurrence, buffer_graph.py:79-85)
         with self.on_stream():
-            T.touch(torch.as_tensor(rows, dtype=torch.long).to(self.device), self.acc, self.last, self.sal,
-                    self.dirty, now)
+            while rows:
+                seen, rest = set(), []
+                for r in rows:
+                    (rest.append(r) if r in seen else seen.add(r))
+                T.touch(torch.as_tensor(list(dict.fromkeys(rows)), dtype=torch.long).to(self.device), self.acc,
+                        self.last, self.sal, self.dirty, now)
+                rows = rest
         self._bump()
 
     def components(self) -> List[np.ndarray]:

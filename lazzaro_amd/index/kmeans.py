@@ -53,6 +53,8 @@ def _assign_grouped(X: torch.Tensor, C16: torch.Tensor, tl: torch.Tensor, top_of
 
     from ..ops import _lib
 
+    if X.dim() != 2 or X.stride(1) != 1:  # the kernel reads rows by index at stride ldx, unit column stride
+        X = X.contiguous()
     n = X.shape[0]
     dev = X.device
     fo = torch.argsort(top_of, stable=True)
@@ -76,9 +78,14 @@ def _assign_grouped(X: torch.Tensor, C16: torch.Tensor, tl: torch.Tensor, top_of
     pos = torch.full((n,), -1, dtype=torch.int32, device=dev)
     if parts:
         blk = np.concatenate(parts).astype(np.int32)
-        assert blk[:, 1].min() >= 1 and blk[:, 3].min() >= 1
-        assert int((blk[:, 0] + np.minimum(blk[:, 1], T)).max()) <= Cs.shape[0]
-        assert int((blk[:, 2] + np.minimum(blk[:, 3], T)).max()) <= n
+        # the kernel reads centroid rows [c0, c0+min(nc,T)) and qidx[p0, p0+min(np,T)):
+        # checked here, not by assert (python -O must not remove a bounds check)
+        if blk[:, 1].min() < 1 or blk[:, 3].min() < 1:
+            raise ValueError("grouped assign: empty block in the block table")
+        if int((blk[:, 0] + np.minimum(blk[:, 1], T)).max()) > Cs.shape[0]:
+            raise ValueError("grouped assign: centroid range past the centroid matrix")
+        if int((blk[:, 2] + np.minimum(blk[:, 3], T)).max()) > n:
+            raise ValueError("grouped assign: query range past the row index")
         blocks = torch.from_numpy(blk).to(dev)
         ws = torch.empty(n, dtype=torch.int64, device=dev)
         _lib.check(_lib.lib().lzk_flat_top1_grouped(Cs.data_ptr(), Cs.stride(0), X.data_ptr(), X.stride(0),

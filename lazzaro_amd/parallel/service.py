@@ -205,14 +205,18 @@ class DistributedMemoryService:
         equal to ``serve`` of that round."""
         prev = None
         for reqs in rounds:
-            h = self._serve_submit(reqs)
+            h = self._serve_submit(reqs, prev)
             if prev is not None:
                 yield self._serve_finish(prev)
             prev = h
         if prev is not None:
             yield self._serve_finish(prev)
 
-    def _serve_submit(self, requests: Sequence[Tuple]):
+    def _serve_submit(self, requests: Sequence[Tuple], prev=None):
+        """Route and start one round. ``prev``: the still-unfinished state of
+        the previous round (serve_stream) -- its batched search is completed
+        locally before a mutating request runs on any of its tenants, so the
+        rows it gathered are mapped to nodes before they can move."""
         comm = self.comm
         out_req: List[List] = [[] for _ in range(comm.world)]
         for i, req in enumerate(requests):
@@ -239,9 +243,12 @@ class DistributedMemoryService:
                     continue
                 if any(p[2] == user for p in pending):
                     flush()
+                if prev is not None and prev[3] is not None and prev[3][0] != "done" and \
+                        any(p[2] == user for p in prev[2]):
+                    prev[3] = ("done", self._search_finish(prev[3]))
                 replies[src].append([i, _jsonable(getattr(self.system(user), method)(*args))])
         handle = self._search_submit(pending) if pending else None
-        return len(requests), replies, list(pending), handle
+        return [len(requests), replies, list(pending), handle]
 
     def _serve_finish(self, state) -> List:
         n, replies, pending, handle = state

@@ -82,3 +82,66 @@ def test_serve_stream_equals_serve(tmp_path):
     got = list(svc.serve_stream(rounds))
     assert got == want
     svc.close()
+
+
+def _seeded_service(tmp_path, emb, users, store=None):
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import LocalLLM
+    from lazzaro_amd.parallel import Communicator
+    from lazzaro_amd.parallel.service import DistributedMemoryService
+
+    def factory(user, load_from_disk=True):
+        return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, enable_async=False,
+                            db_dir=str(tmp_path), user_id=user, device="cuda", load_from_disk=load_from_disk,
+                            store=store, max_buffer_size=60)
+    svc = DistributedMemoryService(Communicator.local(torch.device("cuda")), factory)
+    for j, u in enumerate(users):
+        g = svc.system(u).graph
+        texts = [f"{u} fact {i}" for i in range(40 + 9 * j)]
+        g.add_nodes([f"{u}_{i}" for i in range(len(texts))], texts, torch.tensor(emb.batch_embed(texts), device="cuda"),
+                    shard=g.shard_id("work"), stored=True)
+    return svc
+
+
+def test_serve_stream_with_mutations_equals_serve(tmp_path):
+    """Rounds that mix searches with mutating requests (a conversation whose
+    end evicts rows past max_buffer_size) on the same tenants: serve_stream
+    finishes the previous round's batched search before mutating one of its
+    tenants, so every round equals serve() on an identical replica."""
+    emb = RandEmbedder()
+    users = [f"m{i}" for i in range(6)]
+    rng = np.random.default_rng(3)
+    rounds = []
+    for r in range(6):
+        rr = [(users[int(rng.integers(6))], "search_memories", f"r{r} q{q}", 4) for q in range(24)]
+        u = users[r % 6]
+        rr += [(u, "start_conversation"), (u, "chat", f"{u} round {r}: I work on a project deadline."),
+               (u, "end_conversation")]
+        rounds.append(rr)
+    a = _seeded_service(tmp_path / "a", emb, users)
+    want = [a.serve(r) for r in rounds]
+    a.close()
+    b = _seeded_service(tmp_path / "b", emb, users)
+    got = list(b.serve_stream(rounds))
+    b.close()
+    strip = lambda v: [x for x in v if not isinstance(x, str)]  # status strings carry timings
+    assert [strip(x) for x in got] == [strip(x) for x in want]
+
+
+def test_shared_store_survives_tenant_release(tmp_path):
+    """One HBMStore shared by every tenant (the service's setup): releasing a
+    tenant (LRU, max_resident) unbinds only that tenant's graph, so the fused
+    multi-tenant search keeps serving the others."""
+    from lazzaro_amd.core.vector_store import HBMStore
+    emb = RandEmbedder()
+    store = HBMStore(db_dir=str(tmp_path / "db"), device=torch.device("cuda"))
+    users = [f"r{i}" for i in range(4)]
+    svc = _seeded_service(tmp_path, emb, users, store=store)
+    svc.max_resident = 3
+    svc.system("extra")  # releases r0
+    for u in users[1:]:
+        assert store.bound_graph(u) is svc.systems[u].graph
+        assert svc.systems[u]._store_binds_graph()
+    got = svc.serve([(u, "search_memories", "fact 3", 3) for u in users[1:]])
+    assert all(len(x) == 3 for x in got)
+    svc.close()

@@ -56,3 +56,31 @@ def test_store_search_nodes_multi(tmp_path):
     got = st.search_nodes_multi(qs, users, limit=3)
     want = [st.search_nodes(q, user_id=u, limit=3) for q, u in zip(qs, users)]
     assert got == want and got[3] == []
+
+
+def test_shared_store_release_keeps_other_tenants_bound(tmp_path):
+    """MemorySystem.close() on a tenant whose store was passed in
+    (one HBMStore shared by the service's tenants) unbinds only that tenant;
+    the store itself and the other tenants' graph bindings stay."""
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    from lazzaro_amd.parallel import Communicator
+    from lazzaro_amd.parallel.service import DistributedMemoryService
+    store = HBMStore(db_dir=str(tmp_path), device="cpu")
+    emb = HashEmbedder(dim=32)
+
+    def factory(user, load_from_disk=True):
+        return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, enable_async=False, store=store,
+                            db_dir=str(tmp_path), user_id=user, device="cpu", load_from_disk=load_from_disk)
+    svc = DistributedMemoryService(Communicator.local(), factory, max_resident=2)
+    for u in ("a", "b", "c"):  # building c releases a (LRU)
+        svc.serve([(u, "start_conversation"), (u, "chat", f"{u} works on a project with a deadline."),
+                   (u, "end_conversation")])
+    assert sorted(svc.systems) == ["b", "c"]
+    for u in ("b", "c"):
+        assert store.bound_graph(u) is svc.systems[u].graph and svc.systems[u]._store_binds_graph()
+    assert store.bound_graph("a") is None
+    # a comes back from the store with its memory
+    got = svc.serve([("a", "search_memories", "project deadline", 2)])[0]
+    assert got and all(n["id"].startswith("node_") for n in got)
+    svc.close()
