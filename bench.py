@@ -39,13 +39,32 @@ line (``--consolidate-steps``): ``MemorySystem.consolidate_batch`` on a
 run_consolidation, k-means hierarchy and the persistence commit, all timed
 (bench/bench_consolidate.py).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 launch with
-torch.distributed.run (one rank per GPU, RCCL backend).
+Multi-GPU work inside the JSON line (all timed, every rank, RCCL over xGMI):
+
+* ``serving.routed_*``: the same query stream, but each front end's queries go
+  to tenants on ALL ranks ((N-1)/N remote): embed on the receiving rank, one
+  all-to-all of packed [embedding | tenant key | limit] rows to the owners,
+  the owners' store search, one all-to-all of [score | row] back
+  (``DistributedMemoryService.search_routed``; reference per-user flow
+  memory_system.py:1460-1472).
+* ``serving.global_*``: every front end's queries against EVERY rank's tenant
+  (all-gather of the queries, local scans, one all-to-all of the candidates
+  back to their origin, merge -- SURVEY §2.5 C1 + K2).
+* ``consolidate_sharded``: config 4 as ONE buffer row-sharded over the ranks
+  (``ShardedMemorySystem.consolidate_batch``: facts all-gathered, top-3 lists
+  merged, global eviction, distributed components and k-means).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no
+torchrun environment the script launches N ranks itself through
+torch.distributed.run (127.0.0.1 rendezvous) before touching any GPU, and
+exits with their status; under torchrun, --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -119,6 +138,25 @@ def recall(found_rows, truth_rows):
     return hit / max(tot, 1)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """Run this script as ``n`` ranks under torch.distributed.run (children;
+    this process never initialises the GPU) and return their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,10 +176,18 @@ def main():
     ap.add_argument("--consolidate-convs", type=int, default=128, help="conversations per GPU per step")
     ap.add_argument("--no-persistent-graph", dest="persistent_graph", action="store_false",
                     help="skip the consolidation variant whose seeded edges are never pruned")
+    ap.add_argument("--routed-steps", type=int, default=-1, help="timed routed-search steps (-1: --steps, 0: skip)")
+    ap.add_argument("--global-batch", type=int, default=128, help="queries per rank per global-search step (0: skip)")
+    ap.add_argument("--sharded-steps", type=int, default=5,
+                    help="timed steps of config 4 as one row-sharded buffer (--rows per rank; 0 = skip)")
     ap.add_argument("--cpu", action="store_true", help="CPU / gloo dry run of the whole flow (tests only)")
     a = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # launched by torchrun (even with one rank): the process group and every
@@ -234,27 +280,85 @@ def main():
         el = float(t.item())
     qps = world * a.batch * a.steps / el
 
-    # ---- untimed: the routed path (requests for every rank's tenant cross the
-    # network: one all-to-all-v of the queries, one back with the results) and
-    # a global cross-tenant search (all-gather of candidates + merge) ----
-    routed = {}
-    if distributed:
-        reqs = [(tenants[r], "search_memories", q, a.k) for r in range(world) for q in pool[1][: a.batch // world]]
-        svc.serve(reqs)
+    # ---- timed: routed search (every front end's queries spread over ALL
+    # ranks' tenants: all-to-all there and back) and global search (each
+    # query against every rank's tenant: all-gather + all-to-all + merge) ----
+    serving = {}
+    svc.embedder = emb
+    comm_dev = comm.device
+
+    def timed(n, fn):
+        if distributed:
+            dist.barrier()
         sync()
-        dist.barrier()
         t1 = time.perf_counter()
-        out = svc.serve(reqs)
+        for i in range(n):
+            fn(i)
         sync()
-        dist.barrier()
-        routed["routed_search_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
-        routed["routed_queries_per_rank"] = len(reqs)
-        assert all(len(r) == a.k for r in out)
-        qv = emb.batch_embed_tensor(pool[2][:1])[0]
-        svc.search_global(qv, limit=a.k)
-        t1 = time.perf_counter()
-        svc.search_global(qv, limit=a.k)
-        routed["global_search_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
+        if distributed:
+            dist.barrier()
+        sync()
+        e = time.perf_counter() - t1
+        if distributed:
+            t = torch.tensor([e], device=comm_dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e = float(t.item())
+        return e
+
+    rsteps = a.steps if a.routed_steps < 0 else a.routed_steps
+    if rsteps > 0:
+        rr = random.Random(77 + rank)
+        rusers = [[tenants[rr.randrange(world)] for _ in range(a.batch)] for _ in range(len(pool))]
+        last = {}
+
+        def routed(i):
+            texts, users = pool[i % len(pool)], rusers[i % len(pool)]
+            Q = svc._embed_front(texts)  # the receiving rank's encoder replica (no broadcast, C2)
+            last["Q"], last["users"], last["hits"] = Q, users, svc.search_routed(users, Q, a.k)
+        for i in range(a.warmup):
+            routed(i)
+        el_r = timed(rsteps, routed)
+        remote = sum(svc.owner(u) != rank for u in last["users"])
+        # exactness: every rank checks the queries of ALL front ends that hit
+        # its own tenant against its store search (the routed rows must be the
+        # owner's own top-k); 64 queries per front end
+        m = min(64, a.batch)
+        Qs = last["Q"][:m].float().contiguous()
+        Rs = last["hits"].rows[:m].to(comm_dev).contiguous()
+        own = torch.tensor([svc.owner(u) for u in last["users"][:m]], dtype=torch.int64, device=comm_dev)
+        if distributed:
+            Qs, Rs, own = comm.all_gather_rows(Qs.to(comm_dev)), comm.all_gather_rows(Rs), comm.all_gather_rows(own)
+        mine_q = torch.nonzero(own == rank).flatten()
+        agree = torch.zeros(2, dtype=torch.int64, device=comm_dev)
+        if mine_q.numel():
+            _, ref = g.store_search(Qs[mine_q].to(g.device), a.k, "l2")
+            kind = g.kind[ref.clamp_min(0)]
+            ref = torch.where((ref >= 0) & (kind == 1), ref, torch.full_like(ref, -1))
+            agree[0] = int((ref.to(comm_dev) == Rs[mine_q]).all(1).sum())
+            agree[1] = int(mine_q.numel())
+        if distributed:
+            dist.all_reduce(agree)
+        serving.update({"routed_qps": round(world * a.batch * rsteps / el_r, 2),
+                        "routed_ms_per_step": round(el_r / rsteps * 1e3, 3), "routed_steps": rsteps,
+                        "routed_queries_per_rank": a.batch, "routed_remote_frac_rank0": round(remote / a.batch, 3),
+                        "routed_exact_check": f"{int(agree[0])}/{int(agree[1])}",
+                        "routed_path": "front-end embed -> all_to_all [emb|tenant|limit] -> owner store search "
+                                       "(MFMA scan + fp32 re-rank) -> all_to_all [score|row]"})
+    if a.global_batch > 0:
+        gq = [pool[i % len(pool)][: a.global_batch] for i in range(len(pool))]
+        gb = {}
+
+        def glob(i):
+            gb["h"] = svc.search_global_batch(svc._embed_front(gq[i % len(gq)]), a.k)
+        for i in range(a.warmup):
+            glob(i)
+        gsteps = max(1, rsteps if rsteps > 0 else a.steps)
+        el_g = timed(gsteps, glob)
+        serving.update({"global_qps": round(world * a.global_batch * gsteps / el_g, 2),
+                        "global_ms_per_step": round(el_g / gsteps * 1e3, 3), "global_queries_per_rank": a.global_batch,
+                        "global_corpus_rows": world * a.rows,
+                        "global_path": "all_gather queries -> per-rank store search over its tenant -> all_to_all "
+                                       "candidates to the query's origin -> merge (score desc, key asc)"})
 
     # ---- untimed: breakdown + recall vs float64 truth over the fp32 vectors ----
     def timeit(fn, n=3):
@@ -308,6 +412,18 @@ def main():
                 torch.cuda.empty_cache()
             persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
                                          dim=a.dim, prune_threshold=0.0)
+    sharded = None
+    if a.sharded_steps > 0:
+        # config 4 as ONE buffer row-sharded over the ranks: collectives in
+        # every step (fact all-gather, top-3 merge, global eviction,
+        # distributed components and k-means)
+        if consolidate is None:
+            svc.close()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        sys.path.insert(0, os.path.join(ROOT, "bench"))
+        from bench_consolidate import run_sharded
+        sharded = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_steps, 1, emb, dim=a.dim)
     res = {
         "metric": METRIC,
         "value": round(qps, 2),
@@ -327,7 +443,7 @@ def main():
                    "global_batch": world * a.batch, "seq_len": S_tok, "parallelism": "tenant-dp%d" % world},
         "path": "DistributedMemoryService -> owner's MemorySystem.search_memories_stream (pipelined "
                 "search_memories_batch); tenants placed by rendezvous hashing, one per GPU",
-        "serving": routed,
+        "serving": serving,
         "recall_at_10": round(rec_api, 4),
         "recall_at_10_random_queries": round(rec_rand, 4),
         "recall_truth": "float64 exact L2 over the stored fp32 vectors",
@@ -351,6 +467,10 @@ def main():
         res["consolidate_persistent_graph"] = {k: persistent[k] for k in (
             "turns_per_s", "ms_per_step", "per_step_rank0", "nodes_rank0", "edges_rank0_at_start", "edges_rank0",
             "prune_threshold")}
+    if sharded is not None:
+        res["consolidate_sharded"] = {k: sharded[k] for k in (
+            "turns_per_s", "ms_per_step", "buffer_nodes_total", "nodes_per_rank", "convs_per_rank_step", "per_step",
+            "scan_facts_x_rows_per_rank_step", "path")}
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

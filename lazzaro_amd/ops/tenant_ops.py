@@ -246,11 +246,14 @@ def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:
     return connected_components(src, dst, n)
 
 
-def gather_fields(rows: torch.Tensor, graphs: Sequence, device_out: bool = False) -> Dict:
+def gather_fields(rows: torch.Tensor, graphs: Optional[Sequence], device_out: bool = False,
+                  base: Optional[torch.Tensor] = None) -> Dict:
     """(salience, access count, kind, super flag, shard) of result rows
     [nq, k] where query q's rows belong to ``graphs[q]`` (a TenantGraph per
     query): one device gather over per-query base pointers, one host copy
-    (``device_out``: the device tensors, for an asynchronous copy)."""
+    (``device_out``: the device tensors, for an asynchronous copy). ``base``:
+    the int64 [5, nq] device table of those column pointers when the caller
+    already has it (``routing.TenantTable``); ``graphs`` is then unused."""
     nq, k = rows.shape
     dev = rows.device
     if not rows.is_cuda:
@@ -264,8 +267,10 @@ def gather_fields(rows: torch.Tensor, graphs: Sequence, device_out: bool = False
                     for n in out:
                         out[n][q, j] = getattr(g, n)[int(r)]
         return out
-    base = torch.tensor([[getattr(g, c).data_ptr() for g in graphs] for c in ("sal", "acc", "kind", "sup", "shard")],
-                        dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    if base is None:
+        base = torch.tensor([[getattr(g, c).data_ptr() for g in graphs] for c in ("sal", "acc", "kind", "sup",
+                                                                                  "shard")],
+                            dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
     o = {"sal": torch.empty((nq, k), dtype=torch.float32, device=dev),
          "acc": torch.empty((nq, k), dtype=torch.int32, device=dev),
          "kind": torch.empty((nq, k), dtype=torch.uint8, device=dev),

@@ -28,12 +28,13 @@ All collective methods must be called by every rank in the same order.
 from __future__ import annotations
 
 import inspect
-from collections import OrderedDict
+from collections import OrderedDict, defaultdict
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
+from . import routing
 from .comm import Communicator
 from .placement import tenant_rank
 
@@ -65,7 +66,7 @@ def _jsonable(v):
 
 class DistributedMemoryService:
     def __init__(self, comm: Communicator, factory: Callable[[str], object], owner: Callable[[str], int] = None,
-                 max_resident: int = 1 << 30, placement=None):
+                 max_resident: int = 1 << 30, placement=None, embedder=None):
         """``factory(user_id)`` builds the tenant's MemorySystem on this rank
         (sharing one store / embedder / device; it must load the tenant from
         the store); ``owner`` overrides the rendezvous-hash placement;
@@ -73,14 +74,22 @@ class DistributedMemoryService:
         over the ORIGINAL ids of the live ranks, so :meth:`reform` after a rank
         failure moves only the dead ranks' tenants. At most ``max_resident``
         tenants stay in memory (LRU; an evicted tenant is persisted and
-        reloaded from the store on its next request)."""
+        reloaded from the store on its next request). ``embedder``: this
+        rank's replica of the encoder for the front end's queries on the
+        columnar search paths (default: the first resident tenant's)."""
         self.comm = comm
         self.factory = factory
         self._owner = owner
         self.placement = placement
         self.max_resident = max_resident
+        self.embedder = embedder
         self._moved: Dict[str, int] = {}  # migrate() overrides of the placement
         self.systems: "OrderedDict[str, object]" = OrderedDict()
+        # columnar search routing (routing.py): the device table of resident
+        # tenants, tenant names announced to each owner, key -> name
+        self._table = None
+        self._announced = defaultdict(set)
+        self._key_names: Dict[int, str] = {}
 
     # ------------------------------------------------------------ placement
     def owner(self, user: str) -> int:
@@ -102,12 +111,23 @@ class DistributedMemoryService:
         rank loses no committed state). Returns the released tenants."""
         self.comm, self.placement, self._owner = comm, placement, None
         self._moved = {}
+        self._announced = defaultdict(set)  # owners changed: announce names again
         gone = [u for u in self.systems if not self.is_local(u)]
         for u in gone:
-            ms = self.systems.pop(u)
-            ms._save_to_persistence()
-            ms.close()
+            self._release(u, self.systems.pop(u))
         return gone
+
+    def _release(self, user: str, ms) -> None:
+        """Persist and close a tenant this rank stops holding."""
+        if self._table is not None:
+            self._table.drop(user)
+        ms._save_to_persistence()
+        ms.close()
+
+    def tenant_table(self) -> "routing.TenantTable":
+        if self._table is None:
+            self._table = routing.TenantTable(self.comm.device)
+        return self._table
 
     def is_local(self, user: str) -> bool:
         return self.owner(user) == self.comm.rank
@@ -121,9 +141,8 @@ class DistributedMemoryService:
             ms = self._build(user)
             self.systems[user] = ms
             while len(self.systems) > self.max_resident:
-                _, old = self.systems.popitem(last=False)
-                old._save_to_persistence()
-                old.close()
+                u0, old = self.systems.popitem(last=False)
+                self._release(u0, old)
         else:
             self.systems.move_to_end(user)
         return ms
@@ -145,6 +164,8 @@ class DistributedMemoryService:
             dst = int(moves[user])
             if user in self.systems and dst != me:
                 ms = self.systems.pop(user)
+                if self._table is not None:
+                    self._table.drop(user)
                 ms._save_to_persistence()
                 meta, vec = ms.export_state()
                 out_meta[dst].append([user, meta, list(vec.shape)])
@@ -158,6 +179,7 @@ class DistributedMemoryService:
         rc = comm.exchange_counts(torch.tensor(counts, dtype=torch.int64, device=dev)).cpu().tolist()
         recv = comm.all_to_all_v(flat, counts, rc) if comm.world > 1 else flat
         self._moved.update({u: int(r) for u, r in moves.items()})
+        self._announced = defaultdict(set)
         received, off = [], 0
         for src in range(comm.world):
             for user, meta, shape in got_meta[src]:
@@ -308,20 +330,25 @@ class DistributedMemoryService:
             with tracer.stage("mt_prep", "cpu"):
                 D = Q.shape[1]
                 graphs = {u: ms.graph for u, ms in systems.items()}
-                ok = {u: g.dim == D and g.n > 0 and g.emb32 is not None for u, g in graphs.items()}
-                xp = [graphs[u].emb32.data_ptr() if ok[u] else 0 for u in users]
-                bp = [graphs[u].store_bias("l2").data_ptr() if ok[u] else 0 for u in users]
-                nr = [graphs[u].n if ok[u] else 0 for u in users]
-                ptrs = torch.tensor([xp, bp], dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
-                nrows = torch.tensor(nr, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+                table = self.tenant_table()
+                slots = table.slots(users, systems)
+                ptrs = table.d_ptr[:, slots]
+                nrows = table.d_n[slots]
+                # a tenant of another width contributes no rows
+                wrong = [j for j, u in enumerate(users) if graphs[u].dim != D]
+                if wrong:
+                    nrows = nrows.clone()
+                    nrows[torch.as_tensor(wrong, device=dev)] = 0
             qb = -(Q * Q).sum(1)
             k = max(p[4] for p in pending)
             with tracer.stage("mt_scan", first._device):
-                _, rows = segment_topk_ptrs(ptrs[0], nrows, D, Q.contiguous(), k, bptr=ptrs[1], alpha=2.0, qbias=qb)
-            # the result rows' fields in one gather over per-query column
-            # pointers (the tenants' columns are separate allocations)
+                _, rows = segment_topk_ptrs(ptrs[0].contiguous(), nrows.contiguous(), D, Q.contiguous(), k,
+                                            bptr=ptrs[1].contiguous(), alpha=2.0, qbias=qb)
+            # the result rows' fields in one gather over the per-query column
+            # pointers of the tenant table (the tenants' columns are separate
+            # allocations)
             qg = [graphs[u] for u in users]
-            f = gather_fields(rows, qg, device_out=True)
+            f = gather_fields(rows, None, device_out=True, base=ptrs[2:7].contiguous())
             f["rows"] = rows
             host = {n: torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for n, t in f.items()}
             for n, t in f.items():
@@ -358,6 +385,41 @@ class DistributedMemoryService:
         finally:
             for lk in reversed(locks):
                 lk.release()
+
+    # ------------------------------------------------------------ columnar search (routing.py)
+    def search_routed(self, users: Sequence[str], queries, limit=5) -> "routing.RoutedHits":
+        """SPMD batched search_memories with tensors on the wire: ``queries``
+        are texts (embedded here, by this rank's replica of the encoder) or an
+        embedding tensor [n, D]; each goes to ``users[q]``'s owner in one
+        all-to-all and its (score, row) hits come back in one more. Returns a
+        :class:`~.routing.RoutedHits` in the caller's order."""
+        Q = self._embed_front(queries)
+        return routing.search_routed(self, list(users), Q, limit)
+
+    def search_global_batch(self, queries, limit: int = 5) -> "routing.GlobalHits":
+        """SPMD: this rank's queries against every resident tenant of every
+        rank (all-gather of queries, local search, one all-to-all back)."""
+        return routing.search_global_batch(self, self._embed_front(queries), limit)
+
+    def resolve(self, hits: "routing.RoutedHits") -> List[List[Dict]]:
+        """SPMD: node dicts of routed hits (for callers that need contents)."""
+        return routing.resolve(self, hits)
+
+    def _embed_front(self, queries):
+        if torch.is_tensor(queries):
+            return queries.to(self.comm.device, torch.float32)
+        queries = list(queries)
+        emb = getattr(self, "embedder", None)
+        if emb is None:
+            ms = next(iter(self.systems.values()), None)
+            emb = ms.embedder if ms is not None else None
+        if emb is None or not queries:
+            return torch.zeros((0, 0), dtype=torch.float32, device=self.comm.device)
+        if getattr(type(emb), "batch_embed_tensor", None) is not None:
+            out = emb.batch_embed_tensor(queries)
+        else:
+            out = torch.as_tensor(np.asarray(emb.batch_embed(queries), np.float32))
+        return out.to(self.comm.device, torch.float32)
 
     # ------------------------------------------------------------ directory (C7)
     def get_all_users(self) -> List[str]:

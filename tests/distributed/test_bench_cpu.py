@@ -32,5 +32,43 @@ def test_bench_two_ranks_cpu(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 2 and d["warmup"] == 1
     assert d["recall_at_10"] == 1.0 and d["recall_at_10_random_queries"] == 1.0
-    assert d["serving"]["routed_queries_per_rank"] == 32 and d["serving"]["global_search_ms"] > 0
+    _check_serving(d, 32)
     assert d["consolidate_turns_per_s"] > 0 and d["consolidate"]["per_step_rank0"]["evicted"] > 0
+
+
+def _check_serving(d, batch):
+    sv = d["serving"]
+    assert sv["routed_queries_per_rank"] == batch and sv["routed_qps"] > 0 and sv["global_qps"] > 0
+    ok, tot = map(int, sv["routed_exact_check"].split("/"))
+    assert tot > 0 and ok == tot  # every routed answer equals the owner's own store search
+    assert 0 < sv["routed_remote_frac_rank0"] < 1
+
+
+SMALL = ["--cpu", "--rows", "6000", "--dim", "128", "--model", "tiny", "--batch", "32", "--steps", "2", "--warmup",
+         "1", "--prewarm-s", "0.2", "--recall-queries", "8", "--consolidate-steps", "1", "--consolidate-convs", "4",
+         "--no-persistent-graph", "--sharded-steps", "1", "--global-batch", "8"]
+
+
+def test_bench_self_launches_ranks(tmp_path):
+    """``bench.py --gpus 2`` without a torchrun environment launches the two
+    ranks itself (the parent stays GPU-free) and reports n_gpus == 2 with the
+    RCCL-path numbers (routed / global search, row-sharded consolidation)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env.update(PYTHONPATH=ROOT, LZK_BENCH_DB=str(tmp_path / "db"))
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"].endswith("2")
+    _check_serving(d, 32)
+    assert d["consolidate_sharded"]["turns_per_s"] > 0
+
+
+def test_bench_rejects_gpus_world_mismatch(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL, cwd=str(tmp_path),
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stdout + r.stderr)

@@ -1,0 +1,114 @@
+"""Columnar search routing (lazzaro_amd/parallel/routing.py) on CPU with gloo:
+``search_routed`` (queries embedded by the front end, routed to the tenants'
+owners in one all-to-all, (score, row) hits back in one more), ``resolve``
+and ``search_global_batch`` (all-gather of queries + one all-to-all of
+candidates back to their origin) against single-process truth."""
+import functools
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from tests.distributed.test_dist_gloo import spawn
+
+USERS = [f"tenant{i}" for i in range(9)]
+D = 32
+
+
+def _rows(user):
+    rng = np.random.default_rng(int(user[6:]) + 11)
+    n = 30 + 17 * int(user[6:])
+    return n, rng.standard_normal((n, D)).astype(np.float32)
+
+
+def _factory(db, user, load_from_disk=False):
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    return MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
+                        db_dir=db, user_id=user, device="cpu", load_from_disk=load_from_disk, max_buffer_size=10 ** 6)
+
+
+def _fill(ms, user):
+    n, V = _rows(user)
+    g = ms.graph
+    g.add_nodes([f"{user}_m{i}" for i in range(n)], [f"memory {i} of {user}" for i in range(n)],
+                torch.from_numpy(V), shard=g.shard_id("work"), stored=True)
+
+
+def _queries(rank, n=13):
+    return [f"rank {rank} question {q} about memories" for q in range(n)]
+
+
+def _workload(comm, db):
+    from lazzaro_amd.core.providers import HashEmbedder
+    from lazzaro_amd.parallel.service import DistributedMemoryService
+    svc = DistributedMemoryService(comm, functools.partial(_factory, db), embedder=HashEmbedder(dim=D))
+    for u in USERS:
+        if svc.is_local(u):
+            _fill(svc.system(u), u)
+    rng = np.random.default_rng(comm.rank)
+    qs = _queries(comm.rank)
+    users = [USERS[int(rng.integers(len(USERS)))] for _ in qs]
+    limits = [int(x) for x in rng.integers(1, 6, len(qs))]
+    hits = svc.search_routed(users, qs, limits)
+    nodes = svc.resolve(hits)
+    again = svc.search_routed(users, qs, limits)  # names already announced: tensor-only round
+    same = bool(torch.equal(again.rows, hits.rows))
+    glob = svc.search_global_batch(qs[:5], limit=4)
+    rk, slot, row = glob.split()
+    table = svc.tenant_table()
+    names = {int(s): n for n, s in table.slot.items()}
+    svc.close()
+    return json.dumps({"users": users, "limits": limits, "ids": [[n["id"] for n in r] for r in nodes],
+                       "scores": hits.scores.tolist(), "same": same,
+                       "global": [[[int(a), int(b), int(c)] for a, b, c in zip(x, y, z)]
+                                  for x, y, z in zip(rk.tolist(), slot.tolist(), row.tolist())],
+                       "gscores": glob.scores.tolist(), "names": names, "rank": comm.rank})
+
+
+def _truth(qs, users, limits):
+    from lazzaro_amd.core.providers import HashEmbedder
+    E = np.asarray(HashEmbedder(dim=D).batch_embed(qs), np.float32)
+    out = []
+    for q, (u, k) in enumerate(zip(users, limits)):
+        n, V = _rows(u)
+        d = ((E[q][None, :] - V) ** 2).sum(1)
+        out.append([f"{u}_m{i}" for i in np.argsort(d, kind="stable")[:k]])
+    return out
+
+
+def _global_truth(qs, k):
+    from lazzaro_amd.core.providers import HashEmbedder
+    E = np.asarray(HashEmbedder(dim=D).batch_embed(qs), np.float32)
+    res = []
+    for q in range(len(qs)):
+        c = []
+        for u in USERS:
+            n, V = _rows(u)
+            d = ((E[q][None, :] - V) ** 2).sum(1)
+            c += [(float(d[i]), u, i) for i in range(n)]
+        c.sort()
+        res.append([(u, i) for _, u, i in c[:k]])
+    return res
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_routed_and_global_search(world, tmp_path):
+    fn = functools.partial(_workload, db=str(tmp_path / f"r{world}"))
+    if world == 1:
+        from lazzaro_amd.parallel import Communicator
+        outs = {0: fn(Communicator.local())}
+    else:
+        outs = spawn(world, fn)
+    d = {r: json.loads(v) for r, v in outs.items()}
+    names = {r: {int(s): n for s, n in x["names"].items()} for r, x in d.items()}
+    for r, x in d.items():
+        qs = _queries(r)
+        assert x["same"]
+        assert x["ids"] == _truth(qs, x["users"], x["limits"]), r
+        # scores are exact -|q - x|^2, sorted, -inf past each limit
+        for sc, k in zip(x["scores"], x["limits"]):
+            assert all(s > float("-inf") for s in sc[:k]) and sc[:k] == sorted(sc[:k], reverse=True)
+        got = [[(names[rk][sl], row) for rk, sl, row in qq] for qq in x["global"]]
+        assert got == _global_truth(qs[:5], 4), r

@@ -145,3 +145,37 @@ def test_shared_store_survives_tenant_release(tmp_path):
     got = svc.serve([(u, "search_memories", "fact 3", 3) for u in users[1:]])
     assert all(len(x) == 3 for x in got)
     svc.close()
+
+
+def test_search_routed_matches_per_tenant_gpu(tmp_path):
+    """Columnar routed search on one GPU: small tenants share one fused
+    segment_topk launch (tenant table pointers), a big tenant goes through
+    its store search; every query's hits equal the tenant's own
+    search_memories_batch, and resolve() returns the same nodes."""
+    from lazzaro_amd.parallel import routing
+    emb = RandEmbedder()
+    users = [f"q{i}" for i in range(12)]
+    svc = _seeded_service(tmp_path, emb, users)
+    svc.embedder = emb
+    big = svc.system("big")
+    n = routing.BIG_ROWS + 1000
+    g = big.graph
+    V = torch.nn.functional.normalize(torch.randn(n, 64, device="cuda"), dim=1)
+    g.add_nodes([f"big_{i}" for i in range(n)], [f"big {i}" for i in range(n)], V, shard=g.shard_id("work"),
+                stored=True)
+    rng = np.random.default_rng(5)
+    allu = users + ["big"]
+    qu = [allu[int(rng.integers(len(allu)))] for _ in range(300)]
+    qs = [f"query {i}" for i in range(300)]
+    lim = [int(x) for x in rng.integers(1, 9, 300)]
+    hits = svc.search_routed(qu, qs, lim)
+    nodes = svc.resolve(hits)
+    E = torch.tensor(emb.batch_embed(qs), device="cuda")
+    for q in range(300):
+        ms = svc.system(qu[q])
+        _, rr = ms.graph.store_search(E[q:q + 1], lim[q])
+        kind = ms.graph.mirror("kind")
+        ref = [ms.graph.ids[int(r)] for r in rr[0].tolist() if r >= 0 and kind[int(r)] == 1]
+        assert [x["id"] for x in nodes[q]] == ref, q
+        assert [v.id for v in hits.local_nodes(svc, q)] == ref
+    svc.close()
