@@ -137,8 +137,9 @@ def test_shared_store_survives_tenant_release(tmp_path):
     store = HBMStore(db_dir=str(tmp_path / "db"), device=torch.device("cuda"))
     users = [f"r{i}" for i in range(4)]
     svc = _seeded_service(tmp_path, emb, users, store=store)
-    svc.max_resident = 3
-    svc.system("extra")  # releases r0
+    svc.max_resident = 4
+    svc.system("extra")  # 5 resident > 4: releases r0 (LRU)
+    assert "r0" not in svc.systems and store.bound_graph("r0") is None
     for u in users[1:]:
         assert store.bound_graph(u) is svc.systems[u].graph
         assert svc.systems[u]._store_binds_graph()
