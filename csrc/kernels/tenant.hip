@@ -45,20 +45,26 @@ __device__ __forceinline__ float decay_sal(float s, float keep) {
 // buffer_graph.py:79-85), so this rounds exactly once like the CPU path.
 __device__ __forceinline__ float bump_sal(float s, double delta) { return (float)fmin(1.0, (double)s + delta); }
 
-// Edge pass: w *= keep (keep == 1 -> no decay); flag survivors w >= thr
-// (flag == nullptr -> no prune). Node pass (same launch, grid-stride): the
-// salience of shard nodes (kind 1, not super) decays towards the floor.
+// Edge pass: `steps` rounds of w *= keep (keep == 1 -> no decay), each
+// rounded to fp32 like one end_conversation (a batch of B conversations is B
+// rounds here, not one multiply by keep^B, so a weight at the prune
+// threshold lands exactly where B sequential calls put it); flag survivors
+// w >= thr (flag == nullptr -> no prune; weights only fall, so a survivor
+// of the last round survived every round). Node pass (same launch,
+// grid-stride): the salience of shard nodes (kind 1, not super) decays
+// towards the floor, `steps` rounds.
 __global__ __launch_bounds__(NTB) void tg_decay_kernel(float* __restrict__ w, long ne, float keep, float thr,
                                                        unsigned char* __restrict__ flag, int* __restrict__ block_cnt,
                                                        float* __restrict__ sal, const unsigned char* __restrict__ kind,
-                                                       const unsigned char* __restrict__ sup, long nn, int do_nodes) {
+                                                       const unsigned char* __restrict__ sup, long nn, int do_nodes,
+                                                       int steps) {
   __shared__ int wsum[NTB / 64];
   const long e = (long)blockIdx.x * NTB + threadIdx.x;
   int f = 0;
   if (e < ne) {
     float v = w[e];
     if (keep != 1.f) {
-      v *= keep;
+      for (int t = 0; t < steps; ++t) v *= keep;
       w[e] = v;
     }
     f = v >= thr;
@@ -71,19 +77,22 @@ __global__ __launch_bounds__(NTB) void tg_decay_kernel(float* __restrict__ w, lo
   if (do_nodes) {
     for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
       if (kind[i] != 1 || sup[i]) continue;
-      const float s = sal[i];
-      sal[i] = decay_sal(s, keep);
+      float s = sal[i];
+      for (int t = 0; t < steps; ++t) s = decay_sal(s, keep);
+      sal[i] = s;
     }
   }
 }
 
 // Node-only salience decay (when the edge grid is too small to stream nodes).
 __global__ __launch_bounds__(NTB) void tg_node_decay_kernel(float* __restrict__ sal, const unsigned char* __restrict__ kind,
-                                                            const unsigned char* __restrict__ sup, long nn, float keep) {
+                                                            const unsigned char* __restrict__ sup, long nn, float keep,
+                                                            int steps) {
   for (long i = (long)blockIdx.x * NTB + threadIdx.x; i < nn; i += (long)gridDim.x * NTB) {
     if (kind[i] != 1 || sup[i]) continue;
-    const float s = sal[i];
-    sal[i] = decay_sal(s, keep);
+    float s = sal[i];
+    for (int t = 0; t < steps; ++t) s = decay_sal(s, keep);
+    sal[i] = s;
   }
 }
 
@@ -204,14 +213,54 @@ __global__ __launch_bounds__(NTB) void tg_importance_kernel(const float* __restr
   out[i] = (double)sal[i] * 0.5 + fmin(1.0, (double)acc[i] / 10.0) * 0.3 + (1.0 / (1.0 + days)) * 0.2;
 }
 
+// Exactness check of a batched eviction plan (MemorySystem.consolidate_batch,
+// core/batch_plan.py): the planner picked every eviction's victims from a
+// pool of rows; a row OUTSIDE the pool that nothing touched must not rank
+// before the pool's victims at any eviction. Event e happened after
+// ev_steps[e] decays (ascending) and its last victim had the key
+// (ev_imp, ev_code, ev_row); each thread walks one row through the events,
+// decaying its salience exactly like tg_decay_kernel and scoring it exactly
+// like tg_importance_kernel, and flags a row whose key is smaller.
+__global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __restrict__ sal, const int* __restrict__ acc,
+                                                              const double* __restrict__ last,
+                                                              const unsigned char* __restrict__ kind,
+                                                              const unsigned char* __restrict__ sup,
+                                                              const int* __restrict__ shard,
+                                                              const unsigned char* __restrict__ pool, long n,
+                                                              double now, float keep, int ne,
+                                                              const int* __restrict__ ev_steps,
+                                                              const double* __restrict__ ev_imp,
+                                                              const int* __restrict__ ev_code,
+                                                              const long* __restrict__ ev_row, int* __restrict__ bad) {
+#pragma clang fp contract(off)
+  const long i = (long)blockIdx.x * NTB + threadIdx.x;
+  if (i >= n || kind[i] != 1 || sup[i] || pool[i]) return;
+  float s = sal[i];
+  const double a = fmin(1.0, (double)acc[i] / 10.0) * 0.3;
+  const double d = (1.0 / (1.0 + (now - last[i]) / 86400.0)) * 0.2;
+  const int code = shard[i];
+  int t = 0;
+  for (int e = 0; e < ne; ++e) {
+    const int st = ev_steps[e];
+    for (; t < st; ++t) s = decay_sal(s, keep);
+    const double imp = (double)s * 0.5 + a + d;
+    const double vi = ev_imp[e];
+    if (imp < vi || (imp == vi && (code < ev_code[e] || (code == ev_code[e] && i < ev_row[e])))) {
+      bad[0] = 1;
+      return;
+    }
+  }
+}
+
 inline unsigned blocks_for(long n, int per = NTB) { return (unsigned)((n + per - 1) / per); }
 
 }  // namespace
 
 // ---------------------------------------------------------------- C ABI
 LZK_EXPORT int lzk_tg_decay(float* w, long ne, float keep, float thr, unsigned char* flag, int* block_cnt, float* sal,
-                            const unsigned char* kind, const unsigned char* sup, long nn, int decay_nodes,
+                            const unsigned char* kind, const unsigned char* sup, long nn, int decay_nodes, int steps,
                             void* stream) {
+  if (steps < 0) return (int)hipErrorInvalidValue;
   long nb = (ne + NTB - 1) / NTB;
   if (nb == 0) nb = 1;
   // nodes ride in the edge launch only while its grid can stream them
@@ -219,11 +268,11 @@ LZK_EXPORT int lzk_tg_decay(float* w, long ne, float keep, float thr, unsigned c
   const bool fused = decay_nodes && (nb >= node_blocks || nb >= 2048);
   if (ne > 0 || fused)
     hipLaunchKernelGGL(tg_decay_kernel, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, w, ne, keep, thr, flag,
-                       block_cnt, sal, kind, sup, nn, fused ? 1 : 0);
+                       block_cnt, sal, kind, sup, nn, fused ? 1 : 0, steps);
   if (decay_nodes && !fused && nn > 0) {
     const long g = node_blocks < 4096 ? node_blocks : 4096;
     hipLaunchKernelGGL(tg_node_decay_kernel, dim3((unsigned)g), dim3(NTB), 0, (hipStream_t)stream, sal, kind, sup, nn,
-                       keep);
+                       keep, steps);
   }
   return (int)hipGetLastError();
 }
@@ -268,6 +317,16 @@ LZK_EXPORT int lzk_tg_importance(const float* sal, const int* acc, const double*
   if (n <= 0) return 0;
   hipLaunchKernelGGL(tg_importance_kernel, dim3(blocks_for(n)), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last,
                      kind, sup, n, now, out);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_evict_verify(const float* sal, const int* acc, const double* last, const unsigned char* kind,
+                                   const unsigned char* sup, const int* shard, const unsigned char* pool, long n,
+                                   double now, float keep, int ne, const int* ev_steps, const double* ev_imp,
+                                   const int* ev_code, const long* ev_row, int* bad, void* stream) {
+  if (n <= 0 || ne <= 0) return 0;
+  hipLaunchKernelGGL(tg_evict_verify_kernel, dim3(blocks_for(n)), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last,
+                     kind, sup, shard, pool, n, now, keep, ne, ev_steps, ev_imp, ev_code, ev_row, bad);
   return (int)hipGetLastError();
 }
 

@@ -98,11 +98,26 @@ def batch_dedupe(Qn: torch.Tensor, ct: torch.Tensor, gb_s: torch.Tensor, gb_node
     return S, earlier, dup, batch_best, bb_i, ins
 
 
+def decay_steps_f32(x: torch.Tensor, n: torch.Tensor, keep: float, salience: bool) -> torch.Tensor:
+    """``x`` after ``n[i]`` end_conversation decays, each rounded to fp32 the
+    way ``tg_decay_kernel`` rounds it (salience: floor + (s - floor) * keep
+    op by op; edge weight: w * keep) -- B rounded steps, not one multiply by
+    keep^B, so a value at the prune threshold lands exactly where B
+    sequential calls put it."""
+    x = x.float().clone()
+    kf = torch.tensor(keep, dtype=torch.float32, device=x.device)
+    fl = torch.tensor(SALIENCE_FLOOR_, dtype=torch.float32, device=x.device)
+    n = n.to(x.device)
+    for t in range(int(n.max()) if n.numel() else 0):
+        d = torch.where(x > fl, fl + (x - fl) * kf, fl) if salience else x * kf
+        x = torch.where(n > t, d, x)
+    return x
+
+
 def salience_decayed(s: torch.Tensor, n: torch.Tensor, keep: float) -> torch.Tensor:
-    """Node salience after ``n`` decays (floor SALIENCE_FLOOR_, memory_shard.py:64-77)."""
-    kn = torch.pow(torch.full_like(s, keep), n.double())
-    return torch.where(s > SALIENCE_FLOOR_, SALIENCE_FLOOR_ + (s - SALIENCE_FLOOR_) * kn,
-                       torch.full_like(s, SALIENCE_FLOOR_))
+    """Node salience (fp32) after ``n`` decays (floor SALIENCE_FLOOR_,
+    memory_shard.py:64-77), rounded per step like the sequential calls."""
+    return decay_steps_f32(s, n, keep, True)
 
 
 def batch_link_plan(kidx, new_row, code_all, ct, S, earlier, shard_hits, global_hits, keep: float, B: int, thr,
@@ -182,8 +197,9 @@ def batch_link_plan(kidx, new_row, code_all, ct, S, earlier, shard_hits, global_
         return None, n_cross
     W = torch.cat(ew)
     Ord = torch.cat(order)
-    # decays of the end_conversation calls from the edge's conversation on
-    W = W * torch.pow(torch.full_like(W, keep), (B - torch.div(Ord, 4, rounding_mode="floor")).double())
+    # decays of the end_conversation calls from the edge's conversation on,
+    # rounded per step in fp32 like the sequential calls
+    W = decay_steps_f32(W, B - torch.div(Ord, 4, rounding_mode="floor"), keep, False)
     stats["linked"] += int(Sr.numel())
     stats["cross_links"] += n_cross
     H = torch.cat(eh)
@@ -196,6 +212,26 @@ def batch_link_plan(kidx, new_row, code_all, ct, S, earlier, shard_hits, global_
     if Sr.numel() == 0:
         return None, n_cross
     return (Sr, Dr, W, H), n_cross
+
+
+def _lowest_keys(imp: torch.Tensor, okey: torch.Tensor, P: int) -> torch.Tensor:
+    """Rows of the P smallest (importance, shard, row) keys -- the eviction
+    order: every row with a smaller importance than the P-th, then the tied
+    rows by (shard, row)."""
+    t = torch.topk(imp, P, largest=False, sorted=False).values.max()
+    lt = torch.nonzero(imp < t).flatten()
+    m = P - int(lt.numel())
+    big = torch.iinfo(torch.int64).max
+    tv, ti = torch.topk(torch.where(imp == t, okey, torch.full_like(okey, big)), m, largest=False, sorted=False)
+    return torch.cat([lt, ti[tv != big]])
+
+
+def shard_keys_of(g: TenantGraph, code: int) -> str:
+    """The shard name of a shard code."""
+    for k, c in g.shard_code.items():
+        if c == code:
+            return k
+    raise KeyError(code)
 
 
 def _parse_json(response: str):
@@ -499,11 +535,24 @@ class ConsolidationMixin:
         if fast:
             best_s, best_r = gs[:, 0].clone(), gr[:, 0].clone()
             if g.n_super:
+                # the store's top-1 is by L2: score 2|q||x|cos - |x|^2. The
+                # global list's head is the L2-best unit row; super-nodes (means
+                # of unit rows) are not unit, so every one is scored
                 srows = torch.as_tensor(g.node_rows_where(super_=True), dtype=torch.long).to(dev)
-                ss, sr = g._exact_cos(Qn, torch.zeros(n, dtype=torch.bool, device=dev).index_fill_(0, srows, True), 1)
-                better = (ss[:, 0] > best_s) | ((ss[:, 0] == best_s) & (sr[:, 0] < best_r))
-                best_s = torch.where(better, ss[:, 0], best_s)
-                best_r = torch.where(better, sr[:, 0], best_r)
+                X = g.emb32[srows].double()
+                n2 = g.sqn[srows].double()
+                l2s = 2.0 * (Qd @ X.T) - n2[None, :]
+                j = torch.argmax(l2s, dim=1)  # first maximum: the lowest super row on a tie
+                sl2 = l2s.gather(1, j[:, None])[:, 0]
+                sr = srows[j]
+                hn2 = g.sqn[best_r.clamp_min(0)].double()
+                hl2 = torch.where(best_r >= 0, 2.0 * qn[:, 0] * best_s * hn2.sqrt() - hn2,
+                                  torch.full_like(best_s, float("-inf")))
+                better = (sl2 > hl2) | ((sl2 == hl2) & (sr < best_r))
+                nx = n2.sqrt()[j]
+                scos = (Qn * X[j]).sum(1) / torch.where(nx > 0, nx, torch.ones_like(nx))
+                best_s = torch.where(better, scos, best_s)
+                best_r = torch.where(better, sr, best_r)
             isnode = best_r >= 0
         else:
             _, top = self._store_top1(Q)
@@ -581,39 +630,45 @@ class ConsolidationMixin:
         return made
 
     # ------------------------------------------------------------ batched end_conversation
+    # candidate list length per fact in the batch scan: 3 links + headroom for
+    # rows the batch evicts before the fact's conversation (else: fallback)
+    BATCH_LIST_K = 8
+
     def consolidate_batch(self, conversations: Sequence[Sequence[Dict]], embeddings=None,
-                          now: float = None) -> Dict[str, int]:
+                          now: float = None, cadence: str = "conversation") -> Dict[str, int]:
         """``end_conversation`` for B finished conversations at once, given
         their extracted facts (``conversations[c]`` = fact dicts with
         ``content`` / ``type`` / ``salience`` / ``topic``, the extraction
         LLM's output, reference :684-716). ``embeddings``: optional [F, D]
         vectors aligned with the flattened facts (else the embedder runs once
-        for the whole batch).
+        for the whole batch). ``now``: the clock of the whole batch.
 
-        Result = B sequential ``end_conversation`` calls (reference :580-649,
-        :706-891) -- conversation c's facts dedupe against, and link to, the
-        graph plus the facts kept from conversations < c; then decay
-        (0.01 per conversation) and auto-prune -- computed in one device pass:
+        The result is B sequential ``end_conversation`` calls at the
+        reference's cadence (reference :580-649, :651-933): per conversation
+        dedupe against and links to the graph of that moment, insert,
+        buffer-limit eviction, super-node creation, decay + auto-prune,
+        eviction again; ``run_consolidation`` at every multiple of
+        ``consolidate_every``. :mod:`.batch_plan` simulates the B
+        conversations on the host from ONE fused scan of all facts against
+        the pre-batch graph (eviction: an exact pool argument), and the plan
+        is applied to the device graph in segments that end at the
+        ``run_consolidation`` points, where run_consolidation runs on the
+        real graph. Only the persistence commit is once per batch (the store
+        then holds the same rows / edges / profile as after the last call).
 
-        * ONE fused scan of all facts against the pre-batch graph (dedupe
-          top-1 + within-shard and cross-memory top-3), plus an F x F float64
-          block for the facts of earlier conversations in the batch; in-batch
-          duplicate chains are resolved by a fixed point;
-        * decay is applied in closed form: the pre-batch graph by
-          (1-r)^B in one ``tg_decay_kernel`` pass, a new node / edge of
-          conversation c by (1-r)^(B-c) at insert (the decays of the
-          end_conversation calls that follow it); a duplicate merge onto a
-          node keeps max(decayed salience, decayed fact salience) -- exactly
-          the sequential result, as decay is monotone;
-        * eviction to ``max_buffer_size``, super-node creation, the
-          ``run_consolidation`` trigger (once if any of the B counts crosses a
-          multiple of ``consolidate_every``) and the persistence commit run
-          once per batch instead of once per conversation.
+        ``cadence="batch"``: the coarser batch semantics of the row-sharded
+        buffer (``ShardedMemorySystem``): every conversation's facts are
+        matched against the pre-batch graph plus earlier conversations'
+        facts with closed-form decays, and eviction, super-node creation,
+        ``run_consolidation`` (once, if a multiple of ``consolidate_every``
+        was crossed) happen once at the end of the batch.
 
         Returns counts: conversations, facts, dup, inserted, linked (edges
         created), cross_links (the reference's "cross-conversation links"),
-        pruned (edges removed by decay, incl. new ones below the threshold),
-        evicted."""
+        pruned (edges removed by decay), evicted, consolidations (the
+        run_consolidation calls), fallbacks (candidate lists recomputed)."""
+        if cadence not in ("conversation", "batch"):
+            raise ValueError("cadence must be 'conversation' or 'batch'")
         flat, conv, idx = [], [], []
         j = 0
         for c, fs in enumerate(conversations):
@@ -626,7 +681,7 @@ class ConsolidationMixin:
         B = len(conversations)
         now = time.time() if now is None else now
         stats = {"conversations": B, "facts": len(flat), "dup": 0, "inserted": 0, "linked": 0, "cross_links": 0,
-                 "pruned": 0, "evicted": 0}
+                 "pruned": 0, "evicted": 0, "consolidations": 0, "fallbacks": 0}
         if B == 0:
             return stats
         if embeddings is not None and len(flat):
@@ -638,15 +693,24 @@ class ConsolidationMixin:
         else:
             embs = None
         with self._graph_lock, tracer.stage("consolidate_batch", self._device):
-            self._consolidate_batch(flat, np.asarray(conv, dtype=np.int64), B, embs, now, stats)
-            self._enforce_buffer_limit_counted(stats)
-            c0 = self.conversation_count
-            self.conversation_count += B
-            if self.auto_consolidate and (self.conversation_count // self.consolidate_every
-                                          > c0 // self.consolidate_every):
-                with tracer.stage("run_consolidation", self._device):
-                    self.run_consolidation()
-            self._maybe_cluster(c0)
+            conv = np.asarray(conv, dtype=np.int64)
+            if cadence == "batch":
+                self._consolidate_batch_coarse(flat, conv, B, embs, now, stats)
+                self._enforce_buffer_limit_counted(stats)
+                c0 = self.conversation_count
+                self.conversation_count += B
+                if self.auto_consolidate and (self.conversation_count // self.consolidate_every
+                                              > c0 // self.consolidate_every):
+                    stats["consolidations"] += 1
+                    with tracer.stage("run_consolidation", self._device):
+                        self.run_consolidation()
+                self._maybe_cluster(c0)
+            elif self._plannable():
+                self._consolidate_planned(flat, conv, B, embs, now, stats)
+            else:
+                self._consolidate_stepwise(flat, conv, B, embs, now, stats)
+            if self.query_cache:
+                self.query_cache.invalidate_results()
             self._save_to_persistence()
         return stats
 
@@ -671,7 +735,322 @@ class ConsolidationMixin:
                 self._store_delete([g.ids[r] for r in victims])
             stats["evicted"] += len(victims)
 
-    def _consolidate_batch(self, facts: List[Dict], conv: np.ndarray, B: int, embs, now: float,
+    def _plannable(self) -> bool:
+        """The host plan needs the graph-bound store (its search = the
+        graph's stored node rows, L2) and a run_consolidation that leaves the
+        graph as it is (the reference's no-op merge)."""
+        return (self._store_binds_graph() and getattr(self.vector_store, "metric", "l2") == "l2"
+                and self.merge_mode == "reference")
+
+    def _consolidate_stepwise(self, facts, conv, B, embs, now, stats) -> None:
+        """B end_conversation bodies one after another (third-party stores,
+        merge_mode="pairwise"): the same code path as the sequential calls."""
+        E = None
+        if facts:
+            E, valid = self._fact_matrix(embs, len(facts))
+        for c in range(B):
+            jj = [j for j in np.nonzero(conv == c)[0].tolist() if E is not None and valid[j]]
+            n0 = self.graph.num_nodes()
+            if jj:
+                made = self._ingest_facts([facts[j] for j in jj], E[torch.as_tensor(jj, device=E.device)])
+                stats["inserted"] += len(made)
+                stats["dup"] += len(jj) - len(made)
+            pruned = self.graph.decay(DECAY_RATE, self.prune_threshold if self.auto_prune else None)
+            stats["pruned"] += pruned
+            self._enforce_buffer_limit_counted(stats)
+            self.conversation_count += 1
+            if self.auto_consolidate and self.conversation_count % self.consolidate_every == 0:
+                stats["consolidations"] += 1
+                self.run_consolidation()
+            self._maybe_cluster(self.conversation_count - 1)
+
+    def _consolidate_planned(self, facts, conv, B, embs, now, stats) -> None:
+        from .batch_plan import BatchPlanner, PoolTooSmall
+        g = self.graph
+        M = len(facts)
+        E = None
+        if M:
+            E, valid = self._fact_matrix(embs, M)
+            rejected = M - int(valid.sum())
+            if rejected:
+                self.metrics["rejected_embeddings"] = self.metrics.get("rejected_embeddings", 0) + rejected
+            vidx = np.nonzero(valid)[0]
+            facts = [facts[i] for i in vidx]
+            conv = conv[vidx]
+            E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
+            M = len(facts)
+        dev = g.device
+        # shards are created in fact order, duplicates included (reference :716-718)
+        shard_keys = [f.get("topic", self._infer_shard_key(f["content"])) for f in facts]
+        codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int64)
+        sal_in = np.asarray([float(f.get("salience", 0.5)) for f in facts], dtype=np.float32)
+        thr = self.prune_threshold if self.auto_prune else None
+        keep = 1.0 - DECAY_RATE
+        with tracer.stage("cb_scan", self._device):
+            inputs = self._plan_inputs(E, codes, B, M)
+        P = inputs.pop("P0")
+        while True:
+            pool, pool_mask = self._eviction_pool(B, P, now)
+            try:
+                pl = BatchPlanner(ct=conv, code=codes, sal_in=sal_in, n0=g.n, node_count=g.num_nodes(),
+                                  shard_count=list(g.shard_count), super_codes=self._super_codes(),
+                                  pre_members=lambda c: g.node_rows_where(c, super_=False),
+                                  max_buffer=self.max_buffer_size, super_threshold=self.super_node_threshold,
+                                  ref_hierarchy=self.enable_hierarchy and getattr(self, "hierarchy_mode",
+                                                                                  "reference") == "reference",
+                                  prune_thr=thr, keep=keep, now=now, pool=pool,
+                                  **self._plan_rows(inputs, pool), **inputs)
+                with tracer.stage("cb_plan", "cpu"):
+                    hp = self.hierarchy_params if getattr(self, "hierarchy_mode", "") == "kmeans" else None
+                    segs = pl.run(B, self.conversation_count, self.auto_consolidate, self.consolidate_every,
+                                  hp["every"] if (hp and self.enable_hierarchy) else 0)
+                with tracer.stage("cb_verify", self._device):
+                    if pool_mask is not None and not self._verify_pool(pool_mask, pl.events, now):
+                        raise PoolTooSmall
+                break
+            except PoolTooSmall:
+                if P >= g.n:
+                    raise
+                stats["pool_retries"] = stats.get("pool_retries", 0) + 1
+                P = min(g.n, 4 * P)
+        for k in ("dup", "inserted", "linked", "cross_links", "evicted", "fallbacks"):
+            stats[k] += pl.stats[k]
+        stats["pruned"] += pl.stats["pruned_new"]
+        ids = [self._generate_node_id() for _ in range(int((pl.fact_key >= 0).sum()))]
+        id_of = dict(zip(pl.fact_key[pl.fact_key >= 0].tolist(), ids))
+        count0 = self.conversation_count
+        for seg in segs:
+            with tracer.stage("cb_apply", self._device):
+                stats["pruned"] += self._apply_segment(seg, pl, facts, shard_keys, E, id_of, thr, now)
+            self.conversation_count = count0 + seg.c1 + 1
+            if seg.consolidate:
+                stats["consolidations"] += 1
+                with tracer.stage("run_consolidation", self._device):
+                    self.run_consolidation()
+            if seg.cluster:
+                self._maybe_cluster(self.conversation_count - 1)
+        if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
+            self._maybe_cluster(self.conversation_count - 1)
+
+    def _super_codes(self) -> List[int]:
+        g = self.graph
+        srows = g.node_rows_where(super_=True)
+        return sorted(set(g.mirror("shard")[srows].tolist())) if srows.size else []
+
+    def _plan_inputs(self, E, codes: np.ndarray, B: int, M: int) -> Dict:
+        """One scan of the batch against the pre-batch graph + the F x F
+        block: candidate lists, super-node cosines, the fallback and
+        super-embedding callbacks of the planner."""
+        g = self.graph
+        n = g.n
+        dev = g.device
+        K = self.BATCH_LIST_K
+        NEGF = float("-inf")
+        if M:
+            Q = E.to(dev, torch.float32)
+            Qd = Q.double()
+            qn = Qd.norm(dim=1, keepdim=True)
+            Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        else:
+            Q = Qn = torch.zeros((0, g.dim or 1), dtype=torch.float64, device=dev)
+        link_mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0) if n else None
+        if n and M:
+            with g.on_stream():
+                (gs, gr), (ws, wr) = g.cos_topk(Q, K, link_mask, dual_label=torch.as_tensor(codes),
+                                                min_score=LINK_THRESHOLD)
+        else:
+            gs = ws = torch.full((M, K), NEGF, dtype=torch.float64)
+            gr = wr = torch.full((M, K), -1, dtype=torch.long)
+        # stored super-nodes: the store top-1 compares them by L2 (they are not unit rows)
+        srows = g.node_rows_where(super_=True) if n else np.zeros(0, np.int64)
+        if srows.size and M:
+            with g.on_stream():
+                st = torch.as_tensor(srows, dtype=torch.long).to(dev)
+                X = g.emb32[st].double()
+                nrm = g.sqn[st].double().sqrt()
+                sup_cos = ((Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]).cpu().numpy()
+                sup_n2 = g.sqn[st].double().cpu().numpy()
+        else:
+            sup_cos, sup_n2 = np.zeros((M, 0)), np.zeros(0)
+        # fact x fact cosine with the scan's formula (rows stored as fp32, |x|^2 rounded to fp32)
+        if M:
+            X = Q.double()
+            nrm = (X * X).sum(1).float().double().sqrt()
+            S = ((Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]).cpu().numpy()
+            qnorm = qn.flatten().cpu().numpy()
+            fact_n2 = (X * X).sum(1).float().double().cpu().numpy()
+        else:
+            S, qnorm, fact_n2 = np.zeros((0, 0)), np.zeros(0), np.zeros(0)
+
+        def fallback(j, evicted, same_shard):
+            m = link_mask.clone()
+            if evicted.size:
+                m[torch.as_tensor(evicted, dtype=torch.long).to(dev)] = False
+            with g.on_stream():
+                if same_shard:
+                    s_, r_ = g._exact_cos(Qn[j:j + 1], m, K, row_label=g.shard[:n],
+                                          q_label=torch.as_tensor(codes[j:j + 1]).to(dev))
+                else:
+                    s_, r_ = g._exact_cos(Qn[j:j + 1], m, K)
+            return s_[0].cpu().numpy(), r_[0].cpu().numpy()
+
+        n0 = n
+
+        def super_cos(children, key_fact):
+            """Cosine of every fact against the mean embedding of ``children``
+            (pre-batch rows, then batch rows: the row order the graph's
+            mean_embedding reads), as the dedupe scan of a stored super-node."""
+            ch = np.asarray(children, dtype=np.int64)
+            parts = []
+            pre, new = ch[ch < n0], ch[ch >= n0]
+            if pre.size:
+                parts.append(g.emb32[torch.as_tensor(pre, dtype=torch.long).to(dev)])
+            if new.size:
+                parts.append(Q[torch.as_tensor([key_fact[int(r)] for r in new], dtype=torch.long, device=dev)])
+            if not parts:
+                return np.full(M, NEGF), 1.0
+            e = torch.cat(parts).double().mean(0).float()
+            self._plan_super_emb[tuple(children)] = e
+            ed = e.double()
+            n2 = float((ed * ed).sum().float())
+            en = n2 ** 0.5
+            return (((Qn @ ed) / (en if en > 0 else 1.0)).cpu().numpy() if M else np.zeros(0)), n2
+
+        self._plan_super_emb = {}
+        excess0 = max(0, g.num_nodes() - self.max_buffer_size)
+        return {"glob": (gs.cpu().numpy(), gr.cpu().numpy()), "shard": (ws.cpu().numpy(), wr.cpu().numpy()),
+                "sup_rows": srows, "sup_cos": sup_cos, "sup_n2": sup_n2, "qnorm": qnorm, "fact_n2": fact_n2, "S": S,
+                "super_cos": super_cos, "fallback": fallback, "P0": min(n, 4 * (M + excess0) + 1024)}
+
+    def _eviction_pool(self, B: int, P: int, now: float):
+        """The eviction pool of a batch plan: the P lowest-importance
+        evictable rows now and after all B decays (ties in any order: the
+        plan is verified against every other row afterwards,
+        :meth:`_verify_pool`). Returns (rows, device mask) -- mask None when
+        the pool is every evictable row (nothing to verify)."""
+        from ..ops import tenant_ops as T
+        g = self.graph
+        n = g.n
+        if n == 0:
+            return np.zeros(0, np.int64), None
+        with g.on_stream():
+            imp0 = T.importance(g.sal[:n], g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now)
+            nev = int(torch.isfinite(imp0).sum())
+            if P >= nev:
+                return torch.nonzero(torch.isfinite(imp0)).flatten().cpu().numpy(), None
+            sal = g.sal[:n].clone()
+            empty = {"src": torch.zeros(0, dtype=torch.int32, device=g.device),
+                     "dst": torch.zeros(0, dtype=torch.int32, device=g.device),
+                     "w": torch.zeros(0, dtype=torch.float32, device=g.device)}
+            T.decay_prune(empty, sal, g.kind[:n], g.sup[:n], DECAY_RATE, None, steps=B)
+            impB = T.importance(sal, g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now)
+            okey = g.shard[:n].long() * (1 << 32) + torch.arange(n, device=g.device)
+            mask = torch.zeros(n, dtype=torch.uint8, device=g.device)
+            for imp in (imp0, impB):
+                mask[_lowest_keys(imp, okey, P)] = 1
+            return torch.nonzero(mask).flatten().cpu().numpy(), mask
+
+    def _verify_pool(self, pool_mask: torch.Tensor, events, now: float) -> bool:
+        from ..ops import tenant_ops as T
+        g = self.graph
+        n = g.n
+        with g.on_stream():
+            return T.evict_verify(g.sal[:n], g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], g.shard[:n], pool_mask,
+                                  now, 1.0 - DECAY_RATE, events)
+
+    def _plan_rows(self, inputs: Dict, pool: np.ndarray) -> Dict:
+        """Host state (sal, acc, last, shard, super) of every pre-batch row the
+        batch can touch: the pool, the candidate-list rows, the super-nodes."""
+        g = self.graph
+        gr, wr = inputs["glob"][1], inputs["shard"][1]
+        rows = np.unique(np.concatenate([pool.astype(np.int64), gr[gr >= 0].astype(np.int64),
+                                         wr[wr >= 0].astype(np.int64),
+                                         np.asarray(inputs["sup_rows"], np.int64)]))
+        if rows.size:
+            with g.on_stream():
+                rt = torch.as_tensor(rows, dtype=torch.long).to(g.device)
+                cols = (g.sal[rt].cpu().numpy().astype(np.float32), g.acc[rt].cpu().numpy().astype(np.int64),
+                        g.last[rt].cpu().numpy(), g.shard[rt].cpu().numpy().astype(np.int64),
+                        (g.sup[rt] != 0).cpu().numpy(), g.sqn[rt].double().cpu().numpy())
+        else:
+            cols = (np.zeros(0, np.float32), np.zeros(0, np.int64), np.zeros(0), np.zeros(0, np.int64),
+                    np.zeros(0, bool), np.zeros(0))
+        return {"rows": rows, "cols": cols}
+
+    def _apply_segment(self, seg, pl, facts, shard_keys, E, id_of, thr, now) -> int:
+        """Apply conversations [seg.c0, seg.c1] of the plan to the device graph.
+        Returns edges pruned by the decay of the rows that existed before."""
+        g = self.graph
+        dev = g.device
+        steps = seg.c1 - seg.c0 + 1
+        pruned = g.decay(DECAY_RATE, thr, steps=steps)
+        if seg.touched:
+            rows = np.fromiter(seg.touched.keys(), np.int64)
+            vals = list(seg.touched.values())
+            with g.on_stream():
+                rt = torch.as_tensor(rows, dtype=torch.long).to(dev)
+                g.sal[rt] = torch.as_tensor([v[0] for v in vals], dtype=torch.float32).to(dev)
+                g.acc[rt] = torch.as_tensor([v[1] for v in vals], dtype=torch.int32).to(dev)
+                g.last[rt] = torch.as_tensor([v[2] for v in vals], dtype=torch.float64).to(dev)
+                g.dirty[rt] = 1
+            g._bump()
+        stored = self._store_binds_graph()
+        i = 0
+        ins = seg.inserts
+        while i < len(ins):
+            kind, x = ins[i]
+            if kind == "fact":
+                k = i
+                while k < len(ins) and ins[k][0] == "fact":
+                    k += 1
+                js = [ins[t][1] for t in range(i, k)]
+                keys = [int(pl.fact_key[j]) for j in js]
+                st = [seg.new_state[key] for key in keys]
+                rows = g.add_nodes([id_of[key] for key in keys], [facts[j]["content"] for j in js],
+                                   E[torch.as_tensor(js, dtype=torch.long).to(E.device)],
+                                   shard=pl.code[js].astype(np.int32),
+                                   types=[facts[j].get("type", "semantic") for j in js],
+                                   sal=torch.as_tensor([v[0] for v in st], dtype=torch.float32),
+                                   acc=torch.as_tensor([v[1] for v in st], dtype=torch.int32),
+                                   last=torch.as_tensor([v[2] for v in st], dtype=torch.float64), now=now,
+                                   stored=stored)
+                if rows.tolist() != keys:
+                    raise RuntimeError("batch plan row assignment diverged from the graph")
+                i = k
+            else:
+                sp = pl.supers[x]
+                skey = shard_keys_of(g, sp.code)
+                ch_ids = [g.ids[r] if r < pl.n0 else id_of[r] for r in sp.children]
+                sid = f"super_{skey}_{int(now)}"
+                content = [g.content[r] if r < pl.n0 else facts[self._fact_of_key(pl, r)]["content"]
+                           for r in sp.children[:3]]
+                summary = f"Topic: {skey}. Contains memories about: " + "; ".join(content)
+                emb = self._plan_super_emb[tuple(sp.children)]
+                v = seg.new_state[sp.key]
+                srow = g.add_nodes([sid], [summary], emb[None, :], shard=[sp.code], sup=[1],
+                                   children={0: ch_ids}, stored=False, sal=v[0], acc=v[1], last=v[2], now=now)
+                if int(srow[0]) != sp.key:
+                    raise RuntimeError("batch plan super-node row diverged from the graph")
+                with g.on_stream():
+                    rt = torch.as_tensor(sp.children, dtype=torch.long).to(dev)
+                    g.parent[rt] = srow.to(torch.int32)[0]
+                    g.dirty[rt] = 1
+                g._bump()
+                i += 1
+        if seg.edges:
+            e = seg.edges
+            g.append_edges(torch.as_tensor([pl.e_src[x] for x in e], dtype=torch.long).to(dev),
+                           torch.as_tensor([pl.e_dst[x] for x in e], dtype=torch.long).to(dev),
+                           torch.as_tensor(seg.edge_w, dtype=torch.float32).to(dev),
+                           torch.as_tensor([pl.e_code[x] for x in e], dtype=torch.int32).to(dev),
+                           g.etype("relates_to"), now=now)
+        if seg.victims:
+            ids = [g.ids[r] for r in seg.victims]
+            g.remove_nodes(seg.victims, drop_edges=True, unstore=True)
+            self._store_delete(ids)
+        return pruned
+
+    def _consolidate_batch_coarse(self, facts: List[Dict], conv: np.ndarray, B: int, embs, now: float,
                            stats: Dict[str, int]) -> None:
         g = self.graph
         keep = 1.0 - DECAY_RATE
@@ -688,13 +1067,13 @@ class ConsolidationMixin:
             E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
             M = len(facts)
         if M == 0:
-            stats["pruned"] += g.decay(1.0 - keep ** B, thr)
+            stats["pruned"] += g.decay(DECAY_RATE, thr, steps=B)
             return
         dev = g.device
         # shards are created in fact order, duplicates included (reference :716-718)
         shard_keys = [f.get("topic", self._infer_shard_key(f["content"])) for f in facts]
         codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int32)
-        sal_in = torch.as_tensor([float(f.get("salience", 0.5)) for f in facts], dtype=torch.float64).to(dev)
+        sal_in = torch.as_tensor([float(f.get("salience", 0.5)) for f in facts], dtype=torch.float32).to(dev)
         ct = torch.as_tensor(conv).to(dev)
         Q = E.to(dev, torch.float32)
         Qd = Q.double()
@@ -725,7 +1104,7 @@ class ConsolidationMixin:
 
         # ---- 3. decay + prune the pre-batch graph by B conversations at once
         with tracer.stage("cb_decay", self._device):
-            stats["pruned"] += g.decay(1.0 - keep ** B, thr)
+            stats["pruned"] += g.decay(DECAY_RATE, thr, steps=B)
 
         # ---- 4. duplicate merges (reference :736-740)
         ndup = int(dup.sum())
@@ -789,6 +1168,10 @@ class ConsolidationMixin:
         if plan is not None:
             Sr, Dr, W, H = plan
             g.append_edges(Sr, Dr, W.float(), H.to(torch.int32), g.etype("relates_to"), now=now)
+
+    @staticmethod
+    def _fact_of_key(pl, key: int) -> int:
+        return int(np.nonzero(pl.fact_key == key)[0][0])
 
     # ------------------------------------------------------------ hierarchy (K8/K16)
     def _create_super_nodes_for_shard(self, shard_key: str):

@@ -825,14 +825,20 @@ class TenantGraph:
             self.deleted_edges[(ids[a], ids[b])] = None
 
     # ------------------------------------------------------------------ maintenance
-    def decay(self, rate: float = 0.01, prune_threshold: Optional[float] = None, decay_nodes: bool = True) -> int:
-        """Temporal decay of all edges and shard-node saliences (+ optional
-        prune) in one kernel pass. Returns the number of pruned edges."""
+    def decay(self, rate: float = 0.01, prune_threshold: Optional[float] = None, decay_nodes: bool = True,
+              steps: int = 1) -> int:
+        """Temporal decay of all edges and shard-node saliences, ``steps``
+        rounds (= that many end_conversation calls, each rounded to fp32),
+        + optional prune, in one kernel pass. Returns the number of pruned
+        edges."""
+        if steps <= 0:
+            return 0
         with self.on_stream():
             self.e, n, dropped = T.decay_prune(self.e, self.sal[: self.n], self.kind[: self.n], self.sup[: self.n],
-                                               rate, prune_threshold, decay_nodes, want_dropped=self.track)
+                                               rate, prune_threshold, decay_nodes, want_dropped=self.track,
+                                               steps=steps)
         if rate:
-            self.decay_log += math.log1p(-rate)
+            self.decay_log += steps * math.log1p(-rate)
         if dropped is not None and n:
             self._note_dropped(*dropped)
         self._bump(edges=bool(n) or bool(rate))

@@ -21,12 +21,13 @@ from . import _lib
 P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
 D_ = C.c_double
 
-_lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, P])
+_lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
 _lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
+_lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 
@@ -56,10 +57,11 @@ def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, n
 
 
 def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, threshold: Optional[float],
-                decay_nodes: bool = True, want_dropped: bool = False):
+                decay_nodes: bool = True, want_dropped: bool = False, steps: int = 1):
     """Temporal decay of every edge and shard-node salience (reference
-    memory_shard.py:64-77), then, if ``threshold`` is not None, removal of
-    edges with ``w < threshold`` (:79-84) with stable compaction.
+    memory_shard.py:64-77), ``steps`` rounds (each rounded to fp32, as
+    ``steps`` end_conversation calls), then, if ``threshold`` is not None,
+    removal of edges with ``w < threshold`` (:79-84) with stable compaction.
 
     Returns (edges, n_pruned, dropped) where ``dropped`` is (src, dst, meta)
     of the pruned edges when ``want_dropped`` (for incremental persistence)."""
@@ -68,13 +70,14 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
     nn = int(sal.numel()) if sal is not None else 0
     dropped = None
     if not e["src"].is_cuda:
-        if rate:
-            e["w"].mul_(keep)
-        if decay_nodes and nn:
-            m = (kind == 1) & (sup == 0)
-            dec = torch.where(sal > SALIENCE_FLOOR, SALIENCE_FLOOR + (sal - SALIENCE_FLOOR) * keep,
-                              torch.full_like(sal, SALIENCE_FLOOR))
-            sal.copy_(torch.where(m, dec, sal))
+        for _ in range(steps):
+            if rate:
+                e["w"].mul_(keep)
+            if decay_nodes and nn:
+                m = (kind == 1) & (sup == 0)
+                dec = torch.where(sal > SALIENCE_FLOOR, SALIENCE_FLOOR + (sal - SALIENCE_FLOOR) * keep,
+                                  torch.full_like(sal, SALIENCE_FLOOR))
+                sal.copy_(torch.where(m, dec, sal))
         if threshold is None or ne == 0:
             return e, 0, dropped
         f = e["w"] >= threshold
@@ -91,7 +94,7 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
     thr = float(threshold) if threshold is not None else float("-inf")
     _lib.check(_lib.lib().lzk_tg_decay(e["w"].data_ptr(), ne, float(keep), thr, _lib.ptr(flag), _lib.ptr(bc),
                                        _lib.ptr(sal), _lib.ptr(kind), _lib.ptr(sup), nn,
-                                       1 if (decay_nodes and nn) else 0, _st(e["w"])), "tg_decay")
+                                       1 if (decay_nodes and nn) else 0, int(steps), _st(e["w"])), "tg_decay")
     if threshold is None or ne == 0:
         return e, 0, dropped
     if want_dropped:
@@ -237,6 +240,50 @@ def importance(sal, acc, last, kind, sup, now: float) -> torch.Tensor:
                                             sup.data_ptr(), sal.numel(), float(now), out.data_ptr(), _st(sal)),
                "tg_importance")
     return out
+
+
+def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: float, keep: float,
+                 events: Sequence[Tuple[int, float, int, int]]) -> bool:
+    """True when no row outside ``pool`` (uint8 mask) that nothing touched
+    would have been evicted before the planned victims: ``events`` =
+    (decays before the eviction, importance, shard, row) of each eviction's
+    last victim, in order (core/batch_plan.py)."""
+    if not events:
+        return True
+    n = int(sal.numel())
+    if not sal.is_cuda:
+        import numpy as np
+        m = ((kind == 1) & (sup == 0) & (pool == 0)).numpy()
+        idx = np.nonzero(m)[0]
+        if idx.size == 0:
+            return True
+        s = sal.numpy()[idx].astype(np.float32)
+        a = np.minimum(1.0, acc.numpy()[idx].astype(np.float64) / 10.0) * 0.3
+        d = (1.0 / (1.0 + (np.float64(now) - last.numpy()[idx]) / 86400.0)) * 0.2
+        code = shard.numpy()[idx].astype(np.int64)
+        kf, fl = np.float32(keep), np.float32(SALIENCE_FLOOR)
+        t = 0
+        for st, vi, vc, vr in events:
+            while t < st:
+                s = np.where(s > fl, fl + (s - fl) * kf, fl).astype(np.float32)
+                t += 1
+            imp = s.astype(np.float64) * 0.5 + a + d
+            if ((imp < vi) | ((imp == vi) & ((code < vc) | ((code == vc) & (idx < vr))))).any():
+                return False
+        return True
+    dev = sal.device
+    ev = list(events)
+    steps = torch.tensor([e[0] for e in ev], dtype=torch.int32).to(dev)
+    imp = torch.tensor([e[1] for e in ev], dtype=torch.float64).to(dev)
+    code = torch.tensor([e[2] for e in ev], dtype=torch.int32).to(dev)
+    row = torch.tensor([e[3] for e in ev], dtype=torch.int64).to(dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().lzk_tg_evict_verify(sal.data_ptr(), acc.data_ptr(), last.data_ptr(), kind.data_ptr(),
+                                              sup.data_ptr(), shard.data_ptr(), pool.data_ptr(), n, float(now),
+                                              float(keep), len(ev), steps.data_ptr(), imp.data_ptr(),
+                                              code.data_ptr(), row.data_ptr(), bad.data_ptr(), _st(sal)),
+               "tg_evict_verify")
+    return int(bad.item()) == 0
 
 
 def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:

@@ -8,9 +8,12 @@ each rank's part is an ordinary :class:`~lazzaro_amd.core.MemorySystem` graph
 ``"{user}@{rank}/{world}"``) -- and runs the reference's consolidation over
 the WHOLE buffer with the sequential semantics of the single-process engine:
 ``consolidate_batch`` on N ranks gives the nodes, saliences, edges and
-eviction victims that ``MemorySystem.consolidate_batch`` gives on one process
-holding the union of the rows and all ranks' conversations (rank-major
-order). Reference flow: ``memory_system.py:580-649`` (end_conversation),
+eviction victims that ``MemorySystem.consolidate_batch(cadence="batch")``
+gives on one process holding the union of the rows and all ranks'
+conversations (rank-major order): batch cadence -- eviction, super-nodes and
+``run_consolidation`` once per batch; the single-tenant engine's default
+``cadence="conversation"`` plays them at every conversation like the
+reference. Reference flow: ``memory_system.py:580-649`` (end_conversation),
 ``:651-891`` (dedupe, links), ``:535-578`` (eviction), ``:935-1010``
 (run_consolidation).
 
@@ -372,7 +375,7 @@ class ShardedMemorySystem:
             E = torch.zeros((0, D), dtype=torch.float32, device=dev)
         B_loc = len(conversations)
         stats = {"conversations": 0, "facts": 0, "dup": 0, "inserted": 0, "linked": 0, "cross_links": 0,
-                 "pruned": 0, "evicted": 0}
+                 "pruned": 0, "evicted": 0, "consolidations": 0, "fallbacks": 0}
         with self.local._graph_lock, tracer.stage("sharded_consolidate", dev):
             self._consolidate(flat, conv, E, B_loc, now, stats)
             self._evict(now, stats)
@@ -380,6 +383,7 @@ class ShardedMemorySystem:
             self.conversation_count += stats["conversations"]
             if self.auto_consolidate and (self.conversation_count // self.consolidate_every
                                           > c0 // self.consolidate_every):
+                stats["consolidations"] += 1
                 with tracer.stage("run_consolidation", dev):
                     self.run_consolidation()
             hp = self.hierarchy_params
@@ -406,7 +410,7 @@ class ShardedMemorySystem:
             c_off = int(sum(bl[: self.rank]))
             keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
             keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self.world > 1 else keys
-            sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float64, device=dev)
+            sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
             ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
             Qa, fcnt = self._gather_var(E)
             sal_in, _ = self._gather_var(sal_l)
@@ -415,7 +419,7 @@ class ShardedMemorySystem:
         F = int(Qa.shape[0])
         stats["facts"] = F
         if F == 0:
-            stats["pruned"] += self._sum(g.decay(1.0 - keep ** B, thr))[0]
+            stats["pruned"] += self._sum(g.decay(1.0 - keep, thr, steps=B))[0]
             return
         f_off = int(sum(fcnt[: self.rank]))
         origin = torch.repeat_interleave(torch.arange(self.world, device=dev),
@@ -442,7 +446,7 @@ class ShardedMemorySystem:
 
         # ---- 4. decay + prune this rank's edges / node saliences by B conversations
         with tracer.stage("sc_decay", dev):
-            stats["pruned"] += self._sum(g.decay(1.0 - keep ** B, thr))[0]
+            stats["pruned"] += self._sum(g.decay(1.0 - keep, thr, steps=B))[0]
 
         # ---- 5. duplicate merges onto the rows this rank holds
         stats["dup"] += int(dup.sum())

@@ -117,7 +117,7 @@ def _single(tmp, cfg=CPU):
         real = tgm.time.time
         tgm.time.time = lambda s=s: _now(s)  # the single-process eviction reads the wall clock
         try:
-            stats.append(ms.consolidate_batch(convs, embeddings=V.to(dev), now=_now(s)))
+            stats.append(ms.consolidate_batch(convs, embeddings=V.to(dev), now=_now(s), cadence="batch"))
         finally:
             tgm.time.time = real
     nodes, edges = _graph_state(g)

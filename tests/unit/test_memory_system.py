@@ -420,10 +420,12 @@ def test_kmeans_hierarchy_mode_clusters_and_retrieves(tmp_path):
     ms.consolidate_batch(convs, embeddings=np.asarray(vecs, np.float32))
     g = ms.graph
     assert g.hier and g.hier["top_c"].shape[0] == 4 and ms.get_stats()["num_super_nodes"] == 0
+    # the last pass ran at conversation 10 (every 5, exact cadence): it covers
+    # the rows that existed then
     tops = g.hier["top"][: g.n].tolist()
     # facts of one generating centre share a topic cluster
     by_center = {}
-    for r in range(g.n):
+    for r in range(len(tops)):
         if g.kind_h(r) == 1:
             by_center.setdefault(g.content[r].split()[1], set()).add(tops[r])
     assert all(len(v) == 1 for v in by_center.values()) and len({min(v) for v in by_center.values()}) == 4
