@@ -10,6 +10,7 @@
 #include "colstore.h"
 #include "tokenizer.h"
 #include "graph_host.h"
+#include "batch_plan.h"
 
 namespace py = pybind11;
 using namespace lzrt;
@@ -289,4 +290,5 @@ PYBIND11_MODULE(_lzrt, m) {
         "rendezvous-hash owner of a tenant among an explicit set of rank ids");
   m.def("tenant_rank", &tenant_rank, py::arg("tenant"), py::arg("world"),
         "consistent-hash placement of a tenant id onto one of `world` ranks");
+  register_batch_plan(m);
 }

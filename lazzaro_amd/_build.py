@@ -140,7 +140,9 @@ def build_runtime(verbose: bool = False, sanitize: str = "", outdir: str = "") -
         arrow_so = sorted(f for f in os.listdir(pa_dir) if re.fullmatch(r"libarrow\.so\.\d+", f))
         if not arrow_so:
             raise RuntimeError(f"no libarrow.so.<N> in {pa_dir} (pyarrow wheel)")
-        cmd = [cxx] + opt + ["-std=c++20", "-shared", "-fPIC", "-fvisibility=hidden",
+        # -ffp-contract=off: the batch planner replays the device kernels'
+        # fp32 / fp64 rounding operation by operation (no fma contraction)
+        cmd = [cxx] + opt + ["-std=c++20", "-ffp-contract=off", "-shared", "-fPIC", "-fvisibility=hidden",
                              "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
                              "-I" + pa.get_include(), "-I" + os.path.join(CSRC, "runtime")] + srcs + [
             "-o", out, "-L" + pa_dir, "-l:" + arrow_so[0], "-Wl,-rpath," + pa_dir, "-lpthread"]

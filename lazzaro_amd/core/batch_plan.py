@@ -364,7 +364,8 @@ class BatchPlanner:
             pre = [int(r) for r in self.pre_members(code) if self._present(int(r))]
             new = [int(self.fact_key[j]) for j in np.nonzero((self.fact_key >= 0) & (self.code == code))[0]]
             children = pre + [k for k in new if self._present(k)]
-            cos, n2 = self.super_cos(children, self.key_fact)
+            cos, n2 = self.super_cos(np.asarray(children, np.int64),
+                                     np.asarray([self.key_fact[k] for k in children if k >= self.n0], np.int64))
             sp = Super(code, key, children, c, cos, n2)
             self.supers.append(sp)
             self.super_codes.add(code)
@@ -431,3 +432,65 @@ class BatchPlanner:
         s.edges = [e for e in s.edges if self.e_alive[e]]
         s.edge_w = self.e_w[s.edges].copy() if s.edges else np.zeros(0, F32)  # weights at c1
         return s
+
+
+def segments_as_dicts(pl: "BatchPlanner", segs: List[Segment]) -> List[Dict]:
+    """The Python planner's segments in the native planner's format
+    (``_lzrt.plan_batch``): what ``MemorySystem._apply_segment`` reads."""
+    out = []
+    for sg in segs:
+        kinds = np.asarray([0 if k == "fact" else 1 for k, _ in sg.inserts], np.int32)
+        idx = np.asarray([i for _, i in sg.inserts], np.int32)
+        keys = [int(pl.fact_key[i]) if k == "fact" else pl.supers[i].key for k, i in sg.inserts]
+        st = [sg.new_state[k] for k in keys]
+        tr = list(sg.touched.keys())
+        tv = [sg.touched[r] for r in tr]
+        out.append({"c0": sg.c0, "c1": sg.c1, "consolidate": sg.consolidate, "cluster": sg.cluster,
+                    "ins_kind": kinds, "ins_idx": idx,
+                    "ins_sal": np.asarray([v[0] for v in st], np.float64),
+                    "ins_acc": np.asarray([v[1] for v in st], np.int64),
+                    "ins_last": np.asarray([v[2] for v in st], np.float64),
+                    "edge_src": np.asarray([pl.e_src[e] for e in sg.edges], np.int64),
+                    "edge_dst": np.asarray([pl.e_dst[e] for e in sg.edges], np.int64),
+                    "edge_code": np.asarray([pl.e_code[e] for e in sg.edges], np.int64),
+                    "edge_w": np.asarray(sg.edge_w, np.float32),
+                    "victims": np.asarray(sg.victims, np.int64),
+                    "tch_rows": np.asarray(tr, np.int64),
+                    "tch_sal": np.asarray([v[0] for v in tv], np.float64),
+                    "tch_acc": np.asarray([v[1] for v in tv], np.int64),
+                    "tch_last": np.asarray([v[2] for v in tv], np.float64)})
+    return out
+
+
+def plan(kw: Dict, B: int, count0: int, auto: bool, every: int, cluster_every: int, native: bool = True) -> Dict:
+    """Run the planner (native ``_lzrt.plan_batch`` by default, this module's
+    BatchPlanner as the reference) on one input dict; returns segments,
+    supers, events, fact_key, dup_of and stats in the native format."""
+    if native:
+        from ..store.colstore import _rt
+        args = dict(kw)
+        args.update(B=B, count0=count0, auto=auto, every=every, cluster_every=cluster_every)
+        gs, gr = args.pop("glob")
+        ss, sr = args.pop("shard")
+        args.update(gs=np.ascontiguousarray(gs, np.float64), gr=np.ascontiguousarray(gr, np.int64),
+                    ss=np.ascontiguousarray(ss, np.float64), sr=np.ascontiguousarray(sr, np.int64))
+        rows = args.pop("rows")
+        cols = args.pop("cols")
+        pool = np.asarray(args.pop("pool"), np.int64)
+        args.update(rows=rows, sal=cols[0], acc=cols[1], last=cols[2], ncode=cols[3],
+                    sup=np.asarray(cols[4], np.uint8), n2=cols[5],
+                    pool=np.isin(np.asarray(rows, np.int64), pool).astype(np.uint8))
+        args.setdefault("dedupe_thr", 0.95)
+        args.setdefault("link_thr", 0.5)
+        args.setdefault("link_k", 3)
+        args.setdefault("link_scale", 0.8)
+        args.setdefault("chain_w", 0.5)
+        args["super_codes"] = np.asarray(sorted(args["super_codes"]), np.int64)
+        args["shard_count"] = np.asarray(args["shard_count"], np.int64)
+        return _rt().plan_batch(args)
+    pl = BatchPlanner(**kw)
+    segs = pl.run(B, count0, auto, every, cluster_every)
+    return {"segments": segments_as_dicts(pl, segs),
+            "supers": [{"code": sp.code, "key": sp.key, "conv": sp.conv, "children": np.asarray(sp.children)}
+                       for sp in pl.supers],
+            "events": list(pl.events), "fact_key": pl.fact_key, "dup_of": pl.dup_of, "stats": dict(pl.stats)}

@@ -31,6 +31,7 @@ Fixes, all behind documented defaults:
 from __future__ import annotations
 
 import json
+import os
 import time
 from typing import Dict, List, Sequence, Set, Tuple
 
@@ -764,8 +765,11 @@ class ConsolidationMixin:
                 self.run_consolidation()
             self._maybe_cluster(self.conversation_count - 1)
 
+    # LZK_PY_PLANNER=1: the Python reference planner instead of the native one
+    NATIVE_PLANNER = os.environ.get("LZK_PY_PLANNER", "0") != "1"
+
     def _consolidate_planned(self, facts, conv, B, embs, now, stats) -> None:
-        from .batch_plan import BatchPlanner, PoolTooSmall
+        from .batch_plan import PoolTooSmall, plan
         g = self.graph
         M = len(facts)
         E = None
@@ -779,55 +783,56 @@ class ConsolidationMixin:
             conv = conv[vidx]
             E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
             M = len(facts)
-        dev = g.device
         # shards are created in fact order, duplicates included (reference :716-718)
         shard_keys = [f.get("topic", self._infer_shard_key(f["content"])) for f in facts]
         codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int64)
         sal_in = np.asarray([float(f.get("salience", 0.5)) for f in facts], dtype=np.float32)
         thr = self.prune_threshold if self.auto_prune else None
-        keep = 1.0 - DECAY_RATE
         with tracer.stage("cb_scan", self._device):
             inputs = self._plan_inputs(E, codes, B, M)
         P = inputs.pop("P0")
+        hp = self.hierarchy_params if getattr(self, "hierarchy_mode", "") == "kmeans" else None
+        cl_every = hp["every"] if (hp and self.enable_hierarchy) else 0
         while True:
             pool, pool_mask = self._eviction_pool(B, P, now)
-            try:
-                pl = BatchPlanner(ct=conv, code=codes, sal_in=sal_in, n0=g.n, node_count=g.num_nodes(),
-                                  shard_count=list(g.shard_count), super_codes=self._super_codes(),
-                                  pre_members=lambda c: g.node_rows_where(c, super_=False),
-                                  max_buffer=self.max_buffer_size, super_threshold=self.super_node_threshold,
-                                  ref_hierarchy=self.enable_hierarchy and getattr(self, "hierarchy_mode",
-                                                                                  "reference") == "reference",
-                                  prune_thr=thr, keep=keep, now=now, pool=pool,
-                                  **self._plan_rows(inputs, pool), **inputs)
-                with tracer.stage("cb_plan", "cpu"):
-                    hp = self.hierarchy_params if getattr(self, "hierarchy_mode", "") == "kmeans" else None
-                    segs = pl.run(B, self.conversation_count, self.auto_consolidate, self.consolidate_every,
-                                  hp["every"] if (hp and self.enable_hierarchy) else 0)
-                with tracer.stage("cb_verify", self._device):
-                    if pool_mask is not None and not self._verify_pool(pool_mask, pl.events, now):
-                        raise PoolTooSmall
+            kw = dict(ct=conv, code=codes, sal_in=sal_in, n0=g.n, node_count=g.num_nodes(),
+                      shard_count=list(g.shard_count), super_codes=self._super_codes(),
+                      pre_members=lambda c: np.asarray(g.node_rows_where(c, super_=False), np.int64),
+                      max_buffer=self.max_buffer_size, super_threshold=self.super_node_threshold,
+                      ref_hierarchy=bool(self.enable_hierarchy and getattr(self, "hierarchy_mode",
+                                                                           "reference") == "reference"),
+                      prune_thr=thr, keep=1.0 - DECAY_RATE, now=now, pool=pool, **self._plan_rows(inputs, pool),
+                      **inputs)
+            with tracer.stage("cb_plan", "cpu"):
+                pl = plan(kw, B, self.conversation_count, self.auto_consolidate, self.consolidate_every, cl_every,
+                          native=self.NATIVE_PLANNER)
+            with tracer.stage("cb_verify", self._device):
+                ok = pool_mask is None or self._verify_pool(pool_mask, pl["events"], now)
+            if ok:
                 break
-            except PoolTooSmall:
-                if P >= g.n:
-                    raise
-                stats["pool_retries"] = stats.get("pool_retries", 0) + 1
-                P = min(g.n, 4 * P)
+            if P >= g.n:
+                raise PoolTooSmall("eviction plan failed verification with every row in the pool")
+            stats["pool_retries"] = stats.get("pool_retries", 0) + 1
+            P = min(g.n, 4 * P)
+        ps = pl["stats"]
         for k in ("dup", "inserted", "linked", "cross_links", "evicted", "fallbacks"):
-            stats[k] += pl.stats[k]
-        stats["pruned"] += pl.stats["pruned_new"]
-        ids = [self._generate_node_id() for _ in range(int((pl.fact_key >= 0).sum()))]
-        id_of = dict(zip(pl.fact_key[pl.fact_key >= 0].tolist(), ids))
+            stats[k] += int(ps[k])
+        stats["pruned"] += int(ps["pruned_new"])
+        fact_key = np.asarray(pl["fact_key"], np.int64)
+        keys = fact_key[fact_key >= 0]
+        id_of = dict(zip(keys.tolist(), (self._generate_node_id() for _ in range(keys.size))))
+        fact_of = {int(k): int(j) for j, k in enumerate(fact_key.tolist()) if k >= 0}
         count0 = self.conversation_count
-        for seg in segs:
+        for seg in pl["segments"]:
             with tracer.stage("cb_apply", self._device):
-                stats["pruned"] += self._apply_segment(seg, pl, facts, shard_keys, E, id_of, thr, now)
-            self.conversation_count = count0 + seg.c1 + 1
-            if seg.consolidate:
+                stats["pruned"] += self._apply_segment(seg, pl["supers"], fact_key, fact_of, facts, codes, E,
+                                                       id_of, thr, now)
+            self.conversation_count = count0 + int(seg["c1"]) + 1
+            if seg["consolidate"]:
                 stats["consolidations"] += 1
                 with tracer.stage("run_consolidation", self._device):
                     self.run_consolidation()
-            if seg.cluster:
+            if seg["cluster"]:
                 self._maybe_cluster(self.conversation_count - 1)
         if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
             self._maybe_cluster(self.conversation_count - 1)
@@ -896,21 +901,23 @@ class ConsolidationMixin:
 
         n0 = n
 
-        def super_cos(children, key_fact):
+        def super_cos(children, new_facts):
             """Cosine of every fact against the mean embedding of ``children``
-            (pre-batch rows, then batch rows: the row order the graph's
-            mean_embedding reads), as the dedupe scan of a stored super-node."""
+            (pre-batch rows, then batch rows = facts ``new_facts``: the row
+            order the graph's mean_embedding reads), as the dedupe scan of a
+            stored super-node. Returns (cos [M], |e|^2 of the fp32 row)."""
             ch = np.asarray(children, dtype=np.int64)
+            nf = np.asarray(new_facts, dtype=np.int64)
             parts = []
-            pre, new = ch[ch < n0], ch[ch >= n0]
+            pre = ch[ch < n0]
             if pre.size:
                 parts.append(g.emb32[torch.as_tensor(pre, dtype=torch.long).to(dev)])
-            if new.size:
-                parts.append(Q[torch.as_tensor([key_fact[int(r)] for r in new], dtype=torch.long, device=dev)])
+            if nf.size:
+                parts.append(Q[torch.as_tensor(nf, dtype=torch.long, device=dev)])
             if not parts:
                 return np.full(M, NEGF), 1.0
             e = torch.cat(parts).double().mean(0).float()
-            self._plan_super_emb[tuple(children)] = e
+            self._plan_super_emb[tuple(ch.tolist())] = e
             ed = e.double()
             n2 = float((ed * ed).sum().float())
             en = n2 ** 0.5
@@ -977,76 +984,77 @@ class ConsolidationMixin:
                     np.zeros(0, bool), np.zeros(0))
         return {"rows": rows, "cols": cols}
 
-    def _apply_segment(self, seg, pl, facts, shard_keys, E, id_of, thr, now) -> int:
-        """Apply conversations [seg.c0, seg.c1] of the plan to the device graph.
-        Returns edges pruned by the decay of the rows that existed before."""
+    def _apply_segment(self, seg: Dict, supers: List[Dict], fact_key: np.ndarray, fact_of: Dict[int, int],
+                       facts, codes: np.ndarray, E, id_of, thr, now) -> int:
+        """Apply conversations [c0, c1] of a plan to the device graph: B-step
+        decay + prune of what existed before, the touched rows' state, the
+        inserts (facts and super-nodes, in row order), the new edges, the
+        victims. Returns the edges pruned by the decay."""
         g = self.graph
         dev = g.device
-        steps = seg.c1 - seg.c0 + 1
+        steps = int(seg["c1"]) - int(seg["c0"]) + 1
         pruned = g.decay(DECAY_RATE, thr, steps=steps)
-        if seg.touched:
-            rows = np.fromiter(seg.touched.keys(), np.int64)
-            vals = list(seg.touched.values())
+        tr = np.asarray(seg["tch_rows"], np.int64)
+        if tr.size:
             with g.on_stream():
-                rt = torch.as_tensor(rows, dtype=torch.long).to(dev)
-                g.sal[rt] = torch.as_tensor([v[0] for v in vals], dtype=torch.float32).to(dev)
-                g.acc[rt] = torch.as_tensor([v[1] for v in vals], dtype=torch.int32).to(dev)
-                g.last[rt] = torch.as_tensor([v[2] for v in vals], dtype=torch.float64).to(dev)
+                rt = torch.as_tensor(tr).to(dev)
+                g.sal[rt] = torch.as_tensor(np.asarray(seg["tch_sal"], np.float32)).to(dev)
+                g.acc[rt] = torch.as_tensor(np.asarray(seg["tch_acc"], np.int32)).to(dev)
+                g.last[rt] = torch.as_tensor(np.asarray(seg["tch_last"], np.float64)).to(dev)
                 g.dirty[rt] = 1
             g._bump()
         stored = self._store_binds_graph()
+        kinds = np.asarray(seg["ins_kind"]).tolist()
+        idx = np.asarray(seg["ins_idx"]).tolist()
+        isal = np.asarray(seg["ins_sal"], np.float32)
+        iacc = np.asarray(seg["ins_acc"], np.int32)
+        ilast = np.asarray(seg["ins_last"], np.float64)
         i = 0
-        ins = seg.inserts
-        while i < len(ins):
-            kind, x = ins[i]
-            if kind == "fact":
+        while i < len(kinds):
+            if kinds[i] == 0:
                 k = i
-                while k < len(ins) and ins[k][0] == "fact":
+                while k < len(kinds) and kinds[k] == 0:
                     k += 1
-                js = [ins[t][1] for t in range(i, k)]
-                keys = [int(pl.fact_key[j]) for j in js]
-                st = [seg.new_state[key] for key in keys]
+                js = idx[i:k]
+                keys = fact_key[js].tolist()
                 rows = g.add_nodes([id_of[key] for key in keys], [facts[j]["content"] for j in js],
                                    E[torch.as_tensor(js, dtype=torch.long).to(E.device)],
-                                   shard=pl.code[js].astype(np.int32),
+                                   shard=codes[js].astype(np.int32),
                                    types=[facts[j].get("type", "semantic") for j in js],
-                                   sal=torch.as_tensor([v[0] for v in st], dtype=torch.float32),
-                                   acc=torch.as_tensor([v[1] for v in st], dtype=torch.int32),
-                                   last=torch.as_tensor([v[2] for v in st], dtype=torch.float64), now=now,
-                                   stored=stored)
+                                   sal=torch.from_numpy(isal[i:k]), acc=torch.from_numpy(iacc[i:k]),
+                                   last=torch.from_numpy(ilast[i:k]), now=now, stored=stored)
                 if rows.tolist() != keys:
                     raise RuntimeError("batch plan row assignment diverged from the graph")
                 i = k
             else:
-                sp = pl.supers[x]
-                skey = shard_keys_of(g, sp.code)
-                ch_ids = [g.ids[r] if r < pl.n0 else id_of[r] for r in sp.children]
-                sid = f"super_{skey}_{int(now)}"
-                content = [g.content[r] if r < pl.n0 else facts[self._fact_of_key(pl, r)]["content"]
-                           for r in sp.children[:3]]
+                sp = supers[idx[i]]
+                children = np.asarray(sp["children"], np.int64).tolist()
+                skey = shard_keys_of(g, int(sp["code"]))
+                ch_ids = [id_of[r] if r in fact_of else g.ids[r] for r in children]
+                content = [facts[fact_of[r]]["content"] if r in fact_of else g.content[r] for r in children[:3]]
                 summary = f"Topic: {skey}. Contains memories about: " + "; ".join(content)
-                emb = self._plan_super_emb[tuple(sp.children)]
-                v = seg.new_state[sp.key]
-                srow = g.add_nodes([sid], [summary], emb[None, :], shard=[sp.code], sup=[1],
-                                   children={0: ch_ids}, stored=False, sal=v[0], acc=v[1], last=v[2], now=now)
-                if int(srow[0]) != sp.key:
+                emb = self._plan_super_emb[tuple(children)]
+                srow = g.add_nodes([f"super_{skey}_{int(now)}"], [summary], emb[None, :], shard=[int(sp["code"])],
+                                   sup=[1], children={0: ch_ids}, stored=False, sal=float(isal[i]),
+                                   acc=int(iacc[i]), last=float(ilast[i]), now=now)
+                if int(srow[0]) != int(sp["key"]):
                     raise RuntimeError("batch plan super-node row diverged from the graph")
                 with g.on_stream():
-                    rt = torch.as_tensor(sp.children, dtype=torch.long).to(dev)
+                    rt = torch.as_tensor(children, dtype=torch.long).to(dev)
                     g.parent[rt] = srow.to(torch.int32)[0]
                     g.dirty[rt] = 1
                 g._bump()
                 i += 1
-        if seg.edges:
-            e = seg.edges
-            g.append_edges(torch.as_tensor([pl.e_src[x] for x in e], dtype=torch.long).to(dev),
-                           torch.as_tensor([pl.e_dst[x] for x in e], dtype=torch.long).to(dev),
-                           torch.as_tensor(seg.edge_w, dtype=torch.float32).to(dev),
-                           torch.as_tensor([pl.e_code[x] for x in e], dtype=torch.int32).to(dev),
+        es = np.asarray(seg["edge_src"], np.int64)
+        if es.size:
+            g.append_edges(torch.as_tensor(es).to(dev), torch.as_tensor(np.asarray(seg["edge_dst"], np.int64)).to(dev),
+                           torch.as_tensor(np.asarray(seg["edge_w"], np.float32)).to(dev),
+                           torch.as_tensor(np.asarray(seg["edge_code"], np.int32)).to(dev),
                            g.etype("relates_to"), now=now)
-        if seg.victims:
-            ids = [g.ids[r] for r in seg.victims]
-            g.remove_nodes(seg.victims, drop_edges=True, unstore=True)
+        vic = np.asarray(seg["victims"], np.int64).tolist()
+        if vic:
+            ids = [g.ids[r] for r in vic]
+            g.remove_nodes(vic, drop_edges=True, unstore=True)
             self._store_delete(ids)
         return pruned
 
