@@ -41,6 +41,7 @@ turns/sec = conversations consolidated per second over all ranks.
 """
 from __future__ import annotations
 
+import math
 import os
 import random
 import sys
@@ -183,7 +184,8 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
 
 def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: int, warmup: int, encoder=None,
                 dim: int = 768, dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096,
-                n_top: int = 64, cluster_iters: int = 2, init_edges: int = None, db_dir: str = None):
+                n_top: int = 64, cluster_iters: int = 2, init_edges: int = None, db_dir: str = None,
+                clustered: bool = False, topics_per_rank: int = 32):
     """BASELINE config 4 as ONE tenant: a ``nodes_per_rank * world``-node
     buffer row-sharded over the ranks (``ShardedMemorySystem``); every step
     each rank brings ``convs`` conversations, the whole batch is consolidated
@@ -191,7 +193,14 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     its rows, top-3 lists merged, global eviction, distributed CC, distributed
     k-means hierarchy), each rank commits its rows. Per-rank scan work is
     (world * convs * facts) x nodes_per_rank: the buffer is split N ways,
-    every fact is compared with every memory (the reference's semantics)."""
+    every fact is compared with every memory (the reference's semantics).
+
+    ``clustered``: each rank's rows are ``topics_per_rank`` tight topics of
+    its own (cos ~0.97 to the topic centre) and new nodes are placed on their
+    cluster's home rank (``placement="cluster"``); the exact cone pruning
+    then lets a rank skip the facts no cluster it holds can reach, and the
+    reported ``scan_facts_x_rows_per_rank_step`` is the measured count
+    (``ShardedMemorySystem.last_scan_work``, max over ranks)."""
     from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
     from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
 
@@ -201,7 +210,8 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     sm = ShardedMemorySystem(comm, "buffer", max_buffer_size=nodes_per_rank * world, llm_provider=LocalLLM(),
                              embedding_provider=encoder or HashEmbedder(dim=dim), db_dir=db_dir, device=dev,
                              hierarchy_params={"fine": n_fine, "top": n_top, "every": cluster_every * convs * world,
-                                               "iters": cluster_iters})
+                                               "iters": cluster_iters},
+                             placement="cluster" if clustered else "origin")
     g = sm.g
     g._set_dim(dim)
     g.reserve(int(nodes_per_rank * 1.05) + 65536)
@@ -210,9 +220,16 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     now = time.time()
     chunk = 1 << 20
     t0 = time.perf_counter()
+    if clustered:  # every rank draws the same centres; rank r's rows come from topics r*T .. r*T+T-1
+        cg = torch.Generator().manual_seed(seed)
+        centres = _unit(torch.randn((world * topics_per_rank, dim), generator=cg)).to(dev)
+        sigma = math.tan(math.radians(14.0)) / math.sqrt(dim)  # rows at cos ~0.97 to their topic centre
     for r0 in range(0, nodes_per_rank, chunk):  # collective per chunk: global node numbers, rank-major
         r1 = min(nodes_per_rank, r0 + chunk)
         v = torch.randn((r1 - r0, dim), device=dev, generator=gen)
+        if clustered:
+            t = comm.rank * topics_per_rank + torch.randint(0, topics_per_rank, (r1 - r0,), device=dev, generator=gen)
+            v = centres[t] + sigma * v
         v /= v.norm(dim=1, keepdim=True)
         sm.add_memories([f"memory {comm.rank}.{i}" for i in range(r0, r1)], v, salience=0.5, now=now,
                         shard_codes=codes[torch.arange(r0, r1, device=dev) % len(SHARDS)])
@@ -246,6 +263,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     comm.barrier()
     t0 = time.perf_counter()
     agg = {}
+    work0 = sm.scan_work
     for _ in range(steps):
         for k, v in step().items():
             agg[k] = agg.get(k, 0) + v
@@ -255,6 +273,9 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")
     comm.all_reduce(t, "max")
     el = float(t.item())
+    wk = torch.tensor([(sm.scan_work - work0) / max(steps, 1)], dtype=torch.float64,
+                      device=dev if comm.enabled and dev.type == "cuda" else "cpu")
+    comm.all_reduce(wk, "max")
     from lazzaro_amd.utils.tracing import tracer
     stages = {k: v["p50_ms"] for k, v in tracer.summary().items()} if tracer.enabled else None
     st = sm.get_stats()
@@ -262,7 +283,10 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
            "buffer_nodes_total": st["total_nodes"], "nodes_per_rank": nodes_per_rank, "edges_total": st["total_edges"],
            "convs_per_rank_step": convs, "facts_per_conv": facts,
            "per_step": {k: round(v / steps, 1) for k, v in agg.items()},
-           "scan_facts_x_rows_per_rank_step": int(world * convs * facts * nodes_per_rank),
+           # measured: facts x live rows this rank's scans compared (max over ranks)
+           "scan_facts_x_rows_per_rank_step": int(wk.item()),
+           "scan_facts_x_rows_unpruned_per_rank_step": int(world * convs * facts * nodes_per_rank),
+           "data": "clustered topics, cluster placement" if clustered else "uniform random rows",
            "path": "ShardedMemorySystem.consolidate_batch (one tenant row-sharded over the ranks)",
            "hierarchical_clustering": {"mode": "distributed kmeans", "every_steps": cluster_every, "fine": n_fine,
                                        "top": n_top, "iters_per_pass": cluster_iters,
@@ -298,6 +322,8 @@ if __name__ == "__main__":
     ap.add_argument("--init-edges", type=int, default=None, help="seeded edges (default 2 x nodes)")
     ap.add_argument("--sharded", action="store_true",
                     help="config 4 as one tenant row-sharded over the ranks (--nodes per rank)")
+    ap.add_argument("--clustered", action="store_true",
+                    help="--sharded: per-rank topic clusters + cluster placement (exact scan pruning applies)")
     a = ap.parse_args()
     comm = Communicator.init()
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -309,7 +335,8 @@ if __name__ == "__main__":
     fn = run_sharded if a.sharded else run
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
-             **({} if a.sharded else {"prune_threshold": a.prune_threshold, "persist_async": a.persist_async}))
+             **({"clustered": a.clustered} if a.sharded else {"prune_threshold": a.prune_threshold,
+                                                              "persist_async": a.persist_async}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)
     if comm.enabled:

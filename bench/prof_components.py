@@ -38,6 +38,10 @@ def main():
 
     out["digest_ms"], comps = t(lambda: g.component_digest())
     out["n_qualifying"] = len(comps)
+    g._digest_sorted = True
+    out["digest_sorted_ms"], comps2 = t(lambda: g.component_digest())
+    g._digest_sorted = False
+    out["digest_equal"] = [c.tolist() for c in comps] == [c.tolist() for c in comps2]
     src, dst = g.e["src"].long(), g.e["dst"].long()
     E = src.numel()
     out["unique_ms"], (verts, inv) = t(lambda: torch.unique(torch.cat([src, dst]), return_inverse=True))
@@ -45,8 +49,6 @@ def main():
     s32, d32 = inv[:E].to(torch.int32), inv[E:].to(torch.int32)
     out["cc_ms"], cl = t(lambda: T.components(s32, d32, nv))
     from lazzaro_amd.ops import graph_ops as G
-    out["cc_hook_ms"], lh = t(lambda: G.connected_components(s32, d32, nv, method="hook"))
-    out["uf_equals_hook"] = bool(torch.equal(lh, cl))
     out["cc_full_n_ms"], _ = t(lambda: T.components(g.e["src"], g.e["dst"], g.n))
     cl = cl.long()
     kind_v = g.kind[verts]
@@ -55,7 +57,6 @@ def main():
     out["segsum_w_ms"], _ = t(lambda: TGm._seg_sum_count(cl[inv[:E]], g.e["w"], nv))
     okey = verts.clone()
     first = torch.full((nv,), 1 << 62, dtype=torch.long, device=dev)
-    out["scatter_amin_ms"], _ = t(lambda: first.scatter_reduce_(0, cl, okey, "amin", include_self=True))
     key = torch.randint(0, 1 << 20, (nv,), device=dev)
     out["argsort_nv_ms"], _ = t(lambda: torch.argsort(key * g.n + verts))
     print(json.dumps(out), flush=True)

@@ -1,0 +1,407 @@
+// Component digest of run_consolidation without sorting the graph
+// (reference memory_system.py:967-990: components with >= 3 members and mean
+// edge weight > 0.3 feed the profile prompt with their first 10 contents).
+//
+// Input: union-find labels (graph.hip uf_union/cc_compress: label = smallest
+// row of the component) over a tenant graph's SoA columns. Output: for every
+// qualifying component, its first `take` live shard-node rows in row order,
+// tagged with the component's order key (smallest (super ? 0 : shard + 1) *
+// n + row over its live nodes -- the reference's BufferGraph.nodes order).
+//
+// The sort + segmented-scan formulation (engine/tenant_graph.py, CPU path)
+// sorts every touched row and every edge by label: ~11 ms at 10M rows / 20M
+// edges, almost all of it the sorts. Here every per-component quantity is a
+// keyed reduction with two levels of aggregation so that one giant component
+// (the usual shape: one component holding most rows) does not serialise
+// atomics on one address:
+//   wave   lanes with the leader's label reduce by DPP/shuffle, one push per
+//          distinct label (a few passes, then per-lane pushes)
+//   block  a 1024-slot LDS cache keyed by label absorbs the pushes (LDS
+//          atomics); one global atomic per cached label per block at the end
+// The first-`take` selection is exact and sort-free: components with <= take
+// candidates take all of them (one append pass); larger ones run `take`
+// rounds of "smallest eligible row above the last one selected", where only
+// the first lane of each label in a wave (the smallest row, lanes are in row
+// order) tests the running minimum and issues an atomicMin if it improves it.
+#include "lzk_common.h"
+
+LZK_DEBUG_STATE(digest)
+
+namespace {
+
+constexpr int DNT = 256;
+constexpr int HS = 1024;  // LDS cache slots per block
+constexpr int MATCH_PASSES = 4;
+constexpr long long BIGKEY = 1LL << 62;
+constexpr int NOROW = 0x7fffffff;
+
+__device__ __forceinline__ int slot_of(int L) { return (int)(((unsigned)L * 2654435761u) >> 22); }  // 10 bits
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ long long wave_min_ll(long long v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const long long u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+// Claim (or find) the LDS slot of label L; false when another label holds it.
+__device__ __forceinline__ bool lds_claim(int* keys, int s, int L) {
+  int k = __hip_atomic_load(keys + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (k == L) return true;
+  if (k != -1) return false;
+  k = atomicCAS(keys + s, -1, L);
+  return k == -1 || k == L;
+}
+
+__device__ __forceinline__ void lds_init(int* keys) {
+  for (int i = threadIdx.x; i < HS; i += DNT) keys[i] = -1;
+}
+
+// ---------------------------------------------------------------- edges
+// touched[src] = touched[dst] = 1; per label of src: sum of weights (fp64),
+// edge count.
+__device__ __forceinline__ void push_w(int L, double s, int c, int* keys, double* ssum, int* scnt, double* gsum,
+                                       int* gcnt) {
+  const int sl = slot_of(L);
+  if (lds_claim(keys, sl, L)) {
+    atomicAdd(ssum + sl, s);
+    atomicAdd(scnt + sl, c);
+  } else {
+    unsafeAtomicAdd(gsum + L, s);
+    atomicAdd(gcnt + L, c);
+  }
+}
+
+__global__ __launch_bounds__(DNT) void dg_edges_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                       const float* __restrict__ w, long ne,
+                                                       const int* __restrict__ lab,
+                                                       unsigned char* __restrict__ touched, double* __restrict__ gsum,
+                                                       int* __restrict__ gcnt) {
+  __shared__ int keys[HS];
+  __shared__ double ssum[HS];
+  __shared__ int scnt[HS];
+  lds_init(keys);
+  for (int i = threadIdx.x; i < HS; i += DNT) { ssum[i] = 0.0; scnt[i] = 0; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * DNT;
+  for (long base = (long)blockIdx.x * DNT; base < ne; base += stride) {  // block-uniform trip count
+    const long e = base + threadIdx.x;
+    bool act = e < ne;
+    int L = -1;
+    double v = 0.0;
+    if (act) {
+      const int a = src[e], b = dst[e];
+      touched[a] = 1;
+      touched[b] = 1;
+      L = lab[a];
+      v = (double)w[e];
+    }
+    for (int it = 0; it < MATCH_PASSES; ++it) {
+      const unsigned long long m = __ballot(act);
+      if (m == 0) break;
+      const int leader = __ffsll((long long)m) - 1;
+      const int LL = __shfl(L, leader, 64);
+      const bool mine = act && L == LL;
+      const double s = wave_sum_d(mine ? v : 0.0);
+      const int c = __popcll(__ballot(mine));
+      if (lane == leader) push_w(LL, s, c, keys, ssum, scnt, gsum, gcnt);
+      act = act && !mine;
+    }
+    if (act) push_w(L, v, 1, keys, ssum, scnt, gsum, gcnt);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HS; i += DNT) {
+    const int L = keys[i];
+    if (L >= 0) {
+      unsafeAtomicAdd(gsum + L, ssum[i]);
+      atomicAdd(gcnt + L, scnt[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- rows
+// Members = touched rows that are not free (live nodes and ghost endpoints,
+// like the reference DFS that follows edges to missing ids). Per label:
+// member count, candidate count (live shard nodes: kind 1, not super), and
+// the order key min over live nodes.
+__device__ __forceinline__ void push_r(int L, int sz, int cc, long long fk, int* keys, int* ssz, int* scc,
+                                       long long* sfk, int* gsize, int* gccnt, long long* gfirst) {
+  const int sl = slot_of(L);
+  if (lds_claim(keys, sl, L)) {
+    atomicAdd(ssz + sl, sz);
+    if (cc) atomicAdd(scc + sl, cc);
+    if (fk < BIGKEY) atomicMin(sfk + sl, fk);
+  } else {
+    atomicAdd(gsize + L, sz);
+    if (cc) atomicAdd(gccnt + L, cc);
+    if (fk < BIGKEY) atomicMin(gfirst + L, fk);
+  }
+}
+
+__global__ __launch_bounds__(DNT) void dg_rows_kernel(const int* __restrict__ lab,
+                                                      const unsigned char* __restrict__ touched,
+                                                      const unsigned char* __restrict__ kind,
+                                                      const unsigned char* __restrict__ sup,
+                                                      const int* __restrict__ shard, long n, int* __restrict__ gsize,
+                                                      int* __restrict__ gccnt, long long* __restrict__ gfirst) {
+  __shared__ int keys[HS];
+  __shared__ int ssz[HS];
+  __shared__ int scc[HS];
+  __shared__ long long sfk[HS];
+  lds_init(keys);
+  for (int i = threadIdx.x; i < HS; i += DNT) { ssz[i] = 0; scc[i] = 0; sfk[i] = BIGKEY; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * DNT;
+  for (long base = (long)blockIdx.x * DNT; base < n; base += stride) {
+    const long r = base + threadIdx.x;
+    bool act = false, cand = false;
+    int L = -1;
+    long long fk = BIGKEY;
+    if (r < n && touched[r]) {
+      const unsigned char k = kind[r];
+      if (k != 0) {
+        act = true;
+        L = lab[r];
+        if (k == 1) {
+          const bool s = sup[r] != 0;
+          cand = !s;
+          fk = (s ? 0LL : (long long)shard[r] + 1) * (long long)n + r;
+        }
+      }
+    }
+    for (int it = 0; it < MATCH_PASSES; ++it) {
+      const unsigned long long m = __ballot(act);
+      if (m == 0) break;
+      const int leader = __ffsll((long long)m) - 1;
+      const int LL = __shfl(L, leader, 64);
+      const bool mine = act && L == LL;
+      const int sz = __popcll(__ballot(mine));
+      const int cc = __popcll(__ballot(mine && cand));
+      const long long f = wave_min_ll(mine ? fk : BIGKEY);
+      if (lane == leader) push_r(LL, sz, cc, f, keys, ssz, scc, sfk, gsize, gccnt, gfirst);
+      act = act && !mine;
+    }
+    if (act) push_r(L, 1, cand ? 1 : 0, fk, keys, ssz, scc, sfk, gsize, gccnt, gfirst);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HS; i += DNT) {
+    const int L = keys[i];
+    if (L >= 0) {
+      atomicAdd(gsize + L, ssz[i]);
+      if (scc[i]) atomicAdd(gccnt + L, scc[i]);
+      if (sfk[i] < BIGKEY) atomicMin(gfirst + L, sfk[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- classify
+// cls[L]: 0 = not selected, 1 = qualifies with <= take candidates (all of
+// them are taken), 2 = qualifies with more (selection rounds). counters[0] +=
+// candidates of class-1 labels, counters[1] = number of class-2 labels (also
+// appended to biglist), counters[2] = qualifying components.
+__global__ __launch_bounds__(DNT) void dg_classify_kernel(long n, int min_size, double min_avg_w, int take,
+                                                          const int* __restrict__ gsize,
+                                                          const double* __restrict__ gsum,
+                                                          const int* __restrict__ gcnt,
+                                                          const long long* __restrict__ gfirst,
+                                                          const int* __restrict__ gccnt,
+                                                          unsigned char* __restrict__ cls, int* __restrict__ biglist,
+                                                          int* __restrict__ counters) {
+  __shared__ int red[2][DNT / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int direct = 0, nok = 0;
+  const long stride = (long)gridDim.x * DNT;
+  for (long base = (long)blockIdx.x * DNT; base < n; base += stride) {
+    const long L = base + threadIdx.x;
+    unsigned char c = 0;
+    if (L < n) {
+      const int sz = gsize[L], ec = gcnt[L], cc = gccnt[L];
+      if (sz >= min_size && ec > 0 && cc > 0 && gfirst[L] < BIGKEY && gsum[L] / (double)ec > min_avg_w) {
+        c = cc <= take ? 1 : 2;
+        ++nok;
+        if (c == 1) direct += cc;
+      }
+      cls[L] = c;
+    }
+    const unsigned long long big = __ballot(c == 2);
+    if (big) {
+      int b0 = 0;
+      if (lane == 0) b0 = atomicAdd(counters + 1, __popcll(big));
+      b0 = __shfl(b0, 0, 64);
+      if (c == 2) biglist[b0 + __popcll(big & ((1ULL << lane) - 1))] = (int)L;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    direct += __shfl_xor(direct, o, 64);
+    nok += __shfl_xor(nok, o, 64);
+  }
+  if (lane == 0) { red[0][wv] = direct; red[1][wv] = nok; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int d = 0, k = 0;
+    for (int i = 0; i < DNT / 64; ++i) { d += red[0][i]; k += red[1][i]; }
+    if (d) atomicAdd(counters, d);
+    if (k) atomicAdd(counters + 2, k);
+  }
+}
+
+__device__ __forceinline__ bool is_cand(long r, long n, const unsigned char* touched, const unsigned char* kind,
+                                        const unsigned char* sup) {
+  return r < n && touched[r] && kind[r] == 1 && sup[r] == 0;
+}
+
+// Candidates of class-1 components: appended as (order key, row).
+__global__ __launch_bounds__(DNT) void dg_direct_kernel(const int* __restrict__ lab,
+                                                        const unsigned char* __restrict__ touched,
+                                                        const unsigned char* __restrict__ kind,
+                                                        const unsigned char* __restrict__ sup, long n,
+                                                        const unsigned char* __restrict__ cls,
+                                                        const long long* __restrict__ gfirst,
+                                                        long long* __restrict__ out_key, int* __restrict__ out_row,
+                                                        int cap, int* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * DNT;
+  for (long base = (long)blockIdx.x * DNT; base < n; base += stride) {
+    const long r = base + threadIdx.x;
+    int L = -1;
+    bool sel = false;
+    if (is_cand(r, n, touched, kind, sup)) {
+      L = lab[r];
+      sel = cls[L] == 1;
+    }
+    const unsigned long long m = __ballot(sel);
+    if (m == 0) continue;
+    int b0 = 0;
+    if (lane == 0) b0 = atomicAdd(count, __popcll(m));
+    b0 = __shfl(b0, 0, 64);
+    const int at = b0 + __popcll(m & ((1ULL << lane) - 1));
+    if (sel && at < cap) {
+      out_key[at] = gfirst[L];
+      out_row[at] = (int)r;
+    }
+  }
+}
+
+// One selection round over the class-2 components: cur[L] = smallest
+// candidate row of L above prev[L] (prev == nullptr: round 0).
+__global__ __launch_bounds__(DNT) void dg_round_kernel(const int* __restrict__ lab,
+                                                       const unsigned char* __restrict__ touched,
+                                                       const unsigned char* __restrict__ kind,
+                                                       const unsigned char* __restrict__ sup, long n,
+                                                       const unsigned char* __restrict__ cls,
+                                                       const int* __restrict__ prev, int* __restrict__ cur) {
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * DNT;
+  for (long base = (long)blockIdx.x * DNT; base < n; base += stride) {
+    const long r = base + threadIdx.x;
+    int L = -1;
+    bool act = false;
+    if (is_cand(r, n, touched, kind, sup)) {
+      L = lab[r];
+      act = cls[L] == 2 && (prev == nullptr || (int)r > prev[L]);
+    }
+    while (true) {  // one pass per distinct eligible label in the wave
+      const unsigned long long m = __ballot(act);
+      if (m == 0) break;
+      const int leader = __ffsll((long long)m) - 1;
+      const int LL = __shfl(L, leader, 64);
+      if (lane == leader) {  // lanes are in row order: the leader holds LL's smallest eligible row
+        const int v = __hip_atomic_load(cur + LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)r < v) atomicMin(cur + LL, (int)r);
+      }
+      act = act && L != LL;
+    }
+  }
+}
+
+// After round k: append each class-2 component's selected row (if any) and
+// reset the other buffer (round k's prev, round k+1's cur) for those labels.
+__global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__ biglist, int nbig,
+                                                         const int* __restrict__ cur, int* __restrict__ reset,
+                                                         const long long* __restrict__ gfirst,
+                                                         long long* __restrict__ out_key, int* __restrict__ out_row,
+                                                         int cap, int* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * DNT + threadIdx.x;
+  int L = -1, v = NOROW;
+  if (i < nbig) {
+    L = biglist[i];
+    v = cur[L];
+    reset[L] = NOROW;
+  }
+  const bool sel = v != NOROW;
+  const unsigned long long m = __ballot(sel);
+  if (m == 0) return;
+  int b0 = 0;
+  if (lane == 0) b0 = atomicAdd(count, __popcll(m));
+  b0 = __shfl(b0, 0, 64);
+  const int at = b0 + __popcll(m & ((1ULL << lane) - 1));
+  if (sel && at < cap) {
+    out_key[at] = gfirst[L];
+    out_row[at] = v;
+  }
+}
+
+inline unsigned grid_for(long n, unsigned cap = 4096) {
+  const long b = (n + DNT - 1) / DNT;
+  return (unsigned)(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+}  // namespace
+
+// Stats phase: edge and row reductions + classification. Every output array
+// is indexed by label (length n) and must be zeroed by the caller, except
+// gfirst (filled with 1 << 62) and cls/biglist (written here); counters[3]
+// zeroed. The caller reads counters back (one synchronisation) to size the
+// selection output: counters[0] + take * counters[1] entries.
+LZK_EXPORT int lzk_dg_stats(const int* src, const int* dst, const float* w, long ne, const int* lab, long n,
+                            const unsigned char* kind, const unsigned char* sup, const int* shard, int min_size,
+                            double min_avg_w, int take, unsigned char* touched, double* gsum, int* gcnt, int* gsize,
+                            int* gccnt, long long* gfirst, unsigned char* cls, int* biglist, int* counters,
+                            void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (ne > 0)
+    hipLaunchKernelGGL(dg_edges_kernel, dim3(grid_for(ne, 2048)), dim3(DNT), 0, st, src, dst, w, ne, lab, touched,
+                       gsum, gcnt);
+  hipLaunchKernelGGL(dg_rows_kernel, dim3(grid_for(n, 2048)), dim3(DNT), 0, st, lab, touched, kind, sup, shard, n,
+                     gsize, gccnt, gfirst);
+  hipLaunchKernelGGL(dg_classify_kernel, dim3(grid_for(n, 1024)), dim3(DNT), 0, st, n, min_size, min_avg_w, take,
+                     gsize, gsum, gcnt, gfirst, gccnt, cls, biglist, counters);
+  return (int)hipGetLastError();
+}
+
+// Selection phase: (order key, row) of every selected row, unordered, in
+// out_key/out_row[0 : *count]; cap = counters[0] + take * counters[1].
+// buf0/buf1: int[n] filled with 0x7fffffff.
+LZK_EXPORT int lzk_dg_select(const int* lab, long n, const unsigned char* touched, const unsigned char* kind,
+                             const unsigned char* sup, const unsigned char* cls, const long long* gfirst,
+                             const int* biglist, int nbig, int take, int* buf0, int* buf1, long long* out_key,
+                             int* out_row, int cap, int* count, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(dg_direct_kernel, dim3(grid_for(n)), dim3(DNT), 0, st, lab, touched, kind, sup, n, cls, gfirst,
+                     out_key, out_row, cap, count);
+  int* bufs[2] = {buf0, buf1};
+  for (int k = 0; nbig > 0 && k < take; ++k) {
+    int* cur = bufs[k & 1];
+    int* prv = k ? bufs[(k - 1) & 1] : nullptr;
+    hipLaunchKernelGGL(dg_round_kernel, dim3(grid_for(n)), dim3(DNT), 0, st, lab, touched, kind, sup, n, cls, prv,
+                       cur);
+    // round 0 has no prev to reset: clear the buffer round 1 writes (already
+    // filled by the caller) -- harmless; later rounds reset round k's prev
+    hipLaunchKernelGGL(dg_collect_kernel, dim3((unsigned)((nbig + DNT - 1) / DNT)), dim3(DNT), 0, st, biglist, nbig,
+                       cur, bufs[(k + 1) & 1], gfirst, out_key, out_row, cap, count);
+  }
+  return (int)hipGetLastError();
+}

@@ -253,6 +253,9 @@ class TenantGraph:
 
     # rows of the mini-batch k-means refinement steps of cluster_pass
     CLUSTER_SAMPLE = 1 << 20
+    # component_digest on the GPU: digest.hip keyed reductions (False) or the
+    # sort + segmented-scan formulation the CPU runs (True; tests compare them)
+    _digest_sorted = False
     SAMPLE_TWO_LEVEL = os.environ.get("LZK_SAMPLE_ASSIGN", "two_level") != "full"
 
     # fp8 (e4m3) copy of the rows for the store search's candidate scan
@@ -1042,11 +1045,22 @@ class TenantGraph:
         ``take`` of its live shard-node rows (row order) -- the only rows the
         profile prompt reads (:1032). Components with none are left out.
         Labels, sizes, weight sums and the ordering are device reductions;
-        only the <= ``take`` rows per qualifying component reach the host."""
+        only the <= ``take`` rows per qualifying component reach the host.
+        On the GPU the reductions are the sort-free kernels of digest.hip
+        (ops.tenant_ops.component_digest); the sorted formulation below is
+        the CPU path."""
         n = self.n
         if n == 0 or self.num_edges == 0:
             return []
         dev = self.device
+        if dev.type == "cuda" and min_size >= 2 and take >= 1 and not self._digest_sorted:
+            with self.on_stream():
+                key, rows = T.component_digest(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n],
+                                               self.sup[:n], self.shard[:n], n, min_size, min_avg_w, take)
+                rows_h, key_h = rows.cpu().numpy(), key.cpu().numpy()
+            if rows_h.size == 0:
+                return []
+            return np.split(rows_h, np.nonzero(np.diff(key_h))[0] + 1)
         with self.on_stream():
             # Labels over the rows (one union-find pass over the edges); a row
             # no edge touches is a singleton (size 1 < min_size, no edge

@@ -30,6 +30,8 @@ _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
 _lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
+_lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, P, P, P, P, P, P, P])
+_lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, I, P, P, P, P, I, P, P])
 
 SALIENCE_FLOOR = 0.2
 EDGE_COLS = ("src", "dst", "w", "co", "lu", "meta")
@@ -284,6 +286,58 @@ def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: floa
                                               code.data_ptr(), row.data_ptr(), bad.data_ptr(), _st(sal)),
                "tg_evict_verify")
     return int(bad.item()) == 0
+
+
+def component_digest(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind: torch.Tensor, sup: torch.Tensor,
+                     shard: torch.Tensor, n: int, min_size: int, min_avg_w: float,
+                     take: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Device component digest (``csrc/kernels/digest.hip``): (order key,
+    row) of the first ``take`` live shard-node rows of every component with
+    >= ``min_size`` members and mean edge weight > ``min_avg_w``, sorted by
+    (key, row). Union-find labels, then keyed reductions and selection rounds
+    -- no sort over the graph (see the kernel file). One host synchronisation
+    sizes the output. GPU tensors only (TenantGraph.component_digest has the
+    sort-based CPU formulation); ``min_size`` >= 2, ``take`` >= 1."""
+    assert src.is_cuda and min_size >= 2 and take >= 1
+    dev = src.device
+    lab = components(src, dst, n)
+    ne = int(src.numel())
+    touched = torch.zeros(n, dtype=torch.uint8, device=dev)
+    gsum = torch.zeros(n, dtype=torch.float64, device=dev)
+    gi = torch.zeros((3, n), dtype=torch.int32, device=dev)  # edge count, member count, candidate count
+    gfirst = torch.full((n,), 1 << 62, dtype=torch.int64, device=dev)
+    cls = torch.empty(n, dtype=torch.uint8, device=dev)
+    biglist = torch.empty(n // (take + 1) + 1, dtype=torch.int32, device=dev)
+    counters = torch.zeros(4, dtype=torch.int32, device=dev)
+    src, dst = src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous()
+    w = w.to(torch.float32).contiguous()
+    L_ = _lib.lib()
+    _lib.check(L_.lzk_dg_stats(src.data_ptr(), dst.data_ptr(), w.data_ptr(), ne, lab.data_ptr(), n, kind.data_ptr(),
+                               sup.data_ptr(), shard.data_ptr(), int(min_size), float(min_avg_w), int(take),
+                               touched.data_ptr(), gsum.data_ptr(), gi[0].data_ptr(), gi[1].data_ptr(),
+                               gi[2].data_ptr(), gfirst.data_ptr(), cls.data_ptr(), biglist.data_ptr(),
+                               counters.data_ptr(), _st(src)), "dg_stats")
+    direct, nbig = (int(v) for v in counters[:2].cpu().tolist())
+    cap = direct + take * nbig
+    keys = torch.empty(cap, dtype=torch.int64, device=dev)
+    rows = torch.empty(cap, dtype=torch.int32, device=dev)
+    if cap == 0:
+        return keys, rows.long()
+    bufs = torch.full((2, n), 0x7FFFFFFF, dtype=torch.int32, device=dev) if nbig else torch.empty((2, 1), dtype=torch.int32, device=dev)
+    _lib.check(L_.lzk_dg_select(lab.data_ptr(), n, touched.data_ptr(), kind.data_ptr(), sup.data_ptr(),
+                                cls.data_ptr(), gfirst.data_ptr(), biglist.data_ptr(), nbig, int(take),
+                                bufs[0].data_ptr(), bufs[1].data_ptr(), keys.data_ptr(), rows.data_ptr(), cap,
+                                counters[3:].data_ptr(), _st(src)), "dg_select")
+    m = int(counters[3].item())
+    if m > cap:
+        raise RuntimeError(f"component digest overflow: {m} selected rows for capacity {cap}")
+    keys, rows = keys[:m], rows[:m].long()
+    if m and int(keys.max()) < (1 << 62) // max(n, 1):
+        o = torch.argsort(keys * n + rows)
+    else:  # (key, row) by two stable sorts
+        o = torch.argsort(rows, stable=True)
+        o = o[torch.argsort(keys[o], stable=True)]
+    return keys[o], rows[o]
 
 
 def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:

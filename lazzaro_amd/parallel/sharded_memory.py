@@ -90,12 +90,22 @@ class ShardedMemorySystem:
     ``db_dir``, ``store``, ``device``...). ``max_buffer_size`` is the GLOBAL
     node limit. ``hierarchy_params`` ({"fine", "top", "every", "iters"})
     turns on the distributed k-means hierarchy, re-clustered whenever the
-    global conversation count crosses a multiple of ``every``."""
+    global conversation count crosses a multiple of ``every``.
+
+    ``prune`` (with a hierarchy): exact cross-rank pruning of the
+    consolidation scan -- a fact is compared with this rank's rows only if a
+    fine cluster held here can contain a row at cos > LINK_THRESHOLD (angular
+    radius bound, :meth:`_reach_mask`). ``placement="cluster"``: a new node
+    is held by the home rank of its fine cluster (the rank holding most of
+    that cluster's rows) instead of the rank whose conversation made it, so
+    topics stay together and the pruned scan stays ~(own facts) x (own
+    rows) as ranks are added. Neither changes a decision."""
 
     def __init__(self, comm: Optional[Communicator] = None, user_id: str = "default", *,
                  max_buffer_size: int = 10, consolidate_every: int = 3, auto_consolidate: bool = True,
                  auto_prune: bool = True, prune_threshold: float = 0.5,
-                 hierarchy_params: Optional[Dict] = None, **local_kwargs):
+                 hierarchy_params: Optional[Dict] = None, prune: bool = True, placement: str = "origin",
+                 **local_kwargs):
         from ..core.memory_system import MemorySystem
 
         self.comm = comm or Communicator.local()
@@ -119,6 +129,13 @@ class ShardedMemorySystem:
         self.holder = torch.full((0,), -1, dtype=torch.long, device=self.device)
         self.next_id = 0  # last global node number handed out (identical on every rank)
         self.conversation_count = 0
+        if placement not in ("origin", "cluster"):
+            raise ValueError(f"placement must be 'origin' or 'cluster', not {placement!r}")
+        self.prune = bool(prune)
+        self.placement = placement
+        self._reach: Optional[Dict] = None  # per fine cluster: centroid, angular radius over this rank's rows
+        self.scan_work = 0  # facts x rows this rank's consolidation scans compared (cumulative)
+        self.last_scan_work = 0
 
     # ------------------------------------------------------------------ plumbing
     @property
@@ -214,7 +231,141 @@ class ShardedMemorySystem:
         self.num[rows] = nums
         self.holder[rows] = self.rank
         self.local.node_counter = self.next_id
+        self._reach_add(rows)
         return rows
+
+    # ------------------------------------------------------------------ scan pruning
+    REACH_SLACK = 1e-5  # on the radius cosines: covers fp32 rounding of the row / centroid dots
+    REACH_CHUNK = 1 << 18
+    FAR_MAX = 1 << 15  # rows bounded exactly instead of by their cluster's cone
+
+    def _row_cos(self, rows: torch.Tensor, C: torch.Tensor, lab: Optional[torch.Tensor] = None):
+        """(label, cos) of rows against unit centroids C [K, D] (fp32): the
+        given labels, or the nearest centroid. Rows without a vector -> cos -1
+        (the cluster's radius becomes 180 degrees: never pruned)."""
+        g = self.g
+        labs, coss = [], []
+        for a in range(0, rows.numel(), self.REACH_CHUNK):
+            r = rows[a: a + self.REACH_CHUNK]
+            X = g.emb32[r].float()
+            nrm = g.sqn[r].float().sqrt()
+            S = (X @ C.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[:, None]
+            if lab is None:
+                cs, lb = S.max(1)
+            else:
+                lb = lab[a: a + self.REACH_CHUNK]
+                cs = S.gather(1, lb[:, None]).squeeze(1)
+            cs = torch.where(nrm > 0, cs, torch.full_like(cs, -1.0))
+            labs.append(lb)
+            coss.append(cs.double() - self.REACH_SLACK)
+        if not labs:
+            return rows.new_zeros(0), torch.zeros(0, dtype=torch.float64, device=rows.device)
+        return torch.cat(labs), torch.cat(coss)
+
+    def _build_reach(self, collective: bool = True) -> None:
+        """Per fine cluster of the hierarchy: unit centroid and the cosine of
+        the largest angle between it and a CORE row of this rank (2.0: none).
+        The rows farthest from their centroid (at most FAR_MAX / 2 over all
+        clusters) are kept out of the radii and bounded exactly instead (the
+        "far" rows: each fact's cosine with them is computed), so a few
+        outliers do not open a cluster's cone. Rebuilt after every cluster
+        pass (and locally when the far set overflows); inserts that fall
+        outside their cluster's cone join the far set; deletions leave both
+        (still upper bounds)."""
+        g = self.g
+        h = getattr(g, "hier", None)
+        if h is None or h.get("fine_c") is None or g.dim is None:
+            self._reach = None
+            return
+        dev = self.device
+        D = g.dim
+        C = h["fine_c"][:, :D].float().to(dev)
+        C = C / C.norm(dim=1, keepdim=True).clamp_min(1e-30)
+        K = C.shape[0]
+        n = g.n
+        with g.on_stream():
+            lab = h["fine"][:n].long().to(dev) if h["fine"].numel() >= n else None
+            live = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
+            rows = torch.nonzero(live).flatten()
+            cosr = torch.full((K,), 2.0, dtype=torch.float64, device=dev)
+            far = rows[:0]
+            lr = rows[:0]
+            if rows.numel():
+                lr = lab[rows] if lab is not None else None
+                if lr is not None and bool((lr < 0).any()):
+                    lr = None  # rows the pass did not label: nearest centroid for all
+                lr, cs = self._row_cos(rows, C, lr)
+                nf = min(self.FAR_MAX // 2, rows.numel())
+                core = torch.ones_like(cs, dtype=torch.bool)
+                if nf:
+                    fi = torch.topk(cs, nf, largest=False).indices
+                    core[fi] = False
+                    far = rows[fi]
+                cosr.scatter_reduce_(0, lr[core], cs[core], "amin", include_self=True)
+        home = self._reach.get("home") if (self._reach is not None and not collective) else None
+        self._reach = {"C": C, "Cd": C.double(), "cosr": cosr, "far": far, "far_x": None}
+        if home is not None:
+            self._reach["home"] = home
+        if self.placement == "cluster" and collective:
+            cnt = torch.zeros(K, dtype=torch.int64, device=dev)
+            if lr.numel():
+                cnt.index_add_(0, lr, torch.ones_like(lr))
+            allc = self._gather_rows(cnt[None, :])  # [W, K]
+            best = torch.argmax(allc, 0)  # first max: the lowest rank on ties
+            self._reach["home"] = torch.where(allc.max(0).values > 0, best, torch.arange(K, device=dev) % self.world)
+
+    def _reach_add(self, rows: torch.Tensor) -> None:
+        """New live rows of this rank: inside their nearest cluster's cone
+        they change nothing; outside they join the far set."""
+        r = self._reach
+        if r is None or rows.numel() == 0:
+            return
+        with self.g.on_stream():
+            rows = rows.to(self.device).long()
+            lr, cs = self._row_cos(rows, r["C"])
+            out = cs < r["cosr"][lr]
+            if bool(out.any()):
+                r["far"] = torch.cat([r["far"], rows[out]])
+                r["far_x"] = None
+        if r["far"].numel() > self.FAR_MAX:
+            self._build_reach(collective=False)
+
+    def _reach_mask(self, Qn: torch.Tensor) -> Optional[torch.Tensor]:
+        """Facts (unit float64 rows) that may have a row of this rank at cos >
+        LINK_THRESHOLD. Core rows: angle(q, x) >= angle(q, c) - radius(c) for
+        every core row x of cluster c, so cos(q, x) <= cos(max(0, angle(q, c)
+        - radius(c))). Far rows: the cosine itself (fp32, with slack)."""
+        r = self._reach
+        if r is None or not self.prune:
+            return None
+        g = self.g
+        sel = torch.zeros(Qn.shape[0], dtype=torch.bool, device=Qn.device)
+        cosr = r["cosr"]
+        held = cosr <= 1.0
+        if bool(held.any()):
+            cr = cosr[held].clamp(-1.0, 1.0)
+            sr = torch.sqrt((1.0 - cr * cr).clamp_min(0.0))
+            ct = (Qn @ r["Cd"][held].T).clamp(-1.0, 1.0)
+            st = torch.sqrt((1.0 - ct * ct).clamp_min(0.0))
+            bound = torch.where(ct >= cr[None, :], torch.ones_like(ct), ct * cr[None, :] + st * sr[None, :])
+            sel |= bound.max(1).values > LINK_THRESHOLD - 1e-6
+        far = r["far"]
+        if far.numel():
+            if r["far_x"] is None:
+                X = g.emb32[far].float()
+                nrm = g.sqn[far].float().sqrt()
+                r["far_x"] = X / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[:, None]
+            sel |= (Qn.float() @ r["far_x"].T).max(1).values > LINK_THRESHOLD - self.REACH_SLACK * 10
+        return sel
+
+    def _holders(self, Qn: torch.Tensor, origin: torch.Tensor) -> torch.Tensor:
+        """Rank that will hold each fact's node: its conversation's rank, or
+        (placement="cluster") the home rank of its nearest fine cluster --
+        computed identically on every rank (float64, same inputs)."""
+        r = self._reach
+        if self.placement != "cluster" or r is None or "home" not in r:
+            return origin
+        return r["home"][torch.argmax(Qn @ r["Cd"].T, 1)]
 
     # ------------------------------------------------------------------ queries
     def num_nodes(self) -> int:
@@ -232,11 +383,30 @@ class ShardedMemorySystem:
         F = Q.shape[0]
         dev = self.device
         k = LINK_TOPK
-        if g.n and g.num_nodes():
+        live = g.num_nodes() if g.n else 0
+        sel = None
+        if live:
+            Qd = Q.double()
+            qn = Qd.norm(dim=1, keepdim=True)
+            sel = self._reach_mask(Qd / torch.where(qn > 0, qn, torch.ones_like(qn)))
+        n_scan = F if sel is None else int(sel.sum())
+        self.last_scan_work = n_scan * live
+        self.scan_work += self.last_scan_work
+        if live and n_scan:
             n = g.n
             mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
             # decisions read only entries above LINK_THRESHOLD (as in _scan_batch)
-            (gs, gr), (ws, wr) = g.cos_topk(Q, k, mask, dual_label=codes, min_score=LINK_THRESHOLD)
+            if sel is None or n_scan == F:
+                (gs, gr), (ws, wr) = g.cos_topk(Q, k, mask, dual_label=codes, min_score=LINK_THRESHOLD)
+            else:  # only the facts a cluster held here can reach; the rest get empty lists
+                si = torch.nonzero(sel).flatten()
+                (gs_, gr_), (ws_, wr_) = g.cos_topk(Q[si], k, mask, dual_label=codes[si],
+                                                    min_score=LINK_THRESHOLD)
+                gs = torch.full((F, k), NEG_INF, dtype=torch.float64, device=dev)
+                ws = gs.clone()
+                gr = torch.full((F, k), -1, dtype=torch.long, device=dev)
+                wr = gr.clone()
+                gs[si], gr[si], ws[si], wr[si] = gs_.to(dev), gr_.to(dev), ws_.to(dev), wr_.to(dev)
         else:
             gs = ws = torch.full((F, k), NEG_INF, dtype=torch.float64, device=dev)
             gr = wr = torch.full((F, k), -1, dtype=torch.long, device=dev)
@@ -421,15 +591,22 @@ class ShardedMemorySystem:
         if F == 0:
             stats["pruned"] += self._sum(g.decay(1.0 - keep, thr, steps=B))[0]
             return
-        f_off = int(sum(fcnt[: self.rank]))
         origin = torch.repeat_interleave(torch.arange(self.world, device=dev),
                                          torch.tensor(fcnt, dtype=torch.long, device=dev))
+        origin_conv = origin
         codes = self._register_shards(keys_all)
         code_t = torch.as_tensor(codes).to(dev)
         Q = Qa.float()
         Qd = Q.double()
         qn = Qd.norm(dim=1, keepdim=True)
         Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        origin = self._holders(Qn, origin_conv)  # the rank that will hold each fact's node
+        if origin is not origin_conv:  # the holders need the contents of facts from other ranks
+            flat = [f for part in comm.all_gather_object([{"content": f["content"], "type": f.get("type", "semantic")}
+                                                          for f in flat]) for f in part]
+            f_off = 0
+        else:
+            f_off = int(sum(fcnt[: self.rank]))
 
         # ---- 2. every fact against every rank's rows: local dual scan + merge
         with tracer.stage("sc_scan", dev), g.on_stream():
@@ -491,6 +668,7 @@ class ShardedMemorySystem:
             self.num[rows] = new_num[mk]
             self.holder[rows] = self.rank
             row_of_fact[mk] = rows.to(dev)
+            self._reach_add(rows)
         if self.local.query_cache:
             self.local.query_cache.invalidate_results()
 
@@ -721,6 +899,7 @@ class ShardedMemorySystem:
             self._sync_num()
             self.num[rows] = nums
             self.holder[rows] = self.rank
+            self._reach_add(rows)
         if r_edge.shape[0]:
             src = self._rows_of_nums(r_edge[:, 0].long())
             dn = r_edge[:, 1].long()
@@ -940,7 +1119,9 @@ class ShardedMemorySystem:
 
     def cluster_pass(self) -> Dict:
         hp = self.hierarchy_params or {"fine": 4096, "top": 64, "iters": 2}
-        return self.g.cluster_pass(hp["fine"], hp["top"], hp["iters"], comm=self.comm if self.world > 1 else None)
+        out = self.g.cluster_pass(hp["fine"], hp["top"], hp["iters"], comm=self.comm if self.world > 1 else None)
+        self._build_reach()
+        return out
 
     @property
     def profile(self):

@@ -137,12 +137,17 @@ def _sharded(comm, cfg=CPU):
     X, sal0, keys0, steps = _data(cfg)
     dev = cfg["device"]
     tmp = tempfile.mkdtemp(prefix=f"lzsh{comm.rank}_")
+    pruned = cfg.get("pruned", False)
+    extra = dict(hierarchy_params={"fine": 12, "top": 4, "every": 10 ** 6, "iters": 3}, placement="cluster",
+                 prune=True) if pruned else {}
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
-                             embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev)
+                             embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev, **extra)
     rebal = cfg.get("rebalance", False)
     lo, hi = _split(cfg["rows"], comm.world, comm.rank, [5, 1, 2] if rebal else None)
     sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],
                     salience=torch.tensor(sal0[lo:hi]), now=_now(-1))
+    if pruned:  # pruned scan + cluster placement: the same decisions as the single process
+        sm.cluster_pass()
     spread = []
     stats = []
     for s, (convs, V) in enumerate(steps):
@@ -197,6 +202,11 @@ def check_equivalent(out, world, limit):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_tenant_matches_single_process(world):
     check_equivalent(spawn(world, _sharded), world, LIMIT)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tenant_pruned_cluster_placement_matches_single_process(world):
+    check_equivalent(spawn(world, functools.partial(_sharded, cfg=dict(CPU, pruned=True))), world, LIMIT)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -1,0 +1,56 @@
+"""digest.hip (sort-free component digest) against the sort + segmented-scan
+formulation on the same device graph: a giant component, thousands of small
+ones with more and fewer than ``take`` candidates, ghosts, super-nodes, four
+shards and mean weights on both sides of the threshold."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(n, ne_giant, n_small, seed):
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    rng = np.random.default_rng(seed)
+    g = TenantGraph(device="cuda", dim=8)
+    codes = [g.shard_id(f"s{i}") for i in range(4)]
+    g.add_nodes([f"node_{i}" for i in range(n)], [f"c{i}" for i in range(n)],
+                rng.standard_normal((n, 8)).astype(np.float32).tolist(),
+                shard=[codes[int(c)] for c in rng.integers(0, 4, n)],
+                sup=(rng.random(n) < 0.02).astype(np.int64).tolist())
+    # giant: random edges over the first half; small: chains of 2..30 rows in the rest
+    half = n // 2
+    src = [rng.integers(0, half, ne_giant)]
+    dst = [rng.integers(0, half, ne_giant)]
+    w = [rng.uniform(0.1, 1.0, ne_giant)]
+    perm = rng.permutation(np.arange(half, n))
+    at = 0
+    for _ in range(n_small):
+        k = int(rng.integers(2, 30))
+        if at + k > perm.size:
+            break
+        m = perm[at:at + k]
+        at += k
+        src.append(m[:-1])
+        dst.append(m[1:])
+        w.append(np.full(k - 1, rng.choice([0.2, 0.29, 0.31, 0.6]), dtype=np.float64))
+    s = torch.as_tensor(np.concatenate(src), dtype=torch.int32)
+    d = torch.as_tensor(np.concatenate(dst), dtype=torch.int32)
+    ww = torch.as_tensor(np.concatenate(w), dtype=torch.float32)
+    meta = torch.as_tensor(np.full(s.numel(), codes[0]), dtype=torch.int32)
+    g.append_edges(s.cuda(), d.cuda(), ww.cuda(), meta.cuda())
+    g.remove_nodes(rng.choice(n, n // 50, replace=False).tolist())  # ghosts
+    return g
+
+
+@pytest.mark.parametrize("n,ne,n_small,seed", [(20000, 30000, 500, 1), (300000, 500000, 6000, 2),
+                                                (50000, 0, 3000, 3)])
+def test_digest_kernels_match_sorted(n, ne, n_small, seed):
+    g = _graph(n, ne, n_small, seed)
+    for take in (10, 3):
+        got = [r.tolist() for r in g.component_digest(3, 0.3, take)]
+        g._digest_sorted = True
+        want = [r.tolist() for r in g.component_digest(3, 0.3, take)]
+        g._digest_sorted = False
+        assert got == want and len(want) > 10
+    torch.cuda.synchronize()

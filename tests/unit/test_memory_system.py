@@ -285,16 +285,18 @@ def test_search_memories_stream_matches_batch(tmp_path):
     ms.close()
 
 
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("ne,seed", [(300, 3), (1500, 4), (120, 5)])
-def test_component_digest_matches_materialised_components(ne, seed):
+def test_component_digest_matches_materialised_components(ne, seed, device):
     """run_consolidation's device digest == the per-component reference logic
     (size >= 3, mean edge weight > 0.3, first 10 live shard-node rows), for
-    many small components, one giant component and a sparse graph."""
+    many small components, one giant component and a sparse graph (GPU: the
+    digest.hip keyed-reduction kernels)."""
     import torch
 
     from lazzaro_amd.engine.tenant_graph import NODE, TenantGraph
     rng = np.random.default_rng(seed)
-    g = TenantGraph(device="cpu", dim=8)
+    g = TenantGraph(device=device, dim=8)
     n = 400
     codes = [g.shard_id(f"s{i}") for i in range(4)]
     g.add_nodes([f"node_{i}" for i in range(n)], [f"c{i}" for i in range(n)],
