@@ -993,7 +993,8 @@ class ConsolidationMixin:
         g = self.graph
         dev = g.device
         steps = int(seg["c1"]) - int(seg["c0"]) + 1
-        pruned = g.decay(DECAY_RATE, thr, steps=steps)
+        with tracer.stage("ap_decay", dev):
+            pruned = g.decay(DECAY_RATE, thr, steps=steps)
         tr = np.asarray(seg["tch_rows"], np.int64)
         if tr.size:
             with g.on_stream():
@@ -1010,52 +1011,57 @@ class ConsolidationMixin:
         iacc = np.asarray(seg["ins_acc"], np.int32)
         ilast = np.asarray(seg["ins_last"], np.float64)
         i = 0
-        while i < len(kinds):
-            if kinds[i] == 0:
-                k = i
-                while k < len(kinds) and kinds[k] == 0:
-                    k += 1
-                js = idx[i:k]
-                keys = fact_key[js].tolist()
-                rows = g.add_nodes([id_of[key] for key in keys], [facts[j]["content"] for j in js],
-                                   E[torch.as_tensor(js, dtype=torch.long).to(E.device)],
-                                   shard=codes[js].astype(np.int32),
-                                   types=[facts[j].get("type", "semantic") for j in js],
-                                   sal=torch.from_numpy(isal[i:k]), acc=torch.from_numpy(iacc[i:k]),
-                                   last=torch.from_numpy(ilast[i:k]), now=now, stored=stored)
-                if rows.tolist() != keys:
-                    raise RuntimeError("batch plan row assignment diverged from the graph")
-                i = k
-            else:
-                sp = supers[idx[i]]
-                children = np.asarray(sp["children"], np.int64).tolist()
-                skey = shard_keys_of(g, int(sp["code"]))
-                ch_ids = [id_of[r] if r in fact_of else g.ids[r] for r in children]
-                content = [facts[fact_of[r]]["content"] if r in fact_of else g.content[r] for r in children[:3]]
-                summary = f"Topic: {skey}. Contains memories about: " + "; ".join(content)
-                emb = self._plan_super_emb[tuple(children)]
-                srow = g.add_nodes([f"super_{skey}_{int(now)}"], [summary], emb[None, :], shard=[int(sp["code"])],
-                                   sup=[1], children={0: ch_ids}, stored=False, sal=float(isal[i]),
-                                   acc=int(iacc[i]), last=float(ilast[i]), now=now)
-                if int(srow[0]) != int(sp["key"]):
-                    raise RuntimeError("batch plan super-node row diverged from the graph")
-                with g.on_stream():
-                    rt = torch.as_tensor(children, dtype=torch.long).to(dev)
-                    g.parent[rt] = srow.to(torch.int32)[0]
-                    g.dirty[rt] = 1
-                g._bump()
-                i += 1
+        with tracer.stage("ap_insert", dev):
+            while i < len(kinds):
+                if kinds[i] == 0:
+                    k = i
+                    while k < len(kinds) and kinds[k] == 0:
+                        k += 1
+                    js = idx[i:k]
+                    keys = fact_key[js].tolist()
+                    rows = g.add_nodes([id_of[key] for key in keys], [facts[j]["content"] for j in js],
+                                       E[torch.as_tensor(js, dtype=torch.long).to(E.device)],
+                                       shard=codes[js].astype(np.int32),
+                                       types=[facts[j].get("type", "semantic") for j in js],
+                                       sal=torch.from_numpy(isal[i:k]), acc=torch.from_numpy(iacc[i:k]),
+                                       last=torch.from_numpy(ilast[i:k]), now=now, stored=stored)
+                    if rows.tolist() != keys:
+                        raise RuntimeError("batch plan row assignment diverged from the graph")
+                    i = k
+                else:
+                    sp = supers[idx[i]]
+                    children = np.asarray(sp["children"], np.int64).tolist()
+                    skey = shard_keys_of(g, int(sp["code"]))
+                    ch_ids = [id_of[r] if r in fact_of else g.ids[r] for r in children]
+                    content = [facts[fact_of[r]]["content"] if r in fact_of else g.content[r] for r in children[:3]]
+                    summary = f"Topic: {skey}. Contains memories about: " + "; ".join(content)
+                    emb = self._plan_super_emb[tuple(children)]
+                    srow = g.add_nodes([f"super_{skey}_{int(now)}"], [summary], emb[None, :], shard=[int(sp["code"])],
+                                       sup=[1], children={0: ch_ids}, stored=False, sal=float(isal[i]),
+                                       acc=int(iacc[i]), last=float(ilast[i]), now=now)
+                    if int(srow[0]) != int(sp["key"]):
+                        raise RuntimeError("batch plan super-node row diverged from the graph")
+                    with g.on_stream():
+                        rt = torch.as_tensor(children, dtype=torch.long).to(dev)
+                        g.parent[rt] = srow.to(torch.int32)[0]
+                        g.dirty[rt] = 1
+                    g._bump()
+                    i += 1
         es = np.asarray(seg["edge_src"], np.int64)
         if es.size:
-            g.append_edges(torch.as_tensor(es).to(dev), torch.as_tensor(np.asarray(seg["edge_dst"], np.int64)).to(dev),
-                           torch.as_tensor(np.asarray(seg["edge_w"], np.float32)).to(dev),
-                           torch.as_tensor(np.asarray(seg["edge_code"], np.int32)).to(dev),
-                           g.etype("relates_to"), now=now)
+            with tracer.stage("ap_edges", dev):
+                g.append_edges(torch.as_tensor(es).to(dev),
+                               torch.as_tensor(np.asarray(seg["edge_dst"], np.int64)).to(dev),
+                               torch.as_tensor(np.asarray(seg["edge_w"], np.float32)).to(dev),
+                               torch.as_tensor(np.asarray(seg["edge_code"], np.int32)).to(dev),
+                               g.etype("relates_to"), now=now)
         vic = np.asarray(seg["victims"], np.int64).tolist()
         if vic:
             ids = [g.ids[r] for r in vic]
-            g.remove_nodes(vic, drop_edges=True, unstore=True)
-            self._store_delete(ids)
+            with tracer.stage("ap_remove", dev):
+                g.remove_nodes(vic, drop_edges=True, unstore=True)
+            with tracer.stage("ap_store_delete", "cpu"):
+                self._store_delete(ids)
         return pruned
 
     def _consolidate_batch_coarse(self, facts: List[Dict], conv: np.ndarray, B: int, embs, now: float,
@@ -1212,7 +1218,8 @@ class ConsolidationMixin:
         g = self.graph
         with self._graph_lock:
             if merge_similar:
-                merged = self._merge_similar_nodes(similarity_threshold=DEDUPE_THRESHOLD)
+                with tracer.stage("rc_merge", self._device):
+                    merged = self._merge_similar_nodes(similarity_threshold=DEDUPE_THRESHOLD)
                 if merged > 0:
                     results.append(f"✓ Merged {merged} similar nodes")
             with tracer.stage("components", self._device):
@@ -1221,19 +1228,20 @@ class ConsolidationMixin:
                 digest = g.component_digest(3, 0.3, PROFILE_CONTENTS)
             contents = [[g.content[r] for r in rows.tolist()] for rows in digest]
         updates = 0
-        for cs in contents:
-            r = self._extract_profile_from_contents(cs)
-            if "Updated" in r:
-                updates += 1
-                results.append(r)
-        with self._graph_lock:
+        with tracer.stage("rc_profile", "cpu"):
+            for cs in contents:
+                r = self._extract_profile_from_contents(cs)
+                if "Updated" in r:
+                    updates += 1
+                    results.append(r)
+        with self._graph_lock, tracer.stage("rc_prune", self._device):
             pruned = g.prune(self.prune_threshold)
         if pruned > 0:
             results.append(f"✓ Pruned {pruned} weak edges")
         if updates > 0:
             results.append(f"✓ Updated {updates} profile domains")
         else:
-            with self._graph_lock:
+            with self._graph_lock, tracer.stage("rc_first_rows", self._device):
                 rows = g.first_node_rows_dev(PROFILE_CONTENTS, super_=False)
                 contents = [g.content[r] for r in rows.tolist()]
             if len(contents) >= 3:

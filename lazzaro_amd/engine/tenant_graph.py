@@ -698,6 +698,30 @@ class TenantGraph:
     def num_edges(self) -> int:
         return int(self.e["src"].numel())
 
+    EDGE_SORT_MIN = 1 << 20  # edge lists shorter than this are never re-ordered
+
+    def _maybe_sort_edges(self) -> bool:
+        """Keep the edge list (nearly) ordered by source row: the union-find
+        pass of the component digest hooks / finds ``src`` endpoints in edge
+        order, and on a 10M-row / 20M-edge graph a src-ordered list runs in
+        1.6 ms against 7.5 ms for a random order (bench/probe_cc.py). Links
+        are appended in insertion order (new rows = new sources), so the list
+        stays nearly sorted by itself; when more than 1/32 of adjacent pairs
+        are out of order (seeded or migrated edges) every edge column is
+        permuted by one stable sort. Edge order carries no meaning (every
+        consumer is order-free or re-derives its index lists)."""
+        ne = self.num_edges
+        if ne < self.EDGE_SORT_MIN:
+            return False
+        with self.on_stream():
+            src = self.e["src"]
+            if int((src[1:] < src[:-1]).sum()) * 32 <= ne:
+                return False
+            o = torch.sort(src, stable=True).indices
+            self.e = {k: v[o] for k, v in self.e.items()}
+        self.edge_version += 1
+        return True
+
     def append_edges(self, src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, shard: torch.Tensor,
                      etype: int = 0, co=None, lu=None, now: Optional[float] = None) -> None:
         """Append edges known not to exist yet (every edge a consolidation
@@ -1054,6 +1078,7 @@ class TenantGraph:
             return []
         dev = self.device
         if dev.type == "cuda" and min_size >= 2 and take >= 1 and not self._digest_sorted:
+            self._maybe_sort_edges()
             with self.on_stream():
                 key, rows = T.component_digest(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n],
                                                self.sup[:n], self.shard[:n], n, min_size, min_avg_w, take)

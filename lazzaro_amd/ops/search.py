@@ -519,6 +519,13 @@ def segment_topk_ptrs(xptr: torch.Tensor, nrows: torch.Tensor, ld: int, Q: torch
         raise ValueError("segment_topk supports k <= 16")
     nq, D = Q.shape
     dev = Q.device
+    # the kernel dereferences these tables: a host tensor's address would fault the GPU
+    for name, t in (("xptr", xptr), ("nrows", nrows), ("bptr", bptr), ("sptr", sptr), ("qbias", qbias)):
+        if t is not None and (t.device != dev or not t.is_contiguous() or t.shape[0] != nq):
+            raise ValueError(f"segment_topk_ptrs: {name} must be a contiguous [{nq}] tensor on {dev}, "
+                             f"got {tuple(t.shape)} on {t.device}")
+    if xptr.dtype != torch.int64 or nrows.dtype != torch.int32:
+        raise ValueError("segment_topk_ptrs: xptr int64, nrows int32")
     dt = {torch.bfloat16: 0, torch.float32: 1}[Q.dtype]
     qb = qbias.float().contiguous() if qbias is not None else None
     os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)

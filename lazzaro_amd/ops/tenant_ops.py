@@ -372,6 +372,9 @@ def gather_fields(rows: torch.Tensor, graphs: Optional[Sequence], device_out: bo
         base = torch.tensor([[getattr(g, c).data_ptr() for g in graphs] for c in ("sal", "acc", "kind", "sup",
                                                                                   "shard")],
                             dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+    if base.device != dev or base.dtype != torch.int64 or tuple(base.shape) != (5, nq) or not base.is_contiguous():
+        raise ValueError(f"gather_fields: base must be a contiguous int64 [5, {nq}] tensor on {dev}, "
+                         f"got {base.dtype} {tuple(base.shape)} on {base.device}")
     o = {"sal": torch.empty((nq, k), dtype=torch.float32, device=dev),
          "acc": torch.empty((nq, k), dtype=torch.int32, device=dev),
          "kind": torch.empty((nq, k), dtype=torch.uint8, device=dev),

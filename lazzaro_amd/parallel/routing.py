@@ -185,7 +185,7 @@ def local_search(svc, users: Sequence[str], Q: torch.Tensor, limits: Sequence[in
             from ..ops.tenant_ops import gather_fields
             qi = [j for u in fused for j in groups[u]]
             qu = [users[j] for j in qi]
-            table = svc.tenant_table()
+            table = svc.tenant_table(dev)
             slots = table.slots(qu, systems)
             ptrs = table.d_ptr[:, slots]
             nrows = table.d_n[slots]
@@ -365,8 +365,8 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     NQ = Qall.shape[0]
     best_s = torch.full((NQ, limit), float("-inf"), dtype=torch.float32, device=dev)
     best_k = torch.full((NQ, limit), -1, dtype=torch.int64, device=dev)
-    table = svc.tenant_table()
     users = [u for u, ms in svc.systems.items() if ms.graph.dim == D and ms.graph.n > 0]
+    table = svc.tenant_table(svc.systems[users[0]].graph.device if users else None)
     if users:
         slots = table.slots(users, {u: svc.systems[u] for u in users}).cpu().tolist()
         for u, slot in zip(users, slots):

@@ -124,9 +124,15 @@ class DistributedMemoryService:
         ms._save_to_persistence()
         ms.close()
 
-    def tenant_table(self) -> "routing.TenantTable":
-        if self._table is None:
-            self._table = routing.TenantTable(self.comm.device)
+    def tenant_table(self, device=None) -> "routing.TenantTable":
+        """The device table of resident tenants' column pointers, on the
+        tenants' device (NOT necessarily the communicator's: a CPU/gloo
+        communicator can front GPU tenants)."""
+        dev = torch.device(device) if device is not None else torch.device(self.comm.device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        if self._table is None or self._table.device != dev:
+            self._table = routing.TenantTable(dev)
         return self._table
 
     def is_local(self, user: str) -> bool:
@@ -330,7 +336,7 @@ class DistributedMemoryService:
             with tracer.stage("mt_prep", "cpu"):
                 D = Q.shape[1]
                 graphs = {u: ms.graph for u, ms in systems.items()}
-                table = self.tenant_table()
+                table = self.tenant_table(dev)
                 slots = table.slots(users, systems)
                 ptrs = table.d_ptr[:, slots]
                 nrows = table.d_n[slots]

@@ -28,7 +28,11 @@ class RandEmbedder:
         return [self._v(t) for t in ts]
 
 
-def test_fused_multi_tenant_search_matches_per_tenant(tmp_path):
+@pytest.mark.parametrize("comm_dev", ["cuda", None])
+def test_fused_multi_tenant_search_matches_per_tenant(tmp_path, comm_dev):
+    """comm_dev None: a host communicator fronting GPU tenants (the multi-
+    tenant bench's setup) -- the tenant pointer table must live on the
+    tenants' device, not the communicator's."""
     from lazzaro_amd.core.memory_system import MemorySystem
     from lazzaro_amd.core.providers import LocalLLM
     from lazzaro_amd.parallel import Communicator
@@ -39,7 +43,8 @@ def test_fused_multi_tenant_search_matches_per_tenant(tmp_path):
         return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, enable_async=False,
                             db_dir=str(tmp_path), user_id=user, device="cuda", load_from_disk=load_from_disk,
                             max_buffer_size=10 ** 6)
-    svc = DistributedMemoryService(Communicator.local(torch.device("cuda")), factory)
+    comm = Communicator.local(torch.device(comm_dev)) if comm_dev else Communicator.local()
+    svc = DistributedMemoryService(comm, factory)
     users = [f"t{i}" for i in range(24)]
     rng = np.random.default_rng(0)
     for j, u in enumerate(users):
