@@ -91,9 +91,18 @@ def main():
     reqs = [batch() for _ in range(a.steps)]
     torch.cuda.synchronize()
     comm.barrier()
+    prof = None
+    if os.environ.get("LZK_PROF_HOST") == "1":  # host-side profile of the timed loop (stderr)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     outs = list(svc.serve_stream(reqs)) if a.stream else [svc.serve(r) for r in reqs]
     torch.cuda.synchronize()
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     comm.barrier()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev)

@@ -78,10 +78,19 @@ def main():
         st["store_scan_s"] = time.time() - t
         return r
     HBMStore.load_tenant = timed_scan
+    prof = None
+    if os.environ.get("LZK_PROF_HOST") == "1":  # host-side profile of the reload (stderr)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.time()
     ms2 = make(True)
     torch.cuda.synchronize() if dev.type == "cuda" else None
     t_load = time.time() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
     ok = ms2.graph.n == a.rows and torch.equal(ms2.graph.emb32[: ref.shape[0]].cpu(), ref)
     du = sum(os.path.getsize(os.path.join(r, f)) for r, _, fs in os.walk(db) for f in fs)
     out = {"metric": "tenant reload (store -> HBM tenant graph)", "rows": a.rows, "dim": a.dim,

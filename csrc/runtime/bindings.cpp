@@ -17,13 +17,37 @@ using namespace lzrt;
 
 namespace {
 
-Column to_column(const ColSpec& spec, py::handle obj) {
+// Python column -> Column. String lists are read through the CPython API
+// (the UTF-8 of a compact str is cached in the object: no encode) and a run of
+// the same object (["{}"] * n, a constant user_id) copies the previous value;
+// fp32 arrays are BORROWED (Column::ext) -- `keep` holds them until the call
+// that uses the columns returns.
+Column to_column(const ColSpec& spec, py::handle obj, std::vector<py::object>& keep) {
   Column c;
   c.type = spec.type;
   c.dim = spec.dim;
   switch (spec.type) {
     case ColType::Str: {
-      for (auto item : obj) c.s.push_back(py::cast<std::string>(item));
+      PyObject* seq = PySequence_Fast(obj.ptr(), "string column must be a sequence");
+      if (!seq) throw py::error_already_set();
+      const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+      PyObject** items = PySequence_Fast_ITEMS(seq);
+      c.s.resize((size_t)n);
+      PyObject* prev = nullptr;
+      for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject* o = items[i];
+        if (o == prev) { c.s[i] = c.s[i - 1]; continue; }
+        if (PyUnicode_Check(o)) {
+          Py_ssize_t len = 0;
+          const char* p = PyUnicode_AsUTF8AndSize(o, &len);
+          if (!p) { Py_DECREF(seq); throw py::error_already_set(); }
+          c.s[i].assign(p, (size_t)len);
+        } else {
+          c.s[i] = py::cast<std::string>(py::handle(o));
+        }
+        prev = o;
+      }
+      Py_DECREF(seq);
       break;
     }
     case ColType::F64: {
@@ -33,7 +57,9 @@ Column to_column(const ColSpec& spec, py::handle obj) {
     }
     case ColType::F32: {
       auto a = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(obj);
-      c.f32.assign(a.data(), a.data() + a.size());
+      c.ext = a.data();
+      c.ext_n = (size_t)a.size();
+      keep.push_back(a);
       break;
     }
     case ColType::I32: {
@@ -55,7 +81,9 @@ Column to_column(const ColSpec& spec, py::handle obj) {
       auto a = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(obj);
       if (a.ndim() != 2) throw std::runtime_error("vector column must be 2-D");
       c.dim = (uint32_t)a.shape(1);
-      c.f32.assign(a.data(), a.data() + a.size());
+      c.ext = a.data();
+      c.ext_n = (size_t)a.size();
+      keep.push_back(a);
       break;
     }
   }
@@ -153,9 +181,10 @@ PYBIND11_MODULE(_lzrt, m) {
       .def("compact", [](Table& t) { py::gil_scoped_release r; return t.compact(); })
       .def("append", [](Table& t, py::dict cols) {
         std::vector<Column> cs;
+        std::vector<py::object> keep;
         for (auto& spec : t.schema()) {
           if (!cols.contains(spec.name.c_str())) throw std::runtime_error("missing column " + spec.name);
-          cs.push_back(to_column(spec, cols[spec.name.c_str()]));
+          cs.push_back(to_column(spec, cols[spec.name.c_str()], keep));
         }
         py::gil_scoped_release r;
         return t.append(cs);
@@ -175,10 +204,11 @@ PYBIND11_MODULE(_lzrt, m) {
       .def("stage",
            [](Table& t, py::dict cols) {
              std::vector<Column> cs;
+             std::vector<py::object> keep;
              uint32_t dim = 0;
              for (auto& spec : t.schema()) {
                if (!cols.contains(spec.name.c_str())) throw std::runtime_error("missing column " + spec.name);
-               cs.push_back(to_column(spec, cols[spec.name.c_str()]));
+               cs.push_back(to_column(spec, cols[spec.name.c_str()], keep));
                if (spec.type == ColType::VecF32) dim = cs.back().dim;
              }
              std::pair<std::string, uint64_t> r;
@@ -199,9 +229,10 @@ PYBIND11_MODULE(_lzrt, m) {
               py::object in_vals, py::dict cols) {
              Predicate p = make_pred(eq, in_col, in_vals);
              std::vector<Column> cs;
+             std::vector<py::object> keep;
              for (auto& spec : t.schema()) {
                if (!cols.contains(spec.name.c_str())) throw std::runtime_error("missing column " + spec.name);
-               cs.push_back(to_column(spec, cols[spec.name.c_str()]));
+               cs.push_back(to_column(spec, cols[spec.name.c_str()], keep));
              }
              uint64_t n = 0, v;
              {
@@ -279,6 +310,28 @@ PYBIND11_MODULE(_lzrt, m) {
                                 py::array_t<int32_t>(adj.size(), adj.data()),
                                 py::array_t<int32_t>(eid.size(), eid.data()));
         });
+  m.def("max_node_num",
+        [](py::list ids) {
+          // largest n of "node_<n>" ids (the reference's id scheme), 0 if none
+          long long mx = 0;
+          for (auto h : ids) {
+            PyObject* o = h.ptr();
+            if (!PyUnicode_Check(o)) continue;
+            Py_ssize_t len = 0;
+            const char* p = PyUnicode_AsUTF8AndSize(o, &len);
+            if (!p || len <= 5 || len > 5 + 18 || std::memcmp(p, "node_", 5) != 0) continue;
+            long long v = 0;
+            bool ok = true;
+            for (Py_ssize_t i = 5; i < len; ++i) {
+              if (p[i] < '0' || p[i] > '9') { ok = false; break; }
+              v = v * 10 + (p[i] - '0');
+            }
+            if (ok && v > mx) mx = v;
+          }
+          PyErr_Clear();
+          return mx;
+        },
+        py::arg("ids"));
   m.def("union_find_components",
         [](py::array_t<int32_t, py::array::c_style | py::array::forcecast> src,
            py::array_t<int32_t, py::array::c_style | py::array::forcecast> dst, int n) {

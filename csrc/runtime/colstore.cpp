@@ -109,7 +109,7 @@ std::shared_ptr<arrow::Array> to_arrow(const Column& c, int64_t r0, int64_t r1) 
     }
     case ColType::F32: {
       arrow::FloatBuilder b;
-      check(b.AppendValues(c.f32.data() + r0, n), "f32 column");
+      check(b.AppendValues(c.fdata() + r0, n), "f32 column");
       return ok_or_throw(b.Finish(), "f32 column");
     }
     case ColType::I32: {
@@ -131,7 +131,7 @@ std::shared_ptr<arrow::Array> to_arrow(const Column& c, int64_t r0, int64_t r1) 
       // zero-copy: the Arrow array wraps the column's memory (alive until
       // the fragment is written); no 30 GB builder copy for a 10M-row commit
       const int64_t nv = n * (int64_t)c.dim;
-      auto buf = arrow::Buffer::Wrap(c.f32.data() + (size_t)r0 * c.dim, (size_t)nv);
+      auto buf = arrow::Buffer::Wrap(c.fdata() + (size_t)r0 * c.dim, (size_t)nv);
       auto values = std::make_shared<arrow::FloatArray>(nv, buf);
       return ok_or_throw(arrow::FixedSizeListArray::FromArrays(values, (int32_t)c.dim), "vector column");
     }
@@ -158,7 +158,11 @@ void advise(const void* p, size_t n, int advice, uintptr_t align = 4096) {
   if (e > a) (void)madvise((void*)a, e - a, advice);
 }
 
+// set in a scan's fragment-parallel workers: their copies stay on the thread
+thread_local bool t_serial_copy = false;
+
 void par_copy(void* dst, const void* src, size_t bytes) {
+  if (t_serial_copy) { std::memcpy(dst, src, bytes); return; }
   constexpr size_t kMin = size_t(64) << 20;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   const size_t nt = std::min<size_t>(hw, std::max<size_t>(1, bytes / kMin));
@@ -245,17 +249,105 @@ void from_arrow(const std::shared_ptr<arrow::Array>& a, Column& c, uint64_t nrow
   }
 }
 
+// Rows [0, nrows) of an Arrow array into rows [at, at + nrows) of a column
+// already sized for them (missing array -> defaults).
+void from_arrow_at(const std::shared_ptr<arrow::Array>& a, Column& c, uint64_t at, uint64_t nrows) {
+  switch (c.type) {
+    case ColType::Str: {
+      if (!a) { for (uint64_t r = 0; r < nrows; ++r) c.s[at + r].clear(); break; }
+      auto x = std::static_pointer_cast<arrow::StringArray>(a);
+      for (uint64_t r = 0; r < nrows; ++r) c.s[at + r].assign(x->GetView((int64_t)r));
+      break;
+    }
+    case ColType::F64:
+      if (a) std::memcpy(c.f64.data() + at, std::static_pointer_cast<arrow::DoubleArray>(a)->raw_values(), nrows * 8);
+      else std::fill(c.f64.begin() + at, c.f64.begin() + at + nrows, 0.0);
+      break;
+    case ColType::F32:
+      if (a) std::memcpy(c.f32.data() + at, std::static_pointer_cast<arrow::FloatArray>(a)->raw_values(), nrows * 4);
+      else std::fill(c.f32.begin() + at, c.f32.begin() + at + nrows, 0.f);
+      break;
+    case ColType::I32:
+      if (a) std::memcpy(c.i32.data() + at, std::static_pointer_cast<arrow::Int32Array>(a)->raw_values(), nrows * 4);
+      else std::fill(c.i32.begin() + at, c.i32.begin() + at + nrows, 0);
+      break;
+    case ColType::I64:
+      if (a) std::memcpy(c.i64.data() + at, std::static_pointer_cast<arrow::Int64Array>(a)->raw_values(), nrows * 8);
+      else std::fill(c.i64.begin() + at, c.i64.begin() + at + nrows, 0);
+      break;
+    case ColType::Bool: {
+      if (!a) { std::fill(c.b.begin() + at, c.b.begin() + at + nrows, 0); break; }
+      auto x = std::static_pointer_cast<arrow::BooleanArray>(a);
+      for (uint64_t r = 0; r < nrows; ++r) c.b[at + r] = x->Value((int64_t)r) ? 1 : 0;
+      break;
+    }
+    case ColType::VecF32: {
+      const size_t d = c.dim;
+      if (!a) { std::fill(c.f32.begin() + at * d, c.f32.begin() + (at + nrows) * d, 0.f); break; }
+      auto l = std::static_pointer_cast<arrow::FixedSizeListArray>(a);
+      if ((size_t)l->list_type()->list_size() != d) throw std::runtime_error("colstore: vector dim mismatch in scan");
+      auto v = std::static_pointer_cast<arrow::FloatArray>(l->values());
+      par_copy(c.f32.data() + at * d, v->raw_values() + l->value_offset(0), nrows * d * sizeof(float));
+      break;
+    }
+  }
+}
+
+// One row of an Arrow array into row `dst` of a sized column.
+void row_from_arrow(const std::shared_ptr<arrow::Array>& a, Column& c, uint64_t src, uint64_t dst) {
+  if (!a) {  // defaults (FloatVec storage is not zeroed by resize)
+    if (c.type == ColType::F32) c.f32[dst] = 0.f;
+    if (c.type == ColType::VecF32) std::fill(c.f32.begin() + dst * c.dim, c.f32.begin() + (dst + 1) * c.dim, 0.f);
+    return;
+  }
+  switch (c.type) {
+    case ColType::Str: c.s[dst].assign(std::static_pointer_cast<arrow::StringArray>(a)->GetView((int64_t)src)); break;
+    case ColType::F64: c.f64[dst] = std::static_pointer_cast<arrow::DoubleArray>(a)->Value((int64_t)src); break;
+    case ColType::F32: c.f32[dst] = std::static_pointer_cast<arrow::FloatArray>(a)->Value((int64_t)src); break;
+    case ColType::I32: c.i32[dst] = std::static_pointer_cast<arrow::Int32Array>(a)->Value((int64_t)src); break;
+    case ColType::I64: c.i64[dst] = std::static_pointer_cast<arrow::Int64Array>(a)->Value((int64_t)src); break;
+    case ColType::Bool: c.b[dst] = std::static_pointer_cast<arrow::BooleanArray>(a)->Value((int64_t)src) ? 1 : 0; break;
+    case ColType::VecF32: {
+      auto l = std::static_pointer_cast<arrow::FixedSizeListArray>(a);
+      auto v = std::static_pointer_cast<arrow::FloatArray>(l->values());
+      std::memcpy(c.f32.data() + dst * c.dim, v->raw_values() + l->value_offset((int64_t)src), c.dim * sizeof(float));
+      break;
+    }
+  }
+}
+
+template <class F>
+void par_for(size_t n, size_t max_threads, F&& fn) {
+  const size_t nt = std::min(n, max_threads);
+  if (nt <= 1) { for (size_t i = 0; i < n; ++i) fn(i); return; }
+  std::atomic<size_t> next{0};
+  std::vector<std::exception_ptr> err(nt);
+  std::vector<std::thread> ts;
+  for (size_t t = 0; t < nt; ++t)
+    ts.emplace_back([&, t] {
+      t_serial_copy = true;
+      try {
+        for (size_t i; (i = next++) < n;) fn(i);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    });
+  for (auto& th : ts) th.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
 }  // namespace
 
 size_t Column::size() const {
   switch (type) {
     case ColType::Str: return s.size();
     case ColType::F64: return f64.size();
-    case ColType::F32: return f32.size();
+    case ColType::F32: return fsize();
     case ColType::I32: return i32.size();
     case ColType::I64: return i64.size();
     case ColType::Bool: return b.size();
-    case ColType::VecF32: return dim ? f32.size() / dim : 0;
+    case ColType::VecF32: return dim ? fsize() / dim : 0;
   }
   return 0;
 }
@@ -264,12 +356,12 @@ void Column::append_from(const Column& o, size_t r) {
   switch (type) {
     case ColType::Str: s.push_back(o.s[r]); break;
     case ColType::F64: f64.push_back(o.f64[r]); break;
-    case ColType::F32: f32.push_back(o.f32[r]); break;
+    case ColType::F32: f32.push_back(o.fdata()[r]); break;
     case ColType::I32: i32.push_back(o.i32[r]); break;
     case ColType::I64: i64.push_back(o.i64[r]); break;
     case ColType::Bool: b.push_back(o.b[r]); break;
     case ColType::VecF32:
-      f32.insert(f32.end(), o.f32.begin() + r * o.dim, o.f32.begin() + (r + 1) * o.dim);
+      f32.insert(f32.end(), o.fdata() + r * o.dim, o.fdata() + (r + 1) * o.dim);
       break;
   }
 }
@@ -576,7 +668,7 @@ void Table::fix_dims(const std::vector<Column>& cols) {
   }
 }
 
-void Table::add_fragment(const std::string& file, uint64_t rows, const std::vector<Column>* cols) {
+void Table::add_fragment(const std::string& file, uint64_t rows, const std::vector<Column>* cols, uint64_t r0) {
   Frag f;
   f.file = file;
   f.rows = rows;
@@ -585,14 +677,52 @@ void Table::add_fragment(const std::string& file, uint64_t rows, const std::vect
   const uint32_t fi = (uint32_t)frags_.size() - 1;
   if (!indexed_) return;
   if (cols) {
-    for (uint64_t r = 0; r < rows; ++r) index_.emplace(make_key(*cols, r), std::make_pair(fi, (uint32_t)r));
+    for (uint64_t r = 0; r < rows; ++r) index_.emplace(make_key(*cols, r0 + r), std::make_pair(fi, (uint32_t)r));
     indexed_frags_ = fi + 1;
   } else {
     index_fragment(fi);
   }
 }
 
-void Table::write_fragment(const std::string& file, const std::vector<Column>& cols) {
+// Rows [0, n) of cols as one fragment, or -- past LZK_COLSTORE_PAR_ROWS rows
+// (default 2^20) -- as up to 16 fragments of consecutive row ranges encoded
+// and written by one thread each (a 10M x 768 commit is 31 GB of Arrow IPC:
+// one writer thread held it at ~0.7 GB/s). Caller holds the lock; the
+// fragments join the table in row order, in the caller's one version.
+void Table::write_fragments(const std::vector<Column>& cols, size_t n) {
+  static const size_t kPar = [] {
+    const char* e = getenv("LZK_COLSTORE_PAR_ROWS");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (size_t)v : (size_t(1) << 20);
+  }();
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t nt = std::min<size_t>(hw, std::max<size_t>(1, n / kPar));
+  std::vector<std::string> files(nt);
+  std::vector<size_t> lo(nt + 1);
+  for (size_t t = 0; t <= nt; ++t) lo[t] = n * t / nt;
+  for (auto& f : files) f = uniq_name() + ".arrow";
+  if (nt == 1) {
+    write_fragment(files[0], cols, 0, (int64_t)n);
+  } else {
+    std::vector<std::exception_ptr> err(nt);
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < nt; ++t)
+      ts.emplace_back([&, t] {
+        try {
+          write_fragment(files[t], cols, (int64_t)lo[t], (int64_t)lo[t + 1]);
+        } catch (...) {
+          err[t] = std::current_exception();
+        }
+      });
+    for (auto& th : ts) th.join();
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  }
+  for (size_t t = 0; t < nt; ++t) add_fragment(files[t], lo[t + 1] - lo[t], &cols, lo[t]);
+}
+
+void Table::write_fragment(const std::string& file, const std::vector<Column>& cols, int64_t r_begin,
+                           int64_t r_end) {
   arrow::FieldVector fields;
   std::vector<std::shared_ptr<arrow::Array>> arrays;
   int64_t width = 1;  // values per row of the widest column
@@ -603,7 +733,7 @@ void Table::write_fragment(const std::string& file, const std::vector<Column>& c
     fields.push_back(arrow::field(spec.name, arrow_type(spec), false));
   }
   auto sch = arrow::schema(fields);
-  const int64_t n = cols.empty() ? 0 : (int64_t)cols[0].size();
+  const int64_t n = r_end >= 0 ? r_end : (cols.empty() ? 0 : (int64_t)cols[0].size());
   // record batches of <= 2^30 values per array and <= 2^30 string bytes
   // (LZK_COLSTORE_BATCH_VALUES lowers the cap: tests exercise multi-batch files)
   static const int64_t kMaxVals = [] {
@@ -615,7 +745,7 @@ void Table::write_fragment(const std::string& file, const std::vector<Column>& c
   {
     auto out = ok_or_throw(arrow::io::FileOutputStream::Open(tmp), "open fragment");
     auto w = ok_or_throw(arrow::ipc::MakeFileWriter(out, sch), "fragment writer");
-    int64_t r0 = 0;
+    int64_t r0 = r_begin;
     do {
       int64_t r1 = std::min<int64_t>(n, r0 + std::max<int64_t>(1, kMaxVals / width));
       for (size_t i = 0; i < cols.size(); ++i) {
@@ -715,11 +845,7 @@ uint64_t Table::replace_where(const Predicate& p, const std::vector<Column>& col
     if (n > 0) fix_dims(cols_in);
     const uint64_t nv = cur_version_ + 1;
     if (has_pred) total = apply_delete(p, nv);
-    if (n > 0) {
-      std::string file = uniq_name() + ".arrow";
-      write_fragment(file, cols_in);
-      add_fragment(file, n, &cols_in);
-    }
+    if (n > 0) write_fragments(cols_in, n);
     if (n > 0 || total > 0 || has_pred) write_manifest(nv);
   } catch (...) { unlock(); throw; }
   unlock();
@@ -727,6 +853,12 @@ uint64_t Table::replace_where(const Predicate& p, const std::vector<Column>& col
   return cur_version_;
 }
 
+// Rows matching p, every wanted column. Each fragment is memory-mapped once;
+// rows are selected on zero-copy views of the predicate columns, the output
+// columns are sized once, and the fragments decode straight into their row
+// range -- in parallel over fragments when there are several (a parallel
+// commit leaves ~10 per 10M-row tenant), else with a multi-threaded copy of
+// the vector column. No fragment is materialised and then copied again.
 std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::string>& want_names) {
   lock();  // a consistent fragment list (writers append under the same lock)
   std::vector<Frag> frags;
@@ -738,64 +870,107 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
   std::vector<int> pcols;
   for (auto& kv : p.eq) pcols.push_back(col_index(kv.first));
   if (p.has_in) pcols.push_back(col_index(p.in_col));
+  const bool bad_pred = std::find(pcols.begin(), pcols.end(), -1) != pcols.end();
   std::vector<int> want;
   if (want_names.empty()) {
     for (size_t i = 0; i < schema_.size(); ++i) want.push_back((int)i);
   } else {
     for (auto& n : want_names) { int c = col_index(n); if (c >= 0) want.push_back(c); }
   }
-  std::vector<int> need = want;
-  for (int c : pcols) if (c >= 0 && std::find(need.begin(), need.end(), c) == need.end()) need.push_back(c);
   std::vector<Column> out(schema_.size());
   for (size_t i = 0; i < schema_.size(); ++i) { out[i].type = schema_[i].type; out[i].dim = schema_[i].dim; }
-  for (auto& fr : frags) {
-    if (fr.n_dead == fr.rows) continue;
-    uint64_t nrows = 0;
-    auto cols = read_fragment(fr.file, need, &nrows);
-    for (int c : want)
-      if (out[c].type == ColType::VecF32 && out[c].dim == 0) out[c].dim = cols[c].dim;
+  if (bad_pred) return out;
+  struct FR {
+    std::vector<std::shared_ptr<arrow::RecordBatch>> batches;
+    std::vector<uint64_t> base;  // first row of each batch
+    uint64_t n = 0;
     std::vector<uint32_t> sel;
-    sel.reserve(nrows);
-    for (uint64_t r = 0; r < nrows; ++r)
-      if (!fr.dead[r] && (pcols.empty() || matches(cols, pcols, p, r))) sel.push_back((uint32_t)r);
-    if (sel.size() == nrows) {  // the whole fragment (a tenant's commit): bulk moves
-      for (int c : want) {
-        Column& o = out[c];
-        Column& s = cols[c];
-        switch (o.type) {
-          case ColType::Str: o.s.insert(o.s.end(), std::make_move_iterator(s.s.begin()), std::make_move_iterator(s.s.end())); break;
-          case ColType::F64: o.f64.insert(o.f64.end(), s.f64.begin(), s.f64.end()); break;
-          case ColType::F32: case ColType::VecF32:
-            if (o.f32.empty()) o.f32 = std::move(s.f32);  // the common single-fragment load: no copy
-            else o.f32.insert(o.f32.end(), s.f32.begin(), s.f32.end());
-            break;
-          case ColType::I32: o.i32.insert(o.i32.end(), s.i32.begin(), s.i32.end()); break;
-          case ColType::I64: o.i64.insert(o.i64.end(), s.i64.begin(), s.i64.end()); break;
-          case ColType::Bool: o.b.insert(o.b.end(), s.b.begin(), s.b.end()); break;
-        }
-      }
-      continue;
+    bool all = false;
+  };
+  const size_t F = frags.size();
+  std::vector<FR> fr(F);
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t fthreads = F >= 4 ? hw : 1;
+  par_for(F, fthreads, [&](size_t i) {
+    const Frag& meta = frags[i];
+    FR& f = fr[i];
+    if (meta.n_dead == meta.rows) return;
+    auto mm = ok_or_throw(arrow::io::MemoryMappedFile::Open(dir_ + "/data/" + meta.file, arrow::io::FileMode::READ),
+                          "open fragment");
+    auto rd = ok_or_throw(arrow::ipc::RecordBatchFileReader::Open(mm), "read fragment");
+    for (int bi = 0; bi < rd->num_record_batches(); ++bi) {
+      f.batches.push_back(ok_or_throw(rd->ReadRecordBatch(bi), "fragment batch"));
+      f.base.push_back(f.n);
+      f.n += (uint64_t)f.batches.back()->num_rows();
     }
-    for (int c : want) {
-      Column& o = out[c];
-      Column& s = cols[c];
-      switch (o.type) {
-        case ColType::Str: for (uint32_t r : sel) o.s.push_back(std::move(s.s[r])); break;
-        case ColType::F64: for (uint32_t r : sel) o.f64.push_back(s.f64[r]); break;
-        case ColType::F32: for (uint32_t r : sel) o.f32.push_back(s.f32[r]); break;
-        case ColType::I32: for (uint32_t r : sel) o.i32.push_back(s.i32[r]); break;
-        case ColType::I64: for (uint32_t r : sel) o.i64.push_back(s.i64[r]); break;
-        case ColType::Bool: for (uint32_t r : sel) o.b.push_back(s.b[r]); break;
-        case ColType::VecF32: {
-          const size_t d = s.dim, base = o.f32.size();
-          o.f32.resize(base + sel.size() * d);
-          for (size_t j = 0; j < sel.size(); ++j)
-            std::memcpy(o.f32.data() + base + j * d, s.f32.data() + (size_t)sel[j] * d, d * sizeof(float));
-          break;
-        }
+    f.sel.reserve(f.n);
+    for (size_t bi = 0; bi < f.batches.size(); ++bi) {
+      auto& b = f.batches[bi];
+      std::vector<std::shared_ptr<arrow::StringArray>> pa;
+      bool missing = false;
+      for (int ci : pcols) {
+        auto arr = b->GetColumnByName(schema_[ci].name);
+        if (!arr) missing = true;
+        pa.push_back(std::static_pointer_cast<arrow::StringArray>(arr));
       }
+      const uint64_t m = (uint64_t)b->num_rows();
+      for (uint64_t r = 0; r < m; ++r) {
+        const uint64_t R = f.base[bi] + r;
+        if (R < meta.dead.size() && meta.dead[R]) continue;
+        if (!pcols.empty()) {
+          if (missing) continue;
+          bool ok = true;
+          for (size_t k = 0; k < p.eq.size() && ok; ++k) ok = pa[k]->GetView((int64_t)r) == p.eq[k].second;
+          if (ok && p.has_in) ok = p.in_vals.count(std::string(pa.back()->GetView((int64_t)r))) > 0;
+          if (!ok) continue;
+        }
+        f.sel.push_back((uint32_t)R);
+      }
+    }
+    f.all = f.sel.size() == f.n;
+    if (f.all) std::vector<uint32_t>().swap(f.sel);
+  });
+  std::vector<uint64_t> off(F + 1, 0);
+  for (size_t i = 0; i < F; ++i) off[i + 1] = off[i] + (fr[i].all ? fr[i].n : fr[i].sel.size());
+  const uint64_t total = off[F];
+  for (int c : want) {
+    Column& o = out[c];
+    if (o.type == ColType::VecF32 && o.dim == 0)
+      for (auto& f : fr)
+        if (!f.batches.empty()) {
+          auto a = f.batches[0]->GetColumnByName(schema_[c].name);
+          if (a) { o.dim = (uint32_t)std::static_pointer_cast<arrow::FixedSizeListArray>(a)->list_type()->list_size(); break; }
+        }
+    switch (o.type) {
+      case ColType::Str: o.s.resize(total); break;
+      case ColType::F64: o.f64.resize(total); break;
+      case ColType::F32: o.f32.resize(total); break;
+      case ColType::I32: o.i32.resize(total); break;
+      case ColType::I64: o.i64.resize(total); break;
+      case ColType::Bool: o.b.resize(total); break;
+      case ColType::VecF32: o.f32.resize(total * (size_t)o.dim); break;
     }
   }
+  par_for(F, fthreads, [&](size_t i) {
+    FR& f = fr[i];
+    if (off[i + 1] == off[i]) return;
+    if (f.all) {
+      for (size_t bi = 0; bi < f.batches.size(); ++bi) {
+        const uint64_t m = (uint64_t)f.batches[bi]->num_rows();
+        for (int c : want) from_arrow_at(f.batches[bi]->GetColumnByName(schema_[c].name), out[c], off[i] + f.base[bi], m);
+      }
+      return;
+    }
+    size_t bi = 0;
+    std::vector<std::shared_ptr<arrow::Array>> arrs(schema_.size());
+    auto load = [&](size_t b) { for (int c : want) arrs[c] = f.batches[b]->GetColumnByName(schema_[c].name); };
+    load(0);
+    for (size_t j = 0; j < f.sel.size(); ++j) {
+      const uint64_t R = f.sel[j];
+      while (bi + 1 < f.batches.size() && R >= f.base[bi + 1]) load(++bi);
+      for (int c : want) row_from_arrow(arrs[c], out[c], R - f.base[bi], off[i] + j);
+    }
+  });
   return out;
 }
 

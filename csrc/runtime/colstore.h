@@ -66,6 +66,13 @@ struct Column {
   std::vector<int32_t> i32;
   std::vector<int64_t> i64;
   std::vector<uint8_t> b;
+  // F32 / VecF32 input columns may borrow the caller's buffer instead of
+  // owning a copy (a 10M x 768 commit: 30 GB not copied); the owner keeps it
+  // alive for the duration of the call
+  const float* ext = nullptr;
+  size_t ext_n = 0;
+  const float* fdata() const { return ext ? ext : f32.data(); }
+  size_t fsize() const { return ext ? ext_n : f32.size(); }
   size_t size() const;
   void append_from(const Column& o, size_t row);
 };
@@ -134,10 +141,11 @@ class Table {
   std::string make_key(const std::vector<Column>& cols, size_t r) const;
   bool keyed(const Predicate& p, std::vector<std::string>* keys) const;
   uint64_t apply_delete(const Predicate& p, uint64_t nv);
-  void add_fragment(const std::string& file, uint64_t rows, const std::vector<Column>* cols);
+  void add_fragment(const std::string& file, uint64_t rows, const std::vector<Column>* cols, uint64_t r0 = 0);
+  void write_fragments(const std::vector<Column>& cols, size_t n);
   void fix_dims(const std::vector<Column>& cols);
   std::vector<Column> read_fragment(const std::string& file, const std::vector<int>& want, uint64_t* nrows);
-  void write_fragment(const std::string& file, const std::vector<Column>& cols);
+  void write_fragment(const std::string& file, const std::vector<Column>& cols, int64_t r0 = 0, int64_t r1 = -1);
   bool matches(const std::vector<Column>& cols, const std::vector<int>& pcols, const Predicate& p, size_t r) const;
 };
 

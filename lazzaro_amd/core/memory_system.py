@@ -1147,6 +1147,7 @@ Be clinical yet insightful. Do not include conversational filler."""
             rows = g.node_rows_where()
             nc = export_node_columns(g, rows, device_vectors=True)
             vec = nc.pop("vector", None)
+            nc.pop("fresh", None)
             if vec is None:
                 vec = torch.zeros((0, g.dim or 0), device=g.device)
             nc.pop("count", None)
@@ -1205,7 +1206,13 @@ Be clinical yet insightful. Do not include conversational filler."""
 def export_node_columns(g: TenantGraph, rows: np.ndarray, device_vectors: bool = False) -> Dict:
     """Store columns (SURVEY.md App. D + ``decay_clock``) of graph rows.
     ``device_vectors``: the vector column stays a device tensor (migration
-    over the interconnect) instead of a host array."""
+    over the interconnect) instead of a host array. ``fresh``: rows never
+    committed (the store cannot hold their ids: no delete needed).
+
+    Every per-row column is built by C-level loops (``map`` over the lists,
+    object-array indexing) and the sparse ones (children, parents, odd
+    vectors) are patched from their few entries: a 10M-row commit used to
+    spend ~20 s in per-row ``json.dumps`` / list comprehensions."""
     rows = np.asarray(rows, dtype=np.int64)
     n = rows.size
     D = g.dim or 0
@@ -1219,29 +1226,52 @@ def export_node_columns(g: TenantGraph, rows: np.ndarray, device_vectors: bool =
             vec = g.emb32[rt].cpu().numpy() if g.dim is not None else np.zeros((n, 0), dtype=np.float32)
         cols = {k: getattr(g, c)[rt].cpu().numpy() for k, c in
                 (("timestamp", "ts"), ("access_count", "acc"), ("last_accessed", "last"), ("salience", "sal"),
-                 ("is_super_node", "sup"), ("parent", "parent"), ("shard", "shard"))}
-    for j, r in enumerate(rows.tolist()):
-        if r in g.odd_emb and D:
-            vec[j] = 0.0
+                 ("is_super_node", "sup"), ("parent", "parent"), ("shard", "shard"), ("stored", "stored"))}
+    rl = rows.tolist()
+    # position of each exported row (for the sparse patches below)
+    sparse = [r for r in g.odd_emb] + list(g.children.keys())
+    pos = {}
+    if sparse:
+        rmap = np.full(max(g.n, int(rows.max()) + 1), -1, dtype=np.int64)
+        rmap[rows] = np.arange(n)
+        pos = {r: int(rmap[r]) for r in set(sparse) if r < rmap.size and rmap[r] >= 0}
+    if D:
+        for r in g.odd_emb:
+            j = pos.get(r)
+            if j is not None:
+                vec[j] = 0.0
+    child = ["[]"] * n
+    for r, ch in g.children.items():
+        j = pos.get(r)
+        if j is not None:
+            child[j] = json.dumps(ch)
     par = cols.pop("parent")
+    parent_id = [""] * n
+    pj = np.nonzero(par >= 0)[0]
+    if pj.size:
+        ids = g.ids
+        for j, pr in zip(pj.tolist(), par[pj].tolist()):
+            parent_id[j] = ids[pr]
     sh = cols.pop("shard")
-    ids = [g.ids[r] for r in rows.tolist()]
+    names = np.asarray(list(g.shard_names) + ["default"], dtype=object)
+    shard_key = names[np.where(sh >= 0, sh, len(g.shard_names))].tolist()
     return {
         "count": n,
-        "id": ids,
-        "content": [g.content[r] for r in rows.tolist()],
+        "id": list(map(g.ids.__getitem__, rl)),
+        "content": list(map(g.content.__getitem__, rl)),
         "vector": vec if torch.is_tensor(vec) else np.ascontiguousarray(vec, dtype=np.float32),
-        "type": [g.types[r] for r in rows.tolist()],
+        "type": list(map(g.types.__getitem__, rl)),
         "timestamp": cols["timestamp"].astype(np.float64),
         "access_count": cols["access_count"].astype(np.int32),
         "last_accessed": cols["last_accessed"].astype(np.float64),
         "salience": cols["salience"].astype(np.float32),
         "is_super_node": cols["is_super_node"].astype(np.uint8),
-        "child_ids": [json.dumps(g.children.get(r, [])) for r in rows.tolist()],
-        "parent_id": [g.ids[p] if p >= 0 else "" for p in par.tolist()],
-        "shard_key": [g.shard_names[s] if s >= 0 else "default" for s in sh.tolist()],
+        "child_ids": child,
+        "parent_id": parent_id,
+        "shard_key": shard_key,
         "metadata": ["{}"] * n,
         "decay_clock": np.full(n, g.decay_log, dtype=np.float64),
+        "fresh": cols["stored"] == 0,
     }
 
 
@@ -1407,7 +1437,14 @@ def _jsonable_cols(cols: Dict) -> Dict:
 
 
 def _max_node_num(ids) -> int:
-    """Largest n of the ``node_<n>`` ids (reference id scheme), 0 if none."""
+    """Largest n of the ``node_<n>`` ids (reference id scheme), 0 if none
+    (a C loop over the list when the runtime is built)."""
+    if len(ids) > 4096:
+        try:
+            from ..store.colstore import _rt
+            return int(_rt().max_node_num(ids))
+        except (ImportError, AttributeError):
+            pass
     mx = 0
     for nid in ids:
         m = _NODE_ID.match(nid)

@@ -106,11 +106,22 @@ class HBMStore:
                 n = len(up)
                 if n and self._dim is None and node_cols["vector"].shape[1]:
                     self._dim = node_cols["vector"].shape[1]
-                cols = self._nodes_table.fill_columns({k: v for k, v in node_cols.items() if k != "count"}, n,
-                                                      {"user_id": user_id})
+                cols = self._nodes_table.fill_columns({k: v for k, v in node_cols.items()
+                                                       if k not in ("count", "fresh")}, n, {"user_id": user_id})
                 if n == 0:
                     cols["vector"] = np.zeros((0, self._table_dim() or 0), dtype=np.float32)
-                self._nodes_table.upsert_columns([("user_id", user_id)], "id", up + list(delete_ids), cols)
+                # ids never committed before (``fresh``) cannot be in the table:
+                # only the others (and the deletions) go through the key index
+                fresh = node_cols.get("fresh")
+                if fresh is not None and len(fresh) == n:
+                    old = np.nonzero(~np.asarray(fresh, dtype=bool))[0]
+                    keys = [up[j] for j in old.tolist()] + list(delete_ids)
+                else:
+                    keys = up + list(delete_ids)
+                if keys:
+                    self._nodes_table.upsert_columns([("user_id", user_id)], "id", keys, cols)
+                else:
+                    self._nodes_table.add_columns(cols)
             eu = list(edge_cols.get("id", []))
             if eu or delete_edge_ids:
                 cols = self._edges_table.fill_columns({k: v for k, v in edge_cols.items() if k != "count"}, len(eu),

@@ -250,6 +250,19 @@ class TenantGraph:
         for k, v in new.items():
             setattr(self, k, v)
         self.cap = cap
+        self._alloc_gen = getattr(self, "_alloc_gen", 0) + 1
+
+    def column_ptrs(self) -> Tuple[int, ...]:
+        """Base addresses (emb32, sal, acc, kind, sup, shard) of the current
+        column allocations, recomputed only after a re-allocation -- for
+        pointer tables that index many tenants (parallel/routing.py)."""
+        c = getattr(self, "_ptrs", None)
+        gen = getattr(self, "_alloc_gen", 0)
+        if c is None or c[0] != gen:
+            c = self._ptrs = (gen, (self.emb32.data_ptr() if self.emb32 is not None else 0, self.sal.data_ptr(),
+                                    self.acc.data_ptr(), self.kind.data_ptr(), self.sup.data_ptr(),
+                                    self.shard.data_ptr()))
+        return c[1]
 
     # rows of the mini-batch k-means refinement steps of cluster_pass
     CLUSTER_SAMPLE = 1 << 20

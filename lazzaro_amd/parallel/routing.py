@@ -66,7 +66,7 @@ class TenantTable:
     def __init__(self, device: torch.device):
         self.device = torch.device(device)
         self.slot: Dict[str, int] = {}
-        self.state: List[Tuple[object, int]] = []
+        self.state: List[Tuple[object, int, object]] = []
         self.names: List[str] = []
         self.free: List[int] = []
         self.cap = 0
@@ -82,15 +82,17 @@ class TenantTable:
         hp[:, : self.cap] = self.h_ptr
         hn = np.zeros(cap, np.int32)
         hn[: self.cap] = self.h_n
+        # the new slots join the free list (smallest popped first)
+        self.free = list(range(cap - 1, self.cap - 1, -1)) + self.free
         self.h_ptr, self.h_n, self.cap = hp, hn, cap
-        self.state += [(None, -1)] * (cap - len(self.state))
+        self.state += [(None, -1, None)] * (cap - len(self.state))
         self.names += [""] * (cap - len(self.names))
         self._dirty = True
 
     def drop(self, user: str) -> None:
         s = self.slot.pop(user, None)
         if s is not None:
-            self.state[s] = (None, -1)
+            self.state[s] = (None, -1, None)
             self.h_n[s] = 0
             self.free.append(s)
             self._dirty = True
@@ -104,23 +106,28 @@ class TenantTable:
             if s is None:
                 if not self.free:
                     self._grow(len(self.slot) + 1)
-                    self.free = [i for i in range(self.cap - 1, -1, -1) if self.state[i][0] is None
-                                 and i not in self.slot.values()]
                 s = self.free.pop()
                 self.slot[u] = s
                 self.names[s] = u
             st = self.state[s]
-            if st[0] is not g or st[1] != g.version:
+            # the slot depends on the column allocations, the row count and
+            # the stored-row mask (the bias column), not on row contents
+            key = (getattr(g, "_alloc_gen", 0), g.n, g._store_version)
+            if st[0] is not g or st[1] != key:
                 ok = g.dim is not None and g.n > 0 and g.emb32 is not None
+                b = None
                 if ok:
                     b = g.store_bias("l2")
-                    self.h_ptr[:, s] = [g.emb32.data_ptr(), b.data_ptr(), g.sal.data_ptr(), g.acc.data_ptr(),
-                                        g.kind.data_ptr(), g.sup.data_ptr(), g.shard.data_ptr()]
+                    e, sal, acc, kind, sup, shard = g.column_ptrs()
+                    self.h_ptr[:, s] = (e, b.data_ptr(), sal, acc, kind, sup, shard)
                     self.h_n[s] = g.n
                 else:
                     self.h_ptr[:, s] = 0
                     self.h_n[s] = 0
-                self.state[s] = (g, g.version)
+                # the bias tensor is referenced here: a later store_bias() that
+                # replaces the graph's cached one cannot free memory the table
+                # still points at
+                self.state[s] = (g, key, b)
                 self._dirty = True
             out[j] = s
         if self._dirty:

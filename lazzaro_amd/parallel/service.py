@@ -28,7 +28,9 @@ All collective methods must be called by every rank in the same order.
 from __future__ import annotations
 
 import inspect
+import weakref
 from collections import OrderedDict, defaultdict
+from collections.abc import Sequence as _SeqABC
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -50,7 +52,57 @@ def node_dict(n) -> Dict:
             "shard_key": n.shard_key, "access_count": int(n.access_count), "is_super_node": bool(n.is_super_node)}
 
 
+class SearchHits(_SeqABC):
+    """One request's ``search_memories`` result from the fused multi-tenant
+    path: columnar -- the hit rows and their gathered fields (one host copy
+    per batch) -- and turned into the service's node dicts only when read
+    (indexing, iteration, ``==``, JSON export, a reply to another rank). A
+    batch of 1024 queries x 10 hits no longer builds 10k dicts that a
+    caller may never look at; what a reader sees is
+    exactly the eager result. The service materialises every outstanding
+    result of a tenant before it runs a mutating request on it (or releases
+    / migrates it), so a late read still sees the rows as they were; a
+    caller that mutates a tenant directly (``svc.system(u).chat(...)``)
+    should read its results first."""
+    __slots__ = ("_g", "_cols", "_q", "_limit", "_items", "__weakref__")
+
+    def __init__(self, g, cols: Dict[str, np.ndarray], q: int, limit: int):
+        self._g, self._cols, self._q, self._limit, self._items = g, cols, q, limit, None
+
+    def _mat(self) -> List[Dict]:
+        if self._items is None:
+            c, q, L, g = self._cols, self._q, self._limit, self._g
+            rq, kq = c["rows"][q, :L].tolist(), c["kind"][q, :L].tolist()
+            sq, aq = c["sal"][q, :L].tolist(), c["acc"][q, :L].tolist()
+            pq, hq = c["sup"][q, :L].tolist(), c["shard"][q, :L].tolist()
+            ids, content, types, names = g.ids, g.content, g.types, g.shard_names
+            self._items = [{"id": ids[r], "content": content[r], "type": types[r], "salience": sq[j],
+                            "shard_key": names[hq[j]] if hq[j] >= 0 else "default", "access_count": aq[j],
+                            "is_super_node": bool(pq[j])}
+                           for j, r in enumerate(rq) if r >= 0 and kq[j] == 1]
+            self._g = self._cols = None  # materialised: drop the batch arrays
+        return self._items
+
+    def __len__(self) -> int:
+        return len(self._mat()) if self._items is not None or self._cols is None else \
+            int(((self._cols["rows"][self._q, :self._limit] >= 0) & (self._cols["kind"][self._q, :self._limit] == 1)).sum())
+
+    def __getitem__(self, i):
+        return self._mat()[i]
+
+    def __iter__(self):
+        return iter(self._mat())
+
+    def __eq__(self, other):
+        return isinstance(other, (_SeqABC, list, tuple)) and list(self._mat()) == list(other)
+
+    def __repr__(self) -> str:
+        return repr(self._mat())
+
+
 def _jsonable(v):
+    if isinstance(v, SearchHits):
+        return list(v)
     if hasattr(v, "id") and hasattr(v, "content") and hasattr(v, "salience"):
         return node_dict(v)
     if isinstance(v, (list, tuple)):
@@ -84,6 +136,8 @@ class DistributedMemoryService:
         self.max_resident = max_resident
         self.embedder = embedder
         self._moved: Dict[str, int] = {}  # migrate() overrides of the placement
+        self._own_memo: Dict[str, int] = {}
+        self._lazy: Dict[str, list] = defaultdict(list)  # user -> weakrefs of its unread SearchHits
         self.systems: "OrderedDict[str, object]" = OrderedDict()
         # columnar search routing (routing.py): the device table of resident
         # tenants, tenant names announced to each owner, key -> name
@@ -93,7 +147,17 @@ class DistributedMemoryService:
 
     # ------------------------------------------------------------ placement
     def owner(self, user: str) -> int:
-        """The CURRENT communicator rank that owns ``user``."""
+        """The CURRENT communicator rank that owns ``user`` (memoised: the
+        placement hash is computed once per tenant until the placement
+        changes -- reform / migrate clear the memo)."""
+        r = self._own_memo.get(user)
+        if r is None:
+            r = self._owner_of(user)
+            if len(self._own_memo) < (1 << 22):
+                self._own_memo[user] = r
+        return r
+
+    def _owner_of(self, user: str) -> int:
         if user in self._moved:
             return self._moved[user]
         if self._owner is not None:
@@ -111,14 +175,24 @@ class DistributedMemoryService:
         rank loses no committed state). Returns the released tenants."""
         self.comm, self.placement, self._owner = comm, placement, None
         self._moved = {}
+        self._own_memo = {}
         self._announced = defaultdict(set)  # owners changed: announce names again
         gone = [u for u in self.systems if not self.is_local(u)]
         for u in gone:
             self._release(u, self.systems.pop(u))
         return gone
 
+    def _settle(self, user: str) -> None:
+        """Materialise the outstanding columnar results of ``user`` (before
+        its rows can change)."""
+        for r in self._lazy.pop(user, ()):
+            h = r()
+            if h is not None:
+                h._mat()
+
     def _release(self, user: str, ms) -> None:
         """Persist and close a tenant this rank stops holding."""
+        self._settle(user)
         if self._table is not None:
             self._table.drop(user)
         ms._save_to_persistence()
@@ -169,6 +243,7 @@ class DistributedMemoryService:
         for user in sorted(moves):
             dst = int(moves[user])
             if user in self.systems and dst != me:
+                self._settle(user)
                 ms = self.systems.pop(user)
                 if self._table is not None:
                     self._table.drop(user)
@@ -185,6 +260,8 @@ class DistributedMemoryService:
         rc = comm.exchange_counts(torch.tensor(counts, dtype=torch.int64, device=dev)).cpu().tolist()
         recv = comm.all_to_all_v(flat, counts, rc) if comm.world > 1 else flat
         self._moved.update({u: int(r) for u, r in moves.items()})
+        for u in moves:
+            self._own_memo.pop(u, None)
         self._announced = defaultdict(set)
         received, off = [], 0
         for src in range(comm.world):
@@ -210,10 +287,16 @@ class DistributedMemoryService:
 
     # ------------------------------------------------------------ request routing
     def _exchange(self, outgoing: List[List]) -> List[List]:
-        """outgoing[r] = JSON-able items for rank r -> items received per rank."""
+        """outgoing[r] = JSON-able items for rank r -> items received per rank
+        (this rank's own items stay in process: no serialisation)."""
         if self.comm.world == 1:
             return outgoing
-        return [x if x is not None else [] for x in self.comm.exchange_objects(outgoing)]
+        me = self.comm.rank
+        send = list(outgoing)
+        mine, send[me] = send[me], []
+        got = [x if x is not None else [] for x in self.comm.exchange_objects(send)]
+        got[me] = mine
+        return got
 
     def serve(self, requests: Sequence[Tuple]) -> List:
         """SPMD: ``requests`` = [(user_id, method, args...)] received by this
@@ -274,6 +357,7 @@ class DistributedMemoryService:
                 if prev is not None and prev[3] is not None and prev[3][0] != "done" and \
                         any(p[2] == user for p in prev[2]):
                     prev[3] = ("done", self._search_finish(prev[3]))
+                self._settle(user)
                 replies[src].append([i, _jsonable(getattr(self.system(user), method)(*args))])
         handle = self._search_submit(pending) if pending else None
         return [len(requests), replies, list(pending), handle]
@@ -375,18 +459,20 @@ class DistributedMemoryService:
         try:
             ev.synchronize()
             with tracer.stage("mt_results", "cpu"):
-                # python lists, not numpy scalars: ~10k result dicts per batch
-                rl, kl, sl = host["rows"].tolist(), host["kind"].tolist(), host["sal"].tolist()
-                al, pl, hl = host["acc"].tolist(), host["sup"].tolist(), host["shard"].tolist()
-                out = []
+                cols = {n: t.numpy() for n, t in host.items()}
+                me = self.comm.rank
+                # columnar per request; a reply to another rank is materialised
+                # now (its graph stays here)
+                out = [SearchHits(qg[q], cols, q, p[4]) for q, p in enumerate(pending)]
+                lazy = self._lazy
                 for q, p in enumerate(pending):
-                    g = qg[q]
-                    ids, content, types, names = g.ids, g.content, g.types, g.shard_names
-                    rq, kq, sq, aq, pq, hq = rl[q], kl[q], sl[q], al[q], pl[q], hl[q]
-                    out.append([{"id": ids[r], "content": content[r], "type": types[r], "salience": sq[j],
-                                 "shard_key": names[hq[j]] if hq[j] >= 0 else "default", "access_count": aq[j],
-                                 "is_super_node": bool(pq[j])}
-                                for j, r in enumerate(rq[: p[4]]) if r >= 0 and kq[j] == 1])
+                    if p[0] != me:
+                        out[q] = list(out[q])
+                    else:
+                        lst = lazy[p[2]]
+                        if len(lst) >= 32:  # drop the refs of results already gone
+                            lst[:] = [w for w in lst if w() is not None]
+                        lst.append(weakref.ref(out[q]))
             return out
         finally:
             for lk in reversed(locks):

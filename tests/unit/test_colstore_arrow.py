@@ -146,3 +146,45 @@ def test_fragment_written_as_several_record_batches(tmp_path):
     env = dict(os.environ, LZK_COLSTORE_BATCH_VALUES="1000", PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+_PAR_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+from tests.unit.test_colstore_arrow import _cols
+from lazzaro_amd.store.colstore import NODE_SCHEMA, ColumnarTable
+t = ColumnarTable({path!r}, "nodes", NODE_SCHEMA)
+ids = [f"n{{i}}" for i in range(1000)]
+c = _cols(ids, seed=3)
+c2 = _cols([f"m{{i}}" for i in range(300)], user="v", seed=4)
+t.add_columns(c)           # 1000 rows -> 15 fragments of ~67 rows, written by parallel threads
+t.add_columns(c2)
+t.upsert_columns([("user_id", "u")], "id", ["n5", "n500", "n999"], _cols(["n5", "new"], seed=5))
+nfrag = len([f for f in t.fragment_files() if "_deletions" not in f])
+got = t.scan_columns([("user_id", "u")])
+pos = {{k: j for j, k in enumerate(got["id"])}}
+want = [i for i in ids if i not in ("n5", "n500", "n999")] + ["n5", "new"]
+assert got["id"] == want, got["id"][:5]
+ref = {{k: j for j, k in enumerate(ids)}}
+for k in want[:-2]:
+    assert np.array_equal(got["vector"][pos[k]], c["vector"][ref[k]])
+    assert got["content"][pos[k]] == c["content"][ref[k]]
+assert np.array_equal(got["vector"][pos["new"]], _cols(["n5", "new"], seed=5)["vector"][1])
+assert t.scan_columns([("user_id", "v")])["id"] == c2["id"]
+print("OK", nfrag)
+"""
+
+
+def test_parallel_fragment_commit_and_parallel_scan(tmp_path):
+    """Past LZK_COLSTORE_PAR_ROWS rows a commit is written as several
+    fragments by parallel threads (one version); the scan decodes many
+    fragments in parallel into presized columns -- row order, vectors,
+    strings, upserts and another tenant's rows all as before."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    code = _PAR_SCRIPT.format(root=root, path=str(tmp_path))
+    env = dict(os.environ, LZK_COLSTORE_PAR_ROWS="64")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.startswith("OK") and int(r.stdout.split()[1]) > 8
