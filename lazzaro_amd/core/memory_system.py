@@ -27,6 +27,7 @@ Constructor additions (all keyword, all optional): ``device``, ``metric``
 """
 from __future__ import annotations
 
+import gc
 import json
 import logging
 import math
@@ -989,6 +990,17 @@ STORAGE:
         if getattr(self, "_writer", None) is not None:
             self.flush_persistence()  # our own queued commits land before we read
         self._say(f"🔄 Loading state for user: {self.user_id}...")
+        # a 10M-row tenant creates tens of millions of objects: the cyclic GC
+        # would re-scan the heap many times over (none of them form cycles)
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            self._load_columns()
+        finally:
+            if gc_was:
+                gc.enable()
+
+    def _load_columns(self):
         with self._graph_lock:
             loader = getattr(self.store, "load_tenant", None)
             if loader is not None:
@@ -1021,6 +1033,7 @@ STORAGE:
                 self.node_counter = mx
             if self.query_cache:
                 self.query_cache.invalidate_results()
+            del ncols, ecols
         if n_rows:
             self._say(f"✓ Restored state ({self.graph.num_nodes()} nodes, {n_edges} edges)")
         else:

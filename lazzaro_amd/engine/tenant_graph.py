@@ -464,14 +464,26 @@ class TenantGraph:
                 has = torch.as_tensor(ok, dtype=torch.bool).to(dev)
                 for j, v in odd.items():
                     self.odd_emb[rl[j]] = v
-            e32 = e32 * has[:, None].to(e32.dtype)
-            self.emb32[rt] = e32
-            nrm2 = (e32.double() ** 2).sum(1)
+            # row chunks: a 10M-row load must not hold fp64 copies of the
+            # whole [m, D] block (the squares were 2 x 60 GB of temporaries)
+            contig = isinstance(rl, range)
+            nrm2 = torch.empty(m, dtype=torch.float64, device=dev)
+            ch = max(1, (1 << 28) // max(1, 8 * self.dim))  # ~256 MB of fp64 per chunk
+            for a in range(0, m, ch):
+                b = min(m, a + ch)
+                x = e32[a:b]
+                if info is not None:
+                    x = x * has[a:b, None].to(x.dtype)
+                r = slice(n0 + a, n0 + b) if contig else rt[a:b]
+                self.emb32[r] = x
+                x2 = x.double() ** 2
+                nrm2[a:b] = x2.sum(1)
+                self.sumsq += x2.sum(0)
+                del x2
+                if self.emb16 is not None:
+                    self.emb16[r, : self.dim] = x.to(torch.bfloat16)
+                self._write_fp8(rt[a:b], x)
             self.sqn[rt] = nrm2.float()
-            if self.emb16 is not None:
-                self.emb16[rt, : self.dim] = e32.to(torch.bfloat16)
-            self._write_fp8(rt, e32)
-            self.sumsq += (e32.double() ** 2).sum(0)
             self.n_sumsq += m
             self.has_emb[rt] = has.to(torch.uint8)
             if info is None or any(info[0]):
