@@ -244,24 +244,46 @@ PYBIND11_MODULE(_lzrt, m) {
            py::arg("eq"), py::arg("in_col"), py::arg("in_vals"), py::arg("cols"))
       .def("scan",
            [](Table& t, const std::vector<std::pair<std::string, std::string>>& eq, const std::string& in_col,
-              py::object in_vals, const std::vector<std::string>& want) {
+              py::object in_vals, const std::vector<std::string>& want, bool vec_pieces) {
              Predicate p = make_pred(eq, in_col, in_vals);
              std::vector<Column> cols;
+             std::vector<VecPiece> pieces;
              {
                py::gil_scoped_release r;
-               cols = t.scan(p, want);
+               cols = t.scan(p, want, vec_pieces ? &pieces : nullptr);
              }
              py::dict d;
              const auto& sch = t.schema();
+             bool vec_done = false;
              for (size_t i = 0; i < sch.size(); ++i) {
                bool w = want.empty();
                for (auto& n : want) if (n == sch[i].name) w = true;
-               if (w) d[sch[i].name.c_str()] = from_column(cols[i]);
+               if (!w) continue;
+               if (vec_pieces && !vec_done && sch[i].type == ColType::VecF32) {
+                 // list of [rows, dim] arrays in row order: views of the mapped
+                 // fragments (kept alive by the arrays) or gathered copies
+                 py::list l;
+                 for (auto& pc : pieces) {
+                   const py::ssize_t rows = (py::ssize_t)pc.rows, dim = (py::ssize_t)pc.dim;
+                   if (pc.keep) {
+                     auto* hold = new std::shared_ptr<void>(pc.keep);
+                     py::capsule cap(hold, [](void* q) { delete reinterpret_cast<std::shared_ptr<void>*>(q); });
+                     l.append(py::array_t<float>({rows, dim}, pc.data, cap));
+                   } else {
+                     l.append(adopt(std::move(pc.own), {rows, dim}));
+                   }
+                 }
+                 d[sch[i].name.c_str()] = l;
+                 vec_done = true;
+                 continue;
+               }
+               d[sch[i].name.c_str()] = from_column(cols[i]);
              }
              return d;
            },
            py::arg("eq") = std::vector<std::pair<std::string, std::string>>{}, py::arg("in_col") = "",
-           py::arg("in_vals") = py::none(), py::arg("want") = std::vector<std::string>{});
+           py::arg("in_vals") = py::none(), py::arg("want") = std::vector<std::string>{},
+           py::arg("vec_pieces") = false);
 
   // ---- tokenizer ----
   py::class_<Tokenizer>(m, "Tokenizer")
@@ -310,6 +332,13 @@ PYBIND11_MODULE(_lzrt, m) {
                                 py::array_t<int32_t>(adj.size(), adj.data()),
                                 py::array_t<int32_t>(eid.size(), eid.data()));
         });
+  m.def("par_copy",
+        [](uintptr_t dst, uintptr_t src, size_t bytes) {
+          // multi-threaded host memcpy with the GIL released (staging copies)
+          py::gil_scoped_release r;
+          lzrt::parallel_copy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes);
+        },
+        py::arg("dst"), py::arg("src"), py::arg("bytes"));
   m.def("max_node_num",
         [](py::list ids) {
           // largest n of "node_<n>" ids (the reference's id scheme), 0 if none

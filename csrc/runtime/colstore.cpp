@@ -339,6 +339,23 @@ void par_for(size_t n, size_t max_threads, F&& fn) {
 
 }  // namespace
 
+// Staging copies (pinned destination, mapped-file source): split over up to 16
+// threads at >= 4 MiB each, no madvise of the destination (pinned pages).
+void parallel_copy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kMin = size_t(4) << 20;
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t nt = std::min<size_t>(hw, std::max<size_t>(1, bytes / kMin));
+  if (nt <= 1) { std::memcpy(dst, src, bytes); return; }
+  std::vector<std::thread> ts;
+  const size_t per = ((bytes + nt - 1) / nt + 63) & ~size_t(63);
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t o = t * per;
+    if (o >= bytes) break;
+    ts.emplace_back([=] { std::memcpy((char*)dst + o, (const char*)src + o, std::min(per, bytes - o)); });
+  }
+  for (auto& th : ts) th.join();
+}
+
 size_t Column::size() const {
   switch (type) {
     case ColType::Str: return s.size();
@@ -859,7 +876,8 @@ uint64_t Table::replace_where(const Predicate& p, const std::vector<Column>& col
 // range -- in parallel over fragments when there are several (a parallel
 // commit leaves ~10 per 10M-row tenant), else with a multi-threaded copy of
 // the vector column. No fragment is materialised and then copied again.
-std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::string>& want_names) {
+std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::string>& want_names,
+                                std::vector<VecPiece>* vec_pieces) {
   lock();  // a consistent fragment list (writers append under the same lock)
   std::vector<Frag> frags;
   try {
@@ -933,6 +951,11 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
   std::vector<uint64_t> off(F + 1, 0);
   for (size_t i = 0; i < F; ++i) off[i + 1] = off[i] + (fr[i].all ? fr[i].n : fr[i].sel.size());
   const uint64_t total = off[F];
+  // with vec_pieces the (first) vector column is returned as pieces, not copied
+  int vcol = -1;
+  if (vec_pieces)
+    for (int c : want)
+      if (out[c].type == ColType::VecF32) { vcol = c; break; }
   for (int c : want) {
     Column& o = out[c];
     if (o.type == ColType::VecF32 && o.dim == 0)
@@ -948,18 +971,64 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
       case ColType::I32: o.i32.resize(total); break;
       case ColType::I64: o.i64.resize(total); break;
       case ColType::Bool: o.b.resize(total); break;
-      case ColType::VecF32: o.f32.resize(total * (size_t)o.dim); break;
+      case ColType::VecF32: if (c != vcol) o.f32.resize(total * (size_t)o.dim); break;
     }
   }
+  // vector pieces, in row order: one per batch of a fully selected fragment
+  // (a view of the mapping), one gathered run per partly selected fragment
+  std::vector<std::vector<VecPiece>> fpieces(vcol >= 0 ? F : 0);
+  const uint32_t vdim = vcol >= 0 ? out[vcol].dim : 0;
   par_for(F, fthreads, [&](size_t i) {
     FR& f = fr[i];
     if (off[i + 1] == off[i]) return;
     if (f.all) {
       for (size_t bi = 0; bi < f.batches.size(); ++bi) {
         const uint64_t m = (uint64_t)f.batches[bi]->num_rows();
-        for (int c : want) from_arrow_at(f.batches[bi]->GetColumnByName(schema_[c].name), out[c], off[i] + f.base[bi], m);
+        for (int c : want) {
+          if (c == vcol) {
+            auto a = f.batches[bi]->GetColumnByName(schema_[c].name);
+            VecPiece pc;
+            pc.rows = m;
+            pc.dim = vdim;
+            if (a) {
+              auto l = std::static_pointer_cast<arrow::FixedSizeListArray>(a);
+              if ((uint32_t)l->list_type()->list_size() != vdim) throw std::runtime_error("colstore: vector dim mismatch in scan");
+              auto v = std::static_pointer_cast<arrow::FloatArray>(l->values());
+              pc.data = v->raw_values() + l->value_offset(0);
+              pc.keep = f.batches[bi];
+            } else {
+              pc.own.assign((size_t)m * vdim, 0.f);
+              pc.data = pc.own.data();
+            }
+            fpieces[i].push_back(std::move(pc));
+            continue;
+          }
+          from_arrow_at(f.batches[bi]->GetColumnByName(schema_[c].name), out[c], off[i] + f.base[bi], m);
+        }
       }
       return;
+    }
+    if (vcol >= 0) {
+      VecPiece pc;
+      pc.rows = f.sel.size();
+      pc.dim = vdim;
+      pc.own.resize(pc.rows * (size_t)vdim);
+      Column tmp;
+      tmp.type = ColType::VecF32;
+      tmp.dim = vdim;
+      size_t b2 = 0;
+      std::shared_ptr<arrow::Array> va = f.batches[0]->GetColumnByName(schema_[vcol].name);
+      for (size_t j = 0; j < f.sel.size(); ++j) {
+        const uint64_t R = f.sel[j];
+        while (b2 + 1 < f.batches.size() && R >= f.base[b2 + 1]) va = f.batches[++b2]->GetColumnByName(schema_[vcol].name);
+        if (!va) { std::fill(pc.own.begin() + j * vdim, pc.own.begin() + (j + 1) * vdim, 0.f); continue; }
+        auto l = std::static_pointer_cast<arrow::FixedSizeListArray>(va);
+        auto v = std::static_pointer_cast<arrow::FloatArray>(l->values());
+        std::memcpy(pc.own.data() + j * vdim, v->raw_values() + l->value_offset((int64_t)(R - f.base[b2])),
+                    vdim * sizeof(float));
+      }
+      pc.data = pc.own.data();
+      fpieces[i].push_back(std::move(pc));
     }
     size_t bi = 0;
     std::vector<std::shared_ptr<arrow::Array>> arrs(schema_.size());
@@ -968,9 +1037,13 @@ std::vector<Column> Table::scan(const Predicate& p, const std::vector<std::strin
     for (size_t j = 0; j < f.sel.size(); ++j) {
       const uint64_t R = f.sel[j];
       while (bi + 1 < f.batches.size() && R >= f.base[bi + 1]) load(++bi);
-      for (int c : want) row_from_arrow(arrs[c], out[c], R - f.base[bi], off[i] + j);
+      for (int c : want)
+        if (c != vcol) row_from_arrow(arrs[c], out[c], R - f.base[bi], off[i] + j);
     }
   });
+  if (vcol >= 0)
+    for (auto& v : fpieces)
+      for (auto& pc : v) vec_pieces->push_back(std::move(pc));
   return out;
 }
 

@@ -77,6 +77,20 @@ struct Column {
   void append_from(const Column& o, size_t row);
 };
 
+// One contiguous run of rows of a vector column returned by a scan without
+// copying: a view into a memory-mapped fragment (`keep` holds the mapping),
+// or rows gathered out of a partly selected fragment (`own`).
+struct VecPiece {
+  std::shared_ptr<void> keep;
+  const float* data = nullptr;
+  uint64_t rows = 0;
+  uint32_t dim = 0;
+  FloatVec own;
+};
+
+// memcpy split over threads (huge pages for large destinations)
+void parallel_copy(void* dst, const void* src, size_t bytes);
+
 struct Predicate {
   // conjunction of equalities on string columns + optional IN on one string column
   std::vector<std::pair<std::string, std::string>> eq;
@@ -94,7 +108,8 @@ class Table {
   uint64_t delete_where(const Predicate& p, uint64_t* n_deleted);
   // atomic delete_where(p) + append(cols) in one version
   uint64_t replace_where(const Predicate& p, const std::vector<Column>& cols, uint64_t* n_deleted);
-  std::vector<Column> scan(const Predicate& p, const std::vector<std::string>& want);
+  std::vector<Column> scan(const Predicate& p, const std::vector<std::string>& want,
+                           std::vector<VecPiece>* vec_pieces = nullptr);
   uint64_t count_rows();
   // two-phase multi-writer commit: stage() writes a fragment only,
   // commit_staged() publishes any number of staged fragments in ONE version

@@ -1396,7 +1396,15 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
     V = nc["vector"]
     has = nc.get("_has")
     emb = None
-    if torch.is_tensor(V):  # already a tensor (a migrated tenant's device rows)
+    if isinstance(V, list):  # pieces of the mapped store fragments, in row order
+        D = next((int(x.shape[1]) for x in V if x.shape[1]), 0)
+        if D:
+            if g.on_gpu:
+                emb = _h2d_pieces(V, N, D, g.device)
+            else:
+                emb = torch.from_numpy(np.concatenate([np.asarray(x, dtype=np.float32) for x in V])
+                                       if len(V) > 1 else np.array(V[0], dtype=np.float32))
+    elif torch.is_tensor(V):  # already a tensor (a migrated tenant's device rows)
         emb = V.to(g.device, torch.float32) if V.shape[1] else None
     elif V.shape[1]:
         emb = _h2d(np.ascontiguousarray(V, dtype=np.float32), g.device) if g.on_gpu else torch.from_numpy(
@@ -1464,6 +1472,39 @@ def _max_node_num(ids) -> int:
         if m:
             mx = max(mx, int(m.group(1)))
     return mx
+
+
+def _h2d_pieces(pieces, n: int, d: int, dev, chunk_bytes: int = 256 << 20) -> torch.Tensor:
+    """[n, d] fp32 device tensor from row-ordered host pieces (views of the
+    store's mapped fragments): each 256 MB chunk is copied by the runtime's
+    multi-threaded memcpy (GIL released) into one of two pinned staging
+    buffers while the previous one's async copy to the device runs."""
+    from ..store.colstore import _rt
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    per_rows = max(1, chunk_bytes // (4 * d))
+    bufs = [torch.empty((per_rows, d), dtype=torch.float32).pin_memory() for _ in range(2)]
+    evs = [None, None]
+    st = torch.cuda.current_stream(dev)
+    rt = _rt()
+    r0, j = 0, 0
+    for p in pieces:
+        p = np.ascontiguousarray(p, dtype=np.float32)
+        m = p.shape[0]
+        for a in range(0, m, per_rows):
+            b = min(m, a + per_rows)
+            k = j & 1
+            if evs[k] is not None:
+                evs[k].synchronize()
+            rt.par_copy(bufs[k].data_ptr(), p[a:b].ctypes.data, (b - a) * d * 4)
+            out[r0 + a: r0 + b].copy_(bufs[k][: b - a], non_blocking=True)
+            evs[k] = torch.cuda.Event()
+            evs[k].record(st)
+            j += 1
+        r0 += m
+    if r0 != n:
+        raise RuntimeError(f"vector pieces hold {r0} rows, expected {n}")
+    st.synchronize()
+    return out
 
 
 def _h2d(a: np.ndarray, dev, chunk_bytes: int = 64 << 20) -> torch.Tensor:

@@ -134,11 +134,17 @@ class HBMStore:
         # the columns the graph loader reads (not user_id / metadata: at 10M
         # rows every string column costs seconds of Python objects)
         want = [c for c, _, _ in self._nodes_table.schema if c not in ("user_id", "metadata")]
-        nc = self._nodes_table.scan_columns([("user_id", user_id)], want=want)
+        # the vector column as zero-copy pieces of the mapped fragments: the
+        # loader streams them to the device (no 30 GB host copy to allocate,
+        # fill and free for a 10M x 768 tenant)
+        nc = self._nodes_table.scan_columns([("user_id", user_id)], want=want, vec_pieces=True)
         if not nc or not len(nc.get("id", [])):
             return {"id": []}, {"id": []}
-        if nc["vector"].ndim == 2 and nc["vector"].shape[1]:
-            self._dim = self._dim or nc["vector"].shape[1]
+        v = nc["vector"]
+        d = next((int(x.shape[1]) for x in v if x.shape[1]), 0) if isinstance(v, list) else \
+            (int(v.shape[1]) if v.ndim == 2 else 0)
+        if d:
+            self._dim = self._dim or d
         ec = self._edges_table.scan_columns([("user_id", user_id)])
         return nc, (ec if ec else {"id": []})
 

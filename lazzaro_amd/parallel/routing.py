@@ -179,14 +179,19 @@ def local_search(svc, users: Sequence[str], Q: torch.Tensor, limits: Sequence[in
         for u in per:
             ms = systems[u]
             g = ms.graph
-            idx = torch.as_tensor(groups[u], dtype=torch.long, device=dev)
             if g.dim != D or g.n == 0:
                 continue
-            s, r = g.store_search(Q[idx], k, getattr(ms.store, "metric", "l2"))
+            whole = len(groups[u]) == n  # one tenant takes the whole batch: no gather / scatter
+            idx = None if whole else torch.as_tensor(groups[u], dtype=torch.long).to(dev, non_blocking=True)
+            s, r = g.store_search(Q if whole else Q[idx], k, getattr(ms.store, "metric", "l2"))
             with g.on_stream():
                 bad = (r < 0) | (g.kind[r.clamp_min(0)] != NODE)
-            S[idx] = torch.where(bad, torch.full_like(s, float("-inf")), s.float())
-            R[idx] = torch.where(bad, torch.full_like(r, -1), r)
+            s = torch.where(bad, torch.full_like(s, float("-inf")), s.float())
+            r = torch.where(bad, torch.full_like(r, -1), r)
+            if whole:
+                S, R = s, r
+            else:
+                S[idx], R[idx] = s, r
         if fused:
             from ..ops.search import segment_topk_ptrs
             from ..ops.tenant_ops import gather_fields
@@ -206,9 +211,9 @@ def local_search(svc, users: Sequence[str], Q: torch.Tensor, limits: Sequence[in
             S[qt] = torch.where(bad, torch.full_like(s, float("-inf")), s)
             R[qt] = torch.where(bad, torch.full_like(r, -1), r)
         # a query's results past its own limit are dropped
-        lim = torch.as_tensor(list(limits), dtype=torch.long, device=dev)
-        cut = torch.arange(k, device=dev)[None, :] >= lim[:, None]
-        if bool(cut.any()):
+        if min(limits) < k:  # decided on the host: no device sync on the serving path
+            lim = torch.as_tensor(list(limits), dtype=torch.long).to(dev, non_blocking=True)
+            cut = torch.arange(k, device=dev)[None, :] >= lim[:, None]
             S = torch.where(cut, torch.full_like(S, float("-inf")), S)
             R = torch.where(cut, torch.full_like(R, -1), R)
         # valid hits first, in score order (a filtered row leaves a hole)

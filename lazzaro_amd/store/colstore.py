@@ -150,8 +150,14 @@ class ColumnarTable:
         return int(n), int(v)
 
     def scan_columns(self, eq: Sequence[Tuple[str, str]] = (), in_col: str = "", in_vals=None,
-                     want: Optional[Sequence[str]] = None) -> Dict:
-        return self._t.scan(list(eq), in_col, None if in_vals is None else list(in_vals), list(want or []))
+                     want: Optional[Sequence[str]] = None, vec_pieces: bool = False) -> Dict:
+        """Matching rows' columns. ``vec_pieces``: the vector column comes back
+        as a list of [rows, dim] float32 arrays in row order -- zero-copy
+        views of the memory-mapped fragments where a fragment is wholly
+        selected -- instead of one array copied out of them (a tenant load
+        streams those pieces to the device)."""
+        return self._t.scan(list(eq), in_col, None if in_vals is None else list(in_vals), list(want or []),
+                            bool(vec_pieces))
 
     def scan(self, eq: Sequence[Tuple[str, str]] = (), in_col: str = "", in_vals=None,
              want: Optional[Sequence[str]] = None) -> List[Dict]:
