@@ -292,23 +292,24 @@ __global__ __launch_bounds__(DNT) void dg_direct_kernel(const int* __restrict__ 
   }
 }
 
-// One selection round over the class-2 components: cur[L] = smallest
-// candidate row of L above prev[L] (prev == nullptr: round 0).
+// One selection round over the class-2 components, rows [lo, hi): cur[L] =
+// smallest candidate row of L in the range above last[L] (the last row
+// selected for L, -1 before the first).
 __global__ __launch_bounds__(DNT) void dg_round_kernel(const int* __restrict__ lab,
                                                        const unsigned char* __restrict__ touched,
                                                        const unsigned char* __restrict__ kind,
-                                                       const unsigned char* __restrict__ sup, long n,
+                                                       const unsigned char* __restrict__ sup, long lo, long hi,
                                                        const unsigned char* __restrict__ cls,
-                                                       const int* __restrict__ prev, int* __restrict__ cur) {
+                                                       const int* __restrict__ last, int* __restrict__ cur) {
   const int lane = threadIdx.x & 63;
   const long stride = (long)gridDim.x * DNT;
-  for (long base = (long)blockIdx.x * DNT; base < n; base += stride) {
+  for (long base = lo + (long)blockIdx.x * DNT; base < hi; base += stride) {
     const long r = base + threadIdx.x;
     int L = -1;
     bool act = false;
-    if (is_cand(r, n, touched, kind, sup)) {
+    if (is_cand(r, hi, touched, kind, sup)) {
       L = lab[r];
-      act = cls[L] == 2 && (prev == nullptr || (int)r > prev[L]);
+      act = cls[L] == 2 && (int)r > last[L];
     }
     while (true) {  // one pass per distinct eligible label in the wave
       const unsigned long long m = __ballot(act);
@@ -324,23 +325,38 @@ __global__ __launch_bounds__(DNT) void dg_round_kernel(const int* __restrict__ l
   }
 }
 
-// After round k: append each class-2 component's selected row (if any) and
-// reset the other buffer (round k's prev, round k+1's cur) for those labels.
-__global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__ biglist, int nbig,
-                                                         const int* __restrict__ cur, int* __restrict__ reset,
+// After a round: append each class-2 component's selected row (if any),
+// advance last[L], count it, retire the component (class 3) once it has
+// `take` rows, reset cur[L]; remaining[0] += components still open.
+__global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__ biglist, int nbig, int take,
+                                                         int* __restrict__ cur, int* __restrict__ last,
+                                                         int* __restrict__ cnt, unsigned char* __restrict__ cls,
                                                          const long long* __restrict__ gfirst,
                                                          long long* __restrict__ out_key, int* __restrict__ out_row,
-                                                         int cap, int* __restrict__ count) {
+                                                         int cap, int* __restrict__ count,
+                                                         int* __restrict__ remaining) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * DNT + threadIdx.x;
   int L = -1, v = NOROW;
+  bool open = false;
   if (i < nbig) {
     L = biglist[i];
-    v = cur[L];
-    reset[L] = NOROW;
+    if (cls[L] == 2) {
+      v = cur[L];
+      cur[L] = NOROW;
+      open = true;
+      if (v != NOROW) {
+        last[L] = v;
+        const int c = cnt[L] + 1;
+        cnt[L] = c;
+        if (c >= take) { cls[L] = 3; open = false; }
+      }
+    }
   }
   const bool sel = v != NOROW;
   const unsigned long long m = __ballot(sel);
+  const unsigned long long o = __ballot(open);
+  if (lane == 0 && o) atomicAdd(remaining, __popcll(o));
   if (m == 0) return;
   int b0 = 0;
   if (lane == 0) b0 = atomicAdd(count, __popcll(m));
@@ -383,25 +399,40 @@ LZK_EXPORT int lzk_dg_stats(const int* src, const int* dst, const float* w, long
 
 // Selection phase: (order key, row) of every selected row, unordered, in
 // out_key/out_row[0 : *count]; cap = counters[0] + take * counters[1].
-// buf0/buf1: int[n] filled with 0x7fffffff.
+// cur: int[n] filled with 0x7fffffff; last: int[n] filled with -1; cnt:
+// int[n] zeroed (only class-2 labels' entries are used). cls is updated
+// (class-2 components retire to class 3). First `take` rounds over a prefix
+// window of the rows -- a large component's first candidates are nearly
+// always there -- then, only for components still open (one synchronising
+// read of `remaining`), `take` rounds over the rest.
 LZK_EXPORT int lzk_dg_select(const int* lab, long n, const unsigned char* touched, const unsigned char* kind,
-                             const unsigned char* sup, const unsigned char* cls, const long long* gfirst,
-                             const int* biglist, int nbig, int take, int* buf0, int* buf1, long long* out_key,
-                             int* out_row, int cap, int* count, void* stream) {
+                             const unsigned char* sup, unsigned char* cls, const long long* gfirst,
+                             const int* biglist, int nbig, int take, int* cur, int* last, int* cnt,
+                             long long* out_key, int* out_row, int cap, int* count, int* remaining, long window,
+                             void* stream) {
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(dg_direct_kernel, dim3(grid_for(n)), dim3(DNT), 0, st, lab, touched, kind, sup, n, cls, gfirst,
                      out_key, out_row, cap, count);
-  int* bufs[2] = {buf0, buf1};
-  for (int k = 0; nbig > 0 && k < take; ++k) {
-    int* cur = bufs[k & 1];
-    int* prv = k ? bufs[(k - 1) & 1] : nullptr;
-    hipLaunchKernelGGL(dg_round_kernel, dim3(grid_for(n)), dim3(DNT), 0, st, lab, touched, kind, sup, n, cls, prv,
-                       cur);
-    // round 0 has no prev to reset: clear the buffer round 1 writes (already
-    // filled by the caller) -- harmless; later rounds reset round k's prev
-    hipLaunchKernelGGL(dg_collect_kernel, dim3((unsigned)((nbig + DNT - 1) / DNT)), dim3(DNT), 0, st, biglist, nbig,
-                       cur, bufs[(k + 1) & 1], gfirst, out_key, out_row, cap, count);
+  if (nbig <= 0) return (int)hipGetLastError();
+  const long w = window > 0 && window < n ? window : n;
+  const unsigned cb = (unsigned)((nbig + DNT - 1) / DNT);
+  for (int k = 0; k < take; ++k) {
+    hipLaunchKernelGGL(dg_round_kernel, dim3(grid_for(w)), dim3(DNT), 0, st, lab, touched, kind, sup, 0L, w, cls,
+                       last, cur);
+    (void)hipMemsetAsync(remaining, 0, sizeof(int), st);
+    hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, take, cur, last, cnt, cls,
+                       gfirst, out_key, out_row, cap, count, remaining);
+  }
+  if (w >= n) return (int)hipGetLastError();
+  int open = 0;
+  if (hipMemcpyAsync(&open, remaining, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return (int)hipGetLastError();
+  if (hipStreamSynchronize(st) != hipSuccess) return (int)hipGetLastError();
+  for (int k = 0; k < take && open > 0; ++k) {
+    hipLaunchKernelGGL(dg_round_kernel, dim3(grid_for(n - w)), dim3(DNT), 0, st, lab, touched, kind, sup, w, n, cls,
+                       last, cur);
+    hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, take, cur, last, cnt, cls,
+                       gfirst, out_key, out_row, cap, count, remaining);
   }
   return (int)hipGetLastError();
 }

@@ -647,8 +647,13 @@ class TenantGraph:
 
     def first_node_rows_dev(self, k: int, super_: Optional[bool] = None) -> torch.Tensor:
         """The first ``k`` rows of :meth:`ordered_node_rows_dev` by one top-k
-        pass (no sort of the tenant's rows)."""
+        pass (no sort of the tenant's rows). Shard nodes only (``super_`` is
+        False) on a large tenant: shards in code order from the host counts,
+        rows found in growing windows from row 0 -- the answer is almost
+        always in the first window (no pass over the whole tenant)."""
         n = self.n
+        if super_ is False and n > self.FIRST_ROWS_WINDOW and k > 0:
+            return self._first_shard_rows(k)
         with self.on_stream():
             m = self.kind[:n] == NODE
             if super_ is not None:
@@ -661,6 +666,31 @@ class TenantGraph:
                 return torch.zeros(0, dtype=torch.long, device=self.device)
             v, i = torch.topk(key, kk, largest=False, sorted=True)
             return i
+
+    FIRST_ROWS_WINDOW = 1 << 16
+
+    def _first_shard_rows(self, k: int) -> torch.Tensor:
+        n = self.n
+        out = []
+        need = k
+        with self.on_stream():
+            for c, cnt in enumerate(self.shard_count):
+                if cnt <= 0 or need == 0:
+                    continue
+                got, lo, w = 0, 0, self.FIRST_ROWS_WINDOW
+                while lo < n and need > 0 and got < cnt:
+                    hi = min(n, lo + w)
+                    m = (self.kind[lo:hi] == NODE) & (self.sup[lo:hi] == 0) & (self.shard[lo:hi] == c)
+                    idx = torch.nonzero(m).flatten()[:need]
+                    t = int(idx.numel())
+                    if t:
+                        out.append(idx + lo)
+                        need -= t
+                        got += t
+                    lo, w = hi, w * 4
+            if not out:
+                return torch.zeros(0, dtype=torch.long, device=self.device)
+            return torch.cat(out)
 
     def set_scalar(self, r: int, name: str, value) -> None:
         col = getattr(self, name)
@@ -884,6 +914,10 @@ class TenantGraph:
         + optional prune, in one kernel pass. Returns the number of pruned
         edges."""
         if steps <= 0:
+            return 0
+        if prune_threshold is not None and prune_threshold <= 0.0:
+            prune_threshold = None  # weights never go below 0: nothing to prune, no flag / compaction pass
+        if rate == 0.0 and prune_threshold is None:
             return 0
         with self.on_stream():
             self.e, n, dropped = T.decay_prune(self.e, self.sal[: self.n], self.kind[: self.n], self.sup[: self.n],

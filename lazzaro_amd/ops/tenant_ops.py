@@ -31,7 +31,7 @@ _lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P,
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, P, P, P, P, P, P, P])
-_lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, I, P, P, P, P, I, P, P])
+_lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, I, P, P, P, P, P, I, P, P, L, P])
 
 SALIENCE_FLOOR = 0.2
 EDGE_COLS = ("src", "dst", "w", "co", "lu", "meta")
@@ -99,11 +99,19 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
                                        1 if (decay_nodes and nn) else 0, int(steps), _st(e["w"])), "tg_decay")
     if threshold is None or ne == 0:
         return e, 0, dropped
-    if want_dropped:
-        f = flag[:ne] == 0
-        dropped = (e["src"][f], e["dst"][f], e["meta"][f])
     out, n = _compact(e, flag, bc, ne)
+    if want_dropped:  # only when something went (one nonzero, three gathers)
+        dropped = _dropped(e, flag, ne, n)
     return out, n, dropped
+
+
+def _dropped(e: Dict[str, torch.Tensor], flag: torch.Tensor, ne: int, n: int):
+    """(src, dst, meta) of the edges whose keep flag is 0 (``n`` of them)."""
+    if n == 0:
+        z = e["src"][:0]
+        return z, e["dst"][:0], e["meta"][:0]
+    idx = torch.nonzero(flag[:ne] == 0).flatten()
+    return e["src"][idx], e["dst"][idx], e["meta"][idx]
 
 
 def remove_edges_of(e: Dict[str, torch.Tensor], rm: torch.Tensor, shard: torch.Tensor, want_dropped: bool = False):
@@ -130,11 +138,8 @@ def remove_edges_of(e: Dict[str, torch.Tensor], rm: torch.Tensor, shard: torch.T
     _lib.check(_lib.lib().lzk_tg_flag_remove(e["src"].data_ptr(), e["dst"].data_ptr(), e["meta"].data_ptr(), ne,
                                              rm.data_ptr(), shard.data_ptr(), flag.data_ptr(), bc.data_ptr(),
                                              _st(flag)), "tg_flag_remove")
-    dropped = None
-    if want_dropped:
-        f = flag == 0
-        dropped = (e["src"][f], e["dst"][f], e["meta"][f])
     out, n = _compact(e, flag, bc, ne)
+    dropped = _dropped(e, flag, ne, n) if want_dropped else None
     return out, n, dropped
 
 
@@ -288,6 +293,9 @@ def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: floa
     return int(bad.item()) == 0
 
 
+DIGEST_WINDOW = 1 << 16  # rows of the first selection pass (component_digest)
+
+
 def component_digest(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind: torch.Tensor, sup: torch.Tensor,
                      shard: torch.Tensor, n: int, min_size: int, min_avg_w: float,
                      take: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -323,11 +331,18 @@ def component_digest(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind
     rows = torch.empty(cap, dtype=torch.int32, device=dev)
     if cap == 0:
         return keys, rows.long()
-    bufs = torch.full((2, n), 0x7FFFFFFF, dtype=torch.int32, device=dev) if nbig else torch.empty((2, 1), dtype=torch.int32, device=dev)
+    if nbig:
+        cur = torch.full((n,), 0x7FFFFFFF, dtype=torch.int32, device=dev)
+        last = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    else:
+        cur = last = cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    rem = torch.zeros(1, dtype=torch.int32, device=dev)
     _lib.check(L_.lzk_dg_select(lab.data_ptr(), n, touched.data_ptr(), kind.data_ptr(), sup.data_ptr(),
                                 cls.data_ptr(), gfirst.data_ptr(), biglist.data_ptr(), nbig, int(take),
-                                bufs[0].data_ptr(), bufs[1].data_ptr(), keys.data_ptr(), rows.data_ptr(), cap,
-                                counters[3:].data_ptr(), _st(src)), "dg_select")
+                                cur.data_ptr(), last.data_ptr(), cnt.data_ptr(), keys.data_ptr(), rows.data_ptr(),
+                                cap, counters[3:].data_ptr(), rem.data_ptr(), int(DIGEST_WINDOW), _st(src)),
+               "dg_select")
     m = int(counters[3].item())
     if m > cap:
         raise RuntimeError(f"component digest overflow: {m} selected rows for capacity {cap}")

@@ -43,9 +43,14 @@ def _graph(n, ne_giant, n_small, seed):
     return g
 
 
+@pytest.mark.parametrize("window", [1 << 16, 128])
 @pytest.mark.parametrize("n,ne,n_small,seed", [(20000, 30000, 500, 1), (300000, 500000, 6000, 2),
                                                 (50000, 0, 3000, 3)])
-def test_digest_kernels_match_sorted(n, ne, n_small, seed):
+def test_digest_kernels_match_sorted(n, ne, n_small, seed, window, monkeypatch):
+    """window: rows of the first selection pass (128: every large component
+    continues into the second pass)."""
+    from lazzaro_amd.ops import tenant_ops
+    monkeypatch.setattr(tenant_ops, "DIGEST_WINDOW", window)
     g = _graph(n, ne, n_small, seed)
     for take in (10, 3):
         got = [r.tolist() for r in g.component_digest(3, 0.3, take)]

@@ -592,3 +592,29 @@ def test_write_behind_persistence_equals_sync(tmp_path, fail):
         assert a[0][k][0] == b[0][k][0] and abs(a[0][k][1] - b[0][k][1]) < 1e-6, k
     assert a[1] == b[1]
     assert nfail == (1 if fail else 0)
+
+
+def test_first_shard_rows_fast_path_matches_topk(monkeypatch):
+    """first_node_rows_dev(super_=False) on a large tenant walks the shards in
+    code order through growing row windows (host shard counts); it must equal
+    the one-pass top-k over every row, after removals and with super-nodes."""
+    import torch
+
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    rng = np.random.default_rng(7)
+    g = TenantGraph(device="cpu", dim=4)
+    codes = [g.shard_id(f"s{i}") for i in range(5)]
+    n = 3000
+    sh = rng.choice([codes[1], codes[3], codes[4]], n, p=[0.01, 0.5, 0.49]).tolist()
+    g.add_nodes([f"node_{i}" for i in range(n)], [f"c{i}" for i in range(n)],
+                rng.standard_normal((n, 4)).astype(np.float32).tolist(), shard=sh,
+                sup=(rng.random(n) < 0.05).astype(np.int64).tolist())
+    g.remove_nodes(rng.choice(n, 400, replace=False).tolist())
+    monkeypatch.setattr(TenantGraph, "FIRST_ROWS_WINDOW", 64)
+    for k in (1, 10, 40):
+        fast = g._first_shard_rows(k).tolist()
+        monkeypatch.setattr(TenantGraph, "FIRST_ROWS_WINDOW", 1 << 30)
+        ref = g.first_node_rows_dev(k, super_=False).tolist()
+        monkeypatch.setattr(TenantGraph, "FIRST_ROWS_WINDOW", 64)
+        assert fast == ref and len(ref) == k
+        assert g.first_node_rows_dev(k, super_=False).tolist() == ref
