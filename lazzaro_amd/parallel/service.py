@@ -198,6 +198,16 @@ class DistributedMemoryService:
         ms._save_to_persistence()
         ms.close()
 
+    def warm_table(self) -> int:
+        """Register every resident GPU tenant in the device pointer table (as
+        an index is built at load): the fused search then refreshes only
+        tenants whose columns moved since. Returns the tenants registered."""
+        gpu = [u for u, ms in self.systems.items() if ms.graph.on_gpu and ms.graph.dim is not None]
+        if not gpu:
+            return 0
+        self.tenant_table(self.systems[gpu[0]].graph.device).slots(gpu, self.systems)
+        return len(gpu)
+
     def tenant_table(self, device=None) -> "routing.TenantTable":
         """The device table of resident tenants' column pointers, on the
         tenants' device (NOT necessarily the communicator's: a CPU/gloo
@@ -391,11 +401,12 @@ class DistributedMemoryService:
         users = [p[2] for p in pending]
         systems = {u: self.system(u) for u in dict.fromkeys(users)}
         first = next(iter(systems.values()))
+        emb0 = first.embedder
         fused = (len(systems) >= self.FUSED_MIN_TENANTS and first.graph.on_gpu
                  and first.graph.dim is not None and first.graph.dim % 32 == 0
-                 and all(ms.embedder is first.embedder and ms._store_binds_graph()
-                         and getattr(ms.store, "metric", "l2") == "l2" for ms in systems.values())
-                 and max(p[4] for p in pending) <= 16)
+                 and max(p[4] for p in pending) <= 16
+                 and all(ms.embedder is emb0 and getattr(ms.store, "metric", "l2") == "l2"
+                         and ms._store_binds_graph() for ms in systems.values()))
         if not fused:
             out, j = [], 0
             while j < len(pending):  # consecutive same-tenant, same-limit runs batch
