@@ -52,7 +52,10 @@ Multi-GPU work inside the JSON line (all timed, every rank, RCCL over xGMI):
   back to their origin, merge -- SURVEY §2.5 C1 + K2).
 * ``consolidate_sharded``: config 4 as ONE buffer row-sharded over the ranks
   (``ShardedMemorySystem.consolidate_batch``: facts all-gathered, top-3 lists
-  merged, global eviction, distributed components and k-means).
+  merged, global eviction, distributed components and k-means) on
+  topic-clustered rows with cluster placement; ``scan_facts_x_rows_per_rank_step``
+  is the measured per-rank scan work after the exact cone pruning (the
+  unpruned figure alongside).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no
 torchrun environment the script launches N ranks itself through
@@ -423,7 +426,11 @@ def main():
             torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run_sharded
-        sharded = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_steps, 1, emb, dim=a.dim)
+        # topic-clustered rows with cluster placement: the exact cone pruning
+        # lets each rank skip the facts no cluster it holds can reach, so the
+        # per-rank scan stays (own facts) x (own rows) as ranks are added
+        sharded = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_steps, 1, emb, dim=a.dim,
+                              clustered=True)
     res = {
         "metric": METRIC,
         "value": round(qps, 2),
@@ -470,7 +477,7 @@ def main():
     if sharded is not None:
         res["consolidate_sharded"] = {k: sharded[k] for k in (
             "turns_per_s", "ms_per_step", "buffer_nodes_total", "nodes_per_rank", "convs_per_rank_step", "per_step",
-            "scan_facts_x_rows_per_rank_step", "path")}
+            "scan_facts_x_rows_per_rank_step", "scan_facts_x_rows_unpruned_per_rank_step", "data", "path")}
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)
