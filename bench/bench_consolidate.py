@@ -147,6 +147,11 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
         step()
     _sync(dev)
     comm.barrier()
+    prof = None
+    if os.environ.get("LZK_PROF_HOST") == "1":  # host-side profile of the timed steps (stderr)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     agg = {}
     for _ in range(steps):
@@ -154,6 +159,11 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
             agg[k] = agg.get(k, 0) + v
     ms.flush_persistence()  # write-behind commits of the timed steps land inside the timed region
     _sync(dev)
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
     comm.barrier()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")
