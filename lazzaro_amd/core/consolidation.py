@@ -769,6 +769,12 @@ class ConsolidationMixin:
     NATIVE_PLANNER = os.environ.get("LZK_PY_PLANNER", "0") != "1"
 
     def _consolidate_planned(self, facts, conv, B, embs, now, stats) -> None:
+        # one switch to the graph's stream for the whole batch: the hundreds of
+        # graph operations inside then run without a stream hop each
+        with self.graph.on_stream():
+            self._consolidate_planned_body(facts, conv, B, embs, now, stats)
+
+    def _consolidate_planned_body(self, facts, conv, B, embs, now, stats) -> None:
         from .batch_plan import PoolTooSmall, plan
         g = self.graph
         M = len(facts)
@@ -990,6 +996,7 @@ class ConsolidationMixin:
         decay + prune of what existed before, the touched rows' state, the
         inserts (facts and super-nodes, in row order), the new edges, the
         victims. Returns the edges pruned by the decay."""
+        from ..ops import tenant_ops as T
         g = self.graph
         dev = g.device
         steps = int(seg["c1"]) - int(seg["c0"]) + 1
@@ -998,10 +1005,11 @@ class ConsolidationMixin:
         tr = np.asarray(seg["tch_rows"], np.int64)
         if tr.size:
             with g.on_stream():
-                rt = torch.as_tensor(tr).to(dev)
-                g.sal[rt] = torch.as_tensor(np.asarray(seg["tch_sal"], np.float32)).to(dev)
-                g.acc[rt] = torch.as_tensor(np.asarray(seg["tch_acc"], np.int32)).to(dev)
-                g.last[rt] = torch.as_tensor(np.asarray(seg["tch_last"], np.float64)).to(dev)
+                r64, s64, a64, l64 = T.to_dev_packed([tr, seg["tch_sal"], seg["tch_acc"], seg["tch_last"]], dev)
+                rt = r64.long()
+                g.sal[rt] = s64.float()
+                g.acc[rt] = a64.int()
+                g.last[rt] = l64
                 g.dirty[rt] = 1
             g._bump()
         stored = self._store_binds_graph()
@@ -1050,11 +1058,9 @@ class ConsolidationMixin:
         es = np.asarray(seg["edge_src"], np.int64)
         if es.size:
             with tracer.stage("ap_edges", dev):
-                g.append_edges(torch.as_tensor(es).to(dev),
-                               torch.as_tensor(np.asarray(seg["edge_dst"], np.int64)).to(dev),
-                               torch.as_tensor(np.asarray(seg["edge_w"], np.float32)).to(dev),
-                               torch.as_tensor(np.asarray(seg["edge_code"], np.int32)).to(dev),
-                               g.etype("relates_to"), now=now)
+                s64, d64, w64, c64 = T.to_dev_packed([es, seg["edge_dst"], np.asarray(seg["edge_w"], np.float32),
+                                                      seg["edge_code"]], dev)
+                g.append_edges(s64.long(), d64.long(), w64.float(), c64.int(), g.etype("relates_to"), now=now)
         vic = np.asarray(seg["victims"], np.int64).tolist()
         if vic:
             ids = [g.ids[r] for r in vic]

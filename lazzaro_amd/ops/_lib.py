@@ -98,7 +98,20 @@ def available() -> bool:
     return os.path.exists(LIB_PATH)
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
+    """The current HIP stream of ``device`` as a raw pointer (called for every
+    kernel launch: the raw accessor skips building a Stream object)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        else:
+            idx = device.index if isinstance(device, torch.device) else torch.device(device).index
+            if idx is None:
+                idx = torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

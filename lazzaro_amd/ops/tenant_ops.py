@@ -11,7 +11,7 @@ w f32, co i32, lu f64, meta i32 (shard | type << 24)``.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Dict, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -40,6 +40,22 @@ NTB = 256
 
 def _st(t: torch.Tensor) -> int:
     return _lib.stream_ptr(t.device)
+
+
+def to_dev_packed(cols: Sequence, dev) -> List[torch.Tensor]:
+    """Equal-length host columns -> device float64 rows through ONE pinned,
+    non-blocking copy (exact for int32 / fp32 / fp64 and integers below 2^53).
+    Callers cast each row to its dtype on the device. A pageable ``.to(dev)``
+    per column blocks the host once each."""
+    m = len(cols[0]) if cols else 0
+    blk = torch.empty((len(cols), m), dtype=torch.float64)
+    if dev.type == "cuda":
+        blk = blk.pin_memory()
+    bn = blk.numpy()
+    for j, c in enumerate(cols):
+        bn[j] = np.asarray(c, dtype=np.float64).reshape(-1)
+    d = blk.to(dev, non_blocking=True) if dev.type == "cuda" else blk
+    return [d[j] for j in range(len(cols))]
 
 
 def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, ne: int):
