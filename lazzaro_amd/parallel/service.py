@@ -314,7 +314,10 @@ class DistributedMemoryService:
         one all-to-all-v there and one back -- in order per tenant; the
         ``search_memories`` requests of all tenants an owner receives run as
         one batch (:meth:`_search_submit`). Returns one JSON-able result per
-        request (Nodes as dicts)."""
+        request (Nodes as dicts); a ``search_memories`` result served by the
+        fused GPU path is a :class:`SearchHits` sequence of those dicts, built
+        when first read (``list(r)`` for a plain list, e.g. before
+        ``json.dumps``)."""
         return self._serve_finish(self._serve_submit(requests))
 
     def serve_stream(self, rounds: Iterable[Sequence[Tuple]]):
