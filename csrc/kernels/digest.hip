@@ -65,9 +65,41 @@ __device__ __forceinline__ void lds_init(int* keys) {
   for (int i = threadIdx.x; i < HS; i += DNT) keys[i] = -1;
 }
 
+// ---------------------------------------------------------------- touched
+// touched[r] = r is an endpoint of some edge. With union-find labels that is
+// lab[r] != r (hooked under a smaller row: a component of >= 2 rows), or r
+// is the label of another row, or r has a self-loop (dg_edges_kernel) -- a
+// sequential pass over the labels instead of 2 random byte stores per edge.
+// Rows of a wave are consecutive, so in the usual one-giant-component graph
+// all lanes share the label and one lane marks it.
+__global__ __launch_bounds__(DNT) void dg_touch_kernel(const int* __restrict__ lab, long n,
+                                                       unsigned char* __restrict__ touched) {
+  const int lane = threadIdx.x & 63;
+  const long stride = (long)gridDim.x * DNT;
+  for (long base = (long)blockIdx.x * DNT; base < n; base += stride) {
+    const long r = base + threadIdx.x;
+    int L = -1;
+    if (r < n) {
+      L = lab[r];
+      if (L != (int)r) touched[r] = 1;
+      else L = -1;
+    }
+    bool act = L >= 0;
+    for (int it = 0; it < MATCH_PASSES; ++it) {
+      const unsigned long long m = __ballot(act);
+      if (m == 0) break;
+      const int leader = __ffsll((long long)m) - 1;
+      const int LL = __shfl(L, leader, 64);
+      if (lane == leader) touched[LL] = 1;
+      act = act && L != LL;
+    }
+    if (act) touched[L] = 1;
+  }
+}
+
 // ---------------------------------------------------------------- edges
-// touched[src] = touched[dst] = 1; per label of src: sum of weights (fp64),
-// edge count.
+// Per label of src: sum of weights (fp64), edge count; touched[a] for a
+// self-loop (a, a) (every other endpoint is marked by dg_touch_kernel).
 __device__ __forceinline__ void push_w(int L, double s, int c, int* keys, double* ssum, int* scnt, double* gsum,
                                        int* gcnt) {
   const int sl = slot_of(L);
@@ -99,9 +131,8 @@ __global__ __launch_bounds__(DNT) void dg_edges_kernel(const int* __restrict__ s
     int L = -1;
     double v = 0.0;
     if (act) {
-      const int a = src[e], b = dst[e];
-      touched[a] = 1;
-      touched[b] = 1;
+      const int a = src[e];
+      if (a == dst[e]) touched[a] = 1;
       L = lab[a];
       v = (double)w[e];
     }
@@ -375,7 +406,9 @@ inline unsigned grid_for(long n, unsigned cap = 4096) {
 
 }  // namespace
 
-// Stats phase: edge and row reductions + classification. Every output array
+// Stats phase: edge and row reductions + classification. `lab` must be the
+// union-find labels (smallest row of the component) of exactly these edges:
+// the touched rows are derived from them. Every output array
 // is indexed by label (length n) and must be zeroed by the caller, except
 // gfirst (filled with 1 << 62) and cls/biglist (written here); counters[3]
 // zeroed. The caller reads counters back (one synchronisation) to size the
@@ -387,9 +420,11 @@ LZK_EXPORT int lzk_dg_stats(const int* src, const int* dst, const float* w, long
                             void* stream) {
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (ne > 0)
+  if (ne > 0) {
+    hipLaunchKernelGGL(dg_touch_kernel, dim3(grid_for(n, 4096)), dim3(DNT), 0, st, lab, n, touched);
     hipLaunchKernelGGL(dg_edges_kernel, dim3(grid_for(ne, 2048)), dim3(DNT), 0, st, src, dst, w, ne, lab, touched,
                        gsum, gcnt);
+  }
   hipLaunchKernelGGL(dg_rows_kernel, dim3(grid_for(n, 2048)), dim3(DNT), 0, st, lab, touched, kind, sup, shard, n,
                      gsize, gccnt, gfirst);
   hipLaunchKernelGGL(dg_classify_kernel, dim3(grid_for(n, 1024)), dim3(DNT), 0, st, n, min_size, min_avg_w, take,

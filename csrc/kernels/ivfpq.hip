@@ -16,6 +16,29 @@
 
 namespace {
 
+// Sum of the LUT entries of one PQ code row (M bytes, 16-byte loads; M = 8
+// with one 8-byte load).
+template <int M>
+__device__ __forceinline__ float pq_score(const unsigned char* __restrict__ c, const float* __restrict__ slut,
+                                          float s) {
+  static_assert(M % 16 == 0 || M == 8, "M: 8 or a multiple of 16");
+  if constexpr (M == 8) {
+    const uint2 v = *reinterpret_cast<const uint2*>(c);
+    const unsigned w[2] = {v.x, v.y};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += slut[u * 256 + ((w[u >> 2] >> (8 * (u & 3))) & 0xff)];
+  } else {
+#pragma unroll
+    for (int j0 = 0; j0 < M; j0 += 16) {
+      const uint4 v = *reinterpret_cast<const uint4*>(c + j0);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += slut[(j0 + u) * 256 + ((w[u >> 2] >> (8 * (u & 3))) & 0xff)];
+    }
+  }
+  return s;
+}
+
 template <int K>
 struct LaneTopK {
   float s[K];
@@ -61,17 +84,7 @@ __global__ __launch_bounds__(256) void ivfpq_scan_kernel(const unsigned char* __
   const long r0 = (list >= 0) ? list_off[list] : 0, r1 = (list >= 0) ? list_off[list + 1] : 0;
   for (long r = r0 + threadIdx.x; r < r1; r += 256) {
     const unsigned char* c = codes + r * M;
-    float s = base;
-#pragma unroll
-    for (int j0 = 0; j0 < M; j0 += 16) {
-      uint4 v = *reinterpret_cast<const uint4*>(c + j0);
-      unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int code = (w[u >> 2] >> (8 * (u & 3))) & 0xff;
-        s += slut[(j0 + u) * 256 + code];
-      }
-    }
+    const float s = pq_score<M>(c, slut, base);
     top.push(s, (int)r);
   }
   // wave-level K rounds of argmax over the 64 lane lists
@@ -143,14 +156,7 @@ __global__ __launch_bounds__(256) void ivfpq_scan_deep_kernel(const unsigned cha
   const long r0 = (list >= 0) ? list_off[list] : 0, r1 = (list >= 0) ? list_off[list + 1] : 0;
   for (long r = r0 + threadIdx.x; r < r1; r += 256) {
     const unsigned char* c = codes + r * M;
-    float s = base;
-#pragma unroll
-    for (int j0 = 0; j0 < M; j0 += 16) {
-      uint4 v = *reinterpret_cast<const uint4*>(c + j0);
-      unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += slut[(j0 + u) * 256 + ((w[u >> 2] >> (8 * (u & 3))) & 0xff)];
-    }
+    const float s = pq_score<M>(c, slut, base);
     top.push(s, (int)r);
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -213,14 +219,7 @@ __global__ __launch_bounds__(256) void ivfpq_scan_thresh_kernel(const unsigned c
     float s = LZK_NEG_INF;
     if (r < r1) {
       const unsigned char* c = codes + r * M;
-      s = base;
-#pragma unroll
-      for (int j0 = 0; j0 < M; j0 += 16) {
-        uint4 v = *reinterpret_cast<const uint4*>(c + j0);
-        unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int u = 0; u < 16; ++u) s += slut[(j0 + u) * 256 + ((w[u >> 2] >> (8 * (u & 3))) & 0xff)];
-      }
+      s = pq_score<M>(c, slut, base);
     }
     const bool take = r < r1 && s >= t;
     const unsigned long long m = __ballot(take);
@@ -374,6 +373,7 @@ hipError_t launch_scan(int M, const unsigned char* codes, const long* off, const
                        os, oi);                                                                                     \
   } while (0)
   switch (M) {
+    case 8: GO(8); break;
     case 16: GO(16); break;
     case 32: GO(32); break;
     case 48: GO(48); break;
@@ -404,6 +404,7 @@ LZK_EXPORT int lzk_ivfpq_scan_deep(const void* codes, const long* list_off, cons
                        nprobe, os, oi);                                                                             \
   } while (0)
   switch (M) {
+    case 8: GO(8); break;
     case 16: GO(16); break;
     case 32: GO(32); break;
     case 48: GO(48); break;
@@ -435,6 +436,7 @@ LZK_EXPORT int lzk_ivfpq_scan_thresh(const void* codes, const long* list_off, co
                        nprobe, cap, cnt, os, oi);                                                                   \
   } while (0)
   switch (M) {
+    case 8: GO(8); break;
     case 16: GO(16); break;
     case 32: GO(32); break;
     case 48: GO(48); break;

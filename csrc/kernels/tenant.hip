@@ -99,24 +99,58 @@ __global__ __launch_bounds__(NTB) void tg_node_decay_kernel(float* __restrict__ 
 // Node removal: an edge is dropped when an endpoint is being removed AND the
 // edge lives in that endpoint's shard (the reference deletes only the removed
 // node's shard's incident edges; edges other shards store survive, dangling).
+// The removed rows come as a bitmap (`rmb`, bit r of word r >> 5: 1.25 MB
+// at 10M rows, L2-resident, where a byte array costs a random HBM line per
+// endpoint). `prev` (optional) is an earlier keep flag over the first `nprev` edges --
+// the deferred prune of a consolidation segment (tg_decay_kernel run at the
+// segment's start, the segment's links appended after it) -- so one
+// compaction drops both; `rm` == nullptr: no removals, prev flags only.
 __global__ __launch_bounds__(NTB) void tg_flag_remove_kernel(const int* __restrict__ src, const int* __restrict__ dst,
                                                              const int* __restrict__ meta, long ne,
-                                                             const unsigned char* __restrict__ rm,
+                                                             const unsigned* __restrict__ rmb,
                                                              const int* __restrict__ shard,
+                                                             const unsigned char* __restrict__ prev, long nprev,
                                                              unsigned char* __restrict__ flag,
                                                              int* __restrict__ block_cnt) {
   __shared__ int wsum[NTB / 64];
   const long e = (long)blockIdx.x * NTB + threadIdx.x;
   int f = 0;
   if (e < ne) {
-    const int s = src[e], d = dst[e], es = meta[e] & 0xFFFFFF;
-    LZK_DCHECK(s >= 0 && d >= 0);
-    const bool drop = (rm[s] && shard[s] == es) || (rm[d] && shard[d] == es);
-    f = !drop;
+    f = (prev == nullptr || e >= nprev) ? 1 : (int)prev[e];
+    if (f && rmb) {
+      const int s = src[e], d = dst[e];
+      LZK_DCHECK(s >= 0 && d >= 0);
+      const bool rs = (rmb[s >> 5] >> (s & 31)) & 1u, rd = (rmb[d >> 5] >> (d & 31)) & 1u;
+      if (rs || rd) {
+        const int es = meta[e] & 0xFFFFFF;
+        f = !((rs && shard[s] == es) || (rd && shard[d] == es));
+      }
+    }
     flag[e] = (unsigned char)f;
   }
   const int s = block_ballot_count(f, wsum);
   if (threadIdx.x == 0) block_cnt[blockIdx.x] = s;
+}
+
+// u8 flags -> bitmap: one thread per 32-row word.
+__global__ __launch_bounds__(NTB) void pack_bits_kernel(const unsigned char* __restrict__ f, long n,
+                                                        unsigned* __restrict__ bits) {
+  const long wi = (long)blockIdx.x * NTB + threadIdx.x;
+  const long r0 = wi * 32;
+  if (r0 >= n) return;
+  unsigned b = 0;
+  if (r0 + 32 <= n) {
+    const uint4* p = reinterpret_cast<const uint4*>(f + r0);
+    const uint4 q0 = p[0], q1 = p[1];
+    const unsigned w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) b |= (((w[j] >> (8 * k)) & 0xFFu) != 0u ? 1u : 0u) << (4 * j + k);
+  } else {
+    for (long r = r0; r < n; ++r) b |= (f[r] != 0 ? 1u : 0u) << (r - r0);
+  }
+  bits[wi] = b;
 }
 
 // Stable scatter of flagged edges (block offsets from lzk_scan_blocks).
@@ -277,11 +311,23 @@ LZK_EXPORT int lzk_tg_decay(float* w, long ne, float keep, float thr, unsigned c
   return (int)hipGetLastError();
 }
 
-LZK_EXPORT int lzk_tg_flag_remove(const int* src, const int* dst, const int* meta, long ne, const unsigned char* rm,
-                                  const int* shard, unsigned char* flag, int* block_cnt, void* stream) {
+// rmb: bitmap of the removed rows (lzk_pack_bits), or nullptr (prev only).
+LZK_EXPORT int lzk_tg_flag_remove(const int* src, const int* dst, const int* meta, long ne, const unsigned* rmb,
+                                  const int* shard, const unsigned char* prev, long nprev, unsigned char* flag,
+                                  int* block_cnt, void* stream) {
   if (ne == 0) return 0;
+  if (nprev < 0 || nprev > ne || (prev == nullptr && rmb == nullptr)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tg_flag_remove_kernel, dim3(blocks_for(ne)), dim3(NTB), 0, (hipStream_t)stream, src, dst, meta,
-                     ne, rm, shard, flag, block_cnt);
+                     ne, rmb, shard, prev, nprev, flag, block_cnt);
+  return (int)hipGetLastError();
+}
+
+// bits: (n + 31) / 32 words; f must be 16-byte aligned (a fresh allocation).
+LZK_EXPORT int lzk_pack_bits(const unsigned char* f, long n, unsigned* bits, void* stream) {
+  if (n <= 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(f) & 15) != 0) return (int)hipErrorInvalidValue;
+  const long words = (n + 31) / 32;
+  hipLaunchKernelGGL(pack_bits_kernel, dim3(blocks_for(words)), dim3(NTB), 0, (hipStream_t)stream, f, n, bits);
   return (int)hipGetLastError();
 }
 

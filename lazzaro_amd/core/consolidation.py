@@ -1001,7 +1001,7 @@ class ConsolidationMixin:
         dev = g.device
         steps = int(seg["c1"]) - int(seg["c0"]) + 1
         with tracer.stage("ap_decay", dev):
-            pruned = g.decay(DECAY_RATE, thr, steps=steps)
+            tok = g.segment_begin(DECAY_RATE, thr, steps)  # the prune lands in segment_end, with the victims
         tr = np.asarray(seg["tch_rows"], np.int64)
         if tr.size:
             with g.on_stream():
@@ -1062,10 +1062,10 @@ class ConsolidationMixin:
                                                       seg["edge_code"]], dev)
                 g.append_edges(s64.long(), d64.long(), w64.float(), c64.int(), g.etype("relates_to"), now=now)
         vic = np.asarray(seg["victims"], np.int64).tolist()
-        if vic:
-            ids = [g.ids[r] for r in vic]
-            with tracer.stage("ap_remove", dev):
-                g.remove_nodes(vic, drop_edges=True, unstore=True)
+        ids = [g.ids[r] for r in vic]
+        with tracer.stage("ap_remove", dev):
+            pruned = g.segment_end(tok, vic, unstore=True)
+        if ids:
             with tracer.stage("ap_store_delete", "cpu"):
                 self._store_delete(ids)
         return pruned

@@ -191,6 +191,10 @@ class TenantGraph:
         z = lambda dt: torch.zeros(0, dtype=dt, device=self.device)  # noqa: E731
         self.e = {"src": z(torch.int32), "dst": z(torch.int32), "w": z(torch.float32), "co": z(torch.int32),
                   "lu": z(torch.float64), "meta": z(torch.int32)}
+        # edge columns with room to grow: column -> (buffer, length of the view
+        # self.e holds); an append writes in place only while self.e[k] is
+        # still exactly that view (see _edge_append)
+        self._ebuf: Dict[str, Tuple[torch.Tensor, int]] = {}
         self.emb32 = self.emb16 = self.emb8 = self.sqn = None
         self.sumsq = None  # per-dimension sum of x_i^2 over inserted rows (fp8 error model)
         self.n_sumsq = 0
@@ -819,17 +823,40 @@ class TenantGraph:
         now = time.time() if now is None else now
         dev = self.device
         with self.on_stream():
-            e = self.e
             meta = (shard.to(dev, torch.int32) & SHARD_MASK) | (etype << TYPE_SHIFT) | EDIRTY
-            e["src"] = torch.cat([e["src"], src.to(dev, torch.int32)])
-            e["dst"] = torch.cat([e["dst"], dst.to(dev, torch.int32)])
-            e["w"] = torch.cat([e["w"], w.to(dev, torch.float32)])
-            e["co"] = torch.cat([e["co"], (co.to(dev, torch.int32) if co is not None
-                                           else torch.ones(m, dtype=torch.int32, device=dev))])
-            e["lu"] = torch.cat([e["lu"], (lu.to(dev, torch.float64) if lu is not None
-                                           else torch.full((m,), now, dtype=torch.float64, device=dev))])
-            e["meta"] = torch.cat([e["meta"], meta.to(torch.int32)])
+            self._edge_append({"src": src, "dst": dst, "w": w,
+                               "co": co if co is not None else torch.ones(m, dtype=torch.int32, device=dev),
+                               "lu": lu if lu is not None else torch.full((m,), now, dtype=torch.float64, device=dev),
+                               "meta": meta}, m)
         self._bump(edges=True)
+
+    EDGE_SLACK_MIN = 1 << 14
+
+    def _edge_append(self, new: Dict[str, torch.Tensor], m: int) -> None:
+        """Append ``m`` edges: into the spare tail of the column's buffer when
+        ``self.e[k]`` is still the view this method (or a segment compaction)
+        handed out, else into a fresh buffer with 1/8 headroom. A 20M-edge
+        graph gaining a few hundred links per consolidation segment no longer
+        copies 560 MB per append (``torch.cat``). Older views only ever cover
+        a prefix of the buffer, so writing its tail cannot change them."""
+        e = self.e
+        ne = int(e["src"].numel())
+        for k, dt in (("src", torch.int32), ("dst", torch.int32), ("w", torch.float32), ("co", torch.int32),
+                      ("lu", torch.float64), ("meta", torch.int32)):
+            v, add = e[k], new[k].to(self.device, dt)
+            buf, vn = self._ebuf.get(k, (None, -1))
+            if buf is None or vn != ne or v.numel() != ne or buf.numel() < ne + m or v.data_ptr() != buf.data_ptr():
+                buf = torch.empty(ne + m + max((ne + m) >> 3, self.EDGE_SLACK_MIN), dtype=dt, device=self.device)
+                buf[:ne].copy_(v)
+            buf[ne:ne + m].copy_(add)
+            e[k] = buf[:ne + m]
+            self._ebuf[k] = (buf, ne + m)
+
+    def _adopt_edges(self, e: Dict[str, torch.Tensor]) -> None:
+        """Make ``e`` (views of over-allocated buffers, T._compact(extra=...))
+        the edge list, its spare tails available to :meth:`_edge_append`."""
+        self.e = e
+        self._ebuf = {k: (v._base if v._base is not None else v, int(v.numel())) for k, v in e.items()}
 
     def upsert_edges(self, src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, shard: torch.Tensor,
                      etype: torch.Tensor, co=None, lu=None, now: Optional[float] = None) -> int:
@@ -964,6 +991,96 @@ class TenantGraph:
 
     def prune(self, threshold: float) -> int:
         return self.decay(0.0, threshold, decay_nodes=False)
+
+    # ------------------------------------------------------------------ consolidation segments
+    def segment_begin(self, rate: float, prune_threshold: Optional[float], steps: int) -> Dict:
+        """Start one segment of a batched consolidation: ``steps`` decay rounds
+        of the edges and shard-node saliences now, the prune of ``w <
+        prune_threshold`` deferred to :meth:`segment_end`, which drops those
+        edges together with the segment's victims' in ONE compaction and ONE
+        host sync. Between the two calls the edge list still holds the
+        to-be-pruned edges: only node inserts / row updates and
+        :meth:`append_edges` may run in between. On the CPU this is
+        :meth:`decay` followed by :meth:`remove_nodes` in segment_end."""
+        if prune_threshold is not None and prune_threshold <= 0.0:
+            prune_threshold = None
+        if not self.on_gpu:
+            return {"pruned": self.decay(rate, prune_threshold, steps=steps)}
+        tok = {"flag": None, "ne0": self.num_edges}
+        if steps <= 0 or (rate == 0.0 and prune_threshold is None):
+            return tok
+        with self.on_stream():
+            tok["flag"] = T.decay_flags(self.e, self.sal[: self.n], self.kind[: self.n], self.sup[: self.n], rate,
+                                        prune_threshold, steps)
+        if rate:
+            self.decay_log += steps * math.log1p(-rate)
+        self._bump(edges=bool(rate))
+        return tok
+
+    def segment_end(self, tok: Dict, victims, unstore: bool = True) -> int:
+        """Finish a segment (:meth:`segment_begin`): drop the deferred-pruned
+        edges and remove the ``victims`` rows like :meth:`remove_nodes`
+        (ghost rows, their shard's incident edges gone). Returns #pruned."""
+        vic = victims.tolist() if torch.is_tensor(victims) else list(victims)
+        if "pruned" in tok:
+            if vic:
+                self.remove_nodes(vic, drop_edges=True, unstore=unstore)
+            return tok["pruned"]
+        cand = sorted({r for r in vic if 0 <= r < self.n})
+        prev, ne0 = tok["flag"], tok["ne0"]
+        ne = self.num_edges
+        if not cand and prev is None:
+            return 0
+        with self.on_stream():
+            parts = []
+            rt = live_t = None
+            if cand:
+                rt = self._dev_rows(cand)
+                kd = self.kind[rt]
+                live_t = kd == NODE
+                parts += [kd.int(), self.sup[rt].int(), self.shard[rt]]
+            flag = bc = total = None
+            if ne and (prev is not None or cand):
+                rm = None
+                if cand:
+                    rm = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+                    rm[rt] = live_t.to(torch.uint8)
+                flag, bc, total = T.flag_finish(self.e, rm, self.shard[: self.n], prev)
+                parts.append(total)
+                if prev is not None:
+                    parts.append(ne0 - prev.sum(dtype=torch.int32).view(1))
+            if cand:
+                self.kind[rt] = torch.where(live_t, torch.full_like(kd, GHOST), kd)
+                if unstore:
+                    self.stored[rt] = torch.where(live_t, torch.zeros_like(self.stored[rt]), self.stored[rt])
+            info = torch.cat(parts).cpu().numpy() if parts else np.zeros(0, np.int64)  # the one host sync
+            nc = len(cand)
+            pruned = 0
+            if flag is not None:
+                n_out = int(info[3 * nc])
+                if prev is not None:
+                    pruned = int(info[3 * nc + 1])
+                if n_out != ne:
+                    old = self.e
+                    out, n = T._compact(old, flag, bc, ne, extra=max(ne >> 3, self.EDGE_SLACK_MIN), total=total,
+                                        n_out=n_out)
+                    self._adopt_edges(out)
+                    if self.track:
+                        self._note_dropped(*T._dropped(old, flag, ne, n))
+        if cand:
+            kinds, sups, shards = info[:nc], info[nc:2 * nc], info[2 * nc:3 * nc]
+            for r, k, sp, sh in zip(cand, kinds.tolist(), sups.tolist(), shards.tolist()):
+                if k != NODE:
+                    continue
+                if sp:
+                    self.n_super -= 1
+                elif sh >= 0:
+                    self.shard_count[sh] -= 1
+                self.children.pop(r, None)
+                self.odd_emb.pop(r, None)
+                self.deleted_ids[self.ids[r]] = None
+        self._bump(edges=True, store=bool(cand))
+        return pruned
 
     def remove_nodes(self, rows, drop_edges: bool = True, unstore: bool = False) -> int:
         """Remove live nodes: each becomes a ghost row (its id may still be an

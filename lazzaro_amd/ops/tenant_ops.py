@@ -22,13 +22,14 @@ P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
 D_ = C.c_double
 
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
-_lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, P, P])
+_lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
 _lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
 _lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
+_lib.register("lzk_pack_bits", I, [P, L, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, I, P, P, P, P, P, I, P, P, L, P])
@@ -58,16 +59,22 @@ def to_dev_packed(cols: Sequence, dev) -> List[torch.Tensor]:
     return [d[j] for j in range(len(cols))]
 
 
-def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, ne: int):
-    """Stable device compaction of the flagged edges (scan + scatter)."""
+def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, ne: int, extra: int = 0,
+             total: Optional[torch.Tensor] = None, n_out: Optional[int] = None):
+    """Stable device compaction of the flagged edges (scan + scatter). With
+    ``extra`` each output column is a view of a buffer ``extra`` rows longer
+    (room for appends without a copy, :meth:`TenantGraph._edge_append`).
+    ``total`` / ``n_out``: the block counts were already scanned and the
+    survivor count read by the caller."""
     L_ = _lib.lib()
     dev = e["src"].device
-    total = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.check(L_.lzk_scan_blocks(bc.data_ptr(), bc.numel(), total.data_ptr(), _st(bc)), "scan_blocks")
-    n_out = int(total.item())
+    if n_out is None:
+        total = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(L_.lzk_scan_blocks(bc.data_ptr(), bc.numel(), total.data_ptr(), _st(bc)), "scan_blocks")
+        n_out = int(total.item())
     if n_out == ne:
         return e, 0
-    out = {k: torch.empty(n_out, dtype=e[k].dtype, device=dev) for k in EDGE_COLS}
+    out = {k: torch.empty(n_out + extra, dtype=e[k].dtype, device=dev)[:n_out] for k in EDGE_COLS}
     if n_out:
         _lib.check(L_.lzk_tg_compact(flag.data_ptr(), bc.data_ptr(), ne, *(e[k].data_ptr() for k in EDGE_COLS),
                                      *(out[k].data_ptr() for k in EDGE_COLS), _st(flag)), "tg_compact")
@@ -121,6 +128,14 @@ def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, thresho
     return out, n, dropped
 
 
+def _bits(rm: torch.Tensor) -> torch.Tensor:
+    """u8 row flags (device) -> int32 bitmap words (bit r of word r >> 5)."""
+    n = int(rm.numel())
+    bits = torch.empty(max(1, (n + 31) // 32), dtype=torch.int32, device=rm.device)
+    _lib.check(_lib.lib().lzk_pack_bits(rm.data_ptr(), n, bits.data_ptr(), _st(rm)), "pack_bits")
+    return bits
+
+
 def _dropped(e: Dict[str, torch.Tensor], flag: torch.Tensor, ne: int, n: int):
     """(src, dst, meta) of the edges whose keep flag is 0 (``n`` of them)."""
     if n == 0:
@@ -151,12 +166,54 @@ def remove_edges_of(e: Dict[str, torch.Tensor], rm: torch.Tensor, shard: torch.T
     nb = max(1, (ne + NTB - 1) // NTB)
     flag = torch.empty(ne, dtype=torch.uint8, device=dev)
     bc = torch.empty(nb, dtype=torch.int32, device=dev)
+    rmb = _bits(rm.to(torch.uint8).contiguous())
     _lib.check(_lib.lib().lzk_tg_flag_remove(e["src"].data_ptr(), e["dst"].data_ptr(), e["meta"].data_ptr(), ne,
-                                             rm.data_ptr(), shard.data_ptr(), flag.data_ptr(), bc.data_ptr(),
-                                             _st(flag)), "tg_flag_remove")
+                                             rmb.data_ptr(), shard.data_ptr(), None, 0, flag.data_ptr(),
+                                             bc.data_ptr(), _st(flag)), "tg_flag_remove")
     out, n = _compact(e, flag, bc, ne)
     dropped = _dropped(e, flag, ne, n) if want_dropped else None
     return out, n, dropped
+
+
+def decay_flags(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, threshold: Optional[float], steps: int):
+    """The decay half of :func:`decay_prune` on the device with the prune
+    deferred: ``steps`` decay rounds of every edge and shard-node salience in
+    place, and (``threshold`` not None) the keep flag ``w >= threshold`` of
+    each current edge, returned for :func:`flag_finish`. No host sync."""
+    ne = int(e["src"].numel())
+    dev = e["src"].device
+    nn = int(sal.numel())
+    flag = bc = None
+    if threshold is not None and ne:
+        flag = torch.empty(ne, dtype=torch.uint8, device=dev)
+        bc = torch.empty(max(1, (ne + NTB - 1) // NTB), dtype=torch.int32, device=dev)
+    thr = float(threshold) if threshold is not None else float("-inf")
+    _lib.check(_lib.lib().lzk_tg_decay(e["w"].data_ptr(), ne, float(1.0 - rate), thr, _lib.ptr(flag), _lib.ptr(bc),
+                                       _lib.ptr(sal), _lib.ptr(kind), _lib.ptr(sup), nn, 1 if nn else 0, int(steps),
+                                       _st(e["w"])), "tg_decay")
+    return flag
+
+
+def flag_finish(e: Dict[str, torch.Tensor], rm: Optional[torch.Tensor], shard: torch.Tensor,
+                prev: Optional[torch.Tensor]):
+    """Keep flags of every current edge: ``prev`` (a :func:`decay_flags`
+    result over the first ``prev.numel()`` edges; later edges were appended
+    since) AND not dropped by the removal of the ``rm`` rows (same rule as
+    :func:`remove_edges_of`). Returns (flag, block counts, total) -- the
+    survivor count stays on the device until the caller's one sync."""
+    ne = int(e["src"].numel())
+    dev = e["src"].device
+    flag = torch.empty(ne, dtype=torch.uint8, device=dev)
+    bc = torch.empty(max(1, (ne + NTB - 1) // NTB), dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int32, device=dev)
+    L_ = _lib.lib()
+    rmb = _bits(rm) if rm is not None else None
+    _lib.check(L_.lzk_tg_flag_remove(e["src"].data_ptr(), e["dst"].data_ptr(), e["meta"].data_ptr(), ne,
+                                     _lib.ptr(rmb), shard.data_ptr(), _lib.ptr(prev),
+                                     int(prev.numel()) if prev is not None else 0, flag.data_ptr(), bc.data_ptr(),
+                                     _st(flag)), "tg_flag_remove")
+    _lib.check(L_.lzk_scan_blocks(bc.data_ptr(), bc.numel(), total.data_ptr(), _st(bc)), "scan_blocks")
+    return flag, bc, total
 
 
 def build_visible_csr(e: Dict[str, torch.Tensor], shard: torch.Tensor, n: int):
