@@ -164,6 +164,9 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
         pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(40)
+        # who synchronises: callers of the host-device transfers / syncing ops
+        pstats.Stats(prof, stream=sys.stderr).print_callers(r"method 'cpu'|method 'item'|method 'tolist'|"
+                                                            r"torch.nonzero|method 'numpy'")
     comm.barrier()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")

@@ -837,7 +837,7 @@ class ConsolidationMixin:
             if seg["consolidate"]:
                 stats["consolidations"] += 1
                 with tracer.stage("run_consolidation", self._device):
-                    self.run_consolidation()
+                    self.run_consolidation(prune=not self.auto_prune)
             if seg["cluster"]:
                 self._maybe_cluster(self.conversation_count - 1)
         if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
@@ -1027,13 +1027,13 @@ class ConsolidationMixin:
                         k += 1
                     js = idx[i:k]
                     keys = fact_key[js].tolist()
-                    rows = g.add_nodes([id_of[key] for key in keys], [facts[j]["content"] for j in js],
+                    g.add_nodes([id_of[key] for key in keys], [facts[j]["content"] for j in js],
                                        E[torch.as_tensor(js, dtype=torch.long).to(E.device)],
                                        shard=codes[js].astype(np.int32),
                                        types=[facts[j].get("type", "semantic") for j in js],
                                        sal=torch.from_numpy(isal[i:k]), acc=torch.from_numpy(iacc[i:k]),
                                        last=torch.from_numpy(ilast[i:k]), now=now, stored=stored)
-                    if rows.tolist() != keys:
+                    if list(g.last_add_rows) != keys:  # host rows: no device round trip
                         raise RuntimeError("batch plan row assignment diverged from the graph")
                     i = k
                 else:
@@ -1047,7 +1047,7 @@ class ConsolidationMixin:
                     srow = g.add_nodes([f"super_{skey}_{int(now)}"], [summary], emb[None, :], shard=[int(sp["code"])],
                                        sup=[1], children={0: ch_ids}, stored=False, sal=float(isal[i]),
                                        acc=int(iacc[i]), last=float(ilast[i]), now=now)
-                    if int(srow[0]) != int(sp["key"]):
+                    if int(g.last_add_rows[0]) != int(sp["key"]):
                         raise RuntimeError("batch plan super-node row diverged from the graph")
                     with g.on_stream():
                         rt = torch.as_tensor(children, dtype=torch.long).to(dev)
@@ -1218,7 +1218,14 @@ class ConsolidationMixin:
         self._say(f"  ✓ Created super-node {sid} with {rows.size} children")
 
     # ------------------------------------------------------------ deep consolidation
-    def run_consolidation(self, weight_threshold: float = 0.6, merge_similar: bool = True) -> str:
+    def run_consolidation(self, weight_threshold: float = 0.6, merge_similar: bool = True,
+                          prune: bool = True) -> str:
+        """Reference memory_system.py:951-1010. ``prune=False``: the caller
+        guarantees no edge is below the prune threshold -- consolidate_batch,
+        whose segment just pruned every decayed old edge (segment_end) and
+        whose planner drops new links at each decay (batch_plan end_decay);
+        weights only fall by decay, so the reference's prune here finds
+        nothing."""
         results = []
         self._say("🔄 Running consolidation...")
         g = self.graph
@@ -1240,8 +1247,10 @@ class ConsolidationMixin:
                 if "Updated" in r:
                     updates += 1
                     results.append(r)
-        with self._graph_lock, tracer.stage("rc_prune", self._device):
-            pruned = g.prune(self.prune_threshold)
+        pruned = 0
+        if prune:
+            with self._graph_lock, tracer.stage("rc_prune", self._device):
+                pruned = g.prune(self.prune_threshold)
         if pruned > 0:
             results.append(f"✓ Pruned {pruned} weak edges")
         if updates > 0:

@@ -142,6 +142,21 @@ def _side_stream(dev: torch.device):
     return st
 
 
+def _host_ints(v, m: int, default: int) -> Optional[np.ndarray]:
+    """int64 [m] host values of a per-row argument (scalar, sequence,
+    ndarray or CPU tensor); None for a device tensor."""
+    if v is None:
+        return np.full(m, default, np.int64)
+    if torch.is_tensor(v):
+        if v.is_cuda:
+            return None
+        v = v.numpy()
+    if isinstance(v, (int, float, bool, np.number)):
+        return np.full(m, int(v), np.int64)
+    a = np.asarray(v).reshape(-1).astype(np.int64)
+    return np.broadcast_to(a, (m,)) if a.size == 1 else a
+
+
 class TenantGraph:
     NODE_COLS = (("sal", torch.float32, 0.0), ("acc", torch.int32, 0), ("last", torch.float64, 0.0),
                  ("ts", torch.float64, 0.0), ("shard", torch.int32, -1), ("kind", torch.uint8, FREE),
@@ -169,7 +184,7 @@ class TenantGraph:
         self.n_super = 0
         self.etype_names: List[str] = []
         self.etype_code: Dict[str, int] = {}
-        self.max_norm_dev = 0.0  # max | |x| - 1 | over embedded rows
+        self._max_norm_dev = 0.0  # max | |x| - 1 | over embedded rows (see max_norm_dev)
         self.decay_log = 0.0  # sum of log(1 - rate) over every decay applied
         self.version = 0  # bumps on any mutation (views / caches)
         self.edge_version = 0
@@ -180,7 +195,13 @@ class TenantGraph:
         self._store_version = 0
         self._mirror: Dict[str, Tuple[int, np.ndarray]] = {}
         self.deleted_ids: Dict[str, None] = {}  # node ids to delete from the store at the next commit
-        self.deleted_edges: Dict[Tuple[str, str], None] = {}
+        self._deleted_edges: Dict[Tuple[str, str], None] = {}
+        # removed edges still on the device, (src, dst, meta) -- resolved to
+        # ids when deleted_edges is read (rows never change ids), so removals
+        # inside a consolidation batch cost no host synchronisation
+        self._drop_pending: List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
+        self.last_add_rows: Sequence[int] = range(0)
+        self._norm_dev_pending: List[torch.Tensor] = []
         self.track = True
         self.stream = _side_stream(self.device) if self.on_gpu else None
         self.ann_cfg: Optional[Dict] = None  # store index="ivfpq": IVF-PQ for large tenants (HBMStore.attach)
@@ -524,32 +545,36 @@ class TenantGraph:
             self.has_emb[rt] = has.to(torch.uint8)
             if info is None or any(info[0]):
                 dv = torch.where(has, (nrm2.sqrt() - 1.0).abs(), torch.zeros_like(nrm2)).max()
-                self.max_norm_dev = max(self.max_norm_dev, float(dv))
+                if dv.is_cuda:
+                    self._norm_dev_pending.append(dv)
+                    if len(self._norm_dev_pending) >= 256:
+                        self._norm_dev_pending = [torch.stack(self._norm_dev_pending).max()]
+                else:
+                    self._max_norm_dev = max(self._max_norm_dev, float(dv))
         elif info is not None:
             for j, v in info[1].items():
                 self.odd_emb[rl[j]] = v
-        # host counters
-        sup_any = bool(supv.any()) if m > 64 else None
-        if ghost:
-            pass
-        elif sup_any is False:
-            cnt = np.bincount(sh.cpu().numpy(), minlength=len(self.shard_count))
+        # host counters: from the caller's host values when it passed them
+        # (no device round trip), else from the device columns
+        if not ghost:
+            sh_h, sup_h = _host_ints(shard, m, 0), _host_ints(sup, m, 0)
+            if sh_h is None:
+                sh_h = sh.cpu().numpy().astype(np.int64)
+            if sup_h is None:
+                sup_h = supv.cpu().numpy().astype(np.int64)
+            ns = int(np.count_nonzero(sup_h))
+            self.n_super += ns
+            shs = sh_h[sup_h == 0] if ns else sh_h
+            cnt = np.bincount(shs[shs >= 0], minlength=len(self.shard_count))
             for c in np.nonzero(cnt)[0]:
                 self.shard_count[int(c)] += int(cnt[c])
-        else:
-            sh_h = sh.tolist()
-            sup_h = supv.tolist()
-            for j in range(m):
-                if sup_h[j]:
-                    self.n_super += 1
-                else:
-                    self.shard_count[sh_h[j]] += 1
         if children is not None:
             for j, ch in children.items():
                 self.children[rl[j]] = list(ch)
         if self.deleted_ids:
             for i in ids:
                 self.deleted_ids.pop(i, None)
+        self.last_add_rows = rl  # host rows of this call (range or list)
         self._bump(store=True)
         return rt
 
@@ -781,7 +806,7 @@ class TenantGraph:
             if self.emb16 is not None:
                 self.emb16[r, : self.dim] = v.to(torch.bfloat16)
             self._write_fp8(r, v[None, :])
-        self.max_norm_dev = max(self.max_norm_dev, abs(math.sqrt(n2) - 1.0))
+        self._max_norm_dev = max(self._max_norm_dev, abs(math.sqrt(n2) - 1.0))
         self._bump(store=True)
 
     # ------------------------------------------------------------------ edges
@@ -955,15 +980,53 @@ class TenantGraph:
     def _note_dropped(self, s: torch.Tensor, d: torch.Tensor, meta: Optional[torch.Tensor] = None) -> None:
         """Queue removed edges for deletion from the store -- only those the
         store holds (ESTORED): an edge created and pruned between two
-        commits never reached it."""
-        if meta is not None:
-            keep = (meta & ESTORED) != 0
-            s, d = s[keep], d[keep]
+        commits never reached it. Device tensors wait in _drop_pending until
+        deleted_edges is read."""
         if s.numel() == 0:
             return
-        ids = self.ids
+        if s.is_cuda:
+            self._drop_pending.append((s, d, meta))
+            return
+        self._resolve_dropped(s, d, meta)
+
+    def _resolve_dropped(self, s, d, meta) -> None:
+        s, d = s.cpu().numpy(), d.cpu().numpy()
+        if meta is not None:
+            keep = (meta.cpu().numpy() & ESTORED) != 0
+            s, d = s[keep], d[keep]
+        ids, de = self.ids, self._deleted_edges
         for a, b in zip(s.tolist(), d.tolist()):
-            self.deleted_edges[(ids[a], ids[b])] = None
+            de[(ids[a], ids[b])] = None
+
+    @property
+    def deleted_edges(self) -> Dict[Tuple[str, str], None]:
+        """(src id, dst id) of edges to delete from the store at the next commit."""
+        if self._drop_pending:
+            pend, self._drop_pending = self._drop_pending, []
+            with self.on_stream():
+                for s, d, meta in pend:
+                    self._resolve_dropped(s, d, meta)
+        return self._deleted_edges
+
+    @deleted_edges.setter
+    def deleted_edges(self, v: Dict[Tuple[str, str], None]) -> None:
+        self._drop_pending = []
+        self._deleted_edges = v
+
+    @property
+    def max_norm_dev(self) -> float:
+        """max | |x| - 1 | over embedded rows; inserts leave their device
+        maxima pending (no host synchronisation per insert)."""
+        if self._norm_dev_pending:
+            pend, self._norm_dev_pending = self._norm_dev_pending, []
+            with self.on_stream():
+                self._max_norm_dev = max(self._max_norm_dev, float(torch.stack(pend).max()))
+        return self._max_norm_dev
+
+    @max_norm_dev.setter
+    def max_norm_dev(self, v: float) -> None:
+        self._norm_dev_pending = []
+        self._max_norm_dev = float(v)
 
     # ------------------------------------------------------------------ maintenance
     def decay(self, rate: float = 0.01, prune_threshold: Optional[float] = None, decay_nodes: bool = True,
@@ -1126,7 +1189,7 @@ class TenantGraph:
         rows = [r for r in self.rows_of(ids) if r >= 0]
         if rows:
             with self.on_stream():
-                self.stored[torch.as_tensor(rows, dtype=torch.long).to(self.device)] = 0
+                self.stored[self._dev_rows(rows)] = 0  # pinned async upload, no host block
             self._bump(store=True)
 
     def mark_stored(self, rows) -> None:
@@ -1290,7 +1353,8 @@ class TenantGraph:
             with self.on_stream():
                 key, rows = T.component_digest(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n],
                                                self.sup[:n], self.shard[:n], n, min_size, min_avg_w, take)
-                rows_h, key_h = rows.cpu().numpy(), key.cpu().numpy()
+                kr = torch.stack([key, rows.long()]).cpu().numpy()  # one device -> host copy
+                key_h, rows_h = kr[0], kr[1]
             if rows_h.size == 0:
                 return []
             return np.split(rows_h, np.nonzero(np.diff(key_h))[0] + 1)

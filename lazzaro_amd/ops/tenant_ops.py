@@ -141,7 +141,8 @@ def _dropped(e: Dict[str, torch.Tensor], flag: torch.Tensor, ne: int, n: int):
     if n == 0:
         z = e["src"][:0]
         return z, e["dst"][:0], e["meta"][:0]
-    idx = torch.nonzero(flag[:ne] == 0).flatten()
+    # the count is known: a fixed-size nonzero, no host synchronisation
+    idx = torch.nonzero_static(flag[:ne] == 0, size=n).flatten()
     return e["src"][idx], e["dst"][idx], e["meta"][idx]
 
 
