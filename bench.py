@@ -376,11 +376,13 @@ def main():
     t_embed, Qe = timeit(lambda: emb.batch_embed_tensor(pool[0]))
     t_store, (_, rows_e) = timeit(lambda: g.store_search(Qe, a.k, "l2"))
     Xb = bias = q16 = None
-    t_kernel = None
+    t_kernel = t_lowp = None
     if dev.type == "cuda":  # the bare candidate-scan kernel, for reference
         Xb, bias = g.emb16[: g.n], g.store_bias("l2")
         q16 = g._q16(Qe)
         t_kernel, _ = timeit(lambda: flat_topk(Xb, q16, 16, bias=bias, alpha=2.0))
+        if g.emb8 is not None and g.emb8.dtype == torch.int8:  # the store search's int8 candidate pass
+            t_lowp, _ = timeit(lambda: g._i8_candidates(Qe, q16, 16, bias, 2.0))
     t_batch, res0 = timeit(lambda: ms.search_memories_batch(pool[0], limit=a.k))
     nr = min(a.recall_queries, a.batch)
     _, truth_e = exact_l2_topk(g, Qe[:nr], a.k)
@@ -455,7 +457,12 @@ def main():
         "recall_at_10_random_queries": round(rec_rand, 4),
         "recall_truth": "float64 exact L2 over the stored fp32 vectors",
         "breakdown_ms": {"embed": round(t_embed, 3), "store_search": round(t_store, 3),
-                         "raw_scan_kernel": None if t_kernel is None else round(t_kernel, 3), "search_memories_batch_unpipelined": round(t_batch, 3)},
+                         "raw_scan_kernel": None if t_kernel is None else round(t_kernel, 3),
+                         "i8_candidate_search": None if t_lowp is None else round(t_lowp, 3),
+                         "search_memories_batch_unpipelined": round(t_batch, 3)},
+        "search_precision": ("int8 MFMA candidate scan (error-model margin) -> exact bf16 re-score above the error "
+                             "cut -> fp32 re-rank; recall checked against float64 truth" if t_lowp is not None else
+                             "bf16 MFMA candidate scan -> fp32 re-rank; recall checked against float64 truth"),
         "tokens_per_query": {"padded": S_tok, "real_mean": round(float(lens.float().mean()), 2)},
         "load_s": round(t_load, 1),
         "prewarm_s": round(t_pre, 1),

@@ -119,6 +119,7 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 // keeps every ds_read_b128 lane group on 16 distinct bank slots.
 struct MmaBf16 {
   static constexpr int KPER = 64;  // K elements per 128-B K-row
+  static constexpr bool kInt = false;
   template <int MQ, int NQ>
   __device__ __forceinline__ static void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
     quad_mma<MQ, NQ>(acc, a, b);
@@ -127,6 +128,7 @@ struct MmaBf16 {
 
 struct MmaFp8 {
   static constexpr int KPER = 128;
+  static constexpr bool kInt = false;
   __device__ __forceinline__ static i32x8 cat(const bf16x8& lo, const bf16x8& hi) {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     const i32x4 l = __builtin_bit_cast(i32x4, lo), h = __builtin_bit_cast(i32x4, hi);
@@ -145,6 +147,32 @@ struct MmaFp8 {
         acc[MQ * 4 + mb][NQ * 2 + nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
             aa, bb[nb], acc[MQ * 4 + mb][NQ * 2 + nb], 0, 0, 0, 127, 0, 127);
     }
+  }
+};
+
+// int8 rows / queries (per-row / per-query scales applied by the caller's
+// epilogue): chunks g and g+4 of a 128-B K-row are the 16-byte operands of two
+// v_mfma_i32_16x16x64_i8 (same cycles as 16x16x32 bf16 at twice the K: 2x the
+// bf16 rate, exact int32 sums). acc holds the int32 accumulators' BIT
+// PATTERNS (kInt): the zero-initialised f32x4 is int 0, and an epilogue must
+// read them with __builtin_bit_cast, never as floats.
+struct MmaI8 {
+  static constexpr int KPER = 128;
+  static constexpr bool kInt = true;
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  template <int MQ, int NQ>
+  __device__ __forceinline__ static void quad(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          f32x4& c = acc[MQ * 4 + mb][NQ * 2 + nb];
+          c = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, a[mb][s]),
+                                                                            __builtin_bit_cast(i32x4, b[nb][s]),
+                                                                            __builtin_bit_cast(i32x4, c), 0, 0, 0));
+        }
   }
 };
 

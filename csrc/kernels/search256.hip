@@ -167,7 +167,9 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
 #pragma unroll
     for (int g = wave; g < 4 * EPI_ARRAYS; g += 8) {
       const int a = g >> 2, c = g & 3;  // wave-uniform
-      const bool need = a == 0 || (a == 1 && HAS_BIAS) || ((a == 2 || a == 3) && HAS_LABEL) || (a == 4 && DUAL);
+      // MMA::kInt: arrays 2 / 3 carry the fp32 row / query scales (no labels)
+      const bool need = a == 0 || (a == 1 && HAS_BIAS) || ((a == 2 || a == 3) && (HAS_LABEL || MMA::kInt)) ||
+                        (a == 4 && DUAL);
       if (!need) continue;
       const void* src;
       if (a == 0) src = thr + min(q0 + c * 64 + lane, nq - 1);
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
       const int* e_qlab = reinterpret_cast<const int*>(e_thr + 768);
       const float* e_thr2 = e_thr + 1024;
       int qq[4], ql[4];
-      float th[4], th2[4];
+      float th[4], th2[4], al[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int qlo = wc * 64 + j * 16 + (lane & 15);
@@ -257,6 +259,25 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
         th[j] = (qq[j] < nq) ? e_thr[qlo] : __builtin_huge_valf();
         th2[j] = (DUAL && qq[j] < nq) ? e_thr2[qlo] : __builtin_huge_valf();
         ql[j] = HAS_LABEL ? e_qlab[qlo] : -1;
+        // int8 scan: the query's scale (label slot 3) joins alpha
+        al[j] = MMA::kInt ? alpha * reinterpret_cast<const float*>(e_qlab)[qlo] : alpha;
+      }
+      if constexpr (MMA::kInt) {
+        // int32 sums -> float * the row's scale (label slot 2), in place: the
+        // rest of the epilogue (column prefilter, per-score test) is the bf16
+        // one with alpha = alpha * qscale. Exact: |acc| < 2^24 for D <= 1024.
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const float* e_rs = reinterpret_cast<const float*>(e_lab);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(e_rs + wr * 128 + i * 16 + 4 * (lane >> 4));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const i32x4 v = __builtin_bit_cast(i32x4, acc[i][j]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][e] = (float)v[e] * rs[e];
+          }
+        }
       }
       const bool full = r0 + BM <= nrows;
       // OPT bit 4: column prefilter. For alpha > 0 every score of query
@@ -279,7 +300,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
           const float tmin = DUAL ? fminf(th[j], th2[j]) : th[j];
           // slack of a few ulp: the per-score path may contract alpha*acc+bias differently
           // (tmin = +inf -> NaN -> skipped; tmin = -inf -> kept)
-          if (alpha > 0.f && !(alpha * mx + bmax >= tmin - 1e-6f * fabsf(tmin))) continue;
+          if (al[j] > 0.f && !(al[j] * mx + bmax >= tmin - 1e-6f * fabsf(tmin))) continue;
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -291,7 +312,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
           float m = LZK_NEG_INF;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            sc[e] = alpha * acc[i][j][e] + bv[e];
+            sc[e] = al[j] * acc[i][j][e] + bv[e];
             const bool in = full || (rb + e < nrows);
             if (!in) sc[e] = LZK_NEG_INF;
             if constexpr (HAS_LABEL && !DUAL) {  // single search: the label filters list A
@@ -373,6 +394,7 @@ constexpr int kCandOpt = 24;
 // (profiles/ab_dual_r1.json) 0: 16.27 ms, body2: 15.65, +prefilter 15.90.
 constexpr int kDualOpt = 8;
 int g_dual_opt = -1;  // A/B override of kCandOpt for the dual kernel (lzk_set_dual_opt)
+int g_i8_opt = 0;    // A/B override of kCandOpt for the int8 scan (lzk_set_i8_opt)
 int g_g256_opt = 0;  // A/B override of kCandOpt for the plain (no bias / label) variant; 100 = OPT 0
 int g_n_cu = 0;
 
@@ -575,12 +597,16 @@ __global__ __launch_bounds__(256) void top1_decode_kernel(const unsigned long lo
 // list entry (q, row) gets alpha * <Q16[q], X16[row]> + bias[row] from the
 // bf16 rows (fp32 accumulate), so the top-k select that follows ranks by the
 // same scores as the bf16 path. One 256-thread block per query, 4 waves take
-// alternate candidates; lanes read consecutive 8-B chunks of a row.
+// alternate 64-entry windows of the list and re-score the window's kept
+// entries one by one; lanes read consecutive 8-B chunks of a row. cut
+// (optional, [nq]): entries whose scan score is below cut[q] cannot reach the
+// query's top-k (the caller's error bound) and become -inf without a row read.
 __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict__ X, long ldx,
                                                            const u16* __restrict__ Qm, long ldq, int D,
                                                            const float* __restrict__ bias, float alpha,
                                                            const int* __restrict__ cnt, int cap,
-                                                           float* __restrict__ cs, const int* __restrict__ ci) {
+                                                           float* __restrict__ cs, const int* __restrict__ ci,
+                                                           const float* __restrict__ cut) {
   const int q = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = min(cnt[q] & 0x3fffffff, cap);
@@ -596,8 +622,19 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict
       qv[t][2] = __uint_as_float(u.y << 16); qv[t][3] = __uint_as_float(u.y & 0xffff0000u);
     }
   }
-  for (int p = wave; p < n; p += 4) {
-    const long idx = (long)q * cap + p;
+  const float cq = cut ? cut[q] : LZK_NEG_INF;
+  for (int base = wave * 64; base < n; base += 256) {
+    const long li = (long)q * cap + base + lane;
+    bool keep = base + lane < n;
+    if (keep && cut) {
+      keep = cs[li] >= cq;
+      if (!keep) cs[li] = LZK_NEG_INF;
+    }
+    unsigned long long live = __ballot(keep);
+    while (live) {
+    const int jj = __builtin_ctzll(live);
+    live &= live - 1;
+    const long idx = (long)q * cap + base + jj;
     const int r = ci[idx];
     LZK_DCHECK(r >= 0);
     const u16* xr = X + (long)r * ldx;
@@ -616,6 +653,7 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (lane == 0) cs[idx] = alpha * acc + (bias ? bias[r] : 0.f);
+    }
   }
 }
 
@@ -664,6 +702,7 @@ LZK_EXPORT int lzk_flat_top1_grouped(const void* C, long ldc, const void* Xq, lo
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
+LZK_EXPORT void lzk_set_i8_opt(int o) { g_i8_opt = o; }
 LZK_EXPORT int lzk_set_stamp_buffer(void* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p));
 }
@@ -902,9 +941,61 @@ LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
 
 // Exact bf16 re-score of candidate lists in place (see cand_rescore_kernel).
 LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long ldq, int nq, int D, const float* bias,
-                                float alpha, const int* cnt, int cap, float* cs, const int* ci, void* stream) {
+                                float alpha, const int* cnt, int cap, float* cs, const int* ci, const float* cut,
+                                void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(cand_rescore_kernel, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, (const u16*)X16, ldx,
-                     (const u16*)Q16, ldq, D, bias, alpha, cnt, cap, cs, ci);
+                     (const u16*)Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut);
+  return (int)hipGetLastError();
+}
+
+// int8 candidate pass (rows / queries: int8 bytes, row strides in bytes,
+// D_bytes % 128 == 0, D_bytes <= 1024 so the int32 sums stay exact in fp32):
+// score = alpha * qscale[q] * (<q8, x8> * rscale[row]) + bias[row] >= thr[q]
+// goes to the block-private records (persistent grid). rscale / qscale > 0.
+LZK_EXPORT int lzk_flat_cand_i8(const void* X8, long ldx_bytes, int nrows, const void* Q8, long ldq_bytes, int nq,
+                                int D_bytes, const float* bias, const float* rscale, const float* qscale, float alpha,
+                                const float* thr, int cap, int* cnt, float* cs, int* ci, void* blk_buf, int blk_cap,
+                                int* blk_cnt, void* stream) {
+  if (D_bytes % 128 != 0 || D_bytes > 1024 || (ldx_bytes | ldq_bytes) % 16 != 0 || nq <= 0 || nrows <= 0 ||
+      cap <= 0 || !rscale || !qscale || !(alpha > 0.f))
+    return (int)hipErrorInvalidValue;
+  if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;
+  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt};
+  const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
+  const long nblk = (long)n_rt * n_qt;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X8;
+  const u16* q = (const u16*)Q8;
+  // the scales ride in the label slots of the epilogue staging (HAS_LABEL = false)
+  const int* rs = (const int*)rscale;
+  const int* qs = (const int*)qscale;
+#define LZK_GIO(B, O)                                                                                               \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, false, false, O, MmaI8>,                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, false, false, O, MmaI8>), dim3(grid), dim3(NT), CAND_P_LDS, \
+                       st, x, ldx_bytes / 2, nrows, q, ldq_bytes / 2, nq, D_bytes / 2, bias, rs, qs, alpha, thr,    \
+                       n_qt, (int)nblk, cap, cnt, cs, ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr,    \
+                       (int*)nullptr, blk);                                                                         \
+  } while (0)
+  // g_i8_opt (A/B only): 56 = + cross-tile prefetch (OPT bit 5; KS = D_bytes / 128 must be even)
+  const bool pre = g_i8_opt == 56 && (D_bytes / 128) % 2 == 0;
+  if (bias) {
+    if (pre) LZK_GIO(true, 56);
+    else LZK_GIO(true, kCandOpt);
+  } else {
+    if (pre) LZK_GIO(false, 56);
+    else LZK_GIO(false, kCandOpt);
+  }
+#undef LZK_GIO
   return (int)hipGetLastError();
 }

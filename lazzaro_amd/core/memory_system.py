@@ -709,7 +709,7 @@ class MemorySystem(ConsolidationMixin):
     def _graph_bytes(self) -> int:
         g = self.graph
         return int(sum(t.numel() * t.element_size() for t in
-                       [g.emb32, g.emb16, g.emb8, g.sqn] + [getattr(g, c) for c, _, _ in TenantGraph.NODE_COLS]
+                       [g.emb32, g.emb16, g.emb8, g.rs8, g.sqn] + [getattr(g, c) for c, _, _ in TenantGraph.NODE_COLS]
                        + list(g.e.values()) if t is not None))
 
     def engine_stats(self) -> Dict:

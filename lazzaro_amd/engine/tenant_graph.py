@@ -80,7 +80,7 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # fp8 candidate scan of the store search: large batches over large tenants
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
-FP8_MIN_Q, FP8_MIN_ROWS, FP8_MARGIN_Z = 256, 1 << 20, 8.0
+LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 256, 1 << 20, 8.0
 # cos_topk(min_score=): kernel threshold slack below min_score. Unit rows and
 # queries rounded to bf16 (relative 2^-9 each) move a cosine by at most
 # 2^-8 * sum|q_i x_i| <= 2^-8 ~ 0.0039, plus fp32 accumulation order.
@@ -216,7 +216,8 @@ class TenantGraph:
         # self.e holds); an append writes in place only while self.e[k] is
         # still exactly that view (see _edge_append)
         self._ebuf: Dict[str, Tuple[torch.Tensor, int]] = {}
-        self.emb32 = self.emb16 = self.emb8 = self.sqn = None
+        self.emb32 = self.emb16 = self.emb8 = self.rs8 = self.sqn = None
+        self._rs8_max = None  # device scalar: max per-row int8 scale ever written (error model)
         self.sumsq = None  # per-dimension sum of x_i^2 over inserted rows (fp8 error model)
         self.n_sumsq = 0
         for name, dt, _ in self.NODE_COLS:
@@ -261,15 +262,22 @@ class TenantGraph:
             e32 = torch.zeros((cap, self.dim), dtype=torch.float32, device=dev)
             sq = torch.zeros(cap, dtype=torch.float32, device=dev)
             e16 = torch.zeros((cap, self.Dp), dtype=torch.bfloat16, device=dev) if self.on_gpu else None
-            e8 = torch.zeros((cap, self.Dp), dtype=torch.uint8, device=dev) if self._fp8_ok() else None
+            lowp = self._lowp_mode()
+            e8 = torch.zeros((cap, self.Dp), dtype=torch.int8 if lowp == "i8" else torch.uint8,
+                             device=dev) if lowp else None
+            rs8 = torch.ones(cap, dtype=torch.float32, device=dev) if lowp == "i8" else None
             if self.cap and self.emb32 is not None and self.emb32.shape[1] == self.dim:
                 e32[:n] = self.emb32[:n]
                 sq[:n] = self.sqn[:n]
                 if e16 is not None:
                     e16[:n] = self.emb16[:n]
-                if e8 is not None and self.emb8 is not None:
+                if e8 is not None and self.emb8 is not None and self.emb8.dtype == e8.dtype:
                     e8[:n] = self.emb8[:n]
-            self.emb32, self.sqn, self.emb16, self.emb8 = e32, sq, e16, e8
+                    if rs8 is not None and self.rs8 is not None:
+                        rs8[:n] = self.rs8[:n]
+            self.emb32, self.sqn, self.emb16, self.emb8, self.rs8 = e32, sq, e16, e8, rs8
+            if rs8 is not None and self._rs8_max is None:
+                self._rs8_max = torch.zeros((), dtype=torch.float32, device=dev)
             if self.sumsq is None or self.sumsq.numel() != self.dim:
                 self.sumsq = torch.zeros(self.dim, dtype=torch.float64, device=dev)
         for k, v in new.items():
@@ -304,22 +312,37 @@ class TenantGraph:
     _digest_sorted = False
     SAMPLE_TWO_LEVEL = os.environ.get("LZK_SAMPLE_ASSIGN", "two_level") != "full"
 
-    # fp8 (e4m3) copy of the rows for the store search's candidate scan
-    # (ops.search.flat_topk_fp8): rows are scaled by FP8_ROW_SCALE, which
-    # keeps unit-norm rows (|x_i| <= 1) inside e4m3's normal range
+    # Low-precision copy of the rows for the store search's candidate scan
+    # (LZK_SEARCH_LOWP): "i8" = per-row symmetric int8 + fp32 row scales
+    # (ops.search.flat_topk_i8, v_mfma_i32_16x16x64_i8), "fp8" = e4m3 rows
+    # scaled by FP8_ROW_SCALE (ops.search.flat_topk_fp8), "off" = bf16 scan.
+    # The fp8 path lost (round 2: its 8-sigma margin grew the lists ~5x and the
+    # bf16 re-score of every entry cost 5.9 ms, bench/ab_fp8_search.py); int8
+    # has ~4x less score error on unit rows and re-scores only the entries
+    # above the error cut.
     FP8_ROW_SCALE = 64.0
-    # Off by default: on 10M x 768 x 1024 queries the fp8 candidate kernel
-    # measured 12.1 ms vs 13.4 ms bf16, but the wider fp8 margin grows the
-    # lists ~5x and their bf16 re-score costs 5.9 ms, so the whole store
-    # search is 19.8 vs 14.2 ms (bench/ab_fp8_search.py,
-    # profiles/ab_fp8_search_r2.json). LZK_SEARCH_FP8=1 turns it on.
-    FP8_SCAN = os.environ.get("LZK_SEARCH_FP8", "0") == "1"
+    LOWP = os.environ.get("LZK_SEARCH_LOWP", "i8")
 
-    def _fp8_ok(self) -> bool:
-        return self.on_gpu and self.FP8_SCAN and self.Dp % 128 == 0
+    def _lowp_mode(self) -> str:
+        if not self.on_gpu or self.Dp % 128 != 0:
+            return ""
+        if self.LOWP == "i8" and self.Dp <= 1024:
+            return "i8"
+        return "fp8" if self.LOWP == "fp8" else ""
 
-    def _write_fp8(self, rt, e32: torch.Tensor) -> None:
-        if self.emb8 is not None:
+    def _write_lowp(self, rt, e32: torch.Tensor) -> None:
+        if self.emb8 is None:
+            return
+        if self.emb8.dtype == torch.int8:
+            from ..ops.search import quantize_i8_rows
+            # quantised from the bf16 rows: the scan then estimates the bf16
+            # scores the exact re-score and select rank by
+            q, sc = quantize_i8_rows(e32.to(torch.bfloat16))
+            self.emb8[rt, : self.dim] = q
+            self.rs8[rt] = sc
+            if sc.numel():
+                torch.maximum(self._rs8_max, sc.max(), out=self._rs8_max)
+        else:
             from ..ops.search import quantize_e4m3
             self.emb8[rt, : self.dim] = quantize_e4m3(e32, self.FP8_ROW_SCALE)
 
@@ -539,7 +562,7 @@ class TenantGraph:
                 del x2
                 if self.emb16 is not None:
                     self.emb16[r, : self.dim] = x.to(torch.bfloat16)
-                self._write_fp8(rt[a:b], x)
+                self._write_lowp(rt[a:b], x)
             self.sqn[rt] = nrm2.float()
             self.n_sumsq += m
             self.has_emb[rt] = has.to(torch.uint8)
@@ -788,6 +811,8 @@ class TenantGraph:
                         self.emb16[r] = 0
                     if self.emb8 is not None:
                         self.emb8[r] = 0
+                    if self.rs8 is not None:
+                        self.rs8[r] = 1.0
             self._bump(store=True)
             return
         if self.dim is None:
@@ -805,7 +830,7 @@ class TenantGraph:
             self.dirty[r] = 1
             if self.emb16 is not None:
                 self.emb16[r, : self.dim] = v.to(torch.bfloat16)
-            self._write_fp8(r, v[None, :])
+            self._write_lowp(r, v[None, :])
         self._max_norm_dev = max(self._max_norm_dev, abs(math.sqrt(n2) - 1.0))
         self._bump(store=True)
 
@@ -1589,8 +1614,11 @@ class TenantGraph:
         if self.on_gpu and k <= CAND_SLOTS and (metric != "cosine" or self.unit_rows()) \
                 and M * n >= KERNEL_MIN_WORK // 16:
             q16 = self._q16(Qf)
-            if self.emb8 is not None and self.unit_rows() and M >= FP8_MIN_Q and n >= FP8_MIN_ROWS:
-                _, cand = self._fp8_candidates(Qf, q16, kc, bias, alpha)
+            if self.emb8 is not None and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS:
+                if self.emb8.dtype == torch.int8:
+                    _, cand = self._i8_candidates(Qf, q16, kc, bias, alpha)
+                else:
+                    _, cand = self._fp8_candidates(Qf, q16, kc, bias, alpha)
             else:
                 _, cand = flat_topk(self.emb16[:n], q16, kc, bias=bias, alpha=alpha)
             return self._rerank_store(Qf, cand, k, metric, bias)
@@ -1622,6 +1650,30 @@ class TenantGraph:
             self._ann_covered = r1
         return idx.candidate_ids(Qf, R, cfg["nprobe"])
 
+    def _i8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
+        """Store-search candidates from the int8 scan (``emb8`` / ``rs8``),
+        re-scored from the bf16 rows above the error cut. Error model of the
+        int8 score against the bf16 one, per query (no host sync): with the
+        query's rounding error eta (known exactly) and a row's rounding error
+        delta_i ~ U(-s/2, s/2), s <= the largest row scale s_max,
+          <x^, q^> - <x, q> = <x, eta> + <delta, q> + <delta, eta>
+        var <x, eta> = sum_i eta_i^2 E[x_i^2] (per-dimension second moments
+        of the tenant's rows), var <delta, q> <= |q|^2 s_max^2 / 12, and
+        |<delta, eta>| <= s_max / 2 * |eta|_1 (worst case, added as a floor);
+        the margin is LOWP_MARGIN_Z standard deviations plus that floor."""
+        from ..ops.search import flat_topk_i8, quantize_i8_rows
+        n, d = self.n, self.dim
+        q8, qs = quantize_i8_rows(q16)
+        eta = q8.float() * qs[:, None] - q16.float()
+        mu2 = (self.sumsq / max(self.n_sumsq, 1)).float()
+        smax = self._rs8_max
+        v1 = (eta[:, :d] ** 2 * mu2[None, :]).sum(1)
+        v2 = (q16.float() ** 2).sum(1) * (smax * smax / 12.0)
+        floor = 0.5 * smax * eta.abs().sum(1)
+        margin = (abs(alpha) * (LOWP_MARGIN_Z * torch.sqrt(v1 + v2) + floor)).contiguous()
+        return flat_topk_i8(self.emb8, self.rs8, q8, qs, self.emb16[:n], q16, kc, bias=bias, alpha=alpha,
+                            margin=margin)
+
     def _fp8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
         """Store-search candidates from the fp8 scan (rows in ``emb8``),
         re-scored from the bf16 rows. The threshold margin covers the fp8
@@ -1639,7 +1691,7 @@ class TenantGraph:
         mu2 = (self.sumsq / max(self.n_sumsq, 1)).to(torch.float64)
         sig = (2.0 / 3.0) ** 0.5 * 2.0 ** -4 * torch.sqrt((Qf.double() ** 2 * mu2[None, :]).sum(1))
         floor = 2.0 ** -9 * (1.0 / self.FP8_ROW_SCALE + 1.0 / sq) * Qf.double().abs().sum(1).clamp_min(1.0)
-        margin = (abs(alpha) * (FP8_MARGIN_Z * sig + floor)).float().contiguous()
+        margin = (abs(alpha) * (LOWP_MARGIN_Z * sig + floor)).float().contiguous()
         return flat_topk_fp8(self.emb8, q8, self.FP8_ROW_SCALE * sq, self.emb16[:n], q16, kc, bias=bias,
                              alpha=alpha, margin=margin)
 

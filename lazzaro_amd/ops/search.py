@@ -298,7 +298,10 @@ _lib.register("lzk_flat_cand_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
                                            _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
 _lib.register("lzk_cand_grid_f8", _lib.I, [_lib.I, _lib.I])
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
-                                           _lib.I, _lib.P, _lib.P, _lib.P])
+                                           _lib.I, _lib.P, _lib.P, _lib.P, _lib.P])
+_lib.register("lzk_flat_cand_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P,
+                                           _lib.P, _lib.F, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I,
+                                           _lib.P, _lib.P])
 
 FP8_MAX = 448.0
 
@@ -349,8 +352,85 @@ def flat_topk_fp8(X8: torch.Tensor, Q8: torch.Tensor, scale2: float, X16: torch.
     _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
                                  ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
     _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
-                                  _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(), st),
-               "lzk_cand_rescore")
+                                  _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(), None,
+                                  st), "lzk_cand_rescore")
+    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
+
+
+def quantize_i8_rows(x: torch.Tensor, out: torch.Tensor = None, scale_out: torch.Tensor = None):
+    """Symmetric per-row int8: q = round(x / s), s = max|x_row| / 127 (1 for
+    an all-zero row), so x ~= q * s with |error| <= s / 2 per element.
+    Returns (q int8 [n, D] (or ``out`` filled in its first D columns), s fp32 [n])."""
+    xf = x.float()
+    amax = xf.abs().amax(1)
+    s = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+    q = torch.round(xf / s[:, None]).clamp_(-127, 127).to(torch.int8)
+    if out is not None:
+        out[:, : q.shape[1]] = q
+        q = out
+    if scale_out is not None:
+        scale_out.copy_(s)
+        s = scale_out
+    return q, s
+
+
+def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
+                 X16: torch.Tensor, Q16: torch.Tensor, k: int, *, bias=None, alpha: float = 1.0, margin=None):
+    """Top-k of ``alpha * <Q16, X16> + bias`` with the candidate scan on the
+    int8 MFMA (v_mfma_i32_16x16x64_i8: twice the bf16 rate, half the bytes).
+
+    X8 / Q8: per-row symmetric int8 of X16 / Q16 (:func:`quantize_i8_rows`,
+    Dp % 128 == 0, Dp <= 1024) with fp32 scales ``rscale`` [N] / ``qscale``
+    [nq]; ``margin`` [nq] (fp32, >= 0) bounds |int8 score - bf16 score| for
+    the query (the caller's error model). Steps:
+      1. thr = exact bf16 k-th best of a 1/S row sample (a lower bound of the
+         true k-th score) minus the margin -> the int8 scan keeps every row
+         whose int8 score clears it;
+      2. cut = (k-th best int8 score of the list) - 2 * margin: a row in
+         the true top-k has int8 score >= T - m >= that cut (T the true
+         k-th score, itself >= the list's k-th int8 score - m), so
+         only entries above the cut are re-scored from the bf16 rows -- a few
+         dozen per query instead of the whole list;
+      3. exact select with the bf16 fallback for overflowed lists.
+    Returns (scores fp32 [nq, k], rows int64 [nq, k]) like :func:`flat_topk`."""
+    L = _lib.lib()
+    nq, Dp = Q16.shape
+    N = X16.shape[0]
+    kslot = L.lzk_flat_topk_kslot(int(k))
+    assert kslot > 0 and X8.dtype == torch.int8 and Q8.dtype == torch.int8 and Dp % 128 == 0 and Dp <= 1024
+    assert X8.shape[1] == Dp and X8.stride(1) == 1 and Q8.stride(1) == 1 and X8.shape[0] >= N
+    assert rscale.dtype == torch.float32 and qscale.dtype == torch.float32 and rscale.shape[0] >= N
+    assert alpha > 0
+    dev = X16.device
+    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
+    thr = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
+    if margin is not None:
+        thr = (thr - margin).contiguous()
+    cap = max(2048, 16 * kslot * S)
+    cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    grid = L.lzk_cand_grid_f8(N, nq)
+    bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 1)
+    st = _lib.stream_ptr(dev)
+    qs = qscale.contiguous()
+    _lib.check(L.lzk_flat_cand_i8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp, _lib.ptr(bias),
+                                  rscale.data_ptr(), qs.data_ptr(), float(alpha), thr.data_ptr(), cap, cnt.data_ptr(),
+                                  cs.data_ptr(), ci.data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st),
+               "lzk_flat_cand_i8")
+    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
+                                 ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
+    cut = None
+    if margin is not None:
+        s8 = torch.empty((nq, kslot), dtype=torch.float32, device=dev)
+        i8 = torch.empty((nq, kslot), dtype=torch.long, device=dev)
+        ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
+        _lib.check(L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, kslot, 0,
+                                     s8.data_ptr(), i8.data_ptr(), ovf.data_ptr(), None, st), "lzk_cand_select")
+        kth = s8[:, k - 1]
+        cut = (kth - 2.0 * margin - 1e-6 * (1.0 + kth.abs())).contiguous()
+        cut = torch.nan_to_num(cut, nan=float("-inf"))
+    _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
+                                  _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(),
+                                  _lib.ptr(cut), st), "lzk_cand_rescore")
     return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
 
 

@@ -271,13 +271,15 @@ def test_search_memories_stream_matches_batch_gpu(tmp_path):
     ms.close()
 
 
+@pytest.mark.parametrize("mode", ["i8", "fp8"])
 @pytest.mark.parametrize("data", ["isotropic", "clustered"])
-def test_store_search_fp8_scan_exact_recall_gpu(data):
-    """Large tenant (> FP8_MIN_ROWS) + large batch: candidates from the fp8
-    MFMA scan with the error-model margin, re-scored from bf16 and re-ranked
-    in fp32 == exact fp32 L2 top-10 over the original vectors."""
+def test_store_search_lowp_scan_exact_recall_gpu(data, mode):
+    """Large tenant (> LOWP_MIN_ROWS) + large batch: candidates from the int8
+    (or fp8) MFMA scan with the error-model margin, re-scored from bf16 and
+    re-ranked in fp32 == exact fp32 L2 top-10 over the original vectors."""
     from lazzaro_amd.engine import tenant_graph as TG
-    TG.TenantGraph.FP8_SCAN = True
+    saved = TG.TenantGraph.LOWP
+    TG.TenantGraph.LOWP = mode
     g = TenantGraph(device=DEV)
     N, D = (1 << 20) + 4096, 768
     gen = torch.Generator(device=DEV).manual_seed(7)
@@ -289,12 +291,12 @@ def test_store_search_fp8_scan_exact_recall_gpu(data):
                                                                                         generator=gen)
     X = X / X.norm(dim=1, keepdim=True)
     g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
-    assert g.emb8 is not None
+    assert g.emb8 is not None and g.emb8.dtype == (torch.int8 if mode == "i8" else torch.uint8)
     Q = torch.randn(512, D, device=DEV, generator=gen)
     if data == "clustered":
         Q = X[torch.randint(0, N, (512,), device=DEV, generator=gen)] + 0.3 * Q / D ** 0.5
     Q = Q / Q.norm(dim=1, keepdim=True)
-    assert 512 >= TG.FP8_MIN_Q and N >= TG.FP8_MIN_ROWS
+    assert 512 >= TG.LOWP_MIN_Q and N >= TG.LOWP_MIN_ROWS
     _, rows = g.store_search(Q, 10, "l2")
     Xd, Qd = X.double(), Q.double()
     truth = []
@@ -308,9 +310,38 @@ def test_store_search_fp8_scan_exact_recall_gpu(data):
     hit = sum(len(set(a) & set(b)) for a, b in zip(rows.cpu().tolist(), top.cpu().tolist()))
     assert hit / (512 * 10) == 1.0
     # and the bf16 scan gives the same rows
-    TG.TenantGraph.FP8_SCAN, g.emb8 = False, None
-    _, rows16 = g.store_search(Q, 10, "l2")
+    TG.TenantGraph.LOWP, g.emb8 = "off", None
+    try:
+        _, rows16 = g.store_search(Q, 10, "l2")
+    finally:
+        TG.TenantGraph.LOWP = saved
     assert torch.equal(rows16, rows)
+
+
+def test_flat_topk_i8_matches_bf16_gpu():
+    """int8 scan + error cut + bf16 re-score == the bf16 scan's top-10
+    (scores bit-identical: both come from the same bf16 re-score / scan
+    arithmetic up to accumulation order), with and without a cut."""
+    from lazzaro_amd.ops.search import flat_topk, flat_topk_i8, quantize_i8_rows
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    N, D, nq = 1_300_000, 768, 512
+    X = torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    Q = torch.randn(nq, D, device=DEV, generator=gen)
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
+    bias = -(X * X).sum(1).contiguous()
+    bias[::97] = float("-inf")  # removed rows never surface
+    s16, r16 = flat_topk(X16, Q16, 10, bias=bias, alpha=2.0)
+    X8, rs = quantize_i8_rows(X16)
+    Q8, qs = quantize_i8_rows(Q16)
+    assert X8.dtype == torch.int8 and rs.shape == (N,) and float(rs.min()) > 0
+    for margin in (torch.full((nq,), 0.03, device=DEV), None):
+        s8, r8 = flat_topk_i8(X8, rs, Q8, qs, X16, Q16, 10, bias=bias, alpha=2.0, margin=margin)
+        same = sum(len(set(a) & set(b)) for a, b in zip(r8.cpu().tolist(), r16.cpu().tolist())) / (nq * 10)
+        assert same == 1.0
+        assert torch.allclose(s8, s16, atol=1e-4, rtol=0)
+        assert not bool((r8 % 97 == 0).any())
 
 
 def test_flat_topk_fp8_matches_bf16_candidates_gpu():
