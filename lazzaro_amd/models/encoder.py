@@ -215,12 +215,22 @@ class SentenceEncoder:
         the attention run on sum(lens) tokens instead of B*S -- the padded
         positions never influence the pooled embedding (keys >= len are
         masked, pooling stops at len), so they are pure waste."""
-        x, lens_d, cu, B, S = self._layers(ids, lens, packed)
+        cls = self.cfg.pooling == "cls" and self.CLS_LAST
+        x, lens_d, cu, B, S = self._layers(ids, lens, packed, cls_last=cls)
         return E.pool_norm(x, lens_d, B, S, self.cfg.pooling, pad_to, cu=cu)
 
-    def _layers(self, ids: torch.Tensor, lens: torch.Tensor, packed: Optional[bool]):
+    # CLS pooling reads only each sequence's first token of the last layer, so
+    # that layer's attention output, O projection, FFN and LayerNorms run on
+    # the B CLS rows alone (its QKV still covers every token: K and V feed the
+    # CLS query). Exact -- the other rows' last-layer states are never read.
+    # LZK_CLS_LAST=0 computes the full last layer.
+    CLS_LAST = os.environ.get("LZK_CLS_LAST", "1") != "0"
+
+    def _layers(self, ids: torch.Tensor, lens: torch.Tensor, packed: Optional[bool], cls_last: bool = False):
         """Embedding + every transformer layer. Returns (token states, lens on
-        the device, cu row offsets (packed) or None, B, S)."""
+        the device, cu row offsets (packed) or None, B, S). ``cls_last``: the
+        last layer past its attention only for the CLS rows -- returns their
+        states [B, H] with cu None and S = 1."""
         c, p = self.cfg, self.p
         B, S = ids.shape
         if packed is None:
@@ -245,6 +255,10 @@ class SentenceEncoder:
         for i in range(c.layers):
             qkv = self._lin(x, i, "wqkv", "bqkv")
             ctx = E.attention(qkv, lens, B, S, c.heads, cu=cu)
+            if cls_last and i == c.layers - 1 and B > 0:
+                first = cu[:-1].long() if cu is not None else torch.arange(B, device=x.device) * S
+                ctx, x = ctx.index_select(0, first), x.index_select(0, first)
+                cu, S = None, 1
             x = self._lin_ln(ctx, i, "wo", "bo", x, "ln1", split=self._split_o(x))
             hdn = self._lin(x, i, "w1", "b1", act="gelu")
             x = self._lin_ln(hdn, i, "w2", "b2", x, "ln2", split=self._split_ffn2(x))

@@ -1,4 +1,5 @@
 """CPU tier of the encoder stack: tokenizer + reference forward shapes/norms."""
+import pytest
 import torch
 
 from lazzaro_amd.core.embedders import OnDeviceEmbedder, Tokenizer
@@ -79,3 +80,22 @@ def test_packed_varlen_forward_matches_padded():
     b, _ = enc.forward(ids, lens, packed=True)
     torch.testing.assert_close(a, b, atol=2e-2, rtol=0)  # bf16 CPU reference, same math
     assert ((a * b).sum(1) > 0.9999).all()
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_cls_pooling_last_layer_on_cls_rows_only(packed, monkeypatch):
+    """CLS pooling: the last layer's post-attention work on the CLS rows only
+    gives the same embedding as the full last layer (packed and padded)."""
+    import dataclasses
+
+    from lazzaro_amd.models import encoder as M
+    cfg = dataclasses.replace(M.CONFIGS["tiny"], pooling="cls")
+    monkeypatch.setitem(M.CONFIGS, "tiny-cls", cfg)
+    enc = M.SentenceEncoder("tiny-cls", seed=4)
+    ids = torch.randint(1000, 4000, (5, 20), dtype=torch.int32)
+    lens = torch.tensor([20, 3, 11, 1, 7], dtype=torch.int32)
+    monkeypatch.setattr(M.SentenceEncoder, "CLS_LAST", False)
+    full, _ = enc.forward(ids, lens, packed=packed)
+    monkeypatch.setattr(M.SentenceEncoder, "CLS_LAST", True)
+    cls, _ = enc.forward(ids, lens, packed=packed)
+    torch.testing.assert_close(cls, full, atol=1e-6, rtol=0)
