@@ -288,6 +288,68 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
 
 inline unsigned blocks_for(long n, int per = NTB) { return (unsigned)((n + per - 1) / per); }
 
+
+// Store-search re-rank (reference LanceDBStore.search_nodes ordering,
+// vector_store.py:132-140): one wave per query scores its C <= 64 candidate
+// rows exactly in fp32 from the stored vectors and emits the top-k by (score
+// desc, row asc). metric 0 = l2: 2<q,x> + bias[r] - |q|^2 (bias = -|x|^2, -inf
+// for rows outside the store); 1 = ip: <q,x> + bias[r]; 2 = cosine:
+// <q,x> / |x| + bias[r]. cand < 0 -> empty. Output rows -1 / scores -inf past
+// the valid candidates. Replaces ~20 gather / GEMM / sort launches.
+__global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restrict__ Q, long ldq,
+                                                           const float* __restrict__ X, long ldx, int D,
+                                                           const float* __restrict__ sqn,
+                                                           const float* __restrict__ bias,
+                                                           const long* __restrict__ cand, int C, int M, int k,
+                                                           int metric, float* __restrict__ os,
+                                                           long* __restrict__ oi) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= M) return;
+  const float* qr = Q + (long)q * ldq;
+  float qq = 0.f;
+  for (int d = lane; d < D; d += 64) qq = fmaf(qr[d], qr[d], qq);
+  qq = wave_sum(qq);
+  float my_s = LZK_NEG_INF;
+  long my_r = -1;
+  for (int c = 0; c < C; ++c) {
+    const long r = cand[(long)q * C + c];  // wave-uniform
+    if (r < 0) continue;
+    const float* xr = X + r * ldx;
+    float acc = 0.f;
+    for (int d = lane; d < D; d += 64) acc = fmaf(qr[d], xr[d], acc);
+    acc = wave_sum(acc);
+    float sc;
+    if (metric == 0) {
+      sc = 2.f * acc + bias[r] - qq;
+    } else if (metric == 2) {
+      const float nr = sqrtf(sqn[r]);
+      sc = acc / (nr > 0.f ? nr : 1.f) + bias[r];
+    } else {
+      sc = acc + bias[r];
+    }
+    if (lane == c) { my_s = sc; my_r = r; }
+  }
+  // rank among the wave's (score, row) pairs; -inf scores are empty
+  const bool live = lane < C && my_r >= 0 && my_s != LZK_NEG_INF;
+  int rank = 0;
+  for (int o = 0; o < C; ++o) {
+    const float s2 = __shfl(my_s, o, 64);
+    const long r2 = __shfl(my_r, o, 64);
+    const bool l2 = r2 >= 0 && s2 != LZK_NEG_INF;
+    if (l2 && o != lane && (s2 > my_s || (s2 == my_s && r2 < my_r))) ++rank;
+  }
+  const int nlive = __popcll(__ballot(live));
+  if (live && rank < k) {
+    os[(long)q * k + rank] = my_s;
+    oi[(long)q * k + rank] = my_r;
+  }
+  for (int j = nlive + lane; j < k; j += 64) {
+    os[(long)q * k + j] = LZK_NEG_INF;
+    oi[(long)q * k + j] = -1;
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C ABI
@@ -407,5 +469,14 @@ LZK_EXPORT int lzk_tg_gather_fields(const long* rows, int nq, int k, const void*
   if (n <= 0) return 0;
   hipLaunchKernelGGL(tg_gather_fields_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      rows, nq, k, (const unsigned long long*)base, o_sal, o_acc, o_kind, o_sup, o_shard);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_store_rerank(const float* Q, long ldq, const float* X, long ldx, int D, const float* sqn,
+                                const float* bias, const long* cand, int C, int M, int k, int metric, float* os,
+                                long* oi, void* stream) {
+  if (C <= 0 || C > 64 || M <= 0 || k <= 0 || metric < 0 || metric > 2) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(store_rerank_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Q, ldq,
+                     X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi);
   return (int)hipGetLastError();
 }

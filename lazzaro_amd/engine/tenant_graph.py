@@ -1719,6 +1719,9 @@ class TenantGraph:
         return self._pad_k(best_s, best_i, k)
 
     def _rerank_store(self, Qf, cand, k, metric, bias):
+        if self.on_gpu and 0 < cand.shape[1] <= 64 and metric in ("l2", "ip", "cosine"):
+            from ..ops.tenant_ops import store_rerank
+            return store_rerank(Qf, self.emb32, self.sqn, bias, cand, k, metric)
         valid = cand >= 0
         rows = cand.clamp_min(0)
         s = self._store_scores(Qf, self.emb32[rows], self.sqn[rows], bias[rows], metric)

@@ -22,6 +22,7 @@ P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
 D_ = C.c_double
 
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
+_lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
@@ -476,3 +477,28 @@ def gather_fields(rows: torch.Tensor, graphs: Optional[Sequence], device_out: bo
     if device_out:
         return o
     return {n: t.cpu().numpy() for n, t in o.items()}
+
+
+_METRIC_CODE = {"l2": 0, "ip": 1, "dot": 1, "cosine": 2}
+
+
+def store_rerank(Qf: torch.Tensor, X: torch.Tensor, sqn: torch.Tensor, bias: torch.Tensor, cand: torch.Tensor,
+                 k: int, metric: str):
+    """Exact fp32 re-rank of store-search candidates in one launch
+    (tenant.hip store_rerank_kernel): scores of the rows ``cand`` [M, C]
+    (C <= 64, -1 = empty) against ``Qf`` [M, D], top-k by (score desc, row
+    asc). Returns (scores [M, k], rows int64 [M, k]; -inf / -1 padding)."""
+    M, C = cand.shape
+    D = Qf.shape[1]
+    Qc = Qf.contiguous()
+    cc = cand.contiguous()
+    assert X.stride(1) == 1 and X.shape[1] == D and C <= 64 and Qc.dtype == torch.float32
+    os_ = torch.empty((M, k), dtype=torch.float32, device=Qf.device)
+    oi = torch.empty((M, k), dtype=torch.long, device=Qf.device)
+    if M == 0:
+        return os_, oi
+    _lib.check(_lib.lib().lzk_store_rerank(Qc.data_ptr(), Qc.stride(0), X.data_ptr(), X.stride(0), D, sqn.data_ptr(),
+                                           bias.data_ptr(), cc.data_ptr(), C, M, int(k), _METRIC_CODE[metric],
+                                           os_.data_ptr(), oi.data_ptr(), _lib.stream_ptr(Qf.device)),
+               "lzk_store_rerank")
+    return os_, oi
