@@ -310,25 +310,50 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
   float qq = 0.f;
   for (int d = lane; d < D; d += 64) qq = fmaf(qr[d], qr[d], qq);
   qq = wave_sum(qq);
+  // 16 candidates per pass, 4 lanes each (lane = 4 * c + part): every lane
+  // streams its quarter of one row with independent float4 loads, so the
+  // pass costs one row-read latency instead of one per candidate
+  const int part = lane & 3, cl = lane >> 2;
   float my_s = LZK_NEG_INF;
   long my_r = -1;
-  for (int c = 0; c < C; ++c) {
-    const long r = cand[(long)q * C + c];  // wave-uniform
-    if (r < 0) continue;
-    const float* xr = X + r * ldx;
+  const bool vec = (D % 16) == 0 && (ldq % 4) == 0 && (ldx % 4) == 0;
+  for (int c0 = 0; c0 < C; c0 += 16) {
+    const int c = c0 + cl;
+    const long r = c < C ? cand[(long)q * C + c] : -1;
     float acc = 0.f;
-    for (int d = lane; d < D; d += 64) acc = fmaf(qr[d], xr[d], acc);
-    acc = wave_sum(acc);
-    float sc;
-    if (metric == 0) {
-      sc = 2.f * acc + bias[r] - qq;
-    } else if (metric == 2) {
-      const float nr = sqrtf(sqn[r]);
-      sc = acc / (nr > 0.f ? nr : 1.f) + bias[r];
-    } else {
-      sc = acc + bias[r];
+    if (r >= 0) {
+      const float* xr = X + r * ldx;
+      if (vec) {
+        for (int d = part * 4; d < D; d += 16) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + d);
+          const float4 qv = *reinterpret_cast<const float4*>(qr + d);
+          acc = fmaf(qv.x, xv.x, acc);
+          acc = fmaf(qv.y, xv.y, acc);
+          acc = fmaf(qv.z, xv.z, acc);
+          acc = fmaf(qv.w, xv.w, acc);
+        }
+      } else {
+        for (int d = part; d < D; d += 4) acc = fmaf(qr[d], xr[d], acc);
+      }
     }
-    if (lane == c) { my_s = sc; my_r = r; }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    float sc = LZK_NEG_INF;
+    if (r >= 0) {
+      if (metric == 0) {
+        sc = 2.f * acc + bias[r] - qq;
+      } else if (metric == 2) {
+        const float nr = sqrtf(sqn[r]);
+        sc = acc / (nr > 0.f ? nr : 1.f) + bias[r];
+      } else {
+        sc = acc + bias[r];
+      }
+    }
+    // candidate c0 + j's result sits in lane 4 j; lane c0 + j takes it
+    const int src = 4 * ((lane - c0) & 15);
+    const float s2 = __shfl(sc, src, 64);
+    const long r2 = __shfl(r, src, 64);
+    if (lane >= c0 && lane < c0 + 16 && lane < C) { my_s = s2; my_r = r2; }
   }
   // rank among the wave's (score, row) pairs; -inf scores are empty
   const bool live = lane < C && my_r >= 0 && my_s != LZK_NEG_INF;

@@ -66,6 +66,31 @@ class NodeView(Node):
         return v
 
     @classmethod
+    def of_rows(cls, g: TenantGraph, rows_lists) -> List[List["NodeView"]]:
+        """``[[of(g, r) for r in rows if r >= 0] for rows in rows_lists]`` with
+        the view cache bound once (the per-batch result mapping of the search
+        paths: ~10k rows per 1024-query batch)."""
+        cache = g.__dict__.setdefault("_node_views", {})
+        get = cache.get
+        new = object.__new__
+        out = []
+        for rows in rows_lists:
+            lst = []
+            for r in rows:
+                if r < 0:
+                    continue
+                v = get(r)
+                if v is None:
+                    v = new(cls)
+                    d = v.__dict__
+                    d["_g"] = g
+                    d["_r"] = r
+                    cache[r] = v
+                lst.append(v)
+            out.append(lst)
+        return out
+
+    @classmethod
     def adopt(cls, node: Node, g: TenantGraph, r: int) -> "NodeView":
         cache = g.__dict__.setdefault("_node_views", {})
         if type(node) is Node:

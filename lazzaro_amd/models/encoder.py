@@ -22,6 +22,7 @@ import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from ..ops import encoder_ops as E
@@ -236,15 +237,19 @@ class SentenceEncoder:
         if packed is None:
             packed = self.device.type == "cuda" and ids.device.type == "cpu" and lens.device.type == "cpu"
         if packed:
-            lens_h = lens.to(torch.int64).cpu()
-            S_eff = int(lens_h.max()) if B else 1
-            mask = torch.arange(S)[None, :] < lens_h[:, None]
-            ids_p = _to_dev(ids.cpu()[mask], self.device)
-            pos_p = _to_dev(torch.arange(S).expand(B, S)[mask], self.device)
-            cu_h = torch.zeros(B + 1, dtype=torch.int64)
-            cu_h[1:] = torch.cumsum(lens_h, 0)
-            cu = _to_dev(cu_h, self.device)
-            lens = _to_dev(lens_h, self.device)
+            # host-side packing in numpy: single-threaded and ~0.5 ms for 1024 x 32
+            # tokens, where torch's CPU ops fan tiny work out to the intra-op
+            # thread pool (tens of ms on a shared host)
+            lens_n = lens.cpu().numpy().astype(np.int64)
+            ids_n = ids.cpu().numpy()
+            S_eff = int(lens_n.max()) if B else 1
+            mask = np.arange(S)[None, :] < lens_n[:, None]
+            ids_p = _to_dev(torch.from_numpy(np.ascontiguousarray(ids_n[mask])), self.device)
+            pos_p = _to_dev(torch.from_numpy(np.broadcast_to(np.arange(S, dtype=np.int32), (B, S))[mask]), self.device)
+            cu_n = np.zeros(B + 1, dtype=np.int64)
+            np.cumsum(lens_n, out=cu_n[1:])
+            cu = _to_dev(torch.from_numpy(cu_n), self.device)
+            lens = _to_dev(torch.from_numpy(lens_n), self.device)
             x = E.embed_ln(ids_p, S_eff, p["word"], p["pos"], p["type"], p["emb_g"], p["emb_b"], c.eps, pos=pos_p)
             S = S_eff
         else:
