@@ -81,6 +81,8 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
 LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 256, 1 << 20, 8.0
+# store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
+RERANK_KERNEL = os.environ.get("LZK_RERANK_KERNEL", "1") != "0"
 # cos_topk(min_score=): kernel threshold slack below min_score. Unit rows and
 # queries rounded to bf16 (relative 2^-9 each) move a cosine by at most
 # 2^-8 * sum|q_i x_i| <= 2^-8 ~ 0.0039, plus fp32 accumulation order.
@@ -1719,7 +1721,7 @@ class TenantGraph:
         return self._pad_k(best_s, best_i, k)
 
     def _rerank_store(self, Qf, cand, k, metric, bias):
-        if self.on_gpu and 0 < cand.shape[1] <= 64 and metric in ("l2", "ip", "cosine"):
+        if self.on_gpu and RERANK_KERNEL and 0 < cand.shape[1] <= 64 and metric in ("l2", "ip", "cosine"):
             from ..ops.tenant_ops import store_rerank
             return store_rerank(Qf, self.emb32, self.sqn, bias, cand, k, metric)
         valid = cand >= 0
