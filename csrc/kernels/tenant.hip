@@ -375,6 +375,73 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
   }
 }
 
+
+// Embedding-row writes of a small node insert in ONE launch (the consolidation
+// segments insert ~20 facts, 43 times per 128-conversation step): per row j,
+// x = e32[j] * has[j] goes to emb32[rows[j]], its bf16 copy to emb16, the
+// per-row symmetric int8 copy of the bf16 values + scale (max|x|/127, 1 for a
+// zero row) to emb8 / rs8 (the store search's int8 scan), |x|^2 (fp64 sum,
+// stored fp32) to sqn, x_d^2 to the per-dimension sums (fp64 atomics), and
+// max | |x| - 1 | over the valid rows / the largest row scale to two device
+// maxima (positive floats, max on the bits). Same values as the torch path
+// it replaces (ops/search.py quantize_i8_rows: round half to even).
+__global__ __launch_bounds__(256) void tg_write_emb_kernel(
+    const float* __restrict__ x, long ldx, const unsigned char* __restrict__ has, int m, int D,
+    const long* __restrict__ rows, float* __restrict__ emb32, long ld32, u16* __restrict__ emb16, long ld16,
+    signed char* __restrict__ emb8, long ld8, float* __restrict__ rs8, float* __restrict__ sqn,
+    double* __restrict__ sumsq, float* __restrict__ rs_max, float* __restrict__ dv_max) {
+  __shared__ double red_d[4];
+  __shared__ float red_f[4];
+  const int j = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float hv = (has == nullptr || has[j]) ? 1.f : 0.f;
+  const long r = rows[j];
+  float v[4], vb[4];
+  double s2 = 0.0;
+  float am = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int d = t + 256 * c;
+    v[c] = vb[c] = 0.f;
+    if (d < D) {
+      v[c] = x[(long)j * ldx + d] * hv;
+      emb32[r * ld32 + d] = v[c];
+      const u16 b = f32_to_bf16(v[c]);
+      if (emb16) emb16[r * ld16 + d] = b;
+      vb[c] = bf16_to_f32(b);
+      const double q2 = (double)v[c] * (double)v[c];
+      s2 += q2;
+      if (sumsq) atomicAdd(sumsq + d, q2);
+      am = fmaxf(am, fabsf(vb[c]));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    s2 += __shfl_xor(s2, o, 64);
+    am = fmaxf(am, __shfl_xor(am, o, 64));
+  }
+  if (lane == 0) { red_d[w] = s2; red_f[w] = am; }
+  __syncthreads();
+  s2 = red_d[0] + red_d[1] + red_d[2] + red_d[3];
+  am = fmaxf(fmaxf(red_f[0], red_f[1]), fmaxf(red_f[2], red_f[3]));
+  if (emb8) {
+    const float sc = am > 0.f ? am / 127.f : 1.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int d = t + 256 * c;
+      if (d < D) emb8[r * ld8 + d] = (signed char)fminf(fmaxf(rintf(vb[c] / sc), -127.f), 127.f);
+    }
+    if (t == 0) {
+      rs8[r] = sc;
+      if (rs_max) atomicMax(reinterpret_cast<int*>(rs_max), __float_as_int(sc));
+    }
+  }
+  if (t == 0) {
+    sqn[r] = (float)s2;
+    if (dv_max && hv > 0.f) atomicMax(reinterpret_cast<int*>(dv_max), __float_as_int((float)fabs(sqrt(s2) - 1.0)));
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C ABI
@@ -503,5 +570,15 @@ LZK_EXPORT int lzk_store_rerank(const float* Q, long ldq, const float* X, long l
   if (C <= 0 || C > 64 || M <= 0 || k <= 0 || metric < 0 || metric > 2) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(store_rerank_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Q, ldq,
                      X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_write_emb(const float* x, long ldx, const unsigned char* has, int m, int D, const long* rows,
+                                float* emb32, long ld32, void* emb16, long ld16, void* emb8, long ld8, float* rs8,
+                                float* sqn, double* sumsq, float* rs_max, float* dv_max, void* stream) {
+  if (m <= 0) return 0;
+  if (D <= 0 || D > 1024 || (emb8 && !rs8)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tg_write_emb_kernel, dim3((unsigned)m), dim3(256), 0, (hipStream_t)stream, x, ldx, has, m, D,
+                     rows, emb32, ld32, (u16*)emb16, ld16, (signed char*)emb8, ld8, rs8, sqn, sumsq, rs_max, dv_max);
   return (int)hipGetLastError();
 }

@@ -81,6 +81,8 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
 LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 256, 1 << 20, 8.0
+# inserts of at most this many rows write their embedding columns in one launch
+WRITE_EMB_MAX_ROWS = 8192
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
 RERANK_KERNEL = os.environ.get("LZK_RERANK_KERNEL", "1") != "0"
 # cos_topk(min_score=): kernel threshold slack below min_score. Unit rows and
@@ -546,13 +548,27 @@ class TenantGraph:
                 has = torch.as_tensor(ok, dtype=torch.bool).to(dev)
                 for j, v in odd.items():
                     self.odd_emb[rl[j]] = v
+            mc = m  # rows left to the chunked path
+            if self.on_gpu and m <= WRITE_EMB_MAX_ROWS and self.dim <= 1024 and e32.is_cuda:
+                # small inserts (consolidation segments, chat turns): every
+                # embedding column in one launch (tenant.hip tg_write_emb_kernel)
+                from ..ops.tenant_ops import write_emb
+                dv = torch.zeros(1, dtype=torch.float32, device=dev)
+                write_emb(self, e32, None if info is None else has, rt, dv)
+                self.n_sumsq += m
+                self.has_emb[rt] = has.to(torch.uint8)
+                if info is None or any(info[0]):
+                    self._norm_dev_pending.append(dv[0])
+                    if len(self._norm_dev_pending) >= 256:
+                        self._norm_dev_pending = [torch.stack(self._norm_dev_pending).max()]
+                mc = 0  # columns written; skip the chunked path below
             # row chunks: a 10M-row load must not hold fp64 copies of the
             # whole [m, D] block (the squares were 2 x 60 GB of temporaries)
             contig = isinstance(rl, range)
-            nrm2 = torch.empty(m, dtype=torch.float64, device=dev)
+            nrm2 = torch.empty(mc, dtype=torch.float64, device=dev)
             ch = max(1, (1 << 28) // max(1, 8 * self.dim))  # ~256 MB of fp64 per chunk
-            for a in range(0, m, ch):
-                b = min(m, a + ch)
+            for a in range(0, mc, ch):
+                b = min(mc, a + ch)
                 x = e32[a:b]
                 if info is not None:
                     x = x * has[a:b, None].to(x.dtype)
@@ -565,10 +581,11 @@ class TenantGraph:
                 if self.emb16 is not None:
                     self.emb16[r, : self.dim] = x.to(torch.bfloat16)
                 self._write_lowp(rt[a:b], x)
-            self.sqn[rt] = nrm2.float()
-            self.n_sumsq += m
-            self.has_emb[rt] = has.to(torch.uint8)
-            if info is None or any(info[0]):
+            if mc:
+                self.sqn[rt] = nrm2.float()
+                self.n_sumsq += m
+                self.has_emb[rt] = has.to(torch.uint8)
+            if mc and (info is None or any(info[0])):
                 dv = torch.where(has, (nrm2.sqrt() - 1.0).abs(), torch.zeros_like(nrm2)).max()
                 if dv.is_cuda:
                     self._norm_dev_pending.append(dv)

@@ -22,6 +22,7 @@ P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
 D_ = C.c_double
 
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
+_lib.register("lzk_tg_write_emb", I, [P, L, P, I, I, P, P, L, P, L, P, L, P, P, P, P, P, P])
 _lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
@@ -502,3 +503,23 @@ def store_rerank(Qf: torch.Tensor, X: torch.Tensor, sqn: torch.Tensor, bias: tor
                                            os_.data_ptr(), oi.data_ptr(), _lib.stream_ptr(Qf.device)),
                "lzk_store_rerank")
     return os_, oi
+
+
+def write_emb(g, e32: torch.Tensor, has: Optional[torch.Tensor], rows: torch.Tensor, dv_max: torch.Tensor) -> None:
+    """Embedding columns of ``rows`` from fp32 ``e32`` [m, dim] in one launch
+    (tenant.hip tg_write_emb_kernel): emb32, emb16, the int8 copy + row
+    scale, sqn, the per-dimension fp64 sums of squares, and device maxima of
+    the row scale (``g._rs8_max``) and of | |x| - 1 | (``dv_max`` [1])."""
+    m, D = e32.shape
+    x = e32.contiguous() if e32.dtype == torch.float32 else e32.float().contiguous()
+    r = rows.to(torch.long).contiguous()
+    h = has.to(torch.uint8).contiguous() if has is not None else None
+    i8 = g.emb8 is not None and g.emb8.dtype == torch.int8
+    _lib.check(_lib.lib().lzk_tg_write_emb(
+        x.data_ptr(), x.stride(0), _lib.ptr(h), m, D, r.data_ptr(), g.emb32.data_ptr(), g.emb32.stride(0),
+        _lib.ptr(g.emb16), g.emb16.stride(0) if g.emb16 is not None else 0,
+        g.emb8.data_ptr() if i8 else None, g.emb8.stride(0) if i8 else 0, g.rs8.data_ptr() if i8 else None,
+        g.sqn.data_ptr(), g.sumsq.data_ptr(), g._rs8_max.data_ptr() if i8 else None, dv_max.data_ptr(),
+        _lib.stream_ptr(x.device)), "lzk_tg_write_emb")
+    if g.emb8 is not None and not i8:  # fp8 copy: the torch quantiser
+        g._write_lowp(r, x * h[:, None].to(x.dtype) if h is not None else x)

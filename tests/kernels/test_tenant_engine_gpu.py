@@ -418,3 +418,36 @@ def test_store_rerank_kernel_matches_torch_gpu(metric):
         assert [b for _, b in got] == [b for _, b in pairs]
         assert all(abs(a - b[0]) <= 1e-3 * (1 + abs(b[0])) for (a, _), b in zip(got, pairs))
         assert all(v == -1 for v in r[q, len(pairs):].tolist())
+
+
+def test_write_emb_kernel_matches_torch_path_gpu():
+    """Small inserts write every embedding column in one launch
+    (tg_write_emb_kernel); the columns equal the chunked torch path's."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    gen = torch.Generator(device=DEV).manual_seed(21)
+    D = 768
+    X = torch.randn(300, D, device=DEV, generator=gen) * 0.05
+    X[7] = 0.0
+    lists = [x.tolist() for x in X[:40].cpu()]
+    lists[3] = None  # no embedding
+    saved = TG.WRITE_EMB_MAX_ROWS
+    gs = []
+    try:
+        for lim in (8192, 0):
+            TG.WRITE_EMB_MAX_ROWS = lim
+            g = TenantGraph(device=DEV)
+            g.add_nodes([f"a{i}" for i in range(300)], [""] * 300, X, shard=g.shard_id("work"), stored=True)
+            g.add_nodes([f"b{i}" for i in range(40)], [""] * 40, lists, shard=g.shard_id("work"), stored=True)
+            g.add_nodes(["a5", "a9"], ["", ""], X[100:102], shard=g.shard_id("work"), stored=True)  # replace by id
+            gs.append(g)
+    finally:
+        TG.WRITE_EMB_MAX_ROWS = saved
+    k, t = gs
+    n = k.n
+    assert n == t.n == 340
+    for col in ("emb32", "emb16", "emb8", "rs8", "sqn", "has_emb"):
+        a, b = getattr(k, col)[:n], getattr(t, col)[:n]
+        assert torch.equal(a, b), col
+    torch.testing.assert_close(k.sumsq, t.sumsq, rtol=1e-12, atol=1e-12)
+    assert float(k._rs8_max) == float(t._rs8_max)
+    assert abs(k.max_norm_dev - t.max_norm_dev) < 1e-6
