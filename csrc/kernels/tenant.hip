@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256) void tg_write_emb_kernel(
   s2 = red_d[0] + red_d[1] + red_d[2] + red_d[3];
   am = fmaxf(fmaxf(red_f[0], red_f[1]), fmaxf(red_f[2], red_f[3]));
   if (emb8) {
-    const float sc = am > 0.f ? am / 127.f : 1.f;
+    const float sc = am > 0.f ? am * (1.f / 127.f) : 1.f;  // torch: amax / 127.0 = amax * (1/127)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int d = t + 256 * c;
