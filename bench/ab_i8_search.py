@@ -79,12 +79,6 @@ def main():
         Q, S.flat_topk(g.emb16[:N], q16, 16, bias=bias, alpha=2.0)[1], 10, "l2", bias))
     out["i8_store_search_ms"], (s8, r8) = timeit(lambda: g._rerank_store(
         Q, g._i8_candidates(Q, q16, 16, bias, 2.0)[1], 10, "l2", bias))
-    import ctypes
-    L.lzk_set_i8_opt.argtypes = [ctypes.c_int]
-    for opt in (56, 0):
-        L.lzk_set_i8_opt(opt)
-        out[f"i8_store_search_ms_opt{opt}"], _ = timeit(lambda: g._rerank_store(
-            Q, g._i8_candidates(Q, q16, 16, bias, 2.0)[1], 10, "l2", bias))
     for stride in (32, 128, 64):
         S.CAND_STRIDE = stride
         out[f"i8_store_search_ms_stride{stride}"], _ = timeit(lambda: g._rerank_store(

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_kernel(
 // tile i+1 overlaps the epilogue of tile i and no epilogue global load can
 // drain the in-flight DMA.
 constexpr int EPI_OFF = 8 * HALF;               // u16 offset of the epilogue area (128 KiB)
-constexpr int EPI_ARRAYS = 5;                   // thr | bias | row label | query label | thr2
+constexpr int EPI_ARRAYS = 7;  // thr | bias | row label | query label | thr2 | row scale | query scale (int8)
 constexpr int CNT_OFF = EPI_OFF + 2 * EPI_ARRAYS * 256 * 2;  // u16 offset of the block's append counter
 constexpr int CAND_P_LDS = LDS_BYTES + 2 * EPI_ARRAYS * 256 * 4 + 16;
 typedef __attribute__((address_space(3))) int lds_int;
@@ -125,6 +125,10 @@ struct BlkCands {
   int4* buf;  // [grid][cap]
   int cap;
   int* cnt;   // [grid] records written
+  // int8 scan (MMA::kInt) only: fp32 row / query scales, staged into the
+  // epilogue's slots 5 / 6 with the other per-tile operands
+  const float* rs = nullptr;
+  const float* qs = nullptr;
 };
 
 // DUAL: one GEMM pass serves two searches of the same queries -- list A keeps
@@ -167,16 +171,17 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
 #pragma unroll
     for (int g = wave; g < 4 * EPI_ARRAYS; g += 8) {
       const int a = g >> 2, c = g & 3;  // wave-uniform
-      // MMA::kInt: arrays 2 / 3 carry the fp32 row / query scales (no labels)
-      const bool need = a == 0 || (a == 1 && HAS_BIAS) || ((a == 2 || a == 3) && (HAS_LABEL || MMA::kInt)) ||
-                        (a == 4 && DUAL);
+      const bool need = a == 0 || (a == 1 && HAS_BIAS) || ((a == 2 || a == 3) && HAS_LABEL) || (a == 4 && DUAL) ||
+                        ((a == 5 || a == 6) && MMA::kInt);
       if (!need) continue;
       const void* src;
       if (a == 0) src = thr + min(q0 + c * 64 + lane, nq - 1);
       else if (a == 1) src = bias + min(r0 + c * 64 + lane, nrows - 1);
       else if (a == 2) src = row_label + min(r0 + c * 64 + lane, nrows - 1);
       else if (a == 3) src = q_label + min(q0 + c * 64 + lane, nq - 1);
-      else src = thr2 + min(q0 + c * 64 + lane, nq - 1);
+      else if (a == 4) src = thr2 + min(q0 + c * 64 + lane, nq - 1);
+      else if (a == 5) src = blk.rs + min(r0 + c * 64 + lane, nrows - 1);
+      else src = blk.qs + min(q0 + c * 64 + lane, nq - 1);
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
                                        (lds_void_t*)(epi + par * (EPI_ARRAYS * 256) + a * 256 + c * 64), 4, 0, 0);
     }
@@ -259,15 +264,15 @@ __global__ __launch_bounds__(NT, 1) void flat_cand_persistent_kernel(
         th[j] = (qq[j] < nq) ? e_thr[qlo] : __builtin_huge_valf();
         th2[j] = (DUAL && qq[j] < nq) ? e_thr2[qlo] : __builtin_huge_valf();
         ql[j] = HAS_LABEL ? e_qlab[qlo] : -1;
-        // int8 scan: the query's scale (label slot 3) joins alpha
-        al[j] = MMA::kInt ? alpha * reinterpret_cast<const float*>(e_qlab)[qlo] : alpha;
+        // int8 scan: the query's scale (slot 6) joins alpha
+        al[j] = MMA::kInt ? alpha * e_thr[6 * 256 + qlo] : alpha;
       }
       if constexpr (MMA::kInt) {
-        // int32 sums -> float * the row's scale (label slot 2), in place: the
+        // int32 sums -> float * the row's scale (slot 5), in place: the
         // rest of the epilogue (column prefilter, per-score test) is the bf16
         // one with alpha = alpha * qscale. Exact: |acc| < 2^24 for D <= 1024.
         typedef int i32x4 __attribute__((ext_vector_type(4)));
-        const float* e_rs = reinterpret_cast<const float*>(e_lab);
+        const float* e_rs = e_thr + 5 * 256;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const f32x4 rs = *reinterpret_cast<const f32x4*>(e_rs + wr * 128 + i * 16 + 4 * (lane >> 4));
@@ -394,7 +399,6 @@ constexpr int kCandOpt = 24;
 // (profiles/ab_dual_r1.json) 0: 16.27 ms, body2: 15.65, +prefilter 15.90.
 constexpr int kDualOpt = 8;
 int g_dual_opt = -1;  // A/B override of kCandOpt for the dual kernel (lzk_set_dual_opt)
-int g_i8_opt = 0;    // A/B override of kCandOpt for the int8 scan (lzk_set_i8_opt)
 int g_g256_opt = 0;  // A/B override of kCandOpt for the plain (no bias / label) variant; 100 = OPT 0
 int g_n_cu = 0;
 
@@ -606,7 +610,7 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict
                                                            const float* __restrict__ bias, float alpha,
                                                            const int* __restrict__ cnt, int cap,
                                                            float* __restrict__ cs, const int* __restrict__ ci,
-                                                           const float* __restrict__ cut) {
+                                                           const float* __restrict__ cut, float floor) {
   const int q = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = min(cnt[q] & 0x3fffffff, cap);
@@ -652,7 +656,8 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (lane == 0) cs[idx] = alpha * acc + (bias ? bias[r] : 0.f);
+    const float sc = alpha * acc + (bias ? bias[r] : 0.f);
+    if (lane == 0) cs[idx] = sc >= floor ? sc : LZK_NEG_INF;  // below the caller's floor: dropped
     }
   }
 }
@@ -702,7 +707,6 @@ LZK_EXPORT int lzk_flat_top1_grouped(const void* C, long ldc, const void* Xq, lo
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
-LZK_EXPORT void lzk_set_i8_opt(int o) { g_i8_opt = o; }
 LZK_EXPORT int lzk_set_stamp_buffer(void* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p));
 }
@@ -942,10 +946,10 @@ LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
 // Exact bf16 re-score of candidate lists in place (see cand_rescore_kernel).
 LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long ldq, int nq, int D, const float* bias,
                                 float alpha, const int* cnt, int cap, float* cs, const int* ci, const float* cut,
-                                void* stream) {
+                                float floor, void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(cand_rescore_kernel, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, (const u16*)X16, ldx,
-                     (const u16*)Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut);
+                     (const u16*)Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor);
   return (int)hipGetLastError();
 }
 
@@ -961,7 +965,7 @@ LZK_EXPORT int lzk_flat_cand_i8(const void* X8, long ldx_bytes, int nrows, const
       cap <= 0 || !rscale || !qscale || !(alpha > 0.f))
     return (int)hipErrorInvalidValue;
   if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;
-  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt};
+  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt, rscale, qscale};
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
@@ -975,9 +979,8 @@ LZK_EXPORT int lzk_flat_cand_i8(const void* X8, long ldx_bytes, int nrows, const
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X8;
   const u16* q = (const u16*)Q8;
-  // the scales ride in the label slots of the epilogue staging (HAS_LABEL = false)
-  const int* rs = (const int*)rscale;
-  const int* qs = (const int*)qscale;
+  const int* rs = nullptr;  // no labels
+  const int* qs = nullptr;
 #define LZK_GIO(B, O)                                                                                               \
   do {                                                                                                              \
     (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, false, false, O, MmaI8>,                  \
@@ -987,15 +990,51 @@ LZK_EXPORT int lzk_flat_cand_i8(const void* X8, long ldx_bytes, int nrows, const
                        n_qt, (int)nblk, cap, cnt, cs, ci, (const float*)nullptr, (int*)nullptr, (float*)nullptr,    \
                        (int*)nullptr, blk);                                                                         \
   } while (0)
-  // g_i8_opt (A/B only): 56 = + cross-tile prefetch (OPT bit 5; KS = D_bytes / 128 must be even)
-  const bool pre = g_i8_opt == 56 && (D_bytes / 128) % 2 == 0;
-  if (bias) {
-    if (pre) LZK_GIO(true, 56);
-    else LZK_GIO(true, kCandOpt);
-  } else {
-    if (pre) LZK_GIO(false, 56);
-    else LZK_GIO(false, kCandOpt);
-  }
+  // (a cross-tile prefetch variant, OPT bit 5, measured 11.0 vs 10.0 ms per
+  // store search on 10M x 768 x 1024 -- bench/ab_i8_search.py -- and spills)
+  if (bias) LZK_GIO(true, kCandOpt);
+  else LZK_GIO(false, kCandOpt);
 #undef LZK_GIO
+  return (int)hipGetLastError();
+}
+
+// int8 dual candidate pass (rows / queries int8 bytes with fp32 scales, see
+// lzk_flat_cand_i8; labels as lzk_flat_cand_dual): list A unfiltered (thr),
+// list B label-filtered (thr2), scores alpha * qscale * <q8, x8> * rscale + bias.
+LZK_EXPORT int lzk_flat_cand_dual_i8(const void* X8, long ldx_bytes, int nrows, const void* Q8, long ldq_bytes,
+                                     int nq, int D_bytes, const float* bias, const float* rscale,
+                                     const float* qscale, const int* row_label, const int* q_label, float alpha,
+                                     const float* thr, const float* thr2, int cap, int* cnt, float* cs, int* ci,
+                                     int* cnt2, float* cs2, int* ci2, void* blk_buf, int blk_cap, int* blk_cnt,
+                                     void* stream) {
+  if (D_bytes % 128 != 0 || D_bytes > 1024 || (ldx_bytes | ldq_bytes) % 16 != 0 || nq <= 0 || nrows <= 0 ||
+      cap <= 0 || !rscale || !qscale || !row_label || !q_label || !(alpha > 0.f))
+    return (int)hipErrorInvalidValue;
+  if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;
+  const BlkCands blk{(int4*)blk_buf, blk_cap, blk_cnt, rscale, qscale};
+  const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
+  const long nblk = (long)n_rt * n_qt;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (g_n_cu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
+      g_n_cu = 256;
+  }
+  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X8;
+  const u16* q = (const u16*)Q8;
+#define LZK_GDI(B)                                                                                                  \
+  do {                                                                                                              \
+    (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, true, true, kCandOpt, MmaI8>,             \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, CAND_P_LDS);                              \
+    hipLaunchKernelGGL((flat_cand_persistent_kernel<B, true, true, kCandOpt, MmaI8>), dim3(grid), dim3(NT),        \
+                       CAND_P_LDS, st, x, ldx_bytes / 2, nrows, q, ldq_bytes / 2, nq, D_bytes / 2, bias, row_label, \
+                       q_label, alpha, thr, n_qt, (int)nblk, cap, cnt, cs, ci, thr2, cnt2, cs2, ci2, blk);          \
+  } while (0)
+  if (bias) LZK_GDI(true);
+  else LZK_GDI(false);
+#undef LZK_GDI
   return (int)hipGetLastError();
 }

@@ -1574,8 +1574,17 @@ class TenantGraph:
             if dual_label is not None:
                 ql = dual_label.to(dev, torch.int32).contiguous()
                 floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
-                (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
-                                                  bias=bias, floor=floor)
+                if (self.emb8 is not None and self.emb8.dtype == torch.int8 and self.unit_rows()
+                        and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS):
+                    # the int8 dual scan: same lists (error cut + bf16 re-score)
+                    from ..ops.search import flat_topk_dual_i8
+                    q8, qs, margin = self._i8_query(q16, 1.0)
+                    (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
+                                                         row_label=lab.contiguous(), q_label=ql, bias=bias,
+                                                         margin=margin, floor=floor)
+                else:
+                    (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
+                                                      bias=bias, floor=floor)
                 return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
             _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
             return self._rerank_cos(Qn, ra, k)
@@ -1680,8 +1689,16 @@ class TenantGraph:
         of the tenant's rows), var <delta, q> <= |q|^2 s_max^2 / 12, and
         |<delta, eta>| <= s_max / 2 * |eta|_1 (worst case, added as a floor);
         the margin is LOWP_MARGIN_Z standard deviations plus that floor."""
-        from ..ops.search import flat_topk_i8, quantize_i8_rows
-        n, d = self.n, self.dim
+        from ..ops.search import flat_topk_i8
+        q8, qs, margin = self._i8_query(q16, alpha)
+        return flat_topk_i8(self.emb8, self.rs8, q8, qs, self.emb16[:self.n], q16, kc, bias=bias, alpha=alpha,
+                            margin=margin)
+
+    def _i8_query(self, q16: torch.Tensor, alpha: float):
+        """int8 queries + per-query scales + the error-model margin of
+        :meth:`_i8_candidates` (device tensors, no host sync)."""
+        from ..ops.search import quantize_i8_rows
+        d = self.dim
         q8, qs = quantize_i8_rows(q16)
         eta = q8.float() * qs[:, None] - q16.float()
         mu2 = (self.sumsq / max(self.n_sumsq, 1)).float()
@@ -1690,8 +1707,7 @@ class TenantGraph:
         v2 = (q16.float() ** 2).sum(1) * (smax * smax / 12.0)
         floor = 0.5 * smax * eta.abs().sum(1)
         margin = (abs(alpha) * (LOWP_MARGIN_Z * torch.sqrt(v1 + v2) + floor)).contiguous()
-        return flat_topk_i8(self.emb8, self.rs8, q8, qs, self.emb16[:n], q16, kc, bias=bias, alpha=alpha,
-                            margin=margin)
+        return q8, qs, margin
 
     def _fp8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
         """Store-search candidates from the fp8 scan (rows in ``emb8``),

@@ -298,7 +298,11 @@ _lib.register("lzk_flat_cand_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
                                            _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
 _lib.register("lzk_cand_grid_f8", _lib.I, [_lib.I, _lib.I])
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
-                                           _lib.I, _lib.P, _lib.P, _lib.P, _lib.P])
+                                           _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P])
+_lib.register("lzk_flat_cand_dual_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P,
+                                                _lib.P, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.P, _lib.I,
+                                                _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I,
+                                                _lib.P, _lib.P])
 _lib.register("lzk_flat_cand_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P,
                                            _lib.P, _lib.F, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I,
                                            _lib.P, _lib.P])
@@ -353,7 +357,7 @@ def flat_topk_fp8(X8: torch.Tensor, Q8: torch.Tensor, scale2: float, X16: torch.
                                  ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
     _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
                                   _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(), None,
-                                  st), "lzk_cand_rescore")
+                                  float("-inf"), st), "lzk_cand_rescore")
     return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
 
 
@@ -418,6 +422,18 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
                "lzk_flat_cand_i8")
     _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
                                  ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
+    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
+
+
+def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None):
+    """int8 candidate lists -> exact bf16 scores for the entries that can
+    still reach the query's top-k: cut = (k-th best int8 score) - 2 * margin
+    (see :func:`flat_topk_i8`); the others become -inf without a row read."""
+    L = _lib.lib()
+    nq, Dp = Q16.shape
+    dev = Q16.device
+    st = _lib.stream_ptr(dev)
     cut = None
     if margin is not None:
         s8 = torch.empty((nq, kslot), dtype=torch.float32, device=dev)
@@ -430,8 +446,56 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
         cut = torch.nan_to_num(cut, nan=float("-inf"))
     _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
                                   _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(),
-                                  _lib.ptr(cut), st), "lzk_cand_rescore")
-    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
+                                  _lib.ptr(cut), float("-inf") if floor is None else float(floor), st),
+               "lzk_cand_rescore")
+
+
+def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
+                      X16: torch.Tensor, Q16: torch.Tensor, k: int, *, row_label, q_label, bias=None,
+                      alpha: float = 1.0, margin=None, floor: float = None):
+    """:func:`flat_topk_dual` with the candidate scan on the int8 MFMA (the
+    rows' int8 copy, see :func:`flat_topk_i8`): both thresholds (the sampled
+    bf16 k-th bests, raised to ``floor``) are lowered by ``margin``, both lists
+    are re-scored from the bf16 rows above their error cut, then selected
+    exactly -- the same lists as the bf16 dual scan.
+    Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
+    L = _lib.lib()
+    nq, Dp = Q16.shape
+    N = X16.shape[0]
+    kslot = L.lzk_flat_topk_kslot(int(k))
+    assert kslot > 0 and X8.dtype == torch.int8 and Q8.dtype == torch.int8 and Dp % 128 == 0 and Dp <= 1024
+    assert row_label.dtype == torch.int32 and q_label.dtype == torch.int32 and alpha > 0
+    dev = X16.device
+    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
+    thr_b = _sample_threshold(X16, Q16, k, kslot, bias, row_label, q_label, alpha, S)
+    thr_a = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
+    if floor is not None:
+        thr_a = thr_a.clamp_min(float(floor))
+        thr_b = thr_b.clamp_min(float(floor))
+    if margin is not None:
+        thr_a, thr_b = thr_a - margin, thr_b - margin
+    thr_a, thr_b = thr_a.contiguous(), thr_b.contiguous()
+    cap = max(2048, 16 * kslot * S)
+    ca = _cand_lists(dev, nq, cap, 0)
+    cb = _cand_lists(dev, nq, cap, 1)
+    grid = L.lzk_cand_grid_f8(N, nq)
+    bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 2)
+    st = _lib.stream_ptr(dev)
+    qs = qscale.contiguous()
+    _lib.check(L.lzk_flat_cand_dual_i8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp,
+                                       _lib.ptr(bias), rscale.data_ptr(), qs.data_ptr(), row_label.data_ptr(),
+                                       q_label.data_ptr(), float(alpha), thr_a.data_ptr(), thr_b.data_ptr(), cap,
+                                       ca[0].data_ptr(), ca[1].data_ptr(), ca[2].data_ptr(), cb[0].data_ptr(),
+                                       cb[1].data_ptr(), cb[2].data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st),
+               "lzk_flat_cand_dual_i8")
+    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, ca[0].data_ptr(),
+                                 ca[1].data_ptr(), ca[2].data_ptr(), cb[0].data_ptr(), cb[1].data_ptr(),
+                                 cb[2].data_ptr(), st), "lzk_cand_gather")
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *ca, cap, floor=floor)
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *cb, cap, floor=floor)
+    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap)
+    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap)
+    return ra, rb
 
 
 # Speculative list-B threshold of flat_topk_dual (LZK_DUAL_SPEC=1): aim for

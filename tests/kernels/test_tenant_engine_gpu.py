@@ -455,3 +455,32 @@ def test_write_emb_kernel_matches_torch_path_gpu():
     torch.testing.assert_close(k.sumsq, t.sumsq, rtol=1e-12, atol=1e-12)
     assert abs(float(k._rs8_max) - float(t._rs8_max)) <= 2e-7 * float(t._rs8_max)
     assert abs(k.max_norm_dev - t.max_norm_dev) < 1e-6
+
+
+@pytest.mark.parametrize("floor", [None, 0.1])
+def test_flat_topk_dual_i8_matches_bf16_dual_gpu(floor):
+    """int8 dual scan (consolidation's dedupe / link candidates) == the bf16
+    dual scan: same rows in both lists, scores equal to rounding."""
+    from lazzaro_amd.ops.search import flat_topk_dual, flat_topk_dual_i8, quantize_i8_rows
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    N, D, nq = 1_200_000, 768, 512
+    C = torch.randn(64, D, device=DEV, generator=gen)
+    X = C[torch.randint(0, 64, (N,), device=DEV, generator=gen)] + 2.0 * torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    Q = X[torch.randint(0, N, (nq,), device=DEV, generator=gen)] + 0.5 * torch.randn(nq, D, device=DEV, generator=gen) / D ** 0.5
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
+    lab = torch.randint(0, 12, (N,), device=DEV, generator=gen, dtype=torch.int32)
+    ql = torch.randint(-1, 12, (nq,), device=DEV, generator=gen, dtype=torch.int32)
+    bias = torch.where(torch.rand(N, device=DEV, generator=gen) < 0.05, float("-inf"), 0.0).contiguous()
+    (sa, ra), (sb, rb) = flat_topk_dual(X16, Q16, 16, row_label=lab, q_label=ql, bias=bias, floor=floor)
+    X8, rs = quantize_i8_rows(X16)
+    Q8, qs = quantize_i8_rows(Q16)
+    margin = torch.full((nq,), 0.02, device=DEV)
+    (ta, ia), (tb, ib) = flat_topk_dual_i8(X8, rs, Q8, qs, X16, Q16, 16, row_label=lab, q_label=ql, bias=bias,
+                                           margin=margin, floor=floor)
+    for s0, r0, s1, r1 in ((sa, ra, ta, ia), (sb, rb, tb, ib)):
+        assert torch.equal(r0, r1)
+        fin = torch.isfinite(s0)
+        assert torch.equal(fin, torch.isfinite(s1))
+        assert torch.allclose(s0[fin], s1[fin], atol=1e-4, rtol=0)
