@@ -374,6 +374,11 @@ def main():
         return (time.perf_counter() - t1) / n * 1e3, out
 
     t_embed, Qe = timeit(lambda: emb.batch_embed_tensor(pool[0]))
+    t_embed_dev = None
+    if dev.type == "cuda" and hasattr(emb, "encoder"):  # the encoder alone (texts tokenised beforehand)
+        from lazzaro_amd.core.embedders import EMBED_PARTS
+        ids_, lens_ = emb.tok.encode_batch(pool[0], emb.max_len)
+        t_embed_dev, _ = timeit(lambda: emb.encoder.forward_streams(ids_, lens_, parts=EMBED_PARTS))
     t_store, (_, rows_e) = timeit(lambda: g.store_search(Qe, a.k, "l2"))
     Xb = bias = q16 = None
     t_kernel = t_lowp = None
@@ -456,7 +461,9 @@ def main():
         "recall_at_10": round(rec_api, 4),
         "recall_at_10_random_queries": round(rec_rand, 4),
         "recall_truth": "float64 exact L2 over the stored fp32 vectors",
-        "breakdown_ms": {"embed": round(t_embed, 3), "store_search": round(t_store, 3),
+        "breakdown_ms": {"embed": round(t_embed, 3),
+                         "embed_encoder_only": None if t_embed_dev is None else round(t_embed_dev, 3),
+                         "store_search": round(t_store, 3),
                          "raw_scan_kernel": None if t_kernel is None else round(t_kernel, 3),
                          "i8_candidate_search": None if t_lowp is None else round(t_lowp, 3),
                          "search_memories_batch_unpipelined": round(t_batch, 3)},
