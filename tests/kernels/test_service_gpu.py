@@ -130,6 +130,13 @@ def test_serve_stream_with_mutations_equals_serve(tmp_path):
     got = list(b.serve_stream(rounds))
     b.close()
     strip = lambda v: [x for x in v if not isinstance(x, str)]  # status strings carry timings
+    if [strip(x) for x in got] != [strip(x) for x in want]:  # a compact account of the mismatch
+        for r, (gr, wr) in enumerate(zip(got, want)):
+            for q, (gq, wq) in enumerate(zip(strip(gr), strip(wr))):
+                if gq != wq:
+                    print("MISMATCH round", r, "req", q, rounds[r][q][:3])
+                    print("  got ", [(d["id"], d["salience"], d["access_count"]) for d in gq] if isinstance(gq, list) else gq)
+                    print("  want", [(d["id"], d["salience"], d["access_count"]) for d in wq] if isinstance(wq, list) else wq)
     assert [strip(x) for x in got] == [strip(x) for x in want]
 
 
