@@ -81,6 +81,11 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
 LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 256, 1 << 20, 8.0
+# consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8). Off
+# by default: bench/bench_consolidate.py (random fact vectors) 17.3 -> 11.6 ms
+# per step's scan, but the clustered-topic row-sharded run of bench.py went
+# 175 -> 243 ms per step (profiles/r3_session2/README.md); LZK_DUAL_LOWP=1 on
+DUAL_LOWP = os.environ.get("LZK_DUAL_LOWP", "0") == "1"
 # inserts of at most this many rows write their embedding columns in one launch
 WRITE_EMB_MAX_ROWS = 8192
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
@@ -1574,7 +1579,7 @@ class TenantGraph:
             if dual_label is not None:
                 ql = dual_label.to(dev, torch.int32).contiguous()
                 floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
-                if (self.emb8 is not None and self.emb8.dtype == torch.int8 and self.unit_rows()
+                if (DUAL_LOWP and self.emb8 is not None and self.emb8.dtype == torch.int8 and self.unit_rows()
                         and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS):
                     # the int8 dual scan: same lists (error cut + bf16 re-score)
                     from ..ops.search import flat_topk_dual_i8
