@@ -83,6 +83,14 @@ def main():
         S.CAND_STRIDE = stride
         out[f"i8_store_search_ms_stride{stride}"], _ = timeit(lambda: g._rerank_store(
             Q, g._i8_candidates(Q, q16, 16, bias, 2.0)[1], 10, "l2", bias))
+    S.CAND_STRIDE = 64
+    for m in (128, 200):  # small batches: bf16 lane kernel vs the int8 scan with a mostly empty query tile
+        Qm, qm16 = Q[:m].contiguous(), q16[:m].contiguous()
+        out[f"bf16_store_search_ms_q{m}"], (_, ra) = timeit(lambda: g._rerank_store(
+            Qm, S.flat_topk(g.emb16[:N], qm16, 16, bias=bias, alpha=2.0)[1], 10, "l2", bias))
+        out[f"i8_store_search_ms_q{m}"], (_, rb) = timeit(lambda: g._rerank_store(
+            Qm, g._i8_candidates(Qm, qm16, 16, bias, 2.0)[1], 10, "l2", bias))
+        out[f"same_rows_q{m}"] = bool(torch.equal(ra, rb))
     out["same_rows"] = bool(torch.equal(r16, r8))
     out["same_scores"] = bool(torch.equal(s16, s8))
     # candidate-list sizes of the int8 pass and the entries re-scored

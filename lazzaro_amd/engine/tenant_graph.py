@@ -80,7 +80,7 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # fp8 candidate scan of the store search: large batches over large tenants
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
-LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 256, 1 << 20, 8.0
+LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 128, 1 << 20, 8.0
 # consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8). Off
 # by default: bench/bench_consolidate.py (random fact vectors) 17.3 -> 11.6 ms
 # per step's scan, but the clustered-topic row-sharded run of bench.py went
