@@ -171,7 +171,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--model", default="bge-base")
     ap.add_argument("--max-len", type=int, default=64)
-    ap.add_argument("--recall-queries", type=int, default=256)
+    ap.add_argument("--recall-queries", type=int, default=1024)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--prewarm-s", type=float, default=3.0, help="untimed GPU clock ramp before the warmup steps")
     ap.add_argument("--consolidate-steps", type=int, default=10,
@@ -232,7 +232,10 @@ def main():
         return MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, device=dev, db_dir=tmp,
                             load_from_disk=False, enable_async=False, max_buffer_size=2 * a.rows, user_id=user)
 
-    svc = DistributedMemoryService(comm, factory)
+    # under torch.distributed.run every exchange goes through the communicator,
+    # even at world 1: the RCCL all-to-all / all-gather calls of the N-GPU job
+    # run (and are timed) on one GPU
+    svc = DistributedMemoryService(comm, factory, force_collectives=distributed)
     tenants = {}
     for j in range(100000):
         o = svc.owner(f"tenant{j}")
@@ -346,7 +349,10 @@ def main():
                         "routed_queries_per_rank": a.batch, "routed_remote_frac_rank0": round(remote / a.batch, 3),
                         "routed_exact_check": f"{int(agree[0])}/{int(agree[1])}",
                         "routed_path": "front-end embed -> all_to_all [emb|tenant|limit] -> owner store search "
-                                       "(MFMA scan + fp32 re-rank) -> all_to_all [score|row]"})
+                                       "(MFMA scan + fp32 re-rank) -> all_to_all [score|row]",
+                        "collectives": ("rccl (torch.distributed nccl backend, world %d; header over gloo)" % world)
+                        if distributed and not a.cpu else ("gloo" if distributed else "none (world 1, no process "
+                                                                                       "group)")})
     if a.global_batch > 0:
         gq = [pool[i % len(pool)][: a.global_batch] for i in range(len(pool))]
         gb = {}
@@ -449,7 +455,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16 encoder; int8 scan -> bf16 re-score -> fp32 re-rank",
         "data": "synthetic (random unit fp32 memory vectors, synthetic query texts, random-init encoder weights)",
         "config": {"model": "%s (d=%d) on-device embed + MemorySystem.search_memories top-%d over a "
                             "%d x %d fp32 tenant per GPU (L2, fp32 re-rank)"

@@ -307,6 +307,55 @@ _lib.register("lzk_flat_cand_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
                                            _lib.P, _lib.F, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I,
                                            _lib.P, _lib.P])
 
+_lib.register("lzk_scan8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P,
+                                    _lib.P, _lib.P, _lib.F, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
+_lib.register("lzk_scan8_grid", _lib.I, [_lib.I, _lib.I])
+_lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
+
+# The dedicated int8 scan (csrc/kernels/scan8.hip: one K-tile stream across
+# tiles, int-domain epilogue); LZK_SCAN8=0 takes the shared 256^2 template
+# instead (A/B only).
+SCAN8 = os.environ.get("LZK_SCAN8", "1") != "0"
+_ws_scan8 = _Workspace()
+
+
+def _use_scan8(Dp: int) -> bool:
+    return SCAN8 and Dp % 128 == 0 and 256 <= Dp <= 1024
+
+
+def _wave_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
+    """Per-wave candidate record regions of the int8 scan (scan8.hip: 8
+    regions per block, each filled by one wave without atomics): int4
+    [grid * 8, capw] + int32 counts [grid * 8]; capw ~8x the expected records
+    per wave (a region that overflows marks every query for the fallback)."""
+    regions = grid * 8
+    capw = max(1024, lists * nq * kslot * S // max(grid, 1))
+    ws = _ws_blk.get(dev, regions * capw * 16 + regions * 4)
+    buf = ws[: regions * capw * 16]
+    cnt = ws[regions * capw * 16: regions * capw * 16 + regions * 4].view(torch.int32)
+    return buf, capw, cnt, regions
+
+
+def _scan8(X8, rscale, Q8, qscale, bias, alpha, thr, thr2, row_label, q_label, kslot, S, lists, cap, ca, cb):
+    """int8 candidate pass (scan8.hip) + gather into the per-query lists
+    ``ca`` (and ``cb`` for the dual search)."""
+    L = _lib.lib()
+    nq, Dp = Q8.shape
+    N = X8.shape[0]
+    dev = Q8.device
+    st = _lib.stream_ptr(dev)
+    grid = L.lzk_scan8_grid(N, nq)
+    bbuf, bcap, bcnt, regions = _wave_records(dev, grid, nq, kslot, S, lists)
+    ws = _ws_scan8.get(dev, int(L.lzk_scan8_ws_bytes(N)))
+    _lib.check(L.lzk_scan8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp, _lib.ptr(bias),
+                           rscale.data_ptr(), qscale.data_ptr(), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha),
+                           thr.data_ptr(), _lib.ptr(thr2), ws.data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st),
+               "lzk_scan8")
+    cbp = (cb[0].data_ptr(), cb[1].data_ptr(), cb[2].data_ptr()) if cb is not None else (None, None, None)
+    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), regions, cap, nq, ca[0].data_ptr(),
+                                 ca[1].data_ptr(), ca[2].data_ptr(), *cbp, st), "lzk_cand_gather")
+
+
 FP8_MAX = 448.0
 
 
@@ -412,10 +461,15 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
         thr = (thr - margin).contiguous()
     cap = max(2048, 16 * kslot * S)
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    qs = qscale.contiguous()
+    if _use_scan8(Dp):
+        _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, None, None, None, kslot, 2 * S, 1, cap, (cnt, cs, ci),
+               None)
+        _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
+        return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
     grid = L.lzk_cand_grid_f8(N, nq)
     bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 1)
     st = _lib.stream_ptr(dev)
-    qs = qscale.contiguous()
     _lib.check(L.lzk_flat_cand_i8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp, _lib.ptr(bias),
                                   rscale.data_ptr(), qs.data_ptr(), float(alpha), thr.data_ptr(), cap, cnt.data_ptr(),
                                   cs.data_ptr(), ci.data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st),
@@ -478,10 +532,29 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
     cap = max(2048, 16 * kslot * S)
     ca = _cand_lists(dev, nq, cap, 0)
     cb = _cand_lists(dev, nq, cap, 1)
+    qs = qscale.contiguous()
+    if _use_scan8(Dp):
+        _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, 2 * S, 2, cap,
+               ca, cb)
+    else:
+        _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap,
+                          ca, cb)
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *ca, cap, floor=floor)
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *cb, cap, floor=floor)
+    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap)
+    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap)
+    return ra, rb
+
+
+def _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap, ca, cb):
+    """The dual int8 pass on the shared 256^2 template (LZK_SCAN8=0)."""
+    L = _lib.lib()
+    nq, Dp = Q8.shape
+    N = X16.shape[0]
+    dev = Q8.device
     grid = L.lzk_cand_grid_f8(N, nq)
     bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 2)
     st = _lib.stream_ptr(dev)
-    qs = qscale.contiguous()
     _lib.check(L.lzk_flat_cand_dual_i8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp,
                                        _lib.ptr(bias), rscale.data_ptr(), qs.data_ptr(), row_label.data_ptr(),
                                        q_label.data_ptr(), float(alpha), thr_a.data_ptr(), thr_b.data_ptr(), cap,
@@ -491,11 +564,6 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
     _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, ca[0].data_ptr(),
                                  ca[1].data_ptr(), ca[2].data_ptr(), cb[0].data_ptr(), cb[1].data_ptr(),
                                  cb[2].data_ptr(), st), "lzk_cand_gather")
-    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *ca, cap, floor=floor)
-    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *cb, cap, floor=floor)
-    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap)
-    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap)
-    return ra, rb
 
 
 # Speculative list-B threshold of flat_topk_dual (LZK_DUAL_SPEC=1): aim for

@@ -13,6 +13,13 @@ tensors (tests, host metadata). The collectives this engine needs
 
 ``Communicator.local()`` is the world-of-one stand-in so single-process code
 paths call the same API.
+
+Host metadata (split sizes, tenant announcements, directory entries) travels
+on a second, gloo group between the same ranks (``host_all_gather``,
+``exchange_objects``): reading a count exchanged over RCCL back to the host
+would wait for everything queued before it on the GPU stream, so a serving
+loop that learns its all-to-all split sizes over gloo never stalls its GPU
+pipeline on a device-to-host copy.
 """
 from __future__ import annotations
 
@@ -55,12 +62,19 @@ class Communicator:
             be = dist.get_backend(group) if self.enabled else "gloo"
             device = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else torch.device("cpu")
         self.device = torch.device(device)
+        self._host_group = None
+        if self.enabled:
+            # collective (SPMD): every rank constructs its Communicator together
+            be = dist.get_backend(group)
+            self._host_group = group if be == "gloo" else dist.new_group(
+                ranks=None if group is None else dist.get_process_group_ranks(group), backend="gloo")
 
     @classmethod
     def local(cls, device=None) -> "Communicator":
         c = cls.__new__(cls)
         c.group, c.enabled, c.rank, c.world = None, False, 0, 1
         c.device = torch.device(device) if device is not None else torch.device("cpu")
+        c._host_group = None
         return c
 
     @classmethod
@@ -112,7 +126,7 @@ class Communicator:
         if not self.enabled:
             return [obj]
         out = [None] * self.world
-        dist.all_gather_object(out, obj, group=self.group)
+        dist.all_gather_object(out, obj, group=self._host_group)  # pickled bytes over gloo: no GPU sync
         return out
 
     # ---------------------------------------------------------------- all-to-all-v
@@ -123,6 +137,18 @@ class Communicator:
         recv = torch.empty_like(send_counts)
         dist.all_to_all_single(recv, send_counts, group=self.group)
         return recv
+
+    @_guarded("host_counts")
+    def host_counts(self, send_counts: Sequence[int]) -> List[int]:
+        """Host-side count exchange (gloo): ``send_counts[r]`` items for rank
+        r -> the count each rank sends here. The split sizes of an
+        :meth:`all_to_all_v` without a device-to-host read."""
+        if not self.enabled:
+            return [int(x) for x in send_counts]
+        send = torch.tensor([int(x) for x in send_counts], dtype=torch.int64)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self._host_group)
+        return recv.tolist()
 
     @_guarded("all_to_all_v")
     def all_to_all_v(self, t: torch.Tensor, send_counts: Sequence[int], recv_counts: Sequence[int]) -> torch.Tensor:
@@ -135,17 +161,37 @@ class Communicator:
                                input_split_sizes=list(map(int, send_counts)), group=self.group)
         return out
 
+    # ---------------------------------------------------------------- host metadata (gloo)
+    @_guarded("host_all_gather")
+    def host_all_gather(self, a) -> "np.ndarray":
+        """All-gather of a small host int64 array over the gloo group:
+        returns [world, *a.shape] (no GPU stream involved)."""
+        import numpy as np
+        a = np.ascontiguousarray(np.asarray(a, np.int64))
+        if not self.enabled:
+            return a[None]
+        t = torch.from_numpy(a.reshape(-1).copy())
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64)
+        dist.all_gather_into_tensor(out, t, group=self._host_group)
+        return out.numpy().reshape((self.world,) + a.shape)
+
+    @_guarded("exchange_objects")
     def exchange_objects(self, outgoing: List) -> List:
         """``outgoing[r]`` = a JSON-able object for rank r -> the objects
-        received, one per source rank (JSON bytes over one all-to-all-v)."""
+        received, one per source rank (JSON bytes over one gloo all-to-all-v:
+        host metadata never touches the GPU stream)."""
         if not self.enabled:
             return list(outgoing)
         payload = [json.dumps(x).encode() for x in outgoing]
-        send = torch.tensor([len(p) for p in payload], dtype=torch.int64, device=self.device)
-        recv = self.exchange_counts(send)
+        send = torch.tensor([len(p) for p in payload], dtype=torch.int64)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self._host_group)
         buf = torch.frombuffer(bytearray(b"".join(payload)), dtype=torch.uint8) if sum(map(len, payload)) else \
             torch.zeros(0, dtype=torch.uint8)
-        got = self.all_to_all_v(buf.to(self.device), send.tolist(), recv.tolist()).cpu().numpy().tobytes()
+        out_t = torch.empty(int(recv.sum()), dtype=torch.uint8)
+        dist.all_to_all_single(out_t, buf, output_split_sizes=recv.tolist(), input_split_sizes=send.tolist(),
+                               group=self._host_group)
+        got = out_t.numpy().tobytes()
         out, off = [], 0
         for n in recv.tolist():
             out.append(json.loads(got[off: off + n].decode()) if n else None)
@@ -157,8 +203,6 @@ class Communicator:
         fields as received on this rank (grouped by source rank, original
         relative order preserved)."""
         order = torch.argsort(dest, stable=True)
-        counts = torch.bincount(dest.long(), minlength=self.world).to(torch.int64)
-        sc = counts.to(self.device)
-        rc = self.exchange_counts(sc)
-        s_list, r_list = counts.tolist(), rc.cpu().tolist()
+        s_list = torch.bincount(dest.long(), minlength=self.world).to(torch.int64).tolist()
+        r_list = self.host_counts(s_list)
         return tuple(self.all_to_all_v(f[order.to(f.device)], s_list, r_list) for f in fields)

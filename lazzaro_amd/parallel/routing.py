@@ -99,6 +99,11 @@ class TenantTable:
 
     def slots(self, users: Sequence[str], systems: Dict[str, object]) -> torch.Tensor:
         """Slot per user (int64 device tensor), refreshing stale entries."""
+        return _to_dev(torch.from_numpy(self.slots_host(users, systems)), self.device)
+
+    def slots_host(self, users: Sequence[str], systems: Dict[str, object]) -> np.ndarray:
+        """Slot per user (host int64 array), refreshing stale entries (the
+        device copy of the table is re-uploaded when an entry changed)."""
         out = np.empty(len(users), np.int64)
         for j, u in enumerate(users):
             s = self.slot.get(u)
@@ -134,7 +139,7 @@ class TenantTable:
             self.d_ptr = _to_dev(torch.from_numpy(self.h_ptr.copy()), self.device)
             self.d_n = _to_dev(torch.from_numpy(self.h_n.copy()), self.device)
             self._dirty = False
-        return _to_dev(torch.from_numpy(out), self.device)
+        return out
 
 
 def _to_dev(t: torch.Tensor, device: torch.device) -> torch.Tensor:
@@ -263,13 +268,23 @@ def _unpack_keys(meta: np.ndarray) -> List[int]:
 def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> RoutedHits:
     """SPMD batched ``search_memories`` of queries already embedded by this
     rank's front end, each against its tenant ``users[q]`` wherever it is
-    owned. Every rank must call it (possibly with no queries)."""
+    owned. Every rank must call it (possibly with no queries).
+
+    Host metadata goes over the communicator's gloo group: one all-gather of
+    a [W, 6] header (rows to send, announcements, width, k, the directory
+    epoch this rank believes the destination has, its own epoch) gives every
+    rank its all-to-all split sizes with no device-to-host read. The queries
+    and the results cross in two RCCL all-to-alls. An owner whose every
+    sender knew its current directory (all tenants they route to were
+    announced to it and are pinned resident) maps the received tenant keys
+    on the device (:func:`_owner_search_device`); otherwise it reads the keys
+    back and serves by name (:func:`local_search`)."""
     comm = svc.comm
     W, me = comm.world, comm.rank
     n = len(users)
     limits = [int(limit)] * n if np.isscalar(limit) else [int(x) for x in limit]
     owner = [svc.owner(u) for u in users]
-    if W == 1:
+    if W == 1 and not svc.force_collectives:
         S, R = local_search(svc, list(users), Q, limits) if n else (
             torch.zeros((0, int(limit) if np.isscalar(limit) else 1)), torch.zeros((0, 1), dtype=torch.long))
         return RoutedHits(list(users), owner, S, R)
@@ -277,35 +292,53 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     D = int(Q.shape[1]) if n else 0
     order = sorted(range(n), key=lambda j: owner[j])
     send_n = np.bincount(np.asarray(owner, np.int64), minlength=W) if n else np.zeros(W, np.int64)
-    # first-time (tenant -> key) announcements per owner
+    # first-time (tenant -> key) announcements per owner (this rank included:
+    # an announced tenant is pinned resident by its owner)
     ann: List[List] = [[] for _ in range(W)]
     for u, r in zip(users, owner):
-        if r != me and u not in svc._announced[r]:
+        if u not in svc._announced[r]:
             svc._announced[r].add(u)
             ann[r].append(u)
     for u in users:
         svc._key_names[tenant_key(u)] = u
     kmax = max(limits) if n else 0
-    hdr = torch.tensor([[int(send_n[r]), len(ann[r]), D, kmax] for r in range(W)], dtype=torch.int64, device=dev)
-    allc = comm.all_gather_rows(hdr.reshape(1, -1)).reshape(W, W, 4).cpu().numpy()  # [src, dst, field]
+    hdr = np.array([[int(send_n[r]), len(ann[r]), D, kmax, svc._owner_epoch.get(r, -1), svc._dir_epoch]
+                    for r in range(W)], np.int64)
+    allc = comm.host_all_gather(hdr)  # [src, dst, field]
+    epoch0 = svc._dir_epoch
+    for r in range(W):  # an owner whose directory changed hears every tenant again
+        e = int(allc[r, 0, 5])
+        prev = svc._owner_epoch.get(r)
+        if prev != e:
+            svc._owner_epoch[r] = e
+            if prev is not None:
+                svc._announced[r] = set()
     if allc[:, :, 1].sum():
         for part in comm.exchange_objects(ann):
             for u in part or []:
                 svc._key_names[tenant_key(u)] = u
+                if svc.is_local(u):
+                    svc.pin(u)
     Dg = int(allc[:, :, 2].max())
     K = int(allc[:, :, 3].max())
     recv_n = allc[:, me, 0]
     if Dg == 0 or K == 0:
         return RoutedHits(list(users), owner, torch.zeros((n, 1)), torch.full((n, 1), -1, dtype=torch.long))
+    senders_current = all(int(allc[s, me, 4]) == epoch0 for s in range(W) if allc[s, me, 0] > 0)
+    on_device = senders_current and svc._dir_epoch == epoch0 and svc.device_directory_ok(Dg)
     Qo = Q[torch.as_tensor(order, dtype=torch.long, device=Q.device)] if n else torch.zeros((0, Dg), device=dev)
     pay = _pack_queries(Qo, [tenant_key(users[j]) for j in order], [limits[j] for j in order]) if n else \
         torch.zeros((0, Dg + 3), dtype=torch.int32)
     got = comm.all_to_all_v(pay.to(dev), send_n.tolist(), recv_n.tolist())
     m = got.shape[0]
+    svc.route_stats["device" if (m and on_device) else "host"] += 1
     if m:
-        meta = got[:, Dg:].cpu().numpy()
-        rusers = [svc._key_names[x] for x in _unpack_keys(meta)]
-        S, R = local_search(svc, rusers, got[:, :Dg].contiguous().view(torch.float32), meta[:, 2].tolist())
+        if on_device:
+            S, R = _owner_search_device(svc, got, Dg, K)
+        else:
+            meta = got[:, Dg:].cpu().numpy()
+            rusers = [svc._key_names[x] for x in _unpack_keys(meta)]
+            S, R = local_search(svc, rusers, got[:, :Dg].contiguous().view(torch.float32), meta[:, 2].tolist())
         if S.shape[1] < K:
             S = torch.cat([S, torch.full((m, K - S.shape[1]), float("-inf"), device=S.device)], 1)
             R = torch.cat([R, torch.full((m, K - R.shape[1]), -1, dtype=R.dtype, device=R.device)], 1)
@@ -319,6 +352,40 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     S = res[:, :K].contiguous().view(torch.float32)
     R = res[:, K:].to(torch.int64)
     return RoutedHits(list(users), owner, S, R)
+
+
+def _owner_search_device(svc, got: torch.Tensor, Dg: int, K: int):
+    """Owner side of :func:`search_routed` without reading the received
+    rows back: the tenant key of each row is matched on the device against
+    the pinned tenants (:meth:`DistributedMemoryService.device_directory_ok`:
+    a few large GPU tenants), each of which runs its store search over the
+    batch; a row keeps the results of the tenant whose key it carries. Rows
+    past a query's limit and rows that are not nodes come back -1 / -inf,
+    valid hits first (as :func:`local_search`)."""
+    m = got.shape[0]
+    dev = got.device
+    lo = got[:, Dg].long() & 0xFFFFFFFF
+    keys = (got[:, Dg + 1].long() << 32) | lo
+    lim = got[:, Dg + 2].long()
+    Qr = got[:, :Dg].contiguous().view(torch.float32)
+    S = torch.full((m, K), float("-inf"), dtype=torch.float32, device=dev)
+    R = torch.full((m, K), -1, dtype=torch.int64, device=dev)
+    for key, user in sorted(svc._pinned.items()):
+        ms = svc.systems[user]
+        g = ms.graph
+        with ms._graph_lock:
+            s, r = g.store_search(Qr.to(g.device), K, getattr(ms.store, "metric", "l2"))
+            with g.on_stream():
+                ok = (r >= 0) & (g.kind[r.clamp_min(0)] == NODE)
+        ok = ok.to(dev) & (keys == key)[:, None]
+        S = torch.where(ok, s.float().to(dev), S)
+        R = torch.where(ok, r.to(dev), R)
+    cut = torch.arange(K, device=dev)[None, :] >= lim[:, None]
+    S = torch.where(cut, torch.full_like(S, float("-inf")), S)
+    R = torch.where(cut, torch.full_like(R, -1), R)
+    o = torch.sort(torch.where(R >= 0, S, torch.full_like(S, float("-inf"))), dim=1, descending=True,
+                   stable=True).indices
+    return torch.gather(S, 1, o), torch.gather(R, 1, o)
 
 
 def resolve(svc, hits: RoutedHits) -> List[List[Dict]]:
@@ -365,22 +432,22 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     W, me = comm.world, comm.rank
     dev = comm.device
     b = int(Q.shape[0])
-    counts = comm.all_gather_rows(torch.tensor([[b, int(Q.shape[1]) if b else 0]], dtype=torch.int64,
-                                               device=dev)).cpu().numpy()
+    force = W > 1 or svc.force_collectives
+    counts = comm.host_all_gather(np.array([b, int(Q.shape[1]) if b else 0], np.int64))  # gloo: no GPU sync
     nb = counts[:, 0]
     D = int(counts[:, 1].max())
-    B = int(nb.max()) if W > 1 else b
+    B = int(nb.max()) if force else b
     Qp = torch.zeros((B, D), dtype=torch.float32, device=dev)
     if b:
         Qp[:b] = Q.to(dev, torch.float32)
-    Qall = comm.all_gather_rows(Qp) if W > 1 else Qp  # [W * B, D]
+    Qall = comm.all_gather_rows(Qp) if force else Qp  # [W * B, D]
     NQ = Qall.shape[0]
     best_s = torch.full((NQ, limit), float("-inf"), dtype=torch.float32, device=dev)
     best_k = torch.full((NQ, limit), -1, dtype=torch.int64, device=dev)
     users = [u for u, ms in svc.systems.items() if ms.graph.dim == D and ms.graph.n > 0]
     table = svc.tenant_table(svc.systems[users[0]].graph.device if users else None)
     if users:
-        slots = table.slots(users, {u: svc.systems[u] for u in users}).cpu().tolist()
+        slots = table.slots_host(users, {u: svc.systems[u] for u in users}).tolist()
         for u, slot in zip(users, slots):
             ms = svc.systems[u]
             g = ms.graph
@@ -391,7 +458,7 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
             s = torch.where(ok, s.float(), torch.full_like(s, float("-inf"))).to(dev)
             key = torch.where(ok, (me << 56) | (int(slot) << 32) | r, torch.full_like(r, -1)).to(dev)
             best_s, best_k = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit)
-    if W == 1:
+    if not force:
         return GlobalHits(best_s[:b], best_k[:b])
     # candidates for rank j's queries go back to rank j
     pay = torch.cat([best_s.contiguous().view(torch.int32).reshape(NQ, limit),

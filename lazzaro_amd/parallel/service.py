@@ -28,6 +28,7 @@ All collective methods must be called by every rank in the same order.
 from __future__ import annotations
 
 import inspect
+import os
 import weakref
 from collections import OrderedDict, defaultdict
 from collections.abc import Sequence as _SeqABC
@@ -118,7 +119,7 @@ def _jsonable(v):
 
 class DistributedMemoryService:
     def __init__(self, comm: Communicator, factory: Callable[[str], object], owner: Callable[[str], int] = None,
-                 max_resident: int = 1 << 30, placement=None, embedder=None):
+                 max_resident: int = 1 << 30, placement=None, embedder=None, force_collectives: bool = None):
         """``factory(user_id)`` builds the tenant's MemorySystem on this rank
         (sharing one store / embedder / device; it must load the tenant from
         the store); ``owner`` overrides the rendezvous-hash placement;
@@ -128,7 +129,14 @@ class DistributedMemoryService:
         tenants stay in memory (LRU; an evicted tenant is persisted and
         reloaded from the store on its next request). ``embedder``: this
         rank's replica of the encoder for the front end's queries on the
-        columnar search paths (default: the first resident tenant's)."""
+        columnar search paths (default: the first resident tenant's).
+        ``force_collectives`` (default: env ``LZK_FORCE_COLLECTIVES=1``): run
+        every exchange through the communicator even at world 1 -- under a
+        1-rank ``torch.distributed.run`` the RCCL all-to-all / all-gather
+        calls of an N-GPU job then execute on the one GPU."""
+        if force_collectives is None:
+            force_collectives = os.environ.get("LZK_FORCE_COLLECTIVES", "0") == "1"
+        self.force_collectives = bool(force_collectives) and comm.enabled
         self.comm = comm
         self.factory = factory
         self._owner = owner
@@ -144,6 +152,14 @@ class DistributedMemoryService:
         self._table = None
         self._announced = defaultdict(set)
         self._key_names: Dict[int, str] = {}
+        # owner-side directory of the routed path: tenants announced to this
+        # rank stay pinned resident under the current epoch (bumped whenever
+        # a pinned tenant leaves), so a batch whose senders all know the epoch
+        # is served by matching tenant keys on the device
+        self._pinned: Dict[int, str] = {}
+        self._dir_epoch = 0
+        self.route_stats = {"device": 0, "host": 0}  # routed batches served by device key matching / by name
+        self._owner_epoch: Dict[int, int] = {}
 
     # ------------------------------------------------------------ placement
     def owner(self, user: str) -> int:
@@ -177,6 +193,8 @@ class DistributedMemoryService:
         self._moved = {}
         self._own_memo = {}
         self._announced = defaultdict(set)  # owners changed: announce names again
+        self._owner_epoch = {}
+        self._unpin_all()
         gone = [u for u in self.systems if not self.is_local(u)]
         for u in gone:
             self._release(u, self.systems.pop(u))
@@ -190,8 +208,43 @@ class DistributedMemoryService:
             if h is not None:
                 h._mat()
 
+    # ------------------------------------------------------------ routed directory
+    # device key matching serves at most this many pinned (large) tenants; a
+    # rank with more -- or with small tenants, which share the fused
+    # multi-tenant scan keyed by name -- reads the received keys back
+    DEVICE_ROUTE_MAX_TENANTS = 2
+
+    def pin(self, user: str) -> None:
+        """Keep an announced tenant resident for the routed path (loads it
+        if needed)."""
+        self.system(user)
+        self._pinned[routing.tenant_key(user)] = user
+
+    def _unpin(self, user: str) -> None:
+        if self._pinned.pop(routing.tenant_key(user), None) is not None:
+            self._dir_epoch += 1
+
+    def _unpin_all(self) -> None:
+        if self._pinned:
+            self._pinned = {}
+            self._dir_epoch += 1
+
+    def device_directory_ok(self, D: int) -> bool:
+        """The routed owner side may match tenant keys on the device: every
+        pinned tenant is resident, large (its own store search), on the GPU
+        and of width ``D``."""
+        if not self._pinned or len(self._pinned) > self.DEVICE_ROUTE_MAX_TENANTS:
+            return False
+        for u in self._pinned.values():
+            ms = self.systems.get(u)
+            g = getattr(ms, "graph", None)
+            if g is None or g.dim != D or g.n < routing.BIG_ROWS:
+                return False
+        return True
+
     def _release(self, user: str, ms) -> None:
         """Persist and close a tenant this rank stops holding."""
+        self._unpin(user)
         self._settle(user)
         if self._table is not None:
             self._table.drop(user)
@@ -254,6 +307,7 @@ class DistributedMemoryService:
             dst = int(moves[user])
             if user in self.systems and dst != me:
                 self._settle(user)
+                self._unpin(user)
                 ms = self.systems.pop(user)
                 if self._table is not None:
                     self._table.drop(user)
@@ -267,12 +321,13 @@ class DistributedMemoryService:
         send = [torch.cat(v) if v else torch.zeros(0) for v in out_vec]
         counts = [int(t.numel()) for t in send]
         flat = torch.cat([t.to(dev) for t in send]) if sum(counts) else torch.zeros(0, device=dev)
-        rc = comm.exchange_counts(torch.tensor(counts, dtype=torch.int64, device=dev)).cpu().tolist()
-        recv = comm.all_to_all_v(flat, counts, rc) if comm.world > 1 else flat
+        rc = comm.host_counts(counts)
+        recv = comm.all_to_all_v(flat, counts, rc) if comm.world > 1 or self.force_collectives else flat
         self._moved.update({u: int(r) for u, r in moves.items()})
         for u in moves:
             self._own_memo.pop(u, None)
         self._announced = defaultdict(set)
+        self._owner_epoch = {}
         received, off = [], 0
         for src in range(comm.world):
             for user, meta, shape in got_meta[src]:
@@ -299,7 +354,7 @@ class DistributedMemoryService:
     def _exchange(self, outgoing: List[List]) -> List[List]:
         """outgoing[r] = JSON-able items for rank r -> items received per rank
         (this rank's own items stay in process: no serialisation)."""
-        if self.comm.world == 1:
+        if self.comm.world == 1 and not self.force_collectives:
             return outgoing
         me = self.comm.rank
         send = list(outgoing)
@@ -595,8 +650,8 @@ class DistributedMemoryService:
             meta[dest[j]].append([ids[j], contents[j]])
         counts = [len(m) * D for m in meta]
         flat = V[torch.as_tensor(order, dtype=torch.long)].reshape(-1) if order else torch.zeros(0)
-        rc = comm.exchange_counts(torch.tensor(counts, dtype=torch.int64, device=comm.device)).cpu().tolist()
-        got = comm.all_to_all_v(flat.to(comm.device), counts, rc) if comm.world > 1 else flat
+        rc = comm.host_counts(counts)
+        got = comm.all_to_all_v(flat.to(comm.device), counts, rc) if comm.world > 1 or self.force_collectives else flat
         got_meta = self._exchange(meta)
         rows = [m for part in got_meta for m in part]
         if not rows:

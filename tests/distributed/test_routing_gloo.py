@@ -40,10 +40,15 @@ def _queries(rank, n=13):
     return [f"rank {rank} question {q} about memories" for q in range(n)]
 
 
-def _workload(comm, db):
+def _workload(comm, db, force=False, device_dir=False):
     from lazzaro_amd.core.providers import HashEmbedder
+    from lazzaro_amd.parallel import routing
     from lazzaro_amd.parallel.service import DistributedMemoryService
-    svc = DistributedMemoryService(comm, functools.partial(_factory, db), embedder=HashEmbedder(dim=D))
+    svc = DistributedMemoryService(comm, functools.partial(_factory, db), embedder=HashEmbedder(dim=D),
+                                   force_collectives=force)
+    if device_dir:  # every owned tenant counts as "large": owners match tenant keys on the device
+        routing.BIG_ROWS = 1
+        svc.DEVICE_ROUTE_MAX_TENANTS = len(USERS)
     for u in USERS:
         if svc.is_local(u):
             _fill(svc.system(u), u)
@@ -55,6 +60,8 @@ def _workload(comm, db):
     nodes = svc.resolve(hits)
     again = svc.search_routed(users, qs, limits)  # names already announced: tensor-only round
     same = bool(torch.equal(again.rows, hits.rows))
+    third = svc.search_routed(users, qs, limits)  # every owner knows its senders' view of its directory
+    same = same and bool(torch.equal(third.rows, hits.rows)) and bool(torch.equal(third.scores, hits.scores))
     glob = svc.search_global_batch(qs[:5], limit=4)
     rk, slot, row = glob.split()
     table = svc.tenant_table()
@@ -64,7 +71,8 @@ def _workload(comm, db):
                        "scores": hits.scores.tolist(), "same": same,
                        "global": [[[int(a), int(b), int(c)] for a, b, c in zip(x, y, z)]
                                   for x, y, z in zip(rk.tolist(), slot.tolist(), row.tolist())],
-                       "gscores": glob.scores.tolist(), "names": names, "rank": comm.rank})
+                       "gscores": glob.scores.tolist(), "names": names, "rank": comm.rank,
+                       "route_stats": svc.route_stats, "force": svc.force_collectives})
 
 
 def _truth(qs, users, limits):
@@ -112,3 +120,29 @@ def test_routed_and_global_search(world, tmp_path):
             assert all(s > float("-inf") for s in sc[:k]) and sc[:k] == sorted(sc[:k], reverse=True)
         got = [[(names[rk][sl], row) for rk, sl, row in qq] for qq in x["global"]]
         assert got == _global_truth(qs[:5], 4), r
+
+
+@pytest.mark.parametrize("world,device_dir", [(1, False), (1, True), (2, True), (3, True)])
+def test_routed_forced_collectives_and_device_directory(world, device_dir, tmp_path):
+    """A 1-rank process group with ``force_collectives`` runs every exchange
+    of the N-rank job (the form ``bench.py`` uses under a 1-rank
+    torch.distributed.run on one GPU); with the device directory the owners
+    serve the steady-state rounds by matching tenant keys on the device (no
+    read-back of the received rows) -- results identical to the truth."""
+    fn = functools.partial(_workload, db=str(tmp_path / f"f{world}{device_dir}"), force=True, device_dir=device_dir)
+    outs = spawn(world, fn)
+    d = {r: json.loads(v) for r, v in outs.items()}
+    names = {r: {int(s): n for s, n in x["names"].items()} for r, x in d.items()}
+    for r, x in d.items():
+        qs = _queries(r)
+        assert x["force"] is True
+        assert x["same"]
+        assert x["ids"] == _truth(qs, x["users"], x["limits"]), r
+        got = [[(names[rk][sl], row) for rk, sl, row in qq] for qq in x["global"]]
+        assert got == _global_truth(qs[:5], 4), r
+        st = x["route_stats"]
+        assert st["device"] + st["host"] == 3
+        if device_dir:
+            assert st["device"] >= 1, st  # the third round at the latest
+        else:
+            assert st["device"] == 0
