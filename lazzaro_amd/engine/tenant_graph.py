@@ -1801,7 +1801,7 @@ class TenantGraph:
         with self.on_stream():
             live = (self.kind[:n] == NODE) & (self.sup[:n] == 0) & (self.has_emb[:n] == 1)
             n_live = int(live.sum())
-            dist = comm is not None and comm.world > 1
+            dist = comm is not None and (comm.world > 1 or comm.enabled)
             if dist:
                 t = torch.tensor([n_live], dtype=torch.int64, device=comm.device)
                 comm.all_reduce(t)

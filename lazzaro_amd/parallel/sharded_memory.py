@@ -105,10 +105,16 @@ class ShardedMemorySystem:
                  max_buffer_size: int = 10, consolidate_every: int = 3, auto_consolidate: bool = True,
                  auto_prune: bool = True, prune_threshold: float = 0.5,
                  hierarchy_params: Optional[Dict] = None, prune: bool = True, placement: str = "origin",
-                 **local_kwargs):
+                 force_collectives: Optional[bool] = None, **local_kwargs):
         from ..core.memory_system import MemorySystem
 
         self.comm = comm or Communicator.local()
+        if force_collectives is None:
+            import os
+            force_collectives = os.environ.get("LZK_FORCE_COLLECTIVES", "0") == "1"
+        # every exchange through the communicator (also at world 1 under a
+        # 1-rank torch.distributed.run: the N-rank code path on one GPU)
+        self._coll = self.comm.world > 1 or (bool(force_collectives) and self.comm.enabled)
         self.user_id = user_id
         self.max_buffer_size = int(max_buffer_size)
         self.consolidate_every = int(consolidate_every)
@@ -147,17 +153,17 @@ class ShardedMemorySystem:
         return self.comm.world
 
     def _to_comm(self, t: torch.Tensor) -> torch.Tensor:
-        return t.to(self.comm.device) if self.world > 1 else t
+        return t.to(self.comm.device) if self._coll else t
 
     def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:
         """Equal-shaped tensors of every rank, concatenated in rank order."""
-        if self.world == 1:
+        if not self._coll:
             return t
         return self.comm.all_gather_rows(self._to_comm(t.contiguous())).to(t.device)
 
     def _gather_var(self, t: torch.Tensor) -> Tuple[torch.Tensor, List[int]]:
         """Variable-length rows of every rank in rank order (+ per-rank counts)."""
-        if self.world == 1:
+        if not self._coll:
             return t, [int(t.shape[0])]
         cnt = self._gather_rows(torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)).tolist()
         mx = max(cnt)
@@ -169,7 +175,7 @@ class ShardedMemorySystem:
 
     def _sum(self, *vals) -> List[int]:
         t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)
-        if self.world > 1:
+        if self._coll:
             t = self.comm.all_reduce(self._to_comm(t)).to(self.device)
         return [int(x) for x in t.tolist()]
 
@@ -214,7 +220,7 @@ class ShardedMemorySystem:
         m = len(contents)
         if shard_codes is None:
             keys_all = [k for ks in self.comm.all_gather_object(list(shard_keys)) for k in ks] \
-                if self.world > 1 else list(shard_keys)
+                if self._coll else list(shard_keys)
         counts = self._gather_rows(torch.tensor([m], dtype=torch.int64, device=self.device)).tolist()
         off = sum(counts[: self.rank])
         codes = self._register_shards(keys_all)[off: off + m] if shard_codes is None else shard_codes
@@ -422,7 +428,7 @@ class ShardedMemorySystem:
         out = []
         for s, r in ((gs, gr), (ws, wr)):
             s, meta = pack(s, r)
-            if self.world > 1:
+            if self._coll:
                 s = self._gather_rows(s).view(self.world, F, k).permute(1, 0, 2).reshape(F, -1)
                 meta = self._gather_rows(meta).view(self.world, F, k, 4).permute(1, 0, 2, 3).reshape(F, -1, 4)
                 key = torch.where(meta[:, :, 0] >= 0, meta[:, :, 0], torch.full_like(meta[:, :, 0], BIG))
@@ -463,7 +469,7 @@ class ShardedMemorySystem:
             sc = torch.full((nq, limit), NEG_INF, dtype=torch.float64, device=dev)
             rows = num = torch.full((nq, limit), -1, dtype=torch.long, device=dev)
         meta = torch.stack([num, torch.where(num >= 0, torch.full_like(num, self.rank), num), rows], 2)
-        if self.world > 1:
+        if self._coll:
             sc = self._gather_rows(sc).view(self.world, nq, limit).permute(1, 0, 2).reshape(nq, -1)
             meta = self._gather_rows(meta).view(self.world, nq, limit, 3).permute(1, 0, 2, 3).reshape(nq, -1, 3)
             key = torch.where(meta[:, :, 0] >= 0, meta[:, :, 0], torch.full_like(meta[:, :, 0], BIG))
@@ -480,7 +486,7 @@ class ShardedMemorySystem:
             for j in range(limit):
                 if mh[q, j, 0] >= 0 and mh[q, j, 1] == self.rank and np.isfinite(sh[q, j]):
                     mine[(q, j)] = self._node_dict(int(mh[q, j, 2]))
-        parts = self.comm.all_gather_object(mine) if self.world > 1 else [mine]
+        parts = self.comm.all_gather_object(mine) if self._coll else [mine]
         got = {}
         for p in parts:
             got.update(p)
@@ -516,7 +522,7 @@ class ShardedMemorySystem:
                 j += 1
         # the batch clock: one `now` for every rank (rank 0's)
         t_now = torch.tensor([time.time() if now is None else now], dtype=torch.float64, device=dev)
-        if self.world > 1:
+        if self._coll:
             t_now = self.comm.broadcast(self._to_comm(t_now), 0).to(dev)
         now = float(t_now.item())
         m = len(flat)
@@ -536,7 +542,7 @@ class ShardedMemorySystem:
             E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)].to(dev, torch.float32)
             m = len(flat)
         d = torch.tensor([g.dim or (int(E.shape[1]) if E is not None else 0)], dtype=torch.int64, device=dev)
-        if self.world > 1:
+        if self._coll:
             d = self.comm.all_reduce(self._to_comm(d), "max").to(dev)
         if g.dim is None and int(d.item()):
             g._set_dim(int(d.item()))
@@ -579,7 +585,7 @@ class ShardedMemorySystem:
             B = int(sum(bl))
             c_off = int(sum(bl[: self.rank]))
             keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
-            keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self.world > 1 else keys
+            keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self._coll else keys
             sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
             ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
             Qa, fcnt = self._gather_var(E)
@@ -816,7 +822,7 @@ class ShardedMemorySystem:
         g = self.g
         dev = self.device
         W = self.world
-        if W == 1:
+        if not self._coll:
             return {"moved": 0}
         counts = self._gather_rows(torch.tensor([g.num_nodes()], dtype=torch.int64, device=dev)).tolist()
         T_ = sum(counts)
@@ -948,15 +954,15 @@ class ShardedMemorySystem:
         else:
             s_num = d_num = torch.zeros(0, dtype=torch.long, device=dev)
             w = torch.zeros(0, dtype=torch.float64, device=dev)
-        cdev = self.comm.device if W > 1 else dev
-        verts, lab = distributed_components(self.comm, s_num.to(cdev), d_num.to(cdev))
+        cdev = self.comm.device if self._coll else dev
+        verts, lab = distributed_components(self.comm, s_num.to(cdev), d_num.to(cdev), force=self._coll)
         verts, lab = verts.to(dev), lab.to(dev)
 
         def home(t):
-            return (t % W) if W > 1 else torch.zeros_like(t)
+            return (t % W) if self._coll else torch.zeros_like(t)
 
         def route(dest, rows):
-            if W == 1:
+            if not self._coll:
                 return rows
             got, _ = _route(self.comm, dest.to(cdev), rows.to(cdev))
             return got.to(dev)
@@ -985,7 +991,7 @@ class ShardedMemorySystem:
         rows_t = self._rows_of_nums(verts)
         hold = torch.where(rows_t >= 0, self.holder[rows_t.clamp_min(0)], torch.full_like(rows_t, -1))
         rem = (hold >= 0) & (hold != self.rank)
-        got = route(hold[rem], torch.stack([verts[rem], lab[rem]], 1)) if W > 1 else \
+        got = route(hold[rem], torch.stack([verts[rem], lab[rem]], 1)) if self._coll else \
             torch.zeros((0, 2), dtype=torch.long, device=dev)
         if got.numel():
             vv = torch.cat([verts[~rem], got[:, 0]])
@@ -1049,7 +1055,7 @@ class ShardedMemorySystem:
                 keepm = rank_in < take
                 for f_, v_, r_ in zip(fk[keepm].tolist(), vn[keepm].tolist(), rsel[keepm].tolist()):
                     mine.append((f_, v_, g.content[r_]))
-        parts = self.comm.all_gather_object(mine) if W > 1 else [mine]
+        parts = self.comm.all_gather_object(mine) if self._coll else [mine]
         if self.rank != 0:
             return []
         allm = sorted(x for p in parts for x in p)
@@ -1078,7 +1084,7 @@ class ShardedMemorySystem:
                 v, r = torch.topk(key, k, largest=False, sorted=True)
                 r = r[v < BIG]
                 mine = [(int(key[x]), g.content[x]) for x in r.tolist()]
-        parts = self.comm.all_gather_object(mine) if self.world > 1 else [mine]
+        parts = self.comm.all_gather_object(mine) if self._coll else [mine]
         return [c for _, c in sorted(x for p in parts for x in p)[:take]] if self.rank == 0 else []
 
     def run_consolidation(self) -> str:
@@ -1108,7 +1114,7 @@ class ShardedMemorySystem:
                 r = ms._extract_profile_from_contents(contents)
                 if "Updated" in r:
                     results.append(r)
-        if self.world > 1:
+        if self._coll:
             prof = self.comm.all_gather_object(dict(ms.profile.data) if self.rank == 0 else None)[0]
             for k, v in prof.items():
                 if ms.profile.data.get(k) != v:
@@ -1119,7 +1125,7 @@ class ShardedMemorySystem:
 
     def cluster_pass(self) -> Dict:
         hp = self.hierarchy_params or {"fine": 4096, "top": 64, "iters": 2}
-        out = self.g.cluster_pass(hp["fine"], hp["top"], hp["iters"], comm=self.comm if self.world > 1 else None)
+        out = self.g.cluster_pass(hp["fine"], hp["top"], hp["iters"], comm=self.comm if self._coll else None)
         self._build_reach()
         return out
 

@@ -141,7 +141,8 @@ def _sharded(comm, cfg=CPU):
     extra = dict(hierarchy_params={"fine": 12, "top": 4, "every": 10 ** 6, "iters": 3}, placement="cluster",
                  prune=True) if pruned else {}
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
-                             embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev, **extra)
+                             embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev,
+                             force_collectives=cfg.get("force", False), **extra)
     rebal = cfg.get("rebalance", False)
     lo, hi = _split(cfg["rows"], comm.world, comm.rank, [5, 1, 2] if rebal else None)
     sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],
@@ -202,6 +203,15 @@ def check_equivalent(out, world, limit):
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_tenant_matches_single_process(world):
     check_equivalent(spawn(world, _sharded), world, LIMIT)
+
+
+@pytest.mark.parametrize("pruned", [False, True])
+def test_sharded_tenant_forced_collectives_world1(pruned):
+    """One rank with every exchange forced through the communicator (the
+    path bench.py times under a 1-rank torch.distributed.run): the
+    single-process state."""
+    cfg = dict(CPU, force=True, pruned=pruned)
+    check_equivalent(spawn(1, functools.partial(_sharded, cfg=cfg)), 1, LIMIT)
 
 
 @pytest.mark.parametrize("world", [2, 3])
