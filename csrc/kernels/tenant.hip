@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
 // Embedding-row writes of a small node insert in ONE launch (the consolidation
 // segments insert ~20 facts, 43 times per 128-conversation step): per row j,
 // x = e32[j] * has[j] goes to emb32[rows[j]], its bf16 copy to emb16, the
-// per-row symmetric int8 copy of the bf16 values + scale (max|x|/127, 1 for a
+// per-row symmetric int8 copy of the bf16 values + scale (max|x|/127, 0 for a
 // zero row) to emb8 / rs8 (the store search's int8 scan), |x|^2 (fp64 sum,
 // stored fp32) to sqn, x_d^2 to the per-dimension sums (fp64 atomics), and
 // max | |x| - 1 | over the valid rows / the largest row scale to two device
@@ -425,15 +425,18 @@ __global__ __launch_bounds__(256) void tg_write_emb_kernel(
   s2 = red_d[0] + red_d[1] + red_d[2] + red_d[3];
   am = fmaxf(fmaxf(red_f[0], red_f[1]), fmaxf(red_f[2], red_f[3]));
   if (emb8) {
-    const float sc = am > 0.f ? am * (1.f / 127.f) : 1.f;  // torch: amax / 127.0 = amax * (1/127)
+    // a zero row quantises exactly (q = 0) with scale 0: it must not widen
+    // the tenant's error model (rs_max) nor the scan's row-group bounds
+    const float sc = am > 0.f ? am * (1.f / 127.f) : 0.f;  // torch: amax / 127.0 = amax * (1/127)
+    const float den = am > 0.f ? sc : 1.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int d = t + 256 * c;
-      if (d < D) emb8[r * ld8 + d] = (signed char)fminf(fmaxf(rintf(vb[c] / sc), -127.f), 127.f);
+      if (d < D) emb8[r * ld8 + d] = (signed char)fminf(fmaxf(rintf(vb[c] / den), -127.f), 127.f);
     }
     if (t == 0) {
       rs8[r] = sc;
-      if (rs_max) atomicMax(reinterpret_cast<int*>(rs_max), __float_as_int(sc));
+      if (rs_max && am > 0.f) atomicMax(reinterpret_cast<int*>(rs_max), __float_as_int(sc));
     }
   }
   if (t == 0) {

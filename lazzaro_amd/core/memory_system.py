@@ -909,12 +909,19 @@ STORAGE:
 
     def _commit_incremental(self) -> None:
         tracking, args = self._snapshot_incremental()
+        if getattr(self, "_commit_retry", False):
+            # the previous commit failed part way (e.g. nodes written, edges
+            # not): rows it reported fresh may be in the table now, so every
+            # row goes through the keyed upsert -- a retry never duplicates
+            args[1].pop("fresh", None)
         try:
             with tracer.stage("persist_write", "cpu"):
                 self.store.commit_tenant(*args)
         except Exception:
             self.graph.restore_tracking(*tracking)
+            self._commit_retry = True
             raise
+        self._commit_retry = False
         self._mark_committed(tracking[0], tracking[2])
 
     def _mark_committed(self, rows, del_ids) -> None:
@@ -955,6 +962,8 @@ STORAGE:
                         self.store.save_profile(p, user_id=a[0])
                 except Exception as e:
                     self._unwritten = queue[i:]
+                    for a_, _ in self._unwritten:  # retried by key: the failed write may have landed in part
+                        a_[1].pop("fresh", None)
                     self.metrics["persist_failures"] = self.metrics.get("persist_failures", 0) + 1
                     log.warning("write-behind commit failed for %s: %s", a[0], e)
                     return

@@ -81,6 +81,15 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
 LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 128, 1 << 20, 8.0
+# The default int8 margin is STATISTICAL (LOWP_MARGIN_Z standard deviations of
+# the row-rounding term plus the exact worst case of the query term): on
+# random or clustered data the top-k equals the bf16 scan's (tests, bench
+# recall 1.0), but an adversarial row set could in principle move a true
+# top-k row below the cut. LZK_LOWP_RIGOROUS=1 (or TenantGraph.LOWP_RIGOROUS)
+# uses the worst-case bound of every term instead (|<x, eta>| <= |x| |eta|,
+# |<delta, q>| <= s_max / 2 |q|_1): exact parity with the bf16 path for any
+# data, at ~5x more candidates per query.
+LOWP_RIGOROUS = os.environ.get("LZK_LOWP_RIGOROUS", "0") == "1"
 # consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8). Off
 # by default: bench/bench_consolidate.py (random fact vectors) 17.3 -> 11.6 ms
 # per step's scan, but the clustered-topic row-sharded run of bench.py went
@@ -274,7 +283,7 @@ class TenantGraph:
             lowp = self._lowp_mode()
             e8 = torch.zeros((cap, self.Dp), dtype=torch.int8 if lowp == "i8" else torch.uint8,
                              device=dev) if lowp else None
-            rs8 = torch.ones(cap, dtype=torch.float32, device=dev) if lowp == "i8" else None
+            rs8 = torch.zeros(cap, dtype=torch.float32, device=dev) if lowp == "i8" else None
             if self.cap and self.emb32 is not None and self.emb32.shape[1] == self.dim:
                 e32[:n] = self.emb32[:n]
                 sq[:n] = self.sqn[:n]
@@ -836,7 +845,7 @@ class TenantGraph:
                     if self.emb8 is not None:
                         self.emb8[r] = 0
                     if self.rs8 is not None:
-                        self.rs8[r] = 1.0
+                        self.rs8[r] = 0.0
             self._bump(store=True)
             return
         if self.dim is None:
@@ -1708,9 +1717,14 @@ class TenantGraph:
         eta = q8.float() * qs[:, None] - q16.float()
         mu2 = (self.sumsq / max(self.n_sumsq, 1)).float()
         smax = self._rs8_max
+        floor = 0.5 * smax * eta.abs().sum(1)
+        if LOWP_RIGOROUS or getattr(self, "LOWP_RIGOROUS", False):
+            # worst case of every term (rows of norm <= 1 + max_norm_dev, bf16-rounded)
+            xn = 1.0 + self.max_norm_dev + 2.0 ** -7
+            bound = eta[:, :d].norm(dim=1) * xn + 0.5 * smax * q16.float().abs().sum(1) + floor
+            return q8, qs, (abs(alpha) * bound * (1.0 + 1e-5) + 1e-6).contiguous()
         v1 = (eta[:, :d] ** 2 * mu2[None, :]).sum(1)
         v2 = (q16.float() ** 2).sum(1) * (smax * smax / 12.0)
-        floor = 0.5 * smax * eta.abs().sum(1)
         margin = (abs(alpha) * (LOWP_MARGIN_Z * torch.sqrt(v1 + v2) + floor)).contiguous()
         return q8, qs, margin
 

@@ -411,13 +411,15 @@ def flat_topk_fp8(X8: torch.Tensor, Q8: torch.Tensor, scale2: float, X16: torch.
 
 
 def quantize_i8_rows(x: torch.Tensor, out: torch.Tensor = None, scale_out: torch.Tensor = None):
-    """Symmetric per-row int8: q = round(x / s), s = max|x_row| / 127 (1 for
-    an all-zero row), so x ~= q * s with |error| <= s / 2 per element.
+    """Symmetric per-row int8: q = round(x / s), s = max|x_row| / 127 (0 for
+    an all-zero row, which quantises exactly and so must not widen any error
+    bound), so x ~= q * s with |error| <= s / 2 per element.
     Returns (q int8 [n, D] (or ``out`` filled in its first D columns), s fp32 [n])."""
     xf = x.float()
     amax = xf.abs().amax(1)
-    s = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
-    q = torch.round(xf / s[:, None]).clamp_(-127, 127).to(torch.int8)
+    s = torch.where(amax > 0, amax / 127.0, torch.zeros_like(amax))
+    den = torch.where(amax > 0, s, torch.ones_like(amax))
+    q = torch.round(xf / den[:, None]).clamp_(-127, 127).to(torch.int8)
     if out is not None:
         out[:, : q.shape[1]] = q
         q = out
@@ -434,8 +436,11 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
 
     X8 / Q8: per-row symmetric int8 of X16 / Q16 (:func:`quantize_i8_rows`,
     Dp % 128 == 0, Dp <= 1024) with fp32 scales ``rscale`` [N] / ``qscale``
-    [nq]; ``margin`` [nq] (fp32, >= 0) bounds |int8 score - bf16 score| for
-    the query (the caller's error model). Steps:
+    [nq]; ``margin`` [nq] (fp32, >= 0) is the caller's allowance for
+    |int8 score - bf16 score| of the query: the result equals the bf16 scan's
+    whenever the margin holds for the rows that matter -- TenantGraph's
+    default margin is a statistical bound (8 sigma), its LOWP_RIGOROUS one a
+    worst-case bound. Steps:
       1. thr = exact bf16 k-th best of a 1/S row sample (a lower bound of the
          true k-th score) minus the margin -> the int8 scan keeps every row
          whose int8 score clears it;

@@ -215,6 +215,16 @@ def local_search(svc, users: Sequence[str], Q: torch.Tensor, limits: Sequence[in
             bad = (r < 0) | (o["kind"] != NODE)
             S[qt] = torch.where(bad, torch.full_like(s, float("-inf")), s)
             R[qt] = torch.where(bad, torch.full_like(r, -1), r)
+        if dev.type == "cuda":
+            # the fused launches above read the tenants' columns through raw
+            # addresses asynchronously: order each graph's stream after them
+            # before its lock goes, so a column reallocated (and its memory
+            # reused in the graph stream's order) cannot be read stale
+            cur = torch.cuda.current_stream(dev)
+            for u in fused:
+                gs = getattr(systems[u].graph, "stream", None)
+                if gs is not None and gs.cuda_stream != cur.cuda_stream:
+                    gs.wait_stream(cur)
         # a query's results past its own limit are dropped
         if min(limits) < k:  # decided on the host: no device sync on the serving path
             lim = torch.as_tensor(list(limits), dtype=torch.long).to(dev, non_blocking=True)
@@ -413,14 +423,26 @@ def resolve(svc, hits: RoutedHits) -> List[List[Dict]]:
 @dataclass
 class GlobalHits:
     """:func:`search_global_batch` result: ``scores`` [b, k]; ``keys`` [b, k]
-    int64 = rank << 56 | tenant slot << 32 | row (-1 = none); ``tenants``
-    maps (rank, slot) to the tenant name for the hits (filled lazily)."""
+    int64 = rank << 56 | tenant slot << 32 | row (-1 = none) -- the merge's
+    total order; a slot is only meaningful on its rank at search time (slots
+    are recycled when tenants leave). ``tenant_keys`` [b, k] int64 is the
+    stable 63-bit :func:`tenant_key` of each hit's tenant (-1 = none):
+    :meth:`users` maps them to names."""
     scores: torch.Tensor
     keys: torch.Tensor
+    tenant_keys: Optional[torch.Tensor] = None
 
     def split(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         k = self.keys
         return k >> 56, (k >> 32) & 0xFFFFFF, k & 0xFFFFFFFF
+
+    def users(self, svc) -> List[List[Optional[str]]]:
+        """Tenant name of every hit (None past the hits). Names this rank
+        has not seen yet come from :meth:`DistributedMemoryService.get_all_users`
+        (a collective: call it on every rank when a hit can name a tenant
+        only another rank has served)."""
+        names = svc._key_names
+        return [[names.get(int(t)) if t >= 0 else None for t in row] for row in self.tenant_keys.tolist()]
 
 
 def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
@@ -444,6 +466,7 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     NQ = Qall.shape[0]
     best_s = torch.full((NQ, limit), float("-inf"), dtype=torch.float32, device=dev)
     best_k = torch.full((NQ, limit), -1, dtype=torch.int64, device=dev)
+    best_t = torch.full((NQ, limit), -1, dtype=torch.int64, device=dev)
     users = [u for u, ms in svc.systems.items() if ms.graph.dim == D and ms.graph.n > 0]
     table = svc.tenant_table(svc.systems[users[0]].graph.device if users else None)
     if users:
@@ -457,26 +480,36 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
                     ok = (r >= 0) & (g.kind[r.clamp_min(0)] == NODE)
             s = torch.where(ok, s.float(), torch.full_like(s, float("-inf"))).to(dev)
             key = torch.where(ok, (me << 56) | (int(slot) << 32) | r, torch.full_like(r, -1)).to(dev)
-            best_s, best_k = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit)
+            tk = torch.where(ok, torch.full_like(r, tenant_key(u)), torch.full_like(r, -1)).to(dev)
+            best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
+                                            torch.cat([best_t, tk], 1))
     if not force:
-        return GlobalHits(best_s[:b], best_k[:b])
+        return GlobalHits(best_s[:b], best_k[:b], best_t[:b])
     # candidates for rank j's queries go back to rank j
     pay = torch.cat([best_s.contiguous().view(torch.int32).reshape(NQ, limit),
-                     best_k.view(torch.int32).reshape(NQ, 2 * limit)], 1)
-    got = comm.all_to_all_v(pay, [B] * W, [B] * W)  # [W(src) * B, 3 * limit]
+                     best_k.view(torch.int32).reshape(NQ, 2 * limit),
+                     best_t.view(torch.int32).reshape(NQ, 2 * limit)], 1)
+    got = comm.all_to_all_v(pay, [B] * W, [B] * W)  # [W(src) * B, 5 * limit]
     gs = got[:, :limit].contiguous().view(torch.float32).reshape(W, B, limit)
-    gk = got[:, limit:].contiguous().view(torch.int64).reshape(W, B, limit)
+    gk = got[:, limit:3 * limit].contiguous().view(torch.int64).reshape(W, B, limit)
+    gt = got[:, 3 * limit:].contiguous().view(torch.int64).reshape(W, B, limit)
     gs = gs.permute(1, 0, 2).reshape(B, W * limit)
     gk = gk.permute(1, 0, 2).reshape(B, W * limit)
-    s, k = _merge(gs, gk, limit)
-    return GlobalHits(s[:b], k[:b])
+    gt = gt.permute(1, 0, 2).reshape(B, W * limit)
+    s, k, t = _merge(gs, gk, limit, gt)
+    return GlobalHits(s[:b], k[:b], t[:b])
 
 
-def _merge(s: torch.Tensor, key: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def _merge(s: torch.Tensor, key: torch.Tensor, k: int, extra: Optional[torch.Tensor] = None):
     """Top-k by (score desc, key asc; -1 keys last) -- the same total order on
-    every rank, so the merge is independent of arrival order."""
+    every rank, so the merge is independent of arrival order. ``extra`` (a
+    per-candidate payload) follows its candidate."""
     kk = torch.where(key >= 0, key, torch.full_like(key, (1 << 63) - 1))
     o = torch.argsort(kk, dim=1, stable=True)
     s, key = torch.gather(s, 1, o), torch.gather(key, 1, o)
+    if extra is not None:
+        extra = torch.gather(extra, 1, o)
     o = torch.sort(s, dim=1, descending=True, stable=True).indices[:, :k]
+    if extra is not None:
+        return torch.gather(s, 1, o), torch.gather(key, 1, o), torch.gather(extra, 1, o)
     return torch.gather(s, 1, o), torch.gather(key, 1, o)

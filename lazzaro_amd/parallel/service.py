@@ -591,7 +591,10 @@ class DistributedMemoryService:
             except Exception:
                 pass
         parts = self.comm.all_gather_object(sorted(mine))
-        return sorted({u for p in parts for u in p})
+        users = sorted({u for p in parts for u in p})
+        for u in users:  # the directory also names every tenant key (GlobalHits.users)
+            self._key_names[routing.tenant_key(u)] = u
+        return users
 
     # ------------------------------------------------------------ global search (C1 + K2)
     def search_global(self, query_emb: torch.Tensor, limit: int = 5, metric: str = "l2") -> List[Dict]:

@@ -137,11 +137,13 @@ class ColumnarTable:
         """One committed version that deletes the rows matching ``eq`` whose
         ``key`` is in ``keys`` and appends ``cols`` (upsert + delete)."""
         fault_point("store.commit")
+        fault_point("store.commit." + self.name)
         n, v = self._t.replace_where(list(eq), key, list(keys), cols)
         return int(n), int(v)
 
     def add_columns(self, cols: Dict) -> int:
         fault_point("store.commit")
+        fault_point("store.commit." + self.name)
         return int(self._t.append(cols))
 
     def delete(self, eq: Sequence[Tuple[str, str]], in_col: str = "", in_vals=None) -> Tuple[int, int]:

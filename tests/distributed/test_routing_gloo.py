@@ -64,6 +64,8 @@ def _workload(comm, db, force=False, device_dir=False):
     same = same and bool(torch.equal(third.rows, hits.rows)) and bool(torch.equal(third.scores, hits.scores))
     glob = svc.search_global_batch(qs[:5], limit=4)
     rk, slot, row = glob.split()
+    svc.get_all_users()  # names every tenant key
+    gusers = glob.users(svc)
     table = svc.tenant_table()
     names = {int(s): n for n, s in table.slot.items()}
     svc.close()
@@ -72,7 +74,7 @@ def _workload(comm, db, force=False, device_dir=False):
                        "global": [[[int(a), int(b), int(c)] for a, b, c in zip(x, y, z)]
                                   for x, y, z in zip(rk.tolist(), slot.tolist(), row.tolist())],
                        "gscores": glob.scores.tolist(), "names": names, "rank": comm.rank,
-                       "route_stats": svc.route_stats, "force": svc.force_collectives})
+                       "route_stats": svc.route_stats, "force": svc.force_collectives, "gusers": gusers})
 
 
 def _truth(qs, users, limits):
@@ -120,6 +122,7 @@ def test_routed_and_global_search(world, tmp_path):
             assert all(s > float("-inf") for s in sc[:k]) and sc[:k] == sorted(sc[:k], reverse=True)
         got = [[(names[rk][sl], row) for rk, sl, row in qq] for qq in x["global"]]
         assert got == _global_truth(qs[:5], 4), r
+        assert [[u for u, _ in qq] for qq in got] == x["gusers"]
 
 
 @pytest.mark.parametrize("world,device_dir", [(1, False), (1, True), (2, True), (3, True)])

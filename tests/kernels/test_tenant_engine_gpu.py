@@ -523,3 +523,67 @@ def test_scan8_matches_template_gpu(D, nq):
     assert torch.equal(sa, sb)
     s16, r16 = S.flat_topk(X16, Q16, 16, bias=bias, alpha=2.0)
     assert torch.equal(ra[:, :10], r16[:, :10])
+
+
+def test_zero_row_keeps_int8_error_model_gpu():
+    """An embedding-less (all-zero) row quantises exactly with scale 0: the
+    tenant's int8 error model (max row scale) and the scan's candidate lists
+    stay as they were, and the row still surfaces where its exact score
+    puts it."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    from lazzaro_amd.ops import search as S
+    saved = TG.TenantGraph.LOWP
+    TG.TenantGraph.LOWP = "i8"
+    try:
+        g = TenantGraph(device=DEV)
+        N, D = (1 << 20) + 100, 384
+        gen = torch.Generator(device=DEV).manual_seed(17)
+        X = torch.randn(N, D, device=DEV, generator=gen)
+        X = X / X.norm(dim=1, keepdim=True)
+        g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
+        Q = torch.randn(256, D, device=DEV, generator=gen)
+        Q = Q / Q.norm(dim=1, keepdim=True)
+
+        def cands():
+            g.store_search(Q, 10, "l2")
+            torch.cuda.synchronize()
+            c = S._ws_cand.get(DEV, 0)[: Q.shape[0] * 4].view(torch.int32) & 0x3FFFFFFF
+            return float(c.float().mean())
+        smax0, c0 = float(g._rs8_max), cands()
+        g.add_nodes(["zero"], [""], torch.zeros(1, D, device=DEV), shard=g.shard_id("work"), stored=True)
+        r = g.row_of["zero"]
+        assert float(g.rs8[r]) == 0.0 and int(g.emb8[r].abs().max()) == 0
+        assert float(g._rs8_max) == smax0
+        c1 = cands()
+        assert c1 <= 1.2 * c0 + 2, (c0, c1)
+        # L2: the zero row scores -|q|^2 = -1, above every unit row (-2 + 2<q,x> < -1 for <q,x> < 0.5)
+        _, rows = g.store_search(Q, 10, "l2")
+        assert bool((rows[:, 0] == r).all())
+    finally:
+        TG.TenantGraph.LOWP = saved
+
+
+def test_store_search_i8_rigorous_margin_gpu():
+    """LOWP_RIGOROUS: the worst-case int8 margin (more candidates) gives the
+    same top-10 as exact fp32 L2 on clustered rows."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    saved = TG.TenantGraph.LOWP, getattr(TG.TenantGraph, "LOWP_RIGOROUS", False)
+    TG.TenantGraph.LOWP, TG.TenantGraph.LOWP_RIGOROUS = "i8", True
+    try:
+        g = TenantGraph(device=DEV)
+        N, D = (1 << 20) + 64, 256
+        gen = torch.Generator(device=DEV).manual_seed(23)
+        C = torch.randn(128, D, device=DEV, generator=gen)
+        X = C[torch.randint(0, 128, (N,), device=DEV, generator=gen)] + 0.4 * torch.randn(N, D, device=DEV,
+                                                                                         generator=gen)
+        X = X / X.norm(dim=1, keepdim=True)
+        g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
+        Q = X[torch.randint(0, N, (256,), device=DEV, generator=gen)] + 0.2 * torch.randn(256, D, device=DEV,
+                                                                                         generator=gen) / D ** 0.5
+        Q = Q / Q.norm(dim=1, keepdim=True)
+        _, rows = g.store_search(Q, 10, "l2")
+        ref = torch.topk(-torch.cdist(Q.double(), X.double()), 10, dim=1).indices
+        hit = sum(len(set(a) & set(b)) for a, b in zip(rows.cpu().tolist(), ref.cpu().tolist())) / ref.numel()
+        assert hit == 1.0
+    finally:
+        TG.TenantGraph.LOWP, TG.TenantGraph.LOWP_RIGOROUS = saved

@@ -201,3 +201,41 @@ def test_elastic_placement_moves_only_dead_ranks_tenants():
     moved = p.moved(tenants, q)
     assert moved and all(p.owner(t) == 3 for t in moved) and all(v != 3 for v in moved.values())
     assert all(q.owner(t) == p.owner(t) for t in tenants if t not in moved)
+
+
+def test_commit_retry_after_partial_write_has_no_duplicate_ids(tmp_path):
+    """The nodes table is written, the edges write fails: the retry must go
+    through the keyed upsert (rows reported 'fresh' by the failed attempt
+    may already be in the table) -- no node id twice, edges land once."""
+    # 22 facts of one topic: the shard passes super_node_threshold, and the
+    # super-node row is written by the commit itself (never stored before)
+    facts = [f"User fact number {i} about beekeeping on the rooftop" for i in range(22)]
+    ms = MemorySystem(llm_provider=ScriptedLLM([_facts(*facts)]), embedding_provider=HashEmbedder(),
+                      enable_async=False, db_dir=str(tmp_path), max_buffer_size=100)
+    ms.start_conversation()
+    ms.add_to_short_term("I keep bees on a rooftop and sell the honey")
+    with armed("store.commit.edges", 1, StoreError):  # the consolidation save's edge upsert fails
+        ms.end_conversation()
+    assert ms.metrics["persist_failures"] >= 1 and ms.super_nodes
+    for _ in range(2):
+        ms._save_to_persistence()
+        ids = [r["id"] for r in ms.store.get_nodes(user_id="default")]
+        assert len(ids) == len(set(ids)) == 23, sorted(ids)
+    ms.close()
+
+
+def test_write_behind_retry_after_partial_write_has_no_duplicate_ids(tmp_path):
+    facts = [f"User fact number {i} about beekeeping on the rooftop" for i in range(22)]
+    ms = MemorySystem(llm_provider=ScriptedLLM([_facts(*facts)]), embedding_provider=HashEmbedder(),
+                      enable_async=False, db_dir=str(tmp_path), max_buffer_size=100, persist_async=True)
+    ms.start_conversation()
+    ms.add_to_short_term("I keep bees on a rooftop and sell the honey")
+    with armed("store.commit.edges", 1, StoreError):
+        ms.end_conversation()
+        ms.flush_persistence()
+    ms.flush_persistence()
+    ms._save_to_persistence()
+    ms.flush_persistence()
+    ids = [r["id"] for r in ms.store.get_nodes(user_id="default")]
+    assert len(ids) == len(set(ids)) == 23, sorted(ids)
+    ms.close()
