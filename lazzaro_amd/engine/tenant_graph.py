@@ -90,6 +90,9 @@ LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 128, 1 << 20, 8.0
 # |<delta, q>| <= s_max / 2 |q|_1): exact parity with the bf16 path for any
 # data, at ~5x more candidates per query.
 LOWP_RIGOROUS = os.environ.get("LZK_LOWP_RIGOROUS", "0") == "1"
+# batches below LOWP_MIN_Q (the interactive turn) take the HBM-bound narrow
+# int8 scan (scan8.hip scan8_narrow_kernel); LZK_LOWP_NARROW=0: the bf16 lane kernel
+LOWP_NARROW = os.environ.get("LZK_LOWP_NARROW", "1") != "0"
 # consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8). Off
 # by default: bench/bench_consolidate.py (random fact vectors) 17.3 -> 11.6 ms
 # per step's scan, but the clustered-topic row-sharded run of bench.py went
@@ -1656,7 +1659,8 @@ class TenantGraph:
         if self.on_gpu and k <= CAND_SLOTS and (metric != "cosine" or self.unit_rows()) \
                 and M * n >= KERNEL_MIN_WORK // 16:
             q16 = self._q16(Qf)
-            if self.emb8 is not None and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS:
+            narrow = LOWP_NARROW and self.emb8 is not None and self.emb8.dtype == torch.int8
+            if self.emb8 is not None and self.unit_rows() and (M >= LOWP_MIN_Q or narrow) and n >= LOWP_MIN_ROWS:
                 if self.emb8.dtype == torch.int8:
                     _, cand = self._i8_candidates(Qf, q16, kc, bias, alpha)
                 else:

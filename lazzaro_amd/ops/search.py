@@ -310,6 +310,10 @@ _lib.register("lzk_flat_cand_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
 _lib.register("lzk_scan8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P,
                                     _lib.P, _lib.P, _lib.F, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
 _lib.register("lzk_scan8_grid", _lib.I, [_lib.I, _lib.I])
+_lib.register("lzk_scan8_narrow_grid", _lib.I, [_lib.I])
+_lib.register("lzk_scan8_narrow", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P,
+                                           _lib.P, _lib.F, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
+NARROW_MAX_Q = 128  # below this many queries the int8 scan is the HBM-bound narrow kernel
 _lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
 
 # The dedicated int8 scan (csrc/kernels/scan8.hip: one K-tile stream across
@@ -354,6 +358,24 @@ def _scan8(X8, rscale, Q8, qscale, bias, alpha, thr, thr2, row_label, q_label, k
     cbp = (cb[0].data_ptr(), cb[1].data_ptr(), cb[2].data_ptr()) if cb is not None else (None, None, None)
     _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), regions, cap, nq, ca[0].data_ptr(),
                                  ca[1].data_ptr(), ca[2].data_ptr(), *cbp, st), "lzk_cand_gather")
+
+
+def _scan8_narrow(X8, rscale, Q8, qscale, bias, alpha, thr, kslot, S, cap, ca):
+    """Narrow-batch int8 candidate pass (scan8.hip scan8_narrow_kernel,
+    nq < 128: 16-row blocks streamed into registers against the queries in
+    LDS) + gather into the per-query lists ``ca``."""
+    L = _lib.lib()
+    nq, Dp = Q8.shape
+    N = X8.shape[0]
+    dev = Q8.device
+    st = _lib.stream_ptr(dev)
+    grid = L.lzk_scan8_narrow_grid(N)
+    bbuf, bcap, bcnt, regions = _wave_records(dev, grid, nq, kslot, S, 1)
+    _lib.check(L.lzk_scan8_narrow(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp,
+                                  _lib.ptr(bias), rscale.data_ptr(), qscale.data_ptr(), float(alpha), thr.data_ptr(),
+                                  bbuf.data_ptr(), bcap, bcnt.data_ptr(), st), "lzk_scan8_narrow")
+    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), regions, cap, nq, ca[0].data_ptr(),
+                                 ca[1].data_ptr(), ca[2].data_ptr(), None, None, None, st), "lzk_cand_gather")
 
 
 FP8_MAX = 448.0
@@ -467,6 +489,10 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     cap = max(2048, 16 * kslot * S)
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
     qs = qscale.contiguous()
+    if nq < NARROW_MAX_Q and SCAN8 and Dp % 64 == 0:
+        _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
+        _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
+        return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
     if _use_scan8(Dp):
         _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, None, None, None, kslot, 2 * S, 1, cap, (cnt, cs, ci),
                None)

@@ -587,3 +587,28 @@ def test_store_search_i8_rigorous_margin_gpu():
         assert hit == 1.0
     finally:
         TG.TenantGraph.LOWP, TG.TenantGraph.LOWP_RIGOROUS = saved
+
+
+@pytest.mark.parametrize("nq,D", [(1, 768), (7, 384), (33, 768), (127, 1024)])
+def test_scan8_narrow_matches_bf16_gpu(nq, D):
+    """Narrow batches (nq < 128) take the HBM-bound int8 kernel
+    (scan8_narrow_kernel): the same top-10 as the bf16 scan, for one query
+    and for partial 16-query tiles, with removed rows and a ragged row tail."""
+    from lazzaro_amd.ops import search as S
+    gen = torch.Generator(device=DEV).manual_seed(41 + nq)
+    N = 1_048_583
+    X = torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    Q = torch.randn(nq, D, device=DEV, generator=gen)
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
+    bias = -(X * X).sum(1).contiguous()
+    bias[::101] = float("-inf")
+    X8, rs = S.quantize_i8_rows(X16)
+    Q8, qs = S.quantize_i8_rows(Q16)
+    margin = torch.full((nq,), 0.02, device=DEV)
+    s8, r8 = S.flat_topk_i8(X8, rs, Q8, qs, X16, Q16, 16, bias=bias, alpha=2.0, margin=margin)
+    s16, r16 = S.flat_topk(X16, Q16, 16, bias=bias, alpha=2.0)
+    assert torch.equal(r8[:, :10], r16[:, :10])
+    assert torch.allclose(s8[:, :10], s16[:, :10], atol=1e-4, rtol=0)
+    assert not bool((r8 % 101 == 0).any())
