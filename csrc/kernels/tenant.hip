@@ -376,6 +376,63 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
 }
 
 
+// Consolidation's candidate re-rank in ONE launch (replaces a gather of the
+// [M, c, D] rows in float64, an einsum, a division and two sorts): exact
+// float64 cosine of each fact's kernel candidates -- <qn, x> / |x| with qn the
+// fp64 unit fact and x the fp32 row, |x| = sqrt(fp32 |x|^2) in fp64 (the
+// formula the batch planner replays) -- ranked (score desc, row asc), cut to
+// k; empty slots (-inf, -1). One wave per fact, 4 lanes per candidate.
+__global__ __launch_bounds__(256) void cos_rerank64_kernel(const double* __restrict__ Qn, long ldq,
+                                                           const float* __restrict__ X, long ldx, int D,
+                                                           const float* __restrict__ sqn,
+                                                           const long* __restrict__ cand, int C, int M, int k,
+                                                           double* __restrict__ os, long* __restrict__ oi) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= M) return;
+  const double* qr = Qn + (long)q * ldq;
+  const int part = lane & 3, cl = lane >> 2;
+  double my_s = -__builtin_huge_val();
+  long my_r = -1;
+  for (int c0 = 0; c0 < C; c0 += 16) {
+    const int c = c0 + cl;
+    const long r = c < C ? cand[(long)q * C + c] : -1;
+    double acc = 0.0;
+    if (r >= 0) {
+      const float* xr = X + r * ldx;
+      for (int d = part; d < D; d += 4) acc = fma(qr[d], (double)xr[d], acc);
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    double sc = -__builtin_huge_val();
+    if (r >= 0) {
+      const double nr = sqrt((double)sqn[r]);
+      sc = acc / (nr > 0.0 ? nr : 1.0);
+    }
+    const int src = 4 * ((lane - c0) & 15);
+    const double s2 = __shfl(sc, src, 64);
+    const long r2 = __shfl(r, src, 64);
+    if (lane >= c0 && lane < c0 + 16 && lane < C) { my_s = s2; my_r = r2; }
+  }
+  const bool live = lane < C && my_r >= 0;
+  int rank = 0;
+  for (int o = 0; o < C; ++o) {
+    const double s2 = __shfl(my_s, o, 64);
+    const long r2 = __shfl(my_r, o, 64);
+    // equal (score, row) pairs (a row listed twice) keep their slot order
+    if (r2 >= 0 && o != lane && (s2 > my_s || (s2 == my_s && (r2 < my_r || (r2 == my_r && o < lane))))) ++rank;
+  }
+  const int nlive = __popcll(__ballot(live));
+  if (live && rank < k) {
+    os[(long)q * k + rank] = my_s;
+    oi[(long)q * k + rank] = my_r;
+  }
+  for (int j = nlive + lane; j < k; j += 64) {
+    os[(long)q * k + j] = -__builtin_huge_val();
+    oi[(long)q * k + j] = -1;
+  }
+}
+
 // Embedding-row writes of a small node insert in ONE launch (the consolidation
 // segments insert ~20 facts, 43 times per 128-conversation step): per row j,
 // x = e32[j] * has[j] goes to emb32[rows[j]], its bf16 copy to emb16, the
@@ -583,5 +640,17 @@ LZK_EXPORT int lzk_tg_write_emb(const float* x, long ldx, const unsigned char* h
   if (D <= 0 || D > 1024 || (emb8 && !rs8)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tg_write_emb_kernel, dim3((unsigned)m), dim3(256), 0, (hipStream_t)stream, x, ldx, has, m, D,
                      rows, emb32, ld32, (u16*)emb16, ld16, (signed char*)emb8, ld8, rs8, sqn, sumsq, rs_max, dv_max);
+  return (int)hipGetLastError();
+}
+
+// Exact float64 cosine re-rank of candidate rows (cos_rerank64_kernel).
+// Qn [M, D] fp64 (row stride ldq), X fp32 rows (stride ldx), cand int64 [M, C]
+// (-1 empty, C <= 64), outputs [M, k] (k <= C).
+LZK_EXPORT int lzk_cos_rerank64(const double* Qn, long ldq, const float* X, long ldx, int D, const float* sqn,
+                                const long* cand, int C, int M, int k, double* os, long* oi, void* stream) {
+  if (M <= 0) return 0;
+  if (C <= 0 || C > 64 || k <= 0 || k > C || D <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cos_rerank64_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Qn, ldq,
+                     X, ldx, D, sqn, cand, C, M, k, os, oi);
   return (int)hipGetLastError();
 }

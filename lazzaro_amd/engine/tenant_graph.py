@@ -1534,7 +1534,20 @@ class TenantGraph:
 
     def _rerank_cos(self, Qn: torch.Tensor, cand: torch.Tensor, k: int):
         """Exact float64 cosine of kernel candidates ``cand`` [M, c] (-1 empty),
-        sorted (score desc, row asc), cut to k."""
+        sorted (score desc, row asc), cut to k. GPU: one launch
+        (tenant.hip cos_rerank64_kernel)."""
+        if self.on_gpu and cand.is_cuda and cand.shape[1] <= 64 and k <= cand.shape[1] and RERANK_KERNEL:
+            from ..ops import _lib
+            M, C = cand.shape
+            qd = Qn.to(self.device, torch.float64).contiguous()
+            cd = cand.to(torch.long).contiguous()
+            os_ = torch.empty((M, k), dtype=torch.float64, device=self.device)
+            oi = torch.empty((M, k), dtype=torch.long, device=self.device)
+            _lib.check(_lib.lib().lzk_cos_rerank64(qd.data_ptr(), qd.stride(0), self.emb32.data_ptr(),
+                                                    self.emb32.stride(0), self.dim, self.sqn.data_ptr(), cd.data_ptr(),
+                                                    C, M, k, os_.data_ptr(), oi.data_ptr(),
+                                                    _lib.stream_ptr(self.device)), "lzk_cos_rerank64")
+            return os_, oi
         valid = cand >= 0
         rows = cand.clamp_min(0)
         X = self.emb32[rows].double()  # [M, c, D]

@@ -159,6 +159,20 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
     sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
     if rows is not None:
         sub = rows[sub]
+    if X.is_cuda and X.dtype == torch.bfloat16 and X.shape[1] % 8 == 0 and X.shape[1] <= 2048 and sub.numel():
+        # one fused HIP kernel per pick, enqueued from C++ (csrc/kernels/kmeans.hip)
+        from ..ops import _lib
+        Sb = X[sub].contiguous()
+        m = min(k, Sb.shape[0])
+        L = _lib.lib()
+        picks = torch.empty(m, dtype=torch.int32, device=X.device)
+        ws = torch.empty(int(L.lzk_farthest_first_ws(Sb.shape[0], m)), dtype=torch.uint8, device=X.device)
+        _lib.check(L.lzk_farthest_first(Sb.data_ptr(), Sb.stride(0), Sb.shape[0], Sb.shape[1], m, picks.data_ptr(),
+                                        ws.data_ptr(), _lib.stream_ptr(X.device)), "lzk_farthest_first")
+        c = Sb[picks.long()].float()
+        if c.shape[0] < k:
+            c = torch.cat([c, Sb[torch.randint(0, Sb.shape[0], (k - c.shape[0],), generator=g).to(X.device)].float()])
+        return c
     S = X[sub].float()
     m = min(k, S.shape[0])
     picks = torch.zeros(m, dtype=torch.long, device=S.device)

@@ -313,6 +313,10 @@ _lib.register("lzk_scan8_grid", _lib.I, [_lib.I, _lib.I])
 _lib.register("lzk_scan8_narrow_grid", _lib.I, [_lib.I])
 _lib.register("lzk_scan8_narrow", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P,
                                            _lib.P, _lib.F, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
+_lib.register("lzk_farthest_first_ws", _lib.L, [_lib.I, _lib.I])
+_lib.register("lzk_farthest_first", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P])
+_lib.register("lzk_cos_rerank64", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.I, _lib.I,
+                                           _lib.I, _lib.P, _lib.P, _lib.P])
 NARROW_MAX_Q = 128  # below this many queries the int8 scan is the HBM-bound narrow kernel
 _lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
 

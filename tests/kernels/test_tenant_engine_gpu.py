@@ -612,3 +612,30 @@ def test_scan8_narrow_matches_bf16_gpu(nq, D):
     assert torch.equal(r8[:, :10], r16[:, :10])
     assert torch.allclose(s8[:, :10], s16[:, :10], atol=1e-4, rtol=0)
     assert not bool((r8 % 101 == 0).any())
+
+
+def test_cos_rerank64_kernel_matches_torch_gpu():
+    """Consolidation's float64 candidate re-rank in one launch
+    (cos_rerank64_kernel) == the torch gather / einsum / sort chain."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    gen = torch.Generator(device=DEV).manual_seed(29)
+    g = TenantGraph(device=DEV)
+    N, D, M, C = 4000, 384, 300, 16
+    X = torch.randn(N, D, device=DEV, generator=gen)
+    g.add_nodes([f"r{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("w"), stored=True)
+    Q = torch.randn(M, D, device=DEV, generator=gen, dtype=torch.float64)
+    Qn = Q / Q.norm(dim=1, keepdim=True)
+    cand = torch.stack([torch.randperm(N, device=DEV, generator=gen)[:C] for _ in range(M)])
+    cand[:, -2:] = -1
+    cand[::7, 3] = cand[::7, 4]  # a duplicated row keeps both slots, in row order
+    s1, r1 = g._rerank_cos(Qn, cand, 10)
+    saved = TG.RERANK_KERNEL
+    TG.RERANK_KERNEL = False
+    try:
+        s0, r0 = g._rerank_cos(Qn, cand, 10)
+    finally:
+        TG.RERANK_KERNEL = saved
+    assert torch.equal(r1, r0)
+    fin = torch.isfinite(s0)
+    assert torch.equal(fin, torch.isfinite(s1))
+    assert torch.allclose(s1[fin], s0[fin], atol=1e-12, rtol=0)
