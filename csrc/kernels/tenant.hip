@@ -265,10 +265,12 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
                                                               const int* __restrict__ ev_steps,
                                                               const double* __restrict__ ev_imp,
                                                               const int* __restrict__ ev_code,
-                                                              const long* __restrict__ ev_row, int* __restrict__ bad) {
+                                                              const long* __restrict__ ev_row, int* __restrict__ bad,
+                                                              const long* __restrict__ rowkey) {
 #pragma clang fp contract(off)
   const long i = (long)blockIdx.x * NTB + threadIdx.x;
   if (i >= n || kind[i] != 1 || sup[i] || pool[i]) return;
+  const long key = rowkey ? rowkey[i] : i;  // a row-sharded tenant ranks rows by global number
   float s = sal[i];
   const double a = fmin(1.0, (double)acc[i] / 10.0) * 0.3;
   const double d = (1.0 / (1.0 + (now - last[i]) / 86400.0)) * 0.2;
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
     for (; t < st; ++t) s = decay_sal(s, keep);
     const double imp = (double)s * 0.5 + a + d;
     const double vi = ev_imp[e];
-    if (imp < vi || (imp == vi && (code < ev_code[e] || (code == ev_code[e] && i < ev_row[e])))) {
+    if (imp < vi || (imp == vi && (code < ev_code[e] || (code == ev_code[e] && key < ev_row[e])))) {
       bad[0] = 1;
       return;
     }
@@ -583,10 +585,11 @@ LZK_EXPORT int lzk_tg_importance(const float* sal, const int* acc, const double*
 LZK_EXPORT int lzk_tg_evict_verify(const float* sal, const int* acc, const double* last, const unsigned char* kind,
                                    const unsigned char* sup, const int* shard, const unsigned char* pool, long n,
                                    double now, float keep, int ne, const int* ev_steps, const double* ev_imp,
-                                   const int* ev_code, const long* ev_row, int* bad, void* stream) {
+                                   const int* ev_code, const long* ev_row, int* bad, void* stream,
+                                   const long* rowkey) {
   if (n <= 0 || ne <= 0) return 0;
   hipLaunchKernelGGL(tg_evict_verify_kernel, dim3(blocks_for(n)), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last,
-                     kind, sup, shard, pool, n, now, keep, ne, ev_steps, ev_imp, ev_code, ev_row, bad);
+                     kind, sup, shard, pool, n, now, keep, ne, ev_steps, ev_imp, ev_code, ev_row, bad, rowkey);
   return (int)hipGetLastError();
 }
 

@@ -29,7 +29,7 @@ _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P,
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
 _lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
-_lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P])
+_lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P, P])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 _lib.register("lzk_pack_bits", I, [P, L, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
@@ -326,11 +326,13 @@ def importance(sal, acc, last, kind, sup, now: float) -> torch.Tensor:
 
 
 def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: float, keep: float,
-                 events: Sequence[Tuple[int, float, int, int]]) -> bool:
+                 events: Sequence[Tuple[int, float, int, int]], rowkey: Optional[torch.Tensor] = None) -> bool:
     """True when no row outside ``pool`` (uint8 mask) that nothing touched
     would have been evicted before the planned victims: ``events`` =
     (decays before the eviction, importance, shard, row) of each eviction's
-    last victim, in order (core/batch_plan.py)."""
+    last victim, in order (core/batch_plan.py). ``rowkey`` (int64 [n]): the
+    order key of each row in place of its index (a row-sharded tenant's
+    global row number)."""
     if not events:
         return True
     n = int(sal.numel())
@@ -351,7 +353,8 @@ def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: floa
                 s = np.where(s > fl, fl + (s - fl) * kf, fl).astype(np.float32)
                 t += 1
             imp = s.astype(np.float64) * 0.5 + a + d
-            if ((imp < vi) | ((imp == vi) & ((code < vc) | ((code == vc) & (idx < vr))))).any():
+            key = idx if rowkey is None else rowkey.numpy()[idx]
+            if ((imp < vi) | ((imp == vi) & ((code < vc) | ((code == vc) & (key < vr))))).any():
                 return False
         return True
     dev = sal.device
@@ -364,7 +367,8 @@ def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: floa
     _lib.check(_lib.lib().lzk_tg_evict_verify(sal.data_ptr(), acc.data_ptr(), last.data_ptr(), kind.data_ptr(),
                                               sup.data_ptr(), shard.data_ptr(), pool.data_ptr(), n, float(now),
                                               float(keep), len(ev), steps.data_ptr(), imp.data_ptr(),
-                                              code.data_ptr(), row.data_ptr(), bad.data_ptr(), _st(sal)),
+                                              code.data_ptr(), row.data_ptr(), bad.data_ptr(), _st(sal),
+                                              None if rowkey is None else rowkey.contiguous().data_ptr()),
                "tg_evict_verify")
     return int(bad.item()) == 0
 

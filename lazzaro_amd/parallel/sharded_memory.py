@@ -504,11 +504,18 @@ class ShardedMemorySystem:
 
     # ------------------------------------------------------------------ consolidation
     def consolidate_batch(self, conversations: Sequence[Sequence[Dict]], embeddings=None,
-                          now: Optional[float] = None) -> Dict[str, int]:
+                          now: Optional[float] = None, cadence: str = "conversation") -> Dict[str, int]:
         """Collective batched ``end_conversation`` (see module doc). Each rank
         passes its own finished conversations' extracted facts (and optionally
         their vectors, aligned with the flattened facts). Returns the counts of
-        the WHOLE batch (identical on every rank)."""
+        the WHOLE batch (identical on every rank).
+
+        ``cadence="conversation"`` (default): the reference's per-conversation
+        cadence -- the state ``MemorySystem.consolidate_batch`` (same cadence)
+        reaches on one process holding the union (:meth:`_consolidate_exact`);
+        ``"batch"``: eviction and run_consolidation once per batch."""
+        if cadence not in ("conversation", "batch"):
+            raise ValueError("cadence must be 'conversation' or 'batch'")
         g = self.g
         dev = self.device
         flat, conv, idx = [], [], []
@@ -552,6 +559,13 @@ class ShardedMemorySystem:
         B_loc = len(conversations)
         stats = {"conversations": 0, "facts": 0, "dup": 0, "inserted": 0, "linked": 0, "cross_links": 0,
                  "pruned": 0, "evicted": 0, "consolidations": 0, "fallbacks": 0}
+        if cadence == "conversation":
+            with self.local._graph_lock, tracer.stage("sharded_consolidate", dev):
+                self._consolidate_exact(flat, conv, E, B_loc, now, stats)
+                self.local.node_counter = self.next_id
+                with tracer.stage("persist", "cpu"):
+                    self.local._save_to_persistence()
+            return stats
         with self.local._graph_lock, tracer.stage("sharded_consolidate", dev):
             self._consolidate(flat, conv, E, B_loc, now, stats)
             self._evict(now, stats)
@@ -746,6 +760,406 @@ class ShardedMemorySystem:
             rr = torch.as_tensor([g.row_of[i] for i in ids], dtype=torch.long).to(dev)
             dst_rows[need] = rr
         g.append_edges(src_rows, dst_rows, W.float(), H.to(torch.int32), g.etype("relates_to"), now=now)
+
+    # ------------------------------------------------------------------ reference cadence
+    def _vrows(self, rows: torch.Tensor) -> torch.Tensor:
+        """Global row number of local rows: node number - 1 -- the row the
+        node has in a single process holding the union (nodes only, numbered
+        in creation order), so every order key equals the single process's."""
+        return torch.where(rows >= 0, self.num[rows.clamp_min(0)] - 1, torch.full_like(rows, -1))
+
+    def _held_rows(self, vrows: torch.Tensor) -> torch.Tensor:
+        """Local row of each global row this rank HOLDS live (-1 elsewhere:
+        not here, a ghost, or gone)."""
+        g = self.g
+        if g.n == 0 or vrows.numel() == 0:
+            return torch.full_like(vrows, -1)
+        r = self._rows_of_nums(vrows + 1)
+        rc = r.clamp_min(0)
+        ok = (r >= 0) & (self.holder[rc] == self.rank) & (g.kind[rc] == NODE)
+        return torch.where(ok, r, torch.full_like(r, -1))
+
+    def _merge_lists(self, s: torch.Tensor, v: torch.Tensor, k: int):
+        """Per fact: top-k of the gathered (score, global row) entries by
+        (score desc, row asc); -1 rows last (the single process's order)."""
+        key = torch.where(v >= 0, v, torch.full_like(v, BIG))
+        o = torch.argsort(key, dim=1, stable=True)
+        s, v = torch.gather(s, 1, o), torch.gather(v, 1, o)
+        o = torch.sort(s, dim=1, descending=True, stable=True).indices[:, :k]
+        s, v = torch.gather(s, 1, o), torch.gather(v, 1, o)
+        return s, torch.where(torch.isneginf(s), torch.full_like(v, -1), v)
+
+    def _gather_lists(self, s: torch.Tensor, v: torch.Tensor, k: int):
+        F = s.shape[0]
+        if self._coll:
+            s = self._gather_rows(s.contiguous()).view(self.world, F, k).permute(1, 0, 2).reshape(F, -1)
+            v = self._gather_rows(v.contiguous()).view(self.world, F, k).permute(1, 0, 2).reshape(F, -1)
+        return self._merge_lists(s, v, k)
+
+    def _exact_lists(self, Q: torch.Tensor, code_t: torch.Tensor, K: int):
+        """The planner's candidate lists: every fact's global and same-shard
+        top-K over every rank's live nodes (the same fused scan + float64
+        re-rank per rank, merged by global row). Returns numpy
+        ((gs, gv), (ws, wv)), rows as global row numbers."""
+        g = self.g
+        F = Q.shape[0]
+        dev = self.device
+        live = g.num_nodes() if g.n else 0
+        gs = ws = torch.full((F, K), NEG_INF, dtype=torch.float64, device=dev)
+        gv = wv = torch.full((F, K), -1, dtype=torch.long, device=dev)
+        sel = None
+        if live:
+            Qd = Q.double()
+            qn = Qd.norm(dim=1, keepdim=True)
+            sel = self._reach_mask(Qd / torch.where(qn > 0, qn, torch.ones_like(qn)))
+        n_scan = F if sel is None else int(sel.sum())
+        self.last_scan_work = n_scan * live
+        self.scan_work += self.last_scan_work
+        if live and n_scan:
+            n = g.n
+            mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0) & (self.holder[:n] == self.rank)
+            si = torch.arange(F, device=dev) if sel is None else torch.nonzero(sel).flatten()
+            with g.on_stream():
+                (a, ar), (b, br) = g.cos_topk(Q[si], K, mask, dual_label=code_t[si], min_score=LINK_THRESHOLD)
+            gs, ws = gs.clone(), ws.clone()
+            gv, wv = gv.clone(), wv.clone()
+            gs[si], ws[si] = a.to(dev).double(), b.to(dev).double()
+            gv[si], wv[si] = self._vrows(ar.to(dev)), self._vrows(br.to(dev))
+        (gs, gv), (ws, wv) = self._gather_lists(gs, gv, K), self._gather_lists(ws, wv, K)
+        return ((gs.cpu().numpy(), gv.cpu().numpy()), (ws.cpu().numpy(), wv.cpu().numpy()))
+
+    def _exact_pool(self, B: int, P: int, now: float):
+        """This rank's part of the eviction pool (its P lowest rows by
+        importance now and after all B decays, as the single process picks
+        over the union) -> (global pool rows, local mask or None when every
+        evictable row here is in it)."""
+        from ..core.consolidation import _lowest_keys
+        g = self.g
+        n = g.n
+        dev = self.device
+        local = torch.zeros(0, dtype=torch.long, device=dev)
+        mask = None
+        if n:
+            with g.on_stream():
+                held = (self.holder[:n] == self.rank).to(torch.uint8)
+                kind = torch.where(held.bool(), g.kind[:n], torch.zeros_like(g.kind[:n]))
+                imp0 = T.importance(g.sal[:n], g.acc[:n], g.last[:n], kind, g.sup[:n], now)
+                nev = int(torch.isfinite(imp0).sum())
+                if P >= nev:
+                    local = torch.nonzero(torch.isfinite(imp0)).flatten()
+                else:
+                    sal = g.sal[:n].clone()
+                    empty = {"src": torch.zeros(0, dtype=torch.int32, device=dev),
+                             "dst": torch.zeros(0, dtype=torch.int32, device=dev),
+                             "w": torch.zeros(0, dtype=torch.float32, device=dev)}
+                    T.decay_prune(empty, sal, kind, g.sup[:n], DECAY_RATE, None, steps=B)
+                    impB = T.importance(sal, g.acc[:n], g.last[:n], kind, g.sup[:n], now)
+                    okey = g.shard[:n].long() * (1 << NUM_BITS) + self._vrows(torch.arange(n, device=dev))
+                    mask = torch.zeros(n, dtype=torch.uint8, device=dev)
+                    for imp in (imp0, impB):
+                        mask[_lowest_keys(imp, okey, P)] = 1
+                    local = torch.nonzero(mask).flatten()
+        pv, _ = self._gather_var(self._vrows(local))
+        return torch.unique(pv).cpu().numpy().astype(np.int64), mask
+
+    def _row_states(self, want: np.ndarray):
+        """State (sal, acc, last, shard, super, |x|^2) and holder of global
+        rows ``want`` (sorted unique), each supplied by the rank holding it."""
+        g = self.g
+        dev = self.device
+        wt = torch.as_tensor(want, dtype=torch.long).to(dev)
+        r = self._held_rows(wt)
+        mine = torch.nonzero(r >= 0).flatten()
+        rr = r[mine]
+        with g.on_stream():
+            blk = torch.stack([wt[mine].double(), g.sal[rr].double(), g.acc[rr].double(), g.last[rr].double(),
+                               g.shard[rr].double(), g.sup[rr].double(), g.sqn[rr].double(),
+                               torch.full_like(rr, self.rank).double()], 1) if mine.numel() else \
+                torch.zeros((0, 8), dtype=torch.float64, device=dev)
+        allb, _ = self._gather_var(blk)
+        allb = allb[torch.argsort(allb[:, 0])] if allb.numel() else allb
+        a = allb.cpu().numpy()
+        rows = a[:, 0].astype(np.int64)
+        cols = (a[:, 1].astype(np.float32), a[:, 2].astype(np.int64), a[:, 3], a[:, 4].astype(np.int64),
+                a[:, 5] != 0, a[:, 6])
+        return rows, cols, dict(zip(rows.tolist(), a[:, 7].astype(np.int64).tolist()))
+
+    def _consolidate_exact(self, flat, conv, E, B_loc, now, stats) -> None:
+        """The reference cadence over the row-sharded buffer: every rank runs
+        the SAME native batch planner (core/batch_plan.py) on the global
+        inputs -- all-gathered facts, candidate lists merged over the ranks by
+        global row, the eviction pool as the union of every rank's lowest
+        rows, the touched rows' state from their holders -- so every decision
+        of the B conversations is known everywhere without further exchange
+        (the planner's exact-fallback callback is itself collective and runs
+        at the same point on every rank). The plan is applied in segments:
+        each rank applies what it holds (decay, row updates, inserts of the
+        facts it will hold, the edges whose source it holds, its victims),
+        and the collective ``run_consolidation`` / cluster pass run at the
+        segment ends, as in the single-process engine. The eviction pool is
+        verified on every rank (tg_evict_verify_kernel keyed by global row)."""
+        from ..core.batch_plan import PoolTooSmall, plan
+        g = self.g
+        dev = self.device
+        comm = self.comm
+        keep = 1.0 - DECAY_RATE
+        thr = self.prune_threshold if self.auto_prune else None
+        K = self.local.BATCH_LIST_K
+        # ---- 1. the global fact batch (rank-major conversation order)
+        with tracer.stage("sc_gather", dev):
+            bl = self._gather_rows(torch.tensor([B_loc], dtype=torch.int64, device=dev)).tolist()
+            B = int(sum(bl))
+            c_off = int(sum(bl[: self.rank]))
+            keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
+            keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self._coll else keys
+            sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
+            ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
+            Qa, fcnt = self._gather_var(E)
+            sal_in, _ = self._gather_var(sal_l)
+            ct, _ = self._gather_var(ct_l)
+        stats["conversations"] = B
+        F = int(Qa.shape[0])
+        stats["facts"] = F
+        if B == 0:
+            return
+        origin = torch.repeat_interleave(torch.arange(self.world, device=dev),
+                                         torch.tensor(fcnt, dtype=torch.long, device=dev)) if F else \
+            torch.zeros(0, dtype=torch.long, device=dev)
+        codes = self._register_shards(keys_all).astype(np.int64)
+        code_t = torch.as_tensor(codes).to(dev)
+        Q = Qa.float()
+        Qd = Q.double()
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        if F:
+            origin_conv = origin
+            origin = self._holders(Qn, origin_conv)
+            if origin is not origin_conv:  # holders need the contents of facts from other ranks
+                flat = [f for part in comm.all_gather_object([{"content": f["content"],
+                                                               "type": f.get("type", "semantic")} for f in flat])
+                        for f in part]
+                f_off = 0
+            else:
+                f_off = int(sum(fcnt[: self.rank]))
+        else:
+            f_off = 0
+        # ---- 2. candidate lists + the fact x fact block (the single process's formulas)
+        with tracer.stage("sc_scan", dev):
+            if F and g.dim is not None:
+                glob, shard = self._exact_lists(Q, code_t, K)
+            else:
+                e = (np.full((F, K), NEG_INF), np.full((F, K), -1, np.int64))
+                glob, shard = e, e
+            if F:
+                X = Q.double()
+                nrm = (X * X).sum(1).float().double().sqrt()
+                S = ((Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]).cpu().numpy()
+                qnorm = qn.flatten().cpu().numpy()
+                fact_n2 = (X * X).sum(1).float().double().cpu().numpy()
+            else:
+                S, qnorm, fact_n2 = np.zeros((0, 0)), np.zeros(0), np.zeros(0)
+
+        def fallback(j, evicted, same_shard):  # collective: every rank calls it at the same point
+            n = g.n
+            s_ = torch.full((1, K), NEG_INF, dtype=torch.float64, device=dev)
+            v_ = torch.full((1, K), -1, dtype=torch.long, device=dev)
+            if n and g.dim is not None:
+                m = (g.kind[:n] == NODE) & (g.sup[:n] == 0) & (self.holder[:n] == self.rank)
+                ev = np.asarray(evicted, np.int64)
+                if ev.size:
+                    er = self._held_rows(torch.as_tensor(ev).to(dev))
+                    er = er[er >= 0]
+                    if er.numel():
+                        m = m.clone()
+                        m[er] = False
+                with g.on_stream():
+                    if same_shard:
+                        a, ar = g._exact_cos(Qn[j:j + 1], m, K, row_label=g.shard[:n],
+                                             q_label=code_t[j:j + 1])
+                    else:
+                        a, ar = g._exact_cos(Qn[j:j + 1], m, K)
+                s_, v_ = a.to(dev).double(), self._vrows(ar.to(dev))
+            s_, v_ = self._gather_lists(s_, v_, K)
+            return s_[0].cpu().numpy(), v_[0].cpu().numpy()
+
+        def no_super(*a):
+            raise RuntimeError("a row-sharded tenant has no per-shard mean super-nodes")
+
+        # ---- 3. plan (identical on every rank), eviction pool verified everywhere
+        n0 = int(self.next_id)
+        node_count = self._sum(g.num_nodes())[0]
+        nsh = len(g.shard_count)
+        sc = torch.zeros(nsh, dtype=torch.int64, device=dev)
+        if nsh:
+            sc += torch.as_tensor(g.shard_count, dtype=torch.int64).to(dev)
+            if self._coll:
+                sc = self.comm.all_reduce(self._to_comm(sc)).to(dev)
+        shard_count = sc.cpu().tolist()
+        excess0 = max(0, node_count - self.max_buffer_size)
+        P = 4 * (F + excess0) + 1024  # per rank (a rank with fewer evictable rows pools them all)
+        cl_every = int(self.hierarchy_params["every"]) if self.hierarchy_params else 0
+        ct_np = ct.cpu().numpy().astype(np.int64)
+        sal_np = sal_in.cpu().numpy().astype(np.float32)
+        while True:
+            with tracer.stage("sc_pool", dev):
+                pool, pmask = self._exact_pool(B, P, now)
+                want = np.unique(np.concatenate([pool, glob[1][glob[1] >= 0], shard[1][shard[1] >= 0]]))
+                rows_v, cols, holder_of = self._row_states(want)
+            kw = dict(ct=ct_np, code=codes, sal_in=sal_np, n0=n0, node_count=node_count, shard_count=shard_count,
+                      super_codes=[], pre_members=no_super, max_buffer=self.max_buffer_size,
+                      super_threshold=getattr(self.local, "super_node_threshold", 20), ref_hierarchy=False,
+                      prune_thr=thr, keep=keep, now=now, pool=pool, rows=rows_v, cols=cols, glob=glob, shard=shard,
+                      sup_rows=np.zeros(0, np.int64), sup_cos=np.zeros((F, 0)), sup_n2=np.zeros(0), qnorm=qnorm,
+                      fact_n2=fact_n2, S=S, super_cos=no_super, fallback=fallback)
+            with tracer.stage("cb_plan", "cpu"):
+                pl = plan(kw, B, self.conversation_count, self.auto_consolidate, self.consolidate_every, cl_every,
+                          native=self.local.NATIVE_PLANNER)
+            with tracer.stage("cb_verify", dev):
+                ok = True
+                if pmask is not None and pl["events"]:
+                    n = g.n
+                    with g.on_stream():
+                        ok = T.evict_verify(g.sal[:n], g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], g.shard[:n],
+                                            pmask, now, keep, pl["events"],
+                                            rowkey=self._vrows(torch.arange(n, device=dev)))
+                bad, partial = self._sum(0 if ok else 1, 0 if pmask is None else 1)
+            if bad == 0:
+                break
+            if partial == 0:
+                raise PoolTooSmall("eviction plan failed verification with every row in the pool")
+            stats["pool_retries"] = stats.get("pool_retries", 0) + 1
+            P = 4 * P
+        ps = pl["stats"]
+        for k_ in ("dup", "inserted", "linked", "cross_links", "evicted", "fallbacks"):
+            stats[k_] += int(ps[k_])
+        pruned = int(ps["pruned_new"])
+        fact_key = np.asarray(pl["fact_key"], np.int64)
+        origin_h = origin.cpu().numpy() if F else np.zeros(0, np.int64)
+        # new rows: holder and shard (the ghost rows of edges need them)
+        for j in np.nonzero(fact_key >= 0)[0].tolist():
+            holder_of[int(fact_key[j])] = int(origin_h[j])
+        shard_of = dict(zip(rows_v.tolist(), cols[3].tolist()))
+        for j in np.nonzero(fact_key >= 0)[0].tolist():
+            shard_of[int(fact_key[j])] = int(codes[j])
+        self.next_id = n0 + int(ps["inserted"])
+        count0 = self.conversation_count
+        etype = g.etype("relates_to")
+        for seg in pl["segments"]:
+            with tracer.stage("cb_apply", dev):
+                pruned_local = self._apply_exact_segment(seg, fact_key, origin_h, codes, Q, flat, f_off, holder_of,
+                                                         shard_of, thr, now, etype)
+            pruned += self._sum(pruned_local)[0]
+            self.conversation_count = count0 + int(seg["c1"]) + 1
+            if seg["consolidate"]:
+                stats["consolidations"] += 1
+                with tracer.stage("run_consolidation", dev):
+                    self.run_consolidation()
+            if seg["cluster"]:
+                with tracer.stage("cluster", dev):
+                    self.cluster_pass()
+        stats["pruned"] += pruned
+        if self.hierarchy_params and getattr(g, "hier", None) is None:
+            self.cluster_pass()
+        if self.local.query_cache:
+            self.local.query_cache.invalidate_results()
+
+    def _apply_exact_segment(self, seg, fact_key, origin_h, codes, Q, flat, f_off, holder_of, shard_of, thr, now,
+                             etype) -> int:
+        """This rank's part of one plan segment (see :meth:`_consolidate_exact`).
+        Returns the local edges the segment's decay pruned."""
+        g = self.g
+        dev = self.device
+        me = self.rank
+        steps = int(seg["c1"]) - int(seg["c0"]) + 1
+        tok = g.segment_begin(DECAY_RATE, thr, steps)
+        tr = np.asarray(seg["tch_rows"], np.int64)
+        if tr.size:
+            loc = self._held_rows(torch.as_tensor(tr).to(dev))
+            keep_ = torch.nonzero(loc >= 0).flatten()
+            if keep_.numel():
+                k_h = keep_.cpu().numpy()
+                rt = loc[keep_]
+                with g.on_stream():
+                    g.sal[rt] = torch.as_tensor(np.asarray(seg["tch_sal"])[k_h], dtype=torch.float32).to(dev)
+                    g.acc[rt] = torch.as_tensor(np.asarray(seg["tch_acc"])[k_h], dtype=torch.int32).to(dev)
+                    g.last[rt] = torch.as_tensor(np.asarray(seg["tch_last"])[k_h], dtype=torch.float64).to(dev)
+                    g.dirty[rt] = 1
+                g._bump()
+        kinds = np.asarray(seg["ins_kind"]).tolist()
+        if any(k_ != 0 for k_ in kinds):
+            raise RuntimeError("a row-sharded tenant plans no super-nodes")
+        idx = np.asarray(seg["ins_idx"], np.int64)
+        if idx.size:
+            mine = idx[origin_h[idx] == me]
+            if mine.size:
+                pos = np.nonzero(origin_h[idx] == me)[0]
+                keys = fact_key[mine]
+                lf = [flat[int(j) - f_off] for j in mine]
+                rows = g.add_nodes([f"node_{int(k_) + 1}" for k_ in keys], [f["content"] for f in lf],
+                                   Q[torch.as_tensor(mine, dtype=torch.long).to(dev)], shard=codes[mine].astype(np.int32),
+                                   types=[f.get("type", "semantic") for f in lf],
+                                   sal=torch.as_tensor(np.asarray(seg["ins_sal"], np.float32)[pos]),
+                                   acc=torch.as_tensor(np.asarray(seg["ins_acc"], np.int32)[pos]),
+                                   last=torch.as_tensor(np.asarray(seg["ins_last"], np.float64)[pos]), now=now,
+                                   stored=True)
+                self._sync_num()
+                self.num[rows] = torch.as_tensor(keys + 1, dtype=torch.long).to(dev)
+                self.holder[rows] = me
+                self._reach_add(rows)
+        es = np.asarray(seg["edge_src"], np.int64)
+        if es.size:
+            ed = np.asarray(seg["edge_dst"], np.int64)
+            ew = np.asarray(seg["edge_w"], np.float32)
+            ec = np.asarray(seg["edge_code"], np.int64)
+            sel = np.asarray([holder_of.get(int(x), -1) == me for x in es.tolist()], bool)
+            if sel.any():
+                es, ed, ew, ec = es[sel], ed[sel], ew[sel], ec[sel]
+                src = self._held_rows(torch.as_tensor(es).to(dev))
+                dst = self._held_rows(torch.as_tensor(ed).to(dev))
+                need = torch.nonzero(dst < 0).flatten()
+                if need.numel():  # endpoints held elsewhere: ghost rows (created once per node)
+                    dv = ed[need.cpu().numpy()]
+                    ids = [f"node_{int(x) + 1}" for x in dv]
+                    fresh = {}
+                    for i, x in zip(ids, dv.tolist()):
+                        if g.row_of.get(i, -1) < 0 and i not in fresh:
+                            fresh[i] = (int(shard_of[int(x)]), int(holder_of[int(x)]))
+                    if fresh:
+                        fid = list(fresh)
+                        rn = g.add_nodes(fid, [""] * len(fid), None, shard=[fresh[i][0] for i in fid], ghost=True,
+                                         stored=False, now=now)
+                        self._sync_num()
+                        self.num[rn] = torch.as_tensor([int(i[5:]) for i in fid], dtype=torch.long).to(dev)
+                        self.holder[rn] = torch.as_tensor([fresh[i][1] for i in fid], dtype=torch.long).to(dev)
+                    dst[need] = torch.as_tensor([g.row_of[i] for i in ids], dtype=torch.long).to(dev)
+                g.append_edges(src, dst, torch.as_tensor(ew).to(dev), torch.as_tensor(ec, dtype=torch.int32).to(dev),
+                               etype, now=now)
+        vic = np.asarray(seg["victims"], np.int64)
+        loc_v = []
+        other = np.zeros(0, np.int64)
+        if vic.size:
+            hv = np.asarray([holder_of.get(int(x), -1) for x in vic.tolist()], np.int64)
+            mv = vic[hv == me]
+            if mv.size:
+                lr = self._held_rows(torch.as_tensor(mv).to(dev))
+                loc_v = lr[lr >= 0].cpu().tolist()
+            other = vic[hv != me]
+        ids = [g.ids[r] for r in loc_v]
+        pruned = g.segment_end(tok, loc_v, unstore=True)
+        if ids:
+            self.local._store_delete(ids)
+        if other.size and g.num_edges:  # edges here that point at a victim held elsewhere
+            rows = self._rows_of_nums(torch.as_tensor(other + 1).to(dev))
+            rows = rows[rows >= 0]
+            if rows.numel():
+                with g.on_stream():
+                    rm = torch.zeros(g.n, dtype=torch.uint8, device=dev)
+                    rm[rows] = 1
+                    g.e, k_, dropped = T.remove_edges_of(g.e, rm, g.shard[: g.n], want_dropped=g.track)
+                if dropped is not None and k_:
+                    g._note_dropped(*dropped)
+                g._bump(edges=True)
+        return int(pruned)
 
     # ------------------------------------------------------------------ eviction
     def _evict(self, now: float, stats: Dict[str, int]) -> None:

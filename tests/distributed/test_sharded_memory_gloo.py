@@ -117,7 +117,8 @@ def _single(tmp, cfg=CPU):
         real = tgm.time.time
         tgm.time.time = lambda s=s: _now(s)  # the single-process eviction reads the wall clock
         try:
-            stats.append(ms.consolidate_batch(convs, embeddings=V.to(dev), now=_now(s), cadence="batch"))
+            stats.append(ms.consolidate_batch(convs, embeddings=V.to(dev), now=_now(s),
+                                              cadence=cfg.get("cadence", "batch")))
         finally:
             tgm.time.time = real
     nodes, edges = _graph_state(g)
@@ -155,7 +156,8 @@ def _sharded(comm, cfg=CPU):
         c0, c1 = _split(len(convs), comm.world, comm.rank)
         f0 = sum(len(c) for c in convs[:c0])
         f1 = f0 + sum(len(c) for c in convs[c0:c1])
-        stats.append(sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1].to(dev), now=_now(s)))
+        stats.append(sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1].to(dev), now=_now(s),
+                                          cadence=cfg.get("cadence", "batch")))
         if rebal:  # all-to-all re-shard to even shares between batches; decisions must not change
             sm.rebalance()
             cnt = comm.all_gather_object(sm.g.num_nodes())
@@ -184,7 +186,7 @@ def _sharded(comm, cfg=CPU):
 def check_equivalent(out, world, limit):
     r0 = out[0]
     s_stats, s_nodes, s_edges, s_contents, s_prof, s_found = r0["single"]
-    assert r0["stats"] == s_stats
+    assert r0["stats"] == s_stats, (r0["stats"], s_stats)
     for r in range(world):  # every rank reports the same whole-batch counts and profile
         assert out[r]["stats"] == s_stats
         assert out[r]["prof"] == s_prof
@@ -226,6 +228,34 @@ def test_sharded_tenant_rebalance_keeps_semantics(world):
     out = spawn(world, functools.partial(_sharded, cfg=dict(CPU, rebalance=True)))
     check_equivalent(out, world, LIMIT)
     assert all(s <= 1 for s in out[0]["spread"])
+
+
+EXACT = dict(CPU, cadence="conversation")
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_sharded_tenant_reference_cadence_matches_single_process(world):
+    """cadence="conversation" (the default): the reference's per-conversation
+    cadence over the row-sharded buffer equals a single process's
+    ``consolidate_batch(cadence="conversation")`` on the union -- eviction
+    per conversation, run_consolidation at every multiple of 3."""
+    out = spawn(world, functools.partial(_sharded, cfg=EXACT))
+    check_equivalent(out, world, LIMIT)
+    assert sum(st["consolidations"] for st in out[0]["stats"]) == STEPS * CONVS // 3
+
+
+def test_sharded_tenant_reference_cadence_forced_world1():
+    check_equivalent(spawn(1, functools.partial(_sharded, cfg=dict(EXACT, force=True))), 1, LIMIT)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tenant_reference_cadence_pruned_cluster(world):
+    check_equivalent(spawn(world, functools.partial(_sharded, cfg=dict(EXACT, pruned=True))), world, LIMIT)
+
+
+def test_sharded_tenant_reference_cadence_rebalance():
+    out = spawn(3, functools.partial(_sharded, cfg=dict(EXACT, rebalance=True)))
+    check_equivalent(out, 3, LIMIT)
 
 
 def _sharded_hierarchy(comm):
