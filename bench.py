@@ -51,8 +51,11 @@ Multi-GPU work inside the JSON line (all timed, every rank, RCCL over xGMI):
   (all-gather of the queries, local scans, one all-to-all of the candidates
   back to their origin, merge -- SURVEY §2.5 C1 + K2).
 * ``consolidate_sharded``: config 4 as ONE buffer row-sharded over the ranks
-  (``ShardedMemorySystem.consolidate_batch``: facts all-gathered, top-3 lists
-  merged, global eviction, distributed components and k-means) on
+  (``ShardedMemorySystem.consolidate_batch`` at the reference's
+  per-conversation cadence: facts all-gathered, top-8 candidate lists merged
+  by global row, one replicated native plan of the B conversations, eviction
+  and run_consolidation (distributed components) at every planned point,
+  distributed k-means) on
   topic-clustered rows with cluster placement; ``scan_facts_x_rows_per_rank_step``
   is the measured per-rank scan work after the exact cone pruning (the
   unpruned figure alongside).

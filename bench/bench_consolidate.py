@@ -198,7 +198,7 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
 def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: int, warmup: int, encoder=None,
                 dim: int = 768, dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096,
                 n_top: int = 64, cluster_iters: int = 2, init_edges: int = None, db_dir: str = None,
-                clustered: bool = False, topics_per_rank: int = 32):
+                clustered: bool = False, topics_per_rank: int = 32, cadence: str = "conversation"):
     """BASELINE config 4 as ONE tenant: a ``nodes_per_rank * world``-node
     buffer row-sharded over the ranks (``ShardedMemorySystem``); every step
     each rank brings ``convs`` conversations, the whole batch is consolidated
@@ -213,7 +213,10 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     cluster's home rank (``placement="cluster"``); the exact cone pruning
     then lets a rank skip the facts no cluster it holds can reach, and the
     reported ``scan_facts_x_rows_per_rank_step`` is the measured count
-    (``ShardedMemorySystem.last_scan_work``, max over ranks)."""
+    (``ShardedMemorySystem.last_scan_work``, max over ranks).
+
+    ``cadence``: "conversation" (default, the reference's per-conversation
+    eviction / run_consolidation, planned once per batch) or "batch"."""
     from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
     from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
 
@@ -268,7 +271,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
             from lazzaro_amd.utils.tracing import tracer as _tr
             with _tr.stage("fact_embed", dev):
                 sm.local._batch_embed_any([f["content"] for c in conversations for f in c])
-        return sm.consolidate_batch(conversations, embeddings=V)
+        return sm.consolidate_batch(conversations, embeddings=V, cadence=cadence)
 
     for _ in range(warmup):
         step()
@@ -300,7 +303,8 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
            "scan_facts_x_rows_per_rank_step": int(wk.item()),
            "scan_facts_x_rows_unpruned_per_rank_step": int(world * convs * facts * nodes_per_rank),
            "data": "clustered topics, cluster placement" if clustered else "uniform random rows",
-           "path": "ShardedMemorySystem.consolidate_batch (one tenant row-sharded over the ranks)",
+           "path": "ShardedMemorySystem.consolidate_batch (one tenant row-sharded over the ranks), cadence=%s"
+                   % cadence,
            "hierarchical_clustering": {"mode": "distributed kmeans", "every_steps": cluster_every, "fine": n_fine,
                                        "top": n_top, "iters_per_pass": cluster_iters,
                                        "seed_pass_ms": round(seed_ms, 1)},
@@ -337,6 +341,8 @@ if __name__ == "__main__":
                     help="config 4 as one tenant row-sharded over the ranks (--nodes per rank)")
     ap.add_argument("--clustered", action="store_true",
                     help="--sharded: per-rank topic clusters + cluster placement (exact scan pruning applies)")
+    ap.add_argument("--cadence", default="conversation", choices=["conversation", "batch"],
+                    help="--sharded: reference per-conversation cadence or once-per-batch")
     a = ap.parse_args()
     comm = Communicator.init()
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -348,7 +354,7 @@ if __name__ == "__main__":
     fn = run_sharded if a.sharded else run
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
-             **({"clustered": a.clustered} if a.sharded else {"prune_threshold": a.prune_threshold,
+             **({"clustered": a.clustered, "cadence": a.cadence} if a.sharded else {"prune_threshold": a.prune_threshold,
                                                               "persist_async": a.persist_async}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)

@@ -379,7 +379,9 @@ class Planner {
     s.edges.swap(live);
   }
 
-  void run(int B, i64 count0, bool autoc, i64 every, i64 cluster_every) {
+  // seg_each: close a segment after EVERY conversation (a durable commit
+  // per conversation, like the reference's save per end_conversation)
+  void run(int B, i64 count0, bool autoc, i64 every, i64 cluster_every, bool seg_each) {
     next_row = n0;
     segs.clear();
     segs.push_back(Seg{0, 0});
@@ -400,7 +402,7 @@ class Planner {
       const i64 count = count0 + c + 1;
       const bool point = autoc && every > 0 && count % every == 0;
       const bool clus = cluster_every > 0 && count / cluster_every > (count - 1) / cluster_every;
-      if (point || clus || c == B - 1) {
+      if (point || clus || seg_each || c == B - 1) {
         seg->consolidate = point;
         seg->cluster = clus;
         close();
@@ -501,7 +503,8 @@ py::dict plan_batch(py::dict kw) {
   p.dup_of.assign(M, -1);
   p.fact_live.assign(M, 0);
   p.run(py::cast<int>(kw["B"]), py::cast<i64>(kw["count0"]), py::cast<bool>(kw["auto"]),
-        py::cast<i64>(kw["every"]), py::cast<i64>(kw["cluster_every"]));
+        py::cast<i64>(kw["every"]), py::cast<i64>(kw["cluster_every"]),
+        kw.contains("seg_each") && py::cast<bool>(kw["seg_each"]));
 
   py::list segs;
   for (auto& s : p.segs) {

@@ -386,9 +386,11 @@ class BatchPlanner:
                 self.e_alive &= ~dead
 
     # ------------------------------------------------------------------ driver
-    def run(self, B: int, count0: int, auto: bool, every: int, cluster_every: int) -> List[Segment]:
+    def run(self, B: int, count0: int, auto: bool, every: int, cluster_every: int,
+            seg_each: bool = False) -> List[Segment]:
         """Conversations 0..B-1; segments end where ``run_consolidation``
-        (count % every == 0) or a k-means cluster pass is due, and at B-1."""
+        (count % every == 0) or a k-means cluster pass is due, and at B-1
+        (``seg_each``: after every conversation)."""
         self._next_row = self.n0
         self._pending_dups = {}
         segs: List[Segment] = []
@@ -408,7 +410,7 @@ class BatchPlanner:
             count = count0 + c + 1
             point = bool(auto) and count % every == 0
             clus = bool(cluster_every) and count // cluster_every > (count - 1) // cluster_every
-            if point or clus or c == B - 1:
+            if point or clus or seg_each or c == B - 1:
                 self._seg.consolidate, self._seg.cluster = point, clus
                 segs.append(self._close())
                 if c < B - 1:
@@ -462,14 +464,16 @@ def segments_as_dicts(pl: "BatchPlanner", segs: List[Segment]) -> List[Dict]:
     return out
 
 
-def plan(kw: Dict, B: int, count0: int, auto: bool, every: int, cluster_every: int, native: bool = True) -> Dict:
+def plan(kw: Dict, B: int, count0: int, auto: bool, every: int, cluster_every: int, native: bool = True,
+         seg_each: bool = False) -> Dict:
     """Run the planner (native ``_lzrt.plan_batch`` by default, this module's
     BatchPlanner as the reference) on one input dict; returns segments,
-    supers, events, fact_key, dup_of and stats in the native format."""
+    supers, events, fact_key, dup_of and stats in the native format.
+    ``seg_each``: one segment per conversation (per-conversation commits)."""
     if native:
         from ..store.colstore import _rt
         args = dict(kw)
-        args.update(B=B, count0=count0, auto=auto, every=every, cluster_every=cluster_every)
+        args.update(B=B, count0=count0, auto=auto, every=every, cluster_every=cluster_every, seg_each=seg_each)
         gs, gr = args.pop("glob")
         ss, sr = args.pop("shard")
         args.update(gs=np.ascontiguousarray(gs, np.float64), gr=np.ascontiguousarray(gr, np.int64),
@@ -489,7 +493,7 @@ def plan(kw: Dict, B: int, count0: int, auto: bool, every: int, cluster_every: i
         args["shard_count"] = np.asarray(args["shard_count"], np.int64)
         return _rt().plan_batch(args)
     pl = BatchPlanner(**kw)
-    segs = pl.run(B, count0, auto, every, cluster_every)
+    segs = pl.run(B, count0, auto, every, cluster_every, seg_each)
     return {"segments": segments_as_dicts(pl, segs),
             "supers": [{"code": sp.code, "key": sp.key, "conv": sp.conv, "children": np.asarray(sp.children)}
                        for sp in pl.supers],

@@ -636,7 +636,7 @@ class ConsolidationMixin:
     BATCH_LIST_K = 8
 
     def consolidate_batch(self, conversations: Sequence[Sequence[Dict]], embeddings=None,
-                          now: float = None, cadence: str = "conversation") -> Dict[str, int]:
+                          now: float = None, cadence: str = "conversation", commit: str = "batch") -> Dict[str, int]:
         """``end_conversation`` for B finished conversations at once, given
         their extracted facts (``conversations[c]`` = fact dicts with
         ``content`` / ``type`` / ``salience`` / ``topic``, the extraction
@@ -654,8 +654,13 @@ class ConsolidationMixin:
         the pre-batch graph (eviction: an exact pool argument), and the plan
         is applied to the device graph in segments that end at the
         ``run_consolidation`` points, where run_consolidation runs on the
-        real graph. Only the persistence commit is once per batch (the store
-        then holds the same rows / edges / profile as after the last call).
+        real graph. ``commit="batch"`` (default): one persistence commit per
+        batch (the store then holds the same rows / edges / profile as after
+        the last call; a crash mid-batch loses the batch, not just the
+        current conversation); ``commit="conversation"``: the plan closes a
+        segment after every conversation and each is committed as it is
+        applied -- the reference's save per ``end_conversation`` (reference
+        :648, :785), at the cost of one commit per conversation.
 
         ``cadence="batch"``: the coarser batch semantics of the row-sharded
         buffer (``ShardedMemorySystem``): every conversation's facts are
@@ -670,6 +675,9 @@ class ConsolidationMixin:
         run_consolidation calls), fallbacks (candidate lists recomputed)."""
         if cadence not in ("conversation", "batch"):
             raise ValueError("cadence must be 'conversation' or 'batch'")
+        if commit not in ("conversation", "batch"):
+            raise ValueError("commit must be 'conversation' or 'batch'")
+        self._commit_each = commit == "conversation" and cadence == "conversation"
         flat, conv, idx = [], [], []
         j = 0
         for c, fs in enumerate(conversations):
@@ -764,6 +772,8 @@ class ConsolidationMixin:
                 stats["consolidations"] += 1
                 self.run_consolidation()
             self._maybe_cluster(self.conversation_count - 1)
+            if self._commit_each:
+                self._save_to_persistence()
 
     # LZK_PY_PLANNER=1: the Python reference planner instead of the native one
     NATIVE_PLANNER = os.environ.get("LZK_PY_PLANNER", "0") != "1"
@@ -811,7 +821,7 @@ class ConsolidationMixin:
                       **inputs)
             with tracer.stage("cb_plan", "cpu"):
                 pl = plan(kw, B, self.conversation_count, self.auto_consolidate, self.consolidate_every, cl_every,
-                          native=self.NATIVE_PLANNER)
+                          native=self.NATIVE_PLANNER, seg_each=self._commit_each)
             with tracer.stage("cb_verify", self._device):
                 ok = pool_mask is None or self._verify_pool(pool_mask, pl["events"], now)
             if ok:
@@ -825,11 +835,15 @@ class ConsolidationMixin:
             stats[k] += int(ps[k])
         stats["pruned"] += int(ps["pruned_new"])
         fact_key = np.asarray(pl["fact_key"], np.int64)
-        keys = fact_key[fact_key >= 0]
-        id_of = dict(zip(keys.tolist(), (self._generate_node_id() for _ in range(keys.size))))
         fact_of = {int(k): int(j) for j, k in enumerate(fact_key.tolist()) if k >= 0}
+        id_of = {}
         count0 = self.conversation_count
         for seg in pl["segments"]:
+            # node ids as the segment's facts are inserted (keys grow segment by
+            # segment): a per-segment commit persists the sequential counter
+            ik = np.asarray(seg["ins_kind"])
+            for key in sorted(fact_key[np.asarray(seg["ins_idx"], np.int64)[ik == 0]].tolist()):
+                id_of[key] = self._generate_node_id()
             with tracer.stage("cb_apply", self._device):
                 stats["pruned"] += self._apply_segment(seg, pl["supers"], fact_key, fact_of, facts, codes, E,
                                                        id_of, thr, now)
@@ -840,6 +854,9 @@ class ConsolidationMixin:
                     self.run_consolidation(prune=not self.auto_prune)
             if seg["cluster"]:
                 self._maybe_cluster(self.conversation_count - 1)
+            if self._commit_each:
+                with tracer.stage("commit", "cpu"):
+                    self._save_to_persistence()
         if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
             self._maybe_cluster(self.conversation_count - 1)
 

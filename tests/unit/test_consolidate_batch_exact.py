@@ -168,3 +168,46 @@ def test_batch_equals_sequential_gpu(tmp_path, monkeypatch):
     assert s1["evicted"] + s2["evicted"] > 0
     for k in a:
         assert a[k] == b[k], k
+
+
+def test_batch_commit_per_conversation(tmp_path, monkeypatch):
+    """commit="conversation": a segment per conversation, each committed as it
+    is applied -- every commit sees the graph the sequential run persisted
+    after the same end_conversation (a crash loses at most the conversation
+    in flight, as in the reference)."""
+    import time as _time
+
+    from lazzaro_amd.core.memory_system import MemorySystem
+    monkeypatch.setattr(_time, "time", lambda: 1_900_000_000.0)
+    snaps = {"seq": [], "bat": []}
+    orig = MemorySystem._save_to_persistence
+
+    def rec(self):  # the state each commit leaves (stored / dirty bits included)
+        out = orig(self)
+        snaps[self._tag].append(_state(self))
+        return out
+    monkeypatch.setattr(MemorySystem, "_save_to_persistence", rec)
+    B = 15
+    convs = conversations(B)
+    seq = _system(tmp_path / "seq", "cpu")
+    seq._tag = "seq"
+    for facts in convs:
+        seq.start_conversation()
+        seq.add_to_short_term("FACTS:" + json.dumps(facts), "episodic", 0.7)
+        seq.end_conversation()
+    bat = _system(tmp_path / "bat", "cpu")
+    bat._tag = "bat"
+    st = bat.consolidate_batch(convs, now=1_900_000_000.0, commit="conversation")
+    assert st["evicted"] > 0 and st["consolidations"] == B // 3
+    assert len(snaps["bat"]) == B + 1  # + the batch-end commit (nothing left to write)
+    # the sequential end_conversation commits twice (reference :785 inside the
+    # consolidation, :648 after it); the second is the conversation's state
+    assert len(snaps["seq"]) == 2 * B
+    for c in range(B):
+        a, b = snaps["seq"][2 * c + 1], snaps["bat"][c]
+        for k in a:
+            if k == "shards":  # the batch registers its shards up front (empty ones are not persisted)
+                a[k], b[k] = ({s: n for s, n in x[k].items() if n} for x in (a, b))
+            assert a[k] == b[k], (c, k)
+    with pytest.raises(ValueError):
+        bat.consolidate_batch(convs[:1], commit="sometimes")
