@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--stream", type=int, default=1, help="1: serve_stream (pipelined rounds), 0: serve per round")
+    ap.add_argument("--global-batch", type=int, default=128,
+                    help="queries per rank of the global (every-tenant) search; 0 = skip")
+    ap.add_argument("--global-steps", type=int, default=5)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
@@ -138,6 +141,8 @@ def main():
            "path": ("serve_stream() (round i+1 enqueued before round i is materialised)" if a.stream else "serve()")
            + " -> owner's one embed + one segment_topk over tenants' fp32 rows -> Node dicts",
            "data": "synthetic (random unit vectors, synthetic query texts, random-init encoder)"}
+    if a.global_batch > 0 and a.global_steps > 0:
+        res["global"] = run_global(svc, comm, emb, dev, a, words, rng)
     from lazzaro_amd.utils.tracing import tracer
     if tracer.enabled:
         res["stages_ms"] = {k: v["p50_ms"] for k, v in tracer.summary().items()}
@@ -147,6 +152,47 @@ def main():
             with open(a.out, "w") as f:
                 f.write(json.dumps(res) + "\n")
     svc.close()
+
+
+def run_global(svc, comm, emb, dev, a, words, rng):
+    """Global search (every query against EVERY tenant of every rank:
+    DistributedMemoryService.search_global_batch) on pre-embedded queries:
+    the rank's small tenants in one tile-table MFMA pass (mtscan.hip), the
+    candidates all-to-all'ed back to their origin for N > 1. Exactness: the
+    first batch against the per-tenant store searches (LZK_MT_GLOBAL=0)."""
+    from lazzaro_amd.parallel import routing
+    qs = [" ".join(rng.choice(words) for _ in range(12)) for _ in range(a.global_batch * (a.global_steps + 2))]
+    E = emb.batch_embed_tensor(qs) if hasattr(emb, "batch_embed_tensor") else None
+    E = (E[0] if isinstance(E, tuple) else E).float()
+    Eb = [E[i * a.global_batch:(i + 1) * a.global_batch] for i in range(a.global_steps + 2)]
+    routing.search_global_batch(svc, Eb[0], a.k)  # warm (tile table build)
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.global_steps):
+        got = routing.search_global_batch(svc, Eb[1 + i], a.k)
+    torch.cuda.synchronize()
+    comm.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    comm.all_reduce(t, "max")
+    el = float(t.item())
+    chk = routing.search_global_batch(svc, Eb[-1][:64], a.k)
+    mt = routing.MT_GLOBAL
+    routing.MT_GLOBAL = False
+    try:
+        ref = routing.search_global_batch(svc, Eb[-1][:64], a.k)
+    finally:
+        routing.MT_GLOBAL = mt
+    same = int(torch.equal(chk.keys, ref.keys))
+    ok = torch.tensor([same, 1], dtype=torch.int64, device=dev)
+    comm.all_reduce(ok)
+    return {"qps": round(comm.world * a.global_batch * a.global_steps / el, 1),
+            "qps_per_gpu": round(a.global_batch * a.global_steps / el, 1),
+            "ms_per_step": round(el / a.global_steps * 1e3, 3), "batch_per_rank": a.global_batch,
+            "exact_match_vs_per_tenant_search": f"{int(ok[0])}/{int(ok[1])} ranks (64 queries each)",
+            "path": "routing.search_global_batch: small tenants in one tile-table MFMA pass (mtscan.hip) + "
+                    "fp32 re-rank; all-gather of queries / all-to-all of candidates for N > 1"}
 
 
 if __name__ == "__main__":

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -806,3 +807,113 @@ def topk_large(X, Q, k, *, bias=None, alpha=1.0, idx_offset=0, chunk=1 << 20):
             best_s, o = torch.topk(cs, min(k, cs.shape[1]), dim=1)
             best_i = torch.gather(ci, 1, o)
     return best_s, best_i + idx_offset
+
+
+# ---------------------------------------------------------------------------
+# Multi-tenant global search (csrc/kernels/mtscan.hip): every query against
+# the rows of MANY small tenants in one MFMA pass over a tile table.
+_lib.register("lzk_mt_cand", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.I, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.F,
+                                      _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P])
+_lib.register("lzk_mt_sample", _lib.I, [_lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.L, _lib.I, _lib.P, _lib.P,
+                                        _lib.P])
+_lib.register("lzk_mt_rerank", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.I, _lib.I, _lib.I, _lib.P, _lib.P,
+                                        _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P])
+MT_TILE = 256
+MT_STRIDE = 64  # the threshold sample: rows 0, 64, 128, 192 of every tile
+
+
+class MtTiles:
+    """Tile table of a set of tenants (host-built, uploaded once per change):
+    tile t = rows [row0[t], row0[t] + n[t]) (n <= 256) of tenant slot
+    ``slot[t]``; ``x`` / ``b`` the addresses of its first bf16 row / store
+    bias entry. ``s_tile`` / ``s_row``: the strided threshold sample."""
+
+    def __init__(self, slots: np.ndarray, nrows: np.ndarray, e16: np.ndarray, bias: np.ndarray, ld16: int,
+                 device):
+        nrows = np.asarray(nrows, np.int64)
+        keep = nrows > 0
+        slots, nrows, e16, bias = slots[keep], nrows[keep], e16[keep], bias[keep]
+        nt = (nrows + MT_TILE - 1) // MT_TILE
+        T = int(nt.sum())
+        first = np.repeat(np.cumsum(nt) - nt, nt)
+        which = np.repeat(np.arange(slots.size), nt)
+        row0 = (np.arange(T) - first) * MT_TILE
+        tn = np.minimum(MT_TILE, nrows[which] - row0)
+        self.n_tiles = T
+        self.ld16 = int(ld16)
+        self.rows = int(nrows.sum())
+        h_x = e16[which] + row0 * self.ld16 * 2
+        h_b = bias[which] + row0 * 4
+        # sample rows: every MT_STRIDE-th row of every tile
+        per = (tn + MT_STRIDE - 1) // MT_STRIDE
+        s_first = np.repeat(np.cumsum(per) - per, per)
+        s_tile = np.repeat(np.arange(T), per)
+        s_row = (np.arange(int(per.sum())) - s_first) * MT_STRIDE
+        self.n_sample = int(s_tile.size)
+
+        def up(a, dt):
+            t = torch.from_numpy(np.ascontiguousarray(a, dt))
+            return t.pin_memory().to(device, non_blocking=True) if torch.device(device).type == "cuda" else t
+        self.x, self.b, self.n = up(h_x, np.int64), up(h_b, np.int64), up(tn, np.int32)
+        self.slot, self.row0 = up(slots[which], np.int32), up(row0, np.int32)
+        self.s_tile, self.s_row = up(s_tile, np.int32), up(s_row, np.int32)
+
+
+def _mt_threshold(Xs, bs, Q16, kc, kslot, alpha):
+    """Lower bound of each query's kc-th best score: the sample's exact
+    kc-th best, lowered by the accumulation-order margin (_sample_threshold)."""
+    if Xs.shape[0] < kc:
+        return torch.full((Q16.shape[0],), float("-inf"), dtype=torch.float32, device=Q16.device)
+    ts, _ = _flat_topk_lane(Xs, Q16, kslot, kslot, bs, None, None, alpha, 0, None)
+    thr = ts[:, kc - 1].contiguous()
+    return torch.nan_to_num(thr - 2e-4 * (1.0 + thr.abs()), nan=float("-inf"))
+
+
+def mt_topk(tiles: MtTiles, Q: torch.Tensor, k: int, p_e32: torch.Tensor, p_bias: torch.Tensor,
+            p_kind: torch.Tensor, metric: str = "l2"):
+    """Every query's top-k over all the table's tenants: store scores (L2:
+    -|q-x|^2, ip: <q,x>, + the store bias), bf16 MFMA candidates above a
+    sampled lower bound of the 2k-th best, the best 2k (<= 16) of them
+    re-scored in fp32 from the tenants' rows. Returns (scores fp32 [nq, k],
+    keys int64 [nq, k] = slot << 32 | row, overflow int32 [nq]): a query
+    whose candidate list overflowed (ovf = 1) must be recomputed by the
+    caller; rows that are not live nodes come back as (-inf, -1)."""
+    L = _lib.lib()
+    dev = Q.device
+    nq, D = Q.shape
+    Dp = tiles.ld16
+    kc = min(16, max(k, 2 * k))
+    kslot = L.lzk_flat_topk_kslot(int(kc))
+    if kslot < 0 or k > kc:
+        raise ValueError("mt_topk supports k <= 16")
+    st = _lib.stream_ptr(dev)
+    Qf = Q.to(dev, torch.float32).contiguous()
+    Q16 = torch.zeros((nq, Dp), dtype=torch.bfloat16, device=dev)
+    Q16[:, :D] = Qf
+    alpha = 2.0 if metric == "l2" else 1.0
+    ns = tiles.n_sample
+    # 1. threshold: exact top-kc of the sample (a subset: its kc-th best is <=
+    #    the whole table's), lowered by the accumulation-order margin
+    Xs = torch.empty((ns, Dp), dtype=torch.bfloat16, device=dev)
+    bs = torch.empty((ns,), dtype=torch.float32, device=dev)
+    _lib.check(L.lzk_mt_sample(tiles.x.data_ptr(), tiles.b.data_ptr(), tiles.s_tile.data_ptr(),
+                               tiles.s_row.data_ptr(), ns, Dp, Dp, Xs.data_ptr(), bs.data_ptr(), st), "lzk_mt_sample")
+    thr = _mt_threshold(Xs, bs, Q16, kc, kslot, alpha)
+    # 2. candidates over every tile
+    cap = max(1024, 8 * kslot * MT_STRIDE)
+    cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    _lib.check(L.lzk_mt_cand(tiles.x.data_ptr(), tiles.b.data_ptr(), tiles.n.data_ptr(), tiles.n_tiles, Dp,
+                             Q16.data_ptr(), Dp, nq, Dp, float(alpha), thr.data_ptr(), cap, cnt.data_ptr(),
+                             cs.data_ptr(), ci.data_ptr(), st), "lzk_mt_cand")
+    # 3. best kc by bf16 score, 4. fp32 re-rank to k
+    os_ = torch.empty((nq, kc), dtype=torch.float32, device=dev)
+    oi = torch.empty((nq, kc), dtype=torch.long, device=dev)
+    ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
+    _lib.check(L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, kc, 0,
+                                 os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), None, st), "lzk_cand_select")
+    s = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    key = torch.empty((nq, k), dtype=torch.long, device=dev)
+    _lib.check(L.lzk_mt_rerank(Qf.data_ptr(), D, D, oi.data_ptr(), kc, nq, int(k), tiles.slot.data_ptr(),
+                               tiles.row0.data_ptr(), p_e32.data_ptr(), p_bias.data_ptr(), p_kind.data_ptr(),
+                               0 if metric == "l2" else 1, s.data_ptr(), key.data_ptr(), st), "lzk_mt_rerank")
+    return s, key, ovf

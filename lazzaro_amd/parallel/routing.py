@@ -35,6 +35,7 @@ all-to-alls and one tiny all-gather per batch).
 from __future__ import annotations
 
 import hashlib
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -46,7 +47,7 @@ NODE = 1
 # search (MFMA candidate scan + fp32 re-rank); smaller ones share one fused
 # segment_topk launch over their fp32 rows
 BIG_ROWS = 1 << 18
-_COLS = ("emb32", "bias", "sal", "acc", "kind", "sup", "shard")
+_COLS = ("emb32", "bias", "sal", "acc", "kind", "sup", "shard", "emb16")
 
 
 def tenant_key(name: str, _cache: Dict[str, int] = {}) -> int:
@@ -74,7 +75,10 @@ class TenantTable:
         self.h_n = np.zeros(0, np.int32)
         self.d_ptr = torch.zeros((len(_COLS), 0), dtype=torch.int64, device=self.device)
         self.d_n = torch.zeros(0, dtype=torch.int32, device=self.device)
+        self.h_ld16 = np.zeros(0, np.int64)
         self._dirty = False
+        self.gen = 0  # bumped whenever an entry changes (tile tables key on it)
+        self._tiles = None
 
     def _grow(self, need: int) -> None:
         cap = max(need, 2 * self.cap, 64)
@@ -82,6 +86,9 @@ class TenantTable:
         hp[:, : self.cap] = self.h_ptr
         hn = np.zeros(cap, np.int32)
         hn[: self.cap] = self.h_n
+        hl = np.zeros(cap, np.int64)
+        hl[: self.cap] = self.h_ld16
+        self.h_ld16 = hl
         # the new slots join the free list (smallest popped first)
         self.free = list(range(cap - 1, self.cap - 1, -1)) + self.free
         self.h_ptr, self.h_n, self.cap = hp, hn, cap
@@ -124,7 +131,10 @@ class TenantTable:
                 if ok:
                     b = g.store_bias("l2")
                     e, sal, acc, kind, sup, shard = g.column_ptrs()
-                    self.h_ptr[:, s] = (e, b.data_ptr(), sal, acc, kind, sup, shard)
+                    e16 = getattr(g, "emb16", None)
+                    self.h_ptr[:, s] = (e, b.data_ptr(), sal, acc, kind, sup, shard,
+                                        e16.data_ptr() if e16 is not None else 0)
+                    self.h_ld16[s] = e16.stride(0) if e16 is not None else 0
                     self.h_n[s] = g.n
                 else:
                     self.h_ptr[:, s] = 0
@@ -139,7 +149,23 @@ class TenantTable:
             self.d_ptr = _to_dev(torch.from_numpy(self.h_ptr.copy()), self.device)
             self.d_n = _to_dev(torch.from_numpy(self.h_n.copy()), self.device)
             self._dirty = False
+            self.gen += 1
         return out
+
+    def tiles(self, slots: np.ndarray):
+        """Tile table (ops/search.py MtTiles) of these slots' tenants, rebuilt
+        only when an entry or the slot set changed."""
+        from ..ops.search import MtTiles
+        slots = np.asarray(slots, np.int64)
+        key = (self.gen, slots.tobytes())
+        if self._tiles is None or self._tiles[0] != key:
+            ld = self.h_ld16[slots]
+            if ld.size and (ld != ld[0]).any():
+                raise ValueError("tile table: tenants with different bf16 row strides")
+            t = MtTiles(slots, self.h_n[slots], self.h_ptr[7, slots], self.h_ptr[1, slots],
+                        int(ld[0]) if ld.size else 0, self.device)
+            self._tiles = (key, t)
+        return self._tiles[1]
 
 
 def _to_dev(t: torch.Tensor, device: torch.device) -> torch.Tensor:
@@ -471,18 +497,43 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     table = svc.tenant_table(svc.systems[users[0]].graph.device if users else None)
     if users:
         slots = table.slots_host(users, {u: svc.systems[u] for u in users}).tolist()
-        for u, slot in zip(users, slots):
+        small = [i for i, u in enumerate(users) if MT_GLOBAL and _fused_ok(svc.systems[u], D, limit)]
+        if len(small) >= MT_MIN_TENANTS and NQ:
+            # the small tenants: ONE multi-tenant MFMA pass (ops/search.py mt_topk)
+            s, key, tk, redo = _global_small(svc, table, [users[i] for i in small],
+                                             np.asarray([slots[i] for i in small], np.int64), Qall, limit, me, dev)
+            best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
+                                            torch.cat([best_t, tk], 1))
+            done = set(small)
+            rest = [i for i in range(len(users)) if i not in done]
+            if redo is not None:  # queries whose candidate list overflowed: the per-tenant path
+                rest += sorted(done)
+        else:
+            redo = None
+            rest = list(range(len(users)))
+        for i in rest:
+            u, slot = users[i], slots[i]
+            if redo is not None and i in done:
+                qsel = redo
+            else:
+                qsel = None
             ms = svc.systems[u]
             g = ms.graph
+            Qi = Qall if qsel is None else Qall[qsel]
             with ms._graph_lock:
-                s, r = g.store_search(Qall.to(g.device), limit, getattr(ms.store, "metric", "l2"))
+                s, r = g.store_search(Qi.to(g.device), limit, getattr(ms.store, "metric", "l2"))
                 with g.on_stream():
                     ok = (r >= 0) & (g.kind[r.clamp_min(0)] == NODE)
             s = torch.where(ok, s.float(), torch.full_like(s, float("-inf"))).to(dev)
             key = torch.where(ok, (me << 56) | (int(slot) << 32) | r, torch.full_like(r, -1)).to(dev)
             tk = torch.where(ok, torch.full_like(r, tenant_key(u)), torch.full_like(r, -1)).to(dev)
-            best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
-                                            torch.cat([best_t, tk], 1))
+            if qsel is None:
+                best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
+                                                torch.cat([best_t, tk], 1))
+            else:
+                m_s, m_k, m_t = _merge(torch.cat([best_s[qsel], s], 1), torch.cat([best_k[qsel], key], 1), limit,
+                                       torch.cat([best_t[qsel], tk], 1))
+                best_s[qsel], best_k[qsel], best_t[qsel] = m_s, m_k, m_t
     if not force:
         return GlobalHits(best_s[:b], best_k[:b], best_t[:b])
     # candidates for rank j's queries go back to rank j
@@ -498,6 +549,58 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     gt = gt.permute(1, 0, 2).reshape(B, W * limit)
     s, k, t = _merge(gs, gk, limit, gt)
     return GlobalHits(s[:b], k[:b], t[:b])
+
+
+# global search over >= MT_MIN_TENANTS small tenants: one multi-tenant pass
+# (LZK_MT_GLOBAL=0: the per-tenant store searches)
+MT_GLOBAL = os.environ.get("LZK_MT_GLOBAL", "1") != "0"
+MT_MIN_TENANTS = 2
+
+
+def _global_small(svc, table, users: List[str], slots: np.ndarray, Qall: torch.Tensor, limit: int, me: int, dev):
+    """Every query against every small tenant in one tile-table pass. Returns
+    (scores, keys = rank << 56 | slot << 32 | row, tenant keys, the queries
+    whose candidate list overflowed -- None when none did -- to be redone by
+    the per-tenant path; those queries' rows here are empty)."""
+    from ..ops.search import mt_topk
+    systems = [svc.systems[u] for u in users]
+    locks = [ms._graph_lock for ms in sorted(systems, key=lambda m: id(m))]
+    for lk in locks:
+        lk.acquire()
+    try:
+        gdev = systems[0].graph.device
+        cur = torch.cuda.current_stream(gdev)
+        streams = {}
+        for ms in systems:
+            st = getattr(ms.graph, "stream", None)
+            if st is not None:
+                streams[st.cuda_stream] = st
+        for st in streams.values():  # the tenants' pending column writes first
+            if st.cuda_stream != cur.cuda_stream:
+                cur.wait_stream(st)
+        tiles = table.tiles(slots)
+        s, key, ovf = mt_topk(tiles, Qall.to(gdev), limit, table.d_ptr[0], table.d_ptr[1], table.d_ptr[4])
+        for st in streams.values():  # no column freed / reused under the pass
+            if st.cuda_stream != cur.cuda_stream:
+                st.wait_stream(cur)
+    finally:
+        for lk in reversed(locks):
+            lk.release()
+    # stable tenant key of every slot (host table, uploaded per call: small)
+    tkeys = np.full(table.cap, -1, np.int64)
+    for u, sl in zip(users, slots.tolist()):
+        tkeys[sl] = tenant_key(u)
+    tk_dev = torch.from_numpy(tkeys).to(gdev)
+    ok = key >= 0
+    tk = torch.where(ok, tk_dev[(key >> 32).clamp_min(0)], torch.full_like(key, -1))
+    key = torch.where(ok, (me << 56) | key, torch.full_like(key, -1))
+    redo = None
+    if bool((ovf != 0).any()):  # rare: pathological score distributions
+        redo = torch.nonzero(ovf != 0).flatten()
+        s[redo] = float("-inf")
+        key[redo] = -1
+        tk[redo] = -1
+    return s.to(dev), key.to(dev), tk.to(dev), redo if redo is None else redo.to(dev)
 
 
 def _merge(s: torch.Tensor, key: torch.Tensor, k: int, extra: Optional[torch.Tensor] = None):

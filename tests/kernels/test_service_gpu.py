@@ -202,3 +202,48 @@ def test_search_routed_matches_per_tenant_gpu(tmp_path):
         assert [x["id"] for x in nodes[q]] == ref, q
         assert [v.id for v in hits.local_nodes(svc, q)] == ref
     svc.close()
+
+
+@pytest.mark.parametrize("overflow", [False, True])
+def test_search_global_multi_tenant_pass_matches_per_tenant(tmp_path, monkeypatch, overflow):
+    """search_global_batch over 40 small tenants (1..~700 rows: partial tiles,
+    one-row tenants, removed rows) + one big tenant: the one-pass tile-table
+    scan (csrc/kernels/mtscan.hip) returns the hits of the per-tenant store
+    searches (LZK_MT_GLOBAL=0), scores to fp32 rounding. overflow=True: a
+    threshold that admits every row, so every query's list overflows and is
+    redone by the per-tenant path."""
+    from lazzaro_amd.ops import search as S
+    from lazzaro_amd.parallel import routing
+    emb = RandEmbedder()
+    users = [f"g{i}" for i in range(40)]
+    svc = _seeded_service(tmp_path, emb, [])
+    rng = np.random.default_rng(9)
+    for j, u in enumerate(users):
+        g = svc.system(u).graph
+        n = 1 if j % 13 == 0 else int(rng.integers(2, 700))
+        V = torch.nn.functional.normalize(torch.randn(n, 64, device="cuda"), dim=1)
+        g.add_nodes([f"{u}_{i}" for i in range(n)], [f"{u} {i}" for i in range(n)], V, shard=g.shard_id("work"),
+                    stored=True)
+        if n > 20:
+            g.remove_nodes([3, 7, n - 1], unstore=True)
+    big = svc.system("big").graph
+    n = routing.BIG_ROWS + 500
+    big.add_nodes([f"big_{i}" for i in range(n)], [f"big {i}" for i in range(n)],
+                  torch.nn.functional.normalize(torch.randn(n, 64, device="cuda"), dim=1), shard=big.shard_id("work"),
+                  stored=True)
+    Q = torch.nn.functional.normalize(torch.randn(300, 64, device="cuda"), dim=1)
+    if overflow:
+        monkeypatch.setattr(S, "_mt_threshold", lambda Xs, bs, Q16, *a: torch.full((Q16.shape[0],), float("-inf"),
+                                                                                   device=Q16.device))
+    monkeypatch.setattr(routing, "MT_GLOBAL", True)
+    got = routing.search_global_batch(svc, Q, 6)
+    monkeypatch.setattr(routing, "MT_GLOBAL", False)
+    want = routing.search_global_batch(svc, Q, 6)
+    gu, wu = got.users(svc), want.users(svc)
+    _, _, grow = got.split()
+    _, _, wrow = want.split()
+    assert torch.allclose(got.scores, want.scores, rtol=1e-5, atol=1e-5)
+    assert gu == wu
+    assert torch.equal(grow, wrow)
+    assert (want.keys >= 0).all()
+    svc.close()
