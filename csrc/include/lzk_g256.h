@@ -341,7 +341,7 @@ __device__ __forceinline__ void body2(u16* smem, const Stager& st, int KS, f32x4
 //   C[wr*128 + i*16 + 4*(lane>>4) + e][wc*64 + j*16 + (lane&15)]
 // and every wave has passed the final barrier with all of its DMA retired
 // (smem may be reused or re-staged).
-// OPT (schedule experiments, A/B in bench/ab_search.py): bit 0 = no
+// OPT (schedule experiments, A/B results in profiles/ab_search_sched_r1.json): bit 0 = no
 // s_setprio around the MFMA clusters, bit 1 = no wave-group stagger.
 template <class Mma = MmaBf16, int OPT = 0, class Pre = NoPrefetch>
 __device__ __forceinline__ void body(u16* smem, const Stager& st, int KS, f32x4 (&acc)[8][4],

@@ -992,7 +992,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
   }
   {
     const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
-    // measured (bench/ab_body.py, profiles/ab_body_r1.json): with the two-phase main loop the
+    // measured (profiles/ab_body_r1.json): with the two-phase main loop the
     // 256x256 pipeline beats the 128x128 kernel even on half the chip -- bge-base O / FFN2
     // (N = 768) at 11k tokens: 132 tiles, 24 / 60 us vs 34 / 90 us -- so every grid of at
     // least 64 tiles takes it (from 128: bench forward 5.72 -> 5.13 ms; from 64: the consolidation
@@ -1012,7 +1012,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
       dim3 grid(n_ft * ntt), block(g256::NT);
       if (g_g256_persist < 0) {
         const char* e = getenv("LZK_G256_PERSIST");
-        // off by default (bench/ab_persist.py, profiles/ab_persist_r1.json): with the LDS-image
+        // off by default (profiles/ab_persist_r1.json): with the LDS-image
         // epilogue (2) the per-GEMM times equal the one-tile kernel's and the whole forward is
         // slower (2 streams 5.14 -> 5.50 ms); 8-B stores straight from the MFMA layout (1) cost
         // ~3.5 us per 256x256 tile more than the coalesced image stores (QKV 93 -> 107 us)
@@ -1048,7 +1048,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
       }
       if (g_g256_body < 0) {
         const char* e = getenv("LZK_G256_BODY");
-        g_g256_body = e ? atoi(e) : 1;  // body2: 2-4 % faster on the bge-base projections (bench/ab_body.py)
+        g_g256_body = e ? atoi(e) : 1;  // body2: 2-4 % faster on the bge-base projections (profiles/ab_body_r1.json)
       }
 #define GO1(A, RS, BD)                                                                                        \
   do {                                                                                                        \
@@ -1092,7 +1092,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
         const char* e = getenv("LZK_G256_TAIL");
         // off by default: in isolation FFN2 at 22.6k tokens gains 132 -> 119 us, but the
         // 128x128 tail kernels run at ~1/4 of the per-CU rate (one small tile per CU) and the
-        // whole forward loses (bench/ab_tail.py, profiles/ab_tail_r1.json: 1 stream 5.54 ->
+        // whole forward loses (profiles/ab_tail_r1.json: 1 stream 5.54 ->
         // 5.76 ms, 2 streams 4.97 -> 5.11 ms)
         g_g256_tail = e ? atoi(e) : 0;
       }

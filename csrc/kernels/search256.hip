@@ -389,13 +389,13 @@ __global__ __launch_bounds__(256) void cand_gather_kernel(const int4* __restrict
 int g_cand_persist = -1;
 // Schedule of the persistent candidate kernel (OPT bits): bit 3 = two-phase
 // main loop (body2), bit 4 = column prefilter in the epilogue. Interleaved A/B
-// on one MI355X, 10M x 768 x 1024 queries (bench/ab_search.py,
-// profiles/ab_search_sched_r1.json): four-phase 13.73 ms, +body2 13.09,
+// on one MI355X, 10M x 768 x 1024 queries
+// (profiles/ab_search_sched_r1.json): four-phase 13.73 ms, +body2 13.09,
 // +prefilter 13.38, both 12.80 ms (-6.8 %); cross-tile prefetch (bit 5) was
 // 8 % slower and stays an A/B knob only.
 constexpr int kCandOpt = 24;
 // The dual kernel's list-B threshold comes from a 1/S sample of one shard's
-// rows, so it is low and the column prefilter rarely skips: bench/ab_dual.py
+// rows, so it is low and the column prefilter rarely skips
 // (profiles/ab_dual_r1.json) 0: 16.27 ms, body2: 15.65, +prefilter 15.90.
 constexpr int kDualOpt = 8;
 int g_dual_opt = -1;  // A/B override of kCandOpt for the dual kernel (lzk_set_dual_opt)
