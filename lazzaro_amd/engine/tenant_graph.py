@@ -225,6 +225,7 @@ class TenantGraph:
         self._norm_dev_pending: List[torch.Tensor] = []
         self.track = True
         self.stream = _side_stream(self.device) if self.on_gpu else None
+        self.on_change = None  # called after every mutation (_bump)
         self.ann_cfg: Optional[Dict] = None  # store index="ivfpq": IVF-PQ for large tenants (HBMStore.attach)
         self._ann = None
         self._ann_covered = 0
@@ -394,6 +395,8 @@ class TenantGraph:
             self.edge_version += 1
         if store:
             self._store_version += 1
+        if self.on_change is not None:  # (e.g. the routed directory of parallel/service.py)
+            self.on_change()
 
     # ------------------------------------------------------------------ codes
     def shard_id(self, name: str, live: bool = True) -> int:

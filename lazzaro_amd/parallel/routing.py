@@ -361,7 +361,8 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     if Dg == 0 or K == 0:
         return RoutedHits(list(users), owner, torch.zeros((n, 1)), torch.full((n, 1), -1, dtype=torch.long))
     senders_current = all(int(allc[s, me, 4]) == epoch0 for s in range(W) if allc[s, me, 0] > 0)
-    on_device = senders_current and svc._dir_epoch == epoch0 and svc.device_directory_ok(Dg)
+    ddir = svc.device_directory(Dg, K) if (senders_current and svc._dir_epoch == epoch0) else None
+    on_device = ddir is not None
     Qo = Q[torch.as_tensor(order, dtype=torch.long, device=Q.device)] if n else torch.zeros((0, Dg), device=dev)
     pay = _pack_queries(Qo, [tenant_key(users[j]) for j in order], [limits[j] for j in order]) if n else \
         torch.zeros((0, Dg + 3), dtype=torch.int32)
@@ -370,7 +371,7 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     svc.route_stats["device" if (m and on_device) else "host"] += 1
     if m:
         if on_device:
-            S, R = _owner_search_device(svc, got, Dg, K)
+            S, R = _owner_search_device(svc, got, Dg, K, ddir)
         else:
             meta = got[:, Dg:].cpu().numpy()
             rusers = [svc._key_names[x] for x in _unpack_keys(meta)]
@@ -390,14 +391,16 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     return RoutedHits(list(users), owner, S, R)
 
 
-def _owner_search_device(svc, got: torch.Tensor, Dg: int, K: int):
+def _owner_search_device(svc, got: torch.Tensor, Dg: int, K: int, ddir):
     """Owner side of :func:`search_routed` without reading the received
-    rows back: the tenant key of each row is matched on the device against
-    the pinned tenants (:meth:`DistributedMemoryService.device_directory_ok`:
-    a few large GPU tenants), each of which runs its store search over the
-    batch; a row keeps the results of the tenant whose key it carries. Rows
-    past a query's limit and rows that are not nodes come back -1 / -inf,
-    valid hits first (as :func:`local_search`)."""
+    rows back (:meth:`DistributedMemoryService.device_directory`): each
+    row's tenant key is looked up on the device in the sorted keys of the
+    pinned small tenants -- one segment_topk over their tenant-table rows
+    serves every such row -- and matched against the pinned large tenants,
+    each of which runs its store search over the batch (a row keeps the
+    results of the tenant whose key it carries). Rows past a query's limit
+    and rows that are not nodes come back -1 / -inf, valid hits first (as
+    :func:`local_search`)."""
     m = got.shape[0]
     dev = got.device
     lo = got[:, Dg].long() & 0xFFFFFFFF
@@ -406,7 +409,36 @@ def _owner_search_device(svc, got: torch.Tensor, Dg: int, K: int):
     Qr = got[:, :Dg].contiguous().view(torch.float32)
     S = torch.full((m, K), float("-inf"), dtype=torch.float32, device=dev)
     R = torch.full((m, K), -1, dtype=torch.int64, device=dev)
-    for key, user in sorted(svc._pinned.items()):
+    dk = ddir["keys"]
+    if dk.numel():
+        from ..ops.search import segment_topk_ptrs
+        from ..ops.tenant_ops import gather_fields
+        table = ddir["table"]
+        tdev = dk.device
+        kk = keys.to(tdev)
+        pos = torch.searchsorted(dk, kk).clamp_max(dk.numel() - 1)
+        hit = dk[pos] == kk
+        slot = ddir["slots"][pos]
+        ptrs = table.d_ptr[:, slot]
+        nrows = torch.where(hit, table.d_n[slot], torch.zeros_like(table.d_n[slot])).contiguous()
+        Qs = Qr.to(tdev)
+        cur = torch.cuda.current_stream(tdev) if tdev.type == "cuda" else None
+        for st in ddir["streams"]:  # the tenants' pending column writes first
+            if st.cuda_stream != cur.cuda_stream:
+                cur.wait_stream(st)
+        s, r = segment_topk_ptrs(ptrs[0].contiguous(), nrows, Dg, Qs, K, bptr=ptrs[1].contiguous(), alpha=2.0,
+                                 qbias=-(Qs * Qs).sum(1))
+        o = gather_fields(r, None, device_out=True, base=ptrs[2:7].contiguous())
+        ok = hit[:, None] & (r >= 0) & (o["kind"] == NODE)
+        S = torch.where(ok.to(dev), s.to(dev), S)
+        R = torch.where(ok.to(dev), r.to(dev), R)
+        # the fused scan read the tenants' columns through raw addresses: order
+        # their streams after it before anything can move a column
+        for st in ddir["streams"]:
+            if st.cuda_stream != cur.cuda_stream:
+                st.wait_stream(cur)
+    for user in ddir["big"]:
+        key = tenant_key(user)
         ms = svc.systems[user]
         g = ms.graph
         with ms._graph_lock:

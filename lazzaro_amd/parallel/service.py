@@ -158,6 +158,8 @@ class DistributedMemoryService:
         # is served by matching tenant keys on the device
         self._pinned: Dict[int, str] = {}
         self._dir_epoch = 0
+        self._ddir = None  # the device directory (see device_directory)
+        self._ddir_dirty: set = set()  # pinned tenants mutated since it was built
         self.route_stats = {"device": 0, "host": 0}  # routed batches served by device key matching / by name
         self._owner_epoch: Dict[int, int] = {}
 
@@ -209,38 +211,105 @@ class DistributedMemoryService:
                 h._mat()
 
     # ------------------------------------------------------------ routed directory
-    # device key matching serves at most this many pinned (large) tenants; a
-    # rank with more -- or with small tenants, which share the fused
-    # multi-tenant scan keyed by name -- reads the received keys back
+    # device key matching serves any number of pinned small tenants (one
+    # fused segment_topk over the tenant table) and at most this many pinned
+    # large ones (each its own store search over the whole received batch)
     DEVICE_ROUTE_MAX_TENANTS = 2
 
     def pin(self, user: str) -> None:
         """Keep an announced tenant resident for the routed path (loads it
-        if needed)."""
-        self.system(user)
-        self._pinned[routing.tenant_key(user)] = user
+        if needed); its mutations mark the device directory for refresh."""
+        ms = self.system(user)
+        key = routing.tenant_key(user)
+        if key not in self._pinned:
+            self._pinned[key] = user
+            self._ddir = None
+        g = getattr(ms, "graph", None)
+        if g is not None:
+            g.on_change = lambda u=user: self._ddir_dirty.add(u)
 
     def _unpin(self, user: str) -> None:
         if self._pinned.pop(routing.tenant_key(user), None) is not None:
             self._dir_epoch += 1
+            self._ddir = None
+            ms = self.systems.get(user)
+            if ms is not None and getattr(ms, "graph", None) is not None:
+                ms.graph.on_change = None
 
     def _unpin_all(self) -> None:
         if self._pinned:
+            for u in list(self._pinned.values()):
+                ms = self.systems.get(u)
+                if ms is not None and getattr(ms, "graph", None) is not None:
+                    ms.graph.on_change = None
             self._pinned = {}
             self._dir_epoch += 1
+            self._ddir = None
 
-    def device_directory_ok(self, D: int) -> bool:
-        """The routed owner side may match tenant keys on the device: every
-        pinned tenant is resident, large (its own store search), on the GPU
-        and of width ``D``."""
-        if not self._pinned or len(self._pinned) > self.DEVICE_ROUTE_MAX_TENANTS:
-            return False
+    def _classify(self, user: str, D: int, K: int) -> Optional[str]:
+        """'big' (own store search), 'small' (the fused tenant-table scan) or
+        None (the routed owner must serve this tenant by name)."""
+        ms = self.systems.get(user)
+        g = getattr(ms, "graph", None)
+        if g is None or g.dim != D or getattr(ms, "enable_async", False):
+            return None  # (a background consolidation may move columns under a raw-pointer scan)
+        if g.n >= routing.BIG_ROWS:
+            return "big"
+        return "small" if routing._fused_ok(ms, D, K) else None
+
+    def device_directory(self, D: int, K: int):
+        """The routed owner side's device directory -- sorted pinned tenant
+        keys with their table slots and a small/big flag -- or None when some
+        pinned tenant cannot be served by key on the device (then the owner
+        reads the received keys back). Rebuilt when the pinned set, the width
+        or a mutated tenant's class changed; a mutated small tenant only has
+        its table entry refreshed."""
+        if not self._pinned:
+            return None
+        d = self._ddir
+        if d is not None and d["D"] == D and d["K"] >= K and d["epoch"] == self._dir_epoch:
+            if self._ddir_dirty:
+                dirty, self._ddir_dirty = self._ddir_dirty, set()
+                for u in dirty:
+                    if u in d["cls"] and self._classify(u, D, d["K"]) != d["cls"][u]:
+                        self._ddir = None
+                        return self.device_directory(D, K)
+                small = [u for u in dirty if d["cls"].get(u) == "small"]
+                if small:
+                    d["table"].slots_host(small, self.systems)
+            return d
+        self._ddir_dirty = set()
+        K = max(K, 1)
+        cls = {}
         for u in self._pinned.values():
-            ms = self.systems.get(u)
-            g = getattr(ms, "graph", None)
-            if g is None or g.dim != D or g.n < routing.BIG_ROWS:
-                return False
-        return True
+            c = self._classify(u, D, K)
+            if c is None:
+                return None
+            cls[u] = c
+        big = sorted(u for u, c in cls.items() if c == "big")
+        if len(big) > self.DEVICE_ROUTE_MAX_TENANTS:
+            return None
+        small = sorted(u for u, c in cls.items() if c == "small")
+        table = None
+        keys = np.asarray([routing.tenant_key(u) for u in small], np.int64)
+        slots = np.zeros(0, np.int64)
+        dev = self.systems[(small or big)[0]].graph.device
+        if small:
+            table = self.tenant_table(dev)
+            slots = table.slots_host(small, self.systems)
+        o = np.argsort(keys, kind="stable")
+        streams = {}
+        for u in small:
+            st = getattr(self.systems[u].graph, "stream", None)
+            if st is not None:
+                streams[st.cuda_stream] = st
+        self._ddir = {"D": D, "K": K, "epoch": self._dir_epoch, "cls": cls, "big": big, "table": table,
+                      "streams": list(streams.values()),
+                      "keys": torch.from_numpy(keys[o]).to(dev), "slots": torch.from_numpy(slots[o]).to(dev)}
+        return self._ddir
+
+    def device_directory_ok(self, D: int, K: int = 1) -> bool:
+        return self.device_directory(D, K) is not None
 
     def _release(self, user: str, ms) -> None:
         """Persist and close a tenant this rank stops holding."""

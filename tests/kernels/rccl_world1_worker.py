@@ -58,11 +58,15 @@ def main():
                       "search_ok": bool((hits.rows >= 0).all())}
     svc.close()
 
-    # row-sharded tenant, reference batch semantics, every collective on RCCL
+    # row-sharded tenant, batch cadence, every collective on RCCL
     cfg = {"rows": 30_000, "dim": 64, "limit": 30_040, "steps": 2, "convs": 24, "device": "cuda", "force": True}
     sh = SH._sharded(comm, cfg=cfg)
     SH.check_equivalent({0: sh}, 1, cfg["limit"])
     out["sharded_equal"] = True
+    # ... and at the reference's per-conversation cadence
+    sh = SH._sharded(comm, cfg=dict(cfg, cadence="conversation"))
+    SH.check_equivalent({0: sh}, 1, cfg["limit"])
+    out["sharded_exact_cadence_equal"] = True
     torch.cuda.synchronize()
     dist.barrier()
     print("RESULT " + json.dumps(out), flush=True)

@@ -40,7 +40,9 @@ def test_rccl_world1_serving_and_sharded_paths():
     assert out["backend"] == "nccl" and out["world"] == 1 and out["device"].startswith("cuda")
     for k in ("routed_dir0", "routed_dir1"):
         assert out[k]["exact"] and out[k]["global_exact"] and out[k]["force"], out[k]
-    assert out["routed_dir0"]["route_stats"]["device"] == 0
+    # small GPU tenants: the owner matches keys in the device directory and
+    # serves them with one fused tenant-table scan (no key read-back)
+    assert out["routed_dir0"]["route_stats"]["device"] >= 1, out["routed_dir0"]
     assert out["routed_dir1"]["route_stats"]["device"] >= 1, out["routed_dir1"]
     assert out["migrate"]["received"] == [] and out["migrate"]["search_ok"]
-    assert out["sharded_equal"]
+    assert out["sharded_equal"] and out["sharded_exact_cadence_equal"]
