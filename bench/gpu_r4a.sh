@@ -2,7 +2,7 @@
 set -o pipefail
 export PYTHONPATH=$PWD
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/kernels/test_tenant_engine_gpu.py tests/kernels/test_graph_kernels_gpu.py -k "scan8 or i8 or zero_row or rigorous or farthest or rerank64" > gpurun_out/t_new.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/kernels/test_tenant_engine_gpu.py tests/kernels/test_graph_kernels_gpu.py -k "scan8 or i8 or zero_row or rigorous or farthest or rerank64 or lean" > gpurun_out/t_new.log 2>&1 || exit 1
 timeout -k 10 400 python -u bench/ab_scan8.py > gpurun_out/ab_scan8.json 2> gpurun_out/ab_scan8.err || exit 2
 timeout -k 10 300 python -u bench/ab_scan8_narrow.py > gpurun_out/ab_narrow.json 2> gpurun_out/ab_narrow.err || exit 3
 timeout -k 10 330 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/kernels/test_rccl_world1_gpu.py > gpurun_out/t_rccl.log 2>&1 || exit 4

@@ -597,16 +597,31 @@ __global__ __launch_bounds__(256) void top1_decode_kernel(const unsigned long lo
   row[q] = (int)(0xFFFFFFFFu - (unsigned)(b & 0xFFFFFFFFull));
 }
 
-// Exact re-score of the candidate lists of a low-precision (fp8) scan: the
-// list entry (q, row) gets alpha * <Q16[q], X16[row]> + bias[row] from the
-// bf16 rows (fp32 accumulate), so the top-k select that follows ranks by the
-// same scores as the bf16 path. One 256-thread block per query, 4 waves take
-// alternate 64-entry windows of the list and re-score the window's kept
-// entries one by one; lanes read consecutive 8-B chunks of a row. cut
-// (optional, [nq]): entries whose scan score is below cut[q] cannot reach the
-// query's top-k (the caller's error bound) and become -inf without a row read.
-__global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict__ X, long ldx,
-                                                           const u16* __restrict__ Qm, long ldq, int D,
+// Exact re-score of the candidate lists of a low-precision (fp8 / int8) scan:
+// the list entry (q, row) gets alpha * <Q[q], X[row]> + bias[row] (fp32
+// accumulate) from the bf16 rows (F32 false: the same scores as the bf16 path)
+// or -- a lean tenant that keeps no bf16 copy -- from the fp32 rows and fp32
+// queries (F32 true). One 256-thread block per query, 4 waves take alternate
+// 64-entry windows of the list and re-score the window's kept entries one by
+// one; lane c reads the c-th 4-element chunk of a row (8 B bf16 / 16 B fp32).
+// cut (optional, [nq]): entries whose scan score is below cut[q] cannot reach
+// the query's top-k (the caller's error bound) and become -inf without a row
+// read.
+template <bool F32>
+__device__ __forceinline__ void load4(const void* p, long off, float (&v)[4]) {
+  if constexpr (F32) {
+    const float4 u = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + off);
+    v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const u16*>(p) + off);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+}
+
+template <bool F32>
+__global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restrict__ X, long ldx,
+                                                           const void* __restrict__ Qm, long ldq, int D,
                                                            const float* __restrict__ bias, float alpha,
                                                            const int* __restrict__ cnt, int cap,
                                                            float* __restrict__ cs, const int* __restrict__ ci,
@@ -614,17 +629,13 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict
   const int q = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = min(cnt[q] & 0x3fffffff, cap);
-  const int chunks = D >> 2;  // 4 bf16 per 8-B chunk
+  const int chunks = D >> 2;  // 4 elements per chunk
   constexpr int MAXC = 8;     // D <= 64 * 4 * MAXC = 2048
   float qv[MAXC][4];
 #pragma unroll
   for (int t = 0; t < MAXC; ++t) {
     const int c = lane + 64 * t;
-    if (c < chunks) {
-      const uint2 u = *reinterpret_cast<const uint2*>(Qm + (long)q * ldq + 4 * c);
-      qv[t][0] = __uint_as_float(u.x << 16); qv[t][1] = __uint_as_float(u.x & 0xffff0000u);
-      qv[t][2] = __uint_as_float(u.y << 16); qv[t][3] = __uint_as_float(u.y & 0xffff0000u);
-    }
+    if (c < chunks) load4<F32>(Qm, (long)q * ldq + 4 * c, qv[t]);
   }
   const float cq = cut ? cut[q] : LZK_NEG_INF;
   for (int base = wave * 64; base < n; base += 256) {
@@ -641,17 +652,17 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const u16* __restrict
     const long idx = (long)q * cap + base + jj;
     const int r = ci[idx];
     LZK_DCHECK(r >= 0);
-    const u16* xr = X + (long)r * ldx;
     float acc = 0.f;
 #pragma unroll
     for (int t = 0; t < MAXC; ++t) {
       const int c = lane + 64 * t;
       if (c < chunks) {
-        const uint2 u = *reinterpret_cast<const uint2*>(xr + 4 * c);
-        acc = fmaf(qv[t][0], __uint_as_float(u.x << 16), acc);
-        acc = fmaf(qv[t][1], __uint_as_float(u.x & 0xffff0000u), acc);
-        acc = fmaf(qv[t][2], __uint_as_float(u.y << 16), acc);
-        acc = fmaf(qv[t][3], __uint_as_float(u.y & 0xffff0000u), acc);
+        float xv[4];
+        load4<F32>(X, (long)r * ldx + 4 * c, xv);
+        acc = fmaf(qv[t][0], xv[0], acc);
+        acc = fmaf(qv[t][1], xv[1], acc);
+        acc = fmaf(qv[t][2], xv[2], acc);
+        acc = fmaf(qv[t][3], xv[3], acc);
       }
     }
 #pragma unroll
@@ -948,8 +959,19 @@ LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long
                                 float alpha, const int* cnt, int cap, float* cs, const int* ci, const float* cut,
                                 float floor, void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(cand_rescore_kernel, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, (const u16*)X16, ldx,
-                     (const u16*)Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor);
+  hipLaunchKernelGGL(cand_rescore_kernel<false>, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, X16, ldx,
+                     Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor);
+  return (int)hipGetLastError();
+}
+
+// The same from fp32 rows (X32 [*, ldx] fp32, 16-B aligned rows) and fp32
+// queries (Q32 [nq, ldq]): lean tenants without a bf16 copy. D % 4 == 0.
+LZK_EXPORT int lzk_cand_rescore32(const float* X32, long ldx, const float* Q32, long ldq, int nq, int D,
+                                  const float* bias, float alpha, const int* cnt, int cap, float* cs, const int* ci,
+                                  const float* cut, float floor, void* stream) {
+  if (D % 4 != 0 || D > 2048 || nq <= 0 || ldx % 4 != 0 || ldq % 4 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cand_rescore_kernel<true>, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, X32, ldx, Q32,
+                     ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor);
   return (int)hipGetLastError();
 }
 

@@ -98,6 +98,14 @@ LOWP_NARROW = os.environ.get("LZK_LOWP_NARROW", "1") != "0"
 # per step's scan, but the clustered-topic row-sharded run of bench.py went
 # 175 -> 243 ms per step (profiles/r3_session2/README.md); LZK_DUAL_LOWP=1 on
 DUAL_LOWP = os.environ.get("LZK_DUAL_LOWP", "0") == "1"
+# Lean HBM layout (LZK_LEAN_HBM=1 / TenantGraph.LEAN_HBM): a tenant with the
+# int8 scan copy and at least LOWP_MIN_ROWS rows of capacity keeps NO bf16
+# copy -- fp32 (the store's precision) + int8 + scale, ~5 bytes per dimension
+# instead of ~7: the int8 scans' threshold sample converts its 1/64 of the
+# rows on the fly, their re-score reads the fp32 rows, consolidation's scans
+# take the int8 dual path, and a k-means pass converts the rows for its
+# duration.
+LEAN_HBM = os.environ.get("LZK_LEAN_HBM", "0") == "1"
 # inserts of at most this many rows write their embedding columns in one launch
 WRITE_EMB_MAX_ROWS = 8192
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
@@ -299,10 +307,10 @@ class TenantGraph:
             if fresh:  # first allocation or a width change: nothing to keep
                 self.emb32 = self.emb16 = self.emb8 = self.rs8 = self.sqn = None
             move("emb32", (cap, self.dim), torch.float32)
-            if self.on_gpu:
+            if self.on_gpu and not (lowp == "i8" and self._lean(cap)):
                 move("emb16", (cap, self.Dp), torch.bfloat16)
             else:
-                self.emb16 = None
+                self.emb16 = None  # (lean: released before the int8 column grows)
             if lowp:
                 if self.emb8 is not None and self.emb8.dtype != (torch.int8 if lowp == "i8" else torch.uint8):
                     self.emb8 = None
@@ -361,6 +369,22 @@ class TenantGraph:
     # above the error cut.
     FP8_ROW_SCALE = 64.0
     LOWP = os.environ.get("LZK_SEARCH_LOWP", "i8")
+
+    def _lean(self, cap: int) -> bool:
+        return bool((LEAN_HBM or getattr(self, "LEAN_HBM", False)) and cap >= LOWP_MIN_ROWS)
+
+    @property
+    def lean(self) -> bool:
+        """No bf16 copy in HBM (see LEAN_HBM)."""
+        return self.on_gpu and self.dim is not None and self.emb16 is None and self.emb8 is not None
+
+    def _scan_rows(self, n: int, Q32: torch.Tensor):
+        """The bf16 operand of the scans: the bf16 column, or -- lean -- the
+        fp32 rows standing in for it (ops/search.py LeanRows)."""
+        if self.emb16 is not None:
+            return self.emb16[:n]
+        from ..ops.search import LeanRows
+        return LeanRows(self.emb32[:n], self.Dp, Q32)
 
     def _lowp_mode(self) -> str:
         if not self.on_gpu or self.Dp % 128 != 0:
@@ -1617,15 +1641,18 @@ class TenantGraph:
         qn = Qd.norm(dim=1, keepdim=True)
         Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
         lab = self.shard[:n]
-        if self._use_kernel(M) and k <= CAND_SLOTS:
+        lean = self.lean
+        if lean and not self.unit_rows():  # (no bf16 rows; the int8 error model needs unit rows)
+            pass
+        elif (self._use_kernel(M) or lean) and k <= CAND_SLOTS:
             bias = torch.where(mask, 0.0, NEG_INF).to(torch.float32).contiguous()
             q16 = self._q16(Qn)
-            X = self.emb16[:n]
+            X = self._scan_rows(n, Qn)
             if dual_label is not None:
                 ql = dual_label.to(dev, torch.int32).contiguous()
                 floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
-                if (DUAL_LOWP and self.emb8 is not None and self.emb8.dtype == torch.int8 and self.unit_rows()
-                        and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS):
+                if lean or (DUAL_LOWP and self.emb8 is not None and self.emb8.dtype == torch.int8
+                            and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS):
                     # the int8 dual scan: same lists (error cut + bf16 re-score)
                     from ..ops.search import flat_topk_dual_i8
                     q8, qs, margin = self._i8_query(q16, 1.0)
@@ -1636,7 +1663,12 @@ class TenantGraph:
                     (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
                                                       bias=bias, floor=floor)
                 return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
-            _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
+            if lean:
+                from ..ops.search import flat_topk_i8
+                q8, qs, margin = self._i8_query(q16, 1.0)
+                _, ra = flat_topk_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS, bias=bias, margin=margin)
+            else:
+                _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
             return self._rerank_cos(Qn, ra, k)
         if dual_label is not None:
             ql = dual_label.to(dev, torch.int32)
@@ -1693,7 +1725,10 @@ class TenantGraph:
                 and M * n >= KERNEL_MIN_WORK // 16:
             q16 = self._q16(Qf)
             narrow = LOWP_NARROW and self.emb8 is not None and self.emb8.dtype == torch.int8
-            if self.emb8 is not None and self.unit_rows() and (M >= LOWP_MIN_Q or narrow) and n >= LOWP_MIN_ROWS:
+            if self.lean and not self.unit_rows():
+                return self._exact_store(Qf, k, metric, bias)  # (no bf16 rows to scan; the error model needs unit rows)
+            if self.lean or (self.emb8 is not None and self.unit_rows() and (M >= LOWP_MIN_Q or narrow)
+                             and n >= LOWP_MIN_ROWS):
                 if self.emb8.dtype == torch.int8:
                     _, cand = self._i8_candidates(Qf, q16, kc, bias, alpha)
                 else:
@@ -1742,8 +1777,8 @@ class TenantGraph:
         the margin is LOWP_MARGIN_Z standard deviations plus that floor."""
         from ..ops.search import flat_topk_i8
         q8, qs, margin = self._i8_query(q16, alpha)
-        return flat_topk_i8(self.emb8, self.rs8, q8, qs, self.emb16[:self.n], q16, kc, bias=bias, alpha=alpha,
-                            margin=margin)
+        return flat_topk_i8(self.emb8, self.rs8, q8, qs, self._scan_rows(self.n, Qf), q16, kc, bias=bias,
+                            alpha=alpha, margin=margin)
 
     def _i8_query(self, q16: torch.Tensor, alpha: float):
         """int8 queries + per-query scales + the error-model margin of
@@ -1861,8 +1896,11 @@ class TenantGraph:
                 n_glob = n_live
             if n_glob == 0:
                 return {}
-            if self.on_gpu:
+            if self.on_gpu and self.emb16 is not None:
                 X = self.emb16[:n]
+            elif self.on_gpu:  # lean: the pass's own bf16 copy, released when it ends
+                from ..ops.search import bf16_rows
+                X = bf16_rows(self.emb32[:n], self.Dp)
             else:
                 X = self.emb32[:n] / self.sqn[:n].sqrt().clamp_min(1e-30)[:, None]
             kf = min(n_fine, n_glob)

@@ -247,6 +247,9 @@ def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_o
     rc = L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, int(k),
                            int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), _lib.ptr(need), st)
     _lib.check(rc, "lzk_cand_select")
+    if isinstance(X, LeanRows):
+        _lean_fallback(X, Q, k, bias, row_label, q_label, alpha, idx_offset, os_, oi, ovf)
+        return os_, oi
     nch = L.lzk_flat_topk_chunks(N, nq, TARGET_WGS)
     part = nq * nch * kslot
     wsf = _ws_fallback.get(dev, part * 8)
@@ -260,6 +263,35 @@ def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_o
                                  os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), st)
     _lib.check(rc, "lzk_topk_merge_masked")
     return os_, oi
+
+
+def _lean_fallback(X: LeanRows, Q, k, bias, row_label, q_label, alpha, idx_offset, os_, oi, ovf):
+    """Overflowed queries of a lean tenant's candidate select, recomputed
+    exactly over the rows converted to bf16 one block at a time (one host
+    read of the overflow flags; a block is converted only when some query
+    overflowed -- pathological score distributions)."""
+    bad = torch.nonzero(ovf).flatten()
+    if bad.numel() == 0:
+        return
+    N = X.shape[0]
+    Qb = Q[bad].contiguous()
+    ql = q_label[bad].contiguous() if q_label is not None else None
+    best_s = best_i = None
+    for c0 in range(0, N, X.CHUNK):
+        c1 = min(N, c0 + X.CHUNK)
+        s, i = flat_topk(X[c0:c1], Qb, k, bias=bias[c0:c1].contiguous() if bias is not None else None,
+                         row_label=row_label[c0:c1].contiguous() if row_label is not None else None, q_label=ql,
+                         alpha=alpha, idx_offset=c0 + idx_offset)
+        if best_s is None:
+            best_s, best_i = s, i
+            continue
+        s, i = torch.cat([best_s, s], 1), torch.cat([best_i, i], 1)
+        key = torch.where(i >= 0, i, torch.full_like(i, 1 << 62))
+        o = torch.argsort(key, dim=1, stable=True)
+        s, i = torch.gather(s, 1, o), torch.gather(i, 1, o)
+        o = torch.sort(s, dim=1, descending=True, stable=True).indices[:, :k]
+        best_s, best_i = torch.gather(s, 1, o), torch.gather(i, 1, o)
+    os_[bad], oi[bad] = best_s, best_i
 
 
 def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset):
@@ -300,6 +332,34 @@ _lib.register("lzk_flat_cand_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
 _lib.register("lzk_cand_grid_f8", _lib.I, [_lib.I, _lib.I])
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
                                            _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P])
+_lib.register("lzk_cand_rescore32", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
+                                             _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P])
+
+
+def bf16_rows(X32: torch.Tensor, Dp: int) -> torch.Tensor:
+    """bf16 copy of fp32 rows, zero-padded to Dp columns (the scan layout)."""
+    out = torch.zeros((X32.shape[0], Dp), dtype=torch.bfloat16, device=X32.device)
+    out[:, : X32.shape[1]] = X32
+    return out
+
+
+class LeanRows:
+    """The fp32 rows of a lean tenant (no bf16 copy kept in HBM) standing in
+    for the bf16 operand of the int8 search paths: a slice converts on the fly
+    (bf16, zero-padded to Dp -- the 1/S threshold sample and the rare overflow
+    fallback); the re-score above the error cut reads the fp32 rows and the
+    fp32 queries ``Q32`` directly (lzk_cand_rescore32)."""
+    dtype = torch.bfloat16
+    CHUNK = 1 << 20  # rows per converted block of the overflow fallback
+
+    def __init__(self, X32: torch.Tensor, Dp: int, Q32: torch.Tensor):
+        self.X32, self.Dp = X32, int(Dp)
+        self.Q32 = Q32.float().contiguous()
+        self.device = X32.device
+        self.shape = (X32.shape[0], self.Dp)
+
+    def __getitem__(self, sl):
+        return bf16_rows(self.X32[sl], self.Dp)
 _lib.register("lzk_flat_cand_dual_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P,
                                                 _lib.P, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.P, _lib.I,
                                                 _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I,
@@ -534,10 +594,16 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
         kth = s8[:, k - 1]
         cut = (kth - 2.0 * margin - 1e-6 * (1.0 + kth.abs())).contiguous()
         cut = torch.nan_to_num(cut, nan=float("-inf"))
+    fl = float("-inf") if floor is None else float(floor)
+    if isinstance(X16, LeanRows):
+        X32, Q32 = X16.X32, X16.Q32
+        _lib.check(L.lzk_cand_rescore32(X32.data_ptr(), X32.stride(0), Q32.data_ptr(), Q32.stride(0), nq,
+                                        X32.shape[1], _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap,
+                                        cs.data_ptr(), ci.data_ptr(), _lib.ptr(cut), fl, st), "lzk_cand_rescore32")
+        return
     _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
                                   _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(),
-                                  _lib.ptr(cut), float("-inf") if floor is None else float(floor), st),
-               "lzk_cand_rescore")
+                                  _lib.ptr(cut), fl, st), "lzk_cand_rescore")
 
 
 def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,

@@ -639,3 +639,47 @@ def test_cos_rerank64_kernel_matches_torch_gpu():
     fin = torch.isfinite(s0)
     assert torch.equal(fin, torch.isfinite(s1))
     assert torch.allclose(s1[fin], s0[fin], atol=1e-12, rtol=0)
+
+
+def test_lean_hbm_tenant_matches_full_gpu(monkeypatch):
+    """LEAN_HBM: a large tenant keeps fp32 + int8 + scale only (no bf16
+    copy). Store search (large and interactive batches), consolidation's dual
+    and single candidate scans and the k-means pass return what the same rows
+    give with the bf16 copy; the vector columns cost 4D + D + 8 bytes per row."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    monkeypatch.setattr(TG, "LOWP_MIN_ROWS", 1 << 15)
+    N, D = 70_000, 768
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    C = torch.randn(64, D, device=DEV, generator=gen)
+    X = C[torch.randint(0, 64, (N,), device=DEV, generator=gen)] + 0.7 * torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    lab = torch.randint(0, 5, (N,), device=DEV, generator=gen)
+
+    def build():
+        g = TenantGraph(device=DEV, dim=D, capacity=1 << 17)
+        codes = [g.shard_id(f"s{i}") for i in range(5)]
+        g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=lab.cpu().int(), stored=True)
+        return g, codes
+    full, _ = build()
+    monkeypatch.setattr(TG, "LEAN_HBM", True)
+    lean, _ = build()
+    assert full.emb16 is not None and not full.lean
+    assert lean.emb16 is None and lean.lean and lean.emb8.dtype == torch.int8
+    vec_bytes = sum(t[0].numel() * t.element_size() for t in (lean.emb32, lean.emb8, lean.rs8, lean.sqn))
+    assert vec_bytes == 4 * D + D + 8
+    Q = X[torch.randint(0, N, (300,), device=DEV, generator=gen)] + 0.2 * torch.randn(300, D, device=DEV,
+                                                                                      generator=gen) / D ** 0.5
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    for m in (300, 7):  # the large-batch scan and the narrow interactive one
+        s1, r1 = full.store_search(Q[:m], 10)
+        s2, r2 = lean.store_search(Q[:m], 10)
+        assert torch.equal(r1, r2), m
+        assert torch.allclose(s1, s2, atol=1e-5)
+    mask = full.kind[:N] == NODE
+    ql = torch.randint(0, 5, (300,), device=DEV, generator=gen)
+    (a1, b1), (a2, b2) = (g.cos_topk(Q, 8, mask, dual_label=ql, min_score=0.3) for g in (full, lean))
+    assert torch.equal(a1[1], a2[1]) and torch.equal(b1[1], b2[1])
+    assert torch.equal(full.cos_topk(Q, 8, mask)[1], lean.cos_topk(Q, 8, mask)[1])
+    hf, hl = full.cluster_pass(32, 4, 2), lean.cluster_pass(32, 4, 2)
+    assert torch.equal(full.hier["fine"][:N], lean.hier["fine"][:N])
+    assert lean.emb16 is None  # the pass's bf16 copy is gone
