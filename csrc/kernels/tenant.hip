@@ -288,6 +288,43 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
   }
 }
 
+// Node columns of m inserted / replaced rows in ONE launch (an insert used to
+// be ~16 index_put / cast launches): the per-row values come from a packed
+// float64 block vals [ncols, m] (exact for every f32 / i32 / u8 / f64 value)
+// in the fixed column order below; a column absent from the block (bit c of
+// `present` clear) takes its constant. kind / stored / dirty are constants.
+//   0 sal f32 | 1 acc i32 | 2 last f64 | 3 ts f64 | 4 shard i32 | 5 sup u8 | 6 parent i32
+__global__ __launch_bounds__(256) void tg_set_rows_kernel(const long* __restrict__ rows, int m,
+                                                          const double* __restrict__ vals, int present,
+                                                          const double* __restrict__ consts, float* __restrict__ sal,
+                                                          int* __restrict__ acc, double* __restrict__ last,
+                                                          double* __restrict__ ts, int* __restrict__ shard,
+                                                          unsigned char* __restrict__ sup, int* __restrict__ parent,
+                                                          unsigned char* __restrict__ kind,
+                                                          unsigned char* __restrict__ stored,
+                                                          unsigned char* __restrict__ dirty, int kind_v, int stored_v) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const long r = rows[j];
+  double v[7];
+  int slot = 0;
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    if (present & (1 << c)) v[c] = vals[(long)(slot++) * m + j];
+    else v[c] = consts[c];
+  }
+  sal[r] = (float)v[0];
+  acc[r] = (int)v[1];
+  last[r] = v[2];
+  ts[r] = v[3];
+  shard[r] = (int)v[4];
+  sup[r] = (unsigned char)v[5];
+  parent[r] = (int)v[6];
+  kind[r] = (unsigned char)kind_v;
+  stored[r] = (unsigned char)stored_v;
+  dirty[r] = 1;
+}
+
 inline unsigned blocks_for(long n, int per = NTB) { return (unsigned)((n + per - 1) / per); }
 
 
@@ -633,6 +670,16 @@ LZK_EXPORT int lzk_store_rerank(const float* Q, long ldq, const float* X, long l
   if (C <= 0 || C > 64 || M <= 0 || k <= 0 || metric < 0 || metric > 2) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(store_rerank_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Q, ldq,
                      X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi);
+  return (int)hipGetLastError();
+}
+
+LZK_EXPORT int lzk_tg_set_rows(const long* rows, int m, const double* vals, int present, const double* consts,
+                               float* sal, int* acc, double* last, double* ts, int* shard, unsigned char* sup,
+                               int* parent, unsigned char* kind, unsigned char* stored, unsigned char* dirty,
+                               int kind_v, int stored_v, void* stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(tg_set_rows_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, (hipStream_t)stream, rows, m, vals,
+                     present, consts, sal, acc, last, ts, shard, sup, parent, kind, stored, dirty, kind_v, stored_v);
   return (int)hipGetLastError();
 }
 

@@ -552,11 +552,17 @@ class TenantGraph:
             self.n = r_next
             rt = torch.as_tensor(rl, dtype=torch.long).to(dev)
 
-        # host-side columns of a small batch travel in ONE pinned float64 block
-        # (exact for f32 / i32 / u8 / f64 values) instead of one pageable,
-        # host-blocking copy each: consolidate_batch applies ~40 segments a step
+        # a small batch whose per-row columns are all host values (or
+        # scalars): ONE pinned float64 block -> one H2D copy + one kernel
+        # writing every node column (tenant.hip tg_set_rows_kernel) --
+        # consolidate_batch applies ~40 segments a step, each an insert
+        fused = False
+        if dev.type == "cuda" and m <= (1 << 16) and not (parents is not None and any(parents)):
+            fused = self._set_rows_fused(rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored)
         packed = {}
-        if dev.type == "cuda" and m <= (1 << 16):
+        if fused:
+            sh, supv = None, None
+        elif dev.type == "cuda" and m <= (1 << 16):
             def hostcol(v):
                 if v is None or isinstance(v, (int, float, bool, np.number)):
                     return None
@@ -585,22 +591,23 @@ class TenantGraph:
                 return torch.full((m,), v, dtype=dt, device=dev)
             return torch.as_tensor(np.asarray(v)).to(dev, dt)
 
-        sh = col(shard, torch.int32, 0, "shard")
-        supv = col(sup, torch.uint8, 0, "sup")
-        self.sal[rt] = col(sal, torch.float32, 0.5, "sal")
-        self.acc[rt] = col(acc, torch.int32, 0, "acc")
-        self.last[rt] = col(last, torch.float64, now, "last")
-        self.ts[rt] = col(ts, torch.float64, now, "ts")
-        self.shard[rt] = sh
-        self.kind[rt] = GHOST if ghost else NODE
-        self.sup[rt] = supv
-        self.stored[rt] = 1 if stored else 0
-        self.dirty[rt] = 1
-        if parents is not None and any(parents):
-            par = [self._ensure_row(p) if p else -1 for p in parents]
-            self.parent[rt] = torch.as_tensor(par, dtype=torch.int32).to(dev)
-        else:
-            self.parent[rt] = -1
+        if not fused:
+            sh = col(shard, torch.int32, 0, "shard")
+            supv = col(sup, torch.uint8, 0, "sup")
+            self.sal[rt] = col(sal, torch.float32, 0.5, "sal")
+            self.acc[rt] = col(acc, torch.int32, 0, "acc")
+            self.last[rt] = col(last, torch.float64, now, "last")
+            self.ts[rt] = col(ts, torch.float64, now, "ts")
+            self.shard[rt] = sh
+            self.kind[rt] = GHOST if ghost else NODE
+            self.sup[rt] = supv
+            self.stored[rt] = 1 if stored else 0
+            self.dirty[rt] = 1
+            if parents is not None and any(parents):
+                par = [self._ensure_row(p) if p else -1 for p in parents]
+                self.parent[rt] = torch.as_tensor(par, dtype=torch.int32).to(dev)
+            else:
+                self.parent[rt] = -1
         if self.dim is not None:
             if info is None:
                 has = torch.ones(m, dtype=torch.bool, device=dev)
@@ -680,6 +687,45 @@ class TenantGraph:
         self.last_add_rows = rl  # host rows of this call (range or list)
         self._bump(store=True)
         return rt
+
+    def _set_rows_fused(self, rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored) -> bool:
+        """The node columns of an insert through tg_set_rows_kernel when every
+        per-row value is on the host (else False: the caller's column path)."""
+        vals = []
+        consts = np.empty(7, np.float64)
+        present = 0
+        for c, (v, default) in enumerate(((sal, 0.5), (acc, 0), (last, now), (ts, now), (shard, 0), (sup, 0),
+                                          (None, -1))):
+            if v is None:
+                consts[c] = default
+                continue
+            if isinstance(v, (int, float, bool, np.number)):
+                consts[c] = float(v)
+                continue
+            if torch.is_tensor(v):
+                if v.is_cuda:
+                    return False
+                if v.numel() == 1:
+                    consts[c] = float(v.reshape(-1)[0])
+                    continue
+                v = v.numpy()
+            a = np.asarray(v).reshape(-1)
+            if a.size == 1:
+                consts[c] = float(a[0])
+                continue
+            if a.size != m:
+                return False
+            consts[c] = 0.0
+            vals.append(a)
+            present |= 1 << c
+        blk = torch.empty(7 + len(vals) * m, dtype=torch.float64).pin_memory()
+        bn = blk.numpy()
+        bn[:7] = consts
+        for j, a in enumerate(vals):
+            bn[7 + j * m: 7 + (j + 1) * m] = a
+        T.set_rows(self, rt, blk.to(self.device, non_blocking=True), present, GHOST if ghost else NODE,
+                   1 if stored else 0)
+        return True
 
     def _ensure_row(self, node_id: str) -> int:
         """Row of ``node_id``; unknown ids become ghost rows (edge endpoints /

@@ -23,6 +23,7 @@ D_ = C.c_double
 
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
 _lib.register("lzk_tg_write_emb", I, [P, L, P, I, I, P, P, L, P, L, P, L, P, P, P, P, P, P])
+_lib.register("lzk_tg_set_rows", I, [P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, I, I, P])
 _lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
@@ -507,6 +508,23 @@ def store_rerank(Qf: torch.Tensor, X: torch.Tensor, sqn: torch.Tensor, bias: tor
                                            os_.data_ptr(), oi.data_ptr(), _lib.stream_ptr(Qf.device)),
                "lzk_store_rerank")
     return os_, oi
+
+
+SET_ROWS_COLS = ("sal", "acc", "last", "ts", "shard", "sup", "parent")
+
+
+def set_rows(g, rows: torch.Tensor, block: torch.Tensor, present: int, kind_v: int, stored_v: int) -> None:
+    """Node columns of ``rows`` in one launch (tenant.hip tg_set_rows_kernel):
+    ``block`` is a device float64 vector = 7 constants (one per
+    SET_ROWS_COLS column) followed by [ncols, m] per-row values of the
+    columns whose bit is set in ``present``."""
+    m = int(rows.numel())
+    b = block.data_ptr()
+    _lib.check(_lib.lib().lzk_tg_set_rows(
+        rows.data_ptr(), m, b + 7 * 8, int(present), b, g.sal.data_ptr(), g.acc.data_ptr(), g.last.data_ptr(),
+        g.ts.data_ptr(), g.shard.data_ptr(), g.sup.data_ptr(), g.parent.data_ptr(), g.kind.data_ptr(),
+        g.stored.data_ptr(), g.dirty.data_ptr(), int(kind_v), int(stored_v), _lib.stream_ptr(rows.device)),
+        "lzk_tg_set_rows")
 
 
 def write_emb(g, e32: torch.Tensor, has: Optional[torch.Tensor], rows: torch.Tensor, dv_max: torch.Tensor) -> None:
