@@ -108,8 +108,12 @@ DUAL_LOWP = os.environ.get("LZK_DUAL_LOWP", "0") == "1"
 LEAN_HBM = os.environ.get("LZK_LEAN_HBM", "0") == "1"
 # inserts of at most this many rows write their embedding columns in one launch
 WRITE_EMB_MAX_ROWS = 8192
+# node columns of an insert in one launch (tenant.hip tg_set_rows_kernel); 0 = per-column writes
+SET_ROWS_KERNEL = os.environ.get("LZK_SET_ROWS", "1") != "0"
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
 RERANK_KERNEL = os.environ.get("LZK_RERANK_KERNEL", "1") != "0"
+# consolidation's float64 candidate re-rank as one kernel (cos_rerank64_kernel); 0 = torch chain
+RERANK64_KERNEL = os.environ.get("LZK_RERANK64", "1") != "0"
 # cos_topk(min_score=): kernel threshold slack below min_score. Unit rows and
 # queries rounded to bf16 (relative 2^-9 each) move a cosine by at most
 # 2^-8 * sum|q_i x_i| <= 2^-8 ~ 0.0039, plus fp32 accumulation order.
@@ -557,7 +561,7 @@ class TenantGraph:
         # writing every node column (tenant.hip tg_set_rows_kernel) --
         # consolidate_batch applies ~40 segments a step, each an insert
         fused = False
-        if dev.type == "cuda" and m <= (1 << 16) and not (parents is not None and any(parents)):
+        if SET_ROWS_KERNEL and dev.type == "cuda" and m <= (1 << 16) and not (parents is not None and any(parents)):
             fused = self._set_rows_fused(rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored)
         packed = {}
         if fused:
@@ -1626,7 +1630,7 @@ class TenantGraph:
         """Exact float64 cosine of kernel candidates ``cand`` [M, c] (-1 empty),
         sorted (score desc, row asc), cut to k. GPU: one launch
         (tenant.hip cos_rerank64_kernel)."""
-        if self.on_gpu and cand.is_cuda and cand.shape[1] <= 64 and k <= cand.shape[1] and RERANK_KERNEL:
+        if self.on_gpu and cand.is_cuda and cand.shape[1] <= 64 and k <= cand.shape[1] and RERANK64_KERNEL:
             from ..ops import _lib
             M, C = cand.shape
             qd = Qn.to(self.device, torch.float64).contiguous()

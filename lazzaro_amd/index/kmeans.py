@@ -149,6 +149,10 @@ def assign_two_level(X: torch.Tensor, C16: torch.Tensor, T16: torch.Tensor, top_
     return lab, score
 
 
+# farthest-first seeding as one fused kernel per pick (csrc/kernels/kmeans.hip); 0 = torch GEMV chain
+FF_KERNEL = os.environ.get("LZK_FF_KERNEL", "1") != "0"
+
+
 def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 16,
                     rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Deterministic farthest-first seeding on a subsample (k-means++ without
@@ -159,7 +163,8 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 1
     sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
     if rows is not None:
         sub = rows[sub]
-    if X.is_cuda and X.dtype == torch.bfloat16 and X.shape[1] % 8 == 0 and X.shape[1] <= 2048 and sub.numel():
+    if FF_KERNEL and X.is_cuda and X.dtype == torch.bfloat16 and X.shape[1] % 8 == 0 and X.shape[1] <= 2048 \
+            and sub.numel():
         # one fused HIP kernel per pick, enqueued from C++ (csrc/kernels/kmeans.hip)
         from ..ops import _lib
         Sb = X[sub].contiguous()
