@@ -382,9 +382,11 @@ NARROW_MAX_Q = 128  # below this many queries the int8 scan is the HBM-bound nar
 _lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
 
 # The dedicated int8 scan (csrc/kernels/scan8.hip: one K-tile stream across
-# tiles, int-domain epilogue); LZK_SCAN8=0 takes the shared 256^2 template
-# instead (A/B only).
-SCAN8 = os.environ.get("LZK_SCAN8", "1") != "0"
+# tiles, int-domain epilogue) is opt-in (LZK_SCAN8=1) until it matches the
+# shared 256^2 template on the GPU; the narrow kernel for batches under 128
+# queries (same file) is on (LZK_SCAN8_NARROW=0 disables it).
+SCAN8 = os.environ.get("LZK_SCAN8", "0") == "1"
+SCAN8_NARROW = os.environ.get("LZK_SCAN8_NARROW", "1") != "0"
 _ws_scan8 = _Workspace()
 
 
@@ -554,7 +556,7 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     cap = max(2048, 16 * kslot * S)
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
     qs = qscale.contiguous()
-    if nq < NARROW_MAX_Q and SCAN8 and Dp % 64 == 0:
+    if nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
         _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
         return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)

@@ -525,47 +525,39 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     best_s = torch.full((NQ, limit), float("-inf"), dtype=torch.float32, device=dev)
     best_k = torch.full((NQ, limit), -1, dtype=torch.int64, device=dev)
     best_t = torch.full((NQ, limit), -1, dtype=torch.int64, device=dev)
-    users = [u for u, ms in svc.systems.items() if ms.graph.dim == D and ms.graph.n > 0]
-    table = svc.tenant_table(svc.systems[users[0]].graph.device if users else None)
-    if users:
-        slots = table.slots_host(users, {u: svc.systems[u] for u in users}).tolist()
-        small = [i for i, u in enumerate(users) if MT_GLOBAL and _fused_ok(svc.systems[u], D, limit)]
-        if len(small) >= MT_MIN_TENANTS and NQ:
+    gd = svc.global_directory(D, limit) if D else None
+    redo = None
+    if gd is not None and gd["small"] and NQ:
+        if len(gd["small"]) >= MT_MIN_TENANTS:
             # the small tenants: ONE multi-tenant MFMA pass (ops/search.py mt_topk)
-            s, key, tk, redo = _global_small(svc, table, [users[i] for i in small],
-                                             np.asarray([slots[i] for i in small], np.int64), Qall, limit, me, dev)
+            s, key, tk, redo = _global_small(svc, gd, Qall, limit, me, dev)
             best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
                                             torch.cat([best_t, tk], 1))
-            done = set(small)
-            rest = [i for i in range(len(users)) if i not in done]
-            if redo is not None:  # queries whose candidate list overflowed: the per-tenant path
-                rest += sorted(done)
+            per = [(u, int(sl), redo) for u, sl in zip(gd["small"], gd["slots"].tolist())] if redo is not None \
+                else []
         else:
-            redo = None
-            rest = list(range(len(users)))
-        for i in rest:
-            u, slot = users[i], slots[i]
-            if redo is not None and i in done:
-                qsel = redo
-            else:
-                qsel = None
-            ms = svc.systems[u]
-            g = ms.graph
-            Qi = Qall if qsel is None else Qall[qsel]
-            with ms._graph_lock:
-                s, r = g.store_search(Qi.to(g.device), limit, getattr(ms.store, "metric", "l2"))
-                with g.on_stream():
-                    ok = (r >= 0) & (g.kind[r.clamp_min(0)] == NODE)
-            s = torch.where(ok, s.float(), torch.full_like(s, float("-inf"))).to(dev)
-            key = torch.where(ok, (me << 56) | (int(slot) << 32) | r, torch.full_like(r, -1)).to(dev)
-            tk = torch.where(ok, torch.full_like(r, tenant_key(u)), torch.full_like(r, -1)).to(dev)
-            if qsel is None:
-                best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
-                                                torch.cat([best_t, tk], 1))
-            else:
-                m_s, m_k, m_t = _merge(torch.cat([best_s[qsel], s], 1), torch.cat([best_k[qsel], key], 1), limit,
-                                       torch.cat([best_t[qsel], tk], 1))
-                best_s[qsel], best_k[qsel], best_t[qsel] = m_s, m_k, m_t
+            per = [(u, int(sl), None) for u, sl in zip(gd["small"], gd["slots"].tolist())]
+    else:
+        per = []
+    per += [(u, sl, None) for u, sl in (gd["big"] if gd is not None else [])]
+    for u, slot, qsel in per:
+        ms = svc.systems[u]
+        g = ms.graph
+        Qi = Qall if qsel is None else Qall[qsel]
+        with ms._graph_lock:
+            s, r = g.store_search(Qi.to(g.device), limit, getattr(ms.store, "metric", "l2"))
+            with g.on_stream():
+                ok = (r >= 0) & (g.kind[r.clamp_min(0)] == NODE)
+        s = torch.where(ok, s.float(), torch.full_like(s, float("-inf"))).to(dev)
+        key = torch.where(ok, (me << 56) | (int(slot) << 32) | r, torch.full_like(r, -1)).to(dev)
+        tk = torch.where(ok, torch.full_like(r, tenant_key(u)), torch.full_like(r, -1)).to(dev)
+        if qsel is None:
+            best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,
+                                            torch.cat([best_t, tk], 1))
+        else:
+            m_s, m_k, m_t = _merge(torch.cat([best_s[qsel], s], 1), torch.cat([best_k[qsel], key], 1), limit,
+                                   torch.cat([best_t[qsel], tk], 1))
+            best_s[qsel], best_k[qsel], best_t[qsel] = m_s, m_k, m_t
     if not force:
         return GlobalHits(best_s[:b], best_k[:b], best_t[:b])
     # candidates for rank j's queries go back to rank j
@@ -589,42 +581,33 @@ MT_GLOBAL = os.environ.get("LZK_MT_GLOBAL", "1") != "0"
 MT_MIN_TENANTS = 2
 
 
-def _global_small(svc, table, users: List[str], slots: np.ndarray, Qall: torch.Tensor, limit: int, me: int, dev):
-    """Every query against every small tenant in one tile-table pass. Returns
-    (scores, keys = rank << 56 | slot << 32 | row, tenant keys, the queries
-    whose candidate list overflowed -- None when none did -- to be redone by
-    the per-tenant path; those queries' rows here are empty)."""
+def _global_small(svc, gd, Qall: torch.Tensor, limit: int, me: int, dev):
+    """Every query against every small tenant of the global directory
+    (:meth:`DistributedMemoryService.global_directory`) in one tile-table
+    pass. Returns (scores, keys = rank << 56 | slot << 32 | row, tenant keys,
+    the queries whose candidate list overflowed -- None when none did -- to be
+    redone by the per-tenant path; those queries' rows here are empty)."""
     from ..ops.search import mt_topk
-    systems = [svc.systems[u] for u in users]
-    locks = [ms._graph_lock for ms in sorted(systems, key=lambda m: id(m))]
+    table = gd["table"]
+    locks = [svc.systems[u]._graph_lock for u in gd["small"]] if gd["lock"] else []
     for lk in locks:
         lk.acquire()
     try:
-        gdev = systems[0].graph.device
+        gdev = table.device
         cur = torch.cuda.current_stream(gdev)
-        streams = {}
-        for ms in systems:
-            st = getattr(ms.graph, "stream", None)
-            if st is not None:
-                streams[st.cuda_stream] = st
-        for st in streams.values():  # the tenants' pending column writes first
+        for st in gd["streams"]:  # the tenants' pending column writes first
             if st.cuda_stream != cur.cuda_stream:
                 cur.wait_stream(st)
-        tiles = table.tiles(slots)
+        tiles = table.tiles(gd["slots"])
         s, key, ovf = mt_topk(tiles, Qall.to(gdev), limit, table.d_ptr[0], table.d_ptr[1], table.d_ptr[4])
-        for st in streams.values():  # no column freed / reused under the pass
+        for st in gd["streams"]:  # no column freed / reused under the pass
             if st.cuda_stream != cur.cuda_stream:
                 st.wait_stream(cur)
     finally:
         for lk in reversed(locks):
             lk.release()
-    # stable tenant key of every slot (host table, uploaded per call: small)
-    tkeys = np.full(table.cap, -1, np.int64)
-    for u, sl in zip(users, slots.tolist()):
-        tkeys[sl] = tenant_key(u)
-    tk_dev = torch.from_numpy(tkeys).to(gdev)
     ok = key >= 0
-    tk = torch.where(ok, tk_dev[(key >> 32).clamp_min(0)], torch.full_like(key, -1))
+    tk = torch.where(ok, gd["tkeys"][(key >> 32).clamp_min(0)], torch.full_like(key, -1))
     key = torch.where(ok, (me << 56) | key, torch.full_like(key, -1))
     redo = None
     if bool((ovf != 0).any()):  # rare: pathological score distributions

@@ -160,6 +160,9 @@ class DistributedMemoryService:
         self._dir_epoch = 0
         self._ddir = None  # the device directory (see device_directory)
         self._ddir_dirty: set = set()  # pinned tenants mutated since it was built
+        self._gdir = None  # the global-search directory (see global_directory)
+        self._gdir_dirty: set = set()
+        self._membership = 0  # bumps whenever a tenant becomes / stops being resident
         self.route_stats = {"device": 0, "host": 0}  # routed batches served by device key matching / by name
         self._owner_epoch: Dict[int, int] = {}
 
@@ -219,29 +222,19 @@ class DistributedMemoryService:
     def pin(self, user: str) -> None:
         """Keep an announced tenant resident for the routed path (loads it
         if needed); its mutations mark the device directory for refresh."""
-        ms = self.system(user)
+        self.system(user)
         key = routing.tenant_key(user)
         if key not in self._pinned:
             self._pinned[key] = user
             self._ddir = None
-        g = getattr(ms, "graph", None)
-        if g is not None:
-            g.on_change = lambda u=user: self._ddir_dirty.add(u)
 
     def _unpin(self, user: str) -> None:
         if self._pinned.pop(routing.tenant_key(user), None) is not None:
             self._dir_epoch += 1
             self._ddir = None
-            ms = self.systems.get(user)
-            if ms is not None and getattr(ms, "graph", None) is not None:
-                ms.graph.on_change = None
 
     def _unpin_all(self) -> None:
         if self._pinned:
-            for u in list(self._pinned.values()):
-                ms = self.systems.get(u)
-                if ms is not None and getattr(ms, "graph", None) is not None:
-                    ms.graph.on_change = None
             self._pinned = {}
             self._dir_epoch += 1
             self._ddir = None
@@ -313,6 +306,9 @@ class DistributedMemoryService:
 
     def _release(self, user: str, ms) -> None:
         """Persist and close a tenant this rank stops holding."""
+        self._membership += 1
+        if getattr(ms, "graph", None) is not None:
+            ms.graph.on_change = None
         self._unpin(user)
         self._settle(user)
         if self._table is not None:
@@ -352,12 +348,81 @@ class DistributedMemoryService:
         if ms is None:
             ms = self._build(user)
             self.systems[user] = ms
+            self._resident(user, ms)
             while len(self.systems) > self.max_resident:
                 u0, old = self.systems.popitem(last=False)
                 self._release(u0, old)
         else:
             self.systems.move_to_end(user)
         return ms
+
+    def _resident(self, user: str, ms) -> None:
+        """A tenant became resident: its mutations mark the device and
+        global directories (TenantGraph.on_change)."""
+        self._membership += 1
+        g = getattr(ms, "graph", None)
+        if g is not None:
+            g.on_change = lambda u=user: (self._ddir_dirty.add(u), self._gdir_dirty.add(u))
+
+    def global_directory(self, D: int, k: int):
+        """The resident tenants of width ``D`` as global search sees them:
+        ``small`` (names, table slots, stable tenant keys as a device array
+        indexed by slot, their graph streams, whether any needs its graph
+        lock held) for the one-pass tile-table scan, and ``big`` (name, slot)
+        for per-tenant store searches. Rebuilt when residency, the width or a
+        mutated tenant's class changed; a mutated small tenant only has its
+        table entry refreshed -- no per-call pass over thousands of tenants."""
+        d = self._gdir
+        if d is not None and d["D"] == D and d["k"] >= k and d["membership"] == self._membership:
+            if self._gdir_dirty:
+                dirty, self._gdir_dirty = self._gdir_dirty, set()
+                for u in dirty:
+                    ms = self.systems.get(u)
+                    if ms is None:
+                        continue
+                    if self._global_class(ms, D, d["k"]) != d["cls"].get(u):
+                        self._gdir = None
+                        return self.global_directory(D, k)
+                small = [u for u in dirty if d["cls"].get(u) == "small"]
+                if small and d["table"] is not None:
+                    d["table"].slots_host(small, self.systems)
+            return d
+        self._gdir_dirty = set()
+        k = max(int(k), 1)
+        cls = {u: self._global_class(ms, D, k) for u, ms in self.systems.items()}
+        small = [u for u, c in cls.items() if c == "small"]
+        bigu = [u for u, c in cls.items() if c == "big"]
+        table = None
+        slots = np.zeros(0, np.int64)
+        big = []
+        users = small + bigu
+        if users:
+            table = self.tenant_table(self.systems[users[0]].graph.device)
+            sl = table.slots_host(users, self.systems)
+            slots = sl[: len(small)]
+            big = list(zip(bigu, sl[len(small):].tolist()))
+        tk = tkdev = None
+        streams = {}
+        if small:
+            tk = np.full(table.cap, -1, np.int64)
+            tk[slots] = [routing.tenant_key(u) for u in small]
+            tkdev = torch.from_numpy(tk).to(table.device)
+            for u in small:
+                st = getattr(self.systems[u].graph, "stream", None)
+                if st is not None:
+                    streams[st.cuda_stream] = st
+        self._gdir = {"D": D, "k": k, "membership": self._membership, "cls": cls, "small": small,
+                      "slots": np.asarray(slots, np.int64), "tkeys": tkdev, "big": big, "table": table,
+                      "streams": list(streams.values()),
+                      "lock": any(getattr(self.systems[u], "enable_async", False) for u in small)}
+        return self._gdir
+
+    @staticmethod
+    def _global_class(ms, D: int, k: int) -> Optional[str]:
+        g = getattr(ms, "graph", None)
+        if g is None or g.dim != D or g.n == 0:
+            return None
+        return "small" if (routing.MT_GLOBAL and routing._fused_ok(ms, D, k)) else "big"
 
     def migrate(self, moves: Dict[str, int]) -> List[str]:
         """SPMD live re-shard of tenants (C3): ``moves`` = {user: new rank},
@@ -378,6 +443,8 @@ class DistributedMemoryService:
                 self._settle(user)
                 self._unpin(user)
                 ms = self.systems.pop(user)
+                self._membership += 1
+                ms.graph.on_change = None
                 if self._table is not None:
                     self._table.drop(user)
                 ms._save_to_persistence()
@@ -406,6 +473,7 @@ class DistributedMemoryService:
                 ms = self._build(user, load=False)
                 ms.import_state(meta, vec)
                 self.systems[user] = ms
+                self._resident(user, ms)
                 received.append(user)
         return received
 
