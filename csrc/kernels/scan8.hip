@@ -128,16 +128,22 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
 
   // tile-invariant per-lane staging offsets: piece c = 2 * wave + i covers
   // rows 8c .. 8c+7 of a half-tile; the 16-B chunk is XOR-swizzled on the
-  // SOURCE address (the LDS image is lane-linear), undone by the reads
-  int voA[2], voB[2];
+  // SOURCE address (the LDS image is lane-linear), undone by the reads. The
+  // half-tile's row offset is part of the VGPR offset (index [h]): the buffer
+  // range check covers the VGPR offset only -- not the SGPR offset, which
+  // carries just the K-tile's byte offset (< one row) -- so rows past the
+  // tile's last valid row read as zero instead of past the operand.
+  int voA[2][2], voB[2][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = wave * 2 + i;
-    const int row = 8 * c + (lane >> 3);
-    const int kc = (lane & 7) ^ ((row >> 1) & 7);
-    voA[i] = (int)(row * ldx) + kc * 16;
-    voB[i] = (int)(row * ldq) + kc * 16;
-  }
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = wave * 2 + i;
+      const int row = 8 * c + (lane >> 3);
+      const int kc = (lane & 7) ^ ((row >> 1) & 7);
+      voA[h][i] = (int)((128 * h + row) * ldx) + kc * 16;
+      voB[h][i] = (int)((128 * h + row) * ldq) + kc * 16;
+    }
   // per-lane read bases inside a slot: row l16 of a 16-row block, chunk
   // (4s + lq) ^ ((l16 >> 1) & 7); the block's row offset is an immediate
   int rb[2];
@@ -158,12 +164,12 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
     const int n_left = isA ? min(256, nrows - g.r0) : min(256, nq - g.q0);
     const signed char* base = isA ? X + (long)g.r0 * ldx : Qm + (long)g.q0 * ldq;
     const __amdgpu_buffer_rsrc_t r = make_rsrc(base, (long)n_left * ld);
-    const int soff = kt * 128 + ((H & 1) ? (int)(128 * ld) : 0);
+    const int soff = kt * 128;
     unsigned char* sl = smem + (buf * 4 + H) * SLOT;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(sl + (wave * 2 + i) * 1024), 16,
-                                               isA ? voA[i] : voB[i], soff, 0, 0);
+                                               isA ? voA[H & 1][i] : voB[H & 1][i], soff, 0, 0);
   };
   // epilogue operands of tile t -> parity p: 4 wave-level DMAs (64 x 4 B)
   // per array, spread over the 8 waves
@@ -309,16 +315,18 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
           m = max(m, max(acc[i][j][0], acc[i][j][1]));
           m = max(m, max(acc[i][j][2], acc[i][j][3]));
         }
-        // every score of this lane's column in the wave's rows is <= bound
+        // every score of this lane's column in the wave's rows is <= bound;
+        // the skips are wave-uniform (ballots), so the append counter wpos
+        // stays uniform -- a lane that skipped would miss the counts
         const float bound = (m > 0 ? al * ((float)m * rsmax) : 0.f) + bmax;
-        if (!(bound >= tcut)) continue;
+        if (__ballot(bound >= tcut) == 0ull) continue;
         const int qlab = DUAL ? reinterpret_cast<const int*>(E)[6 * 256 + qlo] : -1;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const i32x4 v = acc[i][j];
           const int mi = max(max(v[0], v[1]), max(v[2], v[3]));
           const float bi = (mi > 0 ? al * ((float)mi * rsmax) : 0.f) + bmax;
-          if (!(bi >= tcut)) continue;
+          if (__ballot(bi >= tcut) == 0ull) continue;
           const int rl = wr * 128 + i * 16 + 4 * lq;
           const f32x4 rsv = *reinterpret_cast<const f32x4*>(E + 2 * 256 + rl);
           f32x4 bv = {0.f, 0.f, 0.f, 0.f};
