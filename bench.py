@@ -144,6 +144,25 @@ def recall(found_rows, truth_rows):
     return hit / max(tot, 1)
 
 
+def recall_misses(g, Q, found_rows, truth_s, truth_rows, limit: int = 8):
+    """The misses of a recall check: for each returned row outside the float64
+    top-k, the float64 score gap between it and the k-th true row. A gap at
+    the fp32 rounding level (~1e-7 of scores of magnitude ~1) is a near-tie
+    that the store's fp32 ranking (the reference's LanceDB precision) may
+    order either way; a larger gap would be a search error."""
+    out = []
+    ts = truth_s.cpu().tolist()
+    for q, (f, t) in enumerate(zip(found_rows, truth_rows.tolist())):
+        for r in set(f) - set(t):
+            x = g.emb32[r].double()
+            qd = Q[q].double()
+            sc = float(-((qd - x) ** 2).sum())
+            out.append({"query": q, "row": int(r), "gap_to_kth": ts[q][-1] - sc})
+            if len(out) >= limit:
+                return out
+    return out
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -406,8 +425,9 @@ def main():
     Qr = torch.randn((nr, a.dim), device=dev, generator=gen)
     Qr /= Qr.norm(dim=1, keepdim=True)
     _, rows_r = g.store_search(Qr, a.k, "l2")
-    _, truth_r = exact_l2_topk(g, Qr, a.k)
+    ts_r, truth_r = exact_l2_topk(g, Qr, a.k)
     rec_rand = recall(rows_r.cpu().tolist(), truth_r)
+    miss_r = recall_misses(g, Qr, rows_r.cpu().tolist(), ts_r, truth_r) if rec_rand < 1.0 else []
     S_tok = int(emb.tok.encode_batch(pool[0], emb.max_len)[0].shape[1])
     lens = emb.tok.encode_batch(pool[0], emb.max_len)[1]
 
@@ -469,6 +489,8 @@ def main():
         "serving": serving,
         "recall_at_10": round(rec_api, 4),
         "recall_at_10_random_queries": round(rec_rand, 4),
+        "recall_queries": nr,
+        "recall_misses_random": miss_r,
         "recall_truth": "float64 exact L2 over the stored fp32 vectors",
         "breakdown_ms": {"embed": round(t_embed, 3),
                          "embed_encoder_only": None if t_embed_dev is None else round(t_embed_dev, 3),

@@ -232,7 +232,7 @@ def local_search(svc, users: Sequence[str], Q: torch.Tensor, limits: Sequence[in
             slots = table.slots(qu, systems)
             ptrs = table.d_ptr[:, slots]
             nrows = table.d_n[slots]
-            qt = torch.as_tensor(qi, dtype=torch.long, device=dev)
+            qt = _to_dev(torch.as_tensor(qi, dtype=torch.long), dev)
             Qs = Q[qt].contiguous()
             s, r = segment_topk_ptrs(ptrs[0].contiguous(), nrows.contiguous(), D, Qs, k,
                                      bptr=ptrs[1].contiguous(), alpha=2.0, qbias=-(Qs * Qs).sum(1))
@@ -363,7 +363,11 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     senders_current = all(int(allc[s, me, 4]) == epoch0 for s in range(W) if allc[s, me, 0] > 0)
     ddir = svc.device_directory(Dg, K) if (senders_current and svc._dir_epoch == epoch0) else None
     on_device = ddir is not None
-    Qo = Q[torch.as_tensor(order, dtype=torch.long, device=Q.device)] if n else torch.zeros((0, Dg), device=dev)
+    # the permutations travel as pinned async copies: a pageable host -> device
+    # copy would wait for every kernel already queued (the previous batch's
+    # search), i.e. a host sync per routed batch
+    order_h = np.asarray(order, np.int64)
+    Qo = Q[_to_dev(torch.from_numpy(order_h), Q.device)] if n else torch.zeros((0, Dg), device=dev)
     pay = _pack_queries(Qo, [tenant_key(users[j]) for j in order], [limits[j] for j in order]) if n else \
         torch.zeros((0, Dg + 3), dtype=torch.int32)
     got = comm.all_to_all_v(pay.to(dev), send_n.tolist(), recv_n.tolist())
@@ -383,9 +387,9 @@ def search_routed(svc, users: Sequence[str], Q: torch.Tensor, limit=5) -> Routed
     else:
         back = torch.zeros((0, 2 * K), dtype=torch.int32, device=dev)
     res = comm.all_to_all_v(back.contiguous(), recv_n.tolist(), send_n.tolist())
-    inv = torch.empty(n, dtype=torch.long)
-    inv[torch.as_tensor(order, dtype=torch.long)] = torch.arange(n)
-    res = res[inv.to(res.device)]
+    inv = np.empty(n, np.int64)
+    inv[order_h] = np.arange(n)
+    res = res[_to_dev(torch.from_numpy(inv), res.device)]
     S = res[:, :K].contiguous().view(torch.float32)
     R = res[:, K:].to(torch.int64)
     return RoutedHits(list(users), owner, S, R)

@@ -187,17 +187,49 @@ class ShardedMemorySystem:
             self.num = torch.cat([self.num, grow])
             self.holder = torch.cat([self.holder, grow.clone()])
 
+    # rows appended since the sorted number index was built are searched in a
+    # small sorted delta; the base is rebuilt once the delta outgrows this
+    NUM_DELTA_MAX = 1 << 16
+
+    def _num_index(self) -> Dict:
+        """Sorted index of the number column: a base over rows [0, n0) and a
+        delta over the rows appended since, each (sorted numbers, rows). A
+        row's number is written once, right after its row is added, so the
+        index only ever grows -- the consolidation looks rows up several
+        times per segment, and re-sorting a 10M-row column each time was the
+        row-sharded step's largest cost."""
+        n = self.g.n
+        ix = getattr(self, "_num_ix", None)
+        dev = self.device
+
+        def build(a, b):
+            key = self.num[a:b]
+            o = torch.argsort(key, stable=True)
+            return key[o], o + a
+        if ix is None or ix["n0"] > n or n - ix["n0"] > max(self.NUM_DELTA_MAX, ix["n0"] >> 4):
+            ks, o = build(0, n)
+            z = torch.zeros(0, dtype=torch.long, device=dev)
+            ix = {"n0": n, "n1": n, "ks": ks, "o": o, "dk": z, "do": z}
+            self._num_ix = ix
+        elif ix["n1"] < n:
+            ix["dk"], ix["do"] = build(ix["n0"], n)
+            ix["n1"] = n
+        return ix
+
     def _rows_of_nums(self, nums: torch.Tensor) -> torch.Tensor:
         """Local row holding each global node number (live or ghost), -1 if
-        none: one sort of the number column + a binary search (no host map)."""
+        none: binary searches in the cached sorted number index (no host map)."""
         n = self.g.n
         if n == 0 or nums.numel() == 0:
             return torch.full_like(nums, -1)
-        key = self.num[:n]
-        o = torch.argsort(key)
-        ks = key[o]
-        pos = torch.searchsorted(ks, nums).clamp_max(n - 1)
-        return torch.where(ks[pos] == nums, o[pos], torch.full_like(nums, -1))
+        ix = self._num_index()
+        out = torch.full_like(nums, -1)
+        for ks, o in ((ix["dk"], ix["do"]), (ix["ks"], ix["o"])):  # the base wins a (never expected) tie
+            if ks.numel() == 0:
+                continue
+            pos = torch.searchsorted(ks, nums).clamp_max(ks.numel() - 1)
+            out = torch.where(ks[pos] == nums, o[pos], out)
+        return out
 
     def _register_shards(self, keys: Sequence[str]) -> np.ndarray:
         return np.asarray([self.g.shard_id(k) for k in keys], dtype=np.int32)
