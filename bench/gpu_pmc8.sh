@@ -18,6 +18,8 @@ for mode in cand inf tmpl; do
     rc=$?
     echo "pass $i mode=$mode rc=$rc" >> $OUT/passes.log
     [ $rc -ne 0 ] && exit $rc
+    python3 $R/bench/pmc_reduce.py $OUT/p$i "scan8_kernel|flat_cand_persistent" > $OUT/p$i.json
+    rm -rf $OUT/p$i
   done
 done
 exit 0
