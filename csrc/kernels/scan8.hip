@@ -52,7 +52,13 @@ constexpr int RING = 8 * SLOT;              // 2 K-tile buffers x {A0, A1, B0, B
 // epilogue operands per tile parity: thr | bias | rs | qs | thr2 | row label | query label | group stats
 constexpr int NARR = 8;
 constexpr int EPI_BYTES = 2 * NARR * 256 * 4;
-constexpr int LDS_TOTAL = RING + EPI_BYTES + 16;
+// candidate records are staged in LDS per wave and written to the wave's
+// global region in batches: a global store in the epilogue would join the
+// vmcnt the K loop counts its operand DMAs with, so the next counted wait
+// would stall on the store's write-back (PMC: 6x the wait cycles)
+constexpr int LREC = 120;                   // staged records per wave (16 B each)
+constexpr int REC_OFF = RING + EPI_BYTES;
+constexpr int LDS_TOTAL = REC_OFF + 8 * LREC * 16;
 
 __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
@@ -60,6 +66,23 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Record staging in LDS through inline asm: the compiler treats any ds_write
+// to the dynamic LDS array as possibly aliasing the in-flight LDS-DMA
+// operand loads and puts an s_waitcnt vmcnt(0) in front of it (draining the
+// K loop's prefetch); the staging slots never overlap the DMA destinations,
+// so these writes / reads wait only on lgkmcnt, which they count in.
+__device__ __forceinline__ void lds_write16(const void* p, int4 v) {
+  const unsigned a = (unsigned)(size_t)(lds_void_t*)p;
+  const i32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(w) : "memory");
+}
+__device__ __forceinline__ int4 lds_read16(const void* p) {
+  const unsigned a = (unsigned)(size_t)(lds_void_t*)p;
+  i32x4 w;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(a) : "memory");
+  return make_int4(w[0], w[1], w[2], w[3]);
+}
 
 struct Recs {
   int4* buf;  // [grid * 8][cap]: one region per wave
@@ -200,14 +223,31 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
   // in-flight operand DMA (vmcnt(0)) before it.
   const int capw = rec.cap;
   int4* wbuf = rec.buf + (long)(bid * 8 + wave) * capw;
-  int wpos = 0;
+  int4* lrec = reinterpret_cast<int4*>(smem + REC_OFF) + wave * LREC;
+  int wpos = 0;  // records of this wave written to its global region (wave-uniform)
+  int lpos = 0;  // records staged in its LDS slots (wave-uniform)
+  auto flush = [&]() {  // staged records -> the global region, one 16-B store per lane
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staged writes landed
+    if (lane < lpos) {
+      const int4 v = lds_read16(lrec + lane);
+      if (wpos + lane < capw) wbuf[wpos + lane] = v;
+    }
+    if (lpos > 64 && lane < lpos - 64) {
+      const int4 v = lds_read16(lrec + 64 + lane);
+      if (wpos + 64 + lane < capw) wbuf[wpos + 64 + lane] = v;
+    }
+    wpos += lpos;
+    lpos = 0;
+  };
   auto append = [&](bool take, int lists, int q, float v, int r) {
     const unsigned long long ball = __ballot(take);
     if (ball == 0ull) return;
-    const int pos = wpos + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32),
+    const int nb = __builtin_popcountll(ball);
+    if (lpos + nb > LREC) flush();
+    const int pos = lpos + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0u));
-    if (take && pos < capw) wbuf[pos] = make_int4(q, r, __float_as_int(v), lists);
-    wpos += __builtin_popcountll(ball);
+    if (take) lds_write16(lrec + pos, make_int4(q, r, __float_as_int(v), lists));
+    lpos += nb;
   };
 
   // ---- prologue: K-tile 0 of the first tile + its epilogue operands (buffer
@@ -351,6 +391,7 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
     cur = nxt;
   }
   if (wr == 0) bar();  // un-stagger
+  flush();
   if (lane == 0) rec.cnt[bid * 8 + wave] = wpos;  // > cap: records were dropped
 }
 
