@@ -1827,6 +1827,10 @@ class TenantGraph:
         the margin is LOWP_MARGIN_Z standard deviations plus that floor."""
         from ..ops.search import flat_topk_i8
         q8, qs, margin = self._i8_query(q16, alpha)
+        if self.emb16 is None:
+            # lean: the re-score reads the fp32 rows, so the margin also covers
+            # |<q16, x16> - <q, x>| <= 2^-8 |q| |x| (both operands rounded to bf16)
+            margin = margin + alpha * 2.0 ** -8 * Qf.norm(dim=1) * (1.0 + self.max_norm_dev)
         return flat_topk_i8(self.emb8, self.rs8, q8, qs, self._scan_rows(self.n, Qf), q16, kc, bias=bias,
                             alpha=alpha, margin=margin)
 

@@ -550,12 +550,36 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     assert alpha > 0
     dev = X16.device
     S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
-    thr = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
+    spec = 0 < SPEC_J < k and S >= SPEC_MIN_STRIDE and nq >= NARROW_MAX_Q
+    if spec:
+        # speculative threshold: the sample's SPEC_J-th best (~SPEC_J * S-th
+        # overall) instead of its k-th -- lists ~k / SPEC_J times shorter; a
+        # query is recomputed exactly unless k entries clear it (see below)
+        Xs = X16[::S]
+        bs = bias[:N:S].contiguous() if bias is not None else None
+        ts, _ = _flat_topk_lane(Xs, Q16, kslot, kslot, bs, None, None, alpha, 0, None)
+        tau = _margin(ts[:, SPEC_J - 1]).contiguous()
+        thr = tau
+    else:
+        thr = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
     if margin is not None:
         thr = (thr - margin).contiguous()
     cap = max(2048, 16 * kslot * S)
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
     qs = qscale.contiguous()
+
+    def need_of():
+        """Speculative threshold check: a query keeps its list only when at
+        least k entries have exact (re-scored) scores >= tau -- then the true
+        k-th score is >= tau, every true top-k row has int8 score >= tau -
+        margin (so it is in the list) and lies above the re-score cut;
+        otherwise need = cap + 1 flags it for the exact fallback."""
+        if not spec:
+            return None
+        c = (cnt & 0x3FFFFFFF).clamp_max(cap)
+        valid = torch.arange(cap, device=dev)[None, :] < c[:, None]
+        hit = ((cs.view(nq, cap) >= tau[:, None]) & valid).sum(1)
+        return torch.where(hit >= k, torch.zeros_like(hit), torch.full_like(hit, cap + 1)).to(torch.int32)
     if nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
         _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
@@ -564,7 +588,8 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
         _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, None, None, None, kslot, 2 * S, 1, cap, (cnt, cs, ci),
                None)
         _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
-        return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
+        return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap,
+                                     need=need_of())
     grid = L.lzk_cand_grid_f8(N, nq)
     bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 1)
     st = _lib.stream_ptr(dev)
@@ -575,7 +600,13 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
                                  ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
     _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
-    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
+    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap, need=need_of())
+
+
+# Speculative store-search threshold (flat_topk_i8, wide batches): the 1/S
+# sample's SPEC_J-th best score; LZK_SPEC_J=0 restores the sample's k-th best.
+SPEC_J = int(os.environ.get("LZK_SPEC_J", "5"))
+SPEC_MIN_STRIDE = 32
 
 
 def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None):
