@@ -94,7 +94,7 @@ def main():
            "vector_bytes_per_row": vec_bytes, "node_column_bytes_per_row": node_bytes,
            "tenant_hbm_gib": round((vec_bytes + node_bytes) * g.cap / 2**30, 1),
            "hbm_allocated_gib": round(torch.cuda.memory_allocated(dev) / 2**30, 1), "load_s": round(t_load, 1),
-           "path": "TenantGraph.store_search: int8 MFMA candidate scan (scan8) -> fp32 re-score above the error "
+           "path": "TenantGraph.store_search: int8 MFMA candidate scan -> fp32 re-score above the error "
                    "cut (lzk_cand_rescore32) -> fp32 L2 re-rank" if g.lean else
                    "TenantGraph.store_search: int8 scan -> bf16 re-score -> fp32 re-rank",
            "data": "synthetic clustered unit vectors (4096 centres)"}
