@@ -41,6 +41,7 @@ turns/sec = conversations consolidated per second over all ranks.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import random
@@ -55,6 +56,25 @@ sys.path.insert(0, ROOT)
 
 SHARDS = ("work", "personal", "learning", "health", "2026-10")
 WORDS = "user likes prefers works lives started visited learned project team python rust garden music".split()
+
+
+@contextlib.contextmanager
+def _ff_timer():
+    """Device time of the farthest-first seeding inside the cold cluster pass
+    (the ``ff_seed`` tracer stage, index/kmeans.py); the rest of the cold
+    pass is the k-means iterations over every row."""
+    from lazzaro_amd.utils.tracing import tracer
+    was = tracer.enabled
+    tracer.enable(True)
+    out = {}
+    try:
+        yield out
+    finally:
+        st = tracer.summary().get("ff_seed")
+        out["ms"] = round(st["total_ms"], 1) if st else None
+        if not was:
+            tracer.reset()
+        tracer.enable(was)
 
 
 def _unit(x):
@@ -128,7 +148,8 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     # passes are warm-started and run inside the timed loop
     _sync(dev)
     t0 = time.perf_counter()
-    ms.graph.cluster_pass(n_fine, n_top, cluster_iters)
+    with _ff_timer() as ff:
+        ms.graph.cluster_pass(n_fine, n_top, cluster_iters)
     _sync(dev)
     seed_ms = (time.perf_counter() - t0) * 1e3
 
@@ -187,7 +208,8 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
            "scan_facts_x_rows_per_rank_step": int(convs * facts * g.n),
            "path": "MemorySystem.consolidate_batch (tenant-DP)",
            "hierarchical_clustering": {"mode": "kmeans", "every_steps": cluster_every, "fine": n_fine, "top": n_top,
-                                       "iters_per_pass": cluster_iters, "seed_pass_ms": round(seed_ms, 1)},
+                                       "iters_per_pass": cluster_iters, "seed_pass_ms": round(seed_ms, 1),
+                                       "farthest_first_ms": ff.get("ms")},
            "persistence": "incremental columnar commit per step (db on local disk)" + (
                ", write-behind (persist_async: commits on a writer thread, flushed inside the timed region)"
                if persist_async else "")}
@@ -258,7 +280,8 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     _sync(dev)
     load_s = time.perf_counter() - t0
     t0 = time.perf_counter()
-    sm.cluster_pass()
+    with _ff_timer() as ff:
+        sm.cluster_pass()
     _sync(dev)
     seed_ms = (time.perf_counter() - t0) * 1e3
     rng = random.Random(seed + comm.rank)
@@ -307,7 +330,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
                    % cadence,
            "hierarchical_clustering": {"mode": "distributed kmeans", "every_steps": cluster_every, "fine": n_fine,
                                        "top": n_top, "iters_per_pass": cluster_iters,
-                                       "seed_pass_ms": round(seed_ms, 1)},
+                                       "seed_pass_ms": round(seed_ms, 1), "farthest_first_ms": ff.get("ms")},
            "load_s": round(load_s, 1), "stages_p50_ms": stages,
            "persistence": "incremental columnar commit of each rank's rows per step"}
     sm.close()

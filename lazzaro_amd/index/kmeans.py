@@ -18,6 +18,7 @@ import torch
 
 from ..ops import graph_ops as G
 from ..ops.search import flat_top1, flat_topk
+from ..utils.tracing import tracer
 
 
 # "top1": the 256x256 argmax kernel (flat_top1); "lane": flat_topk(k=1) on the 128x128 per-lane kernel
@@ -153,11 +154,24 @@ def assign_two_level(X: torch.Tensor, C16: torch.Tensor, T16: torch.Tensor, top_
 FF_KERNEL = os.environ.get("LZK_FF_KERNEL", "1") != "0"
 
 
-def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: int = 1 << 16,
+FF_SAMPLE = int(os.environ.get("LZK_FF_SAMPLE", str(1 << 15)))
+
+
+def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: Optional[int] = None,
                     rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Deterministic farthest-first seeding on a subsample (k-means++ without
     the sampling): avoids two seeds landing in one cluster. ``rows``: the
-    eligible row indices (default all)."""
+    eligible row indices (default all). ``max_sample`` (default
+    ``FF_SAMPLE`` = 32k rows, 8 per seed at k = 4096): every pick is one pass
+    over the sample, so the 4096 picks cost 4096 sample reads -- 64k rows
+    took 27 us per pick (111 ms per seeding, profiles/r4/bench_kernel_summary.txt)."""
+    if max_sample is None:
+        max_sample = FF_SAMPLE
+    with tracer.stage("ff_seed", X.device):
+        return _ff(X, k, seed, max_sample, rows)
+
+
+def _ff(X, k, seed, max_sample, rows):
     n = X.shape[0] if rows is None else rows.numel()
     g = torch.Generator(device="cpu").manual_seed(seed)
     sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
