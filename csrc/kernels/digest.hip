@@ -359,7 +359,8 @@ __global__ __launch_bounds__(DNT) void dg_round_kernel(const int* __restrict__ l
 // After a round: append each class-2 component's selected row (if any),
 // advance last[L], count it, retire the component (class 3) once it has
 // `take` rows, reset cur[L]; remaining[0] += components still open.
-__global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__ biglist, int nbig, int take,
+__global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__ biglist, int nbig,
+                                                         const int* __restrict__ nbig_dev, int take,
                                                          int* __restrict__ cur, int* __restrict__ last,
                                                          int* __restrict__ cnt, unsigned char* __restrict__ cls,
                                                          const long long* __restrict__ gfirst,
@@ -368,6 +369,7 @@ __global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__
                                                          int* __restrict__ remaining) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * DNT + threadIdx.x;
+  if (nbig_dev) nbig = *nbig_dev;  // sync-free mode: the classify pass's count, grid sized for the bound
   int L = -1, v = NOROW;
   bool open = false;
   if (i < nbig) {
@@ -440,24 +442,27 @@ LZK_EXPORT int lzk_dg_stats(const int* src, const int* dst, const float* w, long
 // window of the rows -- a large component's first candidates are nearly
 // always there -- then, only for components still open (one synchronising
 // read of `remaining`), `take` rounds over the rest.
+// nbig_dev (sync-free mode, small n): the class-2 count is read on the
+// device (counters + 1 of lzk_dg_stats); nbig is then its upper bound (the
+// collect grid), every round runs over all n rows and nothing is read back.
 LZK_EXPORT int lzk_dg_select(const int* lab, long n, const unsigned char* touched, const unsigned char* kind,
                              const unsigned char* sup, unsigned char* cls, const long long* gfirst,
-                             const int* biglist, int nbig, int take, int* cur, int* last, int* cnt,
-                             long long* out_key, int* out_row, int cap, int* count, int* remaining, long window,
-                             void* stream) {
+                             const int* biglist, int nbig, const int* nbig_dev, int take, int* cur, int* last,
+                             int* cnt, long long* out_key, int* out_row, int cap, int* count, int* remaining,
+                             long window, void* stream) {
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(dg_direct_kernel, dim3(grid_for(n)), dim3(DNT), 0, st, lab, touched, kind, sup, n, cls, gfirst,
                      out_key, out_row, cap, count);
   if (nbig <= 0) return (int)hipGetLastError();
-  const long w = window > 0 && window < n ? window : n;
+  const long w = (nbig_dev || window <= 0 || window >= n) ? n : window;
   const unsigned cb = (unsigned)((nbig + DNT - 1) / DNT);
   for (int k = 0; k < take; ++k) {
     hipLaunchKernelGGL(dg_round_kernel, dim3(grid_for(w)), dim3(DNT), 0, st, lab, touched, kind, sup, 0L, w, cls,
                        last, cur);
     (void)hipMemsetAsync(remaining, 0, sizeof(int), st);
-    hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, take, cur, last, cnt, cls,
-                       gfirst, out_key, out_row, cap, count, remaining);
+    hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, nbig_dev, take, cur, last, cnt,
+                       cls, gfirst, out_key, out_row, cap, count, remaining);
   }
   if (w >= n) return (int)hipGetLastError();
   int open = 0;
@@ -466,8 +471,8 @@ LZK_EXPORT int lzk_dg_select(const int* lab, long n, const unsigned char* touche
   for (int k = 0; k < take && open > 0; ++k) {
     hipLaunchKernelGGL(dg_round_kernel, dim3(grid_for(n - w)), dim3(DNT), 0, st, lab, touched, kind, sup, w, n, cls,
                        last, cur);
-    hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, take, cur, last, cnt, cls,
-                       gfirst, out_key, out_row, cap, count, remaining);
+    hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, nbig_dev, take, cur, last, cnt,
+                       cls, gfirst, out_key, out_row, cap, count, remaining);
   }
   return (int)hipGetLastError();
 }

@@ -20,11 +20,15 @@
 //    cut by the descriptor's record count (and masked in the epilogue).
 //  * The first K-tile of a tile feeds the MFMAs a literal zero accumulator,
 //    so nothing re-initialises the 128 accumulator registers.
-//  * The epilogue tests the int32 sums before converting any: per query
-//    column the max of its 32 sums (v_max3_i32) bounds every score of the
-//    column through the 128-row group's largest row scale and bias (staged
-//    with the tile's other epilogue operands), then per 16-row block; only a
-//    block that can hold a candidate converts its sums. It sits between two
+//  * The epilogue bounds the scores before converting them: per lane and
+//    16-row block i, the max of its 4 int32 sums times the largest row scale
+//    of those 4 rows (+ their largest bias) bounds all 4 scores (one
+//    {scale, bias} pair per 4-row quad, staged with the tile's other epilogue
+//    operands); a query column whose 8 block bounds all miss its threshold is
+//    skipped, and only a block whose bound clears it converts its sums. (A
+//    bound over the 128-row group's largest scale instead was ~35 % loose on
+//    unit rows: 98 % of the columns and half the blocks went through the
+//    per-score path at a store-search threshold.) It sits between two
 //    MFMA phases of the staggered wave groups, so one group's epilogue runs
 //    beside the other group's MFMAs on every SIMD.
 //
@@ -49,7 +53,8 @@ typedef __attribute__((address_space(3))) int lds_int;
 constexpr int NT = 512;
 constexpr int SLOT = 16384;                 // bytes: 128 rows x 128 B (one half-tile of one K-tile)
 constexpr int RING = 8 * SLOT;              // 2 K-tile buffers x {A0, A1, B0, B1}
-// epilogue operands per tile parity: thr | bias | rs | qs | thr2 | row label | query label | group stats
+// epilogue operands per tile parity: thr | bias | rs | qs | thr2 | row label | query label | quad stats
+// (quad stats: 64 x {max row scale, max bias} of the tile's 4-row quads)
 constexpr int NARR = 8;
 constexpr int EPI_BYTES = 2 * NARR * 256 * 4;
 // candidate records are staged in LDS per wave and written to the wave's
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
     for (int k = wave; k < 4 * NARR; k += 8) {
       const int a = k >> 2, c = k & 3;  // wave-uniform
       const bool need = a == 0 || (a == 1 && HAS_BIAS) || a == 2 || a == 3 || (DUAL && (a == 4 || a == 5 || a == 6)) ||
-                        (a == 7 && c == 0);
+                        (a == 7 && c < 2);
       if (!need) continue;
       const void* src;
       if (a == 0) src = thr + min(g.q0 + c * 64 + lane, nq - 1);
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
       else if (a == 4) src = thr2 + min(g.q0 + c * 64 + lane, nq - 1);
       else if (a == 5) src = row_label + min(g.r0 + c * 64 + lane, nrows - 1);
       else if (a == 6) src = q_label + min(g.q0 + c * 64 + lane, nq - 1);
-      else src = grp + min(2 * (g.r0 >> 7) + lane, 2 * ngrp - 1);  // {rsmax, bmax} of the tile's two row groups
+      else src = grp + min(2 * (g.r0 >> 2) + c * 64 + lane, 2 * ngrp - 1);  // {rs4, b4} of the tile's 64 quads
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(epi + (p * NARR + a) * 256 + c * 64), 4, 0, 0);
     }
   };
@@ -337,8 +342,7 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
     {
       const TileGeo g = geo(cur);
       const float* E = epi + (tix & 1) * (NARR * 256);
-      const float rsmax = E[7 * 256 + 2 * wr];
-      const float bmax = HAS_BIAS ? E[7 * 256 + 2 * wr + 1] : 0.f;
+      const float2* S4 = reinterpret_cast<const float2*>(E + 7 * 256) + wr * 32 + lq;  // quad (i, lq) at [4 i]
       const bool full = g.r0 + 256 <= nrows;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -349,24 +353,25 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
         const float tlo = DUAL ? fminf(th, th2) : th;
         const float tcut = tlo - 1e-6f * fabsf(tlo);  // slack: the per-score path may contract differently
         const float al = alpha * E[3 * 256 + qlo];
-        int m = acc[0][j][0];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          m = max(m, max(acc[i][j][0], acc[i][j][1]));
-          m = max(m, max(acc[i][j][2], acc[i][j][3]));
-        }
-        // every score of this lane's column in the wave's rows is <= bound;
-        // the skips are wave-uniform (ballots), so the append counter wpos
-        // stays uniform -- a lane that skipped would miss the counts
-        const float bound = (m > 0 ? al * ((float)m * rsmax) : 0.f) + bmax;
-        if (__ballot(bound >= tcut) == 0ull) continue;
-        const int qlab = DUAL ? reinterpret_cast<const int*>(E)[6 * 256 + qlo] : -1;
+        // bit i: the bound of the lane's 4 rows of block i clears tcut --
+        // every score there is <= al * max(m, 0) * rs4 + b4 (al >= 0)
+        unsigned pm = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const i32x4 v = acc[i][j];
           const int mi = max(max(v[0], v[1]), max(v[2], v[3]));
-          const float bi = (mi > 0 ? al * ((float)mi * rsmax) : 0.f) + bmax;
-          if (__ballot(bi >= tcut) == 0ull) continue;
+          const float2 s4 = S4[4 * i];
+          const float bnd = (mi > 0 ? al * ((float)mi * s4.x) : 0.f) + s4.y;
+          pm |= (bnd >= tcut ? 1u : 0u) << i;
+        }
+        // the skips are wave-uniform (ballots), so the append counter wpos
+        // stays uniform -- a lane that skipped would miss the counts
+        if (__ballot(pm != 0u) == 0ull) continue;
+        const int qlab = DUAL ? reinterpret_cast<const int*>(E)[6 * 256 + qlo] : -1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (__ballot((pm >> i) & 1u) == 0ull) continue;
+          const i32x4 v = acc[i][j];
           const int rl = wr * 128 + i * 16 + 4 * lq;
           const f32x4 rsv = *reinterpret_cast<const f32x4*>(E + 2 * 256 + rl);
           f32x4 bv = {0.f, 0.f, 0.f, 0.f};
@@ -395,28 +400,23 @@ __global__ __launch_bounds__(NT, 1) void scan8_kernel(
   if (lane == 0) rec.cnt[bid * 8 + wave] = wpos;  // > cap: records were dropped
 }
 
-// {max row scale, max bias} of every 128-row group (the epilogue's bounds).
+// {max row scale, max bias} of every 4-row quad (the epilogue's bounds).
 template <bool HAS_BIAS>
-__global__ __launch_bounds__(256) void group_stats_kernel(const float* __restrict__ rs, const float* __restrict__ bias,
-                                                          int nrows, int ngrp, float* __restrict__ grp) {
-  const int gi = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (gi >= ngrp) return;
-  float m = 0.f, bm = LZK_NEG_INF;
+__global__ __launch_bounds__(256) void quad_stats_kernel(const float* __restrict__ rs, const float* __restrict__ bias,
+                                                         int nrows, int nquad, float* __restrict__ q4) {
+  const int qi = blockIdx.x * 256 + threadIdx.x;
+  if (qi >= nquad) return;
+  float m = 0.f, bm = HAS_BIAS ? LZK_NEG_INF : 0.f;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int r = gi * 128 + h * 64 + lane;
+  for (int e = 0; e < 4; ++e) {
+    const int r = qi * 4 + e;
     if (r < nrows) {
       m = fmaxf(m, rs[r]);
-      bm = HAS_BIAS ? fmaxf(bm, bias[r]) : 0.f;
+      if (HAS_BIAS) bm = fmaxf(bm, bias[r]);
     }
   }
-  m = wave_max(m);
-  bm = wave_max(bm);
-  if (lane == 0) {
-    grp[2 * gi] = m;
-    grp[2 * gi + 1] = HAS_BIAS ? bm : 0.f;
-  }
+  q4[2 * qi] = m;
+  q4[2 * qi + 1] = bm;
 }
 
 int g_n_cu = 0;
@@ -559,7 +559,7 @@ LZK_EXPORT int lzk_scan8_grid(int nrows, int nq) {
 }
 
 // Bytes of the group-stats workspace lzk_scan8 needs.
-LZK_EXPORT long lzk_scan8_ws_bytes(int nrows) { return (long)((nrows + 127) / 128) * 8 + 256; }
+LZK_EXPORT long lzk_scan8_ws_bytes(int nrows) { return (long)((nrows + 3) / 4) * 8 + 256; }
 
 // int8 candidate scan (single list: thr2/labels null; dual: both lists, see
 // lzk_flat_cand_dual). X8 / Q8: int8 rows / queries with byte strides (16-B
@@ -583,12 +583,13 @@ LZK_EXPORT int lzk_scan8(const void* X8, long ldx, int nrows, const void* Q8, lo
   const long nblk = (long)n_rt * n_qt;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int ngrp = (nrows + 127) / 128;
+  const int ngrp = (nrows + 3) / 4;  // 4-row quads
   float* grp = (float*)ws;
   if (bias)
-    hipLaunchKernelGGL(group_stats_kernel<true>, dim3((ngrp + 3) / 4), dim3(256), 0, st, rscale, bias, nrows, ngrp, grp);
+    hipLaunchKernelGGL(quad_stats_kernel<true>, dim3((ngrp + 255) / 256), dim3(256), 0, st, rscale, bias, nrows, ngrp,
+                       grp);
   else
-    hipLaunchKernelGGL(group_stats_kernel<false>, dim3((ngrp + 3) / 4), dim3(256), 0, st, rscale, bias, nrows, ngrp,
+    hipLaunchKernelGGL(quad_stats_kernel<false>, dim3((ngrp + 255) / 256), dim3(256), 0, st, rscale, bias, nrows, ngrp,
                        grp);
   const int grid = lzk_scan8_grid(nrows, nq);
   const Recs rec{(int4*)blk_buf, blk_cap, blk_cnt};

@@ -541,6 +541,65 @@ __global__ __launch_bounds__(256) void tg_write_emb_kernel(
   }
 }
 
+// The first rows of the shard nodes in (shard code, row) order -- the rows
+// run_consolidation's profile prompt reads when no component qualifies
+// (reference memory_system.py:1003-1008, BufferGraph.nodes order) -- without
+// a host round trip: the host turns its per-shard live counts into targets
+// (code tc[t], rows wanted tt[t], output offset to[t]) and ONE block scans
+// the rows from 0 in chunks, appending each target's live rows in row order
+// (block-wide ranks from ballots) until every target is met -- usually
+// within the first chunk or two. out[] must be pre-filled with -1.
+constexpr int FR_NT = 1024;
+constexpr int FR_MAXT = 64;
+__global__ __launch_bounds__(FR_NT) void tg_first_rows_kernel(const unsigned char* __restrict__ kind,
+                                                              const unsigned char* __restrict__ sup,
+                                                              const int* __restrict__ shard, long n,
+                                                              const int* __restrict__ tc, const int* __restrict__ tt,
+                                                              const int* __restrict__ to, int nt,
+                                                              long* __restrict__ out) {
+  __shared__ int s_tc[FR_MAXT], s_tt[FR_MAXT], s_to[FR_MAXT], s_found[FR_MAXT];
+  __shared__ int s_w[FR_NT / 64];
+  __shared__ int s_open;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int t = threadIdx.x; t < nt; t += FR_NT) {
+    s_tc[t] = tc[t];
+    s_tt[t] = tt[t];
+    s_to[t] = to[t];
+    s_found[t] = 0;
+  }
+  __syncthreads();
+  for (long base = 0; base < n; base += FR_NT) {
+    const long r = base + threadIdx.x;
+    const int c = (r < n && kind[r] == 1 && sup[r] == 0) ? shard[r] : -1;
+    int j = -1;
+    for (int t = 0; t < nt; ++t) j = (s_tc[t] == c) ? t : j;
+    for (int t = 0; t < nt; ++t) {
+      const int have = s_found[t], want = s_tt[t];  // block-uniform
+      if (have >= want) continue;
+      const unsigned long long b = __ballot(j == t);
+      if (lane == 0) s_w[wv] = __popcll(b);
+      __syncthreads();
+      int before = 0, total = 0;
+      for (int w = 0; w < FR_NT / 64; ++w) {
+        before += w < wv ? s_w[w] : 0;
+        total += s_w[w];
+      }
+      const int rank = have + before + (int)__popcll(b & ((1ull << lane) - 1));
+      if (j == t && rank < want) out[s_to[t] + rank] = r;
+      __syncthreads();  // every lane read s_found[t] / s_w
+      if (threadIdx.x == 0) s_found[t] = min(want, have + total);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      int open = 0;
+      for (int t = 0; t < nt; ++t) open |= s_found[t] < s_tt[t];
+      s_open = open;
+    }
+    __syncthreads();
+    if (!s_open) break;
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- C ABI
@@ -702,5 +761,16 @@ LZK_EXPORT int lzk_cos_rerank64(const double* Qn, long ldq, const float* X, long
   if (C <= 0 || C > 64 || k <= 0 || k > C || D <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(cos_rerank64_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Qn, ldq,
                      X, ldx, D, sqn, cand, C, M, k, os, oi);
+  return (int)hipGetLastError();
+}
+
+// First shard-node rows (tg_first_rows_kernel): nt <= 64 targets, out[sum tt]
+// pre-filled with -1 by the caller. One block, no host synchronisation.
+LZK_EXPORT int lzk_tg_first_rows(const unsigned char* kind, const unsigned char* sup, const int* shard, long n,
+                                 const int* tc, const int* tt, const int* to, int nt, long* out, void* stream) {
+  if (nt <= 0) return 0;
+  if (nt > FR_MAXT || n < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tg_first_rows_kernel, dim3(1), dim3(FR_NT), 0, (hipStream_t)stream, kind, sup, shard, n, tc, tt,
+                     to, nt, out);
   return (int)hipGetLastError();
 }

@@ -838,6 +838,12 @@ class ConsolidationMixin:
         fact_of = {int(k): int(j) for j, k in enumerate(fact_key.tolist()) if k >= 0}
         id_of = {}
         count0 = self.conversation_count
+        # run_consolidation's profile prompts wait for the end of the batch
+        # (graph reads captured at each point, no host wait in the loop) unless
+        # every conversation is committed on its own, or a super-node of the
+        # batch could re-use a row id (its row's content would change)
+        defer = not self._commit_each and self._supers_fresh(pl, now)
+        pending = []
         for seg in pl["segments"]:
             # node ids as the segment's facts are inserted (keys grow segment by
             # segment): a per-segment commit persists the sequential counter
@@ -851,14 +857,34 @@ class ConsolidationMixin:
             if seg["consolidate"]:
                 stats["consolidations"] += 1
                 with tracer.stage("run_consolidation", self._device):
-                    self.run_consolidation(prune=not self.auto_prune)
+                    if defer:
+                        pending.append(self._rc_device(prune=not self.auto_prune))
+                    else:
+                        self.run_consolidation(prune=not self.auto_prune)
             if seg["cluster"]:
                 self._maybe_cluster(self.conversation_count - 1)
             if self._commit_each:
                 with tracer.stage("commit", "cpu"):
                     self._save_to_persistence()
+        if pending:
+            with tracer.stage("rc_deferred", "cpu"):
+                for cap in pending:
+                    self._rc_host(cap)
         if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
             self._maybe_cluster(self.conversation_count - 1)
+
+    def _supers_fresh(self, pl: Dict, now: float) -> bool:
+        """No super-node of the plan re-uses an id (the id is
+        ``super_<shard>_<int(now)>``): a re-used id rewrites its row's content,
+        which a deferred profile prompt of an earlier point would read."""
+        g = self.graph
+        seen = set()
+        for sp in pl["supers"]:
+            sid = f"super_{shard_keys_of(g, int(sp['code']))}_{int(now)}"
+            if sid in seen or sid in g.row_of:
+                return False
+            seen.add(sid)
+        return True
 
     def _super_codes(self) -> List[int]:
         g = self.graph
@@ -1242,7 +1268,19 @@ class ConsolidationMixin:
         whose segment just pruned every decayed old edge (segment_end) and
         whose planner drops new links at each decay (batch_plan end_decay);
         weights only fall by decay, so the reference's prune here finds
-        nothing."""
+        nothing. The graph work (:meth:`_rc_device`) and the profile prompts
+        it feeds (:meth:`_rc_host`) are split so that consolidate_batch can
+        read the graph at every consolidation point without waiting for the
+        device and run the prompts, in order, at the end of the batch."""
+        return self._rc_host(self._rc_device(merge_similar, prune))
+
+    def _rc_device(self, merge_similar: bool = True, prune: bool = True) -> Dict:
+        """The graph side of run_consolidation at this moment: merge (a no-op
+        in the reference's merge mode), the component digest, the prune and
+        the first shard rows -- the latter two as captures (the rows are read
+        on the host in :meth:`_rc_host`). The first rows do not depend on the
+        edges, so reading them after the prune matches the reference, which
+        reads them after its profile prompts and prune (:1003-1008)."""
         results = []
         self._say("🔄 Running consolidation...")
         g = self.graph
@@ -1255,27 +1293,32 @@ class ConsolidationMixin:
             with tracer.stage("components", self._device):
                 # components with >= 3 members and mean edge weight > 0.3
                 # (reference :967-990), as their first 10 shard-node rows
-                digest = g.component_digest(3, 0.3, PROFILE_CONTENTS)
-            contents = [[g.content[r] for r in rows.tolist()] for rows in digest]
+                digest = g.digest_capture(3, 0.3, PROFILE_CONTENTS)
+            pruned = 0
+            if prune:
+                with tracer.stage("rc_prune", self._device):
+                    pruned = g.prune(self.prune_threshold)
+            with tracer.stage("rc_first_rows", self._device):
+                first = g.first_rows_capture(PROFILE_CONTENTS)
+        return {"results": results, "digest": digest, "pruned": pruned, "first": first}
+
+    def _rc_host(self, cap: Dict) -> str:
+        """The profile prompts of one :meth:`_rc_device` capture."""
+        results = cap["results"]
+        g = self.graph
         updates = 0
         with tracer.stage("rc_profile", "cpu"):
-            for cs in contents:
-                r = self._extract_profile_from_contents(cs)
+            for rows in cap["digest"].get():
+                r = self._extract_profile_from_contents([g.content[x] for x in rows.tolist()])
                 if "Updated" in r:
                     updates += 1
                     results.append(r)
-        pruned = 0
-        if prune:
-            with self._graph_lock, tracer.stage("rc_prune", self._device):
-                pruned = g.prune(self.prune_threshold)
-        if pruned > 0:
-            results.append(f"✓ Pruned {pruned} weak edges")
+        if cap["pruned"] > 0:
+            results.append(f"✓ Pruned {cap['pruned']} weak edges")
         if updates > 0:
             results.append(f"✓ Updated {updates} profile domains")
         else:
-            with self._graph_lock, tracer.stage("rc_first_rows", self._device):
-                rows = g.first_node_rows_dev(PROFILE_CONTENTS, super_=False)
-                contents = [g.content[r] for r in rows.tolist()]
+            contents = [g.content[r] for r in cap["first"].get().tolist()]
             if len(contents) >= 3:
                 r = self._extract_profile_from_contents(contents)
                 if "Updated" in r:

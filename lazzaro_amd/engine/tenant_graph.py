@@ -190,6 +190,33 @@ def _host_ints(v, m: int, default: int) -> Optional[np.ndarray]:
     return np.broadcast_to(a, (m,)) if a.size == 1 else a
 
 
+class Capture:
+    """A result of device work read on the host later: the device tensor is
+    copied into pinned memory on the graph's stream right away (no host
+    wait), and :meth:`get` waits for that copy only when the value is needed
+    -- consolidate_batch keeps its segment loop free of host
+    synchronisations and reads every run_consolidation digest at the end of
+    the batch. ``host``: an already-known host value."""
+
+    __slots__ = ("_h", "_ev", "_fn", "_val")
+
+    def __init__(self, dev_t: Optional[torch.Tensor] = None, fn=None, host=None):
+        self._fn, self._val, self._h, self._ev = fn, host, None, None
+        if dev_t is not None:
+            self._h = torch.empty(tuple(dev_t.shape), dtype=dev_t.dtype, pin_memory=True)
+            self._h.copy_(dev_t, non_blocking=True)
+            self._ev = torch.cuda.Event()
+            self._ev.record()
+
+    def get(self):
+        if self._h is not None:
+            self._ev.synchronize()
+            a = self._h.numpy()
+            self._val = self._fn(a) if self._fn is not None else a
+            self._h = self._ev = None
+        return self._val
+
+
 class TenantGraph:
     NODE_COLS = (("sal", torch.float32, 0.0), ("acc", torch.int32, 0), ("last", torch.float64, 0.0),
                  ("ts", torch.float64, 0.0), ("shard", torch.int32, -1), ("kind", torch.uint8, FREE),
@@ -866,6 +893,10 @@ class TenantGraph:
         rows found in growing windows from row 0 -- the answer is almost
         always in the first window (no pass over the whole tenant)."""
         n = self.n
+        if super_ is False and k > 0 and self.on_gpu:
+            t = self._first_rows_dev(k)
+            if t is not None:
+                return t
         if super_ is False and n > self.FIRST_ROWS_WINDOW and k > 0:
             return self._first_shard_rows(k)
         with self.on_stream():
@@ -882,6 +913,41 @@ class TenantGraph:
             return i
 
     FIRST_ROWS_WINDOW = 1 << 16
+
+    def _first_rows_dev(self, k: int) -> Optional[torch.Tensor]:
+        """:meth:`first_node_rows_dev` (shard nodes) by tenant.hip
+        tg_first_rows_kernel: the per-shard targets come from the host shard
+        counts, one block scans the rows from 0 -- no host synchronisation.
+        None when there are more than 64 target shards."""
+        tgt, need, off = [], k, 0
+        for c, cnt in enumerate(self.shard_count):
+            if cnt <= 0 or need == 0:
+                continue
+            t = min(int(cnt), need)
+            tgt.append((c, t, off))
+            off += t
+            need -= t
+        dev = self.device
+        if not tgt:
+            return torch.zeros(0, dtype=torch.long, device=dev)
+        if len(tgt) > 64:
+            return None
+        with self.on_stream():
+            tv = T.to_dev_packed([np.asarray(x) for x in zip(*tgt)], dev)
+            ti = torch.stack(tv).to(torch.int32)
+            out = torch.full((off,), -1, dtype=torch.long, device=dev)
+            T.first_rows(self.kind, self.sup, self.shard, self.n, ti, out)
+        return out
+
+    def first_rows_capture(self, k: int) -> Capture:
+        """The shard-node rows of :meth:`first_node_rows_dev` as a
+        :class:`Capture` (no host wait on the GPU)."""
+        if self.on_gpu and k > 0:
+            t = self._first_rows_dev(k)
+            if t is not None:
+                with self.on_stream():
+                    return Capture(t, fn=lambda a: a[a >= 0])
+        return Capture(host=self.first_node_rows_dev(k, super_=False).cpu().numpy())
 
     def _first_shard_rows(self, k: int) -> torch.Tensor:
         n = self.n
@@ -1503,6 +1569,9 @@ class TenantGraph:
         if n == 0 or self.num_edges == 0:
             return []
         dev = self.device
+        if self._digest_local(min_size, take):
+            with self.on_stream():
+                return T.digest_lists(self._digest_local_dev(min_size, min_avg_w, take).cpu().numpy())
         if dev.type == "cuda" and min_size >= 2 and take >= 1 and not self._digest_sorted:
             self._maybe_sort_edges()
             with self.on_stream():
@@ -1572,6 +1641,27 @@ class TenantGraph:
             rows_h, key_h = rowsv[o].cpu().numpy(), key[o].cpu().numpy()
         cut = np.nonzero(np.diff(key_h))[0] + 1
         return np.split(rows_h, cut)
+
+    # the O(edges) digest when the edges touch at most 1/DIGEST_LOCAL_FRAC of the rows
+    DIGEST_LOCAL_FRAC = 8
+
+    def _digest_local(self, min_size: int, take: int) -> bool:
+        return (self.on_gpu and min_size >= 2 and take >= 1 and not self._digest_sorted and self.num_edges > 0
+                and 2 * self.num_edges * self.DIGEST_LOCAL_FRAC <= self.n)
+
+    def _digest_local_dev(self, min_size: int, min_avg_w: float, take: int) -> torch.Tensor:
+        n = self.n
+        return T.component_digest_local(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n], self.sup[:n],
+                                        self.shard[:n], min_size, min_avg_w, take)
+
+    def digest_capture(self, min_size: int = 3, min_avg_w: float = 0.3, take: int = 10) -> Capture:
+        """:meth:`component_digest` as a :class:`Capture`: on the GPU with
+        few edges (the O(edges) digest, ops.tenant_ops.component_digest_local)
+        nothing waits for the device; otherwise the lists are computed now."""
+        if self.n and self._digest_local(min_size, take):
+            with self.on_stream():
+                return Capture(self._digest_local_dev(min_size, min_avg_w, take), fn=T.digest_lists)
+        return Capture(host=self.component_digest(min_size, min_avg_w, take))
 
     def component_edge_stats(self, comps: List[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
         """(sum of weights, count) of edges with both endpoints in the same

@@ -35,7 +35,8 @@ _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 _lib.register("lzk_pack_bits", I, [P, L, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, P, P, P, P, P, P, P])
-_lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, I, P, P, P, P, P, I, P, P, L, P])
+_lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P, P, L, P])
+_lib.register("lzk_tg_first_rows", I, [P, P, P, L, P, P, P, I, P, P])
 
 SALIENCE_FLOOR = 0.2
 EDGE_COLS = ("src", "dst", "w", "co", "lu", "meta")
@@ -420,7 +421,7 @@ def component_digest(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind
         cur = last = cnt = torch.empty(1, dtype=torch.int32, device=dev)
     rem = torch.zeros(1, dtype=torch.int32, device=dev)
     _lib.check(L_.lzk_dg_select(lab.data_ptr(), n, touched.data_ptr(), kind.data_ptr(), sup.data_ptr(),
-                                cls.data_ptr(), gfirst.data_ptr(), biglist.data_ptr(), nbig, int(take),
+                                cls.data_ptr(), gfirst.data_ptr(), biglist.data_ptr(), nbig, None, int(take),
                                 cur.data_ptr(), last.data_ptr(), cnt.data_ptr(), keys.data_ptr(), rows.data_ptr(),
                                 cap, counters[3:].data_ptr(), rem.data_ptr(), int(DIGEST_WINDOW), _st(src)),
                "dg_select")
@@ -434,6 +435,107 @@ def component_digest(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind
         o = torch.argsort(rows, stable=True)
         o = o[torch.argsort(keys[o], stable=True)]
     return keys[o], rows[o]
+
+
+def component_digest_local(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind: torch.Tensor,
+                           sup: torch.Tensor, shard: torch.Tensor, min_size: int, min_avg_w: float,
+                           take: int) -> torch.Tensor:
+    """:func:`component_digest` in O(edges) and without a host
+    synchronisation, for graphs whose edges touch few of the tenant's rows
+    (the consolidation buffer at the reference's prune threshold keeps a few
+    thousand edges over 10M rows): the edge endpoints are renumbered 0 .. U-1
+    in row order (one sort of the 2E endpoints; the index space is padded to
+    2E, the padding rows FREE and untouched), the digest kernels run over that
+    space -- the renumbering is monotone, so the row order and the order of
+    the components' first-member keys are the tenant's -- and the result
+    stays on the device, sized by the bound instead of a read-back count:
+    int64 [2, 2E] = (order key, tenant row) sorted by (key, row), the unused
+    tail (key 1 << 62, row -1) last. The caller copies it to the host when
+    it needs the rows (:class:`TenantGraph.DigestCapture`)."""
+    assert src.is_cuda and min_size >= 2 and take >= 1
+    dev = src.device
+    E = int(src.numel())
+    nl = 2 * E
+    BIG = 1 << 62
+    if E == 0:
+        return torch.stack([torch.full((0,), BIG, dtype=torch.int64, device=dev),
+                            torch.full((0,), -1, dtype=torch.int64, device=dev)])
+    ep = torch.cat([src, dst]).long()
+    srt, perm = torch.sort(ep)
+    newf = torch.ones(nl, dtype=torch.bool, device=dev)
+    newf[1:] = srt[1:] != srt[:-1]
+    uid = torch.cumsum(newf, 0, dtype=torch.int64) - 1
+    local = torch.empty(nl, dtype=torch.int32, device=dev)
+    local[perm] = uid.to(torch.int32)
+    rowmap = torch.full((nl,), -1, dtype=torch.int64, device=dev)
+    rowmap[uid] = srt
+    valid = rowmap >= 0
+    rc = rowmap.clamp_min(0)
+    kind_l = torch.where(valid, kind[rc], torch.zeros((), dtype=kind.dtype, device=dev)).contiguous()
+    sup_l, shard_l = sup[rc].contiguous(), shard[rc].contiguous()
+    lsrc, ldst = local[:E].contiguous(), local[E:].contiguous()
+    lab = components(lsrc, ldst, nl)
+    touched = torch.zeros(nl, dtype=torch.uint8, device=dev)
+    gsum = torch.zeros(nl, dtype=torch.float64, device=dev)
+    gi = torch.zeros((3, nl), dtype=torch.int32, device=dev)
+    gfirst = torch.full((nl,), BIG, dtype=torch.int64, device=dev)
+    cls = torch.empty(nl, dtype=torch.uint8, device=dev)
+    nbig_max = nl // (take + 1) + 1
+    biglist = torch.empty(nbig_max, dtype=torch.int32, device=dev)
+    counters = torch.zeros(4, dtype=torch.int32, device=dev)
+    w = w.to(torch.float32).contiguous()
+    L_ = _lib.lib()
+    _lib.check(L_.lzk_dg_stats(lsrc.data_ptr(), ldst.data_ptr(), w.data_ptr(), E, lab.data_ptr(), nl,
+                               kind_l.data_ptr(), sup_l.data_ptr(), shard_l.data_ptr(), int(min_size),
+                               float(min_avg_w), int(take), touched.data_ptr(), gsum.data_ptr(), gi[0].data_ptr(),
+                               gi[1].data_ptr(), gi[2].data_ptr(), gfirst.data_ptr(), cls.data_ptr(),
+                               biglist.data_ptr(), counters.data_ptr(), _st(lsrc)), "dg_stats")
+    # selection by one sort over the (small) index space instead of the
+    # rounds of dg_select: candidates of qualifying components (cls 1 / 2)
+    # grouped by label in row order, the first `take` of each group kept
+    MAXI = torch.iinfo(torch.int64).max
+    idx = torch.arange(nl, device=dev)
+    labl = lab.long()
+    cand = (touched != 0) & (kind_l == 1) & (sup_l == 0) & (cls != 0)
+    o1 = torch.sort(torch.where(cand, labl * (nl + 1) + idx, torch.full_like(idx, MAXI))).indices
+    lab_s, cand_s = labl[o1], cand[o1]
+    newg = torch.ones(nl, dtype=torch.bool, device=dev)
+    newg[1:] = lab_s[1:] != lab_s[:-1]
+    gstart = torch.cummax(torch.where(newg, idx, torch.zeros_like(idx)), 0).values
+    sel = cand_s & ((idx - gstart) < take)
+    key_s = gfirst[lab_s]
+    # (key, row): keys are < (shard codes + 2) * nl, so key * (nl + 1) + row fits
+    comb = torch.where(sel, key_s * (nl + 1) + o1, torch.full_like(o1, MAXI))
+    c2, o2 = torch.sort(comb)
+    ok = c2 != MAXI
+    ks = torch.where(ok, key_s[o2], torch.full_like(c2, BIG))
+    grow = torch.where(ok, rowmap[o1[o2]], torch.full_like(c2, -1))
+    return torch.stack([ks, grow])
+
+
+def first_rows(kind: torch.Tensor, sup: torch.Tensor, shard: torch.Tensor, n: int, tgt: torch.Tensor,
+               out: torch.Tensor) -> None:
+    """tenant.hip tg_first_rows_kernel: ``tgt`` int32 [3, nt] device (shard
+    code, rows wanted, output offset) per target shard in code order; ``out``
+    int64 [sum wanted] pre-filled with -1 receives each target's first live
+    shard-node rows in row order."""
+    nt = int(tgt.shape[1])
+    if nt == 0:
+        return
+    tgt = tgt.contiguous()
+    _lib.check(_lib.lib().lzk_tg_first_rows(kind.data_ptr(), sup.data_ptr(), shard.data_ptr(), int(n),
+                                            tgt[0].data_ptr(), tgt[1].data_ptr(), tgt[2].data_ptr(), nt,
+                                            out.data_ptr(), _st(out)), "tg_first_rows")
+
+
+def digest_lists(kr: np.ndarray) -> List[np.ndarray]:
+    """Host form of a digest: int64 [2, m] (key, row) sorted by (key, row),
+    unused entries (row -1) last -> one row array per component."""
+    ok = kr[1] >= 0
+    key_h, rows_h = kr[0][ok], kr[1][ok]
+    if rows_h.size == 0:
+        return []
+    return np.split(rows_h, np.nonzero(np.diff(key_h))[0] + 1)
 
 
 def components(src: torch.Tensor, dst: torch.Tensor, n: int) -> torch.Tensor:

@@ -59,3 +59,45 @@ def test_digest_kernels_match_sorted(n, ne, n_small, seed, window, monkeypatch):
         g._digest_sorted = False
         assert got == want and len(want) > 10
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_local_digest_matches_sorted(seed):
+    """The O(edges), sync-free digest (ops.tenant_ops.component_digest_local:
+    endpoint renumbering, used when the edges touch few rows) against the
+    sorted formulation, and its Capture form."""
+    g = _graph(200000, 600, 1200, seed)  # a small 'giant' + chains over a 200k-row tenant
+    assert g._digest_local(3, 10)
+    for take in (10, 3):
+        got = [r.tolist() for r in g.component_digest(3, 0.3, take)]
+        cap = [r.tolist() for r in g.digest_capture(3, 0.3, take).get()]
+        g._digest_sorted = True
+        want = [r.tolist() for r in g.component_digest(3, 0.3, take)]
+        g._digest_sorted = False
+        assert got == want == cap and len(want) > 10
+
+
+def test_first_rows_kernel_matches_topk():
+    """tenant.hip tg_first_rows_kernel (first shard-node rows in (shard,
+    row) order from the host shard counts) against the top-k formulation on
+    the CPU copy of the same tenant, after removals, with super-nodes."""
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    rng = np.random.default_rng(7)
+    n = 300000
+    gs = []
+    for dev in ("cpu", "cuda"):
+        g = TenantGraph(device=dev, dim=4)
+        codes = [g.shard_id(f"s{i}") for i in range(5)]
+        r2 = np.random.default_rng(7)
+        sh = r2.choice([codes[1], codes[3], codes[4]], n, p=[0.0001, 0.5, 0.4999]).tolist()
+        g.add_nodes([f"node_{i}" for i in range(n)], [f"c{i}" for i in range(n)],
+                    r2.standard_normal((n, 4)).astype(np.float32).tolist(), shard=sh,
+                    sup=(r2.random(n) < 0.05).astype(np.int64).tolist())
+        g.remove_nodes(np.random.default_rng(8).choice(n, 40000, replace=False).tolist())
+        gs.append(g)
+    cpu, gpu = gs
+    cpu.FIRST_ROWS_WINDOW = 1 << 30  # the one-pass top-k
+    for k in (1, 10, 40, 200):
+        ref = cpu.first_node_rows_dev(k, super_=False).tolist()
+        assert gpu.first_node_rows_dev(k, super_=False).tolist() == ref and len(ref) == k
+        assert gpu.first_rows_capture(k).get().tolist() == ref
