@@ -173,6 +173,11 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    tprof = None
+    if os.environ.get("LZK_PROF_OPS") == "1":  # aten ops per Python call site of the timed steps (stderr)
+        from torch.profiler import ProfilerActivity, profile
+        tprof = profile(activities=[ProfilerActivity.CPU], with_stack=True)
+        tprof.__enter__()
     t0 = time.perf_counter()
     agg = {}
     for _ in range(steps):
@@ -180,6 +185,18 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
             agg[k] = agg.get(k, 0) + v
     ms.flush_persistence()  # write-behind commits of the timed steps land inside the timed region
     _sync(dev)
+    if tprof is not None:
+        tprof.__exit__(None, None, None)
+        ka = tprof.key_averages(group_by_stack_n=3)
+        rows = sorted(ka, key=lambda e: -e.count)
+        print(f"# aten ops over {steps} steps: {sum(e.count for e in ka if e.key.startswith('aten::'))}",
+              file=sys.stderr)
+        for e in rows[:120]:
+            if not e.key.startswith("aten::") and not e.key.startswith("cuda"):
+                continue
+            st = " <- ".join(x.split("/")[-1] for x in (e.stack or [])[:3])
+            print(f"{e.count / steps:8.1f}/step  {e.self_cpu_time_total / steps / 1e3:8.2f} ms  {e.key:32s} {st}",
+                  file=sys.stderr)
     if prof is not None:
         import pstats
         prof.disable()

@@ -401,6 +401,221 @@ __global__ __launch_bounds__(DNT) void dg_collect_kernel(const int* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- small graphs
+// The whole digest of a graph with at most SD_MAXE edges in ONE block: the
+// consolidation buffer at the reference's prune threshold keeps a few
+// hundred to a few thousand edges over millions of rows, and consolidate_batch
+// reads the digest at ~40 points per step -- a chain of tenant-wide passes
+// (or of torch ops over a renumbered index space) costs more in launches
+// than the work. Endpoints are sorted (bitonic, LDS) and renumbered to local
+// ids u (row order), union-find runs on LDS parents (hook the larger root
+// under the smaller: a component's root is its smallest row), the
+// per-component reductions go to a small global scratch, `take` selection
+// rounds pick each component's first candidate rows, and the (order key,
+// row) output is sorted by one more bitonic pass. Same definitions as the
+// kernels above (members: touched rows not free; candidates: live shard
+// nodes; order key over live nodes with the tenant's n and rows); outputs
+// out[0][i] = key, out[1][i] = row for i < count, then (1 << 62, -1).
+constexpr int SD_NT = 1024;
+constexpr int SD_MAXE = 2048;
+constexpr int SD_P = 2 * SD_MAXE;
+
+__device__ __forceinline__ int sd_find(volatile int* par, int x) {
+  while (true) {
+    const int p = par[x];
+    if (p == x) return x;
+    x = p;
+  }
+}
+
+__device__ __forceinline__ int sd_bsearch(const int* a, int n, int v) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+struct SdScratch {  // per local label, in global memory (L2-resident, zeroed here)
+  double* wsum;
+  int* ecnt;
+  int* size;
+  int* ccnt;
+  long long* first;
+  int* cur;
+  int* last;
+  int* taken;
+};
+
+__global__ __launch_bounds__(SD_NT) void dg_small_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                         const float* __restrict__ w, int ne,
+                                                         const unsigned char* __restrict__ kind,
+                                                         const unsigned char* __restrict__ sup,
+                                                         const int* __restrict__ shard, long n, int min_size,
+                                                         double min_avg_w, int take, SdScratch S,
+                                                         long long* __restrict__ out, int cap,
+                                                         int* __restrict__ out_cnt) {
+  __shared__ int ep[SD_P];       // sorted endpoints, then unique rows (urow)
+  __shared__ int par[SD_P];      // union-find parents over local ids
+  __shared__ long long sk[SD_P];  // output sort: keys
+  __shared__ int su[SD_P];        // output sort: local ids
+  __shared__ int s_scan[SD_NT / 64];
+  __shared__ int s_U, s_cnt, s_open;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int P = 2;
+  while (P < 2 * ne) P <<= 1;
+  for (int i = tid; i < P; i += SD_NT) ep[i] = i < ne ? src[i] : (i < 2 * ne ? dst[i - ne] : 0x7fffffff);
+  __syncthreads();
+  // bitonic sort of the endpoints (ascending)
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += SD_NT) {
+        const int l = i ^ j;
+        if (l > i) {
+          const int a = ep[i], b = ep[l];
+          if (((i & k) == 0) == (a > b)) { ep[i] = b; ep[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  // unique -> urow[0 .. U) (in place: a block scan of the first-occurrence
+  // flags, values read before the barrier, written after)
+  int base = 0;
+  for (int c0 = 0; c0 < P; c0 += SD_NT) {
+    const int i = c0 + tid;
+    int v = 0x7fffffff;
+    bool f = false;
+    if (i < P) {
+      v = ep[i];
+      f = v != 0x7fffffff && (i == 0 || ep[i - 1] != v);
+    }
+    const unsigned long long b = __ballot(f);
+    if (lane == 0) s_scan[wv] = __popcll(b);
+    __syncthreads();
+    int before = 0, tot = 0;
+    for (int x = 0; x < SD_NT / 64; ++x) {
+      before += x < wv ? s_scan[x] : 0;
+      tot += s_scan[x];
+    }
+    __syncthreads();
+    if (f) ep[base + before + __popcll(b & ((1ull << lane) - 1))] = v;
+    base += tot;
+    __syncthreads();
+  }
+  const int U = base;
+  for (int u = tid; u < P; u += SD_NT) {
+    par[u] = u;
+    if (u < U) {
+      S.wsum[u] = 0.0;
+      S.ecnt[u] = 0;
+      S.size[u] = 0;
+      S.ccnt[u] = 0;
+      S.first[u] = BIGKEY;
+      S.cur[u] = NOROW;
+      S.last[u] = -1;
+      S.taken[u] = 0;
+    }
+  }
+  if (tid == 0) { s_U = U; s_cnt = 0; }
+  __syncthreads();
+  // union-find: hook the larger root under the smaller
+  for (int e = tid; e < ne; e += SD_NT) {
+    int a = sd_bsearch(ep, U, src[e]), b = sd_bsearch(ep, U, dst[e]);
+    while (true) {
+      a = sd_find(par, a);
+      b = sd_find(par, b);
+      if (a == b) break;
+      if (a > b) { const int t = a; a = b; b = t; }
+      const int old = atomicCAS(&par[b], b, a);
+      if (old == b) break;
+      b = old;
+    }
+  }
+  __syncthreads();
+  for (int u = tid; u < U; u += SD_NT) par[u] = sd_find(par, u);
+  __syncthreads();
+  __threadfence_block();
+  // per-component reductions
+  for (int e = tid; e < ne; e += SD_NT) {
+    const int L = par[sd_bsearch(ep, U, src[e])];
+    atomicAdd(S.wsum + L, (double)w[e]);
+    atomicAdd(S.ecnt + L, 1);
+  }
+  for (int u = tid; u < U; u += SD_NT) {
+    const int r = ep[u];
+    const unsigned char k = kind[r];
+    if (k == 0) continue;
+    const int L = par[u];
+    atomicAdd(S.size + L, 1);
+    if (k == 1) {
+      const bool s = sup[r] != 0;
+      if (!s) atomicAdd(S.ccnt + L, 1);
+      atomicMin(S.first + L, (s ? 0LL : (long long)shard[r] + 1) * (long long)n + r);
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // selection: `take` rounds of "smallest candidate above the last one taken"
+  for (int round = 0; round < take; ++round) {
+    for (int u = tid; u < U; u += SD_NT) {
+      const int r = ep[u];
+      if (kind[r] != 1 || sup[r] != 0) continue;
+      const int L = par[u];
+      const int ec = S.ecnt[L];
+      if (S.size[L] < min_size || ec <= 0 || S.ccnt[L] <= 0 || S.first[L] >= BIGKEY ||
+          !(S.wsum[L] / (double)ec > min_avg_w) || S.taken[L] >= take || u <= S.last[L])
+        continue;
+      atomicMin(S.cur + L, u);
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_open = 0;
+    __syncthreads();
+    for (int u = tid; u < U; u += SD_NT) {
+      if (par[u] != u) continue;  // component roots
+      const int c = S.cur[u];
+      if (c == NOROW) continue;
+      S.cur[u] = NOROW;
+      S.last[u] = c;
+      S.taken[u] += 1;
+      const int at = atomicAdd(&s_cnt, 1);
+      sk[at] = S.first[u];
+      su[at] = c;
+      s_open = 1;
+    }
+    __threadfence();
+    __syncthreads();
+    if (!s_open) break;
+  }
+  const int m = s_cnt;
+  int Q = 2;
+  while (Q < m) Q <<= 1;
+  for (int i = m + tid; i < Q; i += SD_NT) { sk[i] = BIGKEY; su[i] = 0x7fffffff; }
+  __syncthreads();
+  // (key, local id) ascending = (key, row)
+  for (int k = 2; k <= Q; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < Q; i += SD_NT) {
+        const int l = i ^ j;
+        if (l > i) {
+          const long long ka = sk[i], kb = sk[l];
+          const int ua = su[i], ub = su[l];
+          const bool gt = ka > kb || (ka == kb && ua > ub);
+          if (((i & k) == 0) == gt) { sk[i] = kb; sk[l] = ka; su[i] = ub; su[l] = ua; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < cap; i += SD_NT) {
+    const bool ok = i < m;
+    out[i] = ok ? sk[i] : BIGKEY;
+    out[cap + i] = ok ? (long long)ep[su[i]] : -1LL;
+  }
+  if (tid == 0) *out_cnt = m;
+}
+
 inline unsigned grid_for(long n, unsigned cap = 4096) {
   const long b = (n + DNT - 1) / DNT;
   return (unsigned)(b < 1 ? 1 : (b > cap ? cap : b));
@@ -474,5 +689,31 @@ LZK_EXPORT int lzk_dg_select(const int* lab, long n, const unsigned char* touche
     hipLaunchKernelGGL(dg_collect_kernel, dim3(cb), dim3(DNT), 0, st, biglist, nbig, nbig_dev, take, cur, last, cnt,
                        cls, gfirst, out_key, out_row, cap, count, remaining);
   }
+  return (int)hipGetLastError();
+}
+
+// One-block digest of a graph with ne <= 2048 edges (dg_small_kernel): out
+// int64 [2][cap] (cap >= 2 ne; key row pairs sorted, unused key 1 << 62 /
+// row -1), out_cnt int [1]; ws >= lzk_dg_small_ws(ne) bytes. No host
+// synchronisation.
+LZK_EXPORT long lzk_dg_small_ws(int ne) { return (long)2 * (ne > 0 ? ne : 1) * 48 + 256; }
+LZK_EXPORT int lzk_dg_small_max_edges() { return SD_MAXE; }
+LZK_EXPORT int lzk_dg_small(const int* src, const int* dst, const float* w, int ne, const unsigned char* kind,
+                            const unsigned char* sup, const int* shard, long n, int min_size, double min_avg_w,
+                            int take, void* ws, long long* out, int cap, int* out_cnt, void* stream) {
+  if (ne <= 0 || ne > SD_MAXE || cap < 2 * ne || take < 1 || min_size < 2) return (int)hipErrorInvalidValue;
+  const long U = 2L * ne;
+  char* p = (char*)ws;
+  SdScratch S;
+  S.wsum = (double*)p; p += U * 8;
+  S.first = (long long*)p; p += U * 8;
+  S.ecnt = (int*)p; p += U * 4;
+  S.size = (int*)p; p += U * 4;
+  S.ccnt = (int*)p; p += U * 4;
+  S.cur = (int*)p; p += U * 4;
+  S.last = (int*)p; p += U * 4;
+  S.taken = (int*)p;
+  hipLaunchKernelGGL(dg_small_kernel, dim3(1), dim3(SD_NT), 0, (hipStream_t)stream, src, dst, w, ne, kind, sup, shard,
+                     n, min_size, min_avg_w, take, S, out, cap, out_cnt);
   return (int)hipGetLastError();
 }

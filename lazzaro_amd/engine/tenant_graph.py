@@ -1646,11 +1646,18 @@ class TenantGraph:
     DIGEST_LOCAL_FRAC = 8
 
     def _digest_local(self, min_size: int, take: int) -> bool:
-        return (self.on_gpu and min_size >= 2 and take >= 1 and not self._digest_sorted and self.num_edges > 0
-                and 2 * self.num_edges * self.DIGEST_LOCAL_FRAC <= self.n)
+        """The digest over the edges' endpoints only: one block for a few
+        thousand edges (T.component_digest_small), the renumbered torch form
+        while the edges touch at most 1/DIGEST_LOCAL_FRAC of the rows."""
+        ne = self.num_edges
+        return (self.on_gpu and min_size >= 2 and take >= 1 and not self._digest_sorted and ne > 0
+                and (ne <= T.dg_small_max_edges() or 2 * ne * self.DIGEST_LOCAL_FRAC <= self.n))
 
     def _digest_local_dev(self, min_size: int, min_avg_w: float, take: int) -> torch.Tensor:
         n = self.n
+        if self.num_edges <= T.dg_small_max_edges():  # one launch
+            return T.component_digest_small(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n], self.sup[:n],
+                                            self.shard[:n], n, min_size, min_avg_w, take)
         return T.component_digest_local(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n], self.sup[:n],
                                         self.shard[:n], min_size, min_avg_w, take)
 

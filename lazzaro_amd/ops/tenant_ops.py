@@ -37,6 +37,9 @@ _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P, P, L, P])
 _lib.register("lzk_tg_first_rows", I, [P, P, P, L, P, P, P, I, P, P])
+_lib.register("lzk_dg_small_ws", L, [I])
+_lib.register("lzk_dg_small_max_edges", I, [])
+_lib.register("lzk_dg_small", I, [P, P, P, I, P, P, P, L, I, D_, I, P, P, I, P, P])
 
 SALIENCE_FLOOR = 0.2
 EDGE_COLS = ("src", "dst", "w", "co", "lu", "meta")
@@ -496,7 +499,7 @@ def component_digest_local(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor
     MAXI = torch.iinfo(torch.int64).max
     idx = torch.arange(nl, device=dev)
     labl = lab.long()
-    cand = (touched != 0) & (kind_l == 1) & (sup_l == 0) & (cls != 0)
+    cand = (touched != 0) & (kind_l == 1) & (sup_l == 0) & (cls[labl] != 0)  # cls is per label
     o1 = torch.sort(torch.where(cand, labl * (nl + 1) + idx, torch.full_like(idx, MAXI))).indices
     lab_s, cand_s = labl[o1], cand[o1]
     newg = torch.ones(nl, dtype=torch.bool, device=dev)
@@ -526,6 +529,32 @@ def first_rows(kind: torch.Tensor, sup: torch.Tensor, shard: torch.Tensor, n: in
     _lib.check(_lib.lib().lzk_tg_first_rows(kind.data_ptr(), sup.data_ptr(), shard.data_ptr(), int(n),
                                             tgt[0].data_ptr(), tgt[1].data_ptr(), tgt[2].data_ptr(), nt,
                                             out.data_ptr(), _st(out)), "tg_first_rows")
+
+
+def dg_small_max_edges() -> int:
+    return int(_lib.lib().lzk_dg_small_max_edges())
+
+
+def component_digest_small(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind: torch.Tensor,
+                           sup: torch.Tensor, shard: torch.Tensor, n: int, min_size: int, min_avg_w: float,
+                           take: int) -> torch.Tensor:
+    """:func:`component_digest` of a graph with at most
+    :func:`dg_small_max_edges` edges in ONE kernel launch (digest.hip
+    dg_small_kernel: sort + renumber the endpoints, union-find, reductions
+    and selection in one block), no host synchronisation: int64 [2, 2E] =
+    (order key, row) sorted, unused entries (1 << 62, -1) last."""
+    dev = src.device
+    E = int(src.numel())
+    out = torch.empty((2, 2 * E), dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(_lib.lib().lzk_dg_small_ws(E)), dtype=torch.uint8, device=dev)
+    src, dst = src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous()
+    w = w.to(torch.float32).contiguous()
+    _lib.check(_lib.lib().lzk_dg_small(src.data_ptr(), dst.data_ptr(), w.data_ptr(), E, kind.data_ptr(),
+                                       sup.data_ptr(), shard.data_ptr(), int(n), int(min_size), float(min_avg_w),
+                                       int(take), ws.data_ptr(), out.data_ptr(), 2 * E, cnt.data_ptr(), _st(src)),
+               "dg_small")
+    return out
 
 
 def digest_lists(kr: np.ndarray) -> List[np.ndarray]:

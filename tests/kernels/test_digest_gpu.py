@@ -66,7 +66,7 @@ def test_local_digest_matches_sorted(seed):
     """The O(edges), sync-free digest (ops.tenant_ops.component_digest_local:
     endpoint renumbering, used when the edges touch few rows) against the
     sorted formulation, and its Capture form."""
-    g = _graph(200000, 600, 1200, seed)  # a small 'giant' + chains over a 200k-row tenant
+    g = _graph(200000, 600, 300, seed)  # a small "giant" + chains over a 200k-row tenant
     assert g._digest_local(3, 10)
     for take in (10, 3):
         got = [r.tolist() for r in g.component_digest(3, 0.3, take)]
@@ -101,3 +101,21 @@ def test_first_rows_kernel_matches_topk():
         ref = cpu.first_node_rows_dev(k, super_=False).tolist()
         assert gpu.first_node_rows_dev(k, super_=False).tolist() == ref and len(ref) == k
         assert gpu.first_rows_capture(k).get().tolist() == ref
+
+
+@pytest.mark.parametrize("n,ne_giant,n_small,seed", [(5000, 300, 60, 6), (400000, 900, 40, 7), (3000, 2000, 0, 8)])
+def test_small_digest_kernel_matches_sorted(n, ne_giant, n_small, seed):
+    """digest.hip dg_small_kernel (one block, <= 2048 edges: sort + renumber,
+    union-find, reductions, selection rounds) against the sorted formulation,
+    with a giant component of more than `take` candidates, chains, ghosts and
+    super-nodes."""
+    from lazzaro_amd.ops import tenant_ops as T
+    g = _graph(n, ne_giant, n_small, seed)
+    assert 0 < g.num_edges <= T.dg_small_max_edges() and g._digest_local(3, 10)
+    for take in (10, 3, 1):
+        got = [r.tolist() for r in g.component_digest(3, 0.3, take)]
+        cap = [r.tolist() for r in g.digest_capture(3, 0.3, take).get()]
+        g._digest_sorted = True
+        want = [r.tolist() for r in g.component_digest(3, 0.3, take)]
+        g._digest_sorted = False
+        assert got == want == cap and len(want) >= 1
