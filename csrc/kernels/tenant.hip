@@ -111,9 +111,20 @@ __global__ __launch_bounds__(NTB) void tg_flag_remove_kernel(const int* __restri
                                                              const int* __restrict__ shard,
                                                              const unsigned char* __restrict__ prev, long nprev,
                                                              unsigned char* __restrict__ flag,
-                                                             int* __restrict__ block_cnt) {
+                                                             int* __restrict__ block_cnt, int* __restrict__ npruned) {
   __shared__ int wsum[NTB / 64];
+  __shared__ int wz[NTB / 64];
   const long e = (long)blockIdx.x * NTB + threadIdx.x;
+  if (npruned) {  // edges the decay flagged (prev == 0): the segment's prune count
+    const unsigned long long zb = __ballot(prev != nullptr && e < nprev && prev[e] == 0);
+    if ((threadIdx.x & 63) == 0) wz[threadIdx.x >> 6] = __popcll(zb);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int z = 0;
+      for (int i = 0; i < NTB / 64; ++i) z += wz[i];
+      if (z) atomicAdd(npruned, z);
+    }
+  }
   int f = 0;
   if (e < ne) {
     f = (prev == nullptr || e >= nprev) ? 1 : (int)prev[e];
@@ -305,23 +316,29 @@ __global__ __launch_bounds__(256) void tg_set_rows_kernel(const long* __restrict
                                                           unsigned char* __restrict__ dirty, int kind_v, int stored_v) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
-  const long r = rows[j];
-  double v[7];
+  // present bit 15: the rows are the first m values of vals (exact doubles)
+  // instead of `rows`; bits 8-14: columns left as they are (no write);
+  // kind_v / stored_v < 0: kind / stored left as they are
   int slot = 0;
+  long r;
+  if (present & (1 << 15)) r = (long)vals[slot++ * (long)m + j];
+  else r = rows[j];
+  double v[7];
 #pragma unroll
   for (int c = 0; c < 7; ++c) {
     if (present & (1 << c)) v[c] = vals[(long)(slot++) * m + j];
     else v[c] = consts[c];
   }
-  sal[r] = (float)v[0];
-  acc[r] = (int)v[1];
-  last[r] = v[2];
-  ts[r] = v[3];
-  shard[r] = (int)v[4];
-  sup[r] = (unsigned char)v[5];
-  parent[r] = (int)v[6];
-  kind[r] = (unsigned char)kind_v;
-  stored[r] = (unsigned char)stored_v;
+  const int skip = present >> 8;
+  if (!(skip & 1)) sal[r] = (float)v[0];
+  if (!(skip & 2)) acc[r] = (int)v[1];
+  if (!(skip & 4)) last[r] = v[2];
+  if (!(skip & 8)) ts[r] = v[3];
+  if (!(skip & 16)) shard[r] = (int)v[4];
+  if (!(skip & 32)) sup[r] = (unsigned char)v[5];
+  if (!(skip & 64)) parent[r] = (int)v[6];
+  if (kind_v >= 0) kind[r] = (unsigned char)kind_v;
+  if (stored_v >= 0) stored[r] = (unsigned char)stored_v;
   dirty[r] = 1;
 }
 
@@ -541,6 +558,56 @@ __global__ __launch_bounds__(256) void tg_write_emb_kernel(
   }
 }
 
+// Edge append of a consolidation segment from one pinned float64 block
+// [src | dst | w | shard code] x m (exact for rows, codes and fp32 weights):
+// the six edge columns at [ne, ne + m) of buffers with room for them.
+__global__ __launch_bounds__(NTB) void tg_append_edges_kernel(const double* __restrict__ vals, int m, long ne,
+                                                              int meta_bits, double now, int* __restrict__ src,
+                                                              int* __restrict__ dst, float* __restrict__ w,
+                                                              int* __restrict__ co, double* __restrict__ lu,
+                                                              int* __restrict__ meta) {
+  const int j = blockIdx.x * NTB + threadIdx.x;
+  if (j >= m) return;
+  const long o = ne + j;
+  src[o] = (int)vals[j];
+  dst[o] = (int)vals[(long)m + j];
+  w[o] = (float)vals[2L * m + j];
+  co[o] = 1;
+  lu[o] = now;
+  meta[o] = ((int)vals[3L * m + j] & 0xFFFFFF) | meta_bits;
+}
+
+// Segment end (consolidate_batch): the victims' (kind, sup, shard) into
+// info, the live ones marked in the removal bitmap, turned into ghosts and
+// unstored -- the gathers, masks and scatters of the torch formulation in
+// one pass over the victims. The bitmap is persistent and all-zero between
+// segments: tg_clear_bits_kernel clears the victims' words after the flags.
+__global__ __launch_bounds__(NTB) void tg_victims_kernel(const long* __restrict__ rows, int nv,
+                                                         unsigned char* __restrict__ kind,
+                                                         const unsigned char* __restrict__ sup,
+                                                         const int* __restrict__ shard,
+                                                         unsigned char* __restrict__ stored, int unstore,
+                                                         unsigned* __restrict__ rmb, int* __restrict__ info) {
+  const int i = blockIdx.x * NTB + threadIdx.x;
+  if (i >= nv) return;
+  const long r = rows[i];
+  const unsigned char k = kind[r];
+  info[i] = k;
+  info[nv + i] = sup[r];
+  info[2 * nv + i] = shard[r];
+  if (k == 1) {
+    atomicOr(rmb + (r >> 5), 1u << (r & 31));
+    kind[r] = 2;
+    if (unstore) stored[r] = 0;
+  }
+}
+
+__global__ __launch_bounds__(NTB) void tg_clear_bits_kernel(const long* __restrict__ rows, int nv,
+                                                            unsigned* __restrict__ rmb) {
+  const int i = blockIdx.x * NTB + threadIdx.x;
+  if (i < nv) rmb[rows[i] >> 5] = 0u;
+}
+
 // The first rows of the shard nodes in (shard code, row) order -- the rows
 // run_consolidation's profile prompt reads when no component qualifies
 // (reference memory_system.py:1003-1008, BufferGraph.nodes order) -- without
@@ -630,7 +697,7 @@ LZK_EXPORT int lzk_tg_flag_remove(const int* src, const int* dst, const int* met
   if (ne == 0) return 0;
   if (nprev < 0 || nprev > ne || (prev == nullptr && rmb == nullptr)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tg_flag_remove_kernel, dim3(blocks_for(ne)), dim3(NTB), 0, (hipStream_t)stream, src, dst, meta,
-                     ne, rmb, shard, prev, nprev, flag, block_cnt);
+                     ne, rmb, shard, prev, nprev, flag, block_cnt, (int*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -772,5 +839,46 @@ LZK_EXPORT int lzk_tg_first_rows(const unsigned char* kind, const unsigned char*
   if (nt > FR_MAXT || n < 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tg_first_rows_kernel, dim3(1), dim3(FR_NT), 0, (hipStream_t)stream, kind, sup, shard, n, tc, tt,
                      to, nt, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int lzk_scan_blocks(int* cnt, int n, int* total, void* stream);
+
+// One segment end of consolidate_batch (TenantGraph.segment_end): victims
+// (int64 rows, distinct, nv >= 0) -> info[0 .. 3 nv) = their kind / sup /
+// shard before the removal, live ones ghosted (+ unstored) and their shard's
+// edges flagged for removal together with the decay's deferred prune (prev,
+// the keep flags of the first nprev edges): flag / bc (block offsets after
+// the scan) for lzk_tg_compact, info[3 nv] = surviving edges, info[3 nv + 1]
+// = edges the decay pruned. rmb: the graph's persistent all-zero bitmap of
+// (n + 31) / 32 words. Five launches, one host read of info by the caller.
+LZK_EXPORT int lzk_tg_seg_end(const long* vrows, int nv, unsigned char* kind, const unsigned char* sup,
+                              const int* shard, unsigned char* stored, int unstore, unsigned* rmb, const int* src,
+                              const int* dst, const int* meta, long ne, const unsigned char* prev, long nprev,
+                              unsigned char* flag, int* bc, int* info, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (nv < 0 || nprev < 0 || nprev > ne || (ne > 0 && (flag == nullptr || bc == nullptr)))
+    return (int)hipErrorInvalidValue;
+  hipError_t err = hipMemsetAsync(info + 3L * nv, 0, 2 * sizeof(int), st);
+  if (err != hipSuccess) return (int)err;
+  if (nv > 0)
+    hipLaunchKernelGGL(tg_victims_kernel, dim3(blocks_for(nv)), dim3(NTB), 0, st, vrows, nv, kind, sup, shard, stored,
+                       unstore, rmb, info);
+  if (ne > 0) {
+    hipLaunchKernelGGL(tg_flag_remove_kernel, dim3(blocks_for(ne)), dim3(NTB), 0, st, src, dst, meta, ne,
+                       nv > 0 ? rmb : nullptr, shard, prev, nprev, flag, bc, info + 3L * nv + 1);
+    const int rc = lzk_scan_blocks(bc, (int)blocks_for(ne), info + 3L * nv, stream);
+    if (rc != 0) return rc;
+  }
+  if (nv > 0) hipLaunchKernelGGL(tg_clear_bits_kernel, dim3(blocks_for(nv)), dim3(NTB), 0, st, vrows, nv, rmb);
+  return (int)hipGetLastError();
+}
+
+// Segment edge append (tg_append_edges_kernel); vals: device float64 [4][m].
+LZK_EXPORT int lzk_tg_append_edges(const double* vals, int m, long ne, int meta_bits, double now, int* src, int* dst,
+                                   float* w, int* co, double* lu, int* meta, void* stream) {
+  if (m <= 0) return 0;
+  hipLaunchKernelGGL(tg_append_edges_kernel, dim3(blocks_for(m)), dim3(NTB), 0, (hipStream_t)stream, vals, m, ne,
+                     meta_bits, now, src, dst, w, co, lu, meta);
   return (int)hipGetLastError();
 }

@@ -1048,12 +1048,22 @@ class ConsolidationMixin:
         tr = np.asarray(seg["tch_rows"], np.int64)
         if tr.size:
             with g.on_stream():
-                r64, s64, a64, l64 = T.to_dev_packed([tr, seg["tch_sal"], seg["tch_acc"], seg["tch_last"]], dev)
-                rt = r64.long()
-                g.sal[rt] = s64.float()
-                g.acc[rt] = a64.int()
-                g.last[rt] = l64
-                g.dirty[rt] = 1
+                if g.on_gpu:  # one pinned block, one launch (tenant.hip tg_set_rows_kernel)
+                    m = int(tr.size)
+                    blk = torch.empty(7 + 4 * m, dtype=torch.float64).pin_memory()
+                    bn = blk.numpy()
+                    bn[:7] = 0.0
+                    for j, c in enumerate((tr, seg["tch_sal"], seg["tch_acc"], seg["tch_last"])):
+                        bn[7 + j * m: 7 + (j + 1) * m] = np.asarray(c, dtype=np.float64).reshape(-1)
+                    # per-row sal / acc / last; ts, shard, sup, parent, kind, stored untouched
+                    T.set_rows(g, None, blk.to(dev, non_blocking=True), 0b111 | (0b1111000 << 8), -1, -1, m=m)
+                else:
+                    r64, s64, a64, l64 = T.to_dev_packed([tr, seg["tch_sal"], seg["tch_acc"], seg["tch_last"]], dev)
+                    rt = r64.long()
+                    g.sal[rt] = s64.float()
+                    g.acc[rt] = a64.int()
+                    g.last[rt] = l64
+                    g.dirty[rt] = 1
             g._bump()
         stored = self._store_binds_graph()
         kinds = np.asarray(seg["ins_kind"]).tolist()
@@ -1101,9 +1111,8 @@ class ConsolidationMixin:
         es = np.asarray(seg["edge_src"], np.int64)
         if es.size:
             with tracer.stage("ap_edges", dev):
-                s64, d64, w64, c64 = T.to_dev_packed([es, seg["edge_dst"], np.asarray(seg["edge_w"], np.float32),
-                                                      seg["edge_code"]], dev)
-                g.append_edges(s64.long(), d64.long(), w64.float(), c64.int(), g.etype("relates_to"), now=now)
+                g.append_edges_host(es, seg["edge_dst"], seg["edge_w"], seg["edge_code"], g.etype("relates_to"),
+                                    now=now)
         vic = np.asarray(seg["victims"], np.int64).tolist()
         ids = [g.ids[r] for r in vic]
         with tracer.stage("ap_remove", dev):

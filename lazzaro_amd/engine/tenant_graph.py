@@ -110,6 +110,8 @@ LEAN_HBM = os.environ.get("LZK_LEAN_HBM", "0") == "1"
 WRITE_EMB_MAX_ROWS = 8192
 # node columns of an insert in one launch (tenant.hip tg_set_rows_kernel); 0 = per-column writes
 SET_ROWS_KERNEL = os.environ.get("LZK_SET_ROWS", "1") != "0"
+# consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (LZK_SEG_END=0: the torch formulation)
+SEG_END_KERNEL = os.environ.get("LZK_SEG_END", "1") != "0"
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
 RERANK_KERNEL = os.environ.get("LZK_RERANK_KERNEL", "1") != "0"
 # consolidation's float64 candidate re-rank as one kernel (cos_rerank64_kernel); 0 = torch chain
@@ -388,6 +390,7 @@ class TenantGraph:
     # component_digest on the GPU: digest.hip keyed reductions (False) or the
     # sort + segmented-scan formulation the CPU runs (True; tests compare them)
     _digest_sorted = False
+    _rmb = None  # persistent all-zero removal bitmap of the fused segment end
     SAMPLE_TWO_LEVEL = os.environ.get("LZK_SAMPLE_ASSIGN", "two_level") != "full"
 
     # Low-precision copy of the rows for the store search's candidate scan
@@ -1078,6 +1081,42 @@ class TenantGraph:
 
     EDGE_SLACK_MIN = 1 << 14
 
+    def append_edges_host(self, src, dst, w, code, etype: int = 0, now: Optional[float] = None) -> None:
+        """:meth:`append_edges` from host arrays (a consolidation segment's
+        planned links): one pinned float64 block, one copy, one launch
+        (tenant.hip tg_append_edges_kernel) into the columns' spare tails."""
+        m = len(src)
+        if m == 0:
+            return
+        now = time.time() if now is None else now
+        if not self.on_gpu:
+            cols = T.to_dev_packed([src, dst, np.asarray(w, np.float32), code], self.device)
+            self.append_edges(cols[0].long(), cols[1].long(), cols[2].float(), cols[3].int(), etype, now=now)
+            return
+        dev = self.device
+        with self.on_stream():
+            blk = torch.empty(4 * m, dtype=torch.float64).pin_memory()
+            bn = blk.numpy()
+            for j, c in enumerate((src, dst, np.asarray(w, np.float32), code)):
+                bn[j * m:(j + 1) * m] = np.asarray(c, dtype=np.float64).reshape(-1)
+            vals = blk.to(dev, non_blocking=True)
+            e = self.e
+            ne = int(e["src"].numel())
+            for k, dt in (("src", torch.int32), ("dst", torch.int32), ("w", torch.float32), ("co", torch.int32),
+                          ("lu", torch.float64), ("meta", torch.int32)):
+                v = e[k]
+                buf, vn = self._ebuf.get(k, (None, -1))
+                if buf is None or vn != ne or v.numel() != ne or buf.numel() < ne + m or v.data_ptr() != buf.data_ptr():
+                    buf = torch.empty(ne + m + max((ne + m) >> 3, self.EDGE_SLACK_MIN), dtype=dt, device=dev)
+                    buf[:ne].copy_(v)
+                e[k] = buf[:ne + m]
+                self._ebuf[k] = (buf, ne + m)
+            T._lib.check(T._lib.lib().lzk_tg_append_edges(
+                vals.data_ptr(), m, ne, (etype << TYPE_SHIFT) | EDIRTY, float(now), e["src"].data_ptr(),
+                e["dst"].data_ptr(), e["w"].data_ptr(), e["co"].data_ptr(), e["lu"].data_ptr(), e["meta"].data_ptr(),
+                T._st(vals)), "tg_append_edges")
+        self._bump(edges=True)
+
     def _edge_append(self, new: Dict[str, torch.Tensor], m: int) -> None:
         """Append ``m`` edges: into the spare tail of the column's buffer when
         ``self.e[k]`` is still the view this method (or a segment compaction)
@@ -1315,6 +1354,8 @@ class TenantGraph:
         ne = self.num_edges
         if not cand and prev is None:
             return 0
+        if SEG_END_KERNEL:
+            return self._segment_end_fused(cand, prev, ne, unstore)
         with self.on_stream():
             parts = []
             rt = live_t = None
@@ -1353,6 +1394,49 @@ class TenantGraph:
                         self._note_dropped(*T._dropped(old, flag, ne, n))
         if cand:
             kinds, sups, shards = info[:nc], info[nc:2 * nc], info[2 * nc:3 * nc]
+            for r, k, sp, sh in zip(cand, kinds.tolist(), sups.tolist(), shards.tolist()):
+                if k != NODE:
+                    continue
+                if sp:
+                    self.n_super -= 1
+                elif sh >= 0:
+                    self.shard_count[sh] -= 1
+                self.children.pop(r, None)
+                self.odd_emb.pop(r, None)
+                self.deleted_ids[self.ids[r]] = None
+        self._bump(edges=True, store=bool(cand))
+        return pruned
+
+    def _segment_end_fused(self, cand: List[int], prev, ne: int, unstore: bool) -> int:
+        """:meth:`segment_end` through tenant.hip lzk_tg_seg_end: the victims'
+        state, the removal bitmap, the edge flags and both counts in five
+        launches, read back in one copy."""
+        nc = len(cand)
+        dev = self.device
+        with self.on_stream():
+            words = (self.cap + 31) // 32
+            if self._rmb is None or self._rmb.numel() < words:
+                self._rmb = torch.zeros(words, dtype=torch.int32, device=dev)
+            rt = self._dev_rows(cand) if nc else None
+            info = torch.empty(3 * nc + 2, dtype=torch.int32, device=dev)
+            flag = bc = None
+            if ne:
+                flag = torch.empty(ne, dtype=torch.uint8, device=dev)
+                bc = torch.empty(max(1, (ne + T.NTB - 1) // T.NTB), dtype=torch.int32, device=dev)
+            T.seg_end(rt, nc, self.kind, self.sup, self.shard, self.stored, unstore, self._rmb, self.e, prev, flag, bc,
+                      info)
+            info_h = info.cpu().numpy()  # the one host sync
+            pruned = int(info_h[3 * nc + 1]) if prev is not None else 0
+            if ne:
+                n_out = int(info_h[3 * nc])
+                if n_out != ne:
+                    old = self.e
+                    out, n = T._compact(old, flag, bc, ne, extra=max(ne >> 3, self.EDGE_SLACK_MIN), n_out=n_out)
+                    self._adopt_edges(out)
+                    if self.track:
+                        self._note_dropped(*T._dropped(old, flag, ne, n))
+        if nc:
+            kinds, sups, shards = info_h[:nc], info_h[nc:2 * nc], info_h[2 * nc:3 * nc]
             for r, k, sp, sh in zip(cand, kinds.tolist(), sups.tolist(), shards.tolist()):
                 if k != NODE:
                     continue

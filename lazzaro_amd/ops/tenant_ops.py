@@ -38,6 +38,8 @@ _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, 
 _lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P, P, L, P])
 _lib.register("lzk_tg_first_rows", I, [P, P, P, L, P, P, P, I, P, P])
 _lib.register("lzk_dg_small_ws", L, [I])
+_lib.register("lzk_tg_append_edges", I, [P, I, L, I, D_, P, P, P, P, P, P, P])
+_lib.register("lzk_tg_seg_end", I, [P, I, P, P, P, P, I, P, P, P, P, L, P, L, P, P, P, P])
 _lib.register("lzk_dg_small_max_edges", I, [])
 _lib.register("lzk_dg_small", I, [P, P, P, I, P, P, P, L, I, D_, I, P, P, I, P, P])
 
@@ -222,6 +224,22 @@ def flag_finish(e: Dict[str, torch.Tensor], rm: Optional[torch.Tensor], shard: t
                                      _st(flag)), "tg_flag_remove")
     _lib.check(L_.lzk_scan_blocks(bc.data_ptr(), bc.numel(), total.data_ptr(), _st(bc)), "scan_blocks")
     return flag, bc, total
+
+
+def seg_end(vrows: Optional[torch.Tensor], nv: int, kind, sup, shard, stored, unstore: bool, rmb: torch.Tensor,
+            e: Dict[str, torch.Tensor], prev: Optional[torch.Tensor], flag: Optional[torch.Tensor],
+            bc: Optional[torch.Tensor], info: torch.Tensor) -> None:
+    """tenant.hip lzk_tg_seg_end: one segment end of consolidate_batch (see
+    TenantGraph.segment_end) -- victims ghosted and their (kind, sup, shard)
+    in info[:3 nv], the keep flags of every edge (decay prune AND victim
+    removal) with scanned block offsets in flag / bc, info[3 nv] = survivors,
+    info[3 nv + 1] = pruned by the decay. ``rmb``: persistent zero bitmap."""
+    ne = int(e["src"].numel())
+    _lib.check(_lib.lib().lzk_tg_seg_end(_lib.ptr(vrows), int(nv), kind.data_ptr(), sup.data_ptr(), shard.data_ptr(),
+                                         stored.data_ptr(), 1 if unstore else 0, rmb.data_ptr(), e["src"].data_ptr(),
+                                         e["dst"].data_ptr(), e["meta"].data_ptr(), ne, _lib.ptr(prev),
+                                         int(prev.numel()) if prev is not None else 0, _lib.ptr(flag), _lib.ptr(bc),
+                                         info.data_ptr(), _st(info)), "tg_seg_end")
 
 
 def build_visible_csr(e: Dict[str, torch.Tensor], shard: torch.Tensor, n: int):
@@ -644,17 +662,23 @@ def store_rerank(Qf: torch.Tensor, X: torch.Tensor, sqn: torch.Tensor, bias: tor
 SET_ROWS_COLS = ("sal", "acc", "last", "ts", "shard", "sup", "parent")
 
 
-def set_rows(g, rows: torch.Tensor, block: torch.Tensor, present: int, kind_v: int, stored_v: int) -> None:
+def set_rows(g, rows: Optional[torch.Tensor], block: torch.Tensor, present: int, kind_v: int, stored_v: int,
+             m: Optional[int] = None) -> None:
     """Node columns of ``rows`` in one launch (tenant.hip tg_set_rows_kernel):
     ``block`` is a device float64 vector = 7 constants (one per
     SET_ROWS_COLS column) followed by [ncols, m] per-row values of the
-    columns whose bit is set in ``present``."""
-    m = int(rows.numel())
+    columns whose bit is set in ``present``. ``rows`` None: bit 15 of
+    ``present``, the rows are the block's first m per-row values; bits 8-14
+    leave columns unwritten, ``kind_v`` / ``stored_v`` < 0 leave kind /
+    stored."""
+    m = int(rows.numel()) if rows is not None else int(m)
+    if rows is None:
+        present |= 1 << 15
     b = block.data_ptr()
     _lib.check(_lib.lib().lzk_tg_set_rows(
-        rows.data_ptr(), m, b + 7 * 8, int(present), b, g.sal.data_ptr(), g.acc.data_ptr(), g.last.data_ptr(),
+        _lib.ptr(rows), m, b + 7 * 8, int(present), b, g.sal.data_ptr(), g.acc.data_ptr(), g.last.data_ptr(),
         g.ts.data_ptr(), g.shard.data_ptr(), g.sup.data_ptr(), g.parent.data_ptr(), g.kind.data_ptr(),
-        g.stored.data_ptr(), g.dirty.data_ptr(), int(kind_v), int(stored_v), _lib.stream_ptr(rows.device)),
+        g.stored.data_ptr(), g.dirty.data_ptr(), int(kind_v), int(stored_v), _lib.stream_ptr(block.device)),
         "lzk_tg_set_rows")
 
 
