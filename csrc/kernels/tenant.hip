@@ -305,7 +305,7 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
 // in the fixed column order below; a column absent from the block (bit c of
 // `present` clear) takes its constant. kind / stored / dirty are constants.
 //   0 sal f32 | 1 acc i32 | 2 last f64 | 3 ts f64 | 4 shard i32 | 5 sup u8 | 6 parent i32
-__global__ __launch_bounds__(256) void tg_set_rows_kernel(const long* __restrict__ rows, int m,
+__global__ __launch_bounds__(256) void tg_set_rows_kernel(const long* __restrict__ rows, long row0, int m,
                                                           const double* __restrict__ vals, int present,
                                                           const double* __restrict__ consts, float* __restrict__ sal,
                                                           int* __restrict__ acc, double* __restrict__ last,
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void tg_set_rows_kernel(const long* __restrict
   int slot = 0;
   long r;
   if (present & (1 << 15)) r = (long)vals[slot++ * (long)m + j];
-  else r = rows[j];
+  else r = rows ? rows[j] : row0 + j;
   double v[7];
 #pragma unroll
   for (int c = 0; c < 7; ++c) {
@@ -500,15 +500,16 @@ __global__ __launch_bounds__(256) void cos_rerank64_kernel(const double* __restr
 // it replaces (ops/search.py quantize_i8_rows: round half to even).
 __global__ __launch_bounds__(256) void tg_write_emb_kernel(
     const float* __restrict__ x, long ldx, const unsigned char* __restrict__ has, int m, int D,
-    const long* __restrict__ rows, float* __restrict__ emb32, long ld32, u16* __restrict__ emb16, long ld16,
-    signed char* __restrict__ emb8, long ld8, float* __restrict__ rs8, float* __restrict__ sqn,
-    double* __restrict__ sumsq, float* __restrict__ rs_max, float* __restrict__ dv_max) {
+    const long* __restrict__ rows, long row0, float* __restrict__ emb32, long ld32, u16* __restrict__ emb16,
+    long ld16, signed char* __restrict__ emb8, long ld8, float* __restrict__ rs8, float* __restrict__ sqn,
+    double* __restrict__ sumsq, float* __restrict__ rs_max, float* __restrict__ dv_max,
+    unsigned char* __restrict__ has_emb) {
   __shared__ double red_d[4];
   __shared__ float red_f[4];
   const int j = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float hv = (has == nullptr || has[j]) ? 1.f : 0.f;
-  const long r = rows[j];
+  const long r = rows ? rows[j] : row0 + j;  // rows null: the contiguous rows row0 ..
   float v[4], vb[4];
   double s2 = 0.0;
   float am = 0.f;
@@ -555,6 +556,7 @@ __global__ __launch_bounds__(256) void tg_write_emb_kernel(
   if (t == 0) {
     sqn[r] = (float)s2;
     if (dv_max && hv > 0.f) atomicMax(reinterpret_cast<int*>(dv_max), __float_as_int((float)fabs(sqrt(s2) - 1.0)));
+    if (has_emb) has_emb[r] = hv > 0.f ? 1 : 0;
   }
 }
 
@@ -799,23 +801,26 @@ LZK_EXPORT int lzk_store_rerank(const float* Q, long ldq, const float* X, long l
   return (int)hipGetLastError();
 }
 
-LZK_EXPORT int lzk_tg_set_rows(const long* rows, int m, const double* vals, int present, const double* consts,
-                               float* sal, int* acc, double* last, double* ts, int* shard, unsigned char* sup,
-                               int* parent, unsigned char* kind, unsigned char* stored, unsigned char* dirty,
-                               int kind_v, int stored_v, void* stream) {
+LZK_EXPORT int lzk_tg_set_rows(const long* rows, long row0, int m, const double* vals, int present,
+                               const double* consts, float* sal, int* acc, double* last, double* ts, int* shard,
+                               unsigned char* sup, int* parent, unsigned char* kind, unsigned char* stored,
+                               unsigned char* dirty, int kind_v, int stored_v, void* stream) {
   if (m <= 0) return 0;
-  hipLaunchKernelGGL(tg_set_rows_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, (hipStream_t)stream, rows, m, vals,
-                     present, consts, sal, acc, last, ts, shard, sup, parent, kind, stored, dirty, kind_v, stored_v);
+  hipLaunchKernelGGL(tg_set_rows_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, (hipStream_t)stream, rows, row0, m,
+                     vals, present, consts, sal, acc, last, ts, shard, sup, parent, kind, stored, dirty, kind_v,
+                     stored_v);
   return (int)hipGetLastError();
 }
 
 LZK_EXPORT int lzk_tg_write_emb(const float* x, long ldx, const unsigned char* has, int m, int D, const long* rows,
-                                float* emb32, long ld32, void* emb16, long ld16, void* emb8, long ld8, float* rs8,
-                                float* sqn, double* sumsq, float* rs_max, float* dv_max, void* stream) {
+                                long row0, float* emb32, long ld32, void* emb16, long ld16, void* emb8, long ld8,
+                                float* rs8, float* sqn, double* sumsq, float* rs_max, float* dv_max,
+                                unsigned char* has_emb, void* stream) {
   if (m <= 0) return 0;
   if (D <= 0 || D > 1024 || (emb8 && !rs8)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tg_write_emb_kernel, dim3((unsigned)m), dim3(256), 0, (hipStream_t)stream, x, ldx, has, m, D,
-                     rows, emb32, ld32, (u16*)emb16, ld16, (signed char*)emb8, ld8, rs8, sqn, sumsq, rs_max, dv_max);
+                     rows, row0, emb32, ld32, (u16*)emb16, ld16, (signed char*)emb8, ld8, rs8, sqn, sumsq, rs_max,
+                     dv_max, has_emb);
   return (int)hipGetLastError();
 }
 

@@ -1085,7 +1085,7 @@ class ConsolidationMixin:
                                        shard=codes[js].astype(np.int32),
                                        types=[facts[j].get("type", "semantic") for j in js],
                                        sal=torch.from_numpy(isal[i:k]), acc=torch.from_numpy(iacc[i:k]),
-                                       last=torch.from_numpy(ilast[i:k]), now=now, stored=stored)
+                                       last=torch.from_numpy(ilast[i:k]), now=now, stored=stored, want_rows=False)
                     if list(g.last_add_rows) != keys:  # host rows: no device round trip
                         raise RuntimeError("batch plan row assignment diverged from the graph")
                     i = k

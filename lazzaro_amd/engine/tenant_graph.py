@@ -391,6 +391,8 @@ class TenantGraph:
     # sort + segmented-scan formulation the CPU runs (True; tests compare them)
     _digest_sorted = False
     _rmb = None  # persistent all-zero removal bitmap of the fused segment end
+    _dv_acc = None  # device running max of | |x| - 1 | over small inserts
+    _dv_acc_pending = False  # _dv_acc is in _norm_dev_pending
     SAMPLE_TWO_LEVEL = os.environ.get("LZK_SAMPLE_ASSIGN", "two_level") != "full"
 
     # Low-precision copy of the rows for the store search's candidate scan
@@ -522,7 +524,7 @@ class TenantGraph:
     def add_nodes(self, ids: Sequence[str], contents: Sequence[str], emb=None, *, shard=None, types=None,
                   sal=None, acc=None, last=None, ts=None, sup=None, parents: Optional[Sequence[Optional[str]]] = None,
                   children: Optional[Dict[int, List[str]]] = None, stored: bool = False,
-                  now: Optional[float] = None, ghost: bool = False) -> torch.Tensor:
+                  now: Optional[float] = None, ghost: bool = False, want_rows: bool = True) -> torch.Tensor:
         """Append (or replace, by id) ``m`` nodes. Scalars may be python
         sequences, tensors or scalars; ``shard`` holds shard codes; ``children``
         maps batch position -> child id list (super-nodes). ``ghost``: rows
@@ -534,10 +536,10 @@ class TenantGraph:
         now = time.time() if now is None else now
         with self.on_stream():
             return self._add_nodes(ids, contents, emb, shard, types, sal, acc, last, ts, sup, parents, children,
-                                   stored, now, ghost)
+                                   stored, now, ghost, want_rows)
 
     def _add_nodes(self, ids, contents, emb, shard, types, sal, acc, last, ts, sup, parents, children, stored, now,
-                   ghost=False):
+                   ghost=False, want_rows=True):
         m = len(ids)
         dev = self.device
         e32, info = self._as_emb(emb, m)
@@ -558,7 +560,7 @@ class TenantGraph:
                 self.row_of.update(zip(ids, range(n0, n0 + m)))
             self.n = n0 + m
             rl = range(n0, n0 + m)
-            rt = torch.arange(n0, n0 + m, dtype=torch.long, device=dev)
+            rt = None  # contiguous rows n0 ..: materialised only where a row list is needed
         else:
             rows = [self.row_of.get(i, -1) for i in ids]
             fresh = sum(1 for r in rows if r < 0)
@@ -586,13 +588,16 @@ class TenantGraph:
             self.n = r_next
             rt = torch.as_tensor(rl, dtype=torch.long).to(dev)
 
+        def rows_t():
+            return rt if rt is not None else torch.arange(n0, n0 + m, dtype=torch.long, device=dev)
+
         # a small batch whose per-row columns are all host values (or
         # scalars): ONE pinned float64 block -> one H2D copy + one kernel
         # writing every node column (tenant.hip tg_set_rows_kernel) --
         # consolidate_batch applies ~40 segments a step, each an insert
         fused = False
         if SET_ROWS_KERNEL and dev.type == "cuda" and m <= (1 << 16) and not (parents is not None and any(parents)):
-            fused = self._set_rows_fused(rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored)
+            fused = self._set_rows_fused(rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored, row0=n0)
         packed = {}
         if fused:
             sh, supv = None, None
@@ -626,6 +631,7 @@ class TenantGraph:
             return torch.as_tensor(np.asarray(v)).to(dev, dt)
 
         if not fused:
+            rt = rows_t()
             sh = col(shard, torch.int32, 0, "shard")
             supv = col(sup, torch.uint8, 0, "sup")
             self.sal[rt] = col(sal, torch.float32, 0.5, "sal")
@@ -644,7 +650,8 @@ class TenantGraph:
                 self.parent[rt] = -1
         if self.dim is not None:
             if info is None:
-                has = torch.ones(m, dtype=torch.bool, device=dev)
+                has = None if (self.on_gpu and m <= WRITE_EMB_MAX_ROWS and self.dim <= 1024 and e32.is_cuda) \
+                    else torch.ones(m, dtype=torch.bool, device=dev)
             else:
                 ok, odd = info
                 has = torch.as_tensor(ok, dtype=torch.bool).to(dev)
@@ -655,18 +662,19 @@ class TenantGraph:
                 # small inserts (consolidation segments, chat turns): every
                 # embedding column in one launch (tenant.hip tg_write_emb_kernel)
                 from ..ops.tenant_ops import write_emb
-                dv = torch.zeros(1, dtype=torch.float32, device=dev)
-                write_emb(self, e32, None if info is None else has, rt, dv)
+                if self._dv_acc is None:  # running device max of | |x| - 1 | (max_norm_dev)
+                    self._dv_acc = torch.zeros(1, dtype=torch.float32, device=dev)
+                write_emb(self, e32, None if info is None else has, rt, self._dv_acc, row0=n0, has_emb=True)
                 self.n_sumsq += m
-                self.has_emb[rt] = has.to(torch.uint8)
-                if info is None or any(info[0]):
-                    self._norm_dev_pending.append(dv[0])
-                    if len(self._norm_dev_pending) >= 256:
-                        self._norm_dev_pending = [torch.stack(self._norm_dev_pending).max()]
+                if (info is None or any(info[0])) and not self._dv_acc_pending:
+                    self._norm_dev_pending.append(self._dv_acc[0])
+                    self._dv_acc_pending = True
                 mc = 0  # columns written; skip the chunked path below
             # row chunks: a 10M-row load must not hold fp64 copies of the
             # whole [m, D] block (the squares were 2 x 60 GB of temporaries)
             contig = isinstance(rl, range)
+            if mc:
+                rt = rows_t()
             nrm2 = torch.empty(mc, dtype=torch.float64, device=dev)
             ch = max(1, (1 << 28) // max(1, 8 * self.dim))  # ~256 MB of fp64 per chunk
             for a in range(0, mc, ch):
@@ -720,9 +728,9 @@ class TenantGraph:
                 self.deleted_ids.pop(i, None)
         self.last_add_rows = rl  # host rows of this call (range or list)
         self._bump(store=True)
-        return rt
+        return rows_t() if want_rows else None
 
-    def _set_rows_fused(self, rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored) -> bool:
+    def _set_rows_fused(self, rt, m, shard, sup, sal, acc, last, ts, now, ghost, stored, row0=0) -> bool:
         """The node columns of an insert through tg_set_rows_kernel when every
         per-row value is on the host (else False: the caller's column path)."""
         vals = []
@@ -758,7 +766,7 @@ class TenantGraph:
         for j, a in enumerate(vals):
             bn[7 + j * m: 7 + (j + 1) * m] = a
         T.set_rows(self, rt, blk.to(self.device, non_blocking=True), present, GHOST if ghost else NODE,
-                   1 if stored else 0)
+                   1 if stored else 0, m=m, row0=row0 if rt is None else None)
         return True
 
     def _ensure_row(self, node_id: str) -> int:
@@ -1279,6 +1287,7 @@ class TenantGraph:
         maxima pending (no host synchronisation per insert)."""
         if self._norm_dev_pending:
             pend, self._norm_dev_pending = self._norm_dev_pending, []
+            self._dv_acc_pending = False
             with self.on_stream():
                 self._max_norm_dev = max(self._max_norm_dev, float(torch.stack(pend).max()))
         return self._max_norm_dev
@@ -1286,6 +1295,7 @@ class TenantGraph:
     @max_norm_dev.setter
     def max_norm_dev(self, v: float) -> None:
         self._norm_dev_pending = []
+        self._dv_acc, self._dv_acc_pending = None, False
         self._max_norm_dev = float(v)
 
     # ------------------------------------------------------------------ maintenance

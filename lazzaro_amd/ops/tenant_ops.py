@@ -22,8 +22,8 @@ P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
 D_ = C.c_double
 
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
-_lib.register("lzk_tg_write_emb", I, [P, L, P, I, I, P, P, L, P, L, P, L, P, P, P, P, P, P])
-_lib.register("lzk_tg_set_rows", I, [P, I, P, I, P, P, P, P, P, P, P, P, P, P, P, I, I, P])
+_lib.register("lzk_tg_write_emb", I, [P, L, P, I, I, P, L, P, L, P, L, P, L, P, P, P, P, P, P, P])
+_lib.register("lzk_tg_set_rows", I, [P, L, I, P, I, P, P, P, P, P, P, P, P, P, P, P, I, I, P])
 _lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
@@ -663,40 +663,44 @@ SET_ROWS_COLS = ("sal", "acc", "last", "ts", "shard", "sup", "parent")
 
 
 def set_rows(g, rows: Optional[torch.Tensor], block: torch.Tensor, present: int, kind_v: int, stored_v: int,
-             m: Optional[int] = None) -> None:
+             m: Optional[int] = None, row0: Optional[int] = None) -> None:
     """Node columns of ``rows`` in one launch (tenant.hip tg_set_rows_kernel):
     ``block`` is a device float64 vector = 7 constants (one per
     SET_ROWS_COLS column) followed by [ncols, m] per-row values of the
     columns whose bit is set in ``present``. ``rows`` None: bit 15 of
     ``present``, the rows are the block's first m per-row values; bits 8-14
     leave columns unwritten, ``kind_v`` / ``stored_v`` < 0 leave kind /
-    stored."""
+    stored; ``row0``: the contiguous rows row0 .. row0 + m - 1 (no row
+    list)."""
     m = int(rows.numel()) if rows is not None else int(m)
-    if rows is None:
+    if rows is None and row0 is None:
         present |= 1 << 15
     b = block.data_ptr()
     _lib.check(_lib.lib().lzk_tg_set_rows(
-        _lib.ptr(rows), m, b + 7 * 8, int(present), b, g.sal.data_ptr(), g.acc.data_ptr(), g.last.data_ptr(),
+        _lib.ptr(rows), int(row0 or 0), m, b + 7 * 8, int(present), b, g.sal.data_ptr(), g.acc.data_ptr(), g.last.data_ptr(),
         g.ts.data_ptr(), g.shard.data_ptr(), g.sup.data_ptr(), g.parent.data_ptr(), g.kind.data_ptr(),
         g.stored.data_ptr(), g.dirty.data_ptr(), int(kind_v), int(stored_v), _lib.stream_ptr(block.device)),
         "lzk_tg_set_rows")
 
 
-def write_emb(g, e32: torch.Tensor, has: Optional[torch.Tensor], rows: torch.Tensor, dv_max: torch.Tensor) -> None:
+def write_emb(g, e32: torch.Tensor, has: Optional[torch.Tensor], rows: Optional[torch.Tensor], dv_max: torch.Tensor,
+              row0: int = 0, has_emb: bool = False) -> None:
     """Embedding columns of ``rows`` from fp32 ``e32`` [m, dim] in one launch
     (tenant.hip tg_write_emb_kernel): emb32, emb16, the int8 copy + row
     scale, sqn, the per-dimension fp64 sums of squares, and device maxima of
-    the row scale (``g._rs8_max``) and of | |x| - 1 | (``dv_max`` [1])."""
+    the row scale (``g._rs8_max``) and of | |x| - 1 | (``dv_max`` [1]).
+    ``rows`` None: the contiguous rows row0 ..; ``has_emb``: the has_emb
+    column too."""
     m, D = e32.shape
     x = e32.contiguous() if e32.dtype == torch.float32 else e32.float().contiguous()
-    r = rows.to(torch.long).contiguous()
+    r = rows.to(torch.long).contiguous() if rows is not None else None
     h = has.to(torch.uint8).contiguous() if has is not None else None
     i8 = g.emb8 is not None and g.emb8.dtype == torch.int8
     _lib.check(_lib.lib().lzk_tg_write_emb(
-        x.data_ptr(), x.stride(0), _lib.ptr(h), m, D, r.data_ptr(), g.emb32.data_ptr(), g.emb32.stride(0),
+        x.data_ptr(), x.stride(0), _lib.ptr(h), m, D, _lib.ptr(r), int(row0), g.emb32.data_ptr(), g.emb32.stride(0),
         _lib.ptr(g.emb16), g.emb16.stride(0) if g.emb16 is not None else 0,
         g.emb8.data_ptr() if i8 else None, g.emb8.stride(0) if i8 else 0, g.rs8.data_ptr() if i8 else None,
         g.sqn.data_ptr(), g.sumsq.data_ptr(), g._rs8_max.data_ptr() if i8 else None, dv_max.data_ptr(),
-        _lib.stream_ptr(x.device)), "lzk_tg_write_emb")
+        g.has_emb.data_ptr() if has_emb else None, _lib.stream_ptr(x.device)), "lzk_tg_write_emb")
     if g.emb8 is not None and not i8:  # fp8 copy: the torch quantiser
         g._write_lowp(r, x * h[:, None].to(x.dtype) if h is not None else x)
