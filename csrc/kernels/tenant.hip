@@ -620,20 +620,23 @@ __global__ __launch_bounds__(NTB) void tg_clear_bits_kernel(const long* __restri
 // within the first chunk or two. out[] must be pre-filled with -1.
 constexpr int FR_NT = 1024;
 constexpr int FR_MAXT = 64;
+struct FrTargets {  // by value (kernel arguments): no host -> device copy
+  int nt;
+  int tc[FR_MAXT], tt[FR_MAXT], to[FR_MAXT];
+};
 __global__ __launch_bounds__(FR_NT) void tg_first_rows_kernel(const unsigned char* __restrict__ kind,
                                                               const unsigned char* __restrict__ sup,
-                                                              const int* __restrict__ shard, long n,
-                                                              const int* __restrict__ tc, const int* __restrict__ tt,
-                                                              const int* __restrict__ to, int nt,
+                                                              const int* __restrict__ shard, long n, FrTargets T,
                                                               long* __restrict__ out) {
   __shared__ int s_tc[FR_MAXT], s_tt[FR_MAXT], s_to[FR_MAXT], s_found[FR_MAXT];
   __shared__ int s_w[FR_NT / 64];
   __shared__ int s_open;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nt = T.nt;
   for (int t = threadIdx.x; t < nt; t += FR_NT) {
-    s_tc[t] = tc[t];
-    s_tt[t] = tt[t];
-    s_to[t] = to[t];
+    s_tc[t] = T.tc[t];
+    s_tt[t] = T.tt[t];
+    s_to[t] = T.to[t];
     s_found[t] = 0;
   }
   __syncthreads();
@@ -667,6 +670,9 @@ __global__ __launch_bounds__(FR_NT) void tg_first_rows_kernel(const unsigned cha
     __syncthreads();
     if (!s_open) break;
   }
+  // targets not met (inconsistent counts): their remaining slots read -1
+  for (int t = 0; t < nt; ++t)
+    for (int i = s_found[t] + threadIdx.x; i < s_tt[t]; i += FR_NT) out[s_to[t] + i] = -1;
 }
 
 }  // namespace
@@ -838,12 +844,19 @@ LZK_EXPORT int lzk_cos_rerank64(const double* Qn, long ldq, const float* X, long
 
 // First shard-node rows (tg_first_rows_kernel): nt <= 64 targets, out[sum tt]
 // pre-filled with -1 by the caller. One block, no host synchronisation.
+// tc / tt / to: HOST arrays of the nt targets (passed by value to the kernel).
 LZK_EXPORT int lzk_tg_first_rows(const unsigned char* kind, const unsigned char* sup, const int* shard, long n,
                                  const int* tc, const int* tt, const int* to, int nt, long* out, void* stream) {
   if (nt <= 0) return 0;
   if (nt > FR_MAXT || n < 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(tg_first_rows_kernel, dim3(1), dim3(FR_NT), 0, (hipStream_t)stream, kind, sup, shard, n, tc, tt,
-                     to, nt, out);
+  FrTargets T;
+  T.nt = nt;
+  for (int t = 0; t < nt; ++t) {
+    T.tc[t] = tc[t];
+    T.tt[t] = tt[t];
+    T.to[t] = to[t];
+  }
+  hipLaunchKernelGGL(tg_first_rows_kernel, dim3(1), dim3(FR_NT), 0, (hipStream_t)stream, kind, sup, shard, n, T, out);
   return (int)hipGetLastError();
 }
 

@@ -944,10 +944,8 @@ class TenantGraph:
         if len(tgt) > 64:
             return None
         with self.on_stream():
-            tv = T.to_dev_packed([np.asarray(x) for x in zip(*tgt)], dev)
-            ti = torch.stack(tv).to(torch.int32)
-            out = torch.full((off,), -1, dtype=torch.long, device=dev)
-            T.first_rows(self.kind, self.sup, self.shard, self.n, ti, out)
+            out = torch.empty(off, dtype=torch.long, device=dev)
+            T.first_rows(self.kind, self.sup, self.shard, self.n, np.asarray(tgt, dtype=np.int32).T, out)
         return out
 
     def first_rows_capture(self, k: int) -> Capture:

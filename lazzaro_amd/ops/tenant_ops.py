@@ -534,18 +534,18 @@ def component_digest_local(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor
     return torch.stack([ks, grow])
 
 
-def first_rows(kind: torch.Tensor, sup: torch.Tensor, shard: torch.Tensor, n: int, tgt: torch.Tensor,
+def first_rows(kind: torch.Tensor, sup: torch.Tensor, shard: torch.Tensor, n: int, tgt: np.ndarray,
                out: torch.Tensor) -> None:
-    """tenant.hip tg_first_rows_kernel: ``tgt`` int32 [3, nt] device (shard
-    code, rows wanted, output offset) per target shard in code order; ``out``
-    int64 [sum wanted] pre-filled with -1 receives each target's first live
-    shard-node rows in row order."""
+    """tenant.hip tg_first_rows_kernel: ``tgt`` host int32 [3, nt] (shard
+    code, rows wanted, output offset) per target shard in code order, passed
+    to the kernel by value; ``out`` int64 [sum wanted] receives each target's
+    first live shard-node rows in row order (-1 where a target falls short)."""
     nt = int(tgt.shape[1])
     if nt == 0:
         return
-    tgt = tgt.contiguous()
+    tgt = np.ascontiguousarray(tgt, dtype=np.int32)
     _lib.check(_lib.lib().lzk_tg_first_rows(kind.data_ptr(), sup.data_ptr(), shard.data_ptr(), int(n),
-                                            tgt[0].data_ptr(), tgt[1].data_ptr(), tgt[2].data_ptr(), nt,
+                                            tgt[0].ctypes.data, tgt[1].ctypes.data, tgt[2].ctypes.data, nt,
                                             out.data_ptr(), _st(out)), "tg_first_rows")
 
 
