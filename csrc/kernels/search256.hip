@@ -625,9 +625,16 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
                                                            const float* __restrict__ bias, float alpha,
                                                            const int* __restrict__ cnt, int cap,
                                                            float* __restrict__ cs, const int* __restrict__ ci,
-                                                           const float* __restrict__ cut, float floor) {
+                                                           const float* __restrict__ cut, float floor,
+                                                           const float* __restrict__ tau, int k_need,
+                                                           int need_val, int* __restrict__ need) {
+  __shared__ int s_hits;
   const int q = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_hits = 0;
+  __syncthreads();
+  const float tq = tau ? tau[q] : LZK_NEG_INF;
+  int hits = 0;
   const int n = min(cnt[q] & 0x3fffffff, cap);
   const int chunks = D >> 2;  // 4 elements per chunk
   constexpr int MAXC = 8;     // D <= 64 * 4 * MAXC = 2048
@@ -669,7 +676,16 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
     const float sc = alpha * acc + (bias ? bias[r] : 0.f);
     if (lane == 0) cs[idx] = sc >= floor ? sc : LZK_NEG_INF;  // below the caller's floor: dropped
+    hits += (sc >= floor && sc >= tq) ? 1 : 0;  // wave-uniform (sc is the reduced sum)
     }
+  }
+  // speculative-threshold check of the store search: the list is kept only
+  // when k_need re-scored entries reach tau (else need_val sends the query
+  // to the exact fallback)
+  if (need) {
+    if (lane == 0 && hits) atomicAdd(&s_hits, hits);
+    __syncthreads();
+    if (threadIdx.x == 0) need[q] = s_hits >= k_need ? 0 : need_val;
   }
 }
 
@@ -957,10 +973,10 @@ LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
 // Exact bf16 re-score of candidate lists in place (see cand_rescore_kernel).
 LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long ldq, int nq, int D, const float* bias,
                                 float alpha, const int* cnt, int cap, float* cs, const int* ci, const float* cut,
-                                float floor, void* stream) {
+                                float floor, const float* tau, int k_need, int need_val, int* need, void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(cand_rescore_kernel<false>, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, X16, ldx,
-                     Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor);
+                     Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need, need_val, need);
   return (int)hipGetLastError();
 }
 
@@ -968,10 +984,11 @@ LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long
 // queries (Q32 [nq, ldq]): lean tenants without a bf16 copy. D % 4 == 0.
 LZK_EXPORT int lzk_cand_rescore32(const float* X32, long ldx, const float* Q32, long ldq, int nq, int D,
                                   const float* bias, float alpha, const int* cnt, int cap, float* cs, const int* ci,
-                                  const float* cut, float floor, void* stream) {
+                                  const float* cut, float floor, const float* tau, int k_need, int need_val,
+                                  int* need, void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0 || ldx % 4 != 0 || ldq % 4 != 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(cand_rescore_kernel<true>, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, X32, ldx, Q32,
-                     ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor);
+                     ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need, need_val, need);
   return (int)hipGetLastError();
 }
 

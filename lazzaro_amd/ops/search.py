@@ -331,9 +331,11 @@ _lib.register("lzk_flat_cand_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
                                            _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
 _lib.register("lzk_cand_grid_f8", _lib.I, [_lib.I, _lib.I])
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
-                                           _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P])
+                                           _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.I, _lib.I, _lib.P,
+                                           _lib.P])
 _lib.register("lzk_cand_rescore32", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
-                                             _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P])
+                                             _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.I, _lib.I, _lib.P,
+                                             _lib.P])
 
 
 def bf16_rows(X32: torch.Tensor, Dp: int) -> torch.Tensor:
@@ -495,7 +497,7 @@ def flat_topk_fp8(X8: torch.Tensor, Q8: torch.Tensor, scale2: float, X16: torch.
                                  ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
     _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
                                   _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(), None,
-                                  float("-inf"), st), "lzk_cand_rescore")
+                                  float("-inf"), None, 0, 0, None, st), "lzk_cand_rescore")
     return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
 
 
@@ -568,18 +570,16 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
     qs = qscale.contiguous()
 
+    # Speculative threshold check (in the re-score kernel): a query keeps its
+    # list only when at least k entries have exact (re-scored) scores >= tau
+    # -- then the true k-th score is >= tau, every true top-k row has int8
+    # score >= tau - margin (so it is in the list) and lies above the
+    # re-score cut; otherwise need = cap + 1 flags it for the exact fallback.
+    need = torch.empty(nq, dtype=torch.int32, device=dev) if spec else None
+    chk = (tau, k, cap + 1, need) if spec else None
+
     def need_of():
-        """Speculative threshold check: a query keeps its list only when at
-        least k entries have exact (re-scored) scores >= tau -- then the true
-        k-th score is >= tau, every true top-k row has int8 score >= tau -
-        margin (so it is in the list) and lies above the re-score cut;
-        otherwise need = cap + 1 flags it for the exact fallback."""
-        if not spec:
-            return None
-        c = (cnt & 0x3FFFFFFF).clamp_max(cap)
-        valid = torch.arange(cap, device=dev)[None, :] < c[:, None]
-        hit = ((cs.view(nq, cap) >= tau[:, None]) & valid).sum(1)
-        return torch.where(hit >= k, torch.zeros_like(hit), torch.full_like(hit, cap + 1)).to(torch.int32)
+        return need
     if nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
         _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
@@ -587,7 +587,7 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     if _use_scan8(Dp):
         _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, None, None, None, kslot, 2 * S, 1, cap, (cnt, cs, ci),
                None)
-        _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
+        _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, chk=chk)
         return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap,
                                      need=need_of())
     grid = L.lzk_cand_grid_f8(N, nq)
@@ -599,7 +599,7 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
                "lzk_flat_cand_i8")
     _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
                                  ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
-    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, chk=chk)
     return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap, need=need_of())
 
 
@@ -609,10 +609,14 @@ SPEC_J = int(os.environ.get("LZK_SPEC_J", "5"))
 SPEC_MIN_STRIDE = 32
 
 
-def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None):
+def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None, chk=None):
     """int8 candidate lists -> exact bf16 scores for the entries that can
     still reach the query's top-k: cut = (k-th best int8 score) - 2 * margin
-    (see :func:`flat_topk_i8`); the others become -inf without a row read."""
+    (see :func:`flat_topk_i8`); the others become -inf without a row read.
+    ``chk`` = (tau [nq], k, need_val, need [nq] int32): need[q] = 0 when k
+    re-scored entries reach tau[q], else need_val (speculative threshold)."""
+    tau_p, k_need, need_val, need_p = (None, 0, 0, None) if chk is None else (
+        chk[0].data_ptr(), int(chk[1]), int(chk[2]), chk[3].data_ptr())
     L = _lib.lib()
     nq, Dp = Q16.shape
     dev = Q16.device
@@ -632,11 +636,12 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
         X32, Q32 = X16.X32, X16.Q32
         _lib.check(L.lzk_cand_rescore32(X32.data_ptr(), X32.stride(0), Q32.data_ptr(), Q32.stride(0), nq,
                                         X32.shape[1], _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap,
-                                        cs.data_ptr(), ci.data_ptr(), _lib.ptr(cut), fl, st), "lzk_cand_rescore32")
+                                        cs.data_ptr(), ci.data_ptr(), _lib.ptr(cut), fl, tau_p, k_need, need_val,
+                                        need_p, st), "lzk_cand_rescore32")
         return
     _lib.check(L.lzk_cand_rescore(X16.data_ptr(), X16.stride(0), Q16.data_ptr(), Q16.stride(0), nq, Dp,
                                   _lib.ptr(bias), float(alpha), cnt.data_ptr(), cap, cs.data_ptr(), ci.data_ptr(),
-                                  _lib.ptr(cut), fl, st), "lzk_cand_rescore")
+                                  _lib.ptr(cut), fl, tau_p, k_need, need_val, need_p, st), "lzk_cand_rescore")
 
 
 def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
