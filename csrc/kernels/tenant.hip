@@ -172,7 +172,9 @@ __global__ __launch_bounds__(NTB) void tg_compact_kernel(const unsigned char* __
                                                          const double* __restrict__ lu, const int* __restrict__ meta,
                                                          int* __restrict__ osrc, int* __restrict__ odst,
                                                          float* __restrict__ ow, int* __restrict__ oco,
-                                                         double* __restrict__ olu, int* __restrict__ ometa) {
+                                                         double* __restrict__ olu, int* __restrict__ ometa,
+                                                         int* __restrict__ dsrc, int* __restrict__ ddst,
+                                                         int* __restrict__ dmeta) {
   __shared__ int wpre[NTB / 64];
   const long e = (long)blockIdx.x * NTB + threadIdx.x;
   const int f = (e < ne) ? flag[e] : 0;
@@ -191,6 +193,11 @@ __global__ __launch_bounds__(NTB) void tg_compact_kernel(const unsigned char* __
     oco[o] = co[e];
     olu[o] = lu[e];
     ometa[o] = meta[e];
+  } else if (dsrc && e < ne) {  // the dropped edges in order: index e - (kept before e)
+    const long o = e - (off + before);
+    dsrc[o] = src[e];
+    ddst[o] = dst[e];
+    dmeta[o] = meta[e];
   }
 }
 
@@ -720,10 +727,11 @@ LZK_EXPORT int lzk_pack_bits(const unsigned char* f, long n, unsigned* bits, voi
 
 LZK_EXPORT int lzk_tg_compact(const unsigned char* flag, const int* block_off, long ne, const int* src, const int* dst,
                               const float* w, const int* co, const double* lu, const int* meta, int* osrc, int* odst,
-                              float* ow, int* oco, double* olu, int* ometa, void* stream) {
+                              float* ow, int* oco, double* olu, int* ometa, int* dsrc, int* ddst, int* dmeta,
+                              void* stream) {
   if (ne == 0) return 0;
   hipLaunchKernelGGL(tg_compact_kernel, dim3(blocks_for(ne)), dim3(NTB), 0, (hipStream_t)stream, flag, block_off, ne,
-                     src, dst, w, co, lu, meta, osrc, odst, ow, oco, olu, ometa);
+                     src, dst, w, co, lu, meta, osrc, odst, ow, oco, olu, ometa, dsrc, ddst, dmeta);
   return (int)hipGetLastError();
 }
 

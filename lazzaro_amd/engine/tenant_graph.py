@@ -1438,11 +1438,11 @@ class TenantGraph:
             if ne:
                 n_out = int(info_h[3 * nc])
                 if n_out != ne:
-                    old = self.e
-                    out, n = T._compact(old, flag, bc, ne, extra=max(ne >> 3, self.EDGE_SLACK_MIN), n_out=n_out)
+                    out, n, dr = T._compact(self.e, flag, bc, ne, extra=max(ne >> 3, self.EDGE_SLACK_MIN),
+                                            n_out=n_out, dropped=self.track)
                     self._adopt_edges(out)
-                    if self.track:
-                        self._note_dropped(*T._dropped(old, flag, ne, n))
+                    if dr is not None:
+                        self._note_dropped(*dr)
         if nc:
             kinds, sups, shards = info_h[:nc], info_h[nc:2 * nc], info_h[2 * nc:3 * nc]
             for r, k, sp, sh in zip(cand, kinds.tolist(), sups.tolist(), shards.tolist()):

@@ -26,7 +26,7 @@ _lib.register("lzk_tg_write_emb", I, [P, L, P, I, I, P, L, P, L, P, L, P, L, P, 
 _lib.register("lzk_tg_set_rows", I, [P, L, I, P, I, P, P, P, P, P, P, P, P, P, P, P, I, I, P])
 _lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
-_lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P])
+_lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
 _lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
@@ -69,12 +69,13 @@ def to_dev_packed(cols: Sequence, dev) -> List[torch.Tensor]:
 
 
 def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, ne: int, extra: int = 0,
-             total: Optional[torch.Tensor] = None, n_out: Optional[int] = None):
+             total: Optional[torch.Tensor] = None, n_out: Optional[int] = None, dropped: bool = False):
     """Stable device compaction of the flagged edges (scan + scatter). With
     ``extra`` each output column is a view of a buffer ``extra`` rows longer
     (room for appends without a copy, :meth:`TenantGraph._edge_append`).
     ``total`` / ``n_out``: the block counts were already scanned and the
-    survivor count read by the caller."""
+    survivor count read by the caller. ``dropped``: also return (src, dst,
+    meta) of the removed edges in order, written by the same pass."""
     L_ = _lib.lib()
     dev = e["src"].device
     if n_out is None:
@@ -82,12 +83,13 @@ def _compact(e: Dict[str, torch.Tensor], flag: torch.Tensor, bc: torch.Tensor, n
         _lib.check(L_.lzk_scan_blocks(bc.data_ptr(), bc.numel(), total.data_ptr(), _st(bc)), "scan_blocks")
         n_out = int(total.item())
     if n_out == ne:
-        return e, 0
+        return (e, 0, None) if dropped else (e, 0)
     out = {k: torch.empty(n_out + extra, dtype=e[k].dtype, device=dev)[:n_out] for k in EDGE_COLS}
-    if n_out:
-        _lib.check(L_.lzk_tg_compact(flag.data_ptr(), bc.data_ptr(), ne, *(e[k].data_ptr() for k in EDGE_COLS),
-                                     *(out[k].data_ptr() for k in EDGE_COLS), _st(flag)), "tg_compact")
-    return out, ne - n_out
+    dr = [torch.empty(ne - n_out, dtype=torch.int32, device=dev) for _ in range(3)] if dropped else None
+    _lib.check(L_.lzk_tg_compact(flag.data_ptr(), bc.data_ptr(), ne, *(e[k].data_ptr() for k in EDGE_COLS),
+                                 *(out[k].data_ptr() for k in EDGE_COLS),
+                                 *((d.data_ptr() for d in dr) if dr else (None, None, None)), _st(flag)), "tg_compact")
+    return (out, ne - n_out, tuple(dr) if dr else None) if dropped else (out, ne - n_out)
 
 
 def decay_prune(e: Dict[str, torch.Tensor], sal, kind, sup, rate: float, threshold: Optional[float],
