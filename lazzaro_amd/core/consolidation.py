@@ -1119,7 +1119,7 @@ class ConsolidationMixin:
             pruned = g.segment_end(tok, vic, unstore=True)
         if ids:
             with tracer.stage("ap_store_delete", "cpu"):
-                self._store_delete(ids)
+                self._store_delete(ids, graph_unstored=True)
         return pruned
 
     def _consolidate_batch_coarse(self, facts: List[Dict], conv: np.ndarray, B: int, embs, now: float,

@@ -332,9 +332,14 @@ class MemorySystem(ConsolidationMixin):
             return fn(embs, user_id=self.user_id, limit=k)
         return [self.vector_store.search_nodes(e, user_id=self.user_id, limit=k) for e in embs]
 
-    def _store_delete(self, ids: List[str]) -> None:
+    def _store_delete(self, ids: List[str], graph_unstored: bool = False) -> None:
+        """``graph_unstored``: the rows' stored bits are already cleared in
+        the bound graph (segment ends), so the bound store skips that step."""
         if ids:
-            self.vector_store.delete_nodes(ids, user_id=self.user_id)
+            if graph_unstored and self._store_binds_graph():
+                self.vector_store.delete_nodes(ids, user_id=self.user_id, graph_unstored=True)
+            else:
+                self.vector_store.delete_nodes(ids, user_id=self.user_id)
 
     def _store_add_rows(self, rows: List[int], dicts: List[Dict]) -> None:
         """Re-add rows to the store (merge): the bound store only flags them;

@@ -322,7 +322,11 @@ class HBMStore:
             out.append([a.ids[x] for x, v in zip(rs, ss) if x >= 0 and v != float("-inf") and a.ids[x] is not None])
         return out
 
-    def delete_nodes(self, node_ids: Optional[List[str]], user_id: str = "default") -> None:
+    def delete_nodes(self, node_ids: Optional[List[str]], user_id: str = "default",
+                     graph_unstored: bool = False) -> None:
+        """``graph_unstored``: the bound graph already cleared the rows'
+        stored bits (TenantGraph.segment_end(unstore=True)); only the
+        persisted table rows go."""
         g = self._graphs.get(user_id)
         if g is not None:
             with self._lock:
@@ -331,7 +335,8 @@ class HBMStore:
                     g.unstore(list(g.ids))
                 else:
                     self._nodes_table.delete([("user_id", user_id)], "id", list(node_ids))
-                    g.unstore(node_ids)
+                    if not graph_unstored:
+                        g.unstore(node_ids)
             return
         with self._lock:
             a = self._arena(user_id)

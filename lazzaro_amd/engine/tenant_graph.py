@@ -1270,8 +1270,12 @@ class TenantGraph:
         if self._drop_pending:
             pend, self._drop_pending = self._drop_pending, []
             with self.on_stream():
-                for s, d, meta in pend:
-                    self._resolve_dropped(s, d, meta)
+                if len(pend) > 1 and all(m is not None for _, _, m in pend):
+                    # one device -> host copy for every pending batch (in order)
+                    self._resolve_dropped(*(torch.cat([p[i].to(torch.int32) for p in pend]) for i in range(3)))
+                else:
+                    for s, d, meta in pend:
+                        self._resolve_dropped(s, d, meta)
         return self._deleted_edges
 
     @deleted_edges.setter

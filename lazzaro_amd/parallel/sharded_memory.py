@@ -1179,7 +1179,7 @@ class ShardedMemorySystem:
         ids = [g.ids[r] for r in loc_v]
         pruned = g.segment_end(tok, loc_v, unstore=True)
         if ids:
-            self.local._store_delete(ids)
+            self.local._store_delete(ids, graph_unstored=True)
         if other.size and g.num_edges:  # edges here that point at a victim held elsewhere
             rows = self._rows_of_nums(torch.as_tensor(other + 1).to(dev))
             rows = rows[rows >= 0]
