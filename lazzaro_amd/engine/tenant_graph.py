@@ -93,11 +93,20 @@ LOWP_RIGOROUS = os.environ.get("LZK_LOWP_RIGOROUS", "0") == "1"
 # batches below LOWP_MIN_Q (the interactive turn) take the HBM-bound narrow
 # int8 scan (scan8.hip scan8_narrow_kernel); LZK_LOWP_NARROW=0: the bf16 lane kernel
 LOWP_NARROW = os.environ.get("LZK_LOWP_NARROW", "1") != "0"
-# consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8). Off
-# by default: bench/bench_consolidate.py (random fact vectors) 17.3 -> 11.6 ms
-# per step's scan, but the clustered-topic row-sharded run of bench.py went
-# 175 -> 243 ms per step (profiles/r3_session2/README.md); LZK_DUAL_LOWP=1 on
-DUAL_LOWP = os.environ.get("LZK_DUAL_LOWP", "0") == "1"
+# consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8).
+# LZK_DUAL_LOWP=1 always, 0 never, default "auto": int8 while its lists stay
+# short, bf16 for the next DUAL_BACKOFF calls of a tenant whose last int8 call
+# overflowed lists or averaged more than a quarter of the list capacity.
+# Measured: random fact vectors (bench/bench_consolidate.py) 1881 -> 2075
+# conversations/s with int8; the clustered-topic row-sharded run lost with it
+# (437.9 -> 391.4/s, profiles/r4/sharded_clustered_dual_lowp_*.json): facts
+# near a topic centre clear their (link-floor) threshold on thousands of rows,
+# so the lists fill up and the re-score / exact fallback outweigh the scan.
+_DL = os.environ.get("LZK_DUAL_LOWP", "auto")
+DUAL_LOWP = _DL != "0"
+DUAL_LOWP_AUTO = _DL not in ("0", "1")
+DUAL_OVF_MAX = 0.02
+DUAL_BACKOFF = 16
 # Lean HBM layout (LZK_LEAN_HBM=1 / TenantGraph.LEAN_HBM): a tenant with the
 # int8 scan copy and at least LOWP_MIN_ROWS rows of capacity keeps NO bf16
 # copy -- fp32 (the store's precision) + int8 + scale, ~5 bytes per dimension
@@ -1895,13 +1904,17 @@ class TenantGraph:
                 ql = dual_label.to(dev, torch.int32).contiguous()
                 floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
                 if lean or (DUAL_LOWP and self.emb8 is not None and self.emb8.dtype == torch.int8
-                            and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS):
+                            and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS
+                            and self._dual_lowp_ok()):
                     # the int8 dual scan: same lists (error cut + bf16 re-score)
                     from ..ops.search import flat_topk_dual_i8
                     q8, qs, margin = self._i8_query(q16, 1.0)
+                    st = [] if (DUAL_LOWP_AUTO and not lean) else None
                     (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
                                                          row_label=lab.contiguous(), q_label=ql, bias=bias,
-                                                         margin=margin, floor=floor)
+                                                         margin=margin, floor=floor, stats=st)
+                    if st:
+                        self._dual_stats = st
                 else:
                     (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
                                                       bias=bias, floor=floor)
@@ -1917,6 +1930,29 @@ class TenantGraph:
             ql = dual_label.to(dev, torch.int32)
             return (self._exact_cos(Qn, mask, k), self._exact_cos(Qn, mask, k, row_label=lab, q_label=ql))
         return self._exact_cos(Qn, mask, k)
+
+    _dual_stats = None  # (ovf, cnt) x 2 + cap of the last int8 dual scan (auto mode)
+    _dual_bf16 = 0  # calls left on the bf16 dual scan (auto mode back-off)
+
+    def _dual_lowp_ok(self) -> bool:
+        """Auto mode: read the last int8 dual call's list statistics (its
+        kernels finished long ago) and back off to bf16 for DUAL_BACKOFF
+        calls when lists overflowed or ran long."""
+        if not DUAL_LOWP_AUTO:
+            return True
+        if self._dual_stats is not None:
+            (oa, ca), (ob, cb), cap = self._dual_stats
+            self._dual_stats = None
+            with self.on_stream():
+                m = torch.stack([((oa != 0) | (ob != 0)).float().mean(),
+                                 ((ca & 0x3FFFFFFF).clamp_max(cap).float().mean()
+                                  + (cb & 0x3FFFFFFF).clamp_max(cap).float().mean()) / (2 * cap)]).cpu()
+            if float(m[0]) > DUAL_OVF_MAX or float(m[1]) > 0.25:
+                self._dual_bf16 = DUAL_BACKOFF
+        if self._dual_bf16 > 0:
+            self._dual_bf16 -= 1
+            return False
+        return True
 
     def store_bias(self, metric: str) -> torch.Tensor:
         """Per-row fp32 score bias of the store search: -inf for rows not in

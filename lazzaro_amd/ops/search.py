@@ -229,7 +229,7 @@ def _cand_lists(dev, nq, cap, slot):
 
 
 def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset, cnt, cs, ci, cap,
-                          need=None):
+                          need=None, ovf_sink=None):
     """Exact per-query select from a candidate list; queries whose list
     overflowed -- or, with ``need``, holds fewer than need[q] entries (a
     speculative threshold that turned out too high) -- are recomputed by the
@@ -247,6 +247,8 @@ def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_o
     rc = L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, int(k),
                            int(idx_offset), os_.data_ptr(), oi.data_ptr(), ovf.data_ptr(), _lib.ptr(need), st)
     _lib.check(rc, "lzk_cand_select")
+    if ovf_sink is not None:  # the caller's view of the lists: (overflowed query flags, list lengths)
+        ovf_sink.append((ovf, cnt))
     if isinstance(X, LeanRows):
         _lean_fallback(X, Q, k, bias, row_label, q_label, alpha, idx_offset, os_, oi, ovf)
         return os_, oi
@@ -646,12 +648,13 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
 
 def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
                       X16: torch.Tensor, Q16: torch.Tensor, k: int, *, row_label, q_label, bias=None,
-                      alpha: float = 1.0, margin=None, floor: float = None):
+                      alpha: float = 1.0, margin=None, floor: float = None, stats: Optional[list] = None):
     """:func:`flat_topk_dual` with the candidate scan on the int8 MFMA (the
     rows' int8 copy, see :func:`flat_topk_i8`): both thresholds (the sampled
     bf16 k-th bests, raised to ``floor``) are lowered by ``margin``, both lists
     are re-scored from the bf16 rows above their error cut, then selected
-    exactly -- the same lists as the bf16 dual scan.
+    exactly -- the same lists as the bf16 dual scan. ``stats``: receives the
+    (overflow flags, list lengths) device tensors of both lists.
     Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
     L = _lib.lib()
     nq, Dp = Q16.shape
@@ -681,8 +684,10 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
                           ca, cb)
     _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *ca, cap, floor=floor)
     _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *cb, cap, floor=floor)
-    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap)
-    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap)
+    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap, ovf_sink=stats)
+    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap, ovf_sink=stats)
+    if stats is not None:
+        stats.append(cap)
     return ra, rb
 
 
