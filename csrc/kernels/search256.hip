@@ -689,6 +689,68 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
   }
 }
 
+// Query side of the int8 store search in one launch per batch (one block
+// per query): symmetric per-row int8 of the bf16 query (s = max|q| / 127,
+// q8 = rint(q / s) clamped to +-127, s = 0 for a zero row -- ops.search
+// quantize_i8_rows) and the error-model margin of TenantGraph._i8_query:
+// eta = q8 s - q; floor = smax / 2 * sum|eta|; statistical (rig = 0):
+// |alpha| (z sqrt(sum eta^2 mu2 + sum q^2 smax^2 / 12) + floor) with mu2 the
+// rows' per-dimension mean square (sumsq / nsq); worst case (rig = 1):
+// |alpha| (|eta| xn + smax / 2 sum|q| + floor) (1 + 1e-5) + 1e-6. A batch of
+// one query was ~25 torch launches of a few elements each.
+__global__ __launch_bounds__(256) void i8_query_kernel(const u16* __restrict__ q16, long ldq, int Dp, int d,
+                                                       const double* __restrict__ sumsq, double inv_nsq,
+                                                       const float* __restrict__ smax_p, float alpha_abs, float z,
+                                                       int rig, float xn, signed char* __restrict__ q8, long ld8,
+                                                       float* __restrict__ qs, float* __restrict__ margin) {
+  __shared__ float s_f[4];
+  __shared__ double s_d[4][4];
+  const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const u16* row = q16 + (long)q * ldq;
+  float am = 0.f;
+  for (int c = t; c < Dp; c += 256) am = fmaxf(am, fabsf(bf16_to_f32(row[c])));
+  for (int o = 32; o >= 1; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+  if (lane == 0) s_f[w] = am;
+  __syncthreads();
+  am = fmaxf(fmaxf(s_f[0], s_f[1]), fmaxf(s_f[2], s_f[3]));
+  const float sc = am > 0.f ? am / 127.0f : 0.f;
+  const float den = am > 0.f ? sc : 1.f;
+  double a_eta = 0.0, v1 = 0.0, q2 = 0.0, e2 = 0.0;
+  for (int c = t; c < Dp; c += 256) {
+    const float x = bf16_to_f32(row[c]);
+    const float qq = fminf(fmaxf(rintf(x / den), -127.f), 127.f);
+    q8[(long)q * ld8 + c] = (signed char)qq;
+    const float eta = __fsub_rn(__fmul_rn(qq, sc), x);
+    a_eta += fabs((double)eta);
+    q2 += rig ? fabs((double)x) : (double)x * (double)x;
+    if (c < d) {
+      const double e = (double)eta * (double)eta;
+      e2 += e;
+      if (!rig) v1 += e * (double)(float)(sumsq[c] * inv_nsq);
+    }
+  }
+  double vals[4] = {a_eta, v1, q2, e2};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double v = vals[k];
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_d[k][w] = v;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = s_d[k][0] + s_d[k][1] + s_d[k][2] + s_d[k][3];
+    const double smax = (double)smax_p[0];
+    const double fl = 0.5 * smax * r[0];
+    double m;
+    if (rig) m = alpha_abs * (sqrt(r[3]) * xn + 0.5 * smax * r[2] + fl) * (1.0 + 1e-5) + 1e-6;
+    else m = alpha_abs * (z * sqrt(r[1] + r[2] * (smax * smax / 12.0)) + fl);
+    qs[q] = sc;
+    margin[q] = (float)m;
+  }
+}
+
 }  // namespace
 
 // Exact argmax of Q @ X.T per query (no bias/labels). ws: [nq] u64 scratch.
@@ -1075,5 +1137,16 @@ LZK_EXPORT int lzk_flat_cand_dual_i8(const void* X8, long ldx_bytes, int nrows, 
   if (bias) LZK_GDI(true);
   else LZK_GDI(false);
 #undef LZK_GDI
+  return (int)hipGetLastError();
+}
+
+// int8 query + error margin of the store search (i8_query_kernel).
+LZK_EXPORT int lzk_i8_query(const void* q16, long ldq, int nq, int Dp, int d, const double* sumsq, double inv_nsq,
+                            const float* smax, float alpha_abs, float z, int rig, float xn, void* q8, long ld8,
+                            float* qs, float* margin, void* stream) {
+  if (nq <= 0) return 0;
+  if (Dp <= 0 || d > Dp || !sumsq || !smax) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(i8_query_kernel, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, (const u16*)q16, ldq, Dp,
+                     d, sumsq, inv_nsq, smax, alpha_abs, z, rig, xn, (signed char*)q8, ld8, qs, margin);
   return (int)hipGetLastError();
 }

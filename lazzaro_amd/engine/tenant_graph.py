@@ -119,6 +119,8 @@ LEAN_HBM = os.environ.get("LZK_LEAN_HBM", "0") == "1"
 WRITE_EMB_MAX_ROWS = 8192
 # node columns of an insert in one launch (tenant.hip tg_set_rows_kernel); 0 = per-column writes
 SET_ROWS_KERNEL = os.environ.get("LZK_SET_ROWS", "1") != "0"
+# the int8 search's query quantisation + margin in one launch (LZK_I8_QUERY=0: torch ops)
+I8_QUERY_KERNEL = os.environ.get("LZK_I8_QUERY", "1") != "0"
 # consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (LZK_SEG_END=0: the torch formulation)
 SEG_END_KERNEL = os.environ.get("LZK_SEG_END", "1") != "0"
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
@@ -2066,8 +2068,12 @@ class TenantGraph:
     def _i8_query(self, q16: torch.Tensor, alpha: float):
         """int8 queries + per-query scales + the error-model margin of
         :meth:`_i8_candidates` (device tensors, no host sync)."""
-        from ..ops.search import quantize_i8_rows
+        from ..ops.search import i8_query, quantize_i8_rows
         d = self.dim
+        if self.on_gpu and I8_QUERY_KERNEL:  # one launch (search256.hip i8_query_kernel)
+            rig = bool(LOWP_RIGOROUS or getattr(self, "LOWP_RIGOROUS", False))
+            xn = (1.0 + self.max_norm_dev + 2.0 ** -7) if rig else 1.0
+            return i8_query(q16, d, self.sumsq, self.n_sumsq, self._rs8_max, alpha, LOWP_MARGIN_Z, rig, xn)
         q8, qs = quantize_i8_rows(q16)
         eta = q8.float() * qs[:, None] - q16.float()
         mu2 = (self.sumsq / max(self.n_sumsq, 1)).float()

@@ -29,6 +29,7 @@ P = C.c_void_p
 I = C.c_int
 L = C.c_long
 F = C.c_float
+D = C.c_double
 
 # name -> (restype, argtypes)
 _SIGS = {

@@ -198,12 +198,36 @@ def _flat_topk_lane(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset,
                                  _lib.ptr(bias), _lib.ptr(row_label), _lib.ptr(q_label),
                                  float(alpha), D, kslot, nch, ps.data_ptr(), pi.data_ptr(), st)
     _lib.check(rc, "lzk_flat_topk_partial")
+    ncand = nch * kslot
+    G = _merge_groups(nq, nch)
+    if G > 1:
+        # few queries, many partial lists (the 1/S sample of a narrow batch:
+        # 512 chunks x 16 = 8192 candidates on ONE wave took 163 us): merge
+        # G groups per query on G waves, then their G x kslot survivors
+        os1 = torch.empty((nq * G, kslot), dtype=torch.float32, device=dev)
+        oi1 = torch.empty((nq * G, kslot), dtype=torch.long, device=dev)
+        _lib.check(L.lzk_topk_merge(ps.data_ptr(), pi.data_ptr(), ncand // G, nq * G, kslot, kslot, 0,
+                                    os1.data_ptr(), oi1.data_ptr(), st), "lzk_topk_merge")
+        ps, pi, ncand = os1, oi1.to(torch.int32), G * kslot
     os_ = torch.empty((nq, k), dtype=torch.float32, device=dev)
     oi = torch.empty((nq, k), dtype=torch.long, device=dev)
-    rc = L.lzk_topk_merge(ps.data_ptr(), pi.data_ptr(), nch * kslot, nq, kslot, int(k),
+    rc = L.lzk_topk_merge(ps.data_ptr(), pi.data_ptr(), ncand, nq, kslot, int(k),
                           int(idx_offset), os_.data_ptr(), oi.data_ptr(), st)
     _lib.check(rc, "lzk_topk_merge")
     return os_, oi
+
+
+def _merge_groups(nq: int, nch: int) -> int:
+    """Groups per query of the two-level partial-list merge: only when the
+    queries alone leave the chip mostly idle (< 64 merge waves); the largest
+    divisor G <= 64 of nch that keeps >= 8 chunks per group and <= 512
+    first-level waves."""
+    if nq >= 64 or nch < 16:
+        return 1
+    for G in range(min(64, nch // 8, 512 // max(nq, 1)), 1, -1):
+        if nch % G == 0:
+            return G
+    return 1
 
 
 def _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S):
@@ -384,6 +408,8 @@ _lib.register("lzk_cos_rerank64", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.
                                            _lib.I, _lib.P, _lib.P, _lib.P])
 NARROW_MAX_Q = 128  # below this many queries the int8 scan is the HBM-bound narrow kernel
 _lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
+_lib.register("lzk_i8_query", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.D, _lib.P, _lib.F,
+                                       _lib.F, _lib.I, _lib.F, _lib.P, _lib.L, _lib.P, _lib.P, _lib.P])
 
 # The dedicated int8 scan (csrc/kernels/scan8.hip: one K-tile stream across
 # tiles, int-domain epilogue) is opt-in (LZK_SCAN8=1) until it matches the
@@ -520,6 +546,25 @@ def quantize_i8_rows(x: torch.Tensor, out: torch.Tensor = None, scale_out: torch
         scale_out.copy_(s)
         s = scale_out
     return q, s
+
+
+def i8_query(q16: torch.Tensor, d: int, sumsq: torch.Tensor, n_sumsq: int, smax: torch.Tensor, alpha: float,
+             z: float, rigorous: bool = False, xn: float = 1.0):
+    """int8 queries, scales and error margins of the int8 store search in
+    one launch (search256.hip i8_query_kernel): the same quantisation as
+    :func:`quantize_i8_rows` and the margin of TenantGraph._i8_query.
+    Returns (q8 int8 [nq, Dp], qs fp32 [nq], margin fp32 [nq])."""
+    nq, Dp = q16.shape
+    dev = q16.device
+    q8 = torch.empty((nq, Dp), dtype=torch.int8, device=dev)
+    qs = torch.empty(nq, dtype=torch.float32, device=dev)
+    margin = torch.empty(nq, dtype=torch.float32, device=dev)
+    q16 = q16.contiguous()
+    _lib.check(_lib.lib().lzk_i8_query(q16.data_ptr(), q16.stride(0), nq, Dp, int(d), sumsq.data_ptr(),
+                                       1.0 / max(int(n_sumsq), 1), smax.data_ptr(), abs(float(alpha)), float(z),
+                                       1 if rigorous else 0, float(xn), q8.data_ptr(), q8.stride(0), qs.data_ptr(),
+                                       margin.data_ptr(), _lib.stream_ptr(dev)), "lzk_i8_query")
+    return q8, qs, margin
 
 
 def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
