@@ -15,7 +15,7 @@ def test_i8_query_kernel_matches_torch(nq, rig, monkeypatch):
     g = TG.TenantGraph(device="cuda", dim=768)
     X = torch.randn(5000, 768, device="cuda")
     X /= X.norm(dim=1, keepdim=True)
-    g.add_nodes([f"n{i}" for i in range(5000)], [""] * 5000, X, stored=True)
+    g.add_nodes([f"n{i}" for i in range(5000)], [""] * 5000, X, shard=g.shard_id("default"), stored=True)
     if g.emb8 is None or g.emb8.dtype != torch.int8:
         pytest.skip("tenant without an int8 copy")
     Q = torch.randn(nq, 768, device="cuda")
