@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256) void i8_query_kernel(const u16* __restrict__ q
   if (lane == 0) s_f[w] = am;
   __syncthreads();
   am = fmaxf(fmaxf(s_f[0], s_f[1]), fmaxf(s_f[2], s_f[3]));
-  const float sc = am > 0.f ? am / 127.0f : 0.f;
+  const float sc = am > 0.f ? am * (1.f / 127.f) : 0.f;  // torch: amax / 127.0 = amax * (1/127) (scalar divisor)
   const float den = am > 0.f ? sc : 1.f;
   double a_eta = 0.0, v1 = 0.0, q2 = 0.0, e2 = 0.0;
   for (int c = t; c < Dp; c += 256) {
