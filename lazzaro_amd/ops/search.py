@@ -622,11 +622,16 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     # -- then the true k-th score is >= tau, every true top-k row has int8
     # score >= tau - margin (so it is in the list) and lies above the
     # re-score cut; otherwise need = cap + 1 flags it for the exact fallback.
-    need = torch.empty(nq, dtype=torch.int32, device=dev) if spec else None
-    chk = (tau, k, cap + 1, need) if spec else None
+    need = torch.empty(nq, dtype=torch.int32, device=dev) if (spec and SPEC_CHECK_KERNEL) else None
+    chk = (tau, k, cap + 1, need) if need is not None else None
 
     def need_of():
-        return need
+        if need is not None or not spec:
+            return need
+        c = (cnt & 0x3FFFFFFF).clamp_max(cap)
+        valid = torch.arange(cap, device=dev)[None, :] < c[:, None]
+        hit = ((cs.view(nq, cap) >= tau[:, None]) & valid).sum(1)
+        return torch.where(hit >= k, torch.zeros_like(hit), torch.full_like(hit, cap + 1)).to(torch.int32)
     if nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
         _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
@@ -654,6 +659,8 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
 # sample's SPEC_J-th best score; LZK_SPEC_J=0 restores the sample's k-th best.
 SPEC_J = int(os.environ.get("LZK_SPEC_J", "5"))
 SPEC_MIN_STRIDE = 32
+# the speculative check counted in the re-score kernel (LZK_SPEC_CHECK_KERNEL=0: torch ops over the lists)
+SPEC_CHECK_KERNEL = os.environ.get("LZK_SPEC_CHECK_KERNEL", "1") != "0"
 
 
 def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None, chk=None):
