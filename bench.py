@@ -523,6 +523,9 @@ def main():
         res["consolidate_sharded"] = {k: sharded[k] for k in (
             "turns_per_s", "ms_per_step", "buffer_nodes_total", "nodes_per_rank", "convs_per_rank_step", "per_step",
             "scan_facts_x_rows_per_rank_step", "scan_facts_x_rows_unpruned_per_rank_step", "data", "path")}
+    from lazzaro_amd.ops import search as _S
+    if _S.SPEC_STATS:  # LZK_SPEC_STATS=1 (diagnostic): queries sent to the exact fallback per store search
+        res["spec_fallback_queries"] = [int(x) for x in _S.SPEC_STATS[:64]]
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

@@ -121,6 +121,11 @@ WRITE_EMB_MAX_ROWS = 8192
 SET_ROWS_KERNEL = os.environ.get("LZK_SET_ROWS", "1") != "0"
 # the int8 search's query quantisation + margin in one launch (LZK_I8_QUERY=0: torch ops)
 I8_QUERY_KERNEL = os.environ.get("LZK_I8_QUERY", "1") != "0"
+# wide batches keep the torch formulation (LZK_I8_QUERY_WIDE=1: the kernel too):
+# measured with the kernel on wide batches, the pipelined headline loop fell
+# from 82.6k to 54k QPS while every store search alone stayed as fast (open)
+I8_QUERY_WIDE = os.environ.get("LZK_I8_QUERY_WIDE", "0") == "1"
+I8_QUERY_WIDE_MIN = 128
 # consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (LZK_SEG_END=0: the torch formulation)
 SEG_END_KERNEL = os.environ.get("LZK_SEG_END", "1") != "0"
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
@@ -2070,7 +2075,9 @@ class TenantGraph:
         :meth:`_i8_candidates` (device tensors, no host sync)."""
         from ..ops.search import i8_query, quantize_i8_rows
         d = self.dim
-        if self.on_gpu and I8_QUERY_KERNEL:  # one launch (search256.hip i8_query_kernel)
+        if self.on_gpu and I8_QUERY_KERNEL and (q16.shape[0] < I8_QUERY_WIDE_MIN or I8_QUERY_WIDE):
+            # one launch (search256.hip i8_query_kernel): the narrow batches, where
+            # the ~25 torch launches it replaces are most of the query-side time
             rig = bool(LOWP_RIGOROUS or getattr(self, "LOWP_RIGOROUS", False))
             xn = (1.0 + self.max_norm_dev + 2.0 ** -7) if rig else 1.0
             return i8_query(q16, d, self.sumsq, self.n_sumsq, self._rs8_max, alpha, LOWP_MARGIN_Z, rig, xn)

@@ -273,6 +273,8 @@ def _select_with_fallback(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_o
     _lib.check(rc, "lzk_cand_select")
     if ovf_sink is not None:  # the caller's view of the lists: (overflowed query flags, list lengths)
         ovf_sink.append((ovf, cnt))
+    if SPEC_STATS is not None and need is not None:  # LZK_SPEC_STATS=1: queries sent to the exact fallback
+        SPEC_STATS.append((need != 0).sum())
     if isinstance(X, LeanRows):
         _lean_fallback(X, Q, k, bias, row_label, q_label, alpha, idx_offset, os_, oi, ovf)
         return os_, oi
@@ -661,6 +663,7 @@ SPEC_J = int(os.environ.get("LZK_SPEC_J", "5"))
 SPEC_MIN_STRIDE = 32
 # the speculative check counted in the re-score kernel (LZK_SPEC_CHECK_KERNEL=0: torch ops over the lists)
 SPEC_CHECK_KERNEL = os.environ.get("LZK_SPEC_CHECK_KERNEL", "1") != "0"
+SPEC_STATS = [] if os.environ.get("LZK_SPEC_STATS") == "1" else None
 
 
 def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None, chk=None):
