@@ -188,9 +188,13 @@ def _side_stream(dev: torch.device):
     a few queues), and tenants' side work needs no mutual concurrency."""
     st = _SIDE_STREAMS.get(dev)
     if st is None:
-        st = torch.cuda.Stream(device=dev)
+        st = torch.cuda.Stream(device=dev, priority=SIDE_STREAM_PRIORITY)
         _SIDE_STREAMS[dev] = st
     return st
+
+
+# priority of the graphs' side stream (LZK_SIDE_PRIO: 0 normal, -1 high, as torch counts)
+SIDE_STREAM_PRIORITY = int(os.environ.get("LZK_SIDE_PRIO", "0"))
 
 
 def _host_ints(v, m: int, default: int) -> Optional[np.ndarray]:
