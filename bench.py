@@ -292,11 +292,20 @@ def main():
     if distributed:
         dist.barrier()
     sync()
+    hprof = None
+    if os.environ.get("LZK_PROF_HEADLINE") == "1":  # host profile of the timed loop (stderr; diagnostic)
+        import cProfile
+        hprof = cProfile.Profile()
+        hprof.enable()
     t0 = time.perf_counter()
     n_res = 0
     for res in ms.search_memories_stream(batches(a.steps), limit=a.k):
         n_res += len(res)
     sync()
+    if hprof is not None:
+        import pstats
+        hprof.disable()
+        pstats.Stats(hprof, stream=sys.stderr).sort_stats("tottime").print_stats(35)
     if distributed:
         dist.barrier()
     sync()
