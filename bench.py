@@ -304,7 +304,9 @@ def main():
     sync()
     if hprof is not None:
         import pstats
+        import threading
         hprof.disable()
+        print("threads:", [(t.name, t.daemon) for t in threading.enumerate()], file=sys.stderr)
         pstats.Stats(hprof, stream=sys.stderr).sort_stats("tottime").print_stats(35)
     if distributed:
         dist.barrier()
