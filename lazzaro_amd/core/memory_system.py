@@ -61,6 +61,8 @@ from ..utils.tracing import tracer
 # overlaps the scan (LZK_SEARCH_OVERLAP=0 joins the streams after each search;
 # bench.py on one MI355X: 13.9 -> 13.3 ms per 1024-query step)
 SEARCH_OVERLAP = os.environ.get("LZK_SEARCH_OVERLAP", "1") == "1"
+# result events the host waits on sleep instead of spin (LZK_BLOCKING_EVENTS=0: spin)
+BLOCKING_EVENTS = os.environ.get("LZK_BLOCKING_EVENTS", "1") != "0"
 
 # kept for parity with code/tests that patch `...memory_system.openai`
 openai = _providers.openai
@@ -661,7 +663,9 @@ class MemorySystem(ConsolidationMixin):
                     if rows.is_cuda:
                         host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
                         host.copy_(rows, non_blocking=True)
-                        ev = torch.cuda.Event()
+                        # a blocking event: the host sleeps in _search_finish instead of
+                        # spinning on the CPU the next batch's tokenizer and launches need
+                        ev = torch.cuda.Event(blocking=BLOCKING_EVENTS)
                         ev.record()
                         return ("rows", g, host, ev)
                     return ("rows", g, rows, None)
