@@ -679,7 +679,7 @@ class MemorySystem(ConsolidationMixin):
         with self._graph_lock:
             g = self.graph
             if kind_ == "rows" and g is g0:  # non-node rows were set to -1 on the device
-                return NodeView.of_rows(g, data.tolist())
+                return NodeView.of_rows(g, data.numpy().tolist() if not data.is_cuda else data.tolist())
             if kind_ == "rows":  # the tenant was switched while the search ran
                 data = [[g0.ids[r] for r in row if r >= 0] for row in data.tolist()]
             out = []
