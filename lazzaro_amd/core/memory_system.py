@@ -661,19 +661,27 @@ class MemorySystem(ConsolidationMixin):
                             rows = torch.where((rows >= 0) & (g.kind[rows.clamp_min(0)] == NODE), rows,
                                                torch.full_like(rows, -1))
                     if rows.is_cuda:
-                        host = torch.empty(rows.shape, dtype=rows.dtype, pin_memory=True)
-                        host.copy_(rows, non_blocking=True)
-                        # a blocking event: the host sleeps in _search_finish instead of
-                        # spinning on the CPU the next batch's tokenizer and launches need
+                        # the rows stay on the device until _search_finish copies them to
+                        # pageable host memory on a stream that waits for THIS search only
+                        # (host reads of a pinned buffer the device just wrote ran at
+                        # ~16 MB/s in the serving loop: 5-7 ms per 1024 x 10 batch)
                         ev = torch.cuda.Event(blocking=BLOCKING_EVENTS)
                         ev.record()
-                        return ("rows", g, host, ev)
+                        return ("rows_dev", g, rows, ev)
                     return ("rows", g, rows, None)
         with tracer.stage("search", self._device):
             return ("ids", None, self._search_batch(embs, limit), None)
 
     def _search_finish(self, h) -> List[List[Node]]:
         kind_, g0, data, ev = h
+        if kind_ == "rows_dev":
+            st = getattr(self, "_result_stream", None)
+            if st is None:
+                st = self._result_stream = torch.cuda.Stream(data.device)
+            with torch.cuda.stream(st):
+                st.wait_event(ev)
+                data = data.to("cpu")  # pageable; waits for this search's event only
+            kind_, ev = "rows", None
         if ev is not None:
             ev.synchronize()
         with self._graph_lock:
