@@ -293,8 +293,24 @@ def main():
         dist.barrier()
     sync()
     hprof = None
+
+    def _cg():
+        out = {}
+        for f in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu.max"):
+            try:
+                out[f] = open(f).read().split()
+            except OSError:
+                pass
+        try:
+            out["threads"] = [ln for ln in open("/proc/self/status") if ln.startswith("Threads")]
+        except OSError:
+            pass
+        out["affinity"] = len(os.sched_getaffinity(0))
+        out["load"] = os.getloadavg()
+        return out
     if os.environ.get("LZK_PROF_HEADLINE") == "1":  # host profile of the timed loop (stderr; diagnostic)
         import cProfile
+        print("cgroup before:", _cg(), file=sys.stderr)
         hprof = cProfile.Profile()
         hprof.enable()
     t0 = time.perf_counter()
@@ -307,6 +323,7 @@ def main():
         import threading
         hprof.disable()
         print("threads:", [(t.name, t.daemon) for t in threading.enumerate()], file=sys.stderr)
+        print("cgroup after:", _cg(), file=sys.stderr)
         pstats.Stats(hprof, stream=sys.stderr).sort_stats("tottime").print_stats(35)
     if distributed:
         dist.barrier()
