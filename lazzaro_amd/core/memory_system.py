@@ -27,6 +27,7 @@ Constructor additions (all keyword, all optional): ``device``, ``metric``
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import gc
 import json
@@ -61,6 +62,10 @@ from ..utils.tracing import tracer
 # overlaps the scan (LZK_SEARCH_OVERLAP=0 joins the streams after each search;
 # bench.py on one MI355X: 13.9 -> 13.3 ms per 1024-query step)
 SEARCH_OVERLAP = os.environ.get("LZK_SEARCH_OVERLAP", "1") == "1"
+# batches search_memories_stream keeps in flight behind the one the host maps
+# (2: a host stall of up to a step -- tokenizer, result mapping, a collector
+# pass -- is absorbed by queued device work instead of idling the GPU)
+STREAM_DEPTH = int(os.environ.get("LZK_STREAM_DEPTH", "2"))
 # result events the host waits on sleep instead of spin (LZK_BLOCKING_EVENTS=0: spin)
 BLOCKING_EVENTS = os.environ.get("LZK_BLOCKING_EVENTS", "1") != "0"
 
@@ -616,19 +621,19 @@ class MemorySystem(ConsolidationMixin):
         m["search_ms"] = m.get("search_ms", 0.0) + ms
 
     def search_memories_stream(self, batches: Iterable[List[str]], limit: int = 5):
-        """Pipelined ``search_memories_batch`` for serving loops: batch i+1 is
-        tokenised and its embed + scan enqueued on the device BEFORE the host
-        waits for batch i and maps its rows to Nodes, so host work (tokenizer,
-        result mapping) hides under device work. Yields one result list per
-        input batch, in order; results equal ``search_memories_batch``."""
-        pending = None
+        """Pipelined ``search_memories_batch`` for serving loops: batches i+1 ..
+        i+STREAM_DEPTH are tokenised and their embed + scan enqueued on the
+        device BEFORE the host waits for batch i and maps its rows to Nodes,
+        so host work (tokenizer, result mapping) hides under device work.
+        Yields one result list per input batch, in order; results equal
+        ``search_memories_batch``."""
+        pending = collections.deque()
         for qs in batches:
-            h = self._search_submit(qs, limit)
-            if pending is not None:
-                yield self._search_finish(pending)
-            pending = h
-        if pending is not None:
-            yield self._search_finish(pending)
+            pending.append(self._search_submit(qs, limit))
+            if len(pending) > STREAM_DEPTH:
+                yield self._search_finish(pending.popleft())
+        while pending:
+            yield self._search_finish(pending.popleft())
 
     def _search_submit(self, queries, limit: int):
         """Enqueue embed + store search; returns a handle for _search_finish.
