@@ -292,13 +292,6 @@ def main():
     if distributed:
         dist.barrier()
     sync()
-    if os.environ.get("LZK_GC_FREEZE", "1") == "1":
-        # the tenant's host index (10M ids / contents, the id -> row map) is
-        # long-lived: move it out of the cyclic collector's generations, so a
-        # full collection does not traverse it between serving steps
-        import gc
-        gc.collect()
-        gc.freeze()
     hprof = None
 
     def _cg():
