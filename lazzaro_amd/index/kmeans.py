@@ -174,7 +174,14 @@ def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: Optional[int
 def _ff(X, k, seed, max_sample, rows):
     n = X.shape[0] if rows is None else rows.numel()
     g = torch.Generator(device="cpu").manual_seed(seed)
-    sub = torch.randperm(n, generator=g)[: min(n, max_sample)].to(X.device)
+    m0 = min(n, max_sample)
+    if n > 4 * m0:
+        # a sample without a permutation of all n rows (a host randperm of
+        # 10M rows took ~300 ms, most of the seeding)
+        pick = np.random.default_rng(seed).choice(n, size=m0, replace=False, shuffle=True)
+        sub = torch.from_numpy(pick.astype(np.int64)).to(X.device)
+    else:
+        sub = torch.randperm(n, generator=g)[:m0].to(X.device)
     if rows is not None:
         sub = rows[sub]
     if FF_KERNEL and X.is_cuda and X.dtype == torch.bfloat16 and X.shape[1] % 8 == 0 and X.shape[1] <= 2048 \
