@@ -14,6 +14,7 @@ from __future__ import annotations
 import os
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from ..ops import graph_ops as G

@@ -618,3 +618,16 @@ def test_first_shard_rows_fast_path_matches_topk(monkeypatch):
         monkeypatch.setattr(TenantGraph, "FIRST_ROWS_WINDOW", 64)
         assert fast == ref and len(ref) == k
         assert g.first_node_rows_dev(k, super_=False).tolist() == ref
+
+
+def test_farthest_first_large_sample_path():
+    """A tenant larger than 4x the farthest-first sample draws it without a
+    permutation of every row: deterministic, distinct seeds, unit rows."""
+    import torch
+
+    from lazzaro_amd.index.kmeans import _farthest_first
+    X = torch.randn(200_000, 16, generator=torch.Generator().manual_seed(0))
+    X /= X.norm(dim=1, keepdim=True)
+    a, b = _farthest_first(X, 64, seed=1), _farthest_first(X, 64, seed=1)
+    assert a.shape == (64, 16) and torch.equal(a, b)
+    assert torch.unique(a, dim=0).shape[0] == 64
