@@ -330,6 +330,7 @@ __global__ __launch_bounds__(256) void tg_set_rows_kernel(const long* __restrict
   long r;
   if (present & (1 << 15)) r = (long)vals[slot++ * (long)m + j];
   else r = rows ? rows[j] : row0 + j;
+  if (r < 0) return;  // a row this rank does not hold (row-sharded tenants)
   double v[7];
 #pragma unroll
   for (int c = 0; c < 7; ++c) {

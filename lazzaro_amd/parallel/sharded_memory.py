@@ -1107,16 +1107,30 @@ class ShardedMemorySystem:
         tr = np.asarray(seg["tch_rows"], np.int64)
         if tr.size:
             loc = self._held_rows(torch.as_tensor(tr).to(dev))
-            keep_ = torch.nonzero(loc >= 0).flatten()
-            if keep_.numel():
-                k_h = keep_.cpu().numpy()
-                rt = loc[keep_]
+            if g.on_gpu:
+                # one launch over every touched row, rows held elsewhere (-1)
+                # skipped in the kernel: no host read of which rows are local
+                from ..ops import tenant_ops as T
+                m = int(tr.size)
+                blk = torch.empty(7 + 3 * m, dtype=torch.float64).pin_memory()
+                bn = blk.numpy()
+                bn[:7] = 0.0
+                for j, c in enumerate((seg["tch_sal"], seg["tch_acc"], seg["tch_last"])):
+                    bn[7 + j * m: 7 + (j + 1) * m] = np.asarray(c, dtype=np.float64).reshape(-1)
                 with g.on_stream():
-                    g.sal[rt] = torch.as_tensor(np.asarray(seg["tch_sal"])[k_h], dtype=torch.float32).to(dev)
-                    g.acc[rt] = torch.as_tensor(np.asarray(seg["tch_acc"])[k_h], dtype=torch.int32).to(dev)
-                    g.last[rt] = torch.as_tensor(np.asarray(seg["tch_last"])[k_h], dtype=torch.float64).to(dev)
-                    g.dirty[rt] = 1
+                    T.set_rows(g, loc.contiguous(), blk.to(dev, non_blocking=True), 0b111 | (0b1111000 << 8), -1, -1)
                 g._bump()
+            else:
+                keep_ = torch.nonzero(loc >= 0).flatten()
+                if keep_.numel():
+                    k_h = keep_.cpu().numpy()
+                    rt = loc[keep_]
+                    with g.on_stream():
+                        g.sal[rt] = torch.as_tensor(np.asarray(seg["tch_sal"])[k_h], dtype=torch.float32).to(dev)
+                        g.acc[rt] = torch.as_tensor(np.asarray(seg["tch_acc"])[k_h], dtype=torch.int32).to(dev)
+                        g.last[rt] = torch.as_tensor(np.asarray(seg["tch_last"])[k_h], dtype=torch.float64).to(dev)
+                        g.dirty[rt] = 1
+                    g._bump()
         kinds = np.asarray(seg["ins_kind"]).tolist()
         if any(k_ != 0 for k_ in kinds):
             raise RuntimeError("a row-sharded tenant plans no super-nodes")
