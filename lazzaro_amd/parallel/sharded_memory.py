@@ -1110,7 +1110,6 @@ class ShardedMemorySystem:
             if g.on_gpu:
                 # one launch over every touched row, rows held elsewhere (-1)
                 # skipped in the kernel: no host read of which rows are local
-                from ..ops import tenant_ops as T
                 m = int(tr.size)
                 blk = torch.empty(7 + 3 * m, dtype=torch.float64).pin_memory()
                 bn = blk.numpy()
