@@ -1161,8 +1161,11 @@ class ShardedMemorySystem:
                 es, ed, ew, ec = es[sel], ed[sel], ew[sel], ec[sel]
                 src = self._held_rows(torch.as_tensor(es).to(dev))
                 dst = self._held_rows(torch.as_tensor(ed).to(dev))
-                need = torch.nonzero(dst < 0).flatten()
-                if need.numel():  # endpoints held elsewhere: ghost rows (created once per node)
+                # endpoints held elsewhere (known on the host): only then look
+                # for the missing rows on the device (a host read)
+                remote = any(holder_of.get(int(x), -1) != me for x in ed.tolist())
+                need = torch.nonzero(dst < 0).flatten() if remote else None
+                if need is not None and need.numel():  # endpoints held elsewhere: ghost rows (created once per node)
                     dv = ed[need.cpu().numpy()]
                     ids = [f"node_{int(x) + 1}" for x in dv]
                     fresh = {}
