@@ -8,6 +8,8 @@ maintenance of a tenant (decay + prune, eviction, boost, touch) is
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -18,6 +20,13 @@ P, I, L, F = _lib.P, _lib.I, _lib.L, _lib.F
 _lib.register("lzk_cc_hook", I, [P, P, L, P, F, P, P, P])
 _lib.register("lzk_cc_compress", I, [P, L, P])
 _lib.register("lzk_uf_union", I, [P, P, L, P, F, P, P])
+_lib.register("lzk_uf_union_plain", I, [P, P, L, P, F, P, P])
+# Union-find pass switches: cached parent loads (default; LZK_UF_PLAIN=0 =
+# agent-scope atomic loads, 2.8 -> 2.05 ms on 10M rows / 20M edges,
+# profiles/r4/uf_plain_loads.txt), and the number of union stages (0 = by
+# edge count).
+UF_PLAIN = os.environ.get("LZK_UF_PLAIN", "1") != "0"
+UF_STAGES = int(os.environ.get("LZK_UF_STAGES", "0"))
 _lib.register("lzk_pairs_above", I, [P, L, I, I, F, P, I, P, P])
 _lib.register("lzk_seg_sum", I, [P, L, L, I, P, P, P, P])
 _lib.register("lzk_centroids", I, [P, P, I, I, I, P, P, I, P])
@@ -56,12 +65,12 @@ def connected_components(src: torch.Tensor, dst: torch.Tensor, n: int, w: Option
         # the long chains a single pass can leave behind. On 10M-row / 20M-edge
         # uniform graphs one pass runs 1.1-3.4 ms depending on the instance;
         # 8 stages 1.1-1.9 ms (bench/probe_cc_seed.py).
-        stages = max(1, min(8, ne // (2 << 20)))
+        stages = UF_STAGES or max(1, min(8, ne // (2 << 20)))
         step = -(-ne // stages) if ne else 1
         st = _st(src)
         for c0 in range(0, max(ne, 1), step):
             c1 = min(ne, c0 + step)
-            _lib.check(L_.lzk_uf_union(src[c0:].data_ptr(), dst[c0:].data_ptr(), c1 - c0,
+            _lib.check((L_.lzk_uf_union_plain if UF_PLAIN else L_.lzk_uf_union)(src[c0:].data_ptr(), dst[c0:].data_ptr(), c1 - c0,
                                        w[c0:].data_ptr() if w is not None else None, float(min_w),
                                        parent.data_ptr(), st), "uf_union")
             _lib.check(L_.lzk_cc_compress(parent.data_ptr(), n, st), "cc_compress")

@@ -51,6 +51,20 @@ def test_components_methods_large_gpu(method, n, ne, seed):
     assert torch.equal(ref.to(torch.int32), got.cpu())
 
 
+@pytest.mark.parametrize("plain", [True, False])
+def test_union_find_load_flavours_gpu(plain, monkeypatch):
+    """Cached (default) and agent-scope atomic parent loads in uf_union_kernel
+    both give the host union-find's labels, staged (8 stages) and in one pass."""
+    n, ne = 4_000_000, 16_000_000
+    e = _rand_edges(n, ne, 7, "cpu")
+    ref = G.connected_components(e["src"], e["dst"], n).to(torch.int32)
+    s, d = e["src"].to(DEV), e["dst"].to(DEV)
+    monkeypatch.setattr(G, "UF_PLAIN", plain)
+    for stages in (0, 1):
+        monkeypatch.setattr(G, "UF_STAGES", stages)
+        assert torch.equal(ref, G.connected_components(s, d, n).cpu())
+
+
 def test_pairs_above_gpu():
     g = torch.Generator().manual_seed(3)
     base = torch.nn.functional.normalize(torch.randn(200, 128, generator=g), dim=1)
