@@ -60,12 +60,13 @@ def connected_components(src: torch.Tensor, dst: torch.Tensor, n: int, w: Option
         if w is not None:
             w = w.to(torch.float32).contiguous()
         ne = int(src.numel())
-        # Staged: the union pass over ~2M-edge chunks, each followed by a
+        # Staged: the union pass over >= 2M-edge chunks, each followed by a
         # compress pass, so later chunks find flat trees (1-2 hops) instead of
-        # the long chains a single pass can leave behind. On 10M-row / 20M-edge
-        # uniform graphs one pass runs 1.1-3.4 ms depending on the instance;
-        # 8 stages 1.1-1.9 ms (bench/probe_cc_seed.py).
-        stages = UF_STAGES or max(1, min(8, ne // (2 << 20)))
+        # the long chains a single pass can leave behind. At most 4 stages:
+        # on the 20M-edge persistent consolidation graph 4 stages run 894-904
+        # turns/s against 742-747 with 8 and 815 with 3
+        # (profiles/r4/uf_stages_ab.txt).
+        stages = UF_STAGES or max(1, min(4, ne // (2 << 20)))
         step = -(-ne // stages) if ne else 1
         st = _st(src)
         for c0 in range(0, max(ne, 1), step):
