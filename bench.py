@@ -60,10 +60,12 @@ Multi-GPU work inside the JSON line (all timed, every rank, RCCL over xGMI):
   is the measured per-rank scan work after the exact cone pruning (the
   unpruned figure alongside).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no
-torchrun environment the script launches N ranks itself through
-torch.distributed.run (127.0.0.1 rendezvous) before touching any GPU, and
-exits with their status; under torchrun, --gpus must equal WORLD_SIZE.
+Usage: python bench.py [--gpus N --steps K --warmup W]. Without a torchrun
+environment the script launches N ranks itself through torch.distributed.run
+(127.0.0.1 rendezvous) before touching any GPU -- N = 1 included, so every
+serving path runs its collectives on RCCL -- and exits with their status
+(``--no-launch``: one plain process at N = 1); under torchrun, --gpus must
+equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -206,9 +208,14 @@ def main():
     ap.add_argument("--sharded-steps", type=int, default=5,
                     help="timed steps of config 4 as one row-sharded buffer (--rows per rank; 0 = skip)")
     ap.add_argument("--cpu", action="store_true", help="CPU / gloo dry run of the whole flow (tests only)")
+    ap.add_argument("--no-launch", action="store_true",
+                    help="--gpus 1 without the torch.distributed.run child (no process group, no collectives)")
     a = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+    # every GPU job runs as torch.distributed.run ranks -- N = 1 included, so
+    # the driver's 1-GPU run times the RCCL all-to-all / all-gather calls of
+    # the serving paths too; this parent never touches the GPU
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or (a.gpus == 1 and not a.cpu and not a.no_launch)):
         sys.exit(launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:

@@ -927,7 +927,10 @@ class TenantGraph:
         if super_ is False and k > 0 and self.on_gpu:
             t = self._first_rows_dev(k)
             if t is not None:
-                return t
+                # targets the kernel could not fill (host shard counts ahead of
+                # the device columns) stay -1: drop them like first_rows_capture
+                with self.on_stream():
+                    return t[t >= 0]
         if super_ is False and n > self.FIRST_ROWS_WINDOW and k > 0:
             return self._first_shard_rows(k)
         with self.on_stream():
@@ -964,7 +967,7 @@ class TenantGraph:
         if len(tgt) > 64:
             return None
         with self.on_stream():
-            out = torch.empty(off, dtype=torch.long, device=dev)
+            out = torch.full((off,), -1, dtype=torch.long, device=dev)  # the kernel writes found rows only
             T.first_rows(self.kind, self.sup, self.shard, self.n, np.asarray(tgt, dtype=np.int32).T, out)
         return out
 
@@ -1911,6 +1914,11 @@ class TenantGraph:
             bias = torch.where(mask, 0.0, NEG_INF).to(torch.float32).contiguous()
             q16 = self._q16(Qn)
             X = self._scan_rows(n, Qn)
+            # lean: the int8 scans' re-score reads fp32 rows with fp32 queries
+            # while their threshold sample and margin are bf16-based, so every
+            # int8 margin below also covers |<q16, x16> - <q, x>| <= 2^-8 |q| |x|
+            # (both operands rounded to bf16; unit queries) -- as _i8_candidates
+            lean_w = 2.0 ** -8 * (1.0 + self.max_norm_dev) if self.emb16 is None else 0.0
             if dual_label is not None:
                 ql = dual_label.to(dev, torch.int32).contiguous()
                 floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
@@ -1920,6 +1928,8 @@ class TenantGraph:
                     # the int8 dual scan: same lists (error cut + bf16 re-score)
                     from ..ops.search import flat_topk_dual_i8
                     q8, qs, margin = self._i8_query(q16, 1.0)
+                    if lean_w:
+                        margin = (margin + lean_w).contiguous()
                     st = [] if (DUAL_LOWP_AUTO and not lean) else None
                     (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
                                                          row_label=lab.contiguous(), q_label=ql, bias=bias,
@@ -1933,6 +1943,8 @@ class TenantGraph:
             if lean:
                 from ..ops.search import flat_topk_i8
                 q8, qs, margin = self._i8_query(q16, 1.0)
+                if lean_w:
+                    margin = (margin + lean_w).contiguous()
                 _, ra = flat_topk_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS, bias=bias, margin=margin)
             else:
                 _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
@@ -2010,7 +2022,7 @@ class TenantGraph:
             # in fp32 against this graph's rows with the store's row mask
             cand = self._ann_candidates(Qf, max(cfg.get("rerank", 1024), k), cfg)
             return self._rerank_store(Qf, cand, k, metric, bias)
-        kc = min(CAND_SLOTS, max(k, 2 * k))
+        kc = CAND_SLOTS  # the fp32 re-rank sees 16 bf16 candidates for every k <= 16
         if self.on_gpu and k <= CAND_SLOTS and (metric != "cosine" or self.unit_rows()) \
                 and M * n >= KERNEL_MIN_WORK // 16:
             q16 = self._q16(Qf)

@@ -1046,7 +1046,10 @@ def mt_topk(tiles: MtTiles, Q: torch.Tensor, k: int, p_e32: torch.Tensor, p_bias
     dev = Q.device
     nq, D = Q.shape
     Dp = tiles.ld16
-    kc = min(16, max(k, 2 * k))
+    # 16 bf16 candidates for every k <= 16 (the per-tenant store search's
+    # CAND_SLOTS): a bf16 near-tie just past the k-th cannot push the fp32
+    # top-k out of the re-ranked set
+    kc = max(16, k)
     kslot = L.lzk_flat_topk_kslot(int(kc))
     if kslot < 0 or k > kc:
         raise ValueError("mt_topk supports k <= 16")

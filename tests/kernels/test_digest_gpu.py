@@ -103,6 +103,27 @@ def test_first_rows_kernel_matches_topk():
         assert gpu.first_rows_capture(k).get().tolist() == ref
 
 
+def test_first_rows_short_shard_returns_only_found_rows():
+    """The host shard counts claim more live rows than the device columns
+    hold (a shard's rows were turned into super-nodes behind the counts):
+    the kernel leaves the unfilled targets at -1 and both entry points drop
+    them, so every returned row is a real shard node."""
+    from lazzaro_amd.engine.tenant_graph import TenantGraph, NODE
+    g = TenantGraph(device="cuda", dim=4)
+    a, b = g.shard_id("a"), g.shard_id("b")
+    n = 64
+    g.add_nodes([f"node_{i}" for i in range(n)], [f"c{i}" for i in range(n)],
+                np.ones((n, 4), dtype=np.float32).tolist(), shard=[a] * 8 + [b] * (n - 8))
+    g.sup[:4] = 1  # device-side: 4 of shard a's 8 rows are no longer shard nodes; host counts still say 8
+    got = g.first_node_rows_dev(20, super_=False).tolist()
+    cap = g.first_rows_capture(20).get().tolist()
+    assert got == cap
+    assert all(r >= 0 for r in got)
+    kind, sup = g.kind.cpu().numpy(), g.sup.cpu().numpy()
+    assert all(kind[r] == NODE and sup[r] == 0 for r in got)
+    assert got[:4] == [4, 5, 6, 7]
+
+
 @pytest.mark.parametrize("n,ne_giant,n_small,seed", [(5000, 300, 60, 6), (400000, 900, 40, 7), (3000, 2000, 0, 8)])
 def test_small_digest_kernel_matches_sorted(n, ne_giant, n_small, seed):
     """digest.hip dg_small_kernel (one block, <= 2048 edges: sort + renumber,

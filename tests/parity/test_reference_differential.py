@@ -13,11 +13,18 @@ nodes (content, type, salience, access count, shard, parent), every shard's
 edges and weights, the super-nodes and their children, and the profile must
 match; so must three final ``search_memories`` calls.
 
+The reference side of each configuration is also checked in as a JSON
+fixture (``fixtures/reference_scenario_<cfg>.json``: the reference's output
+for this scenario, produced by ``_differential_scenario.py ref`` -- data, not
+reference code). Where /root/reference is absent (the GPU box) the engine is
+compared against the fixture, so the GPU differential always runs; where it
+is present, the fixture must equal a live reference run.
+
 Numerics: the reference keeps salience and weights in Python floats, the
 engine in fp32, so they are compared to 5e-5. The retrieval cache is off on
 both sides: the reference never invalidates cached result lists, lazzaro_amd
 drops them when the tenant's index changes (docs/INVENTORY.md, deliberate
-differences). Skipped where the reference tree is absent."""
+differences)."""
 import json
 import os
 import subprocess
@@ -29,7 +36,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference/src/lazzaro/core/memory_system.py"
 
-pytestmark = pytest.mark.skipif(not os.path.exists(REF), reason="reference source tree not present")
+FIXTURES = os.path.join(HERE, "fixtures")
+HAVE_REF = os.path.exists(REF)
+
+
+def _fixture(cfg):
+    with open(os.path.join(FIXTURES, f"reference_scenario_{cfg}.json")) as f:
+        return json.load(f)
 
 
 def _run(which, db, cfg, device="cpu"):
@@ -66,17 +79,35 @@ def test_engine_matches_reference_conversation_by_conversation(cfg, tmp_path):
     _compare(cfg, tmp_path, "cpu")
 
 
+@pytest.mark.skipif(not HAVE_REF, reason="reference source tree not present")
+@pytest.mark.parametrize("cfg", ["pressure", "defaults"])
+def test_reference_fixture_is_current(cfg, tmp_path):
+    """The checked-in reference output equals a live run of the reference."""
+    (tmp_path / "ref").mkdir()
+    ref = _run("ref", str(tmp_path / "ref"), cfg)
+    fx = _fixture(cfg)
+    for c, (sa, sb) in enumerate(zip(ref["snapshots"], fx["snapshots"])):
+        _assert_same(sa, sb, f"fixture {cfg}: after conversation {c}")
+    _assert_same(ref, fx, f"fixture {cfg}: final")
+    assert ref["search"] == fx["search"]
+
+
 @pytest.mark.gpu
-def test_gpu_engine_matches_reference(tmp_path):
+@pytest.mark.parametrize("cfg", ["pressure", "defaults"])
+def test_gpu_engine_matches_reference(cfg, tmp_path):
     """The same comparison with lazzaro_amd's tenant graph on the GPU (decay,
-    touch, boost, eviction, dedupe/link scans through the HIP kernels)."""
-    _compare("pressure", tmp_path, "cuda")
+    touch, boost, eviction, dedupe/link scans through the HIP kernels) --
+    against the live reference where present, else its checked-in output."""
+    _compare(cfg, tmp_path, "cuda")
 
 
 def _compare(cfg, tmp_path, device):
-    (tmp_path / "ref").mkdir()
     (tmp_path / "ours").mkdir()
-    ref = _run("ref", str(tmp_path / "ref"), cfg)
+    if HAVE_REF:
+        (tmp_path / "ref").mkdir()
+        ref = _run("ref", str(tmp_path / "ref"), cfg)
+    else:
+        ref = _fixture(cfg)
     ours = _run("ours", str(tmp_path / "ours"), cfg, device)
     assert len(ref["snapshots"]) == len(ours["snapshots"]) == 24
     for c, (sa, sb) in enumerate(zip(ref["snapshots"], ours["snapshots"])):
