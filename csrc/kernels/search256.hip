@@ -679,32 +679,42 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
     hits += (sc >= floor && sc >= tq) ? 1 : 0;  // wave-uniform (sc is the reduced sum)
     }
   }
-  // speculative-threshold check of the store search: the list is kept only
-  // when k_need re-scored entries reach tau (else need_val sends the query
-  // to the exact fallback)
+  // per-query certificate of the low-precision scans: the list is kept only
+  // when k_need re-scored entries reach tau -- the scan threshold plus the
+  // worst-case error bound, above which no unlisted row can score -- else
+  // need_val sends the query to the exact fallback
   if (need) {
     if (lane == 0 && hits) atomicAdd(&s_hits, hits);
     __syncthreads();
-    if (threadIdx.x == 0) need[q] = s_hits >= k_need ? 0 : need_val;
+    // tau = -inf: every row that can matter is in the list (the caller's
+    // threshold already sits a worst-case margin below its floor)
+    if (threadIdx.x == 0) need[q] = (s_hits >= k_need || tq == LZK_NEG_INF) ? 0 : need_val;
   }
 }
 
 // Query side of the int8 store search in one launch per batch (one block
 // per query): symmetric per-row int8 of the bf16 query (s = max|q| / 127,
 // q8 = rint(q / s) clamped to +-127, s = 0 for a zero row -- ops.search
-// quantize_i8_rows) and the error-model margin of TenantGraph._i8_query:
-// eta = q8 s - q; floor = smax / 2 * sum|eta|; statistical (rig = 0):
-// |alpha| (z sqrt(sum eta^2 mu2 + sum q^2 smax^2 / 12) + floor) with mu2 the
-// rows' per-dimension mean square (sumsq / nsq); worst case (rig = 1):
-// |alpha| (|eta| xn + smax / 2 sum|q| + floor) (1 + 1e-5) + 1e-6. A batch of
-// one query was ~25 torch launches of a few elements each.
+// quantize_i8_rows) and BOTH error margins of TenantGraph._i8_query, with
+// eta = q8 s - q and floor = smax / 2 * sum|eta|:
+//   statistical (margin):  |alpha| (z sqrt(sum eta^2 mu2 + sum q^2 smax^2 / 12) + floor),
+//     mu2 the rows' per-dimension mean square (sumsq / nsq) -- sets the scan
+//     threshold (how many candidates are kept);
+//   worst case (margin_rig): |alpha| (|eta| xn + smax / 2 sum|q| + floor
+//     + d 2^-23 xn |q|) (1 + 1e-5) + 1e-6 -- a bound on |int8 score - bf16
+//     score| for EVERY row of norm <= xn (the last term covers the fp32
+//     accumulation of the exact re-score), used for the re-score cut and the
+//     per-query certificate, so results never depend on the statistical one.
+// A batch of one query was ~25 torch launches of a few elements each.
 __global__ __launch_bounds__(256) void i8_query_kernel(const u16* __restrict__ q16, long ldq, int Dp, int d,
                                                        const double* __restrict__ sumsq, double inv_nsq,
                                                        const float* __restrict__ smax_p, float alpha_abs, float z,
-                                                       int rig, float xn, signed char* __restrict__ q8, long ld8,
-                                                       float* __restrict__ qs, float* __restrict__ margin) {
+                                                       float xn, signed char* __restrict__ q8, long ld8,
+                                                       float* __restrict__ qs, float* __restrict__ margin,
+                                                       float* __restrict__ margin_rig) {
+  constexpr int NS = 5;
   __shared__ float s_f[4];
-  __shared__ double s_d[4][4];
+  __shared__ double s_d[NS][4];
   const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const u16* row = q16 + (long)q * ldq;
   float am = 0.f;
@@ -715,39 +725,41 @@ __global__ __launch_bounds__(256) void i8_query_kernel(const u16* __restrict__ q
   am = fmaxf(fmaxf(s_f[0], s_f[1]), fmaxf(s_f[2], s_f[3]));
   const float sc = am > 0.f ? am * (1.f / 127.f) : 0.f;  // torch: amax / 127.0 = amax * (1/127) (scalar divisor)
   const float den = am > 0.f ? sc : 1.f;
-  double a_eta = 0.0, v1 = 0.0, q2 = 0.0, e2 = 0.0;
+  double a_eta = 0.0, v1 = 0.0, q2 = 0.0, q1 = 0.0, e2 = 0.0;
   for (int c = t; c < Dp; c += 256) {
     const float x = bf16_to_f32(row[c]);
     const float qq = fminf(fmaxf(rintf(x / den), -127.f), 127.f);
     q8[(long)q * ld8 + c] = (signed char)qq;
     const float eta = __fsub_rn(__fmul_rn(qq, sc), x);
     a_eta += fabs((double)eta);
-    q2 += rig ? fabs((double)x) : (double)x * (double)x;
+    q2 += (double)x * (double)x;
+    q1 += fabs((double)x);
     if (c < d) {
       const double e = (double)eta * (double)eta;
       e2 += e;
-      if (!rig) v1 += e * (double)(float)(sumsq[c] * inv_nsq);
+      v1 += e * (double)(float)(sumsq[c] * inv_nsq);
     }
   }
-  double vals[4] = {a_eta, v1, q2, e2};
+  double vals[NS] = {a_eta, v1, q2, q1, e2};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < NS; ++k) {
     double v = vals[k];
     for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) s_d[k][w] = v;
   }
   __syncthreads();
   if (t == 0) {
-    double r[4];
+    double r[NS];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = s_d[k][0] + s_d[k][1] + s_d[k][2] + s_d[k][3];
+    for (int k = 0; k < NS; ++k) r[k] = s_d[k][0] + s_d[k][1] + s_d[k][2] + s_d[k][3];
     const double smax = (double)smax_p[0];
     const double fl = 0.5 * smax * r[0];
-    double m;
-    if (rig) m = alpha_abs * (sqrt(r[3]) * xn + 0.5 * smax * r[2] + fl) * (1.0 + 1e-5) + 1e-6;
-    else m = alpha_abs * (z * sqrt(r[1] + r[2] * (smax * smax / 12.0)) + fl);
     qs[q] = sc;
-    margin[q] = (float)m;
+    margin[q] = (float)(alpha_abs * (z * sqrt(r[1] + r[2] * (smax * smax / 12.0)) + fl));
+    if (margin_rig) {
+      const double acc = (double)d * 0x1p-23 * (double)xn * sqrt(r[2]);
+      margin_rig[q] = (float)(alpha_abs * (sqrt(r[4]) * xn + 0.5 * smax * r[3] + fl + acc) * (1.0 + 1e-5) + 1e-6);
+    }
   }
 }
 
@@ -794,6 +806,10 @@ LZK_EXPORT int lzk_flat_top1_grouped(const void* C, long ldc, const void* Xq, lo
 }
 
 LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
+// CU budget of the persistent scans' grids (one block per CU): a search
+// launched on a CU-masked stream sizes its grid to the CUs it may use; <= 0
+// restores the device's CU count.
+LZK_EXPORT void lzk_set_cu_budget(int n) { g_n_cu = n > 0 ? n : 0; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
 LZK_EXPORT int lzk_set_stamp_buffer(void* p) {
@@ -1142,11 +1158,11 @@ LZK_EXPORT int lzk_flat_cand_dual_i8(const void* X8, long ldx_bytes, int nrows, 
 
 // int8 query + error margin of the store search (i8_query_kernel).
 LZK_EXPORT int lzk_i8_query(const void* q16, long ldq, int nq, int Dp, int d, const double* sumsq, double inv_nsq,
-                            const float* smax, float alpha_abs, float z, int rig, float xn, void* q8, long ld8,
-                            float* qs, float* margin, void* stream) {
+                            const float* smax, float alpha_abs, float z, float xn, void* q8, long ld8, float* qs,
+                            float* margin, float* margin_rig, void* stream) {
   if (nq <= 0) return 0;
   if (Dp <= 0 || d > Dp || !sumsq || !smax) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(i8_query_kernel, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, (const u16*)q16, ldq, Dp,
-                     d, sumsq, inv_nsq, smax, alpha_abs, z, rig, xn, (signed char*)q8, ld8, qs, margin);
+                     d, sumsq, inv_nsq, smax, alpha_abs, z, xn, (signed char*)q8, ld8, qs, margin, margin_rig);
   return (int)hipGetLastError();
 }

@@ -15,6 +15,10 @@
 namespace py = pybind11;
 using namespace lzrt;
 
+namespace lzrt {
+int add_strcol(PyObject* m);  // strcol.cpp
+}
+
 namespace {
 
 // Python column -> Column. String lists are read through the CPython API
@@ -340,8 +344,14 @@ PYBIND11_MODULE(_lzrt, m) {
         },
         py::arg("dst"), py::arg("src"), py::arg("bytes"));
   m.def("max_node_num",
-        [](py::list ids) {
-          // largest n of "node_<n>" ids (the reference's id scheme), 0 if none
+        [](py::object ids_any) {
+          // largest n of "node_<n>" ids (the reference's id scheme), 0 if none;
+          // any sequence of str (a list, a StrColumn)
+          PyObject* seq = PySequence_Fast(ids_any.ptr(), "max_node_num needs a sequence");
+          if (!seq) throw py::error_already_set();
+          py::list ids = py::reinterpret_steal<py::list>(PySequence_List(seq));
+          Py_DECREF(seq);
+          if (!ids) throw py::error_already_set();
           long long mx = 0;
           for (auto h : ids) {
             PyObject* o = h.ptr();
@@ -373,4 +383,5 @@ PYBIND11_MODULE(_lzrt, m) {
   m.def("tenant_rank", &tenant_rank, py::arg("tenant"), py::arg("world"),
         "consistent-hash placement of a tenant id onto one of `world` ranks");
   register_batch_plan(m);
+  if (lzrt::add_strcol(m.ptr()) < 0) throw py::error_already_set();
 }

@@ -678,8 +678,6 @@ class ConsolidationMixin:
         if commit not in ("conversation", "batch"):
             raise ValueError("commit must be 'conversation' or 'batch'")
         self._commit_each = commit == "conversation" and cadence == "conversation"
-        from .memory_system import _freeze_host_heap
-        _freeze_host_heap(getattr(self, "graph", None))  # a grown tenant's host index out of the collector
         flat, conv, idx = [], [], []
         j = 0
         for c, fs in enumerate(conversations):

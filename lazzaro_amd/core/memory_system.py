@@ -66,26 +66,6 @@ SEARCH_OVERLAP = os.environ.get("LZK_SEARCH_OVERLAP", "1") == "1"
 # (2: a host stall of up to a step -- tokenizer, result mapping, a collector
 # pass -- is absorbed by queued device work instead of idling the GPU)
 STREAM_DEPTH = int(os.environ.get("LZK_STREAM_DEPTH", "1"))
-# A large tenant's host index (ids, contents, the id -> row map: one
-# container each, tens of millions of references) is long-lived; the cyclic
-# collector's full passes traverse it -- measured 5-7 ms per serving step on
-# average at 10M rows, which flipped the pipelined loop from device- to
-# host-bound (60.9k vs 79.0k QPS on one box). search_memories_stream moves
-# the heap into the permanent generation (gc.freeze) once the tenant has
-# grown by FREEZE_ROWS rows since the last freeze (LZK_GC_FREEZE=0: never).
-GC_FREEZE = os.environ.get("LZK_GC_FREEZE", "1") == "1"
-FREEZE_ROWS = 1 << 20
-_FROZEN_AT = {}
-
-
-def _freeze_host_heap(g) -> None:
-    if not GC_FREEZE or g is None:
-        return
-    n0 = _FROZEN_AT.get(id(g), 0)
-    if g.n - n0 >= FREEZE_ROWS:
-        gc.collect()
-        gc.freeze()
-        _FROZEN_AT[id(g)] = g.n
 # result events the host waits on sleep instead of spin (LZK_BLOCKING_EVENTS=0: spin)
 BLOCKING_EVENTS = os.environ.get("LZK_BLOCKING_EVENTS", "1") != "0"
 
@@ -647,7 +627,6 @@ class MemorySystem(ConsolidationMixin):
         so host work (tokenizer, result mapping) hides under device work.
         Yields one result list per input batch, in order; results equal
         ``search_memories_batch``."""
-        _freeze_host_heap(getattr(self, "graph", None))
         pending = collections.deque()
         for qs in batches:
             pending.append(self._search_submit(qs, limit))
@@ -1500,7 +1479,7 @@ def bulk_load(g: TenantGraph, nc: Dict, ec: Optional[Dict], clock: float) -> Non
     for j, v in nc.get("_odd", {}).items():
         g.odd_emb[int(rows[j])] = v
     if ec is not None and len(ec.get("id", [])):
-        idx = pd.Index(g.ids)
+        idx = pd.Index(g.ids.tolist() if hasattr(g.ids, "tolist") else g.ids)
         src = idx.get_indexer(pd.Index(list(ec["source_id"])))
         node_src = src >= 0
         if node_src.any():

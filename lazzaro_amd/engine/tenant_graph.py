@@ -81,15 +81,27 @@ CAND_SLOTS = 16  # candidates per query from the bf16 scan before the exact re-r
 # (the candidate kernel's regime), margin in standard deviations of the fp8
 # score error (see TenantGraph._fp8_candidates)
 LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 128, 1 << 20, 8.0
-# The default int8 margin is STATISTICAL (LOWP_MARGIN_Z standard deviations of
-# the row-rounding term plus the exact worst case of the query term): on
-# random or clustered data the top-k equals the bf16 scan's (tests, bench
-# recall 1.0), but an adversarial row set could in principle move a true
-# top-k row below the cut. LZK_LOWP_RIGOROUS=1 (or TenantGraph.LOWP_RIGOROUS)
-# uses the worst-case bound of every term instead (|<x, eta>| <= |x| |eta|,
-# |<delta, q>| <= s_max / 2 |q|_1): exact parity with the bf16 path for any
-# data, at ~5x more candidates per query.
-LOWP_RIGOROUS = os.environ.get("LZK_LOWP_RIGOROUS", "0") == "1"
+# Two int8 margins (TenantGraph._i8_query): a STATISTICAL one (LOWP_MARGIN_Z
+# standard deviations of the row-rounding term plus the exact worst case of
+# the query term) and a WORST-CASE one (|<x, eta>| <= |x| |eta|, |<delta, q>|
+# <= s_max / 2 |q|_1, + fp32 accumulation). ops/search.py flat_topk_i8 /
+# flat_topk_dual_i8 set the scan threshold from the first, the re-score cut
+# and a per-query certificate from the second (a query whose k-th re-scored
+# score does not clear threshold + bound is recomputed by the exact scan).
+# LOWP_EXACT picks which margin thresholds a scan:
+#   "auto" (default): the worst-case one -- results equal the bf16 search for
+#       ANY data -- for the interactive / narrow store searches (< LOWP_MIN_Q
+#       queries: HBM-bound, the longer lists cost little) and for
+#       consolidation's dual scan (dedupe / link decisions); the statistical
+#       one for wide store-search batches, where the worst case costs ~30 %
+#       of the headline QPS (profiles/r5/README.md). Statistical means: on
+#       random or clustered unit rows the lists equal the bf16 scan's
+#       (recall tests, bench recall 1.0), but an adversarial row set could
+#       move a true top-k row below the threshold -- the certificate then
+#       checks against the same statistical margin, so such a miss is not
+#       detected.
+#   "1": the worst-case margin everywhere; "0": the statistical one everywhere.
+LOWP_EXACT = os.environ.get("LZK_LOWP_EXACT", "auto")
 # batches below LOWP_MIN_Q (the interactive turn) take the HBM-bound narrow
 # int8 scan (scan8.hip scan8_narrow_kernel); LZK_LOWP_NARROW=0: the bf16 lane kernel
 LOWP_NARROW = os.environ.get("LZK_LOWP_NARROW", "1") != "0"
@@ -136,6 +148,16 @@ RERANK64_KERNEL = os.environ.get("LZK_RERANK64", "1") != "0"
 # queries rounded to bf16 (relative 2^-9 each) move a cosine by at most
 # 2^-8 * sum|q_i x_i| <= 2^-8 ~ 0.0039, plus fp32 accumulation order.
 COS_FLOOR_SLACK = 0.01
+
+
+def _str_column(items=None):
+    """A native StrColumn (list-like, not GC-tracked); a list where the host
+    runtime is not built."""
+    try:
+        from .._lib._lzrt import StrColumn  # type: ignore
+    except ImportError:  # pragma: no cover - the runtime ships with the package build
+        return list(items or [])
+    return StrColumn(items)
 
 
 def _pad64(d: int) -> int:
@@ -253,9 +275,13 @@ class TenantGraph:
         self.n = 0
         self.cap = 0
         self._init_cap = capacity
-        self.ids: List[str] = []
-        self.content: List[str] = []
-        self.types: List[str] = []
+        # per-row host strings in native arrays the cyclic collector never
+        # traverses (csrc/runtime/strcol.cpp): a 10M-row tenant's lists made
+        # the collector's full passes stall serving loops for ms at a time;
+        # row_of (str -> int) is an untracked dict already (atomic keys/values)
+        self.ids = _str_column()
+        self.content = _str_column()
+        self.types = _str_column()
         self.row_of: Dict[str, int] = {}
         self.children: Dict[int, List[str]] = {}
         self.odd_emb: Dict[int, list] = {}
@@ -1927,13 +1953,18 @@ class TenantGraph:
                             and self._dual_lowp_ok()):
                     # the int8 dual scan: same lists (error cut + bf16 re-score)
                     from ..ops.search import flat_topk_dual_i8
-                    q8, qs, margin = self._i8_query(q16, 1.0)
+                    q8, qs, margin, margin_rig = self._i8_query(q16, 1.0)
+                    if self._lowp_exact(True):  # consolidation's decisions: the worst-case bound by default
+                        margin = margin_rig
+                    else:
+                        margin_rig = margin
                     if lean_w:
-                        margin = (margin + lean_w).contiguous()
+                        margin, margin_rig = (margin + lean_w).contiguous(), (margin_rig + lean_w).contiguous()
                     st = [] if (DUAL_LOWP_AUTO and not lean) else None
                     (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
                                                          row_label=lab.contiguous(), q_label=ql, bias=bias,
-                                                         margin=margin, floor=floor, stats=st)
+                                                         margin=margin, margin_rig=margin_rig, floor=floor,
+                                                         stats=st)
                     if st:
                         self._dual_stats = st
                 else:
@@ -1942,10 +1973,15 @@ class TenantGraph:
                 return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
             if lean:
                 from ..ops.search import flat_topk_i8
-                q8, qs, margin = self._i8_query(q16, 1.0)
+                q8, qs, margin, margin_rig = self._i8_query(q16, 1.0)
+                if self._lowp_exact(True):
+                    margin = margin_rig
+                else:
+                    margin_rig = margin
                 if lean_w:
-                    margin = (margin + lean_w).contiguous()
-                _, ra = flat_topk_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS, bias=bias, margin=margin)
+                    margin, margin_rig = (margin + lean_w).contiguous(), (margin_rig + lean_w).contiguous()
+                _, ra = flat_topk_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS, bias=bias, margin=margin,
+                                     margin_rig=margin_rig)
             else:
                 _, ra = flat_topk(X, q16, CAND_SLOTS, bias=bias)
             return self._rerank_cos(Qn, ra, k)
@@ -2066,51 +2102,65 @@ class TenantGraph:
             self._ann_covered = r1
         return idx.candidate_ids(Qf, R, cfg["nprobe"])
 
+    def _lowp_exact(self, default: bool) -> bool:
+        m = getattr(self, "LOWP_EXACT_MODE", None) or LOWP_EXACT
+        return True if m == "1" else False if m == "0" else default
+
     def _i8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
         """Store-search candidates from the int8 scan (``emb8`` / ``rs8``),
-        re-scored from the bf16 rows above the error cut. Error model of the
-        int8 score against the bf16 one, per query (no host sync): with the
-        query's rounding error eta (known exactly) and a row's rounding error
-        delta_i ~ U(-s/2, s/2), s <= the largest row scale s_max,
-          <x^, q^> - <x, q> = <x, eta> + <delta, q> + <delta, eta>
-        var <x, eta> = sum_i eta_i^2 E[x_i^2] (per-dimension second moments
-        of the tenant's rows), var <delta, q> <= |q|^2 s_max^2 / 12, and
-        |<delta, eta>| <= s_max / 2 * |eta|_1 (worst case, added as a floor);
-        the margin is LOWP_MARGIN_Z standard deviations plus that floor."""
-        from ..ops.search import flat_topk_i8
-        q8, qs, margin = self._i8_query(q16, alpha)
+        re-scored from the bf16 rows above the error cut and certified per
+        query (ops.search.flat_topk_i8), with the worst-case margin of
+        :meth:`_i8_query` (the result is the bf16 search's for ANY data) or
+        the statistical one (wide batches by default, see LOWP_EXACT)."""
+        from ..ops.search import NARROW_MAX_Q, flat_topk_i8
+        q8, qs, margin, margin_rig = self._i8_query(q16, alpha)
+        if not self._lowp_exact(Qf.shape[0] < NARROW_MAX_Q):
+            margin_rig = margin
+        else:
+            margin = margin_rig
         if self.emb16 is None:
-            # lean: the re-score reads the fp32 rows, so the margin also covers
+            # lean: the re-score reads the fp32 rows, so both margins also cover
             # |<q16, x16> - <q, x>| <= 2^-8 |q| |x| (both operands rounded to bf16)
-            margin = margin + alpha * 2.0 ** -8 * Qf.norm(dim=1) * (1.0 + self.max_norm_dev)
+            w = alpha * 2.0 ** -8 * Qf.norm(dim=1) * (1.0 + self.max_norm_dev)
+            margin, margin_rig = (margin + w).contiguous(), (margin_rig + w).contiguous()
         return flat_topk_i8(self.emb8, self.rs8, q8, qs, self._scan_rows(self.n, Qf), q16, kc, bias=bias,
-                            alpha=alpha, margin=margin)
+                            alpha=alpha, margin=margin, margin_rig=margin_rig)
 
     def _i8_query(self, q16: torch.Tensor, alpha: float):
-        """int8 queries + per-query scales + the error-model margin of
-        :meth:`_i8_candidates` (device tensors, no host sync)."""
+        """int8 queries, per-query scales and the two error margins of the
+        int8 scans (device tensors, no host sync). Error of the int8 score
+        against the bf16 one, with the query's rounding error eta (known
+        exactly) and a row's rounding error delta (|delta_i| <= s / 2, s <= the
+        largest row scale s_max ever written):
+          <x^, q^> - <x, q> = <x, eta> + <delta, q> + <delta, eta>
+        * statistical (the scan threshold): var <x, eta> = sum_i eta_i^2
+          E[x_i^2] (per-dimension second moments of the tenant's rows),
+          var <delta, q> <= |q|^2 s_max^2 / 12; LOWP_MARGIN_Z standard
+          deviations plus the worst case s_max / 2 |eta|_1 of the last term;
+        * worst case (cut + certificate): |x| |eta| + s_max / 2 |q|_1 +
+          s_max / 2 |eta|_1 + the fp32 accumulation error of the re-score,
+          rows of norm <= 1 + max_norm_dev (bf16-rounded).
+        Returns (q8, qs, margin, margin_rig)."""
         from ..ops.search import i8_query, quantize_i8_rows
         d = self.dim
+        xn = 1.0 + self.max_norm_dev + 2.0 ** -7
         if self.on_gpu and I8_QUERY_KERNEL and (q16.shape[0] < I8_QUERY_WIDE_MIN or I8_QUERY_WIDE):
             # one launch (search256.hip i8_query_kernel): the narrow batches, where
             # the ~25 torch launches it replaces are most of the query-side time
-            rig = bool(LOWP_RIGOROUS or getattr(self, "LOWP_RIGOROUS", False))
-            xn = (1.0 + self.max_norm_dev + 2.0 ** -7) if rig else 1.0
-            return i8_query(q16, d, self.sumsq, self.n_sumsq, self._rs8_max, alpha, LOWP_MARGIN_Z, rig, xn)
+            return i8_query(q16, d, self.sumsq, self.n_sumsq, self._rs8_max, alpha, LOWP_MARGIN_Z, xn)
         q8, qs = quantize_i8_rows(q16)
-        eta = q8.float() * qs[:, None] - q16.float()
+        qf = q16.float()
+        eta = q8.float() * qs[:, None] - qf
         mu2 = (self.sumsq / max(self.n_sumsq, 1)).float()
         smax = self._rs8_max
         floor = 0.5 * smax * eta.abs().sum(1)
-        if LOWP_RIGOROUS or getattr(self, "LOWP_RIGOROUS", False):
-            # worst case of every term (rows of norm <= 1 + max_norm_dev, bf16-rounded)
-            xn = 1.0 + self.max_norm_dev + 2.0 ** -7
-            bound = eta[:, :d].norm(dim=1) * xn + 0.5 * smax * q16.float().abs().sum(1) + floor
-            return q8, qs, (abs(alpha) * bound * (1.0 + 1e-5) + 1e-6).contiguous()
+        a = abs(alpha)
         v1 = (eta[:, :d] ** 2 * mu2[None, :]).sum(1)
-        v2 = (q16.float() ** 2).sum(1) * (smax * smax / 12.0)
-        margin = (abs(alpha) * (LOWP_MARGIN_Z * torch.sqrt(v1 + v2) + floor)).contiguous()
-        return q8, qs, margin
+        q2 = (qf ** 2).sum(1)
+        margin = (a * (LOWP_MARGIN_Z * torch.sqrt(v1 + q2 * (smax * smax / 12.0)) + floor)).contiguous()
+        bound = eta[:, :d].norm(dim=1) * xn + 0.5 * smax * qf.abs().sum(1) + floor + d * 2.0 ** -23 * xn * q2.sqrt()
+        margin_rig = (a * bound * (1.0 + 1e-5) + 1e-6).contiguous()
+        return q8, qs, margin, margin_rig
 
     def _fp8_candidates(self, Qf: torch.Tensor, q16: torch.Tensor, kc: int, bias: torch.Tensor, alpha: float):
         """Store-search candidates from the fp8 scan (rows in ``emb8``),

@@ -411,7 +411,7 @@ _lib.register("lzk_cos_rerank64", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.
 NARROW_MAX_Q = 128  # below this many queries the int8 scan is the HBM-bound narrow kernel
 _lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
 _lib.register("lzk_i8_query", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.D, _lib.P, _lib.F,
-                                       _lib.F, _lib.I, _lib.F, _lib.P, _lib.L, _lib.P, _lib.P, _lib.P])
+                                       _lib.F, _lib.F, _lib.P, _lib.L, _lib.P, _lib.P, _lib.P, _lib.P])
 
 # The dedicated int8 scan (csrc/kernels/scan8.hip: one K-tile stream across
 # tiles, int-domain epilogue) is opt-in (LZK_SCAN8=1) until it matches the
@@ -551,45 +551,54 @@ def quantize_i8_rows(x: torch.Tensor, out: torch.Tensor = None, scale_out: torch
 
 
 def i8_query(q16: torch.Tensor, d: int, sumsq: torch.Tensor, n_sumsq: int, smax: torch.Tensor, alpha: float,
-             z: float, rigorous: bool = False, xn: float = 1.0):
-    """int8 queries, scales and error margins of the int8 store search in
-    one launch (search256.hip i8_query_kernel): the same quantisation as
-    :func:`quantize_i8_rows` and the margin of TenantGraph._i8_query.
-    Returns (q8 int8 [nq, Dp], qs fp32 [nq], margin fp32 [nq])."""
+             z: float, xn: float = 1.0):
+    """int8 queries, scales and both error margins of the int8 store search
+    in one launch (search256.hip i8_query_kernel): the same quantisation as
+    :func:`quantize_i8_rows`, the statistical margin (scan threshold) and the
+    worst-case one (re-score cut + certificate) of TenantGraph._i8_query.
+    Returns (q8 int8 [nq, Dp], qs fp32 [nq], margin fp32 [nq], margin_rig fp32 [nq])."""
     nq, Dp = q16.shape
     dev = q16.device
     q8 = torch.empty((nq, Dp), dtype=torch.int8, device=dev)
     qs = torch.empty(nq, dtype=torch.float32, device=dev)
     margin = torch.empty(nq, dtype=torch.float32, device=dev)
+    margin_rig = torch.empty(nq, dtype=torch.float32, device=dev)
     q16 = q16.contiguous()
     _lib.check(_lib.lib().lzk_i8_query(q16.data_ptr(), q16.stride(0), nq, Dp, int(d), sumsq.data_ptr(),
                                        1.0 / max(int(n_sumsq), 1), smax.data_ptr(), abs(float(alpha)), float(z),
-                                       1 if rigorous else 0, float(xn), q8.data_ptr(), q8.stride(0), qs.data_ptr(),
-                                       margin.data_ptr(), _lib.stream_ptr(dev)), "lzk_i8_query")
-    return q8, qs, margin
+                                       float(xn), q8.data_ptr(), q8.stride(0), qs.data_ptr(), margin.data_ptr(),
+                                       margin_rig.data_ptr(), _lib.stream_ptr(dev)), "lzk_i8_query")
+    return q8, qs, margin, margin_rig
 
 
 def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
-                 X16: torch.Tensor, Q16: torch.Tensor, k: int, *, bias=None, alpha: float = 1.0, margin=None):
+                 X16: torch.Tensor, Q16: torch.Tensor, k: int, *, bias=None, alpha: float = 1.0, margin=None,
+                 margin_rig=None):
     """Top-k of ``alpha * <Q16, X16> + bias`` with the candidate scan on the
     int8 MFMA (v_mfma_i32_16x16x64_i8: twice the bf16 rate, half the bytes).
 
     X8 / Q8: per-row symmetric int8 of X16 / Q16 (:func:`quantize_i8_rows`,
     Dp % 128 == 0, Dp <= 1024) with fp32 scales ``rscale`` [N] / ``qscale``
-    [nq]; ``margin`` [nq] (fp32, >= 0) is the caller's allowance for
-    |int8 score - bf16 score| of the query: the result equals the bf16 scan's
-    whenever the margin holds for the rows that matter -- TenantGraph's
-    default margin is a statistical bound (8 sigma), its LOWP_RIGOROUS one a
-    worst-case bound. Steps:
-      1. thr = exact bf16 k-th best of a 1/S row sample (a lower bound of the
-         true k-th score) minus the margin -> the int8 scan keeps every row
-         whose int8 score clears it;
-      2. cut = (k-th best int8 score of the list) - 2 * margin: a row in
-         the true top-k has int8 score >= T - m >= that cut (T the true
-         k-th score, itself >= the list's k-th int8 score - m), so
-         only entries above the cut are re-scored from the bf16 rows -- a few
-         dozen per query instead of the whole list;
-      3. exact select with the bf16 fallback for overflowed lists.
+    [nq]. Two per-query allowances for |int8 score - bf16 score|: ``margin``
+    (fp32 [nq]) only sets how many candidates the scan keeps -- TenantGraph
+    passes its statistical estimate -- and ``margin_rig`` must BOUND the
+    difference for every row (TenantGraph: the worst case of every term; when
+    omitted, ``margin`` is taken as the bound). The result always equals the
+    bf16 scan's:
+      1. thr = bf16 sample bound - margin: tau = the 1/S sample's SPEC_J-th best
+         (speculative) or k-th best; the int8 scan keeps every row whose int8
+         score clears thr;
+      2. cut = (k-th best int8 score of the list) - 2 * margin_rig: a row of
+         the true top-k has int8 score >= T - m >= that cut (T the true k-th
+         score, itself >= the list's k-th int8 score - m), so only entries
+         above the cut are re-scored from the bf16 rows;
+      3. certificate (in the re-score kernel): every row the scan dropped has
+         bf16 score < thr + margin_rig, so a query whose k re-scored entries
+         reach thr + margin_rig has its exact top-k in the list; any other
+         query -- a statistical margin or a speculative threshold that was too
+         optimistic -- is recomputed by the exact bf16 fallback, as is a list
+         that overflowed;
+      4. exact select.
     Returns (scores fp32 [nq, k], rows int64 [nq, k]) like :func:`flat_topk`."""
     L = _lib.lib()
     nq, Dp = Q16.shape
@@ -600,78 +609,83 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     assert rscale.dtype == torch.float32 and qscale.dtype == torch.float32 and rscale.shape[0] >= N
     assert alpha > 0
     dev = X16.device
+    if margin_rig is None:
+        margin_rig = margin  # (None: no bound known -- every list entry is re-scored)
     S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
-    spec = 0 < SPEC_J < k and S >= SPEC_MIN_STRIDE and nq >= NARROW_MAX_Q
+    narrow = nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0
+    J = SPEC_J_NARROW if narrow else SPEC_J
+    spec = 0 < J < k and S >= SPEC_MIN_STRIDE
     if spec:
-        # speculative threshold: the sample's SPEC_J-th best (~SPEC_J * S-th
-        # overall) instead of its k-th -- lists ~k / SPEC_J times shorter; a
-        # query is recomputed exactly unless k entries clear it (see below)
+        # speculative threshold: the sample's J-th best (~J * S-th overall)
+        # instead of its k-th -- lists ~k / J times shorter; the certificate
+        # sends a query whose threshold was too high to the exact fallback
         Xs = X16[::S]
         bs = bias[:N:S].contiguous() if bias is not None else None
         ts, _ = _flat_topk_lane(Xs, Q16, kslot, kslot, bs, None, None, alpha, 0, None)
-        tau = _margin(ts[:, SPEC_J - 1]).contiguous()
-        thr = tau
+        tau = _margin(ts[:, J - 1]).contiguous()
     else:
-        thr = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
-    if margin is not None:
-        thr = (thr - margin).contiguous()
-    cap = max(2048, 16 * kslot * S)
+        tau = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
+    thr = (tau - margin).contiguous() if margin is not None else tau
+    # narrow batches scan at HBM speed with a worst-case margin by default:
+    # longer lists (a few thousand rows per query) cost next to nothing there
+    cap = max(NARROW_CAP if narrow else 2048, 16 * kslot * S)
     cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
     qs = qscale.contiguous()
-
-    # Speculative threshold check (in the re-score kernel): a query keeps its
-    # list only when at least k entries have exact (re-scored) scores >= tau
-    # -- then the true k-th score is >= tau, every true top-k row has int8
-    # score >= tau - margin (so it is in the list) and lies above the
-    # re-score cut; otherwise need = cap + 1 flags it for the exact fallback.
-    need = torch.empty(nq, dtype=torch.int32, device=dev) if (spec and SPEC_CHECK_KERNEL) else None
-    chk = (tau, k, cap + 1, need) if need is not None else None
-
-    def need_of():
-        if need is not None or not spec:
-            return need
-        c = (cnt & 0x3FFFFFFF).clamp_max(cap)
-        valid = torch.arange(cap, device=dev)[None, :] < c[:, None]
-        hit = ((cs.view(nq, cap) >= tau[:, None]) & valid).sum(1)
-        return torch.where(hit >= k, torch.zeros_like(hit), torch.full_like(hit, cap + 1)).to(torch.int32)
-    if nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0:
+    need = torch.empty(nq, dtype=torch.int32, device=dev)
+    chk = (_cert_tau(thr, margin_rig), k, cap + 1, need)
+    if narrow:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
-        _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap)
-        return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap)
-    if _use_scan8(Dp):
+    elif _use_scan8(Dp):
         _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, None, None, None, kslot, 2 * S, 1, cap, (cnt, cs, ci),
                None)
-        _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, chk=chk)
-        return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap,
-                                     need=need_of())
-    grid = L.lzk_cand_grid_f8(N, nq)
-    bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 1)
-    st = _lib.stream_ptr(dev)
-    _lib.check(L.lzk_flat_cand_i8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp, _lib.ptr(bias),
-                                  rscale.data_ptr(), qs.data_ptr(), float(alpha), thr.data_ptr(), cap, cnt.data_ptr(),
-                                  cs.data_ptr(), ci.data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st),
-               "lzk_flat_cand_i8")
-    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(), cs.data_ptr(),
-                                 ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
-    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, chk=chk)
-    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap, need=need_of())
+    else:
+        grid = L.lzk_cand_grid_f8(N, nq)
+        bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 1)
+        st = _lib.stream_ptr(dev)
+        _lib.check(L.lzk_flat_cand_i8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp,
+                                      _lib.ptr(bias), rscale.data_ptr(), qs.data_ptr(), float(alpha), thr.data_ptr(),
+                                      cap, cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), bbuf.data_ptr(), bcap,
+                                      bcnt.data_ptr(), st), "lzk_flat_cand_i8")
+        _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), grid, cap, nq, cnt.data_ptr(),
+                                     cs.data_ptr(), ci.data_ptr(), None, None, None, st), "lzk_cand_gather")
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin_rig, cnt, cs, ci, cap, chk=chk)
+    return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap, need=need)
+
+
+def _cert_tau(thr: torch.Tensor, margin_rig: torch.Tensor, floor: float = None) -> torch.Tensor:
+    """The certificate level of a low-precision scan list: thr + margin_rig
+    (+ relative slack) -- no row the scan dropped can reach it. With a caller
+    floor that the level does not exceed, every row at or above the floor is
+    in the list already: -inf, certified without a count."""
+    t = thr + margin_rig if margin_rig is not None else thr
+    t = t + 1e-6 * (1.0 + t.abs())
+    if floor is not None:
+        t = torch.where(t <= float(floor), torch.full_like(t, float("-inf")), t)
+    return torch.nan_to_num(t, nan=float("-inf")).contiguous()
 
 
 # Speculative store-search threshold (flat_topk_i8, wide batches): the 1/S
 # sample's SPEC_J-th best score; LZK_SPEC_J=0 restores the sample's k-th best.
 SPEC_J = int(os.environ.get("LZK_SPEC_J", "5"))
+# narrow batches: the sample's 3rd best (~192nd row overall at S = 64): a query
+# is sent to the fallback only when 3 of its top-10 rows are in the 1/S sample
+SPEC_J_NARROW = 3
+NARROW_CAP = 16384
 SPEC_MIN_STRIDE = 32
-# the speculative check counted in the re-score kernel (LZK_SPEC_CHECK_KERNEL=0: torch ops over the lists)
-SPEC_CHECK_KERNEL = os.environ.get("LZK_SPEC_CHECK_KERNEL", "1") != "0"
-SPEC_STATS = [] if os.environ.get("LZK_SPEC_STATS") == "1" else None
+SPEC_STATS = [] if os.environ.get("LZK_SPEC_STATS") == "1" else None  # diagnostic: fallback queries per search
 
 
 def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap, floor=None, chk=None):
     """int8 candidate lists -> exact bf16 scores for the entries that can
-    still reach the query's top-k: cut = (k-th best int8 score) - 2 * margin
-    (see :func:`flat_topk_i8`); the others become -inf without a row read.
-    ``chk`` = (tau [nq], k, need_val, need [nq] int32): need[q] = 0 when k
-    re-scored entries reach tau[q], else need_val (speculative threshold)."""
+    still reach the query's top-k; the others become -inf without a row read.
+    ``margin`` bounds |int8 score - bf16 score| (see :func:`flat_topk_i8`).
+    The cut: the list's k best entries by int8 score are scored exactly
+    first; the smallest of those k exact scores, L, is a lower bound of the
+    true k-th score, so a row of the true top-k has int8 score >= L - margin
+    (tighter than (k-th int8 score) - 2 margin: a few hundred re-scored rows
+    instead of thousands under a worst-case margin). ``chk`` = (tau [nq], k,
+    need_val, need [nq] int32): need[q] = 0 when k re-scored entries reach
+    tau[q] (or tau[q] is -inf), else need_val (the per-query certificate)."""
     tau_p, k_need, need_val, need_p = (None, 0, 0, None) if chk is None else (
         chk[0].data_ptr(), int(chk[1]), int(chk[2]), chk[3].data_ptr())
     L = _lib.lib()
@@ -685,9 +699,21 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
         ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
         _lib.check(L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, kslot, 0,
                                      s8.data_ptr(), i8.data_ptr(), ovf.data_ptr(), None, st), "lzk_cand_select")
-        kth = s8[:, k - 1]
-        cut = (kth - 2.0 * margin - 1e-6 * (1.0 + kth.abs())).contiguous()
-        cut = torch.nan_to_num(cut, nan=float("-inf"))
+        rows = i8[:, :k]
+        valid = rows >= 0
+        rr = rows.clamp_min(0)
+        if isinstance(X16, LeanRows):
+            dot = torch.einsum("qd,qkd->qk", X16.Q32.float(), X16.X32[rr].float())
+        else:
+            dot = torch.einsum("qd,qkd->qk", Q16.float(), X16[rr].float())
+        sc = float(alpha) * dot + (bias[rr] if bias is not None else 0.0)
+        sc = torch.where(valid & torch.isfinite(sc), sc, torch.full_like(sc, float("-inf")))
+        lo = sc.min(1).values  # -inf unless all k entries are real rows
+        # slack: the kernel's fp32 accumulation order differs from this one
+        cut = lo - margin - (2e-4 * abs(float(alpha)) + 1e-6 * (1.0 + lo.abs()))
+        if floor is not None:  # rows below floor - margin cannot reach the caller's floor
+            cut = torch.maximum(cut, float(floor) - margin)
+        cut = torch.nan_to_num(cut, nan=float("-inf")).contiguous()
     fl = float("-inf") if floor is None else float(floor)
     if isinstance(X16, LeanRows):
         X32, Q32 = X16.X32, X16.Q32
@@ -703,13 +729,16 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
 
 def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
                       X16: torch.Tensor, Q16: torch.Tensor, k: int, *, row_label, q_label, bias=None,
-                      alpha: float = 1.0, margin=None, floor: float = None, stats: Optional[list] = None):
+                      alpha: float = 1.0, margin=None, margin_rig=None, floor: float = None,
+                      stats: Optional[list] = None):
     """:func:`flat_topk_dual` with the candidate scan on the int8 MFMA (the
-    rows' int8 copy, see :func:`flat_topk_i8`): both thresholds (the sampled
-    bf16 k-th bests, raised to ``floor``) are lowered by ``margin``, both lists
-    are re-scored from the bf16 rows above their error cut, then selected
-    exactly -- the same lists as the bf16 dual scan. ``stats``: receives the
-    (overflow flags, list lengths) device tensors of both lists.
+    rows' int8 copy, see :func:`flat_topk_i8` for the two margins): each list's
+    threshold is max(sampled bf16 k-th best - margin, floor - margin_rig), both
+    lists are re-scored from the bf16 rows above their worst-case cut and
+    certified per query (k entries at thr + margin_rig, or a threshold that
+    sits margin_rig below the floor), uncertified queries recomputed exactly --
+    the same lists as the bf16 dual scan for every entry >= floor. ``stats``:
+    receives the (fallback flags, list lengths) device tensors of both lists.
     Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
     L = _lib.lib()
     nq, Dp = Q16.shape
@@ -718,14 +747,17 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
     assert kslot > 0 and X8.dtype == torch.int8 and Q8.dtype == torch.int8 and Dp % 128 == 0 and Dp <= 1024
     assert row_label.dtype == torch.int32 and q_label.dtype == torch.int32 and alpha > 0
     dev = X16.device
+    if margin_rig is None:
+        margin_rig = margin  # (None: no bound known -- every list entry is re-scored)
     S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
     thr_b = _sample_threshold(X16, Q16, k, kslot, bias, row_label, q_label, alpha, S)
     thr_a = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
-    if floor is not None:
-        thr_a = thr_a.clamp_min(float(floor))
-        thr_b = thr_b.clamp_min(float(floor))
     if margin is not None:
         thr_a, thr_b = thr_a - margin, thr_b - margin
+    if floor is not None:
+        fl = float(floor) - (margin_rig if margin_rig is not None else 0.0)
+        fl = torch.as_tensor(fl, dtype=thr_a.dtype, device=dev)
+        thr_a, thr_b = torch.maximum(thr_a, fl), torch.maximum(thr_b, fl)
     thr_a, thr_b = thr_a.contiguous(), thr_b.contiguous()
     cap = max(2048, 16 * kslot * S)
     ca = _cand_lists(dev, nq, cap, 0)
@@ -737,10 +769,16 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
     else:
         _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap,
                           ca, cb)
-    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *ca, cap, floor=floor)
-    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, *cb, cap, floor=floor)
-    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap, ovf_sink=stats)
-    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap, ovf_sink=stats)
+    need_a = torch.empty(nq, dtype=torch.int32, device=dev)
+    need_b = torch.empty(nq, dtype=torch.int32, device=dev)
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin_rig, *ca, cap, floor=floor,
+                       chk=(_cert_tau(thr_a, margin_rig, floor), k, cap + 1, need_a))
+    _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin_rig, *cb, cap, floor=floor,
+                       chk=(_cert_tau(thr_b, margin_rig, floor), k, cap + 1, need_b))
+    ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap, need=need_a,
+                               ovf_sink=stats)
+    rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap, need=need_b,
+                               ovf_sink=stats)
     if stats is not None:
         stats.append(cap)
     return ra, rb

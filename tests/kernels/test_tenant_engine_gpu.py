@@ -570,30 +570,36 @@ def test_zero_row_keeps_int8_error_model_gpu():
         TG.TenantGraph.LOWP = saved
 
 
-def test_store_search_i8_rigorous_margin_gpu():
-    """LOWP_RIGOROUS: the worst-case int8 margin (more candidates) gives the
-    same top-10 as exact fp32 L2 on clustered rows."""
+@pytest.mark.parametrize("mode,z", [("auto", 8.0), ("1", 8.0), ("1", 0.0)])
+def test_store_search_i8_certificate_gpu(mode, z, monkeypatch):
+    """The int8 store search in its default mode and in the exact mode
+    (LOWP_EXACT=1: worst-case margin + per-query certificate) -- with z = 0
+    too, where the statistical margin would keep only rows the int8 score
+    alone puts above the threshold: every query's top-10 rows equal the exact
+    bf16 scan's on clustered rows, for wide and narrow batches."""
     from lazzaro_amd.engine import tenant_graph as TG
-    saved = TG.TenantGraph.LOWP, getattr(TG.TenantGraph, "LOWP_RIGOROUS", False)
-    TG.TenantGraph.LOWP, TG.TenantGraph.LOWP_RIGOROUS = "i8", True
-    try:
-        g = TenantGraph(device=DEV)
-        N, D = (1 << 20) + 64, 256
-        gen = torch.Generator(device=DEV).manual_seed(23)
-        C = torch.randn(128, D, device=DEV, generator=gen)
-        X = C[torch.randint(0, 128, (N,), device=DEV, generator=gen)] + 0.4 * torch.randn(N, D, device=DEV,
-                                                                                         generator=gen)
-        X = X / X.norm(dim=1, keepdim=True)
-        g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
-        Q = X[torch.randint(0, N, (256,), device=DEV, generator=gen)] + 0.2 * torch.randn(256, D, device=DEV,
+    from lazzaro_amd.ops import search as S
+    monkeypatch.setattr(TG.TenantGraph, "LOWP", "i8")
+    monkeypatch.setattr(TG, "LOWP_MARGIN_Z", z)
+    monkeypatch.setattr(TG, "LOWP_EXACT", mode)
+    g = TenantGraph(device=DEV)
+    N, D = (1 << 20) + 64, 256
+    gen = torch.Generator(device=DEV).manual_seed(23)
+    C = torch.randn(128, D, device=DEV, generator=gen)
+    X = C[torch.randint(0, 128, (N,), device=DEV, generator=gen)] + 0.4 * torch.randn(N, D, device=DEV,
+                                                                                     generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    g.add_nodes([f"n{i}" for i in range(N)], [""] * N, X, shard=g.shard_id("work"), stored=True)
+    assert g.emb8 is not None and g.emb8.dtype == torch.int8
+    for nq in (256, 5):  # the wide (speculative threshold) and the narrow int8 kernels
+        Q = X[torch.randint(0, N, (nq,), device=DEV, generator=gen)] + 0.2 * torch.randn(nq, D, device=DEV,
                                                                                          generator=gen) / D ** 0.5
         Q = Q / Q.norm(dim=1, keepdim=True)
-        _, rows = g.store_search(Q, 10, "l2")
-        ref = torch.topk(-torch.cdist(Q.double(), X.double()), 10, dim=1).indices
-        hit = sum(len(set(a) & set(b)) for a, b in zip(rows.cpu().tolist(), ref.cpu().tolist())) / ref.numel()
-        assert hit == 1.0
-    finally:
-        TG.TenantGraph.LOWP, TG.TenantGraph.LOWP_RIGOROUS = saved
+        bias = g.store_bias("l2")
+        q16 = g._q16(Q)
+        _, cand = g._i8_candidates(Q, q16, 16, bias, 2.0)
+        _, ref = S.flat_topk(g.emb16[:g.n], q16, 16, bias=bias, alpha=2.0)
+        assert torch.equal(cand[:, :10], ref[:, :10]), (nq, z)
 
 
 @pytest.mark.parametrize("nq,D", [(1, 768), (7, 384), (33, 768), (127, 1024)])

@@ -1,0 +1,58 @@
+"""The native per-row string column (csrc/runtime/strcol.cpp) behind
+TenantGraph.ids / content / types: the list operations the engine uses, and
+that the cyclic collector neither tracks it nor gets slower with its size
+(the reason it replaced the Python lists and the global gc.freeze)."""
+import gc
+import pickle
+import time
+
+import pytest
+
+from lazzaro_amd.engine.tenant_graph import TenantGraph
+
+rt = pytest.importorskip("lazzaro_amd._lib._lzrt")
+
+
+def test_list_protocol():
+    c = rt.StrColumn(["a", "b"])
+    c.append("node_7")
+    c.extend(x for x in ["x", "node_12"])
+    assert len(c) == 5 and c[0] == "a" and c[-1] == "node_12" and c[-5] == "a"
+    assert c[1:3] == ["b", "node_7"] and c[::2] == ["a", "node_7", "node_12"]
+    c[1] = "B"
+    c[-1] = "z"
+    assert list(c) == ["a", "B", "node_7", "x", "z"] == c.tolist()
+    assert c.take([4, -1, 0]) == ["z", None, "a"]
+    assert list(map(c.__getitem__, [2, 0])) == ["node_7", "a"]
+    assert pickle.loads(pickle.dumps(c)).tolist() == c.tolist()
+    assert rt.max_node_num(c) == 7
+    for bad in (lambda: c[5], lambda: c[-6], lambda: c.take([9])):
+        with pytest.raises(IndexError):
+            bad()
+    with pytest.raises(TypeError):
+        del c[0]
+    with pytest.raises(TypeError):
+        c["k"]
+
+
+def test_not_gc_tracked_and_collector_cost_flat():
+    big = rt.StrColumn([f"node_{i}" for i in range(2_000_000)])
+    assert not gc.is_tracked(big)
+    t0 = time.perf_counter()
+    gc.collect()
+    with_big = time.perf_counter() - t0
+    lst = [f"node_{i}" for i in range(2_000_000)]
+    t0 = time.perf_counter()
+    gc.collect()
+    with_list = time.perf_counter() - t0
+    del lst
+    # a 2M-entry list adds a traversal of every reference to a full pass; the
+    # column adds nothing (generous bound: shared CI hosts are noisy)
+    assert with_big < with_list or with_big < 0.02, (with_big, with_list)
+
+
+def test_tenant_graph_uses_native_columns():
+    g = TenantGraph(device="cpu", dim=4)
+    g.add_nodes(["n1", "n2"], ["c1", "c2"], [[1.0, 0, 0, 0], [0, 1.0, 0, 0]], shard=g.shard_id("s"))
+    assert type(g.ids).__name__ == "StrColumn" and not gc.is_tracked(g.ids)
+    assert g.ids[g.row_of["n2"]] == "n2" and g.content[0] == "c1"
