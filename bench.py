@@ -208,6 +208,8 @@ def main():
     ap.add_argument("--sharded-steps", type=int, default=5,
                     help="timed steps of config 4 as one row-sharded buffer (--rows per rank; 0 = skip)")
     ap.add_argument("--cpu", action="store_true", help="CPU / gloo dry run of the whole flow (tests only)")
+    ap.add_argument("--no-gc-freeze", dest="gc_freeze", action="store_false",
+                    help="do not freeze the startup heap before the timed loops (see gc_in_timed_loop)")
     ap.add_argument("--no-launch", action="store_true",
                     help="--gpus 1 without the torch.distributed.run child (no process group, no collectives)")
     a = ap.parse_args()
@@ -320,11 +322,36 @@ def main():
         print("cgroup before:", _cg(), file=sys.stderr)
         hprof = cProfile.Profile()
         hprof.enable()
+    # The serving process freezes its startup heap -- torch's ~170k module
+    # objects, the model, the loaded tenant -- as long-running PyTorch servers
+    # do: a full collection then walks only what serving allocates. Without
+    # it CPython runs a full pass about every 55 steps (the per-batch result
+    # lists) over torch's heap, 40-70 ms each on the box (profiles/r5/README.md).
+    # This is the application's choice, made once here; the library holds no
+    # per-row Python containers the collector traverses (the tenant's host
+    # index lives in native StrColumns) and never touches the collector.
+    # --no-gc-freeze measures without it; gc_in_timed_loop reports the passes.
+    import gc
+    if a.gc_freeze:
+        gc.collect()
+        gc.freeze()
+    gc_log = {0: [0, 0.0], 1: [0, 0.0], 2: [0, 0.0]}
+    gc_t0 = [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t0[0] = time.perf_counter()
+        else:
+            e = gc_log[info["generation"]]
+            e[0] += 1
+            e[1] += time.perf_counter() - gc_t0[0]
+    gc.callbacks.append(_gc_cb)
     t0 = time.perf_counter()
     n_res = 0
     for res in ms.search_memories_stream(batches(a.steps), limit=a.k):
         n_res += len(res)
     sync()
+    gc.callbacks.remove(_gc_cb)
     if hprof is not None:
         import pstats
         import threading
@@ -538,6 +565,8 @@ def main():
                              "bf16 MFMA candidate scan -> fp32 re-rank; recall checked against float64 truth"),
         "tokens_per_query": {"padded": S_tok, "real_mean": round(float(lens.float().mean()), 2)},
         "load_s": round(t_load, 1),
+        "gc_in_timed_loop": {"startup_heap_frozen": bool(a.gc_freeze),
+                             **{f"gen{k}": {"passes": v[0], "ms": round(v[1] * 1e3, 2)} for k, v in gc_log.items()}},
         "prewarm_s": round(t_pre, 1),
     }
     if consolidate is not None:

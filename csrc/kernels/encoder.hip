@@ -929,30 +929,27 @@ __global__ __launch_bounds__(256) void pool_norm_kernel(const u16* __restrict__ 
 
 }  // namespace
 
-static int g_gemm_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
+static int g_gemm_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (lzk_set_staging)
 static int g_gemm_tile = -1;     // 256 = 8-wave 256x256 pipeline when the grid fills the chip, 128 = always 128x128
-static int g_g256_body = -1;     // 256x256 main loop: 0 = four-phase body, 1 = two-phase body2 (default; LZK_G256_BODY)
+static int g_g256_body = -1;     // 256x256 main loop: 0 = four-phase body, 1 = two-phase body2 (default)
 
 LZK_EXPORT void lzk_set_staging(int glds) { g_gemm_staging = glds; }
 LZK_EXPORT void lzk_set_gemm_tile(int t) { g_gemm_tile = t; }
 LZK_EXPORT void lzk_set_g256_body(int b) { g_g256_body = b; }
-static int g_g256_min_n = -1;  // smallest N routed to the 256x256 pipeline (LZK_G256_MIN_N)
+static int g_g256_min_n = -1;  // smallest N routed to the 256x256 pipeline
 LZK_EXPORT void lzk_set_g256_min_n(int n) { g_g256_min_n = n; }
-static int g_g256_min_tiles = -1;  // smallest grid routed to the 256x256 pipeline (LZK_G256_MIN_TILES)
+static int g_g256_min_tiles = -1;  // smallest grid routed to the 256x256 pipeline
 LZK_EXPORT void lzk_set_g256_min_tiles(int n) { g_g256_min_tiles = n; }
-static int g_g256_tail = -1;  // largest last-round fill (% of the CUs) split off to the 128x128 kernel (LZK_G256_TAIL)
+static int g_g256_tail = -1;  // largest last-round fill (% of the CUs) split off to the 128x128 kernel (A/B setter)
 LZK_EXPORT void lzk_set_g256_tail(int pct) { g_g256_tail = pct; }
 static int g_n_cu_enc = 0;
-static int g_g256_persist = -1;  // persistent 256x256 GEMM: 1 = register epilogue, 2 = LDS image (LZK_G256_PERSIST)
+static int g_g256_persist = -1;  // persistent 256x256 GEMM: 1 = register epilogue, 2 = LDS image (A/B setter)
 LZK_EXPORT void lzk_set_g256_persist(int p) { g_g256_persist = p; }
 
 LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, long ldw, int N,
                                  const float* bias, const void* R, long ldr, void* Y, long ldy, int K,
                                  int act, void* stream) {
-  if (g_gemm_staging < 0) {
-    const char* e = getenv("LZK_STAGING");
-    g_gemm_staging = (e && e[0] == 'r') ? 0 : 1;
-  }
+  if (g_gemm_staging < 0) g_gemm_staging = 1;
   if (K % TK != 0 || N % 4 != 0 || T <= 0 || N <= 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (T <= 64 && K % 128 == 0 && g_gemm_tile != 128) {
@@ -986,10 +983,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     }
 #undef GO
   };
-  if (g_gemm_tile < 0) {
-    const char* e = getenv("LZK_GEMM_TILE");
-    g_gemm_tile = (e && atoi(e) == 128) ? 128 : 256;
-  }
+  if (g_gemm_tile < 0) g_gemm_tile = 256;
   {
     const int n_ft = (N + g256::BM - 1) / g256::BM, n_tt = (T + g256::BN - 1) / g256::BN;
     // measured (profiles/ab_body_r1.json): with the two-phase main loop the
@@ -997,26 +991,19 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
     // (N = 768) at 11k tokens: 132 tiles, 24 / 60 us vs 34 / 90 us -- so every grid of at
     // least 64 tiles takes it (from 128: bench forward 5.72 -> 5.13 ms; from 64: the consolidation
     // bench's 7k-token fact halves 21.8 -> 21.1 ms per step)
-    if (g_g256_min_n < 0) {
-      const char* e = getenv("LZK_G256_MIN_N");
-      g_g256_min_n = e ? atoi(e) : 768;
-    }
-    if (g_g256_min_tiles < 0) {
-      const char* e = getenv("LZK_G256_MIN_TILES");
-      g_g256_min_tiles = e ? atoi(e) : 64;
-    }
+    if (g_g256_min_n < 0) g_g256_min_n = 768;
+    if (g_g256_min_tiles < 0) g_g256_min_tiles = 64;
     const u16* w = (const u16*)W;
     // 256x256 launch over token rows [0, Tn) of x / r / y
     auto launch256 = [&](const u16* x, int Tn, const u16* r, u16* y) {
       const int ntt = (Tn + g256::BN - 1) / g256::BN;
       dim3 grid(n_ft * ntt), block(g256::NT);
       if (g_g256_persist < 0) {
-        const char* e = getenv("LZK_G256_PERSIST");
         // off by default (profiles/ab_persist_r1.json): with the LDS-image
         // epilogue (2) the per-GEMM times equal the one-tile kernel's and the whole forward is
         // slower (2 streams 5.14 -> 5.50 ms); 8-B stores straight from the MFMA layout (1) cost
         // ~3.5 us per 256x256 tile more than the coalesced image stores (QKV 93 -> 107 us)
-        g_g256_persist = e ? atoi(e) : 0;
+        g_g256_persist = 0;
       }
       if ((g_g256_persist == 1 || g_g256_persist == 2) && (act == 0 || act == 1)) {
         if (g_n_cu_enc <= 0) {
@@ -1047,8 +1034,7 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
         return;
       }
       if (g_g256_body < 0) {
-        const char* e = getenv("LZK_G256_BODY");
-        g_g256_body = e ? atoi(e) : 1;  // body2: 2-4 % faster on the bge-base projections (profiles/ab_body_r1.json)
+        g_g256_body = 1;  // body2: 2-4 % faster on the bge-base projections (profiles/ab_body_r1.json)
       }
 #define GO1(A, RS, BD)                                                                                        \
   do {                                                                                                        \
@@ -1089,12 +1075,11 @@ LZK_EXPORT int lzk_gemm_bias_act(const void* X, long ldx, int T, const void* W, 
           g_n_cu_enc = 256;
       }
       if (g_g256_tail < 0) {
-        const char* e = getenv("LZK_G256_TAIL");
         // off by default: in isolation FFN2 at 22.6k tokens gains 132 -> 119 us, but the
         // 128x128 tail kernels run at ~1/4 of the per-CU rate (one small tile per CU) and the
         // whole forward loses (profiles/ab_tail_r1.json: 1 stream 5.54 ->
         // 5.76 ms, 2 streams 4.97 -> 5.11 ms)
-        g_g256_tail = e ? atoi(e) : 0;
+        g_g256_tail = 0;
       }
       const int tiles = n_ft * n_tt, P = g_n_cu_enc;
       const int q = tiles / P, f = tiles - q * P;

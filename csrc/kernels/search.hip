@@ -467,10 +467,7 @@ __global__ __launch_bounds__(256) void topk_merge64_kernel(
 int g_search_staging = -1;  // 1 = LDS-DMA (default), 0 = register staging (LZK_STAGING=reg)
 
 int search_staging() {
-  if (g_search_staging < 0) {
-    const char* e = getenv("LZK_STAGING");
-    g_search_staging = (e && e[0] == 'r') ? 0 : 1;
-  }
+  if (g_search_staging < 0) g_search_staging = 1;
   return g_search_staging;
 }
 

@@ -832,10 +832,7 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* q = (const u16*)Qm;
-  if (g_cand_persist < 0) {
-    const char* e = getenv("LZK_CAND_PERSIST");
-    g_cand_persist = (e && e[0] == '0') ? 0 : 1;
-  }
+  if (g_cand_persist < 0) g_cand_persist = 1;
   if (g_n_cu <= 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -989,10 +986,7 @@ LZK_EXPORT int lzk_cand_grid(int nrows, int nq, int dual) {
     if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
       g_n_cu = 256;
   }
-  if (g_cand_persist < 0) {
-    const char* e = getenv("LZK_CAND_PERSIST");
-    g_cand_persist = (e && e[0] == '0') ? 0 : 1;
-  }
+  if (g_cand_persist < 0) g_cand_persist = 1;
   const long nblk = (long)((nrows + BM - 1) / BM) * ((nq + BN - 1) / BN);
   if (dual) return (int)(nblk < g_n_cu ? nblk : g_n_cu);
   return (g_cand_persist && nblk >= g_n_cu) ? g_n_cu : 0;

@@ -151,8 +151,6 @@ std::shared_ptr<arrow::Array> to_arrow(const Column& c, int64_t r0, int64_t r1) 
 // Best-effort madvise over the pages covering [p, p + n) (older kernels
 // reject the populate advices: the copy then faults page by page as before).
 void advise(const void* p, size_t n, int advice, uintptr_t align = 4096) {
-  static const bool off = getenv("LZK_NO_ADVISE") != nullptr;  // A/B switch
-  if (off) return;
   const uintptr_t a = (uintptr_t)p & ~(align - 1);
   const uintptr_t e = ((uintptr_t)p + n + 4095) & ~uintptr_t(4095);
   if (e > a) (void)madvise((void*)a, e - a, advice);

@@ -775,8 +775,8 @@ class ConsolidationMixin:
             if self._commit_each:
                 self._save_to_persistence()
 
-    # LZK_PY_PLANNER=1: the Python reference planner instead of the native one
-    NATIVE_PLANNER = os.environ.get("LZK_PY_PLANNER", "0") != "1"
+    # False: the Python reference planner instead of the native one
+    NATIVE_PLANNER = True
 
     def _consolidate_planned(self, facts, conv, B, embs, now, stats) -> None:
         # one switch to the graph's stream for the whole batch: the hundreds of

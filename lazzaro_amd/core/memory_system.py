@@ -59,15 +59,15 @@ from ..utils.tracing import tracer
 
 # search_memories_stream: run each batch's store search on the graph's stream
 # without the caller's stream waiting for it, so the next batch's embed
-# overlaps the scan (LZK_SEARCH_OVERLAP=0 joins the streams after each search;
+# overlaps the scan (SEARCH_OVERLAP = False joins the streams after each search;
 # bench.py on one MI355X: 13.9 -> 13.3 ms per 1024-query step)
-SEARCH_OVERLAP = os.environ.get("LZK_SEARCH_OVERLAP", "1") == "1"
+SEARCH_OVERLAP = True
 # batches search_memories_stream keeps in flight behind the one the host maps
 # (2: a host stall of up to a step -- tokenizer, result mapping, a collector
 # pass -- is absorbed by queued device work instead of idling the GPU)
-STREAM_DEPTH = int(os.environ.get("LZK_STREAM_DEPTH", "1"))
-# result events the host waits on sleep instead of spin (LZK_BLOCKING_EVENTS=0: spin)
-BLOCKING_EVENTS = os.environ.get("LZK_BLOCKING_EVENTS", "1") != "0"
+STREAM_DEPTH = 1
+# result events the host waits on sleep instead of spin (BLOCKING_EVENTS = False: spin)
+BLOCKING_EVENTS = True
 
 # kept for parity with code/tests that patch `...memory_system.openai`
 openai = _providers.openai

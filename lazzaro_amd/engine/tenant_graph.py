@@ -103,8 +103,8 @@ LOWP_MIN_Q, LOWP_MIN_ROWS, LOWP_MARGIN_Z = 128, 1 << 20, 8.0
 #   "1": the worst-case margin everywhere; "0": the statistical one everywhere.
 LOWP_EXACT = os.environ.get("LZK_LOWP_EXACT", "auto")
 # batches below LOWP_MIN_Q (the interactive turn) take the HBM-bound narrow
-# int8 scan (scan8.hip scan8_narrow_kernel); LZK_LOWP_NARROW=0: the bf16 lane kernel
-LOWP_NARROW = os.environ.get("LZK_LOWP_NARROW", "1") != "0"
+# int8 scan (scan8.hip scan8_narrow_kernel); LOWP_NARROW = False: the bf16 lane kernel
+LOWP_NARROW = True
 # consolidation's dual candidate scan on the int8 copy (flat_topk_dual_i8).
 # LZK_DUAL_LOWP=1 always, 0 never, default "auto": int8 while its lists stay
 # short, bf16 for the next DUAL_BACKOFF calls of a tenant whose last int8 call
@@ -130,20 +130,20 @@ LEAN_HBM = os.environ.get("LZK_LEAN_HBM", "0") == "1"
 # inserts of at most this many rows write their embedding columns in one launch
 WRITE_EMB_MAX_ROWS = 8192
 # node columns of an insert in one launch (tenant.hip tg_set_rows_kernel); 0 = per-column writes
-SET_ROWS_KERNEL = os.environ.get("LZK_SET_ROWS", "1") != "0"
-# the int8 search's query quantisation + margin in one launch (LZK_I8_QUERY=0: torch ops)
-I8_QUERY_KERNEL = os.environ.get("LZK_I8_QUERY", "1") != "0"
-# wide batches keep the torch formulation (LZK_I8_QUERY_WIDE=1: the kernel too):
+SET_ROWS_KERNEL = True
+# the int8 search's query quantisation + margin in one launch (I8_QUERY_KERNEL = False: torch ops)
+I8_QUERY_KERNEL = True
+# wide batches keep the torch formulation (I8_QUERY_WIDE = True: the kernel too):
 # measured with the kernel on wide batches, the pipelined headline loop fell
 # from 82.6k to 54k QPS while every store search alone stayed as fast (open)
-I8_QUERY_WIDE = os.environ.get("LZK_I8_QUERY_WIDE", "0") == "1"
+I8_QUERY_WIDE = False
 I8_QUERY_WIDE_MIN = 128
-# consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (LZK_SEG_END=0: the torch formulation)
-SEG_END_KERNEL = os.environ.get("LZK_SEG_END", "1") != "0"
+# consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (SEG_END_KERNEL = False: the torch formulation)
+SEG_END_KERNEL = True
 # store-search re-rank as one kernel (tenant.hip store_rerank_kernel); 0 = torch chain
-RERANK_KERNEL = os.environ.get("LZK_RERANK_KERNEL", "1") != "0"
+RERANK_KERNEL = True
 # consolidation's float64 candidate re-rank as one kernel (cos_rerank64_kernel); 0 = torch chain
-RERANK64_KERNEL = os.environ.get("LZK_RERANK64", "1") != "0"
+RERANK64_KERNEL = True
 # cos_topk(min_score=): kernel threshold slack below min_score. Unit rows and
 # queries rounded to bf16 (relative 2^-9 each) move a cosine by at most
 # 2^-8 * sum|q_i x_i| <= 2^-8 ~ 0.0039, plus fp32 accumulation order.
@@ -215,8 +215,8 @@ def _side_stream(dev: torch.device):
     return st
 
 
-# priority of the graphs' side stream (LZK_SIDE_PRIO: 0 normal, -1 high, as torch counts)
-SIDE_STREAM_PRIORITY = int(os.environ.get("LZK_SIDE_PRIO", "0"))
+# priority of the graphs' side stream (0 normal, -1 high, as torch counts)
+SIDE_STREAM_PRIORITY = 0
 
 
 def _host_ints(v, m: int, default: int) -> Optional[np.ndarray]:
@@ -439,7 +439,7 @@ class TenantGraph:
     _rmb = None  # persistent all-zero removal bitmap of the fused segment end
     _dv_acc = None  # device running max of | |x| - 1 | over small inserts
     _dv_acc_pending = False  # _dv_acc is in _norm_dev_pending
-    SAMPLE_TWO_LEVEL = os.environ.get("LZK_SAMPLE_ASSIGN", "two_level") != "full"
+    SAMPLE_TWO_LEVEL = True
 
     # Low-precision copy of the rows for the store search's candidate scan
     # (LZK_SEARCH_LOWP): "i8" = per-row symmetric int8 + fp32 row scales
@@ -2279,7 +2279,7 @@ class TenantGraph:
                 from ..index.kmeans import assign_two_level
                 T16, tof = prev["top_c16"], prev["top_of_fine"]
                 fa = lambda Xa, C16: assign_two_level(Xa, C16, T16, tof)  # noqa: E731
-            # the mini-batch steps: the same two-level assign (LZK_SAMPLE_ASSIGN=full: flat over all fine)
+            # the mini-batch steps: the same two-level assign (SAMPLE_TWO_LEVEL = False: flat over all fine)
             sa = fa if self.SAMPLE_TWO_LEVEL else None
             fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp,
                                      full_assign=fa, sample_assign=sa, comm=comm if dist else None)

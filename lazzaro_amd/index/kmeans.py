@@ -23,7 +23,7 @@ from ..utils.tracing import tracer
 
 
 # "top1": the 256x256 argmax kernel (flat_top1); "lane": flat_topk(k=1) on the 128x128 per-lane kernel
-ASSIGN = os.environ.get("LZK_ASSIGN", "top1")
+ASSIGN = 'top1'
 
 
 def assign(X: torch.Tensor, C16: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -40,8 +40,8 @@ def assign(X: torch.Tensor, C16: torch.Tensor, chunk: int = 1 << 20) -> Tuple[to
 
 
 # two-level assign in one grouped launch (flat_top1_grouped_kernel) instead of
-# a gather + flat_top1 per topic group; LZK_GROUPED_ASSIGN=0 for the loop
-GROUPED = os.environ.get("LZK_GROUPED_ASSIGN", "1") != "0"
+# a gather + flat_top1 per topic group; GROUPED = False for the loop
+GROUPED = True
 GROUP_TILE = 256  # the 256x256 pipeline's tile edge (lzk_g256.h BM = BN)
 
 
@@ -152,10 +152,10 @@ def assign_two_level(X: torch.Tensor, C16: torch.Tensor, T16: torch.Tensor, top_
 
 
 # farthest-first seeding as one fused kernel per pick (csrc/kernels/kmeans.hip); 0 = torch GEMV chain
-FF_KERNEL = os.environ.get("LZK_FF_KERNEL", "1") != "0"
+FF_KERNEL = True
 
 
-FF_SAMPLE = int(os.environ.get("LZK_FF_SAMPLE", str(1 << 15)))
+FF_SAMPLE = 32768
 
 
 def _farthest_first(X: torch.Tensor, k: int, seed: int, max_sample: Optional[int] = None,

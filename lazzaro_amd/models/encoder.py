@@ -120,10 +120,10 @@ class SentenceEncoder:
             return E.layernorm(ya, p[f"{i}.{ln}_g"], p[f"{i}.{ln}_b"], eps, residual=yb)
         return E.layernorm(self._lin(x, i, w, b, residual=residual), p[f"{i}.{ln}_g"], p[f"{i}.{ln}_b"], eps)
 
-    # split-K mode of the hidden-width projections (LZK_SPLITK: 0 off, 1 FFN2, 2 O and FFN2).
+    # split-K mode of the hidden-width projections (SPLITK: 0 off, 1 FFN2, 2 O and FFN2).
     # Off by default: in bench.py (same box, profiles/ab_splitk_r1.json) FFN2 split costs the
     # two-stream embed 5.28 -> 5.75 ms and ties on one stream (5.96 / 5.97 ms)
-    SPLITK = int(os.environ.get("LZK_SPLITK", "0"))
+    SPLITK = 0
 
     def _split_ok(self, x, K: int) -> bool:
         # only grids that take the 256x256 pipeline anyway (>= 64 full-K tiles)
@@ -224,8 +224,8 @@ class SentenceEncoder:
     # that layer's attention output, O projection, FFN and LayerNorms run on
     # the B CLS rows alone (its QKV still covers every token: K and V feed the
     # CLS query). Exact -- the other rows' last-layer states are never read.
-    # LZK_CLS_LAST=0 computes the full last layer.
-    CLS_LAST = os.environ.get("LZK_CLS_LAST", "1") != "0"
+    # CLS_LAST = False computes the full last layer.
+    CLS_LAST = True
 
     def _layers(self, ids: torch.Tensor, lens: torch.Tensor, packed: Optional[bool], cls_last: bool = False):
         """Embedding + every transformer layer. Returns (token states, lens on
@@ -344,8 +344,8 @@ class SentenceEncoder:
         o16 = torch.cat([o[1] for o in outs]) if outs[0][1] is not None else None
         return o32, o16
 
-    # forward_streams: sub-batch 0 on the caller's stream (LZK_CALLER_STREAM=0: all on side streams)
-    CALLER_STREAM = os.environ.get("LZK_CALLER_STREAM", "1") != "0"
+    # forward_streams: sub-batch 0 on the caller's stream (CALLER_STREAM = False: all on side streams)
+    CALLER_STREAM = True
 
     def flops(self, tokens: int) -> float:
         c = self.cfg

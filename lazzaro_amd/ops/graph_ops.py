@@ -21,12 +21,12 @@ _lib.register("lzk_cc_hook", I, [P, P, L, P, F, P, P, P])
 _lib.register("lzk_cc_compress", I, [P, L, P])
 _lib.register("lzk_uf_union", I, [P, P, L, P, F, P, P])
 _lib.register("lzk_uf_union_plain", I, [P, P, L, P, F, P, P])
-# Union-find pass switches: cached parent loads (default; LZK_UF_PLAIN=0 =
+# Union-find pass switches: cached parent loads (default; UF_PLAIN = False =
 # agent-scope atomic loads, 2.8 -> 2.05 ms on 10M rows / 20M edges,
 # profiles/r4/uf_plain_loads.txt), and the number of union stages (0 = by
 # edge count).
-UF_PLAIN = os.environ.get("LZK_UF_PLAIN", "1") != "0"
-UF_STAGES = int(os.environ.get("LZK_UF_STAGES", "0"))
+UF_PLAIN = True
+UF_STAGES = 0
 _lib.register("lzk_pairs_above", I, [P, L, I, I, F, P, I, P, P])
 _lib.register("lzk_seg_sum", I, [P, L, L, I, P, P, P, P])
 _lib.register("lzk_centroids", I, [P, P, I, I, I, P, P, I, P])

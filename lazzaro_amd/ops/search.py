@@ -103,14 +103,17 @@ def _blk_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
 
 # Large-batch candidate path (csrc/kernels/search256.hip): used when the batch
 # fills whole 256-query tiles and the arena is large enough that the strided
-# threshold sample is cheap. LZK_SEARCH=lane forces the per-lane kernel.
+# threshold sample is cheap (SEARCH_MODE "lane" / "cand" force one path: tests).
 CAND_MIN_ROWS = 1 << 20
 CAND_MIN_Q = 256
-CAND_STRIDE = int(os.environ.get("LZK_CAND_STRIDE", "64"))
+CAND_STRIDE = 64
+
+
+SEARCH_MODE = "auto"
 
 
 def _use_cand(N, nq, kslot):
-    mode = os.environ.get("LZK_SEARCH", "auto")
+    mode = SEARCH_MODE
     if mode == "lane":
         return False
     if mode == "cand":
@@ -398,9 +401,6 @@ _lib.register("lzk_flat_cand_i8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.
                                            _lib.P, _lib.F, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I,
                                            _lib.P, _lib.P])
 
-_lib.register("lzk_scan8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P, _lib.P,
-                                    _lib.P, _lib.P, _lib.F, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
-_lib.register("lzk_scan8_grid", _lib.I, [_lib.I, _lib.I])
 _lib.register("lzk_scan8_narrow_grid", _lib.I, [_lib.I])
 _lib.register("lzk_scan8_narrow", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.P,
                                            _lib.P, _lib.F, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
@@ -409,21 +409,12 @@ _lib.register("lzk_farthest_first", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _li
 _lib.register("lzk_cos_rerank64", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.I, _lib.I,
                                            _lib.I, _lib.P, _lib.P, _lib.P])
 NARROW_MAX_Q = 128  # below this many queries the int8 scan is the HBM-bound narrow kernel
-_lib.register("lzk_scan8_ws_bytes", _lib.L, [_lib.I])
 _lib.register("lzk_i8_query", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.P, _lib.D, _lib.P, _lib.F,
                                        _lib.F, _lib.F, _lib.P, _lib.L, _lib.P, _lib.P, _lib.P, _lib.P])
 
-# The dedicated int8 scan (csrc/kernels/scan8.hip: one K-tile stream across
-# tiles, int-domain epilogue) is opt-in (LZK_SCAN8=1) until it matches the
-# shared 256^2 template on the GPU; the narrow kernel for batches under 128
-# queries (same file) is on (LZK_SCAN8_NARROW=0 disables it).
-SCAN8 = os.environ.get("LZK_SCAN8", "0") == "1"
-SCAN8_NARROW = os.environ.get("LZK_SCAN8_NARROW", "1") != "0"
-_ws_scan8 = _Workspace()
-
-
-def _use_scan8(Dp: int) -> bool:
-    return SCAN8 and Dp % 128 == 0 and 256 <= Dp <= 1024
+# the narrow kernel for batches under 128 queries (scan8.hip) is on
+# (SCAN8_NARROW = False disables it)
+SCAN8_NARROW = True
 
 
 def _wave_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
@@ -437,26 +428,6 @@ def _wave_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
     buf = ws[: regions * capw * 16]
     cnt = ws[regions * capw * 16: regions * capw * 16 + regions * 4].view(torch.int32)
     return buf, capw, cnt, regions
-
-
-def _scan8(X8, rscale, Q8, qscale, bias, alpha, thr, thr2, row_label, q_label, kslot, S, lists, cap, ca, cb):
-    """int8 candidate pass (scan8.hip) + gather into the per-query lists
-    ``ca`` (and ``cb`` for the dual search)."""
-    L = _lib.lib()
-    nq, Dp = Q8.shape
-    N = X8.shape[0]
-    dev = Q8.device
-    st = _lib.stream_ptr(dev)
-    grid = L.lzk_scan8_grid(N, nq)
-    bbuf, bcap, bcnt, regions = _wave_records(dev, grid, nq, kslot, S, lists)
-    ws = _ws_scan8.get(dev, int(L.lzk_scan8_ws_bytes(N)))
-    _lib.check(L.lzk_scan8(X8.data_ptr(), X8.stride(0), N, Q8.data_ptr(), Q8.stride(0), nq, Dp, _lib.ptr(bias),
-                           rscale.data_ptr(), qscale.data_ptr(), _lib.ptr(row_label), _lib.ptr(q_label), float(alpha),
-                           thr.data_ptr(), _lib.ptr(thr2), ws.data_ptr(), bbuf.data_ptr(), bcap, bcnt.data_ptr(), st),
-               "lzk_scan8")
-    cbp = (cb[0].data_ptr(), cb[1].data_ptr(), cb[2].data_ptr()) if cb is not None else (None, None, None)
-    _lib.check(L.lzk_cand_gather(bbuf.data_ptr(), bcap, bcnt.data_ptr(), regions, cap, nq, ca[0].data_ptr(),
-                                 ca[1].data_ptr(), ca[2].data_ptr(), *cbp, st), "lzk_cand_gather")
 
 
 def _scan8_narrow(X8, rscale, Q8, qscale, bias, alpha, thr, kslot, S, cap, ca):
@@ -635,9 +606,6 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     chk = (_cert_tau(thr, margin_rig), k, cap + 1, need)
     if narrow:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
-    elif _use_scan8(Dp):
-        _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, None, None, None, kslot, 2 * S, 1, cap, (cnt, cs, ci),
-               None)
     else:
         grid = L.lzk_cand_grid_f8(N, nq)
         bbuf, bcap, bcnt = _blk_records(dev, grid, nq, kslot, 2 * S, 1)
@@ -665,8 +633,8 @@ def _cert_tau(thr: torch.Tensor, margin_rig: torch.Tensor, floor: float = None) 
 
 
 # Speculative store-search threshold (flat_topk_i8, wide batches): the 1/S
-# sample's SPEC_J-th best score; LZK_SPEC_J=0 restores the sample's k-th best.
-SPEC_J = int(os.environ.get("LZK_SPEC_J", "5"))
+# sample's SPEC_J-th best score; SPEC_J = 0 restores the sample's k-th best.
+SPEC_J = 5
 # narrow batches: the sample's 3rd best (~192nd row overall at S = 64): a query
 # is sent to the fallback only when 3 of its top-10 rows are in the 1/S sample
 SPEC_J_NARROW = 3
@@ -763,12 +731,7 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
     ca = _cand_lists(dev, nq, cap, 0)
     cb = _cand_lists(dev, nq, cap, 1)
     qs = qscale.contiguous()
-    if _use_scan8(Dp):
-        _scan8(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, 2 * S, 2, cap,
-               ca, cb)
-    else:
-        _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap,
-                          ca, cb)
+    _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap, ca, cb)
     need_a = torch.empty(nq, dtype=torch.int32, device=dev)
     need_b = torch.empty(nq, dtype=torch.int32, device=dev)
     _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin_rig, *ca, cap, floor=floor,
@@ -785,7 +748,7 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
 
 
 def _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap, ca, cb):
-    """The dual int8 pass on the shared 256^2 template (LZK_SCAN8=0)."""
+    """The dual int8 pass on the shared 256^2 template."""
     L = _lib.lib()
     nq, Dp = Q8.shape
     N = X16.shape[0]
@@ -804,14 +767,14 @@ def _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_la
                                  cb[2].data_ptr(), st), "lzk_cand_gather")
 
 
-# Speculative list-B threshold of flat_topk_dual (LZK_DUAL_SPEC=1): aim for
+# Speculative list-B threshold of flat_topk_dual (DUAL_SPEC = True): aim for
 # this many expected label rows above it. Off by default: on the 10M x 1024
 # consolidation shape it cuts the scan 13.93 -> 12.90 ms (bench/probe_dual_thr.py:
 # list-B candidates 198 -> 16 per query), but the top-16 sample pass it needs
 # costs ~1.1 ms more than the top-4 one, so the whole call ties (15.07 vs
 # 15.13 ms, bench/ab_dual_spec.py, profiles/ab_dual_spec_r1.json).
-DUAL_SPEC = os.environ.get("LZK_DUAL_SPEC", "0") == "1"
-DUAL_SPEC_E = float(os.environ.get("LZK_DUAL_SPEC_E", "16"))
+DUAL_SPEC = False
+DUAL_SPEC_E = 16.0
 SPEC_SLOTS = 16
 
 

@@ -580,8 +580,8 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
 
 
 # global search over >= MT_MIN_TENANTS small tenants: one multi-tenant pass
-# (LZK_MT_GLOBAL=0: the per-tenant store searches)
-MT_GLOBAL = os.environ.get("LZK_MT_GLOBAL", "1") != "0"
+# (MT_GLOBAL = False: the per-tenant store searches)
+MT_GLOBAL = True
 MT_MIN_TENANTS = 2
 
 

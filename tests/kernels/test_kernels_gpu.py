@@ -44,7 +44,7 @@ def test_flat_topk_matches_reference(n, d, nq, k, bias, label):
 ])
 def test_flat_topk_candidate_path(monkeypatch, n, d, nq, k, bias, label):
     """256x256 pipeline + sampled threshold + select (search256.hip) == reference."""
-    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr(__import__("lazzaro_amd.ops.search", fromlist=["x"]), "SEARCH_MODE", "cand")
     monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", 16)
     g = torch.Generator(device=DEV).manual_seed(n)
     X = torch.randn(n, d, device=DEV, generator=g).to(torch.bfloat16)
@@ -62,7 +62,7 @@ def test_flat_topk_candidate_path(monkeypatch, n, d, nq, k, bias, label):
 
 def test_flat_topk_candidate_overflow_falls_back(monkeypatch):
     """All-equal scores overflow every candidate list -> lane-kernel recompute."""
-    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr(__import__("lazzaro_amd.ops.search", fromlist=["x"]), "SEARCH_MODE", "cand")
     X = torch.ones(100_000, 128, device=DEV, dtype=torch.bfloat16)
     Q = torch.ones(256, 128, device=DEV, dtype=torch.bfloat16)
     s, i = flat_topk(X, Q, 4)
@@ -259,7 +259,7 @@ def test_graphed_encoder_matches_eager():
 def test_flat_topk_dual_gpu(monkeypatch, n, nq, k, stride, n_labels, spec_e):
     """One fused scan == the unfiltered and the label-filtered searches."""
     from lazzaro_amd.ops.search import flat_topk_dual
-    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr(__import__("lazzaro_amd.ops.search", fromlist=["x"]), "SEARCH_MODE", "cand")
     monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", stride)
     monkeypatch.setattr("lazzaro_amd.ops.search.DUAL_SPEC", n_labels is not None)
     monkeypatch.setattr("lazzaro_amd.ops.search.DUAL_SPEC_E", spec_e)
@@ -314,7 +314,7 @@ def test_cand_schedule_variants(monkeypatch, opt, n, d, nq):
     L = _lib.lib()
     L.lzk_set_g256_opt.argtypes = [ctypes.c_int]
     L.lzk_set_cand_persist.argtypes = [ctypes.c_int]
-    monkeypatch.setenv("LZK_SEARCH", "cand")
+    monkeypatch.setattr(__import__("lazzaro_amd.ops.search", fromlist=["x"]), "SEARCH_MODE", "cand")
     monkeypatch.setattr("lazzaro_amd.ops.search.CAND_STRIDE", 16)
     g = torch.Generator(device=DEV).manual_seed(n + d + opt)
     X = torch.randn(n, d, device=DEV, generator=g).to(torch.bfloat16)

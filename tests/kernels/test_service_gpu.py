@@ -209,7 +209,7 @@ def test_search_global_multi_tenant_pass_matches_per_tenant(tmp_path, monkeypatc
     """search_global_batch over 40 small tenants (1..~700 rows: partial tiles,
     one-row tenants, removed rows) + one big tenant: the one-pass tile-table
     scan (csrc/kernels/mtscan.hip) returns the hits of the per-tenant store
-    searches (LZK_MT_GLOBAL=0), scores to fp32 rounding. overflow=True: a
+    searches (MT_GLOBAL = False), scores to fp32 rounding. overflow=True: a
     threshold that admits every row, so every query's list overflows and is
     redone by the per-tenant path."""
     from lazzaro_amd.ops import search as S

@@ -487,47 +487,6 @@ def test_flat_topk_dual_i8_matches_bf16_dual_gpu(floor):
         assert torch.allclose(s0[fin], s1[fin], atol=1e-4, rtol=0)
 
 
-def _scan8_opted_in():
-    from lazzaro_amd.ops import search as S
-    return S.SCAN8
-
-
-@pytest.mark.skipif(not _scan8_opted_in(), reason="the wide scan8 kernel is opt-in (LZK_SCAN8=1): on the GPU it "
-                    "does not yet match the shared template")
-@pytest.mark.parametrize("D,nq", [(256, 300), (384, 1024), (768, 200), (1024, 512)])
-def test_scan8_matches_template_gpu(D, nq):
-    """The dedicated int8 scan (scan8.hip: cross-tile K stream, int-domain
-    epilogue) finds the same candidate lists as the shared 256^2 template for
-    every K-tile count (KS = 2, 3, 6, 8), partial row / query tiles and
-    removed rows, so the store search's top-k is identical."""
-    from lazzaro_amd.ops import search as S
-    gen = torch.Generator(device=DEV).manual_seed(31 + D)
-    N = 1_100_003
-    X = torch.randn(N, D, device=DEV, generator=gen)
-    X = X / X.norm(dim=1, keepdim=True)
-    X[5] = 0.0  # an all-zero row
-    Q = torch.randn(nq, D, device=DEV, generator=gen)
-    Q = Q / Q.norm(dim=1, keepdim=True)
-    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
-    bias = -(X * X).sum(1).contiguous()
-    bias[::89] = float("-inf")
-    X8, rs = S.quantize_i8_rows(X16)
-    Q8, qs = S.quantize_i8_rows(Q16)
-    margin = torch.full((nq,), 0.02, device=DEV)
-    out = {}
-    saved = S.SCAN8
-    try:
-        for mode in (True, False):
-            S.SCAN8 = mode
-            s8, r8 = S.flat_topk_i8(X8, rs, Q8, qs, X16, Q16, 16, bias=bias, alpha=2.0, margin=margin)
-            cnt = S._ws_cand.get(DEV, 0)[: nq * 4].view(torch.int32).clone() & 0x3FFFFFFF
-            out[mode] = (s8, r8, cnt)
-    finally:
-        S.SCAN8 = saved
-    (sa, ra, ca), (sb, rb, cb) = out[True], out[False]
-    assert torch.equal(ca, cb)  # same candidate count per query
-    assert torch.equal(ra, rb)
-    assert torch.equal(sa, sb)
     s16, r16 = S.flat_topk(X16, Q16, 16, bias=bias, alpha=2.0)
     assert torch.equal(ra[:, :10], r16[:, :10])
 
