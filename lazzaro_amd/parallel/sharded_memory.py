@@ -7,17 +7,19 @@ each rank's part is an ordinary :class:`~lazzaro_amd.core.MemorySystem` graph
 (HBM columns, HIP kernels, incremental persistence under the tenant id
 ``"{user}@{rank}/{world}"``) -- and runs the reference's consolidation over
 the WHOLE buffer with the sequential semantics of the single-process engine:
-``consolidate_batch`` on N ranks gives the nodes, saliences, edges and
-eviction victims that ``MemorySystem.consolidate_batch(cadence="batch")``
-gives on one process holding the union of the rows and all ranks'
-conversations (rank-major order): batch cadence -- eviction, super-nodes and
-``run_consolidation`` once per batch; the single-tenant engine's default
-``cadence="conversation"`` plays them at every conversation like the
-reference. Reference flow: ``memory_system.py:580-649`` (end_conversation),
-``:651-891`` (dedupe, links), ``:535-578`` (eviction), ``:935-1010``
-(run_consolidation).
+``consolidate_batch`` on N ranks gives the nodes, saliences, edges,
+super-nodes and eviction victims that ``MemorySystem.consolidate_batch`` with
+the same ``cadence`` gives on one process holding the union of the rows and
+all ranks' conversations (rank-major order). The default
+``cadence="conversation"`` is the reference's: eviction, super-nodes and
+``run_consolidation`` at every conversation (:meth:`_consolidate_exact`, the
+replicated batch planner); ``cadence="batch"`` plays them once per batch
+(steps 1-8 below). Reference flow: ``memory_system.py:580-649``
+(end_conversation), ``:651-891`` (dedupe, links), ``:535-578`` (eviction),
+``:935-1010`` (run_consolidation).
 
-Per batch (every call is collective; each rank brings its own conversations):
+Per batch with ``cadence="batch"`` (every call is collective; each rank
+brings its own conversations):
 
 1. fact rows (vector, salience, conversation, shard key) are all-gathered
    (C1, F x (4 D + 24) bytes): dedupe and linking compare every fact with
@@ -53,9 +55,19 @@ Per-rank work per batch is (all facts) x (own rows): at a fixed buffer the
 scan is split N ways (strong scaling of the buffer); the exchanged bytes are
 O(facts), never O(rows).
 
-Not supported for a row-sharded tenant: the reference's per-shard mean
-super-nodes (``hierarchy_mode="reference"``: a shard's members span ranks;
-the k-means hierarchy replaces them) and ``merge_mode="pairwise"``
+The reference's per-shard mean super-nodes (``hierarchy_mode="reference"``,
+the default without ``hierarchy_params``; memory_system.py:775-780,
+893-933): a shard's members span ranks, so the planner's member and mean
+callbacks are collective -- each rank contributes the global rows of the
+shard's members it holds and the float64 sum of their fp32 rows, the sums
+are all-gathered and added in rank order (every rank gets the same mean).
+The super-node row lives on the rank holding most of its children; a rank
+holding other children points their parent at a ghost row of it. Node ids
+follow the single process's counter, which super-nodes do not advance:
+a node's global number is its row in the union graph, its id that number
+less the super-nodes before it (:meth:`_ids_of_nums`).
+
+Not supported for a row-sharded tenant: ``merge_mode="pairwise"``
 (reference default is the no-op).
 """
 from __future__ import annotations
@@ -105,10 +117,20 @@ class ShardedMemorySystem:
                  max_buffer_size: int = 10, consolidate_every: int = 3, auto_consolidate: bool = True,
                  auto_prune: bool = True, prune_threshold: float = 0.5,
                  hierarchy_params: Optional[Dict] = None, prune: bool = True, placement: str = "origin",
-                 force_collectives: Optional[bool] = None, **local_kwargs):
+                 force_collectives: Optional[bool] = None, enable_hierarchy: bool = True,
+                 hierarchy_mode: Optional[str] = None, super_node_threshold: int = 20, **local_kwargs):
         from ..core.memory_system import MemorySystem
 
         self.comm = comm or Communicator.local()
+        if hierarchy_mode is None:
+            hierarchy_mode = "kmeans" if hierarchy_params else "reference"
+        if hierarchy_mode not in ("reference", "kmeans"):
+            raise ValueError("hierarchy_mode must be 'reference' or 'kmeans'")
+        # the reference's per-shard mean super-nodes (memory_system.py:893-933)
+        self.ref_hierarchy = bool(enable_hierarchy) and hierarchy_mode == "reference"
+        self.super_node_threshold = int(super_node_threshold)
+        self._sup_v = np.zeros(0, np.int64)  # global rows of the tenant's super-nodes (sorted, every rank)
+        self._super_plan: Dict[Tuple[int, ...], Dict] = {}
         if force_collectives is None:
             import os
             force_collectives = os.environ.get("LZK_FORCE_COLLECTIVES", "0") == "1"
@@ -127,7 +149,8 @@ class ShardedMemorySystem:
         local_kwargs.setdefault("enable_caching", False)
         self.local = MemorySystem(user_id=shard_user_id(user_id, self.comm.rank, self.comm.world),
                                   max_buffer_size=1 << 62, auto_consolidate=False, enable_hierarchy=False,
-                                  auto_prune=auto_prune, prune_threshold=prune_threshold, **local_kwargs)
+                                  auto_prune=auto_prune, prune_threshold=prune_threshold,
+                                  super_node_threshold=super_node_threshold, **local_kwargs)
         self.g = self.local.graph
         self.device = self.g.device
         self.num = torch.full((0,), -1, dtype=torch.long, device=self.device)  # global node number per row
@@ -167,6 +190,8 @@ class ShardedMemorySystem:
             return t, [int(t.shape[0])]
         cnt = self._gather_rows(torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)).tolist()
         mx = max(cnt)
+        if mx == 0:  # nothing anywhere (every rank sees the same counts): no empty collective
+            return t, cnt
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
         g = self._gather_rows(pad)
@@ -231,6 +256,21 @@ class ShardedMemorySystem:
             out = torch.where(ks[pos] == nums, o[pos], out)
         return out
 
+    def _ids_of_nums(self, nums) -> List[str]:
+        """Node ids of fact nodes by global number (row + 1). The single
+        process names nodes with a counter that super-nodes do not advance
+        (reference memory_system.py:_generate_node_id), so a node's id is its
+        number less the super-nodes created before it."""
+        a = np.asarray(nums, np.int64).reshape(-1)
+        if self._sup_v.size:
+            a = a - np.searchsorted(self._sup_v, a - 1, side="left")
+        return [f"node_{int(x)}" for x in a.tolist()]
+
+    @property
+    def _fact_count(self) -> int:
+        """The single process's node counter: fact nodes numbered so far."""
+        return int(self.next_id) - int(self._sup_v.size)
+
     def _register_shards(self, keys: Sequence[str]) -> np.ndarray:
         return np.asarray([self.g.shard_id(k) for k in keys], dtype=np.int32)
 
@@ -261,14 +301,14 @@ class ShardedMemorySystem:
         if m == 0:
             return torch.zeros(0, dtype=torch.long, device=self.device)
         nums = torch.arange(base + off + 1, base + off + m + 1, dtype=torch.long, device=self.device)
-        ids = [f"node_{i}" for i in range(base + off + 1, base + off + m + 1)]
+        ids = self._ids_of_nums(np.arange(base + off + 1, base + off + m + 1))
         now = time.time() if now is None else now
         rows = self.g.add_nodes(ids, list(contents), vectors, shard=codes, types=types, sal=salience, now=now,
                                 stored=True)
         self._sync_num()
         self.num[rows] = nums
         self.holder[rows] = self.rank
-        self.local.node_counter = self.next_id
+        self.local.node_counter = self._fact_count
         self._reach_add(rows)
         return rows
 
@@ -594,7 +634,7 @@ class ShardedMemorySystem:
         if cadence == "conversation":
             with self.local._graph_lock, tracer.stage("sharded_consolidate", dev):
                 self._consolidate_exact(flat, conv, E, B_loc, now, stats)
-                self.local.node_counter = self.next_id
+                self.local.node_counter = self._fact_count
                 with tracer.stage("persist", "cpu"):
                     self.local._save_to_persistence()
             return stats
@@ -613,7 +653,7 @@ class ShardedMemorySystem:
                        or getattr(g, "hier", None) is None):
                 with tracer.stage("cluster", dev):
                     self.cluster_pass()
-            self.local.node_counter = self.next_id
+            self.local.node_counter = self._fact_count
             with tracer.stage("persist", "cpu"):
                 self.local._save_to_persistence()
         return stats
@@ -665,6 +705,15 @@ class ShardedMemorySystem:
             (gs, gm), (ws, wm) = self._candidates(Q, code_t)
         gb_s = gs[:, 0]
         gb_node = gm[:, 0, 0] >= 0
+        # the dedupe top-1 is the store's, by L2: a super-node (a mean, not a
+        # unit row) can beat the list head (single process: _scan_batch)
+        sup_win = sup_head = None
+        if self.ref_hierarchy:
+            srows, scos, sn2, _ = self._stored_supers(Qn)
+            if srows.size:
+                sup_win, sup_head, sup_cos = self._super_heads(qn, gs, gm, srows, scos, sn2)
+                gb_s = torch.where(sup_win, sup_cos, gb_s)
+                gb_node = gb_node | sup_win
 
         # ---- 3. replicated decisions
         with tracer.stage("sc_dedupe", dev):
@@ -680,8 +729,13 @@ class ShardedMemorySystem:
         # ---- 5. duplicate merges onto the rows this rank holds
         stats["dup"] += int(dup.sum())
         mine_dup = dup_graph & (gm[:, 0, 2] == self.rank)
+        tgt_row = gm[:, 0, 3]
+        if sup_win is not None:
+            srow_l = self._held_rows(sup_head.clamp_min(0))
+            mine_dup = torch.where(sup_win, dup_graph & (srow_l >= 0), mine_dup)
+            tgt_row = torch.where(sup_win, srow_l, tgt_row)
         if bool(mine_dup.any()):
-            rows = gm[:, 0, 3][mine_dup]
+            rows = tgt_row[mine_dup]
             with g.on_stream():
                 g.sal.scatter_reduce_(0, rows, sal_dec[mine_dup].float(), "amax", include_self=True)
                 g.last[rows] = now
@@ -713,7 +767,7 @@ class ShardedMemorySystem:
             nums_h = new_num[mk].cpu().numpy()
             lf = [flat[int(i) - f_off] for i in mkh]
             with tracer.stage("sc_insert", dev):
-                rows = g.add_nodes([f"node_{int(x)}" for x in nums_h], [f["content"] for f in lf], Q[mk],
+                rows = g.add_nodes(self._ids_of_nums(nums_h), [f["content"] for f in lf], Q[mk],
                                    shard=codes[mkh], types=[f.get("type", "semantic") for f in lf],
                                    sal=sal_new[mk].float(), acc=acc_new[mk], now=now, stored=True)
             self._sync_num()
@@ -730,6 +784,70 @@ class ShardedMemorySystem:
                                       (gs, gm[:, :, 0]), keep, B, thr, stats)
             if plan is not None:
                 self._apply_edges(plan, new_num, row_of_fact, origin, code_t, (gm, wm), now)
+
+        # ---- 8. the reference hierarchy at the batch end (the single
+        # process's coarse path: a shard's super-node over all its members)
+        if self.ref_hierarchy:
+            with tracer.stage("sc_supers", dev):
+                self._make_supers_batch(codes[kidx.cpu().numpy()].tolist(), Q, now)
+
+    def _super_heads(self, qn, gs, gm, srows, scos, sn2):
+        """Per fact: whether the best super-node by the store's L2 score
+        (2 |q| |x| cos - |x|^2) beats the merged global head, that
+        super-node's global row and cosine (a tie: the lower row, as in the
+        single process's ``_scan_batch``). The head's |x|^2 (fp32 column)
+        comes from its holder (one all-reduce of F doubles)."""
+        g = self.g
+        dev = self.device
+        F = gs.shape[0]
+        sc_t = torch.as_tensor(scos, dtype=torch.float64).to(dev)
+        n2_t = torch.as_tensor(sn2, dtype=torch.float64).to(dev)
+        q = qn.reshape(-1).to(dev, torch.float64)
+        l2s = 2.0 * q[:, None] * n2_t.sqrt()[None, :] * sc_t - n2_t[None, :]
+        j = torch.argmax(l2s, 1)  # first maximum: the lowest super row on a tie
+        sl2 = l2s.gather(1, j[:, None])[:, 0]
+        sv = torch.as_tensor(srows, dtype=torch.long).to(dev)[j]
+        hr = gm[:, 0, 3]
+        mine = (gm[:, 0, 2] == self.rank) & (hr >= 0)
+        hn2 = torch.zeros(F, dtype=torch.float64, device=dev)
+        if bool(mine.any()):
+            with g.on_stream():
+                hn2[mine] = g.sqn[hr[mine]].double()
+        if self._coll:
+            hn2 = self.comm.all_reduce(self._to_comm(hn2)).to(dev)
+        hv = gm[:, 0, 0] - 1
+        hs = gs[:, 0].to(dev, torch.float64)
+        hl2 = torch.where(hv >= 0, 2.0 * q * hs * hn2.sqrt() - hn2, torch.full_like(hs, NEG_INF))
+        win = (sl2 > hl2) | ((sl2 == hl2) & (sv < hv))
+        return win, torch.where(win, sv, torch.full_like(sv, -1)), sc_t.gather(1, j[:, None])[:, 0]
+
+    def _make_supers_batch(self, kept_codes: List[int], Q: torch.Tensor, now: float) -> None:
+        """Batch cadence: a super-node for every shard of the batch's kept
+        facts (first-seen order) that passed ``super_node_threshold`` members
+        and has none (reference memory_system.py:775-780, 893-933). Collective."""
+        g = self.g
+        dev = self.device
+        order = list(dict.fromkeys(int(c) for c in kept_codes))
+        if not order:
+            return
+        _, _, _, have = self._stored_supers(torch.zeros((0, g.dim), dtype=torch.float64, device=dev))
+        have = set(have)
+        sc = torch.as_tensor(g.shard_count, dtype=torch.int64).to(dev)
+        if self._coll:
+            sc = self.comm.all_reduce(self._to_comm(sc)).to(dev)
+        sc = sc.cpu().tolist()
+        for code in order:
+            if sc[code] <= self.super_node_threshold or code in have:
+                continue
+            children = self._pre_members(code)
+            info = self._super_mean(children, np.zeros(0, np.int64), Q, BIG, np.zeros(0, np.int64), [], 0)
+            if info is None:
+                continue
+            sp = {"code": code, "key": int(self.next_id), "children": children}
+            self.next_id += 1
+            self._sup_v = np.union1d(self._sup_v, np.asarray([sp["key"]], np.int64))
+            self._insert_super(sp, info, now)
+            have.add(code)
 
     def _apply_edges(self, plan, new_num, row_of_fact, origin, code_t, hits, now) -> None:
         """Append the planned edges whose source this rank holds; an endpoint
@@ -776,18 +894,18 @@ class ShardedMemorySystem:
             dn_h = Dn[need].cpu().numpy()
             sh_h = dst_shard[need].cpu().numpy()
             ho_h = dst_hold[need].cpu().numpy()
-            ids = [f"node_{int(x)}" for x in dn_h]
+            ids = self._ids_of_nums(dn_h)
             have = [g.row_of.get(i, -1) for i in ids]
             fresh = {}
-            for i, r, s_, h_ in zip(ids, have, sh_h.tolist(), ho_h.tolist()):
+            for i, r, x, s_, h_ in zip(ids, have, dn_h.tolist(), sh_h.tolist(), ho_h.tolist()):
                 if r < 0 and i not in fresh:
-                    fresh[i] = (s_, h_)
+                    fresh[i] = (s_, h_, x)
             if fresh:
                 fid = list(fresh)
                 rows_new = g.add_nodes(fid, [""] * len(fid), None, shard=[fresh[i][0] for i in fid], ghost=True,
                                        stored=False, now=now)
                 self._sync_num()
-                self.num[rows_new] = torch.as_tensor([int(i[5:]) for i in fid], dtype=torch.long).to(dev)
+                self.num[rows_new] = torch.as_tensor([fresh[i][2] for i in fid], dtype=torch.long).to(dev)
                 self.holder[rows_new] = torch.as_tensor([fresh[i][1] for i in fid], dtype=torch.long).to(dev)
             rr = torch.as_tensor([g.row_of[i] for i in ids], dtype=torch.long).to(dev)
             dst_rows[need] = rr
@@ -916,6 +1034,156 @@ class ShardedMemorySystem:
                 a[:, 5] != 0, a[:, 6])
         return rows, cols, dict(zip(rows.tolist(), a[:, 7].astype(np.int64).tolist()))
 
+    # ------------------------------------------------------------------ reference hierarchy
+    def _stored_supers(self, Qn: torch.Tensor):
+        """The tenant's super-nodes as the batch planner sees them (the single
+        process's ``_plan_inputs``): global rows (ascending), every fact's
+        cosine with each (fp32 row, |x| from the stored |x|^2), their |x|^2,
+        and the shard codes that have one. Collective (one variable-length
+        gather of a few rows); refreshes the id map."""
+        g = self.g
+        dev = self.device
+        F = int(Qn.shape[0])
+        n = g.n
+        st = torch.zeros(0, dtype=torch.long, device=dev)
+        if n and g.n_super:
+            with g.on_stream():
+                st = torch.nonzero((g.kind[:n] == NODE) & (g.sup[:n] != 0)
+                                   & (self.holder[:n] == self.rank)).flatten()
+        blk = torch.zeros((st.numel(), 3 + F), dtype=torch.float64, device=dev)
+        if st.numel():
+            with g.on_stream():
+                X = g.emb32[st].double()
+                sq = g.sqn[st].double()
+                nrm = sq.sqrt()
+                blk[:, 0] = self._vrows(st).double()
+                blk[:, 1] = g.shard[st].double()
+                blk[:, 2] = sq
+                if F:
+                    blk[:, 3:] = ((Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]).T
+        allb, _ = self._gather_var(blk)
+        a = allb.cpu().numpy()
+        if a.shape[0]:
+            a = a[np.argsort(a[:, 0], kind="stable")]
+        rows = a[:, 0].astype(np.int64)
+        self._sup_v = np.union1d(self._sup_v, rows)
+        cos = np.ascontiguousarray(a[:, 3:].T) if F else np.zeros((0, rows.size))
+        return rows, cos, a[:, 2].copy(), sorted(set(a[:, 1].astype(np.int64).tolist()))
+
+    def _pre_members(self, code: int) -> np.ndarray:
+        """Global rows (ascending) of shard ``code``'s live non-super nodes
+        over every rank -- the planner's ``pre_members`` callback (collective:
+        every rank's planner calls it at the same point)."""
+        g = self.g
+        n = g.n
+        v = torch.zeros(0, dtype=torch.long, device=self.device)
+        if n:
+            with g.on_stream():
+                m = (g.kind[:n] == NODE) & (g.sup[:n] == 0) & (g.shard[:n] == int(code)) & \
+                    (self.holder[:n] == self.rank)
+                v = self._vrows(torch.nonzero(m).flatten())
+        allv, _ = self._gather_var(v)
+        return np.sort(allv.cpu().numpy().astype(np.int64))
+
+    def _super_mean(self, children: np.ndarray, new_facts: np.ndarray, Q: torch.Tensor, n0: int,
+                    origin_h: np.ndarray, flat, f_off: int) -> Optional[Dict]:
+        """A planned super-node's mean embedding, holder and the contents of
+        its first three children (collective). ``children``: global rows, the
+        pre-batch ones (< n0, held anywhere) first, then batch facts
+        ``new_facts`` (rows of ``Q``). Every rank sums the fp32 rows it holds
+        in float64; the per-rank sums are all-gathered and added in rank
+        order, so every rank gets the same mean (the single process sums all
+        rows in one pass: the fp32 mean agrees with its to rounding). Holder:
+        the rank holding the most children (the lowest on a tie)."""
+        g = self.g
+        dev = self.device
+        D = g.dim
+        ch = np.asarray(children, np.int64)
+        nf = np.asarray(new_facts, np.int64)
+        pre = ch[ch < n0]
+        part = torch.zeros((1, D + 1), dtype=torch.float64, device=dev)
+        n_held = 0
+        if pre.size and g.n:
+            loc = self._held_rows(torch.as_tensor(pre).to(dev))
+            loc = loc[loc >= 0]
+            n_held = int(loc.numel())
+            if n_held:
+                with g.on_stream():
+                    part[0, :D] = g.emb32[loc].double().sum(0)
+        if nf.size:
+            n_held += int((origin_h[nf] == self.rank).sum())
+        part[0, D] = float(n_held)
+        allp = self._gather_rows(part)
+        tot = allp[0, :D].clone()
+        for r in range(1, allp.shape[0]):
+            tot += allp[r, :D]
+        cnt = int(pre.size + nf.size)
+        if nf.size:
+            tot += Q[torch.as_tensor(nf, dtype=torch.long).to(Q.device)].to(dev).double().sum(0)
+        # first three children's contents, from the rank that has each
+        txt = {}
+        head = ch[:3]
+        hp = head[head < n0]
+        if hp.size and g.n:
+            lr = self._held_rows(torch.as_tensor(hp).to(dev)).cpu().tolist()
+            for i, r in enumerate(lr):
+                if r >= 0:
+                    txt[i] = g.content[r]
+        for i in range(int(hp.size), int(head.size)):
+            j = int(nf[i - int(pre.size)])
+            if int(origin_h[j]) == self.rank:
+                txt[i] = flat[j - f_off]["content"]
+        if self._coll:
+            for part_ in self.comm.all_gather_object(txt):
+                txt.update(part_)
+        if cnt == 0:
+            return None
+        return {"emb": (tot / cnt).float(), "holder": int(torch.argmax(allp[:, D]).item()),
+                "contents": [txt[i] for i in range(int(head.size))]}
+
+    def _insert_super(self, sp: Dict, info: Dict, now: float, sal: float = 0.5, acc: int = 0,
+                      last: Optional[float] = None) -> None:
+        """Apply one planned super-node on every rank (reference
+        memory_system.py:893-933): its holder adds the row -- id
+        ``super_<shard>_<int(now)>``, the "Topic: ..." summary of the first
+        three children, the mean embedding, every child's id; unstored -- and
+        every rank holding children points their parent at it (a ghost row of
+        the super-node where it is held elsewhere)."""
+        g = self.g
+        dev = self.device
+        code = int(sp["code"])
+        key = int(sp["key"])
+        skey = g.shard_names[code]
+        children = np.asarray(sp["children"], np.int64)
+        sid = f"super_{skey}_{int(now)}"
+        h = int(info["holder"])
+        held = torch.zeros(0, dtype=torch.long, device=dev)
+        if children.size and g.n:
+            loc = self._held_rows(torch.as_tensor(children).to(dev))
+            held = loc[loc >= 0]
+        srow = -1
+        if self.rank == h:
+            summary = f"Topic: {skey}. Contains memories about: " + "; ".join(info["contents"])
+            rows = g.add_nodes([sid], [summary], info["emb"][None, :], shard=[code], sup=[1],
+                               children={0: self._ids_of_nums(children + 1)}, stored=False, sal=float(sal),
+                               acc=int(acc), last=float(now if last is None else last), now=now)
+        elif held.numel() and g.row_of.get(sid, -1) < 0:
+            rows = g.add_nodes([sid], [""], None, shard=[code], sup=[1], ghost=True, stored=False, now=now)
+        else:
+            rows = None
+        if rows is not None:
+            srow = int(rows[0])
+            self._sync_num()
+            self.num[srow] = key + 1
+            self.holder[srow] = h
+        elif held.numel():
+            srow = int(g.row_of[sid])
+        if held.numel():
+            with g.on_stream():
+                g.parent[held] = srow
+                g.dirty[held] = 1
+            g._bump()
+
     def _consolidate_exact(self, flat, conv, E, B_loc, now, stats) -> None:
         """The reference cadence over the row-sharded buffer: every rank runs
         the SAME native batch planner (core/batch_plan.py) on the global
@@ -1014,11 +1282,28 @@ class ShardedMemorySystem:
             s_, v_ = self._gather_lists(s_, v_, K)
             return s_[0].cpu().numpy(), v_[0].cpu().numpy()
 
-        def no_super(*a):
-            raise RuntimeError("a row-sharded tenant has no per-shard mean super-nodes")
+        # ---- the reference hierarchy: stored super-nodes, collective member /
+        # mean callbacks for the ones the plan creates
+        n0 = int(self.next_id)
+        origin_h = origin.cpu().numpy() if F else np.zeros(0, np.int64)
+        self._super_plan = {}
+        if self.ref_hierarchy:
+            sup_rows, sup_cos, sup_n2, super_codes = self._stored_supers(Qn)
+        else:
+            sup_rows, sup_cos, sup_n2, super_codes = np.zeros(0, np.int64), np.zeros((F, 0)), np.zeros(0), []
+
+        def super_cos(children, new_facts):  # collective, like fallback
+            ch = np.asarray(children, np.int64)
+            info = self._super_mean(ch, new_facts, Q, n0, origin_h, flat, f_off)
+            if info is None:
+                return np.full(F, NEG_INF), 1.0
+            self._super_plan[tuple(ch.tolist())] = info
+            ed = info["emb"].double()
+            n2 = float((ed * ed).sum().float())
+            en = n2 ** 0.5
+            return (((Qn @ ed) / (en if en > 0 else 1.0)).cpu().numpy() if F else np.zeros(0)), n2
 
         # ---- 3. plan (identical on every rank), eviction pool verified everywhere
-        n0 = int(self.next_id)
         node_count = self._sum(g.num_nodes())[0]
         nsh = len(g.shard_count)
         sc = torch.zeros(nsh, dtype=torch.int64, device=dev)
@@ -1035,14 +1320,14 @@ class ShardedMemorySystem:
         while True:
             with tracer.stage("sc_pool", dev):
                 pool, pmask = self._exact_pool(B, P, now)
-                want = np.unique(np.concatenate([pool, glob[1][glob[1] >= 0], shard[1][shard[1] >= 0]]))
+                want = np.unique(np.concatenate([pool, glob[1][glob[1] >= 0], shard[1][shard[1] >= 0], sup_rows]))
                 rows_v, cols, holder_of = self._row_states(want)
             kw = dict(ct=ct_np, code=codes, sal_in=sal_np, n0=n0, node_count=node_count, shard_count=shard_count,
-                      super_codes=[], pre_members=no_super, max_buffer=self.max_buffer_size,
-                      super_threshold=getattr(self.local, "super_node_threshold", 20), ref_hierarchy=False,
+                      super_codes=super_codes, pre_members=self._pre_members, max_buffer=self.max_buffer_size,
+                      super_threshold=self.super_node_threshold, ref_hierarchy=self.ref_hierarchy,
                       prune_thr=thr, keep=keep, now=now, pool=pool, rows=rows_v, cols=cols, glob=glob, shard=shard,
-                      sup_rows=np.zeros(0, np.int64), sup_cos=np.zeros((F, 0)), sup_n2=np.zeros(0), qnorm=qnorm,
-                      fact_n2=fact_n2, S=S, super_cos=no_super, fallback=fallback)
+                      sup_rows=sup_rows, sup_cos=sup_cos, sup_n2=sup_n2, qnorm=qnorm,
+                      fact_n2=fact_n2, S=S, super_cos=super_cos, fallback=fallback)
             with tracer.stage("cb_plan", "cpu"):
                 pl = plan(kw, B, self.conversation_count, self.auto_consolidate, self.consolidate_every, cl_every,
                           native=self.local.NATIVE_PLANNER)
@@ -1066,20 +1351,22 @@ class ShardedMemorySystem:
             stats[k_] += int(ps[k_])
         pruned = int(ps["pruned_new"])
         fact_key = np.asarray(pl["fact_key"], np.int64)
-        origin_h = origin.cpu().numpy() if F else np.zeros(0, np.int64)
+        supers = pl["supers"]
+        if supers:  # node ids of the batch's facts skip the super-node rows
+            self._sup_v = np.union1d(self._sup_v, np.asarray([int(sp["key"]) for sp in supers], np.int64))
         # new rows: holder and shard (the ghost rows of edges need them)
         for j in np.nonzero(fact_key >= 0)[0].tolist():
             holder_of[int(fact_key[j])] = int(origin_h[j])
         shard_of = dict(zip(rows_v.tolist(), cols[3].tolist()))
         for j in np.nonzero(fact_key >= 0)[0].tolist():
             shard_of[int(fact_key[j])] = int(codes[j])
-        self.next_id = n0 + int(ps["inserted"])
+        self.next_id = n0 + int(ps["inserted"]) + len(supers)
         count0 = self.conversation_count
         etype = g.etype("relates_to")
         for seg in pl["segments"]:
             with tracer.stage("cb_apply", dev):
-                pruned_local = self._apply_exact_segment(seg, fact_key, origin_h, codes, Q, flat, f_off, holder_of,
-                                                         shard_of, thr, now, etype)
+                pruned_local = self._apply_exact_segment(seg, supers, fact_key, origin_h, codes, Q, flat, f_off,
+                                                         holder_of, shard_of, thr, now, etype)
             pruned += self._sum(pruned_local)[0]
             self.conversation_count = count0 + int(seg["c1"]) + 1
             if seg["consolidate"]:
@@ -1095,8 +1382,8 @@ class ShardedMemorySystem:
         if self.local.query_cache:
             self.local.query_cache.invalidate_results()
 
-    def _apply_exact_segment(self, seg, fact_key, origin_h, codes, Q, flat, f_off, holder_of, shard_of, thr, now,
-                             etype) -> int:
+    def _apply_exact_segment(self, seg, supers, fact_key, origin_h, codes, Q, flat, f_off, holder_of, shard_of, thr,
+                             now, etype) -> int:
         """This rank's part of one plan segment (see :meth:`_consolidate_exact`).
         Returns the local edges the segment's decay pruned."""
         g = self.g
@@ -1130,17 +1417,18 @@ class ShardedMemorySystem:
                         g.last[rt] = torch.as_tensor(np.asarray(seg["tch_last"])[k_h], dtype=torch.float64).to(dev)
                         g.dirty[rt] = 1
                     g._bump()
-        kinds = np.asarray(seg["ins_kind"]).tolist()
-        if any(k_ != 0 for k_ in kinds):
-            raise RuntimeError("a row-sharded tenant plans no super-nodes")
-        idx = np.asarray(seg["ins_idx"], np.int64)
+        kinds = np.asarray(seg["ins_kind"], np.int64).reshape(-1)
+        idx_all = np.asarray(seg["ins_idx"], np.int64).reshape(-1)
+        fpos = np.nonzero(kinds == 0)[0]
+        idx = idx_all[fpos]
         if idx.size:
-            mine = idx[origin_h[idx] == me]
+            sel_ = origin_h[idx] == me
+            mine = idx[sel_]
             if mine.size:
-                pos = np.nonzero(origin_h[idx] == me)[0]
+                pos = fpos[sel_]
                 keys = fact_key[mine]
                 lf = [flat[int(j) - f_off] for j in mine]
-                rows = g.add_nodes([f"node_{int(k_) + 1}" for k_ in keys], [f["content"] for f in lf],
+                rows = g.add_nodes(self._ids_of_nums(keys + 1), [f["content"] for f in lf],
                                    Q[torch.as_tensor(mine, dtype=torch.long).to(dev)], shard=codes[mine].astype(np.int32),
                                    types=[f.get("type", "semantic") for f in lf],
                                    sal=torch.as_tensor(np.asarray(seg["ins_sal"], np.float32)[pos]),
@@ -1151,6 +1439,12 @@ class ShardedMemorySystem:
                 self.num[rows] = torch.as_tensor(keys + 1, dtype=torch.long).to(dev)
                 self.holder[rows] = me
                 self._reach_add(rows)
+        # super-nodes after the facts: their children (earlier keys) all exist
+        for p in np.nonzero(kinds != 0)[0].tolist():
+            sp = supers[int(idx_all[p])]
+            info = self._super_plan[tuple(np.asarray(sp["children"], np.int64).tolist())]
+            self._insert_super(sp, info, now, sal=float(np.asarray(seg["ins_sal"])[p]),
+                               acc=int(np.asarray(seg["ins_acc"])[p]), last=float(np.asarray(seg["ins_last"])[p]))
         es = np.asarray(seg["edge_src"], np.int64)
         if es.size:
             ed = np.asarray(seg["edge_dst"], np.int64)
@@ -1167,17 +1461,17 @@ class ShardedMemorySystem:
                 need = torch.nonzero(dst < 0).flatten() if remote else None
                 if need is not None and need.numel():  # endpoints held elsewhere: ghost rows (created once per node)
                     dv = ed[need.cpu().numpy()]
-                    ids = [f"node_{int(x) + 1}" for x in dv]
+                    ids = self._ids_of_nums(dv + 1)
                     fresh = {}
                     for i, x in zip(ids, dv.tolist()):
                         if g.row_of.get(i, -1) < 0 and i not in fresh:
-                            fresh[i] = (int(shard_of[int(x)]), int(holder_of[int(x)]))
+                            fresh[i] = (int(shard_of[int(x)]), int(holder_of[int(x)]), int(x) + 1)
                     if fresh:
                         fid = list(fresh)
                         rn = g.add_nodes(fid, [""] * len(fid), None, shard=[fresh[i][0] for i in fid], ghost=True,
                                          stored=False, now=now)
                         self._sync_num()
-                        self.num[rn] = torch.as_tensor([int(i[5:]) for i in fid], dtype=torch.long).to(dev)
+                        self.num[rn] = torch.as_tensor([fresh[i][2] for i in fid], dtype=torch.long).to(dev)
                         self.holder[rn] = torch.as_tensor([fresh[i][1] for i in fid], dtype=torch.long).to(dev)
                     dst[need] = torch.as_tensor([g.row_of[i] for i in ids], dtype=torch.long).to(dev)
                 g.append_edges(src, dst, torch.as_tensor(ew).to(dev), torch.as_tensor(ec, dtype=torch.int32).to(dev),
@@ -1361,7 +1655,7 @@ class ShardedMemorySystem:
         if m_in:
             txt = [t for part in got_txt if part for t in part]
             nums = r_num[:, 0].long()
-            rows = g.add_nodes([f"node_{int(x)}" for x in nums.tolist()], [t[0] for t in txt], r_emb,
+            rows = g.add_nodes(self._ids_of_nums(nums.tolist()), [t[0] for t in txt], r_emb,
                                shard=r_num[:, 1].int(), types=[t[1] for t in txt], sal=r_num[:, 2].float(),
                                acc=r_num[:, 3].int(), last=r_num[:, 4], ts=r_num[:, 5], stored=True)
             self._sync_num()
@@ -1376,7 +1670,7 @@ class ShardedMemorySystem:
             if miss.numel():
                 un, first = np.unique(dn[miss].cpu().numpy(), return_index=True)
                 fi = miss[torch.as_tensor(first, dtype=torch.long).to(dev)]
-                rows_g = g.add_nodes([f"node_{int(x)}" for x in un], [""] * len(un), None,
+                rows_g = g.add_nodes(self._ids_of_nums(un), [""] * len(un), None,
                                      shard=r_edge[fi, 7].int(), ghost=True, stored=False)
                 self._sync_num()
                 self.num[rows_g] = torch.as_tensor(un).to(dev)

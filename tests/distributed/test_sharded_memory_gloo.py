@@ -45,6 +45,10 @@ def _data(cfg=CPU):
     rng = random.Random(11)
     sal0 = [round(rng.uniform(0.3, 0.95), 6) for _ in range(ROWS)]
     keys0 = [TOPICS[i % 3] for i in range(ROWS)]
+    tight = cfg.get("tight", False)
+    if tight:  # one tight topic: its super-node's mean is close enough to dedupe facts onto it
+        for i in range(2, ROWS, 3):
+            X[i] = _unit(centers[0] + noise / 3 * torch.randn(DIM, generator=g))
     steps = []
     for s in range(STEPS):
         convs, vecs = [], []
@@ -52,6 +56,12 @@ def _data(cfg=CPU):
             facts = []
             for f in range(rng.randint(1, 4)):
                 kind = rng.random()
+                if tight and 0.8 <= kind < 0.88:
+                    v = _unit(centers[0] + noise / 4 * torch.randn(DIM, generator=g))  # onto the tight topic
+                    facts.append({"content": f"fact {s}.{c}.{f} about learning", "type": "semantic",
+                                  "salience": round(rng.uniform(0.3, 0.95), 6), "topic": "learning"})
+                    vecs.append(v)
+                    continue
                 if kind < 0.2:
                     v = _unit(X[rng.randrange(ROWS)] + noise / 9 * torch.randn(DIM, generator=g))  # duplicate
                 elif kind < 0.3 and vecs:
@@ -80,11 +90,21 @@ def _split(n, world, r, weights=None):
     return lo, lo + per[r]
 
 
+def _sid(i):
+    """Super-node ids without their creation second (the single process's
+    batch cadence stamps them with the wall clock)."""
+    return i.rsplit("_", 1)[0] if i.startswith("super_") else i
+
+
 def _graph_state(g):
     from lazzaro_amd.engine.tenant_graph import NODE
     n = g.n
     kind, sal, acc, sh = (g.kind[:n].tolist(), g.sal[:n].tolist(), g.acc[:n].tolist(), g.shard[:n].tolist())
-    nodes = {g.ids[r]: (round(sal[r], 5), acc[r], g.shard_names[sh[r]]) for r in range(n) if kind[r] == NODE}
+    par, sup = g.parent[:n].tolist(), g.sup[:n].tolist()
+    nodes = {_sid(g.ids[r]): (round(sal[r], 5), acc[r], g.shard_names[sh[r]],
+                              _sid(g.ids[par[r]]) if par[r] >= 0 else None,
+                              (g.content[r], list(g.children.get(r, []))) if sup[r] else None)
+             for r in range(n) if kind[r] == NODE}
     e = g.e
     edges = {}
     for s, d, w, m in zip(e["src"].tolist(), e["dst"].tolist(), e["w"].tolist(), e["meta"].tolist()):
@@ -103,7 +123,8 @@ def _single(tmp, cfg=CPU):
     X, sal0, keys0, steps = _data(cfg)
     dev = cfg["device"]
     ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=cfg["dim"]), enable_async=False,
-                      db_dir=tmp, user_id="solo", device=dev, max_buffer_size=cfg["limit"], enable_hierarchy=False,
+                      db_dir=tmp, user_id="solo", device=dev, max_buffer_size=cfg["limit"],
+                      enable_hierarchy=cfg.get("hier", False), super_node_threshold=cfg.get("sthr", 20),
                       load_from_disk=False, enable_caching=False)
     g = ms.graph
     codes = [g.shard_id(k) for k in keys0]
@@ -141,6 +162,8 @@ def _sharded(comm, cfg=CPU):
     pruned = cfg.get("pruned", False)
     extra = dict(hierarchy_params={"fine": 12, "top": 4, "every": 10 ** 6, "iters": 3}, placement="cluster",
                  prune=True) if pruned else {}
+    if not pruned:
+        extra.update(enable_hierarchy=cfg.get("hier", False), super_node_threshold=cfg.get("sthr", 20))
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
                              embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev,
                              force_collectives=cfg.get("force", False), **extra)
@@ -292,3 +315,35 @@ def test_sharded_hierarchy_distributed_kmeans():
         assert out[r]["same_centroids"]  # the topic level is identical on every rank
         assert out[r]["labelled"] == out[r]["nodes"]  # every live node of the tenant has a fine cluster
         assert out[r]["shape"][0] == 16
+
+
+HIER = dict(EXACT, hier=True, tight=True)
+
+
+def _check_supers(out):
+    nodes = out[0]["nodes"]
+    sups = [k for k, v in nodes.items() if v[4] is not None]
+    assert sups, "no super-node was created"
+    assert sum(1 for v in nodes.values() if v[3] is not None) > 0  # children point at their super-node
+    return nodes, sups
+
+
+@pytest.mark.parametrize("world,sthr", [(1, 20), (2, 20), (3, 62), (8, 62)])
+def test_sharded_tenant_reference_hierarchy_matches_single_process(world, sthr):
+    """The reference's per-shard mean super-nodes over the row-sharded buffer
+    (collective member lists and means): the same super-nodes -- id, summary,
+    children, salience, access count -- the same parents, dedupes onto a
+    super-node and every other decision as the single process with
+    enable_hierarchy=True. sthr=62: shards cross the threshold mid-batch (the
+    children are pre-batch rows AND facts of the batch)."""
+    out = spawn(world, functools.partial(_sharded, cfg=dict(HIER, sthr=sthr)))
+    check_equivalent(out, world, LIMIT)
+    nodes, sups = _check_supers(out)
+    assert any(nodes[s][1] > 0 for s in sups)  # facts were merged onto a super-node
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tenant_reference_hierarchy_batch_cadence(world):
+    out = spawn(world, functools.partial(_sharded, cfg=dict(CPU, hier=True, tight=True)))
+    check_equivalent(out, world, LIMIT)
+    _check_supers(out)

@@ -21,3 +21,16 @@ GPU = {"rows": 100_000, "dim": 128, "limit": 100_050, "steps": 3, "convs": 48, "
 def test_sharded_tenant_gpu_matches_single_process():
     out = spawn(2, functools.partial(_sharded, cfg=GPU))
     check_equivalent(out, 2, GPU["limit"])
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_sharded_tenant_gpu_reference_hierarchy():
+    """The reference cadence with the reference's per-shard mean super-nodes
+    (collective member lists / means, super-node rows held by the rank with
+    most children) on the GPU path: the single process's state, super-nodes
+    and parents included."""
+    cfg = dict(GPU, steps=2, convs=24, cadence="conversation", hier=True, tight=True, sthr=20)
+    out = spawn(2, functools.partial(_sharded, cfg=cfg))
+    check_equivalent(out, 2, cfg["limit"])
+    nodes = out[0]["nodes"]
+    assert any(v[4] is not None for v in nodes.values())

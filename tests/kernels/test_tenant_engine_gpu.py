@@ -487,10 +487,6 @@ def test_flat_topk_dual_i8_matches_bf16_dual_gpu(floor):
         assert torch.allclose(s0[fin], s1[fin], atol=1e-4, rtol=0)
 
 
-    s16, r16 = S.flat_topk(X16, Q16, 16, bias=bias, alpha=2.0)
-    assert torch.equal(ra[:, :10], r16[:, :10])
-
-
 def test_zero_row_keeps_int8_error_model_gpu():
     """An embedding-less (all-zero) row quantises exactly with scale 0: the
     tenant's int8 error model (max row scale) and the scan's candidate lists
