@@ -131,6 +131,7 @@ class ShardedMemorySystem:
         self.super_node_threshold = int(super_node_threshold)
         self._sup_v = np.zeros(0, np.int64)  # global rows of the tenant's super-nodes (sorted, every rank)
         self._super_plan: Dict[Tuple[int, ...], Dict] = {}
+        self._commit_each = False
         if force_collectives is None:
             import os
             force_collectives = os.environ.get("LZK_FORCE_COLLECTIVES", "0") == "1"
@@ -576,7 +577,8 @@ class ShardedMemorySystem:
 
     # ------------------------------------------------------------------ consolidation
     def consolidate_batch(self, conversations: Sequence[Sequence[Dict]], embeddings=None,
-                          now: Optional[float] = None, cadence: str = "conversation") -> Dict[str, int]:
+                          now: Optional[float] = None, cadence: str = "conversation",
+                          commit: str = "batch") -> Dict[str, int]:
         """Collective batched ``end_conversation`` (see module doc). Each rank
         passes its own finished conversations' extracted facts (and optionally
         their vectors, aligned with the flattened facts). Returns the counts of
@@ -585,9 +587,16 @@ class ShardedMemorySystem:
         ``cadence="conversation"`` (default): the reference's per-conversation
         cadence -- the state ``MemorySystem.consolidate_batch`` (same cadence)
         reaches on one process holding the union (:meth:`_consolidate_exact`);
-        ``"batch"``: eviction and run_consolidation once per batch."""
+        ``"batch"``: eviction and run_consolidation once per batch.
+        ``commit="conversation"`` (with the conversation cadence): every rank
+        commits its rows after each conversation of the batch is applied --
+        the reference's save per ``end_conversation`` (memory_system.py:648,
+        785); ``"batch"``: one commit per rank per batch."""
         if cadence not in ("conversation", "batch"):
             raise ValueError("cadence must be 'conversation' or 'batch'")
+        if commit not in ("conversation", "batch"):
+            raise ValueError("commit must be 'conversation' or 'batch'")
+        self._commit_each = commit == "conversation" and cadence == "conversation"
         g = self.g
         dev = self.device
         flat, conv, idx = [], [], []
@@ -1330,7 +1339,7 @@ class ShardedMemorySystem:
                       fact_n2=fact_n2, S=S, super_cos=super_cos, fallback=fallback)
             with tracer.stage("cb_plan", "cpu"):
                 pl = plan(kw, B, self.conversation_count, self.auto_consolidate, self.consolidate_every, cl_every,
-                          native=self.local.NATIVE_PLANNER)
+                          native=self.local.NATIVE_PLANNER, seg_each=self._commit_each)
             with tracer.stage("cb_verify", dev):
                 ok = True
                 if pmask is not None and pl["events"]:
@@ -1363,6 +1372,7 @@ class ShardedMemorySystem:
         self.next_id = n0 + int(ps["inserted"]) + len(supers)
         count0 = self.conversation_count
         etype = g.etype("relates_to")
+        n_fact = n0 - int(np.searchsorted(self._sup_v, n0))
         for seg in pl["segments"]:
             with tracer.stage("cb_apply", dev):
                 pruned_local = self._apply_exact_segment(seg, supers, fact_key, origin_h, codes, Q, flat, f_off,
@@ -1376,6 +1386,11 @@ class ShardedMemorySystem:
             if seg["cluster"]:
                 with tracer.stage("cluster", dev):
                     self.cluster_pass()
+            if self._commit_each:  # the counter as of this conversation
+                n_fact += int((np.asarray(seg["ins_kind"]) == 0).sum())
+                self.local.node_counter = n_fact
+                with tracer.stage("commit", "cpu"):
+                    self.local._save_to_persistence()
         stats["pruned"] += pruned
         if self.hierarchy_params and getattr(g, "hier", None) is None:
             self.cluster_pass()

@@ -347,3 +347,84 @@ def test_sharded_tenant_reference_hierarchy_batch_cadence(world):
     out = spawn(world, functools.partial(_sharded, cfg=dict(CPU, hier=True, tight=True)))
     check_equivalent(out, world, LIMIT)
     _check_supers(out)
+
+
+def _commit_snaps(comm, cfg):
+    """Per-commit graph states of the row-sharded tenant (every rank's part)
+    and, on rank 0, of the single process, both with commit="conversation"."""
+    import tempfile
+
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
+    snaps = []
+    orig = MemorySystem._save_to_persistence
+
+    def rec(self):
+        out = orig(self)
+        snaps.append(_graph_state(self.graph))
+        return out
+    MemorySystem._save_to_persistence = rec
+    X, sal0, keys0, steps = _data(cfg)
+    sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
+                             embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tempfile.mkdtemp(), device="cpu",
+                             enable_hierarchy=True, super_node_threshold=cfg["sthr"])
+    lo, hi = _split(cfg["rows"], comm.world, comm.rank)
+    sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi], keys0[lo:hi],
+                    salience=torch.tensor(sal0[lo:hi]), now=_now(-1))
+    for s, (convs, V) in enumerate(steps):
+        c0, c1 = _split(len(convs), comm.world, comm.rank)
+        f0 = sum(len(c) for c in convs[:c0])
+        f1 = f0 + sum(len(c) for c in convs[c0:c1])
+        snaps.append("batch")
+        sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1], now=_now(s), commit="conversation")
+    sm.close()
+    parts = comm.all_gather_object(snaps)
+    if comm.rank != 0:
+        return None
+    single = []
+    ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=cfg["dim"]), enable_async=False,
+                      db_dir=tempfile.mkdtemp(), user_id="solo", device="cpu", max_buffer_size=cfg["limit"],
+                      enable_hierarchy=True, super_node_threshold=cfg["sthr"], load_from_disk=False,
+                      enable_caching=False)
+    g = ms.graph
+    g.add_nodes([f"node_{i + 1}" for i in range(cfg["rows"])], [f"memory {i + 1}" for i in range(cfg["rows"])], X,
+                shard=[g.shard_id(k) for k in keys0], sal=torch.tensor(sal0), now=_now(-1), stored=True)
+    ms.node_counter = cfg["rows"]
+    snaps.clear()
+    import lazzaro_amd.engine.tenant_graph as tgm
+    for s, (convs, V) in enumerate(steps):
+        real = tgm.time.time
+        tgm.time.time = lambda s=s: _now(s)
+        try:
+            snaps.append("batch")
+            ms.consolidate_batch(convs, embeddings=V, now=_now(s), commit="conversation")
+        finally:
+            tgm.time.time = real
+        single = list(snaps)
+    ms.close()
+    MemorySystem._save_to_persistence = orig
+    return parts, single
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tenant_commit_per_conversation(world):
+    """commit="conversation" on the row-sharded tenant: every rank commits
+    after each conversation of the batch, and the union of the ranks' k-th
+    commits is the single process's k-th commit (commit="conversation",
+    reference hierarchy) -- a crash loses at most the conversation in flight."""
+    cfg = dict(HIER, sthr=62, steps=2)
+    parts, single = spawn(world, functools.partial(_commit_snaps, cfg=cfg))[0]
+    n_commits = [len(p) for p in parts]
+    assert len(set(n_commits)) == 1 and n_commits[0] == len(single)
+    assert sum(1 for x in single if x != "batch") >= 2 * CONVS  # one per conversation (+ the batch ends)
+    for k, want in enumerate(single):
+        if want == "batch":
+            assert all(p[k] == "batch" for p in parts)
+            continue
+        nodes, edges = {}, {}
+        for p in parts:
+            nodes.update(p[k][0])
+            edges.update(p[k][1])
+        assert nodes == want[0], k
+        assert set(edges) == set(want[1]), k
