@@ -369,16 +369,19 @@ __global__ __launch_bounds__(256) void cand_gather_kernel(const int4* __restrict
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
     const int4 v = buf[(long)b * bcap + e];
     if ((unsigned)v.x >= (unsigned)nq) continue;  // (a +inf score of a padding query column)
+    // positions come from the count's low 30 bits: another block may have set
+    // the overflow flag (bit 30) already, and the entries [0, min(count, cap))
+    // must all be written -- cand_select / cand_rescore read exactly those
     if (v.w & 1) {
-      const int pos = atomicAdd(cnt + v.x, 1);
-      if ((unsigned)pos < (unsigned)cap) {
+      const int pos = atomicAdd(cnt + v.x, 1) & 0x3fffffff;
+      if (pos < cap) {
         cs[(long)v.x * cap + pos] = __int_as_float(v.z);
         ci[(long)v.x * cap + pos] = v.y;
       }
     }
     if (v.w & 2) {
-      const int pos = atomicAdd(cnt2 + v.x, 1);
-      if ((unsigned)pos < (unsigned)cap) {
+      const int pos = atomicAdd(cnt2 + v.x, 1) & 0x3fffffff;
+      if (pos < cap) {
         cs2[(long)v.x * cap + pos] = __int_as_float(v.z);
         ci2[(long)v.x * cap + pos] = v.y;
       }
@@ -440,7 +443,9 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
   if (q >= nq) return;
   const int c = cnt[q];
   if (lane == 0) ovf[q] = (c > cap || (need && c < need[q])) ? 1 : 0;
-  const int n = min(c, cap);
+  // bit 30: a block dropped records (cand_gather_kernel) -- only the first
+  // (c & 0x3fffffff) entries were written; ovf is set either way
+  const int n = min(c & 0x3fffffff, cap);
   TopK<K> top;
   top.init();
   const float* s = cs + (long)q * cap;

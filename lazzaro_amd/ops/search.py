@@ -668,8 +668,10 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
         _lib.check(L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, kslot, 0,
                                      s8.data_ptr(), i8.data_ptr(), ovf.data_ptr(), None, st), "lzk_cand_select")
         rows = i8[:, :k]
-        valid = rows >= 0
-        rr = rows.clamp_min(0)
+        # (an overflowed list's entries are real rows, but the gather must
+        # never see an index outside the scanned rows)
+        valid = (rows >= 0) & (rows < X16.shape[0])
+        rr = torch.where(valid, rows, torch.zeros_like(rows))
         if isinstance(X16, LeanRows):
             dot = torch.einsum("qd,qkd->qk", X16.Q32.float(), X16.X32[rr].float())
         else:

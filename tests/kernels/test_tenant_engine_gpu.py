@@ -188,6 +188,73 @@ def _clustered(n, d, n_clusters, seed, noise=0.35):
     return X / X.norm(dim=1, keepdim=True), lab
 
 
+def test_consolidate_batch_int8_dual_decisions_at_scale_gpu(tmp_path, monkeypatch):
+    """A 1.2M-row tenant -- past LOWP_MIN_ROWS, so consolidation's candidate
+    lists come from the int8 dual scan (its default) -- consolidates a batch
+    of 32 conversations (192 facts: duplicates of stored rows, related and new
+    facts) at the reference cadence; the same batch on the same tenant with
+    the int8 scan switched off (bf16 dual scan, itself pinned to the exact
+    float64 scan) makes the same decisions: the same counts, nodes,
+    saliences, access counts, edges and victims."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    from lazzaro_amd.ops import search as S
+    N, D, B, F = 1_200_000, 384, 32, 6
+    X, lab = _clustered(N, D, 256, 21, noise=1.6)
+    gen = torch.Generator().manual_seed(5)
+    facts, vecs = [], []
+    for c in range(B):
+        conv = []
+        for f in range(F):
+            kind = (c * F + f) % 3
+            if kind == 0:  # near-duplicate of a stored row
+                v = X[int(torch.randint(0, N, (1,), generator=gen))] + 0.01 * torch.randn(D, generator=gen) / D ** 0.5
+            elif kind == 1:  # related: a cluster centre's neighbourhood
+                v = X[int(torch.randint(0, N, (1,), generator=gen))] + 0.9 * torch.randn(D, generator=gen) / D ** 0.5
+            else:
+                v = torch.randn(D, generator=gen)
+            vecs.append(v / v.norm())
+            conv.append({"content": f"fact {c}.{f}", "salience": 0.5 + 0.01 * f, "topic": f"topic{(c + f) % 8}"})
+        facts.append(conv)
+    V = torch.stack(vecs)
+    calls = {"i8": 0}
+    real = S.flat_topk_dual_i8
+
+    def counted(*a, **k):
+        calls["i8"] += 1
+        return real(*a, **k)
+    monkeypatch.setattr(S, "flat_topk_dual_i8", counted)
+    out = {}
+    for mode in ("int8", "bf16"):
+        monkeypatch.setattr(TG, "DUAL_LOWP", mode == "int8")
+        monkeypatch.setattr(time, "time", _Clock())
+        ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
+                          db_dir=str(tmp_path / mode), device=DEV, load_from_disk=False, max_buffer_size=N + 40,
+                          super_node_threshold=10 ** 9)
+        g = ms.graph
+        shards = [g.shard_id(f"topic{c}") for c in range(8)]
+        g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"m {i}" for i in range(N)], X.to(DEV),
+                    shard=np.asarray([shards[int(c) % 8] for c in lab], dtype=np.int32),
+                    sal=torch.rand(N, generator=torch.Generator().manual_seed(1)), stored=True)
+        ms.node_counter = N
+        before = calls["i8"]
+        st = ms.consolidate_batch(facts, embeddings=V.to(DEV), now=1.8e9)
+        used = calls["i8"] - before
+        n = g.n
+        live = (g.kind[:n] == NODE).cpu().numpy()
+        e = {k: v.cpu() for k, v in g.e.items()}
+        order = np.lexsort((e["dst"].numpy(), e["src"].numpy()))
+        out[mode] = (st, used, np.nonzero(live)[0], g.sal[:n].cpu().numpy()[live], g.acc[:n].cpu().numpy()[live],
+                     {k: v.numpy()[order] for k, v in e.items() if k in ("src", "dst", "w", "meta")})
+        ms.close()
+    a, b = out["int8"], out["bf16"]
+    assert a[1] >= 1 and b[1] == 0  # the int8 dual scan made the first run's lists, not the second's
+    assert a[0] == b[0]
+    assert a[0]["dup"] > 0 and a[0]["linked"] > 0 and a[0]["evicted"] > 0
+    assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+    for k in a[5]:
+        assert np.array_equal(a[5][k], b[5][k]), k
+
+
 def test_large_tenant_kernel_path_matches_exact_cpu(tmp_path, monkeypatch):
     """60k-node tenant: dedupe + links from the fused dual MFMA scan on the
     GPU vs the exact float64 scan on the CPU; then decay/prune, eviction,
@@ -484,6 +551,43 @@ def test_flat_topk_dual_i8_matches_bf16_dual_gpu(floor):
         assert torch.equal(r0, r1)
         fin = torch.isfinite(s0)
         assert torch.equal(fin, torch.isfinite(s1))
+        assert torch.allclose(s0[fin], s1[fin], atol=1e-4, rtol=0)
+
+
+def test_flat_topk_dual_i8_overflowing_lists_gpu():
+    """Tight topics (every row of a topic at cos > 0.9 to its queries): the
+    int8 dual scan's block records and per-query lists overflow, cand_select
+    reads only the entries that were written, the re-score cut gathers no row
+    outside the table, and the fallback returns the bf16 dual scan's lists
+    for every entry above the floor (the row-sharded bench's clustered load)."""
+    from lazzaro_amd.ops.search import flat_topk_dual, flat_topk_dual_i8, quantize_i8_rows
+    gen = torch.Generator(device=DEV).manual_seed(23)
+    N, D, nq, T_ = 2_000_000, 768, 256, 8
+    C = torch.randn(T_, D, device=DEV, generator=gen)
+    C = C / C.norm(dim=1, keepdim=True)
+    t = torch.randint(0, T_, (N,), device=DEV, generator=gen)
+    X = C[t] + 0.25 / D ** 0.5 * torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    Q = C[torch.randint(0, T_, (nq,), device=DEV, generator=gen)] + 0.25 / D ** 0.5 * torch.randn(
+        nq, D, device=DEV, generator=gen)
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
+    lab = torch.randint(0, 6, (N,), device=DEV, generator=gen, dtype=torch.int32)
+    ql = torch.randint(0, 6, (nq,), device=DEV, generator=gen, dtype=torch.int32)
+    floor = 0.5 - 2.0 ** -7
+    (sa, ra), (sb, rb) = flat_topk_dual(X16, Q16, 16, row_label=lab, q_label=ql, floor=floor)
+    X8, rs = quantize_i8_rows(X16)
+    Q8, qs = quantize_i8_rows(Q16)
+    margin = torch.full((nq,), 0.02, device=DEV)
+    st = []
+    (ta, ia), (tb, ib) = flat_topk_dual_i8(X8, rs, Q8, qs, X16, Q16, 16, row_label=lab, q_label=ql, margin=margin,
+                                           margin_rig=margin, floor=floor, stats=st)
+    torch.cuda.synchronize()
+    (oa, _), (ob, _), _cap = st
+    assert bool((oa != 0).all()) and bool((ob != 0).all())  # every list overflowed: the fallback ran
+    for s0, r0, s1, r1 in ((sa, ra, ta, ia), (sb, rb, tb, ib)):
+        assert torch.equal(r0, r1)
+        fin = torch.isfinite(s0)
         assert torch.allclose(s0[fin], s1[fin], atol=1e-4, rtol=0)
 
 
