@@ -235,7 +235,12 @@ def main():
     else:
         if distributed:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # no device_id: RCCL's communicator (its internal streams and proxy
+            # thread) is created at the first GPU collective -- the serving
+            # section's, after the headline loop. Created before it, it cost
+            # the 1-rank headline ~6 % (the encoder and search streams then
+            # overlap less; profiles/r5/README.md, ab_r4)
+            dist.init_process_group("nccl")
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
 
@@ -298,8 +303,11 @@ def main():
     for _ in ms.search_memories_stream(batches(a.warmup), limit=a.k):
         pass
     sync()
+    # the headline's own synchronisation runs on the host (gloo) group: each
+    # rank serves its own tenant, and no RCCL communicator exists yet
+    hg = comm._host_group if distributed else None
     if distributed:
-        dist.barrier()
+        dist.barrier(group=hg)
     sync()
     hprof = None
 
@@ -360,13 +368,13 @@ def main():
         print("cgroup after:", _cg(), file=sys.stderr)
         pstats.Stats(hprof, stream=sys.stderr).sort_stats("tottime").print_stats(35)
     if distributed:
-        dist.barrier()
+        dist.barrier(group=hg)
     sync()
     el = time.perf_counter() - t0
     assert n_res == a.steps * a.batch
     if distributed:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=hg)
         el = float(t.item())
     qps = world * a.batch * a.steps / el
 
@@ -377,16 +385,19 @@ def main():
     svc.embedder = emb
     comm_dev = comm.device
 
+    def gbar():  # a barrier on the RCCL group (bound to this rank's GPU)
+        dist.barrier(device_ids=[dev.index]) if dev.type == "cuda" else dist.barrier()
+
     def timed(n, fn):
         if distributed:
-            dist.barrier()
+            gbar()
         sync()
         t1 = time.perf_counter()
         for i in range(n):
             fn(i)
         sync()
         if distributed:
-            dist.barrier()
+            gbar()
         sync()
         e = time.perf_counter() - t1
         if distributed:
@@ -597,7 +608,7 @@ def main():
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
     if distributed:
-        dist.barrier()
+        dist.barrier(group=hg)
         dist.destroy_process_group()
 
 

@@ -1,6 +1,7 @@
 #!/bin/bash
 # headline-only bench runs + one full default bench (round-5 working script)
 export TMPDIR=/tmp
+export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
 OUT=${OUT:-gpurun_out/head}
 mkdir -p $OUT
 Q="--consolidate-steps 0 --sharded-steps 0 --routed-steps 0 --global-batch 0"

@@ -1,6 +1,7 @@
 #!/bin/bash
 # round-5 working script: overflow-path probe, its tests, the row-sharded bench section
 export TMPDIR=/tmp
+export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
 OUT=${OUT:-gpurun_out/r5k}
 mkdir -p $OUT
 timeout -k 10 180 python -u bench/probe_dual_ovf.py > $OUT/probe.log 2>&1 || exit 1
