@@ -142,6 +142,36 @@ __global__ __launch_bounds__(NTB) void uf_union_kernel(const int* __restrict__ s
   }
 }
 
+// The union pass over one side of an edge selection (incremental components
+// across a consolidation batch, TenantGraph.cc_begin): an edge is VOLATILE --
+// it may be deleted, or was added, during the batch -- when an endpoint is a
+// row >= n0 (inserted since the mark), an endpoint is marked in vmark (a
+// batch victim; rows < n0), or its weight is below wthr (the prune may take
+// it). sel = 0 unions the stable edges (the batch's base labels, once),
+// sel = 1 the volatile ones (on top of a copy of the base labels, at every
+// consolidation point).
+template <bool PLAIN>
+__global__ __launch_bounds__(NTB) void uf_union_sel_kernel(const int* __restrict__ src, const int* __restrict__ dst,
+                                                           long ne, const float* __restrict__ w, float wthr,
+                                                           const unsigned char* __restrict__ vmark, int n0, int sel,
+                                                           int* __restrict__ parent) {
+  for (long e = (long)blockIdx.x * NTB + threadIdx.x; e < ne; e += (long)gridDim.x * NTB) {
+    int a = src[e], b = dst[e];
+    LZK_DCHECK(a >= 0 && b >= 0);
+    const bool vol = a >= n0 || b >= n0 || vmark[a] || vmark[b] || (w && w[e] < wthr);
+    if (vol != (sel != 0)) continue;
+    while (true) {
+      a = uf_find<PLAIN>(parent, a);
+      b = uf_find<PLAIN>(parent, b);
+      if (a == b) break;
+      if (a < b) { const int t = a; a = b; b = t; }
+      const int old = atomicCAS(parent + a, a, b);
+      if (old == a) break;
+      a = old;
+    }
+  }
+}
+
 __global__ __launch_bounds__(NTB) void cc_compress_kernel(int* __restrict__ parent, long n) {
   const long i = (long)blockIdx.x * NTB + threadIdx.x;
   if (i >= n) return;
@@ -315,6 +345,15 @@ LZK_EXPORT int lzk_uf_union(const int* src, const int* dst, long ne, const float
 LZK_EXPORT int lzk_uf_union_plain(const int* src, const int* dst, long ne, const float* w, float min_w, int* parent,
                                   void* stream) {
   return uf_union_launch(src, dst, ne, w, min_w, parent, true, stream);
+}
+
+LZK_EXPORT int lzk_uf_union_sel(const int* src, const int* dst, long ne, const float* w, float wthr,
+                                const unsigned char* vmark, int n0, int sel, int* parent, void* stream) {
+  if (ne == 0) return 0;
+  const long nb0 = (ne + NTB - 1) / NTB, nb = nb0 < 256L * 32 ? nb0 : 256L * 32;
+  hipLaunchKernelGGL(uf_union_sel_kernel<true>, dim3((unsigned)nb), dim3(NTB), 0, (hipStream_t)stream, src, dst, ne,
+                     w, wthr, vmark, n0, sel, parent);
+  return (int)hipGetLastError();
 }
 
 LZK_EXPORT int lzk_cc_compress(int* parent, long n, void* stream) {

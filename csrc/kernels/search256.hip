@@ -402,6 +402,7 @@ constexpr int kCandOpt = 24;
 // (profiles/ab_dual_r1.json) 0: 16.27 ms, body2: 15.65, +prefilter 15.90.
 constexpr int kDualOpt = 8;
 int g_dual_opt = -1;  // A/B override of kCandOpt for the dual kernel (lzk_set_dual_opt)
+int g_i8_opt = -1;  // A/B override of kCandOpt for the int8 scan (lzk_set_i8_opt; probes only)
 int g_g256_opt = 0;  // A/B override of kCandOpt for the plain (no bias / label) variant; 100 = OPT 0
 int g_n_cu = 0;
 
@@ -817,6 +818,7 @@ LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 LZK_EXPORT void lzk_set_cu_budget(int n) { g_n_cu = n > 0 ? n : 0; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
+LZK_EXPORT void lzk_set_i8_opt(int o) { g_i8_opt = o; }
 LZK_EXPORT int lzk_set_stamp_buffer(void* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p));
 }
@@ -1108,8 +1110,19 @@ LZK_EXPORT int lzk_flat_cand_i8(const void* X8, long ldx_bytes, int nrows, const
   } while (0)
   // (a cross-tile prefetch variant, OPT bit 5, measured 11.0 vs 10.0 ms per
   // store search on 10M x 768 x 1024 -- bench/ab_i8_search.py -- and spills)
-  if (bias) LZK_GIO(true, kCandOpt);
-  else LZK_GIO(false, kCandOpt);
+  // g_i8_opt (probe A/B only, lzk_set_i8_opt): 28 = the GEMM without the
+  // candidate epilogue (OPT bit 2), 8 = no column prefilter
+#define LZK_GIS(B)                              \
+  do {                                          \
+    switch (g_i8_opt) {                         \
+      case 28: LZK_GIO(B, 28); break;           \
+      case 8: LZK_GIO(B, 8); break;             \
+      default: LZK_GIO(B, kCandOpt); break;     \
+    }                                           \
+  } while (0)
+  if (bias) LZK_GIS(true);
+  else LZK_GIS(false);
+#undef LZK_GIS
 #undef LZK_GIO
   return (int)hipGetLastError();
 }

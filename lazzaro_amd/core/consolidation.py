@@ -844,6 +844,30 @@ class ConsolidationMixin:
         # batch could re-use a row id (its row's content would change)
         defer = not self._commit_each and self._supers_fresh(pl, now)
         pending = []
+        # the components of every run_consolidation point of the batch from
+        # one base labelling (TenantGraph.cc_begin): the plan names every
+        # victim of the batch up front
+        cc = False
+        if any(seg["consolidate"] for seg in pl["segments"]):
+            vic = [np.asarray(seg["victims"], np.int64).reshape(-1) for seg in pl["segments"]]
+            with tracer.stage("cc_begin", self._device):
+                cc = g.cc_begin(np.concatenate(vic) if vic else np.zeros(0, np.int64), self.prune_threshold,
+                                1.0 - DECAY_RATE, B)
+        try:
+            self._apply_planned_segments(pl, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
+                                         defer, pending)
+        finally:
+            if cc:
+                g.cc_end()
+        if pending:
+            with tracer.stage("rc_deferred", "cpu"):
+                for cap in pending:
+                    self._rc_host(cap)
+        if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
+            self._maybe_cluster(self.conversation_count - 1)
+
+    def _apply_planned_segments(self, pl, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
+                                defer, pending) -> None:
         for seg in pl["segments"]:
             # node ids as the segment's facts are inserted (keys grow segment by
             # segment): a per-segment commit persists the sequential counter
@@ -866,12 +890,6 @@ class ConsolidationMixin:
             if self._commit_each:
                 with tracer.stage("commit", "cpu"):
                     self._save_to_persistence()
-        if pending:
-            with tracer.stage("rc_deferred", "cpu"):
-                for cap in pending:
-                    self._rc_host(cap)
-        if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
-            self._maybe_cluster(self.conversation_count - 1)
 
     def _supers_fresh(self, pl: Dict, now: float) -> bool:
         """No super-node of the plan re-uses an id (the id is

@@ -27,6 +27,7 @@ _lib.register("lzk_uf_union_plain", I, [P, P, L, P, F, P, P])
 # edge count).
 UF_PLAIN = True
 UF_STAGES = 0
+_lib.register("lzk_uf_union_sel", I, [P, P, L, P, F, P, I, I, P, P])
 _lib.register("lzk_pairs_above", I, [P, L, I, I, F, P, I, P, P])
 _lib.register("lzk_seg_sum", I, [P, L, L, I, P, P, P, P])
 _lib.register("lzk_centroids", I, [P, P, I, I, I, P, P, I, P])
@@ -84,6 +85,37 @@ def connected_components(src: torch.Tensor, dst: torch.Tensor, n: int, w: Option
         _lib.check(L_.lzk_cc_compress(parent.data_ptr(), n, _st(src)), "cc_compress")
         if int(changed.item()) == 0:
             break
+    return parent
+
+
+def components_sel(src: torch.Tensor, dst: torch.Tensor, n: int, w: Optional[torch.Tensor], wthr: float,
+                   vmark: torch.Tensor, n0: int, sel: int, parent: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Union-find labels over one side of an edge selection (graph.hip
+    uf_union_sel_kernel): an edge is volatile when an endpoint is a row >= n0
+    or marked in ``vmark`` (uint8 [n0]), or its weight is below ``wthr``.
+    ``sel`` 0: the stable edges, from singletons (``parent`` None) -- a
+    batch's base labels; 1: the volatile edges on top of ``parent`` (int32
+    [n], a compressed labelling of the base, extended by singletons).
+    Returns the compressed labels (smallest row per component), GPU only."""
+    assert src.is_cuda and vmark.dtype == torch.uint8 and vmark.numel() >= n0
+    if parent is None:
+        parent = torch.arange(n, dtype=torch.int32, device=src.device)
+    src, dst = src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous()
+    if w is not None:
+        w = w.to(torch.float32).contiguous()
+    ne = int(src.numel())
+    L_ = _lib.lib()
+    st = _st(src)
+    # the stable side holds nearly every edge: staged like connected_components;
+    # the volatile side is a few thousand edges found by one filtering pass
+    stages = 1 if sel else (UF_STAGES or max(1, min(4, ne // (2 << 20))))
+    step = -(-ne // stages) if ne else 1
+    for c0 in range(0, max(ne, 1), step):
+        c1 = min(ne, c0 + step)
+        _lib.check(L_.lzk_uf_union_sel(src[c0:].data_ptr(), dst[c0:].data_ptr(), c1 - c0,
+                                       w[c0:].data_ptr() if w is not None else None, float(wthr), vmark.data_ptr(),
+                                       int(n0), int(sel), parent.data_ptr(), st), "uf_union_sel")
+        _lib.check(L_.lzk_cc_compress(parent.data_ptr(), n, st), "cc_compress")
     return parent
 
 

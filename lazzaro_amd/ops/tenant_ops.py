@@ -403,17 +403,20 @@ DIGEST_WINDOW = 1 << 16  # rows of the first selection pass (component_digest)
 
 def component_digest(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, kind: torch.Tensor, sup: torch.Tensor,
                      shard: torch.Tensor, n: int, min_size: int, min_avg_w: float,
-                     take: int) -> Tuple[torch.Tensor, torch.Tensor]:
+                     take: int, lab: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Device component digest (``csrc/kernels/digest.hip``): (order key,
     row) of the first ``take`` live shard-node rows of every component with
     >= ``min_size`` members and mean edge weight > ``min_avg_w``, sorted by
     (key, row). Union-find labels, then keyed reductions and selection rounds
     -- no sort over the graph (see the kernel file). One host synchronisation
     sizes the output. GPU tensors only (TenantGraph.component_digest has the
-    sort-based CPU formulation); ``min_size`` >= 2, ``take`` >= 1."""
+    sort-based CPU formulation); ``min_size`` >= 2, ``take`` >= 1. ``lab``:
+    the components' labels when the caller has them (int32 [n], smallest row
+    per component: TenantGraph's incremental labels within a batch)."""
     assert src.is_cuda and min_size >= 2 and take >= 1
     dev = src.device
-    lab = components(src, dst, n)
+    if lab is None:
+        lab = components(src, dst, n)
     ne = int(src.numel())
     touched = torch.zeros(n, dtype=torch.uint8, device=dev)
     gsum = torch.zeros(n, dtype=torch.float64, device=dev)

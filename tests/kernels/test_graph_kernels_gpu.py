@@ -370,3 +370,58 @@ def test_farthest_first_kernel_matches_torch_gpu():
     ms = (time.perf_counter() - t0) * 1e3
     print(f"farthest_first 4096 x 65536 x 768: {ms:.1f} ms")
     assert c.shape == (4096, 768) and ms < 400
+
+
+@pytest.mark.parametrize("thr", [None, 0.45])
+def test_incremental_components_match_full_recompute_gpu(thr):
+    """TenantGraph.cc_begin / _cc_labels: a random tenant graph (200k rows,
+    400k edges -- the full GPU digest path) goes through a batch of segments
+    that decay (with or without a prune threshold the decays cross), append
+    new rows with edges into the graph, evict victims (their shard's edges
+    go); at every point the incremental labels equal a full union-find over
+    the current edges, label for label, and so do the digests."""
+    import numpy as np
+
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    from lazzaro_amd.ops import tenant_ops as T
+    n, ne, D = 200_000, 400_000, 64
+    gen = torch.Generator().manual_seed(9)
+    g = TenantGraph(device=DEV, dim=D)
+    shards = [g.shard_id(f"s{i}") for i in range(6)]
+    X = torch.randn(n, D, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    g.add_nodes([f"n{i}" for i in range(n)], [f"c{i}" for i in range(n)], X.to(DEV),
+                shard=np.asarray([shards[i % 6] for i in range(n)], np.int32), stored=True)
+    src = torch.randint(0, n, (ne,), generator=gen, dtype=torch.int32)
+    dst = torch.randint(0, n, (ne,), generator=gen, dtype=torch.int32)
+    w = 0.44 + 0.2 * torch.rand(ne, generator=gen)  # some edges cross 0.45 within the batch's decays
+    g.append_edges(src.to(DEV), dst.to(DEV), w.to(DEV), g.shard[src.to(DEV).long()], g.etype("relates_to"))
+    assert not g._digest_local(3, 1)
+    B, keep = 12, 0.99
+    victims = torch.randperm(n, generator=gen)[:3000].numpy()
+    assert g.cc_begin(victims, thr, keep, B)
+    rng = np.random.default_rng(4)
+    for point in range(6):
+        tok = g.segment_begin(1.0 - keep, thr, 2)
+        m = 40  # new rows, each linked to 3 existing rows and to each other
+        n_before = g.n
+        Y = torch.randn(m, D, generator=gen)
+        g.add_nodes([f"p{point}_{j}" for j in range(m)], ["x"] * m, (Y / Y.norm(dim=1, keepdim=True)).to(DEV),
+                    shard=np.asarray([shards[j % 6] for j in range(m)], np.int32), stored=True)
+        s_new = torch.arange(n_before, n_before + m, dtype=torch.int32).repeat(3)
+        d_new = torch.as_tensor(rng.integers(0, n_before, 3 * m), dtype=torch.int32)
+        s_new = torch.cat([s_new, torch.arange(n_before, n_before + m - 1, dtype=torch.int32)])
+        d_new = torch.cat([d_new, torch.arange(n_before + 1, n_before + m, dtype=torch.int32)])
+        g.append_edges(s_new.to(DEV), d_new.to(DEV), torch.full((s_new.numel(),), 0.7, device=DEV),
+                       g.shard[s_new.to(DEV).long()], g.etype("relates_to"))
+        vic = victims[point * 500:(point + 1) * 500].tolist()
+        g.segment_end(tok, vic, unstore=True)
+        inc = g._cc_labels()
+        full = T.components(g.e["src"], g.e["dst"], g.n)
+        assert torch.equal(inc, full.to(torch.int32)), point
+        d_inc = g.component_digest(3, 0.3, 10)
+        saved, g._cc = g._cc, None
+        d_full = g.component_digest(3, 0.3, 10)
+        g._cc = saved
+        assert len(d_inc) == len(d_full) and all(np.array_equal(a, b) for a, b in zip(d_inc, d_full)), point
+    g.cc_end()

@@ -755,3 +755,68 @@ def test_lean_hbm_tenant_matches_full_gpu(monkeypatch):
     hf, hl = full.cluster_pass(32, 4, 2), lean.cluster_pass(32, 4, 2)
     assert torch.equal(full.hier["fine"][:N], lean.hier["fine"][:N])
     assert lean.emb16 is None  # the pass's bf16 copy is gone
+
+
+@pytest.mark.parametrize("prune_threshold", [0.0, 0.5])
+def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, prune_threshold):
+    """consolidate_batch on a tenant with many edges (the full GPU digest
+    path at every run_consolidation point): the batch's incremental
+    components (TenantGraph.cc_begin) give the same digest at every point,
+    the same profile and the same final graph as a union-find over every
+    edge at every point."""
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    N, D, NE, B, F = 80_000, 64, 240_000, 30, 4
+    X, lab = _clustered(N, D, 64, 3, noise=1.2)
+    gen = torch.Generator().manual_seed(12)
+    src = torch.randint(0, N, (NE,), generator=gen, dtype=torch.int32)
+    dst = torch.randint(0, N, (NE,), generator=gen, dtype=torch.int32)
+    w = 0.5 + 0.5 * torch.rand(NE, generator=gen)
+    facts, vecs = [], []
+    for c in range(B):
+        conv = []
+        for f in range(F):
+            v = X[int(torch.randint(0, N, (1,), generator=gen))] + 0.6 * torch.randn(D, generator=gen) / D ** 0.5
+            vecs.append(v / v.norm())
+            conv.append({"content": f"fact {c}.{f} about topic{(c + f) % 5}", "salience": 0.6, "topic": f"topic{f}"})
+        facts.append(conv)
+    V = torch.stack(vecs)
+    out = {}
+    real = TenantGraph.component_digest
+    real_begin = TenantGraph.cc_begin
+    for inc in (True, False):
+        digests = []
+
+        def rec(self, *a, **k):
+            d = real(self, *a, **k)
+            digests.append([x.tolist() for x in d])
+            return d
+        monkeypatch.setattr(TenantGraph, "component_digest", rec)
+        monkeypatch.setattr(TenantGraph, "CC_INCREMENTAL", inc)
+        monkeypatch.setattr(time, "time", _Clock())
+        ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
+                          db_dir=str(tmp_path / f"inc{int(inc)}"), device=DEV, load_from_disk=False,
+                          max_buffer_size=N + 20, prune_threshold=prune_threshold, super_node_threshold=10 ** 9)
+        g = ms.graph
+        shards = [g.shard_id(f"topic{c}") for c in range(5)]
+        g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"m {i}" for i in range(N)], X.to(DEV),
+                    shard=np.asarray([shards[int(c) % 5] for c in lab], dtype=np.int32),
+                    sal=torch.rand(N, generator=torch.Generator().manual_seed(1)), stored=True)
+        g.append_edges(src.to(DEV), dst.to(DEV), w.to(DEV), g.shard[src.to(DEV).long()], g.etype("relates_to"))
+        ms.node_counter = N
+        used = []
+        monkeypatch.setattr(TenantGraph, "cc_begin", lambda self, *a, **k: used.append(real_begin(self, *a, **k))
+                            or used[-1])
+        st = ms.consolidate_batch(facts, embeddings=V.to(DEV), now=1.9e9)
+        e = {k: v.cpu() for k, v in g.e.items()}
+        order = np.lexsort((e["dst"].numpy(), e["src"].numpy()))
+        out[inc] = (st, digests, dict(ms.profile.data), used, g.sal[: g.n].cpu().numpy(),
+                    {k: v.numpy()[order] for k, v in e.items() if k in ("src", "dst", "w")})
+        ms.close()
+    a, b = out[True], out[False]
+    assert a[3] == [True] and b[3] == [False]  # the incremental path ran (thr 0.5: the decays make many edges volatile)
+    assert a[0] == b[0] and a[0]["consolidations"] == B // 3 and a[0]["evicted"] > 0
+    assert a[1] == b[1] and len(a[1]) == B // 3
+    assert a[2] == b[2]
+    assert np.array_equal(a[4], b[4])
+    for k in a[5]:
+        assert np.array_equal(a[5][k], b[5][k]), k
