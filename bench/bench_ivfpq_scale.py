@@ -73,7 +73,8 @@ def main():
     ap.add_argument("--nlist", type=int, default=16384)
     ap.add_argument("--m", type=int, default=64)
     ap.add_argument("--keep", default="int8", choices=["int8", "fp8", "bf16"])
-    ap.add_argument("--train", type=int, default=524_288)
+    ap.add_argument("--train", type=int, default=4_194_304,
+                    help="coarse k-means training rows (~256 per list: 524k left the lists too coarse, coarse recall 0.66)")
     ap.add_argument("--nq", type=int, default=1024)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--nprobes", default="16,32,64,128")
@@ -153,7 +154,16 @@ def main():
         log(f"{a.embed_model} {a.embed_precision} embed of {a.nq} queries: {t_embed * 1e3:.2f} ms")
         del enc
     res = []
+    # the coarse quantiser's share of the recall: how many true top-10 rows sit
+    # in one of the query's probed lists (row -> list through the sorted layout)
+    inv = torch.empty_like(idx._pos[: idx.n])
+    inv[idx._pos[: idx.n]] = torch.arange(idx.n, device=dev)
+    truth_list = idx._list[: idx.n][inv[best_i.clamp_min(0)]]
+    cs_q = torch.nn.functional.normalize(Q.float(), dim=1) @ idx.centroids.T
     for nprobe in map(int, a.nprobes.split(",")):
+        pr = torch.topk(cs_q, nprobe, dim=1).indices
+        hit = (truth_list[:, :, None] == pr[:, None, :].to(truth_list.dtype)).any(-1)
+        log(f"nprobe {nprobe}: coarse recall@10 {float(hit.float().mean()):.4f}")
         for rr in map(int, a.reranks.split(",")):
             idx.search(Q, 10, nprobe=nprobe, rerank=rr)
             torch.cuda.synchronize()
