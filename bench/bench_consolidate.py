@@ -317,6 +317,11 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
         step()
     _sync(dev)
     comm.barrier()
+    prof = None
+    if os.environ.get("LZK_PROF_HOST") == "1":  # host-side profile of the timed steps (stderr)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     agg = {}
     work0 = sm.scan_work
@@ -326,6 +331,13 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     _sync(dev)
     comm.barrier()
     el = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(40)
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("cumulative").print_stats(60)
+        pstats.Stats(prof, stream=sys.stderr).print_callers(r"method 'cpu'|method 'item'|method 'tolist'|"
+                                                            r"torch.nonzero|method 'numpy'")
     t = torch.tensor([el], dtype=torch.float64, device=dev if comm.enabled and dev.type == "cuda" else "cpu")
     comm.all_reduce(t, "max")
     el = float(t.item())

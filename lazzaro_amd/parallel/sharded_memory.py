@@ -91,6 +91,36 @@ BIG = 1 << 62
 NUM_BITS = 40  # global node numbers < 2^40; (shard + 1) << 40 | number orders nodes as the reference does
 
 
+def _digest_compact_host(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor, valid: torch.Tensor,
+                         live: torch.Tensor, shard: torch.Tensor, nl: int, min_size: int, min_avg_w: float,
+                         take: int) -> torch.Tensor:
+    """Host form of the compact digest (:meth:`ShardedMemorySystem.
+    _digest_replicated`; the GPU runs digest.hip): ids 0 .. nl-1, ``valid``
+    ids are members, ``live`` ones (shard ``shard``) are candidates. int64
+    [2, m] = (order key, id) of the first ``take`` live members of every
+    qualifying component, sorted by (key, id)."""
+    lab = T.components(src, dst, nl).long()
+    size = torch.zeros(nl, dtype=torch.long).index_add_(0, lab[valid], torch.ones(int(valid.sum()), dtype=torch.long))
+    wsum, wcnt = _seg_sum_count(lab[src], w.double(), nl)
+    ids = torch.arange(nl)
+    key = torch.where(live, (shard.clamp_min(0) + 1) * nl + ids, torch.full_like(ids, BIG))
+    first = _seg_min(lab, key, nl, BIG)
+    ok = (size >= min_size) & (wcnt > 0) & (wsum / wcnt.clamp_min(1).double() > min_avg_w) & (first < BIG)
+    ci = torch.nonzero(live & ok[lab]).flatten()
+    if ci.numel() == 0:
+        return torch.zeros((2, 0), dtype=torch.long)
+    ci = ci[torch.argsort(lab[ci], stable=True)]  # grouped by component, id order inside
+    cl = lab[ci]
+    newg = torch.ones_like(cl, dtype=torch.bool)
+    newg[1:] = cl[1:] != cl[:-1]
+    gstart = torch.nonzero(newg).flatten()[torch.cumsum(newg.long(), 0) - 1]
+    sel = ci[(torch.arange(ci.numel()) - gstart) < take]
+    k = first[lab[sel]]
+    o = torch.argsort(sel, stable=True)
+    o = o[torch.argsort(k[o], stable=True)]
+    return torch.stack([k[o], sel[o]])
+
+
 def shard_user_id(user: str, rank: int, world: int) -> str:
     return f"{user}@{rank}/{world}"
 
@@ -1706,6 +1736,91 @@ class ShardedMemorySystem:
         return {"moved": total_moved}
 
     # ------------------------------------------------------------------ deep consolidation
+    # Up to this many edges over all ranks the digest replicates them (one
+    # all-gather of 24 B per edge) and every rank runs the single-graph digest
+    # kernels on the endpoints; above it the boundary-label exchange keeps the
+    # work and the bytes distributed (the 20M-edge persistent graph per rank).
+    DIGEST_REPLICATE_MAX = 1 << 22
+
+    def _digest_replicated(self, cnt: List[int], min_size: int, min_avg_w: float, take: int) -> List[List[str]]:
+        """:meth:`component_digest` over the replicated edge list, four
+        collectives in all (edge counts, edges, the endpoints' liveness, the
+        selected contents) instead of the boundary-label rounds and five
+        routed exchanges. Every rank renumbers the endpoints' node numbers
+        0 .. U-1 in number order (identical on every rank: same edges, same
+        order), the holders fill in which endpoints are live shard nodes and
+        their shard (one all-reduce), and the digest runs on that compact
+        graph -- on the GPU the one-block ``dg_small`` kernel or the O(edges)
+        renumbered digest (tenant_ops), no host synchronisation before the
+        selected rows. The renumbering is monotone in the node number, so the
+        components, their (shard, number) first-member order and each
+        component's first ``take`` live members are those of the distributed
+        form."""
+        g = self.g
+        dev = self.device
+        ne = cnt[self.rank] if self._coll else cnt[0]
+        if ne:
+            ed = torch.stack([self.num[g.e["src"].long()], self.num[g.e["dst"].long()],
+                              g.e["w"].float().contiguous().view(torch.int32).long()], 1)
+        else:
+            ed = torch.zeros((0, 3), dtype=torch.long, device=dev)
+        if self._coll:
+            mx = max(cnt)
+            pad = torch.zeros((mx, 3), dtype=torch.long, device=dev)
+            pad[:ne] = ed
+            allr = self._gather_rows(pad)
+            ed = torch.cat([allr[r * mx: r * mx + c] for r, c in enumerate(cnt) if c])
+        E = int(ed.shape[0])
+        if E == 0:
+            return []
+        nl = 2 * E
+        ep = ed[:, :2].reshape(-1)
+        srt, perm = torch.sort(ep)
+        newf = torch.ones(nl, dtype=torch.bool, device=dev)
+        newf[1:] = srt[1:] != srt[:-1]
+        uid = torch.cumsum(newf, 0) - 1
+        local = torch.empty(nl, dtype=torch.int64, device=dev)
+        local[perm] = uid
+        numof = torch.full((nl,), -1, dtype=torch.long, device=dev)  # compact id -> node number
+        numof[uid] = srt
+        valid = numof >= 0
+        rows = self._rows_of_nums(numof.clamp_min(0))
+        rc = rows.clamp_min(0)
+        mine = valid & (rows >= 0) & (self.holder[rc] == self.rank) & (g.kind[rc] == NODE) & (g.sup[rc] == 0)
+        attr = torch.where(mine, g.shard[rc].long() + 1, torch.zeros_like(rows))  # one holder per node
+        if self._coll:
+            attr = self.comm.all_reduce(self._to_comm(attr)).to(dev)
+        live = attr > 0
+        lsrc, ldst = local[0::2].contiguous(), local[1::2].contiguous()
+        w = ed[:, 2].to(torch.int32).view(torch.float32)
+        if dev.type == "cuda":
+            kind_c = torch.where(valid, torch.where(live, 1, 2), 0).to(torch.uint8)
+            sup_c = torch.zeros(nl, dtype=torch.uint8, device=dev)
+            shard_c = (attr - 1).clamp_min(0).to(torch.int32)
+            if E <= T.dg_small_max_edges():
+                res = T.component_digest_small(lsrc, ldst, w, kind_c, sup_c, shard_c, nl, min_size, min_avg_w, take)
+            else:
+                res = T.component_digest_local(lsrc, ldst, w, kind_c, sup_c, shard_c, min_size, min_avg_w, take)
+        else:
+            res = _digest_compact_host(lsrc, ldst, w, valid, live, attr - 1, nl, min_size, min_avg_w, take)
+        ok = res[1] >= 0
+        nums = torch.where(ok, numof[res[1].clamp_min(0)], torch.full_like(res[1], -1))
+        rr = self._rows_of_nums(nums.clamp_min(0))
+        own = ok & (rr >= 0) & (self.holder[rr.clamp_min(0)] == self.rank)
+        kr = torch.stack([res[0], nums, torch.where(own, rr, torch.full_like(rr, -1))]).cpu().numpy()
+        mine_c = [(int(k), int(v), g.content[int(r)]) for k, v, r in zip(kr[0], kr[1], kr[2]) if r >= 0]
+        parts = self.comm.all_gather_object(mine_c) if self._coll else [mine_c]
+        if self.rank != 0:
+            return []
+        out: List[List[str]] = []
+        last = None
+        for f_, _, c in sorted(x for p in parts for x in p):
+            if f_ != last:
+                out.append([])
+                last = f_
+            out[-1].append(c)
+        return out
+
     def component_digest(self, min_size: int = 3, min_avg_w: float = 0.3,
                          take: int = PROFILE_CONTENTS) -> List[List[str]]:
         """``run_consolidation``'s component view of the WHOLE tenant
@@ -1718,7 +1833,11 @@ class ShardedMemorySystem:
         dev = self.device
         W = self.world
         n = g.n
-        if n and g.num_edges:
+        ne = int(g.num_edges) if n else 0
+        cnt = self._gather_rows(torch.tensor([ne], dtype=torch.int64, device=dev)).tolist() if self._coll else [ne]
+        if sum(cnt) <= self.DIGEST_REPLICATE_MAX:
+            return self._digest_replicated(cnt, min_size, min_avg_w, take)
+        if ne:
             s_num = self.num[g.e["src"].long()]
             d_num = self.num[g.e["dst"].long()]
             w = g.e["w"].double()

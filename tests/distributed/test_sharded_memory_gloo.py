@@ -167,6 +167,8 @@ def _sharded(comm, cfg=CPU):
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
                              embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev,
                              force_collectives=cfg.get("force", False), **extra)
+    if "digest_max" in cfg:  # -1: the boundary-label digest instead of the replicated one
+        sm.DIGEST_REPLICATE_MAX = cfg["digest_max"]
     rebal = cfg.get("rebalance", False)
     lo, hi = _split(cfg["rows"], comm.world, comm.rank, [5, 1, 2] if rebal else None)
     sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],
@@ -265,6 +267,15 @@ def test_sharded_tenant_reference_cadence_matches_single_process(world):
     out = spawn(world, functools.partial(_sharded, cfg=EXACT))
     check_equivalent(out, world, LIMIT)
     assert sum(st["consolidations"] for st in out[0]["stats"]) == STEPS * CONVS // 3
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tenant_distributed_digest_matches_single_process(world):
+    """The boundary-label component digest (taken above
+    DIGEST_REPLICATE_MAX edges) gives the same runs as the replicated one."""
+    out = spawn(world, functools.partial(_sharded, cfg=dict(EXACT, digest_max=-1)))
+    check_equivalent(out, world, LIMIT)
+    assert out[0]["contents"]
 
 
 def test_sharded_tenant_reference_cadence_forced_world1():
