@@ -597,7 +597,10 @@ def main():
     if sharded is not None:
         res["consolidate_sharded"] = {k: sharded[k] for k in (
             "turns_per_s", "ms_per_step", "buffer_nodes_total", "nodes_per_rank", "convs_per_rank_step", "per_step",
-            "scan_facts_x_rows_per_rank_step", "scan_facts_x_rows_unpruned_per_rank_step", "data", "path")}
+            "scan_facts_x_rows_per_rank_step", "scan_facts_x_rows_unpruned_per_rank_step", "data", "path",
+            "gc_in_timed_loop")}
+        if sharded.get("stages_p50_ms"):  # LZK_TRACE=1
+            res["consolidate_sharded"]["stages_p50_ms"] = sharded["stages_p50_ms"]
     from lazzaro_amd.ops import search as _S
     if _S.SPEC_STATS:  # LZK_SPEC_STATS=1 (diagnostic): queries sent to the exact fallback per store search
         res["spec_fallback_queries"] = [int(x) for x in _S.SPEC_STATS[:64]]

@@ -322,6 +322,16 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    import gc
+    gcl = [0, 0.0, 0.0]  # passes, seconds, start
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gcl[2] = time.perf_counter()
+        else:
+            gcl[0] += 1
+            gcl[1] += time.perf_counter() - gcl[2]
+    gc.callbacks.append(_gc_cb)
     t0 = time.perf_counter()
     agg = {}
     work0 = sm.scan_work
@@ -331,6 +341,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     _sync(dev)
     comm.barrier()
     el = time.perf_counter() - t0
+    gc.callbacks.remove(_gc_cb)
     if prof is not None:
         import pstats
         prof.disable()
@@ -361,6 +372,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
                                        "top": n_top, "iters_per_pass": cluster_iters,
                                        "seed_pass_ms": round(seed_ms, 1), "farthest_first_ms": ff.get("ms")},
            "load_s": round(load_s, 1), "stages_p50_ms": stages,
+           "gc_in_timed_loop": {"passes": gcl[0], "ms": round(gcl[1] * 1e3, 2)},
            "persistence": "incremental columnar commit of each rank's rows per step"}
     sm.close()
     return out

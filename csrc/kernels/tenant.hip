@@ -869,6 +869,54 @@ LZK_EXPORT int lzk_tg_first_rows(const unsigned char* kind, const unsigned char*
   return (int)hipGetLastError();
 }
 
+// Row-sharded tenants (parallel/sharded_memory.py _rows_of_nums): the local
+// row of each global node number through the sorted number index -- a base
+// over rows [0, n0) and a delta over the rows appended since, each (sorted
+// numbers, rows) -- the base winning a (never expected) tie; -1 if absent.
+// rank >= 0: only rows this rank holds live (holder == rank, kind NODE).
+// One launch instead of two searchsorted passes and their selects.
+__device__ __forceinline__ long lower_idx(const long* __restrict__ k, long n, long v) {
+  long lo = 0, hi = n;
+  while (lo < hi) {
+    const long mid = (lo + hi) >> 1;
+    if (k[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void num_rows_kernel(const long* __restrict__ nums, long add, long m,
+                                                       const long* __restrict__ bk, const long* __restrict__ bo,
+                                                       long nb, const long* __restrict__ dk,
+                                                       const long* __restrict__ dox, long nd,
+                                                       const long* __restrict__ holder,
+                                                       const unsigned char* __restrict__ kind, long rank,
+                                                       long* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  const long v = nums[i] + add;
+  long r = -1;
+  long p = lower_idx(bk, nb, v);
+  if (p < nb && bk[p] == v) {
+    r = bo[p];
+  } else {
+    p = lower_idx(dk, nd, v);
+    if (p < nd && dk[p] == v) r = dox[p];
+  }
+  if (r >= 0 && rank >= 0 && !(holder[r] == rank && kind[r] == 1)) r = -1;
+  out[i] = r;
+}
+
+LZK_EXPORT int lzk_num_rows(const long* nums, long add, long m, const long* bk, const long* bo, long nb,
+                            const long* dk, const long* dox, long nd, const long* holder,
+                            const unsigned char* kind, long rank, long* out, void* stream) {
+  if (m <= 0) return 0;
+  if (nb < 0 || nd < 0 || (rank >= 0 && (!holder || !kind))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(num_rows_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, nums,
+                     add, m, bk, bo, nb, dk, dox, nd, holder, kind, rank, out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int lzk_scan_blocks(int* cnt, int n, int* total, void* stream);
 
 // One segment end of consolidate_batch (TenantGraph.segment_end): victims

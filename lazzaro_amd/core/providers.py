@@ -334,6 +334,8 @@ _DOMAIN_HINTS = {
     "key_experiences": ("started", "moved", "graduated", "born", "won", "lost", "finished"),
 }
 
+_DOMAIN_RX = {d: re.compile("|".join(map(re.escape, h))) for d, h in _DOMAIN_HINTS.items()}
+
 
 def _topic(text: str) -> str:
     low = text.lower()
@@ -416,9 +418,10 @@ class LocalLLM(LLMProvider):
 
     def _profile(self, prompt: str) -> Dict[str, str]:
         lines = [l[2:] for l in prompt.splitlines() if l.startswith("- ")]
+        low = [l.lower() for l in lines]
         out: Dict[str, str] = {}
-        for dom, hints in _DOMAIN_HINTS.items():
-            hit = [l for l in lines if any(h in l.lower() for h in hints)]
+        for dom, rx in _DOMAIN_RX.items():  # substring match of any hint, one scan per line
+            hit = [l for l, lo in zip(lines, low) if rx.search(lo)]
             if hit:
                 out[dom] = "; ".join(hit[:2])
         return out

@@ -37,6 +37,7 @@ _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P, P, L, P])
 _lib.register("lzk_tg_first_rows", I, [P, P, P, L, P, P, P, I, P, P])
+_lib.register("lzk_num_rows", I, [P, L, L, P, P, L, P, P, L, P, P, L, P, P])
 _lib.register("lzk_dg_small_ws", L, [I])
 _lib.register("lzk_tg_append_edges", I, [P, I, L, I, D_, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_seg_end", I, [P, I, P, P, P, P, I, P, P, P, P, L, P, L, P, P, P, P])
@@ -537,6 +538,26 @@ def component_digest_local(src: torch.Tensor, dst: torch.Tensor, w: torch.Tensor
     ks = torch.where(ok, key_s[o2], torch.full_like(c2, BIG))
     grow = torch.where(ok, rowmap[o1[o2]], torch.full_like(c2, -1))
     return torch.stack([ks, grow])
+
+
+def num_rows(nums: torch.Tensor, add: int, base_k: torch.Tensor, base_o: torch.Tensor, delta_k: torch.Tensor,
+             delta_o: torch.Tensor, holder: Optional[torch.Tensor] = None, kind: Optional[torch.Tensor] = None,
+             rank: int = -1) -> torch.Tensor:
+    """tenant.hip num_rows_kernel: the local row of each number ``nums + add``
+    in a sorted number index (base, then delta; int64, -1 if absent); with
+    ``rank`` >= 0 only rows that rank holds live (holder == rank, kind
+    NODE). One launch, no host synchronisation."""
+    nums = nums.to(torch.int64).contiguous()
+    out = torch.empty_like(nums)
+    m = int(nums.numel())
+    if m == 0:
+        return out
+    _lib.check(_lib.lib().lzk_num_rows(nums.data_ptr(), int(add), m, base_k.data_ptr(), base_o.data_ptr(),
+                                       int(base_k.numel()), delta_k.data_ptr(), delta_o.data_ptr(),
+                                       int(delta_k.numel()), holder.data_ptr() if holder is not None else None,
+                                       kind.data_ptr() if kind is not None else None, int(rank), out.data_ptr(),
+                                       _st(nums)), "num_rows")
+    return out
 
 
 def first_rows(kind: torch.Tensor, sup: torch.Tensor, shard: torch.Tensor, n: int, tgt: np.ndarray,

@@ -80,7 +80,7 @@ import torch
 
 from ..core.consolidation import (DECAY_RATE, LINK_THRESHOLD, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS,
                                   batch_dedupe, batch_link_plan, salience_decayed)
-from ..engine.tenant_graph import NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT, _seg_min, _seg_sum_count
+from ..engine.tenant_graph import GHOST, NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT, _seg_min, _seg_sum_count
 from ..ops import tenant_ops as T
 from ..utils.tracing import tracer
 from .comm import Communicator
@@ -219,7 +219,7 @@ class ShardedMemorySystem:
         """Variable-length rows of every rank in rank order (+ per-rank counts)."""
         if not self._coll:
             return t, [int(t.shape[0])]
-        cnt = self._gather_rows(torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)).tolist()
+        cnt = self._host_ints(int(t.shape[0]))[:, 0].tolist()  # counts over gloo: no device read
         mx = max(cnt)
         if mx == 0:  # nothing anywhere (every rank sees the same counts): no empty collective
             return t, cnt
@@ -229,11 +229,14 @@ class ShardedMemorySystem:
         idx = torch.cat([torch.arange(r * mx, r * mx + c) for r, c in enumerate(cnt)]).to(t.device)
         return g[idx], cnt
 
+    def _host_ints(self, *vals) -> np.ndarray:
+        """[world, len(vals)] host ints of every rank (gloo; host metadata
+        never waits on the GPU stream)."""
+        a = np.asarray([int(v) for v in vals], np.int64)
+        return self.comm.host_all_gather(a) if self._coll else a[None]
+
     def _sum(self, *vals) -> List[int]:
-        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)
-        if self._coll:
-            t = self.comm.all_reduce(self._to_comm(t)).to(self.device)
-        return [int(x) for x in t.tolist()]
+        return [int(x) for x in self._host_ints(*vals).sum(0).tolist()]
 
     def _sync_num(self) -> None:
         n = self.g.n
@@ -272,19 +275,31 @@ class ShardedMemorySystem:
             ix["n1"] = n
         return ix
 
-    def _rows_of_nums(self, nums: torch.Tensor) -> torch.Tensor:
-        """Local row holding each global node number (live or ghost), -1 if
-        none: binary searches in the cached sorted number index (no host map)."""
-        n = self.g.n
+    def _rows_of_nums(self, nums: torch.Tensor, held: bool = False, add: int = 0) -> torch.Tensor:
+        """Local row holding each global node number ``nums + add`` (live or
+        ghost), -1 if none: binary searches in the cached sorted number index
+        (no host map) -- on the GPU one kernel (tenant_ops.num_rows). ``held``:
+        only rows this rank holds live."""
+        g = self.g
+        n = g.n
         if n == 0 or nums.numel() == 0:
             return torch.full_like(nums, -1)
         ix = self._num_index()
+        if g.on_gpu:
+            return T.num_rows(nums, add, ix["ks"], ix["o"], ix["dk"], ix["do"], self.holder, g.kind,
+                              self.rank if held else -1)
+        if add:
+            nums = nums + add
         out = torch.full_like(nums, -1)
         for ks, o in ((ix["dk"], ix["do"]), (ix["ks"], ix["o"])):  # the base wins a (never expected) tie
             if ks.numel() == 0:
                 continue
             pos = torch.searchsorted(ks, nums).clamp_max(ks.numel() - 1)
             out = torch.where(ks[pos] == nums, o[pos], out)
+        if held:
+            rc = out.clamp_min(0)
+            ok = (out >= 0) & (self.holder[rc] == self.rank) & (g.kind[rc] == NODE)
+            out = torch.where(ok, out, torch.full_like(out, -1))
         return out
 
     def _ids_of_nums(self, nums) -> List[str]:
@@ -358,12 +373,12 @@ class ShardedMemorySystem:
             r = rows[a: a + self.REACH_CHUNK]
             X = g.emb32[r].float()
             nrm = g.sqn[r].float().sqrt()
-            S = (X @ C.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[:, None]
+            den = torch.where(nrm > 0, nrm, torch.ones_like(nrm))
             if lab is None:
-                cs, lb = S.max(1)
-            else:
+                cs, lb = ((X @ C.T) / den[:, None]).max(1)
+            else:  # the labelled centroid only: a row dot, not a [rows, K] GEMM (10M x 4096 after a pass)
                 lb = lab[a: a + self.REACH_CHUNK]
-                cs = S.gather(1, lb[:, None]).squeeze(1)
+                cs = (X * C[lb]).sum(1) / den
             cs = torch.where(nrm > 0, cs, torch.full_like(cs, -1.0))
             labs.append(lb)
             coss.append(cs.double() - self.REACH_SLACK)
@@ -671,7 +686,9 @@ class ShardedMemorySystem:
         stats = {"conversations": 0, "facts": 0, "dup": 0, "inserted": 0, "linked": 0, "cross_links": 0,
                  "pruned": 0, "evicted": 0, "consolidations": 0, "fallbacks": 0}
         if cadence == "conversation":
-            with self.local._graph_lock, tracer.stage("sharded_consolidate", dev):
+            # one switch to the graph's stream for the whole batch (as the
+            # single process): the graph operations inside skip their stream hop
+            with self.local._graph_lock, tracer.stage("sharded_consolidate", dev), g.on_stream():
                 self._consolidate_exact(flat, conv, E, B_loc, now, stats)
                 self.local.node_counter = self._fact_count
                 with tracer.stage("persist", "cpu"):
@@ -706,7 +723,7 @@ class ShardedMemorySystem:
         m = len(flat)
         # ---- 1. the global fact batch (rank-major conversation order)
         with tracer.stage("sc_gather", dev):
-            bl = self._gather_rows(torch.tensor([B_loc], dtype=torch.int64, device=dev)).tolist()
+            bl = self._host_ints(B_loc)[:, 0].tolist()
             B = int(sum(bl))
             c_off = int(sum(bl[: self.rank]))
             keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
@@ -960,13 +977,7 @@ class ShardedMemorySystem:
     def _held_rows(self, vrows: torch.Tensor) -> torch.Tensor:
         """Local row of each global row this rank HOLDS live (-1 elsewhere:
         not here, a ghost, or gone)."""
-        g = self.g
-        if g.n == 0 or vrows.numel() == 0:
-            return torch.full_like(vrows, -1)
-        r = self._rows_of_nums(vrows + 1)
-        rc = r.clamp_min(0)
-        ok = (r >= 0) & (self.holder[rc] == self.rank) & (g.kind[rc] == NODE)
-        return torch.where(ok, r, torch.full_like(r, -1))
+        return self._rows_of_nums(vrows, held=True, add=1)
 
     def _merge_lists(self, s: torch.Tensor, v: torch.Tensor, k: int):
         """Per fact: top-k of the gathered (score, global row) entries by
@@ -1246,7 +1257,7 @@ class ShardedMemorySystem:
         K = self.local.BATCH_LIST_K
         # ---- 1. the global fact batch (rank-major conversation order)
         with tracer.stage("sc_gather", dev):
-            bl = self._gather_rows(torch.tensor([B_loc], dtype=torch.int64, device=dev)).tolist()
+            bl = self._host_ints(B_loc)[:, 0].tolist()
             B = int(sum(bl))
             c_off = int(sum(bl[: self.rank]))
             keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
@@ -1343,14 +1354,8 @@ class ShardedMemorySystem:
             return (((Qn @ ed) / (en if en > 0 else 1.0)).cpu().numpy() if F else np.zeros(0)), n2
 
         # ---- 3. plan (identical on every rank), eviction pool verified everywhere
-        node_count = self._sum(g.num_nodes())[0]
-        nsh = len(g.shard_count)
-        sc = torch.zeros(nsh, dtype=torch.int64, device=dev)
-        if nsh:
-            sc += torch.as_tensor(g.shard_count, dtype=torch.int64).to(dev)
-            if self._coll:
-                sc = self.comm.all_reduce(self._to_comm(sc)).to(dev)
-        shard_count = sc.cpu().tolist()
+        tot = self._sum(g.num_nodes(), *g.shard_count)  # every rank registered the same shards
+        node_count, shard_count = tot[0], tot[1:]
         excess0 = max(0, node_count - self.max_buffer_size)
         P = 4 * (F + excess0) + 1024  # per rank (a rank with fewer evictable rows pools them all)
         cl_every = int(self.hierarchy_params["every"]) if self.hierarchy_params else 0
@@ -1403,10 +1408,11 @@ class ShardedMemorySystem:
         count0 = self.conversation_count
         etype = g.etype("relates_to")
         n_fact = n0 - int(np.searchsorted(self._sup_v, n0))
+        reach_new: List[torch.Tensor] = []
         for seg in pl["segments"]:
             with tracer.stage("cb_apply", dev):
                 pruned_local = self._apply_exact_segment(seg, supers, fact_key, origin_h, codes, Q, flat, f_off,
-                                                         holder_of, shard_of, thr, now, etype)
+                                                         holder_of, shard_of, thr, now, etype, reach_new)
             pruned += self._sum(pruned_local)[0]
             self.conversation_count = count0 + int(seg["c1"]) + 1
             if seg["consolidate"]:
@@ -1414,6 +1420,9 @@ class ShardedMemorySystem:
                 with tracer.stage("run_consolidation", dev):
                     self.run_consolidation()
             if seg["cluster"]:
+                if reach_new:  # the pass rebuilds the cones from every row
+                    self._reach_add(torch.cat(reach_new))
+                    reach_new.clear()
                 with tracer.stage("cluster", dev):
                     self.cluster_pass()
             if self._commit_each:  # the counter as of this conversation
@@ -1422,13 +1431,15 @@ class ShardedMemorySystem:
                 with tracer.stage("commit", "cpu"):
                     self.local._save_to_persistence()
         stats["pruned"] += pruned
+        if reach_new:
+            self._reach_add(torch.cat(reach_new))
         if self.hierarchy_params and getattr(g, "hier", None) is None:
             self.cluster_pass()
         if self.local.query_cache:
             self.local.query_cache.invalidate_results()
 
     def _apply_exact_segment(self, seg, supers, fact_key, origin_h, codes, Q, flat, f_off, holder_of, shard_of, thr,
-                             now, etype) -> int:
+                             now, etype, reach_new) -> int:
         """This rank's part of one plan segment (see :meth:`_consolidate_exact`).
         Returns the local edges the segment's decay pruned."""
         g = self.g
@@ -1483,7 +1494,7 @@ class ShardedMemorySystem:
                 self._sync_num()
                 self.num[rows] = torch.as_tensor(keys + 1, dtype=torch.long).to(dev)
                 self.holder[rows] = me
-                self._reach_add(rows)
+                reach_new.append(rows)  # cone test once per batch (the next batch's scan reads it)
         # super-nodes after the facts: their children (earlier keys) all exist
         for p in np.nonzero(kinds != 0)[0].tolist():
             sp = supers[int(idx_all[p])]
@@ -1742,6 +1753,26 @@ class ShardedMemorySystem:
     # work and the bytes distributed (the 20M-edge persistent graph per rank).
     DIGEST_REPLICATE_MAX = 1 << 22
 
+    def _digest_world1(self, min_size: int, min_avg_w: float, take: int) -> List[List[str]]:
+        """:meth:`component_digest` of a one-rank tenant on the GPU: the local
+        rows are the whole tenant (no ghosts), rows are appended in node-number
+        order (a fact's number and row both follow the plan's insertion
+        order), so the single-graph digest kernels run on the rows directly --
+        super-node rows passed as non-candidate members, as the distributed
+        form counts them (they are not first-member keys)."""
+        g = self.g
+        n = g.n
+        sup = g.sup[:n]
+        kind = torch.where((g.kind[:n] == NODE) & (sup != 0), torch.full_like(g.kind[:n], GHOST), g.kind[:n])
+        e = g.e
+        if g.num_edges <= T.dg_small_max_edges():
+            res = T.component_digest_small(e["src"], e["dst"], e["w"], kind, sup, g.shard[:n], n, min_size,
+                                           min_avg_w, take)
+        else:
+            res = T.component_digest_local(e["src"], e["dst"], e["w"], kind, sup, g.shard[:n], min_size, min_avg_w,
+                                           take)
+        return [[g.content[int(r)] for r in rows] for rows in T.digest_lists(res.cpu().numpy())]
+
     def _digest_replicated(self, cnt: List[int], min_size: int, min_avg_w: float, take: int) -> List[List[str]]:
         """:meth:`component_digest` over the replicated edge list, four
         collectives in all (edge counts, edges, the endpoints' liveness, the
@@ -1834,7 +1865,9 @@ class ShardedMemorySystem:
         W = self.world
         n = g.n
         ne = int(g.num_edges) if n else 0
-        cnt = self._gather_rows(torch.tensor([ne], dtype=torch.int64, device=dev)).tolist() if self._coll else [ne]
+        if W == 1 and g.on_gpu and ne:
+            return self._digest_world1(min_size, min_avg_w, take)
+        cnt = self._host_ints(ne)[:, 0].tolist()
         if sum(cnt) <= self.DIGEST_REPLICATE_MAX:
             return self._digest_replicated(cnt, min_size, min_avg_w, take)
         if ne:

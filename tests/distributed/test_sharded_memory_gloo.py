@@ -169,6 +169,17 @@ def _sharded(comm, cfg=CPU):
                              force_collectives=cfg.get("force", False), **extra)
     if "digest_max" in cfg:  # -1: the boundary-label digest instead of the replicated one
         sm.DIGEST_REPLICATE_MAX = cfg["digest_max"]
+    if cfg.get("digest_check"):  # one GPU rank: the row digest equals the replicated one at every point
+        real = sm.component_digest
+        seen = []
+
+        def checked(min_size=3, min_avg_w=0.3, take=10):
+            a = real(min_size, min_avg_w, take)
+            b = sm._digest_replicated([sm.g.num_edges], min_size, min_avg_w, take) if sm.g.num_edges else []
+            assert a == b, (a, b)
+            seen.append(len(a))
+            return a
+        sm.component_digest = checked
     rebal = cfg.get("rebalance", False)
     lo, hi = _split(cfg["rows"], comm.world, comm.rank, [5, 1, 2] if rebal else None)
     sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],

@@ -34,3 +34,57 @@ def test_sharded_tenant_gpu_reference_hierarchy():
     check_equivalent(out, 2, cfg["limit"])
     nodes = out[0]["nodes"]
     assert any(v[4] is not None for v in nodes.values())
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_sharded_tenant_gpu_one_rank_row_digest():
+    """One GPU rank: component_digest runs the single-graph digest kernels on
+    the local rows (_digest_world1); at every run_consolidation point it
+    equals the replicated-edge digest, and the run is the single process's."""
+    cfg = dict(GPU, steps=2, convs=24, cadence="conversation", digest_check=True)
+    out = spawn(1, functools.partial(_sharded, cfg=cfg))
+    check_equivalent(out, 1, cfg["limit"])
+    assert out[0]["contents"]
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_num_rows_kernel_matches_searchsorted():
+    """tenant.hip num_rows_kernel (the row-sharded tenant's number -> row
+    lookup): base-then-delta binary search and the held-live filter against
+    the torch searchsorted formulation, with absent numbers, a base/delta tie
+    and an empty delta."""
+    from lazzaro_amd.ops import tenant_ops as T
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(5)
+    nb, nd = 5000, 300
+    nums = torch.randperm(50_000, generator=g)[: nb + nd] * 3 + 1
+    bk, bo = torch.sort(nums[:nb])
+    bo = bo.clone()
+    dk, do = torch.sort(nums[nb:])
+    do = do + nb
+    dk = torch.cat([dk, bk[:1]])  # a number in both: the base wins
+    do = torch.cat([do, torch.tensor([nb + nd])])
+    dk, o = torch.sort(dk)
+    do = do[o]
+    holder = torch.randint(0, 3, (nb + nd + 1,), generator=g)
+    kind = torch.randint(0, 3, (nb + nd + 1,), generator=g).to(torch.uint8)
+    q = torch.cat([nums[torch.randint(0, nb + nd, (4000,), generator=g)], torch.tensor([0, 2, 150_001, bk[0].item()])])
+
+    def ref(q, held, empty_delta):
+        out = torch.full_like(q, -1)
+        pairs = [(bk, bo)] if empty_delta else [(dk, do), (bk, bo)]
+        for ks, oo in pairs:
+            pos = torch.searchsorted(ks, q).clamp_max(ks.numel() - 1)
+            out = torch.where(ks[pos] == q, oo[pos], out)
+        if held >= 0:
+            rc = out.clamp_min(0)
+            out = torch.where((out >= 0) & (holder[rc] == held) & (kind[rc] == 1), out, torch.full_like(out, -1))
+        return out
+
+    for empty_delta in (False, True):
+        d_k = dk[:0] if empty_delta else dk
+        d_o = do[:0] if empty_delta else do
+        for held in (-1, 1):
+            got = T.num_rows(q.to(dev) - 1, 1, bk.to(dev), bo.to(dev), d_k.to(dev), d_o.to(dev), holder.to(dev),
+                             kind.to(dev), held)
+            assert torch.equal(got.cpu(), ref(q, held, empty_delta))
