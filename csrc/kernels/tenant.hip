@@ -917,6 +917,45 @@ LZK_EXPORT int lzk_num_rows(const long* nums, long add, long m, const long* bk, 
   return (int)hipGetLastError();
 }
 
+// Row-sharded cone radii (parallel/sharded_memory.py _row_cos with labels):
+// cos of each row with ITS cluster's unit centroid, fp32 -- one wave per
+// row, 16-B loads, a wave reduction; rows without a vector (sqn 0) -> -1.
+// One read of the rows instead of a [rows x K] GEMM for one column each.
+__global__ __launch_bounds__(256) void row_cent_cos_kernel(const float* __restrict__ X, long ldx, int D,
+                                                           const float* __restrict__ sqn,
+                                                           const long* __restrict__ rows,
+                                                           const long* __restrict__ lab, long m,
+                                                           const float* __restrict__ C, long ldc,
+                                                           float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= m) return;
+  const long r = rows[i];
+  const float* x = X + r * ldx;
+  const float* c = C + lab[i] * ldc;
+  float acc = 0.f;
+  for (int k = lane * 4; k < D; k += 256) {  // D % 4 == 0 (checked by the caller)
+    const float4 a = *reinterpret_cast<const float4*>(x + k);
+    const float4 b = *reinterpret_cast<const float4*>(c + k);
+    acc += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) {
+    const float n2 = sqn[r];
+    out[i] = n2 > 0.f ? acc / sqrtf(n2) : -1.f;
+  }
+}
+
+LZK_EXPORT int lzk_row_cent_cos(const float* X, long ldx, int D, const float* sqn, const long* rows,
+                                const long* lab, long m, const float* C, long ldc, float* out, void* stream) {
+  if (m <= 0) return 0;
+  if (D <= 0 || D % 4 != 0 || ldx % 4 != 0 || ldc % 4 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_cent_cos_kernel, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, X, ldx,
+                     D, sqn, rows, lab, m, C, ldc, out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int lzk_scan_blocks(int* cnt, int n, int* total, void* stream);
 
 // One segment end of consolidate_batch (TenantGraph.segment_end): victims

@@ -38,6 +38,7 @@ _lib.register("lzk_dg_stats", I, [P, P, P, L, P, L, P, P, P, I, D_, I, P, P, P, 
 _lib.register("lzk_dg_select", I, [P, L, P, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P, P, L, P])
 _lib.register("lzk_tg_first_rows", I, [P, P, P, L, P, P, P, I, P, P])
 _lib.register("lzk_num_rows", I, [P, L, L, P, P, L, P, P, L, P, P, L, P, P])
+_lib.register("lzk_row_cent_cos", I, [P, L, I, P, P, P, L, P, L, P, P])
 _lib.register("lzk_dg_small_ws", L, [I])
 _lib.register("lzk_tg_append_edges", I, [P, I, L, I, D_, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_seg_end", I, [P, I, P, P, P, P, I, P, P, P, P, L, P, L, P, P, P, P])
@@ -557,6 +558,24 @@ def num_rows(nums: torch.Tensor, add: int, base_k: torch.Tensor, base_o: torch.T
                                        int(delta_k.numel()), holder.data_ptr() if holder is not None else None,
                                        kind.data_ptr() if kind is not None else None, int(rank), out.data_ptr(),
                                        _st(nums)), "num_rows")
+    return out
+
+
+def row_centroid_cos(X: torch.Tensor, D: int, sqn: torch.Tensor, rows: torch.Tensor, lab: torch.Tensor,
+                     C: torch.Tensor) -> torch.Tensor:
+    """tenant.hip row_cent_cos_kernel: fp32 cos of each row ``X[rows[i], :D]``
+    with its centroid ``C[lab[i]]`` (unit rows), -1 for rows without a vector
+    (``sqn`` 0). One read of the rows; no [rows, K] product."""
+    rows = rows.to(torch.int64).contiguous()
+    lab = lab.to(torch.int64).contiguous()
+    C = C.float().contiguous()
+    out = torch.empty(rows.numel(), dtype=torch.float32, device=rows.device)
+    if rows.numel() == 0:
+        return out
+    assert X.dtype == torch.float32 and X.stride(1) == 1 and sqn.dtype == torch.float32
+    _lib.check(_lib.lib().lzk_row_cent_cos(X.data_ptr(), X.stride(0), int(D), sqn.data_ptr(), rows.data_ptr(),
+                                           lab.data_ptr(), int(rows.numel()), C.data_ptr(), C.stride(0),
+                                           out.data_ptr(), _st(rows)), "row_cent_cos")
     return out
 
 

@@ -368,6 +368,9 @@ class ShardedMemorySystem:
         given labels, or the nearest centroid. Rows without a vector -> cos -1
         (the cluster's radius becomes 180 degrees: never pruned)."""
         g = self.g
+        if lab is not None and g.on_gpu and g.dim % 4 == 0:  # one fused pass over the rows
+            cs = T.row_centroid_cos(g.emb32, g.dim, g.sqn, rows, lab, C)
+            return lab, cs.double() - self.REACH_SLACK
         labs, coss = [], []
         for a in range(0, rows.numel(), self.REACH_CHUNK):
             r = rows[a: a + self.REACH_CHUNK]
@@ -1538,9 +1541,9 @@ class ShardedMemorySystem:
         if vic.size:
             hv = np.asarray([holder_of.get(int(x), -1) for x in vic.tolist()], np.int64)
             mv = vic[hv == me]
-            if mv.size:
-                lr = self._held_rows(torch.as_tensor(mv).to(dev))
-                loc_v = lr[lr >= 0].cpu().tolist()
+            if mv.size:  # victims are live fact nodes held here: their rows by id, no device read
+                ro = g.row_of
+                loc_v = [r for r in (ro.get(i, -1) for i in self._ids_of_nums(mv + 1)) if r >= 0]
             other = vic[hv != me]
         ids = [g.ids[r] for r in loc_v]
         pruned = g.segment_end(tok, loc_v, unstore=True)
@@ -2005,8 +2008,8 @@ class ShardedMemorySystem:
                                   torch.full((n,), BIG, dtype=torch.long, device=self.device))
                 k = min(take, n)
                 v, r = torch.topk(key, k, largest=False, sorted=True)
-                r = r[v < BIG]
-                mine = [(int(key[x]), g.content[x]) for x in r.tolist()]
+                vr = torch.stack([v, r]).cpu().tolist()  # one device read
+                mine = [(int(a), g.content[int(b)]) for a, b in zip(*vr) if a < BIG]
         parts = self.comm.all_gather_object(mine) if self._coll else [mine]
         return [c for _, c in sorted(x for p in parts for x in p)[:take]] if self.rank == 0 else []
 

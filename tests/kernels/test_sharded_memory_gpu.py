@@ -88,3 +88,27 @@ def test_num_rows_kernel_matches_searchsorted():
             got = T.num_rows(q.to(dev) - 1, 1, bk.to(dev), bo.to(dev), d_k.to(dev), d_o.to(dev), holder.to(dev),
                              kind.to(dev), held)
             assert torch.equal(got.cpu(), ref(q, held, empty_delta))
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_row_centroid_cos_kernel():
+    """tenant.hip row_cent_cos_kernel (the cone radii of the row-sharded
+    scan pruning) against the fp32 torch formula, padded row stride, rows
+    without a vector."""
+    from lazzaro_amd.ops import tenant_ops as T
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(3)
+    n, D, Dp, K = 5000, 760, 768, 64
+    X = torch.zeros((n, Dp), device=dev)
+    X[:, :D] = torch.randn((n, D), device=dev, generator=g)
+    X[7] = 0.0
+    sqn = (X * X).sum(1)
+    C = torch.nn.functional.normalize(torch.randn((K, D), device=dev, generator=g), dim=1)
+    rows = torch.randperm(n, device=dev, generator=g)[:3000]
+    lab = torch.randint(0, K, (3000,), device=dev, generator=g)
+    got = T.row_centroid_cos(X, D, sqn, rows, lab, C)
+    nrm = sqn[rows].sqrt()
+    ref = (X[rows, :D] * C[lab]).sum(1) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))
+    ref = torch.where(nrm > 0, ref, torch.full_like(ref, -1.0))
+    assert torch.allclose(got, ref, atol=2e-6, rtol=0)
+    assert float(got[(rows == 7).nonzero().flatten()].sum() if bool((rows == 7).any()) else -1.0) == -1.0
