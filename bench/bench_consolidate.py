@@ -136,7 +136,11 @@ def _sync(dev):
 def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, encoder=None, dim: int = 768,
         dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096, n_top: int = 64,
         cluster_iters: int = 2, init_edges: int = None, db_dir: str = None, prune_threshold: float = 0.5,
-        persist_async: bool = False):
+        persist_async: bool = False, stream: bool = True):
+    """``stream``: the batches go through ``MemorySystem.consolidate_stream``
+    (batch i+1's candidate scan under batch i's apply; results identical to
+    the per-batch calls, tests/kernels/test_tenant_engine_gpu.py); False:
+    one ``consolidate_batch`` call per step."""
     db_dir = db_dir or tempfile.mkdtemp(prefix=f"lzcons{comm.rank}_")
     init_edges = 2 * nodes if init_edges is None else init_edges
     ms = build_tenant(dev, nodes, dim, encoder, seed + 31 * comm.rank, db_dir, cluster_every * convs, n_fine, n_top,
@@ -155,17 +159,25 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
 
     batches = iter([synth_facts(convs, facts, rng) for _ in range(warmup + steps)])
 
-    def step():
+    def make_batch():
         conversations = next(batches)
         V = synth_vectors(ms, convs * facts, dim, dup_rate, gen)
         texts = [f["content"] for c in conversations for f in c]
         from lazzaro_amd.utils.tracing import tracer as _tr
         with _tr.stage("fact_embed", dev):
             ms._batch_embed_any(texts)  # the fact embedding runs (see module doc)
-        return ms.consolidate_batch(conversations, embeddings=V)
+        return conversations, V
 
-    for _ in range(warmup):
-        step()
+    def run_steps(k):
+        if stream:
+            yield from ms.consolidate_stream(make_batch() for _ in range(k))
+        else:
+            for _ in range(k):
+                conversations, V = make_batch()
+                yield ms.consolidate_batch(conversations, embeddings=V)
+
+    for _ in run_steps(warmup):
+        pass
     _sync(dev)
     comm.barrier()
     prof = None
@@ -180,8 +192,8 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
         tprof.__enter__()
     t0 = time.perf_counter()
     agg = {}
-    for _ in range(steps):
-        for k, v in step().items():
+    for st in run_steps(steps):
+        for k, v in st.items():
             agg[k] = agg.get(k, 0) + v
     ms.flush_persistence()  # write-behind commits of the timed steps land inside the timed region
     _sync(dev)
@@ -223,7 +235,8 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
            # per-rank scan work (facts x rows of the rank's own tenant): no
            # rank ever scans another rank's rows, so it is independent of N
            "scan_facts_x_rows_per_rank_step": int(convs * facts * g.n),
-           "path": "MemorySystem.consolidate_batch (tenant-DP)",
+           "path": ("MemorySystem.consolidate_stream (tenant-DP; batch i+1's scan under batch i's apply)" if stream
+                    else "MemorySystem.consolidate_batch (tenant-DP)"),
            "hierarchical_clustering": {"mode": "kmeans", "every_steps": cluster_every, "fine": n_fine, "top": n_top,
                                        "iters_per_pass": cluster_iters, "seed_pass_ms": round(seed_ms, 1),
                                        "farthest_first_ms": ff.get("ms")},
@@ -400,6 +413,8 @@ if __name__ == "__main__":
                     help="MemorySystem(prune_threshold=): 0.5 is the reference default; 0 keeps every edge "
                          "(decay still runs on all of them) -- the large-graph variant")
     ap.add_argument("--persist-async", action="store_true", help="MemorySystem(persist_async=True)")
+    ap.add_argument("--no-stream", dest="stream", action="store_false",
+                    help="one consolidate_batch call per step instead of consolidate_stream")
     ap.add_argument("--init-edges", type=int, default=None, help="seeded edges (default 2 x nodes)")
     ap.add_argument("--sharded", action="store_true",
                     help="config 4 as one tenant row-sharded over the ranks (--nodes per rank)")
@@ -419,7 +434,7 @@ if __name__ == "__main__":
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
              **({"clustered": a.clustered, "cadence": a.cadence} if a.sharded else {"prune_threshold": a.prune_threshold,
-                                                              "persist_async": a.persist_async}))
+                                                              "persist_async": a.persist_async, "stream": a.stream}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)
     if comm.enabled:

@@ -243,6 +243,17 @@ def _parse_json(response: str):
     return json.loads(response)
 
 
+_PF_STREAMS: Dict = {}
+
+
+def _prefetch_stream(dev):
+    """One side stream per device for prefetched candidate scans."""
+    st = _PF_STREAMS.get(dev)
+    if st is None:
+        st = _PF_STREAMS[dev] = torch.cuda.Stream(dev)
+    return st
+
+
 class ConsolidationMixin:
     graph: TenantGraph
 
@@ -678,6 +689,7 @@ class ConsolidationMixin:
         if commit not in ("conversation", "batch"):
             raise ValueError("commit must be 'conversation' or 'batch'")
         self._commit_each = commit == "conversation" and cadence == "conversation"
+        self._batch_src = embeddings  # a prefetched scan is keyed by its batch's embeddings object
         flat, conv, idx = [], [], []
         j = 0
         for c, fs in enumerate(conversations):
@@ -722,6 +734,75 @@ class ConsolidationMixin:
                 self.query_cache.invalidate_results()
             self._save_to_persistence()
         return stats
+
+    def consolidate_stream(self, batches, cadence: str = "conversation", commit: str = "batch"):
+        """:meth:`consolidate_batch` over a stream of batches, yielding each
+        batch's counts. ``batches`` yields ``(conversations, embeddings)`` or
+        ``(conversations, embeddings, now)``. The result is the sequential
+        calls' exactly; what differs is when the work runs: batch i+1's
+        candidate scan (the batch's one pass over the whole tenant) is
+        launched on a side stream as soon as batch i is planned, and runs
+        while batch i's plan is applied on the host and the graph stream;
+        batch i+1 then completes it against the graph as batch i left it
+        (TenantGraph.cos_topk_finish: rows that left re-scanned, rows that
+        arrived re-ranked in). The next item is drawn from ``batches`` before
+        batch i is applied."""
+        it = iter(batches)
+        cur = next(it, None)
+        try:
+            while cur is not None:
+                nxt = next(it, None)
+                self._prefetch_next = nxt
+                convs, embs = cur[0], cur[1]
+                now = cur[2] if len(cur) > 2 else None
+                yield self.consolidate_batch(convs, embeddings=embs, now=now, cadence=cadence, commit=commit)
+                cur = nxt
+        finally:
+            self._prefetch_next = None
+            self._prefetched = None
+
+    _prefetch_next = None
+    _prefetched = None
+
+    def _launch_prefetch(self, pl: Dict) -> None:
+        """Batch i+1's dual candidate scan (see :meth:`consolidate_stream`),
+        launched after batch i's plan. Skipped when batch i runs a cluster
+        pass (it shares the scan workspaces) or the scan is not the kernel
+        path."""
+        nxt, self._prefetch_next = self._prefetch_next, None
+        self._prefetched = None
+        g = self.graph
+        if nxt is None or not g.on_gpu or nxt[1] is None or any(seg["cluster"] for seg in pl["segments"]):
+            return
+        convs, embs = nxt[0], nxt[1]
+        flat, idx, j = [], [], 0
+        for fs in convs:
+            for f in fs:
+                if isinstance(f, dict) and f.get("content") and len(f["content"]) >= MIN_FACT_LEN:
+                    flat.append(f)
+                    idx.append(j)
+                j += 1
+        M = len(flat)
+        if M == 0 or not g.dual_prefetch_ok(M, self.BATCH_LIST_K):
+            return
+        E = embs if torch.is_tensor(embs) else torch.as_tensor(np.asarray(embs, np.float32))
+        E = E[torch.as_tensor(idx, dtype=torch.long).to(E.device)] if len(idx) != len(E) else E
+        E, valid = self._fact_matrix(E, M)
+        vidx = np.nonzero(valid)[0]
+        flat = [flat[i] for i in vidx]
+        E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
+        # the shards of batch i+1 are registered now, in its fact order: the
+        # codes batch i+1 will assign (batch i registers none while applied)
+        codes = np.asarray([g.shard_id(f.get("topic", self._infer_shard_key(f["content"]))) for f in flat],
+                           dtype=np.int64)
+        ps = pl["stats"]
+        g.reserve(g.n + int(ps["inserted"]) + len(pl["supers"]) + 16)  # no column moves under the scan
+        n = g.n
+        with g.on_stream():
+            Q = E.to(g.device, torch.float32)
+            mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
+            h = g.cos_topk_prefetch(Q, mask, torch.as_tensor(codes), LINK_THRESHOLD, _prefetch_stream(g.device))
+        self._prefetched = {"src": embs, "codes": codes, "M": len(flat), "h": h}
 
     def _maybe_cluster(self, c0: int) -> None:
         """hierarchy_mode="kmeans": re-cluster when the conversation count
@@ -834,6 +915,9 @@ class ConsolidationMixin:
         for k in ("dup", "inserted", "linked", "cross_links", "evicted", "fallbacks"):
             stats[k] += int(ps[k])
         stats["pruned"] += int(ps["pruned_new"])
+        if self._prefetch_next is not None:
+            with tracer.stage("cb_prefetch", self._device):
+                self._launch_prefetch(pl)
         fact_key = np.asarray(pl["fact_key"], np.int64)
         fact_of = {int(k): int(j) for j, k in enumerate(fact_key.tolist()) if k >= 0}
         id_of = {}
@@ -926,7 +1010,14 @@ class ConsolidationMixin:
         else:
             Q = Qn = torch.zeros((0, g.dim or 1), dtype=torch.float64, device=dev)
         link_mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0) if n else None
-        if n and M:
+        pf, self._prefetched = self._prefetched, None
+        if not (pf is not None and pf["src"] is getattr(self, "_batch_src", None) and pf["M"] == M
+                and np.array_equal(pf["codes"], codes)):
+            pf = None
+        if n and M and pf is not None:  # batch i+1's scan ran under batch i's apply
+            with g.on_stream(), tracer.stage("cb_prefetch_finish", dev):
+                (gs, gr), (ws, wr) = g.cos_topk_finish(pf["h"], K, link_mask)
+        elif n and M:
             with g.on_stream():
                 (gs, gr), (ws, wr) = g.cos_topk(Q, K, link_mask, dual_label=torch.as_tensor(codes),
                                                 min_score=LINK_THRESHOLD)

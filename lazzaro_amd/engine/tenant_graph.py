@@ -1999,40 +1999,13 @@ class TenantGraph:
         if lean and not self.unit_rows():  # (no bf16 rows; the int8 error model needs unit rows)
             pass
         elif (self._use_kernel(M) or lean) and k <= CAND_SLOTS:
+            if dual_label is not None:
+                ra, rb = self._dual_cands(Qn, mask, dual_label, min_score)
+                return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
             bias = torch.where(mask, 0.0, NEG_INF).to(torch.float32).contiguous()
             q16 = self._q16(Qn)
             X = self._scan_rows(n, Qn)
-            # lean: the int8 scans' re-score reads fp32 rows with fp32 queries
-            # while their threshold sample and margin are bf16-based, so every
-            # int8 margin below also covers |<q16, x16> - <q, x>| <= 2^-8 |q| |x|
-            # (both operands rounded to bf16; unit queries) -- as _i8_candidates
             lean_w = 2.0 ** -8 * (1.0 + self.max_norm_dev) if self.emb16 is None else 0.0
-            if dual_label is not None:
-                ql = dual_label.to(dev, torch.int32).contiguous()
-                floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
-                if lean or (DUAL_LOWP and self.emb8 is not None and self.emb8.dtype == torch.int8
-                            and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS
-                            and self._dual_lowp_ok()):
-                    # the int8 dual scan: same lists (error cut + bf16 re-score)
-                    from ..ops.search import flat_topk_dual_i8
-                    q8, qs, margin, margin_rig = self._i8_query(q16, 1.0)
-                    if self._lowp_exact(True):  # consolidation's decisions: the worst-case bound by default
-                        margin = margin_rig
-                    else:
-                        margin_rig = margin
-                    if lean_w:
-                        margin, margin_rig = (margin + lean_w).contiguous(), (margin_rig + lean_w).contiguous()
-                    st = [] if (DUAL_LOWP_AUTO and not lean) else None
-                    (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
-                                                         row_label=lab.contiguous(), q_label=ql, bias=bias,
-                                                         margin=margin, margin_rig=margin_rig, floor=floor,
-                                                         stats=st)
-                    if st:
-                        self._dual_stats = st
-                else:
-                    (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=lab.contiguous(), q_label=ql,
-                                                      bias=bias, floor=floor)
-                return self._rerank_cos(Qn, ra, k), self._rerank_cos(Qn, rb, k)
             if lean:
                 from ..ops.search import flat_topk_i8
                 q8, qs, margin, margin_rig = self._i8_query(q16, 1.0)
@@ -2051,6 +2024,162 @@ class TenantGraph:
             ql = dual_label.to(dev, torch.int32)
             return (self._exact_cos(Qn, mask, k), self._exact_cos(Qn, mask, k, row_label=lab, q_label=ql))
         return self._exact_cos(Qn, mask, k)
+
+    def _dual_cands(self, Qn: torch.Tensor, mask: torch.Tensor, dual_label: torch.Tensor,
+                    min_score: Optional[float], keep=None):
+        """The candidate scan of the dual :meth:`cos_topk` (kernel path):
+        CAND_SLOTS rows per query for list A (every row in ``mask``) and list
+        B (rows of the query's shard), holding each list's exact top-k (and
+        every entry >= ``min_score``) for the exact float64 re-rank.
+        ``keep``: a list that receives the tensors the scan reads (a caller
+        running it on a side stream protects them from reuse)."""
+        dev = self.device
+        n = self.n
+        M = Qn.shape[0]
+        lab = self.shard[:n]
+        lean = self.lean
+        bias = torch.where(mask, 0.0, NEG_INF).to(torch.float32).contiguous()
+        q16 = self._q16(Qn)
+        X = self._scan_rows(n, Qn)
+        # lean: the int8 scans' re-score reads fp32 rows with fp32 queries
+        # while their threshold sample and margin are bf16-based, so every
+        # int8 margin below also covers |<q16, x16> - <q, x>| <= 2^-8 |q| |x|
+        # (both operands rounded to bf16; unit queries) -- as _i8_candidates
+        lean_w = 2.0 ** -8 * (1.0 + self.max_norm_dev) if self.emb16 is None else 0.0
+        ql = dual_label.to(dev, torch.int32).contiguous()
+        floor = None if min_score is None else float(min_score) - COS_FLOOR_SLACK
+        labc = lab.contiguous()
+        if keep is not None:
+            keep += [bias, q16, X, ql, labc, self.emb32, self.sqn]
+        if lean or (DUAL_LOWP and self.emb8 is not None and self.emb8.dtype == torch.int8
+                    and self.unit_rows() and M >= LOWP_MIN_Q and n >= LOWP_MIN_ROWS
+                    and self._dual_lowp_ok()):
+            # the int8 dual scan: same lists (error cut + bf16 re-score)
+            from ..ops.search import flat_topk_dual_i8
+            q8, qs, margin, margin_rig = self._i8_query(q16, 1.0)
+            if self._lowp_exact(True):  # consolidation's decisions: the worst-case bound by default
+                margin = margin_rig
+            else:
+                margin_rig = margin
+            if lean_w:
+                margin, margin_rig = (margin + lean_w).contiguous(), (margin_rig + lean_w).contiguous()
+            st = [] if (DUAL_LOWP_AUTO and not lean) else None
+            if keep is not None:
+                keep += [self.emb8, self.rs8, q8, qs, margin, margin_rig]
+            (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
+                                                 row_label=labc, q_label=ql, bias=bias,
+                                                 margin=margin, margin_rig=margin_rig, floor=floor,
+                                                 stats=st)
+            if st:
+                self._dual_stats = st
+        else:
+            from ..ops.search import flat_topk_dual
+            (_, ra), (_, rb) = flat_topk_dual(X, q16, CAND_SLOTS, row_label=labc, q_label=ql,
+                                              bias=bias, floor=floor)
+        return ra, rb
+
+    # ------------------------------------------------------------------ prefetched candidate scans
+    def dual_prefetch_ok(self, M: int, k: int) -> bool:
+        """Whether :meth:`cos_topk_prefetch` applies (the dual kernel path)."""
+        return (self.on_gpu and self.n > 0 and M > 0 and self.dim is not None and k <= CAND_SLOTS
+                and not (self.lean and not self.unit_rows()) and (self._use_kernel(M) or self.lean))
+
+    def cos_topk_prefetch(self, Q: torch.Tensor, mask: torch.Tensor, dual_label: torch.Tensor,
+                          min_score: Optional[float], stream) -> Dict:
+        """The candidate scan of a dual :meth:`cos_topk` launched on
+        ``stream`` against the rows as they are now; :meth:`cos_topk_finish`
+        completes it after the graph changed by row INSERTS (rows >= the
+        current n) and rows leaving ``mask`` only -- one consolidation batch.
+        The caller reserves the rows the batch inserts first (no column
+        reallocation under the running scan)."""
+        from ..ops import search as S
+        dev = self.device
+        cur = torch.cuda.current_stream(dev)
+        Qd = Q.to(dev, torch.float64)
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        stream.wait_stream(cur)
+        keep: List[torch.Tensor] = [Qn, mask]
+        with torch.cuda.stream(stream), S.grid_cap(S.PREFETCH_GRID_FRAC):
+            ra, rb = self._dual_cands(Qn, mask, dual_label, min_score, keep=keep)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        for t in keep + [ra, rb]:
+            if t is not None and t.is_cuda:
+                t.record_stream(cur)
+                t.record_stream(stream)
+        return {"n": self.n, "ra": ra, "rb": rb, "ev": ev, "Qn": Qn, "Q": Q, "ql": dual_label.to(dev, torch.int32),
+                "min_score": min_score, "keep": keep}
+
+    def cos_topk_finish(self, h: Dict, k: int, mask: torch.Tensor):
+        """(list A, list B) of a prefetched dual scan against the graph NOW
+        (``mask``: the rows allowed now), exactly :meth:`cos_topk`'s lists
+        for every entry the caller acts on (>= its min_score): a query whose
+        candidates hold a row that left the mask is recomputed by a fresh
+        scan; for the others the candidates still hold the exact top-k of
+        the remaining rows, and the rows inserted since join them through
+        the same float64 re-rank kernel (64-row chunks), merged by (score
+        desc, row asc)."""
+        from ..utils.tracing import tracer
+        dev = self.device
+        if tracer.enabled:  # how long the host would wait for the prefetched scan here
+            with tracer.stage("cb_prefetch_wait", "cpu"):
+                h["ev"].synchronize()
+        torch.cuda.current_stream(dev).wait_event(h["ev"])
+        n0, n = h["n"], self.n
+        Qn, ra, rb, ql = h["Qn"], h["ra"], h["rb"], h["ql"]
+        M = Qn.shape[0]
+        parts = [[self._rerank_cos(Qn, ra, k)], [self._rerank_cos(Qn, rb, k)]]
+        if n > n0:
+            new = torch.nonzero(mask[n0:n]).flatten() + n0
+            nn_ = new.numel()
+            ca_all = new[None, :].expand(M, nn_)
+            cb_all = torch.where(self.shard[:n][new][None, :] == ql[:, None], ca_all, torch.full_like(ca_all, -1))
+            ms_ = h["min_score"]
+            if ms_ is not None and nn_:
+                # only rows that can reach min_score (fp32 cosine with slack;
+                # the caller acts on entries >= min_score only) go to the exact
+                # re-rank, compacted to the front of each query's row
+                Xn = self.emb32[new, : self.dim].float()
+                nrm = self.sqn[new].float().sqrt()
+                S32 = (Qn.float() @ Xn.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]
+                near = S32 >= float(ms_) - 1e-3
+                ca_all = torch.where(near, ca_all, torch.full_like(ca_all, -1))
+                cb_all = torch.where(near, cb_all, torch.full_like(cb_all, -1))
+                width = int(near.sum(1).max())  # one host read
+                o = torch.argsort((ca_all < 0).to(torch.uint8), dim=1, stable=True)[:, : max(width, 1)]
+                ca_all = torch.gather(ca_all, 1, o)
+                o = torch.argsort((cb_all < 0).to(torch.uint8), dim=1, stable=True)[:, : max(width, 1)]
+                cb_all = torch.gather(cb_all, 1, o)
+            w = ca_all.shape[1]
+            for a in range(0, w, 64):  # the re-rank kernel takes 64 candidates per query
+                for li, cc in ((0, ca_all), (1, cb_all)):
+                    blk = torch.full((M, 64), -1, dtype=torch.long, device=dev)
+                    blk[:, : min(64, w - a)] = cc[:, a:a + 64]
+                    parts[li].append(self._rerank_cos(Qn, blk, k))
+        outs = []
+        for pl in parts:  # one merge by (score desc, row asc), as _rerank_cos orders
+            if len(pl) == 1:
+                outs.append(list(pl[0]))
+                continue
+            s_ = torch.cat([p[0] for p in pl], 1)
+            r_ = torch.cat([p[1] for p in pl], 1)
+            key = torch.where(r_ >= 0, r_, torch.full_like(r_, 1 << 62))
+            o = torch.argsort(key, dim=1, stable=True)
+            s_, r_ = torch.gather(s_, 1, o), torch.gather(r_, 1, o)
+            o = torch.sort(s_, dim=1, descending=True, stable=True).indices[:, :k]
+            outs.append(list(self._pad_k(torch.gather(s_, 1, o), torch.gather(r_, 1, o), k)))
+        # queries whose candidates lost a row: a fresh scan of the graph now
+        gone_a = (ra >= 0) & ~mask[ra.clamp(0, n - 1)]
+        gone_b = (rb >= 0) & ~mask[rb.clamp(0, n - 1)]
+        aff = torch.nonzero(gone_a.any(1) | gone_b.any(1)).flatten()
+        if aff.numel():
+            with tracer.stage("cb_prefetch_affected", dev):
+                (sa, ia), (sb, ib) = self._cos_topk(h["Q"][aff], k, mask, ql[aff], h["min_score"])
+            outs[0][0][aff], outs[0][1][aff] = sa, ia
+            outs[1][0][aff], outs[1][1][aff] = sb, ib
+        h.clear()
+        return (outs[0][0], outs[0][1]), (outs[1][0], outs[1][1])
 
     _dual_stats = None  # (ovf, cnt) x 2 + cap of the last int8 dual scan (auto mode)
     _dual_bf16 = 0  # calls left on the bf16 dual scan (auto mode back-off)

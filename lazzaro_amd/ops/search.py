@@ -361,6 +361,30 @@ def _flat_topk_cand(X, Q, k, kslot, bias, row_label, q_label, alpha, idx_offset)
 _lib.register("lzk_flat_cand_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F,
                                            _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P])
 _lib.register("lzk_cand_grid_f8", _lib.I, [_lib.I, _lib.I])
+_lib.register("lzk_set_cu_budget", None, [_lib.I])
+
+# A consolidation batch's candidate scan prefetched under the previous batch's
+# apply (TenantGraph.cos_topk_prefetch) runs its persistent blocks on this
+# fraction of the CUs: the apply's small kernels need free CUs to make progress
+# while the scan (whose waves fill a CU's registers) runs.
+PREFETCH_GRID_FRAC = 0.875
+
+
+class grid_cap:
+    """Context: persistent scans launched inside use at most ``frac`` of the
+    device's CUs (search256.hip g_n_cu, read at launch; restored on exit)."""
+
+    def __init__(self, frac: float):
+        self.frac = float(frac)
+
+    def __enter__(self):
+        n = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        _lib.lib().lzk_set_cu_budget(max(8, int(n * self.frac)))
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().lzk_set_cu_budget(0)
+        return False
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
                                            _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.I, _lib.I, _lib.P,
                                            _lib.P])

@@ -820,3 +820,92 @@ def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, pru
     assert np.array_equal(a[4], b[4])
     for k in a[5]:
         assert np.array_equal(a[5][k], b[5][k]), k
+
+
+def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch):
+    """``consolidate_stream``: batch i+1's int8 dual candidate scan runs on a
+    side stream under batch i's apply and is completed against the graph
+    batch i left (TenantGraph.cos_topk_finish). Three batches on a 1.2M-row
+    tenant -- with facts that duplicate rows batch 1 evicts (their prefetched
+    candidates are re-scanned) and facts that duplicate batch 1's own new
+    facts (rows that arrived after the prefetch: re-ranked in) -- end in the
+    state of three ``consolidate_batch`` calls: counts, nodes, saliences,
+    access counts, edges."""
+    from lazzaro_amd.engine import tenant_graph as TG
+    N, D, B, F = 1_200_000, 384, 32, 6
+    X, lab = _clustered(N, D, 256, 23, noise=1.6)
+    sal0 = torch.rand(N, generator=torch.Generator().manual_seed(2))
+    low = torch.argsort(sal0)[:64]  # the rows the first batch's eviction takes
+    gen = torch.Generator().manual_seed(9)
+    batches = []
+    prev = []
+    for b in range(3):
+        facts, vecs = [], []
+        for c in range(B):
+            conv = []
+            for f in range(F):
+                kind = (c * F + f + b) % 4
+                if kind == 0:
+                    base = X[int(torch.randint(0, N, (1,), generator=gen))]
+                elif kind == 1 and b > 0:  # a row the previous batch may have evicted
+                    base = X[int(low[int(torch.randint(0, low.numel(), (1,), generator=gen))])]
+                elif kind == 2 and prev:  # a fact the previous batch inserted
+                    base = prev[int(torch.randint(0, len(prev), (1,), generator=gen))]
+                else:
+                    base = torch.randn(D, generator=gen)
+                v = base + 0.01 * torch.randn(D, generator=gen) / D ** 0.5
+                vecs.append(v / v.norm())
+                conv.append({"content": f"fact {b}.{c}.{f}", "salience": 0.5 + 0.01 * f,
+                             "topic": f"topic{(c + f) % 8}"})
+            facts.append(conv)
+        V = torch.stack(vecs)
+        prev = list(V)
+        batches.append((facts, V.to(DEV), 1.8e9 + 3600.0 * b))
+    calls = {"finish": 0, "aff": 0}
+    real_finish = TG.TenantGraph.cos_topk_finish
+    real_cos = TG.TenantGraph._cos_topk
+
+    def finish(self, h, k, mask):
+        calls["finish"] += 1
+
+        def cos(self_, *a, **kw):
+            calls["aff"] += 1
+            return real_cos(self_, *a, **kw)
+        monkeypatch.setattr(TG.TenantGraph, "_cos_topk", cos)
+        try:
+            return real_finish(self, h, k, mask)
+        finally:
+            monkeypatch.setattr(TG.TenantGraph, "_cos_topk", real_cos)
+    monkeypatch.setattr(TG.TenantGraph, "cos_topk_finish", finish)
+    out = {}
+    for mode in ("calls", "stream"):
+        monkeypatch.setattr(time, "time", _Clock())
+        ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
+                          db_dir=str(tmp_path / mode), device=DEV, load_from_disk=False, max_buffer_size=N - 100,
+                          super_node_threshold=10 ** 9)
+        g = ms.graph
+        shards = [g.shard_id(f"topic{c}") for c in range(8)]
+        g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"m {i}" for i in range(N)], X.to(DEV),
+                    shard=np.asarray([shards[int(c) % 8] for c in lab], dtype=np.int32), sal=sal0, stored=True)
+        ms.node_counter = N
+        if mode == "calls":
+            stats = [ms.consolidate_batch(f, embeddings=V, now=t) for f, V, t in batches]
+        else:
+            stats = list(ms.consolidate_stream(batches))
+        n = g.n
+        live = (g.kind[:n] == NODE).cpu().numpy()
+        e = {k: v.cpu() for k, v in g.e.items()}
+        order = np.lexsort((e["dst"].numpy(), e["src"].numpy()))
+        out[mode] = (stats, np.nonzero(live)[0], g.sal[:n].cpu().numpy()[live], g.acc[:n].cpu().numpy()[live],
+                     {k: v.numpy()[order] for k, v in e.items() if k in ("src", "dst", "w", "meta")},
+                     [g.ids[r] for r in np.nonzero(live)[0][-50:]])
+        ms.close()
+    a, b = out["calls"], out["stream"]
+    assert calls["finish"] == 2  # batches 2 and 3 came from prefetched scans
+    assert a[0] == b[0]
+    assert sum(s["dup"] for s in a[0]) > 0 and sum(s["evicted"] for s in a[0]) > 0
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+    for k in a[4]:
+        assert np.array_equal(a[4][k], b[4][k]), k
+    assert a[5] == b[5]
+    assert calls["aff"] >= 1, calls  # some prefetched candidates lost a row to the previous batch's eviction
