@@ -1134,9 +1134,11 @@ class ConsolidationMixin:
         if rows.size:
             with g.on_stream():
                 rt = torch.as_tensor(rows, dtype=torch.long).to(g.device)
-                cols = (g.sal[rt].cpu().numpy().astype(np.float32), g.acc[rt].cpu().numpy().astype(np.int64),
-                        g.last[rt].cpu().numpy(), g.shard[rt].cpu().numpy().astype(np.int64),
-                        (g.sup[rt] != 0).cpu().numpy(), g.sqn[rt].double().cpu().numpy())
+                # one float64 block, one device read (every column is exact in float64)
+                a = torch.stack([g.sal[rt].double(), g.acc[rt].double(), g.last[rt], g.shard[rt].double(),
+                                 (g.sup[rt] != 0).double(), g.sqn[rt].double()]).cpu().numpy()
+                cols = (a[0].astype(np.float32), a[1].astype(np.int64), a[2].copy(), a[3].astype(np.int64),
+                        a[4] != 0, a[5].copy())
         else:
             cols = (np.zeros(0, np.float32), np.zeros(0, np.int64), np.zeros(0), np.zeros(0, np.int64),
                     np.zeros(0, bool), np.zeros(0))
