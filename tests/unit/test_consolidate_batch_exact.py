@@ -211,3 +211,27 @@ def test_batch_commit_per_conversation(tmp_path, monkeypatch):
             assert a[k] == b[k], (c, k)
     with pytest.raises(ValueError):
         bat.consolidate_batch(convs[:1], commit="sometimes")
+
+
+def test_consolidate_stream_equals_sequential_cpu(tmp_path, monkeypatch):
+    """``consolidate_stream`` over three batches is the sequential run (on the
+    CPU the next batch's scan is not prefetched: the stream plumbing only;
+    the prefetched GPU path is tests/kernels/test_tenant_engine_gpu.py::
+    test_consolidate_stream_matches_batches_gpu)."""
+    import time as _time
+    monkeypatch.setattr(_time, "time", lambda: 1_900_000_000.0)
+    B = 24
+    convs = conversations(B)
+    seq = _system(tmp_path / "seq", "cpu")
+    for facts in convs:
+        seq.start_conversation()
+        seq.add_to_short_term("FACTS:" + json.dumps(facts), "episodic", 0.7)
+        seq.end_conversation()
+    st = _system(tmp_path / "st", "cpu")
+    embs = [None] * 3  # the embedder runs per batch
+    parts = [convs[:8], convs[8:16], convs[16:]]
+    stats = list(st.consolidate_stream((p, e, 1_900_000_000.0) for p, e in zip(parts, embs)))
+    assert len(stats) == 3 and sum(s["conversations"] for s in stats) == B
+    a, b = _state(seq), _state(st)
+    for k in a:
+        assert a[k] == b[k], k
