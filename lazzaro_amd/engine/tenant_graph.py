@@ -2101,9 +2101,12 @@ class TenantGraph:
         stream.wait_stream(cur)
         keep: List[torch.Tensor] = [Qn, mask]
         with torch.cuda.stream(stream), S.grid_cap(S.PREFETCH_GRID_FRAC):
+            st0 = self._dual_stats
             ra, rb = self._dual_cands(Qn, mask, dual_label, min_score, keep=keep)
             ev = torch.cuda.Event()
             ev.record(stream)
+            if self._dual_stats is not None and self._dual_stats is not st0:
+                self._dual_stats_ev = ev
         for t in keep + [ra, rb]:
             if t is not None and t.is_cuda:
                 t.record_stream(cur)
@@ -2182,6 +2185,7 @@ class TenantGraph:
         return (outs[0][0], outs[0][1]), (outs[1][0], outs[1][1])
 
     _dual_stats = None  # (ovf, cnt) x 2 + cap of the last int8 dual scan (auto mode)
+    _dual_stats_ev = None  # the side-stream event after a prefetched scan that wrote _dual_stats
     _dual_bf16 = 0  # calls left on the bf16 dual scan (auto mode back-off)
 
     def _dual_lowp_ok(self) -> bool:
@@ -2193,6 +2197,9 @@ class TenantGraph:
         if self._dual_stats is not None:
             (oa, ca), (ob, cb), cap = self._dual_stats
             self._dual_stats = None
+            ev, self._dual_stats_ev = self._dual_stats_ev, None
+            if ev is not None:  # written by a prefetched scan on its side stream
+                torch.cuda.current_stream(self.device).wait_event(ev)
             with self.on_stream():
                 m = torch.stack([((oa != 0) | (ob != 0)).float().mean(),
                                  ((ca & 0x3FFFFFFF).clamp_max(cap).float().mean()
