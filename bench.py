@@ -201,6 +201,8 @@ def main():
     ap.add_argument("--consolidate-steps", type=int, default=10,
                     help="second half of the metric: timed consolidation steps on a --rows-node buffer (0 = skip)")
     ap.add_argument("--consolidate-convs", type=int, default=128, help="conversations per GPU per step")
+    ap.add_argument("--consolidate-calls", dest="consolidate_stream", action="store_false",
+                    help="one consolidate_batch call per step instead of consolidate_stream (A/B)")
     ap.add_argument("--no-persistent-graph", dest="persistent_graph", action="store_false",
                     help="skip the consolidation variant whose seeded edges are never pruned")
     ap.add_argument("--routed-steps", type=int, default=-1, help="timed routed-search steps (-1: --steps, 0: skip)")
@@ -514,7 +516,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
         consolidate = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
-                                      dim=a.dim)
+                                      dim=a.dim, stream=a.consolidate_stream)
         if a.persistent_graph:
             # same pipeline, MemorySystem(prune_threshold=0): the 2 x rows seeded
             # edges are never pruned (decay still scales every edge each
@@ -523,7 +525,7 @@ def main():
             if dev.type == "cuda":
                 torch.cuda.empty_cache()
             persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
-                                         dim=a.dim, prune_threshold=0.0)
+                                         dim=a.dim, prune_threshold=0.0, stream=a.consolidate_stream)
     sharded = None
     if a.sharded_steps > 0:
         # config 4 as ONE buffer row-sharded over the ranks: collectives in
@@ -586,6 +588,8 @@ def main():
                                                           "facts_per_conv", "per_step_rank0", "nodes_rank0",
                                                           "edges_rank0", "edges_rank0_at_start", "prune_threshold",
                                                           "path", "hierarchical_clustering", "persistence")}
+        if consolidate.get("stages_ms"):  # LZK_TRACE=1
+            res["consolidate"]["stages_ms"] = consolidate["stages_ms"]
         res["consolidate"]["edge_lifetime_note"] = (
             "reference semantics (prune_threshold 0.5, decay 1%/conversation): a link (w <= 0.8) is pruned within "
             "47 conversations, so the seeded edges are gone after the first step and the steady state holds only "

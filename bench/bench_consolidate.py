@@ -224,9 +224,12 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
     el = float(t.item())
     g = ms.graph
     from lazzaro_amd.utils.tracing import tracer
+    stages = None
     if tracer.enabled:  # LZK_TRACE=1: per-stage device time (hipEvents), warmup included
         import json as _json
-        print(_json.dumps({"stages_ms": tracer.summary()}), flush=True)
+        stages = tracer.summary()
+        print(_json.dumps({"stages_ms": stages}), flush=True)
+        tracer.reset()
     out = {"turns_per_s": round(convs * comm.world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
            "nodes_per_rank": nodes, "convs_per_rank_step": convs, "facts_per_conv": facts,
            "prune_threshold": prune_threshold, "edges_rank0_at_start": edges_start,
@@ -240,6 +243,7 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
            "hierarchical_clustering": {"mode": "kmeans", "every_steps": cluster_every, "fine": n_fine, "top": n_top,
                                        "iters_per_pass": cluster_iters, "seed_pass_ms": round(seed_ms, 1),
                                        "farthest_first_ms": ff.get("ms")},
+           "stages_ms": stages,
            "persistence": "incremental columnar commit per step (db on local disk)" + (
                ", write-behind (persist_async: commits on a writer thread, flushed inside the timed region)"
                if persist_async else "")}

@@ -247,10 +247,13 @@ _PF_STREAMS: Dict = {}
 
 
 def _prefetch_stream(dev):
-    """One side stream per device for prefetched candidate scans."""
+    """One side stream per device for prefetched candidate scans, at high
+    priority: HIP maps streams of one priority round-robin onto a few
+    hardware queues, and a prefetched scan that shared the graph stream's
+    queue would run in line with the apply it is meant to overlap."""
     st = _PF_STREAMS.get(dev)
     if st is None:
-        st = _PF_STREAMS[dev] = torch.cuda.Stream(dev)
+        st = _PF_STREAMS[dev] = torch.cuda.Stream(dev, priority=-1)
     return st
 
 

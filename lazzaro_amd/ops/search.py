@@ -367,7 +367,7 @@ _lib.register("lzk_set_cu_budget", None, [_lib.I])
 # apply (TenantGraph.cos_topk_prefetch) runs its persistent blocks on this
 # fraction of the CUs: the apply's small kernels need free CUs to make progress
 # while the scan (whose waves fill a CU's registers) runs.
-PREFETCH_GRID_FRAC = 0.875
+PREFETCH_GRID_FRAC = 0.75
 
 
 class grid_cap:
