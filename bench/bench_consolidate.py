@@ -254,7 +254,8 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
 def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: int, warmup: int, encoder=None,
                 dim: int = 768, dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096,
                 n_top: int = 64, cluster_iters: int = 2, init_edges: int = None, db_dir: str = None,
-                clustered: bool = False, topics_per_rank: int = 32, cadence: str = "conversation"):
+                clustered: bool = False, topics_per_rank: int = 32, cadence: str = "conversation",
+                stream: bool = False):
     """BASELINE config 4 as ONE tenant: a ``nodes_per_rank * world``-node
     buffer row-sharded over the ranks (``ShardedMemorySystem``); every step
     each rank brings ``convs`` conversations, the whole batch is consolidated
@@ -272,7 +273,11 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     (``ShardedMemorySystem.last_scan_work``, max over ranks).
 
     ``cadence``: "conversation" (default, the reference's per-conversation
-    eviction / run_consolidation, planned once per batch) or "batch"."""
+    eviction / run_consolidation, planned once per batch) or "batch".
+    ``stream``: ``ShardedMemorySystem.consolidate_stream`` instead of
+    per-batch calls -- off by default: on the clustered buffer a batch's
+    victims sit in the next batch's candidate lists, whose facts are then
+    re-scanned (profiles/r5/sharded_stream/)."""
     from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
     from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
 
@@ -321,17 +326,25 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     rng = random.Random(seed + comm.rank)
     batches = iter([synth_facts(convs, facts, rng) for _ in range(warmup + steps)])
 
-    def step():
+    def make_batch():
         conversations = next(batches)
         V = synth_vectors(sm.local, convs * facts, dim, dup_rate, gen)
         if encoder is not None:
             from lazzaro_amd.utils.tracing import tracer as _tr
             with _tr.stage("fact_embed", dev):
                 sm.local._batch_embed_any([f["content"] for c in conversations for f in c])
-        return sm.consolidate_batch(conversations, embeddings=V, cadence=cadence)
+        return conversations, V
 
-    for _ in range(warmup):
-        step()
+    def run_steps(k):
+        if stream:
+            yield from sm.consolidate_stream((make_batch() for _ in range(k)), cadence=cadence)
+        else:
+            for _ in range(k):
+                conversations, V = make_batch()
+                yield sm.consolidate_batch(conversations, embeddings=V, cadence=cadence)
+
+    for _ in run_steps(warmup):
+        pass
     _sync(dev)
     comm.barrier()
     prof = None
@@ -352,8 +365,8 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     t0 = time.perf_counter()
     agg = {}
     work0 = sm.scan_work
-    for _ in range(steps):
-        for k, v in step().items():
+    for st in run_steps(steps):
+        for k, v in st.items():
             agg[k] = agg.get(k, 0) + v
     _sync(dev)
     comm.barrier()
@@ -383,8 +396,8 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
            "scan_facts_x_rows_per_rank_step": int(wk.item()),
            "scan_facts_x_rows_unpruned_per_rank_step": int(world * convs * facts * nodes_per_rank),
            "data": "clustered topics, cluster placement" if clustered else "uniform random rows",
-           "path": "ShardedMemorySystem.consolidate_batch (one tenant row-sharded over the ranks), cadence=%s"
-                   % cadence,
+           "path": ("ShardedMemorySystem.%s (one tenant row-sharded over the ranks), cadence=%s"
+                    % ("consolidate_stream" if stream else "consolidate_batch", cadence)),
            "hierarchical_clustering": {"mode": "distributed kmeans", "every_steps": cluster_every, "fine": n_fine,
                                        "top": n_top, "iters_per_pass": cluster_iters,
                                        "seed_pass_ms": round(seed_ms, 1), "farthest_first_ms": ff.get("ms")},
@@ -437,7 +450,7 @@ if __name__ == "__main__":
     fn = run_sharded if a.sharded else run
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
-             **({"clustered": a.clustered, "cadence": a.cadence} if a.sharded else {"prune_threshold": a.prune_threshold,
+             **({"clustered": a.clustered, "cadence": a.cadence, "stream": a.stream} if a.sharded else {"prune_threshold": a.prune_threshold,
                                                               "persist_async": a.persist_async, "stream": a.stream}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)

@@ -2131,47 +2131,12 @@ class TenantGraph:
         torch.cuda.current_stream(dev).wait_event(h["ev"])
         n0, n = h["n"], self.n
         Qn, ra, rb, ql = h["Qn"], h["ra"], h["rb"], h["ql"]
-        M = Qn.shape[0]
         parts = [[self._rerank_cos(Qn, ra, k)], [self._rerank_cos(Qn, rb, k)]]
         if n > n0:
-            new = torch.nonzero(mask[n0:n]).flatten() + n0
-            nn_ = new.numel()
-            ca_all = new[None, :].expand(M, nn_)
-            cb_all = torch.where(self.shard[:n][new][None, :] == ql[:, None], ca_all, torch.full_like(ca_all, -1))
-            ms_ = h["min_score"]
-            if ms_ is not None and nn_:
-                # only rows that can reach min_score (fp32 cosine with slack;
-                # the caller acts on entries >= min_score only) go to the exact
-                # re-rank, compacted to the front of each query's row
-                Xn = self.emb32[new, : self.dim].float()
-                nrm = self.sqn[new].float().sqrt()
-                S32 = (Qn.float() @ Xn.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]
-                near = S32 >= float(ms_) - 1e-3
-                ca_all = torch.where(near, ca_all, torch.full_like(ca_all, -1))
-                cb_all = torch.where(near, cb_all, torch.full_like(cb_all, -1))
-                width = int(near.sum(1).max())  # one host read
-                o = torch.argsort((ca_all < 0).to(torch.uint8), dim=1, stable=True)[:, : max(width, 1)]
-                ca_all = torch.gather(ca_all, 1, o)
-                o = torch.argsort((cb_all < 0).to(torch.uint8), dim=1, stable=True)[:, : max(width, 1)]
-                cb_all = torch.gather(cb_all, 1, o)
-            w = ca_all.shape[1]
-            for a in range(0, w, 64):  # the re-rank kernel takes 64 candidates per query
-                for li, cc in ((0, ca_all), (1, cb_all)):
-                    blk = torch.full((M, 64), -1, dtype=torch.long, device=dev)
-                    blk[:, : min(64, w - a)] = cc[:, a:a + 64]
-                    parts[li].append(self._rerank_cos(Qn, blk, k))
-        outs = []
-        for pl in parts:  # one merge by (score desc, row asc), as _rerank_cos orders
-            if len(pl) == 1:
-                outs.append(list(pl[0]))
-                continue
-            s_ = torch.cat([p[0] for p in pl], 1)
-            r_ = torch.cat([p[1] for p in pl], 1)
-            key = torch.where(r_ >= 0, r_, torch.full_like(r_, 1 << 62))
-            o = torch.argsort(key, dim=1, stable=True)
-            s_, r_ = torch.gather(s_, 1, o), torch.gather(r_, 1, o)
-            o = torch.sort(s_, dim=1, descending=True, stable=True).indices[:, :k]
-            outs.append(list(self._pad_k(torch.gather(s_, 1, o), torch.gather(r_, 1, o), k)))
+            pa, pb = self._new_rows_parts(Qn, ql, mask, n0, k, h["min_score"])
+            parts[0] += pa
+            parts[1] += pb
+        outs = [self._merge_parts(pl, k) for pl in parts]
         # queries whose candidates lost a row: a fresh scan of the graph now
         gone_a = (ra >= 0) & ~mask[ra.clamp(0, n - 1)]
         gone_b = (rb >= 0) & ~mask[rb.clamp(0, n - 1)]
@@ -2183,6 +2148,72 @@ class TenantGraph:
             outs[1][0][aff], outs[1][1][aff] = sb, ib
         h.clear()
         return (outs[0][0], outs[0][1]), (outs[1][0], outs[1][1])
+
+    def _new_rows_parts(self, Qn, ql, mask, n0: int, k: int, min_score):
+        """Per-query exact top-k lists (list A, list B as parts to merge) over
+        the rows >= ``n0`` allowed by ``mask`` only: the float64 re-rank kernel
+        on 64-row blocks, rows that cannot reach ``min_score`` (fp32 cosine
+        with slack) left out first."""
+        dev = self.device
+        n = self.n
+        M = Qn.shape[0]
+        new = torch.nonzero(mask[n0:n]).flatten() + n0
+        nn_ = new.numel()
+        ca_all = new[None, :].expand(M, nn_)
+        cb_all = torch.where(self.shard[:n][new][None, :] == ql[:, None], ca_all, torch.full_like(ca_all, -1))
+        if min_score is not None and nn_:
+            # only rows that can reach min_score (the caller acts on entries
+            # >= min_score only) go to the exact re-rank, compacted to the front
+            Xn = self.emb32[new, : self.dim].float()
+            nrm = self.sqn[new].float().sqrt()
+            S32 = (Qn.float() @ Xn.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]
+            near = S32 >= float(min_score) - 1e-3
+            ca_all = torch.where(near, ca_all, torch.full_like(ca_all, -1))
+            cb_all = torch.where(near, cb_all, torch.full_like(cb_all, -1))
+            width = int(near.sum(1).max())  # one host read
+            o = torch.argsort((ca_all < 0).to(torch.uint8), dim=1, stable=True)[:, : max(width, 1)]
+            ca_all = torch.gather(ca_all, 1, o)
+            o = torch.argsort((cb_all < 0).to(torch.uint8), dim=1, stable=True)[:, : max(width, 1)]
+            cb_all = torch.gather(cb_all, 1, o)
+        pa, pb = [], []
+        w = ca_all.shape[1]
+        for a in range(0, w, 64):  # the re-rank kernel takes 64 candidates per query
+            for out, cc in ((pa, ca_all), (pb, cb_all)):
+                blk = torch.full((M, 64), -1, dtype=torch.long, device=dev)
+                blk[:, : min(64, w - a)] = cc[:, a:a + 64]
+                out.append(self._rerank_cos(Qn, blk, k))
+        return pa, pb
+
+    def _merge_parts(self, parts, k: int):
+        """Top-k of several (score, row) lists by (score desc, row asc), as
+        _rerank_cos orders."""
+        if len(parts) == 1:
+            return list(parts[0])
+        s_ = torch.cat([p[0] for p in parts], 1)
+        r_ = torch.cat([p[1] for p in parts], 1)
+        key = torch.where(r_ >= 0, r_, torch.full_like(r_, 1 << 62))
+        o = torch.argsort(key, dim=1, stable=True)
+        s_, r_ = torch.gather(s_, 1, o), torch.gather(r_, 1, o)
+        o = torch.sort(s_, dim=1, descending=True, stable=True).indices[:, :k]
+        return list(self._pad_k(torch.gather(s_, 1, o), torch.gather(r_, 1, o), k))
+
+    def cos_topk_new_rows(self, Q: torch.Tensor, k: int, mask: torch.Tensor, n0: int, dual_label: torch.Tensor,
+                          min_score: Optional[float]):
+        """The dual :meth:`cos_topk` lists restricted to rows >= ``n0``
+        (entries >= ``min_score`` exact): for queries whose lists over the
+        older rows are known to hold nothing at that score."""
+        dev = self.device
+        Qd = Q.to(dev, torch.float64)
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        ql = dual_label.to(dev, torch.int32)
+        M = Qn.shape[0]
+        e = self._pad_k(torch.zeros((M, 0), dtype=torch.float64, device=dev),
+                        torch.zeros((M, 0), dtype=torch.long, device=dev), k)
+        if self.n <= n0:
+            return (e[0].clone(), e[1].clone()), (e[0].clone(), e[1].clone())
+        pa, pb = self._new_rows_parts(Qn, ql, mask, n0, k, min_score)
+        return tuple(self._merge_parts([e] + pa, k)), tuple(self._merge_parts([e] + pb, k))
 
     _dual_stats = None  # (ovf, cnt) x 2 + cap of the last int8 dual scan (auto mode)
     _dual_stats_ev = None  # the side-stream event after a prefetched scan that wrote _dual_stats

@@ -645,6 +645,7 @@ class ShardedMemorySystem:
         if commit not in ("conversation", "batch"):
             raise ValueError("commit must be 'conversation' or 'batch'")
         self._commit_each = commit == "conversation" and cadence == "conversation"
+        self._batch_src = embeddings  # a prefetched batch is keyed by its embeddings object
         g = self.g
         dev = self.device
         flat, conv, idx = [], [], []
@@ -999,17 +1000,43 @@ class ShardedMemorySystem:
             v = self._gather_rows(v.contiguous()).view(self.world, F, k).permute(1, 0, 2).reshape(F, -1)
         return self._merge_lists(s, v, k)
 
-    def _exact_lists(self, Q: torch.Tensor, code_t: torch.Tensor, K: int):
+    def _exact_lists(self, Q: torch.Tensor, code_t: torch.Tensor, K: int, pf: Optional[Dict] = None):
         """The planner's candidate lists: every fact's global and same-shard
         top-K over every rank's live nodes (the same fused scan + float64
         re-rank per rank, merged by global row). Returns numpy
-        ((gs, gv), (ws, wv)), rows as global row numbers."""
+        ((gs, gv), (ws, wv)), rows as global row numbers. ``pf``: this batch
+        was prefetched (:meth:`_launch_prefetch`) -- the facts the scan took
+        (those that could reach this rank's rows then) complete it against
+        the rows now (TenantGraph.cos_topk_finish); the others could reach
+        none of the older rows and look at the rows added since only."""
         g = self.g
         F = Q.shape[0]
         dev = self.device
         live = g.num_nodes() if g.n else 0
         gs = ws = torch.full((F, K), NEG_INF, dtype=torch.float64, device=dev)
         gv = wv = torch.full((F, K), -1, dtype=torch.long, device=dev)
+        if pf is not None and pf.get("si") is not None and live:
+            si, h, n0 = pf["si"], pf["h"], pf["n0"]
+            n = g.n
+            mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0) & (self.holder[:n] == self.rank)
+            self.last_scan_work = int(si.numel()) * live
+            self.scan_work += self.last_scan_work
+            gs, ws = gs.clone(), ws.clone()
+            gv, wv = gv.clone(), wv.clone()
+            with g.on_stream():
+                if h is not None:
+                    (a, ar), (b, br) = g.cos_topk_finish(h, K, mask)
+                    gs[si], ws[si] = a.double(), b.double()
+                    gv[si], wv[si] = self._vrows(ar), self._vrows(br)
+                rest = torch.ones(F, dtype=torch.bool, device=dev)
+                rest[si] = False
+                ri = torch.nonzero(rest).flatten()
+                if ri.numel() and n > n0:
+                    (a, ar), (b, br) = g.cos_topk_new_rows(Q[ri], K, mask, n0, code_t[ri], LINK_THRESHOLD)
+                    gs[ri], ws[ri] = a.double(), b.double()
+                    gv[ri], wv[ri] = self._vrows(ar), self._vrows(br)
+            (gs, gv), (ws, wv) = self._gather_lists(gs, gv, K), self._gather_lists(ws, wv, K)
+            return ((gs.cpu().numpy(), gv.cpu().numpy()), (ws.cpu().numpy(), wv.cpu().numpy()))
         sel = None
         if live:
             Qd = Q.double()
@@ -1237,6 +1264,148 @@ class ShardedMemorySystem:
                 g.dirty[held] = 1
             g._bump()
 
+    def _gather_batch(self, flat, conv, E, B_loc) -> Dict:
+        """Step 1 of :meth:`_consolidate_exact` (collective): the global fact
+        batch in rank-major conversation order -- fact vectors, saliences,
+        conversation indices, shard codes (registered in fact order), the
+        rank that will hold each fact's node and the facts' contents where
+        holders need them."""
+        dev = self.device
+        comm = self.comm
+        with tracer.stage("sc_gather", dev):
+            bl = self._host_ints(B_loc)[:, 0].tolist()
+            B = int(sum(bl))
+            c_off = int(sum(bl[: self.rank]))
+            keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
+            keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self._coll else keys
+            sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
+            ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
+            Qa, fcnt = self._gather_var(E)
+            sal_in, _ = self._gather_var(sal_l)
+            ct, _ = self._gather_var(ct_l)
+        F = int(Qa.shape[0])
+        gb = {"B": B, "F": F}
+        if B == 0:
+            return gb
+        origin = torch.repeat_interleave(torch.arange(self.world, device=dev),
+                                         torch.tensor(fcnt, dtype=torch.long, device=dev)) if F else \
+            torch.zeros(0, dtype=torch.long, device=dev)
+        codes = self._register_shards(keys_all).astype(np.int64)
+        code_t = torch.as_tensor(codes).to(dev)
+        Q = Qa.float()
+        Qd = Q.double()
+        qn = Qd.norm(dim=1, keepdim=True)
+        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
+        if F:
+            origin_conv = origin
+            origin = self._holders(Qn, origin_conv)
+            if origin is not origin_conv:  # holders need the contents of facts from other ranks
+                flat = [f for part in comm.all_gather_object([{"content": f["content"],
+                                                               "type": f.get("type", "semantic")} for f in flat])
+                        for f in part]
+                f_off = 0
+            else:
+                f_off = int(sum(fcnt[: self.rank]))
+        else:
+            f_off = 0
+        gb.update(Q=Q, Qn=Qn, qn=qn, code_t=code_t, codes=codes, origin=origin, flat=flat, f_off=f_off,
+                  sal_in=sal_in, ct=ct)
+        return gb
+
+    _prefetch_next = None
+    _prefetched = None
+    prefetched_batches = 0  # batches whose gather + local scan ran under the previous batch's apply
+
+    def consolidate_stream(self, batches, cadence: str = "conversation", commit: str = "batch"):
+        """Collective :meth:`consolidate_batch` over a stream of batches
+        (every rank passes its own, the same number), yielding each batch's
+        counts -- exactly the per-batch calls' results. As in
+        ``MemorySystem.consolidate_stream``, batch i+1 is gathered and this
+        rank's candidate scan of it launched on a side stream once batch i is
+        planned; the scan runs under batch i's apply and batch i+1 completes
+        it against the rows batch i left. ``batches`` yields
+        ``(conversations, embeddings)`` or ``(conversations, embeddings,
+        now)``."""
+        it = iter(batches)
+        cur = next(it, None)
+        try:
+            while cur is not None:
+                nxt = next(it, None)
+                self._prefetch_next = nxt
+                now = cur[2] if len(cur) > 2 else None
+                yield self.consolidate_batch(cur[0], embeddings=cur[1], now=now, cadence=cadence, commit=commit)
+                cur = nxt
+        finally:
+            self._prefetch_next = None
+            self._prefetched = None
+
+    def _prep_facts(self, conversations, embeddings):
+        """consolidate_batch's local fact preparation: (flat, conv, E)."""
+        dev = self.device
+        flat, conv, idx = [], [], []
+        j = 0
+        for c, fs in enumerate(conversations):
+            for f in fs:
+                if isinstance(f, dict) and f.get("content") and len(f["content"]) >= MIN_FACT_LEN:
+                    flat.append(f)
+                    conv.append(c)
+                    idx.append(j)
+                j += 1
+        m = len(flat)
+        if embeddings is not None and m:
+            E = embeddings if torch.is_tensor(embeddings) else torch.as_tensor(np.asarray(embeddings, np.float32))
+            E = E[torch.as_tensor(idx, dtype=torch.long).to(E.device)] if len(idx) != len(E) else E
+        elif m:
+            with tracer.stage("embed_facts", dev):
+                E = self.local._batch_embed_any([f["content"] for f in flat])
+        else:
+            E = None
+        if m:
+            E, valid = self.local._fact_matrix(E, m)
+            vidx = np.nonzero(valid)[0]
+            flat = [flat[i] for i in vidx]
+            conv = [conv[i] for i in vidx]
+            E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)].to(dev, torch.float32)
+        return flat, conv, E
+
+    def _launch_prefetch(self, pl: Dict) -> None:
+        """After batch i's plan (collective: the same point on every rank):
+        gather batch i+1 and launch this rank's candidate scan of it on a
+        side stream (see :meth:`consolidate_stream`). Not when batch i runs a
+        cluster pass (it moves the cluster homes that decide the holders, and
+        shares the scan workspaces), without embeddings, or off the GPU --
+        conditions every rank evaluates alike."""
+        from ..core.consolidation import _prefetch_stream
+        nxt, self._prefetch_next = self._prefetch_next, None
+        self._prefetched = None
+        g = self.g
+        if nxt is None or not g.on_gpu or g.dim is None or nxt[1] is None \
+                or any(seg["cluster"] for seg in pl["segments"]):
+            return
+        flat, conv, E = self._prep_facts(nxt[0], nxt[1])
+        if E is None:
+            E = torch.zeros((0, g.dim), dtype=torch.float32, device=self.device)
+        bad = int(E.shape[1] != g.dim)
+        if self._sum(bad)[0]:
+            return
+        gb = self._gather_batch(flat, conv, E, len(nxt[0]))
+        pf = {"src": nxt[1], "B_loc": len(nxt[0]), "m": len(flat), "gb": gb, "h": None, "si": None, "n0": g.n}
+        F = gb["F"]
+        K = self.local.BATCH_LIST_K
+        if F and g.n and g.dual_prefetch_ok(F, K):
+            ps = pl["stats"]
+            g.reserve(g.n + int(ps["inserted"]) + len(pl["supers"]) + F + 16)  # ghost rows too: no column moves
+            sel = self._reach_mask(gb["Qn"])
+            si = torch.arange(F, device=self.device) if sel is None else torch.nonzero(sel).flatten()
+            n = g.n
+            pf["si"], pf["n0"] = si, n
+            if si.numel():
+                with g.on_stream():
+                    mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0) & (self.holder[:n] == self.rank)
+                    pf["h"] = g.cos_topk_prefetch(gb["Q"][si], mask, gb["code_t"][si], LINK_THRESHOLD,
+                                                  _prefetch_stream(self.device))
+        self._prefetched = pf
+
     def _consolidate_exact(self, flat, conv, E, B_loc, now, stats) -> None:
         """The reference cadence over the row-sharded buffer: every rank runs
         the SAME native batch planner (core/batch_plan.py) on the global
@@ -1259,47 +1428,24 @@ class ShardedMemorySystem:
         thr = self.prune_threshold if self.auto_prune else None
         K = self.local.BATCH_LIST_K
         # ---- 1. the global fact batch (rank-major conversation order)
-        with tracer.stage("sc_gather", dev):
-            bl = self._host_ints(B_loc)[:, 0].tolist()
-            B = int(sum(bl))
-            c_off = int(sum(bl[: self.rank]))
-            keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
-            keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self._coll else keys
-            sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
-            ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
-            Qa, fcnt = self._gather_var(E)
-            sal_in, _ = self._gather_var(sal_l)
-            ct, _ = self._gather_var(ct_l)
+        pf, self._prefetched = self._prefetched, None
+        ok = pf is not None and pf["src"] is getattr(self, "_batch_src", None) and pf["B_loc"] == B_loc \
+            and pf["m"] == len(flat)
+        if pf is not None and self._sum(0 if ok else 1)[0]:  # every rank uses its prefetch, or none does
+            pf = None
+        gb = pf["gb"] if pf is not None else self._gather_batch(flat, conv, E, B_loc)
+        self.prefetched_batches += pf is not None
+        B, F = gb["B"], gb["F"]
         stats["conversations"] = B
-        F = int(Qa.shape[0])
         stats["facts"] = F
         if B == 0:
             return
-        origin = torch.repeat_interleave(torch.arange(self.world, device=dev),
-                                         torch.tensor(fcnt, dtype=torch.long, device=dev)) if F else \
-            torch.zeros(0, dtype=torch.long, device=dev)
-        codes = self._register_shards(keys_all).astype(np.int64)
-        code_t = torch.as_tensor(codes).to(dev)
-        Q = Qa.float()
-        Qd = Q.double()
-        qn = Qd.norm(dim=1, keepdim=True)
-        Qn = Qd / torch.where(qn > 0, qn, torch.ones_like(qn))
-        if F:
-            origin_conv = origin
-            origin = self._holders(Qn, origin_conv)
-            if origin is not origin_conv:  # holders need the contents of facts from other ranks
-                flat = [f for part in comm.all_gather_object([{"content": f["content"],
-                                                               "type": f.get("type", "semantic")} for f in flat])
-                        for f in part]
-                f_off = 0
-            else:
-                f_off = int(sum(fcnt[: self.rank]))
-        else:
-            f_off = 0
+        Q, Qn, qn, code_t, codes = gb["Q"], gb["Qn"], gb["qn"], gb["code_t"], gb["codes"]
+        origin, flat, f_off, sal_in, ct = gb["origin"], gb["flat"], gb["f_off"], gb["sal_in"], gb["ct"]
         # ---- 2. candidate lists + the fact x fact block (the single process's formulas)
         with tracer.stage("sc_scan", dev):
             if F and g.dim is not None:
-                glob, shard = self._exact_lists(Q, code_t, K)
+                glob, shard = self._exact_lists(Q, code_t, K, pf=pf)
             else:
                 e = (np.full((F, K), NEG_INF), np.full((F, K), -1, np.int64))
                 glob, shard = e, e
@@ -1396,6 +1542,9 @@ class ShardedMemorySystem:
         ps = pl["stats"]
         for k_ in ("dup", "inserted", "linked", "cross_links", "evicted", "fallbacks"):
             stats[k_] += int(ps[k_])
+        if self._prefetch_next is not None:
+            with tracer.stage("sc_prefetch", dev):
+                self._launch_prefetch(pl)
         pruned = int(ps["pruned_new"])
         fact_key = np.asarray(pl["fact_key"], np.int64)
         supers = pl["supers"]

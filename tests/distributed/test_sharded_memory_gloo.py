@@ -188,16 +188,25 @@ def _sharded(comm, cfg=CPU):
         sm.cluster_pass()
     spread = []
     stats = []
-    for s, (convs, V) in enumerate(steps):
+
+    def part(s, convs, V):
         c0, c1 = _split(len(convs), comm.world, comm.rank)
         f0 = sum(len(c) for c in convs[:c0])
         f1 = f0 + sum(len(c) for c in convs[c0:c1])
-        stats.append(sm.consolidate_batch(convs[c0:c1], embeddings=V[f0:f1].to(dev), now=_now(s),
-                                          cadence=cfg.get("cadence", "batch")))
+        return convs[c0:c1], V[f0:f1].to(dev), _now(s)
+
+    if cfg.get("stream"):  # consolidate_stream: batch i+1 gathered and scanned under batch i's apply
+        stats = list(sm.consolidate_stream((part(s, c, V) for s, (c, V) in enumerate(steps)),
+                                           cadence=cfg.get("cadence", "batch")))
+        steps = []
+    for s, (convs, V) in enumerate(steps):
+        cv, Vp, t = part(s, convs, V)
+        stats.append(sm.consolidate_batch(cv, embeddings=Vp, now=t, cadence=cfg.get("cadence", "batch")))
         if rebal:  # all-to-all re-shard to even shares between batches; decisions must not change
             sm.rebalance()
             cnt = comm.all_gather_object(sm.g.num_nodes())
             spread.append(max(cnt) - min(cnt))
+    pf_used = sm.prefetched_batches
     nodes, edges = _graph_state(sm.g)
     parts = comm.all_gather_object((nodes, edges))
     contents = sm.component_digest(3, 0.3, 10)
@@ -208,7 +217,7 @@ def _sharded(comm, cfg=CPU):
     found = [f for part in comm.all_gather_object(found) for f in part]
     sm.close()
     if comm.rank != 0:
-        return {"stats": stats, "prof": prof}
+        return {"stats": stats, "prof": prof, "pf_used": pf_used}
     nodes_all, edges_all = {}, {}
     for n_, e_ in parts:
         assert not (set(n_) & set(nodes_all)), "a node is live on two ranks"
@@ -216,7 +225,7 @@ def _sharded(comm, cfg=CPU):
         edges_all.update(e_)
     single = _single(tempfile.mkdtemp(prefix="lzsolo_"), cfg)
     return {"stats": stats, "nodes": nodes_all, "edges": edges_all, "contents": contents, "prof": prof,
-            "total": total, "found": found, "single": single, "spread": spread}
+            "total": total, "found": found, "single": single, "spread": spread, "pf_used": pf_used}
 
 
 def check_equivalent(out, world, limit):
@@ -278,6 +287,14 @@ def test_sharded_tenant_reference_cadence_matches_single_process(world):
     out = spawn(world, functools.partial(_sharded, cfg=EXACT))
     check_equivalent(out, world, LIMIT)
     assert sum(st["consolidations"] for st in out[0]["stats"]) == STEPS * CONVS // 3
+
+
+def test_sharded_tenant_consolidate_stream_cpu():
+    """consolidate_stream at 2 gloo ranks: the per-batch calls' state (on the
+    CPU nothing is prefetched: the stream plumbing; the prefetched GPU path
+    is tests/kernels/test_sharded_memory_gpu.py)."""
+    out = spawn(2, functools.partial(_sharded, cfg=dict(EXACT, stream=True)))
+    check_equivalent(out, 2, LIMIT)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -48,6 +48,19 @@ def test_sharded_tenant_gpu_one_rank_row_digest():
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_tenant_gpu_consolidate_stream(world):
+    """ShardedMemorySystem.consolidate_stream on the GPU: each batch after the
+    first is gathered and scanned on a side stream under the previous
+    batch's apply (prefetched lists completed against the rows it left) --
+    the single process's state, as the per-batch calls."""
+    cfg = dict(GPU, steps=3, convs=48, cadence="conversation", stream=True)
+    out = spawn(world, functools.partial(_sharded, cfg=cfg))
+    check_equivalent(out, world, cfg["limit"])
+    assert all(out[r]["pf_used"] == 2 for r in range(world))  # batches 2 and 3 came from the prefetch
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 def test_num_rows_kernel_matches_searchsorted():
     """tenant.hip num_rows_kernel (the row-sharded tenant's number -> row
     lookup): base-then-delta binary search and the held-live filter against
