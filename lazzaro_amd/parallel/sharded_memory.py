@@ -1423,7 +1423,6 @@ class ShardedMemorySystem:
         from ..core.batch_plan import PoolTooSmall, plan
         g = self.g
         dev = self.device
-        comm = self.comm
         keep = 1.0 - DECAY_RATE
         thr = self.prune_threshold if self.auto_prune else None
         K = self.local.BATCH_LIST_K
