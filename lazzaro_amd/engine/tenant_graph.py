@@ -1106,8 +1106,8 @@ class TenantGraph:
         permuted by one stable sort. Edge order carries no meaning (every
         consumer is order-free or re-derives its index lists)."""
         ne = self.num_edges
-        if ne < self.EDGE_SORT_MIN:
-            return False
+        if ne < self.EDGE_SORT_MIN or (self._cc is not None and self._cc.get("ns") is not None):
+            return False  # (a batch's stable/volatile partition is in place)
         with self.on_stream():
             src = self.e["src"]
             if int((src[1:] < src[:-1]).sum()) * 32 <= ne:
@@ -1478,26 +1478,40 @@ class TenantGraph:
         launches, read back in one copy."""
         nc = len(cand)
         dev = self.device
+        # the stable prefix of a partitioned batch (cc_begin) loses nothing:
+        # flags, survivors and the compaction cover the suffix only
+        ns = self._cc.get("ns") if self._cc is not None else None
+        if ns is not None and (ns > ne or (prev is not None and prev.numel() < ns)):
+            ns = None
+        ns = ns or 0
         with self.on_stream():
             words = (self.cap + 31) // 32
             if self._rmb is None or self._rmb.numel() < words:
                 self._rmb = torch.zeros(words, dtype=torch.int32, device=dev)
             rt = self._dev_rows(cand) if nc else None
             info = torch.empty(3 * nc + 2, dtype=torch.int32, device=dev)
+            es = self.e if ns == 0 else {k: v[ns:] for k, v in self.e.items()}
+            ps = prev if (prev is None or ns == 0) else prev[ns:]
+            nes = ne - ns
             flag = bc = None
-            if ne:
-                flag = torch.empty(ne, dtype=torch.uint8, device=dev)
-                bc = torch.empty(max(1, (ne + T.NTB - 1) // T.NTB), dtype=torch.int32, device=dev)
-            T.seg_end(rt, nc, self.kind, self.sup, self.shard, self.stored, unstore, self._rmb, self.e, prev, flag, bc,
+            if nes:
+                flag = torch.empty(nes, dtype=torch.uint8, device=dev)
+                bc = torch.empty(max(1, (nes + T.NTB - 1) // T.NTB), dtype=torch.int32, device=dev)
+            T.seg_end(rt, nc, self.kind, self.sup, self.shard, self.stored, unstore, self._rmb, es, ps, flag, bc,
                       info)
             info_h = info.cpu().numpy()  # the one host sync
             pruned = int(info_h[3 * nc + 1]) if prev is not None else 0
-            if ne:
+            if nes:
                 n_out = int(info_h[3 * nc])
-                if n_out != ne:
-                    out, n, dr = T._compact(self.e, flag, bc, ne, extra=max(ne >> 3, self.EDGE_SLACK_MIN),
+                if n_out != nes:
+                    out, n, dr = T._compact(es, flag, bc, nes, extra=0 if ns else max(ne >> 3, self.EDGE_SLACK_MIN),
                                             n_out=n_out, dropped=self.track)
-                    self._adopt_edges(out)
+                    if ns:  # survivors back behind the untouched prefix, in the same buffers
+                        for k in T.EDGE_COLS:
+                            self.e[k][ns:ns + n_out].copy_(out[k])
+                        self._adopt_edges({k: v[:ns + n_out] for k, v in self.e.items()})
+                    else:
+                        self._adopt_edges(out)
                     if dr is not None:
                         self._note_dropped(*dr)
         if nc:
@@ -1847,9 +1861,53 @@ class TenantGraph:
             v = v[(v >= 0) & (v < n0)]
             if v.numel():
                 vmark[v.to(self.device)] = 1
-            lab = components_sel(self.e["src"], self.e["dst"], n0, self.e["w"], t0, vmark, n0, 0)
-        self._cc = {"lab": lab, "n0": n0, "vmark": vmark, "t0": t0, "keep": float(keep), "steps": 0}
+            ns = None
+            if self.PARTITION_EDGES:
+                ns = self._partition_stable(vmark, t0)
+            if ns is not None:  # base labels: the stable prefix, every edge of it
+                zero = torch.zeros(n0, dtype=torch.uint8, device=self.device)
+                lab = components_sel(self.e["src"][:ns], self.e["dst"][:ns], n0, None, -math.inf, zero, n0, 0)
+            else:
+                lab = components_sel(self.e["src"], self.e["dst"], n0, self.e["w"], t0, vmark, n0, 0)
+        self._cc = {"lab": lab, "n0": n0, "vmark": vmark, "t0": t0, "keep": float(keep), "steps": 0, "ns": ns}
         return True
+
+    # Within a batch of the incremental components, the edge list is stably
+    # partitioned: the edges that survive the whole batch first (never removed,
+    # never pruned: cc_begin's definition), the volatile ones after them. Every
+    # removal of the batch (victims' edges, decay prunes) and every append then
+    # happens in the suffix, so the segment ends flag and compact only the
+    # suffix, and each point unions only the suffix -- instead of passing over
+    # all 20M edges of a persistent graph twice per point. Edge order carries
+    # no meaning (_maybe_sort_edges); the partition keeps src order inside
+    # each side.
+    PARTITION_EDGES = True
+
+    def _partition_stable(self, vmark: torch.Tensor, t0: float) -> Optional[int]:
+        """Stable partition of the edges into (stable | volatile), in place
+        of the edge list; returns the stable count (None: nothing to split)."""
+        e = self.e
+        ne = int(e["src"].numel())
+        if ne == 0:
+            return None
+        src, dst = e["src"].long(), e["dst"].long()
+        vol = (vmark[src] != 0) | (vmark[dst] != 0)
+        if t0 > -math.inf:
+            vol |= e["w"] < t0
+        iv = torch.nonzero(vol).flatten()
+        nv = int(iv.numel())
+        if nv == 0 or nv == ne:
+            return ne - nv if nv == 0 else None
+        o = torch.cat([torch.nonzero(~vol).flatten(), iv])
+        extra = max(ne >> 3, self.EDGE_SLACK_MIN)
+        out = {}
+        for k in T.EDGE_COLS:
+            buf = torch.empty(ne + extra, dtype=e[k].dtype, device=self.device)
+            torch.index_select(e[k], 0, o, out=buf[:ne])
+            out[k] = buf[:ne]
+        self._adopt_edges(out)
+        self._bump(edges=True)
+        return ne - nv
 
     def cc_end(self) -> None:
         self._cc = None
@@ -1865,6 +1923,12 @@ class TenantGraph:
         lab[:n0] = c["lab"]
         if n > n0:
             lab[n0:] = torch.arange(n0, n, dtype=torch.int32, device=self.device)
+        ns = c.get("ns")
+        if ns is not None and ns <= self.num_edges:  # every suffix edge, on the base of the stable prefix
+            z = c.get("zero")
+            if z is None or z.numel() < n:
+                z = c["zero"] = torch.zeros(max(n, n0 + 65536), dtype=torch.uint8, device=self.device)
+            return components_sel(self.e["src"][ns:], self.e["dst"][ns:], n, None, -math.inf, z, n, 0, parent=lab)
         wthr = c["t0"] * c["keep"] ** c["steps"] * (1.0 + 1e-4) if c["t0"] > -math.inf else -math.inf
         return components_sel(self.e["src"], self.e["dst"], n, self.e["w"], wthr, c["vmark"], n0, 1, parent=lab)
 
