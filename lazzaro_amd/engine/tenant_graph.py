@@ -1863,7 +1863,9 @@ class TenantGraph:
                 vmark[v.to(self.device)] = 1
             ns = None
             if self.PARTITION_EDGES:
-                ns = self._partition_stable(vmark, t0)
+                from ..utils.tracing import tracer
+                with tracer.stage("cc_partition", self.device):
+                    ns = self._partition_stable(vmark, t0)
             if ns is not None:  # base labels: the stable prefix, every edge of it
                 zero = torch.zeros(n0, dtype=torch.uint8, device=self.device)
                 lab = components_sel(self.e["src"][:ns], self.e["dst"][:ns], n0, None, -math.inf, zero, n0, 0)
@@ -1890,15 +1892,24 @@ class TenantGraph:
         ne = int(e["src"].numel())
         if ne == 0:
             return None
-        src, dst = e["src"].long(), e["dst"].long()
-        vol = (vmark[src] != 0) | (vmark[dst] != 0)
+        # (int32 indices throughout: the gathers move half the index bytes)
+        vol = (torch.index_select(vmark, 0, e["src"]) | torch.index_select(vmark, 0, e["dst"])) != 0
         if t0 > -math.inf:
             vol |= e["w"] < t0
-        iv = torch.nonzero(vol).flatten()
-        nv = int(iv.numel())
-        if nv == 0 or nv == ne:
-            return ne - nv if nv == 0 else None
-        o = torch.cat([torch.nonzero(~vol).flatten(), iv])
+        nv = int(vol.sum())
+        if nv == ne:
+            return None
+        src = e["src"]
+        if int((src[1:] < src[:-1]).sum()) * 32 > ne:
+            # not (nearly) src-ordered: one stable sort by (volatile, src) --
+            # the union-find runs ~5x faster over src-ordered edges, and
+            # _maybe_sort_edges does not run while the partition is in place
+            o = torch.sort(vol.to(torch.int64) * (1 << 32) + src.to(torch.int64), stable=True).indices
+            o = o.to(torch.int32)
+        elif nv == 0:
+            return ne
+        else:
+            o = torch.cat([torch.nonzero(~vol).flatten(), torch.nonzero(vol).flatten()]).to(torch.int32)
         extra = max(ne >> 3, self.EDGE_SLACK_MIN)
         out = {}
         for k in T.EDGE_COLS:
