@@ -5,6 +5,7 @@ serve them from the shared columnar store."""
 import os
 import socket
 import tempfile
+import time
 
 import torch.multiprocessing as mp
 
@@ -43,7 +44,10 @@ def _worker(rank, world, port, tmp, q):
             q.close()
             q.join_thread()  # flush the result before the simulated crash
             os._exit(0)  # simulated crash: no group teardown
-        dead = detect_failed(hb, window=1.0)
+        # let rank 2's last beat land before the window opens, and give the
+        # survivors' heartbeat threads slack on a loaded host
+        time.sleep(0.5)
+        dead = detect_failed(hb, window=2.0)
         survivors = [r for r in range(world) if r not in dead]
         reform_group(lambda g, n: dist.FileStore(os.path.join(tmp, f"pg_gen{g}"), n), survivors, rank)
         comm = Communicator()
@@ -124,7 +128,10 @@ def _svc_worker(rank, world, port, tmp, q):
             q.close()
             q.join_thread()
             os._exit(0)
-        dead = detect_failed(hb, window=1.0)
+        # let rank 2's last beat land before the window opens, and give the
+        # survivors' heartbeat threads slack on a loaded host
+        time.sleep(0.5)
+        dead = detect_failed(hb, window=2.0)
         survivors = [r for r in range(world) if r not in dead]
         reform_group(lambda g, n: dist.FileStore(os.path.join(tmp, f"svc_gen{g}"), n), survivors, rank)
         released = svc.reform(Communicator(), place.remove(dead))

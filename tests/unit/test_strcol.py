@@ -36,19 +36,18 @@ def test_list_protocol():
 
 
 def test_not_gc_tracked_and_collector_cost_flat():
+    def collect_s():
+        t0 = time.perf_counter()
+        gc.collect()
+        return time.perf_counter() - t0
+
+    base = min(collect_s() for _ in range(3))
     big = rt.StrColumn([f"node_{i}" for i in range(2_000_000)])
     assert not gc.is_tracked(big)
-    t0 = time.perf_counter()
-    gc.collect()
-    with_big = time.perf_counter() - t0
-    lst = [f"node_{i}" for i in range(2_000_000)]
-    t0 = time.perf_counter()
-    gc.collect()
-    with_list = time.perf_counter() - t0
-    del lst
-    # a 2M-entry list adds a traversal of every reference to a full pass; the
-    # column adds nothing (generous bound: shared CI hosts are noisy)
-    assert with_big < with_list or with_big < 0.02, (with_big, with_list)
+    with_big = min(collect_s() for _ in range(3))
+    # a full pass over the process's tracked objects does not grow with the
+    # column (generous bound: shared CI hosts are noisy)
+    assert with_big < 1.5 * base + 0.02, (with_big, base)
 
 
 def test_tenant_graph_uses_native_columns():
