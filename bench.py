@@ -210,8 +210,9 @@ def main():
     ap.add_argument("--sharded-steps", type=int, default=5,
                     help="timed steps of config 4 as one row-sharded buffer (--rows per rank; 0 = skip)")
     ap.add_argument("--cpu", action="store_true", help="CPU / gloo dry run of the whole flow (tests only)")
-    ap.add_argument("--no-gc-freeze", dest="gc_freeze", action="store_false",
-                    help="do not freeze the startup heap before the timed loops (see gc_in_timed_loop)")
+    ap.add_argument("--gc-freeze", dest="gc_freeze", action="store_true",
+                    help="freeze the startup heap before the timed loops (off by default: the library's results "
+                         "are array-backed, so the loop allocates nothing per row; see gc_in_timed_loop)")
     ap.add_argument("--no-launch", action="store_true",
                     help="--gpus 1 without the torch.distributed.run child (no process group, no collectives)")
     a = ap.parse_args()
@@ -332,15 +333,13 @@ def main():
         print("cgroup before:", _cg(), file=sys.stderr)
         hprof = cProfile.Profile()
         hprof.enable()
-    # The serving process freezes its startup heap -- torch's ~170k module
-    # objects, the model, the loaded tenant -- as long-running PyTorch servers
-    # do: a full collection then walks only what serving allocates. Without
-    # it CPython runs a full pass about every 55 steps (the per-batch result
-    # lists) over torch's heap, 40-70 ms each on the box (profiles/r5/README.md).
-    # This is the application's choice, made once here; the library holds no
-    # per-row Python containers the collector traverses (the tenant's host
-    # index lives in native StrColumns) and never touches the collector.
-    # --no-gc-freeze measures without it; gc_in_timed_loop reports the passes.
+    # No gc.freeze() by default: a batch's results are a ResultBatch over the
+    # row array (engine/views.py; NodeViews made when read), the tenant's host
+    # index lives in native StrColumns, so a serving step allocates nothing
+    # per row and the collector's full pass over torch's ~170k module objects
+    # is not triggered inside the loop (round 5 needed the freeze: it built
+    # 10k views per step, profiles/r5/headline_no_gc_freeze/). --gc-freeze
+    # restores it for an A/B; gc_in_timed_loop reports the passes either way.
     import gc
     if a.gc_freeze:
         gc.collect()

@@ -404,7 +404,22 @@ constexpr int kDualOpt = 8;
 int g_dual_opt = -1;  // A/B override of kCandOpt for the dual kernel (lzk_set_dual_opt)
 int g_i8_opt = -1;  // A/B override of kCandOpt for the int8 scan (lzk_set_i8_opt; probes only)
 int g_g256_opt = 0;  // A/B override of kCandOpt for the plain (no bias / label) variant; 100 = OPT 0
-int g_n_cu = 0;
+int g_dev_cu = 0;  // the device's CU count (read once)
+// grid_cap() budget of the CALLING thread (lzk_set_cu_budget): the grid a
+// launch uses and the record buffers its caller sized from lzk_cand_grid*
+// come from the same thread's budget, so a budget set by another thread (a
+// prefetched consolidation scan beside a search) cannot resize a launch
+// between the sizing call and the launch.
+thread_local int g_cu_budget = 0;
+int n_cu() {
+  if (g_dev_cu <= 0) {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    g_dev_cu = c;
+  }
+  return (g_cu_budget > 0 && g_cu_budget < g_dev_cu) ? g_cu_budget : g_dev_cu;
+}
 
 template <int K>
 struct TopK {
@@ -698,6 +713,67 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
   }
 }
 
+// Re-score cut of a low-precision candidate list (ops.search
+// _rescore_above_cut), one wave per query: the k best list entries by scan
+// score (rows [q, 0..k) of cand_select's output, -1 = empty) are scored
+// exactly -- alpha <Q[q], X[row]> + bias[row] from the bf16 rows (F32 false)
+// or the fp32 rows / queries (F32 true, lean tenants) -- and their minimum L
+// (-inf unless all k are real rows with finite scores) gives
+//   cut[q] = L - margin[q] - (2e-4 |alpha| + 1e-6 (1 + |L|))
+// (the slack covers this kernel's fp32 accumulation order against the
+// re-score kernel's), raised to floor - margin[q] when has_floor. A row of the
+// true top-k has a scan score >= L - margin, so entries below the cut cannot
+// reach the top-k. Replaces a gather + batched GEMM (einsum) + where/min
+// chain of ~10 ATen launches with one.
+template <bool F32>
+__global__ __launch_bounds__(256) void cand_cut_kernel(const void* __restrict__ X, long ldx, long nrows,
+                                                       const void* __restrict__ Qm, long ldq, int D, int nq,
+                                                       const float* __restrict__ bias, float alpha,
+                                                       const long* __restrict__ rows, int ldr, int k,
+                                                       const float* __restrict__ margin, float floor, int has_floor,
+                                                       float* __restrict__ cut) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  const int chunks = D >> 2;
+  constexpr int MAXC = 8;  // D <= 2048
+  float qv[MAXC][4];
+#pragma unroll
+  for (int t = 0; t < MAXC; ++t) {
+    const int c = lane + 64 * t;
+    if (c < chunks) load4<F32>(Qm, (long)q * ldq + 4 * c, qv[t]);
+  }
+  float lo = __builtin_inff();
+  for (int j = 0; j < k; ++j) {
+    const long r = rows[(long)q * ldr + j];  // wave-uniform
+    if (r < 0 || r >= nrows) { lo = LZK_NEG_INF; break; }
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < MAXC; ++t) {
+      const int c = lane + 64 * t;
+      if (c < chunks) {
+        float xv[4];
+        load4<F32>(X, r * ldx + 4 * c, xv);
+        acc = fmaf(qv[t][0], xv[0], acc);
+        acc = fmaf(qv[t][1], xv[1], acc);
+        acc = fmaf(qv[t][2], xv[2], acc);
+        acc = fmaf(qv[t][3], xv[3], acc);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    const float sc = alpha * acc + (bias ? bias[r] : 0.f);
+    if (!(sc > LZK_NEG_INF && sc < __builtin_inff())) { lo = LZK_NEG_INF; break; }  // -inf, +inf or nan
+    lo = fminf(lo, sc);
+  }
+  if (lane != 0) return;
+  const float m = margin[q];
+  float c = lo - m - (2e-4f * fabsf(alpha) + 1e-6f * (1.f + fabsf(lo)));
+  if (has_floor) c = fmaxf(c, floor - m);  // (fmaxf: a nan c takes the floor)
+  if (c != c) c = LZK_NEG_INF;
+  cut[q] = c;
+}
+
 // Query side of the int8 store search in one launch per batch (one block
 // per query): symmetric per-row int8 of the bf16 query (s = max|q| / 127,
 // q8 = rint(q / s) clamped to +-127, s = 0 for a zero row -- ops.search
@@ -815,7 +891,7 @@ LZK_EXPORT void lzk_set_cand_persist(int p) { g_cand_persist = p; }
 // CU budget of the persistent scans' grids (one block per CU): a search
 // launched on a CU-masked stream sizes its grid to the CUs it may use; <= 0
 // restores the device's CU count.
-LZK_EXPORT void lzk_set_cu_budget(int n) { g_n_cu = n > 0 ? n : 0; }
+LZK_EXPORT void lzk_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
 LZK_EXPORT void lzk_set_g256_opt(int o) { g_g256_opt = o; }
 LZK_EXPORT void lzk_set_dual_opt(int o) { g_dual_opt = o; }
 LZK_EXPORT void lzk_set_i8_opt(int o) { g_i8_opt = o; }
@@ -840,15 +916,10 @@ LZK_EXPORT int lzk_flat_cand(const void* X, long ldx, int nrows, const void* Qm,
   const u16* x = (const u16*)X;
   const u16* q = (const u16*)Qm;
   if (g_cand_persist < 0) g_cand_persist = 1;
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
-  if (g_cand_persist && nblk >= g_n_cu) {
+  const int ncu = n_cu();
+  if (g_cand_persist && nblk >= ncu) {
     if (!blk_buf || blk_cap <= 0 || !blk_cnt) return (int)hipErrorInvalidValue;  // lzk_cand_grid() > 0: records needed
-    const int grid = g_n_cu;
+    const int grid = ncu;
 #define LZK_GP(B, L)                                                                                                \
   do {                                                                                                              \
     (void)hipFuncSetAttribute((const void*)flat_cand_persistent_kernel<B, L, false, kCandOpt>,                                \
@@ -920,13 +991,8 @@ LZK_EXPORT int lzk_flat_cand_dual(const void* X, long ldx, int nrows, const void
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
-  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  const int ncu = n_cu();
+  const int grid = (int)(nblk < ncu ? nblk : ncu);
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* q = (const u16*)Qm;
@@ -987,16 +1053,11 @@ LZK_EXPORT int lzk_cand_gather(const void* blk_buf, int blk_cap, const int* blk_
 // Grid of the persistent candidate pass for a shape (the gather's grid); 0
 // when lzk_flat_cand would take the non-persistent kernel (global appends).
 LZK_EXPORT int lzk_cand_grid(int nrows, int nq, int dual) {
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
+  const int ncu = n_cu();
   if (g_cand_persist < 0) g_cand_persist = 1;
   const long nblk = (long)((nrows + BM - 1) / BM) * ((nq + BN - 1) / BN);
-  if (dual) return (int)(nblk < g_n_cu ? nblk : g_n_cu);
-  return (g_cand_persist && nblk >= g_n_cu) ? g_n_cu : 0;
+  if (dual) return (int)(nblk < ncu ? nblk : ncu);
+  return (g_cand_persist && nblk >= ncu) ? ncu : 0;
 }
 
 // fp8 candidate pass (rows / queries: e4m3 bytes, row strides in bytes,
@@ -1013,13 +1074,8 @@ LZK_EXPORT int lzk_flat_cand_f8(const void* X8, long ldx_bytes, int nrows, const
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
-  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  const int ncu = n_cu();
+  const int grid = (int)(nblk < ncu ? nblk : ncu);
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X8;
   const u16* q = (const u16*)Q8;
@@ -1039,14 +1095,9 @@ LZK_EXPORT int lzk_flat_cand_f8(const void* X8, long ldx_bytes, int nrows, const
 }
 
 LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
+  const int ncu = n_cu();
   const long nblk = (long)((nrows + BM - 1) / BM) * ((nq + BN - 1) / BN);
-  return (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  return (int)(nblk < ncu ? nblk : ncu);
 }
 
 // Exact bf16 re-score of candidate lists in place (see cand_rescore_kernel).
@@ -1071,6 +1122,24 @@ LZK_EXPORT int lzk_cand_rescore32(const float* X32, long ldx, const float* Q32, 
   return (int)hipGetLastError();
 }
 
+// The re-score cut of a low-precision candidate list (cand_cut_kernel);
+// f32 = 1: X / Q are fp32 (lean tenants), else bf16. rows: cand_select's
+// int64 output [nq, ldr], the first k columns read.
+LZK_EXPORT int lzk_cand_cut(const void* X, long ldx, long nrows, const void* Q, long ldq, int D, int nq, int f32,
+                            const float* bias, float alpha, const long* rows, int ldr, int k, const float* margin,
+                            float floor, int has_floor, float* cut, void* stream) {
+  if (D % 4 != 0 || D > 2048 || nq <= 0 || k <= 0 || k > ldr || !margin) return (int)hipErrorInvalidValue;
+  if (f32 && (ldx % 4 != 0 || ldq % 4 != 0)) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
+  if (f32)
+    hipLaunchKernelGGL(cand_cut_kernel<true>, grid, block, 0, (hipStream_t)stream, X, ldx, nrows, Q, ldq, D, nq,
+                       bias, alpha, rows, ldr, k, margin, floor, has_floor, cut);
+  else
+    hipLaunchKernelGGL(cand_cut_kernel<false>, grid, block, 0, (hipStream_t)stream, X, ldx, nrows, Q, ldq, D, nq,
+                       bias, alpha, rows, ldr, k, margin, floor, has_floor, cut);
+  return (int)hipGetLastError();
+}
+
 // int8 candidate pass (rows / queries: int8 bytes, row strides in bytes,
 // D_bytes % 128 == 0, D_bytes <= 1024 so the int32 sums stay exact in fp32):
 // score = alpha * qscale[q] * (<q8, x8> * rscale[row]) + bias[row] >= thr[q]
@@ -1087,13 +1156,8 @@ LZK_EXPORT int lzk_flat_cand_i8(const void* X8, long ldx_bytes, int nrows, const
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
-  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  const int ncu = n_cu();
+  const int grid = (int)(nblk < ncu ? nblk : ncu);
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X8;
   const u16* q = (const u16*)Q8;
@@ -1144,13 +1208,8 @@ LZK_EXPORT int lzk_flat_cand_dual_i8(const void* X8, long ldx_bytes, int nrows, 
   const int n_rt = (nrows + BM - 1) / BM, n_qt = (nq + BN - 1) / BN;
   const long nblk = (long)n_rt * n_qt;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-  if (g_n_cu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_n_cu <= 0)
-      g_n_cu = 256;
-  }
-  const int grid = (int)(nblk < g_n_cu ? nblk : g_n_cu);
+  const int ncu = n_cu();
+  const int grid = (int)(nblk < ncu ? nblk : ncu);
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X8;
   const u16* q = (const u16*)Q8;

@@ -46,9 +46,20 @@ int reserve(StrCol* self, Py_ssize_t need) {
 }
 
 void sc_dealloc(StrCol* self) {
+  // a heap type (PyType_FromSpec): every instance holds a reference to it
+  PyTypeObject* tp = Py_TYPE(self);
   for (Py_ssize_t i = 0; i < self->n; ++i) Py_XDECREF(self->items[i]);
   std::free(self->items);
-  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+  tp->tp_free(reinterpret_cast<PyObject*>(self));
+  Py_DECREF(tp);
+}
+
+// Items are str or None only: the type is not GC-tracked, so an item that
+// could refer back to the column would make a cycle the collector never frees.
+int check_item(PyObject* v) {
+  if (v == Py_None || PyUnicode_Check(v)) return 0;
+  PyErr_Format(PyExc_TypeError, "StrColumn holds str or None, not %.100s", Py_TYPE(v)->tp_name);
+  return -1;
 }
 
 int extend_from(StrCol* self, PyObject* it) {
@@ -60,6 +71,12 @@ int extend_from(StrCol* self, PyObject* it) {
     return -1;
   }
   PyObject** src = PySequence_Fast_ITEMS(seq);
+  for (Py_ssize_t i = 0; i < m; ++i) {
+    if (check_item(src[i]) < 0) {
+      Py_DECREF(seq);
+      return -1;
+    }
+  }
   for (Py_ssize_t i = 0; i < m; ++i) {
     Py_INCREF(src[i]);
     self->items[self->n + i] = src[i];
@@ -100,6 +117,7 @@ int sc_ass_item(StrCol* self, Py_ssize_t i, PyObject* v) {
     PyErr_SetString(PyExc_IndexError, "StrColumn assignment index out of range");
     return -1;
   }
+  if (check_item(v) < 0) return -1;
   Py_INCREF(v);
   PyObject* old = self->items[i];
   self->items[i] = v;
@@ -158,7 +176,7 @@ PyObject* sc_iter(StrCol* self) {
 }
 
 PyObject* sc_append(StrCol* self, PyObject* v) {
-  if (reserve(self, self->n + 1) < 0) return nullptr;
+  if (check_item(v) < 0 || reserve(self, self->n + 1) < 0) return nullptr;
   Py_INCREF(v);
   self->items[self->n++] = v;
   Py_RETURN_NONE;

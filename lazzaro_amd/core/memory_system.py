@@ -44,7 +44,7 @@ import numpy as np
 import torch
 
 from ..engine.tenant_graph import NODE, TYPE_MASK, TenantGraph
-from ..engine.views import GraphBuffer, NodeView, ShardView, ShardsMap, SuperNodesMap, import_edges, import_nodes
+from ..engine.views import GraphBuffer, NodeView, ResultBatch, ShardView, ShardsMap, SuperNodesMap, import_edges, import_nodes
 from ..models.graph import Edge, Node
 from . import providers as _providers
 from .consolidation import ConsolidationMixin
@@ -692,7 +692,8 @@ class MemorySystem(ConsolidationMixin):
         with self._graph_lock:
             g = self.graph
             if kind_ == "rows" and g is g0:  # non-node rows were set to -1 on the device
-                return NodeView.of_rows(g, data.numpy().tolist() if not data.is_cuda else data.tolist())
+                # lazy per-row views: no Python object per result row until read
+                return ResultBatch(g, data.numpy() if not data.is_cuda else data.cpu().numpy())
             if kind_ == "rows":  # the tenant was switched while the search ran
                 data = [[g0.ids[r] for r in row if r >= 0] for row in data.tolist()]
             out = []

@@ -2144,7 +2144,7 @@ class TenantGraph:
             (_, ra), (_, rb) = flat_topk_dual_i8(self.emb8, self.rs8, q8, qs, X, q16, CAND_SLOTS,
                                                  row_label=labc, q_label=ql, bias=bias,
                                                  margin=margin, margin_rig=margin_rig, floor=floor,
-                                                 stats=st)
+                                                 floor_tol=0.5 * COS_FLOOR_SLACK, stats=st)
             if st:
                 self._dual_stats = st
         else:

@@ -26,7 +26,7 @@ the boost call the engine directly.
 from __future__ import annotations
 
 import time
-from collections.abc import MutableMapping
+from collections.abc import MutableMapping, Sequence
 from typing import Dict, Iterator, List, Optional, Set, Tuple
 
 import numpy as np
@@ -180,6 +180,92 @@ class NodeView(Node):
         return Node.__eq__(self, other)
 
     __hash__ = object.__hash__
+
+
+class NodeList(Sequence):
+    """One query's search result -- the list of ``Node`` views the reference
+    returns (memory_system.py:1460-1472) -- backed by the result's row array.
+    A :class:`NodeView` is made when an element is read, so a serving step
+    that only passes results along allocates no Python object per row (the
+    collector then has nothing new to walk; bench.py needs no gc.freeze).
+    Compares equal to a list of the same nodes."""
+    __slots__ = ("_g", "_rows")
+
+    def __init__(self, g: TenantGraph, rows: np.ndarray):
+        self._g, self._rows = g, rows
+
+    @property
+    def rows(self) -> np.ndarray:
+        return self._rows
+
+    def __len__(self) -> int:
+        return int(self._rows.shape[0])
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [NodeView.of(self._g, r) for r in self._rows[i].tolist()]
+        return NodeView.of(self._g, int(self._rows[i]))
+
+    def __iter__(self):
+        g = self._g
+        for r in self._rows.tolist():
+            yield NodeView.of(g, r)
+
+    def __eq__(self, other):
+        if isinstance(other, (list, tuple, Sequence)) and not isinstance(other, str):
+            return list(self) == list(other)
+        return NotImplemented
+
+    def __add__(self, other):
+        return list(self) + list(other)
+
+    def __radd__(self, other):
+        return list(other) + list(self)
+
+    def __repr__(self) -> str:
+        return repr(list(self))
+
+
+class ResultBatch(Sequence):
+    """A batch's search results: ``res[q]`` is query q's :class:`NodeList`.
+    Holds the [nq, k] row array (-1 = empty slot or a row that is not a
+    node, marked on the device) and nothing per row."""
+    __slots__ = ("_g", "_rows")
+
+    def __init__(self, g: TenantGraph, rows: np.ndarray):
+        self._g, self._rows = g, np.asarray(rows, dtype=np.int64)
+
+    @property
+    def rows(self) -> np.ndarray:
+        return self._rows
+
+    def __len__(self) -> int:
+        return int(self._rows.shape[0])
+
+    def _one(self, q: int) -> NodeList:
+        r = self._rows[q]
+        return NodeList(self._g, r[r >= 0])
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self._one(q) for q in range(len(self))[i]]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError("ResultBatch index out of range")
+        return self._one(i)
+
+    def __iter__(self):
+        for q in range(len(self)):
+            yield self._one(q)
+
+    def __eq__(self, other):
+        if isinstance(other, (list, tuple, Sequence)) and not isinstance(other, str):
+            return len(self) == len(other) and all(a == b for a, b in zip(self, other))
+        return NotImplemented
+
+    def __repr__(self) -> str:
+        return repr([list(x) for x in self])
 
 
 def _node_kwargs(node: Node) -> Dict:

@@ -371,8 +371,10 @@ PREFETCH_GRID_FRAC = 0.75
 
 
 class grid_cap:
-    """Context: persistent scans launched inside use at most ``frac`` of the
-    device's CUs (search256.hip g_n_cu, read at launch; restored on exit)."""
+    """Context: persistent scans launched inside, by THIS thread, use at most
+    ``frac`` of the device's CUs (search256.hip g_cu_budget is thread-local:
+    the grid-sizing call and the launch of one scan read the same budget, and
+    a search on another thread keeps the whole device; restored on exit)."""
 
     def __init__(self, frac: float):
         self.frac = float(frac)
@@ -388,6 +390,8 @@ class grid_cap:
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
                                            _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.I, _lib.I, _lib.P,
                                            _lib.P])
+_lib.register("lzk_cand_cut", _lib.I, [_lib.P, _lib.L, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.I, _lib.P,
+                                       _lib.F, _lib.P, _lib.I, _lib.I, _lib.P, _lib.F, _lib.I, _lib.P, _lib.P])
 _lib.register("lzk_cand_rescore32", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
                                              _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.I, _lib.I, _lib.P,
                                              _lib.P])
@@ -644,16 +648,25 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     return _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, cnt, cs, ci, cap, need=need)
 
 
-def _cert_tau(thr: torch.Tensor, margin_rig: torch.Tensor, floor: float = None) -> torch.Tensor:
+def _cert_tau(thr: torch.Tensor, margin_rig: torch.Tensor, floor: float = None,
+              floor_tol: float = 0.0) -> torch.Tensor:
     """The certificate level of a low-precision scan list: thr + margin_rig
     (+ relative slack) -- no row the scan dropped can reach it. With a caller
-    floor that the level does not exceed, every row at or above the floor is
-    in the list already: -inf, certified without a count."""
+    floor that the level does not exceed (by more than ``floor_tol``), every
+    row at or above floor + floor_tol is in the list already: -inf, certified
+    without a count. The floor test comes BEFORE the relative slack: a
+    threshold clamped to floor - margin_rig gives thr + margin_rig = floor up
+    to fp32 rounding, which the slack (1e-6 (1 + |t|)) would always push
+    above the floor, so the floor certificate never fired and every
+    floor-clamped query went to the exact fallback."""
     t = thr + margin_rig if margin_rig is not None else thr
+    fl_ok = (t <= float(floor) + float(floor_tol)) if floor is not None else None
     t = t + 1e-6 * (1.0 + t.abs())
-    if floor is not None:
-        t = torch.where(t <= float(floor), torch.full_like(t, float("-inf")), t)
-    return torch.nan_to_num(t, nan=float("-inf")).contiguous()
+    if fl_ok is not None:
+        t = torch.where(fl_ok, torch.full_like(t, float("-inf")), t)
+    # (neginf= too: nan_to_num's default maps -inf to -FLT_MAX, which the
+    # re-score kernel's "tau == -inf: certified" test does not recognise)
+    return torch.nan_to_num(t, nan=float("-inf"), neginf=float("-inf")).contiguous()
 
 
 # Speculative store-search threshold (flat_topk_i8, wide batches): the 1/S
@@ -691,23 +704,21 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
         ovf = torch.empty((nq,), dtype=torch.int32, device=dev)
         _lib.check(L.lzk_cand_select(cnt.data_ptr(), cs.data_ptr(), ci.data_ptr(), cap, nq, kslot, kslot, 0,
                                      s8.data_ptr(), i8.data_ptr(), ovf.data_ptr(), None, st), "lzk_cand_select")
-        rows = i8[:, :k]
-        # (an overflowed list's entries are real rows, but the gather must
-        # never see an index outside the scanned rows)
-        valid = (rows >= 0) & (rows < X16.shape[0])
-        rr = torch.where(valid, rows, torch.zeros_like(rows))
+        # the k best entries scored exactly, their minimum L -> the cut
+        # L - margin (- fp32 slack), raised to floor - margin: ONE launch
+        # (search256.hip cand_cut_kernel; rows outside the scanned ones, e.g.
+        # an overflowed list's, count as missing)
+        cut = torch.empty(nq, dtype=torch.float32, device=dev)
+        mg = margin.float().contiguous()
         if isinstance(X16, LeanRows):
-            dot = torch.einsum("qd,qkd->qk", X16.Q32.float(), X16.X32[rr].float())
+            Xc, Qc, f32 = X16.X32, X16.Q32, 1
         else:
-            dot = torch.einsum("qd,qkd->qk", Q16.float(), X16[rr].float())
-        sc = float(alpha) * dot + (bias[rr] if bias is not None else 0.0)
-        sc = torch.where(valid & torch.isfinite(sc), sc, torch.full_like(sc, float("-inf")))
-        lo = sc.min(1).values  # -inf unless all k entries are real rows
-        # slack: the kernel's fp32 accumulation order differs from this one
-        cut = lo - margin - (2e-4 * abs(float(alpha)) + 1e-6 * (1.0 + lo.abs()))
-        if floor is not None:  # rows below floor - margin cannot reach the caller's floor
-            cut = torch.maximum(cut, float(floor) - margin)
-        cut = torch.nan_to_num(cut, nan=float("-inf")).contiguous()
+            Xc, Qc, f32 = X16, Q16, 0
+        _lib.check(L.lzk_cand_cut(Xc.data_ptr(), Xc.stride(0), int(X16.shape[0]), Qc.data_ptr(), Qc.stride(0),
+                                  int(Xc.shape[1]) if f32 else Dp, nq, f32, _lib.ptr(bias), float(alpha),
+                                  i8.data_ptr(), kslot, int(k), mg.data_ptr(),
+                                  float(floor) if floor is not None else 0.0, int(floor is not None),
+                                  cut.data_ptr(), st), "lzk_cand_cut")
     fl = float("-inf") if floor is None else float(floor)
     if isinstance(X16, LeanRows):
         X32, Q32 = X16.X32, X16.Q32
@@ -724,14 +735,16 @@ def _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin, cnt, cs, ci, cap
 def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscale: torch.Tensor,
                       X16: torch.Tensor, Q16: torch.Tensor, k: int, *, row_label, q_label, bias=None,
                       alpha: float = 1.0, margin=None, margin_rig=None, floor: float = None,
-                      stats: Optional[list] = None):
+                      floor_tol: float = None, stats: Optional[list] = None):
     """:func:`flat_topk_dual` with the candidate scan on the int8 MFMA (the
     rows' int8 copy, see :func:`flat_topk_i8` for the two margins): each list's
     threshold is max(sampled bf16 k-th best - margin, floor - margin_rig), both
     lists are re-scored from the bf16 rows above their worst-case cut and
     certified per query (k entries at thr + margin_rig, or a threshold that
     sits margin_rig below the floor), uncertified queries recomputed exactly --
-    the same lists as the bf16 dual scan for every entry >= floor. ``stats``:
+    the same lists as the bf16 dual scan for every entry >= floor + floor_tol
+    (``floor_tol``: how far above the floor the caller's decisions start;
+    default fp32 rounding, 1e-6 (1 + |floor|)). ``stats``:
     receives the (fallback flags, list lengths) device tensors of both lists.
     Returns ((scores, rows) unfiltered, (scores, rows) filtered)."""
     L = _lib.lib()
@@ -760,10 +773,12 @@ def flat_topk_dual_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, 
     _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_label, q_label, kslot, S, cap, ca, cb)
     need_a = torch.empty(nq, dtype=torch.int32, device=dev)
     need_b = torch.empty(nq, dtype=torch.int32, device=dev)
+    if floor is not None and floor_tol is None:
+        floor_tol = 1e-6 * (1.0 + abs(float(floor)))
     _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin_rig, *ca, cap, floor=floor,
-                       chk=(_cert_tau(thr_a, margin_rig, floor), k, cap + 1, need_a))
+                       chk=(_cert_tau(thr_a, margin_rig, floor, floor_tol or 0.0), k, cap + 1, need_a))
     _rescore_above_cut(X16, Q16, k, kslot, bias, alpha, margin_rig, *cb, cap, floor=floor,
-                       chk=(_cert_tau(thr_b, margin_rig, floor), k, cap + 1, need_b))
+                       chk=(_cert_tau(thr_b, margin_rig, floor, floor_tol or 0.0), k, cap + 1, need_b))
     ra = _select_with_fallback(X16, Q16, k, kslot, bias, None, None, alpha, 0, *ca, cap, need=need_a,
                                ovf_sink=stats)
     rb = _select_with_fallback(X16, Q16, k, kslot, bias, row_label, q_label, alpha, 0, *cb, cap, need=need_b,
@@ -1076,10 +1091,12 @@ def mt_topk(tiles: MtTiles, Q: torch.Tensor, k: int, p_e32: torch.Tensor, p_bias
     # 16 bf16 candidates for every k <= 16 (the per-tenant store search's
     # CAND_SLOTS): a bf16 near-tie just past the k-th cannot push the fp32
     # top-k out of the re-ranked set
-    kc = max(16, k)
-    kslot = L.lzk_flat_topk_kslot(int(kc))
-    if kslot < 0 or k > kc:
+    if k > 16:
         raise ValueError("mt_topk supports k <= 16")
+    kc = 16
+    kslot = L.lzk_flat_topk_kslot(int(kc))
+    if kslot < 0:
+        raise ValueError("mt_topk: no candidate slot count for k = 16")
     st = _lib.stream_ptr(dev)
     Qf = Q.to(dev, torch.float32).contiguous()
     Q16 = torch.zeros((nq, Dp), dtype=torch.bfloat16, device=dev)

@@ -532,7 +532,7 @@ def search_global_batch(svc, Q: torch.Tensor, limit: int = 5) -> GlobalHits:
     gd = svc.global_directory(D, limit) if D else None
     redo = None
     if gd is not None and gd["small"] and NQ:
-        if len(gd["small"]) >= MT_MIN_TENANTS:
+        if len(gd["small"]) >= MT_MIN_TENANTS and limit <= 16:  # (mt_topk's re-rank headroom: k <= 16)
             # the small tenants: ONE multi-tenant MFMA pass (ops/search.py mt_topk)
             s, key, tk, redo = _global_small(svc, gd, Qall, limit, me, dev)
             best_s, best_k, best_t = _merge(torch.cat([best_s, s], 1), torch.cat([best_k, key], 1), limit,

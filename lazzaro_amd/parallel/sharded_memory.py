@@ -1373,20 +1373,23 @@ class ShardedMemorySystem:
         gather batch i+1 and launch this rank's candidate scan of it on a
         side stream (see :meth:`consolidate_stream`). Not when batch i runs a
         cluster pass (it moves the cluster homes that decide the holders, and
-        shares the scan workspaces), without embeddings, or off the GPU --
-        conditions every rank evaluates alike."""
+        shares the scan workspaces) or off the GPU -- conditions every rank
+        evaluates alike -- and when any rank's next batch has no embeddings
+        or the wrong width: those are per-rank, so they are summed over the
+        ranks first (one host all-reduce) and every rank skips or runs the
+        prefetch's collectives together."""
         from ..core.consolidation import _prefetch_stream
         nxt, self._prefetch_next = self._prefetch_next, None
         self._prefetched = None
         g = self.g
-        if nxt is None or not g.on_gpu or g.dim is None or nxt[1] is None \
-                or any(seg["cluster"] for seg in pl["segments"]):
+        if not g.on_gpu or g.dim is None or any(seg["cluster"] for seg in pl["segments"]):
             return
-        flat, conv, E = self._prep_facts(nxt[0], nxt[1])
+        skip = nxt is None or nxt[1] is None
+        flat, conv, E = ([], [], None) if skip else self._prep_facts(nxt[0], nxt[1])
         if E is None:
             E = torch.zeros((0, g.dim), dtype=torch.float32, device=self.device)
-        bad = int(E.shape[1] != g.dim)
-        if self._sum(bad)[0]:
+        n_skip, n_bad = self._sum(int(skip), int(E.shape[1] != g.dim))
+        if n_skip or n_bad:
             return
         gb = self._gather_batch(flat, conv, E, len(nxt[0]))
         pf = {"src": nxt[1], "B_loc": len(nxt[0]), "m": len(flat), "gb": gb, "h": None, "si": None, "n0": g.n}

@@ -554,6 +554,46 @@ def test_flat_topk_dual_i8_matches_bf16_dual_gpu(floor):
         assert torch.allclose(s0[fin], s1[fin], atol=1e-4, rtol=0)
 
 
+def test_flat_topk_dual_i8_floor_certificate_gpu():
+    """Consolidation's shape: random unit rows, a link floor far above the
+    sampled k-th best, so both thresholds sit at floor - margin_rig. The
+    floor certificate must fire for (almost) every query -- no exact
+    fallback, no auto-mode back-off to bf16 (the relative slack
+    used to push the level above the floor, so every query fell back) --
+    and the lists must still equal the bf16 dual scan's for every entry
+    above the floor, planted near-duplicates included."""
+    from lazzaro_amd.ops.search import flat_topk_dual, flat_topk_dual_i8, quantize_i8_rows
+    gen = torch.Generator(device=DEV).manual_seed(31)
+    N, D, nq = 1_500_000, 768, 512
+    X = torch.randn(N, D, device=DEV, generator=gen)
+    X = X / X.norm(dim=1, keepdim=True)
+    Q = torch.randn(nq, D, device=DEV, generator=gen)
+    plant = torch.randint(0, N, (nq // 4,), device=DEV, generator=gen)  # a quarter near rows
+    Q[: nq // 4] = X[plant] + 0.6 / D ** 0.5 * torch.randn(nq // 4, D, device=DEV, generator=gen)
+    Q = Q / Q.norm(dim=1, keepdim=True)
+    X16, Q16 = X.to(torch.bfloat16), Q.to(torch.bfloat16)
+    lab = torch.randint(0, 40, (N,), device=DEV, generator=gen, dtype=torch.int32)
+    ql = torch.randint(0, 40, (nq,), device=DEV, generator=gen, dtype=torch.int32)
+    ql[: nq // 4] = lab[plant]
+    floor = 0.5 - 0.01
+    (sa, ra), (sb, rb) = flat_topk_dual(X16, Q16, 16, row_label=lab, q_label=ql, floor=floor)
+    X8, rs = quantize_i8_rows(X16)
+    Q8, qs = quantize_i8_rows(Q16)
+    margin = torch.full((nq,), 0.02, device=DEV)
+    st = []
+    (ta, ia), (tb, ib) = flat_topk_dual_i8(X8, rs, Q8, qs, X16, Q16, 16, row_label=lab, q_label=ql, margin=margin,
+                                           margin_rig=margin, floor=floor, floor_tol=0.005, stats=st)
+    torch.cuda.synchronize()
+    (oa, _), (ob, _), _cap = st
+    fell_back = float(((oa != 0) | (ob != 0)).float().mean())
+    assert fell_back < 0.02, fell_back
+    assert int((sa[: nq // 4, 0] > 0.5).sum()) > nq // 8  # the planted rows clear the floor
+    for s0, r0, s1, r1 in ((sa, ra, ta, ia), (sb, rb, tb, ib)):
+        keep = s0 >= floor + 0.005
+        assert torch.equal(torch.where(keep, r0, -1), torch.where(s1 >= floor + 0.005, r1, -1))
+        assert torch.allclose(s0[keep], s1[keep], atol=1e-4, rtol=0)
+
+
 def test_flat_topk_dual_i8_overflowing_lists_gpu():
     """Tight topics (every row of a topic at cos > 0.9 to its queries): the
     int8 dual scan's block records and per-query lists overflow, cand_select

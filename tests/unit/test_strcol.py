@@ -55,3 +55,19 @@ def test_tenant_graph_uses_native_columns():
     g.add_nodes(["n1", "n2"], ["c1", "c2"], [[1.0, 0, 0, 0], [0, 1.0, 0, 0]], shard=g.shard_id("s"))
     assert type(g.ids).__name__ == "StrColumn" and not gc.is_tracked(g.ids)
     assert g.ids[g.row_of["n2"]] == "n2" and g.content[0] == "c1"
+
+
+def test_items_are_str_or_none_and_type_refcount_balanced():
+    import sys
+    c = rt.StrColumn(["a", None])
+    for bad in (lambda: c.append(1), lambda: c.extend(["ok", [c]]), lambda: c.__setitem__(0, b"x"),
+                lambda: rt.StrColumn([object()])):
+        with pytest.raises(TypeError):
+            bad()
+    assert c.tolist() == ["a", None]  # a rejected extend appends nothing
+    tp = type(c)
+    before = sys.getrefcount(tp)
+    cols = [rt.StrColumn(["x"]) for _ in range(1000)]
+    del cols
+    gc.collect()
+    assert sys.getrefcount(tp) == before  # each instance gives its type reference back
