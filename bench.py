@@ -184,6 +184,41 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
+HBM_PER_GPU = 288e9  # MI355X HBM3E per GPU (bytes)
+
+
+def hbm_plan(rows: int, dim: int, batch: int, consolidate_convs: int, facts: int = 8) -> dict:
+    """Per-rank HBM plan of every section of this bench (they run one after
+    another, each freeing its tenant: the job's peak is the largest section),
+    from the tenant's column layout (TenantGraph.hbm_bytes_per_row) plus each
+    section's large workspaces. Rows are PER RANK, so the plan does not change
+    with --gpus (weak scaling) except for the row-sharded buffer's ghost rows
+    (edge endpoints held elsewhere; bounded by its edges). Used by
+    --hbm-check and tests/distributed/test_bench_cpu.py; the GPU run reports
+    the measured peaks next to it (hbm_peak_gib)."""
+    from lazzaro_amd.engine.tenant_graph import TenantGraph
+    bpr = TenantGraph.hbm_bytes_per_row(dim)
+    eb = TenantGraph.EDGE_BYTES
+    cap = int(rows * 1.05)  # reserve slack of the loaders
+    encoder = 0.5e9  # bge-base weights + activations of a 1024 x 64-token batch
+    # store search: int8 queries + candidate lists (cap 2048 x 16 slots x 8 B per query) + block records
+    search_ws = batch * (2048 * 16 * 8 + 4 * dim) + 256 * 8 * 2048 * 16
+    head = cap * bpr + encoder + search_ws
+    # consolidation: the tenant, 2 x rows seeded edges (+1/8 append slack), the
+    # dual scan's two candidate lists, k-means (4096 centroids, per-row labels)
+    F = consolidate_convs * facts
+    dual_ws = 2 * F * (2048 * 16 * 8) + 256 * 8 * 2048 * 16 * 2
+    kmeans = 4096 * dim * 6 + rows * 16
+    cons = cap * bpr + 2 * rows * eb * 9 // 8 + encoder + dual_ws + kmeans
+    sharded = cap * bpr + 2 * rows * eb * 9 // 8 + F * 2 * (bpr + 64) + encoder + dual_ws + kmeans
+    secs = {"headline": head, "consolidate": cons, "consolidate_persistent_graph": cons,
+            "consolidate_sharded": sharded}
+    peak = max(secs.values())
+    return {"bytes_per_row": bpr, "sections_gib": {k: round(v / 2 ** 30, 2) for k, v in secs.items()},
+            "peak_gib": round(peak / 2 ** 30, 2), "hbm_gib": round(HBM_PER_GPU / 2 ** 30, 2),
+            "fits": peak <= 0.92 * HBM_PER_GPU}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,7 +250,13 @@ def main():
                          "are array-backed, so the loop allocates nothing per row; see gc_in_timed_loop)")
     ap.add_argument("--no-launch", action="store_true",
                     help="--gpus 1 without the torch.distributed.run child (no process group, no collectives)")
+    ap.add_argument("--hbm-check", action="store_true",
+                    help="print the per-rank HBM plan of every section for these flags (no GPU) and exit")
     a = ap.parse_args()
+    if a.hbm_check:
+        plan = hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs)
+        print(json.dumps({"n_gpus": a.gpus, "rows_per_rank": a.rows, **plan}))
+        sys.exit(0 if plan["fits"] else 1)
 
     # every GPU job runs as torch.distributed.run ranks -- N = 1 included, so
     # the driver's 1-GPU run times the RCCL all-to-all / all-gather calls of
@@ -505,6 +546,15 @@ def main():
     S_tok = int(emb.tok.encode_batch(pool[0], emb.max_len)[0].shape[1])
     lens = emb.tok.encode_batch(pool[0], emb.max_len)[1]
 
+    # measured per-rank HBM peak of each section, next to hbm_plan's estimate
+    hbm_peak = {}
+
+    def peak(name):
+        if dev.type == "cuda":
+            hbm_peak[name] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
+            torch.cuda.reset_peak_memory_stats(dev)
+    peak("headline")
+
     # ---- second half of the metric: consolidate turns/sec ----
     consolidate = persistent = None
     if a.consolidate_steps > 0:
@@ -516,6 +566,7 @@ def main():
         from bench_consolidate import run as run_consolidate
         consolidate = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
                                       dim=a.dim, stream=a.consolidate_stream)
+        peak("consolidate")
         if a.persistent_graph:
             # same pipeline, MemorySystem(prune_threshold=0): the 2 x rows seeded
             # edges are never pruned (decay still scales every edge each
@@ -525,6 +576,7 @@ def main():
                 torch.cuda.empty_cache()
             persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
                                          dim=a.dim, prune_threshold=0.0, stream=a.consolidate_stream)
+            peak("consolidate_persistent_graph")
     sharded = None
     if a.sharded_steps > 0:
         # config 4 as ONE buffer row-sharded over the ranks: collectives in
@@ -541,6 +593,7 @@ def main():
         # per-rank scan stays (own facts) x (own rows) as ranks are added
         sharded = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_steps, 1, emb, dim=a.dim,
                               clustered=True)
+        peak("consolidate_sharded")
     res = {
         "metric": METRIC,
         "value": round(qps, 2),
@@ -580,6 +633,8 @@ def main():
         "gc_in_timed_loop": {"startup_heap_frozen": bool(a.gc_freeze),
                              **{f"gen{k}": {"passes": v[0], "ms": round(v[1] * 1e3, 2)} for k, v in gc_log.items()}},
         "prewarm_s": round(t_pre, 1),
+        "hbm_per_rank": {"peak_gib_measured": hbm_peak,
+                         "plan": hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs)},
     }
     if consolidate is not None:
         res["consolidate_turns_per_s"] = consolidate["turns_per_s"]

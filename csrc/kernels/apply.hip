@@ -1,0 +1,290 @@
+// Native applier of a consolidation batch's segments (consolidate_batch at the
+// reference cadence, reference memory_system.py:580-649, :651-933, :951-1010).
+//
+// The host planner (csrc/runtime/batch_plan.cpp) decides every insert, link,
+// eviction and salience change of B conversations up front; the plan is then
+// applied to the tenant's HBM columns in segments that end at the
+// run_consolidation points (~43 per 128-conversation step). Driving each
+// segment from Python cost ~0.45 ms of interpreter time for ~0.1 ms of GPU
+// work, so the GPU sat idle half of a step (profiles/r5/consolidation_device_busy).
+//
+// Here the whole segment loop is ONE call: Python uploads the batch's data in
+// one pinned block and passes a small op program; this loop issues each
+// segment's fixed kernel chain back to back -- decay (+ deferred prune flags),
+// touched-row updates, node inserts (columns + embeddings), super-node parent
+// links, edge appends, the segment end (victims ghosted, edges flagged, ONE
+// 8-byte-per-victim read of the survivors / prune counts, stable compaction into
+// the other buffer set), and at each run_consolidation point the component
+// digest (digest.hip dg_small_kernel) and the profile's first shard rows
+// (tg_first_rows_kernel) into per-point capture slots. The host bookkeeping
+// (ids, counters, store deletes, captures) is replayed by the caller from
+// the per-segment records this call returns (engine/native_apply.py).
+//
+// The op program (int64 words):
+//   DECAY   steps                       edge decay + keep flags over the current
+//                                       edges, shard-node salience decay over n
+//   ROWS    rows_off row0 m vals_off present consts_off kind_v stored_v
+//                                       tg_set_rows (offsets: bytes into the block)
+//   EMB     x_row m row0                tg_write_emb of rows x[x_row .. +m) of the
+//                                       embedding block at rows row0 ..
+//   N       n                           the tenant's row count from here on
+//   SHARD   code delta                  host shard-node count (first-rows targets)
+//   APPEND  vals_off m                  tg_append_edges at the current edge count
+//   SEGEND  vrows_off nv seg            victims + deferred prune + compaction
+//   POINT   p                           digest + first rows into slot p
+#include "lzk_common.h"
+
+extern "C" {
+int lzk_tg_decay(float* w, long ne, float keep, float thr, unsigned char* flag, int* block_cnt, float* sal,
+                 const unsigned char* kind, const unsigned char* sup, long nn, int decay_nodes, int steps,
+                 void* stream);
+int lzk_tg_set_rows(const long* rows, long row0, int m, const double* vals, int present, const double* consts,
+                    float* sal, int* acc, double* last, double* ts, int* shard, unsigned char* sup, int* parent,
+                    unsigned char* kind, unsigned char* stored, unsigned char* dirty, int kind_v, int stored_v,
+                    void* stream);
+int lzk_tg_write_emb(const float* x, long ldx, const unsigned char* has, int m, int D, const long* rows, long row0,
+                     float* emb32, long ld32, void* emb16, long ld16, void* emb8, long ld8, float* rs8, float* sqn,
+                     double* sumsq, float* rs_max, float* dv_max, unsigned char* has_emb, void* stream);
+int lzk_tg_append_edges(const double* vals, int m, long ne, int meta_bits, double now, int* src, int* dst, float* w,
+                        int* co, double* lu, int* meta, void* stream);
+int lzk_tg_seg_end(const long* vrows, int nv, unsigned char* kind, const unsigned char* sup, const int* shard,
+                   unsigned char* stored, int unstore, unsigned* rmb, const int* src, const int* dst, const int* meta,
+                   long ne, const unsigned char* prev, long nprev, unsigned char* flag, int* bc, int* info,
+                   void* stream);
+int lzk_tg_compact(const unsigned char* flag, const int* block_off, long ne, const int* src, const int* dst,
+                   const float* w, const int* co, const double* lu, const int* meta, int* osrc, int* odst, float* ow,
+                   int* oco, double* olu, int* ometa, int* dsrc, int* ddst, int* dmeta, void* stream);
+int lzk_dg_small(const int* src, const int* dst, const float* w, int ne, const unsigned char* kind,
+                 const unsigned char* sup, const int* shard, long n, int min_size, double min_avg_w, int take,
+                 void* ws, long long* out, int cap, int* out_cnt, void* stream);
+int lzk_tg_first_rows(const unsigned char* kind, const unsigned char* sup, const int* shard, long n, const int* tc,
+                      const int* tt, const int* to, int nt, long* out, void* stream);
+int lzk_dg_small_max_edges();
+}
+
+namespace {
+
+enum Op : long { OP_END = 0, OP_DECAY, OP_ROWS, OP_EMB, OP_N, OP_SHARD, OP_APPEND, OP_SEGEND, OP_POINT };
+
+// column pointers, in this order (ApplyCols.* of engine/native_apply.py)
+struct Cols {
+  float* sal;
+  int* acc;
+  double* last;
+  double* ts;
+  int* shard;
+  unsigned char* sup;
+  int* parent;
+  unsigned char* kind;
+  unsigned char* stored;
+  unsigned char* dirty;
+  float* emb32;
+  void* emb16;
+  void* emb8;
+  float* rs8;
+  float* sqn;
+  double* sumsq;
+  float* rs_max;
+  float* dv_max;
+  unsigned char* has_emb;
+  unsigned* rmb;
+};
+
+struct EdgeSet {
+  int* src;
+  int* dst;
+  float* w;
+  int* co;
+  double* lu;
+  int* meta;
+};
+
+inline EdgeSet edge_set(void* const* p) {
+  return EdgeSet{(int*)p[0], (int*)p[1], (float*)p[2], (int*)p[3], (double*)p[4], (int*)p[5]};
+}
+
+}  // namespace
+
+// Returns 0 or a HIP error / hipErrorInvalidValue (bad program). On return:
+//   state[0] = final edge count, state[1] = buffer set holding them (0 = A,
+//   1 = B), state[2] = dropped edges written, state[3] = ops executed.
+//   seg_out[4 s ..] = (pruned by the decay, surviving edges, dropped edges
+//   written by this segment, offset of its victim records in vinfo) per
+//   segment; vinfo = (kind, sup, shard) x nv per segment, concatenated.
+//   point_out[3 p ..] = (edges at the point, digest written (0 = no edges:
+//   an empty digest), first-rows entries) per point.
+// shard_count (host, int64 [ncodes]) is updated like the host's counters.
+LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk, const float* xblk, int D,
+                                  void* const* colp, long ld32, long ld16, long ld8, void* const* ebuf_a,
+                                  void* const* ebuf_b, long ne0, long cap_e, float thr, float keep, double now,
+                                  int meta_bits, int unstore, unsigned char* flag_a, unsigned char* flag_b, int* bc,
+                                  int* info, long info_cap, int* dsrc, int* ddst, int* dmeta, long drop_cap,
+                                  long long* dg_out, int dg_cap, void* dg_ws, int* dg_cnt, long* fr_out, int fr_k,
+                                  long* shard_count, int ncodes, long* seg_out, int* vinfo, long vinfo_cap,
+                                  long* point_out, long* state, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const Cols& C = *reinterpret_cast<const Cols*>(colp);
+  EdgeSet E[2] = {edge_set(ebuf_a), edge_set(ebuf_b)};
+  int cur = 0;
+  long ne = ne0, n = 0, drop_total = 0, vinfo_used = 0;
+  // the deferred prune of the open segment: keep flags over its first nprev edges
+  unsigned char* prev = nullptr;
+  long nprev = 0;
+  const int dg_max = lzk_dg_small_max_edges();
+  long pc = 0, ops = 0;
+  int rc = 0;
+#define LZK_RC(x)                  \
+  do {                             \
+    rc = (x);                      \
+    if (rc != 0) goto done;        \
+  } while (0)
+  while (pc < nprog) {
+    const long op = prog[pc];
+    ++ops;
+    if (op == OP_END) break;
+    if (op == OP_DECAY) {
+      const int steps = (int)prog[pc + 1];
+      pc += 2;
+      // flag_a: the decay's keep flags (flag_b: the segment end's); thr = -inf:
+      // nothing is pruned, no flags (TenantGraph.segment_begin)
+      prev = (ne > 0 && thr > -__builtin_huge_valf()) ? flag_a : nullptr;
+      nprev = ne;
+      LZK_RC(lzk_tg_decay(E[cur].w, ne, keep, thr, prev, prev ? bc : nullptr, C.sal, C.kind, C.sup, n, n ? 1 : 0,
+                          steps, stream));
+      // the decay's block counts are only needed by a compaction of these
+      // flags alone, which never happens here (the segment end re-flags)
+    } else if (op == OP_ROWS) {
+      const long rows_off = prog[pc + 1], row0 = prog[pc + 2];
+      const int m = (int)prog[pc + 3];
+      const long vals_off = prog[pc + 4];
+      const int present = (int)prog[pc + 5];
+      const long consts_off = prog[pc + 6];
+      const int kind_v = (int)prog[pc + 7], stored_v = (int)prog[pc + 8];
+      pc += 9;
+      LZK_RC(lzk_tg_set_rows(rows_off >= 0 ? (const long*)(blk + rows_off) : nullptr, row0, m,
+                             (const double*)(blk + vals_off), present, (const double*)(blk + consts_off), C.sal,
+                             C.acc, C.last, C.ts, C.shard, C.sup, C.parent, C.kind, C.stored, C.dirty, kind_v,
+                             stored_v, stream));
+    } else if (op == OP_EMB) {
+      const long xr = prog[pc + 1];
+      const int m = (int)prog[pc + 2];
+      const long row0 = prog[pc + 3];
+      pc += 4;
+      LZK_RC(lzk_tg_write_emb(xblk + xr * D, D, nullptr, m, D, nullptr, row0, C.emb32, ld32, C.emb16, ld16, C.emb8,
+                              ld8, C.rs8, C.sqn, C.sumsq, C.rs_max, C.dv_max, C.has_emb, stream));
+    } else if (op == OP_N) {
+      n = prog[pc + 1];
+      pc += 2;
+    } else if (op == OP_SHARD) {
+      const long code = prog[pc + 1], delta = prog[pc + 2];
+      pc += 3;
+      if (code < 0 || code >= ncodes) { rc = (int)hipErrorInvalidValue; goto done; }
+      shard_count[code] += delta;
+    } else if (op == OP_APPEND) {
+      const long vals_off = prog[pc + 1];
+      const int m = (int)prog[pc + 2];
+      pc += 3;
+      if (ne + m > cap_e) { rc = (int)hipErrorInvalidValue; goto done; }
+      const EdgeSet& e = E[cur];
+      LZK_RC(lzk_tg_append_edges((const double*)(blk + vals_off), m, ne, meta_bits, now, e.src, e.dst, e.w, e.co, e.lu,
+                                 e.meta, stream));
+      ne += m;
+    } else if (op == OP_SEGEND) {
+      const long vrows_off = prog[pc + 1];
+      const int nv = (int)prog[pc + 2];
+      const long s = prog[pc + 3];
+      pc += 4;
+      long* so = seg_out + 4 * s;
+      so[0] = 0;
+      so[1] = ne;
+      so[2] = 0;
+      so[3] = vinfo_used;
+      if (nv == 0 && prev == nullptr) continue;  // nothing to flag, nobody removed
+      if (3L * nv + 2 > info_cap || vinfo_used + 3L * nv > vinfo_cap) { rc = (int)hipErrorInvalidValue; goto done; }
+      const EdgeSet& e = E[cur];
+      LZK_RC(lzk_tg_seg_end(nv ? (const long*)(blk + vrows_off) : nullptr, nv, C.kind, C.sup, C.shard, C.stored,
+                            unstore, C.rmb, e.src, e.dst, e.meta, ne, prev, prev ? nprev : 0,
+                            ne ? flag_b : nullptr, ne ? bc : nullptr, info, stream));
+      // the one host read of the segment: victims' (kind, sup, shard),
+      // survivors, pruned
+      if (nv && hipMemcpyAsync(vinfo + vinfo_used, info, sizeof(int) * (3L * nv), hipMemcpyDeviceToHost, st) !=
+                    hipSuccess) {
+        rc = (int)hipGetLastError();
+        goto done;
+      }
+      int tail[2] = {0, 0};
+      if (hipMemcpyAsync(tail, info + 3L * nv, sizeof(tail), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        rc = (int)hipGetLastError();
+        goto done;
+      }
+      const long n_out = ne ? tail[0] : 0;
+      so[0] = prev ? tail[1] : 0;
+      // the victims leave the host counters like TenantGraph.segment_end
+      for (int i = 0; i < nv; ++i) {
+        const int k = vinfo[vinfo_used + i], sp = vinfo[vinfo_used + nv + i], sh = vinfo[vinfo_used + 2 * nv + i];
+        if (k == 1 && !sp && sh >= 0 && sh < ncodes) shard_count[sh] -= 1;
+      }
+      vinfo_used += 3L * nv;
+      if (ne && n_out != ne) {
+        const long nd = ne - n_out;
+        const bool track = dsrc != nullptr;
+        if (track && drop_total + nd > drop_cap) { rc = (int)hipErrorInvalidValue; goto done; }
+        const EdgeSet& o = E[cur ^ 1];
+        LZK_RC(lzk_tg_compact(flag_b, bc, ne, e.src, e.dst, e.w, e.co, e.lu, e.meta, o.src, o.dst, o.w, o.co, o.lu,
+                              o.meta, track ? dsrc + drop_total : nullptr, track ? ddst + drop_total : nullptr,
+                              track ? dmeta + drop_total : nullptr, stream));
+        if (track) {
+          so[2] = nd;
+          drop_total += nd;
+        }
+        cur ^= 1;
+        ne = n_out;
+      }
+      so[1] = ne;
+      prev = nullptr;
+      nprev = 0;
+    } else if (op == OP_POINT) {
+      const long p = prog[pc + 1];
+      pc += 2;
+      long* po = point_out + 3 * p;
+      po[0] = ne;
+      po[1] = 0;
+      po[2] = 0;
+      if (ne > 0) {  // TenantGraph.digest_capture on the one-block digest (ne <= dg_max: the caller's bound)
+        if (ne > dg_max || 2L * ne > dg_cap) { rc = (int)hipErrorInvalidValue; goto done; }
+        const EdgeSet& e = E[cur];
+        LZK_RC(lzk_dg_small(e.src, e.dst, e.w, (int)ne, C.kind, C.sup, C.shard, n, 3, 0.3, fr_k, dg_ws,
+                            dg_out + p * 2L * dg_cap, dg_cap, dg_cnt, stream));
+        po[1] = 1;
+      }
+      // TenantGraph._first_rows_dev: per-shard targets from the host counts
+      int tc[64], tt[64], to[64], nt = 0, need = fr_k, off = 0;
+      for (int c = 0; c < ncodes && need > 0; ++c) {
+        const long cnt = shard_count[c];
+        if (cnt <= 0) continue;
+        if (nt == 64) { rc = (int)hipErrorInvalidValue; goto done; }
+        const int t = (int)(cnt < need ? cnt : need);
+        tc[nt] = c;
+        tt[nt] = t;
+        to[nt] = off;
+        ++nt;
+        off += t;
+        need -= t;
+      }
+      if (nt) LZK_RC(lzk_tg_first_rows(C.kind, C.sup, C.shard, n, tc, tt, to, nt, fr_out + p * (long)fr_k, stream));
+      po[2] = off;
+    } else {
+      rc = (int)hipErrorInvalidValue;
+      goto done;
+    }
+  }
+done:
+#undef LZK_RC
+  state[0] = ne;
+  state[1] = cur;
+  state[2] = drop_total;
+  state[3] = ops;
+  if (rc == 0) rc = (int)hipGetLastError();
+  return rc;
+}

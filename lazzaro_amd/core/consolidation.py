@@ -31,6 +31,7 @@ Fixes, all behind documented defaults:
 from __future__ import annotations
 
 import json
+import math
 import os
 import time
 from typing import Dict, List, Sequence, Set, Tuple
@@ -942,7 +943,7 @@ class ConsolidationMixin:
                                 1.0 - DECAY_RATE, B)
         try:
             self._apply_planned_segments(pl, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
-                                         defer, pending)
+                                         defer, pending, cc=cc)
         finally:
             if cc:
                 g.cc_end()
@@ -953,8 +954,207 @@ class ConsolidationMixin:
         if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
             self._maybe_cluster(self.conversation_count - 1)
 
+    # the segments of a plan through the native applier (csrc/kernels/apply.hip
+    # via engine/native_apply.py) where eligible; False: the per-segment path
+    NATIVE_APPLY = True
+
+    def _native_apply_ok(self, pl: Dict, defer: bool, cc: bool, thr, E) -> bool:
+        """The native applier covers the steady state of the reference
+        cadence on the GPU: captures deferred (no per-point host read), no
+        per-conversation commit, the decay's prune on (auto_prune), no
+        incremental components (graphs whose edges fit the one-block digest,
+        digest.hip dg_small_kernel, for the whole batch), an int8 or no
+        low-precision copy, and every insert a fresh row in plan order."""
+        from ..engine import native_apply as NA
+        from ..engine import tenant_graph as TG
+        g = self.graph
+        if not (self.NATIVE_APPLY and g.on_gpu and defer and not self._commit_each and thr is not None and not cc
+                and TG.SEG_END_KERNEL and TG.SET_ROWS_KERNEL and not g._digest_sorted and NA.available()):
+            return False
+        if g.emb8 is not None and g.emb8.dtype != torch.int8:
+            return False
+        if g.dim is None or g.dim > 1024 or (E is not None and not E.is_cuda) or PROFILE_CONTENTS > 64:
+            return False
+        from ..ops import tenant_ops as T
+        app = sum(len(seg["edge_src"]) for seg in pl["segments"])
+        if g.num_edges + app > T.dg_small_max_edges():
+            return False
+        # every insert is the next fresh row, in plan order (the add_nodes bulk path)
+        fact_key = np.asarray(pl["fact_key"], np.int64)
+        n = g.n
+        nid = self.node_counter
+        for seg in pl["segments"]:
+            kinds = np.asarray(seg["ins_kind"]).tolist()
+            idx = np.asarray(seg["ins_idx"]).tolist()
+            for k, j in zip(kinds, idx):
+                key = int(fact_key[j]) if k == 0 else int(pl["supers"][j]["key"])
+                if key != n:
+                    return False
+                n += 1
+                if k == 0:
+                    nid += 1
+                    if f"node_{nid}" in g.row_of:
+                        return False
+        return True
+
+    def _apply_planned_native(self, pl, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
+                              pending) -> None:
+        """:meth:`_apply_planned_segments` through ONE native call per run of
+        segments (a run ends at a segment that runs a cluster pass): the
+        device work of every segment is issued by csrc/kernels/apply.hip
+        from one uploaded block, and the host bookkeeping is replayed here in
+        segment order from its records (engine/native_apply.py)."""
+        segs = pl["segments"]
+        i = 0
+        while i < len(segs):
+            j = i
+            while j < len(segs) - 1 and not segs[j]["cluster"]:
+                j += 1
+            self._native_run(segs[i:j + 1], pl["supers"], fact_key, fact_of, facts, codes, E, id_of, thr, now,
+                             stats, count0, pending)
+            i = j + 1
+
+    def _native_run(self, segs, supers, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
+                    pending) -> None:
+        from ..engine.native_apply import SegmentProgram
+        g = self.graph
+        stored = self._store_binds_graph()
+        # (the edge type is registered only by a segment that links, as append_edges_host does)
+        etype = g.etype("relates_to") if any(len(seg["edge_src"]) for seg in segs) else 0
+        # a prune threshold <= 0 prunes nothing: no keep flags (TenantGraph.segment_begin)
+        prog = SegmentProgram(g, now, thr if thr is not None and thr > 0.0 else float("-inf"), 1.0 - DECAY_RATE,
+                              etype, PROFILE_CONTENTS)
+        n0 = g.n
+        g.reserve(n0 + sum(len(seg["ins_kind"]) for seg in segs))  # no column moves under the native loop
+        n = n0
+        prog.n(n)
+        host = []  # per segment: the inserts' host columns and the store deletes, replayed after the run
+        with tracer.stage("ap_build", "cpu"):
+            for seg in segs:
+                ik = np.asarray(seg["ins_kind"])
+                for key in sorted(fact_key[np.asarray(seg["ins_idx"], np.int64)[ik == 0]].tolist()):
+                    id_of[key] = self._generate_node_id()
+                prog.decay(int(seg["c1"]) - int(seg["c0"]) + 1)
+                tr = np.asarray(seg["tch_rows"], np.int64)
+                if tr.size:
+                    prog.touch_rows(tr, seg["tch_sal"], seg["tch_acc"], seg["tch_last"])
+                kinds = ik.tolist()
+                idx = np.asarray(seg["ins_idx"]).tolist()
+                isal = np.asarray(seg["ins_sal"], np.float32)
+                iacc = np.asarray(seg["ins_acc"], np.int32)
+                ilast = np.asarray(seg["ins_last"], np.float64)
+                ins = []
+                k = 0
+                while k < len(kinds):
+                    if kinds[k] == 0:
+                        k2 = k
+                        while k2 < len(kinds) and kinds[k2] == 0:
+                            k2 += 1
+                        js = idx[k:k2]
+                        m = len(js)
+                        sh = codes[js].astype(np.int32)
+                        prog.insert_rows(n, m, {"sal": isal[k:k2], "acc": iacc[k:k2], "last": ilast[k:k2],
+                                                "shard": sh}, stored)
+                        prog.embeddings(E[torch.as_tensor(js, dtype=torch.long).to(E.device)], n)
+                        cnt = np.bincount(sh[sh >= 0], minlength=1)
+                        for c in np.nonzero(cnt)[0].tolist():
+                            prog.shard_delta(c, int(cnt[c]))
+                        ins.append(("facts", [id_of[int(fact_key[j])] for j in js],
+                                    [facts[j]["content"] for j in js],
+                                    [facts[j].get("type", "semantic") for j in js], sh))
+                        n += m
+                        prog.n(n)
+                        k = k2
+                    else:
+                        sp = supers[idx[k]]
+                        children = np.asarray(sp["children"], np.int64).tolist()
+                        skey = shard_keys_of(g, int(sp["code"]))
+                        ch_ids = [id_of[r] if r in fact_of else g.ids[r] for r in children]
+                        content = [facts[fact_of[r]]["content"] if r in fact_of else g.content[r]
+                                   for r in children[:3]]
+                        summary = f"Topic: {skey}. Contains memories about: " + "; ".join(content)
+                        emb = self._plan_super_emb[tuple(children)]
+                        prog.insert_rows(n, 1, {"sal": float(isal[k]), "acc": int(iacc[k]), "last": float(ilast[k]),
+                                                "shard": int(sp["code"]), "sup": 1}, False)
+                        prog.embeddings(emb.reshape(1, -1), n)
+                        prog.set_parent(children, n)
+                        ins.append(("super", f"super_{skey}_{int(now)}", summary, ch_ids, n))
+                        n += 1
+                        prog.n(n)
+                        k += 1
+                es = np.asarray(seg["edge_src"], np.int64)
+                if es.size:
+                    prog.append_edges(es, seg["edge_dst"], seg["edge_w"], seg["edge_code"])
+                vic = np.asarray(seg["victims"], np.int64).tolist()
+                prog.segment_end(sorted({r for r in vic if 0 <= r < n}))
+                if seg["consolidate"]:
+                    prog.point()
+                host.append((ins, [g.ids[r] if r < n0 else None for r in vic], vic))
+        with tracer.stage("ap_native", g.device):
+            res = prog.run(g.shard_count)
+        # ---- host replay, segment by segment (TenantGraph.add_nodes / segment_end, _rc_device)
+        p = 0
+        for s, (seg, (ins, vid0, vic)) in enumerate(zip(segs, host)):
+            steps = int(seg["c1"]) - int(seg["c0"]) + 1
+            g.decay_log += steps * math.log1p(-DECAY_RATE)
+            g._bump(edges=True)
+            for it in ins:
+                if it[0] == "facts":
+                    _, ids, contents, types, sh = it
+                    m = len(ids)
+                    r0 = g.n
+                    g.ids.extend(ids)
+                    g.content.extend(contents)
+                    g.types.extend(types)
+                    g.row_of.update(zip(ids, range(r0, r0 + m)))
+                    g.n = r0 + m
+                    g.n_sumsq += m
+                    cnt = np.bincount(sh[sh >= 0], minlength=len(g.shard_count))
+                    for c in np.nonzero(cnt)[0]:
+                        g.shard_count[int(c)] += int(cnt[c])
+                    if g.deleted_ids:
+                        for x in ids:
+                            g.deleted_ids.pop(x, None)
+                    g.last_add_rows = range(r0, r0 + m)
+                else:
+                    _, sid, summary, ch_ids, r = it
+                    g.ids.append(sid)
+                    g.content.append(summary)
+                    g.types.append("semantic")
+                    g.row_of[sid] = r
+                    g.n = r + 1
+                    g.n_sumsq += 1
+                    g.n_super += 1
+                    g.children[r] = list(ch_ids)
+                    if g.deleted_ids:
+                        g.deleted_ids.pop(sid, None)
+                    g.last_add_rows = [r]
+                if not g._dv_acc_pending:
+                    g._norm_dev_pending.append(g._dv_acc[0])
+                    g._dv_acc_pending = True
+                g._bump(store=True)
+            stats["pruned"] += prog.finish_segment(res, s)
+            ids = [x if x is not None else g.ids[r] for x, r in zip(vid0, vic)]
+            if ids:
+                with tracer.stage("ap_store_delete", "cpu"):
+                    self._store_delete(ids, graph_unstored=True)
+            self.conversation_count = count0 + int(seg["c1"]) + 1
+            if seg["consolidate"]:
+                stats["consolidations"] += 1
+                self._say("🔄 Running consolidation...")
+                dig, first = prog.captures(res, p)
+                p += 1
+                pending.append({"results": [], "digest": dig, "pruned": 0, "first": first})
+            if seg["cluster"]:
+                self._maybe_cluster(self.conversation_count - 1)
+        if list(res["shard_count"][:len(g.shard_count)]) != list(g.shard_count):
+            raise RuntimeError("native segment apply diverged from the host shard counts")
+
     def _apply_planned_segments(self, pl, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
-                                defer, pending) -> None:
+                                defer, pending, cc=False) -> None:
+        if self._native_apply_ok(pl, defer, cc, thr, E):
+            return self._apply_planned_native(pl, fact_key, fact_of, facts, codes, E, id_of, thr, now, stats, count0,
+                                              pending)
         for seg in pl["segments"]:
             # node ids as the segment's facts are inserted (keys grow segment by
             # segment): a per-segment commit persists the sequential counter

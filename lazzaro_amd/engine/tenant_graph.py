@@ -411,6 +411,19 @@ class TenantGraph:
         self.cap = cap
         self._alloc_gen = getattr(self, "_alloc_gen", 0) + 1
 
+    @classmethod
+    def hbm_bytes_per_row(cls, dim: int, lowp: str = "i8", lean: bool = False) -> int:
+        """HBM bytes one row of a GPU tenant holds (:meth:`_alloc`'s
+        columns): fp32 vector, bf16 scan copy (not in the lean layout), the
+        low-precision copy + row scale, |x|^2 and the node columns."""
+        dp = _pad64(int(dim))
+        b = 4 * int(dim) + (0 if lean else 2 * dp) + 4
+        if lowp:
+            b += dp + (4 if lowp == "i8" else 0)
+        return b + sum(torch.empty((), dtype=dt).element_size() for _, dt, _ in cls.NODE_COLS)
+
+    EDGE_BYTES = 4 + 4 + 4 + 4 + 8 + 4  # src, dst, w, co, lu, meta
+
     def _dev_rows(self, rows: Sequence[int]) -> torch.Tensor:
         """A short host row list as an int64 device tensor (pinned, async on a
         GPU: no host-blocking pageable copy)."""

@@ -72,3 +72,43 @@ def test_bench_rejects_gpus_world_mismatch(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL, cwd=str(tmp_path),
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stdout + r.stderr)
+
+
+def test_bench_eight_ranks_cpu(tmp_path):
+    """The 8-GPU job's flow rehearsed on 8 gloo/CPU ranks, launched exactly as
+    the driver launches the scaling run (torch.distributed.run, 8 processes):
+    headline, routed search (7/8 of each front end's queries remote, every
+    answer equal to its owner's own search), global search, per-rank
+    consolidation and the row-sharded buffer over all 8 ranks."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--rows", "3000", "--dim", "128", "--model", "tiny", "--batch", "16", "--steps", "1",
+           "--warmup", "1", "--prewarm-s", "0", "--recall-queries", "4", "--consolidate-steps", "1",
+           "--consolidate-convs", "2", "--no-persistent-graph", "--sharded-steps", "1", "--global-batch", "4",
+           "--cpu"]
+    env = dict(os.environ, PYTHONPATH=ROOT, LZK_BENCH_DB=str(tmp_path / "db"), OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "tenant-dp8" and d["value"] > 0
+    assert d["config"]["global_batch"] == 8 * 16
+    _check_serving(d, 16)
+    assert d["consolidate_turns_per_s"] > 0
+    sh = d["consolidate_sharded"]
+    assert sh["turns_per_s"] > 0 and sh["buffer_nodes_total"] == 8 * 3000
+
+
+def test_hbm_plan_eight_gpus_ten_million_rows_fits():
+    """Every section of the 8-GPU job at the headline size (10M x 768 rows per
+    rank) fits one MI355X's HBM with room to spare (bench.py hbm_plan; the GPU
+    run reports the measured per-section peaks next to it)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--hbm-check", "--gpus", "8", "--rows",
+                        "10000000"], env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 8 and d["fits"]
+    assert set(d["sections_gib"]) == {"headline", "consolidate", "consolidate_persistent_graph", "consolidate_sharded"}
+    assert d["peak_gib"] < 0.5 * d["hbm_gib"]
