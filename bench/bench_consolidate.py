@@ -192,9 +192,11 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
         tprof.__enter__()
     t0 = time.perf_counter()
     agg = {}
-    for st in run_steps(steps):
+    for i, st in enumerate(run_steps(steps)):
         for k, v in st.items():
             agg[k] = agg.get(k, 0) + v
+        if comm.rank == 0:  # progress (stderr, one short line per step)
+            print(f"consolidate step {i + 1}/{steps} {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
     ms.flush_persistence()  # write-behind commits of the timed steps land inside the timed region
     _sync(dev)
     if tprof is not None:

@@ -32,6 +32,11 @@
 //   APPEND  vals_off m                  tg_append_edges at the current edge count
 //   SEGEND  vrows_off nv seg            victims + deferred prune + compaction
 //   POINT   p                           digest + first rows into slot p
+#include <algorithm>
+#include <cstring>
+#include <utility>
+#include <vector>
+
 #include "lzk_common.h"
 
 extern "C" {
@@ -60,6 +65,17 @@ int lzk_dg_small(const int* src, const int* dst, const float* w, int ne, const u
 int lzk_tg_first_rows(const unsigned char* kind, const unsigned char* sup, const int* shard, long n, const int* tc,
                       const int* tt, const int* to, int nt, long* out, void* stream);
 int lzk_dg_small_max_edges();
+int lzk_uf_union_sel(const int* src, const int* dst, long ne, const float* w, float wthr, const unsigned char* vmark,
+                     int n0, int sel, int* parent, void* stream);
+int lzk_cc_compress(int* parent, long n, void* stream);
+int lzk_dg_stats(const int* src, const int* dst, const float* w, long ne, const int* lab, long n,
+                 const unsigned char* kind, const unsigned char* sup, const int* shard, int min_size, double min_avg_w,
+                 int take, unsigned char* touched, double* gsum, int* gcnt, int* gsize, int* gccnt, long long* gfirst,
+                 unsigned char* cls, int* biglist, int* counters, void* stream);
+int lzk_dg_select(const int* lab, long n, const unsigned char* touched, const unsigned char* kind,
+                  const unsigned char* sup, unsigned char* cls, const long long* gfirst, const int* biglist, int nbig,
+                  const int* nbig_dev, int take, int* cur, int* last, int* cnt, long long* out_key, int* out_row,
+                  int cap, int* count, int* remaining, long window, void* stream);
 }
 
 namespace {
@@ -103,6 +119,145 @@ inline EdgeSet edge_set(void* const* p) {
   return EdgeSet{(int*)p[0], (int*)p[1], (float*)p[2], (int*)p[3], (double*)p[4], (int*)p[5]};
 }
 
+__global__ void ap_iota_kernel(int* __restrict__ a, long lo, long hi) {
+  const long i = lo + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < hi) a[i] = (int)i;
+}
+
+__global__ void ap_fill64_kernel(long long* __restrict__ a, long n, long long v) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = v;
+}
+
+inline unsigned nblk(long n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+
+// Incremental-components digest of one run_consolidation point (the
+// partitioned batch of TenantGraph.cc_begin: stable prefix [0, ns) labelled
+// once per batch into base_lab over the first n0 rows; this point's labels =
+// base, rows inserted since as singletons, unions over the volatile suffix
+// [ns, ne); then ops.tenant_ops.component_digest: stats, one read of the
+// counters, selection, one read of the count, (key, row) pairs sorted on the
+// host). cc slots: see lzk_apply_segments.
+struct Cc {
+  long ns, mode;
+  const int* base_lab;
+  long n0;
+  int* lab;
+  const unsigned char* zero_vm;
+  unsigned char* touched;
+  double* gsum;
+  int* gi;
+  long long* gfirst;
+  unsigned char* cls;
+  int* biglist;
+  int* counters;
+  long long* keys;
+  int* rows;
+  long sel_cap;
+  int* cur;
+  int* last;
+  int* cnt;
+  int* rem;
+  long window;
+  long n_cap;
+};
+
+Cc cc_args(const long* c) {
+  Cc a;
+  a.ns = c[0];
+  a.mode = c[1];
+  a.base_lab = (const int*)c[2];
+  a.n0 = c[3];
+  a.lab = (int*)c[4];
+  a.zero_vm = (const unsigned char*)c[5];
+  a.touched = (unsigned char*)c[6];
+  a.gsum = (double*)c[7];
+  a.gi = (int*)c[8];
+  a.gfirst = (long long*)c[9];
+  a.cls = (unsigned char*)c[10];
+  a.biglist = (int*)c[11];
+  a.counters = (int*)c[12];
+  a.keys = (long long*)c[13];
+  a.rows = (int*)c[14];
+  a.sel_cap = c[15];
+  a.cur = (int*)c[16];
+  a.last = (int*)c[17];
+  a.cnt = (int*)c[18];
+  a.rem = (int*)c[19];
+  a.window = c[20];
+  a.n_cap = c[21];
+  return a;
+}
+
+// the (key, row) pairs of the last call's incremental digests, every point
+// appended in order (lzk_apply_dig_size / lzk_apply_dig_copy read them)
+thread_local std::vector<long long> g_dig;
+
+// Returns 0 / an error; *m = selected (key, row) pairs appended to g_dig
+// (sorted by key, then row).
+int cc_digest(const Cc& a, const int* src, const int* dst, const float* w, long ne, long n, const unsigned char* kind,
+              const unsigned char* sup, const int* shard, int take, long* m_out, hipStream_t st) {
+  void* stream = (void*)st;
+  *m_out = 0;
+  if (n > a.n_cap || a.ns > ne || n < a.n0) return (int)hipErrorInvalidValue;
+  // TenantGraph._cc_labels
+  if (hipMemcpyAsync(a.lab, a.base_lab, sizeof(int) * a.n0, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return (int)hipGetLastError();
+  if (n > a.n0) hipLaunchKernelGGL(ap_iota_kernel, dim3(nblk(n - a.n0)), dim3(256), 0, st, a.lab, a.n0, n);
+  int rc = lzk_uf_union_sel(src + a.ns, dst + a.ns, ne - a.ns, nullptr, -__builtin_huge_valf(), a.zero_vm, (int)n, 0,
+                            a.lab, stream);
+  if (rc) return rc;
+  if ((rc = lzk_cc_compress(a.lab, n, stream))) return rc;
+  // ops.tenant_ops.component_digest
+  if (hipMemsetAsync(a.touched, 0, n, st) != hipSuccess || hipMemsetAsync(a.gsum, 0, 8 * n, st) != hipSuccess ||
+      hipMemsetAsync(a.gi, 0, 12 * n, st) != hipSuccess || hipMemsetAsync(a.counters, 0, 16, st) != hipSuccess)
+    return (int)hipGetLastError();
+  hipLaunchKernelGGL(ap_fill64_kernel, dim3(nblk(n)), dim3(256), 0, st, a.gfirst, n, 1LL << 62);
+  if ((rc = lzk_dg_stats(src, dst, w, ne, a.lab, n, kind, sup, shard, 3, 0.3, take, a.touched, a.gsum, a.gi,
+                         a.gi + n, a.gi + 2 * n, a.gfirst, a.cls, a.biglist, a.counters, stream)))
+    return rc;
+  int ctr[4] = {0, 0, 0, 0};
+  if (hipMemcpyAsync(ctr, a.counters, sizeof(ctr), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return (int)hipGetLastError();
+  const long direct = ctr[0], nbig = ctr[1];
+  const long cap = direct + (long)take * nbig;
+  if (cap == 0) return 0;
+  if (cap > a.sel_cap) return (int)hipErrorInvalidValue;
+  if (nbig) {
+    if (hipMemsetD32Async((hipDeviceptr_t)a.cur, 0x7FFFFFFF, n, st) != hipSuccess ||
+        hipMemsetD32Async((hipDeviceptr_t)a.last, 0xFFFFFFFFu, n, st) != hipSuccess ||
+        hipMemsetAsync(a.cnt, 0, 4 * n, st) != hipSuccess)
+      return (int)hipGetLastError();
+  }
+  if (hipMemsetAsync(a.rem, 0, 4, st) != hipSuccess) return (int)hipGetLastError();
+  if ((rc = lzk_dg_select(a.lab, n, a.touched, kind, sup, a.cls, a.gfirst, a.biglist, (int)nbig, nullptr, take,
+                          nbig ? a.cur : a.rem, nbig ? a.last : a.rem, nbig ? a.cnt : a.rem, a.keys, a.rows,
+                          (int)cap, a.counters + 3, a.rem, a.window, stream)))
+    return rc;
+  int m = 0;
+  if (hipMemcpyAsync(&m, a.counters + 3, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return (int)hipGetLastError();
+  if (m > cap) return (int)hipErrorInvalidValue;
+  if (m == 0) return 0;
+  std::vector<long long> k(m);
+  std::vector<int> r(m);
+  if (hipMemcpyAsync(k.data(), a.keys, 8L * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(r.data(), a.rows, 4L * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return (int)hipGetLastError();
+  std::vector<std::pair<long long, long long>> kr(m);
+  for (int i = 0; i < m; ++i) kr[i] = {k[i], (long long)r[i]};
+  std::sort(kr.begin(), kr.end());  // (key, row) ascending: the caller's argsort order
+  for (int i = 0; i < m; ++i) {
+    g_dig.push_back(kr[i].first);
+    g_dig.push_back(kr[i].second);
+  }
+  *m_out = m;
+  return 0;
+}
+
 }  // namespace
 
 // Returns 0 or a HIP error / hipErrorInvalidValue (bad program). On return:
@@ -111,8 +266,13 @@ inline EdgeSet edge_set(void* const* p) {
 //   seg_out[4 s ..] = (pruned by the decay, surviving edges, dropped edges
 //   written by this segment, offset of its victim records in vinfo) per
 //   segment; vinfo = (kind, sup, shard) x nv per segment, concatenated.
-//   point_out[3 p ..] = (edges at the point, digest written (0 = no edges:
-//   an empty digest), first-rows entries) per point.
+//   point_out[5 p ..] = (edges at the point, digest kind (0 = no edges: an
+//   empty digest, 1 = one-block digest in dg_out slot p, 2 = incremental
+//   digest), first-rows entries, offset and count of its (key, row) pairs in
+//   the incremental digests' output (lzk_apply_dig_copy)) per point.
+// ccp: int64 slots (ns, mode, base_lab, n0, lab, zero_vm, touched, gsum, gi,
+//   gfirst, cls, biglist, counters, keys, rows, sel_cap, cur, last, cnt, rem,
+//   window, n_cap) -- see Cc.
 // shard_count (host, int64 [ncodes]) is updated like the host's counters.
 LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk, const float* xblk, int D,
                                   void* const* colp, long ld32, long ld16, long ld8, void* const* ebuf_a,
@@ -121,9 +281,19 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
                                   int* info, long info_cap, int* dsrc, int* ddst, int* dmeta, long drop_cap,
                                   long long* dg_out, int dg_cap, void* dg_ws, int* dg_cnt, long* fr_out, int fr_k,
                                   long* shard_count, int ncodes, long* seg_out, int* vinfo, long vinfo_cap,
-                                  long* point_out, long* state, void* stream) {
+                                  long* point_out, long* state, const long* ccp, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const Cols& C = *reinterpret_cast<const Cols*>(colp);
+  // ccp (optional): a partitioned batch (TenantGraph.cc_begin) -- the stable
+  // prefix [0, ns) of buffer set A never changes: flags, survivors and the
+  // compaction cover the suffix only (compacted into set B, copied back
+  // behind the prefix), and a point's digest is the incremental-components
+  // one (mode 1) instead of the one-block digest
+  Cc cc{};
+  if (ccp) cc = cc_args(ccp);
+  const long ns = ccp ? cc.ns : 0;
+  long dig_used = 0;
+  g_dig.clear();
   EdgeSet E[2] = {edge_set(ebuf_a), edge_set(ebuf_b)};
   int cur = 0;
   long ne = ne0, n = 0, drop_total = 0, vinfo_used = 0;
@@ -200,11 +370,15 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
       so[2] = 0;
       so[3] = vinfo_used;
       if (nv == 0 && prev == nullptr) continue;  // nothing to flag, nobody removed
-      if (3L * nv + 2 > info_cap || vinfo_used + 3L * nv > vinfo_cap) { rc = (int)hipErrorInvalidValue; goto done; }
+      if (3L * nv + 2 > info_cap || vinfo_used + 3L * nv > vinfo_cap || ne < ns || (prev && nprev < ns)) {
+        rc = (int)hipErrorInvalidValue;
+        goto done;
+      }
       const EdgeSet& e = E[cur];
+      const long nes = ne - ns;  // the suffix the segment end flags
       LZK_RC(lzk_tg_seg_end(nv ? (const long*)(blk + vrows_off) : nullptr, nv, C.kind, C.sup, C.shard, C.stored,
-                            unstore, C.rmb, e.src, e.dst, e.meta, ne, prev, prev ? nprev : 0,
-                            ne ? flag_b : nullptr, ne ? bc : nullptr, info, stream));
+                            unstore, C.rmb, e.src + ns, e.dst + ns, e.meta + ns, nes, prev ? prev + ns : nullptr,
+                            prev ? nprev - ns : 0, nes ? flag_b : nullptr, nes ? bc : nullptr, info, stream));
       // the one host read of the segment: victims' (kind, sup, shard),
       // survivors, pruned
       if (nv && hipMemcpyAsync(vinfo + vinfo_used, info, sizeof(int) * (3L * nv), hipMemcpyDeviceToHost, st) !=
@@ -218,7 +392,7 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
         rc = (int)hipGetLastError();
         goto done;
       }
-      const long n_out = ne ? tail[0] : 0;
+      const long n_out = nes ? tail[0] : 0;  // survivors of the suffix
       so[0] = prev ? tail[1] : 0;
       // the victims leave the host counters like TenantGraph.segment_end
       for (int i = 0; i < nv; ++i) {
@@ -226,20 +400,33 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
         if (k == 1 && !sp && sh >= 0 && sh < ncodes) shard_count[sh] -= 1;
       }
       vinfo_used += 3L * nv;
-      if (ne && n_out != ne) {
-        const long nd = ne - n_out;
+      if (nes && n_out != nes) {
+        const long nd = nes - n_out;
         const bool track = dsrc != nullptr;
         if (track && drop_total + nd > drop_cap) { rc = (int)hipErrorInvalidValue; goto done; }
         const EdgeSet& o = E[cur ^ 1];
-        LZK_RC(lzk_tg_compact(flag_b, bc, ne, e.src, e.dst, e.w, e.co, e.lu, e.meta, o.src, o.dst, o.w, o.co, o.lu,
-                              o.meta, track ? dsrc + drop_total : nullptr, track ? ddst + drop_total : nullptr,
-                              track ? dmeta + drop_total : nullptr, stream));
+        LZK_RC(lzk_tg_compact(flag_b, bc, nes, e.src + ns, e.dst + ns, e.w + ns, e.co + ns, e.lu + ns, e.meta + ns,
+                              o.src, o.dst, o.w, o.co, o.lu, o.meta, track ? dsrc + drop_total : nullptr,
+                              track ? ddst + drop_total : nullptr, track ? dmeta + drop_total : nullptr, stream));
         if (track) {
           so[2] = nd;
           drop_total += nd;
         }
-        cur ^= 1;
-        ne = n_out;
+        if (ns) {  // survivors back behind the untouched prefix, in the same buffers
+          if (n_out &&
+              (hipMemcpyAsync(e.src + ns, o.src, 4 * n_out, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(e.dst + ns, o.dst, 4 * n_out, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(e.w + ns, o.w, 4 * n_out, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(e.co + ns, o.co, 4 * n_out, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(e.lu + ns, o.lu, 8 * n_out, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+               hipMemcpyAsync(e.meta + ns, o.meta, 4 * n_out, hipMemcpyDeviceToDevice, st) != hipSuccess)) {
+            rc = (int)hipGetLastError();
+            goto done;
+          }
+        } else {
+          cur ^= 1;
+        }
+        ne = ns + n_out;
       }
       so[1] = ne;
       prev = nullptr;
@@ -247,11 +434,20 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
     } else if (op == OP_POINT) {
       const long p = prog[pc + 1];
       pc += 2;
-      long* po = point_out + 3 * p;
+      long* po = point_out + 5 * p;
       po[0] = ne;
       po[1] = 0;
       po[2] = 0;
-      if (ne > 0) {  // TenantGraph.digest_capture on the one-block digest (ne <= dg_max: the caller's bound)
+      po[3] = dig_used;
+      po[4] = 0;
+      if (ne > 0 && ccp && cc.mode == 1) {  // TenantGraph.component_digest with the batch's incremental labels
+        long m = 0;
+        const EdgeSet& e = E[cur];
+        LZK_RC(cc_digest(cc, e.src, e.dst, e.w, ne, n, C.kind, C.sup, C.shard, fr_k, &m, st));
+        po[1] = 2;
+        po[4] = m;
+        dig_used += m;
+      } else if (ne > 0) {  // TenantGraph.digest_capture on the one-block digest (ne <= dg_max: the caller's bound)
         if (ne > dg_max || 2L * ne > dg_cap) { rc = (int)hipErrorInvalidValue; goto done; }
         const EdgeSet& e = E[cur];
         LZK_RC(lzk_dg_small(e.src, e.dst, e.w, (int)ne, C.kind, C.sup, C.shard, n, 3, 0.3, fr_k, dg_ws,
@@ -287,4 +483,11 @@ done:
   state[3] = ops;
   if (rc == 0) rc = (int)hipGetLastError();
   return rc;
+}
+
+// The (key, row) pairs of the last lzk_apply_segments call's incremental
+// digests (this thread), 2 int64 per pair.
+LZK_EXPORT long lzk_apply_dig_size() { return (long)g_dig.size() / 2; }
+LZK_EXPORT void lzk_apply_dig_copy(long long* out) {
+  if (!g_dig.empty()) std::memcpy(out, g_dig.data(), g_dig.size() * sizeof(long long));
 }

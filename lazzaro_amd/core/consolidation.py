@@ -310,6 +310,12 @@ class ConsolidationMixin:
             self._save_to_persistence()
         return "\n".join(results)
 
+    def _fact_shard_key(self, f: Dict) -> str:
+        """A fact's shard: its extracted topic, else the keyword inference
+        (reference :716-718) -- evaluated only when there is no topic."""
+        t = f.get("topic")
+        return t if t is not None or "topic" in f else self._infer_shard_key(f["content"])
+
     def _consolidate_to_buffer(self) -> str:
         with self._queue_lock:
             self.consolidation_queue.append({"memories": list(self.short_term_memory),
@@ -426,7 +432,7 @@ class ConsolidationMixin:
         if vidx.size == 0:
             return []
         # shards are created in fact order, duplicates included (reference :716-718)
-        shard_keys = [facts[i].get("topic", self._infer_shard_key(facts[i]["content"])) for i in vidx]
+        shard_keys = [self._fact_shard_key(facts[i]) for i in vidx]
         codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int32)
         Q = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
         sal_in = torch.as_tensor([float(facts[i].get("salience", 0.5)) for i in vidx], dtype=torch.float32)
@@ -768,15 +774,19 @@ class ConsolidationMixin:
     _prefetch_next = None
     _prefetched = None
 
-    def _launch_prefetch(self, pl: Dict) -> None:
+    def _launch_prefetch(self, new_rows: int, cluster: bool) -> None:
         """Batch i+1's dual candidate scan (see :meth:`consolidate_stream`),
-        launched after batch i's plan. Skipped when batch i runs a cluster
-        pass (it shares the scan workspaces) or the scan is not the kernel
-        path."""
+        launched on a side stream once batch i's own candidate lists are
+        known (before its plan when batch i's scan was itself prefetched, so
+        the scan runs under batch i's planner, verification and apply).
+        ``new_rows``: a bound of the rows batch i inserts (reserved now: no
+        column moves under the scan). Skipped when batch i runs a cluster
+        pass (``cluster``: it rewrites the hierarchy the scan's callers read)
+        or the scan is not the kernel path."""
         nxt, self._prefetch_next = self._prefetch_next, None
         self._prefetched = None
         g = self.graph
-        if nxt is None or not g.on_gpu or nxt[1] is None or any(seg["cluster"] for seg in pl["segments"]):
+        if nxt is None or not g.on_gpu or nxt[1] is None or cluster:
             return
         convs, embs = nxt[0], nxt[1]
         flat, idx, j = [], [], 0
@@ -797,10 +807,9 @@ class ConsolidationMixin:
         E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
         # the shards of batch i+1 are registered now, in its fact order: the
         # codes batch i+1 will assign (batch i registers none while applied)
-        codes = np.asarray([g.shard_id(f.get("topic", self._infer_shard_key(f["content"]))) for f in flat],
+        codes = np.asarray([g.shard_id(self._fact_shard_key(f)) for f in flat],
                            dtype=np.int64)
-        ps = pl["stats"]
-        g.reserve(g.n + int(ps["inserted"]) + len(pl["supers"]) + 16)  # no column moves under the scan
+        g.reserve(g.n + int(new_rows) + 16)  # no column moves under the scan
         n = g.n
         with g.on_stream():
             Q = E.to(g.device, torch.float32)
@@ -885,15 +894,35 @@ class ConsolidationMixin:
             E = E[torch.as_tensor(vidx, dtype=torch.long).to(E.device)]
             M = len(facts)
         # shards are created in fact order, duplicates included (reference :716-718)
-        shard_keys = [f.get("topic", self._infer_shard_key(f["content"])) for f in facts]
+        shard_keys = [self._fact_shard_key(f) for f in facts]
         codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int64)
         sal_in = np.asarray([float(f.get("salience", 0.5)) for f in facts], dtype=np.float32)
         thr = self.prune_threshold if self.auto_prune else None
-        with tracer.stage("cb_scan", self._device):
-            inputs = self._plan_inputs(E, codes, B, M)
-        P = inputs.pop("P0")
         hp = self.hierarchy_params if getattr(self, "hierarchy_mode", "") == "kmeans" else None
         cl_every = hp["every"] if (hp and self.enable_hierarchy) else 0
+        # this batch's candidate scan, if it was prefetched (under the previous batch)
+        pf, self._prefetched = self._prefetched, None
+        if not (pf is not None and pf["src"] is getattr(self, "_batch_src", None) and pf["M"] == M
+                and np.array_equal(pf["codes"], codes)):
+            pf = None
+        # a k-means pass inside this batch (the planner's cluster points), or
+        # the first one at its end
+        c0 = self.conversation_count
+        cluster = bool(cl_every) and ((c0 + B) // cl_every > c0 // cl_every or getattr(g, "hier", None) is None)
+        # rows this batch can insert: its facts and at most one super-node per
+        # shard it touches (a super-node is never evicted, so a shard gets one)
+        new_rows = M + len(set(codes.tolist()))
+        early = pf is not None and self._prefetch_next is not None
+        if early:
+            # batch i+1's scan starts now, on the side stream: it reads the
+            # graph as it is before this batch's apply, as a launch after the
+            # plan did (the plan does not change the graph) -- and runs under
+            # the planner instead of only under the apply
+            with tracer.stage("cb_prefetch", self._device):
+                self._launch_prefetch(new_rows, cluster)
+        with tracer.stage("cb_scan", self._device):
+            inputs = self._plan_inputs(E, codes, B, M, pf)
+        P = inputs.pop("P0")
         while True:
             pool, pool_mask = self._eviction_pool(B, P, now)
             kw = dict(ct=conv, code=codes, sal_in=sal_in, n0=g.n, node_count=g.num_nodes(),
@@ -919,9 +948,10 @@ class ConsolidationMixin:
         for k in ("dup", "inserted", "linked", "cross_links", "evicted", "fallbacks"):
             stats[k] += int(ps[k])
         stats["pruned"] += int(ps["pruned_new"])
-        if self._prefetch_next is not None:
+        if self._prefetch_next is not None and not early:
             with tracer.stage("cb_prefetch", self._device):
-                self._launch_prefetch(pl)
+                self._launch_prefetch(int(pl["stats"]["inserted"]) + len(pl["supers"]),
+                                      any(seg["cluster"] for seg in pl["segments"]))
         fact_key = np.asarray(pl["fact_key"], np.int64)
         fact_of = {int(k): int(j) for j, k in enumerate(fact_key.tolist()) if k >= 0}
         id_of = {}
@@ -968,7 +998,7 @@ class ConsolidationMixin:
         from ..engine import native_apply as NA
         from ..engine import tenant_graph as TG
         g = self.graph
-        if not (self.NATIVE_APPLY and g.on_gpu and defer and not self._commit_each and thr is not None and not cc
+        if not (self.NATIVE_APPLY and g.on_gpu and defer and not self._commit_each and thr is not None
                 and TG.SEG_END_KERNEL and TG.SET_ROWS_KERNEL and not g._digest_sorted and NA.available()):
             return False
         if g.emb8 is not None and g.emb8.dtype != torch.int8:
@@ -977,7 +1007,16 @@ class ConsolidationMixin:
             return False
         from ..ops import tenant_ops as T
         app = sum(len(seg["edge_src"]) for seg in pl["segments"])
-        if g.num_edges + app > T.dg_small_max_edges():
+        n_end = g.n + sum(len(seg["ins_kind"]) for seg in pl["segments"])
+        if cc:
+            # the partitioned batch: every point takes the incremental digest
+            # (TenantGraph.component_digest) -- the stable prefix alone keeps
+            # the graph off the O(edges) local digest at every point
+            c = g._cc
+            ns = c.get("ns") if c is not None else None
+            if ns is None or ns <= T.dg_small_max_edges() or 16 * ns <= n_end:
+                return False
+        elif g.num_edges + app > T.dg_small_max_edges():
             return False
         # every insert is the next fresh row, in plan order (the add_nodes bulk path)
         fact_key = np.asarray(pl["fact_key"], np.int64)
@@ -1055,7 +1094,7 @@ class ConsolidationMixin:
                         sh = codes[js].astype(np.int32)
                         prog.insert_rows(n, m, {"sal": isal[k:k2], "acc": iacc[k:k2], "last": ilast[k:k2],
                                                 "shard": sh}, stored)
-                        prog.embeddings(E[torch.as_tensor(js, dtype=torch.long).to(E.device)], n)
+                        prog.embeddings(js, n)
                         cnt = np.bincount(sh[sh >= 0], minlength=1)
                         for c in np.nonzero(cnt)[0].tolist():
                             prog.shard_delta(c, int(cnt[c]))
@@ -1076,7 +1115,7 @@ class ConsolidationMixin:
                         emb = self._plan_super_emb[tuple(children)]
                         prog.insert_rows(n, 1, {"sal": float(isal[k]), "acc": int(iacc[k]), "last": float(ilast[k]),
                                                 "shard": int(sp["code"]), "sup": 1}, False)
-                        prog.embeddings(emb.reshape(1, -1), n)
+                        prog.embeddings([prog.extra_embedding(emb)], n)
                         prog.set_parent(children, n)
                         ins.append(("super", f"super_{skey}_{int(now)}", summary, ch_ids, n))
                         n += 1
@@ -1091,12 +1130,15 @@ class ConsolidationMixin:
                     prog.point()
                 host.append((ins, [g.ids[r] if r < n0 else None for r in vic], vic))
         with tracer.stage("ap_native", g.device):
-            res = prog.run(g.shard_count)
+            res = prog.run(g.shard_count, E, g._cc)
         # ---- host replay, segment by segment (TenantGraph.add_nodes / segment_end, _rc_device)
         p = 0
+        gone = []  # the victims' ids, deleted from the store in one call (one commit covers the batch)
         for s, (seg, (ins, vid0, vic)) in enumerate(zip(segs, host)):
             steps = int(seg["c1"]) - int(seg["c0"]) + 1
             g.decay_log += steps * math.log1p(-DECAY_RATE)
+            if g._cc is not None:
+                g._cc["steps"] += steps
             g._bump(edges=True)
             for it in ins:
                 if it[0] == "facts":
@@ -1134,10 +1176,7 @@ class ConsolidationMixin:
                     g._dv_acc_pending = True
                 g._bump(store=True)
             stats["pruned"] += prog.finish_segment(res, s)
-            ids = [x if x is not None else g.ids[r] for x, r in zip(vid0, vic)]
-            if ids:
-                with tracer.stage("ap_store_delete", "cpu"):
-                    self._store_delete(ids, graph_unstored=True)
+            gone += [x if x is not None else g.ids[r] for x, r in zip(vid0, vic)]
             self.conversation_count = count0 + int(seg["c1"]) + 1
             if seg["consolidate"]:
                 stats["consolidations"] += 1
@@ -1146,7 +1185,13 @@ class ConsolidationMixin:
                 p += 1
                 pending.append({"results": [], "digest": dig, "pruned": 0, "first": first})
             if seg["cluster"]:
+                if gone:
+                    self._store_delete(gone, graph_unstored=True)
+                    gone = []
                 self._maybe_cluster(self.conversation_count - 1)
+        if gone:
+            with tracer.stage("ap_store_delete", "cpu"):
+                self._store_delete(gone, graph_unstored=True)
         if list(res["shard_count"][:len(g.shard_count)]) != list(g.shard_count):
             raise RuntimeError("native segment apply diverged from the host shard counts")
 
@@ -1196,7 +1241,7 @@ class ConsolidationMixin:
         srows = g.node_rows_where(super_=True)
         return sorted(set(g.mirror("shard")[srows].tolist())) if srows.size else []
 
-    def _plan_inputs(self, E, codes: np.ndarray, B: int, M: int) -> Dict:
+    def _plan_inputs(self, E, codes: np.ndarray, B: int, M: int, pf: Dict = None) -> Dict:
         """One scan of the batch against the pre-batch graph + the F x F
         block: candidate lists, super-node cosines, the fallback and
         super-embedding callbacks of the planner."""
@@ -1213,10 +1258,6 @@ class ConsolidationMixin:
         else:
             Q = Qn = torch.zeros((0, g.dim or 1), dtype=torch.float64, device=dev)
         link_mask = (g.kind[:n] == NODE) & (g.sup[:n] == 0) if n else None
-        pf, self._prefetched = self._prefetched, None
-        if not (pf is not None and pf["src"] is getattr(self, "_batch_src", None) and pf["M"] == M
-                and np.array_equal(pf["codes"], codes)):
-            pf = None
         if n and M and pf is not None:  # batch i+1's scan ran under batch i's apply
             with g.on_stream(), tracer.stage("cb_prefetch_finish", dev):
                 (gs, gr), (ws, wr) = g.cos_topk_finish(pf["h"], K, link_mask)
@@ -1290,12 +1331,20 @@ class ConsolidationMixin:
                 "sup_rows": srows, "sup_cos": sup_cos, "sup_n2": sup_n2, "qnorm": qnorm, "fact_n2": fact_n2, "S": S,
                 "super_cos": super_cos, "fallback": fallback, "P0": min(n, 4 * (M + excess0) + 1024)}
 
+    # the eviction pool's sampled thresholds (GPU, large tenants): row sample
+    # stride and the pool size they aim for, in multiples of P (0: the exact
+    # P lowest rows by four top-k selections)
+    POOL_SAMPLE_STRIDE = 64
+    POOL_OVERSAMPLE = 2.0
+    POOL_MAX_OVER = 8
+
     def _eviction_pool(self, B: int, P: int, now: float):
         """The eviction pool of a batch plan: the P lowest-importance
         evictable rows now and after all B decays (ties in any order: the
         plan is verified against every other row afterwards,
-        :meth:`_verify_pool`). Returns (rows, device mask) -- mask None when
-        the pool is every evictable row (nothing to verify)."""
+        :meth:`_verify_pool`) -- on a large GPU tenant a sampled superset of
+        them (POOL_SAMPLE_STRIDE). Returns (rows, device mask) -- mask None
+        when the pool is every evictable row (nothing to verify)."""
         from ..ops import tenant_ops as T
         g = self.graph
         n = g.n
@@ -1312,6 +1361,26 @@ class ConsolidationMixin:
                      "w": torch.zeros(0, dtype=torch.float32, device=g.device)}
             T.decay_prune(empty, sal, g.kind[:n], g.sup[:n], DECAY_RATE, None, steps=B)
             impB = T.importance(sal, g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now)
+            S = self.POOL_SAMPLE_STRIDE
+            if g.on_gpu and S and n >= 64 * S and 4 * P < nev:
+                # a superset of the P lowest rows of each importance: every
+                # row at or under a threshold set from a 1/S row sample for
+                # ~POOL_OVERSAMPLE x P rows (one pass, two host reads instead
+                # of four top-k selections over the tenant); _verify_pool
+                # checks the plan against every row outside it either way
+                k = int(self.POOL_OVERSAMPLE * P / S) + 16
+                fin = torch.isfinite(imp0)  # (evictable rows; the same rows are finite in impB)
+                sel, ok = [], True
+                for imp in (imp0, impB):
+                    sm = imp[::S]
+                    t = torch.kthvalue(sm, min(k, int(sm.numel())))[0]
+                    sel.append(imp <= t)
+                cnt = torch.stack([(sel[0] & fin).sum(), (sel[1] & fin).sum()]).cpu().tolist()
+                # (a threshold inside a large run of equal importances would
+                # pool the whole run: the exact selection then)
+                if min(cnt) >= P and max(cnt) <= self.POOL_MAX_OVER * P:
+                    mask = ((sel[0] | sel[1]) & fin).to(torch.uint8)
+                    return torch.nonzero(mask).flatten().cpu().numpy(), mask
             okey = g.shard[:n].long() * (1 << 32) + torch.arange(n, device=g.device)
             mask = torch.zeros(n, dtype=torch.uint8, device=g.device)
             for imp in (imp0, impB):
@@ -1457,7 +1526,7 @@ class ConsolidationMixin:
             return
         dev = g.device
         # shards are created in fact order, duplicates included (reference :716-718)
-        shard_keys = [f.get("topic", self._infer_shard_key(f["content"])) for f in facts]
+        shard_keys = [self._fact_shard_key(f) for f in facts]
         codes = np.asarray([g.shard_id(k) for k in shard_keys], dtype=np.int32)
         sal_in = torch.as_tensor([float(f.get("salience", 0.5)) for f in facts], dtype=torch.float32).to(dev)
         ct = torch.as_tensor(conv).to(dev)

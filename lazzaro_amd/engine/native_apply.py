@@ -49,7 +49,9 @@ _lib.register("lzk_apply_segments", I, [
     P, P, P, L,               # dsrc, ddst, dmeta, drop_cap
     P, I, P, P, P, I,         # dg_out, dg_cap, dg_ws, dg_cnt, fr_out, fr_k
     P, I, P, P, L, P, P,      # shard_count, ncodes, seg_out, vinfo, vinfo_cap, point_out, state
-    P])                       # stream
+    P, P])                    # cc slots (or None), stream
+_lib.register("lzk_apply_dig_size", L, [])
+_lib.register("lzk_apply_dig_copy", None, [P])
 
 # set_rows column bits (tenant.hip tg_set_rows_kernel): sal acc last ts shard sup parent
 _SR_COLS = ("sal", "acc", "last", "ts", "shard", "sup", "parent")
@@ -74,7 +76,8 @@ class SegmentProgram:
         self.prog: List[int] = []
         self._parts: List[np.ndarray] = []
         self._nbytes = 0
-        self._x: List[torch.Tensor] = []
+        self._x_idx: List[int] = []
+        self._x_extra: List[torch.Tensor] = []
         self.x_rows = 0
         self.nseg = 0
         self.npoints = 0
@@ -149,11 +152,19 @@ class SegmentProgram:
         v = self._put(np.asarray(rows, np.float64))
         self.prog += [OP_ROWS, -1, 0, m, v, _ROWS_IN_VALS | (0b0111111 << 8), c, -1, -1]
 
-    def embeddings(self, x: torch.Tensor, row0: int) -> None:
-        m = int(x.shape[0])
-        self._x.append(x)
+    def embeddings(self, idx: Sequence[int], row0: int) -> None:
+        """Rows ``idx`` of the embedding source (:meth:`run`'s ``E``, then the
+        :meth:`extra_embedding` rows) written at rows row0 .. row0 + m - 1."""
+        m = len(idx)
+        self._x_idx.extend(int(i) for i in idx)
         self.prog += [OP_EMB, self.x_rows, m, int(row0)]
         self.x_rows += m
+
+    def extra_embedding(self, x: torch.Tensor) -> int:
+        """Register one extra embedding row (a super-node's mean); returns
+        its index in the embedding source, past the facts' rows."""
+        self._x_extra.append(x.reshape(1, -1))
+        return -len(self._x_extra)  # resolved against E's row count in run()
 
     def shard_delta(self, code: int, delta: int) -> None:
         if delta:
@@ -188,9 +199,13 @@ class SegmentProgram:
         return p
 
     # ---- run
-    def run(self, shard_count: List[int]) -> Dict:
-        """Upload and execute. Returns the per-segment / per-point records and
-        the device outputs (the caller adopts the edges and builds captures)."""
+    def run(self, shard_count: List[int], E: Optional[torch.Tensor] = None, cc: Optional[Dict] = None) -> Dict:
+        """Upload and execute. ``E``: the facts' embeddings (device fp32 [M, D])
+        the :meth:`embeddings` indices refer to. ``cc``: the batch's
+        incremental components (TenantGraph._cc with a stable prefix) -- the
+        suffix-only segment ends and the incremental digest. Returns the
+        per-segment / per-point records and the device outputs (the caller
+        adopts the edges and builds captures)."""
         g = self.g
         dev = g.device
         self.prog.append(OP_END)
@@ -206,20 +221,33 @@ class SegmentProgram:
         D = int(g.dim or 1)
         with g.on_stream():
             blk = hblk.to(dev, non_blocking=True)
-            xblk = (torch.cat([x.to(dev, torch.float32) for x in self._x]).contiguous() if self._x
-                    else torch.zeros((1, D), dtype=torch.float32, device=dev))
+            if self._x_idx:  # every inserted row's embedding by ONE gather
+                src = [E.to(dev, torch.float32)] if E is not None else []
+                src += [x.to(dev, torch.float32) for x in self._x_extra]
+                base = torch.cat(src) if len(src) > 1 else src[0]
+                m0 = int(E.shape[0]) if E is not None else 0
+                idx = np.asarray(self._x_idx, np.int64)
+                idx = np.where(idx < 0, m0 + (-idx - 1), idx)
+                xblk = base[torch.from_numpy(idx).to(dev, non_blocking=False)].contiguous()
+            else:
+                xblk = torch.zeros((1, D), dtype=torch.float32, device=dev)
             ne0 = g.num_edges
             cap_e = ne0 + self.total_app
             extra = max(cap_e >> 3, g.EDGE_SLACK_MIN)
-            sets = []
-            for s in range(2):
-                bufs = {}
-                for k in T.EDGE_COLS:
-                    b = torch.empty(cap_e + extra, dtype=g.e[k].dtype, device=dev)
-                    if s == 0 and ne0:
-                        b[:ne0].copy_(g.e[k])
-                    bufs[k] = b
-                sets.append(bufs)
+            ns = int(cc["ns"]) if cc is not None else 0
+            sets = [{}, {}]
+            for k in T.EDGE_COLS:
+                v = g.e[k]
+                base_ = v._base if v._base is not None else v
+                if ns and v.data_ptr() == base_.data_ptr() and base_.numel() >= cap_e:
+                    sets[0][k] = base_  # the partitioned list in place: its prefix never moves
+                else:
+                    b = torch.empty(cap_e + extra, dtype=v.dtype, device=dev)
+                    if ne0:
+                        b[:ne0].copy_(v)
+                    sets[0][k] = b
+                # set B: the ping-pong partner, or (partitioned) the suffix's compaction scratch
+                sets[1][k] = torch.empty(max(cap_e - ns, 1) + (0 if ns else extra), dtype=v.dtype, device=dev)
             words = (g.cap + 31) // 32
             if g._rmb is None or g._rmb.numel() < words:
                 g._rmb = torch.zeros(words, dtype=torch.int32, device=dev)
@@ -249,8 +277,35 @@ class SegmentProgram:
             sc = np.asarray(list(shard_count) or [0], dtype=np.int64)
             seg_out = np.zeros(4 * max(self.nseg, 1), np.int64)
             vinfo = np.zeros(max(self.n_vinfo, 1), np.int32)
-            point_out = np.zeros(3 * P_, np.int64)
+            point_out = np.zeros(5 * P_, np.int64)
             state = np.zeros(4, np.int64)
+            ccp = None
+            if cc is not None:
+                nc = int(g.cap)  # workspace rows: every row the batch can reach
+                take = max(self.k_first, 1)
+                ws = {"lab": torch.empty(nc, dtype=torch.int32, device=dev),
+                      "zero": torch.zeros(max(nc, int(cc["n0"]) + 65536), dtype=torch.uint8, device=dev),
+                      "touched": torch.empty(nc, dtype=torch.uint8, device=dev),
+                      "gsum": torch.empty(nc, dtype=torch.float64, device=dev),
+                      "gi": torch.empty(3 * nc, dtype=torch.int32, device=dev),
+                      "gfirst": torch.empty(nc, dtype=torch.int64, device=dev),
+                      "cls": torch.empty(nc, dtype=torch.uint8, device=dev),
+                      "biglist": torch.empty(nc // (take + 1) + 1, dtype=torch.int32, device=dev),
+                      "counters": torch.zeros(4, dtype=torch.int32, device=dev),
+                      "keys": torch.empty(nc, dtype=torch.int64, device=dev),
+                      "rows": torch.empty(nc, dtype=torch.int32, device=dev),
+                      "cur": torch.empty(nc, dtype=torch.int32, device=dev),
+                      "last": torch.empty(nc, dtype=torch.int32, device=dev),
+                      "cnt": torch.empty(nc, dtype=torch.int32, device=dev),
+                      "rem": torch.zeros(1, dtype=torch.int32, device=dev)}
+                base_lab = cc["lab"].to(torch.int32).contiguous()
+                ws["base"] = base_lab
+                ccp = np.asarray([
+                    ns, 1, base_lab.data_ptr(), int(cc["n0"]), ws["lab"].data_ptr(), ws["zero"].data_ptr(),
+                    ws["touched"].data_ptr(), ws["gsum"].data_ptr(), ws["gi"].data_ptr(), ws["gfirst"].data_ptr(),
+                    ws["cls"].data_ptr(), ws["biglist"].data_ptr(), ws["counters"].data_ptr(), ws["keys"].data_ptr(),
+                    ws["rows"].data_ptr(), nc, ws["cur"].data_ptr(), ws["last"].data_ptr(), ws["cnt"].data_ptr(),
+                    ws["rem"].data_ptr(), int(T.DIGEST_WINDOW), nc], dtype=np.int64)
             rc = _lib.lib().lzk_apply_segments(
                 prog.ctypes.data, int(prog.size), blk.data_ptr(), xblk.data_ptr(), D,
                 cols.ctypes.data, g.emb32.stride(0), g.emb16.stride(0) if g.emb16 is not None else 0,
@@ -261,16 +316,32 @@ class SegmentProgram:
                 dg_out.data_ptr(), dg_cap, dg_ws.data_ptr(), dg_cnt.data_ptr(), fr_out.data_ptr(),
                 max(self.k_first, 1), sc.ctypes.data, int(len(shard_count)), seg_out.ctypes.data,
                 vinfo.ctypes.data, int(vinfo.size), point_out.ctypes.data, state.ctypes.data,
-                _lib.stream_ptr(dev))
+                ccp.ctypes.data if ccp is not None else None, _lib.stream_ptr(dev))
             _lib.check(rc, "lzk_apply_segments")
             ne, cur, nd = int(state[0]), int(state[1]), int(state[2])
             g._adopt_edges({k: sets[cur][k][:ne] for k in T.EDGE_COLS})
+            dig = np.zeros(0, np.int64)
+            if ccp is not None:
+                nd_ = int(_lib.lib().lzk_apply_dig_size())
+                dig = np.zeros(2 * nd_, np.int64)
+                if nd_:
+                    _lib.lib().lzk_apply_dig_copy(dig.ctypes.data)
+            # every point's capture slots in one device -> host copy each
+            # (the captures slice them after one event)
+            P_used = max(self.npoints, 1)
+            h_dg = torch.empty((P_used, 2, dg_cap), dtype=torch.int64, pin_memory=True)
+            h_fr = torch.empty((P_used, max(self.k_first, 1)), dtype=torch.int64, pin_memory=True)
+            if self.npoints:
+                h_dg.copy_(dg_out[:P_used], non_blocking=True)
+                h_fr.copy_(fr_out[:P_used], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
             # the block / workspaces must outlive the queued kernels
             for t in [blk, xblk, flag_a, flag_b, bc, info, dg_ws, dg_cnt] + (drop or []):
                 t.record_stream(torch.cuda.current_stream(dev))
-        return {"seg_out": seg_out.reshape(-1, 4), "vinfo": vinfo, "point_out": point_out.reshape(-1, 3),
-                "shard_count": sc, "dg_out": dg_out, "fr_out": fr_out, "drop": drop, "n_drop": nd,
-                "ne": ne}
+        return {"seg_out": seg_out.reshape(-1, 4), "vinfo": vinfo, "point_out": point_out.reshape(-1, 5),
+                "shard_count": sc, "h_dg": h_dg, "h_fr": h_fr, "ev": ev, "drop": drop, "n_drop": nd,
+                "ne": ne, "dig": dig.reshape(-1, 2)}
 
     # ---- host replay of a segment end (TenantGraph._segment_end_fused's tail)
     def finish_segment(self, res: Dict, s: int) -> int:
@@ -303,11 +374,37 @@ class SegmentProgram:
 
     @staticmethod
     def captures(res: Dict, p: int):
-        """(digest, first rows) Captures of point ``p`` (TenantGraph.digest_capture /
-        first_rows_capture)."""
+        """(digest, first rows) of point ``p`` as Captures
+        (TenantGraph.digest_capture / first_rows_capture): slices of the
+        run's bulk host copies, read after its one event."""
         po = res["point_out"][p]
-        dig = Capture(res["dg_out"][p], fn=T.digest_lists) if int(po[1]) else Capture(host=[])
-        nf = int(po[2])
-        first = Capture(res["fr_out"][p, :nf], fn=lambda a: a[a >= 0]) if nf else Capture(
-            host=np.zeros(0, np.int64))
+        kind, nf = int(po[1]), int(po[2])
+        if kind == 1:
+            dig = _Slice(res, lambda r: T.digest_lists(r["h_dg"][p].numpy()))
+        elif kind == 2:  # the incremental digest's sorted (key, row) pairs
+            o, m = int(po[3]), int(po[4])
+            kr = res["dig"][o:o + m]
+            dig = Capture(host=np.split(kr[:, 1], np.nonzero(np.diff(kr[:, 0]))[0] + 1) if m else [])
+        else:
+            dig = Capture(host=[])
+        if nf:
+            first = _Slice(res, lambda r: (lambda a: a[a >= 0])(r["h_fr"][p, :nf].numpy()))
+        else:
+            first = Capture(host=np.zeros(0, np.int64))
         return dig, first
+
+
+class _Slice:
+    """A Capture-like view of one point of a native run's bulk host copy."""
+    __slots__ = ("_res", "_fn", "_val", "_done")
+
+    def __init__(self, res: Dict, fn):
+        self._res, self._fn, self._val, self._done = res, fn, None, False
+
+    def get(self):
+        if not self._done:
+            self._res["ev"].synchronize()
+            self._val = self._fn(self._res)
+            self._done = True
+            self._res = None
+        return self._val

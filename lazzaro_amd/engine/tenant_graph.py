@@ -1112,7 +1112,7 @@ class TenantGraph:
         """Keep the edge list (nearly) ordered by source row: the union-find
         pass of the component digest hooks / finds ``src`` endpoints in edge
         order, and on a 10M-row / 20M-edge graph a src-ordered list runs in
-        1.6 ms against 7.5 ms for a random order (bench/probe_cc.py). Links
+        1.6 ms against 7.5 ms for a random order (a round-4 probe, since removed). Links
         are appended in insertion order (new rows = new sources), so the list
         stays nearly sorted by itself; when more than 1/32 of adjacent pairs
         are out of order (seeded or migrated edges) every edge column is

@@ -810,7 +810,7 @@ def _dual_i8_template(X8, rscale, Q8, qs, X16, bias, alpha, thr_a, thr_b, row_la
 
 # Speculative list-B threshold of flat_topk_dual (DUAL_SPEC = True): aim for
 # this many expected label rows above it. Off by default: on the 10M x 1024
-# consolidation shape it cuts the scan 13.93 -> 12.90 ms (bench/probe_dual_thr.py:
+# consolidation shape it cuts the scan 13.93 -> 12.90 ms (a round-1 probe:
 # list-B candidates 198 -> 16 per query), but the top-16 sample pass it needs
 # costs ~1.1 ms more than the top-4 one, so the whole call ties (15.07 vs
 # 15.13 ms, bench/ab_dual_spec.py, profiles/ab_dual_spec_r1.json).

@@ -730,7 +730,7 @@ class ShardedMemorySystem:
             bl = self._host_ints(B_loc)[:, 0].tolist()
             B = int(sum(bl))
             c_off = int(sum(bl[: self.rank]))
-            keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
+            keys = [self.local._fact_shard_key(f) for f in flat]
             keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self._coll else keys
             sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
             ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off
@@ -1276,7 +1276,7 @@ class ShardedMemorySystem:
             bl = self._host_ints(B_loc)[:, 0].tolist()
             B = int(sum(bl))
             c_off = int(sum(bl[: self.rank]))
-            keys = [f.get("topic", self.local._infer_shard_key(f["content"])) for f in flat]
+            keys = [self.local._fact_shard_key(f) for f in flat]
             keys_all = [k for ks in comm.all_gather_object(keys) for k in ks] if self._coll else keys
             sal_l = torch.tensor([float(f.get("salience", 0.5)) for f in flat], dtype=torch.float32, device=dev)
             ct_l = torch.tensor(conv, dtype=torch.long, device=dev) + c_off

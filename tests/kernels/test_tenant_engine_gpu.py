@@ -797,14 +797,26 @@ def test_lean_hbm_tenant_matches_full_gpu(monkeypatch):
     assert lean.emb16 is None  # the pass's bf16 copy is gone
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("prune_threshold", [0.0, 0.5])
-def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, prune_threshold):
+def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, prune_threshold, native):
     """consolidate_batch on a tenant with many edges (the full GPU digest
     path at every run_consolidation point): the batch's incremental
     components (TenantGraph.cc_begin) give the same digest at every point,
     the same profile and the same final graph as a union-find over every
-    edge at every point."""
+    edge at every point -- through the native segment applier
+    (csrc/kernels/apply.hip: suffix-only segment ends, the incremental digest
+    in C++) and through the per-segment Python path."""
+    from lazzaro_amd.core import consolidation as Cn
     from lazzaro_amd.engine.tenant_graph import TenantGraph
+    monkeypatch.setattr(Cn.ConsolidationMixin, "NATIVE_APPLY", native)
+    nat = []
+    real_run = Cn.ConsolidationMixin._native_run
+
+    def counted(self, segs, *a, **k):
+        nat.append(self.graph._cc is not None)
+        return real_run(self, segs, *a, **k)
+    monkeypatch.setattr(Cn.ConsolidationMixin, "_native_run", counted)
     N, D, NE, B, F = 80_000, 64, 240_000, 30, 4
     X, lab = _clustered(N, D, 64, 3, noise=1.2)
     gen = torch.Generator().manual_seed(12)
@@ -821,16 +833,15 @@ def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, pru
         facts.append(conv)
     V = torch.stack(vecs)
     out = {}
-    real = TenantGraph.component_digest
+    real = Cn.ConsolidationMixin._rc_host
     real_begin = TenantGraph.cc_begin
     for inc in (True, False):
         digests = []
 
-        def rec(self, *a, **k):
-            d = real(self, *a, **k)
-            digests.append([x.tolist() for x in d])
-            return d
-        monkeypatch.setattr(TenantGraph, "component_digest", rec)
+        def rec(self, cap):  # every point's digest, whichever path computed it
+            digests.append([x.tolist() for x in cap["digest"].get()])
+            return real(self, cap)
+        monkeypatch.setattr(Cn.ConsolidationMixin, "_rc_host", rec)
         monkeypatch.setattr(TenantGraph, "CC_INCREMENTAL", inc)
         monkeypatch.setattr(time, "time", _Clock())
         ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
@@ -854,6 +865,7 @@ def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, pru
         ms.close()
     a, b = out[True], out[False]
     assert a[3] == [True] and b[3] == [False]  # the incremental path ran (thr 0.5: the decays make many edges volatile)
+    assert (True in nat) == native  # the native applier ran the partitioned batch (and only when enabled)
     assert a[0] == b[0] and a[0]["consolidations"] == B // 3 and a[0]["evicted"] > 0
     assert a[1] == b[1] and len(a[1]) == B // 3
     assert a[2] == b[2]

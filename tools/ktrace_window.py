@@ -60,6 +60,17 @@ def main():
         "by_class_frac_of_device_time": {k: v / max(tot, 1) for k, v in cls.items()},
         "top": [{"ms_per_step": v[0] / 1e6 / steps, "n_per_step": v[1] / steps, "kernel": n[:160]} for n, v in top],
     }
+    # the long kernels of the last step in time order (start offset in the
+    # step, duration, queue): where the step's critical path goes
+    t_step = t1 - int(window_ms / steps * 1e6)
+    qcol = next((c for c in ("Queue_Id", "Stream_Id", "Queue_ID") if rows and c in rows[0]), None)
+    tl = []
+    for r in rows:
+        s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if e_ > t_step and (e_ - s_) >= 200_000:
+            tl.append({"t_ms": round((s_ - t_step) / 1e6, 3), "dur_ms": round((e_ - s_) / 1e6, 3),
+                       "q": r.get(qcol) if qcol else None, "kernel": r["Kernel_Name"][:70]})
+    res["last_step_long_kernels"] = sorted(tl, key=lambda x: x["t_ms"])
     js = json.dumps(res, indent=1)
     if len(sys.argv) > 4:
         open(sys.argv[4], "w").write(js)
