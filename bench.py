@@ -554,6 +554,8 @@ def main():
             hbm_peak[name] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
             torch.cuda.reset_peak_memory_stats(dev)
     peak("headline")
+    if rank == 0:
+        print("bench: %s" % "headline done", file=sys.stderr, flush=True)
 
     # ---- second half of the metric: consolidate turns/sec ----
     consolidate = persistent = None

@@ -367,7 +367,9 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     t0 = time.perf_counter()
     agg = {}
     work0 = sm.scan_work
-    for st in run_steps(steps):
+    for i, st in enumerate(run_steps(steps)):
+        if comm.rank == 0:  # progress (stderr)
+            print(f"sharded consolidate step {i + 1}/{steps}", file=sys.stderr, flush=True)
         for k, v in st.items():
             agg[k] = agg.get(k, 0) + v
     _sync(dev)

@@ -228,6 +228,23 @@ def _lowest_keys(imp: torch.Tensor, okey: torch.Tensor, P: int) -> torch.Tensor:
     return torch.cat([lt, ti[tv != big]])
 
 
+def _host_pinned(owner, attr: str, t: torch.Tensor) -> np.ndarray:
+    """``t.cpu().numpy()`` through a pinned buffer cached on ``owner``
+    (grown, never shrunk): the planner's F x F float64 block is 8 MB per
+    1024-fact batch, which a pageable copy moved at a few GB/s. The array is
+    valid until the next call with the same ``attr``."""
+    if not t.is_cuda:
+        return t.cpu().numpy()
+    n = t.numel()
+    buf = getattr(owner, attr, None)
+    if buf is None or buf.numel() < n or buf.dtype != t.dtype:
+        buf = torch.empty(max(n, 1), dtype=t.dtype, pin_memory=True)
+        setattr(owner, attr, buf)
+    h = buf[:n].view(t.shape)
+    h.copy_(t)  # (synchronous: the caller reads it right away)
+    return h.numpy()
+
+
 def shard_keys_of(g: TenantGraph, code: int) -> str:
     """The shard name of a shard code."""
     for k, c in g.shard_code.items():
@@ -1283,7 +1300,7 @@ class ConsolidationMixin:
         if M:
             X = Q.double()
             nrm = (X * X).sum(1).float().double().sqrt()
-            S = ((Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]).cpu().numpy()
+            S = _host_pinned(self, "_pin_S", (Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :])
             qnorm = qn.flatten().cpu().numpy()
             fact_n2 = (X * X).sum(1).float().double().cpu().numpy()
         else:
@@ -1373,7 +1390,8 @@ class ConsolidationMixin:
                 sel, ok = [], True
                 for imp in (imp0, impB):
                     sm = imp[::S]
-                    t = torch.kthvalue(sm, min(k, int(sm.numel())))[0]
+                    # (top-k, not kthvalue: ATen's kthvalue sorts -- 1.4 ms per call here)
+                    t = torch.topk(sm, min(k, int(sm.numel())), largest=False, sorted=False)[0].max()
                     sel.append(imp <= t)
                 cnt = torch.stack([(sel[0] & fin).sum(), (sel[1] & fin).sum()]).cpu().tolist()
                 # (a threshold inside a large run of equal importances would

@@ -136,7 +136,7 @@ I8_QUERY_KERNEL = True
 # wide batches keep the torch formulation (I8_QUERY_WIDE = True: the kernel too):
 # measured with the kernel on wide batches, the pipelined headline loop fell
 # from 82.6k to 54k QPS while every store search alone stayed as fast (open)
-I8_QUERY_WIDE = False
+I8_QUERY_WIDE = os.environ.get("LZK_I8_QUERY_WIDE", "0") == "1"
 I8_QUERY_WIDE_MIN = 128
 # consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (SEG_END_KERNEL = False: the torch formulation)
 SEG_END_KERNEL = True

@@ -79,7 +79,7 @@ import numpy as np
 import torch
 
 from ..core.consolidation import (DECAY_RATE, LINK_THRESHOLD, LINK_TOPK, MIN_FACT_LEN, PROFILE_CONTENTS,
-                                  batch_dedupe, batch_link_plan, salience_decayed)
+                                  _host_pinned, batch_dedupe, batch_link_plan, salience_decayed)
 from ..engine.tenant_graph import GHOST, NODE, SHARD_MASK, TYPE_MASK, TYPE_SHIFT, _seg_min, _seg_sum_count
 from ..ops import tenant_ops as T
 from ..utils.tracing import tracer
@@ -1454,7 +1454,7 @@ class ShardedMemorySystem:
             if F:
                 X = Q.double()
                 nrm = (X * X).sum(1).float().double().sqrt()
-                S = ((Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :]).cpu().numpy()
+                S = _host_pinned(self, "_pin_S", (Qn @ X.T) / torch.where(nrm > 0, nrm, torch.ones_like(nrm))[None, :])
                 qnorm = qn.flatten().cpu().numpy()
                 fact_n2 = (X * X).sum(1).float().double().cpu().numpy()
             else:
