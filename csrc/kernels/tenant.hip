@@ -366,7 +366,9 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
                                                            const float* __restrict__ bias,
                                                            const long* __restrict__ cand, int C, int M, int k,
                                                            int metric, float* __restrict__ os,
-                                                           long* __restrict__ oi) {
+                                                           long* __restrict__ oi,
+                                                           const unsigned char* __restrict__ kind,
+                                                           long* __restrict__ oin) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= M) return;
@@ -432,10 +434,14 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
   if (live && rank < k) {
     os[(long)q * k + rank] = my_s;
     oi[(long)q * k + rank] = my_r;
+    // oin (optional): the same rows with those that are not graph nodes as
+    // -1 (search_memories skips them, reference memory_system.py:1467-1472)
+    if (oin) oin[(long)q * k + rank] = kind[my_r] == 1 ? my_r : -1;
   }
   for (int j = nlive + lane; j < k; j += 64) {
     os[(long)q * k + j] = LZK_NEG_INF;
     oi[(long)q * k + j] = -1;
+    if (oin) oin[(long)q * k + j] = -1;
   }
 }
 
@@ -809,10 +815,11 @@ LZK_EXPORT int lzk_tg_gather_fields(const long* rows, int nq, int k, const void*
 
 LZK_EXPORT int lzk_store_rerank(const float* Q, long ldq, const float* X, long ldx, int D, const float* sqn,
                                 const float* bias, const long* cand, int C, int M, int k, int metric, float* os,
-                                long* oi, void* stream) {
-  if (C <= 0 || C > 64 || M <= 0 || k <= 0 || metric < 0 || metric > 2) return (int)hipErrorInvalidValue;
+                                long* oi, const unsigned char* kind, long* oin, void* stream) {
+  if (C <= 0 || C > 64 || M <= 0 || k <= 0 || metric < 0 || metric > 2 || (oin && !kind))
+    return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(store_rerank_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Q, ldq,
-                     X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi);
+                     X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi, kind, oin);
   return (int)hipGetLastError();
 }
 

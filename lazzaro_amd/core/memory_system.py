@@ -659,12 +659,11 @@ class MemorySystem(ConsolidationMixin):
                     ctx = contextlib.nullcontext()
                 with ctx:
                     with tracer.stage("search", self._device):
-                        _, rows = g.store_search(embs, int(limit), getattr(self.store, "metric", "l2"))
                         # rows the graph does not hold as nodes are skipped (reference
-                        # :1467-1472): marked on the device, so mapping needs no mirror
-                        with g.on_stream():
-                            rows = torch.where((rows >= 0) & (g.kind[rows.clamp_min(0)] == NODE), rows,
-                                               torch.full_like(rows, -1))
+                        # :1467-1472): marked on the device (by the re-rank kernel), so
+                        # mapping needs no mirror
+                        _, rows = g.store_search(embs, int(limit), getattr(self.store, "metric", "l2"),
+                                                 node_rows=True)
                     if rows.is_cuda:
                         # the rows stay on the device until _search_finish copies them to
                         # pageable host memory on a stream that waits for THIS search only

@@ -2345,16 +2345,24 @@ class TenantGraph:
         self._bias_cache[metric] = (self._store_version, b)
         return b
 
-    def store_search(self, Q: torch.Tensor, k: int, metric: str = "l2"):
+    def store_search(self, Q: torch.Tensor, k: int, metric: str = "l2", node_rows: bool = False):
         """The store's vector search over this tenant (reference
         ``LanceDBStore.search_nodes``: flat scan, L2 unless told otherwise,
         vector_store.py:132-140). fp32 scores -- -|q-x|^2 for L2, cosine, or
         dot -- higher is closer; bf16 MFMA candidates are re-ranked in fp32.
-        Returns (scores [M, k], rows [M, k])."""
+        Returns (scores [M, k], rows [M, k]). ``node_rows``: rows that are not
+        graph nodes come back as -1 (search_memories skips them, reference
+        memory_system.py:1467-1472) -- inside the re-rank kernel when it runs."""
         with self.on_stream():
-            return self._store_search(Q, k, metric)
+            s, r = self._store_search(Q, k, metric, node_rows)
+            if node_rows and not self._nodes_marked:
+                r = torch.where((r >= 0) & (self.kind[r.clamp_min(0)] == NODE), r, torch.full_like(r, -1))
+            self._nodes_marked = False
+            return s, r
 
-    def _store_search(self, Q, k, metric):
+    _nodes_marked = False  # the last _store_search already marked non-node rows (re-rank kernel)
+
+    def _store_search(self, Q, k, metric, node_rows=False):
         from ..ops.search import flat_topk
         n = self.n
         dev = self.device
@@ -2390,7 +2398,7 @@ class TenantGraph:
                     _, cand = self._fp8_candidates(Qf, q16, kc, bias, alpha)
             else:
                 _, cand = flat_topk(self.emb16[:n], q16, kc, bias=bias, alpha=alpha)
-            return self._rerank_store(Qf, cand, k, metric, bias)
+            return self._rerank_store(Qf, cand, k, metric, bias, node_rows)
         return self._exact_store(Qf, k, metric, bias)
 
     def _ann_candidates(self, Qf: torch.Tensor, R: int, cfg: Dict) -> torch.Tensor:
@@ -2523,10 +2531,12 @@ class TenantGraph:
             best_s, best_i = torch.gather(cs, 1, o), torch.gather(ci, 1, o)
         return self._pad_k(best_s, best_i, k)
 
-    def _rerank_store(self, Qf, cand, k, metric, bias):
+    def _rerank_store(self, Qf, cand, k, metric, bias, node_rows=False):
         if self.on_gpu and RERANK_KERNEL and 0 < cand.shape[1] <= 64 and metric in ("l2", "ip", "cosine"):
             from ..ops.tenant_ops import store_rerank
-            return store_rerank(Qf, self.emb32, self.sqn, bias, cand, k, metric)
+            self._nodes_marked = bool(node_rows)
+            return store_rerank(Qf, self.emb32, self.sqn, bias, cand, k, metric,
+                                kind=self.kind if node_rows else None)
         valid = cand >= 0
         rows = cand.clamp_min(0)
         s = self._store_scores(Qf, self.emb32[rows], self.sqn[rows], bias[rows], metric)

@@ -24,7 +24,7 @@ D_ = C.c_double
 _lib.register("lzk_tg_decay", I, [P, L, F, F, P, P, P, P, P, L, I, I, P])
 _lib.register("lzk_tg_write_emb", I, [P, L, P, I, I, P, L, P, L, P, L, P, L, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_set_rows", I, [P, L, I, P, I, P, P, P, P, P, P, P, P, P, P, P, I, I, P])
-_lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P])
+_lib.register("lzk_store_rerank", I, [P, L, P, L, I, P, P, P, I, I, I, I, P, P, P, P, P])
 _lib.register("lzk_tg_flag_remove", I, [P, P, P, L, P, P, P, L, P, P, P])
 _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P])
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
@@ -683,11 +683,13 @@ _METRIC_CODE = {"l2": 0, "ip": 1, "dot": 1, "cosine": 2}
 
 
 def store_rerank(Qf: torch.Tensor, X: torch.Tensor, sqn: torch.Tensor, bias: torch.Tensor, cand: torch.Tensor,
-                 k: int, metric: str):
+                 k: int, metric: str, kind: Optional[torch.Tensor] = None):
     """Exact fp32 re-rank of store-search candidates in one launch
     (tenant.hip store_rerank_kernel): scores of the rows ``cand`` [M, C]
     (C <= 64, -1 = empty) against ``Qf`` [M, D], top-k by (score desc, row
-    asc). Returns (scores [M, k], rows int64 [M, k]; -inf / -1 padding)."""
+    asc). Returns (scores [M, k], rows int64 [M, k]; -inf / -1 padding);
+    with ``kind`` (the graph's kind column) the rows that are not graph
+    nodes come back as -1 (the search_memories view), in the same launch."""
     M, C = cand.shape
     D = Qf.shape[1]
     Qc = Qf.contiguous()
@@ -697,11 +699,13 @@ def store_rerank(Qf: torch.Tensor, X: torch.Tensor, sqn: torch.Tensor, bias: tor
     oi = torch.empty((M, k), dtype=torch.long, device=Qf.device)
     if M == 0:
         return os_, oi
+    oin = torch.empty((M, k), dtype=torch.long, device=Qf.device) if kind is not None else None
     _lib.check(_lib.lib().lzk_store_rerank(Qc.data_ptr(), Qc.stride(0), X.data_ptr(), X.stride(0), D, sqn.data_ptr(),
                                            bias.data_ptr(), cc.data_ptr(), C, M, int(k), _METRIC_CODE[metric],
-                                           os_.data_ptr(), oi.data_ptr(), _lib.stream_ptr(Qf.device)),
+                                           os_.data_ptr(), oi.data_ptr(), _lib.ptr(kind), _lib.ptr(oin),
+                                           _lib.stream_ptr(Qf.device)),
                "lzk_store_rerank")
-    return os_, oi
+    return (os_, oin) if kind is not None else (os_, oi)
 
 
 SET_ROWS_COLS = ("sal", "acc", "last", "ts", "shard", "sup", "parent")

@@ -72,6 +72,7 @@ Not supported for a row-sharded tenant: ``merge_mode="pairwise"``
 """
 from __future__ import annotations
 
+import math
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -1563,6 +1564,10 @@ class ShardedMemorySystem:
         etype = g.etype("relates_to")
         n_fact = n0 - int(np.searchsorted(self._sup_v, n0))
         reach_new: List[torch.Tensor] = []
+        if self._native_w1_ok(pl, thr):
+            with tracer.stage("cb_apply_native", dev):
+                pruned += self._native_w1(pl, fact_key, codes, Q, flat, f_off, thr, now, count0, stats, reach_new)
+            pl = {"segments": []}  # applied
         for seg in pl["segments"]:
             with tracer.stage("cb_apply", dev):
                 pruned_local = self._apply_exact_segment(seg, supers, fact_key, origin_h, codes, Q, flat, f_off,
@@ -1591,6 +1596,176 @@ class ShardedMemorySystem:
             self.cluster_pass()
         if self.local.query_cache:
             self.local.query_cache.invalidate_results()
+
+    # one rank (no collectives, every row held here): the plan's segments
+    # through the native applier (csrc/kernels/apply.hip) like the single
+    # process; False: the per-segment path
+    NATIVE_W1 = True
+    native_w1_runs = 0  # batches applied natively (tests)
+
+    def _native_w1_ok(self, pl: Dict, thr) -> bool:
+        """The native applier applies the plan of a one-rank buffer exactly
+        when the tenant's rows are its global node numbers (rows appended in
+        number order, no ghost rows -- then every key of the plan is a row),
+        no super-node is created (the reference hierarchy's ghost-free super
+        rows are the per-segment path's), the decay prunes, and the graph's
+        edges fit the one-block digest for the whole batch (the digest of
+        :meth:`_digest_world1` on a tenant without super-nodes)."""
+        from ..core.consolidation import ConsolidationMixin
+        from ..engine import native_apply as NA
+        from ..engine import tenant_graph as TG
+        g = self.g
+        if not (self.NATIVE_W1 and ConsolidationMixin.NATIVE_APPLY and self.world == 1 and not self._coll
+                and g.on_gpu and thr is not None and not self._commit_each and not pl["supers"]
+                and g.n_super == 0 and TG.SEG_END_KERNEL and TG.SET_ROWS_KERNEL and not g._digest_sorted
+                and NA.available() and self._sup_v.size == 0):
+            return False
+        if g.emb8 is not None and g.emb8.dtype != torch.int8:
+            return False
+        if g.dim is None or g.dim > 1024 or PROFILE_CONTENTS > 64:
+            return False
+        app = sum(len(seg["edge_src"]) for seg in pl["segments"])
+        if g.num_edges + app > T.dg_small_max_edges():
+            return False
+        n = g.n
+        if int(self.next_id) - sum(len(seg["ins_kind"]) for seg in pl["segments"]) != n:
+            return False
+        # every row is its node number (number = row + 1): one pass, one read
+        with g.on_stream():
+            ident = bool((self.num[:n] == torch.arange(1, n + 1, device=self.device)).all()) if n else True
+        return ident
+
+    def _native_w1(self, pl, fact_key, codes, Q, flat, f_off, thr, now, count0, stats, reach_new) -> int:
+        """:meth:`_apply_exact_segment` for every segment of the plan through
+        one native call per run of segments (a run ends at a cluster pass),
+        rows = plan keys; then the host bookkeeping, the new rows' numbers,
+        and run_consolidation's profile prompts (digest / first rows captured
+        at each point, read after the run -- the profile sees the same
+        contents: no content changes inside a batch without super-nodes).
+        Returns the edges the segments' decays pruned."""
+        from ..engine.native_apply import SegmentProgram
+        g = self.g
+        ms = self.local
+        segs = pl["segments"]
+        pruned = 0
+        self.native_w1_runs += 1
+        i = 0
+        while i < len(segs):
+            j = i
+            while j < len(segs) - 1 and not segs[j]["cluster"]:
+                j += 1
+            run = segs[i:j + 1]
+            etype = g.etype("relates_to") if any(len(s["edge_src"]) for s in run) else 0
+            prog = SegmentProgram(g, now, thr if thr > 0.0 else float("-inf"), 1.0 - DECAY_RATE, etype,
+                                  PROFILE_CONTENTS)
+            n0 = g.n
+            g.reserve(n0 + sum(len(s["ins_kind"]) for s in run))
+            n = n0
+            prog.n(n)
+            host = []
+            for seg in run:
+                prog.decay(int(seg["c1"]) - int(seg["c0"]) + 1)
+                tr = np.asarray(seg["tch_rows"], np.int64)
+                if tr.size:
+                    prog.touch_rows(tr, seg["tch_sal"], seg["tch_acc"], seg["tch_last"])
+                kinds = np.asarray(seg["ins_kind"], np.int64).reshape(-1)
+                idx = np.asarray(seg["ins_idx"], np.int64).reshape(-1)
+                isal = np.asarray(seg["ins_sal"], np.float32)
+                iacc = np.asarray(seg["ins_acc"], np.int32)
+                ilast = np.asarray(seg["ins_last"], np.float64)
+                ins = []
+                if idx.size:  # (no super-nodes: every insert is a fact, in key order)
+                    keys = fact_key[idx]
+                    if not np.array_equal(keys, np.arange(n, n + keys.size)):
+                        raise RuntimeError("native apply: plan keys are not the next rows")
+                    sh = codes[idx].astype(np.int32)
+                    prog.insert_rows(n, int(idx.size), {"sal": isal, "acc": iacc, "last": ilast, "shard": sh}, True)
+                    prog.embeddings(idx.tolist(), n)
+                    cnt = np.bincount(sh[sh >= 0], minlength=1)
+                    for c in np.nonzero(cnt)[0].tolist():
+                        prog.shard_delta(c, int(cnt[c]))
+                    lf = [flat[int(x) - f_off] for x in idx]
+                    ins = (self._ids_of_nums(keys + 1), [f["content"] for f in lf],
+                           [f.get("type", "semantic") for f in lf], sh, n)
+                    n += int(idx.size)
+                    prog.n(n)
+                es = np.asarray(seg["edge_src"], np.int64)
+                if es.size:
+                    prog.append_edges(es, seg["edge_dst"], seg["edge_w"], seg["edge_code"])
+                vic = sorted({int(r) for r in np.asarray(seg["victims"], np.int64).tolist() if 0 <= r < n})
+                prog.segment_end(vic)
+                if seg["consolidate"]:
+                    prog.point()
+                host.append((ins, vic))
+            res = prog.run(g.shard_count, Q)
+            p = 0
+            gone = []
+            for s, (seg, (ins, vic)) in enumerate(zip(run, host)):
+                steps = int(seg["c1"]) - int(seg["c0"]) + 1
+                g.decay_log += steps * math.log1p(-DECAY_RATE)
+                g._bump(edges=True)
+                if ins:
+                    ids, contents, types, sh, r0 = ins
+                    m = len(ids)
+                    g.ids.extend(ids)
+                    g.content.extend(contents)
+                    g.types.extend(types)
+                    g.row_of.update(zip(ids, range(r0, r0 + m)))
+                    g.n = r0 + m
+                    g.n_sumsq += m
+                    cnt = np.bincount(sh[sh >= 0], minlength=len(g.shard_count))
+                    for c in np.nonzero(cnt)[0]:
+                        g.shard_count[int(c)] += int(cnt[c])
+                    if g.deleted_ids:
+                        for x in ids:
+                            g.deleted_ids.pop(x, None)
+                    g.last_add_rows = range(r0, r0 + m)
+                    if not g._dv_acc_pending:
+                        g._norm_dev_pending.append(g._dv_acc[0])
+                        g._dv_acc_pending = True
+                    g._bump(store=True)
+                    self._sync_num()
+                    rows = torch.arange(r0, r0 + m, device=self.device)
+                    self.num[r0:r0 + m] = rows + 1
+                    self.holder[r0:r0 + m] = self.rank
+                    reach_new.append(rows)
+                gone += [g.ids[r] for r in vic]
+                pruned += prog.finish_segment(res, s)
+                self.conversation_count = count0 + int(seg["c1"]) + 1
+                if seg["consolidate"]:
+                    stats["consolidations"] += 1
+                    dig, first = prog.captures(res, p)
+                    p += 1
+                    self._rc_w1_host(dig, first)
+            if gone:
+                ms._store_delete(gone, graph_unstored=True)
+            if list(res["shard_count"][:len(g.shard_count)]) != list(g.shard_count):
+                raise RuntimeError("native segment apply diverged from the host shard counts")
+            if run[-1]["cluster"]:
+                if reach_new:  # the pass rebuilds the cones from every row
+                    self._reach_add(torch.cat(reach_new))
+                    reach_new.clear()
+                with tracer.stage("cluster", self.device):
+                    self.cluster_pass()
+            i = j + 1
+        return pruned
+
+    def _rc_w1_host(self, dig, first) -> None:
+        """:meth:`run_consolidation`'s host side on one rank from the native
+        run's captures: the profile prompt of every qualifying component,
+        else of the first shard rows (no prune: the segment end already
+        dropped every edge under the threshold)."""
+        ms = self.local
+        g = self.g
+        updates = 0
+        for rows in dig.get():
+            r = ms._extract_profile_from_contents([g.content[int(x)] for x in rows.tolist()])
+            if "Updated" in r:
+                updates += 1
+        if updates == 0:
+            contents = [g.content[int(r)] for r in first.get().tolist()]
+            if len(contents) >= 3:
+                ms._extract_profile_from_contents(contents)
 
     def _apply_exact_segment(self, seg, supers, fact_key, origin_h, codes, Q, flat, f_off, holder_of, shard_of, thr,
                              now, etype, reach_new) -> int:

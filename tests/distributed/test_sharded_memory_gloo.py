@@ -167,6 +167,8 @@ def _sharded(comm, cfg=CPU):
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
                              embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev,
                              force_collectives=cfg.get("force", False), **extra)
+    if "native_w1" in cfg:  # one rank: the native segment applier on / off
+        sm.NATIVE_W1 = bool(cfg["native_w1"])
     if "digest_max" in cfg:  # -1: the boundary-label digest instead of the replicated one
         sm.DIGEST_REPLICATE_MAX = cfg["digest_max"]
     if cfg.get("digest_check"):  # one GPU rank: the row digest equals the replicated one at every point
@@ -216,8 +218,9 @@ def _sharded(comm, cfg=CPU):
     found = [[d["id"] for d in res] for res in sm.search_memories_batch(QUERIES[q0:q1], 5)]
     found = [f for part in comm.all_gather_object(found) for f in part]
     sm.close()
+    native = sm.native_w1_runs
     if comm.rank != 0:
-        return {"stats": stats, "prof": prof, "pf_used": pf_used}
+        return {"stats": stats, "prof": prof, "pf_used": pf_used, "native": native}
     nodes_all, edges_all = {}, {}
     for n_, e_ in parts:
         assert not (set(n_) & set(nodes_all)), "a node is live on two ranks"
@@ -225,7 +228,7 @@ def _sharded(comm, cfg=CPU):
         edges_all.update(e_)
     single = _single(tempfile.mkdtemp(prefix="lzsolo_"), cfg)
     return {"stats": stats, "nodes": nodes_all, "edges": edges_all, "contents": contents, "prof": prof,
-            "total": total, "found": found, "single": single, "spread": spread, "pf_used": pf_used}
+            "total": total, "found": found, "single": single, "spread": spread, "pf_used": pf_used, "native": native}
 
 
 def check_equivalent(out, world, limit):

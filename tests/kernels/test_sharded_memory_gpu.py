@@ -48,6 +48,17 @@ def test_sharded_tenant_gpu_one_rank_row_digest():
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_sharded_tenant_gpu_one_rank_native_vs_segments():
+    """One GPU rank with and without the native segment applier: both end in
+    the single process's state (nodes, edges, counts, digest, profile)."""
+    for native in (True, False):
+        cfg = dict(GPU, steps=3, convs=32, cadence="conversation", native_w1=native)
+        out = spawn(1, functools.partial(_sharded, cfg=cfg))
+        check_equivalent(out, 1, cfg["limit"])
+        assert (out[0]["native"] > 0) == native, out[0]["native"]
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 @pytest.mark.parametrize("world", [1, 2])
 def test_sharded_tenant_gpu_consolidate_stream(world):
     """ShardedMemorySystem.consolidate_stream on the GPU: each batch after the
@@ -58,6 +69,8 @@ def test_sharded_tenant_gpu_consolidate_stream(world):
     out = spawn(world, functools.partial(_sharded, cfg=cfg))
     check_equivalent(out, world, cfg["limit"])
     assert all(out[r]["pf_used"] == 2 for r in range(world))  # batches 2 and 3 came from the prefetch
+    # one rank: the batches go through the native segment applier (csrc/kernels/apply.hip)
+    assert (out[0]["native"] > 0) == (world == 1), out[0]["native"]
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
