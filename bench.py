@@ -187,7 +187,7 @@ def launch_ranks(n: int) -> int:
 HBM_PER_GPU = 288e9  # MI355X HBM3E per GPU (bytes)
 
 
-def hbm_plan(rows: int, dim: int, batch: int, consolidate_convs: int, facts: int = 8) -> dict:
+def hbm_plan(rows: int, dim: int, batch: int, consolidate_convs: int, facts: int = 8, world: int = 1) -> dict:
     """Per-rank HBM plan of every section of this bench (they run one after
     another, each freeing its tenant: the job's peak is the largest section),
     from the tenant's column layout (TenantGraph.hbm_bytes_per_row) plus each
@@ -212,7 +212,11 @@ def hbm_plan(rows: int, dim: int, batch: int, consolidate_convs: int, facts: int
     cons = cap * bpr + 2 * rows * eb * 9 // 8 + encoder + dual_ws + kmeans
     sharded = cap * bpr + 2 * rows * eb * 9 // 8 + F * 2 * (bpr + 64) + encoder + dual_ws + kmeans
     secs = {"headline": head, "consolidate": cons, "consolidate_persistent_graph": cons,
-            "consolidate_sharded": sharded}
+            "consolidate_sharded": sharded,
+            # + the replicated stable base of the incremental digest (int32
+            # endpoints + fp32 weight, and its all-gather staging at 24 B) --
+            # world-sized: every rank holds every rank's stable edges
+            "consolidate_sharded_persistent_graph": sharded + 2 * rows * world * (12 + 24)}
     peak = max(secs.values())
     return {"bytes_per_row": bpr, "sections_gib": {k: round(v / 2 ** 30, 2) for k, v in secs.items()},
             "peak_gib": round(peak / 2 ** 30, 2), "hbm_gib": round(HBM_PER_GPU / 2 ** 30, 2),
@@ -244,6 +248,8 @@ def main():
     ap.add_argument("--global-batch", type=int, default=128, help="queries per rank per global-search step (0: skip)")
     ap.add_argument("--sharded-steps", type=int, default=5,
                     help="timed steps of config 4 as one row-sharded buffer (--rows per rank; 0 = skip)")
+    ap.add_argument("--sharded-persistent-steps", type=int, default=3,
+                    help="timed steps of the row-sharded buffer with prune_threshold 0 (0 = skip)")
     ap.add_argument("--cpu", action="store_true", help="CPU / gloo dry run of the whole flow (tests only)")
     ap.add_argument("--gc-freeze", dest="gc_freeze", action="store_true",
                     help="freeze the startup heap before the timed loops (off by default: the library's results "
@@ -254,7 +260,7 @@ def main():
                     help="print the per-rank HBM plan of every section for these flags (no GPU) and exit")
     a = ap.parse_args()
     if a.hbm_check:
-        plan = hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs)
+        plan = hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs, world=a.gpus)
         print(json.dumps({"n_gpus": a.gpus, "rows_per_rank": a.rows, **plan}))
         sys.exit(0 if plan["fits"] else 1)
 
@@ -566,7 +572,9 @@ def main():
             torch.cuda.empty_cache()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
-        consolidate = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
+        # two untimed warmup batches: the second is the first that takes the
+        # stream's prefetched scan (its side-stream buffers are allocated there)
+        consolidate = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 2, emb,
                                       dim=a.dim, stream=a.consolidate_stream)
         peak("consolidate")
         if a.persistent_graph:
@@ -576,7 +584,7 @@ def main():
             # on a graph of tens of millions of edges
             if dev.type == "cuda":
                 torch.cuda.empty_cache()
-            persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 1, emb,
+            persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 2, emb,
                                          dim=a.dim, prune_threshold=0.0, stream=a.consolidate_stream)
             peak("consolidate_persistent_graph")
     sharded = None
@@ -596,6 +604,22 @@ def main():
         sharded = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_steps, 1, emb, dim=a.dim,
                               clustered=True)
         peak("consolidate_sharded")
+    sharded_pg = None
+    if a.sharded_persistent_steps > 0:
+        # the same buffer with prune_threshold 0: the 2 x rows seeded edges per
+        # rank stay (decay-prune across the ranks on a graph of tens of millions
+        # of edges); run_consolidation's digest is the incremental one (the
+        # batch's stable base all-gathered and labelled once, the volatile
+        # edges per point)
+        if consolidate is None and sharded is None:
+            svc.close()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        sys.path.insert(0, os.path.join(ROOT, "bench"))
+        from bench_consolidate import run_sharded
+        sharded_pg = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_persistent_steps, 1, emb,
+                                 dim=a.dim, clustered=True, prune_threshold=0.0)
+        peak("consolidate_sharded_persistent_graph")
     res = {
         "metric": METRIC,
         "value": round(qps, 2),
@@ -636,7 +660,7 @@ def main():
                              **{f"gen{k}": {"passes": v[0], "ms": round(v[1] * 1e3, 2)} for k, v in gc_log.items()}},
         "prewarm_s": round(t_pre, 1),
         "hbm_per_rank": {"peak_gib_measured": hbm_peak,
-                         "plan": hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs)},
+                         "plan": hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs, world=a.gpus)},
     }
     if consolidate is not None:
         res["consolidate_turns_per_s"] = consolidate["turns_per_s"]
@@ -661,6 +685,13 @@ def main():
             "gc_in_timed_loop")}
         if sharded.get("stages_p50_ms"):  # LZK_TRACE=1
             res["consolidate_sharded"]["stages_p50_ms"] = sharded["stages_p50_ms"]
+    if sharded_pg is not None:
+        res["consolidate_sharded_persistent_graph"] = {k: sharded_pg[k] for k in (
+            "turns_per_s", "ms_per_step", "buffer_nodes_total", "nodes_per_rank", "per_step", "prune_threshold",
+            "edges_total_at_start", "edges_total", "incremental_digest_points", "incremental_digest_base_edges_max",
+            "path", "gc_in_timed_loop")}
+        if sharded_pg.get("stages_p50_ms"):
+            res["consolidate_sharded_persistent_graph"]["stages_p50_ms"] = sharded_pg["stages_p50_ms"]
     from lazzaro_amd.ops import search as _S
     if _S.SPEC_STATS:  # LZK_SPEC_STATS=1 (diagnostic): queries sent to the exact fallback per store search
         res["spec_fallback_queries"] = [int(x) for x in _S.SPEC_STATS[:64]]

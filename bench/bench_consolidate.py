@@ -257,7 +257,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
                 dim: int = 768, dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096,
                 n_top: int = 64, cluster_iters: int = 2, init_edges: int = None, db_dir: str = None,
                 clustered: bool = False, topics_per_rank: int = 32, cadence: str = "conversation",
-                stream: bool = False):
+                stream: bool = False, prune_threshold: float = 0.5):
     """BASELINE config 4 as ONE tenant: a ``nodes_per_rank * world``-node
     buffer row-sharded over the ranks (``ShardedMemorySystem``); every step
     each rank brings ``convs`` conversations, the whole batch is consolidated
@@ -279,7 +279,10 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     ``stream``: ``ShardedMemorySystem.consolidate_stream`` instead of
     per-batch calls -- off by default: on the clustered buffer a batch's
     victims sit in the next batch's candidate lists, whose facts are then
-    re-scanned (profiles/r5/sharded_stream/)."""
+    re-scanned (profiles/r5/sharded_stream/). ``prune_threshold`` 0: the
+    persistent graph (the seeded 2 x rows edges per rank are never pruned;
+    run_consolidation's digest takes the incremental form,
+    ShardedMemorySystem._dcc_begin)."""
     from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
     from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
 
@@ -290,7 +293,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
                              embedding_provider=encoder or HashEmbedder(dim=dim), db_dir=db_dir, device=dev,
                              hierarchy_params={"fine": n_fine, "top": n_top, "every": cluster_every * convs * world,
                                                "iters": cluster_iters},
-                             placement="cluster" if clustered else "origin")
+                             placement="cluster" if clustered else "origin", prune_threshold=prune_threshold)
     g = sm.g
     g._set_dim(dim)
     g.reserve(int(nodes_per_rank * 1.05) + 65536)
@@ -320,6 +323,7 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     g.clear_tracking(stored=False)
     _sync(dev)
     load_s = time.perf_counter() - t0
+    edges0 = sm.get_stats()["total_edges"]
     t0 = time.perf_counter()
     with _ff_timer() as ff:
         sm.cluster_pass()
@@ -393,6 +397,8 @@ def run_sharded(comm, dev, nodes_per_rank: int, convs: int, facts: int, steps: i
     stages = {k: v["p50_ms"] for k, v in tracer.summary().items()} if tracer.enabled else None
     st = sm.get_stats()
     out = {"turns_per_s": round(convs * world * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
+           "prune_threshold": prune_threshold, "edges_total_at_start": edges0,
+           "incremental_digest_points": sm.dcc_points, "incremental_digest_base_edges_max": sm.dcc_base_max,
            "buffer_nodes_total": st["total_nodes"], "nodes_per_rank": nodes_per_rank, "edges_total": st["total_edges"],
            "convs_per_rank_step": convs, "facts_per_conv": facts,
            "per_step": {k: round(v / steps, 1) for k, v in agg.items()},

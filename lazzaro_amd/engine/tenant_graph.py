@@ -1751,7 +1751,7 @@ class TenantGraph:
         if dev.type == "cuda" and min_size >= 2 and take >= 1 and not self._digest_sorted:
             self._maybe_sort_edges()
             with self.on_stream():
-                lab = self._cc_labels() if self._cc is not None else None
+                lab = self._cc_labels() if self._cc is not None and "lab" in self._cc else None
                 key, rows = T.component_digest(self.e["src"], self.e["dst"], self.e["w"], self.kind[:n],
                                                self.sup[:n], self.shard[:n], n, min_size, min_avg_w, take, lab=lab)
                 kr = torch.stack([key, rows.long()]).cpu().numpy()  # one device -> host copy

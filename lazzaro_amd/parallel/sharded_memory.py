@@ -1568,27 +1568,34 @@ class ShardedMemorySystem:
             with tracer.stage("cb_apply_native", dev):
                 pruned += self._native_w1(pl, fact_key, codes, Q, flat, f_off, thr, now, count0, stats, reach_new)
             pl = {"segments": []}  # applied
-        for seg in pl["segments"]:
-            with tracer.stage("cb_apply", dev):
-                pruned_local = self._apply_exact_segment(seg, supers, fact_key, origin_h, codes, Q, flat, f_off,
-                                                         holder_of, shard_of, thr, now, etype, reach_new)
-            pruned += self._sum(pruned_local)[0]
-            self.conversation_count = count0 + int(seg["c1"]) + 1
-            if seg["consolidate"]:
-                stats["consolidations"] += 1
-                with tracer.stage("run_consolidation", dev):
-                    self.run_consolidation()
-            if seg["cluster"]:
-                if reach_new:  # the pass rebuilds the cones from every row
-                    self._reach_add(torch.cat(reach_new))
-                    reach_new.clear()
-                with tracer.stage("cluster", dev):
-                    self.cluster_pass()
-            if self._commit_each:  # the counter as of this conversation
-                n_fact += int((np.asarray(seg["ins_kind"]) == 0).sum())
-                self.local.node_counter = n_fact
-                with tracer.stage("commit", "cpu"):
-                    self.local._save_to_persistence()
+        with tracer.stage("sc_digest_base", dev):
+            self._dcc_begin(pl)
+        try:
+            for seg in pl["segments"]:
+                with tracer.stage("cb_apply", dev):
+                    pruned_local = self._apply_exact_segment(seg, supers, fact_key, origin_h, codes, Q, flat, f_off,
+                                                             holder_of, shard_of, thr, now, etype, reach_new)
+                if self._dcc is not None:
+                    self._dcc["steps"] += int(seg["c1"]) - int(seg["c0"]) + 1
+                pruned += self._sum(pruned_local)[0]
+                self.conversation_count = count0 + int(seg["c1"]) + 1
+                if seg["consolidate"]:
+                    stats["consolidations"] += 1
+                    with tracer.stage("run_consolidation", dev):
+                        self.run_consolidation()
+                if seg["cluster"]:
+                    if reach_new:  # the pass rebuilds the cones from every row
+                        self._reach_add(torch.cat(reach_new))
+                        reach_new.clear()
+                    with tracer.stage("cluster", dev):
+                        self.cluster_pass()
+                if self._commit_each:  # the counter as of this conversation
+                    n_fact += int((np.asarray(seg["ins_kind"]) == 0).sum())
+                    self.local.node_counter = n_fact
+                    with tracer.stage("commit", "cpu"):
+                        self.local._save_to_persistence()
+        finally:
+            self._dcc_end()
         stats["pruned"] += pruned
         if reach_new:
             self._reach_add(torch.cat(reach_new))
@@ -2163,6 +2170,13 @@ class ShardedMemorySystem:
                 res = T.component_digest_local(lsrc, ldst, w, kind_c, sup_c, shard_c, min_size, min_avg_w, take)
         else:
             res = _digest_compact_host(lsrc, ldst, w, valid, live, attr - 1, nl, min_size, min_avg_w, take)
+        return self._digest_contents(res, numof)
+
+    def _digest_contents(self, res, numof: torch.Tensor) -> List[List[str]]:
+        """The digest's (order key, compact id) pairs as content lists: ids to
+        node numbers (``numof``), the holders fill in the contents (one object
+        all-gather), rank 0 groups them by key."""
+        g = self.g
         ok = res[1] >= 0
         nums = torch.where(ok, numof[res[1].clamp_min(0)], torch.full_like(res[1], -1))
         rr = self._rows_of_nums(nums.clamp_min(0))
@@ -2181,6 +2195,199 @@ class ShardedMemorySystem:
             out[-1].append(c)
         return out
 
+    # ---- incremental digest over the ranks. Within one batch of the
+    # reference cadence the digest at every run_consolidation point is the
+    # batch's STABLE base -- the edges that exist at every point: none incident
+    # to a victim of the plan, none that the batch's decays (or a
+    # run_consolidation prune) can bring under the threshold -- plus the few
+    # volatile edges (TenantGraph.cc_begin's definition, per rank). The base is
+    # all-gathered and labelled ONCE per batch (union-find over the replicated
+    # stable edges), its endpoints' liveness / shard fixed for the batch (no
+    # base endpoint is a victim); each point all-gathers only the volatile
+    # edges, replays the decay rounds since the batch start on the replicated
+    # base weights (the same tg_decay rounds every rank ran on its own edges,
+    # bit for bit), unions the volatile edges on top of the base labels and
+    # runs the digest kernels -- instead of all-gathering every edge of every
+    # rank at every point (~43 per step) or the boundary-label rounds above
+    # DIGEST_REPLICATE_MAX. Vertex ids are a batch-wide universe in node-number
+    # order (the base endpoints, the volatile ones, every endpoint the plan
+    # will link), so first-member keys order components as the full digest
+    # does. Reference: buffer_graph.py:99-120, memory_system.py:967-985.
+    DIGEST_INCREMENTAL = True
+    DIGEST_INCREMENTAL_MIN = 1 << 16  # edges over all ranks at the batch start
+    _dcc = None
+    dcc_points = 0  # points served by the incremental digest (tests)
+    dcc_base_max = 0  # the largest replicated base (edges) so far (tests)
+
+    def _dcc_begin(self, pl: Dict) -> None:
+        """Set up a batch's incremental digest (collective; every rank decides
+        alike from all-gathered counts)."""
+        self._dcc = None
+        segs = pl["segments"]
+        g = self.g
+        if not (self.DIGEST_INCREMENTAL and any(s["consolidate"] for s in segs)):
+            return
+        dev = self.device
+        ne = int(g.num_edges) if g.n else 0
+        tot = self._sum(ne)[0]
+        if tot < max(1, self.DIGEST_INCREMENTAL_MIN):
+            return
+        if self.world == 1 and g.on_gpu and tot <= T.dg_small_max_edges():
+            return  # one GPU rank, a few edges: the one-block row digest (_digest_world1)
+        keep = 1.0 - DECAY_RATE
+        steps = sum(int(s["c1"]) - int(s["c0"]) + 1 for s in segs)
+        t0 = NEG_INF
+        if self.prune_threshold > 0.0:  # the segments' decay-prune and run_consolidation's prune
+            t0 = float(self.prune_threshold) * keep ** (-steps) * (1.0 + 1e-4) + 1e-12
+        vic = [np.asarray(s["victims"], np.int64).reshape(-1) for s in segs]
+        vic = np.concatenate(vic) if vic else np.zeros(0, np.int64)
+        ns = 0
+        if ne:
+            vmark = torch.zeros(g.n, dtype=torch.uint8, device=dev)
+            if vic.size:
+                vr = self._rows_of_nums(torch.as_tensor(vic + 1).to(dev))  # live and ghost rows of the victims
+                vr = vr[vr >= 0]
+                if vr.numel():
+                    vmark[vr] = 1
+            with g.on_stream():
+                p = g._partition_stable(vmark, t0)
+            ns = 0 if p is None else int(p)
+            if ns:  # the stable prefix stays in place: segment ends compact the suffix only
+                g._cc = {"ns": ns, "steps": 0, "sharded": True}
+        # the replicated base: (number, number, weight bits), rank order
+        e = g.e
+        if ns:
+            loc = torch.stack([self.num[e["src"][:ns].long()], self.num[e["dst"][:ns].long()],
+                               e["w"][:ns].float().contiguous().view(torch.int32).long()], 1)
+        else:
+            loc = torch.zeros((0, 3), dtype=torch.long, device=dev)
+        base, _ = self._gather_var(loc)
+        # volatile endpoints now, every endpoint the plan links: the universe
+        if ne > ns:
+            vol = torch.cat([self.num[e["src"][ns:].long()], self.num[e["dst"][ns:].long()]])
+        else:
+            vol = torch.zeros(0, dtype=torch.long, device=dev)
+        vol, _ = self._gather_var(vol)
+        planned = [np.asarray(s[k], np.int64).reshape(-1) for s in segs for k in ("edge_src", "edge_dst")]
+        planned = np.concatenate(planned) + 1 if planned else np.zeros(0, np.int64)
+        A = torch.unique(torch.cat([base[:, 0], base[:, 1], vol, torch.as_tensor(planned).to(dev)]))
+        nl = int(A.numel())
+        bs = torch.searchsorted(A, base[:, 0].contiguous())
+        bd = torch.searchsorted(A, base[:, 1].contiguous())
+        nb = int(bs.numel())
+        inb = torch.zeros(nl, dtype=torch.bool, device=dev)
+        inb[bs] = True
+        inb[bd] = True
+        # base endpoints: liveness and shard are fixed for the batch (one all-reduce)
+        attr = torch.zeros(nl, dtype=torch.long, device=dev)
+        bidx = torch.nonzero(inb).flatten()
+        if bidx.numel():
+            attr[bidx] = self._attr_of(A[bidx])
+        # stats arrays: the base as the prefix, room behind it for the volatile edges
+        cap = nb + max(1024, 2 * int(vol.numel()) // 2 + 2 * int(planned.size))
+        src = torch.empty(cap, dtype=torch.int32, device=dev)
+        dst = torch.empty(cap, dtype=torch.int32, device=dev)
+        w = torch.empty(cap, dtype=torch.float32, device=dev)
+        src[:nb] = bs.to(torch.int32)
+        dst[:nb] = bd.to(torch.int32)
+        w[:nb] = base[:, 2].to(torch.int32).view(torch.float32)
+        lab = None
+        if dev.type == "cuda" and nb:
+            from ..ops.graph_ops import components_sel
+            zero = torch.zeros(nl, dtype=torch.uint8, device=dev)
+            lab = components_sel(src[:nb], dst[:nb], nl, None, NEG_INF, zero, nl, 0)
+        self.dcc_base_max = max(self.dcc_base_max, nb)
+        self._dcc = {"ns": ns, "A": A, "nl": nl, "nb": nb, "src": src, "dst": dst, "w": w, "lab": lab,
+                     "attr": attr, "dyn": torch.nonzero(~inb).flatten(), "steps": 0, "wsteps": 0}
+
+    def _dcc_end(self) -> None:
+        if self._dcc is not None and self.g._cc is not None and self.g._cc.get("sharded"):
+            self.g._cc = None
+        self._dcc = None
+
+    def _attr_of(self, nums: torch.Tensor) -> torch.Tensor:
+        """shard + 1 of the live shard nodes among ``nums`` (0: not a live
+        shard node anywhere), from their holders: one all-reduce."""
+        g = self.g
+        rows = self._rows_of_nums(nums)
+        rc = rows.clamp_min(0)
+        mine = (rows >= 0) & (self.holder[rc] == self.rank) & (g.kind[rc] == NODE) & (g.sup[rc] == 0)
+        attr = torch.where(mine, g.shard[rc].long() + 1, torch.zeros_like(rows))
+        if self._coll:
+            attr = self.comm.all_reduce(self._to_comm(attr)).to(self.device)
+        return attr
+
+    def _digest_incremental(self, min_size: int, min_avg_w: float, take: int) -> Optional[List[List[str]]]:
+        """:meth:`component_digest` at a point of a batch with the incremental
+        base (:meth:`_dcc_begin`); None when a volatile endpoint fell outside
+        the batch's universe (every rank sees the same gathered edges, so every
+        rank falls back alike)."""
+        d = self._dcc
+        g = self.g
+        dev = self.device
+        nb, nl, A = d["nb"], d["nl"], d["A"]
+        k = d["steps"] - d["wsteps"]
+        if k > 0 and nb:  # the decay rounds every rank ran on its own stable edges since the batch start
+            T.decay_prune({"src": d["src"][:nb], "w": d["w"][:nb]}, None, None, None, DECAY_RATE, None, False,
+                          steps=k)
+        d["wsteps"] = d["steps"]
+        ns = d["ns"]
+        e = g.e
+        ne = int(g.num_edges) if g.n else 0
+        if ne > ns:
+            loc = torch.stack([self.num[e["src"][ns:].long()], self.num[e["dst"][ns:].long()],
+                               e["w"][ns:].float().contiguous().view(torch.int32).long()], 1)
+        else:
+            loc = torch.zeros((0, 3), dtype=torch.long, device=dev)
+        vol, _ = self._gather_var(loc)
+        m = int(vol.shape[0])
+        vs = torch.searchsorted(A, vol[:, 0].contiguous()).clamp_max(max(nl - 1, 0))
+        vd = torch.searchsorted(A, vol[:, 1].contiguous()).clamp_max(max(nl - 1, 0))
+        if m and nl == 0:
+            return None
+        if m and not bool(((A[vs] == vol[:, 0]) & (A[vd] == vol[:, 1])).all()):
+            return None
+        if nb + m > d["src"].numel():  # grow the volatile room (the base prefix is copied once)
+            cap = nb + 2 * m
+            for key, dt in (("src", torch.int32), ("dst", torch.int32), ("w", torch.float32)):
+                buf = torch.empty(cap, dtype=dt, device=dev)
+                buf[:nb] = d[key][:nb]
+                d[key] = buf
+        src, dst, w = d["src"], d["dst"], d["w"]
+        src[nb:nb + m] = vs.to(torch.int32)
+        dst[nb:nb + m] = vd.to(torch.int32)
+        w[nb:nb + m] = vol[:, 2].to(torch.int32).view(torch.float32)
+        E = nb + m
+        if E == 0:
+            return []
+        attr = d["attr"].clone()
+        dyn = d["dyn"]
+        if dyn.numel():  # endpoints outside the base: victims, new facts (their liveness changes)
+            attr[dyn] = self._attr_of(A[dyn])
+        live = attr > 0
+        if dev.type == "cuda":
+            kind_c = torch.where(live, 1, 2).to(torch.uint8)
+            sup_c = torch.zeros(nl, dtype=torch.uint8, device=dev)
+            shard_c = (attr - 1).clamp_min(0).to(torch.int32)
+            if d["lab"] is not None:
+                from ..ops.graph_ops import components_sel
+                z = d.get("zero")
+                if z is None:
+                    z = d["zero"] = torch.zeros(nl, dtype=torch.uint8, device=dev)
+                lab = components_sel(src[nb:E], dst[nb:E], nl, None, NEG_INF, z, nl, 0, parent=d["lab"].clone())
+            else:
+                lab = None
+            res = T.component_digest(src[:E], dst[:E], w[:E], kind_c, sup_c, shard_c, nl, min_size, min_avg_w, take,
+                                     lab=lab)
+        else:
+            s_, d_ = src[:E].long(), dst[:E].long()
+            valid = torch.zeros(nl, dtype=torch.bool, device=dev)
+            valid[s_] = True
+            valid[d_] = True
+            res = _digest_compact_host(s_, d_, w[:E], valid, live & valid, attr - 1, nl, min_size, min_avg_w, take)
+        self.dcc_points += 1
+        return self._digest_contents(res, A)
+
     def component_digest(self, min_size: int = 3, min_avg_w: float = 0.3,
                          take: int = PROFILE_CONTENTS) -> List[List[str]]:
         """``run_consolidation``'s component view of the WHOLE tenant
@@ -2194,6 +2401,10 @@ class ShardedMemorySystem:
         W = self.world
         n = g.n
         ne = int(g.num_edges) if n else 0
+        if self._dcc is not None:
+            out = self._digest_incremental(min_size, min_avg_w, take)
+            if out is not None:
+                return out
         if W == 1 and g.on_gpu and ne:
             return self._digest_world1(min_size, min_avg_w, take)
         cnt = self._host_ints(ne)[:, 0].tolist()

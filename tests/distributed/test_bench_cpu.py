@@ -23,7 +23,7 @@ def test_bench_two_ranks_cpu(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--cpu", "--gpus", "2", "--rows", "6000", "--dim", "128", "--model", "tiny", "--batch", "32",
            "--steps", "2", "--warmup", "1", "--prewarm-s", "0.2", "--recall-queries", "8", "--consolidate-steps", "1",
-           "--consolidate-convs", "4"]
+           "--consolidate-convs", "4", "--sharded-persistent-steps", "0"]
     env = dict(os.environ, PYTHONPATH=ROOT, LZK_BENCH_DB=str(tmp_path / "db"))
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -46,7 +46,7 @@ def _check_serving(d, batch):
 
 SMALL = ["--cpu", "--rows", "6000", "--dim", "128", "--model", "tiny", "--batch", "32", "--steps", "2", "--warmup",
          "1", "--prewarm-s", "0.2", "--recall-queries", "8", "--consolidate-steps", "1", "--consolidate-convs", "4",
-         "--no-persistent-graph", "--sharded-steps", "1", "--global-batch", "8"]
+         "--no-persistent-graph", "--sharded-steps", "1", "--global-batch", "8", "--sharded-persistent-steps", "0"]
 
 
 def test_bench_self_launches_ranks(tmp_path):
@@ -82,10 +82,10 @@ def test_bench_eight_ranks_cpu(tmp_path):
     consolidation and the row-sharded buffer over all 8 ranks."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "8", "--rows", "3000", "--dim", "128", "--model", "tiny", "--batch", "16", "--steps", "1",
+           "--gpus", "8", "--rows", "5000", "--dim", "128", "--model", "tiny", "--batch", "16", "--steps", "1",
            "--warmup", "1", "--prewarm-s", "0", "--recall-queries", "4", "--consolidate-steps", "1",
            "--consolidate-convs", "2", "--no-persistent-graph", "--sharded-steps", "1", "--global-batch", "4",
-           "--cpu"]
+           "--sharded-persistent-steps", "1", "--cpu"]
     env = dict(os.environ, PYTHONPATH=ROOT, LZK_BENCH_DB=str(tmp_path / "db"), OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -97,7 +97,12 @@ def test_bench_eight_ranks_cpu(tmp_path):
     _check_serving(d, 16)
     assert d["consolidate_turns_per_s"] > 0
     sh = d["consolidate_sharded"]
-    assert sh["turns_per_s"] > 0 and sh["buffer_nodes_total"] == 8 * 3000
+    assert sh["turns_per_s"] > 0 and sh["buffer_nodes_total"] == 8 * 5000
+    # the persistent-graph buffer (8 x 10k seeded edges kept): the incremental
+    # digest served the run_consolidation points from a replicated stable base
+    pg = d["consolidate_sharded_persistent_graph"]
+    assert pg["turns_per_s"] > 0 and pg["edges_total_at_start"] == 8 * 10000
+    assert pg["incremental_digest_points"] > 0 and pg["incremental_digest_base_edges_max"] > 0
 
 
 def test_hbm_plan_eight_gpus_ten_million_rows_fits():
@@ -110,5 +115,6 @@ def test_hbm_plan_eight_gpus_ten_million_rows_fits():
     assert r.returncode == 0, r.stdout + r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 8 and d["fits"]
-    assert set(d["sections_gib"]) == {"headline", "consolidate", "consolidate_persistent_graph", "consolidate_sharded"}
+    assert set(d["sections_gib"]) == {"headline", "consolidate", "consolidate_persistent_graph", "consolidate_sharded",
+                                      "consolidate_sharded_persistent_graph"}
     assert d["peak_gib"] < 0.5 * d["hbm_gib"]

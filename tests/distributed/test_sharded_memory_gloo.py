@@ -125,7 +125,7 @@ def _single(tmp, cfg=CPU):
     ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=cfg["dim"]), enable_async=False,
                       db_dir=tmp, user_id="solo", device=dev, max_buffer_size=cfg["limit"],
                       enable_hierarchy=cfg.get("hier", False), super_node_threshold=cfg.get("sthr", 20),
-                      load_from_disk=False, enable_caching=False)
+                      load_from_disk=False, enable_caching=False, prune_threshold=cfg.get("prune_thr", 0.5))
     g = ms.graph
     codes = [g.shard_id(k) for k in keys0]
     R = cfg["rows"]
@@ -166,7 +166,21 @@ def _sharded(comm, cfg=CPU):
         extra.update(enable_hierarchy=cfg.get("hier", False), super_node_threshold=cfg.get("sthr", 20))
     sm = ShardedMemorySystem(comm, "big", max_buffer_size=cfg["limit"], llm_provider=LocalLLM(),
                              embedding_provider=HashEmbedder(dim=cfg["dim"]), db_dir=tmp, device=dev,
-                             force_collectives=cfg.get("force", False), **extra)
+                             force_collectives=cfg.get("force", False), prune_threshold=cfg.get("prune_thr", 0.5),
+                             **extra)
+    if "dcc_min" in cfg:  # the incremental digest from this many edges (0: every batch with a point)
+        sm.DIGEST_INCREMENTAL_MIN = cfg["dcc_min"]
+    if cfg.get("dcc_check"):  # every incremental point equals the full replicated digest
+        real_inc = sm._digest_incremental
+        checked_pts = []
+
+        def inc_checked(min_size, min_avg_w, take):
+            a = real_inc(min_size, min_avg_w, take)
+            b = sm._digest_replicated(sm._host_ints(sm.g.num_edges)[:, 0].tolist(), min_size, min_avg_w, take)
+            assert a == b, (a, b)
+            checked_pts.append(len(b))
+            return a
+        sm._digest_incremental = inc_checked
     if "native_w1" in cfg:  # one rank: the native segment applier on / off
         sm.NATIVE_W1 = bool(cfg["native_w1"])
     if "digest_max" in cfg:  # -1: the boundary-label digest instead of the replicated one
@@ -219,8 +233,9 @@ def _sharded(comm, cfg=CPU):
     found = [f for part in comm.all_gather_object(found) for f in part]
     sm.close()
     native = sm.native_w1_runs
+    dcc = (sm.dcc_points, sm.dcc_base_max, sum(checked_pts) if cfg.get("dcc_check") else 0)
     if comm.rank != 0:
-        return {"stats": stats, "prof": prof, "pf_used": pf_used, "native": native}
+        return {"stats": stats, "prof": prof, "pf_used": pf_used, "native": native, "dcc": dcc}
     nodes_all, edges_all = {}, {}
     for n_, e_ in parts:
         assert not (set(n_) & set(nodes_all)), "a node is live on two ranks"
@@ -228,7 +243,8 @@ def _sharded(comm, cfg=CPU):
         edges_all.update(e_)
     single = _single(tempfile.mkdtemp(prefix="lzsolo_"), cfg)
     return {"stats": stats, "nodes": nodes_all, "edges": edges_all, "contents": contents, "prof": prof,
-            "total": total, "found": found, "single": single, "spread": spread, "pf_used": pf_used, "native": native}
+            "total": total, "found": found, "single": single, "spread": spread, "pf_used": pf_used, "native": native,
+            "dcc": dcc}
 
 
 def check_equivalent(out, world, limit):
@@ -307,6 +323,22 @@ def test_sharded_tenant_distributed_digest_matches_single_process(world):
     out = spawn(world, functools.partial(_sharded, cfg=dict(EXACT, digest_max=-1)))
     check_equivalent(out, world, LIMIT)
     assert out[0]["contents"]
+
+
+@pytest.mark.parametrize("world,prune_thr", [(2, 0.5), (3, 0.5), (2, 0.0), (3, 0.0)])
+def test_sharded_tenant_incremental_digest(world, prune_thr):
+    """The incremental digest (a batch's stable base all-gathered and
+    labelled once, only the volatile edges per point): at every
+    run_consolidation point the full replicated digest's lists, and the
+    single process's state -- with the default decay-prune and on a
+    persistent graph (prune_threshold 0: no edge is ever pruned)."""
+    cfg = dict(EXACT, dcc_min=0, dcc_check=True, prune_thr=prune_thr)
+    out = spawn(world, functools.partial(_sharded, cfg=cfg))
+    check_equivalent(out, world, LIMIT)
+    d = [out[r]["dcc"] for r in range(world)]
+    assert all(x[0] > 0 for x in d), d  # points served incrementally
+    assert max(x[1] for x in d) > 0, d  # with a non-empty stable base
+    assert d[0][2] > 0, d  # and qualifying components
 
 
 def test_sharded_tenant_reference_cadence_forced_world1():

@@ -59,6 +59,20 @@ def test_sharded_tenant_gpu_one_rank_native_vs_segments():
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("prune_thr", [0.5, 0.0])
+def test_sharded_tenant_gpu_incremental_digest(prune_thr):
+    """Two GPU ranks, the incremental digest (stable base replicated and
+    labelled once per batch by uf_union_sel, the volatile edges unioned on
+    top, digest.hip stats): every point equals the full replicated digest and
+    the run is the single process's -- decay-prune and persistent graph."""
+    cfg = dict(GPU, steps=3, convs=32, cadence="conversation", dcc_min=0, dcc_check=True, prune_thr=prune_thr)
+    out = spawn(2, functools.partial(_sharded, cfg=cfg))
+    check_equivalent(out, 2, cfg["limit"])
+    d = [out[r]["dcc"] for r in range(2)]
+    assert all(x[0] > 0 for x in d) and max(x[1] for x in d) > 0, d
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 @pytest.mark.parametrize("world", [1, 2])
 def test_sharded_tenant_gpu_consolidate_stream(world):
     """ShardedMemorySystem.consolidate_stream on the GPU: each batch after the
