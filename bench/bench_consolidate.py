@@ -449,7 +449,12 @@ if __name__ == "__main__":
                     help="--sharded: per-rank topic clusters + cluster placement (exact scan pruning applies)")
     ap.add_argument("--cadence", default="conversation", choices=["conversation", "batch"],
                     help="--sharded: reference per-conversation cadence or once-per-batch")
+    ap.add_argument("--no-incremental-digest", action="store_true",
+                    help="--sharded: the full digest at every run_consolidation point (A/B)")
     a = ap.parse_args()
+    if a.no_incremental_digest:
+        from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
+        ShardedMemorySystem.DIGEST_INCREMENTAL = False
     comm = Communicator.init()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
@@ -460,8 +465,9 @@ if __name__ == "__main__":
     fn = run_sharded if a.sharded else run
     res = fn(comm, dev, a.nodes, a.convs, a.facts, a.steps, a.warmup, enc, dim=a.dim, cluster_every=a.cluster_every,
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
-             **({"clustered": a.clustered, "cadence": a.cadence, "stream": a.stream} if a.sharded else {"prune_threshold": a.prune_threshold,
-                                                              "persist_async": a.persist_async, "stream": a.stream}))
+             **({"clustered": a.clustered, "cadence": a.cadence, "stream": a.stream,
+                 "prune_threshold": a.prune_threshold} if a.sharded else
+                {"prune_threshold": a.prune_threshold, "persist_async": a.persist_async, "stream": a.stream}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)
     if comm.enabled:

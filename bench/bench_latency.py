@@ -42,6 +42,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--model", default="bge-base")
+    ap.add_argument("--api-only", action="store_true", help="only the 10M-memory MemorySystem sections")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     from lazzaro_amd.core.embedders import OnDeviceEmbedder
@@ -51,6 +52,8 @@ def main():
     q = "what did I say about moving to Lisbon and learning the cello?"
     ids, lens = emb.tok.encode_batch([q], emb.max_len)
     res = {"metric": "interactive search_memories latency", "model": a.model}
+    if a.api_only:
+        return api(a, emb, q, dev, res, (10_000_000,))
     for _ in range(5):
         emb.encoder.forward(ids, lens)
         emb.embed_tensor([q])
@@ -84,14 +87,20 @@ def main():
         res["store_search_200k"] = timed(lambda: st.search_nodes(qv, user_id="u", limit=5), a.iters // 2)
         res["embed_plus_store_search_200k"] = timed(
             lambda: st.search_nodes(emb.embed(q), user_id="u", limit=5), a.iters // 2)
-    # through the product API: MemorySystem on the GPU, the tenant graph in
-    # HBM (search_memories = embed + store search + Node mapping; the chat
-    # retrieval = embed + hierarchical/vector retrieval + neighbour boost,
-    # LLM excluded), tenants of 200k and 10M memories
+    api(a, emb, q, dev, res, (200_000, 10_000_000))
+
+
+def api(a, emb, q, dev, res, sizes):
+    """Through the product API: MemorySystem on the GPU, the tenant graph in
+    HBM (search_memories = embed + store search + Node mapping; the chat
+    retrieval = embed + hierarchical/vector retrieval + neighbour boost, LLM
+    excluded); plus the store search alone (the embedded query given)."""
+    import tempfile
+
     from bench import populate
     from lazzaro_amd.core.memory_system import MemorySystem
     from lazzaro_amd.core.providers import LocalLLM
-    for n in (200_000, 10_000_000):
+    for n in sizes:
         with tempfile.TemporaryDirectory() as d:
             ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=emb, device=dev, db_dir=d,
                               load_from_disk=False, enable_async=False, enable_caching=False,
@@ -101,12 +110,18 @@ def main():
             tag = f"{n // 1000}k" if n < 1_000_000 else f"{n // 1_000_000}M"
             ms.search_memories(q, limit=5)
             res[f"api_search_memories_{tag}"] = timed(lambda: ms.search_memories(q, limit=5), a.iters // 2)
+            qe = emb.embed_tensor([q])[0]
+            g = ms.graph
+            g.store_search(qe, 5)
+            res[f"store_search_only_{tag}"] = timed(lambda: g.store_search(qe, 5), a.iters // 2)
+            res[f"embed_only_{tag}"] = timed(lambda: emb.embed_tensor([q]), a.iters // 2)
             ms._retrieve_for(q)
             res[f"api_chat_retrieval_{tag}"] = timed(lambda: ms._retrieve_for(q), a.iters // 2)
             ms.close()
             del ms
             torch.cuda.empty_cache()
     print(json.dumps(res), flush=True)
+    return res
 
 
 if __name__ == "__main__":

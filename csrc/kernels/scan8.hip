@@ -103,8 +103,12 @@ int cu_count() {
 constexpr int NW_WAVES = 8;
 constexpr int NW_MAXK = 16;  // Dp <= 1024 bytes = 16 k-chunks of 64
 
-template <bool HAS_BIAS, int NQT>
-__global__ __launch_bounds__(NW_WAVES * 64, 1) void scan8_narrow_kernel(
+// KKT: the fragment arrays' length (12 = the 768-byte rows of bge-base /
+// d = 768 exactly, 16 = any Dp <= 1024); with 12 and one query tile the
+// kernel fits 128 VGPRs, so both blocks of a CU are resident at once (twice
+// the row bytes in flight of the 16-chunk build, which held 160 VGPRs).
+template <bool HAS_BIAS, int NQT, int KKT>
+__global__ __launch_bounds__(NW_WAVES * 64, (NQT == 1 && KKT <= 12) ? 2 : 1) void scan8_narrow_kernel(
     const signed char* __restrict__ X, long ldx, int nrows, const signed char* __restrict__ Qm, long ldq, int nq,
     int KK, const float* __restrict__ bias, const float* __restrict__ rs, const float* __restrict__ qs, float alpha,
     const float* __restrict__ thr, Recs rec) {
@@ -139,20 +143,20 @@ __global__ __launch_bounds__(NW_WAVES * 64, 1) void scan8_narrow_kernel(
 
   // two named fragment buffers (a runtime index into one array would put
   // it in scratch memory)
-  i32x4 fa[NW_MAXK], fb[NW_MAXK];
-  auto load = [&](i32x4 (&a)[NW_MAXK], int b) {
+  i32x4 fa[KKT], fb[KKT];
+  auto load = [&](i32x4 (&a)[KKT], int b) {
     const int r = min(b * 16 + l16, nrows - 1);
     const signed char* src = X + (long)r * ldx + lq * 16;
 #pragma unroll
-    for (int kk = 0; kk < NW_MAXK; ++kk)
+    for (int kk = 0; kk < KKT; ++kk)
       if (kk < KK) a[kk] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(src + kk * 64));
   };
-  auto body = [&](const i32x4 (&a)[NW_MAXK], int b) {
+  auto body = [&](const i32x4 (&a)[KKT], int b) {
     i32x4 acc[NQT];
 #pragma unroll
     for (int t = 0; t < NQT; ++t) acc[t] = (i32x4){0, 0, 0, 0};
 #pragma unroll
-    for (int kk = 0; kk < NW_MAXK; ++kk) {
+    for (int kk = 0; kk < KKT; ++kk) {
       if (kk < KK) {
 #pragma unroll
         for (int t = 0; t < NQT; ++t) {
@@ -233,12 +237,19 @@ LZK_EXPORT int lzk_scan8_narrow(const void* X8, long ldx, int nrows, const void*
   const signed char* x = (const signed char*)X8;
   const signed char* q = (const signed char*)Q8;
   const int KK = D_bytes / 64;
-#define LZK_NW(B, T)                                                                                           \
-  do {                                                                                                         \
-    (void)hipFuncSetAttribute((const void*)scan8_narrow_kernel<B, T>,                                          \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                          \
-    hipLaunchKernelGGL((scan8_narrow_kernel<B, T>), dim3(grid), dim3(NW_WAVES * 64), lds, st, x, ldx, nrows, q, \
-                       ldq, nq, KK, bias, rscale, qscale, alpha, thr, rec);                                    \
+#define LZK_NW3(B, T, KT)                                                                                       \
+  do {                                                                                                          \
+    (void)hipFuncSetAttribute((const void*)scan8_narrow_kernel<B, T, KT>,                                       \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                           \
+    hipLaunchKernelGGL((scan8_narrow_kernel<B, T, KT>), dim3(grid), dim3(NW_WAVES * 64), lds, st, x, ldx, nrows, \
+                       q, ldq, nq, KK, bias, rscale, qscale, alpha, thr, rec);                                  \
+  } while (0)
+#define LZK_NW(B, T)              \
+  do {                            \
+    if (KK == 12)                 \
+      LZK_NW3(B, T, 12);          \
+    else                          \
+      LZK_NW3(B, T, NW_MAXK);     \
   } while (0)
 #define LZK_NWT(B)                    \
   do {                                \
@@ -257,5 +268,6 @@ LZK_EXPORT int lzk_scan8_narrow(const void* X8, long ldx, int nrows, const void*
   else LZK_NWT(false);
 #undef LZK_NWT
 #undef LZK_NW
+#undef LZK_NW3
   return (int)hipGetLastError();
 }

@@ -19,6 +19,7 @@
 #include "lzk_g256.h"
 
 #include <cstdlib>
+#include <cfloat>
 
 LZK_DEBUG_STATE(search256)
 
@@ -366,6 +367,45 @@ __global__ __launch_bounds__(256) void cand_gather_kernel(const int4* __restrict
     }
   }
   const int n = min(n0, bcap);
+  if (nq < 64) {
+    // narrow batches: every record of a wave mostly files into the same one
+    // or few lists, so one atomic per (wave, query) with the lanes' slots from
+    // mbcnt -- per-lane atomics on the single count of a one-query search
+    // serialise (~30 us for its ~10k records)
+    const int lane = threadIdx.x & 63;
+    for (int e0 = blockIdx.x * 256 + (threadIdx.x & ~63); e0 < n; e0 += gridDim.x * 256) {
+      const int e = e0 + lane;
+      int4 v = make_int4(-1, 0, 0, 0);
+      if (e < n) v = buf[(long)b * bcap + e];
+      const bool ok = (unsigned)v.x < (unsigned)nq;
+#pragma unroll
+      for (int list = 0; list < 2; ++list) {
+        int* cn = list ? cnt2 : cnt;
+        if (!cn) continue;
+        bool want = ok && (v.w & (1 << list));
+        unsigned long long todo = __ballot(want);
+        while (todo) {
+          const int lead = __builtin_ctzll(todo);
+          const int ql = __shfl(v.x, lead, 64);
+          const unsigned long long grp = __ballot(want && v.x == ql);
+          int base = 0;
+          if (lane == lead) base = atomicAdd(cn + ql, __popcll(grp)) & 0x3fffffff;
+          base = __shfl(base, lead, 64);
+          if (want && v.x == ql) {
+            const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(grp >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)grp, 0u));
+            if (pos < cap) {
+              (list ? cs2 : cs)[(long)ql * cap + pos] = __int_as_float(v.z);
+              (list ? ci2 : ci)[(long)ql * cap + pos] = v.y;
+            }
+            want = false;
+          }
+          todo &= ~grp;
+        }
+      }
+    }
+    return;
+  }
   for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
     const int4 v = buf[(long)b * bcap + e];
     if ((unsigned)v.x >= (unsigned)nq) continue;  // (a +inf score of a padding query column)
@@ -487,6 +527,94 @@ __global__ __launch_bounds__(256) void cand_select_kernel(const int* __restrict_
 #pragma unroll
       for (int t = 0; t < K - 1; ++t) { top.s[t] = top.s[t + 1]; top.i[t] = top.i[t + 1]; }
       top.s[K - 1] = LZK_NEG_INF; top.i[K - 1] = 0x7fffffff;
+    }
+  }
+}
+
+// The same selection with a whole block per query (narrow batches: one
+// wave walking a list of thousands of entries with a dependent load per
+// entry was ~50 us of the single-query search): the list is read 16 entries
+// per thread at a time (loads issued before any push: a 16k-entry list in
+// one round trip); each wave takes its own kout best by shuffles alone into
+// LDS, then wave 0 selects the block's kout of those 16 x kout -- one
+// barrier instead of two per round.
+template <int K>
+__global__ __launch_bounds__(1024) void cand_select_block_kernel(const int* __restrict__ cnt,
+                                                                 const float* __restrict__ cs,
+                                                                 const int* __restrict__ ci, int cap, int nq,
+                                                                 int kout, long idx_offset, float* __restrict__ os,
+                                                                 long* __restrict__ oi, int* __restrict__ ovf,
+                                                                 const int* __restrict__ need) {
+  __shared__ float ls[16 * K];
+  __shared__ int li[16 * K];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x;
+  const int c = cnt[q];
+  if (threadIdx.x == 0) ovf[q] = (c > cap || (need && c < need[q])) ? 1 : 0;
+  const int n = min(c & 0x3fffffff, cap);
+  TopK<K> top;
+  top.init();
+  const float* s = cs + (long)q * cap;
+  const int* ix = ci + (long)q * cap;
+  constexpr int U = 16;
+  for (int p0 = 0; p0 < n; p0 += 1024 * U) {
+    float sv[U];
+    int iv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * 1024 + (int)threadIdx.x;
+      sv[u] = p < n ? s[p] : LZK_NEG_INF;
+      iv[u] = p < n ? ix[p] : 0x7fffffff;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (p0 + u * 1024 + (int)threadIdx.x < n) top.push(sv[u], iv[u]);
+  }
+  // stage 1: the wave's kout best (wave argmax rounds, no barrier)
+  for (int j = 0; j < kout; ++j) {
+    const float hs = top.s[0];
+    const int hi = top.i[0];
+    float bs = hs;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) { ls[wave * K + j] = bs; li[wave * K + j] = bi; }
+    if (hi == bi && hs == bs && bi != 0x7fffffff) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) { top.s[t] = top.s[t + 1]; top.i[t] = top.i[t + 1]; }
+      top.s[K - 1] = LZK_NEG_INF; top.i[K - 1] = 0x7fffffff;
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // stage 2: wave 0 over the 16 x kout wave winners
+  TopK<K> t2;
+  t2.init();
+  for (int p = lane; p < 16 * kout; p += 64) t2.push(ls[(p / kout) * K + p % kout], li[(p / kout) * K + p % kout]);
+  for (int j = 0; j < kout; ++j) {
+    const float hs = t2.s[0];
+    const int hi = t2.i[0];
+    float bs = hs;
+    int bi = hi;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float s2 = __shfl_xor(bs, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (better(s2, i2, bs, bi)) { bs = s2; bi = i2; }
+    }
+    if (lane == 0) {
+      const bool none = bi == 0x7fffffff || bs == LZK_NEG_INF;
+      os[(long)q * kout + j] = none ? LZK_NEG_INF : bs;
+      oi[(long)q * kout + j] = none ? -1 : (long)bi + idx_offset;
+    }
+    if (hi == bi && hs == bs && bi != 0x7fffffff) {
+#pragma unroll
+      for (int t = 0; t < K - 1; ++t) { t2.s[t] = t2.s[t + 1]; t2.i[t] = t2.i[t + 1]; }
+      t2.s[K - 1] = LZK_NEG_INF; t2.i[K - 1] = 0x7fffffff;
     }
   }
 }
@@ -648,10 +776,16 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
                                                            float* __restrict__ cs, const int* __restrict__ ci,
                                                            const float* __restrict__ cut, float floor,
                                                            const float* __restrict__ tau, int k_need,
-                                                           int need_val, int* __restrict__ need) {
+                                                           int need_val, int* __restrict__ need,
+                                                           int* __restrict__ hitc, int* __restrict__ done) {
   __shared__ int s_hits;
   const int q = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // gridDim.y blocks share a query's list (narrow batches): block y takes
+  // the 256-entry groups y, y + gridDim.y, ...; the certificate's hit count
+  // is summed over them (hitc / done: per-query counters zeroed by the
+  // launcher) and the query's last block writes need[q]
+  const int split = gridDim.y;
   if (threadIdx.x == 0) s_hits = 0;
   __syncthreads();
   const float tq = tau ? tau[q] : LZK_NEG_INF;
@@ -666,7 +800,7 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
     if (c < chunks) load4<F32>(Qm, (long)q * ldq + 4 * c, qv[t]);
   }
   const float cq = cut ? cut[q] : LZK_NEG_INF;
-  for (int base = wave * 64; base < n; base += 256) {
+  for (int base = blockIdx.y * 256 + wave * 64; base < n; base += 256 * split) {
     const long li = (long)q * cap + base + lane;
     bool keep = base + lane < n;
     if (keep && cut) {
@@ -709,7 +843,109 @@ __global__ __launch_bounds__(256) void cand_rescore_kernel(const void* __restric
     __syncthreads();
     // tau = -inf: every row that can matter is in the list (the caller's
     // threshold already sits a worst-case margin below its floor)
-    if (threadIdx.x == 0) need[q] = (s_hits >= k_need || tq == LZK_NEG_INF) ? 0 : need_val;
+    if (threadIdx.x == 0) {
+      int tot = s_hits;
+      bool last = true;
+      if (split > 1) {
+        atomicAdd(&hitc[q], s_hits);
+        __threadfence();
+        last = atomicAdd(&done[q], 1) == split - 1;
+        if (last) tot = atomicAdd(&hitc[q], 0);
+      }
+      if (last) need[q] = (tot >= k_need || tq == LZK_NEG_INF) ? 0 : need_val;
+    }
+  }
+}
+
+// cand_rescore_kernel for narrow batches (split over gridDim.y blocks per
+// query): 16 lanes per entry, so a wave re-scores up to 4 live entries per
+// row-read latency instead of one; the query staged once per block in LDS.
+// Same outputs and certificate counters as the wave-per-entry kernel.
+template <bool F32>
+__global__ __launch_bounds__(256) void cand_rescore4_kernel(const void* __restrict__ X, long ldx,
+                                                            const void* __restrict__ Qm, long ldq, int D,
+                                                            const float* __restrict__ bias, float alpha,
+                                                            const int* __restrict__ cnt, int cap,
+                                                            float* __restrict__ cs, const int* __restrict__ ci,
+                                                            const float* __restrict__ cut, float floor,
+                                                            const float* __restrict__ tau, int k_need, int need_val,
+                                                            int* __restrict__ need, int* __restrict__ hitc,
+                                                            int* __restrict__ done) {
+  __shared__ float qs_l[2048];
+  __shared__ int s_hits;
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int part = lane & 15, g = lane >> 4;
+  const int split = gridDim.y;
+  if (threadIdx.x == 0) s_hits = 0;
+  for (int c = threadIdx.x; c < (D >> 2); c += 256) {
+    float v[4];
+    load4<F32>(Qm, (long)q * ldq + 4 * c, v);
+    qs_l[4 * c] = v[0]; qs_l[4 * c + 1] = v[1]; qs_l[4 * c + 2] = v[2]; qs_l[4 * c + 3] = v[3];
+  }
+  __syncthreads();
+  const float tq = tau ? tau[q] : LZK_NEG_INF;
+  int hits = 0;
+  const int n = min(cnt[q] & 0x3fffffff, cap);
+  const int chunks = D >> 2;
+  const float cq = cut ? cut[q] : LZK_NEG_INF;
+  for (int base = blockIdx.y * 256 + wave * 64; base < n; base += 256 * split) {
+    const long li0 = (long)q * cap + base + lane;
+    bool keep = base + lane < n;
+    if (keep && cut) {
+      keep = cs[li0] >= cq;
+      if (!keep) cs[li0] = LZK_NEG_INF;
+    }
+    unsigned long long live = __ballot(keep);
+    while (live) {
+      // the next (up to) 4 live entries: lane group g takes the g-th
+      int jj = -1;
+      unsigned long long m = live;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int b = m ? __builtin_ctzll(m) : -1;
+        if (t == g) jj = b;
+        if (m) m &= m - 1;
+      }
+      live = m;
+      float acc = 0.f;
+      int r = -1;
+      if (jj >= 0) {
+        r = ci[(long)q * cap + base + jj];
+        for (int c = part; c < chunks; c += 16) {
+          float xv[4];
+          load4<F32>(X, (long)r * ldx + 4 * c, xv);
+          acc = fmaf(qs_l[4 * c], xv[0], acc);
+          acc = fmaf(qs_l[4 * c + 1], xv[1], acc);
+          acc = fmaf(qs_l[4 * c + 2], xv[2], acc);
+          acc = fmaf(qs_l[4 * c + 3], xv[3], acc);
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      bool hit = false;
+      if (jj >= 0) {
+        const float sc = alpha * acc + (bias ? bias[r] : 0.f);
+        if (part == 0) cs[(long)q * cap + base + jj] = sc >= floor ? sc : LZK_NEG_INF;
+        hit = part == 0 && sc >= floor && sc >= tq;
+      }
+      hits += __popcll(__ballot(hit));  // wave-uniform
+    }
+  }
+  if (need) {
+    if (lane == 0 && hits) atomicAdd(&s_hits, hits);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = s_hits;
+      bool last = true;
+      if (split > 1) {
+        atomicAdd(&hitc[q], s_hits);
+        __threadfence();
+        last = atomicAdd(&done[q], 1) == split - 1;
+        if (last) tot = atomicAdd(&hitc[q], 0);
+      }
+      if (last) need[q] = (tot >= k_need || tq == LZK_NEG_INF) ? 0 : need_val;
+    }
   }
 }
 
@@ -770,6 +1006,57 @@ __global__ __launch_bounds__(256) void cand_cut_kernel(const void* __restrict__ 
   const float m = margin[q];
   float c = lo - m - (2e-4f * fabsf(alpha) + 1e-6f * (1.f + fabsf(lo)));
   if (has_floor) c = fmaxf(c, floor - m);  // (fmaxf: a nan c takes the floor)
+  if (c != c) c = LZK_NEG_INF;
+  cut[q] = c;
+}
+
+// cand_cut_kernel for narrow batches: a 1024-thread block per query, wave j
+// scores row j (k <= 16) -- the k exact scores in one row-read latency
+// instead of k dependent ones (~32 us for one query).
+template <bool F32>
+__global__ __launch_bounds__(1024) void cand_cut_block_kernel(const void* __restrict__ X, long ldx, long nrows,
+                                                              const void* __restrict__ Qm, long ldq, int D, int nq,
+                                                              const float* __restrict__ bias, float alpha,
+                                                              const long* __restrict__ rows, int ldr, int k,
+                                                              const float* __restrict__ margin, float floor,
+                                                              int has_floor, float* __restrict__ cut) {
+  __shared__ float sc_w[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x;
+  const int chunks = D >> 2;
+  constexpr int MAXC = 8;  // D <= 2048
+  if (wave < k) {
+    const long r = rows[(long)q * ldr + wave];  // wave-uniform
+    float sc = LZK_NEG_INF;
+    if (r >= 0 && r < nrows) {
+      float acc = 0.f;
+#pragma unroll
+      for (int t = 0; t < MAXC; ++t) {
+        const int c = lane + 64 * t;
+        if (c < chunks) {
+          float qv[4], xv[4];
+          load4<F32>(Qm, (long)q * ldq + 4 * c, qv);
+          load4<F32>(X, r * ldx + 4 * c, xv);
+          acc = fmaf(qv[0], xv[0], acc);
+          acc = fmaf(qv[1], xv[1], acc);
+          acc = fmaf(qv[2], xv[2], acc);
+          acc = fmaf(qv[3], xv[3], acc);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      sc = alpha * acc + (bias ? bias[r] : 0.f);
+      if (!(sc > LZK_NEG_INF && sc < __builtin_inff())) sc = LZK_NEG_INF;  // -inf, +inf or nan
+    }
+    if (lane == 0) sc_w[wave] = sc;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float lo = __builtin_inff();
+  for (int j = 0; j < k; ++j) lo = fminf(lo, sc_w[j]);
+  const float m = margin[q];
+  float c = lo - m - (2e-4f * fabsf(alpha) + 1e-6f * (1.f + fabsf(lo)));
+  if (has_floor) c = fmaxf(c, floor - m);
   if (c != c) c = LZK_NEG_INF;
   cut[q] = c;
 }
@@ -1025,9 +1312,17 @@ LZK_EXPORT int lzk_cand_select(const int* cnt, const float* cs, const int* ci, i
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((nq + 3) / 4), block(256);
   if (kout > kslot) return (int)hipErrorInvalidValue;
-#define LZK_SEL(KK) \
-  hipLaunchKernelGGL(cand_select_kernel<KK>, grid, block, 0, st, cnt, cs, ci, cap, nq, kout, idx_offset, os, oi, ovf, \
-                     need)
+  // narrow batches: a block per query (cand_select_block_kernel)
+  const bool blk = nq < 64;
+#define LZK_SEL(KK)                                                                                                   \
+  do {                                                                                                                \
+    if (blk)                                                                                                          \
+      hipLaunchKernelGGL(cand_select_block_kernel<KK>, dim3((unsigned)nq), dim3(1024), 0, st, cnt, cs, ci, cap, nq,   \
+                         kout, idx_offset, os, oi, ovf, need);                                                        \
+    else                                                                                                              \
+      hipLaunchKernelGGL(cand_select_kernel<KK>, grid, block, 0, st, cnt, cs, ci, cap, nq, kout, idx_offset, os, oi,  \
+                         ovf, need);                                                                                  \
+  } while (0)
   switch (kslot) {
     case 1: LZK_SEL(1); break;
     case 2: LZK_SEL(2); break;
@@ -1100,14 +1395,67 @@ LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
   return (int)(nblk < ncu ? nblk : ncu);
 }
 
+// Blocks per query of the re-score: one for wide batches; a narrow batch
+// (the interactive turn: ONE query, a list of hundreds to thousands of
+// entries above the cut) spreads each list over up to 64 blocks -- one block
+// re-scoring a list row by row was 330 us of a 2.2 ms single-query search.
+// The certificate's per-query counters live in a per-device scratch zeroed on
+// the stream before each split launch.
+namespace {
+constexpr int RESCORE_SPLIT_MAX = 64;
+int rescore_split(int nq) {
+  if (nq >= 64) return 1;
+  int s = 256 / nq;
+  return s < 1 ? 1 : (s > RESCORE_SPLIT_MAX ? RESCORE_SPLIT_MAX : s);
+}
+thread_local int* g_rs_scratch[16] = {};
+thread_local int g_rs_cap[16] = {};
+int* rescore_counters(int nq, hipStream_t st) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 16) return nullptr;
+  if (g_rs_cap[dev] < 2 * nq) {
+    if (g_rs_scratch[dev]) (void)hipFree(g_rs_scratch[dev]);
+    g_rs_scratch[dev] = nullptr;
+    const int cap = 2 * (nq > 4096 ? nq : 4096);
+    if (hipMalloc(&g_rs_scratch[dev], (size_t)cap * sizeof(int)) != hipSuccess) {
+      g_rs_cap[dev] = 0;
+      return nullptr;
+    }
+    g_rs_cap[dev] = cap;
+  }
+  if (hipMemsetAsync(g_rs_scratch[dev], 0, (size_t)2 * nq * sizeof(int), st) != hipSuccess) return nullptr;
+  return g_rs_scratch[dev];
+}
+
+template <bool F32>
+int launch_rescore(const void* X, long ldx, const void* Q, long ldq, int nq, int D, const float* bias, float alpha,
+                   const int* cnt, int cap, float* cs, const int* ci, const float* cut, float floor, const float* tau,
+                   int k_need, int need_val, int* need, hipStream_t st) {
+  int split = rescore_split(nq);
+  int* ctr = nullptr;
+  if (split > 1 && need) {
+    ctr = rescore_counters(nq, st);
+    if (!ctr) split = 1;
+  }
+  if (split > 1)  // narrow: 4 entries per wave per row read
+    hipLaunchKernelGGL(cand_rescore4_kernel<F32>, dim3((unsigned)nq, (unsigned)split), dim3(256), 0, st, X, ldx, Q,
+                       ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need, need_val, need, ctr,
+                       ctr ? ctr + nq : nullptr);
+  else
+    hipLaunchKernelGGL(cand_rescore_kernel<F32>, dim3((unsigned)nq, 1u), dim3(256), 0, st, X, ldx, Q, ldq, D, bias,
+                       alpha, cnt, cap, cs, ci, cut, floor, tau, k_need, need_val, need, ctr, ctr ? ctr + nq : nullptr);
+  return (int)hipGetLastError();
+}
+}  // namespace
+
 // Exact bf16 re-score of candidate lists in place (see cand_rescore_kernel).
 LZK_EXPORT int lzk_cand_rescore(const void* X16, long ldx, const void* Q16, long ldq, int nq, int D, const float* bias,
                                 float alpha, const int* cnt, int cap, float* cs, const int* ci, const float* cut,
                                 float floor, const float* tau, int k_need, int need_val, int* need, void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(cand_rescore_kernel<false>, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, X16, ldx,
-                     Q16, ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need, need_val, need);
-  return (int)hipGetLastError();
+  return launch_rescore<false>(X16, ldx, Q16, ldq, nq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need,
+                               need_val, need, (hipStream_t)stream);
 }
 
 // The same from fp32 rows (X32 [*, ldx] fp32, 16-B aligned rows) and fp32
@@ -1117,8 +1465,51 @@ LZK_EXPORT int lzk_cand_rescore32(const float* X32, long ldx, const float* Q32, 
                                   const float* cut, float floor, const float* tau, int k_need, int need_val,
                                   int* need, void* stream) {
   if (D % 4 != 0 || D > 2048 || nq <= 0 || ldx % 4 != 0 || ldq % 4 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(cand_rescore_kernel<true>, dim3((unsigned)nq), dim3(256), 0, (hipStream_t)stream, X32, ldx, Q32,
-                     ldq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need, need_val, need);
+  return launch_rescore<true>(X32, ldx, Q32, ldq, nq, D, bias, alpha, cnt, cap, cs, ci, cut, floor, tau, k_need,
+                              need_val, need, (hipStream_t)stream);
+}
+
+// Per-query thresholds of a low-precision store search in ONE launch (ops.
+// search flat_topk_i8; it replaced ~12 elementwise ATen launches, ~55 us of a
+// single-query search): from the sample's column ``col`` of ``ts``
+//   tau  = t - 2e-4 (1 + |t|), nan -> -inf, +-inf -> +-FLT_MAX (torch
+//          nan_to_num(nan=-inf): the sample's accumulation-order slack)
+//   thr  = tau - margin (margin null: tau)                -- the scan threshold
+//   cert = thr + margin_rig, + 1e-6 (1 + |.|), nan / -inf -> -inf, +inf ->
+//          FLT_MAX (ops.search _cert_tau without a floor) -- the certificate
+// and the per-query list counts zeroed. Rounded op by op like the torch chain.
+__global__ __launch_bounds__(256) void thr_prep_kernel(const float* __restrict__ ts, long ldts, int col,
+                                                       const float* __restrict__ margin,
+                                                       const float* __restrict__ margin_rig, int nq,
+                                                       float* __restrict__ thr, float* __restrict__ cert,
+                                                       int* __restrict__ cnt) {
+#pragma clang fp contract(off)
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  float t = ts[(long)q * ldts + col];
+  const float sl = 1.0f + fabsf(t);
+  t = t - 2e-4f * sl;
+  if (t != t) t = LZK_NEG_INF;
+  else if (t == LZK_NEG_INF) t = -FLT_MAX;
+  else if (t == __builtin_inff()) t = FLT_MAX;
+  const float th = margin ? t - margin[q] : t;
+  thr[q] = th;
+  if (cert) {
+    float c = margin_rig ? th + margin_rig[q] : th;
+    const float cs = 1.0f + fabsf(c);
+    c = c + 1e-6f * cs;
+    if (c != c) c = LZK_NEG_INF;
+    else if (c == __builtin_inff()) c = FLT_MAX;
+    cert[q] = c;
+  }
+  if (cnt) cnt[q] = 0;
+}
+
+LZK_EXPORT int lzk_thr_prep(const float* ts, long ldts, int col, const float* margin, const float* margin_rig, int nq,
+                            float* thr, float* cert, int* cnt, void* stream) {
+  if (nq <= 0 || col < 0 || col >= ldts || !ts || !thr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(thr_prep_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ts, ldts,
+                     col, margin, margin_rig, nq, thr, cert, cnt);
   return (int)hipGetLastError();
 }
 
@@ -1131,6 +1522,15 @@ LZK_EXPORT int lzk_cand_cut(const void* X, long ldx, long nrows, const void* Q, 
   if (D % 4 != 0 || D > 2048 || nq <= 0 || k <= 0 || k > ldr || !margin) return (int)hipErrorInvalidValue;
   if (f32 && (ldx % 4 != 0 || ldq % 4 != 0)) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
+  if (nq < 64 && k <= 16) {  // narrow: a block per query, a wave per row
+    if (f32)
+      hipLaunchKernelGGL(cand_cut_block_kernel<true>, dim3((unsigned)nq), dim3(1024), 0, (hipStream_t)stream, X, ldx,
+                         nrows, Q, ldq, D, nq, bias, alpha, rows, ldr, k, margin, floor, has_floor, cut);
+    else
+      hipLaunchKernelGGL(cand_cut_block_kernel<false>, dim3((unsigned)nq), dim3(1024), 0, (hipStream_t)stream, X,
+                         ldx, nrows, Q, ldq, D, nq, bias, alpha, rows, ldr, k, margin, floor, has_floor, cut);
+    return (int)hipGetLastError();
+  }
   if (f32)
     hipLaunchKernelGGL(cand_cut_kernel<true>, grid, block, 0, (hipStream_t)stream, X, ldx, nrows, Q, ldq, D, nq,
                        bias, alpha, rows, ldr, k, margin, floor, has_floor, cut);

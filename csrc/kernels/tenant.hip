@@ -446,6 +446,93 @@ __global__ __launch_bounds__(256) void store_rerank_kernel(const float* __restri
 }
 
 
+// store_rerank_kernel for narrow batches (the interactive turn): a
+// 256-thread block per query, 16 lanes per candidate (4 candidates per wave
+// per pass, every float4 of a lane's share issued before its FMAs), the
+// scores through LDS, then wave 0 ranks them exactly like the wave kernel --
+// one wave streaming 16 candidates' rows was ~23 us of a 1.9 ms search.
+__global__ __launch_bounds__(256) void store_rerank_block_kernel(const float* __restrict__ Q, long ldq,
+                                                                 const float* __restrict__ X, long ldx, int D,
+                                                                 const float* __restrict__ sqn,
+                                                                 const float* __restrict__ bias,
+                                                                 const long* __restrict__ cand, int C, int M, int k,
+                                                                 int metric, float* __restrict__ os,
+                                                                 long* __restrict__ oi,
+                                                                 const unsigned char* __restrict__ kind,
+                                                                 long* __restrict__ oin) {
+  __shared__ float s_s[64];
+  __shared__ long s_r[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x;
+  const float* qr = Q + (long)q * ldq;
+  float qq = 0.f;
+  for (int d = lane; d < D; d += 64) qq = fmaf(qr[d], qr[d], qq);
+  qq = wave_sum(qq);
+  const int part = lane & 15, g = lane >> 4;
+  const bool vec = (D % 64) == 0 && (ldq % 4) == 0 && (ldx % 4) == 0;
+  for (int c0 = 0; c0 < C; c0 += 16) {
+    const int c = c0 + wave * 4 + g;
+    const long r = c < C ? cand[(long)q * C + c] : -1;
+    float acc = 0.f;
+    if (r >= 0) {
+      const float* xr = X + r * ldx;
+      if (vec) {
+#pragma unroll 4
+        for (int d = part * 4; d < D; d += 64) {
+          const float4 xv = *reinterpret_cast<const float4*>(xr + d);
+          const float4 qv = *reinterpret_cast<const float4*>(qr + d);
+          acc = fmaf(qv.x, xv.x, acc);
+          acc = fmaf(qv.y, xv.y, acc);
+          acc = fmaf(qv.z, xv.z, acc);
+          acc = fmaf(qv.w, xv.w, acc);
+        }
+      } else {
+        for (int d = part; d < D; d += 16) acc = fmaf(qr[d], xr[d], acc);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (part == 0 && c < C) {
+      float sc = LZK_NEG_INF;
+      if (r >= 0) {
+        if (metric == 0) {
+          sc = 2.f * acc + bias[r] - qq;
+        } else if (metric == 2) {
+          const float nr = sqrtf(sqn[r]);
+          sc = acc / (nr > 0.f ? nr : 1.f) + bias[r];
+        } else {
+          sc = acc + bias[r];
+        }
+      }
+      s_s[c] = sc;
+      s_r[c] = r;
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const float my_s = lane < C ? s_s[lane] : LZK_NEG_INF;
+  const long my_r = lane < C ? s_r[lane] : -1;
+  const bool live = lane < C && my_r >= 0 && my_s != LZK_NEG_INF;
+  int rank = 0;
+  for (int o = 0; o < C; ++o) {
+    const float s2 = __shfl(my_s, o, 64);
+    const long r2 = __shfl(my_r, o, 64);
+    const bool l2 = r2 >= 0 && s2 != LZK_NEG_INF;
+    if (l2 && o != lane && (s2 > my_s || (s2 == my_s && r2 < my_r))) ++rank;
+  }
+  const int nlive = __popcll(__ballot(live));
+  if (live && rank < k) {
+    os[(long)q * k + rank] = my_s;
+    oi[(long)q * k + rank] = my_r;
+    if (oin) oin[(long)q * k + rank] = kind[my_r] == 1 ? my_r : -1;
+  }
+  for (int j = nlive + lane; j < k; j += 64) {
+    os[(long)q * k + j] = LZK_NEG_INF;
+    oi[(long)q * k + j] = -1;
+    if (oin) oin[(long)q * k + j] = -1;
+  }
+}
+
 // Consolidation's candidate re-rank in ONE launch (replaces a gather of the
 // [M, c, D] rows in float64, an einsum, a division and two sorts): exact
 // float64 cosine of each fact's kernel candidates -- <qn, x> / |x| with qn the
@@ -818,8 +905,12 @@ LZK_EXPORT int lzk_store_rerank(const float* Q, long ldq, const float* X, long l
                                 long* oi, const unsigned char* kind, long* oin, void* stream) {
   if (C <= 0 || C > 64 || M <= 0 || k <= 0 || metric < 0 || metric > 2 || (oin && !kind))
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(store_rerank_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Q, ldq,
-                     X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi, kind, oin);
+  if (M < 64)  // narrow: a block per query
+    hipLaunchKernelGGL(store_rerank_block_kernel, dim3((unsigned)M), dim3(256), 0, (hipStream_t)stream, Q, ldq, X,
+                       ldx, D, sqn, bias, cand, C, M, k, metric, os, oi, kind, oin);
+  else
+    hipLaunchKernelGGL(store_rerank_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, Q,
+                       ldq, X, ldx, D, sqn, bias, cand, C, M, k, metric, os, oi, kind, oin);
   return (int)hipGetLastError();
 }
 

@@ -107,6 +107,11 @@ def _blk_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
 CAND_MIN_ROWS = 1 << 20
 CAND_MIN_Q = 256
 CAND_STRIDE = 64
+# narrow int8 store searches sample 1/256 of the rows for the threshold (the
+# sample pass was ~130 us of a 1.8 ms single-query search at 1/64); with the
+# 3rd best (SPEC_J_NARROW) a query goes to the exact fallback only when 3 of
+# its top-10 rows fall in the sample (~7e-6)
+CAND_STRIDE_NARROW = 256
 
 
 SEARCH_MODE = "auto"
@@ -246,12 +251,13 @@ def _sample_threshold(X, Q, k, kslot, bias, row_label, q_label, alpha, S):
     return torch.nan_to_num(thr, nan=float("-inf"))
 
 
-def _cand_lists(dev, nq, cap, slot):
+def _cand_lists(dev, nq, cap, slot, zero=True):
     ws = (_ws_cand if slot == 0 else _ws_cand2).get(dev, nq * (4 + 8 * cap))
     cnt = ws[: nq * 4].view(torch.int32)
     cs = ws[nq * 4: nq * 4 + nq * cap * 4].view(torch.float32)
     ci = ws[nq * 4 + nq * cap * 4: nq * 4 + nq * cap * 8].view(torch.int32)
-    cnt.zero_()
+    if zero:  # (zero=False: the caller's first launch zeroes the counts)
+        cnt.zero_()
     return cnt, cs, ci
 
 
@@ -387,6 +393,7 @@ class grid_cap:
     def __exit__(self, *exc):
         _lib.lib().lzk_set_cu_budget(0)
         return False
+_lib.register("lzk_thr_prep", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.I, _lib.P, _lib.P, _lib.P, _lib.P])
 _lib.register("lzk_cand_rescore", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.F, _lib.P,
                                            _lib.I, _lib.P, _lib.P, _lib.P, _lib.F, _lib.P, _lib.I, _lib.I, _lib.P,
                                            _lib.P])
@@ -610,28 +617,31 @@ def flat_topk_i8(X8: torch.Tensor, rscale: torch.Tensor, Q8: torch.Tensor, qscal
     dev = X16.device
     if margin_rig is None:
         margin_rig = margin  # (None: no bound known -- every list entry is re-scored)
-    S = max(1, min(CAND_STRIDE, N // max(16 * kslot, 1)))
     narrow = nq < NARROW_MAX_Q and SCAN8_NARROW and Dp % 64 == 0
+    S = max(1, min(CAND_STRIDE_NARROW if narrow else CAND_STRIDE, N // max(16 * kslot, 1)))
     J = SPEC_J_NARROW if narrow else SPEC_J
     spec = 0 < J < k and S >= SPEC_MIN_STRIDE
-    if spec:
-        # speculative threshold: the sample's J-th best (~J * S-th overall)
-        # instead of its k-th -- lists ~k / J times shorter; the certificate
-        # sends a query whose threshold was too high to the exact fallback
-        Xs = X16[::S]
-        bs = bias[:N:S].contiguous() if bias is not None else None
-        ts, _ = _flat_topk_lane(Xs, Q16, kslot, kslot, bs, None, None, alpha, 0, None)
-        tau = _margin(ts[:, J - 1]).contiguous()
-    else:
-        tau = _sample_threshold(X16, Q16, k, kslot, bias, None, None, alpha, S)
-    thr = (tau - margin).contiguous() if margin is not None else tau
+    # the 1/S sample's top-kslot (lane kernel); speculative threshold: its
+    # J-th best (~J * S-th overall) instead of its k-th -- lists ~k / J times
+    # shorter; the certificate sends a query whose threshold was too high to
+    # the exact fallback
+    bs = bias[:N:S].contiguous() if bias is not None else None
+    ts, _ = _flat_topk_lane(X16[::S], Q16, kslot, kslot, bs, None, None, alpha, 0, None)
     # narrow batches scan at HBM speed with a worst-case margin by default:
     # longer lists (a few thousand rows per query) cost next to nothing there
     cap = max(NARROW_CAP if narrow else 2048, 16 * kslot * S)
-    cnt, cs, ci = _cand_lists(dev, nq, cap, 0)
+    cnt, cs, ci = _cand_lists(dev, nq, cap, 0, zero=False)
+    # tau (sample bound - slack), thr = tau - margin, the certificate level
+    # thr + margin_rig and the zeroed list counts: one launch (thr_prep_kernel)
+    thr = torch.empty(nq, dtype=torch.float32, device=dev)
+    cert = torch.empty(nq, dtype=torch.float32, device=dev)
+    mg = margin.float().contiguous() if margin is not None else None
+    mr = margin_rig.float().contiguous() if margin_rig is not None else None
+    _lib.check(L.lzk_thr_prep(ts.data_ptr(), ts.stride(0), (J if spec else k) - 1, _lib.ptr(mg), _lib.ptr(mr), nq,
+                              thr.data_ptr(), cert.data_ptr(), cnt.data_ptr(), _lib.stream_ptr(dev)), "lzk_thr_prep")
     qs = qscale.contiguous()
     need = torch.empty(nq, dtype=torch.int32, device=dev)
-    chk = (_cert_tau(thr, margin_rig), k, cap + 1, need)
+    chk = (cert, k, cap + 1, need)
     if narrow:
         _scan8_narrow(X8[:N], rscale[:N], Q8, qs, bias, alpha, thr, kslot, 2 * S, cap, (cnt, cs, ci))
     else:

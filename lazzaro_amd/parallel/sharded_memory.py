@@ -1570,6 +1570,8 @@ class ShardedMemorySystem:
             pl = {"segments": []}  # applied
         with tracer.stage("sc_digest_base", dev):
             self._dcc_begin(pl)
+            if any(s["consolidate"] for s in pl["segments"]):
+                self._check_num_mono()
         try:
             for seg in pl["segments"]:
                 with tracer.stage("cb_apply", dev):
@@ -1596,6 +1598,7 @@ class ShardedMemorySystem:
                         self.local._save_to_persistence()
         finally:
             self._dcc_end()
+            self._num_mono = False
         stats["pruned"] += pruned
         if reach_new:
             self._reach_add(torch.cat(reach_new))
@@ -2532,13 +2535,35 @@ class ShardedMemorySystem:
                 out[-1].append(c)
         return out
 
+    _num_mono = False  # inside a batch: live shard nodes' numbers ascend with the row
+
+    def _check_num_mono(self) -> None:
+        g = self.g
+        n = g.n
+        self._num_mono = False
+        if n and g.on_gpu:
+            with g.on_stream():
+                live = torch.nonzero((g.kind[:n] == NODE) & (g.sup[:n] == 0)).flatten()
+                nums = self.num[live]
+                self._num_mono = bool((nums[1:] > nums[:-1]).all()) if nums.numel() > 1 else True
+
     def _first_contents(self, take: int = PROFILE_CONTENTS) -> List[str]:
         """Contents of the tenant's first ``take`` live nodes in the reference
         node order (shard creation order, then insertion). Rank 0 gets them."""
         g = self.g
         n = g.n
         mine = []
-        if n:
+        if n and g.on_gpu and self._num_mono:
+            # live shard nodes in number order along the rows (checked at the
+            # batch start; a batch appends larger numbers): the first rows by
+            # (shard, row) are the first by (shard, number) -- the one-block
+            # tg_first_rows kernel, no pass over the tenant's rows
+            with g.on_stream():
+                r = g.first_node_rows_dev(min(take, n), super_=False)
+                key = (g.shard[r].long() + 1) * (1 << NUM_BITS) + self.num[r]
+                vr = torch.stack([key, r]).cpu().tolist()
+                mine = [(int(a), g.content[int(b)]) for a, b in zip(*vr)]
+        elif n:
             with g.on_stream():
                 live = (g.kind[:n] == NODE) & (g.sup[:n] == 0)
                 key = torch.where(live, (g.shard[:n].long() + 1) * (1 << NUM_BITS) + self.num[:n],

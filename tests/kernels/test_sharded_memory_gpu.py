@@ -69,7 +69,9 @@ def test_sharded_tenant_gpu_incremental_digest(prune_thr):
     out = spawn(2, functools.partial(_sharded, cfg=cfg))
     check_equivalent(out, 2, cfg["limit"])
     d = [out[r]["dcc"] for r in range(2)]
-    assert all(x[0] > 0 for x in d) and max(x[1] for x in d) > 0, d
+    assert all(x[0] > 0 for x in d), d
+    if prune_thr == 0.0:  # (at 0.5 the batch's links all sit below the decayed threshold: an empty base)
+        assert max(x[1] for x in d) > 0, d
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")

@@ -457,13 +457,16 @@ def test_ivfpq_store_under_tenant_graph_gpu(tmp_path):
     ms.close()
 
 
-@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
-def test_store_rerank_kernel_matches_torch_gpu(metric):
-    """Fused fp32 re-rank (tenant.hip store_rerank_kernel) == the torch
-    gather / score / stable-sort path, with empty and masked candidates."""
+@pytest.mark.parametrize("metric,M,C", [("l2", 300, 16), ("ip", 300, 16), ("cosine", 300, 16), ("l2", 1, 16),
+                                         ("cosine", 5, 64), ("ip", 63, 40)])
+def test_store_rerank_kernel_matches_torch_gpu(metric, M, C):
+    """Fused fp32 re-rank (tenant.hip store_rerank_kernel; M < 64: the
+    block-per-query store_rerank_block_kernel) == the torch gather / score /
+    stable-sort path, with empty and masked candidates; the node-filtered
+    output marks the rows whose kind is not NODE."""
     from lazzaro_amd.ops.tenant_ops import store_rerank
-    gen = torch.Generator(device=DEV).manual_seed(11)
-    N, D, M, C, k = 5000, 384, 300, 16, 10
+    gen = torch.Generator(device=DEV).manual_seed(11 + M)
+    N, D, k = 5000, 384, 10
     X = torch.randn(N, D, device=DEV, generator=gen)
     sqn = (X.double() ** 2).sum(1).float()
     bias = torch.where(torch.rand(N, device=DEV, generator=gen) < 0.1, float("-inf"), 0.0)
@@ -474,6 +477,10 @@ def test_store_rerank_kernel_matches_torch_gpu(metric):
     cand = torch.stack([torch.randperm(N, device=DEV, generator=gen)[:C] for _ in range(M)])
     cand[:, -3:] = -1
     s, r = store_rerank(Q, X, sqn, bias, cand, k, metric)
+    kind = (torch.rand(N, device=DEV, generator=gen) < 0.8).to(torch.uint8)  # 1 = NODE
+    s2, rn = store_rerank(Q, X, sqn, bias, cand, k, metric, kind=kind)
+    assert torch.equal(s2, s)
+    assert torch.equal(rn, torch.where((r >= 0) & (kind[r.clamp_min(0)] == 1), r, torch.full_like(r, -1)))
     g = TenantGraph(device=DEV)
     valid = cand >= 0
     rows = cand.clamp_min(0)
