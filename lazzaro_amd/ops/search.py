@@ -107,11 +107,13 @@ def _blk_records(dev, grid: int, nq: int, kslot: int, S: int, lists: int):
 CAND_MIN_ROWS = 1 << 20
 CAND_MIN_Q = 256
 CAND_STRIDE = 64
-# narrow int8 store searches sample 1/256 of the rows for the threshold (the
-# sample pass was ~130 us of a 1.8 ms single-query search at 1/64); with the
-# 3rd best (SPEC_J_NARROW) a query goes to the exact fallback only when 3 of
-# its top-10 rows fall in the sample (~7e-6)
-CAND_STRIDE_NARROW = 256
+# narrow int8 store searches: the sample stride of the threshold. 1/256
+# halves the sample pass (~45 us of a single-query search) but its threshold
+# sits ~4x more rows down, and the longer lists cost more in the gather and
+# the two selects than the pass saved (+27 us; tools/narrow_margins.py: the
+# worst-case margin, 0.055 at d = 768, keeps 2-5k rows per query at 1/64 and
+# 7-16k at 1/256)
+CAND_STRIDE_NARROW = 64
 
 
 SEARCH_MODE = "auto"
