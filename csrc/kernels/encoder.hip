@@ -765,12 +765,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const u16* __restrict__ 
 // Same op for H % 256 == 0 (bge-base 768, e5-large 1024): half a wave per
 // row, each lane moving C chunks of 8 features as 16-B loads and stores (H =
 // 32 lanes * 8 * C), two rows per wave-instruction, RPW row pairs per wave.
-template <int C, bool RES, int RPW>
+// Q8 (the fp8 encoder): the row is also written as OCP e4m3 with its
+// scale, exactly what quant_fp8_rows_kernel makes of the bf16 output (amax of
+// the bf16-rounded values / 448) -- the next projection's input without the
+// separate quantise pass (one read + one write of the activations per GEMM).
+template <int C, bool RES, int RPW, bool Q8 = false>
 __global__ __launch_bounds__(256) void layernorm16_kernel(const u16* __restrict__ X, long ldx,
                                                           const u16* __restrict__ R, long ldr,
                                                           const float* __restrict__ g,
                                                           const float* __restrict__ bta, int rows, float eps,
-                                                          u16* __restrict__ Y, long ldy) {
+                                                          u16* __restrict__ Y, long ldy,
+                                                          unsigned char* __restrict__ Q = nullptr, long ldq = 0,
+                                                          float* __restrict__ qscale = nullptr) {
   constexpr int H = C * 256;
   const int lane = threadIdx.x & 63;
   const int half = lane >> 5, l32 = lane & 31;
@@ -810,19 +816,41 @@ __global__ __launch_bounds__(256) void layernorm16_kernel(const u16* __restrict_
     for (int o = 16; o >= 1; o >>= 1) var += __shfl_xor(var, o, 64);
     const float rstd = rsqrtf(var * invH + eps);
     const int row = row0 + 2 * rr + half;
-    if (row < rows) {
+    u16x8 ov[C];
+    float amax = 0.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const int col = c * 256 + l32 * 8;
-        const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + col), g1 = *reinterpret_cast<const f32x4*>(g + col + 4);
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(bta + col), b1 = *reinterpret_cast<const f32x4*>(bta + col + 4);
-        u16x8 o;
+    for (int c = 0; c < C; ++c) {
+      const int col = c * 256 + l32 * 8;
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(g + col), g1 = *reinterpret_cast<const f32x4*>(g + col + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bta + col), b1 = *reinterpret_cast<const f32x4*>(bta + col + 4);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          o[u] = f32_to_bf16((v[rr][c][u] - mean) * rstd * g0[u] + b0[u]);
-          o[u + 4] = f32_to_bf16((v[rr][c][u + 4] - mean) * rstd * g1[u] + b1[u]);
+      for (int u = 0; u < 4; ++u) {
+        ov[c][u] = f32_to_bf16((v[rr][c][u] - mean) * rstd * g0[u] + b0[u]);
+        ov[c][u + 4] = f32_to_bf16((v[rr][c][u + 4] - mean) * rstd * g1[u] + b1[u]);
+      }
+      if (Q8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) amax = fmaxf(amax, fabsf(bf16_to_f32(ov[c][u])));
+      }
+      if (row < rows) *reinterpret_cast<u16x8*>(Y + (long)row * ldy + col) = ov[c];
+    }
+    if (Q8) {
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));  // within the half wave
+      const float sc = amax > 0.f ? amax * (1.f / 448.f) : 1.f;
+      const float inv = 1.f / sc;
+      if (row < rows) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const int col = c * 256 + l32 * 8;
+          int lo = 0, hi = 0;
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(ov[c][0]) * inv, bf16_to_f32(ov[c][1]) * inv, lo, false);
+          lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(ov[c][2]) * inv, bf16_to_f32(ov[c][3]) * inv, lo, true);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(ov[c][4]) * inv, bf16_to_f32(ov[c][5]) * inv, hi, false);
+          hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf16_to_f32(ov[c][6]) * inv, bf16_to_f32(ov[c][7]) * inv, hi, true);
+          *reinterpret_cast<uint2*>(Q + (long)row * ldq + col) = make_uint2((unsigned)lo, (unsigned)hi);
         }
-        *reinterpret_cast<u16x8*>(Y + (long)row * ldy + col) = o;
+        if (l32 == 0) qscale[row] = sc;
       }
     }
   }
@@ -1211,6 +1239,36 @@ LZK_EXPORT int lzk_layernorm(const void* X, long ldx, const void* R, long ldr, c
   else if (H <= 768) LN(3);
   else LN(4);
 #undef LN
+  return (int)hipGetLastError();
+}
+
+// lzk_layernorm + the row's e4m3 copy and scale (layernorm16_kernel Q8):
+// H 768 / 1024, 16-B aligned rows only (else hipErrorInvalidValue: the caller
+// quantises separately).
+LZK_EXPORT int lzk_layernorm_q8(const void* X, long ldx, const void* R, long ldr, const float* g, const float* b,
+                                int rows, int H, float eps, void* Y, long ldy, void* Q, long ldq, float* qscale,
+                                void* stream) {
+  const bool v16 = (H == 768 || H == 1024) && ldx % 8 == 0 && ldy % 8 == 0 && (!R || ldr % 8 == 0) &&
+                   ldq % 8 == 0 && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y) |
+                                     reinterpret_cast<uintptr_t>(R) | reinterpret_cast<uintptr_t>(Q)) & 15) == 0;
+  if (!v16 || rows <= 0 || !Q || !qscale) return (int)hipErrorInvalidValue;
+  constexpr int RP = 2;
+  dim3 grid16((rows + 16 - 1) / 16), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  const u16* x = (const u16*)X;
+  const u16* r = (const u16*)R;
+  u16* y = (u16*)Y;
+  unsigned char* q = (unsigned char*)Q;
+#define LNQ(C)                                                                                                     \
+  do {                                                                                                             \
+    if (r) hipLaunchKernelGGL((layernorm16_kernel<C, true, RP, true>), grid16, block, 0, st, x, ldx, r, ldr, g, b, \
+                              rows, eps, y, ldy, q, ldq, qscale);                                                  \
+    else hipLaunchKernelGGL((layernorm16_kernel<C, false, RP, true>), grid16, block, 0, st, x, ldx, r, ldr, g, b,  \
+                            rows, eps, y, ldy, q, ldq, qscale);                                                    \
+  } while (0)
+  if (H == 768) LNQ(3);
+  else LNQ(4);
+#undef LNQ
   return (int)hipGetLastError();
 }
 

@@ -22,6 +22,8 @@ _lib.register("lzk_gemm_split2", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.L
 _lib.register("lzk_gemm_f8", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.P, _lib.P, _lib.L, _lib.I, _lib.P, _lib.P,
                                        _lib.P, _lib.L, _lib.P, _lib.L, _lib.I, _lib.I, _lib.P])
 _lib.register("lzk_quant_fp8_rows", _lib.I, [_lib.P, _lib.L, _lib.I, _lib.I, _lib.P, _lib.L, _lib.P, _lib.P])
+_lib.register("lzk_layernorm_q8", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.P, _lib.I, _lib.I, _lib.F,
+                                           _lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.P])
 _lib.register("lzk_attention", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.I, _lib.I, _lib.I, _lib.I, _lib.F,
                                          _lib.P, _lib.L, _lib.P, _lib.P])
 _lib.register("lzk_layernorm", _lib.I, [_lib.P, _lib.L, _lib.P, _lib.L, _lib.P, _lib.P, _lib.I, _lib.I,
@@ -167,6 +169,25 @@ def layernorm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e
                                   rows, H, float(eps), y.data_ptr(), y.stride(0), _lib.stream_ptr(x.device))
     _lib.check(rc, "lzk_layernorm")
     return y
+
+
+def layernorm_q8(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-12, residual=None):
+    """:func:`layernorm` plus the output's row-wise e4m3 copy -- (y, (q, scale))
+    with (q, scale) == quantize_fp8_rows(y) -- in one launch on the GPU
+    (encoder.hip layernorm16_kernel Q8: H 768 / 1024); elsewhere the two ops."""
+    if x.is_cuda and x.shape[1] in (768, 1024):
+        rows, H = x.shape
+        y = torch.empty_like(x)
+        q = torch.empty((rows, H), dtype=torch.uint8, device=x.device)
+        sc = torch.empty((rows,), dtype=torch.float32, device=x.device)
+        rc = _lib.lib().lzk_layernorm_q8(x.data_ptr(), x.stride(0), _lib.ptr(residual),
+                                         residual.stride(0) if residual is not None else 0, g.data_ptr(),
+                                         b.data_ptr(), rows, H, float(eps), y.data_ptr(), y.stride(0), q.data_ptr(),
+                                         q.stride(0), sc.data_ptr(), _lib.stream_ptr(x.device))
+        if rc == 0:
+            return y, (q, sc)
+    y = layernorm(x, g, b, eps, residual=residual)
+    return y, quantize_fp8_rows(y)
 
 
 def embed_ln(ids: torch.Tensor, S: int, wemb, pemb, temb, g, b, eps: float = 1e-12,

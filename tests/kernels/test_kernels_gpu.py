@@ -194,6 +194,28 @@ def test_multi_arena_search_gpu():
             torch.testing.assert_close(s[j].cpu(), rs[0].cpu(), atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("H,res", [(768, False), (1024, True)])
+def test_layernorm_q8_matches_layernorm_then_quantize_gpu(H, res):
+    """The fp8 encoder's fused LayerNorm (layernorm16_kernel Q8): its e4m3
+    copy / row scales are bit-for-bit quantize_fp8_rows of its own bf16
+    output, which equals layernorm's up to one bf16 rounding (the two
+    instantiations may contract the affine step differently)."""
+    from lazzaro_amd.ops import encoder_ops as E
+    g_ = torch.Generator().manual_seed(H)
+    x = (torch.randn(333, H, generator=g_) * 3).to(torch.bfloat16).to(DEV)
+    r = (torch.randn(333, H, generator=g_)).to(torch.bfloat16).to(DEV) if res else None
+    gam = torch.rand(H, generator=g_).to(DEV) + 0.5
+    bet = torch.randn(H, generator=g_).to(DEV) * 0.1
+    y, (q, sc) = E.layernorm_q8(x, gam, bet, 1e-12, residual=r)
+    y0 = E.layernorm(x, gam, bet, 1e-12, residual=r)
+    q0, sc0 = E.quantize_fp8_rows(y)
+    assert torch.equal(sc, sc0)
+    assert torch.equal(q, q0)
+    d = (y.float() - y0.float()).abs()
+    assert float((d <= 2 ** -7 * y0.float().abs().clamp_min(1e-30)).float().mean()) == 1.0
+    assert float((d > 0).float().mean()) < 0.01
+
+
 def test_quantize_fp8_rows_gpu():
     g = torch.Generator().manual_seed(11)
     x = (torch.randn(1000, 1024, generator=g) * torch.linspace(0.01, 30, 1000)[:, None]).to(torch.bfloat16)
