@@ -460,13 +460,16 @@ def main():
         rusers = [[tenants[rr.randrange(world)] for _ in range(a.batch)] for _ in range(len(pool))]
         last = {}
 
-        def routed(i):
-            texts, users = pool[i % len(pool)], rusers[i % len(pool)]
-            Q = svc._embed_front(texts)  # the receiving rank's encoder replica (no broadcast, C2)
-            last["Q"], last["users"], last["hits"] = Q, users, svc.search_routed(users, Q, a.k)
-        for i in range(a.warmup):
-            routed(i)
-        el_r = timed(rsteps, routed)
+        def routed_run(i0, n):
+            # pipelined like the headline: batch i+1's front-end embed (the
+            # receiving rank's encoder replica, no broadcast, C2) runs on a side
+            # stream under batch i's routed search
+            bs = [(rusers[(i0 + i) % len(pool)], pool[(i0 + i) % len(pool)]) for i in range(n)]
+            for (users, texts), hits in zip(bs, svc.search_routed_stream(bs, a.k)):
+                last["users"], last["hits"], last["texts"] = users, hits, texts
+        routed_run(0, a.warmup)
+        el_r = timed(1, lambda _: routed_run(a.warmup, rsteps))
+        last["Q"] = svc._embed_front(last["texts"])
         remote = sum(svc.owner(u) != rank for u in last["users"])
         # exactness: every rank checks the queries of ALL front ends that hit
         # its own tenant against its store search (the routed rows must be the
@@ -492,7 +495,9 @@ def main():
                         "routed_queries_per_rank": a.batch, "routed_remote_frac_rank0": round(remote / a.batch, 3),
                         "routed_exact_check": f"{int(agree[0])}/{int(agree[1])}",
                         "routed_path": "front-end embed -> all_to_all [emb|tenant|limit] -> owner store search "
-                                       "(MFMA scan + fp32 re-rank) -> all_to_all [score|row]",
+                                       "(MFMA scan + fp32 re-rank) -> all_to_all [score|row]; "
+                                       "DistributedMemoryService.search_routed_stream (batch i+1's embed on a "
+                                       "side stream under batch i's routed search)",
                         "collectives": ("rccl (torch.distributed nccl backend, world %d; header over gloo)" % world)
                         if distributed and not a.cpu else ("gloo" if distributed else "none (world 1, no process "
                                                                                        "group)")})

@@ -694,6 +694,45 @@ class DistributedMemoryService:
         Q = self._embed_front(queries)
         return routing.search_routed(self, list(users), Q, limit)
 
+    def search_routed_stream(self, batches, limit=5):
+        """Pipelined :meth:`search_routed` for serving loops (the routed
+        counterpart of ``MemorySystem.search_memories_stream``): ``batches``
+        yields (users, query texts); batch i+1's front-end embed is enqueued
+        on a side stream BEFORE batch i's routed search (header exchange, the
+        two all-to-alls, the owners' store searches), so the encoder runs
+        under the search instead of after it. Every rank must iterate alike.
+        Yields one :class:`~.routing.RoutedHits` per batch, in order."""
+        dev = self.comm.device
+        side = None
+        if dev.type == "cuda":
+            side = self._routed_side = getattr(self, "_routed_side", None) or torch.cuda.Stream(dev)
+
+        def embed(texts):
+            if side is None:
+                return self._embed_front(texts), None
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                Q = self._embed_front(texts)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return Q, ev
+
+        it = iter(batches)
+        cur = next(it, None)
+        if cur is None:
+            return
+        q_cur = embed(cur[1])
+        while cur is not None:
+            nxt = next(it, None)
+            q_nxt = embed(nxt[1]) if nxt is not None else None
+            Q, ev = q_cur
+            if ev is not None:
+                main = torch.cuda.current_stream(dev)
+                main.wait_event(ev)
+                Q.record_stream(main)
+            yield routing.search_routed(self, list(cur[0]), Q, limit)
+            cur, q_cur = nxt, q_nxt
+
     def search_global_batch(self, queries, limit: int = 5) -> "routing.GlobalHits":
         """SPMD: this rank's queries against every resident tenant of every
         rank (all-gather of queries, local search, one all-to-all back)."""

@@ -62,6 +62,13 @@ def _workload(comm, db, force=False, device_dir=False):
     same = bool(torch.equal(again.rows, hits.rows))
     third = svc.search_routed(users, qs, limits)  # every owner knows its senders' view of its directory
     same = same and bool(torch.equal(third.rows, hits.rows)) and bool(torch.equal(third.scores, hits.scores))
+    stats3 = dict(svc.route_stats)  # (the three calls above)
+    # the pipelined form (search_routed_stream): the same hits, batch by batch
+    streamed = list(svc.search_routed_stream([(users, qs), (users[:5], qs[:5]), (users, qs)], limits[0]))
+    ref5 = svc.search_routed(users[:5], qs[:5], limits[0])
+    refa = svc.search_routed(users, qs, limits[0])
+    same = same and len(streamed) == 3 and bool(torch.equal(streamed[1].rows, ref5.rows)) \
+        and bool(torch.equal(streamed[0].rows, refa.rows)) and bool(torch.equal(streamed[2].scores, refa.scores))
     glob = svc.search_global_batch(qs[:5], limit=4)
     rk, slot, row = glob.split()
     svc.get_all_users()  # names every tenant key
@@ -74,7 +81,7 @@ def _workload(comm, db, force=False, device_dir=False):
                        "global": [[[int(a), int(b), int(c)] for a, b, c in zip(x, y, z)]
                                   for x, y, z in zip(rk.tolist(), slot.tolist(), row.tolist())],
                        "gscores": glob.scores.tolist(), "names": names, "rank": comm.rank,
-                       "route_stats": svc.route_stats, "force": svc.force_collectives, "gusers": gusers})
+                       "route_stats": stats3, "force": svc.force_collectives, "gusers": gusers})
 
 
 def _truth(qs, users, limits):
