@@ -1387,12 +1387,23 @@ class ConsolidationMixin:
                 # checks the plan against every row outside it either way
                 k = int(self.POOL_OVERSAMPLE * P / S) + 16
                 fin = torch.isfinite(imp0)  # (evictable rows; the same rows are finite in impB)
+                okey = g.shard[:n].long() * (1 << 32) + torch.arange(n, device=g.device)
+                big = torch.iinfo(torch.int64).max
                 sel, ok = [], True
                 for imp in (imp0, impB):
-                    sm = imp[::S]
-                    # (top-k, not kthvalue: ATen's kthvalue sorts -- 1.4 ms per call here)
-                    t = torch.topk(sm, min(k, int(sm.numel())), largest=False, sorted=False)[0].max()
-                    sel.append(imp <= t)
+                    sm, so = imp[::S], okey[::S]
+                    kk = min(k, int(sm.numel()))
+                    # the sample's kk-th smallest (importance, shard, row) key: the
+                    # importance t by a top-k (not kthvalue: ATen's kthvalue sorts --
+                    # 1.4 ms per call here), then the tied sample rows' keys -- a
+                    # threshold inside a long run of equal importances (every row
+                    # of a freshly loaded tenant) splits the run by key instead of
+                    # pooling all of it
+                    t = torch.topk(sm, kk, largest=False, sorted=False)[0].max()
+                    j = (kk - (sm < t).sum()).clamp_min(1)
+                    tied = torch.sort(torch.where(sm == t, so, torch.full_like(so, big))).values
+                    to = tied[(j - 1).clamp_max(tied.numel() - 1)]
+                    sel.append((imp < t) | ((imp == t) & (okey <= to)))
                 cnt = torch.stack([(sel[0] & fin).sum(), (sel[1] & fin).sum()]).cpu().tolist()
                 # (a threshold inside a large run of equal importances would
                 # pool the whole run: the exact selection then)

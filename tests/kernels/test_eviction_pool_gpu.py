@@ -1,0 +1,64 @@
+"""The consolidation planner's eviction pool on a large GPU tenant
+(ConsolidationMixin._eviction_pool, the sampled superset): for tenants whose
+importances are all distinct and for a freshly loaded tenant where every row
+ties (the bench's 10M-row buffer), the pool contains the P lowest
+(importance, shard, row) keys now and after the batch's decays -- so the
+plan verification never has to fall back -- without taking the exact
+two-top-k path. Reference: memory_system.py:535-578 (eviction order)."""
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lowest(imp, okey, P):
+    big = torch.iinfo(torch.int64).max
+    fin = torch.isfinite(imp)
+    o = torch.argsort(torch.where(fin, okey, torch.full_like(okey, big)), stable=True)
+    o = o[torch.sort(imp[o], stable=True).indices]
+    o = o[fin[o]]
+    return set(o[:P].tolist())
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("ties", [False, True])
+def test_sampled_eviction_pool_holds_the_lowest_keys(ties, monkeypatch):
+    from lazzaro_amd.core import consolidation as C
+    from lazzaro_amd.core.memory_system import MemorySystem
+    from lazzaro_amd.core.providers import HashEmbedder, LocalLLM
+    from lazzaro_amd.ops import tenant_ops as T
+    dev = torch.device("cuda", 0)
+    n, D, B, P = 200_000, 64, 16, 5000
+    with tempfile.TemporaryDirectory() as d:
+        ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), device=dev, db_dir=d,
+                          load_from_disk=False, enable_async=False, enable_caching=False, max_buffer_size=2 * n)
+        g = ms.graph
+        gen = torch.Generator(device=dev).manual_seed(3)
+        v = torch.randn(n, D, device=dev, generator=gen)
+        shard = torch.tensor([g.shard_id(s) for s in ("work", "personal", "learning")], dtype=torch.int32,
+                             device=dev)[torch.randint(0, 3, (n,), device=dev, generator=gen)]
+        sal = 0.5 if ties else torch.rand(n, generator=torch.Generator().manual_seed(4)) * 0.8 + 0.1
+        g.add_nodes([f"n{i}" for i in range(n)], [""] * n, v / v.norm(dim=1, keepdim=True), shard=shard,
+                    stored=True, now=1.7e9, sal=sal)
+        calls = []
+        real = C._lowest_keys
+        monkeypatch.setattr(C, "_lowest_keys", lambda *a: calls.append(1) or real(*a))
+        now = 1.7e9 + 60.0
+        pool, mask = ms._eviction_pool(B, P, now)
+        assert mask is not None and not calls  # the sampled superset, not the exact path
+        assert P <= pool.size <= ms.POOL_MAX_OVER * P * 2
+        okey = g.shard[:n].long() * (1 << 32) + torch.arange(n, device=dev)
+        imp0 = T.importance(g.sal[:n], g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now)
+        s = g.sal[:n].clone()
+        empty = {"src": torch.zeros(0, dtype=torch.int32, device=dev),
+                 "dst": torch.zeros(0, dtype=torch.int32, device=dev),
+                 "w": torch.zeros(0, dtype=torch.float32, device=dev)}
+        T.decay_prune(empty, s, g.kind[:n], g.sup[:n], C.DECAY_RATE, None, steps=B)
+        impB = T.importance(s, g.acc[:n], g.last[:n], g.kind[:n], g.sup[:n], now)
+        have = set(np.asarray(pool).tolist())
+        for imp in (imp0, impB):
+            assert _lowest(imp, okey, P) <= have
+        ms.close()
