@@ -14,6 +14,9 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <map>
 #include <set>
@@ -38,12 +41,19 @@ inline float decay_sal(float s, float keep) {
   return kSalFloor + m;
 }
 
-inline double importance(float sal, i64 acc, double last, double now) {
+// importance = (a + b) + c with a = 0.5 sal, b from the access count, c from
+// the recency -- rounded op by op like tg_importance_kernel (the GPU verifies
+// the plan's eviction events against it bit for bit). b and c only change
+// when a row is touched, so the planner keeps them per row (imp_b / imp_c)
+// and each eviction pass costs one multiply and two adds per row.
+inline double imp_b(i64 acc) { return std::min(1.0, (double)acc / 10.0) * 0.3; }
+inline double imp_c(double last, double now) {
   const double days = (now - last) / 86400.0;
-  const double a = (double)sal * 0.5;
-  const double b = std::min(1.0, (double)acc / 10.0) * 0.3;
-  const double c = (1.0 / (1.0 + days)) * 0.2;
-  return (a + b) + c;
+  return (1.0 / (1.0 + days)) * 0.2;
+}
+inline double importance_bc(float sal, double b, double c) { return ((double)sal * 0.5 + b) + c; }
+inline double importance(float sal, i64 acc, double last, double now) {
+  return importance_bc(sal, imp_b(acc), imp_c(last, now));
 }
 
 struct Super {
@@ -78,7 +88,9 @@ class Planner {
   int M = 0, K = 0, S = 0;
   std::vector<i64> ct, code;
   std::vector<float> sal_in;
-  std::vector<double> gs, ss, sup_cos, sup_n2, Smat, qnorm, fact_n2;
+  std::vector<double> gs, ss, sup_cos, sup_n2, qnorm, fact_n2;
+  arr<double> Sarr;            // the F x F fact block, read in place (8 MB per 1,024-fact batch)
+  const double* Sp = nullptr;
   std::vector<i64> gr, sr, sup_rows;
   // graph
   i64 n0 = 0, node_count = 0, max_buffer = 0;
@@ -92,7 +104,7 @@ class Planner {
   // node state
   std::vector<i64> row, acc, ncode;
   std::vector<float> sal;
-  std::vector<double> last, n2;
+  std::vector<double> last, n2, ib, ic;  // ib / ic: imp_b(acc), imp_c(last) per row
   std::vector<uint8_t> sup, alive, cand;
   std::unordered_map<i64, int> loc;
   // batch
@@ -115,6 +127,19 @@ class Planner {
   std::vector<Seg> segs;
   Seg* seg = nullptr;
   int conv_first = 0;  // first fact of the current conversation (facts are in conversation order)
+  // near[j]: the facts of earlier conversations whose similarity to fact j is
+  // above the link threshold, in fact order -- the only fact x fact entries
+  // cands() can use (one O(M^2) pass instead of one per cands() call)
+  std::vector<std::vector<std::pair<int, double>>> near;
+
+  void build_near() {
+    near.assign(M, {});
+    for (int j = 0; j < M; ++j) {
+      const double* srow = Sp + (size_t)j * M;
+      for (int i = 0; i < M && ct[i] < ct[j]; ++i)
+        if (srow[i] > link_thr) near[j].emplace_back(i, srow[i]);
+    }
+  }
 
   bool present(i64 r) const { return evicted.find(r) == evicted.end(); }
 
@@ -124,6 +149,8 @@ class Planner {
     sal.push_back(s);
     acc.push_back(0);
     last.push_back(now);
+    ib.push_back(imp_b(0));
+    ic.push_back(imp_c(now, now));
     ncode.push_back(c);
     sup.push_back(is_sup);
     alive.push_back(1);
@@ -151,11 +178,9 @@ class Planner {
         if (r2.data()[t] >= 0 && s2.data()[t] > link_thr && present(r2.data()[t]))
           out.push_back({s2.data()[t], r2.data()[t]});
     }
-    const double* srow = Smat.data() + (size_t)j * M;
-    for (int i = 0; i < conv_first; ++i) {  // kept facts of earlier conversations
+    for (const auto& [i, v] : near[j]) {  // kept facts of earlier conversations above the link threshold
       if (!fact_live[i] || (same && code[i] != code[j])) continue;
-      const double v = srow[i];
-      if (v > link_thr) out.push_back({v, fact_key[i]});
+      out.push_back({v, fact_key[i]});
     }
     std::sort(out.begin(), out.end(), [](const Cand& a, const Cand& b) { return a.v > b.v || (a.v == b.v && a.r < b.r); });
   }
@@ -196,6 +221,8 @@ class Planner {
       sal[i] = m;
       acc[i] += (i64)js.size();
       last[i] = now;
+      ib[i] = imp_b(acc[i]);
+      ic[i] = imp_c(now, now);
       seg->touched.insert(r);
     }
     return kept;
@@ -264,24 +291,40 @@ class Planner {
     }
   }
 
+  std::vector<double> imp_buf;
+  std::vector<int> li;
+
   void evict(int c) {
     const i64 excess = node_count - max_buffer;
     if (excess <= 0) return;
-    std::vector<int> li;
-    li.reserve(row.size());
-    for (int i = 0; i < (int)row.size(); ++i)
-      if (cand[i] && alive[i]) li.push_back(i);
-    if (li.empty()) return;
-    std::vector<double> imp(row.size());
-    for (int i : li) imp[i] = importance(sal[i], acc[i], last[i], now);
+    // the m = excess smallest (importance, shard, row) keys of the evictable
+    // rows in ONE pass: a bounded max-heap (m is a handful of rows per
+    // conversation, the pool thousands) instead of collecting every row and
+    // nth_element -- the same rows in the same order (the key is a total order)
+    if (imp_buf.size() < row.size()) imp_buf.resize(row.size());
+    double* imp = imp_buf.data();
     auto less = [&](int a, int b) {
       if (imp[a] != imp[b]) return imp[a] < imp[b];
       if (ncode[a] != ncode[b]) return ncode[a] < ncode[b];
       return row[a] < row[b];
     };
-    const size_t m = std::min<size_t>((size_t)excess, li.size());
-    if (m < li.size()) std::nth_element(li.begin(), li.begin() + (m - 1), li.end(), less);
-    std::sort(li.begin(), li.begin() + m, less);
+    const size_t mx = (size_t)excess;
+    li.clear();
+    for (int i = 0; i < (int)row.size(); ++i) {
+      if (!(cand[i] && alive[i])) continue;
+      imp[i] = importance_bc(sal[i], ib[i], ic[i]);
+      if (li.size() < mx) {
+        li.push_back(i);
+        std::push_heap(li.begin(), li.end(), less);
+      } else if (less(i, li.front())) {
+        std::pop_heap(li.begin(), li.end(), less);
+        li.back() = i;
+        std::push_heap(li.begin(), li.end(), less);
+      }
+    }
+    if (li.empty()) return;
+    std::sort_heap(li.begin(), li.end(), less);
+    const size_t m = li.size();
     const int lastv = li[m - 1];
     events.emplace_back(decays, imp[lastv], ncode[lastv], row[lastv]);
     for (size_t t = 0; t < m; ++t) {
@@ -338,8 +381,19 @@ class Planner {
 
   void end_decay() {
     ++decays;
-    for (size_t i = 0; i < row.size(); ++i)
-      if (alive[i] && !sup[i]) sal[i] = decay_sal(sal[i], keep);
+    // branch-free over every row (the same rounding as decay_sal): live shard
+    // nodes decay towards the floor, every other row keeps its salience
+    const size_t R = row.size();
+    float* sp = sal.data();
+    const uint8_t* al = alive.data();
+    const uint8_t* su = sup.data();
+    for (size_t i = 0; i < R; ++i) {
+      const float s = sp[i];
+      const float d = s - kSalFloor;
+      const float m = d * keep;
+      const float v = s > kSalFloor ? kSalFloor + m : kSalFloor;
+      sp[i] = (al[i] & (su[i] == 0)) ? v : s;
+    }
     for (size_t e = 0; e < e_w.size(); ++e) {
       if (!e_alive[e]) continue;
       const float w = e_w[e] * keep;
@@ -381,8 +435,16 @@ class Planner {
 
   // seg_each: close a segment after EVERY conversation (a durable commit
   // per conversation, like the reference's save per end_conversation)
+  double tprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+
   void run(int B, i64 count0, bool autoc, i64 every, i64 cluster_every, bool seg_each) {
     next_row = n0;
+    double t0 = now_s();
+    build_near();
+    tprof[0] += now_s() - t0;
     segs.clear();
     segs.push_back(Seg{0, 0});
     seg = &segs.back();
@@ -392,20 +454,29 @@ class Planner {
       conv_first = j0;
       std::vector<int> jj;
       while (j0 < M && ct[j0] == c) jj.push_back(j0++);
+      double t1 = now_s();
       auto kept = dedupe(jj, c);
+      double t2 = now_s();
       insert(kept);
       link(kept, c);
+      double t3 = now_s();
       evict(c);
       make_supers(kept, c);
+      double t4 = now_s();
       end_decay();
+      double t5 = now_s();
       evict(c);
+      double t6 = now_s();
+      tprof[1] += t2 - t1; tprof[2] += t3 - t2; tprof[3] += t4 - t3 + t6 - t5; tprof[4] += t5 - t4;
       const i64 count = count0 + c + 1;
       const bool point = autoc && every > 0 && count % every == 0;
       const bool clus = cluster_every > 0 && count / cluster_every > (count - 1) / cluster_every;
       if (point || clus || seg_each || c == B - 1) {
         seg->consolidate = point;
         seg->cluster = clus;
+        double t7 = now_s();
         close();
+        tprof[5] += now_s() - t7;
         if (c < B - 1) {
           segs.push_back(Seg{c + 1, c + 1});
           seg = &segs.back();
@@ -427,6 +498,7 @@ py::array_t<T> out(const std::vector<T>& v) {
 }
 
 py::dict plan_batch(py::dict kw) {
+  const double tin = Planner::now_s();
   Planner p;
   p.ct = vec<i64>(kw["ct"]);
   p.code = vec<i64>(kw["code"]);
@@ -452,7 +524,8 @@ py::dict plan_batch(py::dict kw) {
   p.S = (int)p.sup_rows.size();
   p.sup_cos = vec<double>(kw["sup_cos"]);
   p.sup_n2 = vec<double>(kw["sup_n2"]);
-  p.Smat = vec<double>(kw["S"]);
+  p.Sarr = py::cast<arr<double>>(kw["S"]);
+  p.Sp = p.Sarr.data();
   p.qnorm = vec<double>(kw["qnorm"]);
   p.fact_n2 = vec<double>(kw["fact_n2"]);
   p.dedupe_thr = py::cast<double>(kw["dedupe_thr"]);
@@ -485,14 +558,18 @@ py::dict plan_batch(py::dict kw) {
     p.n2 = n2;
     p.alive.assign(R, 1);
     p.cand.resize(R);
+    p.ib.resize(R);
+    p.ic.resize(R);
     for (size_t i = 0; i < R; ++i) {
       p.cand[i] = pool[i] && !sup[i];
       p.loc[rows[i]] = (int)i;
+      p.ib[i] = imp_b(acc[i]);
+      p.ic[i] = imp_c(last[i], p.now);
     }
   }
   const size_t M = p.M;
   if (p.sal_in.size() != M || p.code.size() != M || p.qnorm.size() != M || p.fact_n2.size() != M ||
-      p.Smat.size() != M * M || p.gr.size() != p.gs.size() || p.ss.size() != p.gs.size() ||
+      (size_t)p.Sarr.size() != M * M || p.gr.size() != p.gs.size() || p.ss.size() != p.gs.size() ||
       p.sr.size() != p.gs.size() || p.sup_cos.size() != M * (size_t)p.S || p.sup_n2.size() != (size_t)p.S)
     throw std::invalid_argument("plan_batch: inconsistent fact inputs");
   for (size_t j = 1; j < M; ++j)
@@ -502,9 +579,11 @@ py::dict plan_batch(py::dict kw) {
   p.fact_key.assign(M, -1);
   p.dup_of.assign(M, -1);
   p.fact_live.assign(M, 0);
+  const double trun = Planner::now_s();
   p.run(py::cast<int>(kw["B"]), py::cast<i64>(kw["count0"]), py::cast<bool>(kw["auto"]),
         py::cast<i64>(kw["every"]), py::cast<i64>(kw["cluster_every"]),
         kw.contains("seg_each") && py::cast<bool>(kw["seg_each"]));
+  const double tout = Planner::now_s();
 
   py::list segs;
   for (auto& s : p.segs) {
@@ -560,6 +639,12 @@ py::dict plan_batch(py::dict kw) {
   py::dict st;
   for (auto& [k, v] : p.stats) st[py::str(k)] = v;
   res["stats"] = st;
+  if (std::getenv("LZK_PLAN_PROF"))  // diagnostic: planner phases (tools/plan_bench.py)
+    std::fprintf(stderr,
+                 "plan_batch ms: inputs %.3f near %.3f dedupe %.3f insert+link %.3f evict+supers %.3f "
+                 "decay %.3f close %.3f outputs %.3f\n",
+                 (trun - tin) * 1e3, p.tprof[0] * 1e3, p.tprof[1] * 1e3, p.tprof[2] * 1e3, p.tprof[3] * 1e3,
+                 p.tprof[4] * 1e3, p.tprof[5] * 1e3, (Planner::now_s() - tout) * 1e3);
   return res;
 }
 

@@ -38,6 +38,8 @@ The plan is applied to the device graph in segments that end at the
 """
 from __future__ import annotations
 
+import json
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -45,6 +47,7 @@ import numpy as np
 
 F32 = np.float32
 SAL_FLOOR = F32(0.2)
+_plan_calls = 0
 NEG = float("-inf")
 
 
@@ -491,6 +494,14 @@ def plan(kw: Dict, B: int, count0: int, auto: bool, every: int, cluster_every: i
         args.setdefault("chain_w", 0.5)
         args["super_codes"] = np.asarray(sorted(args["super_codes"]), np.int64)
         args["shard_count"] = np.asarray(args["shard_count"], np.int64)
+        dump = os.environ.get("LZK_DUMP_PLAN")  # "path:N": the N-th call's planner inputs (tools/plan_bench.py)
+        global _plan_calls
+        _plan_calls += 1
+        if dump and _plan_calls == int(dump.rsplit(":", 1)[1]):
+            dump = dump.rsplit(":", 1)[0]
+            arrs = {k: v for k, v in args.items() if isinstance(v, np.ndarray)}
+            scal = {k: v for k, v in args.items() if isinstance(v, (int, float, bool, str)) or v is None}
+            np.savez(dump, **arrs, _scalars=np.asarray(json.dumps(scal)))
         return _rt().plan_batch(args)
     pl = BatchPlanner(**kw)
     segs = pl.run(B, count0, auto, every, cluster_every, seg_each)
