@@ -168,6 +168,7 @@ class Planner {
       if (r[t] >= 0 && s[t] > link_thr && present(r[t])) out.push_back({s[t], r[t]});
     const bool full = K > 0 && r[K - 1] >= 0 && s[K - 1] > link_thr;
     if (full && (int)out.size() < link_k + 1) {
+      py::gil_scoped_acquire gil;  // (run() releases the GIL; the callbacks are Python)
       py::array_t<i64> ev(evicted_pre.size(), evicted_pre.data());
       py::tuple res = fallback_fn(j, ev, same);
       auto s2 = py::cast<arr<double>>(res[0]);
@@ -356,6 +357,7 @@ class Planner {
       if ((double)shard_count[cd] <= sthr || (double)shard_count[cd] < sthr || super_codes.count(cd)) continue;
       const i64 key = next_row++;
       std::vector<i64> children;
+      py::gil_scoped_acquire gil;  // (run() releases the GIL; the callbacks are Python)
       auto pre = py::cast<arr<i64>>(pre_members(cd));
       for (py::ssize_t t = 0; t < pre.size(); ++t)
         if (present(pre.data()[t])) children.push_back(pre.data()[t]);
@@ -579,10 +581,17 @@ py::dict plan_batch(py::dict kw) {
   p.fact_key.assign(M, -1);
   p.dup_of.assign(M, -1);
   p.fact_live.assign(M, 0);
+  const int a_B = py::cast<int>(kw["B"]);
+  const i64 a_c0 = py::cast<i64>(kw["count0"]), a_every = py::cast<i64>(kw["every"]),
+            a_cl = py::cast<i64>(kw["cluster_every"]);
+  const bool a_auto = py::cast<bool>(kw["auto"]), a_seg = kw.contains("seg_each") && py::cast<bool>(kw["seg_each"]);
   const double trun = Planner::now_s();
-  p.run(py::cast<int>(kw["B"]), py::cast<i64>(kw["count0"]), py::cast<bool>(kw["auto"]),
-        py::cast<i64>(kw["every"]), py::cast<i64>(kw["cluster_every"]),
-        kw.contains("seg_each") && py::cast<bool>(kw["seg_each"]));
+  {
+    // the plan itself is pure C++ over copied / held arrays: other Python
+    // threads (a write-behind persistence, a serving loop) run meanwhile
+    py::gil_scoped_release nogil;
+    p.run(a_B, a_c0, a_auto, a_every, a_cl, a_seg);
+  }
   const double tout = Planner::now_s();
 
   py::list segs;
