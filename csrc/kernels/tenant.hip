@@ -284,7 +284,8 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
                                                               const double* __restrict__ ev_imp,
                                                               const int* __restrict__ ev_code,
                                                               const long* __restrict__ ev_row, int* __restrict__ bad,
-                                                              const long* __restrict__ rowkey) {
+                                                              const long* __restrict__ rowkey, double vmax,
+                                                              int st_last, double kt, int max_code, long max_key) {
 #pragma clang fp contract(off)
   const long i = (long)blockIdx.x * NTB + threadIdx.x;
   if (i >= n || kind[i] != 1 || sup[i] || pool[i]) return;
@@ -293,6 +294,25 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
   const double a = fmin(1.0, (double)acc[i] / 10.0) * 0.3;
   const double d = (1.0 / (1.0 + (now - last[i]) / 86400.0)) * 0.2;
   const int code = shard[i];
+  // Shortcuts (the importance of a row at or above the floor never rises:
+  // each fp32 decay step lowers s or keeps it), with vmax = the largest event
+  // importance and (max_code, max_key) the largest event key:
+  //  1. a closed-form lower bound of the row's importance after the last
+  //     event's st_last decays -- F + (s - F) keep^st_last minus 4 ulps(1) per
+  //     step of fp32 rounding -- above vmax (+1e-9): no event can rank it first;
+  //  2. the exact sequential importance after st_last decays >= vmax, ties
+  //     only with a row key above every event's: the same.
+  // Everything else walks the events exactly as before.
+  if (s >= SAL_FLOOR) {
+    const double F = (double)SAL_FLOOR;
+    double lb = F + ((double)s - F) * kt - 4.0 * (double)st_last * 5.9604644775390625e-08;
+    if (lb < F) lb = F;
+    if (lb * 0.5 + a + d > vmax + 1e-9) return;
+    float sf = s;
+    for (int u = 0; u < st_last; ++u) sf = decay_sal(sf, keep);
+    const double fin = (double)sf * 0.5 + a + d;
+    if (fin > vmax || (fin == vmax && (code > max_code || (code == max_code && key > max_key)))) return;
+  }
   int t = 0;
   for (int e = 0; e < ne; ++e) {
     const int st = ev_steps[e];
@@ -859,10 +879,12 @@ LZK_EXPORT int lzk_tg_evict_verify(const float* sal, const int* acc, const doubl
                                    const unsigned char* sup, const int* shard, const unsigned char* pool, long n,
                                    double now, float keep, int ne, const int* ev_steps, const double* ev_imp,
                                    const int* ev_code, const long* ev_row, int* bad, void* stream,
-                                   const long* rowkey) {
+                                   const long* rowkey, double vmax, int st_last, double kt, int max_code,
+                                   long max_key) {
   if (n <= 0 || ne <= 0) return 0;
   hipLaunchKernelGGL(tg_evict_verify_kernel, dim3(blocks_for(n)), dim3(NTB), 0, (hipStream_t)stream, sal, acc, last,
-                     kind, sup, shard, pool, n, now, keep, ne, ev_steps, ev_imp, ev_code, ev_row, bad, rowkey);
+                     kind, sup, shard, pool, n, now, keep, ne, ev_steps, ev_imp, ev_code, ev_row, bad, rowkey, vmax,
+                     st_last, kt, max_code, max_key);
   return (int)hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ _lib.register("lzk_tg_compact", I, [P, P, L, P, P, P, P, P, P, P, P, P, P, P, P,
 _lib.register("lzk_tg_boost", I, [P, P, P, P, P, I, P, P, F, D_, D_, P, P, P, P, I, P, P])
 _lib.register("lzk_tg_touch", I, [P, I, P, P, P, P, D_, D_, P])
 _lib.register("lzk_tg_importance", I, [P, P, P, P, P, L, D_, P, P])
-_lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P, P])
+_lib.register("lzk_tg_evict_verify", I, [P, P, P, P, P, P, P, L, D_, F, I, P, P, P, P, P, P, P, D_, I, D_, I, L])
 _lib.register("lzk_scan_blocks", I, [P, I, P, P])
 _lib.register("lzk_pack_bits", I, [P, L, P, P])
 _lib.register("lzk_tg_gather_fields", I, [P, I, I, P, P, P, P, P, P, P])
@@ -391,11 +391,19 @@ def evict_verify(sal, acc, last, kind, sup, shard, pool: torch.Tensor, now: floa
     code = torch.tensor([e[2] for e in ev], dtype=torch.int32).to(dev)
     row = torch.tensor([e[3] for e in ev], dtype=torch.int64).to(dev)
     bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    # the kernel's shortcuts: the largest event importance, the last event's
+    # decay count (steps ascend), keep^that in double, the largest event key
+    import numpy as np
+    st_last = max(int(e[0]) for e in ev)
+    vmax = max(float(e[1]) for e in ev)
+    mc, mk = max((int(e[2]), int(e[3])) for e in ev)
+    kt = float(np.float32(keep)) ** st_last
     _lib.check(_lib.lib().lzk_tg_evict_verify(sal.data_ptr(), acc.data_ptr(), last.data_ptr(), kind.data_ptr(),
                                               sup.data_ptr(), shard.data_ptr(), pool.data_ptr(), n, float(now),
                                               float(keep), len(ev), steps.data_ptr(), imp.data_ptr(),
                                               code.data_ptr(), row.data_ptr(), bad.data_ptr(), _st(sal),
-                                              None if rowkey is None else rowkey.contiguous().data_ptr()),
+                                              None if rowkey is None else rowkey.contiguous().data_ptr(),
+                                              vmax, st_last, kt, mc, mk),
                "tg_evict_verify")
     return int(bad.item()) == 0
 

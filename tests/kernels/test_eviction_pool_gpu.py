@@ -62,3 +62,49 @@ def test_sampled_eviction_pool_holds_the_lowest_keys(ties, monkeypatch):
         for imp in (imp0, impB):
             assert _lowest(imp, okey, P) <= have
         ms.close()
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("ties", [False, True])
+def test_evict_verify_kernel_matches_host(ties):
+    """tg_evict_verify_kernel (with its closed-form and final-importance
+    shortcuts) gives the host walk's verdict on random event lists that pass
+    and that fail -- distinct importances, and a tenant whose rows all tie
+    (the shortcut then rests on the row keys)."""
+    from lazzaro_amd.ops import tenant_ops as T
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(7 + ties)
+    n = 50_000
+    if ties:
+        sal = torch.full((n,), 0.5)
+        acc = torch.zeros(n, dtype=torch.int32)
+        last = torch.full((n,), 1.7e9, dtype=torch.float64)
+    else:
+        sal = torch.rand(n, generator=g) * 0.9 + 0.05  # some rows start under the floor
+        acc = torch.randint(0, 15, (n,), generator=g, dtype=torch.int32)
+        last = 1.7e9 - torch.rand(n, generator=g, dtype=torch.float64) * 86400 * 30
+    kind = torch.ones(n, dtype=torch.uint8)
+    kind[::50] = 2
+    sup = torch.zeros(n, dtype=torch.uint8)
+    shard = torch.randint(0, 3, (n,), generator=g, dtype=torch.int32)
+    now, keep = 1.7e9 + 100.0, 0.99
+    imp0 = T.importance(sal, acc, last, kind, sup, now)
+    okey = shard.long() * (1 << 32) + torch.arange(n)
+    order = torch.argsort(okey, stable=True)
+    order = order[torch.sort(imp0[order], stable=True).indices]
+    pool = torch.zeros(n, dtype=torch.uint8)
+    pool[order[:2000]] = 1
+    verdicts = set()
+    for trial in range(24):
+        ne = int(torch.randint(1, 40, (1,), generator=g))
+        steps = sorted(torch.randint(0, 128, (ne,), generator=g).tolist())
+        # thresholds around the pool's top: some lists pass, some fail
+        pick = order[torch.randint(1500, 2600, (ne,), generator=g)]
+        ev = [(st, float(imp0[r]) - 1e-4 * (trial % 3 == 0) + 3e-4 * (trial % 5 == 1),
+               int(shard[r]), int(r)) for st, r in zip(steps, pick.tolist())]
+        host = T.evict_verify(sal, acc, last, kind, sup, shard, pool, now, keep, ev)
+        gpu = T.evict_verify(sal.to(dev), acc.to(dev), last.to(dev), kind.to(dev), sup.to(dev), shard.to(dev),
+                             pool.to(dev), now, keep, ev)
+        assert gpu == host, (trial, ev[:3])
+        verdicts.add(host)
+    assert verdicts == {True, False}
