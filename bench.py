@@ -468,7 +468,7 @@ def main():
             for (users, texts), hits in zip(bs, svc.search_routed_stream(bs, a.k)):
                 last["users"], last["hits"], last["texts"] = users, hits, texts
         routed_run(0, a.warmup)
-        el_r = timed(1, lambda _: routed_run(a.warmup, rsteps))
+        el_r = timed(1, lambda _: routed_run(0, rsteps))
         last["Q"] = svc._embed_front(last["texts"])
         remote = sum(svc.owner(u) != rank for u in last["users"])
         # exactness: every rank checks the queries of ALL front ends that hit

@@ -8,7 +8,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("nq", [1, 7, 300])
+@pytest.mark.parametrize("nq", [1, 7, 300, 1024])
 def test_i8_query_kernel_matches_torch(nq, monkeypatch):
     from lazzaro_amd.engine import tenant_graph as TG
     g = TG.TenantGraph(device="cuda", dim=768)
@@ -21,6 +21,7 @@ def test_i8_query_kernel_matches_torch(nq, monkeypatch):
     Q[0] = 0.0  # a zero query quantises exactly with scale 0
     q16 = g._q16(Q / Q.norm(dim=1, keepdim=True).clamp_min(1e-30))
     monkeypatch.setattr(TG, "I8_QUERY_KERNEL", True)
+    monkeypatch.setattr(TG, "I8_QUERY_WIDE", True)  # (wide batches: the kernel too, not only nq < 128)
     a8, aq, am, ar = g._i8_query(q16, 2.0)
     monkeypatch.setattr(TG, "I8_QUERY_KERNEL", False)
     b8, bq, bm, br = g._i8_query(q16, 2.0)
