@@ -133,10 +133,12 @@ WRITE_EMB_MAX_ROWS = 8192
 SET_ROWS_KERNEL = True
 # the int8 search's query quantisation + margin in one launch (I8_QUERY_KERNEL = False: torch ops)
 I8_QUERY_KERNEL = True
-# wide batches keep the torch formulation (I8_QUERY_WIDE = True: the kernel too):
-# measured with the kernel on wide batches, the pipelined headline loop fell
-# from 82.6k to 54k QPS while every store search alone stayed as fast (open)
-I8_QUERY_WIDE = os.environ.get("LZK_I8_QUERY_WIDE", "0") == "1"
+# wide batches too (I8_QUERY_WIDE = False: the torch formulation of ~25 launches
+# for batches >= I8_QUERY_WIDE_MIN). Round 5 once measured the pipelined headline
+# at 54k QPS with the kernel; interleaved round-6 runs on one box: 82.5k / 82.7k
+# with it vs 82.1k / 79.2k without, store search 8.08 vs 8.40 ms
+# (profiles/r6/serving/i8_query_wide_ab/; tests/kernels/test_query_prep_gpu.py, nq = 1024)
+I8_QUERY_WIDE = os.environ.get("LZK_I8_QUERY_WIDE", "1") == "1"
 I8_QUERY_WIDE_MIN = 128
 # consolidate_batch segment ends through tenant.hip lzk_tg_seg_end (SEG_END_KERNEL = False: the torch formulation)
 SEG_END_KERNEL = True

@@ -97,11 +97,24 @@ def test_evict_verify_kernel_matches_host(ties):
     verdicts = set()
     for trial in range(24):
         ne = int(torch.randint(1, 40, (1,), generator=g))
-        steps = sorted(torch.randint(0, 128, (ne,), generator=g).tolist())
-        # thresholds around the pool's top: some lists pass, some fail
-        pick = order[torch.randint(1500, 2600, (ne,), generator=g)]
-        ev = [(st, float(imp0[r]) - 1e-4 * (trial % 3 == 0) + 3e-4 * (trial % 5 == 1),
-               int(shard[r]), int(r)) for st, r in zip(steps, pick.tolist())]
+        kind_t = trial % 4
+        if kind_t == 0:  # far under every row (the closed-form shortcut), decays up to 127
+            steps = sorted(torch.randint(0, 128, (ne,), generator=g).tolist())
+            pick = order[torch.randint(0, 2000, (ne,), generator=g)]
+            off = -0.35
+        elif kind_t == 1:  # pool rows' own keys at step 0: the exact walk and its ties, passing
+            steps = [0] * ne
+            pick = order[torch.randint(1000, 2000, (ne,), generator=g)]
+            off = 0.0
+        elif kind_t == 2:  # rows outside the pool as victims: failing
+            steps = [0] * ne
+            pick = order[torch.randint(2000, 2600, (ne,), generator=g)]
+            off = 0.0
+        else:  # anything in between, with decays
+            steps = sorted(torch.randint(0, 128, (ne,), generator=g).tolist())
+            pick = order[torch.randint(1500, 2600, (ne,), generator=g)]
+            off = -1e-4
+        ev = [(st, float(imp0[r]) + off, int(shard[r]), int(r)) for st, r in zip(steps, pick.tolist())]
         host = T.evict_verify(sal, acc, last, kind, sup, shard, pool, now, keep, ev)
         gpu = T.evict_verify(sal.to(dev), acc.to(dev), last.to(dev), kind.to(dev), sup.to(dev), shard.to(dev),
                              pool.to(dev), now, keep, ev)
