@@ -1564,10 +1564,27 @@ class ShardedMemorySystem:
         etype = g.etype("relates_to")
         n_fact = n0 - int(np.searchsorted(self._sup_v, n0))
         reach_new: List[torch.Tensor] = []
-        if self._native_w1_ok(pl, thr):
-            with tracer.stage("cb_apply_native", dev):
-                pruned += self._native_w1(pl, fact_key, codes, Q, flat, f_off, thr, now, count0, stats, reach_new)
-            pl = {"segments": []}  # applied
+        cc_w1 = False
+        base_ok = self._native_w1_base_ok(pl, thr)
+        if base_ok and any(seg["consolidate"] for seg in pl["segments"]) and \
+                g.num_edges + sum(len(seg["edge_src"]) for seg in pl["segments"]) > T.dg_small_max_edges():
+            # a graph past the one-block digest (the persistent graph): the
+            # single tenant's incremental components -- the batch's stable
+            # edges labelled once, the points union the volatile suffix inside
+            # the native applier (rows are the plan's keys here)
+            vic = [np.asarray(seg["victims"], np.int64).reshape(-1) for seg in pl["segments"]]
+            with tracer.stage("cc_begin", dev):
+                cc_w1 = g.cc_begin(np.concatenate(vic) if vic else np.zeros(0, np.int64), self.prune_threshold,
+                                   1.0 - DECAY_RATE, B)
+        try:
+            if base_ok and self._native_w1_ok(pl, thr, cc_w1, base_checked=True):
+                with tracer.stage("cb_apply_native", dev):
+                    pruned += self._native_w1(pl, fact_key, codes, Q, flat, f_off, thr, now, count0, stats,
+                                              reach_new)
+                pl = {"segments": []}  # applied
+        finally:
+            if cc_w1:
+                g.cc_end()
         with tracer.stage("sc_digest_base", dev):
             self._dcc_begin(pl)
             if any(s["consolidate"] for s in pl["segments"]):
@@ -1613,7 +1630,7 @@ class ShardedMemorySystem:
     NATIVE_W1 = True
     native_w1_runs = 0  # batches applied natively (tests)
 
-    def _native_w1_ok(self, pl: Dict, thr) -> bool:
+    def _native_w1_ok(self, pl: Dict, thr, cc: bool = False, base_checked: bool = False) -> bool:
         """The native applier applies the plan of a one-rank buffer exactly
         when the tenant's rows are its global node numbers (rows appended in
         number order, no ghost rows -- then every key of the plan is a row),
@@ -1621,6 +1638,25 @@ class ShardedMemorySystem:
         rows are the per-segment path's), the decay prunes, and the graph's
         edges fit the one-block digest for the whole batch (the digest of
         :meth:`_digest_world1` on a tenant without super-nodes)."""
+        g = self.g
+        if not (base_checked or self._native_w1_base_ok(pl, thr)):
+            return False
+        app = sum(len(seg["edge_src"]) for seg in pl["segments"])
+        if cc:
+            # the partitioned batch (TenantGraph.cc_begin): every point takes the
+            # incremental digest inside the applier
+            c = g._cc
+            ns = c.get("ns") if c is not None else None
+            n_end = g.n + sum(len(seg["ins_kind"]) for seg in pl["segments"])
+            if ns is None or ns <= T.dg_small_max_edges() or 16 * ns <= n_end:
+                return False
+        elif g.num_edges + app > T.dg_small_max_edges():
+            return False
+        return True
+
+    def _native_w1_base_ok(self, pl: Dict, thr) -> bool:
+        """The conditions of :meth:`_native_w1_ok` that do not depend on the
+        graph's edges."""
         from ..core.consolidation import ConsolidationMixin
         from ..engine import native_apply as NA
         from ..engine import tenant_graph as TG
@@ -1633,9 +1669,6 @@ class ShardedMemorySystem:
         if g.emb8 is not None and g.emb8.dtype != torch.int8:
             return False
         if g.dim is None or g.dim > 1024 or PROFILE_CONTENTS > 64:
-            return False
-        app = sum(len(seg["edge_src"]) for seg in pl["segments"])
-        if g.num_edges + app > T.dg_small_max_edges():
             return False
         n = g.n
         if int(self.next_id) - sum(len(seg["ins_kind"]) for seg in pl["segments"]) != n:
@@ -1707,12 +1740,14 @@ class ShardedMemorySystem:
                 if seg["consolidate"]:
                     prog.point()
                 host.append((ins, vic))
-            res = prog.run(g.shard_count, Q)
+            res = prog.run(g.shard_count, Q, g._cc)
             p = 0
             gone = []
             for s, (seg, (ins, vic)) in enumerate(zip(run, host)):
                 steps = int(seg["c1"]) - int(seg["c0"]) + 1
                 g.decay_log += steps * math.log1p(-DECAY_RATE)
+                if g._cc is not None:
+                    g._cc["steps"] += steps
                 g._bump(edges=True)
                 if ins:
                     ids, contents, types, sh, r0 = ins

@@ -79,6 +79,15 @@ def _data(cfg=CPU):
     return X, sal0, keys0, steps
 
 
+def _seed_edges(cfg):
+    """``seed_edges`` random links among the initial rows (weights in [0.55, 1))."""
+    g = torch.Generator().manual_seed(17)
+    m, R = int(cfg["seed_edges"]), cfg["rows"]
+    src = torch.randint(0, R, (m,), generator=g)
+    dst = (src + 1 + torch.randint(0, R - 1, (m,), generator=g)) % R
+    return src, dst, torch.rand(m, generator=g) * 0.45 + 0.55
+
+
 def _split(n, world, r, weights=None):
     if weights:
         w = weights[:world]
@@ -132,6 +141,9 @@ def _single(tmp, cfg=CPU):
     g.add_nodes([f"node_{i + 1}" for i in range(R)], [f"memory {i + 1}" for i in range(R)], X.to(dev),
                 shard=codes, sal=torch.tensor(sal0), now=_now(-1), stored=True)
     ms.node_counter = R
+    if cfg.get("seed_edges"):  # a graph that starts with edges (world-1 comparisons only)
+        src, dst, w = _seed_edges(cfg)
+        g.append_edges(src.to(dev), dst.to(dev), w.to(dev), g.shard[src.to(dev)], g.etype("relates_to"), now=_now(-1))
     stats = []
     for s, (convs, V) in enumerate(steps):
         import lazzaro_amd.engine.tenant_graph as tgm
@@ -200,6 +212,11 @@ def _sharded(comm, cfg=CPU):
     lo, hi = _split(cfg["rows"], comm.world, comm.rank, [5, 1, 2] if rebal else None)
     sm.add_memories([f"memory {i + 1}" for i in range(lo, hi)], X[lo:hi].to(dev), keys0[lo:hi],
                     salience=torch.tensor(sal0[lo:hi]), now=_now(-1))
+    if cfg.get("seed_edges"):
+        assert comm.world == 1, "seeded edges: one rank (every row local)"
+        src, dst, w = _seed_edges(cfg)
+        g = sm.g
+        g.append_edges(src.to(dev), dst.to(dev), w.to(dev), g.shard[src.to(dev)], g.etype("relates_to"), now=_now(-1))
     if pruned:  # pruned scan + cluster placement: the same decisions as the single process
         sm.cluster_pass()
     spread = []

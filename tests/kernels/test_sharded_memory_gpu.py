@@ -59,6 +59,20 @@ def test_sharded_tenant_gpu_one_rank_native_vs_segments():
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_sharded_tenant_gpu_one_rank_native_persistent_graph():
+    """One GPU rank, a graph that keeps its edges (prune_threshold 0, 20k
+    seeded links): the native applier with the single tenant's incremental
+    components (TenantGraph.cc_begin) ends in the single process's state, as
+    the per-segment path does."""
+    for native in (True, False):
+        cfg = dict(GPU, steps=3, convs=32, cadence="conversation", native_w1=native, prune_thr=0.0,
+                   seed_edges=20000)
+        out = spawn(1, functools.partial(_sharded, cfg=cfg))
+        check_equivalent(out, 1, cfg["limit"])
+        assert (out[0]["native"] > 0) == native, out[0]["native"]
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
 @pytest.mark.parametrize("prune_thr", [0.5, 0.0])
 def test_sharded_tenant_gpu_incremental_digest(prune_thr):
     """Two GPU ranks, the incremental digest (stable base replicated and
