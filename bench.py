@@ -560,6 +560,17 @@ def main():
     # measured per-rank HBM peak of each section, next to hbm_plan's estimate
     hbm_peak = {}
 
+    def _release():
+        # the previous section's tenant is freed before the next one is
+        # built: its MemorySystem / graph / store objects hold reference cycles,
+        # so dropping the names alone leaves ~54 GB allocated until a gen-2
+        # collection happens to run (the sections' measured peaks then counted
+        # two tenants)
+        import gc as _gc
+        _gc.collect()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+
     def peak(name):
         if dev.type == "cuda":
             hbm_peak[name] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 2)
@@ -574,7 +585,7 @@ def main():
         svc.close()
         del ms, g, Xb, bias, q16, Qe, res0, api_rows, svc
         if dev.type == "cuda":
-            torch.cuda.empty_cache()
+            _release()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
         # two untimed warmup batches: the second is the first that takes the
@@ -588,7 +599,7 @@ def main():
             # conversation), so decay / components / eviction's edge drops run
             # on a graph of tens of millions of edges
             if dev.type == "cuda":
-                torch.cuda.empty_cache()
+                _release()
             persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 2, emb,
                                          dim=a.dim, prune_threshold=0.0, stream=a.consolidate_stream)
             peak("consolidate_persistent_graph")
@@ -600,7 +611,7 @@ def main():
         if consolidate is None:
             svc.close()
         if dev.type == "cuda":
-            torch.cuda.empty_cache()
+            _release()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run_sharded
         # topic-clustered rows with cluster placement: the exact cone pruning
@@ -619,7 +630,7 @@ def main():
         if consolidate is None and sharded is None:
             svc.close()
         if dev.type == "cuda":
-            torch.cuda.empty_cache()
+            _release()
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run_sharded
         sharded_pg = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_persistent_steps, 1, emb,
