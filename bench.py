@@ -203,14 +203,21 @@ def hbm_plan(rows: int, dim: int, batch: int, consolidate_convs: int, facts: int
     encoder = 0.5e9  # bge-base weights + activations of a 1024 x 64-token batch
     # store search: int8 queries + candidate lists (cap 2048 x 16 slots x 8 B per query) + block records
     search_ws = batch * (2048 * 16 * 8 + 4 * dim) + 256 * 8 * 2048 * 16
-    head = cap * bpr + encoder + search_ws
+    # transients: the loader's 1M-row chunk (fp32 rows + the bf16 / int8
+    # copies and the quantiser's fp32 temporary), and the headline's recall
+    # truth (a 1M-row float64 chunk, its squared copy, and two 1,024-query
+    # float64 score blocks against it: the product and its scaled copy)
+    chunk = 1 << 20
+    load_ws = chunk * dim * (4 + 2 + 1 + 4)
+    recall_ws = chunk * dim * 8 * 2 + 2 * 1024 * chunk * 8
+    head = cap * bpr + encoder + search_ws + max(load_ws, recall_ws)
     # consolidation: the tenant, 2 x rows seeded edges (+1/8 append slack), the
     # dual scan's two candidate lists, k-means (4096 centroids, per-row labels)
     F = consolidate_convs * facts
     dual_ws = 2 * F * (2048 * 16 * 8) + 256 * 8 * 2048 * 16 * 2
     kmeans = 4096 * dim * 6 + rows * 16
-    cons = cap * bpr + 2 * rows * eb * 9 // 8 + encoder + dual_ws + kmeans
-    sharded = cap * bpr + 2 * rows * eb * 9 // 8 + F * 2 * (bpr + 64) + encoder + dual_ws + kmeans
+    cons = cap * bpr + 2 * rows * eb * 9 // 8 + encoder + dual_ws + kmeans + load_ws
+    sharded = cap * bpr + 2 * rows * eb * 9 // 8 + F * 2 * (bpr + 64) + encoder + dual_ws + kmeans + load_ws
     secs = {"headline": head, "consolidate": cons, "consolidate_persistent_graph": cons,
             "consolidate_sharded": sharded,
             # + the replicated stable base of the incremental digest (int32
