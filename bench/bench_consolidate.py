@@ -451,7 +451,12 @@ if __name__ == "__main__":
                     help="--sharded: reference per-conversation cadence or once-per-batch")
     ap.add_argument("--no-incremental-digest", action="store_true",
                     help="--sharded: the full digest at every run_consolidation point (A/B)")
+    ap.add_argument("--no-prefetch-under-cluster", action="store_true",
+                    help="no batch i+1 scan prefetch past a batch that runs a k-means pass (A/B)")
     a = ap.parse_args()
+    if a.no_prefetch_under_cluster:
+        from lazzaro_amd.core.memory_system import MemorySystem
+        MemorySystem.PREFETCH_UNDER_CLUSTER = False
     if a.no_incremental_digest:
         from lazzaro_amd.parallel.sharded_memory import ShardedMemorySystem
         ShardedMemorySystem.DIGEST_INCREMENTAL = False

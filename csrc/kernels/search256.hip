@@ -20,6 +20,8 @@
 
 #include <cstdlib>
 #include <cfloat>
+#include <map>
+#include <mutex>
 
 LZK_DEBUG_STATE(search256)
 
@@ -1404,8 +1406,8 @@ LZK_EXPORT int lzk_cand_grid_f8(int nrows, int nq) {
 // (the interactive turn: ONE query, a list of hundreds to thousands of
 // entries above the cut) spreads each list over up to 64 blocks -- one block
 // re-scoring a list row by row was 330 us of a 2.2 ms single-query search.
-// The certificate's per-query counters live in a per-device scratch zeroed on
-// the stream before each split launch.
+// The certificate's per-query counters live in a per-(device, stream) scratch
+// zeroed on the stream before each split launch.
 namespace {
 constexpr int RESCORE_SPLIT_MAX = 64;
 int rescore_split(int nq) {
@@ -1413,24 +1415,32 @@ int rescore_split(int nq) {
   int s = 256 / nq;
   return s < 1 ? 1 : (s > RESCORE_SPLIT_MAX ? RESCORE_SPLIT_MAX : s);
 }
-thread_local int* g_rs_scratch[16] = {};
-thread_local int g_rs_cap[16] = {};
+// one scratch per (device, stream): two streams re-scoring at once (a
+// serving search beside a consolidation scan on its side stream) never share
+// counters; within a stream the memset and the launch are stream-ordered
+struct RsScratch {
+  int* p = nullptr;
+  int cap = 0;
+};
+std::mutex g_rs_mu;
+std::map<std::pair<int, hipStream_t>, RsScratch> g_rs;
 int* rescore_counters(int nq, hipStream_t st) {
   int dev = 0;
   (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 16) return nullptr;
-  if (g_rs_cap[dev] < 2 * nq) {
-    if (g_rs_scratch[dev]) (void)hipFree(g_rs_scratch[dev]);
-    g_rs_scratch[dev] = nullptr;
+  std::lock_guard<std::mutex> lk(g_rs_mu);
+  RsScratch& s = g_rs[{dev, st}];
+  if (s.cap < 2 * nq) {
+    if (s.p) (void)hipFree(s.p);  // synchronous: no launch still reads it
+    s.p = nullptr;
     const int cap = 2 * (nq > 4096 ? nq : 4096);
-    if (hipMalloc(&g_rs_scratch[dev], (size_t)cap * sizeof(int)) != hipSuccess) {
-      g_rs_cap[dev] = 0;
+    if (hipMalloc(&s.p, (size_t)cap * sizeof(int)) != hipSuccess) {
+      s.cap = 0;
       return nullptr;
     }
-    g_rs_cap[dev] = cap;
+    s.cap = cap;
   }
-  if (hipMemsetAsync(g_rs_scratch[dev], 0, (size_t)2 * nq * sizeof(int), st) != hipSuccess) return nullptr;
-  return g_rs_scratch[dev];
+  if (hipMemsetAsync(s.p, 0, (size_t)2 * nq * sizeof(int), st) != hipSuccess) return nullptr;
+  return s.p;
 }
 
 template <bool F32>

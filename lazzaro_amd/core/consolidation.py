@@ -790,6 +790,9 @@ class ConsolidationMixin:
 
     _prefetch_next = None
     _prefetched = None
+    # False: no prefetch past a batch that runs a k-means pass (A/B only,
+    # bench/bench_consolidate.py --no-prefetch-under-cluster)
+    PREFETCH_UNDER_CLUSTER = True
 
     def _launch_prefetch(self, new_rows: int, cluster: bool) -> None:
         """Batch i+1's dual candidate scan (see :meth:`consolidate_stream`),
@@ -797,13 +800,16 @@ class ConsolidationMixin:
         known (before its plan when batch i's scan was itself prefetched, so
         the scan runs under batch i's planner, verification and apply).
         ``new_rows``: a bound of the rows batch i inserts (reserved now: no
-        column moves under the scan). Skipped when batch i runs a cluster
-        pass (``cluster``: it rewrites the hierarchy the scan's callers read)
-        or the scan is not the kernel path."""
+        column moves under the scan). Skipped when the scan is not the kernel
+        path. A k-means pass inside batch i (``cluster``) does not stop it:
+        the pass only rewrites ``TenantGraph.hier``, which neither the scan
+        nor :meth:`TenantGraph.cos_topk_finish` reads (rows, kinds and
+        super-node flags are untouched), so batch i+1's scan runs under the
+        pass too instead of after it."""
         nxt, self._prefetch_next = self._prefetch_next, None
         self._prefetched = None
         g = self.graph
-        if nxt is None or not g.on_gpu or nxt[1] is None or cluster:
+        if nxt is None or not g.on_gpu or nxt[1] is None or (cluster and not self.PREFETCH_UNDER_CLUSTER):
             return
         convs, embs = nxt[0], nxt[1]
         flat, idx, j = [], [], 0

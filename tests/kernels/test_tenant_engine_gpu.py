@@ -881,7 +881,8 @@ def test_consolidate_batch_incremental_components_gpu(tmp_path, monkeypatch, pru
         assert np.array_equal(a[5][k], b[5][k]), k
 
 
-def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch):
+@pytest.mark.parametrize("hier", ["reference", "kmeans"])
+def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch, hier):
     """``consolidate_stream``: batch i+1's int8 dual candidate scan runs on a
     side stream under batch i's apply and is completed against the graph
     batch i left (TenantGraph.cos_topk_finish). Three batches on a 1.2M-row
@@ -889,7 +890,9 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch):
     candidates are re-scanned) and facts that duplicate batch 1's own new
     facts (rows that arrived after the prefetch: re-ranked in) -- end in the
     state of three ``consolidate_batch`` calls: counts, nodes, saliences,
-    access counts, edges."""
+    access counts, edges. ``kmeans``: the k-means hierarchy re-clusters
+    inside batches 1 and 2 (every 20 conversations) and batch i+1's scan
+    still runs prefetched under them; the hierarchies end equal too."""
     from lazzaro_amd.engine import tenant_graph as TG
     N, D, B, F = 1_200_000, 384, 32, 6
     X, lab = _clustered(N, D, 256, 23, noise=1.6)
@@ -939,9 +942,11 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch):
     out = {}
     for mode in ("calls", "stream"):
         monkeypatch.setattr(time, "time", _Clock())
+        hk = {} if hier == "reference" else {"hierarchy_mode": "kmeans",
+                                             "hierarchy_params": {"fine": 64, "top": 8, "every": 20, "iters": 1}}
         ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
                           db_dir=str(tmp_path / mode), device=DEV, load_from_disk=False, max_buffer_size=N - 100,
-                          super_node_threshold=10 ** 9)
+                          super_node_threshold=10 ** 9, **hk)
         g = ms.graph
         shards = [g.shard_id(f"topic{c}") for c in range(8)]
         g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"m {i}" for i in range(N)], X.to(DEV),
@@ -957,7 +962,9 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch):
         order = np.lexsort((e["dst"].numpy(), e["src"].numpy()))
         out[mode] = (stats, np.nonzero(live)[0], g.sal[:n].cpu().numpy()[live], g.acc[:n].cpu().numpy()[live],
                      {k: v.numpy()[order] for k, v in e.items() if k in ("src", "dst", "w", "meta")},
-                     [g.ids[r] for r in np.nonzero(live)[0][-50:]])
+                     [g.ids[r] for r in np.nonzero(live)[0][-50:]],
+                     {k: v.cpu().numpy() for k, v in (getattr(g, "hier", None) or {}).items()
+                      if k in ("fine", "top", "perm")})
         ms.close()
     a, b = out["calls"], out["stream"]
     assert calls["finish"] == 2  # batches 2 and 3 came from prefetched scans
@@ -967,4 +974,7 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch):
     for k in a[4]:
         assert np.array_equal(a[4][k], b[4][k]), k
     assert a[5] == b[5]
+    assert a[6].keys() == b[6].keys() and all(np.array_equal(a[6][k], b[6][k]) for k in a[6])
+    if hier == "kmeans":
+        assert a[6], "the k-means hierarchy was built"
     assert calls["aff"] >= 1, calls  # some prefetched candidates lost a row to the previous batch's eviction

@@ -41,13 +41,22 @@ def test_not_gc_tracked_and_collector_cost_flat():
         gc.collect()
         return time.perf_counter() - t0
 
-    base = min(collect_s() for _ in range(3))
-    big = rt.StrColumn([f"node_{i}" for i in range(2_000_000)])
-    assert not gc.is_tracked(big)
-    with_big = min(collect_s() for _ in range(3))
     # a full pass over the process's tracked objects does not grow with the
-    # column (generous bound: shared CI hosts are noisy)
-    assert with_big < 1.5 * base + 0.02, (with_big, base)
+    # column (generous bound; up to 3 attempts, each timing the pass without
+    # and with the column back to back: shared CI hosts and parallel test
+    # workers make single timings noisy)
+    seen = []
+    for _ in range(3):
+        base = min(collect_s() for _ in range(3))
+        big = rt.StrColumn([f"node_{i}" for i in range(2_000_000)])
+        assert not gc.is_tracked(big)
+        with_big = min(collect_s() for _ in range(3))
+        del big
+        seen.append((with_big, base))
+        if with_big < 1.5 * base + 0.02:
+            break
+    else:
+        raise AssertionError(seen)
 
 
 def test_tenant_graph_uses_native_columns():
