@@ -453,7 +453,12 @@ if __name__ == "__main__":
                     help="--sharded: the full digest at every run_consolidation point (A/B)")
     ap.add_argument("--no-prefetch-under-cluster", action="store_true",
                     help="no batch i+1 scan prefetch past a batch that runs a k-means pass (A/B)")
+    ap.add_argument("--cluster-inline", action="store_true",
+                    help="k-means passes in line instead of in the background (A/B)")
     a = ap.parse_args()
+    if a.cluster_inline:
+        from lazzaro_amd.core.memory_system import MemorySystem
+        MemorySystem.CLUSTER_BACKGROUND = False
     if a.no_prefetch_under_cluster:
         from lazzaro_amd.core.memory_system import MemorySystem
         MemorySystem.PREFETCH_UNDER_CLUSTER = False

@@ -840,15 +840,22 @@ class ConsolidationMixin:
             h = g.cos_topk_prefetch(Q, mask, torch.as_tensor(codes), LINK_THRESHOLD, _prefetch_stream(g.device))
         self._prefetched = {"src": embs, "codes": codes, "M": len(flat), "h": h}
 
-    def _maybe_cluster(self, c0: int) -> None:
+    # the planned batch's k-means passes run in the background
+    # (TenantGraph.cluster_pass(background=True)): the rest of the batch and
+    # the next one are applied under them. False: in line (A/B,
+    # bench/bench_consolidate.py --cluster-inline)
+    CLUSTER_BACKGROUND = True
+
+    def _maybe_cluster(self, c0: int, background: bool = False) -> None:
         """hierarchy_mode="kmeans": re-cluster when the conversation count
         crosses a multiple of hierarchy_params["every"]."""
         if not self.enable_hierarchy or getattr(self, "hierarchy_mode", "reference") != "kmeans":
             return
         hp = self.hierarchy_params
-        if self.conversation_count // hp["every"] > c0 // hp["every"] or getattr(self.graph, "hier", None) is None:
+        if self.conversation_count // hp["every"] > c0 // hp["every"] or not self.graph.has_hier():
             with tracer.stage("cluster", self._device):
-                self.graph.cluster_pass(hp["fine"], hp["top"], hp["iters"])
+                self.graph.cluster_pass(hp["fine"], hp["top"], hp["iters"],
+                                        background=background and self.CLUSTER_BACKGROUND)
 
     def _enforce_buffer_limit_counted(self, stats: Dict[str, int]) -> None:
         g = self.graph
@@ -931,7 +938,7 @@ class ConsolidationMixin:
         # a k-means pass inside this batch (the planner's cluster points), or
         # the first one at its end
         c0 = self.conversation_count
-        cluster = bool(cl_every) and ((c0 + B) // cl_every > c0 // cl_every or getattr(g, "hier", None) is None)
+        cluster = bool(cl_every) and ((c0 + B) // cl_every > c0 // cl_every or not g.has_hier())
         # rows this batch can insert: its facts and at most one super-node per
         # shard it touches (a super-node is never evicted, so a shard gets one)
         new_rows = M + len(set(codes.tolist()))
@@ -1004,8 +1011,8 @@ class ConsolidationMixin:
             with tracer.stage("rc_deferred", "cpu"):
                 for cap in pending:
                     self._rc_host(cap)
-        if getattr(self, "hierarchy_mode", "") == "kmeans" and getattr(g, "hier", None) is None:
-            self._maybe_cluster(self.conversation_count - 1)
+        if getattr(self, "hierarchy_mode", "") == "kmeans" and not g.has_hier():
+            self._maybe_cluster(self.conversation_count - 1, background=True)
 
     # the segments of a plan through the native applier (csrc/kernels/apply.hip
     # via engine/native_apply.py) where eligible; False: the per-segment path
@@ -1211,7 +1218,7 @@ class ConsolidationMixin:
                 if gone:
                     self._store_delete(gone, graph_unstored=True)
                     gone = []
-                self._maybe_cluster(self.conversation_count - 1)
+                self._maybe_cluster(self.conversation_count - 1, background=True)
         if gone:
             with tracer.stage("ap_store_delete", "cpu"):
                 self._store_delete(gone, graph_unstored=True)
@@ -1241,7 +1248,7 @@ class ConsolidationMixin:
                     else:
                         self.run_consolidation(prune=not self.auto_prune)
             if seg["cluster"]:
-                self._maybe_cluster(self.conversation_count - 1)
+                self._maybe_cluster(self.conversation_count - 1, background=not self._commit_each)
             if self._commit_each:
                 with tracer.stage("commit", "cpu"):
                     self._save_to_persistence()

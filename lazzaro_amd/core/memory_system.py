@@ -1253,6 +1253,9 @@ Be clinical yet insightful. Do not include conversational filler."""
     def close(self):
         if self.background_executor:
             self.background_executor.shutdown(wait=True)
+        g = getattr(self, "graph", None)
+        if g is not None and hasattr(g, "cluster_join"):
+            g.cluster_join()  # a background k-means pass ends before the store closes
         if self._writer is not None:
             self.flush_persistence()
             self._writer.shutdown(wait=True)

@@ -263,6 +263,41 @@ class Capture:
         return self._val
 
 
+_CL_STREAMS: Dict = {}
+
+
+def _cluster_stream(dev):
+    """One side stream per device for background k-means passes."""
+    st = _CL_STREAMS.get(dev)
+    if st is None:
+        st = _CL_STREAMS[dev] = torch.cuda.Stream(dev)
+    return st
+
+
+class _BackgroundJob:
+    """``fn()`` on a worker thread; ``result()`` joins it and re-raises."""
+
+    def __init__(self, fn):
+        import threading
+
+        self._out = self._err = None
+
+        def run():
+            try:
+                self._out = fn()
+            except BaseException as e:  # noqa: BLE001 -- re-raised by result()
+                self._err = e
+
+        self._t = threading.Thread(target=run, name="lzk-cluster", daemon=False)
+        self._t.start()
+
+    def result(self):
+        self._t.join()
+        if self._err is not None:
+            raise self._err
+        return self._out
+
+
 class TenantGraph:
     NODE_COLS = (("sal", torch.float32, 0.0), ("acc", torch.int32, 0), ("last", torch.float64, 0.0),
                  ("ts", torch.float64, 0.0), ("shard", torch.int32, -1), ("kind", torch.uint8, FREE),
@@ -298,6 +333,8 @@ class TenantGraph:
         self.decay_log = 0.0  # sum of log(1 - rate) over every decay applied
         self.version = 0  # bumps on any mutation (views / caches)
         self.edge_version = 0
+        self._hier = None  # the k-means hierarchy (cluster_pass); read through .hier
+        self._hier_job = None  # a background cluster_pass in flight (cluster_join)
         self._csr = None
         self._csr_version = -1
         self._boost_state = T.BoostState()
@@ -2555,7 +2592,25 @@ class TenantGraph:
         return [[ids[x] for x in row if x >= 0] for row in r.cpu().tolist()]
 
     # ------------------------------------------------------------------ k-means hierarchy (K16)
-    def cluster_pass(self, n_fine: int = 4096, n_top: int = 64, iters: int = 2, seed: int = 0, comm=None) -> Dict:
+    @property
+    def hier(self) -> Optional[Dict]:
+        """The k-means hierarchy of the last :meth:`cluster_pass` (joins a
+        pass still running in the background)."""
+        if self._hier_job is not None:
+            self.cluster_join()
+        return self._hier
+
+    @hier.setter
+    def hier(self, value) -> None:
+        self.cluster_join()
+        self._hier = value
+
+    def has_hier(self) -> bool:
+        """Whether a hierarchy exists or is being built (no join)."""
+        return self._hier_job is not None or self._hier is not None
+
+    def cluster_pass(self, n_fine: int = 4096, n_top: int = 64, iters: int = 2, seed: int = 0, comm=None,
+                     background: bool = False) -> Dict:
         """Two-level hierarchical clustering of the live shard nodes (SURVEY.md
         §2.4 K16; ``MemorySystem(hierarchy_mode="kmeans")``): spherical k-means
         into ``n_fine`` clusters over the tenant's rows in place (fused MFMA
@@ -2569,63 +2624,123 @@ class TenantGraph:
         ``comm`` (world > 1): the rows are one row-sharded tenant's local part;
         the fine level is the distributed k-means (centroid sums all-reduced,
         SURVEY.md §2.5 C4) and the topic level runs replicated on the
-        identical fine centroids, so every rank holds the same hierarchy."""
-        from ..index.kmeans import kmeans
+        identical fine centroids, so every rank holds the same hierarchy.
 
+        ``background`` (one GPU tenant, no ``comm``): the pass reads the rows
+        as they are NOW -- the live mask and ``n`` are taken on the graph
+        stream here -- but runs on a side stream from a worker thread, so the
+        graph's next segments (which only append rows >= n and flip flags of
+        rows the mask already fixed; no row's vector below n changes) run
+        under it. ``hier`` joins it; :meth:`has_hier` does not."""
+        self.cluster_join()
         n = self.n
         if n == 0 or self.dim is None:
             return {}
+        dist = comm is not None and (comm.world > 1 or comm.enabled)
         with self.on_stream():
             live = (self.kind[:n] == NODE) & (self.sup[:n] == 0) & (self.has_emb[:n] == 1)
-            n_live = int(live.sum())
-            dist = comm is not None and (comm.world > 1 or comm.enabled)
-            if dist:
-                t = torch.tensor([n_live], dtype=torch.int64, device=comm.device)
-                comm.all_reduce(t)
-                n_glob = int(t.item())
-            else:
-                n_glob = n_live
-            if n_glob == 0:
-                return {}
-            if self.on_gpu and self.emb16 is not None:
-                X = self.emb16[:n]
-            elif self.on_gpu:  # lean: the pass's own bf16 copy, released when it ends
-                from ..ops.search import bf16_rows
-                X = bf16_rows(self.emb32[:n], self.Dp)
-            else:
-                X = self.emb32[:n] / self.sqn[:n].sqrt().clamp_min(1e-30)[:, None]
-            kf = min(n_fine, n_glob)
-            kt = min(n_top, kf)
-            prev = getattr(self, "hier", None) or {}
-            init_f = prev.get("fine_c") if prev.get("fine_c") is not None and prev["fine_c"].shape[0] == kf else None
-            # large tenants: mini-batch refinement steps on a 1M-row sample,
-            # then one full assign + update (labels for every row)
-            smp = self.CLUSTER_SAMPLE if n_live > 2 * self.CLUSTER_SAMPLE else 0
-            # warm passes over large tenants: the full-data assign searches a
-            # row's fine clusters only under its nearest previous topic
-            fa = None
-            if smp and init_f is not None and prev.get("top_c16") is not None and prev.get("top_of_fine") is not None:
-                from ..index.kmeans import assign_two_level
-                T16, tof = prev["top_c16"], prev["top_of_fine"]
-                fa = lambda Xa, C16: assign_two_level(Xa, C16, T16, tof)  # noqa: E731
-            # the mini-batch steps: the same two-level assign (SAMPLE_TWO_LEVEL = False: flat over all fine)
-            sa = fa if self.SAMPLE_TWO_LEVEL else None
-            fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp,
-                                     full_assign=fa, sample_assign=sa, comm=comm if dist else None)
-            init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
-            tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
-            lab = lab.long()
-            top = torch.where(lab >= 0, top_of_fine.long()[lab.clamp_min(0)], torch.full_like(lab, -1))
-            rows = torch.nonzero(top >= 0).flatten()
-            o = torch.argsort(top[rows] * n + rows)
-            perm = rows[o]
-            cnt = torch.bincount(top[rows], minlength=kt)
-            start = torch.zeros(kt + 1, dtype=torch.long, device=self.device)
-            start[1:] = torch.cumsum(cnt, 0)
-            self.hier = {"fine_c": fc32, "top_c": tc32, "fine": lab.to(torch.int32), "top": top.to(torch.int32),
-                         "perm": perm, "start": start, "n": n, "version": self.version,
-                         "top_c16": tc16, "top_of_fine": top_of_fine}
-        return {"fine": kf, "top": kt, "rows": n_glob}
+            src = self.emb16[:n] if (self.on_gpu and self.emb16 is not None) else None
+            if background and self.on_gpu and not dist:
+                ev = torch.cuda.Event()
+                ev.record()
+                graph_st = torch.cuda.current_stream(self.device)
+                st = _cluster_stream(self.device)
+                prev = self._hier or {}
+                version = self.version
+                for t in (live, src):
+                    if t is not None:
+                        t.record_stream(st)
+                emb32 = self.emb32[:n] if src is None else None
+                if emb32 is not None:
+                    emb32.record_stream(st)
+
+                def work():
+                    with torch.cuda.stream(st):
+                        st.wait_event(ev)
+                        out = self._cluster_compute(live, src, emb32, n, n_fine, n_top, iters, seed, None, prev,
+                                                    version)
+                        done = torch.cuda.Event()
+                        done.record(st)
+                    return out, done, graph_st
+
+                self._hier_job = _BackgroundJob(work)
+                return {"background": True}
+            emb32 = self.emb32[:n] if src is None else None
+            out = self._cluster_compute(live, src, emb32, n, n_fine, n_top, iters, seed, comm if dist else None,
+                                        self._hier or {}, self.version)
+        if out is None:
+            return {}
+        self._hier = out
+        return {"fine": out["fine_c"].shape[0], "top": out["top_c"].shape[0], "rows": out["rows"]}
+
+    def cluster_join(self) -> None:
+        """Wait for a background :meth:`cluster_pass` and publish its
+        hierarchy (the graph stream waits for its kernels; its tensors are
+        marked in use there). Re-raises the pass's error."""
+        job, self._hier_job = self._hier_job, None
+        if job is None:
+            return
+        out, done, graph_st = job.result()
+        graph_st.wait_event(done)
+        if out is None:
+            return
+        for t in out.values():
+            if torch.is_tensor(t) and t.is_cuda:
+                t.record_stream(graph_st)
+        self._hier = out
+
+    def _cluster_compute(self, live, src, emb32, n: int, n_fine: int, n_top: int, iters: int, seed: int, comm,
+                         prev: Dict, version: int) -> Optional[Dict]:
+        """The body of :meth:`cluster_pass` on the current stream over rows
+        [0, n): ``live`` mask, ``src`` the bf16 rows (or None: ``emb32``)."""
+        from ..index.kmeans import kmeans
+
+        n_live = int(live.sum())
+        if comm is not None:
+            t = torch.tensor([n_live], dtype=torch.int64, device=comm.device)
+            comm.all_reduce(t)
+            n_glob = int(t.item())
+        else:
+            n_glob = n_live
+        if n_glob == 0:
+            return None
+        if src is not None:
+            X = src
+        elif self.on_gpu:  # lean: the pass's own bf16 copy, released when it ends
+            from ..ops.search import bf16_rows
+            X = bf16_rows(emb32, self.Dp)
+        else:
+            X = emb32 / self.sqn[:n].sqrt().clamp_min(1e-30)[:, None]
+        kf = min(n_fine, n_glob)
+        kt = min(n_top, kf)
+        init_f = prev.get("fine_c") if prev.get("fine_c") is not None and prev["fine_c"].shape[0] == kf else None
+        # large tenants: mini-batch refinement steps on a 1M-row sample,
+        # then one full assign + update (labels for every row)
+        smp = self.CLUSTER_SAMPLE if n_live > 2 * self.CLUSTER_SAMPLE else 0
+        # warm passes over large tenants: the full-data assign searches a
+        # row's fine clusters only under its nearest previous topic
+        fa = None
+        if smp and init_f is not None and prev.get("top_c16") is not None and prev.get("top_of_fine") is not None:
+            from ..index.kmeans import assign_two_level
+            T16, tof = prev["top_c16"], prev["top_of_fine"]
+            fa = lambda Xa, C16: assign_two_level(Xa, C16, T16, tof)  # noqa: E731
+        # the mini-batch steps: the same two-level assign (SAMPLE_TWO_LEVEL = False: flat over all fine)
+        sa = fa if self.SAMPLE_TWO_LEVEL else None
+        fc32, fc16, lab = kmeans(X, kf, iters=iters, seed=seed, init=init_f, mask=live, sample=smp,
+                                 full_assign=fa, sample_assign=sa, comm=comm)
+        init_t = prev.get("top_c") if prev.get("top_c") is not None and prev["top_c"].shape[0] == kt else None
+        tc32, tc16, top_of_fine = kmeans(fc16, kt, iters=iters + 2, seed=seed + 1, init=init_t)
+        lab = lab.long()
+        top = torch.where(lab >= 0, top_of_fine.long()[lab.clamp_min(0)], torch.full_like(lab, -1))
+        rows = torch.nonzero(top >= 0).flatten()
+        o = torch.argsort(top[rows] * n + rows)
+        perm = rows[o]
+        cnt = torch.bincount(top[rows], minlength=kt)
+        start = torch.zeros(kt + 1, dtype=torch.long, device=self.device)
+        start[1:] = torch.cumsum(cnt, 0)
+        return {"fine_c": fc32, "top_c": tc32, "fine": lab.to(torch.int32), "top": top.to(torch.int32),
+                "perm": perm, "start": start, "n": n, "version": version, "top_c16": tc16,
+                "top_of_fine": top_of_fine, "rows": n_glob}
 
     def hier_children(self, q: torch.Tensor, threshold: float, limit: int) -> List[int]:
         """Hierarchical retrieval over the k-means topics (the reference's

@@ -940,8 +940,18 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch, hier):
             monkeypatch.setattr(TG.TenantGraph, "_cos_topk", real_cos)
     monkeypatch.setattr(TG.TenantGraph, "cos_topk_finish", finish)
     out = {}
-    for mode in ("calls", "stream"):
+    bg = {"n": 0}
+    real_pass = TG.TenantGraph.cluster_pass
+
+    def cluster_pass(self, *a, **kw):
+        bg["n"] += bool(kw.get("background"))
+        return real_pass(self, *a, **kw)
+    monkeypatch.setattr(TG.TenantGraph, "cluster_pass", cluster_pass)
+    # kmeans: "inline" = per-batch calls with every k-means pass in line (the
+    # others run the planned batches' passes in the background)
+    for mode in ("calls", "stream") + (("inline",) if hier == "kmeans" else ()):
         monkeypatch.setattr(time, "time", _Clock())
+        monkeypatch.setattr(MemorySystem, "CLUSTER_BACKGROUND", mode != "inline")
         hk = {} if hier == "reference" else {"hierarchy_mode": "kmeans",
                                              "hierarchy_params": {"fine": 64, "top": 8, "every": 20, "iters": 1}}
         ms = MemorySystem(llm_provider=LocalLLM(), embedding_provider=HashEmbedder(dim=D), enable_async=False,
@@ -952,7 +962,7 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch, hier):
         g.add_nodes([f"node_{i + 1}" for i in range(N)], [f"m {i}" for i in range(N)], X.to(DEV),
                     shard=np.asarray([shards[int(c) % 8] for c in lab], dtype=np.int32), sal=sal0, stored=True)
         ms.node_counter = N
-        if mode == "calls":
+        if mode in ("calls", "inline"):
             stats = [ms.consolidate_batch(f, embeddings=V, now=t) for f, V, t in batches]
         else:
             stats = list(ms.consolidate_stream(batches))
@@ -977,4 +987,9 @@ def test_consolidate_stream_matches_batches_gpu(tmp_path, monkeypatch, hier):
     assert a[6].keys() == b[6].keys() and all(np.array_equal(a[6][k], b[6][k]) for k in a[6])
     if hier == "kmeans":
         assert a[6], "the k-means hierarchy was built"
+        assert bg["n"] >= 2, bg  # passes inside the batches ran in the background
+        c = out["inline"]
+        assert a[0] == c[0] and all(np.array_equal(a[i], c[i]) for i in (1, 2, 3))
+        assert all(np.array_equal(a[4][k], c[4][k]) for k in a[4]) and a[5] == c[5]
+        assert a[6].keys() == c[6].keys() and all(np.array_equal(a[6][k], c[6][k]) for k in a[6])
     assert calls["aff"] >= 1, calls  # some prefetched candidates lost a row to the previous batch's eviction

@@ -92,7 +92,7 @@ def test_cls_pooling_last_layer_on_cls_rows_only(packed, monkeypatch):
     cfg = dataclasses.replace(M.CONFIGS["tiny"], pooling="cls")
     monkeypatch.setitem(M.CONFIGS, "tiny-cls", cfg)
     enc = M.SentenceEncoder("tiny-cls", seed=4)
-    ids = torch.randint(1000, 4000, (5, 20), dtype=torch.int32)
+    ids = torch.randint(1000, 4000, (5, 20), dtype=torch.int32, generator=torch.Generator().manual_seed(11))
     lens = torch.tensor([20, 3, 11, 1, 7], dtype=torch.int32)
     monkeypatch.setattr(M.SentenceEncoder, "CLS_LAST", False)
     full, _ = enc.forward(ids, lens, packed=packed)
