@@ -411,6 +411,7 @@ def main():
     gc.callbacks.append(_gc_cb)
     t0 = time.perf_counter()
     n_res = 0
+    res = None
     for res in ms.search_memories_stream(batches(a.steps), limit=a.k):
         n_res += len(res)
     sync()
@@ -462,10 +463,10 @@ def main():
         return e
 
     rsteps = a.steps if a.routed_steps < 0 else a.routed_steps
+    last, gb = {}, {}  # the last routed / global results (cleared before the tenant is freed)
     if rsteps > 0:
         rr = random.Random(77 + rank)
         rusers = [[tenants[rr.randrange(world)] for _ in range(a.batch)] for _ in range(len(pool))]
-        last = {}
 
         def routed_run(i0, n):
             # pipelined like the headline: batch i+1's front-end embed (the
@@ -510,7 +511,6 @@ def main():
                                                                                        "group)")})
     if a.global_batch > 0:
         gq = [pool[i % len(pool)][: a.global_batch] for i in range(len(pool))]
-        gb = {}
 
         def glob(i):
             gb["h"] = svc.search_global_batch(svc._embed_front(gq[i % len(gq)]), a.k)
@@ -564,10 +564,12 @@ def main():
     S_tok = int(emb.tok.encode_batch(pool[0], emb.max_len)[0].shape[1])
     lens = emb.tok.encode_batch(pool[0], emb.max_len)[1]
 
-    # measured per-rank HBM peak of each section, next to hbm_plan's estimate
+    # measured per-rank HBM peak of each section, next to hbm_plan's estimate,
+    # and what was still allocated when the section started
     hbm_peak = {}
+    hbm_start = {}
 
-    def _release():
+    def _release(name):
         # the previous section's tenant is freed before the next one is
         # built: its MemorySystem / graph / store objects hold reference cycles,
         # so dropping the names alone leaves ~54 GB allocated until a gen-2
@@ -577,6 +579,8 @@ def main():
         _gc.collect()
         if dev.type == "cuda":
             torch.cuda.empty_cache()
+            torch.cuda.reset_peak_memory_stats(dev)
+            hbm_start[name] = round(torch.cuda.memory_allocated(dev) / 2 ** 30, 2)
 
     def peak(name):
         if dev.type == "cuda":
@@ -590,9 +594,13 @@ def main():
     consolidate = persistent = None
     if a.consolidate_steps > 0:
         svc.close()
-        del ms, g, Xb, bias, q16, Qe, res0, api_rows, svc
+        # every name that still reaches the headline tenant (a ResultBatch
+        # holds its graph for lazy node views)
+        del ms, g, Xb, bias, q16, Qe, res0, api_rows, svc, res
+        last.clear()
+        gb.clear()
         if dev.type == "cuda":
-            _release()
+            _release("consolidate")
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run as run_consolidate
         # two untimed warmup batches: the second is the first that takes the
@@ -606,7 +614,7 @@ def main():
             # conversation), so decay / components / eviction's edge drops run
             # on a graph of tens of millions of edges
             if dev.type == "cuda":
-                _release()
+                _release("consolidate_persistent_graph")
             persistent = run_consolidate(comm, dev, a.rows, a.consolidate_convs, 8, a.consolidate_steps, 2, emb,
                                          dim=a.dim, prune_threshold=0.0, stream=a.consolidate_stream)
             peak("consolidate_persistent_graph")
@@ -618,7 +626,7 @@ def main():
         if consolidate is None:
             svc.close()
         if dev.type == "cuda":
-            _release()
+            _release("consolidate_sharded")
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run_sharded
         # topic-clustered rows with cluster placement: the exact cone pruning
@@ -637,7 +645,7 @@ def main():
         if consolidate is None and sharded is None:
             svc.close()
         if dev.type == "cuda":
-            _release()
+            _release("consolidate_sharded_persistent_graph")
         sys.path.insert(0, os.path.join(ROOT, "bench"))
         from bench_consolidate import run_sharded
         sharded_pg = run_sharded(comm, dev, a.rows, a.consolidate_convs, 8, a.sharded_persistent_steps, 1, emb,
@@ -682,7 +690,7 @@ def main():
         "gc_in_timed_loop": {"startup_heap_frozen": bool(a.gc_freeze),
                              **{f"gen{k}": {"passes": v[0], "ms": round(v[1] * 1e3, 2)} for k, v in gc_log.items()}},
         "prewarm_s": round(t_pre, 1),
-        "hbm_per_rank": {"peak_gib_measured": hbm_peak,
+        "hbm_per_rank": {"peak_gib_measured": hbm_peak, "allocated_gib_at_section_start": hbm_start,
                          "plan": hbm_plan(a.rows, a.dim, a.batch, a.consolidate_convs, world=a.gpus)},
     }
     if consolidate is not None:
