@@ -212,12 +212,18 @@ def hbm_plan(rows: int, dim: int, batch: int, consolidate_convs: int, facts: int
     recall_ws = chunk * dim * 8 * 2 + 2 * 1024 * chunk * 8
     head = cap * bpr + encoder + search_ws + max(load_ws, recall_ws)
     # consolidation: the tenant, 2 x rows seeded edges (+1/8 append slack), the
-    # dual scan's two candidate lists, k-means (4096 centroids, per-row labels)
+    # dual scan's two candidate lists, k-means (4096 centroids, per-row labels).
+    # Consolidation appends every new fact as a fresh row (an evicted row is
+    # not reused), so the first timed steps take the tenant past the loader's
+    # capacity and TenantGraph.reserve grows every column by 1.5x: the
+    # consolidation sections are planned at that grown capacity (measured:
+    # 81.8 GiB for a 10M-row tenant, profiles/r6/full_bench/)
     F = consolidate_convs * facts
     dual_ws = 2 * F * (2048 * 16 * 8) + 256 * 8 * 2048 * 16 * 2
     kmeans = 4096 * dim * 6 + rows * 16
-    cons = cap * bpr + 2 * rows * eb * 9 // 8 + encoder + dual_ws + kmeans + load_ws
-    sharded = cap * bpr + 2 * rows * eb * 9 // 8 + F * 2 * (bpr + 64) + encoder + dual_ws + kmeans + load_ws
+    ccap = int(cap * 1.5) + 1
+    cons = ccap * bpr + 2 * rows * eb * 9 // 8 + encoder + dual_ws + kmeans + load_ws
+    sharded = ccap * bpr + 2 * rows * eb * 9 // 8 + F * 2 * (bpr + 64) + encoder + dual_ws + kmeans + load_ws
     secs = {"headline": head, "consolidate": cons, "consolidate_persistent_graph": cons,
             "consolidate_sharded": sharded,
             # + the replicated stable base of the incremental digest (int32

@@ -2,7 +2,7 @@
 # round 6: one-rank sharded buffer on a persistent graph through the native applier + incremental components
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
-OUT=${OUT:-gpurun_out/r6shpg2}
+OUT=${OUT:-gpurun_out/r6sharded}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/kernels/test_sharded_memory_gpu.py -m gpu -x -v --timeout 240 \
   --timeout-method thread -k "one_rank or incremental" > $OUT/pytest.log 2>&1 || exit 1
