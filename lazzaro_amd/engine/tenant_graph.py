@@ -2655,7 +2655,9 @@ class TenantGraph:
                     emb32.record_stream(st)
 
                 def work():
-                    with torch.cuda.stream(st):
+                    # a new thread starts on device 0: bind this tenant's GPU
+                    # (multi-GPU processes) before any launch
+                    with torch.cuda.device(self.device), torch.cuda.stream(st):
                         st.wait_event(ev)
                         out = self._cluster_compute(live, src, emb32, n, n_fine, n_top, iters, seed, None, prev,
                                                     version)
