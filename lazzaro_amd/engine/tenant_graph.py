@@ -335,6 +335,7 @@ class TenantGraph:
         self.edge_version = 0
         self._hier = None  # the k-means hierarchy (cluster_pass); read through .hier
         self._hier_job = None  # a background cluster_pass in flight (cluster_join)
+        self._hier_lock = threading.Lock()  # one joiner publishes the job's hierarchy
         self._csr = None
         self._csr_version = -1
         self._boost_state = T.BoostState()
@@ -2679,17 +2680,21 @@ class TenantGraph:
         """Wait for a background :meth:`cluster_pass` and publish its
         hierarchy (the graph stream waits for its kernels; its tensors are
         marked in use there). Re-raises the pass's error."""
-        job, self._hier_job = self._hier_job, None
-        if job is None:
-            return
-        out, done, graph_st = job.result()
-        graph_st.wait_event(done)
-        if out is None:
-            return
-        for t in out.values():
-            if torch.is_tensor(t) and t.is_cuda:
-                t.record_stream(graph_st)
-        self._hier = out
+        with self._hier_lock:
+            job = self._hier_job
+            if job is None:
+                return
+            try:
+                out, done, graph_st = job.result()
+            finally:
+                self._hier_job = None
+            graph_st.wait_event(done)
+            if out is None:
+                return
+            for t in out.values():
+                if torch.is_tensor(t) and t.is_cuda:
+                    t.record_stream(graph_st)
+            self._hier = out
 
     def _cluster_compute(self, live, src, emb32, n: int, n_fine: int, n_top: int, iters: int, seed: int, comm,
                          prev: Dict, version: int) -> Optional[Dict]:
