@@ -136,7 +136,7 @@ def _sync(dev):
 def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, encoder=None, dim: int = 768,
         dup_rate: float = 0.1, seed: int = 7, cluster_every: int = 5, n_fine: int = 4096, n_top: int = 64,
         cluster_iters: int = 2, init_edges: int = None, db_dir: str = None, prune_threshold: float = 0.5,
-        persist_async: bool = False, stream: bool = True):
+        persist_async: bool = False, stream: bool = True, lookahead: int = 2):
     """``stream``: the batches go through ``MemorySystem.consolidate_stream``
     (batch i+1's candidate scan under batch i's apply; results identical to
     the per-batch calls, tests/kernels/test_tenant_engine_gpu.py); False:
@@ -170,7 +170,7 @@ def run(comm, dev, nodes: int, convs: int, facts: int, steps: int, warmup: int, 
 
     def run_steps(k):
         if stream:
-            yield from ms.consolidate_stream(make_batch() for _ in range(k))
+            yield from ms.consolidate_stream((make_batch() for _ in range(k)), lookahead=lookahead)
         else:
             for _ in range(k):
                 conversations, V = make_batch()
@@ -453,6 +453,8 @@ if __name__ == "__main__":
                     help="--sharded: the full digest at every run_consolidation point (A/B)")
     ap.add_argument("--no-prefetch-under-cluster", action="store_true",
                     help="no batch i+1 scan prefetch past a batch that runs a k-means pass (A/B)")
+    ap.add_argument("--lookahead", type=int, default=2,
+                    help="consolidate_stream: batches drawn ahead (1 = the next one only; A/B)")
     ap.add_argument("--cluster-inline", action="store_true",
                     help="k-means passes in line instead of in the background (A/B)")
     a = ap.parse_args()
@@ -477,7 +479,8 @@ if __name__ == "__main__":
              n_fine=a.fine, n_top=a.top, cluster_iters=a.cluster_iters, init_edges=a.init_edges,
              **({"clustered": a.clustered, "cadence": a.cadence, "stream": a.stream,
                  "prune_threshold": a.prune_threshold} if a.sharded else
-                {"prune_threshold": a.prune_threshold, "persist_async": a.persist_async, "stream": a.stream}))
+                {"prune_threshold": a.prune_threshold, "persist_async": a.persist_async, "stream": a.stream,
+                 "lookahead": a.lookahead}))
     if comm.rank == 0:
         print(json.dumps({"metric": "consolidate turns/sec", "n_gpus": comm.world, **res}), flush=True)
     if comm.enabled:

@@ -762,7 +762,8 @@ class ConsolidationMixin:
             self._save_to_persistence()
         return stats
 
-    def consolidate_stream(self, batches, cadence: str = "conversation", commit: str = "batch"):
+    def consolidate_stream(self, batches, cadence: str = "conversation", commit: str = "batch",
+                           lookahead: int = 2):
         """:meth:`consolidate_batch` over a stream of batches, yielding each
         batch's counts. ``batches`` yields ``(conversations, embeddings)`` or
         ``(conversations, embeddings, now)``. The result is the sequential
@@ -772,18 +773,30 @@ class ConsolidationMixin:
         while batch i's plan is applied on the host and the graph stream;
         batch i+1 then completes it against the graph as batch i left it
         (TenantGraph.cos_topk_finish: rows that left re-scanned, rows that
-        arrived re-ranked in). The next item is drawn from ``batches`` before
-        batch i is applied."""
+        arrived re-ranked in). Items are drawn from ``batches`` ``lookahead``
+        batches ahead (>= 1; the default 2 draws batch i+2 before batch i is
+        applied): a generator that embeds its facts on the device then has
+        batch i+1's embed queued a whole batch before the prefetch reads its
+        validity, instead of waiting for it there."""
+        from collections import deque
         it = iter(batches)
-        cur = next(it, None)
+        ahead = deque()
+
+        def fill():
+            while len(ahead) < max(1, int(lookahead)):
+                b = next(it, None)
+                if b is None:
+                    break
+                ahead.append(b)
+        fill()
         try:
-            while cur is not None:
-                nxt = next(it, None)
-                self._prefetch_next = nxt
+            while ahead:
+                cur = ahead.popleft()
+                fill()
+                self._prefetch_next = ahead[0] if ahead else None
                 convs, embs = cur[0], cur[1]
                 now = cur[2] if len(cur) > 2 else None
                 yield self.consolidate_batch(convs, embeddings=embs, now=now, cadence=cadence, commit=commit)
-                cur = nxt
         finally:
             self._prefetch_next = None
             self._prefetched = None
