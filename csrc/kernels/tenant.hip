@@ -302,8 +302,13 @@ __global__ __launch_bounds__(NTB) void tg_evict_verify_kernel(const float* __res
   //     step of fp32 rounding -- above vmax (+1e-9): no event can rank it first;
   //  2. the exact sequential importance after st_last decays >= vmax, ties
   //     only with a row key above every event's: the same.
+  // A row below the floor (s < F) is lifted to F by its first decay step and
+  // stays there, so its lowest importance is the current one (s * 0.5 + a +
+  // d, the loop's own formula): above vmax, no event can rank it first.
   // Everything else walks the events exactly as before.
-  if (s >= SAL_FLOOR) {
+  if (s < SAL_FLOOR) {
+    if ((double)s * 0.5 + a + d > vmax + 1e-9) return;
+  } else {
     const double F = (double)SAL_FLOOR;
     double lb = F + ((double)s - F) * kt - 4.0 * (double)st_last * 5.9604644775390625e-08;
     if (lb < F) lb = F;
