@@ -235,17 +235,27 @@ int cc_digest(const Cc& a, const int* src, const int* dst, const float* w, long 
                           nbig ? a.cur : a.rem, nbig ? a.last : a.rem, nbig ? a.cnt : a.rem, a.keys, a.rows,
                           (int)cap, a.counters + 3, a.rem, a.window, stream)))
     return rc;
+  // the selected count and (speculatively) the first `spec` pairs in ONE
+  // wait; a longer selection reads its remainder after a second one
   int m = 0;
+  const long spec = cap < 8192 ? cap : 8192;
+  std::vector<long long> k(spec);
+  std::vector<int> r(spec);
   if (hipMemcpyAsync(&m, a.counters + 3, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(k.data(), a.keys, 8L * spec, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(r.data(), a.rows, 4L * spec, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return (int)hipGetLastError();
   if (m > cap) return (int)hipErrorInvalidValue;
   if (m == 0) return 0;
-  std::vector<long long> k(m);
-  std::vector<int> r(m);
-  if (hipMemcpyAsync(k.data(), a.keys, 8L * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipMemcpyAsync(r.data(), a.rows, 4L * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
+  if (m > spec) {
+    k.resize(m);
+    r.resize(m);
+  }
+  if (m > spec &&
+      (hipMemcpyAsync(k.data() + spec, a.keys + spec, 8L * (m - spec), hipMemcpyDeviceToHost, st) != hipSuccess ||
+       hipMemcpyAsync(r.data() + spec, a.rows + spec, 4L * (m - spec), hipMemcpyDeviceToHost, st) != hipSuccess ||
+       hipStreamSynchronize(st) != hipSuccess))
     return (int)hipGetLastError();
   std::vector<std::pair<long long, long long>> kr(m);
   for (int i = 0; i < m; ++i) kr[i] = {k[i], (long long)r[i]};
