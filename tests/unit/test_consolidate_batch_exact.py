@@ -231,11 +231,13 @@ def test_batch_commit_per_conversation(tmp_path, monkeypatch):
         bat.consolidate_batch(convs[:1], commit="sometimes")
 
 
-def test_consolidate_stream_equals_sequential_cpu(tmp_path, monkeypatch):
+@pytest.mark.parametrize("lookahead", [1, 2, 5])
+def test_consolidate_stream_equals_sequential_cpu(tmp_path, monkeypatch, lookahead):
     """``consolidate_stream`` over three batches is the sequential run (on the
     CPU the next batch's scan is not prefetched: the stream plumbing only;
     the prefetched GPU path is tests/kernels/test_tenant_engine_gpu.py::
-    test_consolidate_stream_matches_batches_gpu)."""
+    test_consolidate_stream_matches_batches_gpu), however many batches it
+    draws ahead (``lookahead`` 5 > the stream's length)."""
     import time as _time
     monkeypatch.setattr(_time, "time", lambda: 1_900_000_000.0)
     B = 24
@@ -248,7 +250,18 @@ def test_consolidate_stream_equals_sequential_cpu(tmp_path, monkeypatch):
     st = _system(tmp_path / "st", "cpu")
     embs = [None] * 3  # the embedder runs per batch
     parts = [convs[:8], convs[8:16], convs[16:]]
-    stats = list(st.consolidate_stream((p, e, 1_900_000_000.0) for p, e in zip(parts, embs)))
+    drawn = []
+
+    def gen():
+        for p, e in zip(parts, embs):
+            drawn.append(len(drawn))
+            yield p, e, 1_900_000_000.0
+    it = st.consolidate_stream(gen(), lookahead=lookahead)
+    first = next(it)
+    # before batch 1's counts are handed back, exactly `lookahead` batches
+    # past batch 0 were drawn (bounded by the stream's length)
+    assert len(drawn) == min(3, 1 + lookahead)
+    stats = [first] + list(it)
     assert len(stats) == 3 and sum(s["conversations"] for s in stats) == B
     a, b = _state(seq), _state(st)
     for k in a:
