@@ -754,8 +754,11 @@ __global__ __launch_bounds__(FR_NT) void tg_first_rows_kernel(const unsigned cha
                                                               const unsigned char* __restrict__ sup,
                                                               const int* __restrict__ shard, long n, FrTargets T,
                                                               long* __restrict__ out) {
+  // per chunk: every wave ballots each open target once (per-target, per-wave
+  // counts in LDS), ONE barrier, then each row's block-wide rank within its
+  // target -- four barriers per chunk instead of three per open target
   __shared__ int s_tc[FR_MAXT], s_tt[FR_MAXT], s_to[FR_MAXT], s_found[FR_MAXT];
-  __shared__ int s_w[FR_NT / 64];
+  __shared__ int s_cnt[FR_MAXT][FR_NT / 64];
   __shared__ int s_open;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nt = T.nt;
@@ -771,23 +774,30 @@ __global__ __launch_bounds__(FR_NT) void tg_first_rows_kernel(const unsigned cha
     const int c = (r < n && kind[r] == 1 && sup[r] == 0) ? shard[r] : -1;
     int j = -1;
     for (int t = 0; t < nt; ++t) j = (s_tc[t] == c) ? t : j;
+    unsigned long long myb = 0;
     for (int t = 0; t < nt; ++t) {
-      const int have = s_found[t], want = s_tt[t];  // block-uniform
-      if (have >= want) continue;
+      if (s_found[t] >= s_tt[t]) continue;  // block-uniform: s_found changes only behind barriers
       const unsigned long long b = __ballot(j == t);
-      if (lane == 0) s_w[wv] = __popcll(b);
-      __syncthreads();
-      int before = 0, total = 0;
-      for (int w = 0; w < FR_NT / 64; ++w) {
-        before += w < wv ? s_w[w] : 0;
-        total += s_w[w];
-      }
-      const int rank = have + before + (int)__popcll(b & ((1ull << lane) - 1));
-      if (j == t && rank < want) out[s_to[t] + rank] = r;
-      __syncthreads();  // every lane read s_found[t] / s_w
-      if (threadIdx.x == 0) s_found[t] = min(want, have + total);
-      __syncthreads();
+      if (lane == 0) s_cnt[t][wv] = __popcll(b);
+      if (j == t) myb = b;
     }
+    __syncthreads();
+    if (j >= 0 && s_found[j] < s_tt[j]) {
+      int before = 0;
+      for (int w = 0; w < wv; ++w) before += s_cnt[j][w];
+      const int rank = s_found[j] + before + (int)__popcll(myb & ((1ull << lane) - 1));
+      if (rank < s_tt[j]) out[s_to[j] + rank] = r;
+    }
+    __syncthreads();  // every lane read s_found / s_cnt
+    if (threadIdx.x < nt) {
+      const int t = threadIdx.x;
+      if (s_found[t] < s_tt[t]) {
+        int total = 0;
+        for (int w = 0; w < FR_NT / 64; ++w) total += s_cnt[t][w];
+        s_found[t] = min(s_tt[t], s_found[t] + total);
+      }
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
       int open = 0;
       for (int t = 0; t < nt; ++t) open |= s_found[t] < s_tt[t];
