@@ -453,11 +453,16 @@ if __name__ == "__main__":
                     help="--sharded: the full digest at every run_consolidation point (A/B)")
     ap.add_argument("--no-prefetch-under-cluster", action="store_true",
                     help="no batch i+1 scan prefetch past a batch that runs a k-means pass (A/B)")
+    ap.add_argument("--eager-node-decay", action="store_true",
+                    help="native applier: a node-salience pass per segment instead of the lazy stamps (A/B)")
     ap.add_argument("--lookahead", type=int, default=2,
                     help="consolidate_stream: batches drawn ahead (1 = the next one only; A/B)")
     ap.add_argument("--cluster-inline", action="store_true",
                     help="k-means passes in line instead of in the background (A/B)")
     a = ap.parse_args()
+    if a.eager_node_decay:
+        from lazzaro_amd.engine import native_apply
+        native_apply.LAZY_NODE_DECAY = False
     if a.cluster_inline:
         from lazzaro_amd.core.memory_system import MemorySystem
         MemorySystem.CLUSTER_BACKGROUND = False

@@ -104,6 +104,9 @@ struct Cols {
   float* dv_max;
   unsigned char* has_emb;
   unsigned* rmb;
+  // optional (nullptr: every segment's DECAY passes over the shard nodes):
+  // per-row decay stamps of the lazy node decay (see lzk_apply_segments)
+  int* stamp;
 };
 
 struct EdgeSet {
@@ -130,6 +133,59 @@ __global__ void ap_fill64_kernel(long long* __restrict__ a, long n, long long v)
 }
 
 inline unsigned nblk(long n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+
+// Lazy node decay. The segments' DECAY ops each pass over every shard node
+// (one fp32 salience decay per conversation, tenant.hip decay_sal); nothing
+// on the device reads a node's salience between them (the planner wrote the
+// absolute saliences of the rows it touches), so the passes collapse into
+// per-row stamps -- the conversation count a row's salience is current at --
+// and ONE pass at the end that applies the missing steps one by one in the
+// same fp32 order (bit-identical). A victim takes its missing steps at its
+// segment end, before it stops being a shard node.
+constexpr float kSalFloor = 0.2f;  // = tenant.hip SAL_FLOOR
+__device__ __forceinline__ float ap_decay_sal(float s, float keep) {
+#pragma clang fp contract(off)
+  return s > kSalFloor ? kSalFloor + (s - kSalFloor) * keep : kSalFloor;
+}
+
+__global__ void ap_stamp_rows_kernel(const long* __restrict__ rows, long row0, int m, const double* __restrict__ vals,
+                                     int present, int* __restrict__ stamp, int cum) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  long r;  // the row tg_set_rows_kernel writes
+  if (present & (1 << 15)) r = (long)vals[j];
+  else r = rows ? rows[j] : row0 + j;
+  if (r >= 0) stamp[r] = cum;
+}
+
+__global__ void ap_victim_decay_kernel(const long* __restrict__ vrows, int nv, float* __restrict__ sal,
+                                       const unsigned char* __restrict__ kind, const unsigned char* __restrict__ sup,
+                                       int* __restrict__ stamp, int cum, float keep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nv) return;
+  const long r = vrows[i];
+  if (r < 0) return;
+  if (kind[r] == 1 && !sup[r]) {
+    float s = sal[r];
+    for (int t = stamp[r]; t < cum; ++t) s = ap_decay_sal(s, keep);
+    sal[r] = s;
+  }
+  stamp[r] = cum;
+}
+
+__global__ void ap_lazy_decay_kernel(float* __restrict__ sal, const unsigned char* __restrict__ kind,
+                                     const unsigned char* __restrict__ sup, int* __restrict__ stamp, long n, int cum,
+                                     float keep) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int st = stamp[i];
+    if (st < cum && kind[i] == 1 && !sup[i]) {
+      float s = sal[i];
+      for (int t = st; t < cum; ++t) s = ap_decay_sal(s, keep);
+      sal[i] = s;
+    }
+    if (st) stamp[i] = 0;  // every stamp is 0 between calls
+  }
+}
 
 // Incremental-components digest of one run_consolidation point (the
 // partitioned batch of TenantGraph.cc_begin: stable prefix [0, ns) labelled
@@ -307,6 +363,7 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
   EdgeSet E[2] = {edge_set(ebuf_a), edge_set(ebuf_b)};
   int cur = 0;
   long ne = ne0, n = 0, drop_total = 0, vinfo_used = 0;
+  long cum = 0;  // conversations decayed so far (lazy node decay)
   // the deferred prune of the open segment: keep flags over its first nprev edges
   unsigned char* prev = nullptr;
   long nprev = 0;
@@ -329,8 +386,10 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
       // nothing is pruned, no flags (TenantGraph.segment_begin)
       prev = (ne > 0 && thr > -__builtin_huge_valf()) ? flag_a : nullptr;
       nprev = ne;
-      LZK_RC(lzk_tg_decay(E[cur].w, ne, keep, thr, prev, prev ? bc : nullptr, C.sal, C.kind, C.sup, n, n ? 1 : 0,
-                          steps, stream));
+      // lazy node decay (C.stamp): the nodes' steps are only counted here
+      LZK_RC(lzk_tg_decay(E[cur].w, ne, keep, thr, prev, prev ? bc : nullptr, C.sal, C.kind, C.sup, n,
+                          (n && !C.stamp) ? 1 : 0, steps, stream));
+      cum += steps;
       // the decay's block counts are only needed by a compaction of these
       // flags alone, which never happens here (the segment end re-flags)
     } else if (op == OP_ROWS) {
@@ -345,6 +404,11 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
                              (const double*)(blk + vals_off), present, (const double*)(blk + consts_off), C.sal,
                              C.acc, C.last, C.ts, C.shard, C.sup, C.parent, C.kind, C.stored, C.dirty, kind_v,
                              stored_v, stream));
+      // a written salience is current as of now
+      if (C.stamp && m > 0 && !(present & (1 << 8)))
+        hipLaunchKernelGGL(ap_stamp_rows_kernel, dim3(nblk(m)), dim3(256), 0, st,
+                           rows_off >= 0 ? (const long*)(blk + rows_off) : nullptr, row0, m,
+                           (const double*)(blk + vals_off), present, C.stamp, (int)cum);
     } else if (op == OP_EMB) {
       const long xr = prog[pc + 1];
       const int m = (int)prog[pc + 2];
@@ -384,6 +448,9 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
         rc = (int)hipErrorInvalidValue;
         goto done;
       }
+      if (C.stamp && nv)  // the victims' missing decay steps, while they are still shard nodes
+        hipLaunchKernelGGL(ap_victim_decay_kernel, dim3(nblk(nv)), dim3(256), 0, st, (const long*)(blk + vrows_off),
+                           nv, C.sal, C.kind, C.sup, C.stamp, (int)cum, keep);
       const EdgeSet& e = E[cur];
       const long nes = ne - ns;  // the suffix the segment end flags
       LZK_RC(lzk_tg_seg_end(nv ? (const long*)(blk + vrows_off) : nullptr, nv, C.kind, C.sup, C.shard, C.stored,
@@ -484,6 +551,12 @@ LZK_EXPORT int lzk_apply_segments(const long* prog, long nprog, const char* blk,
       rc = (int)hipErrorInvalidValue;
       goto done;
     }
+  }
+  // the lazy node decay's one pass: every shard node's missing steps
+  if (rc == 0 && C.stamp && n > 0) {
+    const long g = (long)nblk(n) < 4096 ? (long)nblk(n) : 4096;
+    hipLaunchKernelGGL(ap_lazy_decay_kernel, dim3((unsigned)g), dim3(256), 0, st, C.sal, C.kind, C.sup, C.stamp, n,
+                       (int)cum, keep);
   }
 done:
 #undef LZK_RC

@@ -65,6 +65,12 @@ def available() -> bool:
         return False
 
 
+
+# The segments' node-salience decay as per-row stamps and one pass at the end
+# of each run (csrc/kernels/apply.hip, bit-identical to a pass per segment).
+# False: a pass over every shard node per segment (A/B).
+LAZY_NODE_DECAY = True
+
 class SegmentProgram:
     """Builder of one native apply call over a run of segments of a plan."""
 
@@ -266,13 +272,19 @@ class SegmentProgram:
             dg_cnt = torch.empty(1, dtype=torch.int32, device=dev)
             fr_out = torch.full((P_, max(self.k_first, 1)), -1, dtype=torch.int64, device=dev)
             i8 = g.emb8 is not None and g.emb8.dtype == torch.int8
+            # lazy node decay (apply.hip): per-row stamps, all zero between runs
+            stamp = None
+            if LAZY_NODE_DECAY:
+                stamp = getattr(g, "_dstamp", None)
+                if stamp is None or stamp.numel() < g.cap:
+                    stamp = g._dstamp = torch.zeros(g.cap, dtype=torch.int32, device=dev)
             cols = np.asarray([
                 g.sal.data_ptr(), g.acc.data_ptr(), g.last.data_ptr(), g.ts.data_ptr(), g.shard.data_ptr(),
                 g.sup.data_ptr(), g.parent.data_ptr(), g.kind.data_ptr(), g.stored.data_ptr(), g.dirty.data_ptr(),
                 g.emb32.data_ptr(), _lib.ptr(g.emb16), g.emb8.data_ptr() if i8 else 0,
                 g.rs8.data_ptr() if i8 else 0, g.sqn.data_ptr(), g.sumsq.data_ptr(),
                 g._rs8_max.data_ptr() if i8 else 0, g._dv_acc.data_ptr(), g.has_emb.data_ptr(),
-                g._rmb.data_ptr()], dtype=np.uint64)
+                g._rmb.data_ptr(), stamp.data_ptr() if stamp is not None else 0], dtype=np.uint64)
             eb = [np.asarray([sets[s][k].data_ptr() for k in T.EDGE_COLS], dtype=np.uint64) for s in range(2)]
             sc = np.asarray(list(shard_count) or [0], dtype=np.int64)
             seg_out = np.zeros(4 * max(self.nseg, 1), np.int64)
@@ -317,6 +329,8 @@ class SegmentProgram:
                 max(self.k_first, 1), sc.ctypes.data, int(len(shard_count)), seg_out.ctypes.data,
                 vinfo.ctypes.data, int(vinfo.size), point_out.ctypes.data, state.ctypes.data,
                 ccp.ctypes.data if ccp is not None else None, _lib.stream_ptr(dev))
+            if rc != 0 and stamp is not None:
+                stamp.zero_()  # a failed run leaves no stale stamps behind
             _lib.check(rc, "lzk_apply_segments")
             ne, cur, nd = int(state[0]), int(state[1]), int(state[2])
             g._adopt_edges({k: sets[cur][k][:ne] for k in T.EDGE_COLS})
