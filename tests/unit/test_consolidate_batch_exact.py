@@ -163,17 +163,21 @@ def test_batch_pairwise_merge_mode_is_sequential(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("native", ["lazy", "eager", False])
 @pytest.mark.parametrize("B,kw", [(30, {"max_buffer_size": 16, "super_node_threshold": 5}), (24, {}),
                                   (30, {"max_buffer_size": 10, "super_node_threshold": 20}),
                                   (21, {"prune_threshold": 0.3, "consolidate_every": 2}),
                                   (27, {"max_buffer_size": 40, "super_node_threshold": 4})])
 def test_batch_equals_sequential_gpu(tmp_path, monkeypatch, native, B, kw):
     """The GPU batch path -- through the native segment applier
-    (csrc/kernels/apply.hip, engine/native_apply.py) and through the
-    per-segment Python path -- equals the sequential end_conversation run."""
+    (csrc/kernels/apply.hip, engine/native_apply.py; its node-salience decay
+    lazy (per-row stamps, one pass per run) or eager (a pass per segment))
+    and through the per-segment Python path -- equals the sequential
+    end_conversation run."""
     from lazzaro_amd.core import consolidation as C
-    monkeypatch.setattr(C.ConsolidationMixin, "NATIVE_APPLY", native)
+    from lazzaro_amd.engine import native_apply as NA
+    monkeypatch.setattr(C.ConsolidationMixin, "NATIVE_APPLY", bool(native))
+    monkeypatch.setattr(NA, "LAZY_NODE_DECAY", native == "lazy")
     runs = []
     orig = C.ConsolidationMixin._native_run
 
@@ -183,7 +187,7 @@ def test_batch_equals_sequential_gpu(tmp_path, monkeypatch, native, B, kw):
     monkeypatch.setattr(C.ConsolidationMixin, "_native_run", counted)
     a, b, (s1, s2) = _run_pair(tmp_path, monkeypatch, "cuda", B, **kw)
     assert s1["evicted"] + s2["evicted"] > 0
-    assert (sum(runs) > 0) == native  # the native applier ran (and only when enabled)
+    assert (sum(runs) > 0) == bool(native)  # the native applier ran (and only when enabled)
     for k in a:
         assert a[k] == b[k], k
 
